@@ -1,0 +1,146 @@
+// ref_harness.cpp — TEST INFRASTRUCTURE ONLY (oracle/). Never linked into the product.
+//
+// Driver that runs the *reference* C++ classes (compiled in place from
+// /root/reference/MetaGenomics by oracle/Makefile into oracle/_ref/) to produce
+// golden vectors and the "reference" CPU baseline.  No reference source is
+// copied: this file only #includes the reference headers where they lie.
+//
+// Modes
+//   edges  <fasta> <l> <out>   : discovery harness (SURVEY §0 recipe):
+//        Dataset(pe={}, se={fa}, l) -> HashTable::insertDataset(ds,l)
+//        (HashTable.cpp:50-80) -> markContainedReads (OverlapGraph.cpp:225-290)
+//        -> insertAllEdgesOfRead(i, explored) for i = 1..N in ID order,
+//        marking i EXPLORED after each call (OverlapGraph.cpp:529-565).
+//        Writes  "#N <n>", "#S <id> <super>" for every contained read,
+//        "#R <id> <canonical forward string>" and one "u v orient offset"
+//        row per directed Edge in graph[u].
+//   time   <fasta> <l> <out>   : the shipped path timing used by SURVEY §6:
+//        wall time of insertDataset + new OverlapGraph(ht)
+//        (main.cpp:45-47, includes transitive reduction + contraction).
+//   disc   <fasta> <l> <out>   : wall time of insertDataset + markContainedReads +
+//        the ID-order discovery loop (no transitive reduction), plus the raw
+//        directed edge count.  This is the apples-to-apples CPU figure for the
+//        GPU path, which also stops at the raw edge multiset.
+//   lookup <fasta> <l> <out> <key>... : HashTable::getListOfReads(key)
+//        (HashTable.cpp:202-221) for each key, in the reference list order.
+#define private public
+#include "Dataset.h"
+#include "HashTable.h"
+#include "OverlapGraph.h"
+#undef private
+
+#include <time.h>
+#include <cstdio>
+#include <cstring>
+
+static double now_s() {
+  struct timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return ts.tv_sec + 1e-9 * ts.tv_nsec;
+}
+
+// Silence the reference's progress chatter (it writes to std::cout).
+struct NullBuf : std::streambuf {
+  int overflow(int c) { return c; }
+};
+
+static OverlapGraph* prepare_graph(Dataset* ds, HashTable* ht) {
+  OverlapGraph* og = new OverlapGraph();
+  og->hashTable = ht;
+  og->dataSet = ds;
+  og->graph = new vector<vector<Edge*>*>;
+  for (UINT64 i = 0; i <= ds->getNumberOfUniqueReads(); i++) og->graph->push_back(new vector<Edge*>);
+  return og;
+}
+
+static void discovery(OverlapGraph* og, Dataset* ds) {
+  og->markContainedReads();
+  vector<nodeType> explored(ds->getNumberOfUniqueReads() + 1, UNEXPLORED);
+  for (UINT64 i = 1; i <= ds->getNumberOfUniqueReads(); i++) {
+    og->insertAllEdgesOfRead(i, &explored);
+    explored[i] = EXPLORED;
+  }
+}
+
+int main(int argc, char** argv) {
+  if (argc < 5) {
+    fprintf(stderr, "usage: %s edges|time|disc|lookup <fasta> <l> <out> [keys...]\n", argv[0]);
+    return 2;
+  }
+  const char* mode = argv[1];
+  string fasta = argv[2];
+  UINT64 l = strtoull(argv[3], 0, 10);
+  FILE* out = fopen(argv[4], "w");
+  if (!out) { perror("open out"); return 2; }
+  NullBuf nb;
+  std::streambuf* old = std::cout.rdbuf(&nb);
+
+  vector<string> pe, se;
+  se.push_back(fasta);
+  double t0 = now_s();
+  Dataset* ds = new Dataset(pe, se, l);
+  double t_ds = now_s() - t0;
+  UINT64 N = ds->getNumberOfUniqueReads();
+
+  if (!strcmp(mode, "time")) {
+    double t1 = now_s();
+    HashTable* ht = new HashTable();
+    ht->insertDataset(ds, l);
+    double t2 = now_s();
+    OverlapGraph* og = new OverlapGraph(ht);  // deletes ht (OverlapGraph.cpp:210)
+    double t3 = now_s();
+    fprintf(out, "{\"n_unique\": %llu, \"dataset_s\": %.6f, \"hash_s\": %.6f, \"graph_s\": %.6f}\n",
+            (unsigned long long)N, t_ds, t2 - t1, t3 - t2);
+    (void)og;
+  } else if (!strcmp(mode, "disc")) {
+    double t1 = now_s();
+    HashTable* ht = new HashTable();
+    ht->insertDataset(ds, l);
+    double t2 = now_s();
+    OverlapGraph* og = prepare_graph(ds, ht);
+    discovery(og, ds);
+    double t3 = now_s();
+    unsigned long long rows = 0;
+    for (UINT64 u = 1; u <= N; u++) rows += og->graph->at(u)->size();
+    fprintf(out, "{\"n_unique\": %llu, \"dataset_s\": %.6f, \"hash_s\": %.6f, \"discovery_s\": %.6f, \"directed_rows\": %llu}\n",
+            (unsigned long long)N, t_ds, t2 - t1, t3 - t2, rows);
+  } else if (!strcmp(mode, "edges")) {
+    HashTable* ht = new HashTable();
+    ht->insertDataset(ds, l);
+    OverlapGraph* og = prepare_graph(ds, ht);
+    discovery(og, ds);
+    fprintf(out, "#N %llu\n", (unsigned long long)N);
+    for (UINT64 i = 1; i <= N; i++) {
+      Read* r = ds->getReadFromID(i);
+      fprintf(out, "#R %llu %s\n", (unsigned long long)i, r->getStringForward().c_str());
+      if (r->superReadID)
+        fprintf(out, "#S %llu %llu\n", (unsigned long long)i, (unsigned long long)r->superReadID);
+    }
+    for (UINT64 u = 1; u <= N; u++) {
+      vector<Edge*>* lst = og->graph->at(u);
+      for (size_t k = 0; k < lst->size(); k++) {
+        Edge* e = lst->at(k);
+        fprintf(out, "%llu %llu %u %llu\n", (unsigned long long)e->getSourceRead()->getReadNumber(),
+                (unsigned long long)e->getDestinationRead()->getReadNumber(), (unsigned)e->getOrientation(),
+                (unsigned long long)e->getOverlapOffset());
+      }
+    }
+  } else if (!strcmp(mode, "lookup")) {
+    HashTable* ht = new HashTable();
+    ht->insertDataset(ds, l);
+    for (int a = 5; a < argc; a++) {
+      vector<UINT64>* lst = ht->getListOfReads(string(argv[a]));
+      fprintf(out, "%s", argv[a]);
+      for (size_t k = 0; k < lst->size(); k++)
+        fprintf(out, " %llu:%llu", (unsigned long long)(lst->at(k) & 0x3FFFFFFFFFFFFFFFULL),
+                (unsigned long long)(lst->at(k) >> 62));
+      fprintf(out, "\n");
+    }
+  } else {
+    fprintf(stderr, "unknown mode %s\n", mode);
+    return 2;
+  }
+  std::cout.rdbuf(old);
+  fclose(out);
+  return 0;
+}

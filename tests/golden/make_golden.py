@@ -1,0 +1,172 @@
+#!/usr/bin/env python3
+"""Generate the golden fixtures in tests/golden/ from the REFERENCE itself.
+
+Runs ``oracle/_ref/ref_harness`` (the reference's own Dataset/HashTable/
+OverlapGraph sources compiled in place by oracle/Makefile; SURVEY §0 recipe)
+on small deterministic read sets and stores, per set:
+
+  <name>.fa.gz / .fq.gz  input reads (data)
+  <name>.edges.gz        sorted directed rows "u v orient offset" of the graph
+                         after the discovery loop (OverlapGraph.cpp:529-565)
+  <name>.json            l, unique reads, row count, sha256 of the sorted rows,
+                         superReadID of every contained read, sha256 of the
+                         ID -> canonical-string map (Dataset.cpp:197-202,316-345)
+
+Only runs in the build container (the reference is not on the GPU box).
+Usage: python tests/golden/make_golden.py [--big]
+"""
+from __future__ import annotations
+
+import gzip
+import hashlib
+import json
+import os
+import subprocess
+import sys
+import tempfile
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+from metagenomics_amd import synth  # noqa: E402
+
+HARNESS = os.path.join(ROOT, "oracle", "_ref", "ref_harness")
+
+
+def run_ref(fa: str, l: int):
+    with tempfile.NamedTemporaryFile("r", suffix=".txt", delete=False) as t:
+        out = t.name
+    subprocess.run([HARNESS, "edges", fa, str(l), out], check=True)
+    n = 0
+    reads, supers, rows = {}, {}, []
+    with open(out) as f:
+        for line in f:
+            if line.startswith("#N"):
+                n = int(line.split()[1])
+            elif line.startswith("#R"):
+                _, i, s = line.split()
+                reads[int(i)] = s
+            elif line.startswith("#S"):
+                _, i, s = line.split()
+                supers[int(i)] = int(s)
+            else:
+                u, v, o, off = map(int, line.split())
+                rows.append((u, v, o, off))
+    os.unlink(out)
+    rows.sort()
+    return n, reads, supers, rows
+
+
+def rows_digest(rows) -> str:
+    h = hashlib.sha256()
+    for r in rows:
+        h.update(("%d %d %d %d\n" % r).encode())
+    return h.hexdigest()
+
+
+def ids_digest(reads: dict) -> str:
+    h = hashlib.sha256()
+    for i in sorted(reads):
+        h.update(("%d %s\n" % (i, reads[i])).encode())
+    return h.hexdigest()
+
+
+def emit(name: str, seqs, l: int, fastq: bool = False, store_rows: bool = True, raw_text=None,
+         store_input: bool = True, recipe=None):
+    ext = ".fq" if fastq else ".fa"
+    with tempfile.TemporaryDirectory() as td:
+        path = os.path.join(td, name + ext)
+        if raw_text is not None:
+            with open(path, "w") as f:
+                f.write(raw_text)
+        elif fastq:
+            synth.write_fastq(path, seqs)
+        else:
+            synth.write_fasta(path, seqs)
+        n, reads, supers, rows = run_ref(path, l)
+        with open(path, "rb") as f:
+            data = f.read()
+    if store_input:
+        with gzip.GzipFile(os.path.join(HERE, name + ext + ".gz"), "wb", mtime=0) as g:
+            g.write(data)
+    if store_rows:
+        with gzip.GzipFile(os.path.join(HERE, name + ".edges.gz"), "wb", mtime=0) as g:
+            g.write("".join("%d %d %d %d\n" % r for r in rows).encode())
+    meta = {
+        "name": name, "input": (name + ext + ".gz") if store_input else None, "recipe": recipe, "l": l, "n_unique": n,
+        "directed_rows": len(rows), "undirected_edges": len(rows) // 2,
+        "rows_sha256": rows_digest(rows), "ids_sha256": ids_digest(reads),
+        "super": {str(k): v for k, v in sorted(supers.items())},
+        "edges_file": (name + ".edges.gz") if store_rows else None,
+    }
+    with open(os.path.join(HERE, name + ".json"), "w") as f:
+        json.dump(meta, f, indent=1, sort_keys=True)
+    print(f"{name}: N={n} rows={len(rows)} contained={len(supers)}")
+
+
+def strs(codes, lengths):
+    return synth.codes_to_strings(codes, lengths)
+
+
+def main():
+    big = "--big" in sys.argv
+    # 1. fixed-length uniform set (SURVEY §0 "small")
+    c, L = synth.uniform_read_set(2000, 100, 20000, seed=1)
+    emit("small", strs(c, L), 40)
+    # 2. mixed lengths 100-250 (containment active, SURVEY §0 "mixed")
+    c, L = synth.uniform_read_set(3000, 0, 30000, seed=5, lo=100, hi=250)
+    emit("mixed", strs(c, L), 50)
+    # 3. high duplicate: 3000 reads from a 2 kb genome (long bucket lists)
+    c, L = synth.uniform_read_set(3000, 100, 2000, seed=9)
+    emit("highdup", strs(c, L), 50)
+    # 4. tandem repeats + palindromes: self-loops and multi-edges
+    g = synth.codes_to_strings(synth.random_genome(3000, 13)[None, :], np.array([3000]))[0]
+    g = g[:1000] + "ACGTTGCAAG" * 60 + g[1000:2000] + "GAATTC" * 30 + g[2000:] + "GATTACA" * 50
+    gc = np.frombuffer(g.encode(), dtype=np.uint8)
+    codes = np.searchsorted(synth.ALPHABET, gc).astype(np.uint8)
+    c, L = synth.sample_reads(codes, 1500, 90, 140, seed=14)
+    emit("tandem", strs(c, L), 40)
+    # 5. two-read hand case: A = X[0:60], B = rc(X[20:80]), l = 30
+    X = synth.codes_to_strings(synth.random_genome(80, 21)[None, :], np.array([80]))[0]
+    emit("tworead", [X[0:60], synth.revcomp_str(X[20:80])], 30)
+    # 6. dirty FASTQ: N bases, lowercase, low complexity (>=80 % one base),
+    #    too-short reads, exact duplicates and reverse-complement duplicates
+    rng = np.random.default_rng(33)
+    c, L = synth.uniform_read_set(600, 0, 4000, seed=31, lo=30, hi=90)
+    seqs = strs(c, L)
+    out = []
+    for i, s in enumerate(seqs):
+        k = i % 11
+        if k == 0:
+            p = int(rng.integers(0, len(s)))
+            s = s[:p] + "N" + s[p + 1:]
+        elif k == 1:
+            s = s.lower()
+        elif k == 2:
+            s = "A" * int(0.8 * len(s) + 1) + s[int(0.8 * len(s) + 1):]
+        elif k == 3:
+            s = s[:20]
+        elif k == 4:
+            out.append(s)
+        elif k == 5:
+            out.append(synth.revcomp_str(s))
+        out.append(s)
+    emit("dirty", out, 20, fastq=True)
+    # 7. wrapped multi-line FASTA (parser: sequence lines joined, Dataset.cpp:139-147)
+    c, L = synth.uniform_read_set(400, 0, 6000, seed=41, lo=60, hi=180)
+    seqs = strs(c, L)
+    text = "".join(">w%d some description\n%s\n" % (i, "\n".join(s[p:p + 50] for p in range(0, len(s), 50)))
+                   for i, s in enumerate(seqs))
+    emit("wrapped", None, 35, raw_text=text)
+    if big:
+        # C1 (BASELINE configs[0]): 100k x 100 bp, l = 40; digest only.
+        c, L = synth.uniform_read_set(100_000, 100, 500_000, seed=7)
+        emit("c1", strs(c, L), 40, store_rows=False, store_input=False,
+             recipe={"fn": "uniform_read_set", "n_reads": 100_000, "read_len": 100,
+                     "genome_len": 500_000, "seed": 7})
+
+
+if __name__ == "__main__":
+    main()
