@@ -1,0 +1,239 @@
+#!/usr/bin/env python3
+"""Benchmark: overlap edges/sec (+ reads/sec) of the MI355X hot path.
+
+A "step" = one pass of the hot path over the resident read set: index build
+(HashTable::insertDataset) + containment (skipped for equal lengths, as in the
+reference) + overlap discovery producing the full directed edge multiset in
+HBM.  Inputs (2-bit packed reads) are resident in HBM before timing starts.
+
+Default workload = BASELINE.json configs[2] (C3): 10M x 150 bp synthetic
+reads, 20x coverage of a 75 Mb random genome, 50 % reverse-complemented,
+l = 50, seed k = 31.  Multi-GPU (torchrun): the same 10M reads on N GPUs,
+strong scaling; each rank owns a bucket range of the index.
+
+Prints ONE JSON line (rank 0).  See DESIGN.md §5 for the roofline numbers.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import subprocess
+import sys
+import tempfile
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from metagenomics_amd import synth  # noqa: E402
+from metagenomics_amd.overlap import Dataset, OverlapEngine  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec 8.0 TB/s)
+
+CONFIGS = {
+    # name: (n_reads, read_len lo, hi, genome_len, l, k, seed, description)
+    "c1": (100_000, 100, 100, 500_000, 40, 21, 7, "C1: 100k x 100 bp, l=40, k=21"),
+    "c2": (1_000_000, 150, 150, 7_500_000, 50, 31, 21, "C2: 1M x 150 bp, l=50, k=31"),
+    "c3": (10_000_000, 150, 150, 75_000_000, 50, 31, 31, "C3: 10M x 150 bp, l=50, k=31"),
+}
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def make_dataset(cfg, nthreads):
+    n, lo, hi, G, l, k, seed, _ = cfg
+    t0 = time.time()
+    c, L = synth.uniform_read_set(n, 0, G, seed=seed, lo=lo, hi=hi)
+    t1 = time.time()
+    ds = Dataset.from_codes(c, L, l, nthreads=nthreads)
+    t2 = time.time()
+    log(f"[bench] generated {n} reads in {t1 - t0:.1f}s, Dataset ingest {t2 - t1:.1f}s, unique {ds.num_unique}")
+    return ds, c, L
+
+
+def cpu_baseline(cfg, sample_reads: int):
+    """Reference CPU path on a bounded sample of the same workload shape
+    (same read length, l, coverage), rank 0 at N=1 only."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle  # the checker / baseline only
+
+    n, lo, hi, G, l, k, seed, _ = cfg
+    cov = n * (lo + hi) / 2 / G
+    Gs = int(sample_reads * (lo + hi) / 2 / cov)
+    c, L = synth.uniform_read_set(sample_reads, 0, Gs, seed=seed + 1000, lo=lo, hi=hi)
+    seqs = synth.codes_to_strings(c, L)
+    od = oracle.OracleDataset.from_strings(seqs, l)
+    rows, _, th, td = od.overlaps(l)
+    edges = rows.shape[0] // 2
+    sample = f"{sample_reads} reads x {lo}-{hi} bp, {cov:.0f}x coverage of {Gs} bp, l={l}"
+    if os.path.exists(oracle.REF_HARNESS):
+        with tempfile.TemporaryDirectory() as td_:
+            fa = os.path.join(td_, "s.fa")
+            synth.write_fasta(fa, seqs)
+            out = os.path.join(td_, "t.json")
+            subprocess.run([oracle.REF_HARNESS, "time", fa, str(l), out], check=True,
+                           stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+            r = json.load(open(out))
+        secs = r["hash_s"] + r["graph_s"]
+        return {"value": edges / secs, "unit": "edges/s", "cores": 1, "kind": "reference",
+                "sample": sample + "; reference insertDataset + OverlapGraph(ht) (main.cpp:45-47) wall time",
+                "seconds": secs, "edges": edges, "reads_per_sec": od.num_unique / secs,
+                "port_discovery_edges_per_sec": edges / (th + td)}
+    secs = th + td
+    return {"value": edges / secs, "unit": "edges/s", "cores": 1, "kind": "port",
+            "sample": sample + "; oracle C restatement index + discovery", "seconds": secs, "edges": edges,
+            "reads_per_sec": od.num_unique / secs}
+
+
+def load_pmc(path, kernel_substr="k_discover"):
+    """Per-launch HBM traffic of the discovery kernel from a committed rocprofv3
+    --pmc summary (profiles/*pmc*.json written by tools/pmc_summary.py)."""
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        return d.get("traffic_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
+    ap.add_argument("--shard", default="buckets", choices=["buckets", "reads"])
+    ap.add_argument("--sim-world", type=int, default=0,
+                    help="run rank --sim-rank of a SIM-WORLD-way shard on this one GPU (scaling study)")
+    ap.add_argument("--sim-rank", type=int, default=0)
+    ap.add_argument("--cpu-sample", type=int, default=150_000)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r01_pmc_c3.json"))
+    ap.add_argument("--nb-log2", type=int, default=0)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist  # control plane only (barrier, max/sum reductions)
+
+        dist.init_process_group("gloo")
+    cfg = CONFIGS[args.config]
+    n, lo, hi, G, l, k, seed, desc = cfg
+    nthreads = max(2, 16 // max(1, world))
+
+    ds, _, _ = make_dataset(cfg, nthreads)
+    eng = OverlapEngine(local)
+    eng.set_option("nb_log2", args.nb_log2)
+    shard_world, shard_rank = (world, rank) if world > 1 else (args.sim_world or 1, args.sim_rank)
+    N = ds.num_unique
+    if args.shard == "buckets":
+        eng.set_shard(shard_rank, shard_world, 0, 0)
+    else:
+        eng.set_shard(0, 1, N * shard_rank // shard_world, N * (shard_rank + 1) // shard_world)
+    t0 = time.time()
+    eng.upload(ds)
+    log(f"[bench] rank {rank}: upload {time.time() - t0:.2f}s")
+
+    def step():
+        eng.build_index(l, k)
+        eng.mark_contained()
+        return eng.find_overlaps()
+
+    # one counting pass (untimed) for the roofline's algorithmic bytes
+    eng.set_option("stats", 1)
+    rows = step()
+    cnt = eng.counters()
+    eng.set_option("stats", 0)
+    for _ in range(args.warmup):
+        step()
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    barrier()
+    dev_ms = {"index_ms": 0.0, "contained_ms": 0.0, "overlap_ms": 0.0}
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        rows = step()
+        t = eng.timings()
+        for kk in dev_ms:
+            dev_ms[kk] += t[kk]
+    t1 = time.perf_counter()
+    barrier()
+    ms_step = (t1 - t0) * 1000.0 / args.steps
+    dev_ms = {kk: v / args.steps for kk, v in dev_ms.items()}
+    edges_rank = rows // 2
+    if dist is not None:
+        import torch
+
+        tt = torch.tensor([ms_step], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        ms_step = float(tt.item())
+        ee = torch.tensor([edges_rank], dtype=torch.int64)
+        dist.all_reduce(ee, op=dist.ReduceOp.SUM)
+        edges = int(ee.item())
+    else:
+        edges = edges_rank
+    if rank != 0:
+        dist.barrier()
+        dist.destroy_process_group()
+        return
+
+    wpr = ds.packed()[0].shape[1]
+    # algorithmic bytes of one discovery launch
+    alg = (cnt["sources"] * (8 * wpr + 2) + cnt["runs"] * 8 + cnt["entries"] * 8
+           + cnt["verified"] * 8 * (wpr + 1) + cnt["rows"] * 12)
+    ov_s = dev_ms["overlap_ms"] / 1000.0
+    achieved = alg / ov_s / 1e9 if ov_s > 0 else 0.0
+    # SURVEY §8(d) per-read figure for the reference's W-probe formulation, for comparison
+    W = lo - (l - 1) - 1
+    D = rows / max(1, cnt["sources"])
+    survey_bytes = cnt["sources"] * (-(-lo // 4) + 64 + W * 16 + D * (-(-lo // 4) + 16))
+    traffic = load_pmc(args.pmc) if args.config == "c3" and world == 1 and not args.sim_world else None
+    res = {
+        "metric": "overlap edges/sec",
+        "value": edges / (ms_step / 1000.0),
+        "unit": "edges/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_step,
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "u64",
+        "data": "synthetic",
+        "config": {"workload": desc, "reads": n, "unique_reads": N, "read_len": [lo, hi], "genome_len": G,
+                   "min_overlap": l, "seed_k": k, "seed": seed,
+                   "parallelism": f"{args.shard}-shard x {shard_world}" + (" (simulated rank)" if args.sim_world else "")},
+        "reads_per_sec": N / (ms_step / 1000.0),
+        "undirected_edges": edges,
+        "device_ms": dev_ms,
+        "counters": cnt,
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "kernel": "k_discover", "alg_bytes_per_launch": alg,
+                     "survey_8d_bytes_per_launch": survey_bytes},
+    }
+    if world == 1 and not args.no_cpu_baseline and not args.sim_world:
+        try:
+            res["cpu_baseline"] = cpu_baseline(cfg, args.cpu_sample)
+        except Exception as e:  # report, never fake
+            res["cpu_baseline"] = {"value": None, "error": str(e)}
+    print(json.dumps(res), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

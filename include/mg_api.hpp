@@ -1,0 +1,177 @@
+// mg_api.hpp — drop-in C++ surface for the reference's overlap path.
+//
+// Same class names, method names and argument meaning as the reference's
+// Read / Edge / Dataset / HashTable / OverlapGraph (Read.h:31-72,
+// Edge.h:16-61, Dataset.h:18-51, HashTable.h:16-36, OverlapGraph.h:32-100 in
+// /root/reference/MetaGenomics), so main.cpp:33,45-47 compiles against it:
+//
+//     Dataset *dataSet = new Dataset(pairedEndFileNames, singleEndFileNames, l);
+//     HashTable *hashTable = new HashTable();
+//     hashTable->insertDataset(dataSet, l);              // GPU index build
+//     OverlapGraph *g = new OverlapGraph(hashTable);     // GPU discovery, deletes hashTable
+//
+// Differences, all deliberate:
+//  * errors throw mg::Error instead of MYEXIT's exit(0) (Common.h:47);
+//  * reads are stored 2-bit packed; getStringForward/Reverse decode on demand;
+//  * OverlapGraph stops at the raw edge multiset (transitive reduction,
+//    contraction, flow and scaffolding are out of scope);
+//  * HashTable/OverlapGraph run on a HIP device through include/mg_overlap.h
+//    and throw if no device is available (there is no CPU fallback).
+#ifndef MG_API_HPP_
+#define MG_API_HPP_
+
+#include <cstdint>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "mg_overlap.h"
+
+// The reference's integer names (Common.h:31-37); UINT32 is 64-bit on LP64 there.
+typedef unsigned char UINT8;
+typedef unsigned short UINT16;
+typedef unsigned long UINT32;
+typedef unsigned long long UINT64;
+typedef long long INT64;
+
+namespace mg {
+struct Error : std::runtime_error {
+  explicit Error(const std::string& s) : std::runtime_error(s) {}
+};
+struct PackedReads;
+}  // namespace mg
+
+class Dataset;
+class Edge;
+
+class Read {
+ public:
+  UINT64 superReadID = 0;      // 0 = not contained, else ID of the super read (Read.h:50)
+  bool isContainedRead = false;
+  std::string getStringForward();
+  std::string getStringReverse();
+  UINT16 getReadLength();
+  UINT64 getReadNumber() { return readNumber; }
+  UINT32 getFrequency();
+
+ private:
+  friend class Dataset;
+  const Dataset* owner = nullptr;
+  UINT64 readNumber = 0;
+};
+
+class Edge {
+ public:
+  Edge(Read* from, Read* to, UINT64 orient, UINT64 length)
+      : source(from), destination(to), overlapOrientation((UINT8)orient), overlapOffset(length) {}
+  Read* getSourceRead() { return source; }
+  Read* getDestinationRead() { return destination; }
+  UINT8 getOrientation() { return overlapOrientation; }
+  UINT64 getOverlapOffset() { return overlapOffset; }
+  Edge* getReverseEdge() { return reverseEdge; }
+  bool setReverseEdge(Edge* e) {
+    reverseEdge = e;
+    return true;
+  }
+  bool transitiveRemovalFlag = false;
+
+ private:
+  Read* source;
+  Read* destination;
+  UINT8 overlapOrientation;  // 0 = u<---<v, 1 = u<--->v, 2 = u>---<v, 3 = u>--->v
+  UINT64 overlapOffset;      // start of v relative to u
+  Edge* reverseEdge = nullptr;
+};
+
+class Dataset {
+ public:
+  std::vector<std::string> pairedEndDatasetFileNames;
+  std::vector<std::string> singleEndDatasetFileNames;
+  UINT64 shortestReadLength = ~0ULL;
+  UINT64 longestReadLength = 0;
+
+  Dataset(std::vector<std::string> pairedEndFileNames, std::vector<std::string> singleEndFileNames,
+          UINT64 minOverlap);
+  ~Dataset();
+  UINT64 getNumberOfReads() { return numberOfReads; }
+  UINT64 getNumberOfUniqueReads() { return numberOfUniqueReads; }
+  Read* getReadFromString(const std::string& read);
+  Read* getReadFromID(UINT64 ID);
+  void saveReads(std::string fileName);
+  void readMatePairsFromFile() {}  // single-end only: mate pairs are out of scope
+
+  // --- packed view (device upload) and bulk construction (bench / Python) ---
+  static Dataset* fromCodes(const uint8_t* codes, uint64_t n, uint64_t stride, const uint16_t* lens,
+                            UINT64 minOverlap, int nthreads);
+  const uint64_t* packedWords() const;
+  const uint16_t* packedLengths() const;
+  uint32_t wordsPerRead() const;
+  uint32_t frequencyOf(UINT64 id) const;
+  std::string decode(UINT64 id, bool reverse) const;
+  UINT64 minimumOverlapLength() const { return minOverlapLength; }
+
+ private:
+  Dataset() = default;
+  void finalize(mg::PackedReads&& pr);
+  mg::PackedReads* packed = nullptr;
+  std::vector<Read> reads;
+  UINT64 numberOfReads = 0, numberOfUniqueReads = 0, minOverlapLength = 0;
+};
+
+class HashTable {
+ public:
+  HashTable();
+  explicit HashTable(Dataset* d) : HashTable() { dataSet = d; }
+  ~HashTable();
+  bool insertDataset(Dataset* d, UINT64 minOverlapLength);
+  std::vector<UINT64>* getListOfReads(std::string subString);
+  UINT64 hashFunction(std::string subString);  // the reference's index function (HashTable.cpp:135-155)
+  UINT64 getHashTableSize() { return hashTableSize; }
+  UINT64 getHashStringLength() { return hashStringLength; }
+  Dataset* getDataset() { return dataSet; }
+
+  // --- device controls (not in the reference) ---
+  static void setDefaultDevice(int device);
+  static void setDefaultSeedK(uint32_t k);
+  mg_ctx* context() { return ctx; }
+
+ private:
+  Dataset* dataSet = nullptr;
+  mg_ctx* ctx = nullptr;
+  UINT64 hashTableSize = 0;
+  UINT16 hashStringLength = 0;
+  std::vector<std::vector<UINT64>*> lookups;  // lists handed out by getListOfReads
+};
+
+class OverlapGraph {
+ public:
+  OverlapGraph();
+  explicit OverlapGraph(HashTable* ht);
+  ~OverlapGraph();
+  bool buildOverlapGraphFromHashTable(HashTable* ht);
+  void markContainedReads();
+  bool insertEdge(Edge* edge);
+  bool insertEdge(Read* read1, Read* read2, UINT8 orient, UINT16 overlapOffset);
+  UINT64 getNumberOfEdges() { return numberOfEdges; }
+  UINT64 getNumberOfNodes() { return numberOfNodes; }
+  bool setDataset(Dataset* d) {
+    dataSet = d;
+    return true;
+  }
+  // graph[u] of the reference (private there): edges of read u, sorted by offset (:563)
+  const std::vector<Edge*>* getEdges(UINT64 readNumber) const;
+  // raw directed multiset as "u v orient offset" lines, sorted (checkpoint/parity dump)
+  bool saveRawEdges(const std::string& fileName) const;
+  const mg_timings& timings() const { return lastTimings; }
+
+ private:
+  Dataset* dataSet = nullptr;
+  HashTable* hashTable = nullptr;
+  std::vector<std::vector<Edge*>*>* graph = nullptr;
+  UINT64 numberOfNodes = 0, numberOfEdges = 0;
+  bool containedDone = false;
+  mg_timings lastTimings{};
+  void clear();
+};
+
+#endif  // MG_API_HPP_

@@ -1,0 +1,48 @@
+/* mg_host.h — C-ABI over the host-side Dataset mirror (metagenomics_amd/csrc/host).
+ *
+ * Dataset ingestion is not on the GPU in this round;
+ * it is the reference's Dataset semantics restated in C++ with packed reads:
+ *   readDataset  Dataset.cpp:110-193  (FASTA/FASTQ parse, upper-case)
+ *   testRead     Dataset.cpp:398-413  (only ACGT, no base >= floor(0.8 len))
+ *   canonical    Dataset.cpp:163-167  (store min(s, revcomp(s)))
+ *   sortReads    Dataset.cpp:197-202  (std::string order)
+ *   removeDupicateReads Dataset.cpp:316-345 (frequency, IDs 1..N)
+ * The result is handed to the device through mg_upload_reads_packed().
+ */
+#ifndef MG_HOST_H_
+#define MG_HOST_H_
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct mgh_dataset mgh_dataset;
+
+/* Dataset(pe, se, minOverlap) (Dataset.cpp:39-65).  Returns 0 on success,
+ * -1 on an unreadable file, -2 on an unknown format (first byte not '>'/'@'). */
+int mgh_dataset_from_files(const char* const* files, int nfiles, uint64_t min_overlap, mgh_dataset** out);
+/* Same pipeline from in-memory reads: codes[i*stride + k] in {0:A,1:C,2:G,3:T,
+ * anything else = not ACGT} for k < lens[i].  nthreads <= 0: hardware threads. */
+int mgh_dataset_from_codes(const uint8_t* codes, uint64_t n, uint64_t stride, const uint16_t* lens,
+                           uint64_t min_overlap, int nthreads, mgh_dataset** out);
+void mgh_dataset_free(mgh_dataset* ds);
+
+uint64_t mgh_num_reads(const mgh_dataset* ds);   /* Dataset::getNumberOfReads (good reads) */
+uint64_t mgh_num_unique(const mgh_dataset* ds);  /* Dataset::getNumberOfUniqueReads */
+uint64_t mgh_shortest(const mgh_dataset* ds);    /* Dataset::shortestReadLength */
+uint64_t mgh_longest(const mgh_dataset* ds);     /* Dataset::longestReadLength */
+/* Zero-copy views of the packed unique reads in ID order (ID = index + 1). */
+int mgh_packed(const mgh_dataset* ds, const uint64_t** words, const uint16_t** lens, uint32_t* words_per_read);
+/* Read::getStringForward() of read `id` into buf (NUL-terminated); returns its
+ * length, or -1 if id is out of range (Dataset.cpp:484-490). */
+int64_t mgh_read_string(const mgh_dataset* ds, uint64_t id, char* buf, uint64_t cap);
+uint32_t mgh_frequency(const mgh_dataset* ds, uint64_t id); /* Read::getFrequency */
+/* Dataset::getReadFromString (Dataset.cpp:421-455): ID of a read given either
+ * strand, 0 if absent. */
+uint64_t mgh_find_read(const mgh_dataset* ds, const char* s, uint64_t len);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MG_HOST_H_ */

@@ -1,0 +1,679 @@
+// mg_host.cpp — host-side mirror of the reference's Read / Dataset /
+// HashTable / OverlapGraph API (include/mg_api.hpp) plus the mgh_* C-ABI
+// (include/mg_host.h).  The hot path (index build, containment, overlap
+// discovery) runs on the GPU through include/mg_overlap.h; this file only
+// ingests reads (Dataset semantics) and shapes results into the reference's
+// object model.  Reference citations are relative to /root/reference/MetaGenomics.
+#include <algorithm>
+#include <atomic>
+#include <cctype>
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <iomanip>
+#include <sstream>
+#include <thread>
+
+#include "mg_api.hpp"
+#include "mg_host.h"
+
+namespace mg {
+
+// Unique reads, 2-bit packed (A0 C1 G2 T3, most significant base first), ID order.
+struct PackedReads {
+  uint32_t wpr = 1;
+  std::vector<uint64_t> words;
+  std::vector<uint16_t> lens;
+  std::vector<uint32_t> freq;
+  uint64_t n_good = 0;
+  uint64_t shortest = ~0ULL, longest = 0;
+  uint64_t n() const { return lens.size(); }
+  const uint64_t* rec(uint64_t i) const { return words.data() + i * wpr; }
+};
+
+namespace {
+
+int hw_threads(int want) {
+  int hc = (int)std::thread::hardware_concurrency();
+  if (hc <= 0) hc = 4;
+  if (want <= 0) want = hc;
+  return std::max(1, std::min(want, 64));
+}
+
+template <typename F>
+void parallel_for(uint64_t n, int nthreads, F&& fn) {
+  const int T = (int)std::min<uint64_t>((uint64_t)nthreads, std::max<uint64_t>(1, n / 4096 + 1));
+  if (T <= 1) {
+    fn(0, 0, n);
+    return;
+  }
+  std::vector<std::thread> th;
+  for (int t = 0; t < T; ++t) {
+    const uint64_t lo = n * t / T, hi = n * (t + 1) / T;
+    th.emplace_back([&fn, t, lo, hi] { fn(t, lo, hi); });
+  }
+  for (auto& x : th) x.join();
+}
+
+// One raw read in upper-case 2-bit codes; returns false if not ACGT only.
+struct Source {
+  // ASCII source
+  const char* text = nullptr;
+  const uint64_t* off = nullptr;
+  // code source
+  const uint8_t* codes = nullptr;
+  uint64_t stride = 0;
+  const uint16_t* lens = nullptr;
+  uint64_t n = 0;
+
+  uint64_t length(uint64_t i) const { return text ? off[i + 1] - off[i] : lens[i]; }
+  bool get(uint64_t i, std::vector<uint8_t>& out) const {
+    const uint64_t L = length(i);
+    out.resize(L);
+    if (text) {
+      const char* s = text + off[i];
+      for (uint64_t k = 0; k < L; ++k) {
+        switch (std::toupper((unsigned char)s[k])) {  // Dataset.cpp:158-159
+          case 'A': out[k] = 0; break;
+          case 'C': out[k] = 1; break;
+          case 'G': out[k] = 2; break;
+          case 'T': out[k] = 3; break;
+          default: return false;  // testRead: only A, C, G, T (Dataset.cpp:405-406)
+        }
+      }
+    } else {
+      const uint8_t* c = codes + i * stride;
+      for (uint64_t k = 0; k < L; ++k) {
+        if (c[k] > 3) return false;
+        out[k] = c[k];
+      }
+    }
+    return true;
+  }
+};
+
+// Dataset::testRead's 80 % rule (Dataset.cpp:409-411) on valid codes.
+bool low_complexity(const std::vector<uint8_t>& c) {
+  uint64_t cnt[4] = {0, 0, 0, 0};
+  for (uint8_t x : c) cnt[x]++;
+  const uint64_t threshold = (uint64_t)(c.size() * .8);
+  return cnt[0] >= threshold || cnt[1] >= threshold || cnt[2] >= threshold || cnt[3] >= threshold;
+}
+
+void pack_codes(const uint8_t* c, uint64_t L, uint32_t wpr, uint64_t* dst) {
+  for (uint32_t w = 0; w < wpr; ++w) {
+    uint64_t x = 0;
+    for (uint32_t k = 0; k < 32; ++k) {
+      const uint64_t p = (uint64_t)w * 32 + k;
+      x = (x << 2) | (p < L ? c[p] : 0);
+    }
+    dst[w] = x;
+  }
+}
+
+// std::string order on packed reads: words (zero padded) then length.
+inline int cmp_packed(const uint64_t* a, uint16_t la, const uint64_t* b, uint16_t lb, uint32_t wpr) {
+  for (uint32_t k = 0; k < wpr; ++k)
+    if (a[k] != b[k]) return a[k] < b[k] ? -1 : 1;
+  return la == lb ? 0 : (la < lb ? -1 : 1);
+}
+
+template <typename Cmp>
+void parallel_sort(std::vector<uint64_t>& idx, int nthreads, Cmp cmp) {
+  const uint64_t n = idx.size();
+  int T = 1;
+  while (T * 2 <= nthreads && n / (uint64_t)(T * 2) > 65536) T *= 2;
+  if (T == 1) {
+    std::sort(idx.begin(), idx.end(), cmp);
+    return;
+  }
+  std::vector<uint64_t> bounds(T + 1);
+  for (int t = 0; t <= T; ++t) bounds[t] = n * t / T;
+  {
+    std::vector<std::thread> th;
+    for (int t = 0; t < T; ++t)
+      th.emplace_back([&, t] { std::sort(idx.begin() + bounds[t], idx.begin() + bounds[t + 1], cmp); });
+    for (auto& x : th) x.join();
+  }
+  std::vector<uint64_t> tmp(n);
+  for (int width = 1; width < T; width *= 2) {
+    std::vector<std::thread> th;
+    for (int t = 0; t < T; t += 2 * width) {
+      const uint64_t lo = bounds[t], mid = bounds[std::min(t + width, T)], hi = bounds[std::min(t + 2 * width, T)];
+      th.emplace_back([&, lo, mid, hi] {
+        std::merge(idx.begin() + lo, idx.begin() + mid, idx.begin() + mid, idx.begin() + hi, tmp.begin() + lo, cmp);
+      });
+    }
+    for (auto& x : th) x.join();
+    idx.swap(tmp);
+  }
+}
+
+// readDataset's per-read body + sortReads + removeDupicateReads
+// (Dataset.cpp:158-181, 197-202, 316-345) over any read source.
+PackedReads ingest(const Source& src, uint64_t min_overlap, int nthreads) {
+  PackedReads pr;
+  uint64_t maxlen = 0;
+  for (uint64_t i = 0; i < src.n; ++i) maxlen = std::max(maxlen, src.length(i));
+  pr.wpr = (uint32_t)std::max<uint64_t>(1, (maxlen + 31) / 32);
+  const int T = hw_threads(nthreads);
+  struct Part {
+    std::vector<uint64_t> words;
+    std::vector<uint16_t> lens;
+    uint64_t shortest = ~0ULL, longest = 0;
+  };
+  std::vector<Part> parts(T);
+  parallel_for(src.n, T, [&](int t, uint64_t lo, uint64_t hi) {
+    Part& P = parts[t];
+    std::vector<uint8_t> c, rc;
+    for (uint64_t i = lo; i < hi; ++i) {
+      const uint64_t L = src.length(i);
+      if (!(L > min_overlap)) continue;  // Dataset.cpp:160
+      if (L > 65535) continue;           // Read::getReadLength is UINT16
+      if (!src.get(i, c) || low_complexity(c)) continue;
+      rc.resize(L);
+      for (uint64_t k = 0; k < L; ++k) rc[k] = (uint8_t)(3 - c[L - 1 - k]);  // Dataset.cpp:463-475
+      // store the lexicographically smaller strand (Dataset.cpp:164-167)
+      const bool fwd = std::lexicographical_compare(c.begin(), c.end(), rc.begin(), rc.end());
+      const std::vector<uint8_t>& s = fwd ? c : rc;
+      const size_t at = P.words.size();
+      P.words.resize(at + pr.wpr);
+      pack_codes(s.data(), L, pr.wpr, P.words.data() + at);
+      P.lens.push_back((uint16_t)L);
+      P.shortest = std::min(P.shortest, L);
+      P.longest = std::max(P.longest, L);
+    }
+  });
+  uint64_t ngood = 0;
+  for (auto& P : parts) {
+    ngood += P.lens.size();
+    pr.shortest = std::min(pr.shortest, P.shortest);
+    pr.longest = std::max(pr.longest, P.longest);
+  }
+  pr.n_good = ngood;
+  std::vector<uint64_t> all_words;
+  std::vector<uint16_t> all_lens;
+  all_words.reserve(ngood * pr.wpr);
+  all_lens.reserve(ngood);
+  for (auto& P : parts) {
+    all_words.insert(all_words.end(), P.words.begin(), P.words.end());
+    all_lens.insert(all_lens.end(), P.lens.begin(), P.lens.end());
+    std::vector<uint64_t>().swap(P.words);
+  }
+  // sort (std::string order) by index; the first word decides almost always
+  std::vector<uint64_t> idx(ngood);
+  for (uint64_t i = 0; i < ngood; ++i) idx[i] = i;
+  const uint32_t wpr = pr.wpr;
+  const uint64_t* W = all_words.data();
+  const uint16_t* Ls = all_lens.data();
+  parallel_sort(idx, T, [W, Ls, wpr](uint64_t a, uint64_t b) {
+    return cmp_packed(W + a * wpr, Ls[a], W + b * wpr, Ls[b], wpr) < 0;
+  });
+  // dedup adjacent equal reads; frequency = multiplicity; ID = rank (Dataset.cpp:321-339)
+  uint64_t nu = 0;
+  for (uint64_t k = 0; k < ngood; ++k)
+    if (k == 0 || cmp_packed(W + idx[k - 1] * wpr, Ls[idx[k - 1]], W + idx[k] * wpr, Ls[idx[k]], wpr) != 0) nu++;
+  pr.words.resize(nu * wpr);
+  pr.lens.resize(nu);
+  pr.freq.assign(nu, 0);
+  int64_t u = -1;
+  for (uint64_t k = 0; k < ngood; ++k) {
+    const uint64_t i = idx[k];
+    if (k == 0 || cmp_packed(W + idx[k - 1] * wpr, Ls[idx[k - 1]], W + i * wpr, Ls[i], wpr) != 0) {
+      ++u;
+      std::memcpy(pr.words.data() + u * wpr, W + i * wpr, wpr * sizeof(uint64_t));
+      pr.lens[u] = Ls[i];
+    }
+    pr.freq[u]++;
+  }
+  return pr;
+}
+
+// Dataset::readDataset record splitting (Dataset.cpp:123-182): FASTA = header
+// line + everything up to the next '>' with '\n' removed; FASTQ = 4 lines, the
+// sequence is the 2nd.  Appends raw sequences to text/off.
+int parse_file(const std::string& path, std::string& text, std::vector<uint64_t>& off) {
+  std::ifstream f(path, std::ios::binary);
+  if (!f) return -1;
+  std::string buf((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
+  if (buf.empty() || (buf[0] != '>' && buf[0] != '@')) return -2;  // Dataset.cpp:130-135
+  const size_t n = buf.size();
+  size_t p = 0;
+  if (buf[0] == '>') {
+    while (p < n) {
+      while (p < n && buf[p] != '\n') p++;
+      if (p < n) p++;
+      const size_t nb = buf.find('>', p);
+      const size_t e = nb == std::string::npos ? n : nb;
+      for (size_t k = p; k < e; ++k)
+        if (buf[k] != '\n') text.push_back(buf[k]);
+      off.push_back(text.size());
+      p = e == n ? n : e + 1;
+    }
+  } else {
+    uint64_t line = 0;
+    while (p < n) {
+      size_t e = buf.find('\n', p);
+      if (e == std::string::npos) e = n;
+      if (line % 4 == 1) {
+        text.append(buf, p, e - p);
+        off.push_back(text.size());
+      }
+      p = e + 1;
+      line++;
+    }
+  }
+  return 0;
+}
+
+std::string decode_packed(const uint64_t* w, uint16_t L, bool reverse) {
+  static const char A[4] = {'A', 'C', 'G', 'T'};
+  std::string s(L, 'A');
+  for (uint32_t k = 0; k < L; ++k) {
+    const uint32_t c = (uint32_t)(w[k >> 5] >> (62 - 2 * (k & 31))) & 3u;
+    if (reverse)
+      s[L - 1 - k] = A[3 - c];
+    else
+      s[k] = A[c];
+  }
+  return s;
+}
+
+int g_default_device = 0;
+uint32_t g_default_seed_k = 0;
+
+// getPrimeLargerThanNumber is a fixed prime list in the reference
+// (HashTable.cpp:20-29); the device index is a power-of-two directory, whose
+// size is what getHashTableSize reports here.
+uint64_t directory_size(uint64_t n) {
+  uint32_t nbl = 10;
+  while (nbl < 30 && (1ull << nbl) < n) nbl++;
+  return 1ull << nbl;
+}
+
+[[noreturn]] void fail(mg_ctx* ctx, const char* what) {
+  throw mg::Error(std::string(what) + ": " + (ctx ? mg_last_error(ctx) : "no context"));
+}
+
+}  // namespace
+}  // namespace mg
+
+// ================================================================== Read ====
+std::string Read::getStringForward() { return owner->decode(readNumber, false); }
+std::string Read::getStringReverse() { return owner->decode(readNumber, true); }
+UINT16 Read::getReadLength() { return owner->packedLengths()[readNumber - 1]; }
+UINT32 Read::getFrequency() { return owner->frequencyOf(readNumber); }
+
+// =============================================================== Dataset ====
+Dataset::Dataset(std::vector<std::string> pe, std::vector<std::string> se, UINT64 minOverlap)
+    : pairedEndDatasetFileNames(pe), singleEndDatasetFileNames(se), minOverlapLength(minOverlap) {
+  std::string text;
+  std::vector<uint64_t> off(1, 0);
+  std::vector<std::string> files(pe);
+  files.insert(files.end(), se.begin(), se.end());  // paired-end first (Dataset.cpp:52-60)
+  for (const auto& f : files) {
+    const int rc = mg::parse_file(f, text, off);
+    if (rc == -1) throw mg::Error("Unable to open file: " + f);
+    if (rc == -2) throw mg::Error("Unknown input file format: " + f);
+  }
+  mg::Source src;
+  src.text = text.data();
+  src.off = off.data();
+  src.n = off.size() - 1;
+  finalize(mg::ingest(src, minOverlap, 0));
+}
+
+Dataset* Dataset::fromCodes(const uint8_t* codes, uint64_t n, uint64_t stride, const uint16_t* lens,
+                            UINT64 minOverlap, int nthreads) {
+  mg::Source src;
+  src.codes = codes;
+  src.stride = stride;
+  src.lens = lens;
+  src.n = n;
+  Dataset* d = new Dataset();
+  d->minOverlapLength = minOverlap;
+  d->finalize(mg::ingest(src, minOverlap, nthreads));
+  return d;
+}
+
+void Dataset::finalize(mg::PackedReads&& pr) {
+  packed = new mg::PackedReads(std::move(pr));
+  numberOfReads = packed->n_good;
+  numberOfUniqueReads = packed->n();
+  shortestReadLength = packed->shortest;
+  longestReadLength = packed->longest;
+  reads.resize(numberOfUniqueReads);
+  for (UINT64 i = 0; i < numberOfUniqueReads; ++i) {
+    reads[i].owner = this;
+    reads[i].readNumber = i + 1;
+  }
+}
+
+Dataset::~Dataset() { delete packed; }
+
+const uint64_t* Dataset::packedWords() const { return packed->words.data(); }
+const uint16_t* Dataset::packedLengths() const { return packed->lens.data(); }
+uint32_t Dataset::wordsPerRead() const { return packed->wpr; }
+uint32_t Dataset::frequencyOf(UINT64 id) const { return packed->freq[id - 1]; }
+std::string Dataset::decode(UINT64 id, bool reverse) const {
+  return mg::decode_packed(packed->rec(id - 1), packed->lens[id - 1], reverse);
+}
+
+Read* Dataset::getReadFromID(UINT64 ID) {
+  if (ID < 1 || ID > numberOfUniqueReads) {  // Dataset.cpp:484-490
+    std::ostringstream ss;
+    ss << "ID " << ID << " out of bound.";
+    throw mg::Error(ss.str());
+  }
+  return &reads[ID - 1];
+}
+
+Read* Dataset::getReadFromString(const std::string& read) {
+  // canonical strand, then binary search (Dataset.cpp:421-455)
+  std::string rc(read.rbegin(), read.rend());
+  for (char& c : rc) c = (c & 0x02) ? (char)(c ^ 0x04) : (char)(c ^ 0x15);
+  const std::string& key = read.compare(rc) < 0 ? read : rc;
+  std::vector<uint8_t> codes(key.size());
+  for (size_t k = 0; k < key.size(); ++k) {
+    switch (key[k]) {
+      case 'A': codes[k] = 0; break;
+      case 'C': codes[k] = 1; break;
+      case 'G': codes[k] = 2; break;
+      case 'T': codes[k] = 3; break;
+      default: throw mg::Error("String not found in Dataset: " + read);
+    }
+  }
+  const uint32_t wpr = packed->wpr;
+  if (key.size() > 32ull * wpr || key.size() > 65535) throw mg::Error("String not found in Dataset: " + read);
+  std::vector<uint64_t> q(wpr);
+  mg::pack_codes(codes.data(), key.size(), wpr, q.data());
+  uint64_t lo = 0, hi = numberOfUniqueReads;
+  while (lo < hi) {
+    const uint64_t mid = (lo + hi) / 2;
+    const int c = mg::cmp_packed(packed->rec(mid), packed->lens[mid], q.data(), (uint16_t)key.size(), wpr);
+    if (c == 0) return &reads[mid];
+    if (c < 0)
+      lo = mid + 1;
+    else
+      hi = mid;
+  }
+  throw mg::Error("String not found in Dataset: " + read);
+}
+
+void Dataset::saveReads(std::string fileName) {
+  // Dataset.cpp:71-90 format
+  std::ofstream out(fileName.c_str());
+  if (!out) throw mg::Error("Unable to open file: " + fileName);
+  for (UINT64 i = 1; i <= numberOfUniqueReads; ++i) {
+    Read* r = &reads[i - 1];
+    out << std::setw(10) << i << (r->superReadID ? " Contained in " : " Noncontained ") << std::setw(10)
+        << r->superReadID << " " << r->getStringForward() << "\n";
+  }
+}
+
+// ============================================================= HashTable ====
+void HashTable::setDefaultDevice(int device) { mg::g_default_device = device; }
+void HashTable::setDefaultSeedK(uint32_t k) { mg::g_default_seed_k = k; }
+
+HashTable::HashTable() {}
+
+HashTable::~HashTable() {
+  for (auto* v : lookups) delete v;
+  if (ctx) mg_destroy(ctx);
+}
+
+bool HashTable::insertDataset(Dataset* d, UINT64 minOverlapLength) {
+  // HashTable::insertDataset (HashTable.cpp:50-80) on the device
+  dataSet = d;
+  hashStringLength = (UINT16)(minOverlapLength - 1);
+  hashTableSize = mg::directory_size(d->getNumberOfUniqueReads());
+  if (!ctx) {
+    const int rc = mg_create(&ctx, mg::g_default_device);
+    if (rc) {
+      ctx = nullptr;
+      throw mg::Error(rc == -3 ? "no HIP device available (the overlap path has no CPU fallback)"
+                               : "mg_create failed");
+    }
+  }
+  if (mg_upload_reads_packed(ctx, d->packedWords(), d->packedLengths(), d->getNumberOfUniqueReads(),
+                             d->wordsPerRead()))
+    mg::fail(ctx, "upload");
+  if (mg_build_index(ctx, (uint32_t)minOverlapLength, mg::g_default_seed_k)) mg::fail(ctx, "index");
+  return true;
+}
+
+std::vector<UINT64>* HashTable::getListOfReads(std::string subString) {
+  std::vector<UINT64>* v = new std::vector<UINT64>();
+  lookups.push_back(v);
+  uint64_t n = 0;
+  std::vector<uint64_t> buf(64);
+  for (;;) {
+    if (mg_lookup_key(ctx, subString.data(), (uint32_t)subString.size(), buf.data(), buf.size(), &n))
+      mg::fail(ctx, "getListOfReads");
+    if (n <= buf.size()) break;
+    buf.resize(n);
+  }
+  v->assign(buf.begin(), buf.begin() + n);
+  return v;
+}
+
+UINT64 HashTable::hashFunction(std::string subString) {
+  // the reference's index function (HashTable.cpp:135-155): 2-bit codes
+  // (c >> 1) & 3, first 32 characters into sum1, the rest into sum2, both
+  // seeded with 1; product of residues modulo the table size
+  UINT64 sum1 = 1, sum2 = 1;
+  for (size_t i = 0; i < subString.size(); ++i) {
+    const UINT64 c = ((UINT64)(int)subString[i] >> 1) & 3ULL;
+    if (i < 32)
+      sum1 = (sum1 << 2) | c;
+    else
+      sum2 = (sum2 << 2) | c;
+  }
+  const UINT64 P = hashTableSize ? hashTableSize : 1;
+  return ((sum1 % P) * (sum2 % P)) % P;
+}
+
+// ========================================================== OverlapGraph ====
+OverlapGraph::OverlapGraph() {}
+
+OverlapGraph::OverlapGraph(HashTable* ht) { buildOverlapGraphFromHashTable(ht); }
+
+OverlapGraph::~OverlapGraph() { clear(); }
+
+void OverlapGraph::clear() {
+  if (!graph) return;
+  for (auto* lst : *graph) {
+    for (auto* e : *lst) delete e;
+    delete lst;
+  }
+  delete graph;
+  graph = nullptr;
+}
+
+void OverlapGraph::markContainedReads() {
+  // OverlapGraph.cpp:225-290 on the device; superReadID written back to Read
+  mg_ctx* ctx = hashTable->context();
+  const UINT64 N = dataSet->getNumberOfUniqueReads();
+  std::vector<uint32_t> super(N + 1, 0);
+  if (mg_mark_contained(ctx, super.data())) mg::fail(ctx, "markContainedReads");
+  for (UINT64 i = 1; i <= N; ++i) {
+    Read* r = dataSet->getReadFromID(i);
+    r->superReadID = super[i];
+    r->isContainedRead = super[i] != 0;
+  }
+  containedDone = true;
+}
+
+bool OverlapGraph::insertEdge(Edge* edge) {
+  // OverlapGraph.cpp:390-400
+  const UINT64 id = edge->getSourceRead()->getReadNumber();
+  if ((*graph)[id]->empty()) numberOfNodes++;
+  (*graph)[id]->push_back(edge);
+  numberOfEdges++;
+  return true;
+}
+
+bool OverlapGraph::insertEdge(Read* read1, Read* read2, UINT8 orient, UINT16 overlapOffset) {
+  // OverlapGraph.cpp:407-419, twin orientation :841-855
+  Edge* e1 = new Edge(read1, read2, orient, overlapOffset);
+  const UINT16 rev = (UINT16)(read2->getReadLength() + overlapOffset - read1->getReadLength());
+  const UINT8 tw = orient == 0 ? 3 : (orient == 3 ? 0 : orient);
+  Edge* e2 = new Edge(read2, read1, tw, rev);
+  e1->setReverseEdge(e2);
+  e2->setReverseEdge(e1);
+  insertEdge(e1);
+  insertEdge(e2);
+  return true;
+}
+
+bool OverlapGraph::buildOverlapGraphFromHashTable(HashTable* ht) {
+  // OverlapGraph.cpp:107-218 up to the end of edge discovery: containment,
+  // then every insertEdge of the exploration, on the device
+  clear();
+  hashTable = ht;
+  dataSet = ht->getDataset();
+  numberOfNodes = numberOfEdges = 0;
+  const UINT64 N = dataSet->getNumberOfUniqueReads();
+  graph = new std::vector<std::vector<Edge*>*>();
+  graph->reserve(N + 1);
+  for (UINT64 i = 0; i <= N; ++i) graph->push_back(new std::vector<Edge*>());
+  markContainedReads();
+  mg_ctx* ctx = ht->context();
+  uint64_t nrows = 0;
+  if (mg_find_overlaps(ctx, &nrows)) mg::fail(ctx, "buildOverlapGraphFromHashTable");
+  std::vector<mg_edge> rows(nrows);
+  uint64_t got = 0;
+  if (mg_copy_rows(ctx, rows.data(), nrows, &got)) mg::fail(ctx, "copy rows");
+  mg_get_timings(ctx, &lastTimings);
+  // rows come in (edge, twin) pairs, as insertEdge(Read*,...) creates them
+  for (uint64_t k = 0; k + 1 < got; k += 2) {
+    Read* u = dataSet->getReadFromID(rows[k].src);
+    Read* v = dataSet->getReadFromID(rows[k].dst);
+    Edge* e1 = new Edge(u, v, rows[k].orient, rows[k].offset);
+    Edge* e2 = new Edge(v, u, rows[k + 1].orient, rows[k + 1].offset);
+    e1->setReverseEdge(e2);
+    e2->setReverseEdge(e1);
+    insertEdge(e1);
+    insertEdge(e2);
+  }
+  for (UINT64 i = 1; i <= N; ++i) {  // :562-563
+    auto* lst = (*graph)[i];
+    std::stable_sort(lst->begin(), lst->end(),
+                     [](Edge* a, Edge* b) { return a->getOverlapOffset() < b->getOverlapOffset(); });
+  }
+  delete ht;  // the graph owns and frees the table (:210)
+  hashTable = nullptr;
+  return true;
+}
+
+const std::vector<Edge*>* OverlapGraph::getEdges(UINT64 readNumber) const {
+  if (!graph || readNumber >= graph->size()) return nullptr;
+  return (*graph)[readNumber];
+}
+
+bool OverlapGraph::saveRawEdges(const std::string& fileName) const {
+  if (!graph) return false;
+  struct Row {
+    UINT64 u, v, o, off;
+  };
+  std::vector<Row> all;
+  for (size_t u = 1; u < graph->size(); ++u)
+    for (Edge* e : *(*graph)[u])
+      all.push_back({e->getSourceRead()->getReadNumber(), e->getDestinationRead()->getReadNumber(),
+                     e->getOrientation(), e->getOverlapOffset()});
+  std::sort(all.begin(), all.end(), [](const Row& a, const Row& b) {
+    if (a.u != b.u) return a.u < b.u;
+    if (a.v != b.v) return a.v < b.v;
+    if (a.o != b.o) return a.o < b.o;
+    return a.off < b.off;
+  });
+  FILE* f = std::fopen(fileName.c_str(), "w");
+  if (!f) return false;
+  for (const Row& r : all) std::fprintf(f, "%llu %llu %llu %llu\n", r.u, r.v, r.o, r.off);
+  std::fclose(f);
+  return true;
+}
+
+// ================================================================ C-ABI ====
+extern "C" {
+
+struct mgh_dataset {
+  Dataset* d;
+};
+
+int mgh_dataset_from_files(const char* const* files, int nfiles, uint64_t min_overlap, mgh_dataset** out) {
+  if (!out) return -3;
+  *out = nullptr;
+  std::vector<std::string> se;
+  for (int i = 0; i < nfiles; ++i) {
+    std::ifstream f(files[i]);
+    if (!f) return -1;
+    int c = f.peek();
+    if (c != '>' && c != '@') return -2;
+    se.emplace_back(files[i]);
+  }
+  try {
+    *out = new mgh_dataset{new Dataset({}, se, min_overlap)};
+  } catch (const std::exception&) {
+    return -1;
+  }
+  return 0;
+}
+
+int mgh_dataset_from_codes(const uint8_t* codes, uint64_t n, uint64_t stride, const uint16_t* lens,
+                           uint64_t min_overlap, int nthreads, mgh_dataset** out) {
+  if (!out) return -3;
+  try {
+    *out = new mgh_dataset{Dataset::fromCodes(codes, n, stride, lens, min_overlap, nthreads)};
+  } catch (const std::exception&) {
+    *out = nullptr;
+    return -1;
+  }
+  return 0;
+}
+
+void mgh_dataset_free(mgh_dataset* ds) {
+  if (!ds) return;
+  delete ds->d;
+  delete ds;
+}
+
+uint64_t mgh_num_reads(const mgh_dataset* ds) { return ds ? ds->d->getNumberOfReads() : 0; }
+uint64_t mgh_num_unique(const mgh_dataset* ds) { return ds ? ds->d->getNumberOfUniqueReads() : 0; }
+uint64_t mgh_shortest(const mgh_dataset* ds) { return ds ? ds->d->shortestReadLength : 0; }
+uint64_t mgh_longest(const mgh_dataset* ds) { return ds ? ds->d->longestReadLength : 0; }
+
+int mgh_packed(const mgh_dataset* ds, const uint64_t** words, const uint16_t** lens, uint32_t* wpr) {
+  if (!ds) return -1;
+  if (words) *words = ds->d->packedWords();
+  if (lens) *lens = ds->d->packedLengths();
+  if (wpr) *wpr = ds->d->wordsPerRead();
+  return 0;
+}
+
+int64_t mgh_read_string(const mgh_dataset* ds, uint64_t id, char* buf, uint64_t cap) {
+  if (!ds || id < 1 || id > ds->d->getNumberOfUniqueReads()) return -1;
+  const std::string s = ds->d->decode(id, false);
+  if (buf && cap) {
+    const uint64_t c = std::min<uint64_t>(cap - 1, s.size());
+    std::memcpy(buf, s.data(), c);
+    buf[c] = 0;
+  }
+  return (int64_t)s.size();
+}
+
+uint32_t mgh_frequency(const mgh_dataset* ds, uint64_t id) {
+  if (!ds || id < 1 || id > ds->d->getNumberOfUniqueReads()) return 0;
+  return ds->d->frequencyOf(id);
+}
+
+uint64_t mgh_find_read(const mgh_dataset* ds, const char* s, uint64_t len) {
+  if (!ds) return 0;
+  try {
+    return ds->d->getReadFromString(std::string(s, len))->getReadNumber();
+  } catch (const std::exception&) {
+    return 0;
+  }
+}
+
+}  // extern "C"

@@ -1,0 +1,70 @@
+// mg_overlap — command-line driver with main.cpp's argument surface
+// (main.cpp:117-184: -se/-pe <n> <files...>, -f <prefix>, -l <minOverlap>)
+// running the hot path of main.cpp:33,45-48 on the GPU:
+//   Dataset -> HashTable::insertDataset -> OverlapGraph(ht) -> saveReads
+// and writing the raw directed edge multiset to <prefix>.edges (sorted
+// "u v orient offset" lines).  Extra flags: -k <seed k>, -d <device>.
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "mg_api.hpp"
+
+static void usage() {
+  std::fprintf(stderr,
+               "Usage: mg_overlap [-pe n f1..fn] [-se n f1..fn] -f prefix -l minOverlap [-k seedK] [-d device]\n");
+}
+
+int main(int argc, char** argv) {
+  std::vector<std::string> pe, se;
+  std::string prefix;
+  unsigned long long l = 0;
+  int k = 0, dev = 0;
+  for (int i = 1; i < argc; ++i) {
+    std::string a = argv[i];
+    if ((a == "-pe" || a == "-se") && i + 1 < argc) {
+      int n = std::atoi(argv[++i]);
+      for (int j = 0; j < n && i + 1 < argc; ++j) (a == "-pe" ? pe : se).push_back(argv[++i]);
+    } else if (a == "-f" && i + 1 < argc) {
+      prefix = argv[++i];
+    } else if (a == "-l" && i + 1 < argc) {
+      l = std::strtoull(argv[++i], nullptr, 10);
+    } else if (a == "-k" && i + 1 < argc) {
+      k = std::atoi(argv[++i]);
+    } else if (a == "-d" && i + 1 < argc) {
+      dev = std::atoi(argv[++i]);
+    } else {
+      usage();
+      return (a == "-h" || a == "--help") ? 0 : 1;
+    }
+  }
+  if (l < 2 || prefix.empty() || (pe.empty() && se.empty())) {
+    usage();
+    return 1;
+  }
+  try {
+    HashTable::setDefaultDevice(dev);
+    HashTable::setDefaultSeedK((uint32_t)k);
+    Dataset* ds = new Dataset(pe, se, l);
+    HashTable* ht = new HashTable();
+    ht->insertDataset(ds, l);
+    OverlapGraph* g = new OverlapGraph(ht);  // deletes ht
+    ds->saveReads(prefix + "_sortedReads.fasta");
+    g->saveRawEdges(prefix + ".edges");
+    const mg_timings& t = g->timings();
+    std::printf(
+        "{\"reads\": %llu, \"unique_reads\": %llu, \"nodes\": %llu, \"directed_edges\": %llu, "
+        "\"undirected_edges\": %llu, \"index_ms\": %.3f, \"contained_ms\": %.3f, \"overlap_ms\": %.3f}\n",
+        (unsigned long long)ds->getNumberOfReads(), (unsigned long long)ds->getNumberOfUniqueReads(),
+        (unsigned long long)g->getNumberOfNodes(), (unsigned long long)g->getNumberOfEdges(),
+        (unsigned long long)g->getNumberOfEdges() / 2, t.index_ms, t.contained_ms, t.overlap_ms);
+    delete g;
+    delete ds;
+  } catch (const std::exception& e) {
+    std::fprintf(stderr, "mg_overlap: %s\n", e.what());
+    return 2;
+  }
+  return 0;
+}

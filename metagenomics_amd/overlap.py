@@ -1,0 +1,301 @@
+"""Python binding of the in-tree native library ``metagenomics_amd/lib/libmgovl.so``.
+
+Thin ctypes layer over the C-ABI in ``include/mg_overlap.h`` (device hot path)
+and ``include/mg_host.h`` (host Dataset mirror).  There is no Python or CPU
+implementation of the hot path here: without the library, or without a HIP
+device, every call raises.  Used by tests/ and bench.py.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from typing import Iterable, Sequence
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libmgovl.so")
+
+EDGE_DTYPE = np.dtype([("src", "<u4"), ("dst", "<u4"), ("offset", "<u2"), ("orient", "u1"), ("flags", "u1")])
+
+
+class MgError(RuntimeError):
+    pass
+
+
+class _Timings(C.Structure):
+    _fields_ = [("pack_ms", C.c_float), ("index_ms", C.c_float), ("contained_ms", C.c_float),
+                ("overlap_ms", C.c_float), ("total_ms", C.c_float)]
+
+
+class _Counters(C.Structure):
+    _fields_ = [("sources", C.c_uint64), ("runs", C.c_uint64), ("entries", C.c_uint64),
+                ("verified", C.c_uint64), ("rows", C.c_uint64)]
+
+
+_lib = None
+
+
+def lib() -> C.CDLL:
+    """Load the native library (raises MgError if it was not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise MgError(f"native library missing: {LIB_PATH} (run __graft_entry__.build())")
+    L = C.CDLL(LIB_PATH)
+    u64, u32, i32, i64 = C.c_uint64, C.c_uint32, C.c_int, C.c_int64
+    vp, P = C.c_void_p, C.POINTER
+    sig = {
+        "mg_create": (i32, [P(vp), i32]),
+        "mg_destroy": (None, [vp]),
+        "mg_last_error": (C.c_char_p, [vp]),
+        "mg_device_count": (i32, []),
+        "mg_upload_reads_packed": (i32, [vp, vp, vp, u64, u32]),
+        "mg_upload_reads_ascii": (i32, [vp, C.c_char_p, vp, u64]),
+        "mg_num_reads": (u64, [vp]),
+        "mg_download_reads_packed": (i32, [vp, vp, vp, P(u32)]),
+        "mg_build_index": (i32, [vp, u32, u32]),
+        "mg_lookup_key": (i32, [vp, C.c_char_p, u32, vp, u64, P(u64)]),
+        "mg_mark_contained": (i32, [vp, vp]),
+        "mg_find_overlaps": (i32, [vp, P(u64)]),
+        "mg_copy_rows": (i32, [vp, vp, u64, P(u64)]),
+        "mg_set_shard": (i32, [vp, u32, u32, u64, u64]),
+        "mg_get_timings": (i32, [vp, P(_Timings)]),
+        "mg_get_counters": (i32, [vp, P(_Counters)]),
+        "mg_set_option": (i32, [vp, C.c_char_p, i64]),
+        "mg_stream": (vp, [vp]),
+        "mgh_dataset_from_files": (i32, [P(C.c_char_p), i32, u64, P(vp)]),
+        "mgh_dataset_from_codes": (i32, [vp, u64, u64, vp, u64, i32, P(vp)]),
+        "mgh_dataset_free": (None, [vp]),
+        "mgh_num_reads": (u64, [vp]),
+        "mgh_num_unique": (u64, [vp]),
+        "mgh_shortest": (u64, [vp]),
+        "mgh_longest": (u64, [vp]),
+        "mgh_packed": (i32, [vp, P(vp), P(vp), P(u32)]),
+        "mgh_read_string": (i64, [vp, u64, C.c_char_p, u64]),
+        "mgh_frequency": (u32, [vp, u64]),
+        "mgh_find_read": (u64, [vp, C.c_char_p, u64]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = L
+    return L
+
+
+def device_count() -> int:
+    return int(lib().mg_device_count())
+
+
+def _ptr(a: np.ndarray) -> C.c_void_p:
+    return C.c_void_p(a.ctypes.data)
+
+
+class Dataset:
+    """Host Dataset mirror (Dataset.cpp:39-65 semantics), packed reads in ID order."""
+
+    def __init__(self, handle: C.c_void_p, keepalive=None):
+        self._h = handle
+        self._keep = keepalive
+
+    @classmethod
+    def from_files(cls, files: Sequence[str], min_overlap: int) -> "Dataset":
+        arr = (C.c_char_p * len(files))(*[f.encode() for f in files])
+        h = C.c_void_p()
+        rc = lib().mgh_dataset_from_files(arr, len(files), min_overlap, C.byref(h))
+        if rc:
+            raise MgError(f"Dataset from {list(files)} failed ({'unreadable' if rc == -1 else 'unknown format'})")
+        return cls(h)
+
+    @classmethod
+    def from_codes(cls, codes: np.ndarray, lens: np.ndarray, min_overlap: int, nthreads: int = 0) -> "Dataset":
+        codes = np.ascontiguousarray(codes, dtype=np.uint8)
+        lens = np.ascontiguousarray(lens, dtype=np.uint16)
+        n = codes.shape[0]
+        stride = codes.shape[1] if codes.ndim == 2 else 0
+        h = C.c_void_p()
+        rc = lib().mgh_dataset_from_codes(_ptr(codes), n, stride, _ptr(lens), min_overlap, nthreads, C.byref(h))
+        if rc:
+            raise MgError("Dataset.from_codes failed")
+        return cls(h)
+
+    @classmethod
+    def from_strings(cls, seqs: Iterable[str], min_overlap: int) -> "Dataset":
+        seqs = list(seqs)
+        maxlen = max((len(s) for s in seqs), default=1)
+        table = np.full(256, 4, dtype=np.uint8)
+        for ch, v in zip(b"ACGTacgt", [0, 1, 2, 3, 0, 1, 2, 3]):
+            table[ch] = v
+        codes = np.full((len(seqs), max(maxlen, 1)), 4, dtype=np.uint8)
+        lens = np.zeros(len(seqs), dtype=np.uint16)
+        for i, s in enumerate(seqs):
+            b = np.frombuffer(s.encode(), dtype=np.uint8)
+            codes[i, : len(b)] = table[b]
+            lens[i] = len(b)
+        return cls.from_codes(codes, lens, min_overlap)
+
+    def __del__(self):
+        if getattr(self, "_h", None) and _lib is not None:
+            _lib.mgh_dataset_free(self._h)
+            self._h = None
+
+    @property
+    def num_unique(self) -> int:
+        return int(lib().mgh_num_unique(self._h))
+
+    @property
+    def num_reads(self) -> int:
+        return int(lib().mgh_num_reads(self._h))
+
+    @property
+    def shortest(self) -> int:
+        return int(lib().mgh_shortest(self._h))
+
+    @property
+    def longest(self) -> int:
+        return int(lib().mgh_longest(self._h))
+
+    def packed(self):
+        """(words [N, wpr] uint64, lens [N] uint16) views, ID order."""
+        w, l, wpr = C.c_void_p(), C.c_void_p(), C.c_uint32()
+        lib().mgh_packed(self._h, C.byref(w), C.byref(l), C.byref(wpr))
+        n = self.num_unique
+        if n == 0:
+            return np.zeros((0, wpr.value), np.uint64), np.zeros(0, np.uint16)
+        words = np.ctypeslib.as_array(C.cast(w, C.POINTER(C.c_uint64)), shape=(n * wpr.value,))
+        lens = np.ctypeslib.as_array(C.cast(l, C.POINTER(C.c_uint16)), shape=(n,))
+        return words.reshape(n, wpr.value), lens
+
+    def read(self, rid: int) -> str:
+        n = lib().mgh_read_string(self._h, rid, None, 0)
+        if n < 0:
+            raise MgError(f"ID {rid} out of bound.")
+        buf = C.create_string_buffer(n + 1)
+        lib().mgh_read_string(self._h, rid, buf, n + 1)
+        return buf.value.decode()
+
+    def frequency(self, rid: int) -> int:
+        return int(lib().mgh_frequency(self._h, rid))
+
+    def find(self, s: str) -> int:
+        b = s.encode()
+        return int(lib().mgh_find_read(self._h, b, len(b)))
+
+
+class OverlapEngine:
+    """One device context (include/mg_overlap.h)."""
+
+    def __init__(self, device: int = 0):
+        L = lib()
+        h = C.c_void_p()
+        rc = L.mg_create(C.byref(h), device)
+        if rc == -3:
+            raise MgError("no HIP device available: the overlap path has no CPU fallback")
+        if rc:
+            raise MgError(f"mg_create({device}) failed: {rc}")
+        self._h = h
+        self.n_reads = 0
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().mg_destroy(self._h)
+            self._h = None
+
+    __del__ = close
+
+    def _check(self, rc: int, what: str):
+        if rc:
+            msg = lib().mg_last_error(self._h)
+            raise MgError(f"{what}: {msg.decode() if msg else rc}")
+
+    # --- reads
+    def upload(self, ds: Dataset):
+        words, lens = ds.packed()
+        self.upload_packed(words, lens)
+
+    def upload_packed(self, words: np.ndarray, lens: np.ndarray):
+        words = np.ascontiguousarray(words, dtype=np.uint64)
+        lens = np.ascontiguousarray(lens, dtype=np.uint16)
+        wpr = words.shape[1] if words.ndim == 2 else 1
+        self._check(lib().mg_upload_reads_packed(self._h, _ptr(words), _ptr(lens), lens.shape[0], wpr), "upload")
+        self.n_reads = int(lens.shape[0])
+
+    def upload_ascii(self, seqs: Sequence[str]):
+        data = "".join(seqs).encode()
+        off = np.zeros(len(seqs) + 1, dtype=np.uint64)
+        off[1:] = np.cumsum([len(s) for s in seqs])
+        self._check(lib().mg_upload_reads_ascii(self._h, data, _ptr(off), len(seqs)), "upload_ascii")
+        self.n_reads = len(seqs)
+
+    def download_packed(self):
+        wpr = C.c_uint32()
+        lib().mg_download_reads_packed(self._h, None, None, C.byref(wpr))
+        words = np.zeros((self.n_reads, wpr.value), np.uint64)
+        lens = np.zeros(self.n_reads, np.uint16)
+        self._check(lib().mg_download_reads_packed(self._h, _ptr(words), _ptr(lens), C.byref(wpr)), "download")
+        return words, lens
+
+    # --- hot path
+    def set_option(self, name: str, value: int):
+        self._check(lib().mg_set_option(self._h, name.encode(), int(value)), f"option {name}")
+
+    def set_shard(self, rank: int, nranks: int, read_lo: int = 0, read_hi: int = 0):
+        self._check(lib().mg_set_shard(self._h, rank, nranks, read_lo, read_hi), "set_shard")
+
+    def build_index(self, min_overlap: int, seed_k: int = 0):
+        self._check(lib().mg_build_index(self._h, min_overlap, seed_k), "build_index")
+
+    def mark_contained(self) -> np.ndarray:
+        sup = np.zeros(self.n_reads + 1, dtype=np.uint32)
+        self._check(lib().mg_mark_contained(self._h, _ptr(sup)), "mark_contained")
+        return sup
+
+    def find_overlaps(self) -> int:
+        n = C.c_uint64()
+        self._check(lib().mg_find_overlaps(self._h, C.byref(n)), "find_overlaps")
+        return int(n.value)
+
+    def rows(self, n_rows: int | None = None) -> np.ndarray:
+        if n_rows is None:
+            n_rows = self.find_overlaps()
+        out = np.zeros(n_rows, dtype=EDGE_DTYPE)
+        got = C.c_uint64()
+        self._check(lib().mg_copy_rows(self._h, _ptr(out), n_rows, C.byref(got)), "copy_rows")
+        return out[: got.value]
+
+    def lookup(self, key: str):
+        n = C.c_uint64()
+        cap = 1024
+        while True:
+            buf = np.zeros(cap, dtype=np.uint64)
+            self._check(lib().mg_lookup_key(self._h, key.encode(), len(key), _ptr(buf), cap, C.byref(n)), "lookup")
+            if n.value <= cap:
+                return [(int(x & ((1 << 62) - 1)), int(x >> 62)) for x in buf[: n.value]]
+            cap = int(n.value)
+
+    def timings(self) -> dict:
+        t = _Timings()
+        lib().mg_get_timings(self._h, C.byref(t))
+        return {k: float(getattr(t, k)) for k, _ in _Timings._fields_}
+
+    def counters(self) -> dict:
+        c = _Counters()
+        lib().mg_get_counters(self._h, C.byref(c))
+        return {k: int(getattr(c, k)) for k, _ in _Counters._fields_}
+
+    def stream(self) -> int:
+        return int(lib().mg_stream(self._h) or 0)
+
+
+def sort_rows(rows: np.ndarray) -> np.ndarray:
+    """Canonical order (src, dst, orient, offset) for multiset comparison."""
+    order = np.lexsort((rows["offset"], rows["orient"], rows["dst"], rows["src"]))
+    return rows[order]
+
+
+def rows_to_tuples(rows: np.ndarray) -> np.ndarray:
+    r = sort_rows(rows)
+    return np.stack([r["src"].astype(np.int64), r["dst"].astype(np.int64), r["orient"].astype(np.int64),
+                     r["offset"].astype(np.int64)], axis=1)

@@ -33,23 +33,29 @@ def revcomp_codes(codes: np.ndarray, lengths: np.ndarray) -> np.ndarray:
 
 
 def sample_reads(genome: np.ndarray, n_reads: int, lo: int, hi: int, seed: int,
-                 rc_fraction: float = 0.5):
+                 rc_fraction: float = 0.5, chunk: int = 1 << 20):
     """Return (codes[n, hi] uint8, lengths[n] uint16).
 
     Each read: length ~ U[lo, hi], start ~ U[0, G-len], reverse-complemented
-    with probability ``rc_fraction``."""
+    with probability ``rc_fraction``.  Built in chunks of ``chunk`` reads so
+    10M-read sets stay within a few GB of host memory."""
     rng = np.random.default_rng(seed)
     G = genome.shape[0]
     lengths = rng.integers(lo, hi + 1, size=n_reads).astype(np.int64)
     starts = rng.integers(0, G - lengths + 1)
     rc = rng.random(n_reads) < rc_fraction
+    codes = np.zeros((n_reads, hi), dtype=np.uint8)
     k = np.arange(hi, dtype=np.int64)[None, :]
-    idx = np.minimum(starts[:, None] + k, G - 1)
-    codes = genome[idx]
-    codes[k >= lengths[:, None]] = 0
-    if rc.any():
-        codes[rc] = revcomp_codes(codes[rc], lengths[rc])
-    return codes.astype(np.uint8), lengths.astype(np.uint16)
+    for a in range(0, n_reads, chunk):
+        b = min(n_reads, a + chunk)
+        idx = np.minimum(starts[a:b, None] + k, G - 1)
+        c = genome[idx]
+        c[k >= lengths[a:b, None]] = 0
+        m = rc[a:b]
+        if m.any():
+            c[m] = revcomp_codes(c[m], lengths[a:b][m])
+        codes[a:b] = c
+    return codes, lengths.astype(np.uint16)
 
 
 def uniform_read_set(n_reads: int, read_len: int, genome_len: int, seed: int,

@@ -1,0 +1,124 @@
+"""TEST INFRASTRUCTURE ONLY — ctypes wrapper of the C restatement (mg_oracle.c).
+
+Imported only by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline
+leg, as the checker.  The product (metagenomics_amd/) never imports this.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "build", "libmgoracle.so")
+REF_HARNESS = os.path.join(HERE, "_ref", "ref_harness")
+
+ROW_DTYPE = np.dtype([("src", "<u4"), ("dst", "<u4"), ("offset", "<u2"), ("orient", "u1"), ("pad", "u1")])
+
+_lib = None
+
+
+def build() -> None:
+    subprocess.run(["make", "-s", "-C", HERE, "oracle"], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            build()
+        L = C.CDLL(LIB)
+        vp, u64 = C.c_void_p, C.c_uint64
+        L.mgo_dataset_from_files.restype = vp
+        L.mgo_dataset_from_files.argtypes = [C.POINTER(C.c_char_p), C.c_int, u64]
+        L.mgo_dataset_from_seqs.restype = vp
+        L.mgo_dataset_from_seqs.argtypes = [C.c_char_p, vp, u64, u64]
+        L.mgo_dataset_free.argtypes = [vp]
+        L.mgo_num_unique.restype = u64
+        L.mgo_num_unique.argtypes = [vp]
+        L.mgo_num_reads.restype = u64
+        L.mgo_num_reads.argtypes = [vp]
+        L.mgo_read.restype = C.c_char_p
+        L.mgo_read.argtypes = [vp, u64, C.POINTER(C.c_uint32)]
+        L.mgo_frequency.restype = C.c_uint32
+        L.mgo_frequency.argtypes = [vp, u64]
+        L.mgo_overlaps.restype = C.c_int
+        L.mgo_overlaps.argtypes = [vp, u64, vp, C.POINTER(vp), C.POINTER(u64), C.POINTER(C.c_double),
+                                   C.POINTER(C.c_double)]
+        L.mgo_lookup.restype = u64
+        L.mgo_lookup.argtypes = [vp, u64, C.c_char_p, vp, u64]
+        L.mgo_free.argtypes = [vp]
+        _lib = L
+    return _lib
+
+
+class OracleDataset:
+    def __init__(self, h):
+        self._h = h
+
+    @classmethod
+    def from_files(cls, files, l):
+        arr = (C.c_char_p * len(files))(*[f.encode() for f in files])
+        h = lib().mgo_dataset_from_files(arr, len(files), l)
+        if not h:
+            raise IOError(f"oracle cannot read {files}")
+        return cls(h)
+
+    @classmethod
+    def from_strings(cls, seqs, l):
+        data = "".join(seqs).encode()
+        off = np.zeros(len(seqs) + 1, dtype=np.uint64)
+        off[1:] = np.cumsum([len(s) for s in seqs])
+        return cls(lib().mgo_dataset_from_seqs(data, C.c_void_p(off.ctypes.data), len(seqs), l))
+
+    def __del__(self):
+        if getattr(self, "_h", None) and _lib is not None:
+            _lib.mgo_dataset_free(self._h)
+            self._h = None
+
+    @property
+    def num_unique(self):
+        return int(lib().mgo_num_unique(self._h))
+
+    @property
+    def num_reads(self):
+        return int(lib().mgo_num_reads(self._h))
+
+    def read(self, rid):
+        return lib().mgo_read(self._h, rid, None).decode()
+
+    def frequency(self, rid):
+        return int(lib().mgo_frequency(self._h, rid))
+
+    def overlaps(self, l):
+        """-> (rows structured array, super[N+1] uint64, t_hash_s, t_disc_s)"""
+        n = self.num_unique
+        sup = np.zeros(n + 1, dtype=np.uint64)
+        rows_p = C.c_void_p()
+        nrows = C.c_uint64()
+        th, td = C.c_double(), C.c_double()
+        rc = lib().mgo_overlaps(self._h, l, C.c_void_p(sup.ctypes.data), C.byref(rows_p), C.byref(nrows),
+                                C.byref(th), C.byref(td))
+        if rc:
+            raise RuntimeError("oracle overlaps failed")
+        if nrows.value:
+            buf = (C.c_char * (nrows.value * ROW_DTYPE.itemsize)).from_address(rows_p.value)
+            rows = np.frombuffer(bytes(buf), dtype=ROW_DTYPE).copy()
+        else:
+            rows = np.zeros(0, dtype=ROW_DTYPE)
+        lib().mgo_free(rows_p)
+        return rows, sup, th.value, td.value
+
+    def lookup(self, l, key):
+        out = np.zeros(1 << 16, dtype=np.uint64)
+        n = lib().mgo_lookup(self._h, l, key.encode(), C.c_void_p(out.ctypes.data), out.shape[0])
+        return [(int(x & ((1 << 62) - 1)), int(x >> 62)) for x in out[: min(n, out.shape[0])]]
+
+
+def sorted_tuples(rows) -> np.ndarray:
+    order = np.lexsort((rows["offset"], rows["orient"], rows["dst"], rows["src"]))
+    r = rows[order]
+    return np.stack([r["src"].astype(np.int64), r["dst"].astype(np.int64), r["orient"].astype(np.int64),
+                     r["offset"].astype(np.int64)], axis=1)

@@ -73,8 +73,33 @@ def ids_digest(reads: dict) -> str:
     return h.hexdigest()
 
 
+def run_lookup(path: str, l: int, keys):
+    with tempfile.NamedTemporaryFile("r", suffix=".txt", delete=False) as t:
+        out = t.name
+    subprocess.run([HARNESS, "lookup", path, str(l), out] + list(keys), check=True)
+    res = {}
+    with open(out) as f:
+        for line in f:
+            parts = line.split()
+            res[parts[0]] = [[int(x) for x in p.split(":")] for p in parts[1:]]
+    os.unlink(out)
+    return res
+
+
+def lookup_keys(reads: dict, l: int, count: int = 24):
+    """prefix/suffix keys of both strands of some reads + windows that are no key."""
+    h = l - 1
+    keys = []
+    ids = sorted(reads)[:: max(1, len(reads) // count)][:count]
+    for i in ids:
+        s = reads[i]
+        r = synth.revcomp_str(s)
+        keys += [s[:h], s[-h:], r[:h], r[-h:], s[1:1 + h]]
+    return sorted(set(k for k in keys if len(k) == h))
+
+
 def emit(name: str, seqs, l: int, fastq: bool = False, store_rows: bool = True, raw_text=None,
-         store_input: bool = True, recipe=None):
+         store_input: bool = True, recipe=None, lookups: bool = False):
     ext = ".fq" if fastq else ".fa"
     with tempfile.TemporaryDirectory() as td:
         path = os.path.join(td, name + ext)
@@ -86,6 +111,7 @@ def emit(name: str, seqs, l: int, fastq: bool = False, store_rows: bool = True, 
         else:
             synth.write_fasta(path, seqs)
         n, reads, supers, rows = run_ref(path, l)
+        lk = run_lookup(path, l, lookup_keys(reads, l)) if lookups else None
         with open(path, "rb") as f:
             data = f.read()
     if store_input:
@@ -101,6 +127,8 @@ def emit(name: str, seqs, l: int, fastq: bool = False, store_rows: bool = True, 
         "super": {str(k): v for k, v in sorted(supers.items())},
         "edges_file": (name + ".edges.gz") if store_rows else None,
     }
+    if lk is not None:
+        meta["lookups"] = lk
     with open(os.path.join(HERE, name + ".json"), "w") as f:
         json.dump(meta, f, indent=1, sort_keys=True)
     print(f"{name}: N={n} rows={len(rows)} contained={len(supers)}")
@@ -117,17 +145,17 @@ def main():
     emit("small", strs(c, L), 40)
     # 2. mixed lengths 100-250 (containment active, SURVEY §0 "mixed")
     c, L = synth.uniform_read_set(3000, 0, 30000, seed=5, lo=100, hi=250)
-    emit("mixed", strs(c, L), 50)
+    emit("mixed", strs(c, L), 50, lookups=True)
     # 3. high duplicate: 3000 reads from a 2 kb genome (long bucket lists)
     c, L = synth.uniform_read_set(3000, 100, 2000, seed=9)
-    emit("highdup", strs(c, L), 50)
+    emit("highdup", strs(c, L), 50, lookups=True)
     # 4. tandem repeats + palindromes: self-loops and multi-edges
     g = synth.codes_to_strings(synth.random_genome(3000, 13)[None, :], np.array([3000]))[0]
     g = g[:1000] + "ACGTTGCAAG" * 60 + g[1000:2000] + "GAATTC" * 30 + g[2000:] + "GATTACA" * 50
     gc = np.frombuffer(g.encode(), dtype=np.uint8)
     codes = np.searchsorted(synth.ALPHABET, gc).astype(np.uint8)
     c, L = synth.sample_reads(codes, 1500, 90, 140, seed=14)
-    emit("tandem", strs(c, L), 40)
+    emit("tandem", strs(c, L), 40, lookups=True)
     # 5. two-read hand case: A = X[0:60], B = rc(X[20:80]), l = 30
     X = synth.codes_to_strings(synth.random_genome(80, 21)[None, :], np.array([80]))[0]
     emit("tworead", [X[0:60], synth.revcomp_str(X[20:80])], 30)

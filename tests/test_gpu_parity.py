@@ -1,0 +1,201 @@
+"""Parity of the HIP path (through the C-ABI) with the reference's golden
+vectors and with the oracle.  Bit-exact: integer/index work."""
+import numpy as np
+import pytest
+
+from conftest import FIXTURES, fixture_input, golden_rows, load_meta, rows_sha256
+from metagenomics_amd import synth
+from metagenomics_amd.overlap import Dataset, OverlapEngine, rows_to_tuples
+from oracle import OracleDataset, sorted_tuples
+
+pytestmark = pytest.mark.gpu
+
+TWIN = {0: 3, 1: 1, 2: 2, 3: 0}
+
+
+@pytest.fixture(scope="module")
+def engine():
+    e = OverlapEngine(0)
+    yield e
+    e.close()
+
+
+def gpu_rows(engine, ds, l, k=0, nb_log2=0, shard=(0, 1, 0, 0)):
+    engine.set_option("nb_log2", nb_log2)
+    engine.set_shard(*shard)
+    engine.upload(ds)
+    engine.build_index(l, k)
+    sup = engine.mark_contained()
+    n = engine.find_overlaps()
+    rows = engine.rows(n)
+    assert rows.shape[0] == n
+    return rows, sup
+
+
+def check_pairs(rows, lens):
+    """rows come as (edge, twin) pairs (insertEdge, OverlapGraph.cpp:407-419)."""
+    a, b = rows[0::2], rows[1::2]
+    assert np.array_equal(a["src"], b["dst"]) and np.array_equal(a["dst"], b["src"])
+    assert all(TWIN[int(x)] == int(y) for x, y in zip(a["orient"][:2000], b["orient"][:2000]))
+    n1 = lens[a["src"].astype(np.int64) - 1].astype(np.int64)
+    n2 = lens[a["dst"].astype(np.int64) - 1].astype(np.int64)
+    assert np.array_equal(((n2 + a["offset"].astype(np.int64) - n1) & 0xFFFF), b["offset"].astype(np.int64))
+
+
+@pytest.mark.parametrize("name", FIXTURES)
+def test_fixture_matches_reference(engine, name):
+    meta = load_meta(name)
+    ds = Dataset.from_files([fixture_input(name)], meta["l"])
+    rows, sup = gpu_rows(engine, ds, meta["l"])
+    t = rows_to_tuples(rows)
+    g = golden_rows(name)
+    assert t.shape == g.shape, (t.shape, g.shape)
+    assert np.array_equal(t, g)
+    assert rows_sha256(t) == meta["rows_sha256"]
+    assert {str(i): int(s) for i, s in enumerate(sup) if s} == meta["super"]
+    check_pairs(rows, ds.packed()[1])
+
+
+@pytest.mark.parametrize("name,k", [("small", 12), ("small", 21), ("small", 32), ("tandem", 8),
+                                    ("tandem", 25), ("mixed", 17), ("highdup", 31), ("highdup", 5)])
+def test_seed_k_does_not_change_results(engine, name, k):
+    meta = load_meta(name)
+    ds = Dataset.from_files([fixture_input(name)], meta["l"])
+    rows, _ = gpu_rows(engine, ds, meta["l"], k=k)
+    assert np.array_equal(rows_to_tuples(rows), golden_rows(name))
+
+
+@pytest.mark.parametrize("name", ["highdup", "tandem", "mixed"])
+def test_tiny_directory_collisions(engine, name):
+    """2^10 buckets: every bucket holds many minimizers; results unchanged."""
+    meta = load_meta(name)
+    ds = Dataset.from_files([fixture_input(name)], meta["l"])
+    rows, sup = gpu_rows(engine, ds, meta["l"], nb_log2=10)
+    assert np.array_equal(rows_to_tuples(rows), golden_rows(name))
+
+
+@pytest.mark.parametrize("name", ["highdup", "tandem", "mixed"])
+def test_lookup_matches_reference(engine, name):
+    """HashTable::getListOfReads (HashTable.cpp:202-221) incl. list order."""
+    meta = load_meta(name)
+    ds = Dataset.from_files([fixture_input(name)], meta["l"])
+    engine.set_option("nb_log2", 0)
+    engine.set_shard(0, 1)
+    engine.upload(ds)
+    engine.build_index(meta["l"])
+    for key, exp in meta["lookups"].items():
+        assert [list(x) for x in engine.lookup(key)] == exp, key
+    assert engine.lookup("A" * (meta["l"] - 2)) == [] or True  # any key of length h is legal
+    assert engine.lookup("ACGT") == []  # wrong length: no such key
+
+
+def test_ascii_upload_equals_packed(engine):
+    meta = load_meta("mixed")
+    ds = Dataset.from_files([fixture_input("mixed")], meta["l"])
+    seqs = [ds.read(i) for i in range(1, ds.num_unique + 1)]
+    engine.set_option("nb_log2", 0)
+    engine.set_shard(0, 1)
+    engine.upload_ascii(seqs)
+    w1, l1 = engine.download_packed()
+    w0, l0 = ds.packed()
+    assert np.array_equal(l0, l1)
+    assert np.array_equal(w0, w1[:, : w0.shape[1]])
+    engine.build_index(meta["l"])
+    engine.mark_contained()
+    rows = engine.rows()
+    assert np.array_equal(rows_to_tuples(rows), golden_rows("mixed"))
+
+
+@pytest.mark.parametrize("name,nranks", [("small", 2), ("highdup", 3), ("tandem", 4)])
+def test_bucket_shards_union(engine, name, nranks):
+    """Bucket-range sharding: the union over ranks is the multiset."""
+    meta = load_meta(name)
+    if meta["super"]:
+        pytest.skip("containment with a sharded index is not supported yet")
+    ds = Dataset.from_files([fixture_input(name)], meta["l"])
+    parts = []
+    for r in range(nranks):
+        rows, _ = gpu_rows(engine, ds, meta["l"], shard=(r, nranks, 0, 0))
+        parts.append(rows)
+    allr = np.concatenate(parts)
+    assert np.array_equal(rows_to_tuples(allr), golden_rows(name))
+
+
+@pytest.mark.parametrize("name", ["small", "mixed", "tandem"])
+def test_read_range_union(engine, name):
+    meta = load_meta(name)
+    ds = Dataset.from_files([fixture_input(name)], meta["l"])
+    n = ds.num_unique
+    cuts = [0, n // 3, n // 2 + 7, n]
+    parts = []
+    for lo, hi in zip(cuts[:-1], cuts[1:]):
+        rows, _ = gpu_rows(engine, ds, meta["l"], shard=(0, 1, lo, hi))
+        parts.append(rows)
+    assert np.array_equal(rows_to_tuples(np.concatenate(parts)), golden_rows(name))
+
+
+def test_c1_digest(engine):
+    """BASELINE configs[0]: 100k x 100 bp, l = 40, k = 21."""
+    meta = load_meta("c1")
+    r = meta["recipe"]
+    c, L = synth.uniform_read_set(r["n_reads"], r["read_len"], r["genome_len"], r["seed"])
+    ds = Dataset.from_codes(c, L, meta["l"])
+    assert ds.num_unique == meta["n_unique"]
+    rows, _ = gpu_rows(engine, ds, meta["l"], k=21)
+    assert rows.shape[0] == meta["directed_rows"]
+    assert rows_sha256(rows_to_tuples(rows)) == meta["rows_sha256"]
+
+
+RANDOM_CASES = [
+    # n, lo, hi, genome, l, k, seed
+    (3000, 60, 60, 4000, 31, 0, 101),       # short reads, l close to length
+    (4000, 50, 300, 20000, 25, 11, 102),    # wide length range, containment
+    (2000, 200, 1000, 30000, 60, 31, 103),  # long reads (up to 32 words)
+    (5000, 100, 100, 800, 40, 20, 104),     # extreme duplication
+    (3000, 35, 40, 6000, 33, 32, 105),      # l-1 = 32 = k
+    (1000, 64, 64, 5000, 10, 5, 106),       # tiny l
+]
+
+
+@pytest.mark.parametrize("case", RANDOM_CASES)
+def test_random_sets_vs_oracle(engine, case):
+    n, lo, hi, G, l, k, seed = case
+    c, L = synth.uniform_read_set(n, 0, G, seed=seed, lo=lo, hi=hi)
+    seqs = synth.codes_to_strings(c, L)
+    ds = Dataset.from_codes(c, L, l)
+    od = OracleDataset.from_strings(seqs, l)
+    assert ds.num_unique == od.num_unique
+    rows, sup = gpu_rows(engine, ds, l, k=k)
+    orows, osup, _, _ = od.overlaps(l)
+    assert np.array_equal(sup.astype(np.uint64), osup)
+    assert np.array_equal(rows_to_tuples(rows), sorted_tuples(orows))
+
+
+def test_metagenome_vs_oracle(engine):
+    c, L = synth.metagenome_read_set(20000, 100, 250, n_genomes=20, total_len=400000, seed=51)
+    ds = Dataset.from_codes(c, L, 50)
+    od = OracleDataset.from_strings(synth.codes_to_strings(c, L), 50)
+    rows, sup = gpu_rows(engine, ds, 50, k=31)
+    orows, osup, _, _ = od.overlaps(50)
+    assert np.array_equal(sup.astype(np.uint64), osup)
+    assert np.array_equal(rows_to_tuples(rows), sorted_tuples(orows))
+
+
+def test_c2_scale_vs_oracle(engine):
+    """BASELINE configs[1] shape (1M x 150 bp, l=50, k=31) against the oracle."""
+    c, L = synth.uniform_read_set(1_000_000, 150, 7_500_000, seed=21)
+    ds = Dataset.from_codes(c, L, 50)
+    rows, _ = gpu_rows(engine, ds, 50, k=31)
+    od = OracleDataset.from_strings(synth.codes_to_strings(c, L), 50)
+    orows, _, _, _ = od.overlaps(50)
+    assert rows.shape[0] == orows.shape[0]
+    assert np.array_equal(rows_to_tuples(rows), sorted_tuples(orows))
+    check_pairs(rows, ds.packed()[1])
+
+
+def test_repeatable(engine):
+    meta = load_meta("highdup")
+    ds = Dataset.from_files([fixture_input("highdup")], meta["l"])
+    a, _ = gpu_rows(engine, ds, meta["l"])
+    b, _ = gpu_rows(engine, ds, meta["l"])
+    assert np.array_equal(rows_to_tuples(a), rows_to_tuples(b))
