@@ -350,6 +350,9 @@ __global__ __launch_bounds__(kBlock) void k_discover(DiscParams p) {
       if (e_idx < e_end) {
         const uint64_t e = p.ent[e_idx++];
         ++st_ent;
+#ifdef MG_DEBUG_PRINT
+        if (p.n <= 4) printf("scan C=%d a=%d idx=%u e=%llx run_p=%d jlo=%d jhi=%d fp=%x\n", (int)CONTAIN, (int)a, e_idx - 1, (unsigned long long)e, run_p, jlo, jhi, run_fp);
+#endif
         const uint32_t hi = (uint32_t)(e >> 32);
         if ((hi >> 12) != run_fp) continue;
         const int q = (int)((hi >> 2) & 1023u);
@@ -357,10 +360,10 @@ __global__ __launch_bounds__(kBlock) void k_discover(DiscParams p) {
         if (jj < jlo || jj > jhi) continue;
         const int oo = (int)(hi & 3u);
         const uint32_t bb = (uint32_t)e;
-        if (!CONTAIN) {
-          if (oo == 1) continue;               // twin of the partner's o=0 discovery
-          if (oo >= 2 && bb < a) continue;     // twin of the partner's o=2/3 discovery
-        }
+        // halving: o = 1 hits are the twins of the partner's o = 0
+        // hits; o = 2/3 hits are kept only for partner >= source
+        const bool keep = CONTAIN || (oo == 0) || (oo >= 2 && (uint64_t)bb >= a);
+        if (!keep) continue;
         have = true;
         bid = bb;
         o = oo;
@@ -453,6 +456,9 @@ __global__ __launch_bounds__(kBlock) void k_discover(DiscParams p) {
             diff |= (av ^ bv) & mask;
           }
         }
+#ifdef MG_DEBUG_PRINT
+        if (p.n <= 4) printf("cand C=%d a=%d b=%u o=%d j=%d L=%d x0=%d y0=%d diff=%llx\n", (int)CONTAIN, (int)a, bid, o, j, L, x0, y0, (unsigned long long)diff);
+#endif
         if (diff == 0) {
           if (CONTAIN) {
             atomicMax(&p.superkey[bid], ((unsigned long long)n1 << 32) | (0xFFFFFFFFu - (uint32_t)a));
@@ -471,6 +477,9 @@ __global__ __launch_bounds__(kBlock) void k_discover(DiscParams p) {
       }
     }
 
+#ifdef MG_DEBUG_PRINT
+    if (p.n <= 4 && have) printf("have a=%d b=%u o=%d j=%d nrec=%d\n", (int)a, bid, o, j, nrec);
+#endif
     // ---- wavefront compaction into the LDS row buffer, flush >= kFlush rows
     if (!CONTAIN) {
       const uint64_t b2 = __ballot(nrec >= 2), b4 = __ballot(nrec == 4);
