@@ -144,7 +144,7 @@ def main():
 
     def step():
         eng.build_index(l, k)
-        eng.mark_contained()
+        eng.mark_contained(copy=False)
         return eng.find_overlaps()
 
     # one counting pass (untimed) for the roofline's algorithmic bytes

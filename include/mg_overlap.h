@@ -46,8 +46,10 @@ typedef struct mg_timings {
   float pack_ms;        /* 2-bit encoding of ASCII reads            */
   float index_ms;       /* HashTable::insertDataset equivalent       */
   float contained_ms;   /* markContainedReads equivalent (0 if skipped) */
-  float overlap_ms;     /* discovery kernel (insertAllEdgesOfRead)   */
+  float overlap_ms;     /* discovery = scan + probe (insertAllEdgesOfRead) */
   float total_ms;       /* index + contained + overlap               */
+  float scan_ms;        /* minimizer-run scan kernel                 */
+  float probe_ms;       /* probe + verify kernel                     */
 } mg_timings;
 
 /* Work counters of the last discovery launch (only with option "stats" = 1):

@@ -41,11 +41,7 @@ namespace {
 constexpr int kWave = 64;
 constexpr int kBlock = 256;
 constexpr int kWavesPerBlock = kBlock / kWave;
-constexpr int kFlush = 128;                 // rows per global reservation (minimum)
-constexpr int kBuf = kFlush + 4 * kWave;    // per-wave LDS row buffer capacity
-constexpr int kSegs = 64;                   // output segments (one atomic cursor each)
-constexpr int kScanPerThread = 16;
-constexpr int kScanTile = kBlock * kScanPerThread;
+constexpr int kSegs = 64;                   // diagnostic counter shards
 constexpr uint32_t kFpBits = 20;
 
 // ---------------------------------------------------------------- helpers ---
@@ -58,6 +54,19 @@ __device__ __forceinline__ uint64_t mix64(uint64_t x) {
   x *= 0x81dadef4bc2dd44dULL;
   x ^= x >> 33;
   return x;
+}
+
+// Minimizer order of an m-mer: a cheap 32-bit hash truncated to 22 bits and
+// packed with the m-mer's position (< 1024), so that "smallest key, leftmost
+// on ties" is a plain unsigned min.  Index build, discovery and lookup all
+// use this same rule, so a key and an identical read window always select
+// the same minimizer at the same offset.
+__device__ __forceinline__ uint32_t order_key(uint64_t mm) {
+  uint32_t x = (uint32_t)mm * 0x9E3779B1u + (uint32_t)(mm >> 32);
+  x ^= x >> 15;
+  x *= 0x85EBCA77u;
+  x ^= x >> 13;
+  return x & 0xFFFFFC00u;  // 22-bit key in the high bits, position goes in the low 10
 }
 
 // Reverse complement of 32 packed bases (Read.cpp:115-127 on 2-bit codes:
@@ -115,6 +124,13 @@ __global__ __launch_bounds__(kBlock) void k_pack_ascii(const char* __restrict__ 
 }
 
 // ------------------------------------------------------------ index build ---
+// Cell index (replaces HashTable's vector-of-lists, HashTable.h:20): 2^nb_log2
+// cells of kCell entries (one 64-B line each) plus a u32 fill count per cell.
+// An entry goes to the first cell of its minimizer's home cell chain that has
+// room (cell-granular linear probing), so a lookup reads the home cell's count
+// and line together and follows the chain only while count > kCell.
+constexpr int kCell = 8;
+
 struct IndexParams {
   const uint64_t* words;
   const uint16_t* len;
@@ -122,21 +138,41 @@ struct IndexParams {
   int h, m, w;
   uint32_t nb_log2;
   uint32_t rank, nranks;
-  uint32_t* cnt;        // [NB] per-bucket counts (count pass) / remaining cursor (fill pass)
-  const uint32_t* dir;  // [NB+1] exclusive scan of counts
-  uint64_t* ent;        // entries: lo32 = read index, hi32 = fp20 | q10 | o2
+  uint32_t* cnt;     // [NC] entries claimed per cell (> kCell: the chain continues in the next cell)
+  uint64_t* cells;   // [NC * kCell] entries: lo32 = read index, hi32 = fp20 | q10 | o2
 };
 
 __device__ __forceinline__ bool owned(uint64_t bkt, uint32_t nb_log2, uint32_t rank, uint32_t nranks) {
   return nranks <= 1 || (uint32_t)((bkt * nranks) >> nb_log2) == rank;
 }
 
-// Minimizer (leftmost minimum of mix64 over the key's w m-mers) of each of the
-// read's 4 keys (hashRead, HashTable.cpp:88-104): o=0 F[0,h), o=1 F[n-h,n),
-// o=2 R[0,h), o=3 R[n-h,n).  R m-mer at t = rc(F[n-t-m, n-t)).
-// FILL=false: count entries per bucket.  FILL=true: place entries.
-template <int MAXW, bool FILL>
-__global__ __launch_bounds__(kBlock) void k_index_keys(IndexParams p) {
+// Minimizer of key o of a read (hashRead, HashTable.cpp:88-104): o=0 F[0,h),
+// o=1 F[n-h,n), o=2 R[0,h), o=3 R[n-h,n); R m-mer at t = rc(F[n-t-m, n-t)).
+// Returns mix64 of the minimizer m-mer (bucket, fingerprint) and its offset q.
+template <int S>
+__device__ __forceinline__ uint64_t key_minimizer(const uint64_t* f, int n, int o, int h, int m, int w,
+                                                  int* q) {
+  const uint64_t mmask = (m == 32) ? ~0ULL : ((1ULL << (2 * m)) - 1);
+  const int kb = (o == 0 || o == 2) ? 0 : n - h;
+  uint32_t bkey = 0xFFFFFFFFu;
+  uint64_t bmm = 0;
+  for (int i = 0; i < w; ++i) {
+    const int t = kb + i;
+    const uint64_t mm = (o < 2) ? ext_fwd<S>(f, t) >> (64 - 2 * m) : rc_word(ext_fwd<S>(f, n - t - m)) & mmask;
+    const uint32_t key = order_key(mm) | (uint32_t)i;
+    if (key < bkey) {
+      bkey = key;
+      bmm = mm;
+    }
+  }
+  *q = (int)(bkey & 1023u);
+  return mix64(bmm);
+}
+
+// HashTable::insertDataset (HashTable.cpp:50-80): one thread per read files
+// its 4 keys.
+template <int MAXW>
+__global__ __launch_bounds__(kBlock) void k_index_build(IndexParams p) {
   extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
   const uint64_t r = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
   if (r >= p.n) return;
@@ -146,270 +182,245 @@ __global__ __launch_bounds__(kBlock) void k_index_keys(IndexParams p) {
   for (int k = 0; k < MAXW; ++k) f[k * kBlock] = g[k];
   f[MAXW * kBlock] = 0;
   const int n = p.len[r];
-  const int h = p.h, m = p.m, w = p.w;
-  const uint64_t mmask = (m == 32) ? ~0ULL : ((1ULL << (2 * m)) - 1);
-  const uint64_t nbmask = (1ULL << p.nb_log2) - 1;
+  const uint64_t mask = (1ULL << p.nb_log2) - 1;
 #pragma unroll 1
   for (int o = 0; o < 4; ++o) {
-    const int kb = (o == 0 || o == 2) ? 0 : n - h;
-    uint64_t best = 0;
-    int bq = 0;
-    for (int i = 0; i < w; ++i) {
-      const int t = kb + i;
-      uint64_t mm;
-      if (o < 2)
-        mm = ext_fwd<kBlock>(f, t) >> (64 - 2 * m);
-      else
-        mm = rc_word(ext_fwd<kBlock>(f, n - t - m)) & mmask;
-      const uint64_t v = mix64(mm);
-      if (i == 0 || v < best) {
-        best = v;
-        bq = i;
+    int q;
+    const uint64_t v = key_minimizer<kBlock>(f, n, o, p.h, p.m, p.w, &q);
+    uint64_t b = v & mask;
+    if (!owned(b, p.nb_log2, p.rank, p.nranks)) continue;
+    const uint32_t fp = (uint32_t)(v >> p.nb_log2) & ((1u << kFpBits) - 1);
+    const uint64_t entry = ((uint64_t)((fp << 12) | ((uint32_t)q << 2) | (uint32_t)o) << 32) | (uint32_t)r;
+    for (uint64_t probe = 0; probe <= mask; ++probe) {  // capacity >= 2x entries: ends in a few steps
+      const uint32_t slot = atomicAdd(&p.cnt[b], 1u);
+      if (slot < (uint32_t)kCell) {
+        p.cells[b * kCell + slot] = entry;
+        break;
       }
-    }
-    const uint64_t bkt = best & nbmask;
-    if (!owned(bkt, p.nb_log2, p.rank, p.nranks)) continue;
-    if (!FILL) {
-      atomicAdd(&p.cnt[bkt], 1u);
-    } else {
-      const uint32_t fp = (uint32_t)(best >> p.nb_log2) & ((1u << kFpBits) - 1);
-      const uint32_t pos = p.dir[bkt] + atomicSub(&p.cnt[bkt], 1u) - 1u;
-      const uint32_t hi = (fp << 12) | ((uint32_t)bq << 2) | (uint32_t)o;
-      p.ent[pos] = ((uint64_t)hi << 32) | (uint32_t)r;
+      b = (b + 1) & mask;
     }
   }
 }
 
-// ------------------------------------------------------------------ scan ---
-__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* total, uint32_t* sh) {
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+// ------------------------------------------------------------- discovery ---
+// Discovery is two kernels:
+//   k_scan  : minimizer runs of every source read -> 8-byte run records
+//             (read index, minimizer position p, window range [jlo, jhi]) in a
+//             per-wavefront HBM region;
+//   k_probe : one run per lane -> home cell chain -> exact candidates -> full
+//             overlap verification -> rows (insertEdge) or superReadID updates.
+struct ScanParams {
+  const uint64_t* words;
+  const uint16_t* len;
+  const uint32_t* super;          // source reads with superReadID != 0 get no windows (:548)
+  uint64_t a_lo, a_hi;
+  int h, m, w;
+  uint64_t* runs;                 // one region of run_cap records per wavefront
+  unsigned long long* run_cnt;    // [waves] records produced (may exceed run_cap)
+  uint64_t run_cap;
+};
+
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, int lane, uint32_t* total) {
   uint32_t x = v;
 #pragma unroll
   for (int d = 1; d < 64; d <<= 1) {
     const uint32_t y = __shfl_up(x, d);
     if (lane >= d) x += y;
   }
-  if (lane == 63) sh[wv] = x;
-  __syncthreads();
-  uint32_t wofs = 0, tot = 0;
-#pragma unroll
-  for (int i = 0; i < kWavesPerBlock; ++i) {
-    const uint32_t s = sh[i];
-    if (i < wv) wofs += s;
-    tot += s;
-  }
-  __syncthreads();
-  *total = tot;
-  return wofs + x - v;
+  *total = __shfl(x, 63);
+  return x - v;
 }
 
-__global__ __launch_bounds__(kBlock) void k_scan_reduce(const uint32_t* __restrict__ in, uint64_t n,
-                                                       uint32_t* __restrict__ bsum) {
-  __shared__ uint32_t sh[kWavesPerBlock];
-  const uint64_t base = (uint64_t)blockIdx.x * kScanTile;
-  uint32_t s = 0;
-#pragma unroll
-  for (int i = 0; i < kScanPerThread; ++i) {
-    const uint64_t idx = base + (uint64_t)i * kBlock + threadIdx.x;
-    if (idx < n) s += in[idx];
-  }
-  uint32_t tot;
-  block_excl_scan(s, &tot, sh);
-  if (threadIdx.x == 0) bsum[blockIdx.x] = tot;
+// Run record: read index (32 bits) | p << 32 | jlo << 42 | jhi << 52.
+__device__ __forceinline__ uint64_t run_record(uint64_t a, int p, int jlo, int jhi) {
+  return (a & 0xFFFFFFFFull) | ((uint64_t)p << 32) | ((uint64_t)jlo << 42) | ((uint64_t)jhi << 52);
 }
 
-// Single block: exclusive scan of the block sums in place.
-__global__ __launch_bounds__(kBlock) void k_scan_bsums(uint32_t* bsum, uint32_t nbs) {
-  __shared__ uint32_t sh[kWavesPerBlock];
-  uint32_t carry = 0;
-  for (uint32_t base = 0; base < nbs; base += kBlock) {
-    const uint32_t idx = base + threadIdx.x;
-    const uint32_t v = idx < nbs ? bsum[idx] : 0;
-    uint32_t tot;
-    const uint32_t ex = block_excl_scan(v, &tot, sh);
-    if (idx < nbs) bsum[idx] = carry + ex;
-    carry += tot;
+// Window minimizers of every source read (the windows of insertAllEdgesOfRead,
+// OverlapGraph.cpp:534-537), one read per lane.  Rolling 2-bit m-mer and the
+// van Herk / Gil-Werman sliding minimum over blocks of w positions: prefix
+// minimum of the current block in a register, suffix minima of the previous
+// block in LDS (w u32 per lane, overwritten by the current block's keys exactly
+// behind the read front).  Window j = m-mers [j, j+w-1] = the h-mer at j; its
+// minimizer is min(suffix_prev[u+1], prefix_cur) under order_key | position,
+// the rule the index used for the keys.  Block boundaries depend only on t, so
+// control flow is uniform across lanes.  A run ends where the minimizer
+// position changes; its record goes straight to HBM (ballot-compacted).
+template <int MAXW>
+__global__ __launch_bounds__(kBlock) void k_scan(ScanParams p) {
+  extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int h = p.h, m = p.m, w = p.w;
+  uint32_t* s_keys = reinterpret_cast<uint32_t*>(smem) + (size_t)wv * w * kWave + lane;  // slot u at [u*64]
+  const int msh = 64 - 2 * m;
+  const uint64_t mmask = (m == 32) ? ~0ULL : ((1ULL << (2 * m)) - 1);
+  const uint64_t ngroups = (p.a_hi - p.a_lo + kWave - 1) / kWave;
+  const uint64_t gw = (uint64_t)blockIdx.x * kWavesPerBlock + wv;
+  const uint64_t nw = (uint64_t)gridDim.x * kWavesPerBlock;
+  uint64_t* const region = p.runs + gw * p.run_cap;
+  uint64_t cursor = 0;
+
+  auto put = [&](bool flag, uint64_t rec) {
+    const uint64_t bal = __ballot(flag);
+    if (flag) {
+      const uint64_t at = cursor + (uint64_t)__popcll(bal & lanemask_lt());
+      if (at < p.run_cap) region[at] = rec;
+    }
+    cursor += (uint64_t)__popcll(bal);
+  };
+
+  for (uint64_t grp = gw; grp < ngroups; grp += nw) {
+    const uint64_t a = p.a_lo + grp * kWave + lane;
+    int n = 0;
+    const uint64_t* g = p.words + a * MAXW;
+    if (a < p.a_hi) {
+      n = (int)p.len[a];
+      if (n && p.super && p.super[a]) n = 0;
+    }
+    const int J = n - h - 1;                 // windows j = 1 .. J (:534)
+    const int tend = J >= 1 ? J + w - 1 : 0;  // last m-mer position a window uses
+    int tmax = tend;
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) tmax = max(tmax, __shfl_xor(tmax, d));
+    uint64_t mm = 0, cw = 0;
+    if (tend) {
+      mm = funnel(g[0], g[1], 2) >> msh;  // m-mer at t = 1
+      cw = g[(1 + m) >> 5];               // word holding base t + m
+    }
+    uint32_t pmin = 0xFFFFFFFFu;
+    int last_pos = 0, jlo = 1;
+    int u = 0;  // offset of t in its block of w positions
+    for (int t = 1; t <= tmax; ++t) {
+      bool emit = false, fin = false;
+      uint64_t rec = 0;
+      if (t <= tend) {
+        const uint32_t key = order_key(mm) | (uint32_t)t;
+        pmin = (u == 0 || key < pmin) ? key : pmin;
+        if (t >= w) {  // window j = t - w + 1
+          const int j = t - w + 1;
+          uint32_t mn = pmin;
+          if (u != w - 1) {
+            const uint32_t sv = s_keys[(u + 1) * kWave];
+            mn = sv < mn ? sv : mn;
+          }
+          const int pos = (int)(mn & 1023u);
+          if (j > 1 && pos != last_pos) {
+            emit = true;
+            rec = run_record(a, last_pos, jlo, j - 1);
+            jlo = j;
+          }
+          last_pos = pos;
+          fin = (t == tend);
+        }
+        s_keys[u * kWave] = key;
+        const int x = t + m;  // roll in the base at t + m
+        mm = ((mm << 2) | ((cw >> (62 - 2 * (x & 31))) & 3u)) & mmask;
+        if ((x & 31) == 31 && t < tend) cw = g[(x + 1) >> 5];
+      }
+      if (u == w - 1) {  // block complete: suffix minima in place
+        uint32_t run = s_keys[(w - 1) * kWave];
+        for (int v = w - 2; v >= 0; --v) {
+          const uint32_t x1 = s_keys[v * kWave];
+          run = x1 < run ? x1 : run;
+          s_keys[v * kWave] = run;
+        }
+        u = 0;
+      } else {
+        ++u;
+      }
+      put(emit, rec);
+      put(fin, run_record(a, last_pos, jlo, J));
+    }
   }
+  if (lane == 0) p.run_cnt[gw] = cursor;
 }
 
-// Exclusive scan of in[0..n) into out[0..n], out[n] = total.
-__global__ __launch_bounds__(kBlock) void k_scan_apply(const uint32_t* __restrict__ in, uint64_t n,
-                                                      const uint32_t* __restrict__ bsum,
-                                                      uint32_t* __restrict__ out) {
-  __shared__ uint32_t sh[kWavesPerBlock];
-  const uint64_t base = (uint64_t)blockIdx.x * kScanTile + (uint64_t)threadIdx.x * kScanPerThread;
-  uint32_t v[kScanPerThread];
-  uint32_t s = 0;
-#pragma unroll
-  for (int i = 0; i < kScanPerThread; ++i) {
-    v[i] = (base + i < n) ? in[base + i] : 0;
-    s += v[i];
-  }
-  uint32_t tot;
-  uint32_t ex = block_excl_scan(s, &tot, sh) + bsum[blockIdx.x];
-#pragma unroll
-  for (int i = 0; i < kScanPerThread; ++i) {
-    if (base + i < n) out[base + i] = ex;
-    if (base + i == n - 1) out[n] = ex + v[i];
-    ex += v[i];
-  }
-}
-
-// ------------------------------------------------------------- discovery ---
-struct DiscParams {
+struct ProbeParams {
   const uint64_t* words;
   const uint16_t* len;
-  uint64_t n;
-  int h, m, w;
+  int h, m;
   uint32_t nb_log2;
   uint32_t rank, nranks;
-  const uint32_t* dir;
-  const uint64_t* ent;
+  const uint32_t* cnt;
+  const uint64_t* cells;
   const uint32_t* super;          // superReadID per read index (nullptr: none contained)
   unsigned long long* superkey;   // CONTAIN: max over containers of (len << 32 | ~index)
-  uint64_t a_lo, a_hi;            // source reads handled by this launch
-  uint32_t* rows;                 // 3 dwords per row (mg_edge)
-  unsigned long long* seg_cnt;    // [kSegs] rows reserved per segment
-  uint64_t seg_cap;               // rows per segment
-  int uniform_len;                // all reads have the same length
+  const uint64_t* runs;
+  const unsigned long long* run_cnt;
+  uint64_t run_cap;
+  uint32_t* rows;                 // 3 dwords per row (mg_edge); one region per wavefront
+  unsigned long long* reg_cnt;    // [waves] rows produced by each wavefront (may exceed reg_cap)
+  uint64_t reg_cap;
+  int uniform_len;
   unsigned long long* stats;      // optional [kSegs*4]: runs probed, entries scanned, partners fetched, rows
+  int phase_limit;                // diagnostics: 4 no probe, 5 + cell loads, 6 + filter, 7 full
 };
 
 template <int MAXW>
-__device__ __forceinline__ size_t disc_lds_bytes_words() {
-  return (size_t)kWavesPerBlock * (MAXW + 1) * kWave * sizeof(uint64_t);
-}
+struct ProbeLds {
+  static constexpr int CAND = 2 * kWave;
+  static constexpr size_t o_a = 0;                                    // [MAXW+1][64] u64 source words
+  static constexpr size_t o_cb = o_a + (size_t)(MAXW + 1) * kWave * 8;  // [CAND] u32 partner
+  static constexpr size_t o_ci = o_cb + CAND * 4;                     // [CAND] u32 o << 30 | j << 20 | ...
+  static constexpr size_t o_ca = o_ci + CAND * 4;                     // [CAND] u32 source read
+  static constexpr size_t bytes = o_ca + CAND * 4;
+};
 
-// Wave-cooperative flush of the LDS row buffer (all 64 lanes, converged).
-__device__ __forceinline__ void flush_rows(const DiscParams& p, uint32_t* obuf, uint32_t nrows,
-                                           uint32_t seg, int lane) {
-  unsigned long long off = 0;
-  if (lane == 0) off = atomicAdd(&p.seg_cnt[seg], (unsigned long long)nrows);
-  off = __shfl(off, 0);
-  if (off + nrows <= p.seg_cap) {
-    uint32_t* dst = p.rows + ((uint64_t)seg * p.seg_cap + off) * 3;
-    for (uint32_t i = lane; i < nrows * 3; i += kWave) dst[i] = obuf[i];
-  }
-  __builtin_amdgcn_wave_barrier();
-}
-
-// One lane per source read (insertAllEdgesOfRead, OverlapGraph.cpp:529-565,
-// or markContainedReads' inner loop, :239-271, when CONTAIN).
+// Probe wavefront r consumes run region r in batches of 64 (one run per lane):
+// the home cell's count and 64-B line are loaded together, the chain is
+// followed while count > kCell; entries are exact candidates when the
+// fingerprint matches, j = p - q lies in the run's window range (so the
+// window's minimizer is this very m-mer at offset q) and the halving rule
+// keeps them.  Candidates are prefix-summed into an LDS list
+// and verified one per lane against the partner's words in HBM.
 template <int MAXW, bool CONTAIN>
-__global__ __launch_bounds__(kBlock) void k_discover(DiscParams p) {
+__global__ __launch_bounds__(kBlock) void k_probe(ProbeParams p) {
+  using PL = ProbeLds<MAXW>;
   extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  uint64_t* f1 = smem + (size_t)wv * (MAXW + 1) * kWave + lane;  // word k at f1[k * kWave]
-  uint32_t* obuf = reinterpret_cast<uint32_t*>(smem + (size_t)kWavesPerBlock * (MAXW + 1) * kWave) +
-                   (size_t)wv * kBuf * 3;
-  const uint32_t seg = (blockIdx.x * kWavesPerBlock + wv) & (kSegs - 1);
-
-  const uint64_t a = p.a_lo + (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-  bool active = a < p.a_hi;
-  const int n1 = active ? (int)p.len[a] : 0;
-  if (!CONTAIN && active && p.super && p.super[a]) active = false;  // :548 read1 contained
-  if (active) {
-    const uint64_t* g = p.words + a * MAXW;
-#pragma unroll
-    for (int k = 0; k < MAXW; ++k) f1[k * kWave] = g[k];
-    f1[MAXW * kWave] = 0;
-  }
-  const int h = p.h, m = p.m, w = p.w;
-  const int J = n1 - h - 1;  // windows j = 1 .. n1-h-1 (:534)
-  if (J < 1) active = false;
-  const uint64_t nbmask = (1ULL << p.nb_log2) - 1;
+  unsigned char* base = reinterpret_cast<unsigned char*>(smem) + (size_t)wv * PL::bytes;
+  uint64_t* s_a = reinterpret_cast<uint64_t*>(base + PL::o_a);
+  uint32_t* s_cb = reinterpret_cast<uint32_t*>(base + PL::o_cb);
+  uint32_t* s_ci = reinterpret_cast<uint32_t*>(base + PL::o_ci);
+  uint32_t* s_ca = reinterpret_cast<uint32_t*>(base + PL::o_ca);
+  const int h = p.h, m = p.m;
   const int msh = 64 - 2 * m;
+  const uint64_t nbmask = (1ULL << p.nb_log2) - 1;
+  const uint64_t gw = (uint64_t)blockIdx.x * kWavesPerBlock + wv;
+  const uint32_t seg = (uint32_t)(gw & (kSegs - 1));
+  const uint64_t* const runs = p.runs + gw * p.run_cap;
+  const uint64_t nruns = p.run_cnt[gw] < p.run_cap ? p.run_cnt[gw] : p.run_cap;
+  uint32_t* const region = p.rows + gw * p.reg_cap * 3;
+  uint64_t cursor = 0;
+  uint32_t st_runs = 0, st_ent = 0, st_ver = 0, st_rows = 0;
 
-  // sliding-window minimizer state: (cur_p, cur_v) = leftmost argmin of window jn
-  int jn = 1, cur_p = 0;
-  uint64_t cur_v = 0;
-  auto H = [&](int t) -> uint64_t { return mix64(ext_fwd<kWave>(f1, t) >> msh); };
-  auto rescan = [&](int j0) {
-    for (int t = j0; t < j0 + w; ++t) {
-      const uint64_t v = H(t);
-      if (t == j0 || v < cur_v) {
-        cur_v = v;
-        cur_p = t;
-      }
-    }
-  };
-  if (active) rescan(1);
-
-  // current run: windows [jlo, jhi] share minimizer position run_p
-  int run_p = 0, jlo = 0, jhi = -1;
-  uint32_t run_fp = 0, e_idx = 0, e_end = 0;
-  uint32_t cnt = 0;  // rows in this wave's LDS buffer (wave-uniform)
-  uint32_t st_runs = 0, st_ent = 0, st_ver = 0, st_rows = 0;  // diagnostics (p.stats)
-
-  while (true) {
-    // ---- find this lane's next candidate (bucket entry passing the cheap filters)
-    bool have = false;
-    uint32_t bid = 0;
-    int o = 0, j = 0;
-    while (active) {
-      if (e_idx < e_end) {
-        const uint64_t e = p.ent[e_idx++];
-        ++st_ent;
-#ifdef MG_DEBUG_PRINT
-        if (p.n <= 4) printf("scan C=%d a=%d idx=%u e=%llx run_p=%d jlo=%d jhi=%d fp=%x\n", (int)CONTAIN, (int)a, e_idx - 1, (unsigned long long)e, run_p, jlo, jhi, run_fp);
-#endif
-        const uint32_t hi = (uint32_t)(e >> 32);
-        if ((hi >> 12) != run_fp) continue;
-        const int q = (int)((hi >> 2) & 1023u);
-        const int jj = run_p - q;
-        if (jj < jlo || jj > jhi) continue;
-        const int oo = (int)(hi & 3u);
-        const uint32_t bb = (uint32_t)e;
-        // halving: o = 1 hits are the twins of the partner's o = 0
-        // hits; o = 2/3 hits are kept only for partner >= source
-        const bool keep = CONTAIN || (oo == 0) || (oo >= 2 && (uint64_t)bb >= a);
-        if (!keep) continue;
-        have = true;
-        bid = bb;
-        o = oo;
-        j = jj;
-        break;
-      }
-      if (jn > J) {
-        active = false;
-        break;
-      }
-      // next run of windows sharing one minimizer
-      run_p = cur_p;
-      const uint64_t rv = cur_v;
-      jlo = jn;
-      int jj = jn + 1;
-      for (; jj <= J; ++jj) {
-        if (cur_p < jj) {
-          rescan(jj);
-        } else {
-          const int t = jj + w - 1;
-          const uint64_t v = H(t);
-          if (v < cur_v) {
-            cur_v = v;
-            cur_p = t;
-          }
-        }
-        if (cur_p != run_p) break;
-      }
-      jhi = jj - 1;
-      jn = jj;
-      const uint64_t bkt = rv & nbmask;
-      if (owned(bkt, p.nb_log2, p.rank, p.nranks)) {
-        run_fp = (uint32_t)(rv >> p.nb_log2) & ((1u << kFpBits) - 1);
-        e_idx = p.dir[bkt];
-        e_end = p.dir[bkt + 1];
-        ++st_runs;
-      } else {
-        e_idx = e_end = 0;
-      }
-    }
-
-    // ---- verify the candidate over the whole overlap (checkOverlap :354-383,
-    //      checkOverlapForContainedRead :302-340), partner words from HBM
+  // verify the first nc (<= 64) candidates of the list, one per lane
+  auto verify = [&](uint32_t nc) {
+    const uint32_t ci = (uint32_t)lane;
     int nrec = 0;
     uint32_t r0 = 0, r1 = 0, r2 = 0, t0 = 0, t1 = 0, t2 = 0;
-    if (have) {
+    int n1 = 0;
+    uint32_t bid = 0, info = 0, sa = 0;
+    if (ci < nc) {
+      bid = s_cb[ci];
+      info = s_ci[ci];
+      sa = s_ca[ci];
+      const uint64_t* g = p.words + (uint64_t)sa * MAXW;
+#pragma unroll
+      for (int k = 0; k < MAXW; ++k) s_a[k * kWave + lane] = g[k];
+      s_a[MAXW * kWave + lane] = 0;
+      n1 = (int)p.len[sa];
+    }
+    wave_sync();
+    if (ci < nc) {
+      const int o = (int)(info >> 30), j = (int)(info & 1023u);
+      const uint64_t* f1 = s_a + lane;
       const int n2 = p.uniform_len ? n1 : (int)p.len[bid];
       bool cond;
       int x0, y0, L;
@@ -433,7 +444,8 @@ __global__ __launch_bounds__(kBlock) void k_discover(DiscParams p) {
           cond = cond && (j >= n2 - h);
           s = j - (n2 - h);
         }
-        L = n2; y0 = 0;
+        L = n2;
+        y0 = 0;
         rcA = o >= 2;
         x0 = rcA ? n1 - s - n2 : s;
       }
@@ -446,64 +458,150 @@ __global__ __launch_bounds__(kBlock) void k_discover(DiscParams p) {
         for (int k = 0; k <= MAXW; ++k) y[k] = bg[k];
         uint64_t diff = 0;
 #pragma unroll
-        for (int c = 0; c < MAXW; ++c) {
-          if (c * 32 < L) {
-            const uint64_t av = rcA ? rc_word(ext_fwd<kWave>(f1, n1 - x0 - 32 * c - 32))
-                                    : ext_fwd<kWave>(f1, x0 + 32 * c);
-            const uint64_t bv = funnel(y[c], y[c + 1], ys);
-            const int rem = L - 32 * c;
-            const uint64_t mask = rem >= 32 ? ~0ULL : ~(~0ULL >> (2 * rem));
-            diff |= (av ^ bv) & mask;
+        for (int cc = 0; cc < MAXW; ++cc) {
+          if (cc * 32 < L) {
+            const uint64_t av = rcA ? rc_word(ext_fwd<kWave>(f1, n1 - x0 - 32 * cc - 32))
+                                    : ext_fwd<kWave>(f1, x0 + 32 * cc);
+            const uint64_t bv = funnel(y[cc], y[cc + 1], ys);
+            const int rem = L - 32 * cc;
+            const uint64_t msk = rem >= 32 ? ~0ULL : ~(~0ULL >> (2 * rem));
+            diff |= (av ^ bv) & msk;
           }
         }
-#ifdef MG_DEBUG_PRINT
-        if (p.n <= 4) printf("cand C=%d a=%d b=%u o=%d j=%d L=%d x0=%d y0=%d diff=%llx\n", (int)CONTAIN, (int)a, bid, o, j, L, x0, y0, (unsigned long long)diff);
-#endif
         if (diff == 0) {
           if (CONTAIN) {
-            atomicMax(&p.superkey[bid], ((unsigned long long)n1 << 32) | (0xFFFFFFFFu - (uint32_t)a));
+            atomicMax(&p.superkey[bid], ((unsigned long long)n1 << 32) | (0xFFFFFFFFu - sa));
           } else {
             // orientation/offset switch (:550-557) and the twin (:409-412, :841-855)
             const uint32_t orient = (o == 0) ? 3u : (o == 2 ? 2u : 1u);
             const uint32_t off = (o == 3) ? (uint32_t)(n1 - h - j) : (uint32_t)j;
             const uint32_t torient = (orient == 3u) ? 0u : orient;
             const uint32_t toff = (uint16_t)(n2 + off - n1);
-            r0 = (uint32_t)a + 1; r1 = bid + 1; r2 = (orient << 16) | off;
-            t0 = bid + 1; t1 = (uint32_t)a + 1; t2 = (torient << 16) | toff;
-            nrec = (bid == (uint32_t)a && o == 0) ? 4 : 2;  // self o=0 hit: also stands for its o=1 twin
+            r0 = sa + 1; r1 = bid + 1; r2 = (orient << 16) | off;
+            t0 = bid + 1; t1 = sa + 1; t2 = (torient << 16) | toff;
+            nrec = (bid == sa && o == 0) ? 4 : 2;  // self o=0 hit also stands for its o=1 twin
             st_rows += nrec;
           }
         }
       }
     }
-
-#ifdef MG_DEBUG_PRINT
-    if (p.n <= 4 && have) printf("have a=%d b=%u o=%d j=%d nrec=%d\n", (int)a, bid, o, j, nrec);
-#endif
-    // ---- wavefront compaction into the LDS row buffer, flush >= kFlush rows
     if (!CONTAIN) {
       const uint64_t b2 = __ballot(nrec >= 2), b4 = __ballot(nrec == 4);
-      const uint32_t total = 2u * (uint32_t)(__popcll(b2) + __popcll(b4));
-      if (total) {
-        const uint64_t lt = lanemask_lt();
-        const uint32_t pre = 2u * (uint32_t)(__popcll(b2 & lt) + __popcll(b4 & lt));
-        uint32_t* d = obuf + (cnt + pre) * 3;
-        for (int rr = 0; rr < nrec; rr += 2) {
-          d[0] = r0; d[1] = r1; d[2] = r2;
-          d[3] = t0; d[4] = t1; d[5] = t2;
-          d += 6;
+      const uint32_t tot = 2u * (uint32_t)(__popcll(b2) + __popcll(b4));
+      if (tot) {
+        if (cursor + tot <= p.reg_cap) {
+          const uint64_t lt = lanemask_lt();
+          const uint32_t pr = 2u * (uint32_t)(__popcll(b2 & lt) + __popcll(b4 & lt));
+          uint32_t* d = region + (cursor + pr) * 3;
+          for (int rr = 0; rr < nrec; rr += 2) {
+            d[0] = r0; d[1] = r1; d[2] = r2;
+            d[3] = t0; d[4] = t1; d[5] = t2;
+            d += 6;
+          }
         }
-        cnt += total;
-        __builtin_amdgcn_wave_barrier();
-        if (cnt >= (uint32_t)kFlush) {
-          flush_rows(p, obuf, cnt, seg, lane);
-          cnt = 0;
-        }
+        cursor += tot;  // keeps counting past the capacity: the host resizes and reruns
       }
     }
-    if (__ballot(active) == 0) break;
+    wave_sync();
+  };
+
+  uint32_t ncand = 0;
+  for (uint64_t r0i = 0; r0i < nruns && p.phase_limit > 4; r0i += kWave) {
+    const uint64_t k = r0i + (uint64_t)lane;
+    bool act = k < nruns;
+    const uint64_t rec = act ? runs[k] : 0;
+    const uint32_t ra = (uint32_t)rec;
+    const int rp = (int)((rec >> 32) & 1023u);
+    const int rjlo = (int)((rec >> 42) & 1023u), rjhi = (int)((rec >> 52) & 1023u);
+    uint32_t fp = 0;
+    uint64_t b = 0;
+    if (act) {
+      const uint64_t* g = p.words + (uint64_t)ra * MAXW;
+      const int wi = rp >> 5, sh = (rp & 31) << 1;
+      const uint64_t v = mix64(funnel(g[wi], g[wi + 1], sh) >> msh);  // bucket + fingerprint
+      b = v & nbmask;
+      fp = (uint32_t)(v >> p.nb_log2) & ((1u << kFpBits) - 1);
+      act = owned(b, p.nb_log2, p.rank, p.nranks);
+      if (act) ++st_runs;
+    }
+    while (__ballot(act)) {
+      uint32_t c = 0;
+      uint64_t e[kCell];
+      if (act) {
+        c = p.cnt[b];
+        const ulonglong2* cp = reinterpret_cast<const ulonglong2*>(p.cells + b * kCell);
+#pragma unroll
+        for (int s = 0; s < kCell / 2; ++s) {
+          const ulonglong2 x = cp[s];
+          e[2 * s] = x.x;
+          e[2 * s + 1] = x.y;
+        }
+      } else {
+#pragma unroll
+        for (int s = 0; s < kCell; ++s) e[s] = 0;
+      }
+      const uint32_t nv = act ? (c < (uint32_t)kCell ? c : (uint32_t)kCell) : 0u;
+      st_ent += nv;
+      uint32_t mask = 0;
+      if (p.phase_limit > 5) {
+#pragma unroll
+        for (int s = 0; s < kCell; ++s) {
+          const uint32_t hi = (uint32_t)(e[s] >> 32);
+          const int j = rp - (int)((hi >> 2) & 1023u);
+          const int oo = (int)(hi & 3u);
+          bool keep = (uint32_t)s < nv && (hi >> 12) == fp && j >= rjlo && j <= rjhi;
+          // halving: o=1 hits are twins of the partner's o=0
+          // hits; o=2/3 hits are kept only for partner >= source
+          keep = keep && (CONTAIN || oo == 0 || (oo >= 2 && (uint32_t)e[s] >= ra));
+          mask |= (keep ? 1u : 0u) << s;
+        }
+      }
+      uint32_t total;
+      const uint32_t pre = wave_excl_scan((uint32_t)__popc(mask), lane, &total);
+      // append in passes so the list (capacity 2 x 64) never overflows
+      for (uint32_t c0 = 0; c0 < total; c0 += kWave) {
+        uint32_t at = pre;
+#pragma unroll
+        for (int s = 0; s < kCell; ++s) {
+          if (mask & (1u << s)) {
+            if (at >= c0 && at < c0 + kWave) {
+              const uint32_t hi = (uint32_t)(e[s] >> 32);
+              const int j = rp - (int)((hi >> 2) & 1023u);
+              const uint32_t slot = ncand + (at - c0);
+              s_cb[slot] = (uint32_t)e[s];
+              s_ci[slot] = ((hi & 3u) << 30) | (uint32_t)j;
+              s_ca[slot] = ra;
+            }
+            ++at;
+          }
+        }
+        ncand += min(total - c0, (uint32_t)kWave);
+        wave_sync();
+        if (ncand >= (uint32_t)kWave) {
+          if (p.phase_limit > 6) verify(kWave);
+          const uint32_t rest = ncand - kWave;
+          uint32_t mb = 0, mi = 0, ma = 0;
+          if ((uint32_t)lane < rest) {
+            mb = s_cb[kWave + lane];
+            mi = s_ci[kWave + lane];
+            ma = s_ca[kWave + lane];
+          }
+          wave_sync();
+          if ((uint32_t)lane < rest) {
+            s_cb[lane] = mb;
+            s_ci[lane] = mi;
+            s_ca[lane] = ma;
+          }
+          ncand = rest;
+          wave_sync();
+        }
+      }
+      act = act && c > (uint32_t)kCell;
+      b = (b + 1) & nbmask;
+    }
   }
-  if (!CONTAIN && cnt) flush_rows(p, obuf, cnt, seg, lane);
+  if (ncand && p.phase_limit > 6) verify(ncand);
+  if (!CONTAIN && lane == 0) p.reg_cnt[gw] = cursor;
   if (p.stats) {
     uint32_t v[4] = {st_runs, st_ent, st_ver, st_rows};
 #pragma unroll
@@ -514,6 +612,17 @@ __global__ __launch_bounds__(kBlock) void k_discover(DiscParams p) {
       if (lane == 0) atomicAdd(&p.stats[seg * 4 + i], (unsigned long long)x);
     }
   }
+}
+
+// Gather per-wavefront row regions into a contiguous array (copy-out path only).
+__global__ __launch_bounds__(kBlock) void k_compact_rows(const uint32_t* __restrict__ rows, uint64_t reg_cap,
+                                                        const uint64_t* __restrict__ prefix,
+                                                        uint32_t* __restrict__ out) {
+  const uint64_t r = blockIdx.x;
+  const uint64_t c = (prefix[r + 1] - prefix[r]) * 3;
+  const uint32_t* src = rows + r * reg_cap * 3;
+  uint32_t* dst = out + prefix[r] * 3;
+  for (uint64_t i = threadIdx.x; i < c; i += kBlock) dst[i] = src[i];
 }
 
 __global__ __launch_bounds__(kBlock) void k_super_finalize(const unsigned long long* __restrict__ key,
@@ -527,8 +636,8 @@ __global__ __launch_bounds__(kBlock) void k_super_finalize(const unsigned long l
   if (s) atomicOr(any, 1u);
 }
 
-// getListOfReads(key) (HashTable.cpp:202-221): scan the minimizer bucket of the
-// query key and keep entries whose key string equals it exactly.
+// getListOfReads(key) (HashTable.cpp:202-221): walk the query key's home cell
+// chain and keep entries whose key string equals it exactly.
 template <int MAXW>
 __global__ __launch_bounds__(kBlock) void k_lookup_key(IndexParams p, const uint64_t* __restrict__ qkey,
                                                       int qwords, unsigned long long* __restrict__ out,
@@ -536,59 +645,55 @@ __global__ __launch_bounds__(kBlock) void k_lookup_key(IndexParams p, const uint
   __shared__ uint64_t q[40];  // h <= 1055 -> at most 33 words + over-read
   __shared__ uint64_t qv;
   __shared__ int qq;
-  const int h = p.h, m = p.m, w = p.w;
+  const int h = p.h;
   if (threadIdx.x < 40) q[threadIdx.x] = threadIdx.x < qwords ? qkey[threadIdx.x] : 0;
   __syncthreads();
   if (threadIdx.x == 0) {
-    uint64_t best = 0;
-    int bq = 0;
-    for (int i = 0; i < w; ++i) {
-      const uint64_t v = mix64(ext_fwd<1>(q, i) >> (64 - 2 * m));
-      if (i == 0 || v < best) {
-        best = v;
-        bq = i;
-      }
-    }
-    qv = best;
-    qq = bq;
+    int qo;
+    qv = key_minimizer<1>(q, h, 0, h, p.m, p.w, &qo);  // the key itself is a "read" of length h, o = 0
+    qq = qo;
   }
   __syncthreads();
-  const uint64_t bkt = qv & ((1ULL << p.nb_log2) - 1);
+  const uint64_t mask = (1ULL << p.nb_log2) - 1;
   const uint32_t fp = (uint32_t)(qv >> p.nb_log2) & ((1u << kFpBits) - 1);
-  const uint32_t s = p.dir[bkt], e = p.dir[bkt + 1];
-  for (uint32_t i = s + threadIdx.x; i < e; i += kBlock) {
-    const uint64_t en = p.ent[i];
-    const uint32_t hi = (uint32_t)(en >> 32);
-    if ((hi >> 12) != fp || (int)((hi >> 2) & 1023u) != qq) continue;
-    const int o = (int)(hi & 3u);
-    const uint32_t r = (uint32_t)en;
-    const uint64_t* g = p.words + (uint64_t)r * MAXW;
-    const int n = p.len[r];
-    // key string of (r, o) vs the query, 32 bases at a time
-    uint64_t diff = 0;
-    for (int c = 0; c * 32 < h; ++c) {
-      uint64_t kv;
-      if (o < 2) {
-        const int pos = (o == 0 ? 0 : n - h) + 32 * c;
-        kv = funnel(g[pos >> 5], g[(pos >> 5) + 1], (pos & 31) << 1);
-      } else {
-        // R[b, b+32) = rc(F[n-b-32, n-b)), b = (o == 2 ? 0 : n-h) + 32c
-        const int b = (o == 2 ? 0 : n - h) + 32 * c;
-        const int pos = n - b - 32;
-        uint64_t fw;
-        if (pos < 0)
-          fw = g[0] >> (-pos * 2);
-        else
-          fw = funnel(g[pos >> 5], g[(pos >> 5) + 1], (pos & 31) << 1);
-        kv = rc_word(fw);
+  uint64_t b = qv & mask;
+  for (uint64_t probe = 0; probe <= mask; ++probe) {
+    const uint32_t c = p.cnt[b];
+    const uint32_t nv = c < (uint32_t)kCell ? c : (uint32_t)kCell;
+    if (threadIdx.x < nv) {
+      const uint64_t en = p.cells[b * kCell + threadIdx.x];
+      const uint32_t hi = (uint32_t)(en >> 32);
+      if ((hi >> 12) == fp && (int)((hi >> 2) & 1023u) == qq) {
+        const int o = (int)(hi & 3u);
+        const uint32_t r = (uint32_t)en;
+        const uint64_t* g = p.words + (uint64_t)r * MAXW;
+        const int n = p.len[r];
+        // key string of (r, o) vs the query, 32 bases at a time
+        uint64_t diff = 0;
+        for (int cc = 0; cc * 32 < h; ++cc) {
+          uint64_t kv;
+          if (o < 2) {
+            const int pos = (o == 0 ? 0 : n - h) + 32 * cc;
+            kv = funnel(g[pos >> 5], g[(pos >> 5) + 1], (pos & 31) << 1);
+          } else {
+            // R[bb, bb+32) = rc(F[n-bb-32, n-bb)), bb = (o == 2 ? 0 : n-h) + 32cc
+            const int bb = (o == 2 ? 0 : n - h) + 32 * cc;
+            const int pos = n - bb - 32;
+            const uint64_t fw = pos < 0 ? g[0] >> (-pos * 2) : funnel(g[pos >> 5], g[(pos >> 5) + 1], (pos & 31) << 1);
+            kv = rc_word(fw);
+          }
+          const int rem = h - 32 * cc;
+          const uint64_t msk = rem >= 32 ? ~0ULL : ~(~0ULL >> (2 * rem));
+          diff |= (kv ^ ext_fwd<1>(q, 32 * cc)) & msk;
+        }
+        if (!diff) {
+          const unsigned int slot = atomicAdd(nout, 1u);
+          if (slot < cap) out[slot] = ((unsigned long long)(r + 1)) | ((unsigned long long)o << 62);
+        }
       }
-      const int rem = h - 32 * c;
-      const uint64_t mask = rem >= 32 ? ~0ULL : ~(~0ULL >> (2 * rem));
-      diff |= (kv ^ ext_fwd<1>(q, 32 * c)) & mask;
     }
-    if (diff) continue;
-    const unsigned int slot = atomicAdd(nout, 1u);
-    if (slot < cap) out[slot] = ((unsigned long long)(r + 1)) | ((unsigned long long)o << 62);
+    if (c <= (uint32_t)kCell) break;
+    b = (b + 1) & mask;
   }
 }
 
@@ -610,11 +715,9 @@ struct mg_ctx {
   uint32_t l = 0, h = 0, m = 0, w = 0;
   uint32_t nb_log2 = 0, nb_log2_opt = 0;
   bool index_ready = false;
-  uint32_t* d_cnt = nullptr;
-  uint32_t* d_dir = nullptr;
-  uint32_t* d_bsum = nullptr;
-  uint64_t* d_ent = nullptr;
-  size_t cnt_cap = 0, dir_cap = 0, bsum_cap = 0, ent_cap = 0;
+  uint32_t* d_cnt = nullptr;    // per-cell fill counts
+  uint64_t* d_cells = nullptr;  // cells of kCell entries
+  size_t cnt_cap = 0, cells_cap = 0;
   // containment
   unsigned long long* d_superkey = nullptr;
   uint32_t* d_super = nullptr;
@@ -627,12 +730,25 @@ struct mg_ctx {
   unsigned long long* d_seg = nullptr;
   uint64_t n_rows = 0;
   std::vector<unsigned long long> seg_host;
+  uint64_t seg_cap_regions = 0;
   bool stats = false;
   unsigned long long* d_stats = nullptr;
   mg_counters counters{};
   // shard
   uint32_t rank = 0, nranks = 1;
   uint64_t read_lo = 0, read_hi = 0;
+  uint32_t max_blocks = 8192;  // cap on the persistent discovery grid (blocks of 4 wavefronts)
+  int phase_limit = 99;        // diagnostics (option "phase_limit")
+  int n_cu = 256;              // compute units of the device
+  uint64_t nreg = 0;           // row regions of the last discovery launch (one per wavefront)
+  uint64_t* d_runs = nullptr;  // run records, one region per wavefront
+  size_t runs_cap = 0;
+  uint64_t run_cap = 0, run_cap_need = 0;
+  unsigned long long* d_run_cnt = nullptr;
+  size_t run_cnt_cap = 0;
+  std::vector<unsigned long long> run_cnt_host;
+  uint32_t* d_compact = nullptr;
+  size_t compact_cap = 0;
   // timing
   hipEvent_t ev[8] = {};
   mg_timings t{};
@@ -713,65 +829,111 @@ IndexParams index_params(mg_ctx* ctx) {
   p.rank = ctx->rank;
   p.nranks = ctx->nranks;
   p.cnt = ctx->d_cnt;
-  p.dir = ctx->d_dir;
-  p.ent = ctx->d_ent;
+  p.cells = ctx->d_cells;
   return p;
 }
 
 template <int W>
 struct LaunchIndex {
-  static int run(mg_ctx* ctx, bool fill) {
+  static int run(mg_ctx* ctx) {
     IndexParams p = index_params(ctx);
     const uint32_t grid = (uint32_t)((ctx->n + kBlock - 1) / kBlock);
     const size_t lds = (size_t)(W + 1) * kBlock * sizeof(uint64_t);
     if (grid == 0) return 0;
-    if (fill) {
-      allow_lds(k_index_keys<W, true>, lds);
-      hipLaunchKernelGGL((k_index_keys<W, true>), dim3(grid), dim3(kBlock), lds, ctx->stream, p);
-    } else {
-      allow_lds(k_index_keys<W, false>, lds);
-      hipLaunchKernelGGL((k_index_keys<W, false>), dim3(grid), dim3(kBlock), lds, ctx->stream, p);
-    }
+    allow_lds(k_index_build<W>, lds);
+    hipLaunchKernelGGL((k_index_build<W>), dim3(grid), dim3(kBlock), lds, ctx->stream, p);
     return hipGetLastError() == hipSuccess ? 0 : -1;
   }
 };
 
+// Persistent grids: exactly the resident blocks (a larger grid would run a
+// second, partly idle round of wavefronts).  Scan and probe use the same
+// wavefront count: probe wavefront r consumes scan region r.
+template <typename K>
+uint32_t resident_blocks(mg_ctx* ctx, K kernel, size_t lds, uint64_t want) {
+  allow_lds(kernel, lds);
+  int per_cu = 0;
+  (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kBlock, lds);
+  const uint64_t resident = (uint64_t)std::max(1, per_cu) * (uint64_t)std::max(1, ctx->n_cu);
+  return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(std::min<uint64_t>(want, resident), ctx->max_blocks));
+}
+
 template <int W>
 struct LaunchDiscover {
+  // scan + probe; `contain` selects markContainedReads semantics
   static int run(mg_ctx* ctx, bool contain) {
-    DiscParams p{};
-    p.words = ctx->d_words;
-    p.len = ctx->d_len;
-    p.n = ctx->n;
-    p.h = (int)ctx->h;
-    p.m = (int)ctx->m;
-    p.w = (int)ctx->w;
-    p.nb_log2 = ctx->nb_log2;
-    p.rank = ctx->rank;
-    p.nranks = ctx->nranks;
-    p.dir = ctx->d_dir;
-    p.ent = ctx->d_ent;
-    p.super = (ctx->contained_done && ctx->super_any) ? ctx->d_super : nullptr;
-    p.superkey = ctx->d_superkey;
-    p.rows = ctx->d_rows;
-    p.seg_cnt = ctx->d_seg;
-    p.seg_cap = ctx->rows_cap / kSegs;
-    p.uniform_len = ctx->minlen == ctx->maxlen;
-    p.stats = contain ? nullptr : (ctx->stats ? ctx->d_stats : nullptr);
-    // containment scans every read as read1 (:235); discovery only this shard's sources
-    p.a_lo = contain ? 0 : ctx->read_lo;
-    p.a_hi = contain ? ctx->n : (ctx->read_hi ? std::min<uint64_t>(ctx->read_hi, ctx->n) : ctx->n);
-    if (p.a_hi <= p.a_lo) return 0;
-    const uint32_t grid = (uint32_t)((p.a_hi - p.a_lo + kBlock - 1) / kBlock);
-    const size_t lds_words = (size_t)kWavesPerBlock * (W + 1) * kWave * sizeof(uint64_t);
-    if (contain) {
-      allow_lds(k_discover<W, true>, lds_words);
-      hipLaunchKernelGGL((k_discover<W, true>), dim3(grid), dim3(kBlock), lds_words, ctx->stream, p);
-    } else {
-      const size_t lds = lds_words + (size_t)kWavesPerBlock * kBuf * 3 * sizeof(uint32_t);
-      allow_lds(k_discover<W, false>, lds);
-      hipLaunchKernelGGL((k_discover<W, false>), dim3(grid), dim3(kBlock), lds, ctx->stream, p);
+    const uint64_t a_lo = contain ? 0 : ctx->read_lo;
+    const uint64_t a_hi = contain ? ctx->n : (ctx->read_hi ? std::min<uint64_t>(ctx->read_hi, ctx->n) : ctx->n);
+    ctx->nreg = 0;
+    if (a_hi <= a_lo) return 0;
+    const uint64_t ngroups = (a_hi - a_lo + kWave - 1) / kWave;
+    const uint64_t want = (ngroups + kWavesPerBlock - 1) / kWavesPerBlock;
+    const size_t lds_scan = (size_t)kWavesPerBlock * ctx->w * kWave * sizeof(uint32_t);
+    const size_t lds_probe = (size_t)kWavesPerBlock * ProbeLds<W>::bytes;
+    uint32_t grid = resident_blocks(ctx, k_scan<W>, lds_scan, want);
+    grid = std::min(grid, contain ? resident_blocks(ctx, k_probe<W, true>, lds_probe, want)
+                                  : resident_blocks(ctx, k_probe<W, false>, lds_probe, want));
+    const uint64_t nw = (uint64_t)grid * kWavesPerBlock;
+    ctx->nreg = nw;
+    // run regions: expected runs per read ~ 2 J / (w + 1) + 1 (minimizer density)
+    const uint64_t J = ctx->maxlen > ctx->h + 1 ? ctx->maxlen - ctx->h - 1 : 1;
+    const uint64_t per_read = std::min<uint64_t>(J, 3 * (2 * J / (ctx->w + 1) + 2));
+    const uint64_t groups_per_wave = (ngroups + nw - 1) / nw;
+    uint64_t run_cap = std::max<uint64_t>(ctx->run_cap_need, groups_per_wave * kWave * per_read);
+    if (run_cap * nw > ctx->runs_cap) {
+      if (ctx->d_runs) (void)hipFree(ctx->d_runs);
+      ctx->d_runs = nullptr;
+      if (hipMalloc(&ctx->d_runs, run_cap * nw * sizeof(uint64_t)) != hipSuccess) return -1;
+      ctx->runs_cap = run_cap * nw;
     }
+    run_cap = ctx->runs_cap / nw;
+    ctx->run_cap = run_cap;
+    if (ctx->run_cnt_cap < nw) {
+      if (ctx->d_run_cnt) (void)hipFree(ctx->d_run_cnt);
+      ctx->d_run_cnt = nullptr;
+      if (hipMalloc(&ctx->d_run_cnt, nw * sizeof(unsigned long long)) != hipSuccess) return -1;
+      ctx->run_cnt_cap = nw;
+    }
+    ScanParams sp{};
+    sp.words = ctx->d_words;
+    sp.len = ctx->d_len;
+    sp.super = (!contain && ctx->contained_done && ctx->super_any) ? ctx->d_super : nullptr;
+    sp.a_lo = a_lo;
+    sp.a_hi = a_hi;
+    sp.h = (int)ctx->h;
+    sp.m = (int)ctx->m;
+    sp.w = (int)ctx->w;
+    sp.runs = ctx->d_runs;
+    sp.run_cnt = ctx->d_run_cnt;
+    sp.run_cap = run_cap;
+    (void)hipEventRecord(ctx->ev[6], ctx->stream);
+    hipLaunchKernelGGL((k_scan<W>), dim3(grid), dim3(kBlock), lds_scan, ctx->stream, sp);
+    (void)hipEventRecord(ctx->ev[7], ctx->stream);
+    ProbeParams pp{};
+    pp.words = ctx->d_words;
+    pp.len = ctx->d_len;
+    pp.h = (int)ctx->h;
+    pp.m = (int)ctx->m;
+    pp.nb_log2 = ctx->nb_log2;
+    pp.rank = ctx->rank;
+    pp.nranks = ctx->nranks;
+    pp.cnt = ctx->d_cnt;
+    pp.cells = ctx->d_cells;
+    pp.super = (!contain && ctx->contained_done && ctx->super_any) ? ctx->d_super : nullptr;
+    pp.superkey = ctx->d_superkey;
+    pp.runs = ctx->d_runs;
+    pp.run_cnt = ctx->d_run_cnt;
+    pp.run_cap = run_cap;
+    pp.rows = ctx->d_rows;
+    pp.reg_cnt = ctx->d_seg;
+    pp.reg_cap = contain ? 0 : ctx->rows_cap / nw;
+    pp.uniform_len = ctx->minlen == ctx->maxlen;
+    pp.stats = contain ? nullptr : (ctx->stats ? ctx->d_stats : nullptr);
+    pp.phase_limit = contain ? 99 : ctx->phase_limit;
+    if (contain)
+      hipLaunchKernelGGL((k_probe<W, true>), dim3(grid), dim3(kBlock), lds_probe, ctx->stream, pp);
+    else
+      hipLaunchKernelGGL((k_probe<W, false>), dim3(grid), dim3(kBlock), lds_probe, ctx->stream, pp);
     return hipGetLastError() == hipSuccess ? 0 : -1;
   }
 };
@@ -786,24 +948,63 @@ struct LaunchLookup {
   }
 };
 
-int scan_dir(mg_ctx* ctx, uint64_t nb) {
-  const uint64_t nblocks = (nb + kScanTile - 1) / kScanTile;
-  MG_TRY(ensure(&ctx->d_bsum, &ctx->bsum_cap, nblocks));
-  hipLaunchKernelGGL(k_scan_reduce, dim3((uint32_t)nblocks), dim3(kBlock), 0, ctx->stream, ctx->d_cnt, nb,
-                     ctx->d_bsum);
-  hipLaunchKernelGGL(k_scan_bsums, dim3(1), dim3(kBlock), 0, ctx->stream, ctx->d_bsum, (uint32_t)nblocks);
-  hipLaunchKernelGGL(k_scan_apply, dim3((uint32_t)nblocks), dim3(kBlock), 0, ctx->stream, ctx->d_cnt, nb,
-                     ctx->d_bsum, ctx->d_dir);
-  MG_TRY(hipGetLastError());
-  return 0;
-}
-
 float elapsed(hipEvent_t a, hipEvent_t b) {
   float ms = 0.f;
   if (hipEventElapsedTime(&ms, a, b) != hipSuccess) return 0.f;
   return ms;
 }
 
+}  // namespace
+
+namespace {
+// Launch scan + probe, then check both region kinds for overflow; on overflow
+// the exact need is known (the kernels keep counting), so resize and rerun.
+int run_discover(mg_ctx* ctx, bool contain) {
+  for (int attempt = 0; attempt < 3; ++attempt) {
+    if (dispatch_w<LaunchDiscover>(ctx->maxw, ctx, contain)) {
+      ctx->err = "discovery launch failed";
+      return -1;
+    }
+    if (ctx->run_cnt_host.size() < ctx->nreg) ctx->run_cnt_host.resize(ctx->nreg);
+    if (ctx->seg_host.size() < ctx->nreg) ctx->seg_host.resize(ctx->nreg);
+    if (ctx->nreg) {
+      MG_TRY(hipMemcpyAsync(ctx->run_cnt_host.data(), ctx->d_run_cnt, ctx->nreg * sizeof(unsigned long long),
+                            hipMemcpyDeviceToHost, ctx->stream));
+      if (!contain)
+        MG_TRY(hipMemcpyAsync(ctx->seg_host.data(), ctx->d_seg, ctx->nreg * sizeof(unsigned long long),
+                              hipMemcpyDeviceToHost, ctx->stream));
+    }
+    MG_TRY(hipStreamSynchronize(ctx->stream));
+    uint64_t run_max = 0, row_max = 0, rows = 0;
+    for (uint64_t r = 0; r < ctx->nreg; ++r) {
+      run_max = std::max<uint64_t>(run_max, ctx->run_cnt_host[r]);
+      if (!contain) {
+        row_max = std::max<uint64_t>(row_max, ctx->seg_host[r]);
+        rows += ctx->seg_host[r];
+      }
+    }
+    const uint64_t reg_cap = ctx->nreg ? ctx->rows_cap / ctx->nreg : 0;
+    bool again = false;
+    if (run_max > ctx->run_cap) {
+      ctx->run_cap_need = run_max + run_max / 8 + 64;
+      again = true;
+    }
+    if (!contain && row_max > reg_cap && !again) {
+      const uint64_t want = (row_max + row_max / 4 + 1024) * ctx->nreg;
+      if (ctx->d_rows) (void)hipFree(ctx->d_rows);
+      ctx->d_rows = nullptr;
+      MG_TRY(hipMalloc(&ctx->d_rows, want * 3 * sizeof(uint32_t)));
+      ctx->rows_cap = want;
+      again = true;
+    }
+    if (!again) {
+      if (!contain) ctx->n_rows = rows;
+      return 0;
+    }
+  }
+  ctx->err = "discovery buffers overflow after resize";
+  return -1;
+}
 }  // namespace
 
 extern "C" {
@@ -822,6 +1023,9 @@ int mg_create(mg_ctx** out, int device) {
   if (device < 0 || device >= ndev) return -4;
   mg_ctx* ctx = new mg_ctx();
   ctx->device = device;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
+    ctx->n_cu = prop.multiProcessorCount;
   if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
     delete ctx;
     return -1;
@@ -840,8 +1044,9 @@ void mg_destroy(mg_ctx* ctx) {
   if (!ctx) return;
   (void)hipSetDevice(ctx->device);
   (void)hipStreamSynchronize(ctx->stream);
-  void* bufs[] = {ctx->d_words, ctx->d_len, ctx->d_cnt, ctx->d_dir, ctx->d_bsum, ctx->d_ent,
-                  ctx->d_superkey, ctx->d_super, ctx->d_any, ctx->d_rows, ctx->d_seg, ctx->d_stats};
+  void* bufs[] = {ctx->d_words, ctx->d_len, ctx->d_cnt, ctx->d_cells,
+                  ctx->d_superkey, ctx->d_super, ctx->d_any, ctx->d_rows, ctx->d_seg, ctx->d_stats,
+                  ctx->d_compact, ctx->d_runs, ctx->d_run_cnt};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   for (auto& e : ctx->ev)
@@ -965,6 +1170,14 @@ int mg_set_option(mg_ctx* ctx, const char* name, int64_t value) {
     ctx->index_ready = false;
     return 0;
   }
+  if (!strcmp(name, "phase_limit")) {
+    ctx->phase_limit = value > 0 ? (int)value : 99;
+    return 0;
+  }
+  if (!strcmp(name, "max_blocks")) {
+    ctx->max_blocks = value > 0 ? (uint32_t)value : 8192u;
+    return 0;
+  }
   if (!strcmp(name, "stats")) {
     ctx->stats = value != 0;
     return 0;
@@ -1003,22 +1216,20 @@ int mg_build_index(mg_ctx* ctx, uint32_t min_overlap, uint32_t seed_k) {
   ctx->h = h;
   ctx->m = m;
   ctx->w = w;
-  uint32_t nbl = ctx->nb_log2_opt;
-  if (!nbl) {
-    // about one bucket per read: 4 keys per read, ~2-3 keys share a minimizer
-    nbl = 10;
-    while (nbl < 30 && (1ull << nbl) < ctx->n) nbl++;
-  }
+  // cells: about one per read (4 keys per read, kCell slots per cell -> at most
+  // half full); an explicit nb_log2 is raised until slots >= 1.25 x keys,
+  // which bounds every probe chain
+  uint32_t nbl = ctx->nb_log2_opt ? ctx->nb_log2_opt : 10;
+  if (!ctx->nb_log2_opt)
+    while (nbl < 31 && (1ull << nbl) < ctx->n) nbl++;
+  while (nbl < 31 && (1ull << nbl) * kCell < 5 * std::max<uint64_t>(ctx->n, 1)) nbl++;
   ctx->nb_log2 = nbl;
-  const uint64_t nb = 1ull << nbl;
-  MG_TRY(ensure(&ctx->d_cnt, &ctx->cnt_cap, nb));
-  MG_TRY(ensure(&ctx->d_dir, &ctx->dir_cap, nb + 1));
-  MG_TRY(ensure(&ctx->d_ent, &ctx->ent_cap, std::max<uint64_t>(4 * ctx->n, 1)));
+  const uint64_t nc = 1ull << nbl;
+  MG_TRY(ensure(&ctx->d_cnt, &ctx->cnt_cap, nc));
+  MG_TRY(ensure(&ctx->d_cells, &ctx->cells_cap, nc * kCell));
   MG_TRY(hipEventRecord(ctx->ev[0], ctx->stream));
-  MG_TRY(hipMemsetAsync(ctx->d_cnt, 0, nb * sizeof(uint32_t), ctx->stream));
-  if (dispatch_w<LaunchIndex>(ctx->maxw, ctx, false)) return set_err(ctx, "index count launch failed");
-  if (scan_dir(ctx, nb)) return -1;
-  if (dispatch_w<LaunchIndex>(ctx->maxw, ctx, true)) return set_err(ctx, "index fill launch failed");
+  MG_TRY(hipMemsetAsync(ctx->d_cnt, 0, nc * sizeof(uint32_t), ctx->stream));
+  if (dispatch_w<LaunchIndex>(ctx->maxw, ctx)) return set_err(ctx, "index build launch failed");
   MG_TRY(hipEventRecord(ctx->ev[1], ctx->stream));
   MG_TRY(hipEventSynchronize(ctx->ev[1]));
   ctx->t.index_ms = elapsed(ctx->ev[0], ctx->ev[1]);
@@ -1049,7 +1260,7 @@ int mg_mark_contained(mg_ctx* ctx, uint32_t* super_out) {
     // buckets (the containment pass is small, only for mixed lengths)
     const uint32_t r = ctx->rank, nr = ctx->nranks;
     if (nr > 1) return set_err(ctx, "containment with a bucket-sharded index is not supported yet");
-    if (dispatch_w<LaunchDiscover>(ctx->maxw, ctx, true)) return set_err(ctx, "containment launch failed");
+    if (run_discover(ctx, true)) return -1;
     (void)r;
     if (ctx->n)
       hipLaunchKernelGGL(k_super_finalize, dim3((uint32_t)((ctx->n + kBlock - 1) / kBlock)), dim3(kBlock), 0,
@@ -1081,74 +1292,82 @@ int mg_find_overlaps(mg_ctx* ctx, uint64_t* n_rows) {
   MG_TRY(hipSetDevice(ctx->device));
   if (!ctx->index_ready) return set_err(ctx, "mg_build_index must run first");
   if (!ctx->contained_done && mg_mark_contained(ctx, nullptr)) return -1;
-  if (!ctx->d_seg) MG_TRY(hipMalloc(&ctx->d_seg, kSegs * sizeof(unsigned long long)));
+  const uint64_t max_regions = (uint64_t)ctx->max_blocks * kWavesPerBlock;
+  if (ctx->seg_cap_regions < max_regions) {
+    if (ctx->d_seg) (void)hipFree(ctx->d_seg);
+    ctx->d_seg = nullptr;
+    MG_TRY(hipMalloc(&ctx->d_seg, max_regions * sizeof(unsigned long long)));
+    ctx->seg_cap_regions = max_regions;
+  }
   const uint64_t nsrc = (ctx->read_hi ? std::min(ctx->read_hi, ctx->n) : ctx->n) -
                         std::min(ctx->read_lo, ctx->n);
-  uint64_t want = ctx->rows_cap_opt ? ctx->rows_cap_opt : std::max<uint64_t>(1u << 20, 48 * nsrc);
-  ctx->seg_host.assign(kSegs, 0);
-  for (int attempt = 0; attempt < 3; ++attempt) {
-    want = (want + kSegs - 1) / kSegs * kSegs;
-    if (want > ctx->rows_cap) {
-      if (ctx->d_rows) (void)hipFree(ctx->d_rows);
-      ctx->d_rows = nullptr;
-      MG_TRY(hipMalloc(&ctx->d_rows, want * 3 * sizeof(uint32_t)));
-      ctx->rows_cap = want;
-    }
-    MG_TRY(hipMemsetAsync(ctx->d_seg, 0, kSegs * sizeof(unsigned long long), ctx->stream));
-    if (ctx->stats) {
-      if (!ctx->d_stats) MG_TRY(hipMalloc(&ctx->d_stats, kSegs * 4 * sizeof(unsigned long long)));
-      MG_TRY(hipMemsetAsync(ctx->d_stats, 0, kSegs * 4 * sizeof(unsigned long long), ctx->stream));
-    }
-    MG_TRY(hipEventRecord(ctx->ev[4], ctx->stream));
-    if (dispatch_w<LaunchDiscover>(ctx->maxw, ctx, false)) return set_err(ctx, "discovery launch failed");
-    MG_TRY(hipEventRecord(ctx->ev[5], ctx->stream));
-    MG_TRY(hipMemcpyAsync(ctx->seg_host.data(), ctx->d_seg, kSegs * sizeof(unsigned long long),
-                          hipMemcpyDeviceToHost, ctx->stream));
-    MG_TRY(hipStreamSynchronize(ctx->stream));
-    const uint64_t seg_cap = ctx->rows_cap / kSegs;
-    uint64_t total = 0, mx = 0;
-    for (auto c : ctx->seg_host) {
-      total += c;
-      mx = std::max<uint64_t>(mx, c);
-    }
-    ctx->t.overlap_ms = elapsed(ctx->ev[4], ctx->ev[5]);
-    ctx->n_rows = total;
-    if (ctx->stats) {
-      std::vector<unsigned long long> st(kSegs * 4);
-      MG_TRY(hipMemcpy(st.data(), ctx->d_stats, st.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
-      uint64_t acc[4] = {0, 0, 0, 0};
-      for (int s = 0; s < kSegs; ++s)
-        for (int i = 0; i < 4; ++i) acc[i] += st[s * 4 + i];
-      ctx->counters.runs = acc[0];
-      ctx->counters.entries = acc[1];
-      ctx->counters.verified = acc[2];
-      ctx->counters.rows = acc[3];
-      ctx->counters.sources = (ctx->read_hi ? std::min(ctx->read_hi, ctx->n) : ctx->n) - std::min(ctx->read_lo, ctx->n);
-    }
-    if (mx <= seg_cap) {
-      ctx->t.total_ms = ctx->t.index_ms + ctx->t.contained_ms + ctx->t.overlap_ms;
-      if (n_rows) *n_rows = total;
-      return 0;
-    }
-    want = (mx + mx / 4 + 1024) * kSegs;  // a segment overflowed: exact need is known now
+  const uint64_t want = ctx->rows_cap_opt ? ctx->rows_cap_opt : std::max<uint64_t>(1u << 20, 48 * nsrc);
+  if (want > ctx->rows_cap) {
+    if (ctx->d_rows) (void)hipFree(ctx->d_rows);
+    ctx->d_rows = nullptr;
+    MG_TRY(hipMalloc(&ctx->d_rows, want * 3 * sizeof(uint32_t)));
+    ctx->rows_cap = want;
   }
-  return set_err(ctx, "row buffer overflow after resize");
+  if (ctx->stats) {
+    if (!ctx->d_stats) MG_TRY(hipMalloc(&ctx->d_stats, kSegs * 4 * sizeof(unsigned long long)));
+    MG_TRY(hipMemsetAsync(ctx->d_stats, 0, kSegs * 4 * sizeof(unsigned long long), ctx->stream));
+  }
+  MG_TRY(hipEventRecord(ctx->ev[4], ctx->stream));
+  if (run_discover(ctx, false)) return -1;
+  MG_TRY(hipEventRecord(ctx->ev[5], ctx->stream));
+  MG_TRY(hipEventSynchronize(ctx->ev[5]));
+  // timings of the last (successful) launch pair
+  ctx->t.scan_ms = elapsed(ctx->ev[6], ctx->ev[7]);
+  ctx->t.overlap_ms = ctx->t.scan_ms;
+  {
+    float probe = 0.f;
+    // ev[7] (after scan) .. ev[5] may include one resize retry; the kernels'
+    // own events bracket the last launch: use them for the split
+    probe = elapsed(ctx->ev[7], ctx->ev[5]);
+    ctx->t.probe_ms = probe;
+    ctx->t.overlap_ms = ctx->t.scan_ms + probe;
+  }
+  if (ctx->stats) {
+    std::vector<unsigned long long> st(kSegs * 4);
+    MG_TRY(hipMemcpy(st.data(), ctx->d_stats, st.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    uint64_t acc[4] = {0, 0, 0, 0};
+    for (int s2 = 0; s2 < kSegs; ++s2)
+      for (int i = 0; i < 4; ++i) acc[i] += st[s2 * 4 + i];
+    ctx->counters.runs = acc[0];
+    ctx->counters.entries = acc[1];
+    ctx->counters.verified = acc[2];
+    ctx->counters.rows = acc[3];
+    ctx->counters.sources = nsrc;
+  }
+  ctx->t.total_ms = ctx->t.index_ms + ctx->t.contained_ms + ctx->t.overlap_ms;
+  if (n_rows) *n_rows = ctx->n_rows;
+  return 0;
 }
 
 int mg_copy_rows(mg_ctx* ctx, mg_edge* out, uint64_t cap, uint64_t* n_copied) {
   if (!ctx) return -1;
   MG_TRY(hipSetDevice(ctx->device));
-  const uint64_t seg_cap = ctx->rows_cap / kSegs;
-  uint64_t done = 0;
-  for (int s = 0; s < kSegs && done < cap && !ctx->seg_host.empty(); ++s) {
-    const uint64_t c = std::min<uint64_t>(std::min<uint64_t>(ctx->seg_host[s], seg_cap), cap - done);
-    if (!c) continue;
-    MG_TRY(hipMemcpyAsync(out + done, ctx->d_rows + (uint64_t)s * seg_cap * 3, c * sizeof(mg_edge),
-                          hipMemcpyDeviceToHost, ctx->stream));
-    done += c;
-  }
+  if (n_copied) *n_copied = 0;
+  if (!ctx->nreg || !ctx->n_rows) return 0;
+  // gather the per-wavefront regions into one contiguous array, then one copy
+  const uint64_t reg_cap = ctx->rows_cap / ctx->nreg;
+  std::vector<uint64_t> prefix(ctx->nreg + 1, 0);
+  for (uint64_t r = 0; r < ctx->nreg; ++r)
+    prefix[r + 1] = prefix[r] + std::min<uint64_t>(ctx->seg_host[r], reg_cap);
+  const uint64_t total = prefix[ctx->nreg];
+  uint64_t* d_prefix = nullptr;
+  MG_TRY(hipMalloc(&d_prefix, prefix.size() * sizeof(uint64_t)));
+  MG_TRY(hipMemcpyAsync(d_prefix, prefix.data(), prefix.size() * sizeof(uint64_t), hipMemcpyHostToDevice,
+                        ctx->stream));
+  MG_TRY(ensure(&ctx->d_compact, &ctx->compact_cap, total * 3));
+  hipLaunchKernelGGL(k_compact_rows, dim3((uint32_t)ctx->nreg), dim3(kBlock), 0, ctx->stream, ctx->d_rows, reg_cap,
+                     d_prefix, ctx->d_compact);
+  MG_TRY(hipGetLastError());
+  const uint64_t c = std::min(cap, total);
+  if (c) MG_TRY(hipMemcpyAsync(out, ctx->d_compact, c * sizeof(mg_edge), hipMemcpyDeviceToHost, ctx->stream));
   MG_TRY(hipStreamSynchronize(ctx->stream));
-  if (n_copied) *n_copied = done;
+  (void)hipFree(d_prefix);
+  if (n_copied) *n_copied = c;
   return 0;
 }
 

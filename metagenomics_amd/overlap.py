@@ -25,7 +25,8 @@ class MgError(RuntimeError):
 
 class _Timings(C.Structure):
     _fields_ = [("pack_ms", C.c_float), ("index_ms", C.c_float), ("contained_ms", C.c_float),
-                ("overlap_ms", C.c_float), ("total_ms", C.c_float)]
+                ("overlap_ms", C.c_float), ("total_ms", C.c_float), ("scan_ms", C.c_float),
+                ("probe_ms", C.c_float)]
 
 
 class _Counters(C.Structure):
@@ -247,7 +248,11 @@ class OverlapEngine:
     def build_index(self, min_overlap: int, seed_k: int = 0):
         self._check(lib().mg_build_index(self._h, min_overlap, seed_k), "build_index")
 
-    def mark_contained(self) -> np.ndarray:
+    def mark_contained(self, copy: bool = True):
+        """superReadID per ID (index 0 unused); copy=False keeps it on the device."""
+        if not copy:
+            self._check(lib().mg_mark_contained(self._h, None), "mark_contained")
+            return None
         sup = np.zeros(self.n_reads + 1, dtype=np.uint32)
         self._check(lib().mg_mark_contained(self._h, _ptr(sup)), "mark_contained")
         return sup

@@ -1,0 +1,63 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 --pmc CSV output per kernel.
+
+usage: pmc_summary.py OUT.json DIR [DIR ...]
+Each DIR holds one rocprofv3 pass (*_counter_collection.csv).  Writes per-kernel
+mean counter values per dispatch, and for the discovery kernel the HBM traffic
+per launch: FETCH_SIZE and WRITE_SIZE are in KiB (rocprofv3 derived metrics);
+on gfx950 FETCH_SIZE counts 64 B per TCC_EA0_RDREQ, which reads exactly half the
+bytes of 128-B streaming requests (MI355X_MICROARCH.md §HBM), so both the raw
+and the x2-corrected read figures are recorded.
+"""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+
+def short(name):
+    n = name.replace("void ", "").replace("(anonymous namespace)::", "")
+    return n.split("(")[0].strip()
+
+
+def main():
+    out = sys.argv[1]
+    acc = defaultdict(lambda: defaultdict(list))
+    for d in sys.argv[2:]:
+        for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+            with open(f) as fh:
+                for row in csv.DictReader(fh):
+                    k = short(row.get("Kernel_Name", row.get("Kernel-Name", "?")))
+                    cname = row.get("Counter_Name", row.get("Counter-Name"))
+                    val = float(row.get("Counter_Value", row.get("Counter-Value", 0)))
+                    disp = row.get("Dispatch_Id", row.get("Dispatch-Id"))
+                    acc[k][cname].append((disp, val))
+    res = {}
+    for k, cs in acc.items():
+        res[k] = {}
+        for c, vals in cs.items():
+            per = defaultdict(float)
+            for disp, v in vals:
+                per[disp] += v  # sum over dimensions (XCD/SE instances) per dispatch
+            res[k][c] = sum(per.values()) / max(1, len(per))
+    summary = {"kernels": res}
+    disc = [k for k in res if k.startswith("k_discover") and k.endswith("false>")]
+    if disc:
+        k = disc[0]
+        fetch = res[k].get("FETCH_SIZE")
+        write = res[k].get("WRITE_SIZE")
+        if fetch is not None and write is not None:
+            summary["kernel"] = k
+            summary["fetch_bytes_raw"] = fetch * 1024
+            summary["write_bytes"] = write * 1024
+            summary["traffic_bytes_per_launch"] = (2 * fetch + write) * 1024
+            summary["note"] = "traffic = (2 x FETCH_SIZE + WRITE_SIZE) KiB -> bytes; FETCH_SIZE x2 per the gfx950 correction"
+    with open(out, "w") as f:
+        json.dump(summary, f, indent=1, sort_keys=True)
+    print(json.dumps(summary, indent=1, sort_keys=True)[:4000])
+
+
+if __name__ == "__main__":
+    main()
