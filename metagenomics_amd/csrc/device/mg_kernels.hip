@@ -2,26 +2,29 @@
 //
 // Reference path replaced (paths relative to /root/reference/MetaGenomics):
 //   Read::setRead / reverseComplement          Read.cpp:75-82,115-127   -> k_pack_ascii, rc_word
-//   HashTable::insertDataset/hashRead/insert   HashTable.cpp:50-195     -> k_index_keys (count/fill) + scan
-//   HashTable::getListOfReads                  HashTable.cpp:202-221    -> run lookup inside k_discover, k_lookup_key
-//   OverlapGraph::markContainedReads           OverlapGraph.cpp:225-340 -> k_discover<CONTAIN=true> + k_super_finalize
-//   OverlapGraph::insertAllEdgesOfRead         OverlapGraph.cpp:529-565 -> k_discover<CONTAIN=false>
-//   OverlapGraph::checkOverlap / insertEdge    OverlapGraph.cpp:354-419 -> verify + emit inside k_discover
+//   HashTable::insertDataset/hashRead/insert   HashTable.cpp:50-195     -> k_index_build
+//   HashTable::getListOfReads                  HashTable.cpp:202-221    -> cell probe inside k_probe, k_lookup_key
+//   OverlapGraph::markContainedReads           OverlapGraph.cpp:225-340 -> k_scan + k_probe<CONTAIN=true> + k_super_finalize
+//   OverlapGraph::insertAllEdgesOfRead         OverlapGraph.cpp:529-565 -> k_scan + k_probe<CONTAIN=false>
+//   OverlapGraph::checkOverlap / insertEdge    OverlapGraph.cpp:354-419 -> verify + emit inside k_probe
 //
 // Design:
-//  * reads: AoS 2-bit words (A0 C1 G2 T3, MSB-first), MAXW words per read; the
-//    reverse strand is never stored, it is derived in registers (rc_word).
+//  * reads: AoS 2-bit words (A0 C1 G2 T3, MSB-first) in power-of-two slots
+//    (150 bp -> one aligned 64-B sector); the reverse strand is never stored,
+//    it is derived in registers (rc_word).
 //  * index: every key (the h = l-1 prefix/suffix of both strands, 4 per read)
-//    is filed under its m-mer minimizer (m = seed k).  A read's window j
-//    matches key K exactly only if both share the minimizer at the same
-//    relative offset q, so each exact-key hit of the reference is found once,
-//    from the run of windows that share that minimizer; every candidate is
-//    then verified over the full overlap, so results are exact.
-//  * discovery: one lane per source read; the read's words live in LDS; each
-//    loop iteration every lane finds its next candidate (run -> bucket ->
-//    entry filter) and verifies it against the partner's words; rows are
-//    compacted per wavefront with ballot/popcount into an LDS buffer and
-//    flushed with one atomic per >=128 rows.
+//    is filed under its m-mer minimizer (m = seed k) in a cell table (8 entries
+//    per 64-B cell, CAS insert, cell-granular linear probing).  A read's
+//    window j matches key K exactly only if both share the minimizer at the
+//    same relative offset q, so each exact-key hit of the reference is found
+//    once, from the run of windows that share that minimizer; every candidate
+//    is then verified over the full overlap, so results are exact.
+//  * discovery = k_scan (one lane per source read: rolling m-mers, van Herk
+//    sliding minimum, one 16-B record per minimizer run) + k_probe (one run
+//    per lane: cell load, fingerprint/offset filter, wavefront prefix-sum
+//    compaction into an LDS candidate list, one candidate per lane verified
+//    against the partner's slot, ballot-compacted rows into a per-wavefront
+//    HBM region).
 //  * only half of the symmetric discoveries are verified: o = 1 hits are the
 //    twins of the partner's o = 0 hits, o = 2/3 hits are kept only when
 //    source <= partner; every verified discovery emits its row and its twin
@@ -42,7 +45,7 @@ constexpr int kWave = 64;
 constexpr int kBlock = 256;
 constexpr int kWavesPerBlock = kBlock / kWave;
 constexpr int kSegs = 64;                   // diagnostic counter shards
-constexpr uint32_t kFpBits = 20;
+constexpr uint32_t kFpBits = 19;
 
 // ---------------------------------------------------------------- helpers ---
 // Invertible 64-bit mixer: x -> minimizer order and bucket.  Bijective, so
@@ -89,6 +92,12 @@ __device__ __forceinline__ uint64_t ext_fwd(const uint64_t* f, int pos) {
   return funnel(f[w * S], f[(w + 1) * S], s);
 }
 
+// Device slot of a read: a power-of-two number of words (W = 5 -> 8 words, one
+// aligned 64-B sector), so a partner fetch never straddles two sectors.
+__host__ __device__ constexpr int slot_words(int w) {
+  return w <= 1 ? 1 : w <= 2 ? 2 : w <= 4 ? 4 : w <= 8 ? 8 : w <= 16 ? 16 : 32;
+}
+
 __device__ __forceinline__ uint64_t lanemask_lt() {
   const uint32_t lane = __lane_id();
   return lane ? (~0ULL >> (64 - lane)) : 0ULL;
@@ -99,7 +108,7 @@ __device__ __forceinline__ uint64_t lanemask_lt() {
 // code = ((c >> 1) ^ (c >> 2)) & 3 maps A,C,G,T (0x41,0x43,0x47,0x54) to 0..3.
 __global__ __launch_bounds__(kBlock) void k_pack_ascii(const char* __restrict__ ascii,
                                                       const uint64_t* __restrict__ off, uint64_t n,
-                                                      uint32_t maxw, uint64_t* __restrict__ words,
+                                                      uint32_t maxw, uint32_t stride, uint64_t* __restrict__ words,
                                                       uint16_t* __restrict__ len) {
   const uint64_t idx = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
   if (idx >= n * maxw) return;
@@ -120,7 +129,7 @@ __global__ __launch_bounds__(kBlock) void k_pack_ascii(const char* __restrict__ 
     }
     wd = (wd << 2) | code;
   }
-  words[r * maxw + k] = wd;
+  words[r * stride + k] = wd;
 }
 
 // ------------------------------------------------------------ index build ---
@@ -130,6 +139,9 @@ __global__ __launch_bounds__(kBlock) void k_pack_ascii(const char* __restrict__ 
 // room (cell-granular linear probing), so a lookup reads the home cell's count
 // and line together and follows the chain only while count > kCell.
 constexpr int kCell = 8;
+constexpr uint64_t kEmpty = ~0ULL;       // free slot (a read index is never 0xFFFFFFFF)
+constexpr uint64_t kChain = 1ULL << 63;  // on a cell's last slot: the chain continues in the next cell
+constexpr uint32_t kFpMask = (1u << kFpBits) - 1;
 
 struct IndexParams {
   const uint64_t* words;
@@ -138,8 +150,7 @@ struct IndexParams {
   int h, m, w;
   uint32_t nb_log2;
   uint32_t rank, nranks;
-  uint32_t* cnt;     // [NC] entries claimed per cell (> kCell: the chain continues in the next cell)
-  uint64_t* cells;   // [NC * kCell] entries: lo32 = read index, hi32 = fp20 | q10 | o2
+  uint64_t* cells;   // [NC * kCell] entries: lo32 = read index, hi32 = chain1 | fp19 | q10 | o2
 };
 
 __device__ __forceinline__ bool owned(uint64_t bkt, uint32_t nb_log2, uint32_t rank, uint32_t nranks) {
@@ -177,7 +188,7 @@ __global__ __launch_bounds__(kBlock) void k_index_build(IndexParams p) {
   const uint64_t r = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
   if (r >= p.n) return;
   uint64_t* f = smem + threadIdx.x;  // word k at f[k * kBlock]
-  const uint64_t* g = p.words + r * MAXW;
+  const uint64_t* g = p.words + r * slot_words(MAXW);
 #pragma unroll
   for (int k = 0; k < MAXW; ++k) f[k * kBlock] = g[k];
   f[MAXW * kBlock] = 0;
@@ -189,14 +200,17 @@ __global__ __launch_bounds__(kBlock) void k_index_build(IndexParams p) {
     const uint64_t v = key_minimizer<kBlock>(f, n, o, p.h, p.m, p.w, &q);
     uint64_t b = v & mask;
     if (!owned(b, p.nb_log2, p.rank, p.nranks)) continue;
-    const uint32_t fp = (uint32_t)(v >> p.nb_log2) & ((1u << kFpBits) - 1);
+    const uint32_t fp = (uint32_t)(v >> p.nb_log2) & kFpMask;
     const uint64_t entry = ((uint64_t)((fp << 12) | ((uint32_t)q << 2) | (uint32_t)o) << 32) | (uint32_t)r;
     for (uint64_t probe = 0; probe <= mask; ++probe) {  // capacity >= 2x entries: ends in a few steps
-      const uint32_t slot = atomicAdd(&p.cnt[b], 1u);
-      if (slot < (uint32_t)kCell) {
-        p.cells[b * kCell + slot] = entry;
-        break;
-      }
+      unsigned long long* cell = reinterpret_cast<unsigned long long*>(p.cells + b * kCell);
+      bool done = false;
+      // slots only ever go from empty to filled: a stale "empty" read just
+      // makes the CAS fail and the walk move on
+      for (int s = 0; s < kCell && !done; ++s)
+        if (cell[s] == kEmpty) done = atomicCAS(&cell[s], kEmpty, (unsigned long long)entry) == kEmpty;
+      if (done) break;
+      atomicOr(&cell[kCell - 1], (unsigned long long)kChain);  // slot 7 is filled: the flag lands on an entry
       b = (b + 1) & mask;
     }
   }
@@ -215,7 +229,8 @@ struct ScanParams {
   const uint32_t* super;          // source reads with superReadID != 0 get no windows (:548)
   uint64_t a_lo, a_hi;
   int h, m, w;
-  uint64_t* runs;                 // one region of run_cap records per wavefront
+  uint32_t nb_log2, rank, nranks;
+  ulonglong2* runs;               // one region of run_cap records per wavefront
   unsigned long long* run_cnt;    // [waves] records produced (may exceed run_cap)
   uint64_t run_cap;
 };
@@ -237,8 +252,9 @@ __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, int lane, uint32_
   return x - v;
 }
 
-// Run record: read index (32 bits) | p << 32 | jlo << 42 | jhi << 52.
-__device__ __forceinline__ uint64_t run_record(uint64_t a, int p, int jlo, int jhi) {
+// Run record (16 B): x = mix64 of the minimizer m-mer (bucket | fingerprint),
+// y = read index (32 bits) | p << 32 | jlo << 42 | jhi << 52.
+__device__ __forceinline__ uint64_t run_meta(uint64_t a, int p, int jlo, int jhi) {
   return (a & 0xFFFFFFFFull) | ((uint64_t)p << 32) | ((uint64_t)jlo << 42) | ((uint64_t)jhi << 52);
 }
 
@@ -263,14 +279,22 @@ __global__ __launch_bounds__(kBlock) void k_scan(ScanParams p) {
   const uint64_t ngroups = (p.a_hi - p.a_lo + kWave - 1) / kWave;
   const uint64_t gw = (uint64_t)blockIdx.x * kWavesPerBlock + wv;
   const uint64_t nw = (uint64_t)gridDim.x * kWavesPerBlock;
-  uint64_t* const region = p.runs + gw * p.run_cap;
+  ulonglong2* const region = p.runs + gw * p.run_cap;
+  const uint64_t nbmask = (1ULL << p.nb_log2) - 1;
   uint64_t cursor = 0;
 
-  auto put = [&](bool flag, uint64_t rec) {
+  // close the run of minimizer position pos over windows [jlo, jhi]; runs whose
+  // bucket another rank owns are dropped here
+  auto put = [&](bool flag, const uint64_t* g, uint64_t a, int pos, int jlo, int jhi) {
+    uint64_t v = 0;
+    if (flag) {
+      v = mix64(funnel(g[pos >> 5], g[(pos >> 5) + 1], (pos & 31) << 1) >> msh);
+      flag = owned(v & nbmask, p.nb_log2, p.rank, p.nranks);
+    }
     const uint64_t bal = __ballot(flag);
     if (flag) {
       const uint64_t at = cursor + (uint64_t)__popcll(bal & lanemask_lt());
-      if (at < p.run_cap) region[at] = rec;
+      if (at < p.run_cap) region[at] = make_ulonglong2(v, run_meta(a, pos, jlo, jhi));
     }
     cursor += (uint64_t)__popcll(bal);
   };
@@ -278,7 +302,7 @@ __global__ __launch_bounds__(kBlock) void k_scan(ScanParams p) {
   for (uint64_t grp = gw; grp < ngroups; grp += nw) {
     const uint64_t a = p.a_lo + grp * kWave + lane;
     int n = 0;
-    const uint64_t* g = p.words + a * MAXW;
+    const uint64_t* g = p.words + a * slot_words(MAXW);
     if (a < p.a_hi) {
       n = (int)p.len[a];
       if (n && p.super && p.super[a]) n = 0;
@@ -298,7 +322,7 @@ __global__ __launch_bounds__(kBlock) void k_scan(ScanParams p) {
     int u = 0;  // offset of t in its block of w positions
     for (int t = 1; t <= tmax; ++t) {
       bool emit = false, fin = false;
-      uint64_t rec = 0;
+      int e_pos = 0, e_jlo = 0, e_jhi = 0;
       if (t <= tend) {
         const uint32_t key = order_key(mm) | (uint32_t)t;
         pmin = (u == 0 || key < pmin) ? key : pmin;
@@ -312,7 +336,9 @@ __global__ __launch_bounds__(kBlock) void k_scan(ScanParams p) {
           const int pos = (int)(mn & 1023u);
           if (j > 1 && pos != last_pos) {
             emit = true;
-            rec = run_record(a, last_pos, jlo, j - 1);
+            e_pos = last_pos;
+            e_jlo = jlo;
+            e_jhi = j - 1;
             jlo = j;
           }
           last_pos = pos;
@@ -334,8 +360,8 @@ __global__ __launch_bounds__(kBlock) void k_scan(ScanParams p) {
       } else {
         ++u;
       }
-      put(emit, rec);
-      put(fin, run_record(a, last_pos, jlo, J));
+      put(emit, g, a, e_pos, e_jlo, e_jhi);
+      put(fin, g, a, last_pos, jlo, J);
     }
   }
   if (lane == 0) p.run_cnt[gw] = cursor;
@@ -347,13 +373,13 @@ struct ProbeParams {
   int h, m;
   uint32_t nb_log2;
   uint32_t rank, nranks;
-  const uint32_t* cnt;
   const uint64_t* cells;
   const uint32_t* super;          // superReadID per read index (nullptr: none contained)
   unsigned long long* superkey;   // CONTAIN: max over containers of (len << 32 | ~index)
-  const uint64_t* runs;
+  const ulonglong2* runs;
   const unsigned long long* run_cnt;
   uint64_t run_cap;
+  uint32_t run_regions_per_wave;  // probe wavefront r consumes scan regions r + i * (probe wavefronts)
   uint32_t* rows;                 // 3 dwords per row (mg_edge); one region per wavefront
   unsigned long long* reg_cnt;    // [waves] rows produced by each wavefront (may exceed reg_cap)
   uint64_t reg_cap;
@@ -389,42 +415,33 @@ __global__ __launch_bounds__(kBlock) void k_probe(ProbeParams p) {
   uint32_t* s_cb = reinterpret_cast<uint32_t*>(base + PL::o_cb);
   uint32_t* s_ci = reinterpret_cast<uint32_t*>(base + PL::o_ci);
   uint32_t* s_ca = reinterpret_cast<uint32_t*>(base + PL::o_ca);
-  const int h = p.h, m = p.m;
-  const int msh = 64 - 2 * m;
+  const int h = p.h;
   const uint64_t nbmask = (1ULL << p.nb_log2) - 1;
   const uint64_t gw = (uint64_t)blockIdx.x * kWavesPerBlock + wv;
   const uint32_t seg = (uint32_t)(gw & (kSegs - 1));
-  const uint64_t* const runs = p.runs + gw * p.run_cap;
-  const uint64_t nruns = p.run_cnt[gw] < p.run_cap ? p.run_cnt[gw] : p.run_cap;
+  const uint64_t nwp = (uint64_t)gridDim.x * kWavesPerBlock;
   uint32_t* const region = p.rows + gw * p.reg_cap * 3;
   uint64_t cursor = 0;
   uint32_t st_runs = 0, st_ent = 0, st_ver = 0, st_rows = 0;
 
   // verify the first nc (<= 64) candidates of the list, one per lane
   auto verify = [&](uint32_t nc) {
-    const uint32_t ci = (uint32_t)lane;
+    const bool have = (uint32_t)lane < nc;
     int nrec = 0;
     uint32_t r0 = 0, r1 = 0, r2 = 0, t0 = 0, t1 = 0, t2 = 0;
-    int n1 = 0;
-    uint32_t bid = 0, info = 0, sa = 0;
-    if (ci < nc) {
-      bid = s_cb[ci];
-      info = s_ci[ci];
-      sa = s_ca[ci];
-      const uint64_t* g = p.words + (uint64_t)sa * MAXW;
-#pragma unroll
-      for (int k = 0; k < MAXW; ++k) s_a[k * kWave + lane] = g[k];
-      s_a[MAXW * kWave + lane] = 0;
+    int n1 = 0, n2 = 0, o = 0, j = 0;
+    uint32_t bid = 0, sa = 0;
+    bool cond = false, rcA = false;
+    int x0 = 0, y0 = 0, L = 0;
+    uint64_t y[MAXW + 1];
+    if (have) {
+      bid = s_cb[lane];
+      const uint32_t info = s_ci[lane];
+      sa = s_ca[lane];
+      o = (int)(info >> 30);
+      j = (int)(info & 1023u);
       n1 = (int)p.len[sa];
-    }
-    wave_sync();
-    if (ci < nc) {
-      const int o = (int)(info >> 30), j = (int)(info & 1023u);
-      const uint64_t* f1 = s_a + lane;
-      const int n2 = p.uniform_len ? n1 : (int)p.len[bid];
-      bool cond;
-      int x0, y0, L;
-      bool rcA;
+      n2 = p.uniform_len ? n1 : (int)p.len[bid];
       if (!CONTAIN) {
         if (o == 0) {        // F1[j, n1) == F2[0, L)
           L = n1 - j; cond = L < n2; x0 = j; y0 = 0; rcA = false;
@@ -433,7 +450,6 @@ __global__ __launch_bounds__(kBlock) void k_probe(ProbeParams p) {
         } else {             // F1[0, L) == R2[n2-L, n2)  <=>  R1[n1-L, n1) == F2[0, L)
           L = j + h; cond = j <= n2 - h; x0 = n1 - L; y0 = 0; rcA = true;
         }
-        if (cond && p.super && p.super[bid]) cond = false;  // :548 read2 contained
       } else {
         int s;
         cond = n1 > n2;
@@ -449,39 +465,51 @@ __global__ __launch_bounds__(kBlock) void k_probe(ProbeParams p) {
         rcA = o >= 2;
         x0 = rcA ? n1 - s - n2 : s;
       }
-      if (cond) {
-        ++st_ver;
-        const uint64_t* bg = p.words + (uint64_t)bid * MAXW + (y0 >> 5);
-        const int ys = (y0 & 31) << 1;
-        uint64_t y[MAXW + 1];
+    }
+    // partner words first (the long-latency random loads), then stage the source
+    if (cond) {
+      // only the words [y0, y0 + L) spans: all inside the partner's own slot
+      const uint64_t* bg = p.words + (uint64_t)bid * slot_words(MAXW) + (y0 >> 5);
+      const int need = (((y0 & 31) + L - 1) >> 5) + 1;
 #pragma unroll
-        for (int k = 0; k <= MAXW; ++k) y[k] = bg[k];
-        uint64_t diff = 0;
+      for (int k = 0; k <= MAXW; ++k) y[k] = k < need ? bg[k] : 0;
+    }
+    if (have) {
+      const uint64_t* g = p.words + (uint64_t)sa * slot_words(MAXW);
 #pragma unroll
-        for (int cc = 0; cc < MAXW; ++cc) {
-          if (cc * 32 < L) {
-            const uint64_t av = rcA ? rc_word(ext_fwd<kWave>(f1, n1 - x0 - 32 * cc - 32))
-                                    : ext_fwd<kWave>(f1, x0 + 32 * cc);
-            const uint64_t bv = funnel(y[cc], y[cc + 1], ys);
-            const int rem = L - 32 * cc;
-            const uint64_t msk = rem >= 32 ? ~0ULL : ~(~0ULL >> (2 * rem));
-            diff |= (av ^ bv) & msk;
-          }
+      for (int k = 0; k < MAXW; ++k) s_a[k * kWave + lane] = g[k];
+      s_a[MAXW * kWave + lane] = 0;
+    }
+    wave_sync();
+    if (cond) {
+      ++st_ver;
+      const uint64_t* f1 = s_a + lane;
+      const int ys = (y0 & 31) << 1;
+      uint64_t diff = 0;
+#pragma unroll
+      for (int cc = 0; cc < MAXW; ++cc) {
+        if (cc * 32 < L) {
+          const uint64_t av = rcA ? rc_word(ext_fwd<kWave>(f1, n1 - x0 - 32 * cc - 32))
+                                  : ext_fwd<kWave>(f1, x0 + 32 * cc);
+          const uint64_t bv = funnel(y[cc], y[cc + 1], ys);
+          const int rem = L - 32 * cc;
+          const uint64_t msk = rem >= 32 ? ~0ULL : ~(~0ULL >> (2 * rem));
+          diff |= (av ^ bv) & msk;
         }
-        if (diff == 0) {
-          if (CONTAIN) {
-            atomicMax(&p.superkey[bid], ((unsigned long long)n1 << 32) | (0xFFFFFFFFu - sa));
-          } else {
-            // orientation/offset switch (:550-557) and the twin (:409-412, :841-855)
-            const uint32_t orient = (o == 0) ? 3u : (o == 2 ? 2u : 1u);
-            const uint32_t off = (o == 3) ? (uint32_t)(n1 - h - j) : (uint32_t)j;
-            const uint32_t torient = (orient == 3u) ? 0u : orient;
-            const uint32_t toff = (uint16_t)(n2 + off - n1);
-            r0 = sa + 1; r1 = bid + 1; r2 = (orient << 16) | off;
-            t0 = bid + 1; t1 = sa + 1; t2 = (torient << 16) | toff;
-            nrec = (bid == sa && o == 0) ? 4 : 2;  // self o=0 hit also stands for its o=1 twin
-            st_rows += nrec;
-          }
+      }
+      if (diff == 0) {
+        if (CONTAIN) {
+          atomicMax(&p.superkey[bid], ((unsigned long long)n1 << 32) | (0xFFFFFFFFu - sa));
+        } else if (!(p.super && p.super[bid])) {  // :548 read2 contained
+          // orientation/offset switch (:550-557) and the twin (:409-412, :841-855)
+          const uint32_t orient = (o == 0) ? 3u : (o == 2 ? 2u : 1u);
+          const uint32_t off = (o == 3) ? (uint32_t)(n1 - h - j) : (uint32_t)j;
+          const uint32_t torient = (orient == 3u) ? 0u : orient;
+          const uint32_t toff = (uint16_t)(n2 + off - n1);
+          r0 = sa + 1; r1 = bid + 1; r2 = (orient << 16) | off;
+          t0 = bid + 1; t1 = sa + 1; t2 = (torient << 16) | toff;
+          nrec = (bid == sa && o == 0) ? 4 : 2;  // self o=0 hit also stands for its o=1 twin
+          st_rows += nrec;
         }
       }
     }
@@ -506,29 +534,24 @@ __global__ __launch_bounds__(kBlock) void k_probe(ProbeParams p) {
   };
 
   uint32_t ncand = 0;
+  for (uint32_t rg = 0; rg < p.run_regions_per_wave; ++rg) {
+  const uint64_t reg = gw + (uint64_t)rg * nwp;
+  const ulonglong2* const runs = p.runs + reg * p.run_cap;
+  const uint64_t nruns = p.run_cnt[reg] < p.run_cap ? p.run_cnt[reg] : p.run_cap;
   for (uint64_t r0i = 0; r0i < nruns && p.phase_limit > 4; r0i += kWave) {
     const uint64_t k = r0i + (uint64_t)lane;
     bool act = k < nruns;
-    const uint64_t rec = act ? runs[k] : 0;
-    const uint32_t ra = (uint32_t)rec;
-    const int rp = (int)((rec >> 32) & 1023u);
-    const int rjlo = (int)((rec >> 42) & 1023u), rjhi = (int)((rec >> 52) & 1023u);
-    uint32_t fp = 0;
-    uint64_t b = 0;
-    if (act) {
-      const uint64_t* g = p.words + (uint64_t)ra * MAXW;
-      const int wi = rp >> 5, sh = (rp & 31) << 1;
-      const uint64_t v = mix64(funnel(g[wi], g[wi + 1], sh) >> msh);  // bucket + fingerprint
-      b = v & nbmask;
-      fp = (uint32_t)(v >> p.nb_log2) & ((1u << kFpBits) - 1);
-      act = owned(b, p.nb_log2, p.rank, p.nranks);
-      if (act) ++st_runs;
-    }
+    const ulonglong2 rec = act ? runs[k] : make_ulonglong2(0, 0);
+    const uint64_t meta = rec.y;
+    const uint32_t ra = (uint32_t)meta;
+    const int rp = (int)((meta >> 32) & 1023u);
+    const int rjlo = (int)((meta >> 42) & 1023u), rjhi = (int)((meta >> 52) & 1023u);
+    uint64_t b = rec.x & nbmask;  // the scan kept owned buckets only
+    const uint32_t fp = (uint32_t)(rec.x >> p.nb_log2) & kFpMask;
+    if (act) ++st_runs;
     while (__ballot(act)) {
-      uint32_t c = 0;
       uint64_t e[kCell];
       if (act) {
-        c = p.cnt[b];
         const ulonglong2* cp = reinterpret_cast<const ulonglong2*>(p.cells + b * kCell);
 #pragma unroll
         for (int s = 0; s < kCell / 2; ++s) {
@@ -538,10 +561,12 @@ __global__ __launch_bounds__(kBlock) void k_probe(ProbeParams p) {
         }
       } else {
 #pragma unroll
-        for (int s = 0; s < kCell; ++s) e[s] = 0;
+        for (int s = 0; s < kCell; ++s) e[s] = kEmpty;
       }
-      const uint32_t nv = act ? (c < (uint32_t)kCell ? c : (uint32_t)kCell) : 0u;
-      st_ent += nv;
+      if (p.stats) {
+#pragma unroll
+        for (int s = 0; s < kCell; ++s) st_ent += e[s] != kEmpty ? 1u : 0u;
+      }
       uint32_t mask = 0;
       if (p.phase_limit > 5) {
 #pragma unroll
@@ -549,7 +574,7 @@ __global__ __launch_bounds__(kBlock) void k_probe(ProbeParams p) {
           const uint32_t hi = (uint32_t)(e[s] >> 32);
           const int j = rp - (int)((hi >> 2) & 1023u);
           const int oo = (int)(hi & 3u);
-          bool keep = (uint32_t)s < nv && (hi >> 12) == fp && j >= rjlo && j <= rjhi;
+          bool keep = e[s] != kEmpty && ((hi >> 12) & kFpMask) == fp && j >= rjlo && j <= rjhi;
           // halving: o=1 hits are twins of the partner's o=0
           // hits; o=2/3 hits are kept only for partner >= source
           keep = keep && (CONTAIN || oo == 0 || (oo >= 2 && (uint32_t)e[s] >= ra));
@@ -596,9 +621,10 @@ __global__ __launch_bounds__(kBlock) void k_probe(ProbeParams p) {
           wave_sync();
         }
       }
-      act = act && c > (uint32_t)kCell;
+      act = act && (e[kCell - 1] & kChain) && e[kCell - 1] != kEmpty;
       b = (b + 1) & nbmask;
     }
+  }
   }
   if (ncand && p.phase_limit > 6) verify(ncand);
   if (!CONTAIN && lane == 0) p.reg_cnt[gw] = cursor;
@@ -655,18 +681,17 @@ __global__ __launch_bounds__(kBlock) void k_lookup_key(IndexParams p, const uint
   }
   __syncthreads();
   const uint64_t mask = (1ULL << p.nb_log2) - 1;
-  const uint32_t fp = (uint32_t)(qv >> p.nb_log2) & ((1u << kFpBits) - 1);
+  const uint32_t fp = (uint32_t)(qv >> p.nb_log2) & kFpMask;
   uint64_t b = qv & mask;
   for (uint64_t probe = 0; probe <= mask; ++probe) {
-    const uint32_t c = p.cnt[b];
-    const uint32_t nv = c < (uint32_t)kCell ? c : (uint32_t)kCell;
-    if (threadIdx.x < nv) {
+    const uint64_t last = p.cells[b * kCell + kCell - 1];
+    if (threadIdx.x < (unsigned)kCell) {
       const uint64_t en = p.cells[b * kCell + threadIdx.x];
       const uint32_t hi = (uint32_t)(en >> 32);
-      if ((hi >> 12) == fp && (int)((hi >> 2) & 1023u) == qq) {
+      if (en != kEmpty && ((hi >> 12) & kFpMask) == fp && (int)((hi >> 2) & 1023u) == qq) {
         const int o = (int)(hi & 3u);
         const uint32_t r = (uint32_t)en;
-        const uint64_t* g = p.words + (uint64_t)r * MAXW;
+        const uint64_t* g = p.words + (uint64_t)r * slot_words(MAXW);
         const int n = p.len[r];
         // key string of (r, o) vs the query, 32 bases at a time
         uint64_t diff = 0;
@@ -692,7 +717,7 @@ __global__ __launch_bounds__(kBlock) void k_lookup_key(IndexParams p, const uint
         }
       }
     }
-    if (c <= (uint32_t)kCell) break;
+    if (last == kEmpty || !(last & kChain)) break;
     b = (b + 1) & mask;
   }
 }
@@ -707,6 +732,7 @@ struct mg_ctx {
   // reads
   uint64_t n = 0;
   uint32_t maxw = 0;
+  uint32_t stride = 0;  // words per device slot (slot_words(maxw))
   uint32_t minlen = 0, maxlen = 0;
   uint64_t* d_words = nullptr;
   uint16_t* d_len = nullptr;
@@ -715,9 +741,8 @@ struct mg_ctx {
   uint32_t l = 0, h = 0, m = 0, w = 0;
   uint32_t nb_log2 = 0, nb_log2_opt = 0;
   bool index_ready = false;
-  uint32_t* d_cnt = nullptr;    // per-cell fill counts
   uint64_t* d_cells = nullptr;  // cells of kCell entries
-  size_t cnt_cap = 0, cells_cap = 0;
+  size_t cells_cap = 0;
   // containment
   unsigned long long* d_superkey = nullptr;
   uint32_t* d_super = nullptr;
@@ -740,8 +765,9 @@ struct mg_ctx {
   uint32_t max_blocks = 8192;  // cap on the persistent discovery grid (blocks of 4 wavefronts)
   int phase_limit = 99;        // diagnostics (option "phase_limit")
   int n_cu = 256;              // compute units of the device
-  uint64_t nreg = 0;           // row regions of the last discovery launch (one per wavefront)
-  uint64_t* d_runs = nullptr;  // run records, one region per wavefront
+  uint64_t nreg = 0;           // row regions of the last discovery launch (one per probe wavefront)
+  uint64_t nrun_reg = 0;       // run regions (one per scan wavefront)
+  ulonglong2* d_runs = nullptr;  // run records, one region per wavefront
   size_t runs_cap = 0;
   uint64_t run_cap = 0, run_cap_need = 0;
   unsigned long long* d_run_cnt = nullptr;
@@ -828,7 +854,6 @@ IndexParams index_params(mg_ctx* ctx) {
   p.nb_log2 = ctx->nb_log2;
   p.rank = ctx->rank;
   p.nranks = ctx->nranks;
-  p.cnt = ctx->d_cnt;
   p.cells = ctx->d_cells;
   return p;
 }
@@ -865,16 +890,23 @@ struct LaunchDiscover {
     const uint64_t a_lo = contain ? 0 : ctx->read_lo;
     const uint64_t a_hi = contain ? ctx->n : (ctx->read_hi ? std::min<uint64_t>(ctx->read_hi, ctx->n) : ctx->n);
     ctx->nreg = 0;
+    ctx->nrun_reg = 0;
     if (a_hi <= a_lo) return 0;
     const uint64_t ngroups = (a_hi - a_lo + kWave - 1) / kWave;
     const uint64_t want = (ngroups + kWavesPerBlock - 1) / kWavesPerBlock;
     const size_t lds_scan = (size_t)kWavesPerBlock * ctx->w * kWave * sizeof(uint32_t);
     const size_t lds_probe = (size_t)kWavesPerBlock * ProbeLds<W>::bytes;
-    uint32_t grid = resident_blocks(ctx, k_scan<W>, lds_scan, want);
-    grid = std::min(grid, contain ? resident_blocks(ctx, k_probe<W, true>, lds_probe, want)
-                                  : resident_blocks(ctx, k_probe<W, false>, lds_probe, want));
-    const uint64_t nw = (uint64_t)grid * kWavesPerBlock;
-    ctx->nreg = nw;
+    // probe grid = its resident blocks; the scan (fewer registers) runs k
+    // times as many wavefronts and probe wavefront r consumes k scan regions
+    const uint32_t grid = contain ? resident_blocks(ctx, k_probe<W, true>, lds_probe, want)
+                                  : resident_blocks(ctx, k_probe<W, false>, lds_probe, want);
+    const uint32_t scan_res = resident_blocks(ctx, k_scan<W>, lds_scan, ~0ull >> 1);
+    const uint32_t kreg = (uint32_t)std::max<uint64_t>(
+        1, std::min<uint64_t>(scan_res / grid, (want + grid - 1) / grid));
+    const uint32_t sgrid = grid * kreg;
+    const uint64_t nw = (uint64_t)sgrid * kWavesPerBlock;  // scan wavefronts = run regions
+    ctx->nreg = (uint64_t)grid * kWavesPerBlock;           // probe wavefronts = row regions
+    ctx->nrun_reg = nw;
     // run regions: expected runs per read ~ 2 J / (w + 1) + 1 (minimizer density)
     const uint64_t J = ctx->maxlen > ctx->h + 1 ? ctx->maxlen - ctx->h - 1 : 1;
     const uint64_t per_read = std::min<uint64_t>(J, 3 * (2 * J / (ctx->w + 1) + 2));
@@ -883,7 +915,7 @@ struct LaunchDiscover {
     if (run_cap * nw > ctx->runs_cap) {
       if (ctx->d_runs) (void)hipFree(ctx->d_runs);
       ctx->d_runs = nullptr;
-      if (hipMalloc(&ctx->d_runs, run_cap * nw * sizeof(uint64_t)) != hipSuccess) return -1;
+      if (hipMalloc(&ctx->d_runs, run_cap * nw * sizeof(ulonglong2)) != hipSuccess) return -1;
       ctx->runs_cap = run_cap * nw;
     }
     run_cap = ctx->runs_cap / nw;
@@ -903,11 +935,14 @@ struct LaunchDiscover {
     sp.h = (int)ctx->h;
     sp.m = (int)ctx->m;
     sp.w = (int)ctx->w;
+    sp.nb_log2 = ctx->nb_log2;
+    sp.rank = contain ? 0 : ctx->rank;
+    sp.nranks = contain ? 1 : ctx->nranks;
     sp.runs = ctx->d_runs;
     sp.run_cnt = ctx->d_run_cnt;
     sp.run_cap = run_cap;
     (void)hipEventRecord(ctx->ev[6], ctx->stream);
-    hipLaunchKernelGGL((k_scan<W>), dim3(grid), dim3(kBlock), lds_scan, ctx->stream, sp);
+    hipLaunchKernelGGL((k_scan<W>), dim3(sgrid), dim3(kBlock), lds_scan, ctx->stream, sp);
     (void)hipEventRecord(ctx->ev[7], ctx->stream);
     ProbeParams pp{};
     pp.words = ctx->d_words;
@@ -917,16 +952,16 @@ struct LaunchDiscover {
     pp.nb_log2 = ctx->nb_log2;
     pp.rank = ctx->rank;
     pp.nranks = ctx->nranks;
-    pp.cnt = ctx->d_cnt;
     pp.cells = ctx->d_cells;
     pp.super = (!contain && ctx->contained_done && ctx->super_any) ? ctx->d_super : nullptr;
     pp.superkey = ctx->d_superkey;
     pp.runs = ctx->d_runs;
     pp.run_cnt = ctx->d_run_cnt;
     pp.run_cap = run_cap;
+    pp.run_regions_per_wave = kreg;
     pp.rows = ctx->d_rows;
     pp.reg_cnt = ctx->d_seg;
-    pp.reg_cap = contain ? 0 : ctx->rows_cap / nw;
+    pp.reg_cap = contain ? 0 : ctx->rows_cap / ctx->nreg;
     pp.uniform_len = ctx->minlen == ctx->maxlen;
     pp.stats = contain ? nullptr : (ctx->stats ? ctx->d_stats : nullptr);
     pp.phase_limit = contain ? 99 : ctx->phase_limit;
@@ -965,10 +1000,10 @@ int run_discover(mg_ctx* ctx, bool contain) {
       ctx->err = "discovery launch failed";
       return -1;
     }
-    if (ctx->run_cnt_host.size() < ctx->nreg) ctx->run_cnt_host.resize(ctx->nreg);
+    if (ctx->run_cnt_host.size() < ctx->nrun_reg) ctx->run_cnt_host.resize(ctx->nrun_reg);
     if (ctx->seg_host.size() < ctx->nreg) ctx->seg_host.resize(ctx->nreg);
     if (ctx->nreg) {
-      MG_TRY(hipMemcpyAsync(ctx->run_cnt_host.data(), ctx->d_run_cnt, ctx->nreg * sizeof(unsigned long long),
+      MG_TRY(hipMemcpyAsync(ctx->run_cnt_host.data(), ctx->d_run_cnt, ctx->nrun_reg * sizeof(unsigned long long),
                             hipMemcpyDeviceToHost, ctx->stream));
       if (!contain)
         MG_TRY(hipMemcpyAsync(ctx->seg_host.data(), ctx->d_seg, ctx->nreg * sizeof(unsigned long long),
@@ -976,8 +1011,8 @@ int run_discover(mg_ctx* ctx, bool contain) {
     }
     MG_TRY(hipStreamSynchronize(ctx->stream));
     uint64_t run_max = 0, row_max = 0, rows = 0;
+    for (uint64_t r = 0; r < ctx->nrun_reg; ++r) run_max = std::max<uint64_t>(run_max, ctx->run_cnt_host[r]);
     for (uint64_t r = 0; r < ctx->nreg; ++r) {
-      run_max = std::max<uint64_t>(run_max, ctx->run_cnt_host[r]);
       if (!contain) {
         row_max = std::max<uint64_t>(row_max, ctx->seg_host[r]);
         rows += ctx->seg_host[r];
@@ -1044,7 +1079,7 @@ void mg_destroy(mg_ctx* ctx) {
   if (!ctx) return;
   (void)hipSetDevice(ctx->device);
   (void)hipStreamSynchronize(ctx->stream);
-  void* bufs[] = {ctx->d_words, ctx->d_len, ctx->d_cnt, ctx->d_cells,
+  void* bufs[] = {ctx->d_words, ctx->d_len, ctx->d_cells,
                   ctx->d_superkey, ctx->d_super, ctx->d_any, ctx->d_rows, ctx->d_seg, ctx->d_stats,
                   ctx->d_compact, ctx->d_runs, ctx->d_run_cnt};
   for (void* b : bufs)
@@ -1093,15 +1128,16 @@ int mg_upload_reads_packed(mg_ctx* ctx, const uint64_t* words, const uint16_t* l
   if (!maxw) return set_err(ctx, "reads longer than 1024 bp are not supported");
   ctx->n = n_reads;
   ctx->maxw = maxw;
-  const size_t nw = (size_t)(n_reads + 2) * maxw + 2;  // zero pad for partner over-reads
+  ctx->stride = slot_words((int)maxw);
+  const size_t nw = (size_t)(n_reads + 2) * ctx->stride + 2;  // zero pad for over-reads
   MG_TRY(ensure(&ctx->d_words, &ctx->words_cap, nw));
   MG_TRY(ensure(&ctx->d_len, &ctx->len_cap, n_reads + 1));
   MG_TRY(hipMemsetAsync(ctx->d_words, 0, nw * sizeof(uint64_t), ctx->stream));
-  if (maxw == words_per_read) {
-    MG_TRY(hipMemcpyAsync(ctx->d_words, words, n_reads * maxw * sizeof(uint64_t), hipMemcpyHostToDevice,
+  if (n_reads && ctx->stride == words_per_read) {
+    MG_TRY(hipMemcpyAsync(ctx->d_words, words, n_reads * ctx->stride * sizeof(uint64_t), hipMemcpyHostToDevice,
                           ctx->stream));
-  } else {
-    MG_TRY(hipMemcpy2DAsync(ctx->d_words, maxw * sizeof(uint64_t), words, words_per_read * sizeof(uint64_t),
+  } else if (n_reads) {
+    MG_TRY(hipMemcpy2DAsync(ctx->d_words, ctx->stride * sizeof(uint64_t), words, words_per_read * sizeof(uint64_t),
                             words_per_read * sizeof(uint64_t), n_reads, hipMemcpyHostToDevice, ctx->stream));
   }
   if (n_reads)
@@ -1126,12 +1162,13 @@ int mg_upload_reads_ascii(mg_ctx* ctx, const char* concat, const uint64_t* offse
   if (!maxw) return set_err(ctx, "reads longer than 1024 bp are not supported");
   ctx->n = n_reads;
   ctx->maxw = maxw;
+  ctx->stride = slot_words((int)maxw);
   const uint64_t total = n_reads ? offsets[n_reads] : 0;
   char* d_ascii = nullptr;
   uint64_t* d_off = nullptr;
   MG_TRY(hipMalloc(&d_ascii, std::max<uint64_t>(total, 1)));
   MG_TRY(hipMalloc(&d_off, (n_reads + 1) * sizeof(uint64_t)));
-  const size_t nw = (size_t)(n_reads + 2) * maxw + 2;
+  const size_t nw = (size_t)(n_reads + 2) * ctx->stride + 2;
   MG_TRY(ensure(&ctx->d_words, &ctx->words_cap, nw));
   MG_TRY(ensure(&ctx->d_len, &ctx->len_cap, n_reads + 1));
   MG_TRY(hipMemsetAsync(ctx->d_words, 0, nw * sizeof(uint64_t), ctx->stream));
@@ -1141,7 +1178,7 @@ int mg_upload_reads_ascii(mg_ctx* ctx, const char* concat, const uint64_t* offse
   const uint64_t threads = n_reads * maxw;
   if (threads) {
     hipLaunchKernelGGL(k_pack_ascii, dim3((uint32_t)((threads + kBlock - 1) / kBlock)), dim3(kBlock), 0,
-                       ctx->stream, d_ascii, d_off, n_reads, maxw, ctx->d_words, ctx->d_len);
+                       ctx->stream, d_ascii, d_off, n_reads, maxw, ctx->stride, ctx->d_words, ctx->d_len);
     MG_TRY(hipGetLastError());
   }
   MG_TRY(hipEventRecord(ctx->ev[1], ctx->stream));
@@ -1157,7 +1194,8 @@ int mg_download_reads_packed(mg_ctx* ctx, uint64_t* words, uint16_t* lens, uint3
   MG_TRY(hipSetDevice(ctx->device));
   if (words_per_read) *words_per_read = ctx->maxw;
   if (words && ctx->n)
-    MG_TRY(hipMemcpy(words, ctx->d_words, ctx->n * ctx->maxw * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    MG_TRY(hipMemcpy2D(words, ctx->maxw * sizeof(uint64_t), ctx->d_words, ctx->stride * sizeof(uint64_t),
+                       ctx->maxw * sizeof(uint64_t), ctx->n, hipMemcpyDeviceToHost));
   if (lens && ctx->n) MG_TRY(hipMemcpy(lens, ctx->d_len, ctx->n * sizeof(uint16_t), hipMemcpyDeviceToHost));
   return 0;
 }
@@ -1225,10 +1263,9 @@ int mg_build_index(mg_ctx* ctx, uint32_t min_overlap, uint32_t seed_k) {
   while (nbl < 31 && (1ull << nbl) * kCell < 5 * std::max<uint64_t>(ctx->n, 1)) nbl++;
   ctx->nb_log2 = nbl;
   const uint64_t nc = 1ull << nbl;
-  MG_TRY(ensure(&ctx->d_cnt, &ctx->cnt_cap, nc));
   MG_TRY(ensure(&ctx->d_cells, &ctx->cells_cap, nc * kCell));
   MG_TRY(hipEventRecord(ctx->ev[0], ctx->stream));
-  MG_TRY(hipMemsetAsync(ctx->d_cnt, 0, nc * sizeof(uint32_t), ctx->stream));
+  MG_TRY(hipMemsetAsync(ctx->d_cells, 0xFF, nc * kCell * sizeof(uint64_t), ctx->stream));  // kEmpty
   if (dispatch_w<LaunchIndex>(ctx->maxw, ctx)) return set_err(ctx, "index build launch failed");
   MG_TRY(hipEventRecord(ctx->ev[1], ctx->stream));
   MG_TRY(hipEventSynchronize(ctx->ev[1]));
