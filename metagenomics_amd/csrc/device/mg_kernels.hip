@@ -98,9 +98,9 @@ __host__ __device__ constexpr int slot_words(int w) {
   return w <= 1 ? 1 : w <= 2 ? 2 : w <= 4 ? 4 : w <= 8 ? 8 : w <= 16 ? 16 : 32;
 }
 
-__device__ __forceinline__ uint64_t lanemask_lt() {
-  const uint32_t lane = __lane_id();
-  return lane ? (~0ULL >> (64 - lane)) : 0ULL;
+// Number of set bits of a ballot below this lane (v_mbcnt_lo/hi).
+__device__ __forceinline__ uint32_t lane_prefix(uint64_t bal) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
 }
 
 // ------------------------------------------------------------ 2-bit pack ---
@@ -139,6 +139,7 @@ __global__ __launch_bounds__(kBlock) void k_pack_ascii(const char* __restrict__ 
 // room (cell-granular linear probing), so a lookup reads the home cell's count
 // and line together and follows the chain only while count > kCell.
 constexpr int kCell = 8;
+constexpr int kScanBuf = 3 * 64;  // staged run metas per scan wavefront (two puts per step: < 64 + 128)
 constexpr uint64_t kEmpty = ~0ULL;       // free slot (a read index is never 0xFFFFFFFF)
 constexpr uint64_t kChain = 1ULL << 63;  // on a cell's last slot: the chain continues in the next cell
 constexpr uint32_t kFpMask = (1u << kFpBits) - 1;
@@ -180,12 +181,17 @@ __device__ __forceinline__ uint64_t key_minimizer(const uint64_t* f, int n, int 
   return mix64(bmm);
 }
 
-// HashTable::insertDataset (HashTable.cpp:50-80): one thread per read files
-// its 4 keys.
+// HashTable::insertDataset (HashTable.cpp:50-80): one thread per key (read r,
+// key o = hashRead's four strings, HashTable.cpp:88-104) finds the key's
+// minimizer and files the entry: one 64-B cell load, then CAS into the slots
+// that looked empty (slots only ever go from empty to filled, so a stale view
+// just makes a CAS fail); a full cell gets the chain flag and the walk moves on.
 template <int MAXW>
 __global__ __launch_bounds__(kBlock) void k_index_build(IndexParams p) {
   extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
-  const uint64_t r = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  const uint64_t gid = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  const uint64_t r = gid >> 2;
+  const int o = (int)(gid & 3);
   if (r >= p.n) return;
   uint64_t* f = smem + threadIdx.x;  // word k at f[k * kBlock]
   const uint64_t* g = p.words + r * slot_words(MAXW);
@@ -194,25 +200,31 @@ __global__ __launch_bounds__(kBlock) void k_index_build(IndexParams p) {
   f[MAXW * kBlock] = 0;
   const int n = p.len[r];
   const uint64_t mask = (1ULL << p.nb_log2) - 1;
-#pragma unroll 1
-  for (int o = 0; o < 4; ++o) {
-    int q;
-    const uint64_t v = key_minimizer<kBlock>(f, n, o, p.h, p.m, p.w, &q);
-    uint64_t b = v & mask;
-    if (!owned(b, p.nb_log2, p.rank, p.nranks)) continue;
-    const uint32_t fp = (uint32_t)(v >> p.nb_log2) & kFpMask;
-    const uint64_t entry = ((uint64_t)((fp << 12) | ((uint32_t)q << 2) | (uint32_t)o) << 32) | (uint32_t)r;
-    for (uint64_t probe = 0; probe <= mask; ++probe) {  // capacity >= 2x entries: ends in a few steps
-      unsigned long long* cell = reinterpret_cast<unsigned long long*>(p.cells + b * kCell);
-      bool done = false;
-      // slots only ever go from empty to filled: a stale "empty" read just
-      // makes the CAS fail and the walk move on
-      for (int s = 0; s < kCell && !done; ++s)
-        if (cell[s] == kEmpty) done = atomicCAS(&cell[s], kEmpty, (unsigned long long)entry) == kEmpty;
-      if (done) break;
-      atomicOr(&cell[kCell - 1], (unsigned long long)kChain);  // slot 7 is filled: the flag lands on an entry
-      b = (b + 1) & mask;
+  int q;
+  const uint64_t v = key_minimizer<kBlock>(f, n, o, p.h, p.m, p.w, &q);
+  uint64_t b = v & mask;
+  if (!owned(b, p.nb_log2, p.rank, p.nranks)) return;
+  const uint32_t fp = (uint32_t)(v >> p.nb_log2) & kFpMask;
+  const unsigned long long entry =
+      ((unsigned long long)((fp << 12) | ((uint32_t)q << 2) | (uint32_t)o) << 32) | (uint32_t)r;
+  for (uint64_t probe = 0; probe <= mask; ++probe) {  // capacity >= 2x entries: ends in a few steps
+    unsigned long long* cell = reinterpret_cast<unsigned long long*>(p.cells + b * kCell);
+    uint64_t e[kCell];
+    const ulonglong2* cp = reinterpret_cast<const ulonglong2*>(cell);
+#pragma unroll
+    for (int s = 0; s < kCell / 2; ++s) {
+      const ulonglong2 x = cp[s];
+      e[2 * s] = x.x;
+      e[2 * s + 1] = x.y;
     }
+    bool done = false;
+#pragma unroll
+    for (int s = 0; s < kCell; ++s)
+      if (!done && e[s] == kEmpty) done = atomicCAS(&cell[s], kEmpty, entry) == kEmpty;
+    if (done) return;
+    // every slot is filled now: flag the chain (slot 7 holds an entry)
+    if (e[kCell - 1] == kEmpty || !(e[kCell - 1] & kChain)) atomicOr(&cell[kCell - 1], (unsigned long long)kChain);
+    b = (b + 1) & mask;
   }
 }
 
@@ -239,17 +251,6 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, int lane, uint32_t* total) {
-  uint32_t x = v;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t y = __shfl_up(x, d);
-    if (lane >= d) x += y;
-  }
-  *total = __shfl(x, 63);
-  return x - v;
 }
 
 // Run record (16 B): x = mix64 of the minimizer m-mer (bucket | fingerprint),
@@ -279,24 +280,47 @@ __global__ __launch_bounds__(kBlock) void k_scan(ScanParams p) {
   const uint64_t ngroups = (p.a_hi - p.a_lo + kWave - 1) / kWave;
   const uint64_t gw = (uint64_t)blockIdx.x * kWavesPerBlock + wv;
   const uint64_t nw = (uint64_t)gridDim.x * kWavesPerBlock;
+  uint64_t* s_buf = reinterpret_cast<uint64_t*>(smem) + (size_t)kWavesPerBlock * ((w * kWave + 1) / 2) +
+                    (size_t)wv * kScanBuf;
   ulonglong2* const region = p.runs + gw * p.run_cap;
   const uint64_t nbmask = (1ULL << p.nb_log2) - 1;
   uint64_t cursor = 0;
+  uint32_t nbuf = 0;  // run metas staged in s_buf (wavefront-uniform)
 
-  // close the run of minimizer position pos over windows [jlo, jhi]; runs whose
-  // bucket another rank owns are dropped here
-  auto put = [&](bool flag, const uint64_t* g, uint64_t a, int pos, int jlo, int jhi) {
-    uint64_t v = 0;
+  // close the run of minimizer position pos over windows [jlo, jhi]: stage its
+  // meta in LDS (the hashing and the HBM write happen 64 at a time in flush)
+  auto put = [&](bool flag, uint64_t meta) {
+    const uint64_t bal = __ballot(flag);
+    if (flag) s_buf[nbuf + lane_prefix(bal)] = meta;
+    nbuf += (uint32_t)__popcll(bal);
+  };
+  // hash the first k (<= 64) staged runs with every lane busy, drop runs whose
+  // bucket another rank owns, write full-wavefront 16-B records
+  auto flush = [&](uint32_t k) {
+    wave_sync();
+    bool flag = (uint32_t)lane < k;
+    uint64_t v = 0, meta = 0;
     if (flag) {
-      v = mix64(funnel(g[pos >> 5], g[(pos >> 5) + 1], (pos & 31) << 1) >> msh);
+      meta = s_buf[lane];
+      const uint64_t* g2 = p.words + (meta & 0xFFFFFFFFull) * slot_words(MAXW);
+      const int pos = (int)((meta >> 32) & 1023u);
+      v = mix64(funnel(g2[pos >> 5], g2[(pos >> 5) + 1], (pos & 31) << 1) >> msh);
       flag = owned(v & nbmask, p.nb_log2, p.rank, p.nranks);
     }
     const uint64_t bal = __ballot(flag);
     if (flag) {
-      const uint64_t at = cursor + (uint64_t)__popcll(bal & lanemask_lt());
-      if (at < p.run_cap) region[at] = make_ulonglong2(v, run_meta(a, pos, jlo, jhi));
+      const uint64_t at = cursor + lane_prefix(bal);
+      if (at < p.run_cap) region[at] = make_ulonglong2(v, meta);
     }
     cursor += (uint64_t)__popcll(bal);
+    const uint32_t rest = nbuf - k;  // < 128 left: move them to the front
+    const uint64_t m0 = (uint32_t)lane < rest ? s_buf[k + lane] : 0;
+    const uint64_t m1 = (uint32_t)lane + kWave < rest ? s_buf[k + kWave + lane] : 0;
+    wave_sync();
+    if ((uint32_t)lane < rest) s_buf[lane] = m0;
+    if ((uint32_t)lane + kWave < rest) s_buf[kWave + lane] = m1;
+    nbuf = rest;
+    wave_sync();
   };
 
   for (uint64_t grp = gw; grp < ngroups; grp += nw) {
@@ -312,6 +336,7 @@ __global__ __launch_bounds__(kBlock) void k_scan(ScanParams p) {
     int tmax = tend;
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) tmax = max(tmax, __shfl_xor(tmax, d));
+    tmax = __builtin_amdgcn_readfirstlane(tmax);  // wavefront-uniform loop bound
     uint64_t mm = 0, cw = 0;
     if (tend) {
       mm = funnel(g[0], g[1], 2) >> msh;  // m-mer at t = 1
@@ -321,8 +346,8 @@ __global__ __launch_bounds__(kBlock) void k_scan(ScanParams p) {
     int last_pos = 0, jlo = 1;
     int u = 0;  // offset of t in its block of w positions
     for (int t = 1; t <= tmax; ++t) {
-      bool emit = false, fin = false;
-      int e_pos = 0, e_jlo = 0, e_jhi = 0;
+      bool emit = false;
+      uint64_t e_meta = 0;
       if (t <= tend) {
         const uint32_t key = order_key(mm) | (uint32_t)t;
         pmin = (u == 0 || key < pmin) ? key : pmin;
@@ -336,13 +361,10 @@ __global__ __launch_bounds__(kBlock) void k_scan(ScanParams p) {
           const int pos = (int)(mn & 1023u);
           if (j > 1 && pos != last_pos) {
             emit = true;
-            e_pos = last_pos;
-            e_jlo = jlo;
-            e_jhi = j - 1;
+            e_meta = run_meta(a, last_pos, jlo, j - 1);
             jlo = j;
           }
           last_pos = pos;
-          fin = (t == tend);
         }
         s_keys[u * kWave] = key;
         const int x = t + m;  // roll in the base at t + m
@@ -360,10 +382,13 @@ __global__ __launch_bounds__(kBlock) void k_scan(ScanParams p) {
       } else {
         ++u;
       }
-      put(emit, g, a, e_pos, e_jlo, e_jhi);
-      put(fin, g, a, last_pos, jlo, J);
+      put(emit, e_meta);
+      while (nbuf >= (uint32_t)kWave) flush(kWave);
     }
+    put(tend > 0, run_meta(a, last_pos, jlo, J));  // each read's last run
+    while (nbuf >= (uint32_t)kWave) flush(kWave);
   }
+  while (nbuf) flush(nbuf < (uint32_t)kWave ? nbuf : (uint32_t)kWave);
   if (lane == 0) p.run_cnt[gw] = cursor;
 }
 
@@ -383,28 +408,35 @@ struct ProbeParams {
   uint32_t* rows;                 // 3 dwords per row (mg_edge); one region per wavefront
   unsigned long long* reg_cnt;    // [waves] rows produced by each wavefront (may exceed reg_cap)
   uint64_t reg_cap;
-  int uniform_len;
+  int uniform_len;                // every read has this length (0: lengths differ)
   unsigned long long* stats;      // optional [kSegs*4]: runs probed, entries scanned, partners fetched, rows
   int phase_limit;                // diagnostics: 4 no probe, 5 + cell loads, 6 + filter, 7 full
 };
 
 template <int MAXW>
 struct ProbeLds {
-  static constexpr int CAND = 2 * kWave;
-  static constexpr size_t o_a = 0;                                    // [MAXW+1][64] u64 source words
-  static constexpr size_t o_cb = o_a + (size_t)(MAXW + 1) * kWave * 8;  // [CAND] u32 partner
-  static constexpr size_t o_ci = o_cb + CAND * 4;                     // [CAND] u32 o << 30 | j << 20 | ...
-  static constexpr size_t o_ca = o_ci + CAND * 4;                     // [CAND] u32 source read
+  static constexpr int CAND = 3 * kWave;  // candidate list (verified 64 at a time)
+  static constexpr int PEND = 2 * kWave;  // chained probe items waiting for a batch of their own
+  static constexpr size_t o_a = 0;                                      // [MAXW+1][64] u64 source words
+  static constexpr size_t o_pk = o_a + (size_t)(MAXW + 1) * kWave * 8;  // [PEND] u64 bucket | fp << 32
+  static constexpr size_t o_pm = o_pk + PEND * 8;                       // [PEND] u64 run meta
+  static constexpr size_t o_cb = o_pm + PEND * 8;                       // [CAND] u32 partner
+  static constexpr size_t o_ci = o_cb + CAND * 4;                       // [CAND] u32 o << 30 | j
+  static constexpr size_t o_ca = o_ci + CAND * 4;                       // [CAND] u32 source read
   static constexpr size_t bytes = o_ca + CAND * 4;
 };
 
-// Probe wavefront r consumes run region r in batches of 64 (one run per lane):
-// the home cell's count and 64-B line are loaded together, the chain is
-// followed while count > kCell; entries are exact candidates when the
-// fingerprint matches, j = p - q lies in the run's window range (so the
-// window's minimizer is this very m-mer at offset q) and the halving rule
-// keeps them.  Candidates are prefix-summed into an LDS list
-// and verified one per lane against the partner's words in HBM.
+// Probe wavefront r consumes its run regions in batches of 64 probe items (one
+// per lane).  An item is a run (bucket, fingerprint, read, minimizer position
+// p, window range [jlo, jhi]) or the continuation of a chained cell.  The cell
+// load of the NEXT batch is issued before the current batch is processed, so
+// one random 64-B line per lane is always in flight behind the work.  Entries
+// are exact candidates when the fingerprint matches, j = p - q lies in the
+// run's window range (the window's minimizer is this very m-mer at offset q)
+// and the halving rule keeps them.  Candidates go to an LDS list
+// (ballot + mbcnt per slot) and are verified one per lane against the
+// partner's slot in HBM; a full cell's chain flag turns the lane's item into a
+// pending item (LDS) that a later batch probes at the next cell.
 template <int MAXW, bool CONTAIN>
 __global__ __launch_bounds__(kBlock) void k_probe(ProbeParams p) {
   using PL = ProbeLds<MAXW>;
@@ -412,17 +444,20 @@ __global__ __launch_bounds__(kBlock) void k_probe(ProbeParams p) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   unsigned char* base = reinterpret_cast<unsigned char*>(smem) + (size_t)wv * PL::bytes;
   uint64_t* s_a = reinterpret_cast<uint64_t*>(base + PL::o_a);
+  uint64_t* s_pk = reinterpret_cast<uint64_t*>(base + PL::o_pk);
+  uint64_t* s_pm = reinterpret_cast<uint64_t*>(base + PL::o_pm);
   uint32_t* s_cb = reinterpret_cast<uint32_t*>(base + PL::o_cb);
   uint32_t* s_ci = reinterpret_cast<uint32_t*>(base + PL::o_ci);
   uint32_t* s_ca = reinterpret_cast<uint32_t*>(base + PL::o_ca);
   const int h = p.h;
   const uint64_t nbmask = (1ULL << p.nb_log2) - 1;
   const uint64_t gw = (uint64_t)blockIdx.x * kWavesPerBlock + wv;
-  const uint32_t seg = (uint32_t)(gw & (kSegs - 1));
   const uint64_t nwp = (uint64_t)gridDim.x * kWavesPerBlock;
+  const uint32_t seg = (uint32_t)(gw & (kSegs - 1));
   uint32_t* const region = p.rows + gw * p.reg_cap * 3;
   uint64_t cursor = 0;
   uint32_t st_runs = 0, st_ent = 0, st_ver = 0, st_rows = 0;
+  uint32_t ncand = 0, npend = 0;
 
   // verify the first nc (<= 64) candidates of the list, one per lane
   auto verify = [&](uint32_t nc) {
@@ -440,8 +475,8 @@ __global__ __launch_bounds__(kBlock) void k_probe(ProbeParams p) {
       sa = s_ca[lane];
       o = (int)(info >> 30);
       j = (int)(info & 1023u);
-      n1 = (int)p.len[sa];
-      n2 = p.uniform_len ? n1 : (int)p.len[bid];
+      n1 = p.uniform_len ? p.uniform_len : (int)p.len[sa];
+      n2 = p.uniform_len ? p.uniform_len : (int)p.len[bid];
       if (!CONTAIN) {
         if (o == 0) {        // F1[j, n1) == F2[0, L)
           L = n1 - j; cond = L < n2; x0 = j; y0 = 0; rcA = false;
@@ -518,13 +553,12 @@ __global__ __launch_bounds__(kBlock) void k_probe(ProbeParams p) {
       const uint32_t tot = 2u * (uint32_t)(__popcll(b2) + __popcll(b4));
       if (tot) {
         if (cursor + tot <= p.reg_cap) {
-          const uint64_t lt = lanemask_lt();
-          const uint32_t pr = 2u * (uint32_t)(__popcll(b2 & lt) + __popcll(b4 & lt));
-          uint32_t* d = region + (cursor + pr) * 3;
+          const uint32_t pr = 2u * (lane_prefix(b2) + lane_prefix(b4));
+          uint3* d = reinterpret_cast<uint3*>(region + (cursor + pr) * 3);
           for (int rr = 0; rr < nrec; rr += 2) {
-            d[0] = r0; d[1] = r1; d[2] = r2;
-            d[3] = t0; d[4] = t1; d[5] = t2;
-            d += 6;
+            d[0] = make_uint3(r0, r1, r2);
+            d[1] = make_uint3(t0, t1, t2);
+            d += 2;
           }
         }
         cursor += tot;  // keeps counting past the capacity: the host resizes and reruns
@@ -533,98 +567,183 @@ __global__ __launch_bounds__(kBlock) void k_probe(ProbeParams p) {
     wave_sync();
   };
 
-  uint32_t ncand = 0;
-  for (uint32_t rg = 0; rg < p.run_regions_per_wave; ++rg) {
-  const uint64_t reg = gw + (uint64_t)rg * nwp;
-  const ulonglong2* const runs = p.runs + reg * p.run_cap;
-  const uint64_t nruns = p.run_cnt[reg] < p.run_cap ? p.run_cnt[reg] : p.run_cap;
-  for (uint64_t r0i = 0; r0i < nruns && p.phase_limit > 4; r0i += kWave) {
-    const uint64_t k = r0i + (uint64_t)lane;
-    bool act = k < nruns;
-    const ulonglong2 rec = act ? runs[k] : make_ulonglong2(0, 0);
-    const uint64_t meta = rec.y;
+  // ---- run stream: this wavefront's run regions, 64 records per batch
+  uint32_t rg = 0;
+  uint64_t rpos = 0, rcnt = 0;
+  const ulonglong2* rbase = p.runs;
+  auto open_region = [&](uint32_t r) {
+    const uint64_t reg = gw + (uint64_t)r * nwp;
+    rbase = p.runs + reg * p.run_cap;
+    const uint64_t c = p.run_cnt[reg];
+    rcnt = c < p.run_cap ? c : p.run_cap;
+    rpos = 0;
+  };
+  // skip to the next non-empty batch position; false once the regions are exhausted
+  auto hbm_settle = [&]() -> bool {
+    while (rpos >= rcnt) {
+      if (rg + 1 >= p.run_regions_per_wave) return false;
+      open_region(++rg);
+    }
+    return true;
+  };
+  // next batch: pending items first once 64 are waiting, else the run stream
+  // (prefetched one batch ahead), else the last pending items
+  ulonglong2 rec_pf = make_ulonglong2(0, 0);
+  bool pf_ok = false, pf_any = false;
+  // (re)load the run batch at the stream position, unconditionally and outside
+  // any branch: no branch-merged value ever waits on a load in flight
+  auto hbm_fetch = [&]() {
+    const uint64_t k = rpos + (uint64_t)lane;
+    pf_ok = pf_any && k < rcnt;
+    rec_pf = rbase[pf_ok ? k : 0];
+  };
+  auto take_item = [&](uint64_t& key, uint64_t& meta, bool& valid) -> bool {
+    if (npend >= (uint32_t)kWave) {
+      npend -= kWave;
+      key = s_pk[npend + lane];
+      meta = s_pm[npend + lane];
+      valid = true;
+      return true;
+    }
+    if (pf_any) {
+      valid = pf_ok;
+      meta = rec_pf.y;
+      key = (rec_pf.x & nbmask) | ((uint64_t)((uint32_t)(rec_pf.x >> p.nb_log2) & kFpMask) << 32);
+      if (valid) ++st_runs;
+      rpos += kWave;
+      pf_any = hbm_settle();
+      return true;
+    }
+    if (npend) {
+      valid = (uint32_t)lane < npend;
+      key = valid ? s_pk[lane] : 0;
+      meta = valid ? s_pm[lane] : 0;
+      npend = 0;
+      return true;
+    }
+    valid = false;
+    return false;
+  };
+  // unconditional loads (invalid lanes read cell 0 and discard it): with no
+  // branch around them the compiler's vmcnt waits stay exact, so the next
+  // batch's line really is in flight behind the current batch
+  auto load_cell = [&](uint64_t key, bool valid, uint64_t* e) {
+    const ulonglong2* cp = reinterpret_cast<const ulonglong2*>(p.cells + (valid ? (key & 0xFFFFFFFFull) : 0) * kCell);
+#pragma unroll
+    for (int s = 0; s < kCell / 2; ++s) {
+      const ulonglong2 x = cp[s];
+      e[2 * s] = valid ? x.x : kEmpty;
+      e[2 * s + 1] = valid ? x.y : kEmpty;
+    }
+  };
+  auto process = [&](uint64_t key, uint64_t meta, bool valid, const uint64_t* e) {
     const uint32_t ra = (uint32_t)meta;
     const int rp = (int)((meta >> 32) & 1023u);
     const int rjlo = (int)((meta >> 42) & 1023u), rjhi = (int)((meta >> 52) & 1023u);
-    uint64_t b = rec.x & nbmask;  // the scan kept owned buckets only
-    const uint32_t fp = (uint32_t)(rec.x >> p.nb_log2) & kFpMask;
-    if (act) ++st_runs;
-    while (__ballot(act)) {
-      uint64_t e[kCell];
-      if (act) {
-        const ulonglong2* cp = reinterpret_cast<const ulonglong2*>(p.cells + b * kCell);
+    const uint32_t fp = (uint32_t)(key >> 32);
+    if (p.stats) {
 #pragma unroll
-        for (int s = 0; s < kCell / 2; ++s) {
-          const ulonglong2 x = cp[s];
-          e[2 * s] = x.x;
-          e[2 * s + 1] = x.y;
-        }
-      } else {
-#pragma unroll
-        for (int s = 0; s < kCell; ++s) e[s] = kEmpty;
-      }
-      if (p.stats) {
-#pragma unroll
-        for (int s = 0; s < kCell; ++s) st_ent += e[s] != kEmpty ? 1u : 0u;
-      }
-      uint32_t mask = 0;
-      if (p.phase_limit > 5) {
-#pragma unroll
-        for (int s = 0; s < kCell; ++s) {
-          const uint32_t hi = (uint32_t)(e[s] >> 32);
-          const int j = rp - (int)((hi >> 2) & 1023u);
-          const int oo = (int)(hi & 3u);
-          bool keep = e[s] != kEmpty && ((hi >> 12) & kFpMask) == fp && j >= rjlo && j <= rjhi;
-          // halving: o=1 hits are twins of the partner's o=0
-          // hits; o=2/3 hits are kept only for partner >= source
-          keep = keep && (CONTAIN || oo == 0 || (oo >= 2 && (uint32_t)e[s] >= ra));
-          mask |= (keep ? 1u : 0u) << s;
-        }
-      }
-      uint32_t total;
-      const uint32_t pre = wave_excl_scan((uint32_t)__popc(mask), lane, &total);
-      // append in passes so the list (capacity 2 x 64) never overflows
-      for (uint32_t c0 = 0; c0 < total; c0 += kWave) {
-        uint32_t at = pre;
-#pragma unroll
-        for (int s = 0; s < kCell; ++s) {
-          if (mask & (1u << s)) {
-            if (at >= c0 && at < c0 + kWave) {
-              const uint32_t hi = (uint32_t)(e[s] >> 32);
-              const int j = rp - (int)((hi >> 2) & 1023u);
-              const uint32_t slot = ncand + (at - c0);
-              s_cb[slot] = (uint32_t)e[s];
-              s_ci[slot] = ((hi & 3u) << 30) | (uint32_t)j;
-              s_ca[slot] = ra;
-            }
-            ++at;
-          }
-        }
-        ncand += min(total - c0, (uint32_t)kWave);
-        wave_sync();
-        if (ncand >= (uint32_t)kWave) {
-          if (p.phase_limit > 6) verify(kWave);
-          const uint32_t rest = ncand - kWave;
-          uint32_t mb = 0, mi = 0, ma = 0;
-          if ((uint32_t)lane < rest) {
-            mb = s_cb[kWave + lane];
-            mi = s_ci[kWave + lane];
-            ma = s_ca[kWave + lane];
-          }
-          wave_sync();
-          if ((uint32_t)lane < rest) {
-            s_cb[lane] = mb;
-            s_ci[lane] = mi;
-            s_ca[lane] = ma;
-          }
-          ncand = rest;
-          wave_sync();
-        }
-      }
-      act = act && (e[kCell - 1] & kChain) && e[kCell - 1] != kEmpty;
-      b = (b + 1) & nbmask;
+      for (int s = 0; s < kCell; ++s) st_ent += e[s] != kEmpty ? 1u : 0u;
     }
-  }
+    if (p.phase_limit <= 5) return;
+    // a full cell's chain flag: probe the next cell in a later batch
+    const bool chain = valid && e[kCell - 1] != kEmpty && (e[kCell - 1] & kChain);
+    const uint64_t cb = __ballot(chain);
+    if (chain) {
+      const uint32_t at = npend + lane_prefix(cb);
+      s_pk[at] = (((key & 0xFFFFFFFFull) + 1) & nbmask) | (key & 0xFFFFFFFF00000000ull);
+      s_pm[at] = meta;
+    }
+    npend += (uint32_t)__popcll(cb);
+    uint32_t keepm = 0;
+#pragma unroll
+    for (int s = 0; s < kCell; ++s) {
+      const uint32_t hi = (uint32_t)(e[s] >> 32);
+      const int j = rp - (int)((hi >> 2) & 1023u);
+      const int oo = (int)(hi & 3u);
+      bool keep = e[s] != kEmpty && ((hi >> 12) & kFpMask) == fp && j >= rjlo && j <= rjhi;
+      // halving: o=1 hits are twins of the partner's o=0
+      // hits; o=2/3 hits are kept only for partner >= source
+      keep = keep && (CONTAIN || oo == 0 || (oo >= 2 && (uint32_t)e[s] >= ra));
+      keepm |= (keep ? 1u : 0u) << s;
+    }
+    while (__ballot(keepm != 0)) {
+      // append slot groups while they fit, then verify a full wavefront
+#pragma unroll
+      for (int s = 0; s < kCell; ++s) {
+        const bool k = (keepm >> s) & 1u;
+        const uint64_t bal = __ballot(k);
+        const uint32_t nb = (uint32_t)__popcll(bal);
+        if (nb && ncand + nb <= (uint32_t)PL::CAND) {
+          if (k) {
+            const uint32_t hi = (uint32_t)(e[s] >> 32);
+            const uint32_t at = ncand + lane_prefix(bal);
+            s_cb[at] = (uint32_t)e[s];
+            s_ci[at] = ((hi & 3u) << 30) | (uint32_t)(rp - (int)((hi >> 2) & 1023u));
+            s_ca[at] = ra;
+            keepm &= ~(1u << s);
+          }
+          ncand += nb;
+        }
+      }
+      while (ncand >= (uint32_t)kWave) {
+        wave_sync();
+        if (p.phase_limit > 6) verify(kWave);
+        const uint32_t rest = ncand - kWave;  // < 128: move to the front
+        uint32_t mb0 = 0, mi0 = 0, ma0 = 0, mb1 = 0, mi1 = 0, ma1 = 0;
+        if ((uint32_t)lane < rest) {
+          mb0 = s_cb[kWave + lane]; mi0 = s_ci[kWave + lane]; ma0 = s_ca[kWave + lane];
+        }
+        if ((uint32_t)lane + kWave < rest) {
+          mb1 = s_cb[2 * kWave + lane]; mi1 = s_ci[2 * kWave + lane]; ma1 = s_ca[2 * kWave + lane];
+        }
+        wave_sync();
+        if ((uint32_t)lane < rest) {
+          s_cb[lane] = mb0; s_ci[lane] = mi0; s_ca[lane] = ma0;
+        }
+        if ((uint32_t)lane + kWave < rest) {
+          s_cb[kWave + lane] = mb1; s_ci[kWave + lane] = mi1; s_ca[kWave + lane] = ma1;
+        }
+        ncand = rest;
+        wave_sync();
+      }
+    }
+  };
+
+  if (p.phase_limit > 4 && p.run_regions_per_wave) {
+    open_region(0);
+    pf_any = hbm_settle();
+    hbm_fetch();
+    uint64_t key_c = 0, meta_c = 0, key_n = 0, meta_n = 0;
+    bool val_c = false, val_n = false;
+    uint64_t eA[kCell], eB[kCell];
+    bool have = take_item(key_c, meta_c, val_c);
+    hbm_fetch();
+    load_cell(key_c, val_c, eA);
+    // two batches per trip with ping-pong cell registers (no copies, so the
+    // compiler's vmcnt waits only ever cover the older batch's line)
+    while (have) {
+      bool have_n = take_item(key_n, meta_n, val_n);
+      hbm_fetch();
+      load_cell(key_n, val_n, eB);
+      process(key_c, meta_c, val_c, eA);
+      if (!have_n) {  // the stream ran dry: this batch may have left pending items
+        have_n = take_item(key_n, meta_n, val_n);
+        if (!have_n) break;
+        load_cell(key_n, val_n, eB);
+      }
+      key_c = key_n; meta_c = meta_n; val_c = val_n;
+      have_n = take_item(key_n, meta_n, val_n);
+      hbm_fetch();
+      load_cell(key_n, val_n, eA);
+      process(key_c, meta_c, val_c, eB);
+      if (!have_n) {
+        have_n = take_item(key_n, meta_n, val_n);
+        if (!have_n) break;
+        load_cell(key_n, val_n, eA);
+      }
+      key_c = key_n; meta_c = meta_n; val_c = val_n;
+    }
   }
   if (ncand && p.phase_limit > 6) verify(ncand);
   if (!CONTAIN && lane == 0) p.reg_cnt[gw] = cursor;
@@ -862,7 +981,7 @@ template <int W>
 struct LaunchIndex {
   static int run(mg_ctx* ctx) {
     IndexParams p = index_params(ctx);
-    const uint32_t grid = (uint32_t)((ctx->n + kBlock - 1) / kBlock);
+    const uint32_t grid = (uint32_t)((4 * ctx->n + kBlock - 1) / kBlock);  // one thread per key
     const size_t lds = (size_t)(W + 1) * kBlock * sizeof(uint64_t);
     if (grid == 0) return 0;
     allow_lds(k_index_build<W>, lds);
@@ -894,7 +1013,7 @@ struct LaunchDiscover {
     if (a_hi <= a_lo) return 0;
     const uint64_t ngroups = (a_hi - a_lo + kWave - 1) / kWave;
     const uint64_t want = (ngroups + kWavesPerBlock - 1) / kWavesPerBlock;
-    const size_t lds_scan = (size_t)kWavesPerBlock * ctx->w * kWave * sizeof(uint32_t);
+    const size_t lds_scan = (size_t)kWavesPerBlock * (((ctx->w * kWave + 1) / 2) + kScanBuf) * sizeof(uint64_t);
     const size_t lds_probe = (size_t)kWavesPerBlock * ProbeLds<W>::bytes;
     // probe grid = its resident blocks; the scan (fewer registers) runs k
     // times as many wavefronts and probe wavefront r consumes k scan regions
@@ -962,7 +1081,7 @@ struct LaunchDiscover {
     pp.rows = ctx->d_rows;
     pp.reg_cnt = ctx->d_seg;
     pp.reg_cap = contain ? 0 : ctx->rows_cap / ctx->nreg;
-    pp.uniform_len = ctx->minlen == ctx->maxlen;
+    pp.uniform_len = ctx->minlen == ctx->maxlen ? (int)ctx->maxlen : 0;
     pp.stats = contain ? nullptr : (ctx->stats ? ctx->d_stats : nullptr);
     pp.phase_limit = contain ? 99 : ctx->phase_limit;
     if (contain)
