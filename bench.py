@@ -90,15 +90,19 @@ def cpu_baseline(cfg, sample_reads: int):
             "reads_per_sec": od.num_unique / secs}
 
 
-def load_pmc(path, kernel_substr="k_discover"):
-    """Per-launch HBM traffic of the discovery kernel from a committed rocprofv3
-    --pmc summary (profiles/*pmc*.json written by tools/pmc_summary.py)."""
+def load_pmc(path):
+    """HBM traffic of one step from a committed rocprofv3 --pmc summary
+    (tools/pmc_summary.py): (2 x FETCH_SIZE + WRITE_SIZE) summed over the step's
+    kernels, per launch (MI355X_MICROARCH.md §HBM gfx950 correction)."""
     try:
         with open(path) as f:
             d = json.load(f)
-        return d.get("traffic_bytes_per_launch")
     except Exception:
         return None
+    tr = d.get("traffic", {})
+    tot = sum(v["traffic_bytes_per_launch"] for k, v in tr.items()
+              if k.startswith(("k_index_build", "k_scan", "k_probe")))
+    return tot or None
 
 
 def main():
@@ -113,7 +117,7 @@ def main():
     ap.add_argument("--sim-rank", type=int, default=0)
     ap.add_argument("--cpu-sample", type=int, default=150_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r01_pmc_c3.json"))
+    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r01s2_pmc_c3.json"))
     ap.add_argument("--nb-log2", type=int, default=0)
     args = ap.parse_args()
 
@@ -160,7 +164,7 @@ def main():
             dist.barrier()
 
     barrier()
-    dev_ms = {"index_ms": 0.0, "contained_ms": 0.0, "overlap_ms": 0.0}
+    dev_ms = {"index_ms": 0.0, "contained_ms": 0.0, "overlap_ms": 0.0, "scan_ms": 0.0, "probe_ms": 0.0}
     t0 = time.perf_counter()
     for _ in range(args.steps):
         rows = step()
@@ -188,16 +192,17 @@ def main():
         dist.destroy_process_group()
         return
 
-    wpr = ds.packed()[0].shape[1]
-    # algorithmic bytes of one discovery launch
-    alg = (cnt["sources"] * (8 * wpr + 2) + cnt["runs"] * 8 + cnt["entries"] * 8
-           + cnt["verified"] * 8 * (wpr + 1) + cnt["rows"] * 12)
-    ov_s = dev_ms["overlap_ms"] / 1000.0
-    achieved = alg / ov_s / 1e9 if ov_s > 0 else 0.0
-    # SURVEY §8(d) per-read figure for the reference's W-probe formulation, for comparison
-    W = lo - (l - 1) - 1
+    # Roofline: SURVEY §8(d) algorithmic bytes per read,
+    #   B = ceil(n/4) + 4*16 + W*16 + D*(ceil(n/4) + 16),  D = directed rows per read,
+    # times the reads one step processes, over the step's summed kernel durations
+    # (HIP events on the context's stream: index build incl. cell memset, scan, probe).
+    nbar = (lo + hi) / 2.0
+    W = max(0.0, nbar - (l - 1) - 1)
     D = rows / max(1, cnt["sources"])
-    survey_bytes = cnt["sources"] * (-(-lo // 4) + 64 + W * 16 + D * (-(-lo // 4) + 16))
+    per_read = -(-nbar // 4) + 64 + W * 16 + D * (-(-nbar // 4) + 16)
+    alg = N * per_read
+    kern_ms = dev_ms["index_ms"] + dev_ms["contained_ms"] + dev_ms["overlap_ms"]
+    achieved = alg / (kern_ms / 1000.0) / 1e9 if kern_ms > 0 else 0.0
     traffic = load_pmc(args.pmc) if args.config == "c3" and world == 1 and not args.sim_world else None
     res = {
         "metric": "overlap edges/sec",
@@ -221,8 +226,9 @@ def main():
         "counters": cnt,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": "k_discover", "alg_bytes_per_launch": alg,
-                     "survey_8d_bytes_per_launch": survey_bytes},
+                     "kernel": "step = k_index_build + k_scan + k_probe (dominant: k_probe)",
+                     "alg_bytes_per_step": alg, "alg_bytes_per_read": per_read, "kernel_ms_per_step": kern_ms,
+                     "probe_ms": dev_ms.get("probe_ms"), "scan_ms": dev_ms.get("scan_ms")},
     }
     if world == 1 and not args.no_cpu_baseline and not args.sim_world:
         try:

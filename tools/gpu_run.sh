@@ -1,0 +1,40 @@
+#!/bin/bash
+# One GPU-box session: parity tests, C3 bench (with CPU baseline), rocprofv3
+# kernel-trace stats of the same bench command, and FETCH_SIZE / WRITE_SIZE PMC
+# passes (each its own run, --kernel-trace only).  Every GPU step has its own
+# time limit; the first failure ends the script.
+#   usage: tools/gpu_run.sh TAG [tests|bench|prof|pmc ...]   (default: all)
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+TAG=${1:-run}; shift
+STEPS=${@:-tests bench prof pmc}
+OUT=gpurun_out/$TAG
+mkdir -p $OUT
+for s in $STEPS; do
+  case $s in
+  tests)
+    timeout -k 10 900 python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread > $OUT/gpu_tests.log 2>&1
+    rc=$?; echo "tests rc=$rc"; tail -3 $OUT/gpu_tests.log ;;
+  smoke)
+    timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1
+    rc=$?; echo "smoke rc=$rc"; tail -3 $OUT/smoke.log ;;
+  bench)
+    timeout -k 10 600 python -u bench.py > $OUT/bench.json 2> $OUT/bench.err
+    rc=$?; echo "bench rc=$rc"; cat $OUT/bench.json ;;
+  benchc2)
+    timeout -k 10 300 python -u bench.py --config c2 --no-cpu-baseline > $OUT/bench_c2.json 2> $OUT/bench_c2.err
+    rc=$?; echo "bench c2 rc=$rc"; cat $OUT/bench_c2.json ;;
+  prof)
+    timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o kt -- python3 bench.py --steps 5 --no-cpu-baseline > $OUT/prof_bench.json 2> $OUT/prof_bench.err
+    rc=$?; echo "prof rc=$rc"; cat $OUT/prof_bench.json ;;
+  pmc)
+    for set in "FETCH_SIZE" "WRITE_SIZE"; do
+      timeout -s KILL 300 rocprofv3 --pmc $set --kernel-trace --output-format csv -d $OUT/pmc_$set -o p -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline > $OUT/pmc_$set.log 2>&1
+      rc=$?; echo "pmc $set rc=$rc"; [ $rc -ne 0 ] && break
+    done
+    [ $rc -eq 0 ] && python3 tools/pmc_summary.py $OUT/pmc_summary.json $OUT/pmc_* > /dev/null ;;
+  *) echo "unknown step $s"; rc=2 ;;
+  esac
+  if [ $rc -ne 0 ]; then tail -30 $OUT/*.err 2>/dev/null; exit $rc; fi
+done
+exit 0
