@@ -8,8 +8,13 @@ HBM.  Inputs (2-bit packed reads) are resident in HBM before timing starts.
 
 Default workload = BASELINE.json configs[2] (C3): 10M x 150 bp synthetic
 reads, 20x coverage of a 75 Mb random genome, 50 % reverse-complemented,
-l = 50, seed k = 31.  Multi-GPU (torchrun): the same 10M reads on N GPUs,
-strong scaling; each rank owns a bucket range of the index.
+l = 50, seed k = 31.  Multi-GPU (torchrun, one process per GPU): the same 10M
+reads on N GPUs (strong scaling) in exchange mode:
+each rank owns a bucket range of the index and a source-read range; key
+records, window runs and rows move between ranks with RCCL all-to-all(v) over
+xGMI (torch.distributed "nccl"), and each rank ends with the rows whose src it
+owns.  --sim-world P runs all P ranks of that mode inside one process on one
+GPU (buffers exchanged on the device) to check and time the sharded kernels.
 
 Prints ONE JSON line (rank 0).  See DESIGN.md §5 for the roofline numbers.
 """
@@ -111,10 +116,8 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
-    ap.add_argument("--shard", default="buckets", choices=["buckets", "reads"])
     ap.add_argument("--sim-world", type=int, default=0,
-                    help="run rank --sim-rank of a SIM-WORLD-way shard on this one GPU (scaling study)")
-    ap.add_argument("--sim-rank", type=int, default=0)
+                    help="run all SIM-WORLD ranks of the exchange mode in this process on one GPU")
     ap.add_argument("--cpu-sample", type=int, default=150_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r01s2_pmc_c3.json"))
@@ -124,69 +127,102 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:
-        import torch.distributed as dist  # control plane only (barrier, max/sum reductions)
-
-        dist.init_process_group("gloo")
     cfg = CONFIGS[args.config]
     n, lo, hi, G, l, k, seed, desc = cfg
     nthreads = max(2, 16 // max(1, world))
-
     ds, _, _ = make_dataset(cfg, nthreads)
-    eng = OverlapEngine(local)
-    eng.set_option("nb_log2", args.nb_log2)
-    shard_world, shard_rank = (world, rank) if world > 1 else (args.sim_world or 1, args.sim_rank)
     N = ds.num_unique
-    if args.shard == "buckets":
-        eng.set_shard(shard_rank, shard_world, 0, 0)
+
+    import torch
+
+    dist = None
+    xchg = None
+    if world > 1:
+        import torch.distributed as dist
+
+        from metagenomics_amd.sharded import TorchExchange
+
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))  # RCCL over xGMI
+        xchg = TorchExchange(torch.device("cuda", local))
+        mode = "exchange"
+    elif args.sim_world > 1:
+        from metagenomics_amd.sharded import LocalExchange
+
+        xchg = LocalExchange(args.sim_world, torch.device("cuda", local))
+        mode = "exchange-sim"
     else:
-        eng.set_shard(0, 1, N * shard_rank // shard_world, N * (shard_rank + 1) // shard_world)
+        mode = "fused"
+    P = world if world > 1 else max(1, args.sim_world)
+
+    engines = []
     t0 = time.time()
-    eng.upload(ds)
-    log(f"[bench] rank {rank}: upload {time.time() - t0:.2f}s")
+    for r in ([rank] if world > 1 else range(P)):
+        e = OverlapEngine(local)
+        e.set_option("nb_log2", args.nb_log2)
+        e.set_shard(r, P, 0, 0)
+        e.upload(ds)
+        engines.append(e)
+    log(f"[bench] rank {rank}: upload {time.time() - t0:.2f}s ({mode}, P={P})")
+
+    from metagenomics_amd.sharded import sharded_step
 
     def step():
-        eng.build_index(l, k)
-        eng.mark_contained(copy=False)
-        return eng.find_overlaps()
+        """one pass of the hot path; returns directed rows held by this process"""
+        if mode == "fused":
+            e = engines[0]
+            e.build_index(l, k)
+            e.mark_contained(copy=False)
+            return e.find_overlaps()
+        res = sharded_step(engines, xchg, l, k)
+        for kk, v in res.ms.items():
+            phase_ms[kk] = phase_ms.get(kk, 0.0) + v
+        return sum(nr for _, nr in res.rows)
+
+    phase_ms = {}
+
+    def sync_barrier():
+        torch.cuda.synchronize(local)
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize(local)
 
     # one counting pass (untimed) for the roofline's algorithmic bytes
-    eng.set_option("stats", 1)
+    for e in engines:
+        e.set_option("stats", 1)
     rows = step()
-    cnt = eng.counters()
-    eng.set_option("stats", 0)
+    cnt = {}
+    for e in engines:
+        for kk, v in e.counters().items():
+            cnt[kk] = cnt.get(kk, 0) + v
+        e.set_option("stats", 0)
+    cnt["sources"] = N if mode != "exchange" else cnt.get("sources", 0)
     for _ in range(args.warmup):
         step()
 
-    def barrier():
-        if dist is not None:
-            dist.barrier()
-
-    barrier()
     dev_ms = {"index_ms": 0.0, "contained_ms": 0.0, "overlap_ms": 0.0, "scan_ms": 0.0, "probe_ms": 0.0}
+    phase_ms.clear()
+    sync_barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         rows = step()
-        t = eng.timings()
-        for kk in dev_ms:
-            dev_ms[kk] += t[kk]
+        for e in engines:
+            t = e.timings()
+            for kk in dev_ms:
+                dev_ms[kk] += t[kk]
+    torch.cuda.synchronize(local)
     t1 = time.perf_counter()
-    barrier()
+    sync_barrier()
     ms_step = (t1 - t0) * 1000.0 / args.steps
     dev_ms = {kk: v / args.steps for kk, v in dev_ms.items()}
-    edges_rank = rows // 2
     if dist is not None:
-        import torch
-
-        tt = torch.tensor([ms_step], dtype=torch.float64)
+        tt = torch.tensor([ms_step], dtype=torch.float64, device="cuda")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         ms_step = float(tt.item())
-        ee = torch.tensor([edges_rank], dtype=torch.int64)
+        ee = torch.tensor([rows], dtype=torch.int64, device="cuda")
         dist.all_reduce(ee, op=dist.ReduceOp.SUM)
-        edges = int(ee.item())
-    else:
-        edges = edges_rank
+        rows = int(ee.item())
+    edges = rows // 2
     if rank != 0:
         dist.barrier()
         dist.destroy_process_group()
@@ -198,12 +234,29 @@ def main():
     # (HIP events on the context's stream: index build incl. cell memset, scan, probe).
     nbar = (lo + hi) / 2.0
     W = max(0.0, nbar - (l - 1) - 1)
-    D = rows / max(1, cnt["sources"])
+    D = rows / max(1, N)
     per_read = -(-nbar // 4) + 64 + W * 16 + D * (-(-nbar // 4) + 16)
     alg = N * per_read
     kern_ms = dev_ms["index_ms"] + dev_ms["contained_ms"] + dev_ms["overlap_ms"]
-    achieved = alg / (kern_ms / 1000.0) / 1e9 if kern_ms > 0 else 0.0
-    traffic = load_pmc(args.pmc) if args.config == "c3" and world == 1 and not args.sim_world else None
+    roof = None
+    if mode == "fused":
+        achieved = alg / (kern_ms / 1000.0) / 1e9 if kern_ms > 0 else 0.0
+        traffic = load_pmc(args.pmc) if args.config == "c3" else None
+        roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                "kernel": "step = k_index_build + k_scan + k_probe (dominant: k_probe)",
+                "alg_bytes_per_step": alg, "alg_bytes_per_read": per_read, "kernel_ms_per_step": kern_ms,
+                "probe_ms": dev_ms["probe_ms"], "scan_ms": dev_ms["scan_ms"]}
+    else:
+        # per-rank work is 1/P of the reads: roofline of rank 0's kernels on its share
+        achieved = alg / P / (kern_ms / 1000.0) / 1e9 if kern_ms > 0 else 0.0
+        roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                "kernel": "rank 0 step kernels (key records + insert, scan, probe)",
+                "alg_bytes_per_step": alg / P, "kernel_ms_per_step": kern_ms}
+    par = {"fused": "1 GPU, fused path",
+           "exchange": f"{P} ranks: bucket-range index + source-range shards, RCCL all-to-all",
+           "exchange-sim": f"{P} simulated ranks on 1 GPU (device-local exchange)"}[mode]
     res = {
         "metric": "overlap edges/sec",
         "value": edges / (ms_step / 1000.0),
@@ -218,19 +271,15 @@ def main():
         "dtype": "u64",
         "data": "synthetic",
         "config": {"workload": desc, "reads": n, "unique_reads": N, "read_len": [lo, hi], "genome_len": G,
-                   "min_overlap": l, "seed_k": k, "seed": seed,
-                   "parallelism": f"{args.shard}-shard x {shard_world}" + (" (simulated rank)" if args.sim_world else "")},
+                   "min_overlap": l, "seed_k": k, "seed": seed, "parallelism": par},
         "reads_per_sec": N / (ms_step / 1000.0),
         "undirected_edges": edges,
         "device_ms": dev_ms,
+        "phase_wall_ms": {kk: v / args.steps for kk, v in phase_ms.items()} or None,
         "counters": cnt,
-        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": "step = k_index_build + k_scan + k_probe (dominant: k_probe)",
-                     "alg_bytes_per_step": alg, "alg_bytes_per_read": per_read, "kernel_ms_per_step": kern_ms,
-                     "probe_ms": dev_ms.get("probe_ms"), "scan_ms": dev_ms.get("scan_ms")},
+        "roofline": roof,
     }
-    if world == 1 and not args.no_cpu_baseline and not args.sim_world:
+    if world == 1 and mode == "fused" and not args.no_cpu_baseline:
         try:
             res["cpu_baseline"] = cpu_baseline(cfg, args.cpu_sample)
         except Exception as e:  # report, never fake

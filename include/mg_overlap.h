@@ -123,6 +123,49 @@ int mg_copy_rows(mg_ctx* ctx, mg_edge* out, uint64_t cap, uint64_t* n_copied);
  * this shard's part of the multiset; the union over ranks is the whole. */
 int mg_set_shard(mg_ctx* ctx, uint32_t rank, uint32_t nranks, uint64_t read_lo, uint64_t read_hi);
 
+/* --- exchange mode: one process per GPU, SURVEY §8(e) ------------------------
+ * Rank r of P (mg_set_shard(ctx, r, P, 0, 0)) owns the index buckets b with
+ * floor(b P / 2^nb) == r and the source reads (IDs - 1) in
+ * [floor(r N / P), floor((r+1) N / P)); every rank holds all packed reads.
+ * One step (the host moves each packed buffer with an all-to-all(v), e.g.
+ * torch.distributed.all_to_all_single over RCCL; metagenomics_amd/sharded.py):
+ *   mg_key_records -> mg_pack(MG_KEYS) -> a2a -> mg_insert_keys     (insertDataset)
+ *   mg_begin_contained(superkey buffer)
+ *   [lengths differ: mg_scan_runs(1) -> mg_pack(MG_RUNS) -> a2a
+ *    -> mg_probe_runs(1) -> all-reduce MAX of the superkey buffer]   (markContainedReads)
+ *   mg_finalize_contained
+ *   mg_scan_runs(0) -> mg_pack(MG_RUNS) -> a2a -> mg_probe_runs(0)   (insertAllEdgesOfRead)
+ *   -> mg_pack(MG_ROWS) -> a2a: every rank ends with the rows whose src it owns.
+ * counts[P] out-parameters give the records bound for each rank (the send
+ * split sizes); mg_pack writes them grouped by destination rank, in rank order,
+ * into a caller-owned device buffer.  Record sizes: mg_record_bytes(). */
+enum { MG_KEYS = 0, MG_RUNS = 1, MG_ROWS = 2 };
+uint32_t mg_record_bytes(int what);
+/* Keys of this rank's source reads (hashRead, HashTable.cpp:88-104) as 16-B
+ * index records; sets up (and clears) this rank's part of the index. */
+int mg_key_records(mg_ctx* ctx, uint32_t min_overlap, uint32_t seed_k, uint64_t* counts);
+/* File n received key records (device pointer) into the local index
+ * (insertIntoTable, HashTable.cpp:163-195). */
+int mg_insert_keys(mg_ctx* ctx, const void* recs, uint64_t n);
+/* Minimizer runs of this rank's source reads' windows (OverlapGraph.cpp:534-537)
+ * as 16-B run records; contain = 1 for the markContainedReads pass. */
+int mg_scan_runs(mg_ctx* ctx, int contain, uint64_t* counts);
+/* Probe n received run records (device pointer) against the local index;
+ * contain = 0: verified rows (+ twins) stay in the context, counts[P] = rows
+ * per src owner; contain = 1: containment keys (atomicMax) into the superkey
+ * buffer of mg_begin_contained. */
+int mg_probe_runs(mg_ctx* ctx, int contain, const void* runs, uint64_t n, uint64_t* counts);
+/* Copy the last routable output (keys, runs or rows) grouped by destination
+ * rank into dst (device pointer, capacity cap records). */
+int mg_pack(mg_ctx* ctx, int what, void* dst, uint64_t cap);
+/* Containment: *needed = 1 when read lengths differ (OverlapGraph.cpp:228-233).
+ * superkey = caller-owned device array of n_reads u64 (NULL: context-owned),
+ * cleared here; the contain probe atomicMax-es (len << 32 | ~index) into it,
+ * the host all-reduces it with MAX over the ranks, and mg_finalize_contained
+ * turns it into superReadID (super_out optional, n_reads + 1 entries). */
+int mg_begin_contained(mg_ctx* ctx, void* superkey, int* needed);
+int mg_finalize_contained(mg_ctx* ctx, uint32_t* super_out);
+
 /* --- diagnostics ----------------------------------------------------------- */
 int mg_get_timings(const mg_ctx* ctx, mg_timings* t);
 int mg_get_counters(const mg_ctx* ctx, mg_counters* c);

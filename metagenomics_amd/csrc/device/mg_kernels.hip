@@ -151,7 +151,8 @@ struct IndexParams {
   int h, m, w;
   uint32_t nb_log2;
   uint32_t rank, nranks;
-  uint64_t* cells;   // [NC * kCell] entries: lo32 = read index, hi32 = chain1 | fp19 | q10 | o2
+  uint64_t cell_lo, cell_n;  // this rank's bucket range [cell_lo, cell_lo + cell_n): local cell = bucket - cell_lo
+  uint64_t* cells;   // [cell_n * kCell] entries: lo32 = read index, hi32 = chain1 | fp19 | q10 | o2
 };
 
 __device__ __forceinline__ bool owned(uint64_t bkt, uint32_t nb_log2, uint32_t rank, uint32_t nranks) {
@@ -181,11 +182,45 @@ __device__ __forceinline__ uint64_t key_minimizer(const uint64_t* f, int n, int 
   return mix64(bmm);
 }
 
+// Next cell of a chain inside the rank's local range (wraps at its end).
+__device__ __forceinline__ uint64_t next_cell(uint64_t c, uint64_t n) { return c + 1 == n ? 0 : c + 1; }
+
+// Index entry: lo32 = read index, hi32 = fp19 << 12 | q10 << 2 | o2 (the chain
+// bit, bit 63, is set on a full cell's last slot).
+__device__ __forceinline__ unsigned long long make_entry(uint64_t v, uint32_t nb_log2, int q, int o, uint32_t r) {
+  const uint32_t fp = (uint32_t)(v >> nb_log2) & kFpMask;
+  return ((unsigned long long)((fp << 12) | ((uint32_t)q << 2) | (uint32_t)o) << 32) | r;
+}
+
+// insertIntoTable (HashTable.cpp:163-195) for one entry: one 64-B cell load,
+// then CAS into the slots that looked empty (slots only ever go from empty to
+// filled, so a stale view just makes a CAS fail); a full cell gets the chain
+// flag and the walk moves to the next cell of the local range.
+__device__ __forceinline__ void cell_insert(uint64_t* cells, uint64_t c, uint64_t cell_n, unsigned long long entry) {
+  for (uint64_t probe = 0; probe < cell_n; ++probe) {  // capacity >= 2x entries: ends in a few steps
+    unsigned long long* cell = reinterpret_cast<unsigned long long*>(cells + c * kCell);
+    uint64_t e[kCell];
+    const ulonglong2* cp = reinterpret_cast<const ulonglong2*>(cell);
+#pragma unroll
+    for (int s = 0; s < kCell / 2; ++s) {
+      const ulonglong2 x = cp[s];
+      e[2 * s] = x.x;
+      e[2 * s + 1] = x.y;
+    }
+    bool done = false;
+#pragma unroll
+    for (int s = 0; s < kCell; ++s)
+      if (!done && e[s] == kEmpty) done = atomicCAS(&cell[s], kEmpty, entry) == kEmpty;
+    if (done) return;
+    // every slot is filled now: flag the chain (slot 7 holds an entry)
+    if (e[kCell - 1] == kEmpty || !(e[kCell - 1] & kChain)) atomicOr(&cell[kCell - 1], (unsigned long long)kChain);
+    c = next_cell(c, cell_n);
+  }
+}
+
 // HashTable::insertDataset (HashTable.cpp:50-80): one thread per key (read r,
 // key o = hashRead's four strings, HashTable.cpp:88-104) finds the key's
-// minimizer and files the entry: one 64-B cell load, then CAS into the slots
-// that looked empty (slots only ever go from empty to filled, so a stale view
-// just makes a CAS fail); a full cell gets the chain flag and the walk moves on.
+// minimizer and files the entry in its home cell (this rank's buckets only).
 template <int MAXW>
 __global__ __launch_bounds__(kBlock) void k_index_build(IndexParams p) {
   extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
@@ -202,30 +237,42 @@ __global__ __launch_bounds__(kBlock) void k_index_build(IndexParams p) {
   const uint64_t mask = (1ULL << p.nb_log2) - 1;
   int q;
   const uint64_t v = key_minimizer<kBlock>(f, n, o, p.h, p.m, p.w, &q);
-  uint64_t b = v & mask;
+  const uint64_t b = v & mask;
   if (!owned(b, p.nb_log2, p.rank, p.nranks)) return;
-  const uint32_t fp = (uint32_t)(v >> p.nb_log2) & kFpMask;
-  const unsigned long long entry =
-      ((unsigned long long)((fp << 12) | ((uint32_t)q << 2) | (uint32_t)o) << 32) | (uint32_t)r;
-  for (uint64_t probe = 0; probe <= mask; ++probe) {  // capacity >= 2x entries: ends in a few steps
-    unsigned long long* cell = reinterpret_cast<unsigned long long*>(p.cells + b * kCell);
-    uint64_t e[kCell];
-    const ulonglong2* cp = reinterpret_cast<const ulonglong2*>(cell);
+  cell_insert(p.cells, b - p.cell_lo, p.cell_n, make_entry(v, p.nb_log2, q, o, (uint32_t)r));
+}
+
+// Exchange mode, step 1: the index records of the keys of source reads
+// [a_lo, a_hi) (16 B: x = mix64(minimizer), y = entry without fingerprint),
+// written densely in key order; k_part routes them to the bucket owners.
+template <int MAXW>
+__global__ __launch_bounds__(kBlock) void k_key_records(IndexParams p, uint64_t a_lo, uint64_t a_hi,
+                                                       ulonglong2* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
+  const uint64_t gid = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  const uint64_t r = a_lo + (gid >> 2);
+  const int o = (int)(gid & 3);
+  if (r >= a_hi) return;
+  uint64_t* f = smem + threadIdx.x;
+  const uint64_t* g = p.words + r * slot_words(MAXW);
 #pragma unroll
-    for (int s = 0; s < kCell / 2; ++s) {
-      const ulonglong2 x = cp[s];
-      e[2 * s] = x.x;
-      e[2 * s + 1] = x.y;
-    }
-    bool done = false;
-#pragma unroll
-    for (int s = 0; s < kCell; ++s)
-      if (!done && e[s] == kEmpty) done = atomicCAS(&cell[s], kEmpty, entry) == kEmpty;
-    if (done) return;
-    // every slot is filled now: flag the chain (slot 7 holds an entry)
-    if (e[kCell - 1] == kEmpty || !(e[kCell - 1] & kChain)) atomicOr(&cell[kCell - 1], (unsigned long long)kChain);
-    b = (b + 1) & mask;
-  }
+  for (int k = 0; k < MAXW; ++k) f[k * kBlock] = g[k];
+  f[MAXW * kBlock] = 0;
+  int q;
+  const uint64_t v = key_minimizer<kBlock>(f, p.len[r], o, p.h, p.m, p.w, &q);
+  out[gid] = make_ulonglong2(v, ((unsigned long long)(((uint32_t)q << 2) | (uint32_t)o) << 32) | (uint32_t)r);
+}
+
+// Exchange mode, step 2: file the records routed to this rank.
+__global__ __launch_bounds__(kBlock) void k_insert_records(IndexParams p, const ulonglong2* __restrict__ rec,
+                                                           uint64_t n) {
+  const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  const ulonglong2 x = rec[i];
+  const uint64_t b = x.x & ((1ULL << p.nb_log2) - 1);
+  const uint32_t hi = (uint32_t)(x.y >> 32);
+  cell_insert(p.cells, b - p.cell_lo, p.cell_n,
+              make_entry(x.x, p.nb_log2, (int)((hi >> 2) & 1023u), (int)(hi & 3u), (uint32_t)x.y));
 }
 
 // ------------------------------------------------------------- discovery ---
@@ -398,6 +445,7 @@ struct ProbeParams {
   int h, m;
   uint32_t nb_log2;
   uint32_t rank, nranks;
+  uint64_t cell_lo, cell_n;       // local bucket range of the cell table (IndexParams)
   const uint64_t* cells;
   const uint32_t* super;          // superReadID per read index (nullptr: none contained)
   unsigned long long* superkey;   // CONTAIN: max over containers of (len << 32 | ~index)
@@ -608,7 +656,8 @@ __global__ __launch_bounds__(kBlock) void k_probe(ProbeParams p) {
     if (pf_any) {
       valid = pf_ok;
       meta = rec_pf.y;
-      key = (rec_pf.x & nbmask) | ((uint64_t)((uint32_t)(rec_pf.x >> p.nb_log2) & kFpMask) << 32);
+      key = (valid ? (rec_pf.x & nbmask) - p.cell_lo : 0) |
+            ((uint64_t)((uint32_t)(rec_pf.x >> p.nb_log2) & kFpMask) << 32);
       if (valid) ++st_runs;
       rpos += kWave;
       pf_any = hbm_settle();
@@ -651,7 +700,7 @@ __global__ __launch_bounds__(kBlock) void k_probe(ProbeParams p) {
     const uint64_t cb = __ballot(chain);
     if (chain) {
       const uint32_t at = npend + lane_prefix(cb);
-      s_pk[at] = (((key & 0xFFFFFFFFull) + 1) & nbmask) | (key & 0xFFFFFFFF00000000ull);
+      s_pk[at] = next_cell(key & 0xFFFFFFFFull, p.cell_n) | (key & 0xFFFFFFFF00000000ull);
       s_pm[at] = meta;
     }
     npend += (uint32_t)__popcll(cb);
@@ -770,6 +819,125 @@ __global__ __launch_bounds__(kBlock) void k_compact_rows(const uint32_t* __restr
   for (uint64_t i = threadIdx.x; i < c; i += kBlock) dst[i] = src[i];
 }
 
+// ------------------------------------------------------- exchange routing ---
+// Records produced in per-wavefront regions (or one flat array) are routed to
+// their owning rank for one all-to-all(v), as a stable-per-block counting sort
+// by destination: pass 0 counts per (block, destination) in LDS, k_part_scan
+// turns the counts into send offsets (destination-major, so the send buffer is
+// grouped by rank in rank order), pass 1 re-walks the same regions with the
+// same grid and scatters through LDS cursors (no global atomics).  Within a
+// wavefront the lanes bound for one destination take one LDS cursor step
+// together (ballot + mbcnt); order inside a destination is irrelevant (the
+// result is a multiset).
+//   OWN_BUCKET: 16-B key/run records, owner of mix64 value x = bucket range
+//               (same rule as owned());
+//   OWN_SRC   : 12-B rows, owner of src ID = source-read range
+//               [floor(r N / P), floor((r+1) N / P)) -> (src P - 1) / N.
+enum OwnerKind { OWN_BUCKET = 0, OWN_SRC = 1 };
+constexpr int kMaxRanks = 64;
+
+struct PartParams {
+  const void* base;                 // region r starts at base + r * cap records
+  uint64_t cap;                     // records per region
+  const unsigned long long* cnt;    // records per region (nullptr: flat array of flat_n records)
+  uint64_t nreg, flat_n;
+  uint32_t nranks, nb_log2;
+  uint64_t n_reads;
+  unsigned long long* blk;          // [gridDim.x * nranks]: pass 0 counts, then send offsets
+  void* out;
+};
+
+template <int KIND, int PASS>
+__global__ __launch_bounds__(kBlock) void k_part(PartParams p) {
+  __shared__ unsigned long long s_cnt[kMaxRanks];
+  const int lane = threadIdx.x & 63;
+  if (threadIdx.x < kMaxRanks)
+    s_cnt[threadIdx.x] = (PASS == 1 && threadIdx.x < p.nranks) ? p.blk[(uint64_t)blockIdx.x * p.nranks + threadIdx.x] : 0;
+  __syncthreads();
+  for (uint64_t r = blockIdx.x; r < p.nreg; r += gridDim.x) {
+    uint64_t c = p.cnt ? p.cnt[r] : (p.flat_n > r * p.cap ? p.flat_n - r * p.cap : 0);
+    c = c < p.cap ? c : p.cap;
+    for (uint64_t i0 = 0; i0 < c; i0 += kBlock) {
+      const uint64_t i = i0 + threadIdx.x;
+      const bool valid = i < c;
+      uint32_t d = 0;
+      ulonglong2 x16 = make_ulonglong2(0, 0);
+      uint3 x12 = make_uint3(0, 0, 0);
+      if (valid) {
+        if (KIND == OWN_BUCKET) {
+          x16 = reinterpret_cast<const ulonglong2*>(p.base)[r * p.cap + i];
+          d = (uint32_t)(((x16.x & ((1ULL << p.nb_log2) - 1)) * p.nranks) >> p.nb_log2);
+        } else {
+          x12 = reinterpret_cast<const uint3*>(p.base)[r * p.cap + i];
+          d = (uint32_t)(((uint64_t)x12.x * p.nranks - 1) / p.n_reads);  // src is the 1-based ID
+        }
+      }
+      uint64_t todo = __ballot(valid);
+      while (todo) {
+        const int leader = __ffsll((unsigned long long)todo) - 1;
+        const uint32_t dd = (uint32_t)__shfl((int)d, leader);
+        const uint64_t m = __ballot(valid && d == dd);
+        unsigned long long at = 0;
+        if (lane == leader) at = atomicAdd(&s_cnt[dd], (unsigned long long)__popcll(m));
+        if (PASS == 1) {
+          at = __shfl(at, leader);
+          if (valid && d == dd) {
+            const uint64_t k = at + lane_prefix(m);
+            if (KIND == OWN_BUCKET) reinterpret_cast<ulonglong2*>(p.out)[k] = x16;
+            else reinterpret_cast<uint3*>(p.out)[k] = x12;
+          }
+        }
+        todo &= ~m;
+      }
+    }
+  }
+  if (PASS == 0) {
+    __syncthreads();
+    if (threadIdx.x < p.nranks) p.blk[(uint64_t)blockIdx.x * p.nranks + threadIdx.x] = s_cnt[threadIdx.x];
+  }
+}
+
+// Per-(block, destination) counts -> send offsets, destination-major:
+// off[b][d] = sum_{d' < d} total[d'] + sum_{b' < b} cnt[b'][d].  One block;
+// totals[d] out for the host (the all-to-all split sizes).
+__global__ __launch_bounds__(1024) void k_part_scan(unsigned long long* blk, uint32_t nblk, uint32_t nranks,
+                                                    unsigned long long* totals) {
+  __shared__ unsigned long long s_part[1024];
+  __shared__ unsigned long long s_base;
+  if (threadIdx.x == 0) s_base = 0;
+  __syncthreads();
+  for (uint32_t d = 0; d < nranks; ++d) {
+    const unsigned long long before = s_base;
+    for (uint32_t b0 = 0; b0 < nblk; b0 += 1024) {
+      const uint32_t b = b0 + threadIdx.x;
+      const unsigned long long v = b < nblk ? blk[(uint64_t)b * nranks + d] : 0;
+      s_part[threadIdx.x] = v;
+      __syncthreads();
+      for (uint32_t o = 1; o < 1024; o <<= 1) {  // inclusive Hillis-Steele scan
+        const unsigned long long t = threadIdx.x >= o ? s_part[threadIdx.x - o] : 0;
+        __syncthreads();
+        s_part[threadIdx.x] += t;
+        __syncthreads();
+      }
+      if (b < nblk) blk[(uint64_t)b * nranks + d] = s_base + s_part[threadIdx.x] - v;
+      __syncthreads();
+      if (threadIdx.x == 1023) s_base += s_part[1023];
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) totals[d] = s_base - before;
+    __syncthreads();
+  }
+}
+
+// Region counts that tile a flat array of n records (probe input in exchange mode).
+__global__ __launch_bounds__(kBlock) void k_flat_counts(unsigned long long* cnt, uint64_t nreg, uint64_t cap,
+                                                        uint64_t n) {
+  const uint64_t r = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (r >= nreg) return;
+  const uint64_t lo = r * cap;
+  cnt[r] = lo >= n ? 0 : (n - lo < cap ? n - lo : cap);
+}
+
 __global__ __launch_bounds__(kBlock) void k_super_finalize(const unsigned long long* __restrict__ key,
                                                           uint64_t n, uint32_t* __restrict__ super,
                                                           unsigned int* __restrict__ any) {
@@ -801,8 +969,8 @@ __global__ __launch_bounds__(kBlock) void k_lookup_key(IndexParams p, const uint
   __syncthreads();
   const uint64_t mask = (1ULL << p.nb_log2) - 1;
   const uint32_t fp = (uint32_t)(qv >> p.nb_log2) & kFpMask;
-  uint64_t b = qv & mask;
-  for (uint64_t probe = 0; probe <= mask; ++probe) {
+  uint64_t b = (qv & mask) - p.cell_lo;  // unsharded index only: cell_lo = 0
+  for (uint64_t probe = 0; probe < p.cell_n; ++probe) {
     const uint64_t last = p.cells[b * kCell + kCell - 1];
     if (threadIdx.x < (unsigned)kCell) {
       const uint64_t en = p.cells[b * kCell + threadIdx.x];
@@ -837,7 +1005,7 @@ __global__ __launch_bounds__(kBlock) void k_lookup_key(IndexParams p, const uint
       }
     }
     if (last == kEmpty || !(last & kChain)) break;
-    b = (b + 1) & mask;
+    b = next_cell(b, p.cell_n);
   }
 }
 
@@ -860,10 +1028,12 @@ struct mg_ctx {
   uint32_t l = 0, h = 0, m = 0, w = 0;
   uint32_t nb_log2 = 0, nb_log2_opt = 0;
   bool index_ready = false;
-  uint64_t* d_cells = nullptr;  // cells of kCell entries
+  uint64_t* d_cells = nullptr;  // cells of kCell entries (this rank's bucket range)
   size_t cells_cap = 0;
+  uint64_t cell_lo = 0, cell_n = 0;  // local bucket range [cell_lo, cell_lo + cell_n)
   // containment
   unsigned long long* d_superkey = nullptr;
+  unsigned long long* superkey = nullptr;  // the containment key array in use (d_superkey or caller-owned)
   uint32_t* d_super = nullptr;
   unsigned int* d_any = nullptr;
   size_t super_cap = 0;
@@ -894,6 +1064,15 @@ struct mg_ctx {
   std::vector<unsigned long long> run_cnt_host;
   uint32_t* d_compact = nullptr;
   size_t compact_cap = 0;
+  // exchange mode (one process per GPU)
+  ulonglong2* d_keyrec = nullptr;   // key records of this rank's source reads
+  size_t keyrec_cap = 0;
+  uint64_t n_keyrec = 0;
+  unsigned long long* d_blk = nullptr;   // routing: per-(block, rank) counts / offsets + totals
+  size_t blk_cap = 0;
+  int packable = -1;                     // MG_KEYS / MG_RUNS / MG_ROWS: what mg_pack copies out
+  unsigned long long* d_flat_cnt = nullptr;
+  size_t flat_cnt_cap = 0;
   // timing
   hipEvent_t ev[8] = {};
   mg_timings t{};
@@ -973,6 +1152,8 @@ IndexParams index_params(mg_ctx* ctx) {
   p.nb_log2 = ctx->nb_log2;
   p.rank = ctx->rank;
   p.nranks = ctx->nranks;
+  p.cell_lo = ctx->cell_lo;
+  p.cell_n = ctx->cell_n;
   p.cells = ctx->d_cells;
   return p;
 }
@@ -1002,30 +1183,38 @@ uint32_t resident_blocks(mg_ctx* ctx, K kernel, size_t lds, uint64_t want) {
   return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(std::min<uint64_t>(want, resident), ctx->max_blocks));
 }
 
+// Geometry of one discovery pass over source reads [a_lo, a_hi): probe grid =
+// its resident blocks; the scan (fewer registers) runs kreg times as many
+// wavefronts and probe wavefront r consumes scan regions r + i * (probe waves).
+struct DiscGeom {
+  uint32_t grid = 0, sgrid = 0, kreg = 1;
+  size_t lds_scan = 0, lds_probe = 0;
+};
+
 template <int W>
-struct LaunchDiscover {
-  // scan + probe; `contain` selects markContainedReads semantics
-  static int run(mg_ctx* ctx, bool contain) {
-    const uint64_t a_lo = contain ? 0 : ctx->read_lo;
-    const uint64_t a_hi = contain ? ctx->n : (ctx->read_hi ? std::min<uint64_t>(ctx->read_hi, ctx->n) : ctx->n);
-    ctx->nreg = 0;
-    ctx->nrun_reg = 0;
-    if (a_hi <= a_lo) return 0;
-    const uint64_t ngroups = (a_hi - a_lo + kWave - 1) / kWave;
-    const uint64_t want = (ngroups + kWavesPerBlock - 1) / kWavesPerBlock;
-    const size_t lds_scan = (size_t)kWavesPerBlock * (((ctx->w * kWave + 1) / 2) + kScanBuf) * sizeof(uint64_t);
-    const size_t lds_probe = (size_t)kWavesPerBlock * ProbeLds<W>::bytes;
-    // probe grid = its resident blocks; the scan (fewer registers) runs k
-    // times as many wavefronts and probe wavefront r consumes k scan regions
-    const uint32_t grid = contain ? resident_blocks(ctx, k_probe<W, true>, lds_probe, want)
-                                  : resident_blocks(ctx, k_probe<W, false>, lds_probe, want);
-    const uint32_t scan_res = resident_blocks(ctx, k_scan<W>, lds_scan, ~0ull >> 1);
-    const uint32_t kreg = (uint32_t)std::max<uint64_t>(
-        1, std::min<uint64_t>(scan_res / grid, (want + grid - 1) / grid));
-    const uint32_t sgrid = grid * kreg;
+DiscGeom disc_geom(mg_ctx* ctx, bool contain, uint64_t nsrc) {
+  DiscGeom g;
+  const uint64_t ngroups = (nsrc + kWave - 1) / kWave;
+  const uint64_t want = std::max<uint64_t>(1, (ngroups + kWavesPerBlock - 1) / kWavesPerBlock);
+  g.lds_scan = (size_t)kWavesPerBlock * (((ctx->w * kWave + 1) / 2) + kScanBuf) * sizeof(uint64_t);
+  g.lds_probe = (size_t)kWavesPerBlock * ProbeLds<W>::bytes;
+  g.grid = contain ? resident_blocks(ctx, k_probe<W, true>, g.lds_probe, want)
+                   : resident_blocks(ctx, k_probe<W, false>, g.lds_probe, want);
+  const uint32_t scan_res = resident_blocks(ctx, k_scan<W>, g.lds_scan, ~0ull >> 1);
+  g.kreg = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(scan_res / g.grid, (want + g.grid - 1) / g.grid));
+  g.sgrid = g.grid * g.kreg;
+  return g;
+}
+
+// k_scan over source reads [a_lo, a_hi) into ctx->d_runs (one region per scan
+// wavefront).  filter: keep only runs whose bucket this rank owns (replicated
+// scan of SURVEY §8(e)); exchange mode scans its own sources unfiltered.
+template <int W>
+struct LaunchScan {
+  static int run(mg_ctx* ctx, bool contain, uint64_t a_lo, uint64_t a_hi, uint32_t sgrid, bool filter) {
     const uint64_t nw = (uint64_t)sgrid * kWavesPerBlock;  // scan wavefronts = run regions
-    ctx->nreg = (uint64_t)grid * kWavesPerBlock;           // probe wavefronts = row regions
     ctx->nrun_reg = nw;
+    const uint64_t ngroups = (a_hi - a_lo + kWave - 1) / kWave;
     // run regions: expected runs per read ~ 2 J / (w + 1) + 1 (minimizer density)
     const uint64_t J = ctx->maxlen > ctx->h + 1 ? ctx->maxlen - ctx->h - 1 : 1;
     const uint64_t per_read = std::min<uint64_t>(J, 3 * (2 * J / (ctx->w + 1) + 2));
@@ -1055,14 +1244,27 @@ struct LaunchDiscover {
     sp.m = (int)ctx->m;
     sp.w = (int)ctx->w;
     sp.nb_log2 = ctx->nb_log2;
-    sp.rank = contain ? 0 : ctx->rank;
-    sp.nranks = contain ? 1 : ctx->nranks;
+    sp.rank = filter ? ctx->rank : 0;
+    sp.nranks = filter ? ctx->nranks : 1;
     sp.runs = ctx->d_runs;
     sp.run_cnt = ctx->d_run_cnt;
     sp.run_cap = run_cap;
+    const size_t lds = (size_t)kWavesPerBlock * (((ctx->w * kWave + 1) / 2) + kScanBuf) * sizeof(uint64_t);
+    allow_lds(k_scan<W>, lds);
     (void)hipEventRecord(ctx->ev[6], ctx->stream);
-    hipLaunchKernelGGL((k_scan<W>), dim3(sgrid), dim3(kBlock), lds_scan, ctx->stream, sp);
+    hipLaunchKernelGGL((k_scan<W>), dim3(sgrid), dim3(kBlock), lds, ctx->stream, sp);
     (void)hipEventRecord(ctx->ev[7], ctx->stream);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+  }
+};
+
+// k_probe over run regions (runs + r * run_cap, run_cnt[r] records), rows into
+// ctx->d_rows (one region per probe wavefront) or superkey updates (contain).
+template <int W>
+struct LaunchProbe {
+  static int run(mg_ctx* ctx, bool contain, const ulonglong2* runs, const unsigned long long* run_cnt,
+                 uint64_t run_cap, uint32_t kreg, uint32_t grid) {
+    ctx->nreg = (uint64_t)grid * kWavesPerBlock;  // probe wavefronts = row regions
     ProbeParams pp{};
     pp.words = ctx->d_words;
     pp.len = ctx->d_len;
@@ -1071,11 +1273,13 @@ struct LaunchDiscover {
     pp.nb_log2 = ctx->nb_log2;
     pp.rank = ctx->rank;
     pp.nranks = ctx->nranks;
+    pp.cell_lo = ctx->cell_lo;
+    pp.cell_n = ctx->cell_n;
     pp.cells = ctx->d_cells;
     pp.super = (!contain && ctx->contained_done && ctx->super_any) ? ctx->d_super : nullptr;
-    pp.superkey = ctx->d_superkey;
-    pp.runs = ctx->d_runs;
-    pp.run_cnt = ctx->d_run_cnt;
+    pp.superkey = ctx->superkey;
+    pp.runs = runs;
+    pp.run_cnt = run_cnt;
     pp.run_cap = run_cap;
     pp.run_regions_per_wave = kreg;
     pp.rows = ctx->d_rows;
@@ -1084,11 +1288,28 @@ struct LaunchDiscover {
     pp.uniform_len = ctx->minlen == ctx->maxlen ? (int)ctx->maxlen : 0;
     pp.stats = contain ? nullptr : (ctx->stats ? ctx->d_stats : nullptr);
     pp.phase_limit = contain ? 99 : ctx->phase_limit;
+    const size_t lds = (size_t)kWavesPerBlock * ProbeLds<W>::bytes;
     if (contain)
-      hipLaunchKernelGGL((k_probe<W, true>), dim3(grid), dim3(kBlock), lds_probe, ctx->stream, pp);
+      hipLaunchKernelGGL((k_probe<W, true>), dim3(grid), dim3(kBlock), lds, ctx->stream, pp);
     else
-      hipLaunchKernelGGL((k_probe<W, false>), dim3(grid), dim3(kBlock), lds_probe, ctx->stream, pp);
+      hipLaunchKernelGGL((k_probe<W, false>), dim3(grid), dim3(kBlock), lds, ctx->stream, pp);
     return hipGetLastError() == hipSuccess ? 0 : -1;
+  }
+};
+
+template <int W>
+struct LaunchDiscover {
+  // fused scan + probe over the context's source range; `contain` selects
+  // markContainedReads semantics
+  static int run(mg_ctx* ctx, bool contain) {
+    const uint64_t a_lo = contain ? 0 : ctx->read_lo;
+    const uint64_t a_hi = contain ? ctx->n : (ctx->read_hi ? std::min<uint64_t>(ctx->read_hi, ctx->n) : ctx->n);
+    ctx->nreg = 0;
+    ctx->nrun_reg = 0;
+    if (a_hi <= a_lo) return 0;
+    const DiscGeom g = disc_geom<W>(ctx, contain, a_hi - a_lo);
+    if (LaunchScan<W>::run(ctx, contain, a_lo, a_hi, g.sgrid, !contain)) return -1;
+    return LaunchProbe<W>::run(ctx, contain, ctx->d_runs, ctx->d_run_cnt, ctx->run_cap, g.kreg, g.grid);
   }
 };
 
@@ -1111,50 +1332,38 @@ float elapsed(hipEvent_t a, hipEvent_t b) {
 }  // namespace
 
 namespace {
-// Launch scan + probe, then check both region kinds for overflow; on overflow
-// the exact need is known (the kernels keep counting), so resize and rerun.
+// Read back the scan's per-region run counts; on overflow size the regions
+// for the exact need (the scan keeps counting past capacity) and report "again".
+int settle_runs(mg_ctx* ctx, bool* again) {
+  *again = false;
+  if (ctx->run_cnt_host.size() < ctx->nrun_reg) ctx->run_cnt_host.resize(ctx->nrun_reg);
+  if (ctx->nrun_reg)
+    MG_TRY(hipMemcpyAsync(ctx->run_cnt_host.data(), ctx->d_run_cnt, ctx->nrun_reg * sizeof(unsigned long long),
+                          hipMemcpyDeviceToHost, ctx->stream));
+  MG_TRY(hipStreamSynchronize(ctx->stream));
+  uint64_t run_max = 0;
+  for (uint64_t r = 0; r < ctx->nrun_reg; ++r) run_max = std::max<uint64_t>(run_max, ctx->run_cnt_host[r]);
+  if (run_max > ctx->run_cap) {
+    ctx->run_cap_need = run_max + run_max / 8 + 64;
+    *again = true;
+  }
+  return 0;
+}
+
+int settle_rows(mg_ctx* ctx, bool* again);
+
+// Fused scan + probe, then check both region kinds for overflow; on overflow
+// the exact need is known, so resize and rerun.
 int run_discover(mg_ctx* ctx, bool contain) {
   for (int attempt = 0; attempt < 3; ++attempt) {
     if (dispatch_w<LaunchDiscover>(ctx->maxw, ctx, contain)) {
       ctx->err = "discovery launch failed";
       return -1;
     }
-    if (ctx->run_cnt_host.size() < ctx->nrun_reg) ctx->run_cnt_host.resize(ctx->nrun_reg);
-    if (ctx->seg_host.size() < ctx->nreg) ctx->seg_host.resize(ctx->nreg);
-    if (ctx->nreg) {
-      MG_TRY(hipMemcpyAsync(ctx->run_cnt_host.data(), ctx->d_run_cnt, ctx->nrun_reg * sizeof(unsigned long long),
-                            hipMemcpyDeviceToHost, ctx->stream));
-      if (!contain)
-        MG_TRY(hipMemcpyAsync(ctx->seg_host.data(), ctx->d_seg, ctx->nreg * sizeof(unsigned long long),
-                              hipMemcpyDeviceToHost, ctx->stream));
-    }
-    MG_TRY(hipStreamSynchronize(ctx->stream));
-    uint64_t run_max = 0, row_max = 0, rows = 0;
-    for (uint64_t r = 0; r < ctx->nrun_reg; ++r) run_max = std::max<uint64_t>(run_max, ctx->run_cnt_host[r]);
-    for (uint64_t r = 0; r < ctx->nreg; ++r) {
-      if (!contain) {
-        row_max = std::max<uint64_t>(row_max, ctx->seg_host[r]);
-        rows += ctx->seg_host[r];
-      }
-    }
-    const uint64_t reg_cap = ctx->nreg ? ctx->rows_cap / ctx->nreg : 0;
     bool again = false;
-    if (run_max > ctx->run_cap) {
-      ctx->run_cap_need = run_max + run_max / 8 + 64;
-      again = true;
-    }
-    if (!contain && row_max > reg_cap && !again) {
-      const uint64_t want = (row_max + row_max / 4 + 1024) * ctx->nreg;
-      if (ctx->d_rows) (void)hipFree(ctx->d_rows);
-      ctx->d_rows = nullptr;
-      MG_TRY(hipMalloc(&ctx->d_rows, want * 3 * sizeof(uint32_t)));
-      ctx->rows_cap = want;
-      again = true;
-    }
-    if (!again) {
-      if (!contain) ctx->n_rows = rows;
-      return 0;
-    }
+    if (settle_runs(ctx, &again)) return -1;
+    if (!contain && !again && settle_rows(ctx, &again)) return -1;
+    if (!again) return 0;
   }
   ctx->err = "discovery buffers overflow after resize";
   return -1;
@@ -1200,7 +1409,7 @@ void mg_destroy(mg_ctx* ctx) {
   (void)hipStreamSynchronize(ctx->stream);
   void* bufs[] = {ctx->d_words, ctx->d_len, ctx->d_cells,
                   ctx->d_superkey, ctx->d_super, ctx->d_any, ctx->d_rows, ctx->d_seg, ctx->d_stats,
-                  ctx->d_compact, ctx->d_runs, ctx->d_run_cnt};
+                  ctx->d_compact, ctx->d_runs, ctx->d_run_cnt, ctx->d_keyrec, ctx->d_blk, ctx->d_flat_cnt};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   for (auto& e : ctx->ev)
@@ -1358,8 +1567,13 @@ int mg_set_shard(mg_ctx* ctx, uint32_t rank, uint32_t nranks, uint64_t read_lo, 
   return 0;
 }
 
-int mg_build_index(mg_ctx* ctx, uint32_t min_overlap, uint32_t seed_k) {
-  if (!ctx) return -1;
+}  // extern "C"
+
+namespace {
+// Index geometry shared by the fused and the exchange paths: h, m, w, the
+// directory size 2^nb (same on every rank: it depends on the global read
+// count only) and this rank's bucket range; allocates and clears the local cells.
+int setup_index(mg_ctx* ctx, uint32_t min_overlap, uint32_t seed_k) {
   MG_TRY(hipSetDevice(ctx->device));
   if (min_overlap < 2) return set_err(ctx, "min_overlap must be >= 2");
   const uint32_t h = min_overlap - 1;  // HashTable.cpp:54
@@ -1381,17 +1595,193 @@ int mg_build_index(mg_ctx* ctx, uint32_t min_overlap, uint32_t seed_k) {
     while (nbl < 31 && (1ull << nbl) < ctx->n) nbl++;
   while (nbl < 31 && (1ull << nbl) * kCell < 5 * std::max<uint64_t>(ctx->n, 1)) nbl++;
   ctx->nb_log2 = nbl;
-  const uint64_t nc = 1ull << nbl;
-  MG_TRY(ensure(&ctx->d_cells, &ctx->cells_cap, nc * kCell));
+  // rank r owns buckets b with floor(b P / 2^nb) == r, i.e. [ceil(r 2^nb / P), ceil((r+1) 2^nb / P))
+  const uint64_t NB = 1ull << nbl, P = ctx->nranks, r = ctx->rank;
+  ctx->cell_lo = (r * NB + P - 1) / P;
+  ctx->cell_n = ((r + 1) * NB + P - 1) / P - ctx->cell_lo;
+  MG_TRY(ensure(&ctx->d_cells, &ctx->cells_cap, ctx->cell_n * kCell));
+  MG_TRY(hipMemsetAsync(ctx->d_cells, 0xFF, ctx->cell_n * kCell * sizeof(uint64_t), ctx->stream));  // kEmpty
+  ctx->index_ready = false;
+  ctx->contained_done = false;
+  ctx->super_any = false;
+  return 0;
+}
+
+// this rank's source reads in exchange mode: [floor(r N / P), floor((r+1) N / P))
+void source_range(const mg_ctx* ctx, uint64_t* lo, uint64_t* hi) {
+  *lo = ctx->n * ctx->rank / ctx->nranks;
+  *hi = ctx->n * (ctx->rank + 1) / ctx->nranks;
+}
+
+// Routing pass over 16-B or 12-B records (k_part): counts per destination
+// into counts[] (host) and send offsets per (block, destination) on the device,
+// which the following route_scatter over the same records consumes.
+uint32_t part_grid(uint64_t nreg) { return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(nreg, 8192)); }
+
+template <int KIND>
+PartParams part_params(mg_ctx* ctx, const void* base, uint64_t cap, const unsigned long long* cnt, uint64_t nreg,
+                       uint64_t flat_n) {
+  PartParams pp{};
+  pp.base = base;
+  pp.cap = cap;
+  pp.cnt = cnt;
+  pp.nreg = nreg;
+  pp.flat_n = flat_n;
+  pp.nranks = ctx->nranks;
+  pp.nb_log2 = ctx->nb_log2;
+  pp.n_reads = ctx->n;
+  pp.blk = ctx->d_blk;
+  return pp;
+}
+
+template <int KIND>
+int route_count(mg_ctx* ctx, const void* base, uint64_t cap, const unsigned long long* cnt, uint64_t nreg,
+                uint64_t flat_n, uint64_t* counts) {
+  if (ctx->nranks > (uint32_t)kMaxRanks) return set_err(ctx, "at most 64 ranks");
+  const uint32_t grid = part_grid(nreg);
+  MG_TRY(ensure(&ctx->d_blk, &ctx->blk_cap, (size_t)grid * ctx->nranks + kMaxRanks));
+  unsigned long long* totals = ctx->d_blk + (size_t)grid * ctx->nranks;
+  PartParams pp = part_params<KIND>(ctx, base, cap, cnt, nreg, flat_n);
+  hipLaunchKernelGGL((k_part<KIND, 0>), dim3(grid), dim3(kBlock), 0, ctx->stream, pp);
+  MG_TRY(hipGetLastError());
+  hipLaunchKernelGGL(k_part_scan, dim3(1), dim3(1024), 0, ctx->stream, ctx->d_blk, grid, ctx->nranks, totals);
+  MG_TRY(hipGetLastError());
+  std::vector<unsigned long long> c(ctx->nranks);
+  MG_TRY(hipMemcpyAsync(c.data(), totals, ctx->nranks * sizeof(unsigned long long), hipMemcpyDeviceToHost,
+                        ctx->stream));
+  MG_TRY(hipStreamSynchronize(ctx->stream));
+  for (uint32_t i = 0; i < ctx->nranks; ++i) counts[i] = c[i];
+  return 0;
+}
+
+template <int KIND>
+int route_scatter(mg_ctx* ctx, const void* base, uint64_t cap, const unsigned long long* cnt, uint64_t nreg,
+                  uint64_t flat_n, void* out) {
+  PartParams pp = part_params<KIND>(ctx, base, cap, cnt, nreg, flat_n);
+  pp.out = out;
+  hipLaunchKernelGGL((k_part<KIND, 1>), dim3(part_grid(nreg)), dim3(kBlock), 0, ctx->stream, pp);
+  MG_TRY(hipGetLastError());
+  MG_TRY(hipStreamSynchronize(ctx->stream));
+  return 0;
+}
+
+constexpr uint64_t kFlatRegion = 4096;  // records per routing region of a flat array
+
+template <int W>
+struct LaunchKeyRecords {
+  static int run(mg_ctx* ctx, uint64_t a_lo, uint64_t a_hi) {
+    IndexParams p = index_params(ctx);
+    const uint64_t nk = 4 * (a_hi - a_lo);
+    if (!nk) return 0;
+    const size_t lds = (size_t)(W + 1) * kBlock * sizeof(uint64_t);
+    allow_lds(k_key_records<W>, lds);
+    hipLaunchKernelGGL((k_key_records<W>), dim3((uint32_t)((nk + kBlock - 1) / kBlock)), dim3(kBlock), lds,
+                       ctx->stream, p, a_lo, a_hi, ctx->d_keyrec);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+  }
+};
+
+// exchange-mode probe over a flat array of n received run records
+template <int W>
+struct LaunchProbeFlat {
+  static int run(mg_ctx* ctx, bool contain, const ulonglong2* runs, uint64_t n) {
+    const uint64_t approx_src = std::max<uint64_t>(1, n / 8);  // grid sizing only
+    DiscGeom g = disc_geom<W>(ctx, contain, approx_src);
+    const uint64_t nw = (uint64_t)g.grid * kWavesPerBlock;
+    const uint64_t cap = std::max<uint64_t>(1, (n + nw - 1) / nw);
+    if (ctx->flat_cnt_cap < nw) {
+      if (ctx->d_flat_cnt) (void)hipFree(ctx->d_flat_cnt);
+      ctx->d_flat_cnt = nullptr;
+      if (hipMalloc(&ctx->d_flat_cnt, nw * sizeof(unsigned long long)) != hipSuccess) return -1;
+      ctx->flat_cnt_cap = nw;
+    }
+    hipLaunchKernelGGL(k_flat_counts, dim3((uint32_t)((nw + kBlock - 1) / kBlock)), dim3(kBlock), 0, ctx->stream,
+                       ctx->d_flat_cnt, nw, cap, n);
+    if (hipGetLastError() != hipSuccess) return -1;
+    (void)hipEventRecord(ctx->ev[7], ctx->stream);
+    return LaunchProbe<W>::run(ctx, contain, runs, ctx->d_flat_cnt, cap, 1, g.grid);
+  }
+};
+
+int ensure_rows(mg_ctx* ctx, uint64_t nsrc) {
+  const uint64_t max_regions = (uint64_t)ctx->max_blocks * kWavesPerBlock;
+  if (ctx->seg_cap_regions < max_regions) {
+    if (ctx->d_seg) (void)hipFree(ctx->d_seg);
+    ctx->d_seg = nullptr;
+    MG_TRY(hipMalloc(&ctx->d_seg, max_regions * sizeof(unsigned long long)));
+    ctx->seg_cap_regions = max_regions;
+  }
+  const uint64_t want = ctx->rows_cap_opt ? ctx->rows_cap_opt : std::max<uint64_t>(1u << 20, 48 * nsrc);
+  if (want > ctx->rows_cap) {
+    if (ctx->d_rows) (void)hipFree(ctx->d_rows);
+    ctx->d_rows = nullptr;
+    MG_TRY(hipMalloc(&ctx->d_rows, want * 3 * sizeof(uint32_t)));
+    ctx->rows_cap = want;
+  }
+  if (ctx->stats) {
+    if (!ctx->d_stats) MG_TRY(hipMalloc(&ctx->d_stats, kSegs * 4 * sizeof(unsigned long long)));
+    MG_TRY(hipMemsetAsync(ctx->d_stats, 0, kSegs * 4 * sizeof(unsigned long long), ctx->stream));
+  }
+  return 0;
+}
+
+// read back the per-region row counts of the last probe; on overflow grow the
+// row buffer and report "again" (the kernels keep counting past capacity)
+int settle_rows(mg_ctx* ctx, bool* again) {
+  *again = false;
+  if (ctx->seg_host.size() < ctx->nreg) ctx->seg_host.resize(ctx->nreg);
+  if (ctx->nreg)
+    MG_TRY(hipMemcpyAsync(ctx->seg_host.data(), ctx->d_seg, ctx->nreg * sizeof(unsigned long long),
+                          hipMemcpyDeviceToHost, ctx->stream));
+  MG_TRY(hipStreamSynchronize(ctx->stream));
+  uint64_t row_max = 0, rows = 0;
+  for (uint64_t r = 0; r < ctx->nreg; ++r) {
+    row_max = std::max<uint64_t>(row_max, ctx->seg_host[r]);
+    rows += ctx->seg_host[r];
+  }
+  const uint64_t reg_cap = ctx->nreg ? ctx->rows_cap / ctx->nreg : 0;
+  if (row_max > reg_cap) {
+    const uint64_t want = (row_max + row_max / 4 + 1024) * ctx->nreg;
+    if (ctx->d_rows) (void)hipFree(ctx->d_rows);
+    ctx->d_rows = nullptr;
+    MG_TRY(hipMalloc(&ctx->d_rows, want * 3 * sizeof(uint32_t)));
+    ctx->rows_cap = want;
+    *again = true;
+    return 0;
+  }
+  ctx->n_rows = rows;
+  return 0;
+}
+
+void read_stats(mg_ctx* ctx, uint64_t nsrc) {
+  if (!ctx->stats) return;
+  std::vector<unsigned long long> st(kSegs * 4);
+  if (hipMemcpy(st.data(), ctx->d_stats, st.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost) !=
+      hipSuccess)
+    return;
+  uint64_t acc[4] = {0, 0, 0, 0};
+  for (int s2 = 0; s2 < kSegs; ++s2)
+    for (int i = 0; i < 4; ++i) acc[i] += st[s2 * 4 + i];
+  ctx->counters.runs = acc[0];
+  ctx->counters.entries = acc[1];
+  ctx->counters.verified = acc[2];
+  ctx->counters.rows = acc[3];
+  ctx->counters.sources = nsrc;
+}
+}  // namespace
+
+extern "C" {
+
+int mg_build_index(mg_ctx* ctx, uint32_t min_overlap, uint32_t seed_k) {
+  if (!ctx) return -1;
+  MG_TRY(hipSetDevice(ctx->device));
   MG_TRY(hipEventRecord(ctx->ev[0], ctx->stream));
-  MG_TRY(hipMemsetAsync(ctx->d_cells, 0xFF, nc * kCell * sizeof(uint64_t), ctx->stream));  // kEmpty
+  if (setup_index(ctx, min_overlap, seed_k)) return -1;
   if (dispatch_w<LaunchIndex>(ctx->maxw, ctx)) return set_err(ctx, "index build launch failed");
   MG_TRY(hipEventRecord(ctx->ev[1], ctx->stream));
   MG_TRY(hipEventSynchronize(ctx->ev[1]));
   ctx->t.index_ms = elapsed(ctx->ev[0], ctx->ev[1]);
   ctx->index_ready = true;
-  ctx->contained_done = false;
-  ctx->super_any = false;
   return 0;
 }
 
@@ -1409,6 +1799,7 @@ int mg_mark_contained(mg_ctx* ctx, uint32_t* super_out) {
       ctx->d_superkey = nullptr;
     }
     MG_TRY(ensure(&ctx->d_superkey, &skcap, ctx->n + 1));
+    ctx->superkey = ctx->d_superkey;
     MG_TRY(hipMemsetAsync(ctx->d_superkey, 0, (ctx->n + 1) * sizeof(unsigned long long), ctx->stream));
     MG_TRY(hipMemsetAsync(ctx->d_any, 0, sizeof(unsigned int), ctx->stream));
     MG_TRY(hipEventRecord(ctx->ev[2], ctx->stream));
@@ -1448,55 +1839,201 @@ int mg_find_overlaps(mg_ctx* ctx, uint64_t* n_rows) {
   MG_TRY(hipSetDevice(ctx->device));
   if (!ctx->index_ready) return set_err(ctx, "mg_build_index must run first");
   if (!ctx->contained_done && mg_mark_contained(ctx, nullptr)) return -1;
-  const uint64_t max_regions = (uint64_t)ctx->max_blocks * kWavesPerBlock;
-  if (ctx->seg_cap_regions < max_regions) {
-    if (ctx->d_seg) (void)hipFree(ctx->d_seg);
-    ctx->d_seg = nullptr;
-    MG_TRY(hipMalloc(&ctx->d_seg, max_regions * sizeof(unsigned long long)));
-    ctx->seg_cap_regions = max_regions;
-  }
   const uint64_t nsrc = (ctx->read_hi ? std::min(ctx->read_hi, ctx->n) : ctx->n) -
                         std::min(ctx->read_lo, ctx->n);
-  const uint64_t want = ctx->rows_cap_opt ? ctx->rows_cap_opt : std::max<uint64_t>(1u << 20, 48 * nsrc);
-  if (want > ctx->rows_cap) {
-    if (ctx->d_rows) (void)hipFree(ctx->d_rows);
-    ctx->d_rows = nullptr;
-    MG_TRY(hipMalloc(&ctx->d_rows, want * 3 * sizeof(uint32_t)));
-    ctx->rows_cap = want;
-  }
-  if (ctx->stats) {
-    if (!ctx->d_stats) MG_TRY(hipMalloc(&ctx->d_stats, kSegs * 4 * sizeof(unsigned long long)));
-    MG_TRY(hipMemsetAsync(ctx->d_stats, 0, kSegs * 4 * sizeof(unsigned long long), ctx->stream));
-  }
+  if (ensure_rows(ctx, nsrc)) return -1;
   MG_TRY(hipEventRecord(ctx->ev[4], ctx->stream));
   if (run_discover(ctx, false)) return -1;
   MG_TRY(hipEventRecord(ctx->ev[5], ctx->stream));
   MG_TRY(hipEventSynchronize(ctx->ev[5]));
-  // timings of the last (successful) launch pair
+  // the scan's own events bracket the last launch pair (a resize retry included
+  // in ev[4]..ev[5] is not kernel time)
   ctx->t.scan_ms = elapsed(ctx->ev[6], ctx->ev[7]);
-  ctx->t.overlap_ms = ctx->t.scan_ms;
-  {
-    float probe = 0.f;
-    // ev[7] (after scan) .. ev[5] may include one resize retry; the kernels'
-    // own events bracket the last launch: use them for the split
-    probe = elapsed(ctx->ev[7], ctx->ev[5]);
-    ctx->t.probe_ms = probe;
-    ctx->t.overlap_ms = ctx->t.scan_ms + probe;
-  }
-  if (ctx->stats) {
-    std::vector<unsigned long long> st(kSegs * 4);
-    MG_TRY(hipMemcpy(st.data(), ctx->d_stats, st.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
-    uint64_t acc[4] = {0, 0, 0, 0};
-    for (int s2 = 0; s2 < kSegs; ++s2)
-      for (int i = 0; i < 4; ++i) acc[i] += st[s2 * 4 + i];
-    ctx->counters.runs = acc[0];
-    ctx->counters.entries = acc[1];
-    ctx->counters.verified = acc[2];
-    ctx->counters.rows = acc[3];
-    ctx->counters.sources = nsrc;
-  }
+  ctx->t.probe_ms = elapsed(ctx->ev[7], ctx->ev[5]);
+  ctx->t.overlap_ms = ctx->t.scan_ms + ctx->t.probe_ms;
+  read_stats(ctx, nsrc);
   ctx->t.total_ms = ctx->t.index_ms + ctx->t.contained_ms + ctx->t.overlap_ms;
+  ctx->packable = MG_ROWS;
   if (n_rows) *n_rows = ctx->n_rows;
+  return 0;
+}
+
+/* ---------------------------------------------------------- exchange mode --- */
+uint32_t mg_record_bytes(int what) { return what == MG_ROWS ? 12u : (what == MG_KEYS || what == MG_RUNS) ? 16u : 0u; }
+
+int mg_key_records(mg_ctx* ctx, uint32_t min_overlap, uint32_t seed_k, uint64_t* counts) {
+  if (!ctx || !counts) return -1;
+  MG_TRY(hipSetDevice(ctx->device));
+  MG_TRY(hipEventRecord(ctx->ev[0], ctx->stream));
+  if (setup_index(ctx, min_overlap, seed_k)) return -1;
+  uint64_t lo, hi;
+  source_range(ctx, &lo, &hi);
+  ctx->n_keyrec = 4 * (hi - lo);
+  MG_TRY(ensure(&ctx->d_keyrec, &ctx->keyrec_cap, ctx->n_keyrec));
+  if (dispatch_w<LaunchKeyRecords>(ctx->maxw, ctx, lo, hi)) return set_err(ctx, "key record launch failed");
+  if (route_count<OWN_BUCKET>(ctx, ctx->d_keyrec, kFlatRegion, nullptr, (ctx->n_keyrec + kFlatRegion - 1) / kFlatRegion,
+                              ctx->n_keyrec, counts))
+    return -1;
+  ctx->packable = MG_KEYS;
+  return 0;
+}
+
+int mg_insert_keys(mg_ctx* ctx, const void* recs, uint64_t n) {
+  if (!ctx) return -1;
+  MG_TRY(hipSetDevice(ctx->device));
+  if (!ctx->cell_n) return set_err(ctx, "mg_key_records must run first");
+  if (n) {
+    IndexParams p = index_params(ctx);
+    hipLaunchKernelGGL(k_insert_records, dim3((uint32_t)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, ctx->stream, p,
+                       reinterpret_cast<const ulonglong2*>(recs), n);
+    MG_TRY(hipGetLastError());
+  }
+  MG_TRY(hipEventRecord(ctx->ev[1], ctx->stream));
+  MG_TRY(hipEventSynchronize(ctx->ev[1]));
+  ctx->t.index_ms = elapsed(ctx->ev[0], ctx->ev[1]);
+  ctx->index_ready = true;
+  return 0;
+}
+
+int mg_scan_runs(mg_ctx* ctx, int contain, uint64_t* counts) {
+  if (!ctx || !counts) return -1;
+  MG_TRY(hipSetDevice(ctx->device));
+  if (!ctx->index_ready) return set_err(ctx, "mg_insert_keys must run first");
+  if (!contain && !ctx->contained_done) return set_err(ctx, "containment must be settled first (mg_finalize_contained)");
+  uint64_t lo, hi;
+  source_range(ctx, &lo, &hi);
+  ctx->nrun_reg = 0;
+  if (hi > lo) {
+    for (int attempt = 0;; ++attempt) {
+      if (attempt == 3) return set_err(ctx, "run buffers overflow after resize");
+      uint32_t sgrid = 0;
+      switch (ctx->maxw) {
+#define MG_G(W) case W: sgrid = disc_geom<W>(ctx, contain != 0, hi - lo).sgrid; break;
+        MG_G(1) MG_G(2) MG_G(3) MG_G(4) MG_G(5) MG_G(6) MG_G(8) MG_G(12) MG_G(16) MG_G(32)
+#undef MG_G
+      }
+      if (dispatch_w<LaunchScan>(ctx->maxw, ctx, contain != 0, lo, hi, sgrid, false))
+        return set_err(ctx, "scan launch failed");
+      bool again = false;
+      if (settle_runs(ctx, &again)) return -1;
+      if (!again) break;
+    }
+  }
+  ctx->t.scan_ms = ctx->nrun_reg ? elapsed(ctx->ev[6], ctx->ev[7]) : 0.f;
+  if (route_count<OWN_BUCKET>(ctx, ctx->d_runs, ctx->run_cap, ctx->d_run_cnt, ctx->nrun_reg, 0, counts)) return -1;
+  ctx->packable = MG_RUNS;
+  return 0;
+}
+
+int mg_probe_runs(mg_ctx* ctx, int contain, const void* runs, uint64_t n, uint64_t* counts) {
+  if (!ctx) return -1;
+  MG_TRY(hipSetDevice(ctx->device));
+  if (!ctx->index_ready) return set_err(ctx, "mg_insert_keys must run first");
+  if (contain && !ctx->superkey) return set_err(ctx, "mg_begin_contained must run first (lengths differ)");
+  if (!contain && !ctx->contained_done) return set_err(ctx, "containment must be settled first");
+  ctx->nreg = 0;
+  ctx->n_rows = 0;
+  if (!contain && ensure_rows(ctx, std::max<uint64_t>(1, n / 12))) return -1;  // ~4 rows per run
+  for (int attempt = 0;; ++attempt) {
+    if (attempt == 3) return set_err(ctx, "row buffers overflow after resize");
+    MG_TRY(hipEventRecord(ctx->ev[4], ctx->stream));
+    if (n && dispatch_w<LaunchProbeFlat>(ctx->maxw, ctx, contain != 0, reinterpret_cast<const ulonglong2*>(runs), n))
+      return set_err(ctx, "probe launch failed");
+    MG_TRY(hipEventRecord(ctx->ev[5], ctx->stream));
+    bool again = false;
+    if (!contain && settle_rows(ctx, &again)) return -1;
+    if (!again) break;
+  }
+  MG_TRY(hipEventSynchronize(ctx->ev[5]));
+  ctx->t.probe_ms = n ? elapsed(ctx->ev[7], ctx->ev[5]) : 0.f;
+  if (contain) return 0;
+  ctx->t.overlap_ms = ctx->t.scan_ms + ctx->t.probe_ms;
+  read_stats(ctx, 0);
+  if (counts) {
+    const uint64_t reg_cap = ctx->nreg ? ctx->rows_cap / ctx->nreg : 0;
+    if (route_count<OWN_SRC>(ctx, ctx->d_rows, reg_cap, ctx->d_seg, ctx->nreg, 0, counts)) return -1;
+  }
+  ctx->packable = MG_ROWS;
+  return 0;
+}
+
+int mg_pack(mg_ctx* ctx, int what, void* dst, uint64_t cap) {
+  if (!ctx) return -1;
+  MG_TRY(hipSetDevice(ctx->device));
+  if (what != ctx->packable) return set_err(ctx, "mg_pack: nothing of that kind to pack (call order)");
+  std::vector<uint64_t> counts(ctx->nranks);
+  uint64_t total = 0;
+  if (what == MG_KEYS) {
+    const uint64_t nreg = (ctx->n_keyrec + kFlatRegion - 1) / kFlatRegion;
+    if (route_count<OWN_BUCKET>(ctx, ctx->d_keyrec, kFlatRegion, nullptr, nreg, ctx->n_keyrec, counts.data())) return -1;
+    for (auto c : counts) total += c;
+    if (total > cap) return set_err(ctx, "mg_pack: destination too small");
+    return route_scatter<OWN_BUCKET>(ctx, ctx->d_keyrec, kFlatRegion, nullptr, nreg, ctx->n_keyrec, dst);
+  }
+  if (what == MG_RUNS) {
+    if (route_count<OWN_BUCKET>(ctx, ctx->d_runs, ctx->run_cap, ctx->d_run_cnt, ctx->nrun_reg, 0, counts.data()))
+      return -1;
+    for (auto c : counts) total += c;
+    if (total > cap) return set_err(ctx, "mg_pack: destination too small");
+    return route_scatter<OWN_BUCKET>(ctx, ctx->d_runs, ctx->run_cap, ctx->d_run_cnt, ctx->nrun_reg, 0, dst);
+  }
+  const uint64_t reg_cap = ctx->nreg ? ctx->rows_cap / ctx->nreg : 0;
+  if (route_count<OWN_SRC>(ctx, ctx->d_rows, reg_cap, ctx->d_seg, ctx->nreg, 0, counts.data())) return -1;
+  for (auto c : counts) total += c;
+  if (total > cap) return set_err(ctx, "mg_pack: destination too small");
+  return route_scatter<OWN_SRC>(ctx, ctx->d_rows, reg_cap, ctx->d_seg, ctx->nreg, 0, dst);
+}
+
+int mg_begin_contained(mg_ctx* ctx, void* superkey, int* needed) {
+  if (!ctx || !needed) return -1;
+  MG_TRY(hipSetDevice(ctx->device));
+  *needed = ctx->minlen != ctx->maxlen;  // OverlapGraph.cpp:228-233
+  ctx->contained_done = false;
+  ctx->superkey = nullptr;
+  if (*needed) {
+    if (superkey) {
+      ctx->superkey = reinterpret_cast<unsigned long long*>(superkey);
+    } else {
+      size_t skcap = 0;
+      if (ctx->d_superkey) (void)hipFree(ctx->d_superkey);
+      ctx->d_superkey = nullptr;
+      MG_TRY(ensure(&ctx->d_superkey, &skcap, ctx->n + 1));
+      ctx->superkey = ctx->d_superkey;
+    }
+    MG_TRY(hipMemsetAsync(ctx->superkey, 0, ctx->n * sizeof(unsigned long long), ctx->stream));
+    MG_TRY(hipStreamSynchronize(ctx->stream));
+  }
+  return 0;
+}
+
+int mg_finalize_contained(mg_ctx* ctx, uint32_t* super_out) {
+  if (!ctx) return -1;
+  MG_TRY(hipSetDevice(ctx->device));
+  MG_TRY(ensure(&ctx->d_super, &ctx->super_cap, ctx->n + 1));
+  if (!ctx->d_any) MG_TRY(hipMalloc(&ctx->d_any, sizeof(unsigned int)));
+  ctx->super_any = false;
+  if (ctx->minlen != ctx->maxlen && ctx->superkey) {
+    MG_TRY(hipMemsetAsync(ctx->d_any, 0, sizeof(unsigned int), ctx->stream));
+    if (ctx->n)
+      hipLaunchKernelGGL(k_super_finalize, dim3((uint32_t)((ctx->n + kBlock - 1) / kBlock)), dim3(kBlock), 0,
+                         ctx->stream, ctx->superkey, ctx->n, ctx->d_super, ctx->d_any);
+    MG_TRY(hipGetLastError());
+    unsigned int any = 0;
+    MG_TRY(hipMemcpyAsync(&any, ctx->d_any, sizeof(any), hipMemcpyDeviceToHost, ctx->stream));
+    MG_TRY(hipStreamSynchronize(ctx->stream));
+    ctx->super_any = any != 0;
+  } else {
+    MG_TRY(hipMemsetAsync(ctx->d_super, 0, (ctx->n + 1) * sizeof(uint32_t), ctx->stream));
+  }
+  ctx->contained_done = true;
+  ctx->superkey = nullptr;  // a caller-owned key array is not referenced past this call
+  if (super_out) {
+    super_out[0] = 0;
+    if (ctx->n)
+      MG_TRY(hipMemcpyAsync(super_out + 1, ctx->d_super, ctx->n * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                            ctx->stream));
+  }
+  MG_TRY(hipStreamSynchronize(ctx->stream));
   return 0;
 }
 

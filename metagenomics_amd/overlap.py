@@ -16,6 +16,10 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libmgovl.so")
 
+# exchange-mode record kinds (include/mg_overlap.h)
+MG_KEYS, MG_RUNS, MG_ROWS = 0, 1, 2
+RECORD_BYTES = {MG_KEYS: 16, MG_RUNS: 16, MG_ROWS: 12}
+
 EDGE_DTYPE = np.dtype([("src", "<u4"), ("dst", "<u4"), ("offset", "<u2"), ("orient", "u1"), ("flags", "u1")])
 
 
@@ -44,6 +48,14 @@ def lib() -> C.CDLL:
         return _lib
     if not os.path.exists(LIB_PATH):
         raise MgError(f"native library missing: {LIB_PATH} (run __graft_entry__.build())")
+    # One HIP runtime per process: torch bundles its own libamdhip64 (same
+    # SONAME, libamdhip64.so.7).  Loading torch first makes the library bind to
+    # that instance, so device buffers are shared with torch (the multi-GPU
+    # exchange buffers, sharded.py) instead of two runtimes fighting over the GPU.
+    try:
+        import torch  # noqa: F401
+    except Exception:
+        pass
     L = C.CDLL(LIB_PATH)
     u64, u32, i32, i64 = C.c_uint64, C.c_uint32, C.c_int, C.c_int64
     vp, P = C.c_void_p, C.POINTER
@@ -66,6 +78,14 @@ def lib() -> C.CDLL:
         "mg_get_counters": (i32, [vp, P(_Counters)]),
         "mg_set_option": (i32, [vp, C.c_char_p, i64]),
         "mg_stream": (vp, [vp]),
+        "mg_record_bytes": (u32, [i32]),
+        "mg_key_records": (i32, [vp, u32, u32, vp]),
+        "mg_insert_keys": (i32, [vp, vp, u64]),
+        "mg_scan_runs": (i32, [vp, i32, vp]),
+        "mg_probe_runs": (i32, [vp, i32, vp, u64, vp]),
+        "mg_pack": (i32, [vp, i32, vp, u64]),
+        "mg_begin_contained": (i32, [vp, vp, P(i32)]),
+        "mg_finalize_contained": (i32, [vp, vp]),
         "mgh_dataset_from_files": (i32, [P(C.c_char_p), i32, u64, P(vp)]),
         "mgh_dataset_from_codes": (i32, [vp, u64, u64, vp, u64, i32, P(vp)]),
         "mgh_dataset_free": (None, [vp]),
@@ -198,6 +218,7 @@ class OverlapEngine:
             raise MgError(f"mg_create({device}) failed: {rc}")
         self._h = h
         self.n_reads = 0
+        self.lengths_differ = False
 
     def close(self):
         if getattr(self, "_h", None):
@@ -222,6 +243,7 @@ class OverlapEngine:
         wpr = words.shape[1] if words.ndim == 2 else 1
         self._check(lib().mg_upload_reads_packed(self._h, _ptr(words), _ptr(lens), lens.shape[0], wpr), "upload")
         self.n_reads = int(lens.shape[0])
+        self.lengths_differ = bool(lens.shape[0]) and int(lens.min()) != int(lens.max())
 
     def upload_ascii(self, seqs: Sequence[str]):
         data = "".join(seqs).encode()
@@ -229,6 +251,7 @@ class OverlapEngine:
         off[1:] = np.cumsum([len(s) for s in seqs])
         self._check(lib().mg_upload_reads_ascii(self._h, data, _ptr(off), len(seqs)), "upload_ascii")
         self.n_reads = len(seqs)
+        self.lengths_differ = len({len(x) for x in seqs}) > 1
 
     def download_packed(self):
         wpr = C.c_uint32()
@@ -279,6 +302,45 @@ class OverlapEngine:
             if n.value <= cap:
                 return [(int(x & ((1 << 62) - 1)), int(x >> 62)) for x in buf[: n.value]]
             cap = int(n.value)
+
+    # --- exchange mode (one process per GPU; metagenomics_amd/sharded.py drives it)
+    def _counts(self, nranks: int) -> np.ndarray:
+        return np.zeros(max(1, nranks), dtype=np.uint64)
+
+    def key_records(self, min_overlap: int, seed_k: int, nranks: int) -> np.ndarray:
+        c = self._counts(nranks)
+        self._check(lib().mg_key_records(self._h, min_overlap, seed_k, _ptr(c)), "key_records")
+        return c
+
+    def insert_keys(self, dptr: int, n: int):
+        self._check(lib().mg_insert_keys(self._h, C.c_void_p(dptr), n), "insert_keys")
+
+    def scan_runs(self, contain: bool, nranks: int) -> np.ndarray:
+        c = self._counts(nranks)
+        self._check(lib().mg_scan_runs(self._h, int(contain), _ptr(c)), "scan_runs")
+        return c
+
+    def probe_runs(self, contain: bool, dptr: int, n: int, nranks: int) -> np.ndarray:
+        c = self._counts(nranks)
+        self._check(lib().mg_probe_runs(self._h, int(contain), C.c_void_p(dptr), n, _ptr(c)), "probe_runs")
+        return c
+
+    def pack(self, what: int, dptr: int, cap: int):
+        self._check(lib().mg_pack(self._h, what, C.c_void_p(dptr), cap), "pack")
+
+    def begin_contained(self, superkey_dptr: int | None) -> bool:
+        need = C.c_int()
+        self._check(lib().mg_begin_contained(self._h, C.c_void_p(superkey_dptr or 0), C.byref(need)),
+                    "begin_contained")
+        return bool(need.value)
+
+    def finalize_contained(self, copy: bool = False):
+        if not copy:
+            self._check(lib().mg_finalize_contained(self._h, None), "finalize_contained")
+            return None
+        sup = np.zeros(self.n_reads + 1, dtype=np.uint32)
+        self._check(lib().mg_finalize_contained(self._h, _ptr(sup)), "finalize_contained")
+        return sup
 
     def timings(self) -> dict:
         t = _Timings()

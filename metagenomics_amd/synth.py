@@ -45,6 +45,17 @@ def sample_reads(genome: np.ndarray, n_reads: int, lo: int, hi: int, seed: int,
     starts = rng.integers(0, G - lengths + 1)
     rc = rng.random(n_reads) < rc_fraction
     codes = np.zeros((n_reads, hi), dtype=np.uint8)
+    if lo == hi and G >= hi:
+        # fixed length: rows of a sliding-window view, reversed + complemented in
+        # place for the rc reads (same values as the general path below)
+        win = np.lib.stride_tricks.sliding_window_view(genome, hi)
+        for a in range(0, n_reads, chunk):
+            b = min(n_reads, a + chunk)
+            c = win[starts[a:b]]
+            m = rc[a:b]
+            c[m] = 3 - c[m][:, ::-1]
+            codes[a:b] = c
+        return codes, lengths.astype(np.uint16)
     k = np.arange(hi, dtype=np.int64)[None, :]
     for a in range(0, n_reads, chunk):
         b = min(n_reads, a + chunk)

@@ -199,3 +199,61 @@ def test_repeatable(engine):
     a, _ = gpu_rows(engine, ds, meta["l"])
     b, _ = gpu_rows(engine, ds, meta["l"])
     assert np.array_equal(rows_to_tuples(a), rows_to_tuples(b))
+
+
+# ---- exchange mode: P simulated ranks in this process, buffers
+# moved by LocalExchange on the device; the same sharded_step drives RCCL ranks
+def exchange_rows(ds, l, world, k=0, want_super=True):
+    import torch
+
+    from metagenomics_amd.sharded import LocalExchange, sharded_step, source_range
+
+    engines = []
+    for r in range(world):
+        e = OverlapEngine(0)
+        e.set_shard(r, world, 0, 0)
+        e.upload(ds)
+        engines.append(e)
+    res = sharded_step(engines, LocalExchange(world, torch.device("cuda:0")), l, k, want_super=want_super)
+    parts = []
+    for r in range(world):
+        rows = res.rows_numpy(r)
+        lo, hi = source_range(ds.num_unique, r, world)
+        assert np.all((rows["src"] >= lo + 1) & (rows["src"] <= hi)), "row at a rank that does not own its src"
+        parts.append(rows)
+    for e in engines:
+        e.close()
+    return np.concatenate(parts), res.super_read_id
+
+
+@pytest.mark.parametrize("name,world", [("small", 2), ("mixed", 3), ("tandem", 4), ("highdup", 2),
+                                        ("dirty", 3), ("tworead", 2), ("wrapped", 5)])
+def test_exchange_mode_matches_reference(name, world):
+    meta = load_meta(name)
+    ds = Dataset.from_files([fixture_input(name)], meta["l"])
+    rows, sup = exchange_rows(ds, meta["l"], world)
+    assert np.array_equal(rows_to_tuples(rows), golden_rows(name))
+    assert {str(i): int(s) for i, s in enumerate(sup) if s} == meta["super"]
+
+
+@pytest.mark.parametrize("case", RANDOM_CASES[:4])
+def test_exchange_mode_random_vs_oracle(case):
+    n, lo, hi, G, l, k, seed = case
+    c, L = synth.uniform_read_set(n, 0, G, seed=seed, lo=lo, hi=hi)
+    ds = Dataset.from_codes(c, L, l)
+    od = OracleDataset.from_strings(synth.codes_to_strings(c, L), l)
+    orows, osup, _, _ = od.overlaps(l)
+    rows, sup = exchange_rows(ds, l, 3, k=k)
+    assert np.array_equal(sup.astype(np.uint64), osup)
+    assert np.array_equal(rows_to_tuples(rows), sorted_tuples(orows))
+
+
+def test_exchange_mode_c2_scale_matches_fused(engine):
+    """1M x 150 bp (configs[1] shape): 4 exchange ranks == the fused single-GPU path."""
+    c, L = synth.uniform_read_set(1_000_000, 150, 7_500_000, seed=21)
+    ds = Dataset.from_codes(c, L, 50)
+    fused, _ = gpu_rows(engine, ds, 50, k=31)
+    rows, _ = exchange_rows(ds, 50, 4, k=31, want_super=False)
+    assert rows.shape[0] == fused.shape[0]
+    assert np.array_equal(rows_to_tuples(rows), rows_to_tuples(fused))
+    check_pairs(fused, ds.packed()[1])

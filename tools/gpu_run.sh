@@ -21,12 +21,20 @@ for s in $STEPS; do
   bench)
     timeout -k 10 600 python -u bench.py > $OUT/bench.json 2> $OUT/bench.err
     rc=$?; echo "bench rc=$rc"; cat $OUT/bench.json ;;
+  sim)
+    for P in 2 4 8; do
+      timeout -k 10 300 python -u bench.py --sim-world $P --steps 3 > $OUT/bench_sim$P.json 2> $OUT/bench_sim$P.err
+      rc=$?; echo "bench sim $P rc=$rc"; cat $OUT/bench_sim$P.json; [ $rc -ne 0 ] && break
+    done ;;
   benchc2)
     timeout -k 10 300 python -u bench.py --config c2 --no-cpu-baseline > $OUT/bench_c2.json 2> $OUT/bench_c2.err
     rc=$?; echo "bench c2 rc=$rc"; cat $OUT/bench_c2.json ;;
   prof)
     timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o kt -- python3 bench.py --steps 5 --no-cpu-baseline > $OUT/prof_bench.json 2> $OUT/prof_bench.err
     rc=$?; echo "prof rc=$rc"; cat $OUT/prof_bench.json ;;
+  profsim)
+    timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/profsim -o kt -- python3 bench.py --sim-world 4 --steps 2 --no-cpu-baseline > $OUT/profsim_bench.json 2> $OUT/profsim_bench.err
+    rc=$?; echo "profsim rc=$rc"; cat $OUT/profsim_bench.json; cat $OUT/profsim/kt_kernel_stats.csv ;;
   pmc)
     for set in "FETCH_SIZE" "WRITE_SIZE"; do
       timeout -s KILL 300 rocprofv3 --pmc $set --kernel-trace --output-format csv -d $OUT/pmc_$set -o p -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline > $OUT/pmc_$set.log 2>&1
