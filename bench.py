@@ -118,6 +118,8 @@ def main():
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--sim-world", type=int, default=0,
                     help="run all SIM-WORLD ranks of the exchange mode in this process on one GPU")
+    ap.add_argument("--exchange", action="store_true",
+                    help="use the RCCL exchange mode even with one rank (checks the torch.distributed plumbing)")
     ap.add_argument("--cpu-sample", type=int, default=150_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r01s2_pmc_c3.json"))
@@ -137,13 +139,16 @@ def main():
 
     dist = None
     xchg = None
-    if world > 1:
+    if world > 1 or args.exchange:
         import torch.distributed as dist
 
         from metagenomics_amd.sharded import TorchExchange
 
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))  # RCCL over xGMI
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29517")
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local), rank=rank,
+                                world_size=world)  # RCCL over xGMI
         xchg = TorchExchange(torch.device("cuda", local))
         mode = "exchange"
     elif args.sim_world > 1:
@@ -153,11 +158,11 @@ def main():
         mode = "exchange-sim"
     else:
         mode = "fused"
-    P = world if world > 1 else max(1, args.sim_world)
+    P = world if mode == "exchange" else max(1, args.sim_world)
 
     engines = []
     t0 = time.time()
-    for r in ([rank] if world > 1 else range(P)):
+    for r in ([rank] if mode == "exchange" else range(P)):
         e = OverlapEngine(local)
         e.set_option("nb_log2", args.nb_log2)
         e.set_shard(r, P, 0, 0)

@@ -21,6 +21,7 @@ process, for single-GPU parity tests. The step logic in :func:`sharded_step` is 
 """
 from __future__ import annotations
 
+import os
 import time
 from dataclasses import dataclass, field
 
@@ -54,16 +55,24 @@ class Exchange:
 
 
 class TorchExchange(Exchange):
-    """One rank per process over a torch.distributed group (nccl = RCCL on ROCm, or gloo)."""
+    """One rank per process over a torch.distributed group (nccl = RCCL on ROCm, or gloo).
 
-    def __init__(self, device=None):
+    Every all-to-all(v) call moves at most ``chunk_bytes`` in total per rank:
+    the torch-bundled RCCL (2.26.6, ROCm 7.0) corrupts ``all_to_all_single``
+    payloads above ~1 GiB per call (measured with one rank, every dtype:
+    tools/a2a_probe.py), so larger exchanges run in rounds of
+    per-peer slices."""
+
+    def __init__(self, device=None, chunk_bytes: int = 256 << 20):
         import torch
         import torch.distributed as dist
 
         self.torch, self.dist = torch, dist
         self.world = dist.get_world_size()
-        self.ranks = [dist.get_rank()]
+        self.rank = dist.get_rank()
+        self.ranks = [self.rank]
         self.device = device if device is not None else torch.device("cpu")
+        self.chunk_bytes = int(os.environ.get("MG_A2A_CHUNK_BYTES", chunk_bytes))
 
     def empty(self, nbytes: int):
         return self.torch.empty(max(1, int(nbytes)), dtype=self.torch.uint8, device=self.device)
@@ -75,22 +84,48 @@ class TorchExchange(Exchange):
     def all_to_all(self, sends, counts, rec_bytes):
         torch, dist = self.torch, self.dist
         (send,), (cnt,) = sends, counts
+        P, me, rb = self.world, self.rank, rec_bytes
+        # the full P x P count matrix: M[s, d] = records s -> d
         sc = torch.tensor([int(c) for c in cnt], dtype=torch.int64, device=self.device)
-        rc = torch.empty_like(sc)
-        dist.all_to_all_single(rc, sc)
-        rcl = [int(x) for x in rc.tolist()]
-        n_in = sum(rcl)
-        recv = self.empty(n_in * rec_bytes)
-        n_out = int(sum(int(c) for c in cnt))
-        dist.all_to_all_single(recv[: n_in * rec_bytes], send[: n_out * rec_bytes],
-                               output_split_sizes=[c * rec_bytes for c in rcl],
-                               input_split_sizes=[int(c) * rec_bytes for c in cnt])
+        mat = torch.empty(P * P, dtype=torch.int64, device=self.device)
+        dist.all_gather_into_tensor(mat, sc)
+        M = mat.view(P, P).cpu().numpy()
+        scnt, rcnt = M[me, :], M[:, me]
+        soff = np.concatenate([[0], np.cumsum(scnt)])
+        roff = np.concatenate([[0], np.cumsum(rcnt)])
+        n_in = int(rcnt.sum())
+        recv = self.empty(n_in * rb)
+        per_peer = max(1, self.chunk_bytes // (P * rb))  # records per peer per round
+        rounds = max(1, -(-int(M.max()) // per_peer))
+        if rounds == 1:
+            dist.all_to_all_single(recv[: n_in * rb], send[: int(soff[-1]) * rb],
+                                   output_split_sizes=[int(c) * rb for c in rcnt],
+                                   input_split_sizes=[int(c) * rb for c in scnt])
+        else:
+            for t in range(rounds):
+                lo = t * per_peer
+                s_sz = np.clip(scnt - lo, 0, per_peer)
+                r_sz = np.clip(rcnt - lo, 0, per_peer)
+                sbuf = torch.cat([send[int(soff[d] + lo) * rb: int(soff[d] + lo + s_sz[d]) * rb] for d in range(P)])
+                rbuf = self.empty(int(r_sz.sum()) * rb)
+                dist.all_to_all_single(rbuf[: int(r_sz.sum()) * rb], sbuf,
+                                       output_split_sizes=[int(c) * rb for c in r_sz],
+                                       input_split_sizes=[int(c) * rb for c in s_sz])
+                at = 0
+                for s_ in range(P):
+                    nbytes = int(r_sz[s_]) * rb
+                    if nbytes:
+                        dst = int(roff[s_] + lo) * rb
+                        recv[dst: dst + nbytes].copy_(rbuf[at: at + nbytes])
+                    at += nbytes
         self.sync()
         return [(recv, n_in)]
 
     def allreduce_max(self, bufs):
         (b,) = bufs
-        self.dist.all_reduce(b, op=self.dist.ReduceOp.MAX)
+        step = max(1, self.chunk_bytes // b.element_size())
+        for i in range(0, b.numel(), step):
+            self.dist.all_reduce(b[i: i + step], op=self.dist.ReduceOp.MAX)
         self.sync()
 
     def barrier(self):

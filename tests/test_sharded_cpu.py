@@ -25,8 +25,10 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, name, outdir):
+def _worker(rank, world, port, name, outdir, chunk):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    if chunk:
+        os.environ["MG_A2A_CHUNK_BYTES"] = str(chunk)  # force the multi-round exchange
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import torch.distributed as dist
@@ -51,11 +53,12 @@ def _worker(rank, world, port, name, outdir):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("name,world", [("small", 2), ("tandem", 3), ("mixed", 2)])
-def test_exchange_routes_every_record(tmp_path, name, world):
+@pytest.mark.parametrize("name,world,chunk", [("small", 2, 0), ("tandem", 3, 0), ("mixed", 2, 0),
+                                              ("small", 2, 4096), ("tandem", 3, 8192)])
+def test_exchange_routes_every_record(tmp_path, name, world, chunk):
     from mock_engine import expected_super_keys, src_owner
 
-    mp.spawn(_worker, args=(world, _free_port(), name, str(tmp_path)), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), name, str(tmp_path), chunk), nprocs=world, join=True)
     meta = load_meta(name)
     n = meta["n_unique"]
     parts, keys = [], 0

@@ -26,6 +26,15 @@ for s in $STEPS; do
       timeout -k 10 300 python -u bench.py --sim-world $P --steps 3 > $OUT/bench_sim$P.json 2> $OUT/bench_sim$P.err
       rc=$?; echo "bench sim $P rc=$rc"; cat $OUT/bench_sim$P.json; [ $rc -ne 0 ] && break
     done ;;
+  xchg1)
+    timeout -k 10 300 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29511 bench.py --exchange --steps 3 --no-cpu-baseline > $OUT/bench_xchg1.json 2> $OUT/bench_xchg1.err
+    rc=$?; echo "bench exchange(RCCL, 1 rank) rc=$rc"; cat $OUT/bench_xchg1.json ;;
+  xdebug)
+    timeout -k 10 300 python -u tools/xchg_debug.py > $OUT/xchg_debug.log 2>&1
+    rc=$?; echo "xchg_debug rc=$rc"; grep -v Warn $OUT/xchg_debug.log | tail -30 ;;
+  a2a)
+    timeout -k 10 300 python -u tools/a2a_probe.py > $OUT/a2a_probe.log 2>&1
+    rc=$?; echo "a2a_probe rc=$rc"; grep MB $OUT/a2a_probe.log ;;
   benchc2)
     timeout -k 10 300 python -u bench.py --config c2 --no-cpu-baseline > $OUT/bench_c2.json 2> $OUT/bench_c2.err
     rc=$?; echo "bench c2 rc=$rc"; cat $OUT/bench_c2.json ;;
