@@ -124,6 +124,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r01s2_pmc_c3.json"))
     ap.add_argument("--nb-log2", type=int, default=0)
+    ap.add_argument("--split-probe", action="store_true", help="probe -> candidates -> verify kernels (option split = 1)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -165,6 +166,7 @@ def main():
     for r in ([rank] if mode == "exchange" else range(P)):
         e = OverlapEngine(local)
         e.set_option("nb_log2", args.nb_log2)
+        e.set_option("split", 1 if args.split_probe else 0)
         e.set_shard(r, P, 0, 0)
         e.upload(ds)
         engines.append(e)
@@ -205,7 +207,8 @@ def main():
     for _ in range(args.warmup):
         step()
 
-    dev_ms = {"index_ms": 0.0, "contained_ms": 0.0, "overlap_ms": 0.0, "scan_ms": 0.0, "probe_ms": 0.0}
+    dev_ms = {"index_ms": 0.0, "contained_ms": 0.0, "overlap_ms": 0.0, "scan_ms": 0.0, "probe_ms": 0.0,
+              "verify_ms": 0.0}
     phase_ms.clear()
     sync_barrier()
     t0 = time.perf_counter()
@@ -249,9 +252,9 @@ def main():
         traffic = load_pmc(args.pmc) if args.config == "c3" else None
         roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                "kernel": "step = k_index_build + k_scan + k_probe (dominant: k_probe)",
+                "kernel": "step = k_index_build + k_scan + k_probe + k_verify",
                 "alg_bytes_per_step": alg, "alg_bytes_per_read": per_read, "kernel_ms_per_step": kern_ms,
-                "probe_ms": dev_ms["probe_ms"], "scan_ms": dev_ms["scan_ms"]}
+                "probe_ms": dev_ms["probe_ms"], "verify_ms": dev_ms["verify_ms"], "scan_ms": dev_ms["scan_ms"]}
     else:
         # per-rank work is 1/P of the reads: roofline of rank 0's kernels on its share
         achieved = alg / P / (kern_ms / 1000.0) / 1e9 if kern_ms > 0 else 0.0

@@ -49,7 +49,8 @@ typedef struct mg_timings {
   float overlap_ms;     /* discovery = scan + probe (insertAllEdgesOfRead) */
   float total_ms;       /* index + contained + overlap               */
   float scan_ms;        /* minimizer-run scan kernel                 */
-  float probe_ms;       /* probe + verify kernel                     */
+  float probe_ms;       /* probe kernel (fused path: probe + verify) */
+  float verify_ms;      /* verify kernel of the split path (0 fused) */
 } mg_timings;
 
 /* Work counters of the last discovery launch (only with option "stats" = 1):
@@ -170,7 +171,8 @@ int mg_finalize_contained(mg_ctx* ctx, uint32_t* super_out);
 int mg_get_timings(const mg_ctx* ctx, mg_timings* t);
 int mg_get_counters(const mg_ctx* ctx, mg_counters* c);
 /* Options: "nb_log2" (log2 directory buckets, 0 = auto), "rows_cap" (initial
- * row capacity, 0 = auto), "stats" (1 = count work units in the next launches). */
+ * row capacity, 0 = auto), "stats" (1 = count work units in the next launches),
+ * "split" (1 = probe -> candidates -> verify kernels, 0 = fused probe (default)). */
 int mg_set_option(mg_ctx* ctx, const char* name, int64_t value);
 /* HIP stream the context launches on (hipStream_t as void*), for callers that
  * time or capture it themselves. */

@@ -459,6 +459,10 @@ struct ProbeParams {
   int uniform_len;                // every read has this length (0: lengths differ)
   unsigned long long* stats;      // optional [kSegs*4]: runs probed, entries scanned, partners fetched, rows
   int phase_limit;                // diagnostics: 4 no probe, 5 + cell loads, 6 + filter, 7 full
+  // split path (k_probe<SPLIT=true> + k_verify): candidates {partner, source, o << 30 | j}
+  uint3* cand;                    // one region of cand_cap records per probe wavefront
+  unsigned long long* cand_cnt;   // [waves] candidates written (may exceed cand_cap)
+  uint64_t cand_cap;
 };
 
 template <int MAXW>
@@ -472,6 +476,8 @@ struct ProbeLds {
   static constexpr size_t o_ci = o_cb + CAND * 4;                       // [CAND] u32 o << 30 | j
   static constexpr size_t o_ca = o_ci + CAND * 4;                       // [CAND] u32 source read
   static constexpr size_t bytes = o_ca + CAND * 4;
+  // split path (k_probe<.., SPLIT = true>): only the pending arrays, at offset 0
+  static constexpr size_t split_bytes = 2 * PEND * 8;
 };
 
 // Probe wavefront r consumes its run regions in batches of 64 probe items (one
@@ -485,15 +491,15 @@ struct ProbeLds {
 // (ballot + mbcnt per slot) and are verified one per lane against the
 // partner's slot in HBM; a full cell's chain flag turns the lane's item into a
 // pending item (LDS) that a later batch probes at the next cell.
-template <int MAXW, bool CONTAIN>
+template <int MAXW, bool CONTAIN, bool SPLIT>
 __global__ __launch_bounds__(kBlock) void k_probe(ProbeParams p) {
   using PL = ProbeLds<MAXW>;
   extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  unsigned char* base = reinterpret_cast<unsigned char*>(smem) + (size_t)wv * PL::bytes;
+  unsigned char* base = reinterpret_cast<unsigned char*>(smem) + (size_t)wv * (SPLIT ? PL::split_bytes : PL::bytes);
   uint64_t* s_a = reinterpret_cast<uint64_t*>(base + PL::o_a);
-  uint64_t* s_pk = reinterpret_cast<uint64_t*>(base + PL::o_pk);
-  uint64_t* s_pm = reinterpret_cast<uint64_t*>(base + PL::o_pm);
+  uint64_t* s_pk = reinterpret_cast<uint64_t*>(base + (SPLIT ? 0 : PL::o_pk));
+  uint64_t* s_pm = reinterpret_cast<uint64_t*>(base + (SPLIT ? PL::PEND * 8 : PL::o_pm));
   uint32_t* s_cb = reinterpret_cast<uint32_t*>(base + PL::o_cb);
   uint32_t* s_ci = reinterpret_cast<uint32_t*>(base + PL::o_ci);
   uint32_t* s_ca = reinterpret_cast<uint32_t*>(base + PL::o_ca);
@@ -504,6 +510,8 @@ __global__ __launch_bounds__(kBlock) void k_probe(ProbeParams p) {
   const uint32_t seg = (uint32_t)(gw & (kSegs - 1));
   uint32_t* const region = p.rows + gw * p.reg_cap * 3;
   uint64_t cursor = 0;
+  uint3* const cregion = SPLIT ? p.cand + gw * p.cand_cap : nullptr;
+  uint64_t ccur = 0;
   uint32_t st_runs = 0, st_ent = 0, st_ver = 0, st_rows = 0;
   uint32_t ncand = 0, npend = 0;
 
@@ -716,6 +724,24 @@ __global__ __launch_bounds__(kBlock) void k_probe(ProbeParams p) {
       keep = keep && (CONTAIN || oo == 0 || (oo >= 2 && (uint32_t)e[s] >= ra));
       keepm |= (keep ? 1u : 0u) << s;
     }
+    if (SPLIT) {
+      // candidates straight to this wavefront's HBM region (k_verify checks them)
+#pragma unroll
+      for (int s = 0; s < kCell; ++s) {
+        const bool k = (keepm >> s) & 1u;
+        const uint64_t bal = __ballot(k);
+        if (bal) {
+          if (k) {
+            const uint32_t hi = (uint32_t)(e[s] >> 32);
+            const uint64_t at = ccur + lane_prefix(bal);
+            if (at < p.cand_cap)
+              cregion[at] = make_uint3((uint32_t)e[s], ra, ((hi & 3u) << 30) | (uint32_t)(rp - (int)((hi >> 2) & 1023u)));
+          }
+          ccur += (uint64_t)__popcll(bal);
+        }
+      }
+      return;
+    }
     while (__ballot(keepm != 0)) {
       // append slot groups while they fit, then verify a full wavefront
 #pragma unroll
@@ -794,8 +820,9 @@ __global__ __launch_bounds__(kBlock) void k_probe(ProbeParams p) {
       key_c = key_n; meta_c = meta_n; val_c = val_n;
     }
   }
-  if (ncand && p.phase_limit > 6) verify(ncand);
-  if (!CONTAIN && lane == 0) p.reg_cnt[gw] = cursor;
+  if (!SPLIT && ncand && p.phase_limit > 6) verify(ncand);
+  if (SPLIT && lane == 0) p.cand_cnt[gw] = ccur;
+  if (!SPLIT && !CONTAIN && lane == 0) p.reg_cnt[gw] = cursor;
   if (p.stats) {
     uint32_t v[4] = {st_runs, st_ent, st_ver, st_rows};
 #pragma unroll
@@ -804,6 +831,171 @@ __global__ __launch_bounds__(kBlock) void k_probe(ProbeParams p) {
 #pragma unroll
       for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d);
       if (lane == 0) atomicAdd(&p.stats[seg * 4 + i], (unsigned long long)x);
+    }
+  }
+}
+
+// Split path, stage 2 helpers.  One candidate {partner, source, o << 30 | j}
+// -> the overlap to compare: L bases of the source at x0 (reverse strand when
+// rcA) against the partner's forward bases at y0 (checkOverlap,
+// OverlapGraph.cpp:354-383; checkOverlapForContainedRead :302-340).
+struct Cand {
+  uint32_t bid, sa;
+  int o, j, n1, n2, L, x0, y0;
+  bool cond, rcA;
+};
+
+template <bool CONTAIN>
+__device__ __forceinline__ Cand cand_setup(const ProbeParams& p, uint3 c, bool have) {
+  Cand k{};
+  k.bid = c.x;
+  k.sa = c.y;
+  if (!have) return k;
+  const int h = p.h;
+  k.o = (int)(c.z >> 30);
+  k.j = (int)(c.z & 1023u);
+  k.n1 = p.uniform_len ? p.uniform_len : (int)p.len[k.sa];
+  k.n2 = p.uniform_len ? p.uniform_len : (int)p.len[k.bid];
+  const int o = k.o, j = k.j, n1 = k.n1, n2 = k.n2;
+  if (!CONTAIN) {
+    if (o == 0) {        // F1[j, n1) == F2[0, L)
+      k.L = n1 - j; k.cond = k.L < n2; k.x0 = j; k.y0 = 0; k.rcA = false;
+    } else if (o == 2) { // F1[j, n1) == R2[0, L)  <=>  R1[0, L) == F2[n2-L, n2)
+      k.L = n1 - j; k.cond = k.L < n2; k.x0 = 0; k.y0 = n2 - k.L; k.rcA = true;
+    } else {             // F1[0, L) == R2[n2-L, n2)  <=>  R1[n1-L, n1) == F2[0, L)
+      k.L = j + h; k.cond = j <= n2 - h; k.x0 = n1 - k.L; k.y0 = 0; k.rcA = true;
+    }
+  } else {
+    int sft;
+    k.cond = n1 > n2;
+    if (o == 0 || o == 2) {
+      k.cond = k.cond && (j <= n1 - n2);
+      sft = j;
+    } else {
+      k.cond = k.cond && (j >= n2 - h);
+      sft = j - (n2 - h);
+    }
+    k.L = n2;
+    k.y0 = 0;
+    k.rcA = o >= 2;
+    k.x0 = k.rcA ? n1 - sft - n2 : sft;
+  }
+  return k;
+}
+
+// the partner words [y0, y0 + L) spans: all inside the partner's own slot
+template <int MAXW>
+__device__ __forceinline__ void cand_load(const ProbeParams& p, const Cand& k, uint64_t* y) {
+  const uint64_t* bg = p.words + (uint64_t)k.bid * slot_words(MAXW) + (k.y0 >> 5);
+  const int need = (((k.y0 & 31) + k.L - 1) >> 5) + 1;
+#pragma unroll
+  for (int w = 0; w <= MAXW; ++w) y[w] = (k.cond && w < need) ? bg[w] : 0;
+}
+
+// compare against the source slot (read straight from memory: the candidates
+// of a batch come from a handful of consecutive source reads, so these are
+// L1/L2 hits)
+template <int MAXW>
+__device__ __forceinline__ bool cand_match(const ProbeParams& p, const Cand& k, const uint64_t* y) {
+  const uint64_t* f1 = p.words + (uint64_t)k.sa * slot_words(MAXW);
+  const int ys = (k.y0 & 31) << 1;
+  uint64_t diff = 0;
+#pragma unroll
+  for (int cc = 0; cc < MAXW; ++cc) {
+    if (cc * 32 < k.L) {
+      const uint64_t av = k.rcA ? rc_word(ext_fwd<1>(f1, k.n1 - k.x0 - 32 * cc - 32)) : ext_fwd<1>(f1, k.x0 + 32 * cc);
+      const uint64_t bv = funnel(y[cc], y[cc + 1], ys);
+      const int rem = k.L - 32 * cc;
+      const uint64_t msk = rem >= 32 ? ~0ULL : ~(~0ULL >> (2 * rem));
+      diff |= (av ^ bv) & msk;
+    }
+  }
+  return diff == 0;
+}
+
+// Split path, stage 2: verify the candidates of k_probe<SPLIT>, two batches of
+// 64 per trip (two partner slots in flight per lane; the next pair's candidate
+// records load behind them).  A verified discovery becomes a row + twin
+// (insertEdge :407-419, orientation/offset switch :550-557, twin :841-855) in
+// this wavefront's row region, or a superReadID key (atomicMax) in CONTAIN
+// mode.  Wavefront r verifies the candidate regions r, r + nw, ... of the probe.
+template <int MAXW, bool CONTAIN>
+__global__ __launch_bounds__(kBlock) void k_verify(ProbeParams p, uint64_t cand_regions) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int h = p.h;
+  const uint64_t gw = (uint64_t)blockIdx.x * kWavesPerBlock + wv;
+  const uint64_t nw = (uint64_t)gridDim.x * kWavesPerBlock;
+  const uint32_t seg = (uint32_t)(gw & (kSegs - 1));
+  uint32_t* const region = p.rows + gw * p.reg_cap * 3;
+  uint64_t cursor = 0;
+  uint32_t st_ver = 0, st_rows = 0;
+
+  auto emit = [&](const Cand& k, bool ok) {
+    int nrec = 0;
+    uint32_t r2 = 0, t2 = 0;
+    if (ok) {
+      if (CONTAIN) {
+        atomicMax(&p.superkey[k.bid], ((unsigned long long)k.n1 << 32) | (0xFFFFFFFFu - k.sa));
+      } else if (!(p.super && p.super[k.bid])) {  // :548 read2 contained
+        const uint32_t orient = (k.o == 0) ? 3u : (k.o == 2 ? 2u : 1u);
+        const uint32_t off = (k.o == 3) ? (uint32_t)(k.n1 - h - k.j) : (uint32_t)k.j;
+        const uint32_t torient = (orient == 3u) ? 0u : orient;
+        const uint32_t toff = (uint16_t)(k.n2 + off - k.n1);
+        r2 = (orient << 16) | off;
+        t2 = (torient << 16) | toff;
+        nrec = (k.bid == k.sa && k.o == 0) ? 4 : 2;  // self o=0 hit also stands for its o=1 twin
+        st_rows += nrec;
+      }
+    }
+    if (CONTAIN) return;
+    const uint64_t b2 = __ballot(nrec >= 2), b4 = __ballot(nrec == 4);
+    const uint32_t tot = 2u * (uint32_t)(__popcll(b2) + __popcll(b4));
+    if (tot) {
+      if (cursor + tot <= p.reg_cap) {
+        const uint32_t pr = 2u * (lane_prefix(b2) + lane_prefix(b4));
+        uint3* d = reinterpret_cast<uint3*>(region + (cursor + pr) * 3);
+        for (int rr = 0; rr < nrec; rr += 2) {
+          d[0] = make_uint3(k.sa + 1, k.bid + 1, r2);
+          d[1] = make_uint3(k.bid + 1, k.sa + 1, t2);
+          d += 2;
+        }
+      }
+      cursor += tot;  // keeps counting past the capacity: the host resizes and reruns
+    }
+  };
+
+  for (uint64_t cr = gw; cr < cand_regions; cr += nw) {
+    const uint3* cbase = p.cand + cr * p.cand_cap;
+    uint64_t cn = p.cand_cnt[cr];
+    cn = cn < p.cand_cap ? cn : p.cand_cap;
+    uint3 nA = (uint64_t)lane < cn ? cbase[lane] : make_uint3(0, 0, 0);
+    uint3 nB = (uint64_t)lane + kWave < cn ? cbase[kWave + lane] : make_uint3(0, 0, 0);
+    for (uint64_t b0 = 0; b0 < cn; b0 += 2 * kWave) {
+      const bool hA = b0 + lane < cn, hB = b0 + kWave + lane < cn;
+      const Cand kA = cand_setup<CONTAIN>(p, nA, hA);
+      const Cand kB = cand_setup<CONTAIN>(p, nB, hB);
+      uint64_t yA[MAXW + 1], yB[MAXW + 1];
+      cand_load<MAXW>(p, kA, yA);
+      cand_load<MAXW>(p, kB, yB);
+      const uint64_t q = b0 + 2 * kWave + lane;
+      nA = q < cn ? cbase[q] : make_uint3(0, 0, 0);
+      nB = q + kWave < cn ? cbase[q + kWave] : make_uint3(0, 0, 0);
+      const bool okA = kA.cond && cand_match<MAXW>(p, kA, yA);
+      const bool okB = kB.cond && cand_match<MAXW>(p, kB, yB);
+      st_ver += (kA.cond ? 1u : 0u) + (kB.cond ? 1u : 0u);
+      emit(kA, okA);
+      emit(kB, okB);
+    }
+  }
+  if (!CONTAIN && lane == 0) p.reg_cnt[gw] = cursor;
+  if (p.stats) {
+    uint32_t v[2] = {st_ver, st_rows};
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      uint32_t x = v[i];
+#pragma unroll
+      for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d);
+      if (lane == 0) atomicAdd(&p.stats[seg * 4 + 2 + i], (unsigned long long)x);
     }
   }
 }
@@ -1074,7 +1266,15 @@ struct mg_ctx {
   unsigned long long* d_flat_cnt = nullptr;
   size_t flat_cnt_cap = 0;
   // timing
-  hipEvent_t ev[8] = {};
+  hipEvent_t ev[12] = {};
+  // split probe (k_probe<SPLIT> + k_verify)
+  bool split = false;  // option "split": k_probe<SPLIT> + k_verify instead of the fused probe
+  uint3* d_cand = nullptr;
+  size_t cand_cap_total = 0;
+  uint64_t cand_cap_need = 0;
+  unsigned long long* d_cand_cnt = nullptr;
+  size_t cand_cnt_cap = 0;
+  std::vector<unsigned long long> cand_cnt_host;
   mg_timings t{};
 };
 
@@ -1197,9 +1397,15 @@ DiscGeom disc_geom(mg_ctx* ctx, bool contain, uint64_t nsrc) {
   const uint64_t ngroups = (nsrc + kWave - 1) / kWave;
   const uint64_t want = std::max<uint64_t>(1, (ngroups + kWavesPerBlock - 1) / kWavesPerBlock);
   g.lds_scan = (size_t)kWavesPerBlock * (((ctx->w * kWave + 1) / 2) + kScanBuf) * sizeof(uint64_t);
-  g.lds_probe = (size_t)kWavesPerBlock * ProbeLds<W>::bytes;
-  g.grid = contain ? resident_blocks(ctx, k_probe<W, true>, g.lds_probe, want)
-                   : resident_blocks(ctx, k_probe<W, false>, g.lds_probe, want);
+  if (ctx->split) {
+    g.lds_probe = (size_t)kWavesPerBlock * ProbeLds<W>::split_bytes;
+    g.grid = contain ? resident_blocks(ctx, k_probe<W, true, true>, g.lds_probe, want)
+                     : resident_blocks(ctx, k_probe<W, false, true>, g.lds_probe, want);
+  } else {
+    g.lds_probe = (size_t)kWavesPerBlock * ProbeLds<W>::bytes;
+    g.grid = contain ? resident_blocks(ctx, k_probe<W, true, false>, g.lds_probe, want)
+                     : resident_blocks(ctx, k_probe<W, false, false>, g.lds_probe, want);
+  }
   const uint32_t scan_res = resident_blocks(ctx, k_scan<W>, g.lds_scan, ~0ull >> 1);
   g.kreg = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(scan_res / g.grid, (want + g.grid - 1) / g.grid));
   g.sgrid = g.grid * g.kreg;
@@ -1258,12 +1464,15 @@ struct LaunchScan {
   }
 };
 
+int settle_rows(mg_ctx* ctx, bool* again);
+int settle_runs(mg_ctx* ctx, bool* again);
+
 // k_probe over run regions (runs + r * run_cap, run_cnt[r] records), rows into
 // ctx->d_rows (one region per probe wavefront) or superkey updates (contain).
 template <int W>
 struct LaunchProbe {
   static int run(mg_ctx* ctx, bool contain, const ulonglong2* runs, const unsigned long long* run_cnt,
-                 uint64_t run_cap, uint32_t kreg, uint32_t grid) {
+                 uint64_t run_cap, uint32_t kreg, uint32_t grid, uint64_t total_runs) {
     ctx->nreg = (uint64_t)grid * kWavesPerBlock;  // probe wavefronts = row regions
     ProbeParams pp{};
     pp.words = ctx->d_words;
@@ -1288,12 +1497,81 @@ struct LaunchProbe {
     pp.uniform_len = ctx->minlen == ctx->maxlen ? (int)ctx->maxlen : 0;
     pp.stats = contain ? nullptr : (ctx->stats ? ctx->d_stats : nullptr);
     pp.phase_limit = contain ? 99 : ctx->phase_limit;
+    if (ctx->split) return run_split(ctx, contain, pp, grid, total_runs);
     const size_t lds = (size_t)kWavesPerBlock * ProbeLds<W>::bytes;
     if (contain)
-      hipLaunchKernelGGL((k_probe<W, true>), dim3(grid), dim3(kBlock), lds, ctx->stream, pp);
+      hipLaunchKernelGGL((k_probe<W, true, false>), dim3(grid), dim3(kBlock), lds, ctx->stream, pp);
     else
-      hipLaunchKernelGGL((k_probe<W, false>), dim3(grid), dim3(kBlock), lds, ctx->stream, pp);
+      hipLaunchKernelGGL((k_probe<W, false, false>), dim3(grid), dim3(kBlock), lds, ctx->stream, pp);
     return hipGetLastError() == hipSuccess ? 0 : -1;
+  }
+
+  // k_probe<SPLIT> -> candidates (regions resized and the probe rerun on
+  // overflow), then k_verify -> rows (row regions resized and the verify rerun
+  // on overflow).  Synchronous; rows are settled here (ctx->n_rows).
+  static int run_split(mg_ctx* ctx, bool contain, ProbeParams pp, uint32_t grid, uint64_t total_runs) {
+    const uint64_t nwp = (uint64_t)grid * kWavesPerBlock;
+    const size_t lds_p = (size_t)kWavesPerBlock * ProbeLds<W>::split_bytes;
+    allow_lds(k_probe<W, true, true>, lds_p);
+    allow_lds(k_probe<W, false, true>, lds_p);
+    if (ctx->cand_cnt_cap < nwp) {
+      if (ctx->d_cand_cnt) (void)hipFree(ctx->d_cand_cnt);
+      ctx->d_cand_cnt = nullptr;
+      if (hipMalloc(&ctx->d_cand_cnt, nwp * sizeof(unsigned long long)) != hipSuccess) return -1;
+      ctx->cand_cnt_cap = nwp;
+    }
+    if (ctx->cand_cnt_host.size() < nwp) ctx->cand_cnt_host.resize(nwp);
+    for (int attempt = 0;; ++attempt) {
+      if (attempt == 3) return -1;
+      const uint64_t cap = std::max<uint64_t>(ctx->cand_cap_need, total_runs * 3 / 2 / nwp + 256);
+      if (cap * nwp > ctx->cand_cap_total) {
+        if (ctx->d_cand) (void)hipFree(ctx->d_cand);
+        ctx->d_cand = nullptr;
+        if (hipMalloc(&ctx->d_cand, cap * nwp * sizeof(uint3)) != hipSuccess) return -1;
+        ctx->cand_cap_total = cap * nwp;
+      }
+      pp.cand = ctx->d_cand;
+      pp.cand_cnt = ctx->d_cand_cnt;
+      pp.cand_cap = ctx->cand_cap_total / nwp;
+      (void)hipEventRecord(ctx->ev[8], ctx->stream);
+      if (contain)
+        hipLaunchKernelGGL((k_probe<W, true, true>), dim3(grid), dim3(kBlock), lds_p, ctx->stream, pp);
+      else
+        hipLaunchKernelGGL((k_probe<W, false, true>), dim3(grid), dim3(kBlock), lds_p, ctx->stream, pp);
+      if (hipGetLastError() != hipSuccess) return -1;
+      (void)hipEventRecord(ctx->ev[9], ctx->stream);
+      if (hipMemcpyAsync(ctx->cand_cnt_host.data(), ctx->d_cand_cnt, nwp * sizeof(unsigned long long),
+                         hipMemcpyDeviceToHost, ctx->stream) != hipSuccess ||
+          hipStreamSynchronize(ctx->stream) != hipSuccess)
+        return -1;
+      uint64_t mx = 0;
+      for (uint64_t r = 0; r < nwp; ++r) mx = std::max<uint64_t>(mx, ctx->cand_cnt_host[r]);
+      if (mx <= pp.cand_cap) break;
+      ctx->cand_cap_need = mx + mx / 4 + 256;
+    }
+    const size_t lds_v = 0;
+    const uint32_t vgrid = contain ? resident_blocks(ctx, k_verify<W, true>, lds_v, ~0ull >> 1)
+                                   : resident_blocks(ctx, k_verify<W, false>, lds_v, ~0ull >> 1);
+    ctx->nreg = (uint64_t)vgrid * kWavesPerBlock;  // verify wavefronts = row regions
+    for (int attempt = 0;; ++attempt) {
+      if (attempt == 3) return -1;
+      pp.reg_cap = contain ? 0 : ctx->rows_cap / ctx->nreg;
+      pp.rows = ctx->d_rows;
+      (void)hipEventRecord(ctx->ev[10], ctx->stream);
+      if (contain)
+        hipLaunchKernelGGL((k_verify<W, true>), dim3(vgrid), dim3(kBlock), lds_v, ctx->stream, pp, nwp);
+      else
+        hipLaunchKernelGGL((k_verify<W, false>), dim3(vgrid), dim3(kBlock), lds_v, ctx->stream, pp, nwp);
+      if (hipGetLastError() != hipSuccess) return -1;
+      (void)hipEventRecord(ctx->ev[11], ctx->stream);
+      if (contain) break;
+      bool again = false;
+      if (settle_rows(ctx, &again)) return -1;
+      if (!again) break;
+      if (ctx->stats && hipMemsetAsync(ctx->d_stats, 0, kSegs * 4 * sizeof(unsigned long long), ctx->stream) != hipSuccess)
+        return -1;  // counters of a rerun would double (the probe's are lost too: diagnostics only)
+    }
+    return 0;
   }
 };
 
@@ -1309,7 +1587,14 @@ struct LaunchDiscover {
     if (a_hi <= a_lo) return 0;
     const DiscGeom g = disc_geom<W>(ctx, contain, a_hi - a_lo);
     if (LaunchScan<W>::run(ctx, contain, a_lo, a_hi, g.sgrid, !contain)) return -1;
-    return LaunchProbe<W>::run(ctx, contain, ctx->d_runs, ctx->d_run_cnt, ctx->run_cap, g.kreg, g.grid);
+    uint64_t total_runs = 0;
+    if (ctx->split) {  // the split probe sizes its candidate regions from the run count
+      bool again = false;
+      if (settle_runs(ctx, &again)) return -1;
+      if (again) return 1;
+      for (uint64_t r = 0; r < ctx->nrun_reg; ++r) total_runs += std::min<uint64_t>(ctx->run_cnt_host[r], ctx->run_cap);
+    }
+    return LaunchProbe<W>::run(ctx, contain, ctx->d_runs, ctx->d_run_cnt, ctx->run_cap, g.kreg, g.grid, total_runs);
   }
 };
 
@@ -1356,9 +1641,14 @@ int settle_rows(mg_ctx* ctx, bool* again);
 // the exact need is known, so resize and rerun.
 int run_discover(mg_ctx* ctx, bool contain) {
   for (int attempt = 0; attempt < 3; ++attempt) {
-    if (dispatch_w<LaunchDiscover>(ctx->maxw, ctx, contain)) {
+    const int rc = dispatch_w<LaunchDiscover>(ctx->maxw, ctx, contain);
+    if (rc < 0) {
       ctx->err = "discovery launch failed";
       return -1;
+    }
+    if (ctx->split) {  // runs and rows were settled inside (rc 1: run regions resized)
+      if (rc == 0) return 0;
+      continue;
     }
     bool again = false;
     if (settle_runs(ctx, &again)) return -1;
@@ -1409,7 +1699,7 @@ void mg_destroy(mg_ctx* ctx) {
   (void)hipStreamSynchronize(ctx->stream);
   void* bufs[] = {ctx->d_words, ctx->d_len, ctx->d_cells,
                   ctx->d_superkey, ctx->d_super, ctx->d_any, ctx->d_rows, ctx->d_seg, ctx->d_stats,
-                  ctx->d_compact, ctx->d_runs, ctx->d_run_cnt, ctx->d_keyrec, ctx->d_blk, ctx->d_flat_cnt};
+                  ctx->d_compact, ctx->d_runs, ctx->d_run_cnt, ctx->d_keyrec, ctx->d_blk, ctx->d_flat_cnt, ctx->d_cand, ctx->d_cand_cnt};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   for (auto& e : ctx->ev)
@@ -1542,6 +1832,10 @@ int mg_set_option(mg_ctx* ctx, const char* name, int64_t value) {
   }
   if (!strcmp(name, "max_blocks")) {
     ctx->max_blocks = value > 0 ? (uint32_t)value : 8192u;
+    return 0;
+  }
+  if (!strcmp(name, "split")) {
+    ctx->split = value != 0;
     return 0;
   }
   if (!strcmp(name, "stats")) {
@@ -1699,7 +1993,7 @@ struct LaunchProbeFlat {
                        ctx->d_flat_cnt, nw, cap, n);
     if (hipGetLastError() != hipSuccess) return -1;
     (void)hipEventRecord(ctx->ev[7], ctx->stream);
-    return LaunchProbe<W>::run(ctx, contain, runs, ctx->d_flat_cnt, cap, 1, g.grid);
+    return LaunchProbe<W>::run(ctx, contain, runs, ctx->d_flat_cnt, cap, 1, g.grid, n);
   }
 };
 
@@ -1846,11 +2140,17 @@ int mg_find_overlaps(mg_ctx* ctx, uint64_t* n_rows) {
   if (run_discover(ctx, false)) return -1;
   MG_TRY(hipEventRecord(ctx->ev[5], ctx->stream));
   MG_TRY(hipEventSynchronize(ctx->ev[5]));
-  // the scan's own events bracket the last launch pair (a resize retry included
+  // the kernels' own events bracket the last launches (a resize retry included
   // in ev[4]..ev[5] is not kernel time)
   ctx->t.scan_ms = elapsed(ctx->ev[6], ctx->ev[7]);
-  ctx->t.probe_ms = elapsed(ctx->ev[7], ctx->ev[5]);
-  ctx->t.overlap_ms = ctx->t.scan_ms + ctx->t.probe_ms;
+  if (ctx->split) {
+    ctx->t.probe_ms = elapsed(ctx->ev[8], ctx->ev[9]);
+    ctx->t.verify_ms = elapsed(ctx->ev[10], ctx->ev[11]);
+  } else {
+    ctx->t.probe_ms = elapsed(ctx->ev[7], ctx->ev[5]);
+    ctx->t.verify_ms = 0.f;
+  }
+  ctx->t.overlap_ms = ctx->t.scan_ms + ctx->t.probe_ms + ctx->t.verify_ms;
   read_stats(ctx, nsrc);
   ctx->t.total_ms = ctx->t.index_ms + ctx->t.contained_ms + ctx->t.overlap_ms;
   ctx->packable = MG_ROWS;
@@ -1941,13 +2241,19 @@ int mg_probe_runs(mg_ctx* ctx, int contain, const void* runs, uint64_t n, uint64
       return set_err(ctx, "probe launch failed");
     MG_TRY(hipEventRecord(ctx->ev[5], ctx->stream));
     bool again = false;
-    if (!contain && settle_rows(ctx, &again)) return -1;
+    if (!contain && !ctx->split && settle_rows(ctx, &again)) return -1;
     if (!again) break;
   }
   MG_TRY(hipEventSynchronize(ctx->ev[5]));
-  ctx->t.probe_ms = n ? elapsed(ctx->ev[7], ctx->ev[5]) : 0.f;
+  if (ctx->split) {
+    ctx->t.probe_ms = n ? elapsed(ctx->ev[8], ctx->ev[9]) : 0.f;
+    ctx->t.verify_ms = n ? elapsed(ctx->ev[10], ctx->ev[11]) : 0.f;
+  } else {
+    ctx->t.probe_ms = n ? elapsed(ctx->ev[7], ctx->ev[5]) : 0.f;
+    ctx->t.verify_ms = 0.f;
+  }
   if (contain) return 0;
-  ctx->t.overlap_ms = ctx->t.scan_ms + ctx->t.probe_ms;
+  ctx->t.overlap_ms = ctx->t.scan_ms + ctx->t.probe_ms + ctx->t.verify_ms;
   read_stats(ctx, 0);
   if (counts) {
     const uint64_t reg_cap = ctx->nreg ? ctx->rows_cap / ctx->nreg : 0;

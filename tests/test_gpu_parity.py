@@ -257,3 +257,16 @@ def test_exchange_mode_c2_scale_matches_fused(engine):
     assert rows.shape[0] == fused.shape[0]
     assert np.array_equal(rows_to_tuples(rows), rows_to_tuples(fused))
     check_pairs(fused, ds.packed()[1])
+
+
+@pytest.mark.parametrize("name", ["small", "mixed", "tandem", "highdup"])
+def test_split_probe_path(name):
+    """option split = 1: probe -> candidates -> verify kernels give the same multiset."""
+    meta = load_meta(name)
+    ds = Dataset.from_files([fixture_input(name)], meta["l"])
+    e = OverlapEngine(0)
+    e.set_option("split", 1)
+    rows, sup = gpu_rows(e, ds, meta["l"])
+    e.close()
+    assert np.array_equal(rows_to_tuples(rows), golden_rows(name))
+    assert {str(i): int(s) for i, s in enumerate(sup) if s} == meta["super"]

@@ -35,15 +35,30 @@ for s in $STEPS; do
   a2a)
     timeout -k 10 300 python -u tools/a2a_probe.py > $OUT/a2a_probe.log 2>&1
     rc=$?; echo "a2a_probe rc=$rc"; grep MB $OUT/a2a_probe.log ;;
+  benchq)
+    timeout -k 10 300 python -u bench.py --no-cpu-baseline > $OUT/benchq.json 2> $OUT/benchq.err
+    rc=$?; echo "benchq rc=$rc"; python3 -c "import json;d=json.load(open('$OUT/benchq.json'));print('ms/step',round(d['ms_per_step'],3),'edges',d['undirected_edges'],{k:round(v,3) for k,v in d['device_ms'].items()})" ;;
+  benchsplit)
+    timeout -k 10 300 python -u bench.py --split-probe --no-cpu-baseline > $OUT/bench_split.json 2> $OUT/bench_split.err
+    rc=$?; echo "bench split-probe rc=$rc"; cat $OUT/bench_split.json ;;
   benchc2)
     timeout -k 10 300 python -u bench.py --config c2 --no-cpu-baseline > $OUT/bench_c2.json 2> $OUT/bench_c2.err
     rc=$?; echo "bench c2 rc=$rc"; cat $OUT/bench_c2.json ;;
   prof)
     timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o kt -- python3 bench.py --steps 5 --no-cpu-baseline > $OUT/prof_bench.json 2> $OUT/prof_bench.err
-    rc=$?; echo "prof rc=$rc"; cat $OUT/prof_bench.json ;;
+    rc=$?; echo "prof rc=$rc"; cat $OUT/prof_bench.json; head -8 $OUT/prof/kt_kernel_stats.csv | cut -c1-200 ;;
   profsim)
     timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/profsim -o kt -- python3 bench.py --sim-world 4 --steps 2 --no-cpu-baseline > $OUT/profsim_bench.json 2> $OUT/profsim_bench.err
     rc=$?; echo "profsim rc=$rc"; cat $OUT/profsim_bench.json; cat $OUT/profsim/kt_kernel_stats.csv ;;
+  pmcsq)
+    i=0
+    for set in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY SQ_INSTS_VALU SQ_INSTS_VMEM_RD" \
+               "SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_WR SQ_LDS_BANK_CONFLICT TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE"; do
+      i=$((i+1))
+      timeout -s KILL 300 rocprofv3 --pmc $set --kernel-trace --output-format csv -d $OUT/pmcsq_$i -o p -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline > $OUT/pmcsq_$i.log 2>&1
+      rc=$?; echo "pmcsq $i rc=$rc"; [ $rc -ne 0 ] && break
+    done
+    [ $rc -eq 0 ] && python3 tools/pmc_summary.py $OUT/pmcsq_summary.json $OUT/pmcsq_* > /dev/null ;;
   pmc)
     for set in "FETCH_SIZE" "WRITE_SIZE"; do
       timeout -s KILL 300 rocprofv3 --pmc $set --kernel-trace --output-format csv -d $OUT/pmc_$set -o p -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline > $OUT/pmc_$set.log 2>&1
