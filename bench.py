@@ -58,7 +58,27 @@ def make_dataset(cfg, nthreads):
     ds = Dataset.from_codes(c, L, l, nthreads=nthreads)
     t2 = time.time()
     log(f"[bench] generated {n} reads in {t1 - t0:.1f}s, Dataset ingest {t2 - t1:.1f}s, unique {ds.num_unique}")
-    return ds, c, L
+    return ds, c, L, t2 - t1
+
+
+def device_ingest(ds, codes, lens, l, device, host_s, nthreads):
+    """the same Dataset built on the device (mg_ingest_codes),
+    checked against the host mirror's packed reads (IDs, lengths, frequencies)."""
+    e = OverlapEngine(device)
+    try:
+        e.ingest_codes(codes, lens, l)  # warm-up (hipcub temp sizing, code load)
+        t0 = time.perf_counter()
+        nu = e.ingest_codes(codes, lens, l)
+        wall = time.perf_counter() - t0
+        t = e.timings()
+        w1, l1 = e.download_packed()
+        w0, l0 = ds.packed()
+        ok = (nu == ds.num_unique and np.array_equal(l0, l1) and np.array_equal(w0, w1[:, : w0.shape[1]])
+              and e.dataset_counts()[0] == ds.num_reads)
+        return {"device_ms": t["ingest_ms"], "h2d_ms": t["upload_ms"], "wall_s": wall,
+                "host_s": host_s, "host_threads": nthreads, "unique_reads": nu, "match_host": bool(ok)}
+    finally:
+        e.close()
 
 
 def cpu_baseline(cfg, sample_reads: int):
@@ -122,6 +142,7 @@ def main():
                     help="use the RCCL exchange mode even with one rank (checks the torch.distributed plumbing)")
     ap.add_argument("--cpu-sample", type=int, default=150_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-ingest", action="store_true", help="skip the device Dataset ingest measurement")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r01s2_pmc_c3.json"))
     ap.add_argument("--nb-log2", type=int, default=0)
     ap.add_argument("--split-probe", action="store_true", help="probe -> candidates -> verify kernels (option split = 1)")
@@ -133,7 +154,7 @@ def main():
     cfg = CONFIGS[args.config]
     n, lo, hi, G, l, k, seed, desc = cfg
     nthreads = max(2, 16 // max(1, world))
-    ds, _, _ = make_dataset(cfg, nthreads)
+    ds, codes, lens, host_ingest_s = make_dataset(cfg, nthreads)
     N = ds.num_unique
 
     import torch
@@ -287,6 +308,11 @@ def main():
         "counters": cnt,
         "roofline": roof,
     }
+    if world == 1 and mode == "fused" and not args.no_ingest:
+        try:
+            res["dataset_ingest"] = device_ingest(ds, codes, lens, l, local, host_ingest_s, nthreads)
+        except Exception as e:  # report, never fake
+            res["dataset_ingest"] = {"error": str(e)}
     if world == 1 and mode == "fused" and not args.no_cpu_baseline:
         try:
             res["cpu_baseline"] = cpu_baseline(cfg, args.cpu_sample)

@@ -51,6 +51,8 @@ typedef struct mg_timings {
   float scan_ms;        /* minimizer-run scan kernel                 */
   float probe_ms;       /* probe kernel (fused path: probe + verify) */
   float verify_ms;      /* verify kernel of the split path (0 fused) */
+  float upload_ms;      /* H2D copy of raw reads (mg_ingest_*)        */
+  float ingest_ms;      /* device Dataset ingest (mg_ingest_*)        */
 } mg_timings;
 
 /* Work counters of the last discovery launch (only with option "stats" = 1):
@@ -84,6 +86,25 @@ int mg_upload_reads_packed(mg_ctx* ctx, const uint64_t* words, const uint16_t* l
  * (replaces Read::setRead's string storage, Read.cpp:75-82). */
 int mg_upload_reads_ascii(mg_ctx* ctx, const char* concat, const uint64_t* offsets, uint64_t n_reads);
 uint64_t mg_num_reads(const mg_ctx* ctx);
+/* Dataset ingest ON THE DEVICE: raw reads in, the unique
+ * canonical reads in ID order out, resident in the context exactly as
+ * mg_upload_reads_packed would leave them.  Restates Dataset::Dataset's
+ * per-read path (Dataset.cpp:39-65): upper-case (:158-159), testRead (length >
+ * min_overlap, only ACGT, no base >= floor(0.8 len); :160, :398-413),
+ * canonical strand min(s, revcomp(s)) (:163-167), sortReads in std::string
+ * order (:197-202) and removeDupicateReads (frequency, IDs 1..N; :316-345).
+ * ASCII: read i = concat[offsets[i], offsets[i+1]) (FASTA/FASTQ record text as
+ * readDataset extracts it, Dataset.cpp:123-182); codes: codes[i*stride + k]
+ * in {0:A,1:C,2:G,3:T, >3: not ACGT}, k < lens[i].  *n_unique = unique reads. */
+int mg_ingest_ascii(mg_ctx* ctx, const char* concat, const uint64_t* offsets, uint64_t n_raw, uint32_t min_overlap,
+                    uint64_t* n_unique);
+int mg_ingest_codes(mg_ctx* ctx, const uint8_t* codes, uint64_t n_raw, uint64_t stride, const uint16_t* lens,
+                    uint32_t min_overlap, uint64_t* n_unique);
+/* Dataset::getNumberOfReads (reads that passed testRead) and
+ * getNumberOfUniqueReads of the last device ingest. */
+int mg_dataset_counts(const mg_ctx* ctx, uint64_t* n_good, uint64_t* n_unique);
+/* Read::getFrequency of every unique read (n_reads entries, ID order). */
+int mg_download_frequency(mg_ctx* ctx, uint32_t* freq);
 /* Copy back the packed reads (words_per_read words each) for inspection. */
 int mg_download_reads_packed(mg_ctx* ctx, uint64_t* words, uint16_t* lens, uint32_t* words_per_read);
 

@@ -37,6 +37,7 @@
 #include <string>
 #include <vector>
 
+#include "mg_ctx.hpp"
 #include "mg_overlap.h"
 
 namespace {
@@ -92,11 +93,6 @@ __device__ __forceinline__ uint64_t ext_fwd(const uint64_t* f, int pos) {
   return funnel(f[w * S], f[(w + 1) * S], s);
 }
 
-// Device slot of a read: a power-of-two number of words (W = 5 -> 8 words, one
-// aligned 64-B sector), so a partner fetch never straddles two sectors.
-__host__ __device__ constexpr int slot_words(int w) {
-  return w <= 1 ? 1 : w <= 2 ? 2 : w <= 4 ? 4 : w <= 8 ? 8 : w <= 16 ? 16 : 32;
-}
 
 // Number of set bits of a ballot below this lane (v_mbcnt_lo/hi).
 __device__ __forceinline__ uint32_t lane_prefix(uint64_t bal) {
@@ -1204,117 +1200,8 @@ __global__ __launch_bounds__(kBlock) void k_lookup_key(IndexParams p, const uint
 }  // namespace
 
 // ===================================================================== ABI ===
-struct mg_ctx {
-  int device = 0;
-  hipStream_t stream = nullptr;
-  std::string err;
-  // reads
-  uint64_t n = 0;
-  uint32_t maxw = 0;
-  uint32_t stride = 0;  // words per device slot (slot_words(maxw))
-  uint32_t minlen = 0, maxlen = 0;
-  uint64_t* d_words = nullptr;
-  uint16_t* d_len = nullptr;
-  size_t words_cap = 0, len_cap = 0;
-  // index
-  uint32_t l = 0, h = 0, m = 0, w = 0;
-  uint32_t nb_log2 = 0, nb_log2_opt = 0;
-  bool index_ready = false;
-  uint64_t* d_cells = nullptr;  // cells of kCell entries (this rank's bucket range)
-  size_t cells_cap = 0;
-  uint64_t cell_lo = 0, cell_n = 0;  // local bucket range [cell_lo, cell_lo + cell_n)
-  // containment
-  unsigned long long* d_superkey = nullptr;
-  unsigned long long* superkey = nullptr;  // the containment key array in use (d_superkey or caller-owned)
-  uint32_t* d_super = nullptr;
-  unsigned int* d_any = nullptr;
-  size_t super_cap = 0;
-  bool contained_done = false, super_any = false;
-  // rows
-  uint32_t* d_rows = nullptr;
-  uint64_t rows_cap = 0, rows_cap_opt = 0;
-  unsigned long long* d_seg = nullptr;
-  uint64_t n_rows = 0;
-  std::vector<unsigned long long> seg_host;
-  uint64_t seg_cap_regions = 0;
-  bool stats = false;
-  unsigned long long* d_stats = nullptr;
-  mg_counters counters{};
-  // shard
-  uint32_t rank = 0, nranks = 1;
-  uint64_t read_lo = 0, read_hi = 0;
-  uint32_t max_blocks = 8192;  // cap on the persistent discovery grid (blocks of 4 wavefronts)
-  int phase_limit = 99;        // diagnostics (option "phase_limit")
-  int n_cu = 256;              // compute units of the device
-  uint64_t nreg = 0;           // row regions of the last discovery launch (one per probe wavefront)
-  uint64_t nrun_reg = 0;       // run regions (one per scan wavefront)
-  ulonglong2* d_runs = nullptr;  // run records, one region per wavefront
-  size_t runs_cap = 0;
-  uint64_t run_cap = 0, run_cap_need = 0;
-  unsigned long long* d_run_cnt = nullptr;
-  size_t run_cnt_cap = 0;
-  std::vector<unsigned long long> run_cnt_host;
-  uint32_t* d_compact = nullptr;
-  size_t compact_cap = 0;
-  // exchange mode (one process per GPU)
-  ulonglong2* d_keyrec = nullptr;   // key records of this rank's source reads
-  size_t keyrec_cap = 0;
-  uint64_t n_keyrec = 0;
-  unsigned long long* d_blk = nullptr;   // routing: per-(block, rank) counts / offsets + totals
-  size_t blk_cap = 0;
-  int packable = -1;                     // MG_KEYS / MG_RUNS / MG_ROWS: what mg_pack copies out
-  unsigned long long* d_flat_cnt = nullptr;
-  size_t flat_cnt_cap = 0;
-  // timing
-  hipEvent_t ev[12] = {};
-  // split probe (k_probe<SPLIT> + k_verify)
-  bool split = false;  // option "split": k_probe<SPLIT> + k_verify instead of the fused probe
-  uint3* d_cand = nullptr;
-  size_t cand_cap_total = 0;
-  uint64_t cand_cap_need = 0;
-  unsigned long long* d_cand_cnt = nullptr;
-  size_t cand_cnt_cap = 0;
-  std::vector<unsigned long long> cand_cnt_host;
-  mg_timings t{};
-};
-
 namespace {
 
-#define MG_TRY(expr)                                                                  \
-  do {                                                                                \
-    hipError_t e_ = (expr);                                                           \
-    if (e_ != hipSuccess) {                                                           \
-      ctx->err = std::string(#expr) + " failed: " + hipGetErrorString(e_);            \
-      return -1;                                                                      \
-    }                                                                                 \
-  } while (0)
-
-int set_err(mg_ctx* ctx, const std::string& s) {
-  ctx->err = s;
-  return -1;
-}
-
-template <typename T>
-hipError_t ensure(T** p, size_t* cap, size_t count) {
-  if (*cap >= count && *p) return hipSuccess;
-  if (*p) {
-    hipError_t e = hipFree(*p);
-    if (e != hipSuccess) return e;
-    *p = nullptr;
-  }
-  const size_t c = std::max<size_t>(count, 1);
-  hipError_t e = hipMalloc(reinterpret_cast<void**>(p), c * sizeof(T));
-  if (e == hipSuccess) *cap = c;
-  return e;
-}
-
-const uint32_t kSupportedW[] = {1, 2, 3, 4, 5, 6, 8, 12, 16, 32};
-
-uint32_t supported_maxw(uint32_t need) {
-  for (uint32_t w : kSupportedW)
-    if (w >= need) return w;
-  return 0;
-}
 
 template <template <int> class F, typename... Args>
 int dispatch_w(uint32_t maxw, Args&&... args) {
@@ -1699,7 +1586,7 @@ void mg_destroy(mg_ctx* ctx) {
   (void)hipStreamSynchronize(ctx->stream);
   void* bufs[] = {ctx->d_words, ctx->d_len, ctx->d_cells,
                   ctx->d_superkey, ctx->d_super, ctx->d_any, ctx->d_rows, ctx->d_seg, ctx->d_stats,
-                  ctx->d_compact, ctx->d_runs, ctx->d_run_cnt, ctx->d_keyrec, ctx->d_blk, ctx->d_flat_cnt, ctx->d_cand, ctx->d_cand_cnt};
+                  ctx->d_compact, ctx->d_runs, ctx->d_run_cnt, ctx->d_keyrec, ctx->d_blk, ctx->d_flat_cnt, ctx->d_cand, ctx->d_cand_cnt, ctx->d_freq};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   for (auto& e : ctx->ev)
@@ -1714,12 +1601,6 @@ void* mg_stream(mg_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
 
 uint64_t mg_num_reads(const mg_ctx* ctx) { return ctx ? ctx->n : 0; }
 
-static void reset_derived(mg_ctx* ctx) {
-  ctx->index_ready = false;
-  ctx->contained_done = false;
-  ctx->super_any = false;
-  ctx->n_rows = 0;
-}
 
 static int finish_upload(mg_ctx* ctx, const uint16_t* lens_host) {
   // min/max length (Dataset::shortestReadLength / longestReadLength, Dataset.h:35-36)
@@ -1761,6 +1642,7 @@ int mg_upload_reads_packed(mg_ctx* ctx, const uint64_t* words, const uint16_t* l
   if (n_reads)
     MG_TRY(hipMemcpyAsync(ctx->d_len, lens, n_reads * sizeof(uint16_t), hipMemcpyHostToDevice, ctx->stream));
   MG_TRY(hipStreamSynchronize(ctx->stream));
+  ctx->n_good = n_reads;
   return finish_upload(ctx, lens);
 }
 

@@ -30,7 +30,8 @@ class MgError(RuntimeError):
 class _Timings(C.Structure):
     _fields_ = [("pack_ms", C.c_float), ("index_ms", C.c_float), ("contained_ms", C.c_float),
                 ("overlap_ms", C.c_float), ("total_ms", C.c_float), ("scan_ms", C.c_float),
-                ("probe_ms", C.c_float), ("verify_ms", C.c_float)]
+                ("probe_ms", C.c_float), ("verify_ms", C.c_float), ("upload_ms", C.c_float),
+                ("ingest_ms", C.c_float)]
 
 
 class _Counters(C.Structure):
@@ -79,6 +80,10 @@ def lib() -> C.CDLL:
         "mg_set_option": (i32, [vp, C.c_char_p, i64]),
         "mg_stream": (vp, [vp]),
         "mg_record_bytes": (u32, [i32]),
+        "mg_ingest_ascii": (i32, [vp, C.c_char_p, vp, u64, u32, P(u64)]),
+        "mg_ingest_codes": (i32, [vp, vp, u64, u64, vp, u32, P(u64)]),
+        "mg_dataset_counts": (i32, [vp, P(u64), P(u64)]),
+        "mg_download_frequency": (i32, [vp, vp]),
         "mg_key_records": (i32, [vp, u32, u32, vp]),
         "mg_insert_keys": (i32, [vp, vp, u64]),
         "mg_scan_runs": (i32, [vp, i32, vp]),
@@ -252,6 +257,50 @@ class OverlapEngine:
         self._check(lib().mg_upload_reads_ascii(self._h, data, _ptr(off), len(seqs)), "upload_ascii")
         self.n_reads = len(seqs)
         self.lengths_differ = len({len(x) for x in seqs}) > 1
+
+    def ingest_ascii(self, seqs: Sequence[str] | None = None, min_overlap: int = 0, text: bytes | None = None,
+                     offsets: np.ndarray | None = None) -> int:
+        """Dataset ingest on the device (mg_ingest_ascii): raw reads -> unique
+        canonical reads in ID order, resident for build_index.  Returns the
+        number of unique reads."""
+        if text is None:
+            text = "".join(seqs).encode()
+            offsets = np.zeros(len(seqs) + 1, dtype=np.uint64)
+            offsets[1:] = np.cumsum([len(s) for s in seqs])
+        offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+        nu = C.c_uint64()
+        self._check(lib().mg_ingest_ascii(self._h, text, _ptr(offsets), offsets.shape[0] - 1, min_overlap,
+                                          C.byref(nu)), "ingest_ascii")
+        self._after_ingest()
+        return int(nu.value)
+
+    def ingest_codes(self, codes: np.ndarray, lens: np.ndarray, min_overlap: int) -> int:
+        codes = np.ascontiguousarray(codes, dtype=np.uint8)
+        lens = np.ascontiguousarray(lens, dtype=np.uint16)
+        stride = codes.shape[1] if codes.ndim == 2 else 0
+        nu = C.c_uint64()
+        self._check(lib().mg_ingest_codes(self._h, _ptr(codes), lens.shape[0], stride, _ptr(lens), min_overlap,
+                                          C.byref(nu)), "ingest_codes")
+        self._after_ingest()
+        return int(nu.value)
+
+    def _after_ingest(self):
+        self.n_reads = int(lib().mg_num_reads(self._h))
+        if self.n_reads:
+            _, lens = self.download_packed()
+            self.lengths_differ = int(lens.min()) != int(lens.max())
+        else:
+            self.lengths_differ = False
+
+    def dataset_counts(self):
+        g, u = C.c_uint64(), C.c_uint64()
+        lib().mg_dataset_counts(self._h, C.byref(g), C.byref(u))
+        return int(g.value), int(u.value)
+
+    def frequency(self) -> np.ndarray:
+        f = np.zeros(self.n_reads, dtype=np.uint32)
+        self._check(lib().mg_download_frequency(self._h, _ptr(f)), "download_frequency")
+        return f
 
     def download_packed(self):
         wpr = C.c_uint32()

@@ -270,3 +270,73 @@ def test_split_probe_path(name):
     e.close()
     assert np.array_equal(rows_to_tuples(rows), golden_rows(name))
     assert {str(i): int(s) for i, s in enumerate(sup) if s} == meta["super"]
+
+
+# ---- Dataset ingest on the device vs the host mirror,
+# which tests/test_host_dataset.py pins to the reference's ID map
+def read_records(path):
+    """Record text as Dataset::readDataset extracts it (Dataset.cpp:123-182)."""
+    data = open(path, "rb").read().decode()
+    if data.startswith(">"):
+        out = []
+        for rec in data[1:].split(">"):
+            nl = rec.find("\n")
+            out.append(rec[nl + 1:].replace("\n", "") if nl >= 0 else "")
+        return out
+    lines = data.split("\n")
+    return [lines[i] for i in range(1, len(lines), 4)]
+
+
+def assert_same_dataset(engine, ds):
+    w1, l1 = engine.download_packed()
+    w0, l0 = ds.packed()
+    assert engine.n_reads == ds.num_unique
+    assert np.array_equal(l0, l1)
+    assert np.array_equal(w0, w1[:, : w0.shape[1]])
+    assert not np.any(w1[:, w0.shape[1]:])
+    assert engine.dataset_counts() == (ds.num_reads, ds.num_unique)
+    f = engine.frequency()
+    assert [int(x) for x in f[:2000]] == [ds.frequency(i) for i in range(1, min(2000, ds.num_unique) + 1)]
+    assert int(f.sum()) == ds.num_reads
+
+
+@pytest.mark.parametrize("name", FIXTURES)
+def test_device_ingest_matches_host_dataset(engine, name):
+    meta = load_meta(name)
+    path = fixture_input(name)
+    ds = Dataset.from_files([path], meta["l"])
+    engine.set_option("nb_log2", 0)
+    engine.set_shard(0, 1)
+    nu = engine.ingest_ascii(read_records(path), meta["l"])
+    assert nu == meta["n_unique"]
+    assert_same_dataset(engine, ds)
+    engine.build_index(meta["l"])
+    sup = engine.mark_contained()
+    rows = engine.rows()
+    assert np.array_equal(rows_to_tuples(rows), golden_rows(name))
+    assert {str(i): int(s) for i, s in enumerate(sup) if s} == meta["super"]
+
+
+@pytest.mark.parametrize("case", [(20000, 80, 200, 30000, 40, 7), (30000, 100, 100, 2000, 30, 8),
+                                  (5000, 300, 1000, 40000, 60, 9)])
+def test_device_ingest_codes_random(engine, case):
+    n, lo, hi, G, l, seed = case
+    c, L = synth.uniform_read_set(n, 0, G, seed=seed, lo=lo, hi=hi)
+    # sprinkle invalid bases and low-complexity reads (testRead, Dataset.cpp:398-413)
+    rng = np.random.default_rng(seed)
+    bad = rng.choice(n, n // 50, replace=False)
+    c[bad, rng.integers(0, lo, bad.shape[0])] = 4
+    lowc = rng.choice(n, n // 100, replace=False)
+    c[lowc, :] = 2
+    ds = Dataset.from_codes(c, L, l)
+    engine.set_shard(0, 1)
+    engine.ingest_codes(c, L, l)
+    assert_same_dataset(engine, ds)
+
+
+def test_device_ingest_c2_scale(engine):
+    c, L = synth.uniform_read_set(1_000_000, 150, 7_500_000, seed=21)
+    ds = Dataset.from_codes(c, L, 50)
+    engine.set_shard(0, 1)
+    engine.ingest_codes(c, L, 50)
+    assert_same_dataset(engine, ds)
