@@ -13,8 +13,10 @@
 // Differences, all deliberate:
 //  * errors throw mg::Error instead of MYEXIT's exit(0) (Common.h:47);
 //  * reads are stored 2-bit packed; getStringForward/Reverse decode on demand;
-//  * OverlapGraph stops at the raw edge multiset (transitive reduction,
-//    contraction, flow and scaffolding are out of scope);
+//  * OverlapGraph stops before the contraction loop (OverlapGraph.cpp:211-215):
+//    discovery on the device, then the reference's exploration order and
+//    transitive reduction replayed on the host; contraction,
+//    flow and scaffolding are out of scope;
 //  * HashTable/OverlapGraph run on a HIP device through include/mg_overlap.h
 //    and throw if no device is available (there is no CPU fallback).
 #ifndef MG_API_HPP_
@@ -160,8 +162,15 @@ class OverlapGraph {
   }
   // graph[u] of the reference (private there): edges of read u, sorted by offset (:563)
   const std::vector<Edge*>* getEdges(UINT64 readNumber) const;
-  // raw directed multiset as "u v orient offset" lines, sorted (checkpoint/parity dump)
+  // current edges as "u v orient offset" lines, sorted (checkpoint/parity dump)
   bool saveRawEdges(const std::string& fileName) const;
+  // every graph[u] list in list order after "#C numberOfNodes numberOfEdges"
+  bool saveGraphLists(const std::string& fileName) const;
+  // true (default): buildOverlapGraphFromHashTable replays the reference's
+  // exploration order and transitive reduction (OverlapGraph.cpp:144-204,
+  // 574-661) on the device's discoveries, so the graph equals the reference's
+  // just before contraction; false: keep the raw discovery multiset.
+  static bool replayExploration;
   const mg_timings& timings() const { return lastTimings; }
 
  private:

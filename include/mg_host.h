@@ -13,6 +13,8 @@
 #define MG_HOST_H_
 #include <stdint.h>
 
+#include "mg_overlap.h"
+
 #ifdef __cplusplus
 extern "C" {
 #endif
@@ -41,6 +43,24 @@ uint32_t mgh_frequency(const mgh_dataset* ds, uint64_t id); /* Read::getFrequenc
 /* Dataset::getReadFromString (Dataset.cpp:421-455): ID of a read given either
  * strand, 0 if absent. */
 uint64_t mgh_find_read(const mgh_dataset* ds, const char* s, uint64_t len);
+
+/* --- graph construction order ----------------------------
+ * Replays OverlapGraph::buildOverlapGraphFromHashTable's exploration and
+ * transitive reduction (OverlapGraph.cpp:144-204, 574-661) on the device's
+ * discovery multiset (mg_find_overlaps + mg_copy_rows, or the rows of every
+ * rank in exchange mode): the resulting graph[u] lists, in list order, and the
+ * numberOfNodes / numberOfEdges counters are the reference's just before its
+ * contraction loop (:211-215).  lens[id - 1] = read lengths, h = l - 1. */
+typedef struct mgh_graph mgh_graph;
+/* 0 = ok; -1 bad arguments; -2 rows inconsistent with lens / h; -3 unpaired self rows */
+int mgh_graph_replay(const mg_edge* rows, uint64_t n_rows, const uint16_t* lens, uint64_t n_reads, uint32_t h,
+                     mgh_graph** out);
+void mgh_graph_free(mgh_graph* g);
+uint64_t mgh_graph_nodes(const mgh_graph* g); /* OverlapGraph::getNumberOfNodes */
+uint64_t mgh_graph_edges(const mgh_graph* g); /* OverlapGraph::getNumberOfEdges (directed) */
+/* All lists concatenated in u order, each in list order (n_out = edges).
+ * Returns the number of rows written (<= cap); cap = 0 returns the count. */
+uint64_t mgh_graph_rows(const mgh_graph* g, mg_edge* out, uint64_t cap);
 
 #ifdef __cplusplus
 }

@@ -15,6 +15,7 @@
 #include <thread>
 
 #include "mg_api.hpp"
+#include "mg_graph.hpp"
 #include "mg_host.h"
 
 namespace mg {
@@ -545,21 +546,43 @@ bool OverlapGraph::buildOverlapGraphFromHashTable(HashTable* ht) {
   uint64_t got = 0;
   if (mg_copy_rows(ctx, rows.data(), nrows, &got)) mg::fail(ctx, "copy rows");
   mg_get_timings(ctx, &lastTimings);
-  // rows come in (edge, twin) pairs, as insertEdge(Read*,...) creates them
-  for (uint64_t k = 0; k + 1 < got; k += 2) {
-    Read* u = dataSet->getReadFromID(rows[k].src);
-    Read* v = dataSet->getReadFromID(rows[k].dst);
-    Edge* e1 = new Edge(u, v, rows[k].orient, rows[k].offset);
-    Edge* e2 = new Edge(v, u, rows[k + 1].orient, rows[k + 1].offset);
-    e1->setReverseEdge(e2);
-    e2->setReverseEdge(e1);
-    insertEdge(e1);
-    insertEdge(e2);
-  }
-  for (UINT64 i = 1; i <= N; ++i) {  // :562-563
-    auto* lst = (*graph)[i];
-    std::stable_sort(lst->begin(), lst->end(),
-                     [](Edge* a, Edge* b) { return a->getOverlapOffset() < b->getOverlapOffset(); });
+  if (!replayExploration) {
+    // the raw discovery multiset: rows come in (edge, twin) pairs, as
+    // insertEdge(Read*,...) creates them
+    for (uint64_t k = 0; k + 1 < got; k += 2) {
+      Read* u = dataSet->getReadFromID(rows[k].src);
+      Read* v = dataSet->getReadFromID(rows[k].dst);
+      Edge* e1 = new Edge(u, v, rows[k].orient, rows[k].offset);
+      Edge* e2 = new Edge(v, u, rows[k + 1].orient, rows[k + 1].offset);
+      e1->setReverseEdge(e2);
+      e2->setReverseEdge(e1);
+      insertEdge(e1);
+      insertEdge(e2);
+    }
+    for (UINT64 i = 1; i <= N; ++i) {  // :562-563
+      auto* lst = (*graph)[i];
+      std::stable_sort(lst->begin(), lst->end(),
+                       [](Edge* a, Edge* b) { return a->getOverlapOffset() < b->getOverlapOffset(); });
+    }
+  } else {
+    // the reference's exploration order + transitive reduction (:144-204,
+    // 574-661) replayed on the rows: same lists, same order, same counters
+    mg::GraphReplay rp;
+    const int rc = rp.build(rows.data(), got, dataSet->packedLengths(), N, (uint32_t)ht->getHashStringLength());
+    if (rc) throw mg::Error("graph replay: rows inconsistent with the Dataset (" + std::to_string(rc) + ")");
+    std::vector<Edge*> made(rp.pool.size(), nullptr);
+    for (UINT64 u = 1; u <= N; ++u)
+      for (uint32_t e : rp.lists[u]) {
+        const mg::GraphEdge& x = rp.pool[e];
+        made[e] = new Edge(dataSet->getReadFromID(x.src), dataSet->getReadFromID(x.dst), x.orient, x.offset);
+      }
+    for (UINT64 u = 1; u <= N; ++u)
+      for (uint32_t e : rp.lists[u]) {
+        made[e]->setReverseEdge(made[rp.pool[e].rev]);
+        (*graph)[u]->push_back(made[e]);
+      }
+    numberOfNodes = rp.nodes;
+    numberOfEdges = rp.edges;
   }
   delete ht;  // the graph owns and frees the table (:210)
   hashTable = nullptr;
@@ -569,6 +592,22 @@ bool OverlapGraph::buildOverlapGraphFromHashTable(HashTable* ht) {
 const std::vector<Edge*>* OverlapGraph::getEdges(UINT64 readNumber) const {
   if (!graph || readNumber >= graph->size()) return nullptr;
   return (*graph)[readNumber];
+}
+
+bool OverlapGraph::replayExploration = true;
+
+bool OverlapGraph::saveGraphLists(const std::string& fileName) const {
+  if (!graph) return false;
+  FILE* f = std::fopen(fileName.c_str(), "w");
+  if (!f) return false;
+  std::fprintf(f, "#C %llu %llu\n", (unsigned long long)numberOfNodes, (unsigned long long)numberOfEdges);
+  for (size_t u = 1; u < graph->size(); ++u)
+    for (Edge* e : *(*graph)[u])
+      std::fprintf(f, "%llu %llu %u %llu\n", (unsigned long long)u,
+                   (unsigned long long)e->getDestinationRead()->getReadNumber(), (unsigned)e->getOrientation(),
+                   (unsigned long long)e->getOverlapOffset());
+  std::fclose(f);
+  return true;
 }
 
 bool OverlapGraph::saveRawEdges(const std::string& fileName) const {
@@ -674,6 +713,47 @@ uint64_t mgh_find_read(const mgh_dataset* ds, const char* s, uint64_t len) {
   } catch (const std::exception&) {
     return 0;
   }
+}
+
+struct mgh_graph {
+  mg::GraphReplay g;
+};
+
+int mgh_graph_replay(const mg_edge* rows, uint64_t n_rows, const uint16_t* lens, uint64_t n_reads, uint32_t h,
+                     mgh_graph** out) {
+  if (!out || (n_rows && !rows) || (n_reads && !lens)) return -1;
+  *out = nullptr;
+  try {
+    mgh_graph* g = new mgh_graph();
+    const int rc = g->g.build(rows, n_rows, lens, n_reads, h);
+    if (rc) {
+      delete g;
+      return rc;
+    }
+    *out = g;
+  } catch (const std::exception&) {
+    return -1;
+  }
+  return 0;
+}
+
+void mgh_graph_free(mgh_graph* g) { delete g; }
+uint64_t mgh_graph_nodes(const mgh_graph* g) { return g ? g->g.nodes : 0; }
+uint64_t mgh_graph_edges(const mgh_graph* g) { return g ? g->g.edges : 0; }
+
+uint64_t mgh_graph_rows(const mgh_graph* g, mg_edge* out, uint64_t cap) {
+  if (!g) return 0;
+  uint64_t n = 0;
+  for (size_t u = 1; u < g->g.lists.size(); ++u) {
+    for (uint32_t e : g->g.lists[u]) {
+      if (out && n < cap) {
+        const mg::GraphEdge& x = g->g.pool[e];
+        out[n] = mg_edge{x.src, x.dst, x.offset, x.orient, 0};
+      }
+      n++;
+    }
+  }
+  return out ? std::min(n, cap) : n;
 }
 
 }  // extern "C"

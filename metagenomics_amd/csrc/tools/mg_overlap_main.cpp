@@ -2,8 +2,10 @@
 // (main.cpp:117-184: -se/-pe <n> <files...>, -f <prefix>, -l <minOverlap>)
 // running the hot path of main.cpp:33,45-48 on the GPU:
 //   Dataset -> HashTable::insertDataset -> OverlapGraph(ht) -> saveReads
-// and writing the raw directed edge multiset to <prefix>.edges (sorted
-// "u v orient offset" lines).  Extra flags: -k <seed k>, -d <device>.
+// and writing <prefix>.graph: every graph[u] list in list order after the
+// reference's exploration + transitive reduction ("#C nodes edges" first), or
+// with -raw the raw discovery multiset to <prefix>.edges (sorted "u v orient
+// offset" lines).  Extra flags: -k <seed k>, -d <device>, -raw.
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -14,7 +16,7 @@
 
 static void usage() {
   std::fprintf(stderr,
-               "Usage: mg_overlap [-pe n f1..fn] [-se n f1..fn] -f prefix -l minOverlap [-k seedK] [-d device]\n");
+               "Usage: mg_overlap [-pe n f1..fn] [-se n f1..fn] -f prefix -l minOverlap [-k seedK] [-d device] [-raw]\n");
 }
 
 int main(int argc, char** argv) {
@@ -22,6 +24,7 @@ int main(int argc, char** argv) {
   std::string prefix;
   unsigned long long l = 0;
   int k = 0, dev = 0;
+  bool raw = false;
   for (int i = 1; i < argc; ++i) {
     std::string a = argv[i];
     if ((a == "-pe" || a == "-se") && i + 1 < argc) {
@@ -35,6 +38,8 @@ int main(int argc, char** argv) {
       k = std::atoi(argv[++i]);
     } else if (a == "-d" && i + 1 < argc) {
       dev = std::atoi(argv[++i]);
+    } else if (a == "-raw") {
+      raw = true;
     } else {
       usage();
       return (a == "-h" || a == "--help") ? 0 : 1;
@@ -47,12 +52,16 @@ int main(int argc, char** argv) {
   try {
     HashTable::setDefaultDevice(dev);
     HashTable::setDefaultSeedK((uint32_t)k);
+    OverlapGraph::replayExploration = !raw;
     Dataset* ds = new Dataset(pe, se, l);
     HashTable* ht = new HashTable();
     ht->insertDataset(ds, l);
     OverlapGraph* g = new OverlapGraph(ht);  // deletes ht
     ds->saveReads(prefix + "_sortedReads.fasta");
-    g->saveRawEdges(prefix + ".edges");
+    if (raw)
+      g->saveRawEdges(prefix + ".edges");
+    else
+      g->saveGraphLists(prefix + ".graph");
     const mg_timings& t = g->timings();
     std::printf(
         "{\"reads\": %llu, \"unique_reads\": %llu, \"nodes\": %llu, \"directed_edges\": %llu, "

@@ -102,6 +102,11 @@ def lib() -> C.CDLL:
         "mgh_read_string": (i64, [vp, u64, C.c_char_p, u64]),
         "mgh_frequency": (u32, [vp, u64]),
         "mgh_find_read": (u64, [vp, C.c_char_p, u64]),
+        "mgh_graph_replay": (i32, [vp, u64, vp, u64, u32, P(vp)]),
+        "mgh_graph_free": (None, [vp]),
+        "mgh_graph_nodes": (u64, [vp]),
+        "mgh_graph_edges": (u64, [vp]),
+        "mgh_graph_rows": (u64, [vp, vp, u64]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -403,6 +408,27 @@ class OverlapEngine:
 
     def stream(self) -> int:
         return int(lib().mg_stream(self._h) or 0)
+
+
+def replay_graph(rows: np.ndarray, lens: np.ndarray, min_overlap: int):
+    """The reference's graph after buildOverlapGraphFromHashTable's exploration
+    and transitive reduction (OverlapGraph.cpp:144-204, 574-661), replayed on a
+    discovery multiset (mgh_graph_replay, host C++).  Returns (numberOfNodes,
+    numberOfEdges, rows of every graph[u] list in list order, u ascending)."""
+    rows = np.ascontiguousarray(rows, dtype=EDGE_DTYPE)
+    lens = np.ascontiguousarray(lens, dtype=np.uint16)
+    L = lib()
+    g = C.c_void_p()
+    rc = L.mgh_graph_replay(_ptr(rows), rows.shape[0], _ptr(lens), lens.shape[0], min_overlap - 1, C.byref(g))
+    if rc:
+        raise MgError(f"graph replay failed ({rc})")
+    try:
+        n = int(L.mgh_graph_rows(g, None, 0))
+        out = np.zeros(n, dtype=EDGE_DTYPE)
+        L.mgh_graph_rows(g, _ptr(out), n)
+        return int(L.mgh_graph_nodes(g)), int(L.mgh_graph_edges(g)), out
+    finally:
+        L.mgh_graph_free(g)
 
 
 def sort_rows(rows: np.ndarray) -> np.ndarray:

@@ -23,6 +23,14 @@
 //        GPU path, which also stops at the raw edge multiset.
 //   lookup <fasta> <l> <out> <key>... : HashTable::getListOfReads(key)
 //        (HashTable.cpp:202-221) for each key, in the reference list order.
+//   bfs    <fasta> <l> <out>   : the graph as buildOverlapGraphFromHashTable
+//        leaves it before its contraction loop (OverlapGraph.cpp:107-209):
+//        markContainedReads, then the component-by-component exploration with
+//        the reference's own insertAllEdgesOfRead / markTransitiveEdges /
+//        removeTransitiveEdges (the driving loop of :144-204 restated here,
+//        since the reference inlines it ahead of the contraction at :211-215).
+//        Writes "#C <numberOfNodes> <numberOfEdges>" and every graph[u] list
+//        IN LIST ORDER as "u v orient offset" rows.
 #define private public
 #include "Dataset.h"
 #include "HashTable.h"
@@ -59,6 +67,61 @@ static void discovery(OverlapGraph* og, Dataset* ds) {
   for (UINT64 i = 1; i <= ds->getNumberOfUniqueReads(); i++) {
     og->insertAllEdgesOfRead(i, &explored);
     explored[i] = EXPLORED;
+  }
+}
+
+// Exploration order of OverlapGraph.cpp:144-204: a queue per component; a
+// popped read is explored if needed, its unexplored neighbours are explored
+// and queued, its transitive edges marked; then each explored-but-unmarked
+// neighbour queues its own unexplored neighbours and gets its transitive edges
+// marked, and the popped read's transitive edges are removed.
+static void explore_components(OverlapGraph* og, Dataset* ds) {
+  const UINT64 N = ds->getNumberOfUniqueReads();
+  vector<nodeType> state(N + 1, UNEXPLORED);
+  vector<markType> marks(N + 1, VACANT);
+  vector<UINT64> queue(N + 1, 0);
+  og->markContainedReads();
+  for (UINT64 seed = 1; seed <= N; seed++) {
+    if (state[seed] != UNEXPLORED) continue;
+    UINT64 head = 0, tail = 0;
+    queue[tail++] = seed;
+    while (head < tail) {
+      const UINT64 u = queue[head++];
+      if (state[u] == UNEXPLORED) {
+        og->insertAllEdgesOfRead(u, &state);
+        state[u] = EXPLORED;
+      }
+      if (og->graph->at(u)->empty()) continue;
+      if (state[u] == EXPLORED) {
+        for (UINT64 a = 0; a < og->graph->at(u)->size(); a++) {
+          const UINT64 v = og->graph->at(u)->at(a)->getDestinationRead()->getReadNumber();
+          if (state[v] == UNEXPLORED) {
+            queue[tail++] = v;
+            og->insertAllEdgesOfRead(v, &state);
+            state[v] = EXPLORED;
+          }
+        }
+        og->markTransitiveEdges(u, &marks);
+        state[u] = EXPLORED_AND_TRANSITIVE_EDGES_MARKED;
+      }
+      if (state[u] == EXPLORED_AND_TRANSITIVE_EDGES_MARKED) {
+        for (UINT64 a = 0; a < og->graph->at(u)->size(); a++) {
+          const UINT64 v = og->graph->at(u)->at(a)->getDestinationRead()->getReadNumber();
+          if (state[v] != EXPLORED) continue;
+          for (UINT64 b = 0; b < og->graph->at(v)->size(); b++) {
+            const UINT64 w = og->graph->at(v)->at(b)->getDestinationRead()->getReadNumber();
+            if (state[w] == UNEXPLORED) {
+              queue[tail++] = w;
+              og->insertAllEdgesOfRead(w, &state);
+              state[w] = EXPLORED;
+            }
+          }
+          og->markTransitiveEdges(v, &marks);
+          state[v] = EXPLORED_AND_TRANSITIVE_EDGES_MARKED;
+        }
+        og->removeTransitiveEdges(u);
+      }
+    }
   }
 }
 
@@ -121,6 +184,24 @@ int main(int argc, char** argv) {
       for (size_t k = 0; k < lst->size(); k++) {
         Edge* e = lst->at(k);
         fprintf(out, "%llu %llu %u %llu\n", (unsigned long long)e->getSourceRead()->getReadNumber(),
+                (unsigned long long)e->getDestinationRead()->getReadNumber(), (unsigned)e->getOrientation(),
+                (unsigned long long)e->getOverlapOffset());
+      }
+    }
+  } else if (!strcmp(mode, "bfs")) {
+    HashTable* ht = new HashTable();
+    ht->insertDataset(ds, l);
+    OverlapGraph* og = prepare_graph(ds, ht);
+    double t1 = now_s();
+    explore_components(og, ds);
+    double t2 = now_s();
+    fprintf(out, "#C %llu %llu\n", (unsigned long long)og->numberOfNodes, (unsigned long long)og->numberOfEdges);
+    fprintf(out, "#T %.6f\n", t2 - t1);
+    for (UINT64 u = 1; u <= N; u++) {
+      vector<Edge*>* lst = og->graph->at(u);
+      for (size_t k = 0; k < lst->size(); k++) {
+        Edge* e = lst->at(k);
+        fprintf(out, "%llu %llu %u %llu\n", (unsigned long long)u,
                 (unsigned long long)e->getDestinationRead()->getReadNumber(), (unsigned)e->getOrientation(),
                 (unsigned long long)e->getOverlapOffset());
       }

@@ -13,7 +13,12 @@ on small deterministic read sets and stores, per set:
                          ID -> canonical-string map (Dataset.cpp:197-202,316-345)
 
 Only runs in the build container (the reference is not on the GPU box).
-Usage: python tests/golden/make_golden.py [--big]
+  <name>.bfs.gz          (--bfs) the graph[u] lists IN LIST ORDER after the
+                         reference's exploration + transitive reduction,
+                         before contraction (ref_harness bfs; OverlapGraph.cpp:
+                         107-209), with numberOfNodes / numberOfEdges in the json
+
+Usage: python tests/golden/make_golden.py [--big] | --bfs
 """
 from __future__ import annotations
 
@@ -138,7 +143,54 @@ def strs(codes, lengths):
     return synth.codes_to_strings(codes, lengths)
 
 
+def run_bfs(path: str, l: int):
+    with tempfile.NamedTemporaryFile("r", suffix=".txt", delete=False) as t:
+        out = t.name
+    subprocess.run([HARNESS, "bfs", path, str(l), out], check=True)
+    nodes = edges = 0
+    rows = []
+    with open(out) as f:
+        for line in f:
+            if line.startswith("#C"):
+                _, nodes, edges = line.split()
+            elif not line.startswith("#"):
+                rows.append(tuple(map(int, line.split())))
+    os.unlink(out)
+    return int(nodes), int(edges), rows
+
+
+def add_bfs():
+    """Attach the reference's post-exploration graph to every fixture."""
+    for fn in sorted(os.listdir(HERE)):
+        if not fn.endswith(".json"):
+            continue
+        with open(os.path.join(HERE, fn)) as f:
+            meta = json.load(f)
+        with tempfile.TemporaryDirectory() as td:
+            if meta.get("input"):
+                path = os.path.join(td, meta["input"][:-3])
+                with gzip.open(os.path.join(HERE, meta["input"]), "rb") as g, open(path, "wb") as o:
+                    o.write(g.read())
+            else:  # C1: regenerate from the recipe
+                r = meta["recipe"]
+                c, L = synth.uniform_read_set(r["n_reads"], r["read_len"], r["genome_len"], r["seed"])
+                path = os.path.join(td, "in.fa")
+                synth.write_fasta(path, strs(c, L))
+            nodes, edges, rows = run_bfs(path, meta["l"])
+        meta["bfs"] = {"nodes": nodes, "edges": edges, "rows": len(rows), "rows_sha256": rows_digest(rows)}
+        if meta.get("input"):
+            meta["bfs"]["file"] = meta["name"] + ".bfs.gz"
+            with gzip.GzipFile(os.path.join(HERE, meta["bfs"]["file"]), "wb", mtime=0) as g:
+                g.write("".join("%d %d %d %d\n" % r for r in rows).encode())
+        with open(os.path.join(HERE, fn), "w") as f:
+            json.dump(meta, f, indent=1, sort_keys=True)
+        print(f"{meta['name']}: bfs nodes={nodes} edges={edges}")
+
+
 def main():
+    if "--bfs" in sys.argv:
+        add_bfs()
+        return
     big = "--big" in sys.argv
     # 1. fixed-length uniform set (SURVEY §0 "small")
     c, L = synth.uniform_read_set(2000, 100, 20000, seed=1)

@@ -340,3 +340,26 @@ def test_device_ingest_c2_scale(engine):
     engine.set_shard(0, 1)
     engine.ingest_codes(c, L, 50)
     assert_same_dataset(engine, ds)
+
+
+@pytest.mark.parametrize("name", ["small", "mixed", "tandem", "dirty", "wrapped", "tworead"])
+def test_cli_graph_matches_reference(tmp_path, name):
+    """main.cpp's pipeline through the C++ drop-in (mg_overlap CLI: Dataset ->
+    HashTable -> OverlapGraph): graph[u] lists in list order and the node/edge
+    counters equal the reference's graph before contraction."""
+    import gzip
+    import os
+    import subprocess
+
+    from conftest import GOLDEN, ROOT
+
+    meta = load_meta(name)
+    exe = os.path.join(ROOT, "metagenomics_amd", "lib", "mg_overlap")
+    prefix = str(tmp_path / name)
+    subprocess.run([exe, "-se", "1", fixture_input(name), "-f", prefix, "-l", str(meta["l"])], check=True,
+                   stdout=subprocess.DEVNULL, timeout=120)
+    lines = open(prefix + ".graph").read().split("\n")
+    _, nodes, edges = lines[0].split()
+    assert (int(nodes), int(edges)) == (meta["bfs"]["nodes"], meta["bfs"]["edges"])
+    with gzip.open(os.path.join(GOLDEN, meta["bfs"]["file"]), "rt") as f:
+        assert [x for x in lines[1:] if x] == [x for x in f.read().split("\n") if x]

@@ -38,6 +38,9 @@ for s in $STEPS; do
   benchq)
     timeout -k 10 300 python -u bench.py --no-cpu-baseline > $OUT/benchq.json 2> $OUT/benchq.err
     rc=$?; echo "benchq rc=$rc"; python3 -c "import json;d=json.load(open('$OUT/benchq.json'));print('ms/step',round(d['ms_per_step'],3),'edges',d['undirected_edges'],{k:round(v,3) for k,v in d['device_ms'].items()})" ;;
+  replay)
+    timeout -k 10 600 python -u bench.py --replay --no-cpu-baseline --no-ingest --steps 2 > $OUT/bench_replay.json 2> $OUT/bench_replay.err
+    rc=$?; echo "bench replay rc=$rc"; python3 -c "import json;d=json.load(open('$OUT/bench_replay.json'));print(d.get('graph_replay'))" ;;
   benchsplit)
     timeout -k 10 300 python -u bench.py --split-probe --no-cpu-baseline > $OUT/bench_split.json 2> $OUT/bench_split.err
     rc=$?; echo "bench split-probe rc=$rc"; cat $OUT/bench_split.json ;;
