@@ -156,22 +156,32 @@ __device__ __forceinline__ bool owned(uint64_t bkt, uint32_t nb_log2, uint32_t r
 }
 
 // Minimizer of key o of a read (hashRead, HashTable.cpp:88-104): o=0 F[0,h),
-// o=1 F[n-h,n), o=2 R[0,h), o=3 R[n-h,n); R m-mer at t = rc(F[n-t-m, n-t)).
-// Returns mix64 of the minimizer m-mer (bucket, fingerprint) and its offset q.
+// o=1 F[n-h,n), o=2 R[0,h), o=3 R[n-h,n); the m-mer at key offset i is
+// F[s0+i, s0+i+m) for o < 2 and, for o >= 2, R's m-mer = rc(F[t0-i, t0-i+m))
+// with t0 = n-m (o=2) or h-m (o=3).  One m-mer is extracted, the other w-1
+// are rolled in (one base per step: F[s0+i+m] forward, or the complement of
+// F[t0-i-1] appended on the right for the reverse strand), so a key costs w
+// hashes and no funnel shifts.  Returns mix64 of the minimizer m-mer (bucket,
+// fingerprint) and its offset q.
 template <int S>
 __device__ __forceinline__ uint64_t key_minimizer(const uint64_t* f, int n, int o, int h, int m, int w,
                                                   int* q) {
   const uint64_t mmask = (m == 32) ? ~0ULL : ((1ULL << (2 * m)) - 1);
-  const int kb = (o == 0 || o == 2) ? 0 : n - h;
+  const bool fwd = o < 2;
+  const int s0 = fwd ? (o == 0 ? 0 : n - h) : (o == 2 ? n - m : h - m);
+  uint64_t mm = fwd ? ext_fwd<S>(f, s0) >> (64 - 2 * m) : rc_word(ext_fwd<S>(f, s0)) & mmask;
   uint32_t bkey = 0xFFFFFFFFu;
   uint64_t bmm = 0;
   for (int i = 0; i < w; ++i) {
-    const int t = kb + i;
-    const uint64_t mm = (o < 2) ? ext_fwd<S>(f, t) >> (64 - 2 * m) : rc_word(ext_fwd<S>(f, n - t - m)) & mmask;
     const uint32_t key = order_key(mm) | (uint32_t)i;
     if (key < bkey) {
       bkey = key;
       bmm = mm;
+    }
+    if (i + 1 < w) {
+      const int x = fwd ? s0 + i + m : s0 - i - 1;  // base rolled in next
+      const uint64_t b = (f[(x >> 5) * S] >> (62 - 2 * (x & 31))) & 3u;
+      mm = ((mm << 2) | (fwd ? b : 3u - b)) & mmask;
     }
   }
   *q = (int)(bkey & 1023u);
