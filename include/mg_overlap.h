@@ -44,11 +44,11 @@ typedef struct mg_edge {
  * stream), milliseconds. */
 typedef struct mg_timings {
   float pack_ms;        /* 2-bit encoding of ASCII reads            */
-  float index_ms;       /* HashTable::insertDataset equivalent       */
+  float index_ms;       /* HashTable::insertDataset equivalent (with the window scan when fused) */
   float contained_ms;   /* markContainedReads equivalent (0 if skipped) */
   float overlap_ms;     /* discovery = scan + probe (insertAllEdgesOfRead) */
-  float total_ms;       /* index + contained + overlap               */
-  float scan_ms;        /* minimizer-run scan kernel                 */
+  float total_ms;       /* device wall of index + contained + overlap */
+  float scan_ms;        /* minimizer-run scan kernel (0: fused into index_ms) */
   float probe_ms;       /* probe kernel (fused path: probe + verify) */
   float verify_ms;      /* verify kernel of the split path (0 fused) */
   float upload_ms;      /* H2D copy of raw reads (mg_ingest_*)        */
@@ -193,7 +193,10 @@ int mg_get_timings(const mg_ctx* ctx, mg_timings* t);
 int mg_get_counters(const mg_ctx* ctx, mg_counters* c);
 /* Options: "nb_log2" (log2 directory buckets, 0 = auto), "rows_cap" (initial
  * row capacity, 0 = auto), "stats" (1 = count work units in the next launches),
- * "split" (1 = probe -> candidates -> verify kernels, 0 = fused probe (default)). */
+ * "split" (1 = probe -> candidates -> verify kernels, 0 = fused probe (default)),
+ * "overlap_scan" (1 = unsharded contexts build the index inside one window
+ * scan of all reads, k_scan<INDEX>, and both probes reuse its runs (default);
+ * 0 = separate index build and a scan per probe pass). */
 int mg_set_option(mg_ctx* ctx, const char* name, int64_t value);
 /* HIP stream the context launches on (hipStream_t as void*), for callers that
  * time or capture it themselves. */

@@ -81,6 +81,10 @@ struct mg_ctx {
   size_t flat_cnt_cap = 0;
   // timing
   hipEvent_t ev[12] = {};
+  // unsharded contexts build the index inside the window scan (k_scan<INDEX>);
+  // its runs then serve the containment and the discovery probes
+  int scan_state = 0;        // 0 none, 1 launched (not settled), 2 settled
+  bool overlap_scan = true;  // option "overlap_scan" (0: separate index build, a scan per probe pass)
   // split probe (k_probe<SPLIT> + k_verify)
   bool split = false;  // option "split": k_probe<SPLIT> + k_verify instead of the fused probe
   uint3* d_cand = nullptr;
@@ -134,6 +138,7 @@ inline uint32_t supported_maxw(uint32_t need) {
 
 // new reads invalidate everything derived from them
 inline void reset_derived(mg_ctx* ctx) {
+  ctx->scan_state = 0;
   ctx->index_ready = false;
   ctx->contained_done = false;
   ctx->super_any = false;

@@ -363,3 +363,18 @@ def test_cli_graph_matches_reference(tmp_path, name):
     assert (int(nodes), int(edges)) == (meta["bfs"]["nodes"], meta["bfs"]["edges"])
     with gzip.open(os.path.join(GOLDEN, meta["bfs"]["file"]), "rt") as f:
         assert [x for x in lines[1:] if x] == [x for x in f.read().split("\n") if x]
+
+
+@pytest.mark.parametrize("name", ["mixed", "tandem", "highdup", "dirty"])
+def test_scan_inside_probe_path(name):
+    """option overlap_scan = 0: the window scan runs inside each probe pass
+    (containment and discovery scan separately) instead of once, on a second
+    stream, next to the index build."""
+    meta = load_meta(name)
+    ds = Dataset.from_files([fixture_input(name)], meta["l"])
+    e = OverlapEngine(0)
+    e.set_option("overlap_scan", 0)
+    rows, sup = gpu_rows(e, ds, meta["l"])
+    e.close()
+    assert np.array_equal(rows_to_tuples(rows), golden_rows(name))
+    assert {str(i): int(s) for i, s in enumerate(sup) if s} == meta["super"]
