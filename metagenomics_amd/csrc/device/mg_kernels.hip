@@ -515,6 +515,50 @@ __global__ __launch_bounds__(kBlock) void k_scan(ScanParams p) {
   if (lane == 0) p.run_cnt[gw] = cursor;
 }
 
+// The partner's slot as it lies in memory: words 0 .. MAXW-1 (plus one pad
+// word), fetched as 16-B pieces of one aligned line.
+template <int MAXW>
+__device__ __forceinline__ void load_slot(const uint64_t* words, uint32_t bid, uint64_t* y) {
+  const uint64_t* g = words + (uint64_t)bid * slot_words(MAXW);
+  if (slot_words(MAXW) < 2) {
+    y[0] = g[0];
+    y[1] = 0;
+  } else {
+    const ulonglong2* gp = reinterpret_cast<const ulonglong2*>(g);
+#pragma unroll
+    for (int k = 0; k < (MAXW + 1) / 2; ++k) {
+      const ulonglong2 x = gp[k];
+      y[2 * k] = x.x;
+      if (2 * k + 1 <= MAXW) y[2 * k + 1] = x.y;
+    }
+    if (MAXW % 2 == 0) y[MAXW] = 0;
+  }
+}
+
+// checkOverlap's string compare (OverlapGraph.cpp:354-383) on packed words:
+// the L partner bases [y0, y0+L) against the source bases [x0, x0+L) of the
+// forward strand, or of the reverse strand when rcA.  Partner words are used in
+// place (word k holds partner bases [32k, 32k+32)); the source side is
+// extracted at the matching shift from the LDS-staged words (stride S), so no
+// register array is indexed at run time.  Returns the XOR of the compared
+// bases (0 = equal).
+template <int MAXW, int S>
+__device__ __forceinline__ uint64_t overlap_diff(const uint64_t* f1, int n1, int x0, int y0, int L, bool rcA,
+                                                 const uint64_t* y) {
+  uint64_t diff = 0;
+#pragma unroll
+  for (int k = 0; k < MAXW; ++k) {
+    const int lo = max(y0 - 32 * k, 0), hi = min(y0 + L - 32 * k, 32);
+    if (hi > lo) {
+      const int s = x0 - y0 + 32 * k;  // source position of partner base 32k
+      const uint64_t av = rcA ? rc_word(ext_fwd<S>(f1, n1 - s - 32)) : ext_fwd<S>(f1, s);
+      const uint64_t msk = (lo ? (~0ULL >> (2 * lo)) : ~0ULL) & (hi < 32 ? ~(~0ULL >> (2 * hi)) : ~0ULL);
+      diff |= (av ^ y[k]) & msk;
+    }
+  }
+  return diff;
+}
+
 struct ProbeParams {
   const uint64_t* words;
   const uint16_t* len;
@@ -635,14 +679,9 @@ __global__ __launch_bounds__(kBlock) void k_probe(ProbeParams p) {
         x0 = rcA ? n1 - s - n2 : s;
       }
     }
-    // partner words first (the long-latency random loads), then stage the source
-    if (cond) {
-      // only the words [y0, y0 + L) spans: all inside the partner's own slot
-      const uint64_t* bg = p.words + (uint64_t)bid * slot_words(MAXW) + (y0 >> 5);
-      const int need = (((y0 & 31) + L - 1) >> 5) + 1;
-#pragma unroll
-      for (int k = 0; k <= MAXW; ++k) y[k] = k < need ? bg[k] : 0;
-    }
+    // partner slot first (the long-latency random load: its words in 16-B
+    // pieces of one aligned line), then stage the source
+    if (cond) load_slot<MAXW>(p.words, bid, y);
     if (have) {
       const uint64_t* g = p.words + (uint64_t)sa * slot_words(MAXW);
 #pragma unroll
@@ -652,20 +691,7 @@ __global__ __launch_bounds__(kBlock) void k_probe(ProbeParams p) {
     wave_sync();
     if (cond) {
       ++st_ver;
-      const uint64_t* f1 = s_a + lane;
-      const int ys = (y0 & 31) << 1;
-      uint64_t diff = 0;
-#pragma unroll
-      for (int cc = 0; cc < MAXW; ++cc) {
-        if (cc * 32 < L) {
-          const uint64_t av = rcA ? rc_word(ext_fwd<kWave>(f1, n1 - x0 - 32 * cc - 32))
-                                  : ext_fwd<kWave>(f1, x0 + 32 * cc);
-          const uint64_t bv = funnel(y[cc], y[cc + 1], ys);
-          const int rem = L - 32 * cc;
-          const uint64_t msk = rem >= 32 ? ~0ULL : ~(~0ULL >> (2 * rem));
-          diff |= (av ^ bv) & msk;
-        }
-      }
+      const uint64_t diff = overlap_diff<MAXW, kWave>(s_a + lane, n1, x0, y0, L, rcA, y);
       if (diff == 0) {
         if (CONTAIN) {
           atomicMax(&p.superkey[bid], ((unsigned long long)n1 << 32) | (0xFFFFFFFFu - sa));
