@@ -44,6 +44,9 @@ for s in $STEPS; do
   variants)
     timeout -k 10 400 python -u tools/variant_sweep.py > $OUT/variant_sweep.log 2>&1
     rc=$?; echo "variants rc=$rc"; grep opts $OUT/variant_sweep.log ;;
+  phases)
+    timeout -k 10 400 python -u tools/phase_sweep.py > $OUT/phase_sweep.log 2>&1
+    rc=$?; echo "phases rc=$rc"; grep phase $OUT/phase_sweep.log ;;
   benchsplit)
     timeout -k 10 300 python -u bench.py --split-probe --no-cpu-baseline > $OUT/bench_split.json 2> $OUT/bench_split.err
     rc=$?; echo "bench split-probe rc=$rc"; cat $OUT/bench_split.json ;;

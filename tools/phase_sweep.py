@@ -22,7 +22,7 @@ for opt in [None] + extra:
         for _ in range(3):
             eng.find_overlaps()
             t = eng.timings()
-            ts.append((t["overlap_ms"], t.get("scan_ms", 0.0), t.get("probe_ms", 0.0)))
+            ts.append((t["probe_ms"], t.get("scan_ms", 0.0), t.get("probe_ms", 0.0)))
         best = min(ts)
         res[f"{opt}:{ph}"] = best[0]
         print(opt, "phase", ph, "overlap_ms", round(best[0], 3), "scan", round(best[1], 3),
