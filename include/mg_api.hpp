@@ -13,16 +13,18 @@
 // Differences, all deliberate:
 //  * errors throw mg::Error instead of MYEXIT's exit(0) (Common.h:47);
 //  * reads are stored 2-bit packed; getStringForward/Reverse decode on demand;
-//  * OverlapGraph stops before the contraction loop (OverlapGraph.cpp:211-215):
-//    discovery on the device, then the reference's exploration order and
-//    transitive reduction replayed on the host; contraction,
-//    flow and scaffolding are out of scope;
+//  * OverlapGraph(ht) returns the reference's graph: discovery on the device,
+//    then the reference's exploration order and transitive reduction
+//     and its contraction loop (OverlapGraph.cpp:211-215,
+//    row 3) replayed on the host; flow and scaffolding are out of scope
+//    (SURVEY §2 rows 8-13);
 //  * HashTable/OverlapGraph run on a HIP device through include/mg_overlap.h
 //    and throw if no device is available (there is no CPU fallback).
 #ifndef MG_API_HPP_
 #define MG_API_HPP_
 
 #include <cstdint>
+#include <memory>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -37,6 +39,7 @@ typedef unsigned long long UINT64;
 typedef long long INT64;
 
 namespace mg {
+class UnitigGraph;
 struct Error : std::runtime_error {
   explicit Error(const std::string& s) : std::runtime_error(s) {}
 };
@@ -55,11 +58,27 @@ class Read {
   UINT16 getReadLength();
   UINT64 getReadNumber() { return readNumber; }
   UINT32 getFrequency();
+  // composite edges holding this read's forward / reverse string and the read's
+  // distance on each (Read.h:39-42, maintained by OverlapGraph.cpp:1048-1115)
+  std::vector<Edge*>* getListOfEdgesForward() { return &locations().edgesForward; }
+  std::vector<UINT64>* getLocationOnEdgeForward() { return &locations().locationForward; }
+  std::vector<Edge*>* getListOfEdgesReverse() { return &locations().edgesReverse; }
+  std::vector<UINT64>* getLocationOnEdgeReverse() { return &locations().locationReverse; }
 
  private:
   friend class Dataset;
+  friend class OverlapGraph;
+  struct Locations {
+    std::vector<Edge*> edgesForward, edgesReverse;
+    std::vector<UINT64> locationForward, locationReverse;
+  };
+  Locations& locations() {
+    if (!loc) loc.reset(new Locations());
+    return *loc;
+  }
   const Dataset* owner = nullptr;
   UINT64 readNumber = 0;
+  std::unique_ptr<Locations> loc;  // allocated on first use (most reads are on no composite edge)
 };
 
 class Edge {
@@ -75,7 +94,12 @@ class Edge {
     reverseEdge = e;
     return true;
   }
+  // ordered reads inside a composite edge (Edge.h:30-32; empty for a simple edge)
+  std::vector<UINT64>* getListOfReads() { return &listOfReads; }
+  std::vector<UINT16>* getListOfOverlapOffsets() { return &listOfOverlapOffsets; }
+  std::vector<UINT8>* getListOfOrientations() { return &listOfOrientations; }
   bool transitiveRemovalFlag = false;
+  UINT16 flow = 0;  // Edge.h:42 (0 until flow is computed)
 
  private:
   Read* source;
@@ -83,6 +107,9 @@ class Edge {
   UINT8 overlapOrientation;  // 0 = u<---<v, 1 = u<--->v, 2 = u>---<v, 3 = u>--->v
   UINT64 overlapOffset;      // start of v relative to u
   Edge* reverseEdge = nullptr;
+  std::vector<UINT64> listOfReads;
+  std::vector<UINT16> listOfOverlapOffsets;
+  std::vector<UINT8> listOfOrientations;
 };
 
 class Dataset {
@@ -168,9 +195,17 @@ class OverlapGraph {
   bool saveGraphLists(const std::string& fileName) const;
   // true (default): buildOverlapGraphFromHashTable replays the reference's
   // exploration order and transitive reduction (OverlapGraph.cpp:144-204,
-  // 574-661) on the device's discoveries, so the graph equals the reference's
-  // just before contraction; false: keep the raw discovery multiset.
+  // 574-661) on the device's discoveries; false: keep the raw discovery multiset.
   static bool replayExploration;
+  // true (default, as the reference): then run the contraction loop
+  // (OverlapGraph.cpp:211-215); false: stop just before it
+  static bool contractPaths;
+  // the contraction loop's steps (:669-696, :931-988) on the current graph
+  // (available once the graph was built with replayExploration)
+  UINT64 contractCompositePaths();
+  UINT64 removeDeadEndNodes();
+  void sortEdges();                                // :2799-2808
+  bool saveGraphToFile(const std::string& fileName);  // the .unitig checkpoint (:1219-1261)
   const mg_timings& timings() const { return lastTimings; }
 
  private:
@@ -180,7 +215,9 @@ class OverlapGraph {
   UINT64 numberOfNodes = 0, numberOfEdges = 0;
   bool containedDone = false;
   mg_timings lastTimings{};
+  mg::UnitigGraph* unitig = nullptr;  // the list state the contraction steps work on
   void clear();
+  void materialize();  // graph / Edge objects / read locations from `unitig`
 };
 
 #endif  // MG_API_HPP_

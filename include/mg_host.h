@@ -62,6 +62,45 @@ uint64_t mgh_graph_edges(const mgh_graph* g); /* OverlapGraph::getNumberOfEdges 
  * Returns the number of rows written (<= cap); cap = 0 returns the count. */
 uint64_t mgh_graph_rows(const mgh_graph* g, mg_edge* out, uint64_t cap);
 
+/* --- unitig contraction + .unitig checkpoint -------------
+ * Runs the loop that ends new OverlapGraph(ht) (OverlapGraph.cpp:211-215):
+ *   do { contractCompositePaths() :669-696; removeDeadEndNodes() :931-988 }
+ *   while (anything merged or removed)
+ * on the replayed graph, with the reference's mergeEdges / mergeList /
+ * removeEdge list surgery and (track_locations != 0) the per-read location
+ * lists of updateReadLocations / removeReadLocations (:1048-1115).  After it,
+ * mgh_graph_nodes / mgh_graph_edges are the reference's counters after the
+ * loop and mgh_graph_rows returns 0 (offsets of composite edges exceed 16 bits:
+ * use mgh_graph_unitig_edges).  0 = ok; -1 bad handle / already contracted;
+ * -4 an orientation pair mergedEdgeOrientation rejects (:830-833 MYEXIT). */
+int mgh_graph_contract(mgh_graph* g, int track_locations, uint64_t* iterations, uint64_t* merged,
+                       uint64_t* dead_end_nodes);
+/* sortEdges (:2799-2808): every list sorted by destination ID (std::sort). */
+int mgh_graph_sort_edges(mgh_graph* g);
+/* saveGraphToFile (:1219-1261): the .unitig checkpoint of the current graph
+ * (main.cpp:49-50 calls it after sortEdges).  0 = ok, -1 = open/write error. */
+int mgh_graph_save_unitig(const mgh_graph* g, const char* path);
+/* every list in list order as "u v orient offset nreads r:o:d ..." rows, then
+ * the read location lists as "F|R read src dst orient offset location" rows
+ * (the parity dump of oracle/ref_harness unitig). */
+int mgh_graph_save_lists(const mgh_graph* g, const char* path);
+typedef struct mgh_unitig_edge {
+  uint32_t src, dst;  /* getSourceRead / getDestinationRead IDs */
+  uint64_t offset;    /* getOverlapOffset (UINT64) */
+  uint32_t n_reads;   /* getListOfReads()->size() */
+  uint8_t orient;     /* getOrientation */
+  uint8_t pad[3];
+} mgh_unitig_edge;
+/* contracted lists concatenated in u order, each in list order; the reads of
+ * edge k are reads[read_start[k] .. read_start[k] + n_reads) (with their
+ * listOfOverlapOffsets / listOfOrientations entries in offs / ors).  Any
+ * output may be NULL.  Returns the number of edges; *n_reads_total the
+ * length of reads/offs/ors.  Edges beyond edge_cap or reads beyond read_cap
+ * are not written. */
+uint64_t mgh_graph_unitig_edges(const mgh_graph* g, mgh_unitig_edge* edges, uint64_t edge_cap,
+                                uint64_t* read_start, uint32_t* reads, uint16_t* offs, uint8_t* ors,
+                                uint64_t read_cap, uint64_t* n_reads_total);
+
 #ifdef __cplusplus
 }
 #endif

@@ -15,6 +15,7 @@
 #include <thread>
 
 #include "mg_api.hpp"
+#include "mg_unitig.hpp"
 #include "mg_graph.hpp"
 #include "mg_host.h"
 
@@ -481,7 +482,8 @@ OverlapGraph::OverlapGraph(HashTable* ht) { buildOverlapGraphFromHashTable(ht); 
 
 OverlapGraph::~OverlapGraph() { clear(); }
 
-void OverlapGraph::clear() {
+namespace {
+void free_graph(std::vector<std::vector<Edge*>*>*& graph) {
   if (!graph) return;
   for (auto* lst : *graph) {
     for (auto* e : *lst) delete e;
@@ -489,6 +491,93 @@ void OverlapGraph::clear() {
   }
   delete graph;
   graph = nullptr;
+}
+}  // namespace
+
+void OverlapGraph::clear() {
+  free_graph(graph);
+  delete unitig;
+  unitig = nullptr;
+}
+
+void OverlapGraph::materialize() {
+  // Edge objects for the current lists of `unitig`, in list order, with their
+  // read lists; the read location lists point at them (Read.h:39-42)
+  const mg::UnitigGraph& ug = *unitig;
+  free_graph(graph);
+  const UINT64 N = dataSet->getNumberOfUniqueReads();
+  for (UINT64 i = 1; i <= N; ++i) dataSet->getReadFromID(i)->loc.reset();
+  graph = new std::vector<std::vector<Edge*>*>();
+  graph->reserve(N + 1);
+  for (UINT64 i = 0; i <= N; ++i) graph->push_back(new std::vector<Edge*>());
+  std::vector<Edge*> made(ug.pool.size(), nullptr);
+  for (UINT64 u = 1; u <= N && u < ug.lists.size(); ++u)
+    for (uint32_t e : ug.lists[u]) {
+      const mg::UnitigEdge& x = ug.pool[e];
+      Edge* ed = new Edge(dataSet->getReadFromID(x.src), dataSet->getReadFromID(x.dst), x.orient, x.offset);
+      ed->flow = x.flow;
+      if (const mg::EdgeReads* r = ug.reads[e].get()) {
+        ed->getListOfReads()->assign(r->reads.begin(), r->reads.end());
+        *ed->getListOfOverlapOffsets() = r->offs;
+        *ed->getListOfOrientations() = r->ors;
+      }
+      made[e] = ed;
+    }
+  for (UINT64 u = 1; u <= N && u < ug.lists.size(); ++u)
+    for (uint32_t e : ug.lists[u]) {
+      made[e]->setReverseEdge(made[ug.pool[e].rev]);
+      (*graph)[u]->push_back(made[e]);
+    }
+  if (ug.track) {
+    for (UINT64 i = 1; i <= N && i < ug.loc_fwd.size(); ++i) {
+      if (ug.loc_fwd[i].empty() && ug.loc_rev[i].empty()) continue;
+      Read::Locations& L = dataSet->getReadFromID(i)->locations();
+      for (const mg::ReadLoc& l : ug.loc_fwd[i]) {
+        L.edgesForward.push_back(made[l.edge]);
+        L.locationForward.push_back(l.loc);
+      }
+      for (const mg::ReadLoc& l : ug.loc_rev[i]) {
+        L.edgesReverse.push_back(made[l.edge]);
+        L.locationReverse.push_back(l.loc);
+      }
+    }
+  }
+  numberOfNodes = ug.nodes;
+  numberOfEdges = ug.edges;
+}
+
+UINT64 OverlapGraph::contractCompositePaths() {
+  if (!unitig) throw mg::Error("contractCompositePaths: no replayed graph");
+  const UINT64 n = unitig->contract_composite_paths();
+  if (unitig->bad_merge) throw mg::Error("Unable to merge.");  // OverlapGraph.cpp:830-833
+  materialize();
+  return n;
+}
+
+UINT64 OverlapGraph::removeDeadEndNodes() {
+  if (!unitig) throw mg::Error("removeDeadEndNodes: no replayed graph");
+  const UINT64 n = unitig->remove_dead_end_nodes();
+  materialize();
+  return n;
+}
+
+void OverlapGraph::sortEdges() {
+  // :2799-2808; the Edge lists and the list state stay in step
+  if (unitig) {
+    unitig->sort_edges();
+    materialize();
+  } else if (graph) {
+    for (size_t i = 1; i < graph->size(); ++i)
+      std::sort((*graph)[i]->begin(), (*graph)[i]->end(), [](Edge* a, Edge* b) {
+        return a->getDestinationRead()->getReadNumber() < b->getDestinationRead()->getReadNumber();
+      });
+  }
+}
+
+bool OverlapGraph::saveGraphToFile(const std::string& fileName) {
+  if (!unitig) throw mg::Error("saveGraphToFile: no replayed graph");
+  if (unitig->save_unitig(fileName.c_str())) throw mg::Error("Unable to open file: " + fileName);
+  return true;
 }
 
 void OverlapGraph::markContainedReads() {
@@ -570,19 +659,10 @@ bool OverlapGraph::buildOverlapGraphFromHashTable(HashTable* ht) {
     mg::GraphReplay rp;
     const int rc = rp.build(rows.data(), got, dataSet->packedLengths(), N, (uint32_t)ht->getHashStringLength());
     if (rc) throw mg::Error("graph replay: rows inconsistent with the Dataset (" + std::to_string(rc) + ")");
-    std::vector<Edge*> made(rp.pool.size(), nullptr);
-    for (UINT64 u = 1; u <= N; ++u)
-      for (uint32_t e : rp.lists[u]) {
-        const mg::GraphEdge& x = rp.pool[e];
-        made[e] = new Edge(dataSet->getReadFromID(x.src), dataSet->getReadFromID(x.dst), x.orient, x.offset);
-      }
-    for (UINT64 u = 1; u <= N; ++u)
-      for (uint32_t e : rp.lists[u]) {
-        made[e]->setReverseEdge(made[rp.pool[e].rev]);
-        (*graph)[u]->push_back(made[e]);
-      }
-    numberOfNodes = rp.nodes;
-    numberOfEdges = rp.edges;
+    unitig = new mg::UnitigGraph();
+    unitig->init(rp, N, true);
+    if (contractPaths && unitig->contract() < 0) throw mg::Error("Unable to merge.");  // :211-215
+    materialize();
   }
   delete ht;  // the graph owns and frees the table (:210)
   hashTable = nullptr;
@@ -595,6 +675,7 @@ const std::vector<Edge*>* OverlapGraph::getEdges(UINT64 readNumber) const {
 }
 
 bool OverlapGraph::replayExploration = true;
+bool OverlapGraph::contractPaths = true;
 
 bool OverlapGraph::saveGraphLists(const std::string& fileName) const {
   if (!graph) return false;
@@ -717,6 +798,7 @@ uint64_t mgh_find_read(const mgh_dataset* ds, const char* s, uint64_t len) {
 
 struct mgh_graph {
   mg::GraphReplay g;
+  std::unique_ptr<mg::UnitigGraph> u;  // set once contracted
 };
 
 int mgh_graph_replay(const mg_edge* rows, uint64_t n_rows, const uint16_t* lens, uint64_t n_reads, uint32_t h,
@@ -738,11 +820,11 @@ int mgh_graph_replay(const mg_edge* rows, uint64_t n_rows, const uint16_t* lens,
 }
 
 void mgh_graph_free(mgh_graph* g) { delete g; }
-uint64_t mgh_graph_nodes(const mgh_graph* g) { return g ? g->g.nodes : 0; }
-uint64_t mgh_graph_edges(const mgh_graph* g) { return g ? g->g.edges : 0; }
+uint64_t mgh_graph_nodes(const mgh_graph* g) { return g ? (g->u ? g->u->nodes : g->g.nodes) : 0; }
+uint64_t mgh_graph_edges(const mgh_graph* g) { return g ? (g->u ? g->u->edges : g->g.edges) : 0; }
 
 uint64_t mgh_graph_rows(const mgh_graph* g, mg_edge* out, uint64_t cap) {
-  if (!g) return 0;
+  if (!g || g->u) return 0;
   uint64_t n = 0;
   for (size_t u = 1; u < g->g.lists.size(); ++u) {
     for (uint32_t e : g->g.lists[u]) {
@@ -754,6 +836,71 @@ uint64_t mgh_graph_rows(const mgh_graph* g, mg_edge* out, uint64_t cap) {
     }
   }
   return out ? std::min(n, cap) : n;
+}
+
+int mgh_graph_contract(mgh_graph* g, int track_locations, uint64_t* iterations, uint64_t* merged,
+                       uint64_t* dead_end_nodes) {
+  if (!g || g->u) return -1;
+  try {
+    auto u = std::make_unique<mg::UnitigGraph>();
+    u->init(g->g, g->g.lists.empty() ? 0 : g->g.lists.size() - 1, track_locations != 0);
+    const int64_t it = u->contract();
+    if (it < 0) return -4;
+    if (iterations) *iterations = (uint64_t)it;
+    if (merged) *merged = u->merged_total;
+    if (dead_end_nodes) *dead_end_nodes = u->dead_end_total;
+    g->u = std::move(u);
+    // the pre-contraction graph is no longer needed
+    std::vector<mg::GraphEdge>().swap(g->g.pool);
+    std::vector<std::vector<uint32_t>>().swap(g->g.lists);
+  } catch (const std::exception&) {
+    return -1;
+  }
+  return 0;
+}
+
+int mgh_graph_sort_edges(mgh_graph* g) {
+  if (!g || !g->u) return -1;
+  g->u->sort_edges();
+  return 0;
+}
+
+int mgh_graph_save_unitig(const mgh_graph* g, const char* path) {
+  if (!g || !g->u || !path) return -1;
+  return g->u->save_unitig(path);
+}
+
+int mgh_graph_save_lists(const mgh_graph* g, const char* path) {
+  if (!g || !g->u || !path) return -1;
+  return g->u->save_lists(path);
+}
+
+uint64_t mgh_graph_unitig_edges(const mgh_graph* g, mgh_unitig_edge* edges, uint64_t edge_cap,
+                                uint64_t* read_start, uint32_t* reads, uint16_t* offs, uint8_t* ors,
+                                uint64_t read_cap, uint64_t* n_reads_total) {
+  if (!g || !g->u) return 0;
+  const mg::UnitigGraph& u = *g->u;
+  uint64_t k = 0, r = 0;
+  for (size_t v = 1; v < u.lists.size(); ++v) {
+    for (uint32_t e : u.lists[v]) {
+      const mg::UnitigEdge& x = u.pool[e];
+      const mg::EdgeReads* lr = u.reads[e].get();
+      const uint32_t nr = lr ? (uint32_t)lr->reads.size() : 0;
+      if (k < edge_cap) {
+        if (edges) edges[k] = mgh_unitig_edge{x.src, x.dst, x.offset, nr, x.orient, {0, 0, 0}};
+        if (read_start) read_start[k] = r;
+      }
+      for (uint32_t q = 0; q < nr; ++q, ++r) {
+        if (r >= read_cap) continue;
+        if (reads) reads[r] = lr->reads[q];
+        if (offs) offs[r] = lr->offs[q];
+        if (ors) ors[r] = lr->ors[q];
+      }
+      k++;
+    }
+  }
+  if (n_reads_total) *n_reads_total = r;
+  return k;
 }
 
 }  // extern "C"

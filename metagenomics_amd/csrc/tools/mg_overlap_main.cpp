@@ -1,11 +1,16 @@
 // mg_overlap — command-line driver with main.cpp's argument surface
 // (main.cpp:117-184: -se/-pe <n> <files...>, -f <prefix>, -l <minOverlap>)
-// running the hot path of main.cpp:33,45-48 on the GPU:
-//   Dataset -> HashTable::insertDataset -> OverlapGraph(ht) -> saveReads
-// and writing <prefix>.graph: every graph[u] list in list order after the
-// reference's exploration + transitive reduction ("#C nodes edges" first), or
-// with -raw the raw discovery multiset to <prefix>.edges (sorted "u v orient
-// offset" lines).  Extra flags: -k <seed k>, -d <device>, -raw.
+// running main.cpp:33,45-50 with the overlap path on the GPU:
+//   Dataset -> HashTable::insertDataset -> OverlapGraph(ht) (discovery on the
+//   device; exploration order, transitive reduction and the contraction loop
+//   replayed on the host) -> saveReads -> sortEdges -> saveGraphToFile
+// writing <prefix>_sortedReads.fasta and <prefix>.unitig as the reference does.
+// Extra flags: -k <seed k>, -d <device>;
+//   -nocontract  stop before the contraction loop (OverlapGraph.cpp:211-215) and
+//                write every graph[u] list in list order to <prefix>.graph
+//                ("#C nodes edges" first) instead of the .unitig;
+//   -raw         the raw discovery multiset to <prefix>.edges (sorted
+//                "u v orient offset" lines).
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -16,7 +21,7 @@
 
 static void usage() {
   std::fprintf(stderr,
-               "Usage: mg_overlap [-pe n f1..fn] [-se n f1..fn] -f prefix -l minOverlap [-k seedK] [-d device] [-raw]\n");
+               "Usage: mg_overlap [-pe n f1..fn] [-se n f1..fn] -f prefix -l minOverlap [-k seedK] [-d device] [-nocontract | -raw]\n");
 }
 
 int main(int argc, char** argv) {
@@ -24,7 +29,7 @@ int main(int argc, char** argv) {
   std::string prefix;
   unsigned long long l = 0;
   int k = 0, dev = 0;
-  bool raw = false;
+  bool raw = false, nocontract = false;
   for (int i = 1; i < argc; ++i) {
     std::string a = argv[i];
     if ((a == "-pe" || a == "-se") && i + 1 < argc) {
@@ -40,6 +45,8 @@ int main(int argc, char** argv) {
       dev = std::atoi(argv[++i]);
     } else if (a == "-raw") {
       raw = true;
+    } else if (a == "-nocontract") {
+      nocontract = true;
     } else {
       usage();
       return (a == "-h" || a == "--help") ? 0 : 1;
@@ -53,15 +60,20 @@ int main(int argc, char** argv) {
     HashTable::setDefaultDevice(dev);
     HashTable::setDefaultSeedK((uint32_t)k);
     OverlapGraph::replayExploration = !raw;
+    OverlapGraph::contractPaths = !nocontract;
     Dataset* ds = new Dataset(pe, se, l);
     HashTable* ht = new HashTable();
     ht->insertDataset(ds, l);
     OverlapGraph* g = new OverlapGraph(ht);  // deletes ht
     ds->saveReads(prefix + "_sortedReads.fasta");
-    if (raw)
+    if (raw) {
       g->saveRawEdges(prefix + ".edges");
-    else
+    } else if (nocontract) {
       g->saveGraphLists(prefix + ".graph");
+    } else {
+      g->sortEdges();  // main.cpp:49-50
+      g->saveGraphToFile(prefix + ".unitig");
+    }
     const mg_timings& t = g->timings();
     std::printf(
         "{\"reads\": %llu, \"unique_reads\": %llu, \"nodes\": %llu, \"directed_edges\": %llu, "

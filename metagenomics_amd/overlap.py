@@ -107,6 +107,11 @@ def lib() -> C.CDLL:
         "mgh_graph_nodes": (u64, [vp]),
         "mgh_graph_edges": (u64, [vp]),
         "mgh_graph_rows": (u64, [vp, vp, u64]),
+        "mgh_graph_contract": (i32, [vp, i32, P(u64), P(u64), P(u64)]),
+        "mgh_graph_sort_edges": (i32, [vp]),
+        "mgh_graph_save_unitig": (i32, [vp, C.c_char_p]),
+        "mgh_graph_save_lists": (i32, [vp, C.c_char_p]),
+        "mgh_graph_unitig_edges": (u64, [vp, vp, u64, vp, vp, vp, vp, u64, P(u64)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -429,6 +434,81 @@ def replay_graph(rows: np.ndarray, lens: np.ndarray, min_overlap: int):
         return int(L.mgh_graph_nodes(g)), int(L.mgh_graph_edges(g)), out
     finally:
         L.mgh_graph_free(g)
+
+
+UNITIG_EDGE_DTYPE = np.dtype({"names": ["src", "dst", "offset", "n_reads", "orient"],
+                              "formats": ["<u4", "<u4", "<u8", "<u4", "u1"],
+                              "offsets": [0, 4, 8, 16, 20], "itemsize": 24})
+
+
+class UnitigGraph:
+    """The graph new OverlapGraph(ht) returns (OverlapGraph.cpp:107-218): the
+    exploration + transitive reduction replay (mgh_graph_replay), then the
+    contraction loop :211-215 (contractCompositePaths + removeDeadEndNodes,
+    mgh_graph_contract), on host C++.  main.cpp:48-50's sortEdges +
+    saveGraphToFile are sort_edges() / save_unitig()."""
+
+    def __init__(self, rows: np.ndarray, lens: np.ndarray, min_overlap: int, track_locations: bool = True):
+        rows = np.ascontiguousarray(rows, dtype=EDGE_DTYPE)
+        lens = np.ascontiguousarray(lens, dtype=np.uint16)
+        L = self._L = lib()
+        self._g = C.c_void_p()
+        rc = L.mgh_graph_replay(_ptr(rows), rows.shape[0], _ptr(lens), lens.shape[0], min_overlap - 1,
+                                C.byref(self._g))
+        if rc:
+            raise MgError(f"graph replay failed ({rc})")
+        self.replay_nodes, self.replay_edges = int(L.mgh_graph_nodes(self._g)), int(L.mgh_graph_edges(self._g))
+        it, merged, dead = C.c_uint64(), C.c_uint64(), C.c_uint64()
+        rc = L.mgh_graph_contract(self._g, int(track_locations), C.byref(it), C.byref(merged), C.byref(dead))
+        if rc:
+            self.close()
+            raise MgError(f"contraction failed ({rc})")
+        self.iterations, self.merged, self.dead_end_nodes = it.value, merged.value, dead.value
+
+    @property
+    def nodes(self) -> int:
+        return int(self._L.mgh_graph_nodes(self._g))
+
+    @property
+    def edges(self) -> int:
+        return int(self._L.mgh_graph_edges(self._g))
+
+    def sort_edges(self):
+        if self._L.mgh_graph_sort_edges(self._g):
+            raise MgError("sort_edges failed")
+
+    def save_unitig(self, path: str):
+        if self._L.mgh_graph_save_unitig(self._g, os.fsencode(path)):
+            raise MgError(f"cannot write {path}")
+
+    def save_lists(self, path: str):
+        if self._L.mgh_graph_save_lists(self._g, os.fsencode(path)):
+            raise MgError(f"cannot write {path}")
+
+    def unitig_edges(self):
+        """(edges[UNITIG_EDGE_DTYPE], read_start, reads, offs, ors) of the current lists in list order."""
+        L = self._L
+        nr = C.c_uint64()
+        n = int(L.mgh_graph_unitig_edges(self._g, None, 0, None, None, None, None, 0, C.byref(nr)))
+        e = np.zeros(n, dtype=UNITIG_EDGE_DTYPE)
+        st = np.zeros(n, dtype=np.uint64)
+        reads = np.zeros(nr.value, dtype=np.uint32)
+        offs = np.zeros(nr.value, dtype=np.uint16)
+        ors = np.zeros(nr.value, dtype=np.uint8)
+        L.mgh_graph_unitig_edges(self._g, _ptr(e), n, _ptr(st), _ptr(reads), _ptr(offs), _ptr(ors), nr.value,
+                                 C.byref(nr))
+        return e, st, reads, offs, ors
+
+    def close(self):
+        if self._g:
+            self._L.mgh_graph_free(self._g)
+            self._g = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def sort_rows(rows: np.ndarray) -> np.ndarray:

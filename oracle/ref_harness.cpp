@@ -31,6 +31,18 @@
 //        since the reference inlines it ahead of the contraction at :211-215).
 //        Writes "#C <numberOfNodes> <numberOfEdges>" and every graph[u] list
 //        IN LIST ORDER as "u v orient offset" rows.
+//   unitig <fasta> <l> <out>   : as bfs, then the reference's own contraction
+//        loop (OverlapGraph.cpp:211-215: contractCompositePaths +
+//        removeDeadEndNodes until neither changes anything), i.e. the graph
+//        new OverlapGraph(ht) returns (main.cpp:47).  Writes
+//        "#C <numberOfNodes> <numberOfEdges>", "#I <loop iterations>", every
+//        graph[u] list IN LIST ORDER as "u v orient offset nreads r:o:d ..."
+//        rows (the edge's listOfReads / listOfOverlapOffsets /
+//        listOfOrientations), then every read's location lists
+//        (Read.h:39-42, maintained by :1048-1115) as
+//        "F|R <read> <src> <dst> <orient> <offset> <location>" rows; then
+//        sortEdges (:2799-2808) and saveGraphToFile (:1219-1261) into
+//        <out>.unitig (main.cpp:49-50).
 #define private public
 #include "Dataset.h"
 #include "HashTable.h"
@@ -206,6 +218,52 @@ int main(int argc, char** argv) {
                 (unsigned long long)e->getOverlapOffset());
       }
     }
+  } else if (!strcmp(mode, "unitig")) {
+    HashTable* ht = new HashTable();
+    ht->insertDataset(ds, l);
+    OverlapGraph* og = prepare_graph(ds, ht);
+    double t1 = now_s();
+    explore_components(og, ds);
+    double t2 = now_s();
+    UINT64 counter = 0, iters = 0;
+    do {  // OverlapGraph.cpp:211-215
+      counter = og->contractCompositePaths();
+      counter += og->removeDeadEndNodes();
+      iters++;
+    } while (counter > 0);
+    double t3 = now_s();
+    fprintf(out, "#C %llu %llu\n", (unsigned long long)og->numberOfNodes, (unsigned long long)og->numberOfEdges);
+    fprintf(out, "#I %llu\n", (unsigned long long)iters);
+    fprintf(out, "#T %.6f %.6f\n", t2 - t1, t3 - t2);
+    for (UINT64 u = 1; u <= N; u++) {
+      vector<Edge*>* lst = og->graph->at(u);
+      for (size_t k = 0; k < lst->size(); k++) {
+        Edge* e = lst->at(k);
+        fprintf(out, "%llu %llu %u %llu %llu", (unsigned long long)u,
+                (unsigned long long)e->getDestinationRead()->getReadNumber(), (unsigned)e->getOrientation(),
+                (unsigned long long)e->getOverlapOffset(), (unsigned long long)e->getListOfReads()->size());
+        for (size_t q = 0; q < e->getListOfReads()->size(); q++)
+          fprintf(out, " %llu:%u:%u", (unsigned long long)e->getListOfReads()->at(q),
+                  (unsigned)e->getListOfOverlapOffsets()->at(q), (unsigned)e->getListOfOrientations()->at(q));
+        fprintf(out, "\n");
+      }
+    }
+    for (UINT64 r = 1; r <= N; r++) {
+      Read* rd = ds->getReadFromID(r);
+      for (int side = 0; side < 2; side++) {
+        vector<Edge*>* le = side ? rd->getListOfEdgesReverse() : rd->getListOfEdgesForward();
+        vector<UINT64>* ll = side ? rd->getLocationOnEdgeReverse() : rd->getLocationOnEdgeForward();
+        for (size_t q = 0; q < le->size(); q++) {
+          Edge* e = le->at(q);
+          fprintf(out, "%c %llu %llu %llu %u %llu %llu\n", side ? 'R' : 'F', (unsigned long long)r,
+                  (unsigned long long)e->getSourceRead()->getReadNumber(),
+                  (unsigned long long)e->getDestinationRead()->getReadNumber(), (unsigned)e->getOrientation(),
+                  (unsigned long long)e->getOverlapOffset(), (unsigned long long)ll->at(q));
+        }
+      }
+    }
+    og->sortEdges();
+    og->saveGraphToFile(string(argv[4]) + ".unitig");
   } else if (!strcmp(mode, "lookup")) {
     HashTable* ht = new HashTable();
     ht->insertDataset(ds, l);

@@ -18,7 +18,14 @@ Only runs in the build container (the reference is not on the GPU box).
                          before contraction (ref_harness bfs; OverlapGraph.cpp:
                          107-209), with numberOfNodes / numberOfEdges in the json
 
-Usage: python tests/golden/make_golden.py [--big] | --bfs
+  <name>.unitig.gz       (--unitig) the .unitig checkpoint main.cpp:47-50 writes
+                         (contraction loop OverlapGraph.cpp:211-215, sortEdges,
+                         saveGraphToFile :1219-1261; ref_harness unitig)
+  <name>.ulists.gz       (--unitig) the contracted graph[u] lists in list order
+                         with each edge's read lists, then every read's location
+                         lists (Read.h:39-42), before sortEdges
+
+Usage: python tests/golden/make_golden.py [--big] | --bfs | --branchy | --unitig
 """
 from __future__ import annotations
 
@@ -187,9 +194,105 @@ def add_bfs():
         print(f"{meta['name']}: bfs nodes={nodes} edges={edges}")
 
 
+def run_unitig(path: str, l: int):
+    with tempfile.TemporaryDirectory() as td:
+        out = os.path.join(td, "u.txt")
+        subprocess.run([HARNESS, "unitig", path, str(l), out], check=True)
+        head, lists = {}, []
+        with open(out) as f:
+            for line in f:
+                if line.startswith("#"):
+                    k, *v = line.split()
+                    head[k] = v
+                else:
+                    lists.append(line)
+        with open(out + ".unitig") as f:
+            unitig = f.read()
+    return head, "".join(lists), unitig
+
+
+def add_unitig():
+    """Attach the reference's contracted graph and .unitig file to every fixture."""
+    for fn in sorted(os.listdir(HERE)):
+        if not fn.endswith(".json"):
+            continue
+        with open(os.path.join(HERE, fn)) as f:
+            meta = json.load(f)
+        with tempfile.TemporaryDirectory() as td:
+            if meta.get("input"):
+                path = os.path.join(td, meta["input"][:-3])
+                with gzip.open(os.path.join(HERE, meta["input"]), "rb") as g, open(path, "wb") as o:
+                    o.write(g.read())
+            else:  # C1: regenerate from the recipe
+                r = meta["recipe"]
+                c, L = synth.uniform_read_set(r["n_reads"], r["read_len"], r["genome_len"], r["seed"])
+                path = os.path.join(td, "in.fa")
+                synth.write_fasta(path, strs(c, L))
+            head, lists, unitig = run_unitig(path, meta["l"])
+        meta["unitig"] = {
+            "nodes": int(head["#C"][0]), "edges": int(head["#C"][1]), "iterations": int(head["#I"][0]),
+            "lists_sha256": hashlib.sha256(lists.encode()).hexdigest(),
+            "unitig_sha256": hashlib.sha256(unitig.encode()).hexdigest(),
+            # one record per undirected edge; both halves of a self-loop sit in the same list
+            "unitig_records": sum(1 for ln in lists.splitlines() if ln[0].isdigit()
+                                  and int(ln.split()[0]) < int(ln.split()[1]))
+            + sum(1 for ln in lists.splitlines() if ln[0].isdigit()
+                  and int(ln.split()[0]) == int(ln.split()[1])) // 2,
+        }
+        if meta.get("input"):
+            meta["unitig"]["file"] = meta["name"] + ".unitig.gz"
+            meta["unitig"]["lists_file"] = meta["name"] + ".ulists.gz"
+            with gzip.GzipFile(os.path.join(HERE, meta["unitig"]["file"]), "wb", mtime=0) as g:
+                g.write(unitig.encode())
+            with gzip.GzipFile(os.path.join(HERE, meta["unitig"]["lists_file"]), "wb", mtime=0) as g:
+                g.write(lists.encode())
+        with open(os.path.join(HERE, fn), "w") as f:
+            json.dump(meta, f, indent=1, sort_keys=True)
+        print(f"{meta['name']}: unitig nodes={meta['unitig']['nodes']} edges={meta['unitig']['edges']} "
+              f"iterations={meta['unitig']['iterations']}")
+
+
+def branchy():
+    """Contraction stress set: a 12 kb genome with a 300 bp repeat at four
+    places (two of them reverse-complemented), an inverted-repeat hairpin, a
+    low-coverage stretch, and 1-substitution reads (tips and bubbles), so that
+    merges, dead-end removal over several loop iterations, self-loops and
+    multi-edges all occur."""
+    rng = np.random.default_rng(77)
+    G = synth.codes_to_strings(synth.random_genome(12000, 78)[None, :], np.array([12000]))[0]
+    R = synth.codes_to_strings(synth.random_genome(300, 79)[None, :], np.array([300]))[0]
+    H = G[500:700]
+    g = (G[:2000] + R + G[2000:4500] + synth.revcomp_str(R) + G[4500:6000] + H + "ACGT" + synth.revcomp_str(H)
+         + G[6000:8500] + R + G[8500:10500] + synth.revcomp_str(R) + G[10500:])
+    gc = np.frombuffer(g.encode(), dtype=np.uint8)
+    codes = np.searchsorted(synth.ALPHABET, gc).astype(np.uint8)
+    c, L = synth.sample_reads(codes, 2600, 90, 150, seed=80)
+    seqs = strs(c, L)
+    # thin one stretch out (coverage gaps -> dead ends) and add errors
+    lo, hi = 7000, 9000
+    out = []
+    for s in seqs:
+        p = g.find(s)
+        if p < 0:
+            p = g.find(synth.revcomp_str(s))
+        if lo <= p < hi and rng.random() < 0.75:
+            continue
+        if rng.random() < 0.06:
+            q = int(rng.integers(5, len(s) - 5))
+            s = s[:q] + "ACGT"[("ACGT".index(s[q]) + int(rng.integers(1, 4))) % 4] + s[q + 1:]
+        out.append(s)
+    emit("branchy", out, 40, lookups=True)
+
+
 def main():
     if "--bfs" in sys.argv:
         add_bfs()
+        return
+    if "--unitig" in sys.argv:
+        add_unitig()
+        return
+    if "--branchy" in sys.argv:
+        branchy()
         return
     big = "--big" in sys.argv
     # 1. fixed-length uniform set (SURVEY §0 "small")

@@ -356,13 +356,59 @@ def test_cli_graph_matches_reference(tmp_path, name):
     meta = load_meta(name)
     exe = os.path.join(ROOT, "metagenomics_amd", "lib", "mg_overlap")
     prefix = str(tmp_path / name)
-    subprocess.run([exe, "-se", "1", fixture_input(name), "-f", prefix, "-l", str(meta["l"])], check=True,
-                   stdout=subprocess.DEVNULL, timeout=120)
+    subprocess.run([exe, "-se", "1", fixture_input(name), "-f", prefix, "-l", str(meta["l"]), "-nocontract"],
+                   check=True, stdout=subprocess.DEVNULL, timeout=120)
     lines = open(prefix + ".graph").read().split("\n")
     _, nodes, edges = lines[0].split()
     assert (int(nodes), int(edges)) == (meta["bfs"]["nodes"], meta["bfs"]["edges"])
     with gzip.open(os.path.join(GOLDEN, meta["bfs"]["file"]), "rt") as f:
         assert [x for x in lines[1:] if x] == [x for x in f.read().split("\n") if x]
+
+
+@pytest.mark.parametrize("name", FIXTURES)
+def test_cli_unitig_matches_reference(tmp_path, name):
+    """main.cpp:45-50 end to end through the C++ drop-in: the .unitig checkpoint
+    (contraction loop OverlapGraph.cpp:211-215, sortEdges, saveGraphToFile)
+    equals the reference's byte for byte."""
+    import gzip
+    import os
+    import subprocess
+
+    from conftest import GOLDEN, ROOT
+
+    meta = load_meta(name)
+    exe = os.path.join(ROOT, "metagenomics_amd", "lib", "mg_overlap")
+    prefix = str(tmp_path / name)
+    subprocess.run([exe, "-se", "1", fixture_input(name), "-f", prefix, "-l", str(meta["l"])], check=True,
+                   stdout=subprocess.DEVNULL, timeout=120)
+    with gzip.open(os.path.join(GOLDEN, meta["unitig"]["file"]), "rt") as f:
+        assert open(prefix + ".unitig").read() == f.read()
+
+
+@pytest.mark.parametrize("name", ["branchy", "tandem"])
+def test_device_rows_to_unitig(name, tmp_path):
+    """Device discovery rows (any order) -> replay -> contraction: the lists,
+    read locations and .unitig equal the reference's."""
+    import gzip
+    import os
+
+    from conftest import GOLDEN
+    from metagenomics_amd.overlap import UnitigGraph
+
+    meta = load_meta(name)
+    ds = Dataset.from_files([fixture_input(name)], meta["l"])
+    e = OverlapEngine(0)
+    rows, _ = gpu_rows(e, ds, meta["l"])
+    e.close()
+    g = UnitigGraph(rows, ds.packed()[1], meta["l"])
+    assert (g.nodes, g.edges) == (meta["unitig"]["nodes"], meta["unitig"]["edges"])
+    g.save_lists(str(tmp_path / "lists"))
+    with gzip.open(os.path.join(GOLDEN, meta["unitig"]["lists_file"]), "rt") as f:
+        assert (tmp_path / "lists").read_text() == f.read()
+    g.sort_edges()
+    g.save_unitig(str(tmp_path / "u"))
+    with gzip.open(os.path.join(GOLDEN, meta["unitig"]["file"]), "rt") as f:
+        assert (tmp_path / "u").read_text() == f.read()
 
 
 @pytest.mark.parametrize("name", ["mixed", "tandem", "highdup", "dirty"])
