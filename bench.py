@@ -144,7 +144,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-ingest", action="store_true", help="skip the device Dataset ingest measurement")
     ap.add_argument("--replay", action="store_true",
-                    help="also time the host replay of the exploration + transitive reduction on the rows")
+                    help="also time the host replay of the exploration + transitive reduction + contraction on the rows")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r01s2_pmc_c3.json"))
     ap.add_argument("--nb-log2", type=int, default=0)
     ap.add_argument("--split-probe", action="store_true", help="probe -> candidates -> verify kernels (option split = 1)")
@@ -313,15 +313,17 @@ def main():
         "roofline": roof,
     }
     if world == 1 and mode == "fused" and args.replay:
-        from metagenomics_amd.overlap import replay_graph
+        from metagenomics_amd.overlap import UnitigGraph
 
         t0 = time.perf_counter()
         allrows = engines[0].rows(rows)
         t1 = time.perf_counter()
-        nodes, dedges, _ = replay_graph(allrows, ds.packed()[1], l)
-        t2 = time.perf_counter()
-        res["graph_replay"] = {"copy_rows_s": t1 - t0, "replay_s": t2 - t1, "nodes": nodes,
-                               "edges_after_reduction": dedges, "threads": 1}
+        ug = UnitigGraph(allrows, ds.packed()[1], l)
+        res["graph_replay"] = {"copy_rows_s": t1 - t0, "replay_s": ug.replay_s, "nodes": ug.replay_nodes,
+                               "edges_after_reduction": ug.replay_edges, "contract_s": ug.contract_s,
+                               "unitig_nodes": ug.nodes, "unitig_edges": ug.edges,
+                               "contract_iterations": ug.iterations, "threads": 1}
+        ug.close()
         del allrows
     if world == 1 and mode == "fused" and not args.no_ingest:
         try:

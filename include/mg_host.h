@@ -1,7 +1,7 @@
 /* mg_host.h — C-ABI over the host-side Dataset mirror (metagenomics_amd/csrc/host).
  *
- * Dataset ingestion is not on the GPU in this round;
- * it is the reference's Dataset semantics restated in C++ with packed reads:
+ * The host Dataset mirror (the device version is mg_ingest_* in mg_overlap.h)
+ * is the reference's Dataset semantics restated in C++ with packed reads:
  *   readDataset  Dataset.cpp:110-193  (FASTA/FASTQ parse, upper-case)
  *   testRead     Dataset.cpp:398-413  (only ACGT, no base >= floor(0.8 len))
  *   canonical    Dataset.cpp:163-167  (store min(s, revcomp(s)))
@@ -43,6 +43,23 @@ uint32_t mgh_frequency(const mgh_dataset* ds, uint64_t id); /* Read::getFrequenc
 /* Dataset::getReadFromString (Dataset.cpp:421-455): ID of a read given either
  * strand, 0 if absent. */
 uint64_t mgh_find_read(const mgh_dataset* ds, const char* s, uint64_t len);
+
+/* --- record splitting -------------------------------------
+ * Dataset::readDataset's record splitting (Dataset.cpp:110-193) on a
+ * memory-mapped file with nthreads host threads (<= 0: all): FASTA = header
+ * line, then everything up to the next '>' with '\n' removed; FASTQ = the 2nd
+ * of every 4 lines.  Record i's raw sequence (bytes as in the file, before
+ * upper-casing / testRead) is text[off[i] .. off[i+1]); n_records + 1 offsets.
+ * The outputs are malloc'ed: release with mgh_parse_free.  They are the input
+ * mg_ingest_ascii (include/mg_overlap.h) takes.  0 = ok, -1 = cannot open,
+ * -2 = unknown format (first byte not '>' / '@'), -3 = out of memory. */
+int mgh_parse_file(const char* path, int nthreads, char** text, uint64_t** offsets, uint64_t* n_records,
+                   double* seconds);
+int mgh_parse_buffer(const char* buf, uint64_t n, int nthreads, char** text, uint64_t** offsets,
+                     uint64_t* n_records, double* seconds);
+void mgh_parse_free(void* p);
+/* smallest chunk one thread splits (default 1 MiB; 0 restores it) */
+void mgh_parse_set_min_chunk(uint64_t bytes);
 
 /* --- graph construction order ----------------------------
  * Replays OverlapGraph::buildOverlapGraphFromHashTable's exploration and

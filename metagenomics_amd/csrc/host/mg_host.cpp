@@ -8,6 +8,7 @@
 #include <atomic>
 #include <cctype>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <fstream>
 #include <iomanip>
@@ -15,6 +16,7 @@
 #include <thread>
 
 #include "mg_api.hpp"
+#include "mg_parse.hpp"
 #include "mg_unitig.hpp"
 #include "mg_graph.hpp"
 #include "mg_host.h"
@@ -231,43 +233,6 @@ PackedReads ingest(const Source& src, uint64_t min_overlap, int nthreads) {
   return pr;
 }
 
-// Dataset::readDataset record splitting (Dataset.cpp:123-182): FASTA = header
-// line + everything up to the next '>' with '\n' removed; FASTQ = 4 lines, the
-// sequence is the 2nd.  Appends raw sequences to text/off.
-int parse_file(const std::string& path, std::string& text, std::vector<uint64_t>& off) {
-  std::ifstream f(path, std::ios::binary);
-  if (!f) return -1;
-  std::string buf((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
-  if (buf.empty() || (buf[0] != '>' && buf[0] != '@')) return -2;  // Dataset.cpp:130-135
-  const size_t n = buf.size();
-  size_t p = 0;
-  if (buf[0] == '>') {
-    while (p < n) {
-      while (p < n && buf[p] != '\n') p++;
-      if (p < n) p++;
-      const size_t nb = buf.find('>', p);
-      const size_t e = nb == std::string::npos ? n : nb;
-      for (size_t k = p; k < e; ++k)
-        if (buf[k] != '\n') text.push_back(buf[k]);
-      off.push_back(text.size());
-      p = e == n ? n : e + 1;
-    }
-  } else {
-    uint64_t line = 0;
-    while (p < n) {
-      size_t e = buf.find('\n', p);
-      if (e == std::string::npos) e = n;
-      if (line % 4 == 1) {
-        text.append(buf, p, e - p);
-        off.push_back(text.size());
-      }
-      p = e + 1;
-      line++;
-    }
-  }
-  return 0;
-}
-
 std::string decode_packed(const uint64_t* w, uint16_t L, bool reverse) {
   static const char A[4] = {'A', 'C', 'G', 'T'};
   std::string s(L, 'A');
@@ -314,7 +279,7 @@ Dataset::Dataset(std::vector<std::string> pe, std::vector<std::string> se, UINT6
   std::vector<std::string> files(pe);
   files.insert(files.end(), se.begin(), se.end());  // paired-end first (Dataset.cpp:52-60)
   for (const auto& f : files) {
-    const int rc = mg::parse_file(f, text, off);
+    const int rc = mg::parse_file_parallel(f, text, off, 0);  // Dataset.cpp:110-193
     if (rc == -1) throw mg::Error("Unable to open file: " + f);
     if (rc == -2) throw mg::Error("Unknown input file format: " + f);
   }
@@ -902,5 +867,58 @@ uint64_t mgh_graph_unitig_edges(const mgh_graph* g, mgh_unitig_edge* edges, uint
   if (n_reads_total) *n_reads_total = r;
   return k;
 }
+
+namespace {
+int parse_out(int rc, std::string& text, std::vector<uint64_t>& off, const mg::ParseStats& st, char** text_out,
+              uint64_t** off_out, uint64_t* n_records, double* seconds) {
+  if (rc) return rc;
+  char* t = static_cast<char*>(std::malloc(std::max<size_t>(text.size(), 1)));
+  uint64_t* o = static_cast<uint64_t*>(std::malloc(off.size() * sizeof(uint64_t)));
+  if (!t || !o) {
+    std::free(t);
+    std::free(o);
+    return -3;
+  }
+  std::memcpy(t, text.data(), text.size());
+  std::memcpy(o, off.data(), off.size() * sizeof(uint64_t));
+  *text_out = t;
+  *off_out = o;
+  *n_records = off.size() - 1;
+  if (seconds) *seconds = st.seconds;
+  return 0;
+}
+}  // namespace
+
+int mgh_parse_file(const char* path, int nthreads, char** text_out, uint64_t** off_out, uint64_t* n_records,
+                   double* seconds) {
+  if (!path || !text_out || !off_out || !n_records) return -1;
+  try {
+    std::string text;
+    std::vector<uint64_t> off(1, 0);
+    mg::ParseStats st;
+    const int rc = mg::parse_file_parallel(path, text, off, nthreads, &st);
+    return parse_out(rc, text, off, st, text_out, off_out, n_records, seconds);
+  } catch (const std::exception&) {
+    return -3;
+  }
+}
+
+int mgh_parse_buffer(const char* buf, uint64_t n, int nthreads, char** text_out, uint64_t** off_out,
+                     uint64_t* n_records, double* seconds) {
+  if ((!buf && n) || !text_out || !off_out || !n_records) return -1;
+  try {
+    std::string text;
+    std::vector<uint64_t> off(1, 0);
+    mg::ParseStats st;
+    const int rc = mg::parse_buffer_parallel(buf, n, text, off, nthreads, &st);
+    return parse_out(rc, text, off, st, text_out, off_out, n_records, seconds);
+  } catch (const std::exception&) {
+    return -3;
+  }
+}
+
+void mgh_parse_free(void* p) { std::free(p); }
+
+void mgh_parse_set_min_chunk(uint64_t bytes) { mg::g_parse_min_chunk = bytes ? bytes : (1 << 20); }
 
 }  // extern "C"

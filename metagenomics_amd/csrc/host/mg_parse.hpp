@@ -1,0 +1,34 @@
+// mg_parse.hpp — INTERNAL: parallel FASTA/FASTQ record splitter with the
+// reference's readDataset semantics (Dataset.cpp:110-193).  See mg_parse.cpp.
+#ifndef MG_PARSE_HPP_
+#define MG_PARSE_HPP_
+#include <cstdint>
+#include <string>
+#include <vector>
+
+namespace mg {
+
+struct ParseStats {
+  uint64_t bytes = 0;    // file size
+  uint64_t records = 0;  // records split (good and bad)
+  double seconds = 0;    // map + split + gather wall time
+  int threads = 1;
+};
+
+// Appends every record's raw sequence (bytes as in the file, '\n' removed) to
+// text and its end offset to off (off must hold the start offset already).
+// 0 = ok, -1 = cannot open / map, -2 = first byte neither '>' nor '@'
+// (the reference's "Unknown input file format.", Dataset.cpp:130-135).
+// nthreads <= 0: hardware threads.
+int parse_file_parallel(const std::string& path, std::string& text, std::vector<uint64_t>& off, int nthreads,
+                        ParseStats* stats = nullptr);
+
+// smallest chunk a thread gets (bytes; tests lower it to exercise the chunk seams)
+extern uint64_t g_parse_min_chunk;
+
+// The same on a buffer already in memory.
+int parse_buffer_parallel(const char* buf, uint64_t n, std::string& text, std::vector<uint64_t>& off, int nthreads,
+                          ParseStats* stats = nullptr);
+
+}  // namespace mg
+#endif  // MG_PARSE_HPP_

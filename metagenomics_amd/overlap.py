@@ -9,6 +9,7 @@ from __future__ import annotations
 
 import ctypes as C
 import os
+import time
 from typing import Iterable, Sequence
 
 import numpy as np
@@ -107,6 +108,10 @@ def lib() -> C.CDLL:
         "mgh_graph_nodes": (u64, [vp]),
         "mgh_graph_edges": (u64, [vp]),
         "mgh_graph_rows": (u64, [vp, vp, u64]),
+        "mgh_parse_file": (i32, [C.c_char_p, i32, P(vp), P(vp), P(u64), P(C.c_double)]),
+        "mgh_parse_buffer": (i32, [vp, u64, i32, P(vp), P(vp), P(u64), P(C.c_double)]),
+        "mgh_parse_free": (None, [vp]),
+        "mgh_parse_set_min_chunk": (None, [u64]),
         "mgh_graph_contract": (i32, [vp, i32, P(u64), P(u64), P(u64)]),
         "mgh_graph_sort_edges": (i32, [vp]),
         "mgh_graph_save_unitig": (i32, [vp, C.c_char_p]),
@@ -436,6 +441,48 @@ def replay_graph(rows: np.ndarray, lens: np.ndarray, min_overlap: int):
         L.mgh_graph_free(g)
 
 
+def _parse_result(L, rc, t, o, n, what):
+    if rc:
+        raise MgError({-1: f"Unable to open file: {what}", -2: f"Unknown input file format: {what}"}.get(
+            rc, f"parse failed ({rc})"))
+    try:
+        offs = np.ctypeslib.as_array(C.cast(o, C.POINTER(C.c_uint64)), shape=(n.value + 1,)).copy()
+        size = int(offs[-1])
+        text = (np.ctypeslib.as_array(C.cast(t, C.POINTER(C.c_uint8)), shape=(size,)).copy() if size
+                else np.zeros(0, np.uint8))
+    finally:
+        L.mgh_parse_free(t)
+        L.mgh_parse_free(o)
+    return text, offs
+
+
+def parse_file(path: str, nthreads: int = 0):
+    """Dataset::readDataset's record splitting (Dataset.cpp:110-193) on a
+    memory-mapped file with all host threads (mgh_parse_file).  Returns
+    (text uint8, offsets uint64[n+1], seconds): record i's raw sequence is
+    text[offsets[i]:offsets[i+1]], the input of OverlapEngine.ingest_ascii."""
+    L = lib()
+    t, o, n, sec = C.c_void_p(), C.c_void_p(), C.c_uint64(), C.c_double()
+    rc = L.mgh_parse_file(os.fsencode(path), nthreads, C.byref(t), C.byref(o), C.byref(n), C.byref(sec))
+    text, offs = _parse_result(L, rc, t, o, n, path)
+    return text, offs, sec.value
+
+
+def parse_buffer(data: bytes, nthreads: int = 0, min_chunk: int = 0):
+    """parse_file on bytes in memory; min_chunk > 0 lowers the per-thread chunk
+    size (tests: exercises the chunk seams on small inputs)."""
+    L = lib()
+    buf = np.frombuffer(data, dtype=np.uint8) if len(data) else np.zeros(1, np.uint8)
+    t, o, n, sec = C.c_void_p(), C.c_void_p(), C.c_uint64(), C.c_double()
+    L.mgh_parse_set_min_chunk(min_chunk)
+    try:
+        rc = L.mgh_parse_buffer(_ptr(buf), len(data), nthreads, C.byref(t), C.byref(o), C.byref(n), C.byref(sec))
+    finally:
+        L.mgh_parse_set_min_chunk(0)
+    text, offs = _parse_result(L, rc, t, o, n, "<buffer>")
+    return text, offs
+
+
 UNITIG_EDGE_DTYPE = np.dtype({"names": ["src", "dst", "offset", "n_reads", "orient"],
                               "formats": ["<u4", "<u4", "<u8", "<u4", "u1"],
                               "offsets": [0, 4, 8, 16, 20], "itemsize": 24})
@@ -453,16 +500,19 @@ class UnitigGraph:
         lens = np.ascontiguousarray(lens, dtype=np.uint16)
         L = self._L = lib()
         self._g = C.c_void_p()
+        t0 = time.perf_counter()
         rc = L.mgh_graph_replay(_ptr(rows), rows.shape[0], _ptr(lens), lens.shape[0], min_overlap - 1,
                                 C.byref(self._g))
         if rc:
             raise MgError(f"graph replay failed ({rc})")
         self.replay_nodes, self.replay_edges = int(L.mgh_graph_nodes(self._g)), int(L.mgh_graph_edges(self._g))
+        t1 = time.perf_counter()
         it, merged, dead = C.c_uint64(), C.c_uint64(), C.c_uint64()
         rc = L.mgh_graph_contract(self._g, int(track_locations), C.byref(it), C.byref(merged), C.byref(dead))
         if rc:
             self.close()
             raise MgError(f"contraction failed ({rc})")
+        self.replay_s, self.contract_s = t1 - t0, time.perf_counter() - t1
         self.iterations, self.merged, self.dead_end_nodes = it.value, merged.value, dead.value
 
     @property

@@ -122,3 +122,47 @@ def sorted_tuples(rows) -> np.ndarray:
     r = rows[order]
     return np.stack([r["src"].astype(np.int64), r["dst"].astype(np.int64), r["orient"].astype(np.int64),
                      r["offset"].astype(np.int64)], axis=1)
+
+
+def readdataset_records(data: bytes) -> list:
+    """Dataset::readDataset's record splitting (Dataset.cpp:110-193), restated
+    with libstdc++'s getline semantics: getline erases its string only when the
+    stream is still good on entry, so after EOF a record keeps the previous
+    string (a FASTA file that ends inside a header line yields that header as
+    the last record's sequence).  Returns the raw sequence of every record,
+    good or bad, in file order (bytes as in the file, before upper-casing).
+    Pure Python: small inputs only."""
+    if not data or data[:1] not in (b">", b"@"):
+        raise ValueError("Unknown input file format.")  # :126-135
+    n = len(data)
+    st = {"pos": 0, "eof": False, "fail": False}
+
+    def getline(cur: bytes, delim: bytes) -> bytes:
+        if st["eof"] or st["fail"]:  # sentry fails: failbit, string untouched
+            st["fail"] = True
+            return cur
+        p = st["pos"]
+        q = data.find(delim, p)
+        if q < 0:  # runs into EOF
+            st["eof"] = True
+            if p == n:
+                st["fail"] = True
+            st["pos"] = n
+            return data[p:]
+        st["pos"] = q + 1
+        return data[p:q]
+
+    recs, text = [], b""
+    fasta = data[:1] == b">"
+    while not st["eof"]:  # while(!myFile.eof())
+        if fasta:
+            text = getline(text, b"\n")
+            text = getline(text, b">")
+            recs.append(text.replace(b"\n", b""))
+        else:
+            lines = []
+            for _ in range(4):
+                text = getline(text, b"\n")
+                lines.append(text)
+            recs.append(lines[1])
+    return recs

@@ -31,6 +31,8 @@
 //        since the reference inlines it ahead of the contraction at :211-215).
 //        Writes "#C <numberOfNodes> <numberOfEdges>" and every graph[u] list
 //        IN LIST ORDER as "u v orient offset" rows.
+//   dataset <fasta> <l> <out>  : Dataset(pe={}, se={fa}, l) only: "#N <unique>",
+//        "#G <numberOfReads>", "#R <id> <string>" (Dataset.cpp:39-65,110-193).
 //   unitig <fasta> <l> <out>   : as bfs, then the reference's own contraction
 //        loop (OverlapGraph.cpp:211-215: contractCompositePaths +
 //        removeDeadEndNodes until neither changes anything), i.e. the graph
@@ -157,7 +159,11 @@ int main(int argc, char** argv) {
   double t_ds = now_s() - t0;
   UINT64 N = ds->getNumberOfUniqueReads();
 
-  if (!strcmp(mode, "time")) {
+  if (!strcmp(mode, "dataset")) {
+    fprintf(out, "#N %llu\n#G %llu\n", (unsigned long long)N, (unsigned long long)ds->getNumberOfReads());
+    for (UINT64 i = 1; i <= N; i++)
+      fprintf(out, "#R %llu %s\n", (unsigned long long)i, ds->getReadFromID(i)->getStringForward().c_str());
+  } else if (!strcmp(mode, "time")) {
     double t1 = now_s();
     HashTable* ht = new HashTable();
     ht->insertDataset(ds, l);

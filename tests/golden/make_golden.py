@@ -25,7 +25,11 @@ Only runs in the build container (the reference is not on the GPU box).
                          with each edge's read lists, then every read's location
                          lists (Read.h:39-42), before sortEdges
 
-Usage: python tests/golden/make_golden.py [--big] | --bfs | --branchy | --unitig
+  parse_cases.json       (--parse) hand-made FASTA/FASTQ files with the reference
+                         Dataset's unique reads (ref_harness dataset): the record
+                         splitting quirks of Dataset.cpp:110-193
+
+Usage: python tests/golden/make_golden.py [--big] | --bfs | --branchy | --unitig | --parse
 """
 from __future__ import annotations
 
@@ -284,7 +288,58 @@ def branchy():
     emit("branchy", out, 40, lookups=True)
 
 
+PARSE_CASES = [
+    # name, ext, l, text
+    ("fasta_basic", ".fa", 10, ">a\nACGTACGTACGTAC\n>b desc\nTTTTGGGGCCCCAAAT\n"),
+    ("fasta_wrapped_crlf", ".fa", 10, ">a\nACGTAC\nGTACGTAC\n>b\r\nACGTACGTAAAC\r\nGG\r\n>c\nGATTACAGATTACA"),
+    ("fasta_gt_in_header", ".fa", 10, ">a x>y>z\nACGTACGTACGTTT\n>b\nCCAGTACGTACGTTG\n"),
+    ("fasta_gt_mid_sequence", ".fa", 8, ">a\nACGTACGTAC>GTACGTACGATCG\nTTGACCATGA\n"),
+    ("fasta_lowercase_n", ".fa", 8, ">a\nacgtacgtacgtaa\n>b\nACGTNACGTACGTA\n>c\nAAAAAAAAAAAAAC\n"),
+    ("fasta_empty_records", ".fa", 8, ">a\n>b\n\n>c\nACGGTCAGTTACGA\n>\n"),
+    ("fasta_tail_header_no_newline", ".fa", 20,
+     ">r1\nCCGTAATGCCTTTCCCTAACAGAGTTTTTCGAACTCG\n>tcagttaaatggcagaaaactggcagggcttttagtcgtgg"),
+    ("fasta_tail_header_newline", ".fa", 20, ">r1\nCCGTAATGCCTTTCCCTAACAGAGTTTTTCGAACTCG\n>acgtacgtacgtacgtacgtacgtaa\n"),
+    # (a file with no good read at all makes the reference crash: not a case)
+    ("fastq_basic", ".fq", 8, "@a\nACGTACGTACGTAC\n+\nIIIIIIIIIIIIII\n@b\nTTGGCCAAGTCAGT\n+\nIIIIIIIIIIIIII\n"),
+    ("fastq_no_trailing_newline", ".fq", 8, "@a\nACGTACGTACGTAC\n+\nIIIIIIIIIIIIII\n@b\nTTGGCCAAGTCAGT\n+\nIIIIIIIIIIIIII"),
+    ("fastq_truncated_record", ".fq", 8, "@a\nACGTACGTACGTAC\n+\nIIIIIIIIIIIIII\n@b\nTTGGCCAAGTCAGTGG"),
+    ("fastq_truncated_after_seq", ".fq", 8, "@a\nACGTACGTACGTAC\n+\nIIIIIIIIIIIIII\n@b\nTTGGCCAAGTCAGTGG\n"),
+    ("fastq_at_in_quality", ".fq", 8, "@a\nACGTACGTACGTAC\n+\n@@@@@@@@@@@@@@\n@b\nTTGGCCAAGTCAGT\n+\n>>>>>>>>>>>>>>\n"),
+    ("fastq_crlf", ".fq", 8, "@a\r\nACGTACGTACGTAC\r\n+\r\nIIIIIIIIIIIIII\r\n@b\nTTGGCCAAGTCAGT\n+\nIIIIIIIIIIIIII\n"),
+    ("fastq_blank_lines", ".fq", 8, "@a\nACGTACGTACGTAC\n+\nIIIIIIIIIIIIII\n\n\n@b\nTTGGCCAAGTCAGT\n+\nIIIIIIIIIIIIII\n"),
+]
+
+
+def add_parse_cases():
+    out = []
+    for name, ext, l, text in PARSE_CASES:
+        with tempfile.TemporaryDirectory() as td:
+            path = os.path.join(td, "in" + ext)
+            with open(path, "w", newline="") as f:
+                f.write(text)
+            res = os.path.join(td, "out.txt")
+            subprocess.run([HARNESS, "dataset", path, str(l), res], check=True)
+            reads, n, g = {}, 0, 0
+            with open(res) as f:
+                for line in f:
+                    k, *v = line.split()
+                    if k == "#N":
+                        n = int(v[0])
+                    elif k == "#G":
+                        g = int(v[0])
+                    elif k == "#R":
+                        reads[int(v[0])] = v[1]
+        out.append({"name": name, "ext": ext, "l": l, "input": text, "n_unique": n, "n_reads": g,
+                    "ids_sha256": ids_digest(reads), "reads": [reads[i] for i in sorted(reads)]})
+        print(f"{name}: reads={g} unique={n}")
+    with open(os.path.join(HERE, "parse_cases.json"), "w") as f:
+        json.dump(out, f, indent=1)
+
+
 def main():
+    if "--parse" in sys.argv:
+        add_parse_cases()
+        return
     if "--bfs" in sys.argv:
         add_bfs()
         return
