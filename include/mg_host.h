@@ -55,6 +55,9 @@ uint64_t mgh_find_read(const mgh_dataset* ds, const char* s, uint64_t len);
  * -2 = unknown format (first byte not '>' / '@'), -3 = out of memory. */
 int mgh_parse_file(const char* path, int nthreads, char** text, uint64_t** offsets, uint64_t* n_records,
                    double* seconds);
+/* several files, concatenated in order (Dataset.cpp:52-60 reads paired-end files first) */
+int mgh_parse_files(const char* const* paths, int nfiles, int nthreads, char** text, uint64_t** offsets,
+                    uint64_t* n_records, double* seconds);
 int mgh_parse_buffer(const char* buf, uint64_t n, int nthreads, char** text, uint64_t** offsets,
                      uint64_t* n_records, double* seconds);
 void mgh_parse_free(void* p);

@@ -274,20 +274,28 @@ UINT32 Read::getFrequency() { return owner->frequencyOf(readNumber); }
 // =============================================================== Dataset ====
 Dataset::Dataset(std::vector<std::string> pe, std::vector<std::string> se, UINT64 minOverlap)
     : pairedEndDatasetFileNames(pe), singleEndDatasetFileNames(se), minOverlapLength(minOverlap) {
-  std::string text;
-  std::vector<uint64_t> off(1, 0);
+  mg::ParsedText parsed;
   std::vector<std::string> files(pe);
   files.insert(files.end(), se.begin(), se.end());  // paired-end first (Dataset.cpp:52-60)
   for (const auto& f : files) {
-    const int rc = mg::parse_file_parallel(f, text, off, 0);  // Dataset.cpp:110-193
+    const int rc = mg::parse_file_parallel(f, parsed, 0);  // Dataset.cpp:110-193
+    if (rc) parsed.release();
     if (rc == -1) throw mg::Error("Unable to open file: " + f);
     if (rc == -2) throw mg::Error("Unknown input file format: " + f);
+    if (rc) throw mg::Error("Out of memory reading " + f);
   }
+  static const uint64_t kNoOffsets[1] = {0};
   mg::Source src;
-  src.text = text.data();
-  src.off = off.data();
-  src.n = off.size() - 1;
-  finalize(mg::ingest(src, minOverlap, 0));
+  src.text = parsed.text;
+  src.off = parsed.n_rec ? parsed.off : kNoOffsets;
+  src.n = parsed.n_rec;
+  try {
+    finalize(mg::ingest(src, minOverlap, 0));
+  } catch (...) {
+    parsed.release();
+    throw;
+  }
+  parsed.release();
 }
 
 Dataset* Dataset::fromCodes(const uint8_t* codes, uint64_t n, uint64_t stride, const uint16_t* lens,
@@ -869,21 +877,20 @@ uint64_t mgh_graph_unitig_edges(const mgh_graph* g, mgh_unitig_edge* edges, uint
 }
 
 namespace {
-int parse_out(int rc, std::string& text, std::vector<uint64_t>& off, const mg::ParseStats& st, char** text_out,
-              uint64_t** off_out, uint64_t* n_records, double* seconds) {
-  if (rc) return rc;
-  char* t = static_cast<char*>(std::malloc(std::max<size_t>(text.size(), 1)));
-  uint64_t* o = static_cast<uint64_t*>(std::malloc(off.size() * sizeof(uint64_t)));
-  if (!t || !o) {
-    std::free(t);
-    std::free(o);
-    return -3;
+int parse_out(int rc, mg::ParsedText& pt, const mg::ParseStats& st, char** text_out, uint64_t** off_out,
+              uint64_t* n_records, double* seconds) {
+  if (rc) {
+    pt.release();
+    return rc;
   }
-  std::memcpy(t, text.data(), text.size());
-  std::memcpy(o, off.data(), off.size() * sizeof(uint64_t));
-  *text_out = t;
-  *off_out = o;
-  *n_records = off.size() - 1;
+  if (!pt.off) {  // no record at all
+    pt.off = static_cast<uint64_t*>(std::calloc(1, sizeof(uint64_t)));
+    if (!pt.off) return -3;
+  }
+  if (!pt.text) pt.text = static_cast<char*>(std::malloc(1));
+  *text_out = pt.text;  // ownership passes to the caller (mgh_parse_free)
+  *off_out = pt.off;
+  *n_records = pt.n_rec;
   if (seconds) *seconds = st.seconds;
   return 0;
 }
@@ -891,30 +898,41 @@ int parse_out(int rc, std::string& text, std::vector<uint64_t>& off, const mg::P
 
 int mgh_parse_file(const char* path, int nthreads, char** text_out, uint64_t** off_out, uint64_t* n_records,
                    double* seconds) {
-  if (!path || !text_out || !off_out || !n_records) return -1;
+  return mgh_parse_files(&path, 1, nthreads, text_out, off_out, n_records, seconds);
+}
+
+int mgh_parse_files(const char* const* paths, int nfiles, int nthreads, char** text_out, uint64_t** off_out,
+                    uint64_t* n_records, double* seconds) {
+  if (!paths || nfiles < 0 || !text_out || !off_out || !n_records) return -1;
+  mg::ParsedText pt;
+  mg::ParseStats st;
+  double total = 0;
   try {
-    std::string text;
-    std::vector<uint64_t> off(1, 0);
-    mg::ParseStats st;
-    const int rc = mg::parse_file_parallel(path, text, off, nthreads, &st);
-    return parse_out(rc, text, off, st, text_out, off_out, n_records, seconds);
+    for (int i = 0; i < nfiles; ++i) {
+      if (!paths[i]) return parse_out(-1, pt, st, text_out, off_out, n_records, seconds);
+      const int rc = mg::parse_file_parallel(paths[i], pt, nthreads, &st);
+      total += st.seconds;
+      if (rc) return parse_out(rc, pt, st, text_out, off_out, n_records, seconds);
+    }
   } catch (const std::exception&) {
-    return -3;
+    return parse_out(-3, pt, st, text_out, off_out, n_records, seconds);
   }
+  st.seconds = total;
+  return parse_out(0, pt, st, text_out, off_out, n_records, seconds);
 }
 
 int mgh_parse_buffer(const char* buf, uint64_t n, int nthreads, char** text_out, uint64_t** off_out,
                      uint64_t* n_records, double* seconds) {
   if ((!buf && n) || !text_out || !off_out || !n_records) return -1;
+  mg::ParsedText pt;
+  mg::ParseStats st;
+  int rc;
   try {
-    std::string text;
-    std::vector<uint64_t> off(1, 0);
-    mg::ParseStats st;
-    const int rc = mg::parse_buffer_parallel(buf, n, text, off, nthreads, &st);
-    return parse_out(rc, text, off, st, text_out, off_out, n_records, seconds);
+    rc = mg::parse_buffer_parallel(buf, n, pt, nthreads, &st);
   } catch (const std::exception&) {
-    return -3;
+    rc = -3;
   }
+  return parse_out(rc, pt, st, text_out, off_out, n_records, seconds);
 }
 
 void mgh_parse_free(void* p) { std::free(p); }

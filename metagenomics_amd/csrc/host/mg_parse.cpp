@@ -21,10 +21,12 @@
 //   started in HDR or contains a '>'.  Chunk start states are composed
 //   sequentially from that (one value per chunk), then every chunk is split
 //   independently.
-// Each chunk is scanned twice with its start state known: once to size its
-// sequence bytes and records, once to write them straight into their final
-// place (no per-chunk staging copy).  The result equals the serial splitter's
-// (tests/test_parse.py).
+// Pass 1 sizes every chunk without knowing its start (FASTQ: bytes and records
+// per residue of the local line index; FASTA: for either start state); a
+// sequential sweep over one value per chunk resolves them; pass 2 writes every
+// chunk straight into its final place in an uninitialised (malloc'ed) buffer:
+// two reads of the file and one write of the sequences in all.  The result
+// equals the reference's record sequence (tests/test_parse.py).
 #include "mg_parse.hpp"
 
 #include <fcntl.h>
@@ -35,6 +37,7 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <thread>
 
@@ -73,31 +76,67 @@ inline const char* find(const char* p, const char* e, char ch) {
 }
 
 struct ChunkOut {
-  uint64_t bytes = 0, records = 0;  // pass-1 sizes
-  uint64_t text_base = 0, rec_base = 0;
+  // pass 1: FASTQ line statistics per residue of the local line index
+  uint64_t nl = 0;                      // '\n' inside the chunk
+  uint64_t fq_bytes[4] = {0, 0, 0, 0};  // bytes of the lines starting here, by local index mod 4
+  uint64_t fq_recs[4] = {0, 0, 0, 0};
+  bool lead_nl = false;                 // the chunk's first line start follows a '\n' inside it
+  // pass 1: FASTA, for either start state
+  bool has_nl = false, end_hdr = false, any_gt = false;
+  uint64_t fa_bytes_rest = 0, fa_close_rest = 0;  // from the first '\n' on (state SEQ there)
+  uint64_t fa_bytes_pre = 0, fa_close_pre = 0;    // before the first '\n' if the chunk starts in SEQ
+  // resolved
   uint64_t line_base = 0;  // FASTQ: '\n' before the chunk start
-  uint64_t nl = 0;         // FASTQ: '\n' inside the chunk
   bool start_hdr = false;  // FASTA: state at the chunk start
+  uint64_t bytes = 0, records = 0, text_base = 0, rec_base = 0;
 };
 
-// FASTQ: the lines starting in [b, e); emit(ptr, len) for every sequence line
+// first line start in [b, e) and its index relative to line_base; false = none
+inline bool first_line(const char* buf, uint64_t b, uint64_t e, const char** p, uint64_t* rel) {
+  if (b == 0 || buf[b - 1] == '\n') {
+    *p = buf + b;
+    *rel = 0;
+    return b < e;
+  }
+  const char* q = find(buf + b, buf + e, '\n');
+  if (q == buf + e) return false;
+  *p = q + 1;
+  *rel = 1;
+  return true;
+}
+
+// FASTQ pass 1: newline count + line bytes by local index residue
+void fastq_stats(const char* buf, uint64_t n, uint64_t b, uint64_t e, ChunkOut& c) {
+  const char* end = buf + n;
+  const char* ce = buf + e;
+  const char* p;
+  uint64_t rel;
+  if (!first_line(buf, b, e, &p, &rel)) {
+    c.nl = (uint64_t)std::count(buf + b, ce, '\n');  // (0 here)
+    return;
+  }
+  c.lead_nl = rel == 1;
+  uint64_t nl = rel, k = 0;
+  while (p < ce) {
+    const char* q = find(p, end, '\n');
+    c.fq_bytes[k & 3] += (uint64_t)(q - p);
+    c.fq_recs[k & 3]++;
+    if (q < ce) nl++;
+    p = q + 1;
+    k++;
+  }
+  c.nl = nl;
+}
+
+// FASTQ pass 2: the sequence lines starting in [b, e) (global index 1 mod 4)
 template <typename Emit>
 void fastq_lines(const char* buf, uint64_t n, uint64_t b, uint64_t e, uint64_t line_base, Emit&& emit) {
   const char* end = buf + n;
   const char* p;
-  uint64_t idx;
-  if (b == 0) {
-    p = buf;
-    idx = 0;
-  } else if (buf[b - 1] == '\n') {
-    p = buf + b;
-    idx = line_base;
-  } else {
-    const char* q = find(buf + b, buf + e, '\n');
-    if (q == buf + e) return;  // no line starts in this chunk
-    p = q + 1;
-    idx = line_base + 1;
-  }
+  uint64_t rel;
+  if (!first_line(buf, b, e, &p, &rel)) return;
+  uint64_t idx = line_base + rel;
+  // jump to the first sequence line, then every 4th line
   while (p < buf + e) {
     const char* q = find(p, end, '\n');
     if ((idx & 3) == 1) emit(p, (uint64_t)(q - p));
@@ -133,10 +172,61 @@ void fasta_split(const char* buf, uint64_t b, uint64_t e, bool hdr, Seq&& seq, C
   }
 }
 
+// FASTA pass 1: end state and sizes for either start state
+void fasta_stats(const char* buf, uint64_t b, uint64_t e, ChunkOut& c) {
+  const char* cb = buf + b;
+  const char* ce = buf + e;
+  const char* first_nl = find(cb, ce, '\n');
+  c.has_nl = first_nl != ce;
+  if (!c.has_nl) {
+    c.any_gt = find(cb, ce, '>') != ce;
+  } else {
+    // prefix [b, first_nl) from SEQ: bytes up to the first '>', which closes
+    const char* gt = find(cb, first_nl, '>');
+    c.fa_bytes_pre = (uint64_t)(gt - cb);
+    c.fa_close_pre = gt != first_nl;
+  }
+  // from SEQ after the first '\n' (or nothing)
+  bool hdr = false;
+  uint64_t bytes = 0, closes = 0;
+  if (c.has_nl) {
+    const char* p = first_nl + 1;
+    while (p < ce) {
+      if (hdr) {
+        const char* q = find(p, ce, '\n');
+        if (q == ce) break;
+        p = q + 1;
+        hdr = false;
+      } else {
+        const char* g = find(p, ce, '>');
+        while (p < g) {
+          const char* nl = find(p, g, '\n');
+          bytes += (uint64_t)(nl - p);
+          p = nl < g ? nl + 1 : g;
+        }
+        if (g == ce) break;
+        closes++;
+        p = g + 1;
+        hdr = true;
+      }
+    }
+  }
+  c.end_hdr = hdr;
+  c.fa_bytes_rest = bytes;
+  c.fa_close_rest = closes;
+}
+
 }  // namespace
 
-int parse_buffer_parallel(const char* buf, uint64_t n, std::string& text, std::vector<uint64_t>& off, int nthreads,
-                          ParseStats* stats) {
+void ParsedText::release() {
+  std::free(text);
+  std::free(off);
+  text = nullptr;
+  off = nullptr;
+  n_text = n_rec = 0;
+}
+
+int parse_buffer_parallel(const char* buf, uint64_t n, ParsedText& out, int nthreads, ParseStats* stats) {
   const auto t0 = std::chrono::steady_clock::now();
   if (n == 0 || (buf[0] != '>' && buf[0] != '@')) return -2;
   const bool fastq = buf[0] == '@';
@@ -149,56 +239,43 @@ int parse_buffer_parallel(const char* buf, uint64_t n, std::string& text, std::v
   std::vector<ChunkOut> ch(C);
   bool final_hdr = false;  // FASTA: the file ends inside a header line
 
+  // pass 1 (parallel) + the sequential composition of one value per chunk
   if (fastq) {
-    run_chunks(C, T, [&](uint64_t c) {
-      ch[c].nl = (uint64_t)std::count(buf + cs[c], buf + cs[c + 1], '\n');
-    });
-    for (uint64_t c = 1; c < C; ++c) ch[c].line_base = ch[c - 1].line_base + ch[c - 1].nl;
-    run_chunks(C, T, [&](uint64_t c) {
-      uint64_t bytes = 0, recs = 0;
-      fastq_lines(buf, n, cs[c], cs[c + 1], ch[c].line_base, [&](const char*, uint64_t len) {
-        bytes += len;
-        recs++;
-      });
-      ch[c].bytes = bytes;
-      ch[c].records = recs;
-    });
+    run_chunks(C, T, [&](uint64_t c) { fastq_stats(buf, n, cs[c], cs[c + 1], ch[c]); });
+    for (uint64_t c = 0; c < C; ++c) {
+      if (c) ch[c].line_base = ch[c - 1].line_base + ch[c - 1].nl;
+      const uint64_t first = ch[c].line_base + (ch[c].lead_nl ? 1 : 0);  // index of the first line start
+      const uint64_t k = (1 - first) & 3;  // local residue of the sequence lines
+      ch[c].bytes = ch[c].fq_bytes[k];
+      ch[c].records = ch[c].fq_recs[k];
+    }
   } else {
-    // chunk end states, then start states composed in order
-    std::vector<int8_t> end_has_nl(C), end_hdr(C), any_gt(C);
-    run_chunks(C, T, [&](uint64_t c) {
-      const char* b = buf + cs[c];
-      const char* e = buf + cs[c + 1];
-      const char* last_nl = nullptr;
-      for (const char* p = e; p > b;)
-        if (*--p == '\n') {
-          last_nl = p;
-          break;
-        }
-      end_has_nl[c] = last_nl != nullptr;
-      if (last_nl)
-        end_hdr[c] = find(last_nl + 1, e, '>') != e;
-      else
-        any_gt[c] = find(b, e, '>') != e;
-    });
+    run_chunks(C, T, [&](uint64_t c) { fasta_stats(buf, cs[c], cs[c + 1], ch[c]); });
     bool st = true;  // the file starts inside the first header line
     for (uint64_t c = 0; c < C; ++c) {
-      ch[c].start_hdr = st;
-      st = end_has_nl[c] ? (bool)end_hdr[c] : (st || any_gt[c]);
+      ChunkOut& x = ch[c];
+      x.start_hdr = st;
+      x.bytes = x.fa_bytes_rest + (st ? 0 : x.fa_bytes_pre);
+      x.records = x.fa_close_rest + (st ? 0 : x.fa_close_pre);
+      if (!x.has_nl) {  // no '\n': the whole chunk is the prefix
+        x.bytes = 0;
+        x.records = 0;
+        if (!st) {
+          const char* cb = buf + cs[c];
+          const char* ce = buf + cs[c + 1];
+          const char* gt = find(cb, ce, '>');
+          x.bytes = (uint64_t)(gt - cb);
+          x.records = gt != ce;
+        }
+        st = st || x.any_gt;
+      } else {
+        st = x.end_hdr;
+      }
     }
     final_hdr = st;
-    run_chunks(C, T, [&](uint64_t c) {
-      uint64_t bytes = 0, closes = 0;
-      fasta_split(
-          buf, cs[c], cs[c + 1], ch[c].start_hdr, [&](const char*, uint64_t len) { bytes += len; },
-          [&] { closes++; });
-      ch[c].bytes = bytes;
-      ch[c].records = closes;
-    });
   }
 
-  // bases, then write in place
-  const uint64_t text0 = text.size(), off0 = off.size();
+  // bases; grow the (uninitialised) outputs; pass 2 writes in place
   uint64_t tb = 0, rb = 0;
   for (uint64_t c = 0; c < C; ++c) {
     ch[c].text_base = tb;
@@ -207,16 +284,23 @@ int parse_buffer_parallel(const char* buf, uint64_t n, std::string& text, std::v
     rb += ch[c].records;
   }
   const uint64_t nrec = fastq ? rb : rb + 1;  // FASTA: EOF closes the last record
-  text.resize(text0 + tb);
-  off.resize(off0 + nrec);
-  char* out = &text[0] + text0;
-  uint64_t* o = off.data() + off0;
-  const uint64_t start = text0;
+  // the header-at-EOF case below may append up to n bytes
+  const uint64_t text_cap = out.n_text + tb + (fastq ? 0 : n) + 1;
+  char* nt = static_cast<char*>(std::realloc(out.text, text_cap));
+  if (!nt) return -3;
+  out.text = nt;
+  uint64_t* no = static_cast<uint64_t*>(std::realloc(out.off, (out.n_rec + nrec + 1) * sizeof(uint64_t)));
+  if (!no) return -3;
+  out.off = no;
+  if (out.n_rec == 0) out.off[0] = out.n_text;
+  char* dst = out.text + out.n_text;
+  uint64_t* o = out.off + out.n_rec + 1;
+  const uint64_t start = out.n_text;
   if (fastq) {
     run_chunks(C, T, [&](uint64_t c) {
       uint64_t t = ch[c].text_base, r = ch[c].rec_base;
       fastq_lines(buf, n, cs[c], cs[c + 1], ch[c].line_base, [&](const char* p, uint64_t len) {
-        std::memcpy(out + t, p, len);
+        std::memcpy(dst + t, p, len);
         t += len;
         o[r++] = start + t;
       });
@@ -227,7 +311,7 @@ int parse_buffer_parallel(const char* buf, uint64_t n, std::string& text, std::v
       fasta_split(
           buf, cs[c], cs[c + 1], ch[c].start_hdr,
           [&](const char* p, uint64_t len) {
-            std::memcpy(out + t, p, len);
+            std::memcpy(dst + t, p, len);
             t += len;
           },
           [&] { o[r++] = start + t; });
@@ -246,16 +330,17 @@ int parse_buffer_parallel(const char* buf, uint64_t n, std::string& text, std::v
           last_nl = p;
           break;
         }
-      const char* from = last_nl ? last_nl + 1 : buf;
-      const char* gt = find(from, e, '>');
-      if (gt != e && last_nl) {  // the header opened by this '>' runs to EOF
+      const char* gt = last_nl ? find(last_nl + 1, e, '>') : e;
+      if (gt != e) {  // the header opened by this '>' runs to EOF
         const uint64_t len = (uint64_t)(e - (gt + 1));
-        text.resize(text0 + tb + len);
-        std::memcpy(&text[0] + text0 + tb, gt + 1, len);
-        off[off0 + nrec - 1] = start + tb + len;
+        std::memcpy(dst + tb, gt + 1, len);
+        tb += len;
+        o[nrec - 1] = start + tb;
       }
     }
   }
+  out.n_text += tb;
+  out.n_rec += nrec;
   if (stats) {
     stats->bytes = n;
     stats->records = nrec;
@@ -265,8 +350,7 @@ int parse_buffer_parallel(const char* buf, uint64_t n, std::string& text, std::v
   return 0;
 }
 
-int parse_file_parallel(const std::string& path, std::string& text, std::vector<uint64_t>& off, int nthreads,
-                        ParseStats* stats) {
+int parse_file_parallel(const std::string& path, ParsedText& out, int nthreads, ParseStats* stats) {
   const auto t0 = std::chrono::steady_clock::now();
   const int fd = ::open(path.c_str(), O_RDONLY);
   if (fd < 0) return -1;
@@ -284,7 +368,7 @@ int parse_file_parallel(const std::string& path, std::string& text, std::vector<
   ::close(fd);
   if (m == MAP_FAILED) return -1;
   ::madvise(m, n, MADV_WILLNEED);
-  const int rc = parse_buffer_parallel(static_cast<const char*>(m), n, text, off, nthreads, stats);
+  const int rc = parse_buffer_parallel(static_cast<const char*>(m), n, out, nthreads, stats);
   ::munmap(m, n);
   if (stats) stats->seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   return rc;

@@ -109,6 +109,7 @@ def lib() -> C.CDLL:
         "mgh_graph_edges": (u64, [vp]),
         "mgh_graph_rows": (u64, [vp, vp, u64]),
         "mgh_parse_file": (i32, [C.c_char_p, i32, P(vp), P(vp), P(u64), P(C.c_double)]),
+        "mgh_parse_files": (i32, [P(C.c_char_p), i32, i32, P(vp), P(vp), P(u64), P(C.c_double)]),
         "mgh_parse_buffer": (i32, [vp, u64, i32, P(vp), P(vp), P(u64), P(C.c_double)]),
         "mgh_parse_free": (None, [vp]),
         "mgh_parse_set_min_chunk": (None, [u64]),
@@ -288,6 +289,31 @@ class OverlapEngine:
                                           C.byref(nu)), "ingest_ascii")
         self._after_ingest()
         return int(nu.value)
+
+    def ingest_files(self, files: Sequence[str], min_overlap: int, nthreads: int = 0) -> dict:
+        """Dataset(pe, se, l) on the device from FASTA/FASTQ files: the host
+        splits the records (mgh_parse_files: mmap, all threads), the device
+        canonicalises, sorts and deduplicates them (mg_ingest_ascii).  The
+        record buffers go straight from the splitter to the device.  Returns
+        {"n_unique", "n_records", "parse_s", "ingest_s"}."""
+        L = lib()
+        arr = (C.c_char_p * len(files))(*[os.fsencode(f) for f in files])
+        t, o, n, sec = C.c_void_p(), C.c_void_p(), C.c_uint64(), C.c_double()
+        rc = L.mgh_parse_files(arr, len(files), nthreads, C.byref(t), C.byref(o), C.byref(n), C.byref(sec))
+        if rc:
+            raise MgError({-1: f"Unable to open file: {list(files)}", -2: f"Unknown input file format: {list(files)}"}
+                          .get(rc, f"parse failed ({rc})"))
+        try:
+            nu = C.c_uint64()
+            t0 = time.perf_counter()
+            self._check(L.mg_ingest_ascii(self._h, C.cast(t, C.c_char_p), o, n.value, min_overlap, C.byref(nu)),
+                        "ingest_files")
+            t1 = time.perf_counter()
+        finally:
+            L.mgh_parse_free(t)
+            L.mgh_parse_free(o)
+        self._after_ingest()
+        return {"n_unique": int(nu.value), "n_records": int(n.value), "parse_s": sec.value, "ingest_s": t1 - t0}
 
     def ingest_codes(self, codes: np.ndarray, lens: np.ndarray, min_overlap: int) -> int:
         codes = np.ascontiguousarray(codes, dtype=np.uint8)

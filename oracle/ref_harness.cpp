@@ -33,6 +33,7 @@
 //        IN LIST ORDER as "u v orient offset" rows.
 //   dataset <fasta> <l> <out>  : Dataset(pe={}, se={fa}, l) only: "#N <unique>",
 //        "#G <numberOfReads>", "#R <id> <string>" (Dataset.cpp:39-65,110-193).
+//   dstime <fasta> <l> <out>   : "#T <seconds>" of the Dataset constructor alone.
 //   unitig <fasta> <l> <out>   : as bfs, then the reference's own contraction
 //        loop (OverlapGraph.cpp:211-215: contractCompositePaths +
 //        removeDeadEndNodes until neither changes anything), i.e. the graph
@@ -159,7 +160,9 @@ int main(int argc, char** argv) {
   double t_ds = now_s() - t0;
   UINT64 N = ds->getNumberOfUniqueReads();
 
-  if (!strcmp(mode, "dataset")) {
+  if (!strcmp(mode, "dstime")) {
+    fprintf(out, "#T %.6f\n", t_ds);
+  } else if (!strcmp(mode, "dataset")) {
     fprintf(out, "#N %llu\n#G %llu\n", (unsigned long long)N, (unsigned long long)ds->getNumberOfReads());
     for (UINT64 i = 1; i <= N; i++)
       fprintf(out, "#R %llu %s\n", (unsigned long long)i, ds->getReadFromID(i)->getStringForward().c_str());

@@ -411,6 +411,48 @@ def test_device_rows_to_unitig(name, tmp_path):
         assert (tmp_path / "u").read_text() == f.read()
 
 
+@pytest.mark.parametrize("name", FIXTURES)
+def test_ingest_files_matches_host_dataset(name):
+    """FASTA/FASTQ file -> parallel record splitter -> device ingest gives the
+    reference's Dataset (IDs, strings, frequencies) and then the golden rows."""
+    meta = load_meta(name)
+    ds = Dataset.from_files([fixture_input(name)], meta["l"])
+    e = OverlapEngine(0)
+    e.set_shard(0, 1)
+    info = e.ingest_files([fixture_input(name)], meta["l"])
+    assert info["n_unique"] == ds.num_unique == meta["n_unique"]
+    assert_same_dataset(e, ds)
+    e.build_index(meta["l"], 0)
+    sup = e.mark_contained()
+    rows = e.rows(e.find_overlaps())
+    e.close()
+    assert np.array_equal(rows_to_tuples(rows), golden_rows(name))
+    assert {str(i): int(s) for i, s in enumerate(sup) if s} == meta["super"]
+
+
+def test_ingest_files_parse_cases(tmp_path):
+    """The record-splitting quirks (tests/golden/parse_cases.json) through the
+    device ingest: same Dataset as the reference's."""
+    import json
+    import os
+
+    from conftest import GOLDEN
+
+    with open(os.path.join(GOLDEN, "parse_cases.json")) as f:
+        cases = json.load(f)
+    e = OverlapEngine(0)
+    e.set_shard(0, 1)
+    for case in cases:
+        p = tmp_path / (case["name"] + case["ext"])
+        p.write_bytes(case["input"].encode())
+        info = e.ingest_files([str(p)], case["l"])
+        assert info["n_unique"] == case["n_unique"], case["name"]
+        assert e.dataset_counts() == (case["n_reads"], case["n_unique"]), case["name"]
+        ds = Dataset.from_files([str(p)], case["l"])
+        assert_same_dataset(e, ds)
+    e.close()
+
+
 @pytest.mark.parametrize("name", ["mixed", "tandem", "highdup", "dirty"])
 def test_scan_inside_probe_path(name):
     """option overlap_scan = 0: the window scan runs inside each probe pass

@@ -41,6 +41,9 @@ for s in $STEPS; do
   replay)
     timeout -k 10 600 python -u bench.py --replay --no-cpu-baseline --no-ingest --steps 2 > $OUT/bench_replay.json 2> $OUT/bench_replay.err
     rc=$?; echo "bench replay rc=$rc"; python3 -c "import json;d=json.load(open('$OUT/bench_replay.json'));print(d.get('graph_replay'))" ;;
+  parse)
+    timeout -k 10 900 python -u tools/parse_bench.py > $OUT/parse_bench.json 2> $OUT/parse_bench.err
+    rc=$?; echo "parse rc=$rc"; tail -12 $OUT/parse_bench.err; cat $OUT/parse_bench.json ;;
   variants)
     timeout -k 10 400 python -u tools/variant_sweep.py > $OUT/variant_sweep.log 2>&1
     rc=$?; echo "variants rc=$rc"; grep opts $OUT/variant_sweep.log ;;
