@@ -145,7 +145,7 @@ def main():
     ap.add_argument("--no-ingest", action="store_true", help="skip the device Dataset ingest measurement")
     ap.add_argument("--replay", action="store_true",
                     help="also time the host replay of the exploration + transitive reduction + contraction on the rows")
-    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r01s2_pmc_c3.json"))
+    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r01s3_pmc_c3.json"))
     ap.add_argument("--nb-log2", type=int, default=0)
     ap.add_argument("--split-probe", action="store_true", help="probe -> candidates -> verify kernels (option split = 1)")
     args = ap.parse_args()
@@ -277,7 +277,8 @@ def main():
         traffic = load_pmc(args.pmc) if args.config == "c3" else None
         roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                "kernel": "step = k_index_build || k_scan, then k_probe (device wall, HIP events)",
+                "kernel": "step = k_scan<INDEX> (window scan + fused index build), then k_probe "
+                          "(containment, then discovery); device wall, HIP events",
                 "alg_bytes_per_step": alg, "alg_bytes_per_read": per_read, "kernel_ms_per_step": kern_ms,
                 "probe_ms": dev_ms["probe_ms"], "verify_ms": dev_ms["verify_ms"], "scan_ms": dev_ms["scan_ms"]}
     else:
