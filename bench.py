@@ -148,6 +148,8 @@ def main():
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r01s3_pmc_c3.json"))
     ap.add_argument("--nb-log2", type=int, default=0)
     ap.add_argument("--split-probe", action="store_true", help="probe -> candidates -> verify kernels (option split = 1)")
+    ap.add_argument("--sort-runs", type=int, default=None,
+                    help="option sort_runs: bucket-ordered runs before the probe (default: the library's)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -190,6 +192,8 @@ def main():
         e = OverlapEngine(local)
         e.set_option("nb_log2", args.nb_log2)
         e.set_option("split", 1 if args.split_probe else 0)
+        if args.sort_runs is not None:
+            e.set_option("sort_runs", args.sort_runs)
         e.set_shard(r, P, 0, 0)
         e.upload(ds)
         engines.append(e)

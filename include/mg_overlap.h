@@ -53,6 +53,7 @@ typedef struct mg_timings {
   float verify_ms;      /* verify kernel of the split path (0 fused) */
   float upload_ms;      /* H2D copy of raw reads (mg_ingest_*)        */
   float ingest_ms;      /* device Dataset ingest (mg_ingest_*)        */
+  float sort_ms;        /* run records ordered by bucket (option "sort_runs"; 0 otherwise) */
 } mg_timings;
 
 /* Work counters of the last discovery launch (only with option "stats" = 1):

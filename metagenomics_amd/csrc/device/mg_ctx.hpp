@@ -93,6 +93,20 @@ struct mg_ctx {
   unsigned long long* d_cand_cnt = nullptr;
   size_t cand_cnt_cap = 0;
   std::vector<unsigned long long> cand_cnt_host;
+  // bucket-ordered runs (option "sort_runs"): the shared scan's runs as SoA
+  // (x, meta) sorted by bucket, so the probe meets each cell's runs together
+  bool sort_runs = false;
+  uint64_t* d_sk[2] = {nullptr, nullptr};
+  uint64_t* d_sm[2] = {nullptr, nullptr};
+  size_t sk_cap = 0;
+  int sk_sel = 0;  // which buffer holds the sorted result
+  void* d_sort_tmp = nullptr;
+  size_t sort_tmp_cap = 0;
+  unsigned long long* d_run_off = nullptr;
+  size_t run_off_cap = 0;
+  uint64_t n_sorted = 0;
+  int sorted_state = 0;  // 0 none, 2 sorted (for the current scan)
+  int sort_bits = 0;     // diagnostics: sort only the top sort_bits bucket bits (0: all)
   mg_timings t{};
   // Dataset ingest on the device (mg_ingest_*): frequency of each unique read
   uint32_t* d_freq = nullptr;
@@ -139,6 +153,7 @@ inline uint32_t supported_maxw(uint32_t need) {
 // new reads invalidate everything derived from them
 inline void reset_derived(mg_ctx* ctx) {
   ctx->scan_state = 0;
+  ctx->sorted_state = 0;
   ctx->index_ready = false;
   ctx->contained_done = false;
   ctx->super_any = false;

@@ -31,6 +31,8 @@
 //    (DESIGN.md §4 proves this reproduces the reference multiset).
 #include <hip/hip_runtime.h>
 
+#include <hipcub/hipcub.hpp>
+
 #include <algorithm>
 #include <cstdint>
 #include <cstring>
@@ -65,10 +67,14 @@ __device__ __forceinline__ uint64_t mix64(uint64_t x) {
 // on ties" is a plain unsigned min.  Index build, discovery and lookup all
 // use this same rule, so a key and an identical read window always select
 // the same minimizer at the same offset.
+// Two rounds of 24-bit multiply-add (v_mad_u32_u24, full rate; a 32-bit
+// v_mul_lo_u32 is not) with xor-shifts; the bits a 24-bit product drops come
+// back through the added shift.
 __device__ __forceinline__ uint32_t order_key(uint64_t mm) {
-  uint32_t x = (uint32_t)mm * 0x9E3779B1u + (uint32_t)(mm >> 32);
+  const uint32_t lo = (uint32_t)mm, hi = (uint32_t)(mm >> 32);
+  uint32_t x = __umul24(lo, 0x9E3779u) + (hi ^ (lo >> 8));
   x ^= x >> 15;
-  x *= 0x85EBCA77u;
+  x = __umul24(x, 0xEBCA77u) + (x >> 8);
   x ^= x >> 13;
   return x & 0xFFFFFC00u;  // 22-bit key in the high bits, position goes in the low 10
 }
@@ -402,27 +408,43 @@ __global__ __launch_bounds__(kBlock) void k_scan(ScanParams p) {
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) tmax = max(tmax, __shfl_xor(tmax, d));
     tmax = __builtin_amdgcn_readfirstlane(tmax);  // wavefront-uniform loop bound
-    uint64_t mm = 0, cw = 0;
-    if (tend) {
-      mm = funnel(g[0], g[1], 2) >> msh;  // m-mer at t = 1
-      cw = g[(1 + m) >> 5];               // word holding base t + m
+    // the read's words in registers (no global load inside the base loop); the
+    // word holding base t + m is picked by a wavefront-uniform index
+    constexpr int kRw = MAXW + 1 <= slot_words(MAXW) ? MAXW + 1 : slot_words(MAXW);
+    uint64_t rw[MAXW + 1];
+    {
+      const uint64_t* gs = a < p.a_hi ? g : p.words;  // a slot every lane may read
+#pragma unroll
+      for (int k = 0; k <= MAXW; ++k) rw[k] = k < kRw ? gs[k] : 0;
     }
+    auto word_at = [&](int idx) {  // idx wavefront-uniform
+      uint64_t v = rw[0];
+#pragma unroll
+      for (int k = 1; k <= MAXW; ++k) v = idx == k ? rw[k] : v;
+      return v;
+    };
+    uint64_t mm = 0;
+    if (tend) mm = funnel(rw[0], rw[1], 2) >> msh;  // m-mer at t = 1
+    uint64_t cw = word_at(__builtin_amdgcn_readfirstlane((1 + m) >> 5));  // word holding base t + m
     // INDEX: best (order_key | i) and m-mer of keys o = 0..3; rcm = reverse-strand m-mer
     uint32_t kb0 = 0xFFFFFFFFu, kb1 = 0xFFFFFFFFu, kb2 = 0xFFFFFFFFu, kb3 = 0xFFFFFFFFu;
     uint64_t mb0 = 0, mb1 = 0, mb2 = 0, mb3 = 0, rcm = 0;
     if (INDEX && tend) {
-      const uint64_t m0 = g[0] >> msh;  // t = 0 (window j = 0 is no scan window)
-      rcm = rc_word(g[0]) & mmask;
+      const uint64_t m0 = rw[0] >> msh;  // t = 0 (window j = 0 is no scan window)
+      rcm = rc_word(rw[0]) & mmask;
       kb0 = order_key(m0);
       mb0 = m0;
       kb3 = order_key(rcm) | (uint32_t)(w - 1);
       mb3 = rcm;
-      const uint64_t b = (g[m >> 5] >> (62 - 2 * (m & 31))) & 3u;  // base at 0 + m
+      const uint64_t b = (word_at(__builtin_amdgcn_readfirstlane(m >> 5)) >> (62 - 2 * (m & 31))) & 3u;  // base at 0 + m
       rcm = (rcm >> 2) | ((3u - b) << (2 * m - 2));
     }
     uint32_t pmin = 0xFFFFFFFFu;
     int last_pos = 0, jlo = 1;
     int u = 0;  // offset of t in its block of w positions
+    // previous block's suffix minimum at u + 1, read one step ahead so the
+    // LDS latency hides behind the step's ALU work
+    uint32_t sv_pf = s_keys[kWave];
     for (int t = 1; t <= tmax; ++t) {
       bool emit = false;
       uint64_t e_meta = 0;
@@ -457,10 +479,7 @@ __global__ __launch_bounds__(kBlock) void k_scan(ScanParams p) {
         if (t >= w) {  // window j = t - w + 1
           const int j = t - w + 1;
           uint32_t mn = pmin;
-          if (u != w - 1) {
-            const uint32_t sv = s_keys[(u + 1) * kWave];
-            mn = sv < mn ? sv : mn;
-          }
+          if (u != w - 1) mn = sv_pf < mn ? sv_pf : mn;
           const int pos = (int)(mn & 1023u);
           if (j > 1 && pos != last_pos) {
             emit = true;
@@ -472,19 +491,28 @@ __global__ __launch_bounds__(kBlock) void k_scan(ScanParams p) {
         s_keys[u * kWave] = key;
         const int x = t + m;  // roll in the base at t + m
         mm = ((mm << 2) | ((cw >> (62 - 2 * (x & 31))) & 3u)) & mmask;
-        if ((x & 31) == 31 && t < tend) cw = g[(x + 1) >> 5];
       }
-      if (u == w - 1) {  // block complete: suffix minima in place
-        uint32_t run = s_keys[(w - 1) * kWave];
-        for (int v = w - 2; v >= 0; --v) {
-          const uint32_t x1 = s_keys[v * kWave];
-          run = x1 < run ? x1 : run;
-          s_keys[v * kWave] = run;
+      {
+        const int xu = __builtin_amdgcn_readfirstlane(t + m);
+        if ((xu & 31) == 31) cw = word_at((xu + 1) >> 5);  // next word (don't-care past a read's end)
+      }
+      if (u == w - 1) {  // block complete: suffix minima in place, 8 reads in flight at a time
+        uint32_t run = 0xFFFFFFFFu;
+        for (int v0 = w - 1; v0 >= 0; v0 -= 8) {
+          uint32_t x8[8];
+#pragma unroll
+          for (int k = 0; k < 8; ++k) x8[k] = v0 - k >= 0 ? s_keys[(v0 - k) * kWave] : 0xFFFFFFFFu;
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            run = x8[k] < run ? x8[k] : run;
+            if (v0 - k >= 0) s_keys[(v0 - k) * kWave] = run;
+          }
         }
         u = 0;
       } else {
         ++u;
       }
+      sv_pf = s_keys[(u + 1 < w ? u + 1 : 0) * kWave];
       put(emit, e_meta);
       while (nbuf >= (uint32_t)kWave) flush(kWave);
     }
@@ -573,6 +601,8 @@ struct ProbeParams {
   const unsigned long long* run_cnt;
   uint64_t run_cap;
   uint64_t run_regions;           // probe wavefront r consumes run regions r, r + nw, r + 2 nw, ... < run_regions
+  const uint64_t* fkeys;          // non-null: runs as SoA (x, meta), region r = [r * run_cap, + run_cnt[r])
+  const uint64_t* fmeta;
   const uint32_t* src_super;      // runs of sources with superReadID != 0 are dropped (:548; nullptr: none)
   uint64_t src_lo, src_hi;        // only runs of sources in [src_lo, src_hi) (src_hi = 0: all)
   uint32_t* rows;                 // 3 dwords per row (mg_edge); one region per wavefront
@@ -731,9 +761,11 @@ __global__ __launch_bounds__(kBlock) void k_probe(ProbeParams p) {
   uint32_t rg = 0;
   uint64_t rpos = 0, rcnt = 0;
   const ulonglong2* rbase = p.runs;
+  uint64_t rbase_i = 0;
   auto open_region = [&](uint32_t r) {
     const uint64_t reg = gw + (uint64_t)r * nwp;
-    rbase = p.runs + reg * p.run_cap;
+    rbase = p.runs + (p.fkeys ? 0 : reg * p.run_cap);
+    rbase_i = reg * p.run_cap;
     const uint64_t c = p.run_cnt[reg];
     rcnt = c < p.run_cap ? c : p.run_cap;
     rpos = 0;
@@ -755,7 +787,12 @@ __global__ __launch_bounds__(kBlock) void k_probe(ProbeParams p) {
   auto hbm_fetch = [&]() {
     const uint64_t k = rpos + (uint64_t)lane;
     pf_ok = pf_any && k < rcnt;
-    rec_pf = rbase[pf_ok ? k : 0];
+    if (p.fkeys) {
+      const uint64_t i = rbase_i + (pf_ok ? k : 0);
+      rec_pf = make_ulonglong2(p.fkeys[i], p.fmeta[i]);
+    } else {
+      rec_pf = rbase[pf_ok ? k : 0];
+    }
   };
   auto take_item = [&](uint64_t& key, uint64_t& meta, bool& valid) -> bool {
     if (npend >= (uint32_t)kWave) {
@@ -1238,6 +1275,21 @@ __global__ __launch_bounds__(kBlock) void k_flat_counts(unsigned long long* cnt,
   cnt[r] = lo >= n ? 0 : (n - lo < cap ? n - lo : cap);
 }
 
+// Run regions -> SoA flat arrays (x, meta) at off[r] (the sort input of option
+// "sort_runs"); one block per region.
+__global__ __launch_bounds__(kBlock) void k_runs_soa(const ulonglong2* __restrict__ runs, uint64_t cap,
+                                                     const unsigned long long* __restrict__ off,
+                                                     uint64_t* __restrict__ keys, uint64_t* __restrict__ meta) {
+  const uint64_t r = blockIdx.x;
+  const uint64_t lo = off[r], c = off[r + 1] - lo;
+  const ulonglong2* src = runs + r * cap;
+  for (uint64_t i = threadIdx.x; i < c; i += kBlock) {
+    const ulonglong2 x = src[i];
+    keys[lo + i] = x.x;
+    meta[lo + i] = x.y;
+  }
+}
+
 __global__ __launch_bounds__(kBlock) void k_super_finalize(const unsigned long long* __restrict__ key,
                                                           uint64_t n, uint32_t* __restrict__ super,
                                                           unsigned int* __restrict__ any) {
@@ -1481,7 +1533,8 @@ template <int W>
 struct LaunchProbe {
   static int run(mg_ctx* ctx, bool contain, const ulonglong2* runs, const unsigned long long* run_cnt,
                  uint64_t run_cap, uint64_t run_regions, uint32_t grid, uint64_t total_runs,
-                 const uint32_t* src_super = nullptr, uint64_t src_lo = 0, uint64_t src_hi = 0) {
+                 const uint32_t* src_super = nullptr, uint64_t src_lo = 0, uint64_t src_hi = 0,
+                 const uint64_t* fkeys = nullptr, const uint64_t* fmeta = nullptr) {
     ctx->nreg = (uint64_t)grid * kWavesPerBlock;  // probe wavefronts = row regions
     ProbeParams pp{};
     pp.words = ctx->d_words;
@@ -1500,6 +1553,8 @@ struct LaunchProbe {
     pp.run_cnt = run_cnt;
     pp.run_cap = run_cap;
     pp.run_regions = run_regions;
+    pp.fkeys = fkeys;
+    pp.fmeta = fmeta;
     pp.src_super = src_super;
     pp.src_lo = src_lo;
     pp.src_hi = src_hi;
@@ -1712,7 +1767,8 @@ void mg_destroy(mg_ctx* ctx) {
   (void)hipStreamSynchronize(ctx->stream);
   void* bufs[] = {ctx->d_words, ctx->d_len, ctx->d_cells,
                   ctx->d_superkey, ctx->d_super, ctx->d_any, ctx->d_rows, ctx->d_seg, ctx->d_stats,
-                  ctx->d_compact, ctx->d_runs, ctx->d_run_cnt, ctx->d_keyrec, ctx->d_blk, ctx->d_flat_cnt, ctx->d_cand, ctx->d_cand_cnt, ctx->d_freq};
+                  ctx->d_compact, ctx->d_runs, ctx->d_run_cnt, ctx->d_keyrec, ctx->d_blk, ctx->d_flat_cnt, ctx->d_cand, ctx->d_cand_cnt, ctx->d_freq,
+                  ctx->d_sk[0], ctx->d_sk[1], ctx->d_sm[0], ctx->d_sm[1], ctx->d_sort_tmp, ctx->d_run_off};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   for (auto& e : ctx->ev)
@@ -1845,6 +1901,17 @@ int mg_set_option(mg_ctx* ctx, const char* name, int64_t value) {
   if (!strcmp(name, "overlap_scan")) {
     ctx->overlap_scan = value != 0;
     ctx->scan_state = 0;
+    ctx->sorted_state = 0;
+    return 0;
+  }
+  if (!strcmp(name, "sort_runs")) {
+    ctx->sort_runs = value != 0;
+    ctx->sorted_state = 0;
+    return 0;
+  }
+  if (!strcmp(name, "sort_bits")) {  // diagnostics: sort only the top sort_bits bucket bits (0: all)
+    ctx->sort_bits = (int)value;
+    ctx->sorted_state = 0;
     return 0;
   }
   if (!strcmp(name, "split")) {
@@ -2102,6 +2169,7 @@ int ensure_scan(mg_ctx* ctx) {
     ctx->scan_state = again ? 0 : 2;
     if (!again) return 0;
   }
+  ctx->sorted_state = 0;
   for (int attempt = 0; attempt < 3; ++attempt) {
     if (ctx->n && dispatch_w<LaunchScanAll>(ctx->maxw, ctx, ctx->stream, false))
       return set_err(ctx, "scan launch failed");
@@ -2125,14 +2193,94 @@ struct LaunchProbeShared {
     const uint32_t* sup = (!contain && ctx->contained_done && ctx->super_any) ? ctx->d_super : nullptr;
     const uint64_t lo = contain ? 0 : ctx->read_lo;
     const uint64_t hi = contain ? 0 : (ctx->read_hi ? std::min(ctx->read_hi, ctx->n) : 0);
+    if (ctx->sort_runs && ctx->sorted_state == 2) {
+      // bucket-ordered runs: one contiguous tile per probe wavefront
+      const uint64_t n = ctx->n_sorted;
+      const uint64_t nw = (uint64_t)g.grid * kWavesPerBlock;
+      const uint64_t cap = std::max<uint64_t>(1, (n + nw - 1) / nw);
+      if (ctx->flat_cnt_cap < nw) {
+        if (ctx->d_flat_cnt) (void)hipFree(ctx->d_flat_cnt);
+        ctx->d_flat_cnt = nullptr;
+        if (hipMalloc(&ctx->d_flat_cnt, nw * sizeof(unsigned long long)) != hipSuccess) return -1;
+        ctx->flat_cnt_cap = nw;
+      }
+      hipLaunchKernelGGL(k_flat_counts, dim3((uint32_t)((nw + kBlock - 1) / kBlock)), dim3(kBlock), 0, ctx->stream,
+                         ctx->d_flat_cnt, nw, cap, n);
+      if (hipGetLastError() != hipSuccess) return -1;
+      return LaunchProbe<W>::run(ctx, contain, nullptr, ctx->d_flat_cnt, cap, nw, g.grid, n, sup, lo, hi,
+                                 ctx->d_sk[ctx->sk_sel], ctx->d_sm[ctx->sk_sel]);
+    }
     return LaunchProbe<W>::run(ctx, contain, ctx->d_runs, ctx->d_run_cnt, ctx->run_cap, ctx->nrun_reg, g.grid, total,
                                sup, lo, hi);
   }
 };
 
+// option "sort_runs": the settled shared-scan runs -> SoA arrays (k_runs_soa)
+// -> rocprim radix sort by bucket (8 bits per pass), so consecutive probe items share
+// cells and, through the cells' entries, partner reads.  Option "sort_bits"
+// (diagnostics) sorts only the top sort_bits bucket bits.
+int sort_shared_runs(mg_ctx* ctx) {
+  if (ctx->sorted_state == 2) return 0;
+  const uint64_t nreg = ctx->nrun_reg;
+  std::vector<unsigned long long> off(nreg + 1, 0);
+  for (uint64_t r = 0; r < nreg; ++r) off[r + 1] = off[r] + std::min<uint64_t>(ctx->run_cnt_host[r], ctx->run_cap);
+  const uint64_t n = off[nreg];
+  if (n > 0x7FFFFFFFull) return set_err(ctx, "sort_runs: more than 2^31 runs");
+  MG_TRY(ensure(&ctx->d_run_off, &ctx->run_off_cap, nreg + 1));
+  if (n > ctx->sk_cap) {
+    for (int b = 0; b < 2; ++b) {
+      if (ctx->d_sk[b]) (void)hipFree(ctx->d_sk[b]);
+      if (ctx->d_sm[b]) (void)hipFree(ctx->d_sm[b]);
+      ctx->d_sk[b] = ctx->d_sm[b] = nullptr;
+    }
+    ctx->sk_cap = 0;
+    for (int b = 0; b < 2; ++b) {
+      MG_TRY(hipMalloc(&ctx->d_sk[b], std::max<uint64_t>(n, 1) * sizeof(uint64_t)));
+      MG_TRY(hipMalloc(&ctx->d_sm[b], std::max<uint64_t>(n, 1) * sizeof(uint64_t)));
+    }
+    ctx->sk_cap = n;
+  }
+  MG_TRY(hipEventRecord(ctx->ev[10], ctx->stream));
+  MG_TRY(hipMemcpyAsync(ctx->d_run_off, off.data(), (nreg + 1) * sizeof(unsigned long long), hipMemcpyHostToDevice,
+                        ctx->stream));
+  if (nreg)
+    hipLaunchKernelGGL(k_runs_soa, dim3((uint32_t)nreg), dim3(kBlock), 0, ctx->stream, ctx->d_runs, ctx->run_cap,
+                       ctx->d_run_off, ctx->d_sk[0], ctx->d_sm[0]);
+  MG_TRY(hipGetLastError());
+  const unsigned nb = ctx->nb_log2;
+  const unsigned lo_bit = (ctx->sort_bits > 0 && (unsigned)ctx->sort_bits < nb) ? nb - (unsigned)ctx->sort_bits : 0u;
+  auto sort = [&](void* tmp, size_t& tb, int& sel) -> hipError_t {
+    rocprim::double_buffer<uint64_t> keys(ctx->d_sk[0], ctx->d_sk[1]);
+    rocprim::double_buffer<uint64_t> vals(ctx->d_sm[0], ctx->d_sm[1]);
+    hipError_t e = rocprim::radix_sort_pairs(tmp, tb, keys, vals, n, lo_bit, nb, ctx->stream);
+    sel = keys.current() == ctx->d_sk[0] ? 0 : 1;
+    if (e == hipSuccess && tmp && (vals.current() == ctx->d_sm[0] ? 0 : 1) != sel) e = hipErrorUnknown;
+    return e;
+  };
+  size_t tb = 0;
+  int sel = 0;
+  MG_TRY(sort(nullptr, tb, sel));
+  if (tb > ctx->sort_tmp_cap) {
+    if (ctx->d_sort_tmp) (void)hipFree(ctx->d_sort_tmp);
+    ctx->d_sort_tmp = nullptr;
+    MG_TRY(hipMalloc(&ctx->d_sort_tmp, tb));
+    ctx->sort_tmp_cap = tb;
+  }
+  tb = ctx->sort_tmp_cap;
+  MG_TRY(sort(ctx->d_sort_tmp, tb, sel));
+  MG_TRY(hipEventRecord(ctx->ev[11], ctx->stream));
+  ctx->sk_sel = sel;
+  ctx->n_sorted = n;
+  ctx->sorted_state = 2;
+  return 0;
+}
+
 // probe the shared scan's runs (rows settled for the discovery probe)
 int probe_shared(mg_ctx* ctx, bool contain) {
   if (ensure_scan(ctx)) return -1;
+  if (ctx->sort_runs && !ctx->split) {
+    if (sort_shared_runs(ctx)) return -1;
+  }
   for (int attempt = 0; attempt < 3; ++attempt) {
     ctx->nreg = 0;
     if (!ctx->split) MG_TRY(hipEventRecord(ctx->ev[8], ctx->stream));
@@ -2155,6 +2303,8 @@ int mg_build_index(mg_ctx* ctx, uint32_t min_overlap, uint32_t seed_k) {
   MG_TRY(hipEventRecord(ctx->ev[0], ctx->stream));
   if (setup_index(ctx, min_overlap, seed_k)) return -1;
   ctx->scan_state = 0;
+  ctx->sorted_state = 0;
+  ctx->t.sort_ms = 0.f;
   if (shared_scan(ctx)) {
     // one pass over the reads: the index inserts ride on the window scan
     // (k_scan<INDEX>), whose runs then serve the containment and discovery
@@ -2243,7 +2393,9 @@ int mg_find_overlaps(mg_ctx* ctx, uint64_t* n_rows) {
     ctx->t.probe_ms = shared_scan(ctx) ? elapsed(ctx->ev[8], ctx->ev[9]) : elapsed(ctx->ev[7], ctx->ev[5]);
     ctx->t.verify_ms = 0.f;
   }
-  ctx->t.overlap_ms = ctx->t.scan_ms + ctx->t.probe_ms + ctx->t.verify_ms;
+  ctx->t.sort_ms = (shared_scan(ctx) && ctx->sort_runs && !ctx->split && ctx->sorted_state == 2)
+                       ? elapsed(ctx->ev[10], ctx->ev[11]) : 0.f;
+  ctx->t.overlap_ms = ctx->t.scan_ms + ctx->t.sort_ms + ctx->t.probe_ms + ctx->t.verify_ms;
   read_stats(ctx, nsrc);
   // device wall of the step: index build start .. last discovery kernel end
   ctx->t.total_ms = shared_scan(ctx) ? elapsed(ctx->ev[0], ctx->ev[5])
@@ -2348,7 +2500,9 @@ int mg_probe_runs(mg_ctx* ctx, int contain, const void* runs, uint64_t n, uint64
     ctx->t.verify_ms = 0.f;
   }
   if (contain) return 0;
-  ctx->t.overlap_ms = ctx->t.scan_ms + ctx->t.probe_ms + ctx->t.verify_ms;
+  ctx->t.sort_ms = (shared_scan(ctx) && ctx->sort_runs && !ctx->split && ctx->sorted_state == 2)
+                       ? elapsed(ctx->ev[10], ctx->ev[11]) : 0.f;
+  ctx->t.overlap_ms = ctx->t.scan_ms + ctx->t.sort_ms + ctx->t.probe_ms + ctx->t.verify_ms;
   read_stats(ctx, 0);
   if (counts) {
     const uint64_t reg_cap = ctx->nreg ? ctx->rows_cap / ctx->nreg : 0;

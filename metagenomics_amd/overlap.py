@@ -32,7 +32,7 @@ class _Timings(C.Structure):
     _fields_ = [("pack_ms", C.c_float), ("index_ms", C.c_float), ("contained_ms", C.c_float),
                 ("overlap_ms", C.c_float), ("total_ms", C.c_float), ("scan_ms", C.c_float),
                 ("probe_ms", C.c_float), ("verify_ms", C.c_float), ("upload_ms", C.c_float),
-                ("ingest_ms", C.c_float)]
+                ("ingest_ms", C.c_float), ("sort_ms", C.c_float)]
 
 
 class _Counters(C.Structure):

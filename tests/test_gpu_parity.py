@@ -453,6 +453,20 @@ def test_ingest_files_parse_cases(tmp_path):
     e.close()
 
 
+@pytest.mark.parametrize("name", FIXTURES)
+def test_sorted_runs_path(name):
+    """option sort_runs = 1: the shared scan's runs are radix-sorted by bucket
+    before the containment and discovery probes; same rows and superReadIDs."""
+    meta = load_meta(name)
+    ds = Dataset.from_files([fixture_input(name)], meta["l"])
+    e = OverlapEngine(0)
+    e.set_option("sort_runs", 1)
+    rows, sup = gpu_rows(e, ds, meta["l"])
+    e.close()
+    assert np.array_equal(rows_to_tuples(rows), golden_rows(name))
+    assert {str(i): int(s) for i, s in enumerate(sup) if s} == meta["super"]
+
+
 @pytest.mark.parametrize("name", ["mixed", "tandem", "highdup", "dirty"])
 def test_scan_inside_probe_path(name):
     """option overlap_scan = 0: the window scan runs inside each probe pass

@@ -59,6 +59,9 @@ for s in $STEPS; do
   prof)
     timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o kt -- python3 bench.py --steps 5 --no-cpu-baseline > $OUT/prof_bench.json 2> $OUT/prof_bench.err
     rc=$?; echo "prof rc=$rc"; cat $OUT/prof_bench.json; head -8 $OUT/prof/kt_kernel_stats.csv | cut -c1-200 ;;
+  profsort)
+    timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/profsort -o kt -- python3 bench.py --steps 3 --no-cpu-baseline --no-ingest --sort-runs 1 > $OUT/profsort_bench.json 2> $OUT/profsort_bench.err
+    rc=$?; echo "profsort rc=$rc"; python3 -c "import json;d=json.load(open('$OUT/profsort_bench.json'));print(d['ms_per_step'], d['device_ms'])"; head -12 $OUT/profsort/kt_kernel_stats.csv | cut -c1-150 ;;
   profsim)
     timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/profsim -o kt -- python3 bench.py --sim-world 4 --steps 2 --no-cpu-baseline > $OUT/profsim_bench.json 2> $OUT/profsim_bench.err
     rc=$?; echo "profsim rc=$rc"; cat $OUT/profsim_bench.json; cat $OUT/profsim/kt_kernel_stats.csv ;;

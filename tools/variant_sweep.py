@@ -14,9 +14,10 @@ n = int(sys.argv[1]) if len(sys.argv) > 1 else 10_000_000
 c, L = synth.uniform_read_set(n, 150, n * 150 // 20, seed=31)
 ds = Dataset.from_codes(c, L, 50, nthreads=16)
 VARIANTS = [
-    {"overlap_scan": 0},
     {"overlap_scan": 1},
-    {"overlap_scan": 1, "split": 1},
+    {"sort_runs": 1},
+    {"sort_runs": 1, "sort_bits": 16},
+    {"sort_runs": 1, "sort_bits": 12},
 ]
 res = []
 for opts in VARIANTS:
@@ -31,10 +32,10 @@ for opts in VARIANTS:
         e.mark_contained(copy=False)
         rows = e.find_overlaps()
         t = e.timings()
-        ts.append((t["total_ms"], t["index_ms"], t["scan_ms"], t["probe_ms"]))
+        ts.append((t["total_ms"], t["index_ms"], t["scan_ms"], t["probe_ms"], t["sort_ms"]))
     e.close()
     best = min(ts[1:])
     r = {"opts": opts, "rows": rows, "total_ms": round(best[0], 3), "index_ms": round(best[1], 3),
-         "scan_ms": round(best[2], 3), "probe_ms": round(best[3], 3)}
+         "scan_ms": round(best[2], 3), "probe_ms": round(best[3], 3), "sort_ms": round(best[4], 3)}
     res.append(r)
     print(json.dumps(r), flush=True)
