@@ -9,12 +9,16 @@ HBM.  Inputs (2-bit packed reads) are resident in HBM before timing starts.
 Default workload = BASELINE.json configs[2] (C3): 10M x 150 bp synthetic
 reads, 20x coverage of a 75 Mb random genome, 50 % reverse-complemented,
 l = 50, seed k = 31.  Multi-GPU (torchrun, one process per GPU): the same 10M
-reads on N GPUs (strong scaling) in exchange mode:
-each rank owns a bucket range of the index and a source-read range; key
-records, window runs and rows move between ranks with RCCL all-to-all(v) over
-xGMI (torch.distributed "nccl"), and each rank ends with the rows whose src it
-owns.  --sim-world P runs all P ranks of that mode inside one process on one
-GPU (buffers exchanged on the device) to check and time the sharded kernels.
+reads on N GPUs (strong scaling), DESIGN.md §6:
+  --multi replicated (default): every rank builds the whole index and
+    discovers from its source-read range; no data-path collective (the
+    process group carries only the barrier and the step clock);
+  --multi exchange: each rank owns a bucket range of the index and a
+    source-read range; key records, window runs and rows move between ranks
+    with RCCL all-to-all(v) over xGMI (torch.distributed "nccl").
+--sim-world P runs all P ranks of the chosen mode inside one process on one
+GPU (replicated: each rank timed alone, step = slowest rank; exchange:
+buffers exchanged on the device).
 
 Prints ONE JSON line (rank 0).  See DESIGN.md §5 for the roofline numbers.
 """
@@ -140,6 +144,10 @@ def main():
                     help="run all SIM-WORLD ranks of the exchange mode in this process on one GPU")
     ap.add_argument("--exchange", action="store_true",
                     help="use the RCCL exchange mode even with one rank (checks the torch.distributed plumbing)")
+    ap.add_argument("--multi", choices=["replicated", "exchange"], default="replicated",
+                    help="N > 1 (and --sim-world): replicated = every rank builds the whole index and probes its "
+                         "source-read range, no data-path collective (SURVEY 8(e)(ii)); exchange = bucket-range "
+                         "index shards + RCCL all-to-all of keys, runs and rows (SURVEY 8(e) main design)")
     ap.add_argument("--cpu-sample", type=int, default=150_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-ingest", action="store_true", help="skip the device Dataset ingest measurement")
@@ -170,44 +178,83 @@ def main():
 
         from metagenomics_amd.sharded import TorchExchange
 
-        torch.cuda.set_device(local)
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29517")
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local), rank=rank,
-                                world_size=world)  # RCCL over xGMI
-        xchg = TorchExchange(torch.device("cuda", local))
-        mode = "exchange"
+        backend = os.environ.get("MG_BENCH_PG_BACKEND", "nccl")
+        if backend == "gloo" and args.multi == "replicated" and not args.exchange:
+            # rehearsal of the replicated mode with several ranks on fewer GPUs:
+            # it has no data-path collective, so gloo carries the barrier and the clocks
+            local = local % max(1, torch.cuda.device_count())
+            torch.cuda.set_device(local)
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+        else:
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local), rank=rank,
+                                    world_size=world)  # RCCL over xGMI
+        if args.multi == "exchange" or args.exchange:
+            xchg = TorchExchange(torch.device("cuda", local))
+            mode = "exchange"
+        else:
+            mode = "replicated"  # the process group only times the step (barrier, MAX of the clocks)
     elif args.sim_world > 1:
-        from metagenomics_amd.sharded import LocalExchange
+        if args.multi == "exchange":
+            from metagenomics_amd.sharded import LocalExchange
 
-        xchg = LocalExchange(args.sim_world, torch.device("cuda", local))
-        mode = "exchange-sim"
+            xchg = LocalExchange(args.sim_world, torch.device("cuda", local))
+            mode = "exchange-sim"
+        else:
+            mode = "replicated-sim"
     else:
         mode = "fused"
-    P = world if mode == "exchange" else max(1, args.sim_world)
+    P = world if mode in ("exchange", "replicated") else max(1, args.sim_world)
+
+    from metagenomics_amd.sharded import sharded_step, source_range
 
     engines = []
     t0 = time.time()
-    for r in ([rank] if mode == "exchange" else range(P)):
+    for r in ([rank] if mode in ("exchange", "replicated") else range(P)):
         e = OverlapEngine(local)
         e.set_option("nb_log2", args.nb_log2)
         e.set_option("split", 1 if args.split_probe else 0)
         if args.sort_runs is not None:
             e.set_option("sort_runs", args.sort_runs)
-        e.set_shard(r, P, 0, 0)
+        if mode.startswith("replicated"):
+            # the whole index on every rank, this rank's source reads only: the
+            # index build (k_index_build) then a scan + probe of [lo, hi)
+            s_lo, s_hi = source_range(N, r, P)
+            if s_hi == s_lo:  # more ranks than reads (read_hi = 0 would mean "all")
+                e.close()
+                continue
+            e.set_shard(0, 1, s_lo, s_hi)
+            e.set_option("overlap_scan", 0)
+        else:
+            e.set_shard(r, P, 0, 0)
         e.upload(ds)
         engines.append(e)
     log(f"[bench] rank {rank}: upload {time.time() - t0:.2f}s ({mode}, P={P})")
 
-    from metagenomics_amd.sharded import sharded_step
+    rank_ms = [0.0] * len(engines)  # replicated-sim: per simulated rank, summed over the timed steps
 
     def step():
         """one pass of the hot path; returns directed rows held by this process"""
-        if mode == "fused":
+        if mode in ("fused", "replicated"):
+            if not engines:
+                return 0
             e = engines[0]
             e.build_index(l, k)
             e.mark_contained(copy=False)
             return e.find_overlaps()
+        if mode == "replicated-sim":
+            tot = 0
+            for i, e in enumerate(engines):  # the ranks one after the other, each timed alone
+                torch.cuda.synchronize(local)
+                ta = time.perf_counter()
+                e.build_index(l, k)
+                e.mark_contained(copy=False)
+                tot += e.find_overlaps()
+                torch.cuda.synchronize(local)
+                rank_ms[i] += (time.perf_counter() - ta) * 1e3
+            return tot
         res = sharded_step(engines, xchg, l, k)
         for kk, v in res.ms.items():
             phase_ms[kk] = phase_ms.get(kk, 0.0) + v
@@ -237,6 +284,7 @@ def main():
     dev_ms = {"index_ms": 0.0, "contained_ms": 0.0, "overlap_ms": 0.0, "scan_ms": 0.0, "probe_ms": 0.0,
               "verify_ms": 0.0, "total_ms": 0.0}
     phase_ms.clear()
+    rank_ms[:] = [0.0] * len(engines)
     sync_barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -250,11 +298,18 @@ def main():
     sync_barrier()
     ms_step = (t1 - t0) * 1000.0 / args.steps
     dev_ms = {kk: v / args.steps for kk, v in dev_ms.items()}
+    sim_rank_ms = None
+    if mode == "replicated-sim":
+        # P ranks with no data-path collective: the job's step is its slowest rank
+        sim_rank_ms = [v / args.steps for v in rank_ms]
+        ms_step = max(sim_rank_ms)
+        dev_ms = {kk: v / P for kk, v in dev_ms.items()}
     if dist is not None:
-        tt = torch.tensor([ms_step], dtype=torch.float64, device="cuda")
+        red_dev = "cpu" if dist.get_backend() == "gloo" else "cuda"
+        tt = torch.tensor([ms_step], dtype=torch.float64, device=red_dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         ms_step = float(tt.item())
-        ee = torch.tensor([rows], dtype=torch.int64, device="cuda")
+        ee = torch.tensor([rows], dtype=torch.int64, device=red_dev)
         dist.all_reduce(ee, op=dist.ReduceOp.SUM)
         rows = int(ee.item())
     edges = rows // 2
@@ -290,9 +345,13 @@ def main():
         achieved = alg / P / (kern_ms / 1000.0) / 1e9 if kern_ms > 0 else 0.0
         roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                "kernel": "rank 0 step kernels (key records + insert, scan, probe)",
+                "kernel": ("rank 0 step kernels (whole index build, scan + probe of its source range)"
+                           if mode.startswith("replicated") else
+                           "rank 0 step kernels (key records + insert, scan, probe)"),
                 "alg_bytes_per_step": alg / P, "kernel_ms_per_step": kern_ms}
     par = {"fused": "1 GPU, fused path",
+           "replicated": f"{P} ranks: whole index on every rank, source-read range shards, no data-path collective",
+           "replicated-sim": f"{P} simulated ranks on 1 GPU (whole index each, source-read shards; step = slowest rank)",
            "exchange": f"{P} ranks: bucket-range index + source-range shards, RCCL all-to-all",
            "exchange-sim": f"{P} simulated ranks on 1 GPU (device-local exchange)"}[mode]
     res = {
@@ -317,6 +376,8 @@ def main():
         "counters": cnt,
         "roofline": roof,
     }
+    if sim_rank_ms is not None:
+        res["sim_rank_ms"] = sim_rank_ms
     if world == 1 and mode == "fused" and args.replay:
         from metagenomics_amd.overlap import UnitigGraph
 

@@ -617,6 +617,15 @@ struct ProbeParams {
   uint64_t cand_cap;
 };
 
+// Which side of a self-symmetric (o = 2/3) discovery pair {a, b} emits it:
+// exactly one of rc_side_keeps(a, b), rc_side_keeps(b, a) holds for a != b,
+// and a self pair is kept.  Alternating by the parity of a + b (instead of
+// "b >= a") spreads the pairs evenly over the source IDs, so source-range
+// shards (bench --multi replicated) carry even verification loads.
+__device__ __forceinline__ bool rc_side_keeps(uint32_t a, uint32_t b) {
+  return a == b || (((a ^ b) & 1u) ? b > a : b < a);
+}
+
 template <int MAXW>
 struct ProbeLds {
   static constexpr int CAND = 3 * kWave;  // candidate list (verified 64 at a time)
@@ -865,8 +874,8 @@ __global__ __launch_bounds__(kBlock) void k_probe(ProbeParams p) {
       const int oo = (int)(hi & 3u);
       bool keep = e[s] != kEmpty && ((hi >> 12) & kFpMask) == fp && j >= rjlo && j <= rjhi;
       // halving: o=1 hits are twins of the partner's o=0
-      // hits; o=2/3 hits are kept only for partner >= source
-      keep = keep && (CONTAIN || oo == 0 || (oo >= 2 && (uint32_t)e[s] >= ra));
+      // hits; an o=2/3 pair is kept on one side only (rc_side_keeps)
+      keep = keep && (CONTAIN || oo == 0 || (oo >= 2 && rc_side_keeps(ra, (uint32_t)e[s])));
       keepm |= (keep ? 1u : 0u) << s;
     }
     if (SPLIT) {

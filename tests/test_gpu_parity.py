@@ -467,6 +467,33 @@ def test_sorted_runs_path(name):
     assert {str(i): int(s) for i, s in enumerate(sup) if s} == meta["super"]
 
 
+@pytest.mark.parametrize("name", FIXTURES)
+def test_replicated_index_source_shards(name):
+    """Multi-GPU replicated mode (bench --multi replicated): every rank builds
+    the whole index and discovers only from its source-read range; each rank
+    holds its discoveries' rows and twins (DESIGN.md §4 halving: every pair is
+    discovered from one side only), and the union over ranks is the reference
+    multiset."""
+    from metagenomics_amd.sharded import source_range
+
+    meta = load_meta(name)
+    ds = Dataset.from_files([fixture_input(name)], meta["l"])
+    P = 3
+    parts = []
+    for r in range(P):
+        lo, hi = source_range(ds.num_unique, r, P)
+        if hi == lo:  # an empty range (read_hi = 0 would mean "all")
+            continue
+        e = OverlapEngine(0)
+        e.set_option("overlap_scan", 0)
+        rows, sup = gpu_rows(e, ds, meta["l"], shard=(0, 1, lo, hi))
+        e.close()
+        assert {str(i): int(s) for i, s in enumerate(sup) if s} == meta["super"]
+        parts.append(rows)
+    allrows = np.concatenate(parts) if parts else parts
+    assert np.array_equal(rows_to_tuples(allrows), golden_rows(name))
+
+
 @pytest.mark.parametrize("name", ["mixed", "tandem", "highdup", "dirty"])
 def test_scan_inside_probe_path(name):
     """option overlap_scan = 0: the window scan runs inside each probe pass

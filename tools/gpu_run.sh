@@ -23,8 +23,13 @@ for s in $STEPS; do
     rc=$?; echo "bench rc=$rc"; cat $OUT/bench.json ;;
   sim)
     for P in 2 4 8; do
-      timeout -k 10 300 python -u bench.py --sim-world $P --steps 3 > $OUT/bench_sim$P.json 2> $OUT/bench_sim$P.err
+      timeout -k 10 300 python -u bench.py --sim-world $P --multi exchange --steps 3 > $OUT/bench_sim$P.json 2> $OUT/bench_sim$P.err
       rc=$?; echo "bench sim $P rc=$rc"; cat $OUT/bench_sim$P.json; [ $rc -ne 0 ] && break
+    done ;;
+  simrep)
+    for P in 2 4 8; do
+      timeout -k 10 300 python -u bench.py --sim-world $P --multi replicated --steps 3 --no-cpu-baseline --no-ingest > $OUT/bench_simrep$P.json 2> $OUT/bench_simrep$P.err
+      rc=$?; echo "bench sim replicated $P rc=$rc"; python3 -c "import json;d=json.load(open('$OUT/bench_simrep$P.json'));print(d['ms_per_step'], d['value'], d['undirected_edges'], d.get('sim_rank_ms'))"; [ $rc -ne 0 ] && break
     done ;;
   xchg1)
     timeout -k 10 300 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29511 bench.py --exchange --steps 3 --no-cpu-baseline > $OUT/bench_xchg1.json 2> $OUT/bench_xchg1.err
@@ -63,7 +68,7 @@ for s in $STEPS; do
     timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/profsort -o kt -- python3 bench.py --steps 3 --no-cpu-baseline --no-ingest --sort-runs 1 > $OUT/profsort_bench.json 2> $OUT/profsort_bench.err
     rc=$?; echo "profsort rc=$rc"; python3 -c "import json;d=json.load(open('$OUT/profsort_bench.json'));print(d['ms_per_step'], d['device_ms'])"; head -12 $OUT/profsort/kt_kernel_stats.csv | cut -c1-150 ;;
   profsim)
-    timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/profsim -o kt -- python3 bench.py --sim-world 4 --steps 2 --no-cpu-baseline > $OUT/profsim_bench.json 2> $OUT/profsim_bench.err
+    timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/profsim -o kt -- python3 bench.py --sim-world 4 --multi exchange --steps 2 --no-cpu-baseline > $OUT/profsim_bench.json 2> $OUT/profsim_bench.err
     rc=$?; echo "profsim rc=$rc"; cat $OUT/profsim_bench.json; cat $OUT/profsim/kt_kernel_stats.csv ;;
   pmcsq)
     i=0
