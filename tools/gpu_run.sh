@@ -49,6 +49,9 @@ for s in $STEPS; do
   parse)
     timeout -k 10 900 python -u tools/parse_bench.py > $OUT/parse_bench.json 2> $OUT/parse_bench.err
     rc=$?; echo "parse rc=$rc"; tail -12 $OUT/parse_bench.err; cat $OUT/parse_bench.json ;;
+  indexcost)
+    timeout -k 10 300 python -u tools/index_cost.py > $OUT/index_cost.log 2>&1
+    rc=$?; echo "indexcost rc=$rc"; grep index_ms $OUT/index_cost.log ;;
   variants)
     timeout -k 10 400 python -u tools/variant_sweep.py > $OUT/variant_sweep.log 2>&1
     rc=$?; echo "variants rc=$rc"; grep opts $OUT/variant_sweep.log ;;
