@@ -47,17 +47,25 @@ CONFIGS = {
     "c1": (100_000, 100, 100, 500_000, 40, 21, 7, "C1: 100k x 100 bp, l=40, k=21"),
     "c2": (1_000_000, 150, 150, 7_500_000, 50, 31, 21, "C2: 1M x 150 bp, l=50, k=31"),
     "c3": (10_000_000, 150, 150, 75_000_000, 50, 31, 31, "C3: 10M x 150 bp, l=50, k=31"),
+    # C5 (BASELINE configs[4]): metagenome of 100 random genomes, log-normal
+    # abundance, 437.5 Mb in total (20x mean coverage), 100-250 bp reads
+    "c5": (50_000_000, 100, 250, 437_500_000, 50, 31, 55,
+           "C5: 50M x 100-250 bp metagenome (100 genomes), l=50, k=31"),
 }
+META_GENOMES = {"c5": 100}
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def make_dataset(cfg, nthreads):
+def make_dataset(cfg, nthreads, name=""):
     n, lo, hi, G, l, k, seed, _ = cfg
     t0 = time.time()
-    c, L = synth.uniform_read_set(n, 0, G, seed=seed, lo=lo, hi=hi)
+    if name in META_GENOMES:
+        c, L = synth.metagenome_read_set(n, lo, hi, META_GENOMES[name], G, seed)
+    else:
+        c, L = synth.uniform_read_set(n, 0, G, seed=seed, lo=lo, hi=hi)
     t1 = time.time()
     ds = Dataset.from_codes(c, L, l, nthreads=nthreads)
     t2 = time.time()
@@ -166,7 +174,7 @@ def main():
     cfg = CONFIGS[args.config]
     n, lo, hi, G, l, k, seed, desc = cfg
     nthreads = max(2, 16 // max(1, world))
-    ds, codes, lens, host_ingest_s = make_dataset(cfg, nthreads)
+    ds, codes, lens, host_ingest_s = make_dataset(cfg, nthreads, args.config)
     N = ds.num_unique
 
     import torch

@@ -56,15 +56,21 @@ def sample_reads(genome: np.ndarray, n_reads: int, lo: int, hi: int, seed: int,
             c[m] = 3 - c[m][:, ::-1]
             codes[a:b] = c
         return codes, lengths.astype(np.uint16)
+    # mixed lengths: windows of hi bases of a zero-padded genome.  A forward read
+    # is the window at its start; a reverse-complemented one is the window that
+    # ENDS at its last base, reversed and complemented (so its first len codes
+    # are rc(genome[start:start+len])); codes past len are zeroed.
     k = np.arange(hi, dtype=np.int64)[None, :]
+    gp = np.zeros(G + 2 * hi, dtype=np.uint8)
+    gp[hi:hi + G] = genome
+    win = np.lib.stride_tricks.sliding_window_view(gp, hi)
     for a in range(0, n_reads, chunk):
         b = min(n_reads, a + chunk)
-        idx = np.minimum(starts[a:b, None] + k, G - 1)
-        c = genome[idx]
-        c[k >= lengths[a:b, None]] = 0
-        m = rc[a:b]
+        s0, ln, m = starts[a:b], lengths[a:b], rc[a:b]
+        c = win[s0 + hi]
         if m.any():
-            c[m] = revcomp_codes(c[m], lengths[a:b][m])
+            c[m] = 3 - win[s0[m] + ln[m]][:, ::-1]
+        c[k >= ln[:, None]] = 0
         codes[a:b] = c
     return codes, lengths.astype(np.uint16)
 
