@@ -59,6 +59,7 @@ struct mg_ctx {
   uint64_t read_lo = 0, read_hi = 0;
   uint32_t max_blocks = 8192;  // cap on the persistent discovery grid (blocks of 4 wavefronts)
   int phase_limit = 99;        // diagnostics (option "phase_limit")
+  bool halving_low = false;    // option "halving": o=2/3 pair side rule
   int n_cu = 256;              // compute units of the device
   uint64_t nreg = 0;           // row regions of the last discovery launch (one per probe wavefront)
   uint64_t nrun_reg = 0;       // run regions (one per scan wavefront)

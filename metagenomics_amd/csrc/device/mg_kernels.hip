@@ -611,6 +611,7 @@ struct ProbeParams {
   int uniform_len;                // every read has this length (0: lengths differ)
   unsigned long long* stats;      // optional [kSegs*4]: runs probed, entries scanned, partners fetched, rows
   int phase_limit;                // diagnostics: 4 no probe, 5 + cell loads, 6 + filter, 7 full
+  int halving_low;                // option "halving" = 1: keep o=2/3 pairs at the lower ID (else rc_side_keeps)
   // split path (k_probe<SPLIT=true> + k_verify): candidates {partner, source, o << 30 | j}
   uint3* cand;                    // one region of cand_cap records per probe wavefront
   unsigned long long* cand_cnt;   // [waves] candidates written (may exceed cand_cap)
@@ -875,7 +876,8 @@ __global__ __launch_bounds__(kBlock) void k_probe(ProbeParams p) {
       bool keep = e[s] != kEmpty && ((hi >> 12) & kFpMask) == fp && j >= rjlo && j <= rjhi;
       // halving: o=1 hits are twins of the partner's o=0
       // hits; an o=2/3 pair is kept on one side only (rc_side_keeps)
-      keep = keep && (CONTAIN || oo == 0 || (oo >= 2 && rc_side_keeps(ra, (uint32_t)e[s])));
+      keep = keep && (CONTAIN || oo == 0 ||
+                      (oo >= 2 && (p.halving_low ? (uint32_t)e[s] >= ra : rc_side_keeps(ra, (uint32_t)e[s]))));
       keepm |= (keep ? 1u : 0u) << s;
     }
     if (SPLIT) {
@@ -1309,8 +1311,10 @@ __global__ __launch_bounds__(kBlock) void k_super_finalize(const unsigned long l
     s = k ? (0xFFFFFFFFu - (uint32_t)k) + 1u : 0u;  // container index -> ID
     super[i] = s;
   }
-  // one flag update per wavefront (every lane on one address serialises: 8.9 ms at C5)
-  if (__ballot(s != 0) && (threadIdx.x & 63) == 0) atomicOr(any, 1u);
+  // the flag is set once: waves that already see it set skip the atomic
+  // (an atomic per contained read on one address serialised: 8.9 ms at C5)
+  if (__ballot(s != 0) && (threadIdx.x & 63) == 0 && __hip_atomic_load(any, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u)
+    atomicOr(any, 1u);
 }
 
 // getListOfReads(key) (HashTable.cpp:202-221): walk the query key's home cell
@@ -1576,6 +1580,7 @@ struct LaunchProbe {
     pp.uniform_len = ctx->minlen == ctx->maxlen ? (int)ctx->maxlen : 0;
     pp.stats = contain ? nullptr : (ctx->stats ? ctx->d_stats : nullptr);
     pp.phase_limit = contain ? 99 : ctx->phase_limit;
+    pp.halving_low = ctx->halving_low ? 1 : 0;
     if (ctx->split) return run_split(ctx, contain, pp, grid, total_runs);
     const size_t lds = (size_t)kWavesPerBlock * ProbeLds<W>::bytes;
     if (contain)
@@ -1914,6 +1919,10 @@ int mg_set_option(mg_ctx* ctx, const char* name, int64_t value) {
     ctx->overlap_scan = value != 0;
     ctx->scan_state = 0;
     ctx->sorted_state = 0;
+    return 0;
+  }
+  if (!strcmp(name, "halving")) {  // 0: parity-alternating o=2/3 side (default), 1: lower ID keeps
+    ctx->halving_low = value != 0;
     return 0;
   }
   if (!strcmp(name, "sort_runs")) {

@@ -14,10 +14,10 @@ n = int(sys.argv[1]) if len(sys.argv) > 1 else 10_000_000
 c, L = synth.uniform_read_set(n, 150, n * 150 // 20, seed=31)
 ds = Dataset.from_codes(c, L, 50, nthreads=16)
 VARIANTS = [
-    {"overlap_scan": 1},
-    {"sort_runs": 1},
-    {"sort_runs": 1, "sort_bits": 16},
-    {"sort_runs": 1, "sort_bits": 12},
+    {"halving": 0},
+    {"halving": 1},
+    {"halving": 0},
+    {"halving": 1},
 ]
 res = []
 for opts in VARIANTS:
