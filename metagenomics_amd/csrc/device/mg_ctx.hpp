@@ -106,6 +106,9 @@ struct mg_ctx {
   unsigned long long* d_run_off = nullptr;
   size_t run_off_cap = 0;
   uint64_t n_sorted = 0;
+  bool scan_flat = false;          // the shared scan wrote d_sk[0] / d_sm[0] directly
+  unsigned long long* d_flat_cursor = nullptr;
+  uint64_t flat_need = 0, n_flat = 0;
   int sorted_state = 0;  // 0 none, 2 sorted (for the current scan)
   int sort_bits = 0;     // diagnostics: sort only the top sort_bits bucket bits (0: all)
   mg_timings t{};

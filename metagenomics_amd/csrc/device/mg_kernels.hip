@@ -145,6 +145,8 @@ constexpr int kScanBuf = 3 * 64;  // staged run metas per scan wavefront (two pu
 constexpr uint64_t kEmpty = ~0ULL;       // free slot (a read index is never 0xFFFFFFFF)
 constexpr uint64_t kChain = 1ULL << 63;  // on a cell's last slot: the chain continues in the next cell
 constexpr uint32_t kFpMask = (1u << kFpBits) - 1;
+constexpr uint64_t kFlatChunk = 512;   // flat scan output: records per wavefront chunk
+constexpr uint64_t kFlatHole = ~0ULL;  // meta of an unused flat slot (a run meta never has bit 63)
 
 struct IndexParams {
   const uint64_t* words;
@@ -307,6 +309,12 @@ struct ScanParams {
   uint64_t run_cap;
   uint64_t* cells;                // k_scan<INDEX>: the (unsharded) cell table the keys go into
   uint64_t cell_n;
+  // flat SoA output (option "sort_runs"): x / meta arrays filled through one
+  // cursor, 64 records per atomic; regions are not written
+  uint64_t* flat_keys;
+  uint64_t* flat_meta;
+  unsigned long long* flat_cursor;
+  uint64_t flat_cap;
 };
 
 __device__ __forceinline__ void wave_sync() {
@@ -357,6 +365,7 @@ __global__ __launch_bounds__(kBlock) void k_scan(ScanParams p) {
   const uint64_t nbmask = (1ULL << p.nb_log2) - 1;
   uint64_t cursor = 0;
   uint32_t nbuf = 0;  // run metas staged in s_buf (wavefront-uniform)
+  uint64_t fbase = 0, fused = 0, fcap = 0;  // flat output: current chunk, records used, chunk size
 
   // close the run of minimizer position pos over windows [jlo, jhi]: stage its
   // meta in LDS (the hashing and the HBM write happen 64 at a time in flush)
@@ -379,7 +388,33 @@ __global__ __launch_bounds__(kBlock) void k_scan(ScanParams p) {
       flag = owned(v & nbmask, p.nb_log2, p.rank, p.nranks);
     }
     const uint64_t bal = __ballot(flag);
-    if (flag) {
+    if (p.flat_keys) {
+      // this wavefront's current chunk of the flat arrays; a new chunk (one
+      // atomic per kFlatChunk records: a cursor bumped per flush serialised at
+      // 20 ms) takes whatever does not fit in the current one
+      const uint64_t npop = (uint64_t)__popcll(bal);
+      const uint64_t room = fcap - fused;
+      unsigned long long nbase = 0;
+      if (npop > room) {
+        if (lane == 0) nbase = atomicAdd(p.flat_cursor, (unsigned long long)kFlatChunk);
+        nbase = __shfl(nbase, 0);
+      }
+      if (flag) {
+        const uint64_t pr = lane_prefix(bal);
+        const uint64_t at = pr < room ? fbase + fused + pr : nbase + (pr - room);
+        if (at < p.flat_cap) {
+          p.flat_keys[at] = v;
+          p.flat_meta[at] = meta;
+        }
+      }
+      if (npop > room) {
+        fbase = nbase;
+        fused = npop - room;
+        fcap = kFlatChunk;
+      } else {
+        fused += npop;
+      }
+    } else if (flag) {
       const uint64_t at = cursor + lane_prefix(bal);
       if (at < p.run_cap) region[at] = make_ulonglong2(v, meta);
     }
@@ -540,6 +575,15 @@ __global__ __launch_bounds__(kBlock) void k_scan(ScanParams p) {
     }
   }
   while (nbuf) flush(nbuf < (uint32_t)kWave ? nbuf : (uint32_t)kWave);
+  if (p.flat_keys) {  // the unused tail of the last chunk: records the probe skips
+    for (uint64_t i = fused + lane; i < fcap; i += kWave) {
+      const uint64_t at = fbase + i;
+      if (at < p.flat_cap) {
+        p.flat_keys[at] = kEmpty;
+        p.flat_meta[at] = kFlatHole;
+      }
+    }
+  }
   if (lane == 0) p.run_cnt[gw] = cursor;
 }
 
@@ -813,7 +857,7 @@ __global__ __launch_bounds__(kBlock) void k_probe(ProbeParams p) {
       return true;
     }
     if (pf_any) {
-      valid = pf_ok;
+      valid = pf_ok && rec_pf.y != kFlatHole;
       meta = rec_pf.y;
       if (valid && (p.src_super || p.src_hi)) {  // contained or foreign sources contribute no windows
         const uint32_t ra = (uint32_t)meta;
@@ -1485,7 +1529,7 @@ DiscGeom disc_geom(mg_ctx* ctx, bool contain, uint64_t nsrc) {
 template <int W>
 struct LaunchScan {
   static int run(mg_ctx* ctx, bool contain, uint64_t a_lo, uint64_t a_hi, uint32_t sgrid, bool filter,
-                 hipStream_t stream = nullptr, bool no_super = false, bool index = false) {
+                 hipStream_t stream = nullptr, bool no_super = false, bool index = false, bool flat = false) {
     if (!stream) stream = ctx->stream;
     const uint64_t nw = (uint64_t)sgrid * kWavesPerBlock;  // scan wavefronts = run regions
     ctx->nrun_reg = nw;
@@ -1527,6 +1571,32 @@ struct LaunchScan {
     const size_t lds = (size_t)kWavesPerBlock * (((ctx->w * kWave + 1) / 2) + kScanBuf) * sizeof(uint64_t);
     sp.cells = ctx->d_cells;
     sp.cell_n = ctx->cell_n;
+    ctx->scan_flat = flat;
+    if (flat) {
+      // SoA output for the bucket sort: ~2 J / (w + 1) + 1 runs per read, sized
+      // with 20 % slack (or the exact need after an overflow)
+      const uint64_t est = (a_hi - a_lo) * (2 * J / (ctx->w + 1) + 2) * 6 / 5 + 4096;
+      const uint64_t cap = std::max<uint64_t>(ctx->flat_need, est);
+      if (cap > ctx->sk_cap) {
+        for (int b = 0; b < 2; ++b) {
+          if (ctx->d_sk[b]) (void)hipFree(ctx->d_sk[b]);
+          if (ctx->d_sm[b]) (void)hipFree(ctx->d_sm[b]);
+          ctx->d_sk[b] = ctx->d_sm[b] = nullptr;
+        }
+        ctx->sk_cap = 0;
+        for (int b = 0; b < 2; ++b) {
+          if (hipMalloc(&ctx->d_sk[b], cap * sizeof(uint64_t)) != hipSuccess) return -1;
+          if (hipMalloc(&ctx->d_sm[b], cap * sizeof(uint64_t)) != hipSuccess) return -1;
+        }
+        ctx->sk_cap = cap;
+      }
+      if (!ctx->d_flat_cursor && hipMalloc(&ctx->d_flat_cursor, sizeof(unsigned long long)) != hipSuccess) return -1;
+      if (hipMemsetAsync(ctx->d_flat_cursor, 0, sizeof(unsigned long long), stream) != hipSuccess) return -1;
+      sp.flat_keys = ctx->d_sk[0];
+      sp.flat_meta = ctx->d_sm[0];
+      sp.flat_cursor = ctx->d_flat_cursor;
+      sp.flat_cap = ctx->sk_cap;
+    }
     (void)hipEventRecord(ctx->ev[6], stream);
     if (index) {  // unsharded only (the whole key space is this context's)
       allow_lds(k_scan<W, true>, lds);
@@ -1785,7 +1855,8 @@ void mg_destroy(mg_ctx* ctx) {
   void* bufs[] = {ctx->d_words, ctx->d_len, ctx->d_cells,
                   ctx->d_superkey, ctx->d_super, ctx->d_any, ctx->d_rows, ctx->d_seg, ctx->d_stats,
                   ctx->d_compact, ctx->d_runs, ctx->d_run_cnt, ctx->d_keyrec, ctx->d_blk, ctx->d_flat_cnt, ctx->d_cand, ctx->d_cand_cnt, ctx->d_freq,
-                  ctx->d_sk[0], ctx->d_sk[1], ctx->d_sm[0], ctx->d_sm[1], ctx->d_sort_tmp, ctx->d_run_off};
+                  ctx->d_sk[0], ctx->d_sk[1], ctx->d_sm[0], ctx->d_sm[1], ctx->d_sort_tmp, ctx->d_run_off,
+                  ctx->d_flat_cursor};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   for (auto& e : ctx->ev)
@@ -2175,18 +2246,36 @@ struct LaunchScanAll {
     const uint64_t groups = (ctx->n + kWave - 1) / kWave;
     const uint32_t sgrid = index ? resident_blocks(ctx, k_scan<W, true>, lds, (groups + kWavesPerBlock - 1) / kWavesPerBlock)
                                  : resident_blocks(ctx, k_scan<W, false>, lds, (groups + kWavesPerBlock - 1) / kWavesPerBlock);
-    return LaunchScan<W>::run(ctx, true, 0, ctx->n, sgrid, false, st, true, index);
+    return LaunchScan<W>::run(ctx, true, 0, ctx->n, sgrid, false, st, true, index, ctx->sort_runs && !ctx->split);
   }
 };
 
 bool shared_scan(const mg_ctx* ctx) { return ctx->nranks == 1 && ctx->overlap_scan; }
 
 // the shared scan's region counts settled (rerun without the index part on overflow)
+// flat scan output: the cursor is the run count; on overflow size for it and rerun
+int settle_flat(mg_ctx* ctx, bool* again) {
+  *again = false;
+  unsigned long long c = 0;
+  if (ctx->n) MG_TRY(hipMemcpyAsync(&c, ctx->d_flat_cursor, sizeof(c), hipMemcpyDeviceToHost, ctx->stream));
+  MG_TRY(hipStreamSynchronize(ctx->stream));
+  if (c > ctx->sk_cap) {
+    ctx->flat_need = c + c / 8 + 4096;
+    *again = true;
+  }
+  ctx->n_flat = c;
+  return 0;
+}
+
+int settle_scan(mg_ctx* ctx, bool* again) {
+  return ctx->scan_flat ? settle_flat(ctx, again) : settle_runs(ctx, again);
+}
+
 int ensure_scan(mg_ctx* ctx) {
   if (ctx->scan_state == 2) return 0;
   if (ctx->scan_state == 1) {
     bool again = false;
-    if (settle_runs(ctx, &again)) return -1;
+    if (settle_scan(ctx, &again)) return -1;
     ctx->scan_state = again ? 0 : 2;
     if (!again) return 0;
   }
@@ -2196,7 +2285,7 @@ int ensure_scan(mg_ctx* ctx) {
       return set_err(ctx, "scan launch failed");
     if (!ctx->n) ctx->nrun_reg = 0;
     bool again = false;
-    if (settle_runs(ctx, &again)) return -1;
+    if (settle_scan(ctx, &again)) return -1;
     if (!again) {
       ctx->scan_state = 2;
       return 0;
@@ -2209,7 +2298,9 @@ template <int W>
 struct LaunchProbeShared {
   static int run(mg_ctx* ctx, bool contain) {
     uint64_t total = 0;
-    for (uint64_t r = 0; r < ctx->nrun_reg; ++r) total += std::min<uint64_t>(ctx->run_cnt_host[r], ctx->run_cap);
+    if (!ctx->scan_flat)  // (a flat scan leaves no per-region counts on the host)
+      for (uint64_t r = 0; r < ctx->nrun_reg && r < ctx->run_cnt_host.size(); ++r)
+        total += std::min<uint64_t>(ctx->run_cnt_host[r], ctx->run_cap);
     const DiscGeom g = disc_geom<W>(ctx, contain, std::max<uint64_t>(ctx->n, 1));
     const uint32_t* sup = (!contain && ctx->contained_done && ctx->super_any) ? ctx->d_super : nullptr;
     const uint64_t lo = contain ? 0 : ctx->read_lo;
@@ -2242,13 +2333,14 @@ struct LaunchProbeShared {
 // (diagnostics) sorts only the top sort_bits bucket bits.
 int sort_shared_runs(mg_ctx* ctx) {
   if (ctx->sorted_state == 2) return 0;
-  const uint64_t nreg = ctx->nrun_reg;
+  const bool flat = ctx->scan_flat;  // the scan already wrote d_sk[0] / d_sm[0]
+  const uint64_t nreg = flat ? 0 : ctx->nrun_reg;
   std::vector<unsigned long long> off(nreg + 1, 0);
   for (uint64_t r = 0; r < nreg; ++r) off[r + 1] = off[r] + std::min<uint64_t>(ctx->run_cnt_host[r], ctx->run_cap);
-  const uint64_t n = off[nreg];
+  const uint64_t n = flat ? ctx->n_flat : off[nreg];
   if (n > 0x7FFFFFFFull) return set_err(ctx, "sort_runs: more than 2^31 runs");
   MG_TRY(ensure(&ctx->d_run_off, &ctx->run_off_cap, nreg + 1));
-  if (n > ctx->sk_cap) {
+  if (!flat && n > ctx->sk_cap) {
     for (int b = 0; b < 2; ++b) {
       if (ctx->d_sk[b]) (void)hipFree(ctx->d_sk[b]);
       if (ctx->d_sm[b]) (void)hipFree(ctx->d_sm[b]);
@@ -2262,8 +2354,9 @@ int sort_shared_runs(mg_ctx* ctx) {
     ctx->sk_cap = n;
   }
   MG_TRY(hipEventRecord(ctx->ev[10], ctx->stream));
-  MG_TRY(hipMemcpyAsync(ctx->d_run_off, off.data(), (nreg + 1) * sizeof(unsigned long long), hipMemcpyHostToDevice,
-                        ctx->stream));
+  if (!flat)
+    MG_TRY(hipMemcpyAsync(ctx->d_run_off, off.data(), (nreg + 1) * sizeof(unsigned long long),
+                          hipMemcpyHostToDevice, ctx->stream));
   if (nreg)
     hipLaunchKernelGGL(k_runs_soa, dim3((uint32_t)nreg), dim3(kBlock), 0, ctx->stream, ctx->d_runs, ctx->run_cap,
                        ctx->d_run_off, ctx->d_sk[0], ctx->d_sm[0]);

@@ -13,12 +13,7 @@ from metagenomics_amd.overlap import Dataset, OverlapEngine  # noqa: E402
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 10_000_000
 c, L = synth.uniform_read_set(n, 150, n * 150 // 20, seed=31)
 ds = Dataset.from_codes(c, L, 50, nthreads=16)
-VARIANTS = [
-    {"halving": 0},
-    {"halving": 1},
-    {"halving": 0},
-    {"halving": 1},
-]
+VARIANTS = [{"sort_runs": i % 2} for i in range(8)]
 res = []
 for opts in VARIANTS:
     e = OverlapEngine(0)
@@ -27,7 +22,7 @@ for opts in VARIANTS:
     e.upload(ds)
     ts = []
     rows = 0
-    for _ in range(4):
+    for _ in range(6):
         e.build_index(50, 31)
         e.mark_contained(copy=False)
         rows = e.find_overlaps()
