@@ -357,9 +357,10 @@ __global__ __launch_bounds__(kBlock) void k_scan(ScanParams p) {
   const int msh = 64 - 2 * m;
   const uint64_t mmask = (m == 32) ? ~0ULL : ((1ULL << (2 * m)) - 1);
   const uint64_t ngroups = (p.a_hi - p.a_lo + kWave - 1) / kWave;
-  const uint64_t gw = (uint64_t)blockIdx.x * kWavesPerBlock + wv;
-  const uint64_t nw = (uint64_t)gridDim.x * kWavesPerBlock;
-  uint64_t* s_buf = reinterpret_cast<uint64_t*>(smem) + (size_t)kWavesPerBlock * ((w * kWave + 1) / 2) +
+  const int wpb = (int)(blockDim.x >> 6);  // 4, or fewer when w's LDS arrays need it (scan_wpb)
+  const uint64_t gw = (uint64_t)blockIdx.x * wpb + wv;
+  const uint64_t nw = (uint64_t)gridDim.x * wpb;
+  uint64_t* s_buf = reinterpret_cast<uint64_t*>(smem) + (size_t)wpb * ((w * kWave + 1) / 2) +
                     (size_t)wv * kScanBuf;
   ulonglong2* const region = p.runs + gw * p.run_cap;
   const uint64_t nbmask = (1ULL << p.nb_log2) - 1;
@@ -1486,12 +1487,23 @@ struct LaunchIndex {
 // second, partly idle round of wavefronts).  Scan and probe use the same
 // wavefront count: probe wavefront r consumes scan region r.
 template <typename K>
-uint32_t resident_blocks(mg_ctx* ctx, K kernel, size_t lds, uint64_t want) {
+uint32_t resident_blocks(mg_ctx* ctx, K kernel, size_t lds, uint64_t want, int block = kBlock) {
   allow_lds(kernel, lds);
   int per_cu = 0;
-  (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kBlock, lds);
+  (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, block, lds);
   const uint64_t resident = (uint64_t)std::max(1, per_cu) * (uint64_t)std::max(1, ctx->n_cu);
   return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(std::min<uint64_t>(want, resident), ctx->max_blocks));
+}
+
+// LDS of one scan wavefront: the w suffix-minimum keys per lane + the staged
+// run metas; blocks carry 4 wavefronts, or 2 / 1 when that does not fit
+// (long windows: w = l - k grows with min_overlap).  0 = w too large.
+constexpr size_t kLdsPerCu = 160 * 1024;
+inline size_t scan_lds_per_wave(uint32_t w) { return (((size_t)w * kWave + 1) / 2 + kScanBuf) * sizeof(uint64_t); }
+inline uint32_t scan_wpb(uint32_t w) {
+  for (uint32_t wpb = kWavesPerBlock; wpb >= 1; wpb >>= 1)
+    if (wpb * scan_lds_per_wave(w) <= kLdsPerCu) return wpb;
+  return 0;
 }
 
 // Geometry of one discovery pass over source reads [a_lo, a_hi): probe grid =
@@ -1507,7 +1519,7 @@ DiscGeom disc_geom(mg_ctx* ctx, bool contain, uint64_t nsrc) {
   DiscGeom g;
   const uint64_t ngroups = (nsrc + kWave - 1) / kWave;
   const uint64_t want = std::max<uint64_t>(1, (ngroups + kWavesPerBlock - 1) / kWavesPerBlock);
-  g.lds_scan = (size_t)kWavesPerBlock * (((ctx->w * kWave + 1) / 2) + kScanBuf) * sizeof(uint64_t);
+  g.lds_scan = (size_t)scan_wpb(ctx->w) * scan_lds_per_wave(ctx->w);
   if (ctx->split) {
     g.lds_probe = (size_t)kWavesPerBlock * ProbeLds<W>::split_bytes;
     g.grid = contain ? resident_blocks(ctx, k_probe<W, true, true>, g.lds_probe, want)
@@ -1517,7 +1529,7 @@ DiscGeom disc_geom(mg_ctx* ctx, bool contain, uint64_t nsrc) {
     g.grid = contain ? resident_blocks(ctx, k_probe<W, true, false>, g.lds_probe, want)
                      : resident_blocks(ctx, k_probe<W, false, false>, g.lds_probe, want);
   }
-  const uint32_t scan_res = resident_blocks(ctx, k_scan<W, false>, g.lds_scan, ~0ull >> 1);
+  const uint32_t scan_res = resident_blocks(ctx, k_scan<W, false>, g.lds_scan, ~0ull >> 1, scan_wpb(ctx->w) * kWave);
   g.kreg = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(scan_res / g.grid, (want + g.grid - 1) / g.grid));
   g.sgrid = g.grid * g.kreg;
   return g;
@@ -1531,7 +1543,8 @@ struct LaunchScan {
   static int run(mg_ctx* ctx, bool contain, uint64_t a_lo, uint64_t a_hi, uint32_t sgrid, bool filter,
                  hipStream_t stream = nullptr, bool no_super = false, bool index = false, bool flat = false) {
     if (!stream) stream = ctx->stream;
-    const uint64_t nw = (uint64_t)sgrid * kWavesPerBlock;  // scan wavefronts = run regions
+    const uint32_t wpb = scan_wpb(ctx->w);
+    const uint64_t nw = (uint64_t)sgrid * wpb;  // scan wavefronts = run regions
     ctx->nrun_reg = nw;
     const uint64_t ngroups = (a_hi - a_lo + kWave - 1) / kWave;
     // run regions: expected runs per read ~ 2 J / (w + 1) + 1 (minimizer density)
@@ -1568,7 +1581,7 @@ struct LaunchScan {
     sp.runs = ctx->d_runs;
     sp.run_cnt = ctx->d_run_cnt;
     sp.run_cap = run_cap;
-    const size_t lds = (size_t)kWavesPerBlock * (((ctx->w * kWave + 1) / 2) + kScanBuf) * sizeof(uint64_t);
+    const size_t lds = (size_t)wpb * scan_lds_per_wave(ctx->w);
     sp.cells = ctx->d_cells;
     sp.cell_n = ctx->cell_n;
     ctx->scan_flat = flat;
@@ -1600,10 +1613,10 @@ struct LaunchScan {
     (void)hipEventRecord(ctx->ev[6], stream);
     if (index) {  // unsharded only (the whole key space is this context's)
       allow_lds(k_scan<W, true>, lds);
-      hipLaunchKernelGGL((k_scan<W, true>), dim3(sgrid), dim3(kBlock), lds, stream, sp);
+      hipLaunchKernelGGL((k_scan<W, true>), dim3(sgrid), dim3(wpb * kWave), lds, stream, sp);
     } else {
       allow_lds(k_scan<W, false>, lds);
-      hipLaunchKernelGGL((k_scan<W, false>), dim3(sgrid), dim3(kBlock), lds, stream, sp);
+      hipLaunchKernelGGL((k_scan<W, false>), dim3(sgrid), dim3(wpb * kWave), lds, stream, sp);
     }
     (void)hipEventRecord(ctx->ev[7], stream);
     return hipGetLastError() == hipSuccess ? 0 : -1;
@@ -2047,6 +2060,7 @@ int setup_index(mg_ctx* ctx, uint32_t min_overlap, uint32_t seed_k) {
   if (m > 32 || m > h) return set_err(ctx, "seed k must satisfy 1 <= k <= min(32, l-1)");
   const uint32_t w = h - m + 1;
   if (w > 1024) return set_err(ctx, "l-1 - k + 1 must be <= 1024");
+  if (!scan_wpb(w)) return set_err(ctx, "l-1 - k + 1 too large for the scan's LDS window (use a larger seed k)");
   if (ctx->minlen && ctx->minlen <= min_overlap)
     return set_err(ctx, "every read must be longer than min_overlap (Dataset.cpp:160)");
   ctx->l = min_overlap;
@@ -2242,10 +2256,11 @@ void read_stats(mg_ctx* ctx, uint64_t nsrc) {
 template <int W>
 struct LaunchScanAll {
   static int run(mg_ctx* ctx, hipStream_t st, bool index) {
-    const size_t lds = (size_t)kWavesPerBlock * (((ctx->w * kWave + 1) / 2) + kScanBuf) * sizeof(uint64_t);
+    const uint32_t wpb = scan_wpb(ctx->w);
+    const size_t lds = (size_t)wpb * scan_lds_per_wave(ctx->w);
     const uint64_t groups = (ctx->n + kWave - 1) / kWave;
-    const uint32_t sgrid = index ? resident_blocks(ctx, k_scan<W, true>, lds, (groups + kWavesPerBlock - 1) / kWavesPerBlock)
-                                 : resident_blocks(ctx, k_scan<W, false>, lds, (groups + kWavesPerBlock - 1) / kWavesPerBlock);
+    const uint32_t sgrid = index ? resident_blocks(ctx, k_scan<W, true>, lds, (groups + wpb - 1) / wpb, wpb * kWave)
+                                 : resident_blocks(ctx, k_scan<W, false>, lds, (groups + wpb - 1) / wpb, wpb * kWave);
     return LaunchScan<W>::run(ctx, true, 0, ctx->n, sgrid, false, st, true, index, ctx->sort_runs && !ctx->split);
   }
 };

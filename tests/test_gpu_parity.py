@@ -171,6 +171,36 @@ def test_random_sets_vs_oracle(engine, case):
     assert np.array_equal(rows_to_tuples(rows), sorted_tuples(orows))
 
 
+EDGE_SETS = {
+    # name: (reads as strings, l)
+    "empty": ([], 20),
+    "all_invalid": (["ACGTNACGTACGTACGTACGTACGT", "A" * 30], 20),
+    "single": (["ACGTTGCAAGGCTTACGATCGATTACGGATCCA"], 20),
+    "single_tandem": (["ACGTTGCAAG" * 8], 20),  # self-overlaps of one read
+    "l_plus_one": (None, 40),                    # every read exactly l + 1 bases
+    "max_len": (None, 200),                      # reads up to 1024 bases (32 words)
+}
+
+
+@pytest.mark.parametrize("name", sorted(EDGE_SETS))
+def test_edge_sets_vs_oracle(engine, name):
+    """Empty and degenerate inputs and the length extremes, against the oracle."""
+    seqs, l = EDGE_SETS[name]
+    if name == "l_plus_one":
+        c, L = synth.uniform_read_set(3000, l + 1, 4000, seed=111)
+        seqs = synth.codes_to_strings(c, L)
+    elif name == "max_len":
+        c, L = synth.uniform_read_set(600, 0, 40000, seed=112, lo=1000, hi=1024)
+        seqs = synth.codes_to_strings(c, L)
+    ds = Dataset.from_strings(seqs, l)
+    od = OracleDataset.from_strings(seqs, l)
+    assert ds.num_unique == od.num_unique
+    rows, sup = gpu_rows(engine, ds, l, k=0)
+    orows, osup, _, _ = od.overlaps(l)
+    assert np.array_equal(sup.astype(np.uint64), osup)
+    assert np.array_equal(rows_to_tuples(rows), sorted_tuples(orows))
+
+
 def test_metagenome_vs_oracle(engine):
     c, L = synth.metagenome_read_set(20000, 100, 250, n_genomes=20, total_len=400000, seed=51)
     ds = Dataset.from_codes(c, L, 50)
