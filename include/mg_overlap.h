@@ -197,7 +197,15 @@ int mg_get_counters(const mg_ctx* ctx, mg_counters* c);
  * "split" (1 = probe -> candidates -> verify kernels, 0 = fused probe (default)),
  * "overlap_scan" (1 = unsharded contexts build the index inside one window
  * scan of all reads, k_scan<INDEX>, and both probes reuse its runs (default);
- * 0 = separate index build and a scan per probe pass). */
+ * 0 = separate index build and a scan per probe pass; source-range shards
+ * with the whole index, bench --multi replicated, use 0),
+ * "sort_runs" (1 = the shared scan's runs are radix-sorted by bucket before
+ * the probes: cell and partner loads then coalesce; 0 = default),
+ * "sort_bits" (diagnostics: sort only the top bucket bits, 0 = all),
+ * "halving" (which side emits a self-symmetric o=2/3 discovery pair:
+ * 0 = parity-alternating (default, even load over source IDs), 1 = lower ID),
+ * "phase_limit" / "max_blocks" (diagnostics: stop the probe after a phase /
+ * cap the persistent grid).  Results never depend on any option. */
 int mg_set_option(mg_ctx* ctx, const char* name, int64_t value);
 /* HIP stream the context launches on (hipStream_t as void*), for callers that
  * time or capture it themselves. */
