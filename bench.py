@@ -344,8 +344,8 @@ def main():
         traffic = load_pmc(args.pmc) if args.config == "c3" else None
         roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                "kernel": "step = k_scan<INDEX> (window scan + fused index build), then k_probe "
-                          "(containment, then discovery); device wall, HIP events",
+                "kernel": "step = k_scan<INDEX> (window scan + fused index build), bucket sort of the runs "
+                          "(rocprim onesweep), then k_probe (containment, then discovery); device wall, HIP events",
                 "alg_bytes_per_step": alg, "alg_bytes_per_read": per_read, "kernel_ms_per_step": kern_ms,
                 "probe_ms": dev_ms["probe_ms"], "verify_ms": dev_ms["verify_ms"], "scan_ms": dev_ms["scan_ms"]}
     else:

@@ -200,7 +200,9 @@ int mg_get_counters(const mg_ctx* ctx, mg_counters* c);
  * 0 = separate index build and a scan per probe pass; source-range shards
  * with the whole index, bench --multi replicated, use 0),
  * "sort_runs" (1 = the shared scan's runs are radix-sorted by bucket before
- * the probes: cell and partner loads then coalesce; 0 = default),
+ * the probes, so cell and partner loads coalesce (default); 0 = the probe
+ * walks the scan's per-wavefront run regions),
+ * "flat_cap" (tests: initial capacity of the sorted-run arrays, 0 = auto),
  * "sort_bits" (diagnostics: sort only the top bucket bits, 0 = all),
  * "halving" (which side emits a self-symmetric o=2/3 discovery pair:
  * 0 = parity-alternating (default, even load over source IDs), 1 = lower ID),

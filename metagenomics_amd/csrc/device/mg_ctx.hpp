@@ -96,7 +96,7 @@ struct mg_ctx {
   std::vector<unsigned long long> cand_cnt_host;
   // bucket-ordered runs (option "sort_runs"): the shared scan's runs as SoA
   // (x, meta) sorted by bucket, so the probe meets each cell's runs together
-  bool sort_runs = false;
+  bool sort_runs = true;
   uint64_t* d_sk[2] = {nullptr, nullptr};
   uint64_t* d_sm[2] = {nullptr, nullptr};
   size_t sk_cap = 0;
@@ -109,6 +109,7 @@ struct mg_ctx {
   bool scan_flat = false;          // the shared scan wrote d_sk[0] / d_sm[0] directly
   unsigned long long* d_flat_cursor = nullptr;
   uint64_t flat_need = 0, n_flat = 0;
+  uint64_t flat_cap_opt = 0;       // option "flat_cap" (tests: force the overflow rerun)
   int sorted_state = 0;  // 0 none, 2 sorted (for the current scan)
   int sort_bits = 0;     // diagnostics: sort only the top sort_bits bucket bits (0: all)
   mg_timings t{};

@@ -1588,9 +1588,10 @@ struct LaunchScan {
     if (flat) {
       // SoA output for the bucket sort: ~2 J / (w + 1) + 1 runs per read, sized
       // with 20 % slack (or the exact need after an overflow)
-      const uint64_t est = (a_hi - a_lo) * (2 * J / (ctx->w + 1) + 2) * 6 / 5 + 4096;
+      const uint64_t est = ctx->flat_cap_opt ? ctx->flat_cap_opt
+                                             : (a_hi - a_lo) * (2 * J / (ctx->w + 1) + 2) * 6 / 5 + 4096;
       const uint64_t cap = std::max<uint64_t>(ctx->flat_need, est);
-      if (cap > ctx->sk_cap) {
+      if (cap > ctx->sk_cap || (ctx->flat_cap_opt && cap < ctx->sk_cap)) {
         for (int b = 0; b < 2; ++b) {
           if (ctx->d_sk[b]) (void)hipFree(ctx->d_sk[b]);
           if (ctx->d_sm[b]) (void)hipFree(ctx->d_sm[b]);
@@ -2012,6 +2013,11 @@ int mg_set_option(mg_ctx* ctx, const char* name, int64_t value) {
   if (!strcmp(name, "sort_runs")) {
     ctx->sort_runs = value != 0;
     ctx->sorted_state = 0;
+    return 0;
+  }
+  if (!strcmp(name, "flat_cap")) {  // tests: initial capacity of the flat run arrays (0 = auto)
+    ctx->flat_cap_opt = value > 0 ? (uint64_t)value : 0;
+    ctx->flat_need = 0;
     return 0;
   }
   if (!strcmp(name, "sort_bits")) {  // diagnostics: sort only the top sort_bits bucket bits (0: all)

@@ -497,6 +497,34 @@ def test_sorted_runs_path(name):
     assert {str(i): int(s) for i, s in enumerate(sup) if s} == meta["super"]
 
 
+@pytest.mark.parametrize("name", ["mixed", "branchy", "highdup"])
+def test_sorted_runs_flat_overflow(name):
+    """The flat run arrays start far too small: the scan's chunk cursor keeps
+    counting, the host resizes to the exact need and reruns the scan."""
+    meta = load_meta(name)
+    ds = Dataset.from_files([fixture_input(name)], meta["l"])
+    e = OverlapEngine(0)
+    e.set_option("sort_runs", 1)
+    e.set_option("flat_cap", 700)
+    rows, sup = gpu_rows(e, ds, meta["l"])
+    e.close()
+    assert np.array_equal(rows_to_tuples(rows), golden_rows(name))
+    assert {str(i): int(s) for i, s in enumerate(sup) if s} == meta["super"]
+
+
+@pytest.mark.parametrize("name", FIXTURES)
+def test_unsorted_runs_path(name):
+    """option sort_runs = 0: the probe walks the scan's per-wavefront regions."""
+    meta = load_meta(name)
+    ds = Dataset.from_files([fixture_input(name)], meta["l"])
+    e = OverlapEngine(0)
+    e.set_option("sort_runs", 0)
+    rows, sup = gpu_rows(e, ds, meta["l"])
+    e.close()
+    assert np.array_equal(rows_to_tuples(rows), golden_rows(name))
+    assert {str(i): int(s) for i, s in enumerate(sup) if s} == meta["super"]
+
+
 @pytest.mark.parametrize("name", FIXTURES)
 def test_replicated_index_source_shards(name):
     """Multi-GPU replicated mode (bench --multi replicated): every rank builds
