@@ -110,6 +110,8 @@ struct mg_ctx {
   unsigned long long* d_flat_cursor = nullptr;
   uint64_t flat_need = 0, n_flat = 0;
   uint64_t flat_cap_opt = 0;       // option "flat_cap" (tests: force the overflow rerun)
+  bool pack_runs = true;           // option "pack_runs": 12-B sort records when the widths fit
+  int pack_a = 0, pack_w = 0;      // packing of the current flat runs (0: 16-B records)
   int sorted_state = 0;  // 0 none, 2 sorted (for the current scan)
   int sort_bits = 0;     // diagnostics: sort only the top sort_bits bucket bits (0: all)
   mg_timings t{};

@@ -146,6 +146,7 @@ constexpr uint64_t kEmpty = ~0ULL;       // free slot (a read index is never 0xF
 constexpr uint64_t kChain = 1ULL << 63;  // on a cell's last slot: the chain continues in the next cell
 constexpr uint32_t kFpMask = (1u << kFpBits) - 1;
 constexpr uint64_t kFlatChunk = 512;   // flat scan output: records per wavefront chunk
+constexpr uint32_t kFlatCounters = 8;  // chunk counters (one per XCD: one counter serialised at 0.2 ms)
 constexpr uint64_t kFlatHole = ~0ULL;  // meta of an unused flat slot (a run meta never has bit 63)
 
 struct IndexParams {
@@ -315,7 +316,36 @@ struct ScanParams {
   uint64_t* flat_meta;
   unsigned long long* flat_cursor;
   uint64_t flat_cap;
+  int pack_a, pack_w;  // pack_a > 0: 12-B records (run_pack_key / run_pack_meta) instead of 16-B
 };
+
+// Sort records of 12 B instead of 16 (option "sort_runs" when the widths fit,
+// packable_runs): key32 = bucket | low (32 - nb) fingerprint bits; meta64 =
+// read (A bits) | jlo (10) | jhi - jlo (WB) | p - jhi (WB) | high fingerprint
+// bits.  A run's minimizer lies in all its windows, so p - jhi and jhi - jlo
+// are both < w.  A = bit width of the read count, so a read index is never all
+// ones and an all-ones meta stays free for holes.
+__device__ __forceinline__ uint32_t run_pack_key(uint64_t v, uint32_t nb) {
+  const uint32_t fp = (uint32_t)(v >> nb) & kFpMask;
+  return (uint32_t)(v & ((1ULL << nb) - 1)) | (fp << nb);
+}
+__device__ __forceinline__ uint64_t run_pack_meta(uint64_t meta, uint64_t v, uint32_t nb, int a, int wb) {
+  const uint64_t ra = meta & 0xFFFFFFFFull, pos = (meta >> 32) & 1023u, jlo = (meta >> 42) & 1023u,
+                 jhi = (meta >> 52) & 1023u;
+  const uint64_t fph = (uint64_t)(((uint32_t)(v >> nb) & kFpMask) >> (32 - nb));
+  return ra | (jlo << a) | ((jhi - jlo) << (a + 10)) | ((pos - jhi) << (a + 10 + wb)) | (fph << (a + 10 + 2 * wb));
+}
+// back to the bucket, fingerprint and 64-bit run meta the probe works on
+__device__ __forceinline__ void run_unpack(uint32_t k32, uint64_t m, uint32_t nb, int a, int wb, uint64_t* bucket,
+                                           uint32_t* fp, uint64_t* meta) {
+  const uint64_t amask = (1ULL << a) - 1, wmask = (1ULL << wb) - 1;
+  const uint64_t ra = m & amask, jlo = (m >> a) & 1023u, djh = (m >> (a + 10)) & wmask,
+                 dp = (m >> (a + 10 + wb)) & wmask, fph = m >> (a + 10 + 2 * wb);
+  const uint64_t jhi = jlo + djh, pos = jhi + dp;
+  *bucket = k32 & (uint32_t)((1ULL << nb) - 1);
+  *fp = ((k32 >> nb) | (uint32_t)(fph << (32 - nb))) & kFpMask;
+  *meta = ra | (pos << 32) | (jlo << 42) | (jhi << 52);
+}
 
 __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -396,16 +426,22 @@ __global__ __launch_bounds__(kBlock) void k_scan(ScanParams p) {
       const uint64_t npop = (uint64_t)__popcll(bal);
       const uint64_t room = fcap - fused;
       unsigned long long nbase = 0;
-      if (npop > room) {
-        if (lane == 0) nbase = atomicAdd(p.flat_cursor, (unsigned long long)kFlatChunk);
+      if (npop > room) {  // chunk ids x, x + 8, x + 16, ... belong to counter x = blockIdx % 8
+        const uint32_t x = blockIdx.x & (kFlatCounters - 1);
+        if (lane == 0) nbase = (atomicAdd(&p.flat_cursor[x], 1ull) * kFlatCounters + x) * kFlatChunk;
         nbase = __shfl(nbase, 0);
       }
       if (flag) {
         const uint64_t pr = lane_prefix(bal);
         const uint64_t at = pr < room ? fbase + fused + pr : nbase + (pr - room);
         if (at < p.flat_cap) {
-          p.flat_keys[at] = v;
-          p.flat_meta[at] = meta;
+          if (p.pack_a) {
+            reinterpret_cast<uint32_t*>(p.flat_keys)[at] = run_pack_key(v, p.nb_log2);
+            p.flat_meta[at] = run_pack_meta(meta, v, p.nb_log2, p.pack_a, p.pack_w);
+          } else {
+            p.flat_keys[at] = v;
+            p.flat_meta[at] = meta;
+          }
         }
       }
       if (npop > room) {
@@ -580,7 +616,10 @@ __global__ __launch_bounds__(kBlock) void k_scan(ScanParams p) {
     for (uint64_t i = fused + lane; i < fcap; i += kWave) {
       const uint64_t at = fbase + i;
       if (at < p.flat_cap) {
-        p.flat_keys[at] = kEmpty;
+        if (p.pack_a)
+          reinterpret_cast<uint32_t*>(p.flat_keys)[at] = 0xFFFFFFFFu;
+        else
+          p.flat_keys[at] = kEmpty;
         p.flat_meta[at] = kFlatHole;
       }
     }
@@ -648,6 +687,7 @@ struct ProbeParams {
   uint64_t run_regions;           // probe wavefront r consumes run regions r, r + nw, r + 2 nw, ... < run_regions
   const uint64_t* fkeys;          // non-null: runs as SoA (x, meta), region r = [r * run_cap, + run_cnt[r])
   const uint64_t* fmeta;
+  int pack_a, pack_w;             // pack_a > 0: fkeys holds 32-bit packed keys (run_unpack)
   const uint32_t* src_super;      // runs of sources with superReadID != 0 are dropped (:548; nullptr: none)
   uint64_t src_lo, src_hi;        // only runs of sources in [src_lo, src_hi) (src_hi = 0: all)
   uint32_t* rows;                 // 3 dwords per row (mg_edge); one region per wavefront
@@ -844,7 +884,7 @@ __global__ __launch_bounds__(kBlock) void k_probe(ProbeParams p) {
     pf_ok = pf_any && k < rcnt;
     if (p.fkeys) {
       const uint64_t i = rbase_i + (pf_ok ? k : 0);
-      rec_pf = make_ulonglong2(p.fkeys[i], p.fmeta[i]);
+      rec_pf = make_ulonglong2(p.pack_a ? reinterpret_cast<const uint32_t*>(p.fkeys)[i] : p.fkeys[i], p.fmeta[i]);
     } else {
       rec_pf = rbase[pf_ok ? k : 0];
     }
@@ -859,13 +899,20 @@ __global__ __launch_bounds__(kBlock) void k_probe(ProbeParams p) {
     }
     if (pf_any) {
       valid = pf_ok && rec_pf.y != kFlatHole;
-      meta = rec_pf.y;
+      uint64_t bucket;
+      uint32_t fpv;
+      if (p.pack_a) {
+        run_unpack((uint32_t)rec_pf.x, rec_pf.y, p.nb_log2, p.pack_a, p.pack_w, &bucket, &fpv, &meta);
+      } else {
+        meta = rec_pf.y;
+        bucket = rec_pf.x & nbmask;
+        fpv = (uint32_t)(rec_pf.x >> p.nb_log2) & kFpMask;
+      }
       if (valid && (p.src_super || p.src_hi)) {  // contained or foreign sources contribute no windows
         const uint32_t ra = (uint32_t)meta;
         if ((p.src_super && p.src_super[ra]) || (p.src_hi && (ra < p.src_lo || ra >= p.src_hi))) valid = false;
       }
-      key = (valid ? (rec_pf.x & nbmask) - p.cell_lo : 0) |
-            ((uint64_t)((uint32_t)(rec_pf.x >> p.nb_log2) & kFpMask) << 32);
+      key = (valid ? bucket - p.cell_lo : 0) | ((uint64_t)fpv << 32);
       if (valid) ++st_runs;
       rpos += kWave;
       pf_any = hbm_settle();
@@ -1506,6 +1553,19 @@ inline uint32_t scan_wpb(uint32_t w) {
   return 0;
 }
 
+// 12-B sort records fit when read index, jlo, two window deltas and the
+// fingerprint bits the 32-bit key cannot hold share 64 bits (run_pack_meta).
+inline void packable_runs(const mg_ctx* ctx, int* a, int* wb) {
+  auto bits = [](uint64_t x) { int b = 0; while (x) { ++b; x >>= 1; } return b; };
+  const int A = std::max(1, bits(ctx->n));  // n < 2^A: an index is never all ones
+  const int WB = bits(ctx->w > 0 ? ctx->w - 1 : 0);
+  const int nb = (int)ctx->nb_log2;
+  const int fph = std::max(0, (int)kFpBits - (32 - nb));
+  const bool ok = ctx->pack_runs && nb < 32 && A + 10 + 2 * WB + fph <= 64;
+  *a = ok ? A : 0;
+  *wb = ok ? WB : 0;
+}
+
 // Geometry of one discovery pass over source reads [a_lo, a_hi): probe grid =
 // its resident blocks; the scan (fewer registers) runs kreg times as many
 // wavefronts and probe wavefront r consumes scan regions r + i * (probe waves).
@@ -1604,12 +1664,20 @@ struct LaunchScan {
         }
         ctx->sk_cap = cap;
       }
-      if (!ctx->d_flat_cursor && hipMalloc(&ctx->d_flat_cursor, sizeof(unsigned long long)) != hipSuccess) return -1;
-      if (hipMemsetAsync(ctx->d_flat_cursor, 0, sizeof(unsigned long long), stream) != hipSuccess) return -1;
+      if (!ctx->d_flat_cursor &&
+          hipMalloc(&ctx->d_flat_cursor, kFlatCounters * sizeof(unsigned long long)) != hipSuccess)
+        return -1;
+      if (hipMemsetAsync(ctx->d_flat_cursor, 0, kFlatCounters * sizeof(unsigned long long), stream) != hipSuccess)
+        return -1;
       sp.flat_keys = ctx->d_sk[0];
       sp.flat_meta = ctx->d_sm[0];
       sp.flat_cursor = ctx->d_flat_cursor;
       sp.flat_cap = ctx->sk_cap;
+      packable_runs(ctx, &ctx->pack_a, &ctx->pack_w);
+      sp.pack_a = ctx->pack_a;
+      sp.pack_w = ctx->pack_w;
+    } else {
+      ctx->pack_a = ctx->pack_w = 0;
     }
     (void)hipEventRecord(ctx->ev[6], stream);
     if (index) {  // unsharded only (the whole key space is this context's)
@@ -1634,7 +1702,8 @@ struct LaunchProbe {
   static int run(mg_ctx* ctx, bool contain, const ulonglong2* runs, const unsigned long long* run_cnt,
                  uint64_t run_cap, uint64_t run_regions, uint32_t grid, uint64_t total_runs,
                  const uint32_t* src_super = nullptr, uint64_t src_lo = 0, uint64_t src_hi = 0,
-                 const uint64_t* fkeys = nullptr, const uint64_t* fmeta = nullptr) {
+                 const uint64_t* fkeys = nullptr, const uint64_t* fmeta = nullptr, int pack_a = 0,
+                 int pack_w = 0) {
     ctx->nreg = (uint64_t)grid * kWavesPerBlock;  // probe wavefronts = row regions
     ProbeParams pp{};
     pp.words = ctx->d_words;
@@ -1655,6 +1724,8 @@ struct LaunchProbe {
     pp.run_regions = run_regions;
     pp.fkeys = fkeys;
     pp.fmeta = fmeta;
+    pp.pack_a = pack_a;
+    pp.pack_w = pack_w;
     pp.src_super = src_super;
     pp.src_lo = src_lo;
     pp.src_hi = src_hi;
@@ -2015,6 +2086,12 @@ int mg_set_option(mg_ctx* ctx, const char* name, int64_t value) {
     ctx->sorted_state = 0;
     return 0;
   }
+  if (!strcmp(name, "pack_runs")) {  // 12-B sort records when the widths fit (default 1)
+    ctx->pack_runs = value != 0;
+    ctx->scan_state = 0;
+    ctx->sorted_state = 0;
+    return 0;
+  }
   if (!strcmp(name, "flat_cap")) {  // tests: initial capacity of the flat run arrays (0 = auto)
     ctx->flat_cap_opt = value > 0 ? (uint64_t)value : 0;
     ctx->flat_need = 0;
@@ -2277,14 +2354,30 @@ bool shared_scan(const mg_ctx* ctx) { return ctx->nranks == 1 && ctx->overlap_sc
 // flat scan output: the cursor is the run count; on overflow size for it and rerun
 int settle_flat(mg_ctx* ctx, bool* again) {
   *again = false;
-  unsigned long long c = 0;
-  if (ctx->n) MG_TRY(hipMemcpyAsync(&c, ctx->d_flat_cursor, sizeof(c), hipMemcpyDeviceToHost, ctx->stream));
+  unsigned long long c[kFlatCounters] = {};
+  if (ctx->n)
+    MG_TRY(hipMemcpyAsync(c, ctx->d_flat_cursor, sizeof(c), hipMemcpyDeviceToHost, ctx->stream));
   MG_TRY(hipStreamSynchronize(ctx->stream));
-  if (c > ctx->sk_cap) {
-    ctx->flat_need = c + c / 8 + 4096;
+  // chunk ids claimed: x + 8 k for k < c[x]; the array extends to the highest one
+  uint64_t ext = 0;
+  for (uint32_t x = 0; x < kFlatCounters; ++x)
+    if (c[x]) ext = std::max<uint64_t>(ext, (c[x] - 1) * kFlatCounters + x + 1);
+  const uint64_t n = ext * kFlatChunk;
+  if (n > ctx->sk_cap) {
+    ctx->flat_need = n + n / 8 + 4096;
     *again = true;
+    return 0;
   }
-  ctx->n_flat = c;
+  // ids below the extent that a counter never reached hold nothing: mark them
+  // as holes (all-ones key and meta) so the sort and the probe skip them
+  const size_t kb = ctx->pack_a ? sizeof(uint32_t) : sizeof(uint64_t);
+  for (uint32_t x = 0; x < kFlatCounters; ++x)
+    for (uint64_t id = c[x] * kFlatCounters + x; id < ext; id += kFlatCounters) {
+      MG_TRY(hipMemsetAsync(reinterpret_cast<char*>(ctx->d_sk[0]) + id * kFlatChunk * kb, 0xFF, kFlatChunk * kb,
+                            ctx->stream));
+      MG_TRY(hipMemsetAsync(ctx->d_sm[0] + id * kFlatChunk, 0xFF, kFlatChunk * sizeof(uint64_t), ctx->stream));
+    }
+  ctx->n_flat = n;
   return 0;
 }
 
@@ -2341,7 +2434,7 @@ struct LaunchProbeShared {
                          ctx->d_flat_cnt, nw, cap, n);
       if (hipGetLastError() != hipSuccess) return -1;
       return LaunchProbe<W>::run(ctx, contain, nullptr, ctx->d_flat_cnt, cap, nw, g.grid, n, sup, lo, hi,
-                                 ctx->d_sk[ctx->sk_sel], ctx->d_sm[ctx->sk_sel]);
+                                 ctx->d_sk[ctx->sk_sel], ctx->d_sm[ctx->sk_sel], ctx->pack_a, ctx->pack_w);
     }
     return LaunchProbe<W>::run(ctx, contain, ctx->d_runs, ctx->d_run_cnt, ctx->run_cap, ctx->nrun_reg, g.grid, total,
                                sup, lo, hi);
@@ -2384,11 +2477,20 @@ int sort_shared_runs(mg_ctx* ctx) {
   MG_TRY(hipGetLastError());
   const unsigned nb = ctx->nb_log2;
   const unsigned lo_bit = (ctx->sort_bits > 0 && (unsigned)ctx->sort_bits < nb) ? nb - (unsigned)ctx->sort_bits : 0u;
+  const bool packed = flat && ctx->pack_a;  // 32-bit keys (run_pack_key)
   auto sort = [&](void* tmp, size_t& tb, int& sel) -> hipError_t {
-    rocprim::double_buffer<uint64_t> keys(ctx->d_sk[0], ctx->d_sk[1]);
     rocprim::double_buffer<uint64_t> vals(ctx->d_sm[0], ctx->d_sm[1]);
-    hipError_t e = rocprim::radix_sort_pairs(tmp, tb, keys, vals, n, lo_bit, nb, ctx->stream);
-    sel = keys.current() == ctx->d_sk[0] ? 0 : 1;
+    hipError_t e;
+    if (packed) {
+      rocprim::double_buffer<uint32_t> keys(reinterpret_cast<uint32_t*>(ctx->d_sk[0]),
+                                            reinterpret_cast<uint32_t*>(ctx->d_sk[1]));
+      e = rocprim::radix_sort_pairs(tmp, tb, keys, vals, n, lo_bit, nb, ctx->stream);
+      sel = keys.current() == reinterpret_cast<uint32_t*>(ctx->d_sk[0]) ? 0 : 1;
+    } else {
+      rocprim::double_buffer<uint64_t> keys(ctx->d_sk[0], ctx->d_sk[1]);
+      e = rocprim::radix_sort_pairs(tmp, tb, keys, vals, n, lo_bit, nb, ctx->stream);
+      sel = keys.current() == ctx->d_sk[0] ? 0 : 1;
+    }
     if (e == hipSuccess && tmp && (vals.current() == ctx->d_sm[0] ? 0 : 1) != sel) e = hipErrorUnknown;
     return e;
   };

@@ -513,6 +513,20 @@ def test_sorted_runs_flat_overflow(name):
 
 
 @pytest.mark.parametrize("name", FIXTURES)
+def test_sorted_runs_16b_records(name):
+    """option pack_runs = 0: the bucket sort moves 16-B run records instead of
+    the packed 12-B ones."""
+    meta = load_meta(name)
+    ds = Dataset.from_files([fixture_input(name)], meta["l"])
+    e = OverlapEngine(0)
+    e.set_option("pack_runs", 0)
+    rows, sup = gpu_rows(e, ds, meta["l"])
+    e.close()
+    assert np.array_equal(rows_to_tuples(rows), golden_rows(name))
+    assert {str(i): int(s) for i, s in enumerate(sup) if s} == meta["super"]
+
+
+@pytest.mark.parametrize("name", FIXTURES)
 def test_unsorted_runs_path(name):
     """option sort_runs = 0: the probe walks the scan's per-wavefront regions."""
     meta = load_meta(name)
