@@ -137,8 +137,15 @@ def load_pmc(path):
     except Exception:
         return None
     tr = d.get("traffic", {})
-    tot = sum(v["traffic_bytes_per_launch"] for k, v in tr.items()
-              if k.startswith(("k_index_build", "k_scan", "k_probe")))
+    step = ("k_index_build", "k_scan", "k_probe")
+    if any("dispatches" in v for v in tr.values()):
+        # every dispatch of the step's kernels (the bucket sort's rocprim passes
+        # included) over the number of step passes (one k_scan each)
+        passes = sum(v.get("dispatches", 0) for k, v in tr.items() if k.startswith("k_scan")) or 1
+        tot = sum(v["traffic_bytes_per_launch"] * v.get("dispatches", 1) for k, v in tr.items()
+                  if k.startswith(step) or "radix_sort_onesweep" in k) / passes
+    else:
+        tot = sum(v["traffic_bytes_per_launch"] for k, v in tr.items() if k.startswith(step))
     return tot or None
 
 
@@ -161,7 +168,7 @@ def main():
     ap.add_argument("--no-ingest", action="store_true", help="skip the device Dataset ingest measurement")
     ap.add_argument("--replay", action="store_true",
                     help="also time the host replay of the exploration + transitive reduction + contraction on the rows")
-    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r01s3_pmc_c3.json"))
+    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r01s4_pmc_c3.json"))
     ap.add_argument("--nb-log2", type=int, default=0)
     ap.add_argument("--split-probe", action="store_true", help="probe -> candidates -> verify kernels (option split = 1)")
     ap.add_argument("--sort-runs", type=int, default=None,

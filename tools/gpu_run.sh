@@ -84,7 +84,7 @@ for s in $STEPS; do
     [ $rc -eq 0 ] && python3 tools/pmc_summary.py $OUT/pmcsq_summary.json $OUT/pmcsq_* > /dev/null ;;
   pmc)
     for set in "FETCH_SIZE" "WRITE_SIZE"; do
-      timeout -s KILL 300 rocprofv3 --pmc $set --kernel-trace --output-format csv -d $OUT/pmc_$set -o p -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline > $OUT/pmc_$set.log 2>&1
+      timeout -s KILL 300 rocprofv3 --pmc $set --kernel-trace --output-format csv -d $OUT/pmc_$set -o p -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-ingest > $OUT/pmc_$set.log 2>&1
       rc=$?; echo "pmc $set rc=$rc"; [ $rc -ne 0 ] && break
     done
     [ $rc -eq 0 ] && python3 tools/pmc_summary.py $OUT/pmc_summary.json $OUT/pmc_* > /dev/null ;;

@@ -35,6 +35,7 @@ def main():
                     disp = row.get("Dispatch_Id", row.get("Dispatch-Id"))
                     acc[k][cname].append((disp, val))
     res = {}
+    disp_n = {}
     for k, cs in acc.items():
         res[k] = {}
         for c, vals in cs.items():
@@ -42,13 +43,15 @@ def main():
             for disp, v in vals:
                 per[disp] += v  # sum over dimensions (XCD/SE instances) per dispatch
             res[k][c] = sum(per.values()) / max(1, len(per))
+            disp_n[k] = max(disp_n.get(k, 0), len(per))
     summary = {"kernels": res}
     per_kernel = {}
     for k, cs in res.items():
         fetch, write = cs.get("FETCH_SIZE"), cs.get("WRITE_SIZE")
         if fetch is not None and write is not None:
             per_kernel[k] = {"fetch_bytes_raw": fetch * 1024, "write_bytes": write * 1024,
-                             "traffic_bytes_per_launch": (2 * fetch + write) * 1024}
+                             "traffic_bytes_per_launch": (2 * fetch + write) * 1024,
+                             "dispatches": disp_n.get(k, 0)}
     summary["traffic"] = per_kernel
     main_k = [k for k in per_kernel if k.startswith("k_probe") and k.endswith("false>")]
     if main_k:
