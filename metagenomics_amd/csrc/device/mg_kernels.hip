@@ -258,6 +258,32 @@ __global__ __launch_bounds__(kBlock) void k_index_build(IndexParams p) {
   }
 }
 
+// Sorted index build (option "sorted_index"): the key records sorted by bucket
+// (stable rocprim radix sort) are filed without atomics.  A record's rank among
+// the records of its bucket is found by looking back over at most kCell
+// neighbours; ranks below kCell take home slot `rank` with a plain store
+// (OVERFLOW = false), the rest go through cell_insert's chain walk in a second
+// launch, after every home slot is written (OVERFLOW = true).  Same cell
+// contents as the CAS build up to the order inside a cell, which nothing reads
+// (probe and getListOfReads filter every slot).
+template <bool OVERFLOW>
+__global__ __launch_bounds__(kBlock) void k_fill_cells(const uint32_t* __restrict__ bk,
+                                                       const uint64_t* __restrict__ ent, uint64_t n,
+                                                       uint64_t* __restrict__ cells, uint64_t cell_n) {
+  const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t e = ent[i];
+  if (e == kEmpty) return;
+  const uint32_t b = bk[i];
+  int r = 0;
+  while (r < kCell && i > (uint64_t)r && bk[i - r - 1] == b) ++r;
+  if (!OVERFLOW) {
+    if (r < kCell) cells[(uint64_t)b * kCell + r] = e;
+  } else if (r >= kCell) {
+    cell_insert(cells, b, cell_n, e);
+  }
+}
+
 // Exchange mode, step 1: the index records of the keys of source reads
 // [a_lo, a_hi) (16 B: x = mix64(minimizer), y = entry without fingerprint),
 // written densely in key order; k_part routes them to the bucket owners.
@@ -317,6 +343,12 @@ struct ScanParams {
   unsigned long long* flat_cursor;
   uint64_t flat_cap;
   int pack_a, pack_w;  // pack_a > 0: 12-B records (run_pack_key / run_pack_meta) instead of 16-B
+  // k_scan<INDEX> with a sorted index build (option "sorted_index"): the four key
+  // records of read a go to key_bk / key_ent[o * key_n + a] (bucket, entry)
+  // instead of a CAS into the cells; k_fill_cells files them after a bucket sort
+  uint32_t* key_bk;
+  uint64_t* key_ent;
+  uint64_t key_n;
 };
 
 // Sort records of 12 B instead of 16 (option "sort_runs" when the widths fit,
@@ -607,7 +639,19 @@ __global__ __launch_bounds__(kBlock) void k_scan(ScanParams p) {
 #pragma unroll
       for (int o = 0; o < 4; ++o) {
         const uint64_t v = mix64(mb[o]);
-        cell_insert(p.cells, v & nbm, p.cell_n, make_entry(v, p.nb_log2, (int)(kb[o] & 1023u), o, (uint32_t)a));
+        const unsigned long long e = make_entry(v, p.nb_log2, (int)(kb[o] & 1023u), o, (uint32_t)a);
+        if (p.key_bk) {  // o-major: each store is one coalesced wavefront line
+          p.key_bk[o * p.key_n + a] = (uint32_t)(v & nbm);
+          p.key_ent[o * p.key_n + a] = e;
+        } else {
+          cell_insert(p.cells, v & nbm, p.cell_n, e);
+        }
+      }
+    } else if (INDEX && p.key_bk && a < p.a_hi) {  // no keys (n <= l cannot pass setup_index): holes
+#pragma unroll
+      for (int o = 0; o < 4; ++o) {
+        p.key_bk[o * p.key_n + a] = 0;
+        p.key_ent[o * p.key_n + a] = kEmpty;
       }
     }
   }
@@ -1679,6 +1723,11 @@ struct LaunchScan {
     } else {
       ctx->pack_a = ctx->pack_w = 0;
     }
+    if (index && ctx->sorted_index) {  // key records for the sorted build (mg_build_index files them)
+      sp.key_bk = ctx->d_kb[0];
+      sp.key_ent = ctx->d_ke[0];
+      sp.key_n = ctx->n;
+    }
     (void)hipEventRecord(ctx->ev[6], stream);
     if (index) {  // unsharded only (the whole key space is this context's)
       allow_lds(k_scan<W, true>, lds);
@@ -1941,7 +1990,7 @@ void mg_destroy(mg_ctx* ctx) {
                   ctx->d_superkey, ctx->d_super, ctx->d_any, ctx->d_rows, ctx->d_seg, ctx->d_stats,
                   ctx->d_compact, ctx->d_runs, ctx->d_run_cnt, ctx->d_keyrec, ctx->d_blk, ctx->d_flat_cnt, ctx->d_cand, ctx->d_cand_cnt, ctx->d_freq,
                   ctx->d_sk[0], ctx->d_sk[1], ctx->d_sm[0], ctx->d_sm[1], ctx->d_sort_tmp, ctx->d_run_off,
-                  ctx->d_flat_cursor};
+                  ctx->d_flat_cursor, ctx->d_kb[0], ctx->d_kb[1], ctx->d_ke[0], ctx->d_ke[1]};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   for (auto& e : ctx->ev)
@@ -2084,6 +2133,11 @@ int mg_set_option(mg_ctx* ctx, const char* name, int64_t value) {
   if (!strcmp(name, "sort_runs")) {
     ctx->sort_runs = value != 0;
     ctx->sorted_state = 0;
+    return 0;
+  }
+  if (!strcmp(name, "sorted_index")) {  // 1: bucket-sorted key records + plain stores; 0 (default): CAS inserts
+    ctx->sorted_index = value != 0;
+    ctx->index_ready = false;
     return 0;
   }
   if (!strcmp(name, "pack_runs")) {  // 12-B sort records when the widths fit (default 1)
@@ -2534,6 +2588,42 @@ int probe_shared(mg_ctx* ctx, bool contain) {
 
 extern "C" {
 
+// Sorted index build, after k_scan<INDEX> wrote the 4N key records to
+// d_kb[0] / d_ke[0]: stable radix sort by bucket (nb bits), then the home-slot
+// fill and the overflow chain walk (k_fill_cells).
+int fill_sorted_index(mg_ctx* ctx) {
+  const uint64_t n = 4 * ctx->n;
+  if (!n) return 0;
+  if (n > 0xFFFFFFFFull) return set_err(ctx, "sorted_index: more than 2^32 keys");
+  auto sort = [&](void* tmp, size_t& tb, int& sel) -> hipError_t {
+    rocprim::double_buffer<uint32_t> keys(ctx->d_kb[0], ctx->d_kb[1]);
+    rocprim::double_buffer<uint64_t> vals(ctx->d_ke[0], ctx->d_ke[1]);
+    hipError_t e = rocprim::radix_sort_pairs(tmp, tb, keys, vals, (unsigned int)n, 0u, ctx->nb_log2, ctx->stream);
+    sel = keys.current() == ctx->d_kb[0] ? 0 : 1;
+    if (e == hipSuccess && tmp && (vals.current() == ctx->d_ke[0] ? 0 : 1) != sel) e = hipErrorUnknown;
+    return e;
+  };
+  size_t tb = 0;
+  int sel = 0;
+  MG_TRY(sort(nullptr, tb, sel));
+  if (tb > ctx->sort_tmp_cap) {
+    if (ctx->d_sort_tmp) (void)hipFree(ctx->d_sort_tmp);
+    ctx->d_sort_tmp = nullptr;
+    MG_TRY(hipMalloc(&ctx->d_sort_tmp, tb));
+    ctx->sort_tmp_cap = tb;
+  }
+  tb = ctx->sort_tmp_cap;
+  MG_TRY(sort(ctx->d_sort_tmp, tb, sel));
+  const uint32_t grid = (uint32_t)((n + kBlock - 1) / kBlock);
+  hipLaunchKernelGGL(k_fill_cells<false>, dim3(grid), dim3(kBlock), 0, ctx->stream, ctx->d_kb[sel], ctx->d_ke[sel], n,
+                     ctx->d_cells, ctx->cell_n);
+  MG_TRY(hipGetLastError());
+  hipLaunchKernelGGL(k_fill_cells<true>, dim3(grid), dim3(kBlock), 0, ctx->stream, ctx->d_kb[sel], ctx->d_ke[sel], n,
+                     ctx->d_cells, ctx->cell_n);
+  MG_TRY(hipGetLastError());
+  return 0;
+}
+
 int mg_build_index(mg_ctx* ctx, uint32_t min_overlap, uint32_t seed_k) {
   if (!ctx) return -1;
   MG_TRY(hipSetDevice(ctx->device));
@@ -2547,9 +2637,16 @@ int mg_build_index(mg_ctx* ctx, uint32_t min_overlap, uint32_t seed_k) {
     // (k_scan<INDEX>), whose runs then serve the containment and discovery
     // probes.  Measured at C3 (same box): 3.58 ms vs index 2.05 + scan 1.83
     // separately; a concurrent scan on a second stream did not overlap (3.95).
+    if (ctx->sorted_index) {
+      MG_TRY(ensure(&ctx->d_kb[0], &ctx->kb_cap, 4 * ctx->n));
+      MG_TRY(ensure(&ctx->d_kb[1], &ctx->kb1_cap, 4 * ctx->n));
+      MG_TRY(ensure(&ctx->d_ke[0], &ctx->ke_cap, 4 * ctx->n));
+      MG_TRY(ensure(&ctx->d_ke[1], &ctx->ke1_cap, 4 * ctx->n));
+    }
     if (ctx->n && dispatch_w<LaunchScanAll>(ctx->maxw, ctx, ctx->stream, true))
       return set_err(ctx, "index build launch failed");
     if (!ctx->n) ctx->nrun_reg = 0;
+    if (ctx->sorted_index && fill_sorted_index(ctx)) return -1;
     ctx->scan_state = 1;
   } else if (dispatch_w<LaunchIndex>(ctx->maxw, ctx)) {
     return set_err(ctx, "index build launch failed");

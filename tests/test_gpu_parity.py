@@ -89,6 +89,25 @@ def test_lookup_matches_reference(engine, name):
     assert engine.lookup("ACGT") == []  # wrong length: no such key
 
 
+@pytest.mark.parametrize("name", ["highdup", "tandem", "mixed"])
+def test_lookup_tiny_directory(engine, name):
+    """getListOfReads through long overflow chains: with 2^10 requested buckets
+    the directory runs at ~70 % load, so many entries sit outside their home
+    cell; both index builds (CAS, and sorted + k_fill_cells<OVERFLOW>)."""
+    meta = load_meta(name)
+    ds = Dataset.from_files([fixture_input(name)], meta["l"])
+    engine.set_option("nb_log2", 10)
+    engine.set_shard(0, 1)
+    engine.upload(ds)
+    for sorted_index in (0, 1):
+        engine.set_option("sorted_index", sorted_index)
+        engine.build_index(meta["l"])
+        for key, exp in meta["lookups"].items():
+            assert [list(x) for x in engine.lookup(key)] == exp, key
+    engine.set_option("sorted_index", 0)
+    engine.set_option("nb_log2", 0)
+
+
 def test_ascii_upload_equals_packed(engine):
     meta = load_meta("mixed")
     ds = Dataset.from_files([fixture_input("mixed")], meta["l"])
@@ -534,6 +553,21 @@ def test_unsorted_runs_path(name):
     e = OverlapEngine(0)
     e.set_option("sort_runs", 0)
     rows, sup = gpu_rows(e, ds, meta["l"])
+    e.close()
+    assert np.array_equal(rows_to_tuples(rows), golden_rows(name))
+    assert {str(i): int(s) for i, s in enumerate(sup) if s} == meta["super"]
+
+
+@pytest.mark.parametrize("name,nb", [(f, 0) for f in FIXTURES] + [("highdup", 10), ("mixed", 10)])
+def test_sorted_index_path(name, nb):
+    """option sorted_index = 1: the fused scan writes its key records, a bucket
+    sort orders them and k_fill_cells files them with plain stores (overflow
+    through the chain walk) instead of per-key CAS; same results."""
+    meta = load_meta(name)
+    ds = Dataset.from_files([fixture_input(name)], meta["l"])
+    e = OverlapEngine(0)
+    e.set_option("sorted_index", 1)
+    rows, sup = gpu_rows(e, ds, meta["l"], nb_log2=nb)
     e.close()
     assert np.array_equal(rows_to_tuples(rows), golden_rows(name))
     assert {str(i): int(s) for i, s in enumerate(sup) if s} == meta["super"]

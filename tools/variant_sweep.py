@@ -13,7 +13,7 @@ from metagenomics_amd.overlap import Dataset, OverlapEngine  # noqa: E402
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 10_000_000
 c, L = synth.uniform_read_set(n, 150, n * 150 // 20, seed=31)
 ds = Dataset.from_codes(c, L, 50, nthreads=16)
-VARIANTS = [{"pack_runs": i % 2} for i in range(6)] + [{"sort_runs": 0}]
+VARIANTS = [{"sorted_index": i % 2} for i in range(6)]
 res = []
 for opts in VARIANTS:
     e = OverlapEngine(0)
