@@ -81,7 +81,7 @@ struct mg_ctx {
   unsigned long long* d_flat_cnt = nullptr;
   size_t flat_cnt_cap = 0;
   // timing
-  hipEvent_t ev[12] = {};
+  hipEvent_t ev[14] = {};
   // unsharded contexts build the index inside the window scan (k_scan<INDEX>);
   // its runs then serve the containment and the discovery probes
   int scan_state = 0;        // 0 none, 1 launched (not settled), 2 settled

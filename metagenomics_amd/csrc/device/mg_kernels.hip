@@ -410,8 +410,11 @@ __device__ __forceinline__ uint64_t run_meta(uint64_t a, int p, int jlo, int jhi
 // [0, w), i = w-1-t.  Same keys (order_key | i) as key_minimizer, so lookups
 // and the exchange mode's k_key_records agree.  The CAS inserts of a read's
 // four keys overlap the ALU-bound scan of the other wavefronts.
+// 6 waves per SIMD (the LDS limit: 6 blocks of 4 wavefronts per CU): 80 VGPRs
+// with a 12-B spill beat 83 VGPRs / 5 waves, index 3.72 vs 3.93 ms at C3
+// (profiles/r01s5_ab_scan_waves.log)
 template <int MAXW, bool INDEX>
-__global__ __launch_bounds__(kBlock) void k_scan(ScanParams p) {
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) void k_scan(ScanParams p) {
   extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int h = p.h, m = p.m, w = p.w;
@@ -529,7 +532,6 @@ __global__ __launch_bounds__(kBlock) void k_scan(ScanParams p) {
     };
     uint64_t mm = 0;
     if (tend) mm = funnel(rw[0], rw[1], 2) >> msh;  // m-mer at t = 1
-    uint64_t cw = word_at(__builtin_amdgcn_readfirstlane((1 + m) >> 5));  // word holding base t + m
     // INDEX: best (order_key | i) and m-mer of keys o = 0..3; rcm = reverse-strand m-mer
     uint32_t kb0 = 0xFFFFFFFFu, kb1 = 0xFFFFFFFFu, kb2 = 0xFFFFFFFFu, kb3 = 0xFFFFFFFFu;
     uint64_t mb0 = 0, mb1 = 0, mb2 = 0, mb3 = 0, rcm = 0;
@@ -540,7 +542,7 @@ __global__ __launch_bounds__(kBlock) void k_scan(ScanParams p) {
       mb0 = m0;
       kb3 = order_key(rcm) | (uint32_t)(w - 1);
       mb3 = rcm;
-      const uint64_t b = (word_at(__builtin_amdgcn_readfirstlane(m >> 5)) >> (62 - 2 * (m & 31))) & 3u;  // base at 0 + m
+      const uint64_t b = (((m >> 5) ? rw[1] : rw[0]) >> (62 - 2 * (m & 31))) & 3u;  // base at 0 + m (m <= 32)
       rcm = (rcm >> 2) | ((3u - b) << (2 * m - 2));
     }
     uint32_t pmin = 0xFFFFFFFFu;
@@ -549,7 +551,8 @@ __global__ __launch_bounds__(kBlock) void k_scan(ScanParams p) {
     // previous block's suffix minimum at u + 1, read one step ahead so the
     // LDS latency hides behind the step's ALU work
     uint32_t sv_pf = s_keys[kWave];
-    for (int t = 1; t <= tmax; ++t) {
+    // one base step t; cw = the read word holding base t + m
+    auto step = [&](int t, uint64_t cw) {
       bool emit = false;
       uint64_t e_meta = 0;
       if (t <= tend) {
@@ -596,10 +599,6 @@ __global__ __launch_bounds__(kBlock) void k_scan(ScanParams p) {
         const int x = t + m;  // roll in the base at t + m
         mm = ((mm << 2) | ((cw >> (62 - 2 * (x & 31))) & 3u)) & mmask;
       }
-      {
-        const int xu = __builtin_amdgcn_readfirstlane(t + m);
-        if ((xu & 31) == 31) cw = word_at((xu + 1) >> 5);  // next word (don't-care past a read's end)
-      }
       if (u == w - 1) {  // block complete: suffix minima in place, 8 reads in flight at a time
         uint32_t run = 0xFFFFFFFFu;
         for (int v0 = w - 1; v0 >= 0; v0 -= 8) {
@@ -619,6 +618,24 @@ __global__ __launch_bounds__(kBlock) void k_scan(ScanParams p) {
       sv_pf = s_keys[(u + 1 < w ? u + 1 : 0) * kWave];
       put(emit, e_meta);
       while (nbuf >= (uint32_t)kWave) flush(kWave);
+    };
+    if constexpr (MAXW <= 8) {
+      // one loop per read word (t + m <= n - 1 < 32 MAXW): the word is a
+      // compile-time register, so rw[] never goes to scratch and no vmcnt wait
+      // (which would also wait for the flushes' stores) sits in the loop
+#pragma unroll
+      for (int k = 0; k < MAXW; ++k) {
+        const int t0 = max(1, 32 * k - m), t1 = min(tmax, 32 * k + 31 - m);
+        for (int t = t0; t <= t1; ++t) step(t, rw[k]);
+      }
+    } else {
+      int cwi = __builtin_amdgcn_readfirstlane((1 + m) >> 5);
+      uint64_t cw = word_at(cwi);
+      for (int t = 1; t <= tmax; ++t) {
+        step(t, cw);
+        const int xu = __builtin_amdgcn_readfirstlane(t + m);
+        if ((xu & 31) == 31) cw = word_at((xu + 1) >> 5);  // next word (don't-care past a read's end)
+      }
     }
     put(tend > 0, run_meta(a, last_pos, jlo, J));  // each read's last run
     while (nbuf >= (uint32_t)kWave) flush(kWave);
@@ -2398,7 +2415,7 @@ struct LaunchScanAll {
     const uint64_t groups = (ctx->n + kWave - 1) / kWave;
     const uint32_t sgrid = index ? resident_blocks(ctx, k_scan<W, true>, lds, (groups + wpb - 1) / wpb, wpb * kWave)
                                  : resident_blocks(ctx, k_scan<W, false>, lds, (groups + wpb - 1) / wpb, wpb * kWave);
-    return LaunchScan<W>::run(ctx, true, 0, ctx->n, sgrid, false, st, true, index, ctx->sort_runs && !ctx->split);
+    return LaunchScan<W>::run(ctx, true, 0, ctx->n, sgrid, false, st, true, index, ctx->sort_runs);
   }
 };
 
@@ -2521,7 +2538,7 @@ int sort_shared_runs(mg_ctx* ctx) {
     }
     ctx->sk_cap = n;
   }
-  MG_TRY(hipEventRecord(ctx->ev[10], ctx->stream));
+  MG_TRY(hipEventRecord(ctx->ev[12], ctx->stream));
   if (!flat)
     MG_TRY(hipMemcpyAsync(ctx->d_run_off, off.data(), (nreg + 1) * sizeof(unsigned long long),
                           hipMemcpyHostToDevice, ctx->stream));
@@ -2559,7 +2576,7 @@ int sort_shared_runs(mg_ctx* ctx) {
   }
   tb = ctx->sort_tmp_cap;
   MG_TRY(sort(ctx->d_sort_tmp, tb, sel));
-  MG_TRY(hipEventRecord(ctx->ev[11], ctx->stream));
+  MG_TRY(hipEventRecord(ctx->ev[13], ctx->stream));
   ctx->sk_sel = sel;
   ctx->n_sorted = n;
   ctx->sorted_state = 2;
@@ -2569,7 +2586,7 @@ int sort_shared_runs(mg_ctx* ctx) {
 // probe the shared scan's runs (rows settled for the discovery probe)
 int probe_shared(mg_ctx* ctx, bool contain) {
   if (ensure_scan(ctx)) return -1;
-  if (ctx->sort_runs && !ctx->split) {
+  if (ctx->sort_runs) {
     if (sort_shared_runs(ctx)) return -1;
   }
   for (int attempt = 0; attempt < 3; ++attempt) {
@@ -2727,8 +2744,8 @@ int mg_find_overlaps(mg_ctx* ctx, uint64_t* n_rows) {
     ctx->t.probe_ms = shared_scan(ctx) ? elapsed(ctx->ev[8], ctx->ev[9]) : elapsed(ctx->ev[7], ctx->ev[5]);
     ctx->t.verify_ms = 0.f;
   }
-  ctx->t.sort_ms = (shared_scan(ctx) && ctx->sort_runs && !ctx->split && ctx->sorted_state == 2)
-                       ? elapsed(ctx->ev[10], ctx->ev[11]) : 0.f;
+  ctx->t.sort_ms = (shared_scan(ctx) && ctx->sort_runs && ctx->sorted_state == 2)
+                       ? elapsed(ctx->ev[12], ctx->ev[13]) : 0.f;
   ctx->t.overlap_ms = ctx->t.scan_ms + ctx->t.sort_ms + ctx->t.probe_ms + ctx->t.verify_ms;
   read_stats(ctx, nsrc);
   // device wall of the step: index build start .. last discovery kernel end
@@ -2834,8 +2851,8 @@ int mg_probe_runs(mg_ctx* ctx, int contain, const void* runs, uint64_t n, uint64
     ctx->t.verify_ms = 0.f;
   }
   if (contain) return 0;
-  ctx->t.sort_ms = (shared_scan(ctx) && ctx->sort_runs && !ctx->split && ctx->sorted_state == 2)
-                       ? elapsed(ctx->ev[10], ctx->ev[11]) : 0.f;
+  ctx->t.sort_ms = (shared_scan(ctx) && ctx->sort_runs && ctx->sorted_state == 2)
+                       ? elapsed(ctx->ev[12], ctx->ev[13]) : 0.f;
   ctx->t.overlap_ms = ctx->t.scan_ms + ctx->t.sort_ms + ctx->t.probe_ms + ctx->t.verify_ms;
   read_stats(ctx, 0);
   if (counts) {

@@ -15,7 +15,7 @@ from typing import Iterable, Sequence
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libmgovl.so")
+LIB_PATH = os.environ.get("MG_LIB") or os.path.join(_HERE, "lib", "libmgovl.so")  # MG_LIB: A/B builds (tools/)
 
 # exchange-mode record kinds (include/mg_overlap.h)
 MG_KEYS, MG_RUNS, MG_ROWS = 0, 1, 2
