@@ -168,7 +168,7 @@ def main():
     ap.add_argument("--no-ingest", action="store_true", help="skip the device Dataset ingest measurement")
     ap.add_argument("--replay", action="store_true",
                     help="also time the host replay of the exploration + transitive reduction + contraction on the rows")
-    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r01s4_pmc_c3.json"))
+    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r01s5_pmc_c3.json"))
     ap.add_argument("--nb-log2", type=int, default=0)
     ap.add_argument("--split-probe", action="store_true", help="probe -> candidates -> verify kernels (option split = 1)")
     ap.add_argument("--sort-runs", type=int, default=None,
