@@ -856,8 +856,13 @@ __global__ __launch_bounds__(kBlock) void k_probe(ProbeParams p) {
           cond = cond && (j <= n1 - n2);
           s = j;
         } else {
-          cond = cond && (j >= n2 - h);
-          s = j - (n2 - h);
+          // o = 1/3 (the partner's suffix key) place the partner at offset
+          // s = j - (n2 - h) >= 0, but every s >= 1 is also found by its o = 0/2
+          // hit at window j = s (checkOverlapForContainedRead, :302-340, both
+          // ranges end at s = n1 - n2), and the atomicMax result depends only on
+          // the pair: only s = 0 (a prefix of the container) needs this side
+          cond = cond && (j == n2 - h);
+          s = 0;
         }
         L = n2;
         y0 = 0;
@@ -1181,7 +1186,7 @@ __device__ __forceinline__ Cand cand_setup(const ProbeParams& p, uint3 c, bool h
       k.cond = k.cond && (j <= n1 - n2);
       sft = j;
     } else {
-      k.cond = k.cond && (j >= n2 - h);
+      k.cond = k.cond && (j == n2 - h);  // s = 0 only: s >= 1 is the o = 0/2 hit's (k_probe verify)
       sft = j - (n2 - h);
     }
     k.L = n2;
