@@ -202,6 +202,14 @@ int mg_get_counters(const mg_ctx* ctx, mg_counters* c);
  * "sort_runs" (1 = the shared scan's runs are radix-sorted by bucket before
  * the probes, so cell and partner loads coalesce (default); 0 = the probe
  * walks the scan's per-wavefront run regions),
+ * "pack_runs" (1 = 12-byte sort records when the field widths fit (default);
+ * 0 = 16-byte records),
+ * "sorted_index" (1 = k_scan<INDEX> writes the key records, a bucket sort
+ * orders them and the cells are filled with plain stores; 0 = per-key CAS
+ * inserts inside the scan (default, faster at C3)),
+ * "prefix_contain" (1 = mixed-length sets find offset-0 containments with
+ * k_prefix_contain and the containment probe skips suffix-key hits (default);
+ * 0 = the probe verifies suffix-key hits at offset 0 itself),
  * "flat_cap" (tests: initial capacity of the sorted-run arrays, 0 = auto),
  * "sort_bits" (diagnostics: sort only the top bucket bits, 0 = all),
  * "halving" (which side emits a self-symmetric o=2/3 discovery pair:

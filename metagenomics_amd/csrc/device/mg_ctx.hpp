@@ -120,6 +120,13 @@ struct mg_ctx {
   // at C3: index 5.6 vs 3.9 ms (the CAS inserts hide behind the scan's ALU work;
   // the key sort alone costs 1.2 ms), so CAS stays the default
   bool sorted_index = false;
+  // prefix containments (k_prefix_contain): each read's o = 0 key (bucket,
+  // fingerprint, q) written by k_scan<INDEX> for mixed-length sets; when ready
+  // the containment probe skips suffix-key hits (containment)
+  uint64_t* d_key0 = nullptr;
+  size_t key0_cap = 0;
+  bool key0_ready = false;
+  bool prefix_contain = true;  // option "prefix_contain"
   uint32_t* d_kb[2] = {nullptr, nullptr};
   uint64_t* d_ke[2] = {nullptr, nullptr};
   size_t kb_cap = 0, ke_cap = 0, kb1_cap = 0, ke1_cap = 0;

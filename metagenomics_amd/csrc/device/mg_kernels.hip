@@ -284,6 +284,72 @@ __global__ __launch_bounds__(kBlock) void k_fill_cells(const uint32_t* __restric
   }
 }
 
+// markContainedReads at offset s = 0 (OverlapGraph.cpp:225-340): read2 (or
+// its reverse strand) is a prefix of read1.  The reference meets these only
+// through read2's suffix key (o = 1/3 at window j = n2 - h), because window
+// j = 0 is never scanned; every offset s >= 1 is a prefix-key hit (o = 0/2) at
+// window j = s.  A prefix of read1 shares read1's own o = 0 key exactly, so one
+// thread per read1 walks that key's cell chain: entries with o = 0/2, the same
+// fingerprint and offset q, a shorter read2 and F1[0, n2) == F2 (o = 0) or R2
+// (o = 2) -> the same atomicMax as the probe.  With this kernel the
+// containment probe drops all o = 1/3 hits (ProbeParams::contain_even).
+template <int MAXW>
+__global__ __launch_bounds__(kBlock) void k_prefix_contain(const uint64_t* __restrict__ words,
+                                                           const uint16_t* __restrict__ len,
+                                                           const uint64_t* __restrict__ key0,
+                                                           const uint64_t* __restrict__ cells, uint64_t cell_n,
+                                                           uint32_t nb_log2, uint64_t n,
+                                                           unsigned long long* __restrict__ superkey) {
+  const uint64_t a = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (a >= n) return;
+  const uint64_t k0 = key0[a];
+  if (k0 == kEmpty) return;
+  const int n1 = len[a];
+  const uint32_t fp = (uint32_t)(k0 >> nb_log2) & kFpMask;
+  const uint32_t q = (uint32_t)(k0 >> 54);
+  const uint64_t* f1 = words + a * slot_words(MAXW);
+  uint64_t c = k0 & ((1ULL << nb_log2) - 1);
+  for (uint64_t probe = 0; probe < cell_n; ++probe) {
+    const ulonglong2* cp = reinterpret_cast<const ulonglong2*>(cells + c * kCell);
+    uint64_t e[kCell];
+#pragma unroll
+    for (int s = 0; s < kCell / 2; ++s) {
+      const ulonglong2 x = cp[s];
+      e[2 * s] = x.x;
+      e[2 * s + 1] = x.y;
+    }
+    for (int s = 0; s < kCell; ++s) {
+      if (e[s] == kEmpty) continue;
+      const uint32_t hi = (uint32_t)(e[s] >> 32), r2 = (uint32_t)e[s];
+      const int o = (int)(hi & 3u);
+      if ((o & 1) || r2 == (uint32_t)a || ((hi >> 12) & kFpMask) != fp || ((hi >> 2) & 1023u) != q) continue;
+      const int n2 = len[r2];
+      if (n2 >= n1) continue;
+      const uint64_t* f2 = words + (uint64_t)r2 * slot_words(MAXW);
+      uint64_t diff = 0;
+      for (int k = 0; 32 * k < n2; ++k) {  // F1 bases [32k, 32k + 32) vs T's
+        const uint64_t bv = o == 0 ? f2[k] : rc_word(ext_fwd<1>(f2, n2 - 32 * k - 32));
+        const int rem = n2 - 32 * k;
+        diff |= (f1[k] ^ bv) & (rem >= 32 ? ~0ULL : ~(~0ULL >> (2 * rem)));
+      }
+      if (!diff) atomicMax(&superkey[r2], ((unsigned long long)n1 << 32) | (0xFFFFFFFFu - (uint32_t)a));
+    }
+    if (e[kCell - 1] == kEmpty || !(e[kCell - 1] & kChain)) break;
+    c = next_cell(c, cell_n);
+  }
+}
+
+template <int W>
+struct LaunchPrefixContain {
+  static int run(mg_ctx* ctx) {
+    if (!ctx->n) return 0;
+    hipLaunchKernelGGL(k_prefix_contain<W>, dim3((uint32_t)((ctx->n + kBlock - 1) / kBlock)), dim3(kBlock), 0,
+                       ctx->stream, ctx->d_words, ctx->d_len, ctx->d_key0, ctx->d_cells, ctx->cell_n, ctx->nb_log2,
+                       ctx->n, ctx->d_superkey);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+  }
+};
+
 // Exchange mode, step 1: the index records of the keys of source reads
 // [a_lo, a_hi) (16 B: x = mix64(minimizer), y = entry without fingerprint),
 // written densely in key order; k_part routes them to the bucket owners.
@@ -349,6 +415,9 @@ struct ScanParams {
   uint32_t* key_bk;
   uint64_t* key_ent;
   uint64_t key_n;
+  // per read: its o = 0 key's hash bits (bucket | fingerprint, 50 bits) | q << 54
+  // (k_prefix_contain); nullptr: not written
+  uint64_t* key0;
 };
 
 // Sort records of 12 B instead of 16 (option "sort_runs" when the widths fit,
@@ -657,6 +726,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) voi
       for (int o = 0; o < 4; ++o) {
         const uint64_t v = mix64(mb[o]);
         const unsigned long long e = make_entry(v, p.nb_log2, (int)(kb[o] & 1023u), o, (uint32_t)a);
+        if (o == 0 && p.key0) p.key0[a] = (v & ((1ULL << 50) - 1)) | ((uint64_t)(kb[0] & 1023u) << 54);
         if (p.key_bk) {  // o-major: each store is one coalesced wavefront line
           p.key_bk[o * p.key_n + a] = (uint32_t)(v & nbm);
           p.key_ent[o * p.key_n + a] = e;
@@ -664,11 +734,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) voi
           cell_insert(p.cells, v & nbm, p.cell_n, e);
         }
       }
-    } else if (INDEX && p.key_bk && a < p.a_hi) {  // no keys (n <= l cannot pass setup_index): holes
-#pragma unroll
-      for (int o = 0; o < 4; ++o) {
-        p.key_bk[o * p.key_n + a] = 0;
-        p.key_ent[o * p.key_n + a] = kEmpty;
+    } else if (INDEX && a < p.a_hi) {  // no keys (n <= l cannot pass setup_index): holes
+      if (p.key0) p.key0[a] = kEmpty;
+      if (p.key_bk) {
+        for (int o = 0; o < 4; ++o) {
+          p.key_bk[o * p.key_n + a] = 0;
+          p.key_ent[o * p.key_n + a] = kEmpty;
+        }
       }
     }
   }
@@ -758,6 +830,7 @@ struct ProbeParams {
   unsigned long long* stats;      // optional [kSegs*4]: runs probed, entries scanned, partners fetched, rows
   int phase_limit;                // diagnostics: 4 no probe, 5 + cell loads, 6 + filter, 7 full
   int halving_low;                // option "halving" = 1: keep o=2/3 pairs at the lower ID (else rc_side_keeps)
+  int contain_even;               // CONTAIN: drop o = 1/3 hits (k_prefix_contain finds the s = 0 containments)
   // split path (k_probe<SPLIT=true> + k_verify): candidates {partner, source, o << 30 | j}
   uint3* cand;                    // one region of cand_cap records per probe wavefront
   unsigned long long* cand_cnt;   // [waves] candidates written (may exceed cand_cap)
@@ -1036,6 +1109,9 @@ __global__ __launch_bounds__(kBlock) void k_probe(ProbeParams p) {
       // hits; an o=2/3 pair is kept on one side only (rc_side_keeps)
       keep = keep && (CONTAIN || oo == 0 ||
                       (oo >= 2 && (p.halving_low ? (uint32_t)e[s] >= ra : rc_side_keeps(ra, (uint32_t)e[s]))));
+      // containment with k_prefix_contain covering offset s = 0: suffix-key
+      // hits (o = 1/3) add nothing (see the verify's CONTAIN case)
+      keep = keep && !(CONTAIN && p.contain_even && (oo & 1));
       keepm |= (keep ? 1u : 0u) << s;
     }
     if (SPLIT) {
@@ -1745,6 +1821,7 @@ struct LaunchScan {
     } else {
       ctx->pack_a = ctx->pack_w = 0;
     }
+    if (index && ctx->key0_ready) sp.key0 = ctx->d_key0;  // mg_build_index allocated it (mixed lengths)
     if (index && ctx->sorted_index) {  // key records for the sorted build (mg_build_index files them)
       sp.key_bk = ctx->d_kb[0];
       sp.key_ent = ctx->d_ke[0];
@@ -1807,6 +1884,7 @@ struct LaunchProbe {
     pp.stats = contain ? nullptr : (ctx->stats ? ctx->d_stats : nullptr);
     pp.phase_limit = contain ? 99 : ctx->phase_limit;
     pp.halving_low = ctx->halving_low ? 1 : 0;
+    pp.contain_even = (contain && ctx->key0_ready) ? 1 : 0;
     if (ctx->split) return run_split(ctx, contain, pp, grid, total_runs);
     const size_t lds = (size_t)kWavesPerBlock * ProbeLds<W>::bytes;
     if (contain)
@@ -2012,7 +2090,7 @@ void mg_destroy(mg_ctx* ctx) {
                   ctx->d_superkey, ctx->d_super, ctx->d_any, ctx->d_rows, ctx->d_seg, ctx->d_stats,
                   ctx->d_compact, ctx->d_runs, ctx->d_run_cnt, ctx->d_keyrec, ctx->d_blk, ctx->d_flat_cnt, ctx->d_cand, ctx->d_cand_cnt, ctx->d_freq,
                   ctx->d_sk[0], ctx->d_sk[1], ctx->d_sm[0], ctx->d_sm[1], ctx->d_sort_tmp, ctx->d_run_off,
-                  ctx->d_flat_cursor, ctx->d_kb[0], ctx->d_kb[1], ctx->d_ke[0], ctx->d_ke[1]};
+                  ctx->d_flat_cursor, ctx->d_kb[0], ctx->d_kb[1], ctx->d_ke[0], ctx->d_ke[1], ctx->d_key0};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   for (auto& e : ctx->ev)
@@ -2157,6 +2235,11 @@ int mg_set_option(mg_ctx* ctx, const char* name, int64_t value) {
     ctx->sorted_state = 0;
     return 0;
   }
+  if (!strcmp(name, "prefix_contain")) {  // 1 (default): k_prefix_contain + even-o containment probe
+    ctx->prefix_contain = value != 0;
+    ctx->index_ready = false;
+    return 0;
+  }
   if (!strcmp(name, "sorted_index")) {  // 1: bucket-sorted key records + plain stores; 0 (default): CAS inserts
     ctx->sorted_index = value != 0;
     ctx->index_ready = false;
@@ -2243,6 +2326,7 @@ int setup_index(mg_ctx* ctx, uint32_t min_overlap, uint32_t seed_k) {
   ctx->index_ready = false;
   ctx->contained_done = false;
   ctx->super_any = false;
+  ctx->key0_ready = false;  // set by the fused build when it writes the o = 0 keys
   return 0;
 }
 
@@ -2659,6 +2743,9 @@ int mg_build_index(mg_ctx* ctx, uint32_t min_overlap, uint32_t seed_k) {
     // (k_scan<INDEX>), whose runs then serve the containment and discovery
     // probes.  Measured at C3 (same box): 3.58 ms vs index 2.05 + scan 1.83
     // separately; a concurrent scan on a second stream did not overlap (3.95).
+    // mixed lengths: each read's o = 0 key for the prefix-containment kernel
+    ctx->key0_ready = ctx->minlen != ctx->maxlen && ctx->prefix_contain;
+    if (ctx->key0_ready) MG_TRY(ensure(&ctx->d_key0, &ctx->key0_cap, ctx->n + 1));
     if (ctx->sorted_index) {
       MG_TRY(ensure(&ctx->d_kb[0], &ctx->kb_cap, 4 * ctx->n));
       MG_TRY(ensure(&ctx->d_kb[1], &ctx->kb1_cap, 4 * ctx->n));
@@ -2701,7 +2788,10 @@ int mg_mark_contained(mg_ctx* ctx, uint32_t* super_out) {
     // sharded contexts still need the full superReadID vector: run over all
     // buckets (the containment pass is small, only for mixed lengths)
     if (ctx->nranks > 1) return set_err(ctx, "containment with a bucket-sharded index: use the exchange mode");
+    if (!shared_scan(ctx)) ctx->key0_ready = false;  // only the shared scan writes the o = 0 keys
     if (shared_scan(ctx) ? probe_shared(ctx, true) : run_discover(ctx, true)) return -1;
+    if (ctx->key0_ready && dispatch_w<LaunchPrefixContain>(ctx->maxw, ctx))
+      return set_err(ctx, "prefix containment launch failed");
     if (ctx->n)
       hipLaunchKernelGGL(k_super_finalize, dim3((uint32_t)((ctx->n + kBlock - 1) / kBlock)), dim3(kBlock), 0,
                          ctx->stream, ctx->d_superkey, ctx->n, ctx->d_super, ctx->d_any);

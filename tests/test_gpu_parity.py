@@ -198,7 +198,24 @@ EDGE_SETS = {
     "single_tandem": (["ACGTTGCAAG" * 8], 20),  # self-overlaps of one read
     "l_plus_one": (None, 40),                    # every read exactly l + 1 bases
     "max_len": (None, 200),                      # reads up to 1024 bases (32 words)
+    "prefixes": (None, 40),                      # nested exact prefixes, both strands (containment s = 0)
 }
+
+
+def prefix_reads(seed=113):
+    """Reads that are exact prefixes (or reverse-complement prefixes) of longer
+    reads, nested, plus suffixes and inner pieces: containment at offset 0,
+    which the reference finds only through suffix keys (k_prefix_contain)."""
+    rng = np.random.default_rng(seed)
+    comp = str.maketrans("ACGT", "TGCA")
+    out = []
+    for _ in range(6):
+        g = "".join(rng.choice(list("ACGT"), 420))
+        rc = lambda x: x.translate(comp)[::-1]  # noqa: E731
+        out += [g[:n] for n in (45, 50, 60, 75, 90, 120, 160, 220, 300, 420)]
+        out += [rc(g[:n]) for n in (55, 70, 130, 260)]
+        out += [g[420 - n:] for n in (48, 100, 250)] + [g[30:130], rc(g[10:200])]
+    return out
 
 
 @pytest.mark.parametrize("name", sorted(EDGE_SETS))
@@ -211,6 +228,8 @@ def test_edge_sets_vs_oracle(engine, name):
     elif name == "max_len":
         c, L = synth.uniform_read_set(600, 0, 40000, seed=112, lo=1000, hi=1024)
         seqs = synth.codes_to_strings(c, L)
+    elif name == "prefixes":
+        seqs = prefix_reads()
     ds = Dataset.from_strings(seqs, l)
     od = OracleDataset.from_strings(seqs, l)
     assert ds.num_unique == od.num_unique
@@ -571,6 +590,30 @@ def test_sorted_index_path(name, nb):
     e.close()
     assert np.array_equal(rows_to_tuples(rows), golden_rows(name))
     assert {str(i): int(s) for i, s in enumerate(sup) if s} == meta["super"]
+
+
+@pytest.mark.parametrize("name", FIXTURES + ["prefixes"])
+def test_prefix_contain_off(name):
+    """option prefix_contain = 0: the containment probe verifies suffix-key
+    hits too (at offset s = 0 only) instead of running k_prefix_contain; the
+    same superReadID and rows."""
+    if name == "prefixes":
+        seqs, l = prefix_reads(), 40
+        ds = Dataset.from_strings(seqs, l)
+        orows, osup, _, _ = OracleDataset.from_strings(seqs, l).overlaps(l)
+        want_rows, want_sup = sorted_tuples(orows), {str(i): int(x) for i, x in enumerate(osup) if x}
+    else:
+        meta = load_meta(name)
+        l = meta["l"]
+        ds = Dataset.from_files([fixture_input(name)], l)
+        want_rows, want_sup = golden_rows(name), meta["super"]
+    for flag in (0, 1):
+        e = OverlapEngine(0)
+        e.set_option("prefix_contain", flag)
+        rows, sup = gpu_rows(e, ds, l)
+        e.close()
+        assert np.array_equal(rows_to_tuples(rows), want_rows), flag
+        assert {str(i): int(x) for i, x in enumerate(sup) if x} == want_sup, flag
 
 
 @pytest.mark.parametrize("name", FIXTURES)
