@@ -509,67 +509,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) voi
     if (flag) s_buf[nbuf + lane_prefix(bal)] = meta;
     nbuf += (uint32_t)__popcll(bal);
   };
-  // hash the first k (<= 64) staged runs with every lane busy, drop runs whose
-  // bucket another rank owns, write full-wavefront 16-B records
-  auto flush = [&](uint32_t k) {
-    wave_sync();
-    bool flag = (uint32_t)lane < k;
-    uint64_t v = 0, meta = 0;
-    if (flag) {
-      meta = s_buf[lane];
-      const uint64_t* g2 = p.words + (meta & 0xFFFFFFFFull) * slot_words(MAXW);
-      const int pos = (int)((meta >> 32) & 1023u);
-      v = mix64(funnel(g2[pos >> 5], g2[(pos >> 5) + 1], (pos & 31) << 1) >> msh);
-      flag = owned(v & nbmask, p.nb_log2, p.rank, p.nranks);
-    }
-    const uint64_t bal = __ballot(flag);
-    if (p.flat_keys) {
-      // this wavefront's current chunk of the flat arrays; a new chunk (one
-      // atomic per kFlatChunk records: a cursor bumped per flush serialised at
-      // 20 ms) takes whatever does not fit in the current one
-      const uint64_t npop = (uint64_t)__popcll(bal);
-      const uint64_t room = fcap - fused;
-      unsigned long long nbase = 0;
-      if (npop > room) {  // chunk ids x, x + 8, x + 16, ... belong to counter x = blockIdx % 8
-        const uint32_t x = blockIdx.x & (kFlatCounters - 1);
-        if (lane == 0) nbase = (atomicAdd(&p.flat_cursor[x], 1ull) * kFlatCounters + x) * kFlatChunk;
-        nbase = __shfl(nbase, 0);
-      }
-      if (flag) {
-        const uint64_t pr = lane_prefix(bal);
-        const uint64_t at = pr < room ? fbase + fused + pr : nbase + (pr - room);
-        if (at < p.flat_cap) {
-          if (p.pack_a) {
-            reinterpret_cast<uint32_t*>(p.flat_keys)[at] = run_pack_key(v, p.nb_log2);
-            p.flat_meta[at] = run_pack_meta(meta, v, p.nb_log2, p.pack_a, p.pack_w);
-          } else {
-            p.flat_keys[at] = v;
-            p.flat_meta[at] = meta;
-          }
-        }
-      }
-      if (npop > room) {
-        fbase = nbase;
-        fused = npop - room;
-        fcap = kFlatChunk;
-      } else {
-        fused += npop;
-      }
-    } else if (flag) {
-      const uint64_t at = cursor + lane_prefix(bal);
-      if (at < p.run_cap) region[at] = make_ulonglong2(v, meta);
-    }
-    cursor += (uint64_t)__popcll(bal);
-    const uint32_t rest = nbuf - k;  // < 128 left: move them to the front
-    const uint64_t m0 = (uint32_t)lane < rest ? s_buf[k + lane] : 0;
-    const uint64_t m1 = (uint32_t)lane + kWave < rest ? s_buf[k + kWave + lane] : 0;
-    wave_sync();
-    if ((uint32_t)lane < rest) s_buf[lane] = m0;
-    if ((uint32_t)lane + kWave < rest) s_buf[kWave + lane] = m1;
-    nbuf = rest;
-    wave_sync();
-  };
-
   for (uint64_t grp = gw; grp < ngroups; grp += nw) {
     const uint64_t a = p.a_lo + grp * kWave + lane;
     int n = 0;
@@ -598,6 +537,86 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) voi
 #pragma unroll
       for (int k = 1; k <= MAXW; ++k) v = idx == k ? rw[k] : v;
       return v;
+    };
+    const uint64_t a0 = p.a_lo + grp * kWave;  // lane l holds read a0 + l
+    // hash the first k (<= 64) staged runs with every lane busy, drop runs whose
+    // bucket another rank owns, write full-wavefront 16-B records
+    auto flush = [&](uint32_t k) {
+      wave_sync();
+      bool flag = (uint32_t)lane < k;
+      uint64_t v = 0, meta = 0;
+      if (flag) meta = s_buf[lane];
+      if constexpr (MAXW <= 8) {
+        // every staged run belongs to a read of this group (flushed before the
+        // next group): its words come from the owner lane's registers, not HBM
+        // (a global load here made every flush wait for the earlier stores)
+        const int pos = (int)((meta >> 32) & 1023u), wi = pos >> 5;
+        const int src = flag ? (int)((uint32_t)meta - (uint32_t)a0) : lane;
+        uint64_t w0 = 0, w1 = 0;
+  #pragma unroll
+        for (int kk = 0; kk <= MAXW; ++kk) {
+          const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute(src << 2, (int)(uint32_t)rw[kk]);
+          const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_bpermute(src << 2, (int)(uint32_t)(rw[kk] >> 32));
+          const uint64_t x = ((uint64_t)hi << 32) | lo;
+          w0 = wi == kk ? x : w0;
+          w1 = wi + 1 == kk ? x : w1;
+        }
+        if (flag) {
+          v = mix64(funnel(w0, w1, (pos & 31) << 1) >> msh);
+          flag = owned(v & nbmask, p.nb_log2, p.rank, p.nranks);
+        }
+      } else if (flag) {
+        const uint64_t* g2 = p.words + (meta & 0xFFFFFFFFull) * slot_words(MAXW);
+        const int pos = (int)((meta >> 32) & 1023u);
+        v = mix64(funnel(g2[pos >> 5], g2[(pos >> 5) + 1], (pos & 31) << 1) >> msh);
+        flag = owned(v & nbmask, p.nb_log2, p.rank, p.nranks);
+      }
+      const uint64_t bal = __ballot(flag);
+      if (p.flat_keys) {
+        // this wavefront's current chunk of the flat arrays; a new chunk (one
+        // atomic per kFlatChunk records: a cursor bumped per flush serialised at
+        // 20 ms) takes whatever does not fit in the current one
+        const uint64_t npop = (uint64_t)__popcll(bal);
+        const uint64_t room = fcap - fused;
+        unsigned long long nbase = 0;
+        if (npop > room) {  // chunk ids x, x + 8, x + 16, ... belong to counter x = blockIdx % 8
+          const uint32_t x = blockIdx.x & (kFlatCounters - 1);
+          if (lane == 0) nbase = (atomicAdd(&p.flat_cursor[x], 1ull) * kFlatCounters + x) * kFlatChunk;
+          nbase = __shfl(nbase, 0);
+        }
+        if (flag) {
+          const uint64_t pr = lane_prefix(bal);
+          const uint64_t at = pr < room ? fbase + fused + pr : nbase + (pr - room);
+          if (at < p.flat_cap) {
+            if (p.pack_a) {
+              reinterpret_cast<uint32_t*>(p.flat_keys)[at] = run_pack_key(v, p.nb_log2);
+              p.flat_meta[at] = run_pack_meta(meta, v, p.nb_log2, p.pack_a, p.pack_w);
+            } else {
+              p.flat_keys[at] = v;
+              p.flat_meta[at] = meta;
+            }
+          }
+        }
+        if (npop > room) {
+          fbase = nbase;
+          fused = npop - room;
+          fcap = kFlatChunk;
+        } else {
+          fused += npop;
+        }
+      } else if (flag) {
+        const uint64_t at = cursor + lane_prefix(bal);
+        if (at < p.run_cap) region[at] = make_ulonglong2(v, meta);
+      }
+      cursor += (uint64_t)__popcll(bal);
+      const uint32_t rest = nbuf - k;  // < 128 left: move them to the front
+      const uint64_t m0 = (uint32_t)lane < rest ? s_buf[k + lane] : 0;
+      const uint64_t m1 = (uint32_t)lane + kWave < rest ? s_buf[k + kWave + lane] : 0;
+      wave_sync();
+      if ((uint32_t)lane < rest) s_buf[lane] = m0;
+      if ((uint32_t)lane + kWave < rest) s_buf[kWave + lane] = m1;
+      nbuf = rest;
+      wave_sync();
     };
     uint64_t mm = 0;
     if (tend) mm = funnel(rw[0], rw[1], 2) >> msh;  // m-mer at t = 1
@@ -707,7 +726,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) voi
       }
     }
     put(tend > 0, run_meta(a, last_pos, jlo, J));  // each read's last run
-    while (nbuf >= (uint32_t)kWave) flush(kWave);
+    while (nbuf) flush(nbuf < (uint32_t)kWave ? nbuf : (uint32_t)kWave);  // the group's runs leave with its registers
     if (INDEX && tend) {
       // t = n-m, one past the last window position: the rolled m-mers sit there
       const uint32_t hk = order_key(mm), hr = order_key(rcm);
@@ -744,7 +763,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) voi
       }
     }
   }
-  while (nbuf) flush(nbuf < (uint32_t)kWave ? nbuf : (uint32_t)kWave);
   if (p.flat_keys) {  // the unused tail of the last chunk: records the probe skips
     for (uint64_t i = fused + lane; i < fcap; i += kWave) {
       const uint64_t at = fbase + i;
