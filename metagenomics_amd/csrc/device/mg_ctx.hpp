@@ -109,6 +109,9 @@ struct mg_ctx {
   bool scan_flat = false;          // the shared scan wrote d_sk[0] / d_sm[0] directly
   unsigned long long* d_flat_cursor = nullptr;
   uint64_t flat_need = 0, n_flat = 0;
+  uint64_t* d_holes = nullptr;  // chunk ids of the flat arrays no counter reached (k_fill_holes)
+  size_t holes_cap = 0;
+  std::vector<uint64_t> holes_host;
   uint64_t flat_cap_opt = 0;       // option "flat_cap" (tests: force the overflow rerun)
   bool pack_runs = true;           // option "pack_runs": 12-B sort records when the widths fit
   int pack_a = 0, pack_w = 0;      // packing of the current flat runs (0: 16-B records)

@@ -1690,6 +1690,22 @@ struct LaunchIndex {
   }
 };
 
+// Flat scan output: chunk ids below the extent that no counter reached hold
+// nothing; one block per such chunk marks its records as holes (all-ones key
+// and meta) that the sort moves to the end and the probe skips.  One launch
+// instead of two memsets per chunk (~40 per C3 step, ~0.4 ms of launches).
+__global__ __launch_bounds__(kBlock) void k_fill_holes(const uint64_t* __restrict__ ids, uint64_t* keys,
+                                                       uint64_t* meta, int packed) {
+  const uint64_t base = ids[blockIdx.x] * kFlatChunk;
+  for (uint32_t i = threadIdx.x; i < kFlatChunk; i += kBlock) {
+    if (packed)
+      reinterpret_cast<uint32_t*>(keys)[base + i] = 0xFFFFFFFFu;
+    else
+      keys[base + i] = kEmpty;
+    meta[base + i] = kFlatHole;
+  }
+}
+
 // Persistent grids: exactly the resident blocks (a larger grid would run a
 // second, partly idle round of wavefronts).  Scan and probe use the same
 // wavefront count: probe wavefront r consumes scan region r.
@@ -2108,7 +2124,7 @@ void mg_destroy(mg_ctx* ctx) {
                   ctx->d_superkey, ctx->d_super, ctx->d_any, ctx->d_rows, ctx->d_seg, ctx->d_stats,
                   ctx->d_compact, ctx->d_runs, ctx->d_run_cnt, ctx->d_keyrec, ctx->d_blk, ctx->d_flat_cnt, ctx->d_cand, ctx->d_cand_cnt, ctx->d_freq,
                   ctx->d_sk[0], ctx->d_sk[1], ctx->d_sm[0], ctx->d_sm[1], ctx->d_sort_tmp, ctx->d_run_off,
-                  ctx->d_flat_cursor, ctx->d_kb[0], ctx->d_kb[1], ctx->d_ke[0], ctx->d_ke[1], ctx->d_key0};
+                  ctx->d_flat_cursor, ctx->d_kb[0], ctx->d_kb[1], ctx->d_ke[0], ctx->d_ke[1], ctx->d_key0, ctx->d_holes};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   for (auto& e : ctx->ev)
@@ -2548,13 +2564,18 @@ int settle_flat(mg_ctx* ctx, bool* again) {
   }
   // ids below the extent that a counter never reached hold nothing: mark them
   // as holes (all-ones key and meta) so the sort and the probe skip them
-  const size_t kb = ctx->pack_a ? sizeof(uint32_t) : sizeof(uint64_t);
+  ctx->holes_host.clear();
   for (uint32_t x = 0; x < kFlatCounters; ++x)
-    for (uint64_t id = c[x] * kFlatCounters + x; id < ext; id += kFlatCounters) {
-      MG_TRY(hipMemsetAsync(reinterpret_cast<char*>(ctx->d_sk[0]) + id * kFlatChunk * kb, 0xFF, kFlatChunk * kb,
-                            ctx->stream));
-      MG_TRY(hipMemsetAsync(ctx->d_sm[0] + id * kFlatChunk, 0xFF, kFlatChunk * sizeof(uint64_t), ctx->stream));
-    }
+    for (uint64_t id = c[x] * kFlatCounters + x; id < ext; id += kFlatCounters) ctx->holes_host.push_back(id);
+  if (!ctx->holes_host.empty()) {
+    const size_t nh = ctx->holes_host.size();
+    MG_TRY(ensure(&ctx->d_holes, &ctx->holes_cap, nh));
+    MG_TRY(hipMemcpyAsync(ctx->d_holes, ctx->holes_host.data(), nh * sizeof(uint64_t), hipMemcpyHostToDevice,
+                          ctx->stream));
+    hipLaunchKernelGGL(k_fill_holes, dim3((uint32_t)nh), dim3(kBlock), 0, ctx->stream, ctx->d_holes, ctx->d_sk[0],
+                       ctx->d_sm[0], ctx->pack_a ? 1 : 0);
+    MG_TRY(hipGetLastError());
+  }
   ctx->n_flat = n;
   return 0;
 }
