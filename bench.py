@@ -51,8 +51,13 @@ CONFIGS = {
     # abundance, 437.5 Mb in total (20x mean coverage), 100-250 bp reads
     "c5": (50_000_000, 100, 250, 437_500_000, 50, 31, 55,
            "C5: 50M x 100-250 bp metagenome (100 genomes), l=50, k=31"),
+    # C5-shaped at the size the reference itself finishes in the build
+    # container (tests/golden/c5s.json pins it)
+    "c5s": (5_000_000, 100, 250, 43_750_000, 50, 31, 55,
+            "C5-shaped: 5M x 100-250 bp metagenome (100 genomes), l=50, k=31"),
 }
-META_GENOMES = {"c5": 100}
+META_GENOMES = {"c5": 100, "c5s": 100}
+GOLDEN_DIGEST = os.path.join(ROOT, "tests", "golden", "{}.json")  # reference digests (make_scale_golden.py)
 
 
 def log(*a):
@@ -93,9 +98,17 @@ def device_ingest(ds, codes, lens, l, device, host_s, nthreads):
         e.close()
 
 
-def cpu_baseline(cfg, sample_reads: int):
-    """Reference CPU path on a bounded sample of the same workload shape
-    (same read length, l, coverage), rank 0 at N=1 only."""
+def cpu_baseline(cfg, sample_reads: int, full_build: bool = True):
+    """Reference CPU path on a bounded sample of the same workload shape (same
+    read length, l, coverage), rank 0 at N=1 only.
+
+    value = the reference's own `ref_harness disc` (oracle/ref_harness.cpp):
+    HashTable::insertDataset + markContainedReads + the insertAllEdgesOfRead loop
+    (HashTable.cpp:50-80, OverlapGraph.cpp:225-290,529-565), i.e. the same work
+    as the GPU step (index + containment + raw edge multiset).  The shipped
+    path's full `new OverlapGraph(ht)` (with the interleaved transitive
+    reduction and the contraction loop, main.cpp:45-47) is reported beside it as
+    full_build_edges_per_sec.  The reference is single-threaded: cores = 1."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle  # the checker / baseline only
 
@@ -108,23 +121,80 @@ def cpu_baseline(cfg, sample_reads: int):
     rows, _, th, td = od.overlaps(l)
     edges = rows.shape[0] // 2
     sample = f"{sample_reads} reads x {lo}-{hi} bp, {cov:.0f}x coverage of {Gs} bp, l={l}"
+    share = os.environ.get("OMP_NUM_THREADS")
+    common = {"unit": "edges/s", "cores": 1, "host_cores_total": os.cpu_count(),
+              "host_cores_share": int(share) if share and share.isdigit() else None,
+              "edges": edges, "port_discovery_edges_per_sec": edges / (th + td)}
     if os.path.exists(oracle.REF_HARNESS):
         with tempfile.TemporaryDirectory() as td_:
             fa = os.path.join(td_, "s.fa")
             synth.write_fasta(fa, seqs)
-            out = os.path.join(td_, "t.json")
-            subprocess.run([oracle.REF_HARNESS, "time", fa, str(l), out], check=True,
+            out = os.path.join(td_, "d.json")
+            subprocess.run([oracle.REF_HARNESS, "disc", fa, str(l), out], check=True,
                            stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
             r = json.load(open(out))
-        secs = r["hash_s"] + r["graph_s"]
-        return {"value": edges / secs, "unit": "edges/s", "cores": 1, "kind": "reference",
-                "sample": sample + "; reference insertDataset + OverlapGraph(ht) (main.cpp:45-47) wall time",
-                "seconds": secs, "edges": edges, "reads_per_sec": od.num_unique / secs,
-                "port_discovery_edges_per_sec": edges / (th + td)}
+            full = None
+            if full_build:
+                subprocess.run([oracle.REF_HARNESS, "time", fa, str(l), out], check=True,
+                               stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+                full = json.load(open(out))
+        if r["directed_rows"] != rows.shape[0]:
+            raise RuntimeError(f"reference rows {r['directed_rows']} != oracle rows {rows.shape[0]}")
+        secs = r["hash_s"] + r["discovery_s"]
+        res = dict(common, value=edges / secs, kind="reference", seconds=secs,
+                   sample=sample + "; reference insertDataset + markContainedReads + insertAllEdgesOfRead loop "
+                                   "(oracle/_ref/ref_harness disc: the GPU step's work), 1 thread",
+                   reads_per_sec=od.num_unique / secs)
+        if full is not None:
+            fs = full["hash_s"] + full["graph_s"]
+            res["full_build_edges_per_sec"] = edges / fs
+            res["full_build_seconds"] = fs
+        return res
     secs = th + td
-    return {"value": edges / secs, "unit": "edges/s", "cores": 1, "kind": "port",
-            "sample": sample + "; oracle C restatement index + discovery", "seconds": secs, "edges": edges,
-            "reads_per_sec": od.num_unique / secs}
+    return dict(common, value=edges / secs, kind="port", seconds=secs,
+                sample=sample + "; oracle C restatement index + containment + discovery, 1 thread",
+                reads_per_sec=od.num_unique / secs)
+
+
+def combine_digests(ds):
+    out = {"n": 0, "sum": 0, "xor": 0, "sum2": 0}
+    for d in ds:
+        out = {"n": out["n"] + d["n"], "sum": (out["sum"] + d["sum"]) % 2**64, "xor": out["xor"] ^ d["xor"],
+               "sum2": (out["sum2"] + d["sum2"]) % 2**64}
+    return out
+
+
+def parity_digest(engines, last, mode, dist, config):
+    """Digests (include/mg_overlap.h mg_rows_digest / mg_super_digest) of the
+    last step's rows and superReadIDs, computed on the device, combined over
+    the ranks, and compared with the reference's own digest of the same
+    workload (tests/golden/<config>.json, made by oracle/_ref/ref_harness)."""
+    import torch
+
+    if mode.startswith("exchange"):
+        rows = [e.rows_digest(buf.data_ptr(), n) for e, (buf, n) in zip(engines, last.rows)]
+    else:
+        rows = [e.rows_digest() for e in engines]
+    sup = engines[0].super_digest() if engines else {"n": 0, "sum": 0, "xor": 0, "sum2": 0}
+    rd = combine_digests(rows)
+    if dist is not None:  # gather every rank's rows digest (xor does not all-reduce)
+        mine = torch.tensor([rd[k] - (2**64 if rd[k] >= 2**63 else 0) for k in ("n", "sum", "xor", "sum2")],
+                            dtype=torch.int64)
+        dev = "cpu" if dist.get_backend() == "gloo" else "cuda"
+        allv = [torch.zeros(4, dtype=torch.int64, device=dev) for _ in range(dist.get_world_size())]
+        dist.all_gather(allv, mine.to(dev))
+        rd = combine_digests([{k: int(v) % 2**64 for k, v in zip(("n", "sum", "xor", "sum2"), t.cpu().tolist())}
+                              for t in allv])
+    out = {"rows": rd, "super": sup}
+    path = GOLDEN_DIGEST.format(config)
+    if os.path.exists(path):
+        g = json.load(open(path))
+        out["golden"] = os.path.relpath(path, ROOT)
+        out["digest_ok"] = bool(g["rows"] == rd and g["super"] == sup)
+    else:
+        out["golden"] = None
+        out["digest_ok"] = None
+    return out
 
 
 def load_pmc(path):
@@ -163,7 +233,8 @@ def main():
                     help="N > 1 (and --sim-world): replicated = every rank builds the whole index and probes its "
                          "source-read range, no data-path collective (SURVEY 8(e)(ii)); exchange = bucket-range "
                          "index shards + RCCL all-to-all of keys, runs and rows (SURVEY 8(e) main design)")
-    ap.add_argument("--cpu-sample", type=int, default=150_000)
+    ap.add_argument("--cpu-sample", type=int, default=200_000)
+    ap.add_argument("--no-cpu-full", action="store_true", help="skip the reference's full-build timing")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-ingest", action="store_true", help="skip the device Dataset ingest measurement")
     ap.add_argument("--replay", action="store_true",
@@ -271,11 +342,13 @@ def main():
                 rank_ms[i] += (time.perf_counter() - ta) * 1e3
             return tot
         res = sharded_step(engines, xchg, l, k)
+        last_res[0] = res
         for kk, v in res.ms.items():
             phase_ms[kk] = phase_ms.get(kk, 0.0) + v
         return sum(nr for _, nr in res.rows)
 
     phase_ms = {}
+    last_res = [None]
 
     def sync_barrier():
         torch.cuda.synchronize(local)
@@ -328,6 +401,9 @@ def main():
         dist.all_reduce(ee, op=dist.ReduceOp.SUM)
         rows = int(ee.item())
     edges = rows // 2
+    # parity at the bench's own size: device digests of the last step vs the
+    # reference's digests of the same workload (outside the timed region)
+    parity = parity_digest(engines, last_res[0], mode, dist, args.config)
     if rank != 0:
         dist.barrier()
         dist.destroy_process_group()
@@ -390,6 +466,7 @@ def main():
         "phase_wall_ms": {kk: v / args.steps for kk, v in phase_ms.items()} or None,
         "counters": cnt,
         "roofline": roof,
+        "parity": parity,
     }
     if sim_rank_ms is not None:
         res["sim_rank_ms"] = sim_rank_ms
@@ -413,7 +490,7 @@ def main():
             res["dataset_ingest"] = {"error": str(e)}
     if world == 1 and mode == "fused" and not args.no_cpu_baseline:
         try:
-            res["cpu_baseline"] = cpu_baseline(cfg, args.cpu_sample)
+            res["cpu_baseline"] = cpu_baseline(cfg, args.cpu_sample, not args.no_cpu_full)
         except Exception as e:  # report, never fake
             res["cpu_baseline"] = {"value": None, "error": str(e)}
     print(json.dumps(res), flush=True)

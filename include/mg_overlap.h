@@ -189,6 +189,23 @@ int mg_pack(mg_ctx* ctx, int what, void* dst, uint64_t cap);
 int mg_begin_contained(mg_ctx* ctx, void* superkey, int* needed);
 int mg_finalize_contained(mg_ctx* ctx, uint32_t* super_out);
 
+/* --- parity digests (no reference counterpart: test/bench support) ----------
+ * Order-independent digests of the directed edge multiset and of the
+ * superReadID vector, computed on the device, so that a 10^8-row result is
+ * compared with the reference's (oracle/_ref/ref_harness digest) without a
+ * multi-GB download.  out[4] = {count, sum h, xor h, sum mix64(h ^ SALT)}
+ * mod 2^64, with mix64 the bijective finaliser (x ^= x>>31; x *= 0x7fb5d329728ea185;
+ * x ^= x>>27; x *= 0x81dadef4bc2dd44d; x ^= x>>33), SALT = 0xD6E8FEB86659FD93 and
+ *   row (u, v, orient, offset): h = mix64(((u << 32) | v) ^ mix64(((orient << 16) | offset)
+ *                                   + 0x9E3779B97F4A7C15))
+ *   contained read id:          h = mix64((id << 32) | superReadID)
+ * Digests of disjoint parts combine by adding count/sum/sum2 and xor-ing xor.
+ * mg_rows_digest: rows = NULL digests the context's rows of the last
+ * mg_find_overlaps / mg_probe_runs; else `rows` is a device array of n_rows
+ * mg_edge records (e.g. an exchange-mode receive buffer). */
+int mg_rows_digest(mg_ctx* ctx, const void* rows, uint64_t n_rows, uint64_t* out);
+int mg_super_digest(mg_ctx* ctx, uint64_t* out);
+
 /* --- diagnostics ----------------------------------------------------------- */
 int mg_get_timings(const mg_ctx* ctx, mg_timings* t);
 int mg_get_counters(const mg_ctx* ctx, mg_counters* c);

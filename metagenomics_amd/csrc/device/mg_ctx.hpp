@@ -42,6 +42,7 @@ struct mg_ctx {
   unsigned long long* superkey = nullptr;  // the containment key array in use (d_superkey or caller-owned)
   uint32_t* d_super = nullptr;
   unsigned int* d_any = nullptr;
+  unsigned long long* d_digest = nullptr;  // mg_rows_digest / mg_super_digest accumulators (4 u64)
   size_t super_cap = 0;
   bool contained_done = false, super_any = false;
   // rows

@@ -1569,6 +1569,70 @@ __global__ __launch_bounds__(kBlock) void k_super_finalize(const unsigned long l
     atomicOr(any, 1u);
 }
 
+// Order-independent digests (include/mg_overlap.h, mg_rows_digest): per row
+// h = mix64(((src << 32) | dst) ^ mix64(((orient << 16) | offset) + GOLD));
+// accumulators {n, sum h, xor h, sum mix64(h ^ SALT)} mod 2^64.  The rows are
+// either per-wavefront regions (cnt != nullptr: region r holds cnt[r] rows at
+// r * cap) or one flat array of `flat_n` rows; super: g = mix64((id << 32) | sup)
+// over contained reads.  One wavefront reduction and 4 atomics per wavefront.
+constexpr uint64_t kDigestGold = 0x9E3779B97F4A7C15ULL, kDigestSalt = 0xD6E8FEB86659FD93ULL;
+
+__device__ __forceinline__ void digest_flush(unsigned long long* acc, uint64_t n, uint64_t s, uint64_t x, uint64_t s2) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) {
+    n += __shfl_xor(n, d);
+    s += __shfl_xor(s, d);
+    x ^= __shfl_xor(x, d);
+    s2 += __shfl_xor(s2, d);
+  }
+  if ((threadIdx.x & 63) == 0 && n) {
+    atomicAdd(&acc[0], (unsigned long long)n);
+    atomicAdd(&acc[1], (unsigned long long)s);
+    atomicXor(&acc[2], (unsigned long long)x);
+    atomicAdd(&acc[3], (unsigned long long)s2);
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_rows_digest(const uint32_t* __restrict__ rows, uint64_t cap,
+                                                        const unsigned long long* __restrict__ cnt, uint64_t nreg,
+                                                        uint64_t flat_n, unsigned long long* acc) {
+  uint64_t n = 0, s = 0, x = 0, s2 = 0;
+  auto add = [&](const uint32_t* r) {
+    const uint64_t k2 = (uint64_t)r[2];  // orient << 16 | offset
+    const uint64_t hv = mix64((((uint64_t)r[0] << 32) | r[1]) ^ mix64(k2 + kDigestGold));
+    n += 1;
+    s += hv;
+    x ^= hv;
+    s2 += mix64(hv ^ kDigestSalt);
+  };
+  if (cnt) {
+    for (uint64_t reg = blockIdx.x; reg < nreg; reg += gridDim.x) {
+      const uint64_t c = cnt[reg] < cap ? cnt[reg] : cap;
+      for (uint64_t i = threadIdx.x; i < c; i += kBlock) add(rows + (reg * cap + i) * 3);
+    }
+  } else {
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < flat_n; i += (uint64_t)gridDim.x * kBlock)
+      add(rows + i * 3);
+  }
+  digest_flush(acc, n, s, x, s2);
+}
+
+__global__ __launch_bounds__(kBlock) void k_super_digest(const uint32_t* __restrict__ super, uint64_t n_reads,
+                                                         unsigned long long* acc) {
+  uint64_t n = 0, s = 0, x = 0, s2 = 0;
+  for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n_reads; i += (uint64_t)gridDim.x * kBlock) {
+    const uint32_t sp = super[i];
+    if (sp) {
+      const uint64_t g = mix64(((i + 1) << 32) | sp);
+      n += 1;
+      s += g;
+      x ^= g;
+      s2 += mix64(g ^ kDigestSalt);
+    }
+  }
+  digest_flush(acc, n, s, x, s2);
+}
+
 // getListOfReads(key) (HashTable.cpp:202-221): walk the query key's home cell
 // chain and keep entries whose key string equals it exactly.
 template <int MAXW>
@@ -2124,7 +2188,8 @@ void mg_destroy(mg_ctx* ctx) {
                   ctx->d_superkey, ctx->d_super, ctx->d_any, ctx->d_rows, ctx->d_seg, ctx->d_stats,
                   ctx->d_compact, ctx->d_runs, ctx->d_run_cnt, ctx->d_keyrec, ctx->d_blk, ctx->d_flat_cnt, ctx->d_cand, ctx->d_cand_cnt, ctx->d_freq,
                   ctx->d_sk[0], ctx->d_sk[1], ctx->d_sm[0], ctx->d_sm[1], ctx->d_sort_tmp, ctx->d_run_off,
-                  ctx->d_flat_cursor, ctx->d_kb[0], ctx->d_kb[1], ctx->d_ke[0], ctx->d_ke[1], ctx->d_key0, ctx->d_holes};
+                  ctx->d_flat_cursor, ctx->d_kb[0], ctx->d_kb[1], ctx->d_ke[0], ctx->d_ke[1], ctx->d_key0, ctx->d_holes,
+                  ctx->d_digest};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   for (auto& e : ctx->ev)
@@ -2202,10 +2267,19 @@ int mg_upload_reads_ascii(mg_ctx* ctx, const char* concat, const uint64_t* offse
   ctx->maxw = maxw;
   ctx->stride = slot_words((int)maxw);
   const uint64_t total = n_reads ? offsets[n_reads] : 0;
-  char* d_ascii = nullptr;
-  uint64_t* d_off = nullptr;
-  MG_TRY(hipMalloc(&d_ascii, std::max<uint64_t>(total, 1)));
-  MG_TRY(hipMalloc(&d_off, (n_reads + 1) * sizeof(uint64_t)));
+  // staging buffers freed on every exit path (an error return included)
+  struct Staging {
+    char* ascii = nullptr;
+    uint64_t* off = nullptr;
+    ~Staging() {
+      if (ascii) (void)hipFree(ascii);
+      if (off) (void)hipFree(off);
+    }
+  } st;
+  MG_TRY(hipMalloc(&st.ascii, std::max<uint64_t>(total, 1)));
+  MG_TRY(hipMalloc(&st.off, (n_reads + 1) * sizeof(uint64_t)));
+  char* const d_ascii = st.ascii;
+  uint64_t* const d_off = st.off;
   const size_t nw = (size_t)(n_reads + 2) * ctx->stride + 2;
   MG_TRY(ensure(&ctx->d_words, &ctx->words_cap, nw));
   MG_TRY(ensure(&ctx->d_len, &ctx->len_cap, n_reads + 1));
@@ -2222,8 +2296,6 @@ int mg_upload_reads_ascii(mg_ctx* ctx, const char* concat, const uint64_t* offse
   MG_TRY(hipEventRecord(ctx->ev[1], ctx->stream));
   MG_TRY(hipStreamSynchronize(ctx->stream));
   ctx->t.pack_ms = elapsed(ctx->ev[0], ctx->ev[1]);
-  (void)hipFree(d_ascii);
-  (void)hipFree(d_off);
   return finish_upload(ctx, lens.data());
 }
 
@@ -3152,6 +3224,50 @@ int mg_lookup_key(mg_ctx* ctx, const char* key, uint32_t key_len, uint64_t* out,
   for (uint64_t i = 0; i < res.size() && i < cap; i++) out[i] = res[i];
   if (n_out) *n_out = n;
   return 0;
+}
+
+static int digest_begin(mg_ctx* ctx) {
+  if (!ctx->d_digest) MG_TRY(hipMalloc(&ctx->d_digest, 4 * sizeof(unsigned long long)));
+  MG_TRY(hipMemsetAsync(ctx->d_digest, 0, 4 * sizeof(unsigned long long), ctx->stream));
+  return 0;
+}
+
+static int digest_end(mg_ctx* ctx, uint64_t* out) {
+  MG_TRY(hipGetLastError());
+  unsigned long long h[4];
+  MG_TRY(hipMemcpyAsync(h, ctx->d_digest, sizeof(h), hipMemcpyDeviceToHost, ctx->stream));
+  MG_TRY(hipStreamSynchronize(ctx->stream));
+  for (int i = 0; i < 4; ++i) out[i] = h[i];
+  return 0;
+}
+
+int mg_rows_digest(mg_ctx* ctx, const void* rows, uint64_t n_rows, uint64_t* out) {
+  if (!ctx || !out) return -1;
+  MG_TRY(hipSetDevice(ctx->device));
+  if (digest_begin(ctx)) return -1;
+  const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(4096, ((uint64_t)ctx->n_cu) * 8));
+  if (rows) {
+    if (n_rows)
+      hipLaunchKernelGGL(k_rows_digest, dim3(grid), dim3(kBlock), 0, ctx->stream,
+                         reinterpret_cast<const uint32_t*>(rows), (uint64_t)0, nullptr, (uint64_t)0, n_rows,
+                         ctx->d_digest);
+  } else if (ctx->nreg && ctx->n_rows) {
+    hipLaunchKernelGGL(k_rows_digest, dim3(grid), dim3(kBlock), 0, ctx->stream, ctx->d_rows,
+                       ctx->rows_cap / ctx->nreg, ctx->d_seg, ctx->nreg, (uint64_t)0, ctx->d_digest);
+  }
+  return digest_end(ctx, out);
+}
+
+int mg_super_digest(mg_ctx* ctx, uint64_t* out) {
+  if (!ctx || !out) return -1;
+  MG_TRY(hipSetDevice(ctx->device));
+  if (!ctx->contained_done) return set_err(ctx, "mg_mark_contained must run first");
+  if (digest_begin(ctx)) return -1;
+  if (ctx->super_any && ctx->n) {
+    const uint32_t grid = (uint32_t)std::min<uint64_t>(4096, (ctx->n + kBlock - 1) / kBlock);
+    hipLaunchKernelGGL(k_super_digest, dim3(grid), dim3(kBlock), 0, ctx->stream, ctx->d_super, ctx->n, ctx->d_digest);
+  }
+  return digest_end(ctx, out);
 }
 
 int mg_get_timings(const mg_ctx* ctx, mg_timings* t) {

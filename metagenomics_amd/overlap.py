@@ -92,6 +92,8 @@ def lib() -> C.CDLL:
         "mg_pack": (i32, [vp, i32, vp, u64]),
         "mg_begin_contained": (i32, [vp, vp, P(i32)]),
         "mg_finalize_contained": (i32, [vp, vp]),
+        "mg_rows_digest": (i32, [vp, vp, u64, vp]),
+        "mg_super_digest": (i32, [vp, vp]),
         "mgh_dataset_from_files": (i32, [P(C.c_char_p), i32, u64, P(vp)]),
         "mgh_dataset_from_codes": (i32, [vp, u64, u64, vp, u64, i32, P(vp)]),
         "mgh_dataset_free": (None, [vp]),
@@ -431,6 +433,22 @@ class OverlapEngine:
         sup = np.zeros(self.n_reads + 1, dtype=np.uint32)
         self._check(lib().mg_finalize_contained(self._h, _ptr(sup)), "finalize_contained")
         return sup
+
+    # --- parity digests (include/mg_overlap.h; tests/digest.py restates them)
+    @staticmethod
+    def _digest(a: np.ndarray) -> dict:
+        return {"n": int(a[0]), "sum": int(a[1]), "xor": int(a[2]), "sum2": int(a[3])}
+
+    def rows_digest(self, dptr: int | None = None, n: int = 0) -> dict:
+        """Digest of the context's rows (dptr None) or of n mg_edge rows at device pointer dptr."""
+        out = np.zeros(4, dtype=np.uint64)
+        self._check(lib().mg_rows_digest(self._h, C.c_void_p(dptr or 0), n, _ptr(out)), "rows_digest")
+        return self._digest(out)
+
+    def super_digest(self) -> dict:
+        out = np.zeros(4, dtype=np.uint64)
+        self._check(lib().mg_super_digest(self._h, _ptr(out)), "super_digest")
+        return self._digest(out)
 
     def timings(self) -> dict:
         t = _Timings()

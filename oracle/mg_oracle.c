@@ -7,6 +7,7 @@
  */
 #define _POSIX_C_SOURCE 199309L
 #include "mg_oracle.h"
+#include "mg_digest.h"
 
 #include <ctype.h>
 #include <stdio.h>
@@ -431,3 +432,24 @@ uint64_t mgo_lookup(mgo_dataset* ds, uint64_t min_overlap, const char* key, uint
 }
 
 void mgo_free(void* p) { free(p); }
+
+/* Digests of oracle/mg_digest.h over rows / a superReadID vector (the
+ * checker's side of mg_rows_digest / mg_super_digest). */
+void mgo_rows_digest(const mgo_row* rows, uint64_t n, uint64_t* out) {
+  mgo_digest d = {0, 0, 0, 0};
+  for (uint64_t i = 0; i < n; i++) mgo_digest_add(&d, mgo_row_hash(rows[i].src, rows[i].dst, rows[i].orient, rows[i].offset));
+  out[0] = d.n;
+  out[1] = d.sum;
+  out[2] = d.xr;
+  out[3] = d.sum2;
+}
+
+void mgo_super_digest(const uint64_t* super, uint64_t n_unique, uint64_t* out) {
+  mgo_digest d = {0, 0, 0, 0};
+  for (uint64_t i = 1; i <= n_unique; i++)
+    if (super[i]) mgo_digest_add(&d, mgo_super_hash(i, super[i]));
+  out[0] = d.n;
+  out[1] = d.sum;
+  out[2] = d.xr;
+  out[3] = d.sum2;
+}

@@ -57,6 +57,10 @@ uint64_t mgo_lookup(mgo_dataset* ds, uint64_t min_overlap, const char* key, uint
 
 void mgo_free(void* p);
 
+/* Order-independent digests (oracle/mg_digest.h): out[4] = {n, sum, xor, sum2}. */
+void mgo_rows_digest(const mgo_row* rows, uint64_t n, uint64_t* out);
+void mgo_super_digest(const uint64_t* super, uint64_t n_unique, uint64_t* out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -50,6 +50,8 @@ def lib():
         L.mgo_lookup.restype = u64
         L.mgo_lookup.argtypes = [vp, u64, C.c_char_p, vp, u64]
         L.mgo_free.argtypes = [vp]
+        L.mgo_rows_digest.argtypes = [vp, u64, vp]
+        L.mgo_super_digest.argtypes = [vp, u64, vp]
         _lib = L
     return _lib
 
@@ -115,6 +117,21 @@ class OracleDataset:
         out = np.zeros(1 << 16, dtype=np.uint64)
         n = lib().mgo_lookup(self._h, l, key.encode(), C.c_void_p(out.ctypes.data), out.shape[0])
         return [(int(x & ((1 << 62) - 1)), int(x >> 62)) for x in out[: min(n, out.shape[0])]]
+
+
+def rows_digest(rows) -> dict:
+    """oracle/mg_digest.h over a ROW_DTYPE array (C)."""
+    rows = np.ascontiguousarray(rows, dtype=ROW_DTYPE)
+    out = np.zeros(4, dtype=np.uint64)
+    lib().mgo_rows_digest(C.c_void_p(rows.ctypes.data), rows.shape[0], C.c_void_p(out.ctypes.data))
+    return {"n": int(out[0]), "sum": int(out[1]), "xor": int(out[2]), "sum2": int(out[3])}
+
+
+def super_digest(sup) -> dict:
+    sup = np.ascontiguousarray(sup, dtype=np.uint64)
+    out = np.zeros(4, dtype=np.uint64)
+    lib().mgo_super_digest(C.c_void_p(sup.ctypes.data), max(0, sup.shape[0] - 1), C.c_void_p(out.ctypes.data))
+    return {"n": int(out[0]), "sum": int(out[1]), "xor": int(out[2]), "sum2": int(out[3])}
 
 
 def sorted_tuples(rows) -> np.ndarray:

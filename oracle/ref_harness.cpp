@@ -21,6 +21,16 @@
 //        the ID-order discovery loop (no transitive reduction), plus the raw
 //        directed edge count.  This is the apples-to-apples CPU figure for the
 //        GPU path, which also stops at the raw edge multiset.
+//   digest <fasta> <l> <out>   : as edges, but instead of dumping the rows it
+//        folds every directed Edge of graph[u] into the order-independent
+//        digest of oracle/mg_digest.h as soon as u is explored (graph[u] is
+//        final then: later reads skip explored partners, :546) and frees it, so
+//        10^8-row configs (C3) fit in host memory.  Writes one JSON line with
+//        the row digest, the superReadID digest and the phase times.
+//   hash   <fasta> <l> <out>   : HashTable::getHashTableSize() and
+//        hashFunction(key) (HashTable.cpp:20-29,56,135-155) for the four keys
+//        of the first 64 reads (hashRead's order, :88-104): "#P <size>" then
+//        "<key> <hash>" lines.
 //   lookup <fasta> <l> <out> <key>... : HashTable::getListOfReads(key)
 //        (HashTable.cpp:202-221) for each key, in the reference list order.
 //   bfs    <fasta> <l> <out>   : the graph as buildOverlapGraphFromHashTable
@@ -54,6 +64,8 @@
 
 #include <time.h>
 #include <cstdio>
+
+#include "mg_digest.h"
 #include <cstring>
 
 static double now_s() {
@@ -188,6 +200,54 @@ int main(int argc, char** argv) {
     for (UINT64 u = 1; u <= N; u++) rows += og->graph->at(u)->size();
     fprintf(out, "{\"n_unique\": %llu, \"dataset_s\": %.6f, \"hash_s\": %.6f, \"discovery_s\": %.6f, \"directed_rows\": %llu}\n",
             (unsigned long long)N, t_ds, t2 - t1, t3 - t2, rows);
+  } else if (!strcmp(mode, "digest")) {
+    double t1 = now_s();
+    HashTable* ht = new HashTable();
+    ht->insertDataset(ds, l);
+    double t2 = now_s();
+    OverlapGraph* og = prepare_graph(ds, ht);
+    og->markContainedReads();
+    double t3 = now_s();
+    mgo_digest sd = {0, 0, 0, 0}, rd = {0, 0, 0, 0};
+    for (UINT64 i = 1; i <= N; i++) {
+      Read* r = ds->getReadFromID(i);
+      if (r->superReadID) mgo_digest_add(&sd, mgo_super_hash(i, r->superReadID));
+    }
+    vector<nodeType> explored(N + 1, UNEXPLORED);
+    for (UINT64 u = 1; u <= N; u++) {
+      og->insertAllEdgesOfRead(u, &explored);
+      explored[u] = EXPLORED;
+      vector<Edge*>* lst = og->graph->at(u);
+      for (size_t k = 0; k < lst->size(); k++) {
+        Edge* e = lst->at(k);
+        mgo_digest_add(&rd, mgo_row_hash(u, e->getDestinationRead()->getReadNumber(), e->getOrientation(),
+                                         e->getOverlapOffset()));
+        delete e;  // its twin (in an unexplored list) is never dereferenced again
+      }
+      vector<Edge*>().swap(*lst);
+    }
+    double t4 = now_s();
+    fprintf(out,
+            "{\"n_unique\": %llu, \"n_reads\": %llu, \"directed_rows\": %llu, \"rows_sum\": %llu, "
+            "\"rows_xor\": %llu, \"rows_sum2\": %llu, \"contained\": %llu, \"super_sum\": %llu, "
+            "\"super_xor\": %llu, \"super_sum2\": %llu, \"dataset_s\": %.3f, \"hash_s\": %.3f, "
+            "\"contain_s\": %.3f, \"discovery_s\": %.3f}\n",
+            (unsigned long long)N, (unsigned long long)ds->getNumberOfReads(), (unsigned long long)rd.n,
+            (unsigned long long)rd.sum, (unsigned long long)rd.xr, (unsigned long long)rd.sum2,
+            (unsigned long long)sd.n, (unsigned long long)sd.sum, (unsigned long long)sd.xr,
+            (unsigned long long)sd.sum2, t_ds, t2 - t1, t3 - t2, t4 - t3);
+  } else if (!strcmp(mode, "hash")) {
+    HashTable* ht = new HashTable();
+    ht->insertDataset(ds, l);
+    fprintf(out, "#P %llu\n", (unsigned long long)ht->getHashTableSize());
+    const UINT64 h = ht->getHashStringLength();
+    for (UINT64 i = 1; i <= N && i <= 64; i++) {
+      Read* r = ds->getReadFromID(i);
+      const string f = r->getStringForward(), b = r->getStringReverse();
+      const string keys[4] = {f.substr(0, h), f.substr(f.length() - h, h), b.substr(0, h), b.substr(b.length() - h, h)};
+      for (int o = 0; o < 4; o++)
+        fprintf(out, "%s %llu\n", keys[o].c_str(), (unsigned long long)ht->hashFunction(keys[o]));
+    }
   } else if (!strcmp(mode, "edges")) {
     HashTable* ht = new HashTable();
     ht->insertDataset(ds, l);

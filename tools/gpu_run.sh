@@ -34,9 +34,9 @@ for s in $STEPS; do
   xchg1)
     timeout -k 10 300 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29511 bench.py --exchange --steps 3 --no-cpu-baseline > $OUT/bench_xchg1.json 2> $OUT/bench_xchg1.err
     rc=$?; echo "bench exchange(RCCL, 1 rank) rc=$rc"; cat $OUT/bench_xchg1.json ;;
-  xdebug)
-    timeout -k 10 300 python -u tools/xchg_debug.py > $OUT/xchg_debug.log 2>&1
-    rc=$?; echo "xchg_debug rc=$rc"; grep -v Warn $OUT/xchg_debug.log | tail -30 ;;
+  digest)
+    timeout -k 10 600 python -u -m pytest tests/test_scale_digest.py -x -v -m gpu --timeout 300 --timeout-method thread > $OUT/digest_tests.log 2>&1
+    rc=$?; echo "digest tests rc=$rc"; grep -E "PASS|FAIL|SKIP|Error" $OUT/digest_tests.log | tail -12 ;;
   a2a)
     timeout -k 10 300 python -u tools/a2a_probe.py > $OUT/a2a_probe.log 2>&1
     rc=$?; echo "a2a_probe rc=$rc"; grep MB $OUT/a2a_probe.log ;;
@@ -64,6 +64,9 @@ for s in $STEPS; do
   benchc2)
     timeout -k 10 300 python -u bench.py --config c2 --no-cpu-baseline > $OUT/bench_c2.json 2> $OUT/bench_c2.err
     rc=$?; echo "bench c2 rc=$rc"; cat $OUT/bench_c2.json ;;
+  benchc5s)
+    timeout -k 10 300 python -u bench.py --config c5s --no-cpu-baseline --no-ingest > $OUT/bench_c5s.json 2> $OUT/bench_c5s.err
+    rc=$?; echo "bench c5s rc=$rc"; cat $OUT/bench_c5s.json ;;
   prof)
     timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o kt -- python3 bench.py --steps 5 --no-cpu-baseline > $OUT/prof_bench.json 2> $OUT/prof_bench.err
     rc=$?; echo "prof rc=$rc"; cat $OUT/prof_bench.json; head -8 $OUT/prof/kt_kernel_stats.csv | cut -c1-200 ;;
