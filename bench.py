@@ -369,8 +369,8 @@ def main():
     for _ in range(args.warmup):
         step()
 
-    dev_ms = {"index_ms": 0.0, "contained_ms": 0.0, "overlap_ms": 0.0, "scan_ms": 0.0, "probe_ms": 0.0,
-              "verify_ms": 0.0, "total_ms": 0.0}
+    dev_ms = {"index_ms": 0.0, "contained_ms": 0.0, "overlap_ms": 0.0, "scan_ms": 0.0, "sort_ms": 0.0,
+              "probe_ms": 0.0, "verify_ms": 0.0, "total_ms": 0.0}
     phase_ms.clear()
     rank_ms[:] = [0.0] * len(engines)
     sync_barrier()

@@ -48,7 +48,7 @@ typedef struct mg_timings {
   float contained_ms;   /* markContainedReads equivalent (0 if skipped) */
   float overlap_ms;     /* discovery = scan + probe (insertAllEdgesOfRead) */
   float total_ms;       /* device wall of index + contained + overlap */
-  float scan_ms;        /* minimizer-run scan kernel (0: fused into index_ms) */
+  float scan_ms;        /* minimizer-run scan kernel (unsharded: the index-building scan, part of index_ms) */
   float probe_ms;       /* probe kernel (fused path: probe + verify) */
   float verify_ms;      /* verify kernel of the split path (0 fused) */
   float upload_ms;      /* H2D copy of raw reads (mg_ingest_*)        */

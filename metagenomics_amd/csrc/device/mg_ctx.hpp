@@ -87,6 +87,7 @@ struct mg_ctx {
   // its runs then serve the containment and the discovery probes
   int scan_state = 0;        // 0 none, 1 launched (not settled), 2 settled
   bool overlap_scan = true;  // option "overlap_scan" (0: separate index build, a scan per probe pass)
+  bool scan_reg = false;     // option "scan_reg": register sliding minimum (k_scan_reg) when w <= 32
   // split probe (k_probe<SPLIT> + k_verify)
   bool split = false;  // option "split": k_probe<SPLIT> + k_verify instead of the fused probe
   uint3* d_cand = nullptr;
@@ -135,6 +136,7 @@ struct mg_ctx {
   uint64_t* d_ke[2] = {nullptr, nullptr};
   size_t kb_cap = 0, ke_cap = 0, kb1_cap = 0, ke1_cap = 0;
   float keysort_ms = 0.f;
+  float shared_scan_ms = 0.f;  // k_scan<INDEX> kernel time of the last mg_build_index
   mg_timings t{};
   // Dataset ingest on the device (mg_ingest_*): frequency of each unique read
   uint32_t* d_freq = nullptr;

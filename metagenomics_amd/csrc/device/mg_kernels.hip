@@ -142,6 +142,7 @@ __global__ __launch_bounds__(kBlock) void k_pack_ascii(const char* __restrict__ 
 // and line together and follows the chain only while count > kCell.
 constexpr int kCell = 8;
 constexpr int kScanBuf = 3 * 64;  // staged run metas per scan wavefront (two puts per step: < 64 + 128)
+constexpr int kStageRing = 512;   // register scan: LDS ring of staged run metas per wavefront
 constexpr uint64_t kEmpty = ~0ULL;       // free slot (a read index is never 0xFFFFFFFF)
 constexpr uint64_t kChain = 1ULL << 63;  // on a cell's last slot: the chain continues in the next cell
 constexpr uint32_t kFpMask = (1u << kFpBits) - 1;
@@ -776,6 +777,290 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) voi
     }
   }
   if (lane == 0) p.run_cnt[gw] = cursor;
+}
+
+// ---------------------------------------------------------------------------
+// Run staging of the register scan: runs are staged in an LDS ring of 64-bit
+// metas (ballot + mbcnt), then flushed 64 at a time with every lane busy: the
+// minimizer m-mer is re-extracted from the owner lane's registers
+// (ds_bpermute), hashed (mix64 -> bucket | fingerprint) and written as one
+// coalesced record per lane, either into this wavefront's region (16-B
+// records) or into the flat SoA arrays of the bucket sort (chunks of
+// kFlatChunk records claimed from kFlatCounters counters).
+template <int MAXW>
+struct RunStage {
+  const ScanParams& p;
+  uint64_t* s_buf;
+  ulonglong2* region;
+  int lane, msh;
+  uint64_t nbmask;
+  uint64_t cursor = 0;
+  uint32_t head = 0, nbuf = 0;              // staged metas: ring [head, head + nbuf) (wavefront-uniform)
+  uint64_t fbase = 0, fused = 0, fcap = 0;  // flat output: chunk base, used, size
+
+  __device__ RunStage(const ScanParams& pp, uint64_t* buf, ulonglong2* reg, int ln)
+      : p(pp), s_buf(buf), region(reg), lane(ln), msh(64 - 2 * pp.m), nbmask((1ULL << pp.nb_log2) - 1) {}
+
+  __device__ __forceinline__ void put(bool flag, uint64_t meta) {
+    const uint64_t bal = __ballot(flag);
+    if (flag) s_buf[(head + nbuf + lane_prefix(bal)) & (kStageRing - 1)] = meta;
+    nbuf += (uint32_t)__popcll(bal);
+  }
+
+  // hash + write the first k (<= 64) staged runs; rw = this lane's read words,
+  // a0 = read index of lane 0 (every staged run belongs to a lane of the group)
+  __device__ void flush(uint32_t k, const uint64_t* rw, uint64_t a0) {
+    wave_sync();
+    bool flag = (uint32_t)lane < k;
+    uint64_t v = 0, meta = 0;
+    if (flag) meta = s_buf[(head + lane) & (kStageRing - 1)];
+    if constexpr (MAXW <= 8) {
+      const int pos = (int)((meta >> 32) & 1023u), wi = pos >> 5;
+      const int src = flag ? (int)((uint32_t)meta - (uint32_t)a0) : lane;
+      uint64_t w0 = 0, w1 = 0;
+#pragma unroll
+      for (int kk = 0; kk <= MAXW; ++kk) {
+        const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute(src << 2, (int)(uint32_t)rw[kk]);
+        const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_bpermute(src << 2, (int)(uint32_t)(rw[kk] >> 32));
+        const uint64_t x = ((uint64_t)hi << 32) | lo;
+        w0 = wi == kk ? x : w0;
+        w1 = wi + 1 == kk ? x : w1;
+      }
+      if (flag) v = mix64(funnel(w0, w1, (pos & 31) << 1) >> msh);
+    } else if (flag) {
+      const uint64_t* g2 = p.words + (meta & 0xFFFFFFFFull) * slot_words(MAXW);
+      const int pos = (int)((meta >> 32) & 1023u);
+      v = mix64(funnel(g2[pos >> 5], g2[(pos >> 5) + 1], (pos & 31) << 1) >> msh);
+    }
+    if (flag) flag = owned(v & nbmask, p.nb_log2, p.rank, p.nranks);
+    const uint64_t bal = __ballot(flag);
+    if (p.flat_keys) {
+      const uint64_t npop = (uint64_t)__popcll(bal);
+      const uint64_t room = fcap - fused;
+      unsigned long long nbase = 0;
+      if (npop > room) {  // chunk ids x, x + 8, ... belong to counter x = blockIdx % 8
+        const uint32_t x = blockIdx.x & (kFlatCounters - 1);
+        if (lane == 0) nbase = (atomicAdd(&p.flat_cursor[x], 1ull) * kFlatCounters + x) * kFlatChunk;
+        nbase = __shfl(nbase, 0);
+      }
+      if (flag) {
+        const uint64_t pr = lane_prefix(bal);
+        const uint64_t at = pr < room ? fbase + fused + pr : nbase + (pr - room);
+        if (at < p.flat_cap) {
+          if (p.pack_a) {
+            reinterpret_cast<uint32_t*>(p.flat_keys)[at] = run_pack_key(v, p.nb_log2);
+            p.flat_meta[at] = run_pack_meta(meta, v, p.nb_log2, p.pack_a, p.pack_w);
+          } else {
+            p.flat_keys[at] = v;
+            p.flat_meta[at] = meta;
+          }
+        }
+      }
+      if (npop > room) {
+        fbase = nbase;
+        fused = npop - room;
+        fcap = kFlatChunk;
+      } else {
+        fused += npop;
+      }
+    } else if (flag) {
+      const uint64_t at = cursor + lane_prefix(bal);
+      if (at < p.run_cap) region[at] = make_ulonglong2(v, meta);
+    }
+    cursor += (uint64_t)__popcll(bal);
+    head += k;
+    nbuf -= k;
+    wave_sync();
+  }
+
+  // unused tail of the last flat chunk (holes the sort and probe skip) and the region count
+  __device__ void finish(uint64_t gw) {
+    if (p.flat_keys) {
+      for (uint64_t i = fused + lane; i < fcap; i += kWave) {
+        const uint64_t at = fbase + i;
+        if (at < p.flat_cap) {
+          if (p.pack_a)
+            reinterpret_cast<uint32_t*>(p.flat_keys)[at] = 0xFFFFFFFFu;
+          else
+            p.flat_keys[at] = kEmpty;
+          p.flat_meta[at] = kFlatHole;
+        }
+      }
+    }
+    if (lane == 0) p.run_cnt[gw] = cursor;
+  }
+};
+
+// 32 bases of a lane's read starting at base `pos` (per-lane), from its words
+// in registers (pos >> 5 selected by a compare chain, not a register index,
+// which would go through scratch)
+template <int MAXW>
+__device__ __forceinline__ uint64_t ext_reg(const uint64_t* rw, int pos) {
+  const int wi = pos >> 5;
+  uint64_t w0 = rw[0], w1 = rw[1];
+#pragma unroll
+  for (int k = 1; k <= MAXW; ++k) {
+    w0 = wi == k ? rw[k] : w0;
+    w1 = wi + 1 == k ? rw[k] : w1;
+  }
+  if (wi + 1 > MAXW) w1 = 0;
+  return funnel(w0, w1, (pos & 31) << 1);
+}
+
+constexpr int kRegW = 32;       // largest w (= h - m + 1) of the register scan
+constexpr int kStageEvery = 6;  // register scan: flush check every kStageEvery bases (< 64 + 6 * 64 staged)
+
+// Window minimizers of every source read, one read per lane, with the sliding
+// minimum kept in REGISTERS: van Herk / Gil-Werman over blocks of w positions
+// (prefix minimum of the current block in a register, suffix minima of the
+// previous block in S[0..w), overwritten by the current block's keys exactly
+// behind the step that last reads them).  The block loop is unrolled by
+// kRegW with a uniform exit at u = w, so every S index is static and no LDS
+// or scratch is touched per base (the LDS version, k_scan, stays for w >
+// kRegW).  Same windows, keys and runs as k_scan (OverlapGraph.cpp:534-537):
+// window j covers m-mers t in [j, j + w - 1]; key = order_key | t; a run ends
+// where the minimizer position changes.
+// INDEX (HashTable::insertDataset / hashRead, HashTable.cpp:50-104): o = 0 is
+// window j = 0 and o = 1 window j = n - h of this same scan (the key's offset i
+// is t shifted by a constant, so the argmin is the same); o = 2 / 3 (the
+// reverse strand's keys) come from a w-step pass of rolled reverse-complement
+// m-mers after the read's scan; then the four CAS inserts (or key records).
+template <int MAXW, bool INDEX>
+__global__ __launch_bounds__(kBlock) void k_scan_reg(ScanParams p) {
+  extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int h = p.h, m = p.m, w = p.w;
+  const int msh = 64 - 2 * m;
+  const uint64_t mmask = (m == 32) ? ~0ULL : ((1ULL << (2 * m)) - 1);
+  const uint64_t ngroups = (p.a_hi - p.a_lo + kWave - 1) / kWave;
+  const uint64_t gw = (uint64_t)blockIdx.x * kWavesPerBlock + wv;
+  const uint64_t nw = (uint64_t)gridDim.x * kWavesPerBlock;
+  RunStage<MAXW> st(p, smem + (size_t)wv * kStageRing, p.runs + gw * p.run_cap, lane);
+
+  for (uint64_t grp = gw; grp < ngroups; grp += nw) {
+    const uint64_t a = p.a_lo + grp * kWave + lane;
+    int n = 0;
+    if (a < p.a_hi) {
+      n = (int)p.len[a];
+      if (n && p.super && p.super[a]) n = 0;
+    }
+    const int J = n - h - 1;                  // windows j = 1 .. J (:534)
+    const int tend = J >= 1 ? J + w - 1 : -1;  // last m-mer position a scanned window uses
+    const int tlast = INDEX ? (n ? n - m : -1) : tend;  // INDEX: up to window j = n - h (key o = 1)
+    int tmax = tlast;
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) tmax = max(tmax, __shfl_xor(tmax, d));
+    tmax = __builtin_amdgcn_readfirstlane(tmax);
+    uint64_t rw[MAXW + 1];
+    {
+      constexpr int kRw = MAXW + 1 <= slot_words(MAXW) ? MAXW + 1 : slot_words(MAXW);
+      const uint64_t* gs = p.words + (a < p.a_hi ? a : 0) * slot_words(MAXW);
+#pragma unroll
+      for (int k = 0; k <= MAXW; ++k) rw[k] = k < kRw ? gs[k] : 0;
+    }
+    const uint64_t a0 = p.a_lo + grp * kWave;
+    uint32_t S[kRegW + 1];
+#pragma unroll
+    for (int u = 0; u <= kRegW; ++u) S[u] = 0xFFFFFFFFu;
+    uint64_t mm = rw[0] >> msh;  // m-mer at t = 0
+    uint64_t cwd = 0;            // read word holding base t + m (refilled at word edges)
+    uint32_t pm = 0, kw0 = 0xFFFFFFFFu, kw1 = 0xFFFFFFFFu;  // prefix min; INDEX: windows j = 0 and n - h
+    int last = 0, jlo = 1;
+    const int t1 = n - m;  // this lane's key-o=1 window position (INDEX)
+    for (int t0 = 0; t0 <= tmax; t0 += w) {
+#pragma unroll
+      for (int u = 0; u < kRegW; ++u) {
+        const int t = t0 + u;
+        if (u >= w || t > tmax) continue;  // uniform; no break, so the loop unrolls fully
+        const int x = t + m;  // base rolled in after this step
+        if (t == 0 || (x & 31) == 0) {
+          const int xi = x >> 5;
+          uint64_t c = rw[0];
+#pragma unroll
+          for (int k = 1; k <= MAXW; ++k) c = xi == k ? rw[k] : c;
+          cwd = c;
+        }
+        const uint32_t key = order_key(mm) | (uint32_t)t;
+        pm = u == 0 ? key : (key < pm ? key : pm);
+        const uint32_t win = S[u + 1] < pm ? S[u + 1] : pm;  // S[w] stays all ones
+        S[u] = key;
+        if (t >= w - 1) {
+          const int j = t - w + 1;
+          const int pos = (int)(win & 1023u);
+          if (INDEX) {
+            if (j == 0) kw0 = win;
+            if (t == t1) kw1 = win;
+          }
+          const bool act = j >= 1 && t <= tend;
+          const bool emit = act && j > 1 && pos != last;
+          st.put(emit, run_meta(a, last, jlo, j - 1));
+          if (emit) jlo = j;
+          if (act) last = pos;
+        }
+        mm = ((mm << 2) | ((cwd >> (62 - 2 * (x & 31))) & 3u)) & mmask;
+        if (u % kStageEvery == kStageEvery - 1)  // a few flush sites per block (code size)
+          while (st.nbuf >= (uint32_t)kWave) st.flush(kWave, rw, a0);
+      }
+      while (st.nbuf >= (uint32_t)kWave) st.flush(kWave, rw, a0);
+      // suffix minima of this block in place: S[u] = min over [u, w)
+#pragma unroll
+      for (int u = kRegW - 2; u >= 0; --u)
+        if (u < w - 1) S[u] = S[u + 1] < S[u] ? S[u + 1] : S[u];
+    }
+    st.put(tend >= 0, run_meta(a, last, jlo, J));  // each read's last run
+    while (st.nbuf) st.flush(st.nbuf < (uint32_t)kWave ? st.nbuf : (uint32_t)kWave, rw, a0);
+    if constexpr (INDEX) {
+      if (n) {
+        // keys o = 3 (R[n-h, n) = rc F[0, h): m-mer i = rc of F's at t = w-1-i) and
+        // o = 2 (R[0, h) = rc F[n-h, n): m-mer i = rc of F's at t = n-m-i), both
+        // rolled towards smaller t, one base per step
+        const uint64_t A = ext_reg<MAXW>(rw, n - h);  // F[n-h, n-h+32)
+        uint64_t r3 = rc_word(funnel(rw[0], rw[1], 2 * (w - 1))) & mmask;  // rc(F[w-1, w-1+m))
+        uint64_t r2 = rc_word(ext_reg<MAXW>(rw, n - m)) & mmask;             // rc(F[n-m, n))
+        uint32_t kb3 = 0xFFFFFFFFu, kb2 = 0xFFFFFFFFu;
+        uint64_t mb3 = 0, mb2 = 0;
+        for (int i = 0; i < w; ++i) {
+          const uint32_t k3 = order_key(r3) | (uint32_t)i, k2 = order_key(r2) | (uint32_t)i;
+          if (k3 < kb3) { kb3 = k3; mb3 = r3; }
+          if (k2 < kb2) { kb2 = k2; mb2 = r2; }
+          if (i + 1 < w) {
+            const int t3 = w - 2 - i;  // F base entering the rc m-mer at t - 1
+            const uint64_t b3 = (rw[0] >> (62 - 2 * t3)) & 3u;
+            const uint64_t b2 = (A >> (62 - 2 * t3)) & 3u;  // F[n-m-1-i] = F[n-h + (w-2-i)]
+            r3 = ((r3 << 2) | (3u - b3)) & mmask;
+            r2 = ((r2 << 2) | (3u - b2)) & mmask;
+          }
+        }
+        const int p0 = (int)(kw0 & 1023u), p1 = (int)(kw1 & 1023u);
+        const uint64_t mb0 = funnel(rw[0], rw[1], p0 << 1) >> msh;  // p0 < w <= 32
+        const uint64_t mb1 = ext_reg<MAXW>(rw, p1) >> msh;
+        const uint64_t nbm = (1ULL << p.nb_log2) - 1;
+        const uint64_t mb[4] = {mb0, mb1, mb2, mb3};
+        const int qq[4] = {p0, p1 - (n - h), (int)(kb2 & 1023u), (int)(kb3 & 1023u)};
+#pragma unroll
+        for (int o = 0; o < 4; ++o) {
+          const uint64_t v = mix64(mb[o]);
+          const unsigned long long e = make_entry(v, p.nb_log2, qq[o], o, (uint32_t)a);
+          if (o == 0 && p.key0) p.key0[a] = (v & ((1ULL << 50) - 1)) | ((uint64_t)qq[0] << 54);
+          if (p.key_bk) {
+            p.key_bk[o * p.key_n + a] = (uint32_t)(v & nbm);
+            p.key_ent[o * p.key_n + a] = e;
+          } else {
+            cell_insert(p.cells, v & nbm, p.cell_n, e);
+          }
+        }
+      } else if (a < p.a_hi) {
+        if (p.key0) p.key0[a] = kEmpty;
+        if (p.key_bk) {
+          for (int o = 0; o < 4; ++o) {
+            p.key_bk[o * p.key_n + a] = 0;
+            p.key_ent[o * p.key_n + a] = kEmpty;
+          }
+        }
+      }
+    }
+  }
+  st.finish(gw);
 }
 
 // The partner's slot as it lies in memory: words 0 .. MAXW-1 (plus one pad
@@ -1787,10 +2072,29 @@ uint32_t resident_blocks(mg_ctx* ctx, K kernel, size_t lds, uint64_t want, int b
 // (long windows: w = l - k grows with min_overlap).  0 = w too large.
 constexpr size_t kLdsPerCu = 160 * 1024;
 inline size_t scan_lds_per_wave(uint32_t w) { return (((size_t)w * kWave + 1) / 2 + kScanBuf) * sizeof(uint64_t); }
+// the register scan (k_scan_reg) when its window fits in registers
+inline bool use_scan_reg(const mg_ctx* ctx) { return ctx->scan_reg && ctx->w <= (uint32_t)kRegW; }
+inline uint32_t scan_block_waves(const mg_ctx* ctx);
+inline size_t scan_lds(const mg_ctx* ctx);
 inline uint32_t scan_wpb(uint32_t w) {
   for (uint32_t wpb = kWavesPerBlock; wpb >= 1; wpb >>= 1)
     if (wpb * scan_lds_per_wave(w) <= kLdsPerCu) return wpb;
   return 0;
+}
+inline uint32_t scan_block_waves(const mg_ctx* ctx) { return use_scan_reg(ctx) ? kWavesPerBlock : scan_wpb(ctx->w); }
+inline size_t scan_lds(const mg_ctx* ctx) {
+  return use_scan_reg(ctx) ? (size_t)kWavesPerBlock * kStageRing * sizeof(uint64_t)
+                           : (size_t)scan_wpb(ctx->w) * scan_lds_per_wave(ctx->w);
+}
+template <int W>
+uint32_t scan_resident(mg_ctx* ctx, bool index, uint64_t want) {
+  const size_t lds = scan_lds(ctx);
+  const int block = (int)scan_block_waves(ctx) * kWave;
+  if (use_scan_reg(ctx))
+    return index ? resident_blocks(ctx, k_scan_reg<W, true>, lds, want, block)
+                 : resident_blocks(ctx, k_scan_reg<W, false>, lds, want, block);
+  return index ? resident_blocks(ctx, k_scan<W, true>, lds, want, block)
+               : resident_blocks(ctx, k_scan<W, false>, lds, want, block);
 }
 
 // 12-B sort records fit when read index, jlo, two window deltas and the
@@ -1819,7 +2123,7 @@ DiscGeom disc_geom(mg_ctx* ctx, bool contain, uint64_t nsrc) {
   DiscGeom g;
   const uint64_t ngroups = (nsrc + kWave - 1) / kWave;
   const uint64_t want = std::max<uint64_t>(1, (ngroups + kWavesPerBlock - 1) / kWavesPerBlock);
-  g.lds_scan = (size_t)scan_wpb(ctx->w) * scan_lds_per_wave(ctx->w);
+  g.lds_scan = scan_lds(ctx);
   if (ctx->split) {
     g.lds_probe = (size_t)kWavesPerBlock * ProbeLds<W>::split_bytes;
     g.grid = contain ? resident_blocks(ctx, k_probe<W, true, true>, g.lds_probe, want)
@@ -1829,7 +2133,7 @@ DiscGeom disc_geom(mg_ctx* ctx, bool contain, uint64_t nsrc) {
     g.grid = contain ? resident_blocks(ctx, k_probe<W, true, false>, g.lds_probe, want)
                      : resident_blocks(ctx, k_probe<W, false, false>, g.lds_probe, want);
   }
-  const uint32_t scan_res = resident_blocks(ctx, k_scan<W, false>, g.lds_scan, ~0ull >> 1, scan_wpb(ctx->w) * kWave);
+  const uint32_t scan_res = scan_resident<W>(ctx, false, ~0ull >> 1);
   g.kreg = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(scan_res / g.grid, (want + g.grid - 1) / g.grid));
   g.sgrid = g.grid * g.kreg;
   return g;
@@ -1843,7 +2147,7 @@ struct LaunchScan {
   static int run(mg_ctx* ctx, bool contain, uint64_t a_lo, uint64_t a_hi, uint32_t sgrid, bool filter,
                  hipStream_t stream = nullptr, bool no_super = false, bool index = false, bool flat = false) {
     if (!stream) stream = ctx->stream;
-    const uint32_t wpb = scan_wpb(ctx->w);
+    const uint32_t wpb = scan_block_waves(ctx);
     const uint64_t nw = (uint64_t)sgrid * wpb;  // scan wavefronts = run regions
     ctx->nrun_reg = nw;
     const uint64_t ngroups = (a_hi - a_lo + kWave - 1) / kWave;
@@ -1881,7 +2185,7 @@ struct LaunchScan {
     sp.runs = ctx->d_runs;
     sp.run_cnt = ctx->d_run_cnt;
     sp.run_cap = run_cap;
-    const size_t lds = (size_t)wpb * scan_lds_per_wave(ctx->w);
+    const size_t lds = scan_lds(ctx);
     sp.cells = ctx->d_cells;
     sp.cell_n = ctx->cell_n;
     ctx->scan_flat = flat;
@@ -1926,7 +2230,15 @@ struct LaunchScan {
       sp.key_n = ctx->n;
     }
     (void)hipEventRecord(ctx->ev[6], stream);
-    if (index) {  // unsharded only (the whole key space is this context's)
+    if (use_scan_reg(ctx)) {
+      if (index) {
+        allow_lds(k_scan_reg<W, true>, lds);
+        hipLaunchKernelGGL((k_scan_reg<W, true>), dim3(sgrid), dim3(wpb * kWave), lds, stream, sp);
+      } else {
+        allow_lds(k_scan_reg<W, false>, lds);
+        hipLaunchKernelGGL((k_scan_reg<W, false>), dim3(sgrid), dim3(wpb * kWave), lds, stream, sp);
+      }
+    } else if (index) {  // unsharded only (the whole key space is this context's)
       allow_lds(k_scan<W, true>, lds);
       hipLaunchKernelGGL((k_scan<W, true>), dim3(sgrid), dim3(wpb * kWave), lds, stream, sp);
     } else {
@@ -2332,6 +2644,12 @@ int mg_set_option(mg_ctx* ctx, const char* name, int64_t value) {
     ctx->sorted_state = 0;
     return 0;
   }
+  if (!strcmp(name, "scan_reg")) {  // 1 (default): register sliding minimum when w <= 32; 0: LDS version
+    ctx->scan_reg = value != 0;
+    ctx->scan_state = 0;
+    ctx->sorted_state = 0;
+    return 0;
+  }
   if (!strcmp(name, "halving")) {  // 0: parity-alternating o=2/3 side (default), 1: lower ID keeps
     ctx->halving_low = value != 0;
     return 0;
@@ -2605,11 +2923,9 @@ void read_stats(mg_ctx* ctx, uint64_t nsrc) {
 template <int W>
 struct LaunchScanAll {
   static int run(mg_ctx* ctx, hipStream_t st, bool index) {
-    const uint32_t wpb = scan_wpb(ctx->w);
-    const size_t lds = (size_t)wpb * scan_lds_per_wave(ctx->w);
+    const uint32_t wpb = scan_block_waves(ctx);
     const uint64_t groups = (ctx->n + kWave - 1) / kWave;
-    const uint32_t sgrid = index ? resident_blocks(ctx, k_scan<W, true>, lds, (groups + wpb - 1) / wpb, wpb * kWave)
-                                 : resident_blocks(ctx, k_scan<W, false>, lds, (groups + wpb - 1) / wpb, wpb * kWave);
+    const uint32_t sgrid = scan_resident<W>(ctx, index, (groups + wpb - 1) / wpb);
     return LaunchScan<W>::run(ctx, true, 0, ctx->n, sgrid, false, st, true, index, ctx->sort_runs);
   }
 };
@@ -2874,6 +3190,7 @@ int mg_build_index(mg_ctx* ctx, uint32_t min_overlap, uint32_t seed_k) {
   MG_TRY(hipEventRecord(ctx->ev[1], ctx->stream));
   MG_TRY(hipEventSynchronize(ctx->ev[1]));
   ctx->t.index_ms = elapsed(ctx->ev[0], ctx->ev[1]);
+  ctx->shared_scan_ms = (shared_scan(ctx) && ctx->n) ? elapsed(ctx->ev[6], ctx->ev[7]) : 0.f;
   ctx->index_ready = true;
   return 0;
 }
@@ -2942,7 +3259,8 @@ int mg_find_overlaps(mg_ctx* ctx, uint64_t* n_rows) {
   MG_TRY(hipEventSynchronize(ctx->ev[5]));
   // the kernels' own events bracket the last launches (a resize retry included
   // in ev[4]..ev[5] is not kernel time)
-  ctx->t.scan_ms = shared_scan(ctx) ? 0.f : elapsed(ctx->ev[6], ctx->ev[7]);  // shared: inside index_ms
+  // scan kernel time (shared scan: measured at build time, part of index_ms)
+  ctx->t.scan_ms = shared_scan(ctx) ? ctx->shared_scan_ms : elapsed(ctx->ev[6], ctx->ev[7]);
   if (ctx->split) {
     ctx->t.probe_ms = elapsed(ctx->ev[8], ctx->ev[9]);
     ctx->t.verify_ms = elapsed(ctx->ev[10], ctx->ev[11]);
@@ -2952,7 +3270,7 @@ int mg_find_overlaps(mg_ctx* ctx, uint64_t* n_rows) {
   }
   ctx->t.sort_ms = (shared_scan(ctx) && ctx->sort_runs && ctx->sorted_state == 2)
                        ? elapsed(ctx->ev[12], ctx->ev[13]) : 0.f;
-  ctx->t.overlap_ms = ctx->t.scan_ms + ctx->t.sort_ms + ctx->t.probe_ms + ctx->t.verify_ms;
+  ctx->t.overlap_ms = (shared_scan(ctx) ? 0.f : ctx->t.scan_ms) + ctx->t.sort_ms + ctx->t.probe_ms + ctx->t.verify_ms;
   read_stats(ctx, nsrc);
   // device wall of the step: index build start .. last discovery kernel end
   ctx->t.total_ms = shared_scan(ctx) ? elapsed(ctx->ev[0], ctx->ev[5])
@@ -2995,6 +3313,7 @@ int mg_insert_keys(mg_ctx* ctx, const void* recs, uint64_t n) {
   MG_TRY(hipEventRecord(ctx->ev[1], ctx->stream));
   MG_TRY(hipEventSynchronize(ctx->ev[1]));
   ctx->t.index_ms = elapsed(ctx->ev[0], ctx->ev[1]);
+  ctx->shared_scan_ms = (shared_scan(ctx) && ctx->n) ? elapsed(ctx->ev[6], ctx->ev[7]) : 0.f;
   ctx->index_ready = true;
   return 0;
 }

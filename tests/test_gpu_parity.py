@@ -186,7 +186,11 @@ def test_random_sets_vs_oracle(engine, case):
     ds = Dataset.from_codes(c, L, l)
     od = OracleDataset.from_strings(seqs, l)
     assert ds.num_unique == od.num_unique
-    rows, sup = gpu_rows(engine, ds, l, k=k)
+    engine.set_option("scan_reg", 1)
+    try:
+        rows, sup = gpu_rows(engine, ds, l, k=k)
+    finally:
+        engine.set_option("scan_reg", 0)
     orows, osup, _, _ = od.overlaps(l)
     assert np.array_equal(sup.astype(np.uint64), osup)
     assert np.array_equal(rows_to_tuples(rows), sorted_tuples(orows))
@@ -658,3 +662,36 @@ def test_scan_inside_probe_path(name):
     e.close()
     assert np.array_equal(rows_to_tuples(rows), golden_rows(name))
     assert {str(i): int(s) for i, s in enumerate(sup) if s} == meta["super"]
+
+
+@pytest.mark.parametrize("name", FIXTURES)
+def test_scan_register_path(name):
+    """option scan_reg = 1: the register sliding-minimum scan (k_scan_reg)
+    instead of the LDS one (k_scan); same runs, keys and rows."""
+    meta = load_meta(name)
+    ds = Dataset.from_files([fixture_input(name)], meta["l"])
+    e = OverlapEngine(0)
+    e.set_option("scan_reg", 1)
+    rows, sup = gpu_rows(e, ds, meta["l"])
+    e.close()
+    assert np.array_equal(rows_to_tuples(rows), golden_rows(name))
+    assert {str(i): int(s) for i, s in enumerate(sup) if s} == meta["super"]
+
+
+@pytest.mark.parametrize("l,k", [(33, 1), (40, 8), (50, 17), (50, 18), (20, 19), (50, 31), (60, 32)])
+def test_register_scan_window_extremes(engine, l, k):
+    """w = l - k = 32 (the register scan's largest window), 33 (falls back to the
+    LDS scan), 1 and typical ones, against the oracle on mixed lengths
+    (containment, all four keys, runs crossing block edges)."""
+    c, L = synth.uniform_read_set(3000, 0, 15000, seed=120 + k, lo=l + 1, hi=l + 90)
+    seqs = synth.codes_to_strings(c, L)
+    ds = Dataset.from_codes(c, L, l)
+    od = OracleDataset.from_strings(seqs, l)
+    engine.set_option("scan_reg", 1)
+    try:
+        rows, sup = gpu_rows(engine, ds, l, k=k)
+    finally:
+        engine.set_option("scan_reg", 0)
+    orows, osup, _, _ = od.overlaps(l)
+    assert np.array_equal(sup.astype(np.uint64), osup)
+    assert np.array_equal(rows_to_tuples(rows), sorted_tuples(orows))
