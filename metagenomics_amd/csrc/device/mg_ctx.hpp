@@ -88,6 +88,18 @@ struct mg_ctx {
   int scan_state = 0;        // 0 none, 1 launched (not settled), 2 settled
   bool overlap_scan = true;  // option "overlap_scan" (0: separate index build, a scan per probe pass)
   bool scan_reg = false;     // option "scan_reg": register sliding minimum (k_scan_reg) when w <= 32
+  // partitioned join (option "join", default): keys + runs as sorted join
+  // records, per-partition LDS tables (k_join); cells only on demand (lookups)
+  bool join = true;
+  int join_P = 0, join_A = 0, join_QB = 0, join_WB = 0;  // record geometry of the current build (0: not join)
+  int join_P_opt = 0;        // option "join_parts_log2" (0: auto)
+  bool join_ready = false;   // the sorted join records + partition bounds are current
+  bool cells_ready = false;  // the cell table holds the current index
+  uint64_t n_join = 0;       // join records (holes excluded)
+  unsigned long long* d_bnd = nullptr;
+  unsigned long long* d_mid = nullptr;
+  size_t bnd_cap = 0, mid_cap = 0;
+  unsigned int* d_queue = nullptr;
   // split probe (k_probe<SPLIT> + k_verify)
   bool split = false;  // option "split": k_probe<SPLIT> + k_verify instead of the fused probe
   uint3* d_cand = nullptr;
@@ -185,6 +197,8 @@ inline void reset_derived(mg_ctx* ctx) {
   ctx->scan_state = 0;
   ctx->sorted_state = 0;
   ctx->index_ready = false;
+  ctx->join_ready = false;
+  ctx->cells_ready = false;
   ctx->contained_done = false;
   ctx->super_any = false;
   ctx->n_rows = 0;

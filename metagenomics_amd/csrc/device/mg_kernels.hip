@@ -34,6 +34,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdint>
 #include <cstring>
 #include <string>
@@ -419,7 +420,41 @@ struct ScanParams {
   // per read: its o = 0 key's hash bits (bucket | fingerprint, 50 bits) | q << 54
   // (k_prefix_contain); nullptr: not written
   uint64_t* key0;
+  // partitioned join (option "join"): join_P > 0 packs runs AND the four keys of
+  // every read as 12-B join records (join_k32 / join_run_val / join_key_val)
+  // into the flat arrays instead of inserting keys into cells
+  int join_P, join_A, join_QB, join_WB;
 };
+
+// ---------------------------------------------------------------- join ---
+// Partitioned hash join: every index key (hashRead's four keys,
+// HashTable.cpp:88-104) and every window run becomes a 12-B record {k32, val64}
+// keyed by the partition f = top P bits of v = mix64(minimizer m-mer).  One
+// radix sort on the low P + 2 bits of k32 groups each partition's keys, then its
+// runs; k_join builds the partition's exact-key table in LDS and probes its runs
+// against it.  k32 = H32 << (P + 2) | f << 1 | is_run (bit P + 1 is 0; holes
+// are all ones and sort last), H32 = low 32 bits of v; the P + 2 high bits of
+// H32 that k32 cannot hold ride in val64:
+//   run: read (A) | jlo (10) | jhi - jlo (WB) | p - jhi (WB) | H32 >> (30 - P)
+//   key: read (A) | o (2)    | q (QB)                       | H32 >> (30 - P)
+__device__ __forceinline__ uint32_t join_k32(uint64_t v, int P, uint32_t is_run) {
+  return ((uint32_t)v << (P + 2)) | ((uint32_t)(v >> (64 - P)) << 1) | is_run;
+}
+__device__ __forceinline__ uint64_t join_hhi(uint64_t v, int P) { return (uint64_t)((uint32_t)v >> (30 - P)); }
+__device__ __forceinline__ uint64_t join_run_val(uint64_t meta, uint64_t v, const ScanParams& p) {
+  const uint64_t ra = meta & 0xFFFFFFFFull, pos = (meta >> 32) & 1023u, jlo = (meta >> 42) & 1023u,
+                 jhi = (meta >> 52) & 1023u;
+  const int A = p.join_A, WB = p.join_WB;
+  return ra | (jlo << A) | ((jhi - jlo) << (A + 10)) | ((pos - jhi) << (A + 10 + WB)) |
+         (join_hhi(v, p.join_P) << (A + 10 + 2 * WB));
+}
+__device__ __forceinline__ uint64_t join_key_val(uint32_t r, int o, int q, uint64_t v, const ScanParams& p) {
+  const int A = p.join_A;
+  return (uint64_t)r | ((uint64_t)o << A) | ((uint64_t)q << (A + 2)) | (join_hhi(v, p.join_P) << (A + 2 + p.join_QB));
+}
+__device__ __forceinline__ uint32_t join_h32(uint32_t k32, uint64_t val, int P, int shift) {
+  return (k32 >> (P + 2)) | ((uint32_t)(val >> shift) << (30 - P));
+}
 
 // Sort records of 12 B instead of 16 (option "sort_runs" when the widths fit,
 // packable_runs): key32 = bucket | low (32 - nb) fingerprint bits; meta64 =
@@ -847,7 +882,10 @@ struct RunStage {
         const uint64_t pr = lane_prefix(bal);
         const uint64_t at = pr < room ? fbase + fused + pr : nbase + (pr - room);
         if (at < p.flat_cap) {
-          if (p.pack_a) {
+          if (p.join_P) {
+            reinterpret_cast<uint32_t*>(p.flat_keys)[at] = join_k32(v, p.join_P, 1u);
+            p.flat_meta[at] = join_run_val(meta, v, p);
+          } else if (p.pack_a) {
             reinterpret_cast<uint32_t*>(p.flat_keys)[at] = run_pack_key(v, p.nb_log2);
             p.flat_meta[at] = run_pack_meta(meta, v, p.nb_log2, p.pack_a, p.pack_w);
           } else {
@@ -856,13 +894,7 @@ struct RunStage {
           }
         }
       }
-      if (npop > room) {
-        fbase = nbase;
-        fused = npop - room;
-        fcap = kFlatChunk;
-      } else {
-        fused += npop;
-      }
+      advance(npop, room, nbase);
     } else if (flag) {
       const uint64_t at = cursor + lane_prefix(bal);
       if (at < p.run_cap) region[at] = make_ulonglong2(v, meta);
@@ -873,13 +905,48 @@ struct RunStage {
     wave_sync();
   }
 
+  // flat chunk bookkeeping after npop records were placed (room = what the old chunk had left)
+  __device__ __forceinline__ void advance(uint64_t npop, uint64_t room, uint64_t nbase) {
+    if (npop > room) {
+      fbase = nbase;
+      fused = npop - room;
+      fcap = kFlatChunk;
+    } else {
+      fused += npop;
+    }
+  }
+
+  // one ready 32-bit-key record per flagged lane straight into the flat arrays
+  // (the join mode's index keys)
+  __device__ void emit_ready(bool flag, uint32_t k32, uint64_t val) {
+    const uint64_t bal = __ballot(flag);
+    const uint64_t npop = (uint64_t)__popcll(bal);
+    if (!npop) return;
+    const uint64_t room = fcap - fused;
+    unsigned long long nbase = 0;
+    if (npop > room) {
+      const uint32_t x = blockIdx.x & (kFlatCounters - 1);
+      if (lane == 0) nbase = (atomicAdd(&p.flat_cursor[x], 1ull) * kFlatCounters + x) * kFlatChunk;
+      nbase = __shfl(nbase, 0);
+    }
+    if (flag) {
+      const uint64_t pr = lane_prefix(bal);
+      const uint64_t at = pr < room ? fbase + fused + pr : nbase + (pr - room);
+      if (at < p.flat_cap) {
+        reinterpret_cast<uint32_t*>(p.flat_keys)[at] = k32;
+        p.flat_meta[at] = val;
+      }
+    }
+    advance(npop, room, nbase);
+  }
+
   // unused tail of the last flat chunk (holes the sort and probe skip) and the region count
   __device__ void finish(uint64_t gw) {
     if (p.flat_keys) {
       for (uint64_t i = fused + lane; i < fcap; i += kWave) {
         const uint64_t at = fbase + i;
         if (at < p.flat_cap) {
-          if (p.pack_a)
+          if (p.pack_a || p.join_P)
             reinterpret_cast<uint32_t*>(p.flat_keys)[at] = 0xFFFFFFFFu;
           else
             p.flat_keys[at] = kEmpty;
@@ -1010,6 +1077,8 @@ __global__ __launch_bounds__(kBlock) void k_scan_reg(ScanParams p) {
     st.put(tend >= 0, run_meta(a, last, jlo, J));  // each read's last run
     while (st.nbuf) st.flush(st.nbuf < (uint32_t)kWave ? st.nbuf : (uint32_t)kWave, rw, a0);
     if constexpr (INDEX) {
+      uint32_t jk[4] = {0, 0, 0, 0};
+      uint64_t jv[4] = {0, 0, 0, 0};
       if (n) {
         // keys o = 3 (R[n-h, n) = rc F[0, h): m-mer i = rc of F's at t = w-1-i) and
         // o = 2 (R[0, h) = rc F[n-h, n): m-mer i = rc of F's at t = n-m-i), both
@@ -1037,6 +1106,14 @@ __global__ __launch_bounds__(kBlock) void k_scan_reg(ScanParams p) {
         const uint64_t nbm = (1ULL << p.nb_log2) - 1;
         const uint64_t mb[4] = {mb0, mb1, mb2, mb3};
         const int qq[4] = {p0, p1 - (n - h), (int)(kb2 & 1023u), (int)(kb3 & 1023u)};
+        if (p.join_P) {  // partitioned join: the keys become join records (emitted below), no cells
+#pragma unroll
+          for (int o = 0; o < 4; ++o) {
+            const uint64_t v = mix64(mb[o]);
+            jk[o] = join_k32(v, p.join_P, 0u);
+            jv[o] = join_key_val((uint32_t)a, o, qq[o], v, p);
+          }
+        } else {
 #pragma unroll
         for (int o = 0; o < 4; ++o) {
           const uint64_t v = mix64(mb[o]);
@@ -1049,6 +1126,7 @@ __global__ __launch_bounds__(kBlock) void k_scan_reg(ScanParams p) {
             cell_insert(p.cells, v & nbm, p.cell_n, e);
           }
         }
+        }
       } else if (a < p.a_hi) {
         if (p.key0) p.key0[a] = kEmpty;
         if (p.key_bk) {
@@ -1057,6 +1135,10 @@ __global__ __launch_bounds__(kBlock) void k_scan_reg(ScanParams p) {
             p.key_ent[o * p.key_n + a] = kEmpty;
           }
         }
+      }
+      if (p.join_P) {  // every lane takes part (the flat-chunk state is wavefront-uniform)
+#pragma unroll
+        for (int o = 0; o < 4; ++o) st.emit_ready(n > 0, jk[o], jv[o]);
       }
     }
   }
@@ -1693,6 +1775,319 @@ __global__ __launch_bounds__(kBlock) void k_verify(ProbeParams p, uint64_t cand_
   }
 }
 
+// ----------------------------------------------------------- k_join ---
+// One partition of the sorted join records at a time per workgroup (dynamic
+// queue): the partition's keys go into an exact-key table in LDS (open
+// addressing, 8-B entries read | fp19 << 32 | q << 51 | o << 61, slot = low
+// kJoinTBits bits of H32, fp = H32 bits 13..31), then every run of the
+// partition walks its slot chain: an entry with the run's fingerprint and
+// q such that j = p - q lies in the run's window range [jlo, jhi] is the exact
+// candidate of getListOfReads(F1[j, j+h)) (HashTable.cpp:202-221) that the
+// reference meets at window j (OverlapGraph.cpp:534-547).  Candidates go to a
+// per-wavefront LDS ring and are verified 64 at a time against both reads'
+// slots (checkOverlap :354-383 / checkOverlapForContainedRead :302-340), with
+// the source read's words in registers.  More keys than kJoinCap: the table is
+// refilled per chunk of keys and the runs streamed again (skewed partitions).
+// CONTAIN with prefix queries: every o = 0 key of the partition also probes the
+// table for shorter reads whose o = 0/2 key is the same string at the same q
+// (a prefix of read1 at offset 0, which the reference meets only through the
+// shorter read's suffix key), the k_prefix_contain rule.
+constexpr int kJoinBlock = 512;
+constexpr int kJoinWaves = kJoinBlock / kWave;
+constexpr int kJoinTBits = 13;
+constexpr int kJoinT = 1 << kJoinTBits;   // LDS table slots (64 KiB)
+constexpr int kJoinCap = kJoinT / 2;      // keys per table fill (load <= 50 %)
+constexpr int kJoinRing = 128;            // per-wavefront candidate ring
+constexpr size_t kJoinLds = (size_t)kJoinT * 8 + (size_t)kJoinWaves * kJoinRing * 12 + 16;
+
+struct JoinParams {
+  const uint64_t* words;
+  const uint16_t* len;
+  int h, P, A, QB, WB;
+  const uint32_t* k32;               // sorted join records
+  const uint64_t* val;
+  const unsigned long long* bnd;     // [nparts + 1] first record of each partition (its keys come first)
+  const unsigned long long* mid;     // [nparts] first run record of each partition
+  uint32_t nparts;
+  unsigned int* queue;               // partition dequeue counter (zeroed before the launch)
+  const uint32_t* super;             // discovery: partners with superReadID != 0 dropped at emit (:548)
+  const uint32_t* src_super;         // discovery: runs of contained sources dropped (:548)
+  uint64_t src_lo, src_hi;           // only runs of sources in [src_lo, src_hi) (src_hi = 0: all)
+  unsigned long long* superkey;      // CONTAIN: max (len << 32 | ~index) per contained read
+  int contain_even;                  // CONTAIN: drop o = 1/3 hits (the prefix queries cover s = 0)
+  int prefix_queries;                // CONTAIN: o = 0 keys query the table (offset-0 containments)
+  uint32_t* rows;                    // 3 dwords per row, one region per wavefront
+  unsigned long long* reg_cnt;
+  uint64_t reg_cap;
+  int uniform_len, halving_low;
+  unsigned long long* stats;         // optional [kSegs * 4]: runs, entries, verified, rows
+};
+
+// 32 bases of a read held in registers starting at pos (pos >= -31; bases
+// before 0 read as 0)
+template <int MAXW>
+__device__ __forceinline__ uint64_t ext_reg_s(const uint64_t* rw, int pos) {
+  const uint64_t neg = rw[0] >> ((pos < 0 ? -pos : 0) * 2);
+  const uint64_t x = ext_reg<MAXW>(rw, pos < 0 ? 0 : pos);
+  return pos < 0 ? neg : x;
+}
+
+template <int MAXW, bool CONTAIN>
+__global__ __launch_bounds__(kJoinBlock) void k_join(JoinParams p) {
+  extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  uint64_t* const table = smem;
+  uint32_t* const rb = reinterpret_cast<uint32_t*>(smem + kJoinT) + (size_t)wv * kJoinRing * 3;  // ring: b | info | a
+  uint32_t* const s_part = reinterpret_cast<uint32_t*>(smem + kJoinT) + (size_t)kJoinWaves * kJoinRing * 3;
+  const int h = p.h, P = p.P, A = p.A;
+  const uint64_t amask = (1ULL << A) - 1;
+  const int run_sh = A + 10 + 2 * p.WB, key_sh = A + 2 + p.QB;
+  const uint64_t gw = (uint64_t)blockIdx.x * kJoinWaves + wv;
+  const uint32_t seg = (uint32_t)(gw & (kSegs - 1));
+  uint32_t* const region = p.rows + gw * p.reg_cap * 3;
+  uint64_t cursor = 0;
+  uint32_t st_runs = 0, st_ent = 0, st_ver = 0, st_rows = 0;
+  uint32_t rhead = 0, rcnt = 0;  // candidate ring (wavefront-uniform)
+
+  // verify the first k (<= 64) candidates of the ring, one per lane
+  auto verify = [&](uint32_t k) {
+    const bool have = (uint32_t)lane < k;
+    int nrec = 0;
+    uint32_t r2 = 0, t2 = 0;
+    uint32_t bid = 0, sa = 0;
+    int n1 = 0, n2 = 0, o = 0, j = 0, x0 = 0, y0 = 0, L = 0;
+    bool cond = false, rcA = false;
+    if (have) {
+      const uint32_t at = (rhead + lane) & (kJoinRing - 1);
+      bid = rb[at];
+      const uint32_t info = rb[kJoinRing + at];
+      sa = rb[2 * kJoinRing + at];
+      o = (int)(info >> 30);
+      j = (int)(info & 1023u);
+      n1 = p.uniform_len ? p.uniform_len : (int)p.len[sa];
+      n2 = p.uniform_len ? p.uniform_len : (int)p.len[bid];
+      if (!CONTAIN) {
+        if (o == 0) {        // F1[j, n1) == F2[0, L)
+          L = n1 - j; cond = L < n2; x0 = j; y0 = 0; rcA = false;
+        } else if (o == 2) { // F1[j, n1) == R2[0, L)  <=>  R1[0, L) == F2[n2-L, n2)
+          L = n1 - j; cond = L < n2; x0 = 0; y0 = n2 - L; rcA = true;
+        } else {             // F1[0, L) == R2[n2-L, n2)  <=>  R1[n1-L, n1) == F2[0, L)
+          L = j + h; cond = j <= n2 - h; x0 = n1 - L; y0 = 0; rcA = true;
+        }
+      } else {
+        int sft;
+        cond = n1 > n2;
+        if (o == 0 || o == 2) {
+          cond = cond && (j <= n1 - n2);
+          sft = j;
+        } else {  // o = 1/3: only s = 0 (see k_probe's verify)
+          cond = cond && (j == n2 - h);
+          sft = 0;
+        }
+        L = n2;
+        y0 = 0;
+        rcA = o >= 2;
+        x0 = rcA ? n1 - sft - n2 : sft;
+      }
+    }
+    rhead += k;
+    rcnt -= k;
+    uint64_t y[MAXW + 1], xs[MAXW + 1];
+    load_slot<MAXW>(p.words, cond ? bid : 0u, y);  // partner slot (random line)
+    load_slot<MAXW>(p.words, cond ? sa : 0u, xs);  // source slot (random line)
+    if (cond) {
+      ++st_ver;
+      uint64_t diff = 0;
+#pragma unroll
+      for (int kk = 0; kk < MAXW; ++kk) {
+        const int lo = max(y0 - 32 * kk, 0), hi = min(y0 + L - 32 * kk, 32);
+        if (hi > lo) {
+          const int s = x0 - y0 + 32 * kk;  // source position of partner base 32 kk
+          const uint64_t av = rcA ? rc_word(ext_reg_s<MAXW>(xs, n1 - s - 32)) : ext_reg_s<MAXW>(xs, s);
+          const uint64_t msk = (lo ? (~0ULL >> (2 * lo)) : ~0ULL) & (hi < 32 ? ~(~0ULL >> (2 * hi)) : ~0ULL);
+          diff |= (av ^ y[kk]) & msk;
+        }
+      }
+      if (diff == 0) {
+        if (CONTAIN) {
+          atomicMax(&p.superkey[bid], ((unsigned long long)n1 << 32) | (0xFFFFFFFFu - sa));
+        } else if (!(p.super && p.super[bid])) {  // :548 read2 contained
+          // orientation/offset switch (:550-557) and the twin (:409-412, :841-855)
+          const uint32_t orient = (o == 0) ? 3u : (o == 2 ? 2u : 1u);
+          const uint32_t off = (o == 3) ? (uint32_t)(n1 - h - j) : (uint32_t)j;
+          const uint32_t torient = (orient == 3u) ? 0u : orient;
+          r2 = (orient << 16) | off;
+          t2 = (torient << 16) | (uint32_t)(uint16_t)(n2 + off - n1);
+          nrec = (bid == sa && o == 0) ? 4 : 2;  // a self o = 0 hit also stands for its o = 1 twin
+          st_rows += nrec;
+        }
+      }
+    }
+    if (!CONTAIN) {
+      const uint64_t b2 = __ballot(nrec >= 2), b4 = __ballot(nrec == 4);
+      const uint32_t tot = 2u * (uint32_t)(__popcll(b2) + __popcll(b4));
+      if (tot) {
+        if (cursor + tot <= p.reg_cap) {
+          const uint32_t pr = 2u * (lane_prefix(b2) + lane_prefix(b4));
+          uint3* d = reinterpret_cast<uint3*>(region + (cursor + pr) * 3);
+          for (int rr = 0; rr < nrec; rr += 2) {
+            d[0] = make_uint3(sa + 1, bid + 1, r2);
+            d[1] = make_uint3(bid + 1, sa + 1, t2);
+            d += 2;
+          }
+        }
+        cursor += tot;  // keeps counting past the capacity: the host resizes and reruns
+      }
+    }
+  };
+
+  // append one candidate per flagged lane to the ring; verify full batches
+  auto push = [&](bool flag, uint32_t b, uint32_t info, uint32_t a) {
+    const uint64_t bal = __ballot(flag);
+    if (!bal) return;
+    if (flag) {
+      const uint32_t at = (rhead + rcnt + lane_prefix(bal)) & (kJoinRing - 1);
+      rb[at] = b;
+      rb[kJoinRing + at] = info;
+      rb[2 * kJoinRing + at] = a;
+    }
+    rcnt += (uint32_t)__popcll(bal);
+    if (rcnt >= (uint32_t)kWave) {
+      wave_sync();
+      verify(kWave);
+      wave_sync();
+    }
+  };
+
+  for (;;) {
+    __syncthreads();  // every wave is done with the previous partition's table and s_part
+    if (threadIdx.x == 0) s_part[0] = atomicAdd(p.queue, 1u);
+    __syncthreads();
+    const uint32_t f = s_part[0];
+    if (f >= p.nparts) break;
+    const uint64_t kb = p.bnd[f], kr = p.mid[f], ke = p.bnd[f + 1];
+    if (kr == kb) continue;                                // no keys: nothing to find
+    if (ke == kr && !(CONTAIN && p.prefix_queries)) continue;  // no runs and no prefix queries
+    for (uint64_t c0 = kb; c0 < kr; c0 += kJoinCap) {
+      const uint64_t c1 = min(kr, c0 + (uint64_t)kJoinCap);
+      if (c0 != kb) __syncthreads();  // the previous chunk's probes are done
+      {
+        ulonglong2* t2 = reinterpret_cast<ulonglong2*>(table);
+        for (int i = threadIdx.x; i < kJoinT / 2; i += kJoinBlock) t2[i] = make_ulonglong2(kEmpty, kEmpty);
+      }
+      __syncthreads();
+      // the chunk's keys into the table
+      for (uint64_t i = c0 + threadIdx.x; i < c1; i += kJoinBlock) {
+        const uint64_t v = p.val[i];
+        const uint32_t H = join_h32(p.k32[i], v, P, key_sh);
+        const uint64_t e = (v & amask) | ((uint64_t)(H >> kJoinTBits) << 32) |
+                           (((v >> (A + 2)) & ((1ULL << p.QB) - 1)) << 51) | (((v >> A) & 3u) << 61);
+        uint32_t sl = H & (kJoinT - 1);
+        for (;;) {  // capacity 2x the chunk: an empty slot always exists
+          if (atomicCAS(reinterpret_cast<unsigned long long*>(&table[sl]), kEmpty, (unsigned long long)e) == kEmpty)
+            break;
+          sl = (sl + 1) & (kJoinT - 1);
+        }
+      }
+      __syncthreads();
+      // probe items: CONTAIN prefix queries (the partition's o = 0 keys), then runs
+      const uint64_t q0 = (CONTAIN && p.prefix_queries) ? kb : kr;
+      for (uint64_t i0 = q0 + (uint64_t)wv * kWave; i0 < ke; i0 += kJoinBlock) {
+        const uint64_t i = i0 + lane;
+        bool live = i < ke;
+        const bool is_run = i >= kr;
+        uint32_t H = 0, ra = 0, fpr = 0;
+        int rp = 0, jlo = 0, jhi = 0, qa = 0;
+        if (live) {
+          const uint64_t v = p.val[i];
+          const uint32_t k = p.k32[i];
+          ra = (uint32_t)(v & amask);
+          if (is_run) {
+            H = join_h32(k, v, P, run_sh);
+            jlo = (int)((v >> A) & 1023u);
+            jhi = jlo + (int)((v >> (A + 10)) & ((1ULL << p.WB) - 1));
+            rp = jhi + (int)((v >> (A + 10 + p.WB)) & ((1ULL << p.WB) - 1));
+            if ((p.src_super && p.src_super[ra]) || (p.src_hi && (ra < p.src_lo || ra >= p.src_hi))) live = false;
+          } else {  // prefix query: only o = 0 keys
+            H = join_h32(k, v, P, key_sh);
+            qa = (int)((v >> (A + 2)) & ((1ULL << p.QB) - 1));
+            if (((v >> A) & 3u) != 0) live = false;
+          }
+          fpr = H >> kJoinTBits;
+        }
+        if (live && is_run) ++st_runs;
+        uint32_t sl = H & (kJoinT - 1);
+        while (__ballot(live)) {
+          const uint64_t e = live ? table[sl] : kEmpty;
+          if (e == kEmpty) live = false;
+          bool keep = false;
+          uint32_t b = 0, info = 0;
+          if (live) {
+            ++st_ent;
+            b = (uint32_t)e;
+            const uint32_t hi = (uint32_t)(e >> 32);
+            const int oo = (int)(hi >> 29), q = (int)((hi >> 19) & 1023u);
+            if ((hi & 0x7FFFFu) == fpr) {
+              if (is_run) {
+                const int j = rp - q;
+                keep = j >= jlo && j <= jhi;
+                // halving: o = 1 hits are twins of the partner's o = 0
+                // hits; an o = 2/3 pair is kept on one side only (rc_side_keeps)
+                keep = keep && (CONTAIN || oo == 0 ||
+                                (oo >= 2 && (p.halving_low ? b >= ra : rc_side_keeps(ra, b))));
+                keep = keep && !(CONTAIN && p.contain_even && (oo & 1));
+                info = ((uint32_t)oo << 30) | (uint32_t)j;
+              } else {
+                // read b's o = 0/2 key is read1's o = 0 key (same string at the same q):
+                // b (or its reverse strand) may be a prefix of read1 (offset j = 0)
+                keep = q == qa && !(oo & 1) && b != ra;
+                info = (uint32_t)oo << 30;
+              }
+            }
+          }
+          push(keep, b, info, ra);
+          sl = (sl + 1) & (kJoinT - 1);
+        }
+      }
+    }
+  }
+  while (rcnt) {
+    const uint32_t k = rcnt < (uint32_t)kWave ? rcnt : (uint32_t)kWave;
+    wave_sync();
+    verify(k);
+    wave_sync();
+  }
+  if (!CONTAIN && lane == 0) p.reg_cnt[gw] = cursor;
+  if (p.stats) {
+    uint32_t vv[4] = {st_runs, st_ent, st_ver, st_rows};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      uint32_t x = vv[i];
+#pragma unroll
+      for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d);
+      if (lane == 0) atomicAdd(&p.stats[seg * 4 + i], (unsigned long long)x);
+    }
+  }
+}
+
+// Partition bounds of the sorted join records: bnd[f] = first record whose
+// (partition, type) sort bits are >= (f, key), mid[f] = first >= (f, run).
+__global__ __launch_bounds__(kBlock) void k_join_bounds(const uint32_t* __restrict__ k32, uint64_t n, int P,
+                                                        unsigned long long* __restrict__ bnd,
+                                                        unsigned long long* __restrict__ mid, uint32_t nparts) {
+  const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
+  if (t > 2 * nparts) return;  // targets 0 .. 2 nparts: (f << 1) | type, the last = end
+  const uint32_t mask = (1u << (P + 2)) - 1, target = t;
+  uint64_t lo = 0, hi = n;
+  while (lo < hi) {
+    const uint64_t md = (lo + hi) / 2;
+    if ((k32[md] & mask) < target) lo = md + 1;
+    else hi = md;
+  }
+  if (t & 1) mid[t >> 1] = lo;
+  else bnd[t >> 1] = lo;
+}
+
 // Gather per-wavefront row regions into a contiguous array (copy-out path only).
 __global__ __launch_bounds__(kBlock) void k_compact_rows(const uint32_t* __restrict__ rows, uint64_t reg_cap,
                                                         const uint64_t* __restrict__ prefix,
@@ -2073,7 +2468,8 @@ uint32_t resident_blocks(mg_ctx* ctx, K kernel, size_t lds, uint64_t want, int b
 constexpr size_t kLdsPerCu = 160 * 1024;
 inline size_t scan_lds_per_wave(uint32_t w) { return (((size_t)w * kWave + 1) / 2 + kScanBuf) * sizeof(uint64_t); }
 // the register scan (k_scan_reg) when its window fits in registers
-inline bool use_scan_reg(const mg_ctx* ctx) { return ctx->scan_reg && ctx->w <= (uint32_t)kRegW; }
+inline bool use_scan_reg_w(const mg_ctx* ctx) { return ctx->w <= (uint32_t)kRegW; }
+inline bool use_scan_reg(const mg_ctx* ctx) { return (ctx->scan_reg || ctx->join_P) && use_scan_reg_w(ctx); }
 inline uint32_t scan_block_waves(const mg_ctx* ctx);
 inline size_t scan_lds(const mg_ctx* ctx);
 inline uint32_t scan_wpb(uint32_t w) {
@@ -2192,8 +2588,10 @@ struct LaunchScan {
     if (flat) {
       // SoA output for the bucket sort: ~2 J / (w + 1) + 1 runs per read, sized
       // with 20 % slack (or the exact need after an overflow)
+      // (join mode: + the four key records of every read)
       const uint64_t est = ctx->flat_cap_opt ? ctx->flat_cap_opt
-                                             : (a_hi - a_lo) * (2 * J / (ctx->w + 1) + 2) * 6 / 5 + 4096;
+                                             : (a_hi - a_lo) * (2 * J / (ctx->w + 1) + 2 + (ctx->join_P ? 4 : 0)) * 6 / 5 +
+                                                   4096;
       const uint64_t cap = std::max<uint64_t>(ctx->flat_need, est);
       if (cap > ctx->sk_cap || (ctx->flat_cap_opt && cap < ctx->sk_cap)) {
         for (int b = 0; b < 2; ++b) {
@@ -2217,7 +2615,15 @@ struct LaunchScan {
       sp.flat_meta = ctx->d_sm[0];
       sp.flat_cursor = ctx->d_flat_cursor;
       sp.flat_cap = ctx->sk_cap;
-      packable_runs(ctx, &ctx->pack_a, &ctx->pack_w);
+      if (ctx->join_P && index) {  // join records (runs + keys), no cells
+        ctx->pack_a = ctx->pack_w = 0;
+        sp.join_P = ctx->join_P;
+        sp.join_A = ctx->join_A;
+        sp.join_QB = ctx->join_QB;
+        sp.join_WB = ctx->join_WB;
+      } else {
+        packable_runs(ctx, &ctx->pack_a, &ctx->pack_w);
+      }
       sp.pack_a = ctx->pack_a;
       sp.pack_w = ctx->pack_w;
     } else {
@@ -2501,7 +2907,7 @@ void mg_destroy(mg_ctx* ctx) {
                   ctx->d_compact, ctx->d_runs, ctx->d_run_cnt, ctx->d_keyrec, ctx->d_blk, ctx->d_flat_cnt, ctx->d_cand, ctx->d_cand_cnt, ctx->d_freq,
                   ctx->d_sk[0], ctx->d_sk[1], ctx->d_sm[0], ctx->d_sm[1], ctx->d_sort_tmp, ctx->d_run_off,
                   ctx->d_flat_cursor, ctx->d_kb[0], ctx->d_kb[1], ctx->d_ke[0], ctx->d_ke[1], ctx->d_key0, ctx->d_holes,
-                  ctx->d_digest};
+                  ctx->d_digest, ctx->d_bnd, ctx->d_mid, ctx->d_queue};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   for (auto& e : ctx->ev)
@@ -2644,6 +3050,19 @@ int mg_set_option(mg_ctx* ctx, const char* name, int64_t value) {
     ctx->sorted_state = 0;
     return 0;
   }
+  if (!strcmp(name, "join_parts_log2")) {  // 0: auto (~2.5k keys per partition); tests force few partitions
+    if (value < 0 || value > 16) return set_err(ctx, "join_parts_log2 out of range [0,16]");
+    ctx->join_P_opt = (int)value;
+    ctx->index_ready = false;
+    ctx->join_ready = false;
+    return 0;
+  }
+  if (!strcmp(name, "join")) {  // 1 (default): partitioned join (k_join) when it applies; 0: cell index + probe
+    ctx->join = value != 0;
+    ctx->index_ready = false;
+    ctx->join_ready = false;
+    return 0;
+  }
   if (!strcmp(name, "scan_reg")) {  // 1 (default): register sliding minimum when w <= 32; 0: LDS version
     ctx->scan_reg = value != 0;
     ctx->scan_state = 0;
@@ -2718,7 +3137,8 @@ namespace {
 // Index geometry shared by the fused and the exchange paths: h, m, w, the
 // directory size 2^nb (same on every rank: it depends on the global read
 // count only) and this rank's bucket range; allocates and clears the local cells.
-int setup_index(mg_ctx* ctx, uint32_t min_overlap, uint32_t seed_k) {
+int setup_cells(mg_ctx* ctx);
+int setup_index(mg_ctx* ctx, uint32_t min_overlap, uint32_t seed_k, bool cells = true) {
   MG_TRY(hipSetDevice(ctx->device));
   if (min_overlap < 2) return set_err(ctx, "min_overlap must be >= 2");
   const uint32_t h = min_overlap - 1;  // HashTable.cpp:54
@@ -2745,13 +3165,42 @@ int setup_index(mg_ctx* ctx, uint32_t min_overlap, uint32_t seed_k) {
   const uint64_t NB = 1ull << nbl, P = ctx->nranks, r = ctx->rank;
   ctx->cell_lo = (r * NB + P - 1) / P;
   ctx->cell_n = ((r + 1) * NB + P - 1) / P - ctx->cell_lo;
-  MG_TRY(ensure(&ctx->d_cells, &ctx->cells_cap, ctx->cell_n * kCell));
-  MG_TRY(hipMemsetAsync(ctx->d_cells, 0xFF, ctx->cell_n * kCell * sizeof(uint64_t), ctx->stream));  // kEmpty
+  ctx->cells_ready = false;
+  ctx->join_ready = false;
+  if (cells && setup_cells(ctx)) return -1;
   ctx->index_ready = false;
   ctx->contained_done = false;
   ctx->super_any = false;
   ctx->key0_ready = false;  // set by the fused build when it writes the o = 0 keys
   return 0;
+}
+
+// the (cleared) cell table of this rank's bucket range
+int setup_cells(mg_ctx* ctx) {
+  MG_TRY(ensure(&ctx->d_cells, &ctx->cells_cap, ctx->cell_n * kCell));
+  MG_TRY(hipMemsetAsync(ctx->d_cells, 0xFF, ctx->cell_n * kCell * sizeof(uint64_t), ctx->stream));  // kEmpty
+  return 0;
+}
+
+// Partitioned join geometry (option "join"): the unsharded fused
+// path with a register scan (w <= kRegW) whose record fields fit 12 bytes.
+// P = partition bits, chosen for ~2.5k keys per partition (one LDS table fill).
+bool join_geometry(mg_ctx* ctx) {
+  auto bits = [](uint64_t x) { int b = 0; while (x) { ++b; x >>= 1; } return b; };
+  ctx->join_P = 0;
+  if (!ctx->join || ctx->nranks != 1 || !ctx->overlap_scan || !use_scan_reg_w(ctx) || ctx->maxw > 32) return false;
+  const int A = std::max(1, bits(ctx->n));  // read index < 2^A
+  const int WB = bits(ctx->w - 1), QB = WB;
+  const double keys = 4.0 * (double)std::max<uint64_t>(ctx->n, 1);
+  int P = (int)std::lround(std::log2(std::max(2.0, keys / 2500.0)));
+  P = std::min(16, std::max(1, P));
+  if (ctx->join_P_opt) P = ctx->join_P_opt;  // option "join_parts_log2" (tests: force multi-chunk partitions)
+  if (A > 32 || A + 12 + 2 * WB + P > 64 || A + 4 + QB + P > 64) return false;
+  ctx->join_P = P;
+  ctx->join_A = A;
+  ctx->join_QB = QB;
+  ctx->join_WB = WB;
+  return true;
 }
 
 // this rank's source reads in exchange mode: [floor(r N / P), floor((r+1) N / P))
@@ -2926,7 +3375,8 @@ struct LaunchScanAll {
     const uint32_t wpb = scan_block_waves(ctx);
     const uint64_t groups = (ctx->n + kWave - 1) / kWave;
     const uint32_t sgrid = scan_resident<W>(ctx, index, (groups + wpb - 1) / wpb);
-    return LaunchScan<W>::run(ctx, true, 0, ctx->n, sgrid, false, st, true, index, ctx->sort_runs);
+    return LaunchScan<W>::run(ctx, true, 0, ctx->n, sgrid, false, st, true, index,
+                              ctx->sort_runs || (index && ctx->join_P));
   }
 };
 
@@ -2961,7 +3411,7 @@ int settle_flat(mg_ctx* ctx, bool* again) {
     MG_TRY(hipMemcpyAsync(ctx->d_holes, ctx->holes_host.data(), nh * sizeof(uint64_t), hipMemcpyHostToDevice,
                           ctx->stream));
     hipLaunchKernelGGL(k_fill_holes, dim3((uint32_t)nh), dim3(kBlock), 0, ctx->stream, ctx->d_holes, ctx->d_sk[0],
-                       ctx->d_sm[0], ctx->pack_a ? 1 : 0);
+                       ctx->d_sm[0], (ctx->pack_a || ctx->join_P) ? 1 : 0);
     MG_TRY(hipGetLastError());
   }
   ctx->n_flat = n;
@@ -3119,6 +3569,135 @@ int probe_shared(mg_ctx* ctx, bool contain) {
 }
 }  // namespace
 
+namespace {
+// ------------------------------------------------------ join host path ---
+// k_scan_reg<INDEX> with join records -> settle (overflow: resize, rerun) ->
+// radix sort by (partition, type) -> partition bounds.
+int build_join(mg_ctx* ctx) {
+  ctx->join_ready = false;
+  for (int attempt = 0;; ++attempt) {
+    if (attempt == 3) return set_err(ctx, "join record buffers overflow after resize");
+    if (ctx->n && dispatch_w<LaunchScanAll>(ctx->maxw, ctx, ctx->stream, true))
+      return set_err(ctx, "index build launch failed");
+    bool again = false;
+    if (ctx->n) {
+      if (settle_flat(ctx, &again)) return -1;
+    } else {
+      ctx->n_flat = 0;
+    }
+    if (!again) break;
+  }
+  ctx->shared_scan_ms = ctx->n ? elapsed(ctx->ev[6], ctx->ev[7]) : 0.f;
+  const uint64_t n = ctx->n_flat;
+  if (n > 0x7FFFFFFFull) return set_err(ctx, "join: more than 2^31 records");
+  const unsigned bits = (unsigned)ctx->join_P + 2;
+  MG_TRY(hipEventRecord(ctx->ev[12], ctx->stream));
+  int sel = 0;
+  if (n) {
+    auto sort = [&](void* tmp, size_t& tb) -> hipError_t {
+      rocprim::double_buffer<uint32_t> keys(reinterpret_cast<uint32_t*>(ctx->d_sk[0]),
+                                            reinterpret_cast<uint32_t*>(ctx->d_sk[1]));
+      rocprim::double_buffer<uint64_t> vals(ctx->d_sm[0], ctx->d_sm[1]);
+      hipError_t e = rocprim::radix_sort_pairs(tmp, tb, keys, vals, (unsigned int)n, 0u, bits, ctx->stream);
+      sel = keys.current() == reinterpret_cast<uint32_t*>(ctx->d_sk[0]) ? 0 : 1;
+      if (e == hipSuccess && tmp && (vals.current() == ctx->d_sm[0] ? 0 : 1) != sel) e = hipErrorUnknown;
+      return e;
+    };
+    size_t tb = 0;
+    MG_TRY(sort(nullptr, tb));
+    if (tb > ctx->sort_tmp_cap) {
+      if (ctx->d_sort_tmp) (void)hipFree(ctx->d_sort_tmp);
+      ctx->d_sort_tmp = nullptr;
+      MG_TRY(hipMalloc(&ctx->d_sort_tmp, tb));
+      ctx->sort_tmp_cap = tb;
+    }
+    tb = ctx->sort_tmp_cap;
+    MG_TRY(sort(ctx->d_sort_tmp, tb));
+  }
+  ctx->sk_sel = sel;
+  const uint32_t nparts = 1u << ctx->join_P;
+  MG_TRY(ensure(&ctx->d_bnd, &ctx->bnd_cap, (size_t)nparts + 1));
+  MG_TRY(ensure(&ctx->d_mid, &ctx->mid_cap, (size_t)nparts));
+  const uint32_t targets = 2 * nparts + 1;
+  hipLaunchKernelGGL(k_join_bounds, dim3((targets + kBlock - 1) / kBlock), dim3(kBlock), 0, ctx->stream,
+                     reinterpret_cast<const uint32_t*>(ctx->d_sk[sel]), n, ctx->join_P, ctx->d_bnd, ctx->d_mid, nparts);
+  MG_TRY(hipGetLastError());
+  MG_TRY(hipEventRecord(ctx->ev[13], ctx->stream));
+  ctx->join_ready = true;
+  return 0;
+}
+
+template <int W>
+struct LaunchJoin {
+  static int run(mg_ctx* ctx, bool contain) {
+    JoinParams jp{};
+    jp.words = ctx->d_words;
+    jp.len = ctx->d_len;
+    jp.h = (int)ctx->h;
+    jp.P = ctx->join_P;
+    jp.A = ctx->join_A;
+    jp.QB = ctx->join_QB;
+    jp.WB = ctx->join_WB;
+    jp.k32 = reinterpret_cast<const uint32_t*>(ctx->d_sk[ctx->sk_sel]);
+    jp.val = ctx->d_sm[ctx->sk_sel];
+    jp.bnd = ctx->d_bnd;
+    jp.mid = ctx->d_mid;
+    jp.nparts = 1u << ctx->join_P;
+    jp.queue = ctx->d_queue;
+    const bool sup = !contain && ctx->contained_done && ctx->super_any;
+    jp.super = sup ? ctx->d_super : nullptr;
+    jp.src_super = sup ? ctx->d_super : nullptr;
+    jp.src_lo = contain ? 0 : ctx->read_lo;
+    jp.src_hi = contain ? 0 : (ctx->read_hi ? std::min(ctx->read_hi, ctx->n) : 0);
+    jp.superkey = ctx->superkey;
+    jp.prefix_queries = (contain && ctx->prefix_contain) ? 1 : 0;
+    jp.contain_even = jp.prefix_queries;
+    jp.uniform_len = ctx->minlen == ctx->maxlen ? (int)ctx->maxlen : 0;
+    jp.halving_low = ctx->halving_low ? 1 : 0;
+    jp.stats = contain ? nullptr : (ctx->stats ? ctx->d_stats : nullptr);
+    const uint32_t grid = contain ? resident_blocks(ctx, k_join<W, true>, kJoinLds, jp.nparts, kJoinBlock)
+                                  : resident_blocks(ctx, k_join<W, false>, kJoinLds, jp.nparts, kJoinBlock);
+    ctx->nreg = (uint64_t)grid * kJoinWaves;  // join wavefronts = row regions
+    jp.rows = ctx->d_rows;
+    jp.reg_cnt = ctx->d_seg;
+    jp.reg_cap = contain ? 0 : ctx->rows_cap / ctx->nreg;
+    if (hipMemsetAsync(ctx->d_queue, 0, sizeof(unsigned int), ctx->stream) != hipSuccess) return -1;
+    if (contain)
+      hipLaunchKernelGGL((k_join<W, true>), dim3(grid), dim3(kJoinBlock), kJoinLds, ctx->stream, jp);
+    else
+      hipLaunchKernelGGL((k_join<W, false>), dim3(grid), dim3(kJoinBlock), kJoinLds, ctx->stream, jp);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+  }
+};
+
+// one join pass (containment or discovery); discovery rows are settled
+// (resized and rerun on overflow)
+int probe_join(mg_ctx* ctx, bool contain) {
+  if (!ctx->d_queue) MG_TRY(hipMalloc(&ctx->d_queue, sizeof(unsigned int)));
+  for (int attempt = 0; attempt < 3; ++attempt) {
+    ctx->nreg = 0;
+    MG_TRY(hipEventRecord(ctx->ev[8], ctx->stream));
+    if (dispatch_w<LaunchJoin>(ctx->maxw, ctx, contain)) return set_err(ctx, "join launch failed");
+    MG_TRY(hipEventRecord(ctx->ev[9], ctx->stream));
+    if (contain) return 0;
+    bool again = false;
+    if (settle_rows(ctx, &again)) return -1;
+    if (!again) return 0;
+    if (ctx->stats) MG_TRY(hipMemsetAsync(ctx->d_stats, 0, kSegs * 4 * sizeof(unsigned long long), ctx->stream));
+  }
+  return set_err(ctx, "row buffers overflow after resize");
+}
+
+// the cell table for getListOfReads when the index was built as join records
+int ensure_cells(mg_ctx* ctx) {
+  if (ctx->cells_ready) return 0;
+  if (setup_cells(ctx)) return -1;
+  if (ctx->n && dispatch_w<LaunchIndex>(ctx->maxw, ctx)) return set_err(ctx, "cell index launch failed");
+  ctx->cells_ready = true;
+  return 0;
+}
+}  // namespace
+
 extern "C" {
 
 // Sorted index build, after k_scan<INDEX> wrote the 4N key records to
@@ -3161,10 +3740,24 @@ int mg_build_index(mg_ctx* ctx, uint32_t min_overlap, uint32_t seed_k) {
   if (!ctx) return -1;
   MG_TRY(hipSetDevice(ctx->device));
   MG_TRY(hipEventRecord(ctx->ev[0], ctx->stream));
-  if (setup_index(ctx, min_overlap, seed_k)) return -1;
+  if (setup_index(ctx, min_overlap, seed_k, false)) return -1;
+  const bool join = join_geometry(ctx);
+  if (!join && setup_cells(ctx)) return -1;
   ctx->scan_state = 0;
   ctx->sorted_state = 0;
   ctx->t.sort_ms = 0.f;
+  if (join) {
+    // partitioned join: one register scan writes runs + keys as join records,
+    // one radix sort by partition, partition bounds (no cell table)
+    ctx->key0_ready = false;
+    if (build_join(ctx)) return -1;
+    MG_TRY(hipEventRecord(ctx->ev[1], ctx->stream));
+    MG_TRY(hipEventSynchronize(ctx->ev[1]));
+    ctx->t.index_ms = elapsed(ctx->ev[0], ctx->ev[1]);
+    ctx->t.sort_ms = elapsed(ctx->ev[12], ctx->ev[13]);
+    ctx->index_ready = true;
+    return 0;
+  }
   if (shared_scan(ctx)) {
     // one pass over the reads: the index inserts ride on the window scan
     // (k_scan<INDEX>), whose runs then serve the containment and discovery
@@ -3192,6 +3785,7 @@ int mg_build_index(mg_ctx* ctx, uint32_t min_overlap, uint32_t seed_k) {
   ctx->t.index_ms = elapsed(ctx->ev[0], ctx->ev[1]);
   ctx->shared_scan_ms = (shared_scan(ctx) && ctx->n) ? elapsed(ctx->ev[6], ctx->ev[7]) : 0.f;
   ctx->index_ready = true;
+  ctx->cells_ready = true;
   return 0;
 }
 
@@ -3216,10 +3810,14 @@ int mg_mark_contained(mg_ctx* ctx, uint32_t* super_out) {
     // sharded contexts still need the full superReadID vector: run over all
     // buckets (the containment pass is small, only for mixed lengths)
     if (ctx->nranks > 1) return set_err(ctx, "containment with a bucket-sharded index: use the exchange mode");
-    if (!shared_scan(ctx)) ctx->key0_ready = false;  // only the shared scan writes the o = 0 keys
-    if (shared_scan(ctx) ? probe_shared(ctx, true) : run_discover(ctx, true)) return -1;
-    if (ctx->key0_ready && dispatch_w<LaunchPrefixContain>(ctx->maxw, ctx))
-      return set_err(ctx, "prefix containment launch failed");
+    if (ctx->join_ready) {  // the join's prefix queries cover offset-0 containments
+      if (probe_join(ctx, true)) return -1;
+    } else {
+      if (!shared_scan(ctx)) ctx->key0_ready = false;  // only the shared scan writes the o = 0 keys
+      if (shared_scan(ctx) ? probe_shared(ctx, true) : run_discover(ctx, true)) return -1;
+      if (ctx->key0_ready && dispatch_w<LaunchPrefixContain>(ctx->maxw, ctx))
+        return set_err(ctx, "prefix containment launch failed");
+    }
     if (ctx->n)
       hipLaunchKernelGGL(k_super_finalize, dim3((uint32_t)((ctx->n + kBlock - 1) / kBlock)), dim3(kBlock), 0,
                          ctx->stream, ctx->d_superkey, ctx->n, ctx->d_super, ctx->d_any);
@@ -3254,7 +3852,8 @@ int mg_find_overlaps(mg_ctx* ctx, uint64_t* n_rows) {
                         std::min(ctx->read_lo, ctx->n);
   if (ensure_rows(ctx, nsrc)) return -1;
   MG_TRY(hipEventRecord(ctx->ev[4], ctx->stream));
-  if (shared_scan(ctx) ? probe_shared(ctx, false) : run_discover(ctx, false)) return -1;
+  if (ctx->join_ready ? probe_join(ctx, false) : shared_scan(ctx) ? probe_shared(ctx, false) : run_discover(ctx, false))
+    return -1;
   MG_TRY(hipEventRecord(ctx->ev[5], ctx->stream));
   MG_TRY(hipEventSynchronize(ctx->ev[5]));
   // the kernels' own events bracket the last launches (a resize retry included
@@ -3268,9 +3867,13 @@ int mg_find_overlaps(mg_ctx* ctx, uint64_t* n_rows) {
     ctx->t.probe_ms = shared_scan(ctx) ? elapsed(ctx->ev[8], ctx->ev[9]) : elapsed(ctx->ev[7], ctx->ev[5]);
     ctx->t.verify_ms = 0.f;
   }
-  ctx->t.sort_ms = (shared_scan(ctx) && ctx->sort_runs && ctx->sorted_state == 2)
-                       ? elapsed(ctx->ev[12], ctx->ev[13]) : 0.f;
-  ctx->t.overlap_ms = (shared_scan(ctx) ? 0.f : ctx->t.scan_ms) + ctx->t.sort_ms + ctx->t.probe_ms + ctx->t.verify_ms;
+  if (ctx->join_ready)  // the sort ran in mg_build_index (part of index_ms)
+    ctx->t.sort_ms = elapsed(ctx->ev[12], ctx->ev[13]);
+  else
+    ctx->t.sort_ms = (shared_scan(ctx) && ctx->sort_runs && ctx->sorted_state == 2)
+                         ? elapsed(ctx->ev[12], ctx->ev[13]) : 0.f;
+  ctx->t.overlap_ms = (shared_scan(ctx) ? 0.f : ctx->t.scan_ms) + (ctx->join_ready ? 0.f : ctx->t.sort_ms) +
+                      ctx->t.probe_ms + ctx->t.verify_ms;
   read_stats(ctx, nsrc);
   // device wall of the step: index build start .. last discovery kernel end
   ctx->t.total_ms = shared_scan(ctx) ? elapsed(ctx->ev[0], ctx->ev[5])
@@ -3313,8 +3916,8 @@ int mg_insert_keys(mg_ctx* ctx, const void* recs, uint64_t n) {
   MG_TRY(hipEventRecord(ctx->ev[1], ctx->stream));
   MG_TRY(hipEventSynchronize(ctx->ev[1]));
   ctx->t.index_ms = elapsed(ctx->ev[0], ctx->ev[1]);
-  ctx->shared_scan_ms = (shared_scan(ctx) && ctx->n) ? elapsed(ctx->ev[6], ctx->ev[7]) : 0.f;
   ctx->index_ready = true;
+  ctx->cells_ready = true;
   return 0;
 }
 
@@ -3502,6 +4105,7 @@ int mg_lookup_key(mg_ctx* ctx, const char* key, uint32_t key_len, uint64_t* out,
   if (n_out) *n_out = 0;
   if (key_len != ctx->h) return 0;  // no key of another length exists
   if (ctx->nranks > 1) return set_err(ctx, "lookup on a bucket-sharded index");
+  if (ensure_cells(ctx)) return -1;  // join builds keep no cell table until a lookup asks for one
   const int qwords = (int)((key_len + 31) / 32);
   std::vector<uint64_t> q(qwords + 1, 0);
   for (uint32_t i = 0; i < key_len; i++) {

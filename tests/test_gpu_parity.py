@@ -186,11 +186,7 @@ def test_random_sets_vs_oracle(engine, case):
     ds = Dataset.from_codes(c, L, l)
     od = OracleDataset.from_strings(seqs, l)
     assert ds.num_unique == od.num_unique
-    engine.set_option("scan_reg", 1)
-    try:
-        rows, sup = gpu_rows(engine, ds, l, k=k)
-    finally:
-        engine.set_option("scan_reg", 0)
+    rows, sup = gpu_rows(engine, ds, l, k=k)
     orows, osup, _, _ = od.overlaps(l)
     assert np.array_equal(sup.astype(np.uint64), osup)
     assert np.array_equal(rows_to_tuples(rows), sorted_tuples(orows))
@@ -339,6 +335,7 @@ def test_split_probe_path(name):
     meta = load_meta(name)
     ds = Dataset.from_files([fixture_input(name)], meta["l"])
     e = OverlapEngine(0)
+    e.set_option("join", 0)
     e.set_option("split", 1)
     rows, sup = gpu_rows(e, ds, meta["l"])
     e.close()
@@ -534,6 +531,7 @@ def test_sorted_runs_path(name):
     meta = load_meta(name)
     ds = Dataset.from_files([fixture_input(name)], meta["l"])
     e = OverlapEngine(0)
+    e.set_option("join", 0)
     e.set_option("sort_runs", 1)
     rows, sup = gpu_rows(e, ds, meta["l"])
     e.close()
@@ -549,6 +547,7 @@ def test_sorted_runs_flat_overflow(name):
     ds = Dataset.from_files([fixture_input(name)], meta["l"])
     e = OverlapEngine(0)
     e.set_option("sort_runs", 1)
+    e.set_option("join", 0)
     e.set_option("flat_cap", 700)
     rows, sup = gpu_rows(e, ds, meta["l"])
     e.close()
@@ -563,6 +562,7 @@ def test_sorted_runs_16b_records(name):
     meta = load_meta(name)
     ds = Dataset.from_files([fixture_input(name)], meta["l"])
     e = OverlapEngine(0)
+    e.set_option("join", 0)
     e.set_option("pack_runs", 0)
     rows, sup = gpu_rows(e, ds, meta["l"])
     e.close()
@@ -576,6 +576,7 @@ def test_unsorted_runs_path(name):
     meta = load_meta(name)
     ds = Dataset.from_files([fixture_input(name)], meta["l"])
     e = OverlapEngine(0)
+    e.set_option("join", 0)
     e.set_option("sort_runs", 0)
     rows, sup = gpu_rows(e, ds, meta["l"])
     e.close()
@@ -591,6 +592,7 @@ def test_sorted_index_path(name, nb):
     meta = load_meta(name)
     ds = Dataset.from_files([fixture_input(name)], meta["l"])
     e = OverlapEngine(0)
+    e.set_option("join", 0)
     e.set_option("sorted_index", 1)
     rows, sup = gpu_rows(e, ds, meta["l"], nb_log2=nb)
     e.close()
@@ -613,13 +615,15 @@ def test_prefix_contain_off(name):
         l = meta["l"]
         ds = Dataset.from_files([fixture_input(name)], l)
         want_rows, want_sup = golden_rows(name), meta["super"]
-    for flag in (0, 1):
-        e = OverlapEngine(0)
-        e.set_option("prefix_contain", flag)
-        rows, sup = gpu_rows(e, ds, l)
-        e.close()
-        assert np.array_equal(rows_to_tuples(rows), want_rows), flag
-        assert {str(i): int(x) for i, x in enumerate(sup) if x} == want_sup, flag
+    for join in (0, 1):
+        for flag in (0, 1):
+            e = OverlapEngine(0)
+            e.set_option("join", join)
+            e.set_option("prefix_contain", flag)
+            rows, sup = gpu_rows(e, ds, l)
+            e.close()
+            assert np.array_equal(rows_to_tuples(rows), want_rows), (join, flag)
+            assert {str(i): int(x) for i, x in enumerate(sup) if x} == want_sup, (join, flag)
 
 
 @pytest.mark.parametrize("name", FIXTURES)
@@ -657,6 +661,7 @@ def test_scan_inside_probe_path(name):
     meta = load_meta(name)
     ds = Dataset.from_files([fixture_input(name)], meta["l"])
     e = OverlapEngine(0)
+    e.set_option("join", 0)
     e.set_option("overlap_scan", 0)
     rows, sup = gpu_rows(e, ds, meta["l"])
     e.close()
@@ -681,17 +686,69 @@ def test_scan_register_path(name):
 @pytest.mark.parametrize("l,k", [(33, 1), (40, 8), (50, 17), (50, 18), (20, 19), (50, 31), (60, 32)])
 def test_register_scan_window_extremes(engine, l, k):
     """w = l - k = 32 (the register scan's largest window), 33 (falls back to the
-    LDS scan), 1 and typical ones, against the oracle on mixed lengths
-    (containment, all four keys, runs crossing block edges)."""
+    LDS scan and the cell index), 1 and typical ones, against the oracle on mixed
+    lengths (containment, all four keys, runs crossing block edges), through the
+    join (default) and through the cell index with the register scan."""
     c, L = synth.uniform_read_set(3000, 0, 15000, seed=120 + k, lo=l + 1, hi=l + 90)
     seqs = synth.codes_to_strings(c, L)
     ds = Dataset.from_codes(c, L, l)
     od = OracleDataset.from_strings(seqs, l)
-    engine.set_option("scan_reg", 1)
+    orows, osup, _, _ = od.overlaps(l)
+    for join in (1, 0):
+        engine.set_option("join", join)
+        engine.set_option("scan_reg", 1)
+        try:
+            rows, sup = gpu_rows(engine, ds, l, k=k)
+        finally:
+            engine.set_option("scan_reg", 0)
+            engine.set_option("join", 1)
+        assert np.array_equal(sup.astype(np.uint64), osup), join
+        assert np.array_equal(rows_to_tuples(rows), sorted_tuples(orows)), join
+
+
+@pytest.mark.parametrize("name", FIXTURES)
+def test_cell_probe_path(name):
+    """option join = 0: the cell index (CAS inserts inside the scan) + bucket-sorted
+    run probe instead of the partitioned join; same rows and superReadIDs."""
+    meta = load_meta(name)
+    ds = Dataset.from_files([fixture_input(name)], meta["l"])
+    e = OverlapEngine(0)
+    e.set_option("join", 0)
+    rows, sup = gpu_rows(e, ds, meta["l"])
+    e.close()
+    assert np.array_equal(rows_to_tuples(rows), golden_rows(name))
+    assert {str(i): int(s) for i, s in enumerate(sup) if s} == meta["super"]
+
+
+@pytest.mark.parametrize("name,parts", [("highdup", 1), ("tandem", 1), ("mixed", 1), ("branchy", 1), ("small", 3),
+                                        ("highdup", 12)])
+def test_join_forced_partitions(name, parts):
+    """join_parts_log2: two partitions hold thousands of keys each, so the LDS
+    table is filled in several chunks and the runs (and the containment prefix
+    queries) are streamed once per chunk; or many nearly empty partitions."""
+    meta = load_meta(name)
+    ds = Dataset.from_files([fixture_input(name)], meta["l"])
+    e = OverlapEngine(0)
+    e.set_option("join_parts_log2", parts)
+    rows, sup = gpu_rows(e, ds, meta["l"])
+    e.close()
+    assert np.array_equal(rows_to_tuples(rows), golden_rows(name))
+    assert {str(i): int(s) for i, s in enumerate(sup) if s} == meta["super"]
+
+
+def test_join_chunked_containment_vs_oracle(engine):
+    """Mixed lengths, many nested prefixes, 2 partitions: containment queries
+    across key chunks of one partition."""
+    seqs, l = prefix_reads(seed=7) * 1, 40
+    c, L = synth.metagenome_read_set(20000, 100, 250, n_genomes=20, total_len=400000, seed=57)
+    seqs = seqs + synth.codes_to_strings(c, L)
+    ds = Dataset.from_strings(seqs, l)
+    od = OracleDataset.from_strings(seqs, l)
+    engine.set_option("join_parts_log2", 1)
     try:
-        rows, sup = gpu_rows(engine, ds, l, k=k)
+        rows, sup = gpu_rows(engine, ds, l, k=0)
     finally:
-        engine.set_option("scan_reg", 0)
+        engine.set_option("join_parts_log2", 0)
     orows, osup, _, _ = od.overlaps(l)
     assert np.array_equal(sup.astype(np.uint64), osup)
     assert np.array_equal(rows_to_tuples(rows), sorted_tuples(orows))
