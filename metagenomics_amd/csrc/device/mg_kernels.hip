@@ -1026,6 +1026,32 @@ __global__ __launch_bounds__(kBlock) void k_scan_reg(ScanParams p) {
       for (int k = 0; k <= MAXW; ++k) rw[k] = k < kRw ? gs[k] : 0;
     }
     const uint64_t a0 = p.a_lo + grp * kWave;
+    // INDEX, reverse-strand keys first (before the scan's registers are live):
+    // o = 3 (R[n-h, n) = rc F[0, h): m-mer i = rc of F's at t = w-1-i) and
+    // o = 2 (R[0, h) = rc F[n-h, n): m-mer i = rc of F's at t = n-m-i), both
+    // rolled towards smaller t, one base per step
+    uint32_t kb3 = 0xFFFFFFFFu, kb2 = 0xFFFFFFFFu;
+    uint64_t mb3 = 0, mb2 = 0;
+    if (INDEX && n) {
+      const uint64_t Aw = ext_reg<MAXW>(rw, n - h);                      // F[n-h, n-h+32)
+      uint64_t r3 = rc_word(funnel(rw[0], rw[1], 2 * (w - 1))) & mmask;  // rc(F[w-1, w-1+m))
+      uint64_t r2 = rc_word(ext_reg<MAXW>(rw, n - m)) & mmask;          // rc(F[n-m, n))
+      for (int i = 0; i < w; ++i) {
+        const uint32_t k3 = order_key(r3) | (uint32_t)i, k2 = order_key(r2) | (uint32_t)i;
+        if (k3 < kb3) { kb3 = k3; mb3 = r3; }
+        if (k2 < kb2) { kb2 = k2; mb2 = r2; }
+        const int t3 = w - 2 - i;  // F base entering the rc m-mer at t - 1 (both keys: offset w-2-i)
+        if (t3 >= 0) {
+          r3 = ((r3 << 2) | (3u - ((rw[0] >> (62 - 2 * t3)) & 3u))) & mmask;
+          r2 = ((r2 << 2) | (3u - ((Aw >> (62 - 2 * t3)) & 3u))) & mmask;  // F[n-m-1-i] = F[n-h + w-2-i]
+        }
+      }
+    }
+    if (INDEX) {  // emit them now (every lane: the flat-chunk state is wavefront-uniform)
+      const uint64_t v2 = mix64(mb2), v3 = mix64(mb3);
+      st.emit_ready(n > 0, join_k32(v2, p.join_P, 0u), join_key_val((uint32_t)a, 2, (int)(kb2 & 1023u), v2, p));
+      st.emit_ready(n > 0, join_k32(v3, p.join_P, 0u), join_key_val((uint32_t)a, 3, (int)(kb3 & 1023u), v3, p));
+    }
     uint32_t S[kRegW + 1];
 #pragma unroll
     for (int u = 0; u <= kRegW; ++u) S[u] = 0xFFFFFFFFu;
@@ -1076,70 +1102,15 @@ __global__ __launch_bounds__(kBlock) void k_scan_reg(ScanParams p) {
     }
     st.put(tend >= 0, run_meta(a, last, jlo, J));  // each read's last run
     while (st.nbuf) st.flush(st.nbuf < (uint32_t)kWave ? st.nbuf : (uint32_t)kWave, rw, a0);
-    if constexpr (INDEX) {
-      uint32_t jk[4] = {0, 0, 0, 0};
-      uint64_t jv[4] = {0, 0, 0, 0};
+    if constexpr (INDEX) {  // (join mode only: the cell index is built by k_scan / k_index_build)
+      const int p0 = (int)(kw0 & 1023u), p1 = (int)(kw1 & 1023u);
+      uint64_t v0 = 0, v1 = 0;
       if (n) {
-        // keys o = 3 (R[n-h, n) = rc F[0, h): m-mer i = rc of F's at t = w-1-i) and
-        // o = 2 (R[0, h) = rc F[n-h, n): m-mer i = rc of F's at t = n-m-i), both
-        // rolled towards smaller t, one base per step
-        const uint64_t A = ext_reg<MAXW>(rw, n - h);  // F[n-h, n-h+32)
-        uint64_t r3 = rc_word(funnel(rw[0], rw[1], 2 * (w - 1))) & mmask;  // rc(F[w-1, w-1+m))
-        uint64_t r2 = rc_word(ext_reg<MAXW>(rw, n - m)) & mmask;             // rc(F[n-m, n))
-        uint32_t kb3 = 0xFFFFFFFFu, kb2 = 0xFFFFFFFFu;
-        uint64_t mb3 = 0, mb2 = 0;
-        for (int i = 0; i < w; ++i) {
-          const uint32_t k3 = order_key(r3) | (uint32_t)i, k2 = order_key(r2) | (uint32_t)i;
-          if (k3 < kb3) { kb3 = k3; mb3 = r3; }
-          if (k2 < kb2) { kb2 = k2; mb2 = r2; }
-          if (i + 1 < w) {
-            const int t3 = w - 2 - i;  // F base entering the rc m-mer at t - 1
-            const uint64_t b3 = (rw[0] >> (62 - 2 * t3)) & 3u;
-            const uint64_t b2 = (A >> (62 - 2 * t3)) & 3u;  // F[n-m-1-i] = F[n-h + (w-2-i)]
-            r3 = ((r3 << 2) | (3u - b3)) & mmask;
-            r2 = ((r2 << 2) | (3u - b2)) & mmask;
-          }
-        }
-        const int p0 = (int)(kw0 & 1023u), p1 = (int)(kw1 & 1023u);
-        const uint64_t mb0 = funnel(rw[0], rw[1], p0 << 1) >> msh;  // p0 < w <= 32
-        const uint64_t mb1 = ext_reg<MAXW>(rw, p1) >> msh;
-        const uint64_t nbm = (1ULL << p.nb_log2) - 1;
-        const uint64_t mb[4] = {mb0, mb1, mb2, mb3};
-        const int qq[4] = {p0, p1 - (n - h), (int)(kb2 & 1023u), (int)(kb3 & 1023u)};
-        if (p.join_P) {  // partitioned join: the keys become join records (emitted below), no cells
-#pragma unroll
-          for (int o = 0; o < 4; ++o) {
-            const uint64_t v = mix64(mb[o]);
-            jk[o] = join_k32(v, p.join_P, 0u);
-            jv[o] = join_key_val((uint32_t)a, o, qq[o], v, p);
-          }
-        } else {
-#pragma unroll
-        for (int o = 0; o < 4; ++o) {
-          const uint64_t v = mix64(mb[o]);
-          const unsigned long long e = make_entry(v, p.nb_log2, qq[o], o, (uint32_t)a);
-          if (o == 0 && p.key0) p.key0[a] = (v & ((1ULL << 50) - 1)) | ((uint64_t)qq[0] << 54);
-          if (p.key_bk) {
-            p.key_bk[o * p.key_n + a] = (uint32_t)(v & nbm);
-            p.key_ent[o * p.key_n + a] = e;
-          } else {
-            cell_insert(p.cells, v & nbm, p.cell_n, e);
-          }
-        }
-        }
-      } else if (a < p.a_hi) {
-        if (p.key0) p.key0[a] = kEmpty;
-        if (p.key_bk) {
-          for (int o = 0; o < 4; ++o) {
-            p.key_bk[o * p.key_n + a] = 0;
-            p.key_ent[o * p.key_n + a] = kEmpty;
-          }
-        }
+        v0 = mix64(funnel(rw[0], rw[1], p0 << 1) >> msh);  // p0 < w <= 32
+        v1 = mix64(ext_reg<MAXW>(rw, p1) >> msh);
       }
-      if (p.join_P) {  // every lane takes part (the flat-chunk state is wavefront-uniform)
-#pragma unroll
-        for (int o = 0; o < 4; ++o) st.emit_ready(n > 0, jk[o], jv[o]);
-      }
+      st.emit_ready(n > 0, join_k32(v0, p.join_P, 0u), join_key_val((uint32_t)a, 0, p0, v0, p));
+      st.emit_ready(n > 0, join_k32(v1, p.join_P, 0u), join_key_val((uint32_t)a, 1, p1 - (n - h), v1, p));
     }
   }
   st.finish(gw);
@@ -1777,28 +1748,33 @@ __global__ __launch_bounds__(kBlock) void k_verify(ProbeParams p, uint64_t cand_
 
 // ----------------------------------------------------------- k_join ---
 // One partition of the sorted join records at a time per workgroup (dynamic
-// queue): the partition's keys go into an exact-key table in LDS (open
-// addressing, 8-B entries read | fp19 << 32 | q << 51 | o << 61, slot = low
-// kJoinTBits bits of H32, fp = H32 bits 13..31), then every run of the
-// partition walks its slot chain: an entry with the run's fingerprint and
-// q such that j = p - q lies in the run's window range [jlo, jhi] is the exact
-// candidate of getListOfReads(F1[j, j+h)) (HashTable.cpp:202-221) that the
-// reference meets at window j (OverlapGraph.cpp:534-547).  Candidates go to a
-// per-wavefront LDS ring and are verified 64 at a time against both reads'
-// slots (checkOverlap :354-383 / checkOverlapForContainedRead :302-340), with
-// the source read's words in registers.  More keys than kJoinCap: the table is
-// refilled per chunk of keys and the runs streamed again (skewed partitions).
-// CONTAIN with prefix queries: every o = 0 key of the partition also probes the
-// table for shorter reads whose o = 0/2 key is the same string at the same q
-// (a prefix of read1 at offset 0, which the reference meets only through the
-// shorter read's suffix key), the k_prefix_contain rule.
+// queue): the partition's keys are filed into an exact-key index in LDS, then
+// every run of the partition looks its minimizer up there.  The LDS index is
+// the global cell index in small: kJoinCells cells of kCell 8-B entries
+// (read | fp19 << 32 | q << 51 | o << 61, fp = H32 bits 13..31), cell =
+// H32 mod kJoinCells; a key takes the next free entry of its cell (LDS
+// atomicAdd on the cell's count) or, when the cell is full, of the following
+// cells, so a lookup reads one 64-B cell and continues only while the count
+// says a key went past it.  A run's candidate is an entry with its
+// fingerprint and a q such that j = p - q lies in the run's window range
+// [jlo, jhi]: the exact candidate of getListOfReads(F1[j, j+h))
+// (HashTable.cpp:202-221) that the reference meets at window j
+// (OverlapGraph.cpp:534-547).  Candidates go to a per-wavefront LDS ring and
+// are verified 64 at a time against both reads' slots (checkOverlap :354-383 /
+// checkOverlapForContainedRead :302-340), the source read's words in
+// registers.  More keys than kJoinCap: the index is refilled per chunk of
+// keys and the runs are streamed again (skewed partitions).  CONTAIN with
+// prefix queries: every o = 0 key of the partition also looks up shorter reads
+// whose o = 0/2 key is the same string at the same q (a prefix of read1 at
+// offset 0, which the reference meets only through the shorter read's suffix
+// key): the k_prefix_contain rule.
 constexpr int kJoinBlock = 512;
 constexpr int kJoinWaves = kJoinBlock / kWave;
-constexpr int kJoinTBits = 13;
-constexpr int kJoinT = 1 << kJoinTBits;   // LDS table slots (64 KiB)
-constexpr int kJoinCap = kJoinT / 2;      // keys per table fill (load <= 50 %)
-constexpr int kJoinRing = 128;            // per-wavefront candidate ring
-constexpr size_t kJoinLds = (size_t)kJoinT * 8 + (size_t)kJoinWaves * kJoinRing * 12 + 16;
+constexpr int kJoinCells = 1024;                 // LDS cells of kCell entries (64 KiB)
+constexpr int kJoinCap = kJoinCells * kCell / 2;  // keys per fill (cells at most half full)
+constexpr int kJoinRing = 128;                   // per-wavefront candidate ring
+constexpr size_t kJoinLds = (size_t)kJoinCells * kCell * 8 + (size_t)kJoinCells * 4 +
+                            (size_t)kJoinWaves * kJoinRing * 10 + 16;
 
 struct JoinParams {
   const uint64_t* words;
@@ -1815,12 +1791,13 @@ struct JoinParams {
   uint64_t src_lo, src_hi;           // only runs of sources in [src_lo, src_hi) (src_hi = 0: all)
   unsigned long long* superkey;      // CONTAIN: max (len << 32 | ~index) per contained read
   int contain_even;                  // CONTAIN: drop o = 1/3 hits (the prefix queries cover s = 0)
-  int prefix_queries;                // CONTAIN: o = 0 keys query the table (offset-0 containments)
+  int prefix_queries;                // CONTAIN: o = 0 keys query the index (offset-0 containments)
   uint32_t* rows;                    // 3 dwords per row, one region per wavefront
   unsigned long long* reg_cnt;
   uint64_t reg_cap;
   int uniform_len, halving_low;
   unsigned long long* stats;         // optional [kSegs * 4]: runs, entries, verified, rows
+  int phase_limit;                   // diagnostics: 5 index only, 6 + lookups (no candidates), 7 full
 };
 
 // 32 bases of a read held in registers starting at pos (pos >= -31; bases
@@ -1832,13 +1809,19 @@ __device__ __forceinline__ uint64_t ext_reg_s(const uint64_t* rw, int pos) {
   return pos < 0 ? neg : x;
 }
 
+__device__ __forceinline__ uint32_t join_cell(uint32_t H) { return H & (kJoinCells - 1); }
+
 template <int MAXW, bool CONTAIN>
 __global__ __launch_bounds__(kJoinBlock) void k_join(JoinParams p) {
   extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  uint64_t* const table = smem;
-  uint32_t* const rb = reinterpret_cast<uint32_t*>(smem + kJoinT) + (size_t)wv * kJoinRing * 3;  // ring: b | info | a
-  uint32_t* const s_part = reinterpret_cast<uint32_t*>(smem + kJoinT) + (size_t)kJoinWaves * kJoinRing * 3;
+  uint64_t* const cells = smem;                                                   // [kJoinCells][kCell]
+  uint32_t* const ccnt = reinterpret_cast<uint32_t*>(smem + kJoinCells * kCell);  // [kJoinCells]
+  uint32_t* const rbase = ccnt + kJoinCells;
+  uint32_t* const rb = rbase + (size_t)wv * kJoinRing * 2;  // ring: partner [128] | source [128]
+  uint16_t* const ri = reinterpret_cast<uint16_t*>(rbase + (size_t)kJoinWaves * kJoinRing * 2) +
+                       (size_t)wv * kJoinRing;              // ring: o << 10 | j
+  uint32_t* const s_part = reinterpret_cast<uint32_t*>(ri + (size_t)(kJoinWaves - wv) * kJoinRing);
   const int h = p.h, P = p.P, A = p.A;
   const uint64_t amask = (1ULL << A) - 1;
   const int run_sh = A + 10 + 2 * p.WB, key_sh = A + 2 + p.QB;
@@ -1860,9 +1843,9 @@ __global__ __launch_bounds__(kJoinBlock) void k_join(JoinParams p) {
     if (have) {
       const uint32_t at = (rhead + lane) & (kJoinRing - 1);
       bid = rb[at];
-      const uint32_t info = rb[kJoinRing + at];
-      sa = rb[2 * kJoinRing + at];
-      o = (int)(info >> 30);
+      sa = rb[kJoinRing + at];
+      const uint32_t info = ri[at];
+      o = (int)(info >> 10);
       j = (int)(info & 1023u);
       n1 = p.uniform_len ? p.uniform_len : (int)p.len[sa];
       n2 = p.uniform_len ? p.uniform_len : (int)p.len[bid];
@@ -1948,8 +1931,8 @@ __global__ __launch_bounds__(kJoinBlock) void k_join(JoinParams p) {
     if (flag) {
       const uint32_t at = (rhead + rcnt + lane_prefix(bal)) & (kJoinRing - 1);
       rb[at] = b;
-      rb[kJoinRing + at] = info;
-      rb[2 * kJoinRing + at] = a;
+      rb[kJoinRing + at] = a;
+      ri[at] = (uint16_t)info;
     }
     rcnt += (uint32_t)__popcll(bal);
     if (rcnt >= (uint32_t)kWave) {
@@ -1960,43 +1943,44 @@ __global__ __launch_bounds__(kJoinBlock) void k_join(JoinParams p) {
   };
 
   for (;;) {
-    __syncthreads();  // every wave is done with the previous partition's table and s_part
+    __syncthreads();  // every wave is done with the previous partition's index and s_part
     if (threadIdx.x == 0) s_part[0] = atomicAdd(p.queue, 1u);
     __syncthreads();
     const uint32_t f = s_part[0];
     if (f >= p.nparts) break;
     const uint64_t kb = p.bnd[f], kr = p.mid[f], ke = p.bnd[f + 1];
-    if (kr == kb) continue;                                // no keys: nothing to find
+    if (kr == kb) continue;                                    // no keys: nothing to find
     if (ke == kr && !(CONTAIN && p.prefix_queries)) continue;  // no runs and no prefix queries
     for (uint64_t c0 = kb; c0 < kr; c0 += kJoinCap) {
       const uint64_t c1 = min(kr, c0 + (uint64_t)kJoinCap);
-      if (c0 != kb) __syncthreads();  // the previous chunk's probes are done
-      {
-        ulonglong2* t2 = reinterpret_cast<ulonglong2*>(table);
-        for (int i = threadIdx.x; i < kJoinT / 2; i += kJoinBlock) t2[i] = make_ulonglong2(kEmpty, kEmpty);
-      }
+      if (c0 != kb) __syncthreads();  // the previous chunk's lookups are done
+      for (int i = threadIdx.x; i < kJoinCells; i += kJoinBlock) ccnt[i] = 0;
       __syncthreads();
-      // the chunk's keys into the table
+      // the chunk's keys into the LDS cells
       for (uint64_t i = c0 + threadIdx.x; i < c1; i += kJoinBlock) {
         const uint64_t v = p.val[i];
         const uint32_t H = join_h32(p.k32[i], v, P, key_sh);
-        const uint64_t e = (v & amask) | ((uint64_t)(H >> kJoinTBits) << 32) |
+        const uint64_t e = (v & amask) | ((uint64_t)(H >> 13) << 32) |
                            (((v >> (A + 2)) & ((1ULL << p.QB) - 1)) << 51) | (((v >> A) & 3u) << 61);
-        uint32_t sl = H & (kJoinT - 1);
-        for (;;) {  // capacity 2x the chunk: an empty slot always exists
-          if (atomicCAS(reinterpret_cast<unsigned long long*>(&table[sl]), kEmpty, (unsigned long long)e) == kEmpty)
+        uint32_t c = join_cell(H);
+        for (;;) {  // at most half the entries are used: a free one always exists
+          const uint32_t at = atomicAdd(&ccnt[c], 1u);
+          if (at < (uint32_t)kCell) {
+            cells[c * kCell + at] = e;
             break;
-          sl = (sl + 1) & (kJoinT - 1);
+          }
+          c = (c + 1) & (kJoinCells - 1);
         }
       }
       __syncthreads();
-      // probe items: CONTAIN prefix queries (the partition's o = 0 keys), then runs
+      // lookups: CONTAIN prefix queries (the partition's o = 0 keys), then runs
       const uint64_t q0 = (CONTAIN && p.prefix_queries) ? kb : kr;
-      for (uint64_t i0 = q0 + (uint64_t)wv * kWave; i0 < ke; i0 += kJoinBlock) {
+      const uint64_t qe = p.phase_limit <= 5 ? q0 : ke;
+      for (uint64_t i0 = q0 + (uint64_t)wv * kWave; i0 < qe; i0 += kJoinBlock) {
         const uint64_t i = i0 + lane;
-        bool live = i < ke;
+        bool live = i < qe;
         const bool is_run = i >= kr;
-        uint32_t H = 0, ra = 0, fpr = 0;
+        uint32_t H = 0, ra = 0;
         int rp = 0, jlo = 0, jhi = 0, qa = 0;
         if (live) {
           const uint64_t v = p.val[i];
@@ -2013,40 +1997,53 @@ __global__ __launch_bounds__(kJoinBlock) void k_join(JoinParams p) {
             qa = (int)((v >> (A + 2)) & ((1ULL << p.QB) - 1));
             if (((v >> A) & 3u) != 0) live = false;
           }
-          fpr = H >> kJoinTBits;
         }
         if (live && is_run) ++st_runs;
-        uint32_t sl = H & (kJoinT - 1);
+        const uint32_t fpr = H >> 13;
+        uint32_t c = join_cell(H);
         while (__ballot(live)) {
-          const uint64_t e = live ? table[sl] : kEmpty;
-          if (e == kEmpty) live = false;
-          bool keep = false;
-          uint32_t b = 0, info = 0;
-          if (live) {
-            ++st_ent;
-            b = (uint32_t)e;
-            const uint32_t hi = (uint32_t)(e >> 32);
-            const int oo = (int)(hi >> 29), q = (int)((hi >> 19) & 1023u);
-            if ((hi & 0x7FFFFu) == fpr) {
-              if (is_run) {
-                const int j = rp - q;
-                keep = j >= jlo && j <= jhi;
-                // halving: o = 1 hits are twins of the partner's o = 0
-                // hits; an o = 2/3 pair is kept on one side only (rc_side_keeps)
-                keep = keep && (CONTAIN || oo == 0 ||
-                                (oo >= 2 && (p.halving_low ? b >= ra : rc_side_keeps(ra, b))));
-                keep = keep && !(CONTAIN && p.contain_even && (oo & 1));
-                info = ((uint32_t)oo << 30) | (uint32_t)j;
-              } else {
-                // read b's o = 0/2 key is read1's o = 0 key (same string at the same q):
-                // b (or its reverse strand) may be a prefix of read1 (offset j = 0)
-                keep = q == qa && !(oo & 1) && b != ra;
-                info = (uint32_t)oo << 30;
-              }
+          const uint32_t cnt = live ? ccnt[c] : 0u;
+          uint64_t e[kCell];
+          {
+            const ulonglong2* cp = reinterpret_cast<const ulonglong2*>(cells + (live ? c : 0u) * kCell);
+#pragma unroll
+            for (int s2 = 0; s2 < kCell / 2; ++s2) {
+              const ulonglong2 x = cp[s2];
+              e[2 * s2] = x.x;
+              e[2 * s2 + 1] = x.y;
             }
           }
-          push(keep, b, info, ra);
-          sl = (sl + 1) & (kJoinT - 1);
+#pragma unroll
+          for (int sl = 0; sl < kCell; ++sl) {
+            bool keep = false;
+            uint32_t b = 0, info = 0;
+            if ((uint32_t)sl < cnt) {  // entries past the count are stale
+              ++st_ent;
+              b = (uint32_t)e[sl];
+              const uint32_t hi = (uint32_t)(e[sl] >> 32);
+              const int oo = (int)(hi >> 29), q = (int)((hi >> 19) & 1023u);
+              if ((hi & 0x7FFFFu) == fpr) {
+                if (is_run) {
+                  const int j = rp - q;
+                  keep = j >= jlo && j <= jhi;
+                  // halving: o = 1 hits are twins of the partner's o = 0
+                  // hits; an o = 2/3 pair is kept on one side only (rc_side_keeps)
+                  keep = keep && (CONTAIN || oo == 0 ||
+                                  (oo >= 2 && (p.halving_low ? b >= ra : rc_side_keeps(ra, b))));
+                  keep = keep && !(CONTAIN && p.contain_even && (oo & 1));
+                  info = ((uint32_t)oo << 10) | (uint32_t)j;
+                } else {
+                  // read b's o = 0/2 key is read1's o = 0 key (same string at the same q):
+                  // b (or its reverse strand) may be a prefix of read1 (offset j = 0)
+                  keep = q == qa && !(oo & 1) && b != ra;
+                  info = (uint32_t)oo << 10;
+                }
+              }
+            }
+            push(keep && p.phase_limit > 6, b, info, ra);
+          }
+          live = live && cnt > (uint32_t)kCell;  // a key went past this cell: continue in the next
+          c = (c + 1) & (kJoinCells - 1);
         }
       }
     }
@@ -2470,6 +2467,9 @@ inline size_t scan_lds_per_wave(uint32_t w) { return (((size_t)w * kWave + 1) / 
 // the register scan (k_scan_reg) when its window fits in registers
 inline bool use_scan_reg_w(const mg_ctx* ctx) { return ctx->w <= (uint32_t)kRegW; }
 inline bool use_scan_reg(const mg_ctx* ctx) { return (ctx->scan_reg || ctx->join_P) && use_scan_reg_w(ctx); }
+// the index-building scan: k_scan_reg<INDEX> writes join records only; the
+// cell index rides on k_scan<INDEX>
+inline bool use_scan_reg_index(const mg_ctx* ctx) { return ctx->join_P && use_scan_reg_w(ctx); }
 inline uint32_t scan_block_waves(const mg_ctx* ctx);
 inline size_t scan_lds(const mg_ctx* ctx);
 inline uint32_t scan_wpb(uint32_t w) {
@@ -2477,16 +2477,19 @@ inline uint32_t scan_wpb(uint32_t w) {
     if (wpb * scan_lds_per_wave(w) <= kLdsPerCu) return wpb;
   return 0;
 }
-inline uint32_t scan_block_waves(const mg_ctx* ctx) { return use_scan_reg(ctx) ? kWavesPerBlock : scan_wpb(ctx->w); }
-inline size_t scan_lds(const mg_ctx* ctx) {
-  return use_scan_reg(ctx) ? (size_t)kWavesPerBlock * kStageRing * sizeof(uint64_t)
-                           : (size_t)scan_wpb(ctx->w) * scan_lds_per_wave(ctx->w);
+inline bool scan_is_reg(const mg_ctx* ctx, bool index) { return index ? use_scan_reg_index(ctx) : use_scan_reg(ctx); }
+inline uint32_t scan_block_waves(const mg_ctx* ctx, bool index) {
+  return scan_is_reg(ctx, index) ? kWavesPerBlock : scan_wpb(ctx->w);
+}
+inline size_t scan_lds(const mg_ctx* ctx, bool index) {
+  return scan_is_reg(ctx, index) ? (size_t)kWavesPerBlock * kStageRing * sizeof(uint64_t)
+                                 : (size_t)scan_wpb(ctx->w) * scan_lds_per_wave(ctx->w);
 }
 template <int W>
 uint32_t scan_resident(mg_ctx* ctx, bool index, uint64_t want) {
-  const size_t lds = scan_lds(ctx);
-  const int block = (int)scan_block_waves(ctx) * kWave;
-  if (use_scan_reg(ctx))
+  const size_t lds = scan_lds(ctx, index);
+  const int block = (int)scan_block_waves(ctx, index) * kWave;
+  if (scan_is_reg(ctx, index))
     return index ? resident_blocks(ctx, k_scan_reg<W, true>, lds, want, block)
                  : resident_blocks(ctx, k_scan_reg<W, false>, lds, want, block);
   return index ? resident_blocks(ctx, k_scan<W, true>, lds, want, block)
@@ -2519,7 +2522,7 @@ DiscGeom disc_geom(mg_ctx* ctx, bool contain, uint64_t nsrc) {
   DiscGeom g;
   const uint64_t ngroups = (nsrc + kWave - 1) / kWave;
   const uint64_t want = std::max<uint64_t>(1, (ngroups + kWavesPerBlock - 1) / kWavesPerBlock);
-  g.lds_scan = scan_lds(ctx);
+  g.lds_scan = scan_lds(ctx, false);
   if (ctx->split) {
     g.lds_probe = (size_t)kWavesPerBlock * ProbeLds<W>::split_bytes;
     g.grid = contain ? resident_blocks(ctx, k_probe<W, true, true>, g.lds_probe, want)
@@ -2543,7 +2546,7 @@ struct LaunchScan {
   static int run(mg_ctx* ctx, bool contain, uint64_t a_lo, uint64_t a_hi, uint32_t sgrid, bool filter,
                  hipStream_t stream = nullptr, bool no_super = false, bool index = false, bool flat = false) {
     if (!stream) stream = ctx->stream;
-    const uint32_t wpb = scan_block_waves(ctx);
+    const uint32_t wpb = scan_block_waves(ctx, index);
     const uint64_t nw = (uint64_t)sgrid * wpb;  // scan wavefronts = run regions
     ctx->nrun_reg = nw;
     const uint64_t ngroups = (a_hi - a_lo + kWave - 1) / kWave;
@@ -2581,7 +2584,7 @@ struct LaunchScan {
     sp.runs = ctx->d_runs;
     sp.run_cnt = ctx->d_run_cnt;
     sp.run_cap = run_cap;
-    const size_t lds = scan_lds(ctx);
+    const size_t lds = scan_lds(ctx, index);
     sp.cells = ctx->d_cells;
     sp.cell_n = ctx->cell_n;
     ctx->scan_flat = flat;
@@ -2636,7 +2639,7 @@ struct LaunchScan {
       sp.key_n = ctx->n;
     }
     (void)hipEventRecord(ctx->ev[6], stream);
-    if (use_scan_reg(ctx)) {
+    if (scan_is_reg(ctx, index)) {
       if (index) {
         allow_lds(k_scan_reg<W, true>, lds);
         hipLaunchKernelGGL((k_scan_reg<W, true>), dim3(sgrid), dim3(wpb * kWave), lds, stream, sp);
@@ -3372,7 +3375,7 @@ void read_stats(mg_ctx* ctx, uint64_t nsrc) {
 template <int W>
 struct LaunchScanAll {
   static int run(mg_ctx* ctx, hipStream_t st, bool index) {
-    const uint32_t wpb = scan_block_waves(ctx);
+    const uint32_t wpb = scan_block_waves(ctx, index);
     const uint64_t groups = (ctx->n + kWave - 1) / kWave;
     const uint32_t sgrid = scan_resident<W>(ctx, index, (groups + wpb - 1) / wpb);
     return LaunchScan<W>::run(ctx, true, 0, ctx->n, sgrid, false, st, true, index,
@@ -3655,6 +3658,7 @@ struct LaunchJoin {
     jp.uniform_len = ctx->minlen == ctx->maxlen ? (int)ctx->maxlen : 0;
     jp.halving_low = ctx->halving_low ? 1 : 0;
     jp.stats = contain ? nullptr : (ctx->stats ? ctx->d_stats : nullptr);
+    jp.phase_limit = contain ? 99 : ctx->phase_limit;
     const uint32_t grid = contain ? resident_blocks(ctx, k_join<W, true>, kJoinLds, jp.nparts, kJoinBlock)
                                   : resident_blocks(ctx, k_join<W, false>, kJoinLds, jp.nparts, kJoinBlock);
     ctx->nreg = (uint64_t)grid * kJoinWaves;  // join wavefronts = row regions
