@@ -244,6 +244,8 @@ def main():
     ap.add_argument("--split-probe", action="store_true", help="probe -> candidates -> verify kernels (option split = 1)")
     ap.add_argument("--sort-runs", type=int, default=None,
                     help="option sort_runs: bucket-ordered runs before the probe (default: the library's)")
+    ap.add_argument("--opt", action="append", default=[],
+                    help="engine option NAME=VALUE (mg_set_option), repeatable; diagnostics / A-B runs")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -304,6 +306,9 @@ def main():
         e.set_option("split", 1 if args.split_probe else 0)
         if args.sort_runs is not None:
             e.set_option("sort_runs", args.sort_runs)
+        for kv in args.opt:
+            name, val = kv.split("=", 1)
+            e.set_option(name, int(val))
         if mode.startswith("replicated"):
             # the whole index on every rank, this rank's source reads only: the
             # index build (k_index_build) then a scan + probe of [lo, hi)

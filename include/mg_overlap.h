@@ -64,6 +64,7 @@ typedef struct mg_counters {
   uint64_t entries;   /* bucket entries scanned                       */
   uint64_t verified;  /* partner reads fetched and compared           */
   uint64_t rows;      /* directed rows emitted                        */
+  uint64_t trips;     /* join: wavefront index-lookup trips (diagnostics) */
 } mg_counters;
 
 /* --- context ------------------------------------------------------------ */

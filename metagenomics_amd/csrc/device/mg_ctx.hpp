@@ -87,10 +87,11 @@ struct mg_ctx {
   // its runs then serve the containment and the discovery probes
   int scan_state = 0;        // 0 none, 1 launched (not settled), 2 settled
   bool overlap_scan = true;  // option "overlap_scan" (0: separate index build, a scan per probe pass)
-  bool scan_reg = false;     // option "scan_reg": register sliding minimum (k_scan_reg) when w <= 32
+  bool scan_reg = true;      // option "scan_reg": register sliding minimum (k_scan_reg) for the run scans when w <= 32
+  bool reg_index = false;    // option "reg_index": also for the cell index build (key records + k_insert_dense)
   // partitioned join (option "join", default): keys + runs as sorted join
   // records, per-partition LDS tables (k_join); cells only on demand (lookups)
-  bool join = true;
+  bool join = false;
   int join_P = 0, join_A = 0, join_QB = 0, join_WB = 0;  // record geometry of the current build (0: not join)
   int join_P_opt = 0;        // option "join_parts_log2" (0: auto)
   bool join_ready = false;   // the sorted join records + partition bounds are current
@@ -127,6 +128,7 @@ struct mg_ctx {
   size_t holes_cap = 0;
   std::vector<uint64_t> holes_host;
   uint64_t flat_cap_opt = 0;       // option "flat_cap" (tests: force the overflow rerun)
+  uint64_t flat_off = 0;           // records ahead of the flat chunks (join: the 4 N dense key records)
   bool pack_runs = true;           // option "pack_runs": 12-B sort records when the widths fit
   int pack_a = 0, pack_w = 0;      // packing of the current flat runs (0: 16-B records)
   int sorted_state = 0;  // 0 none, 2 sorted (for the current scan)

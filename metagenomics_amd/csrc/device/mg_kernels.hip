@@ -286,6 +286,17 @@ __global__ __launch_bounds__(kBlock) void k_fill_cells(const uint32_t* __restric
   }
 }
 
+// insertIntoTable (HashTable.cpp:163-195) for the o-major key records the
+// register scan and k_rc_keys wrote: one thread per key, CAS into its home
+// cell chain (independent inserts, so the whole device hides their latency).
+__global__ __launch_bounds__(kBlock) void k_insert_dense(const uint32_t* __restrict__ bk, const uint64_t* __restrict__ ent,
+                                                         uint64_t n, uint64_t* __restrict__ cells, uint64_t cell_n) {
+  for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBlock) {
+    const uint64_t e = ent[i];
+    if (e != kEmpty) cell_insert(cells, bk[i], cell_n, e);
+  }
+}
+
 // markContainedReads at offset s = 0 (OverlapGraph.cpp:225-340): read2 (or
 // its reverse strand) is a prefix of read1.  The reference meets these only
 // through read2's suffix key (o = 1/3 at window j = n2 - h), because window
@@ -424,6 +435,8 @@ struct ScanParams {
   // every read as 12-B join records (join_k32 / join_run_val / join_key_val)
   // into the flat arrays instead of inserting keys into cells
   int join_P, join_A, join_QB, join_WB;
+  uint32_t* join_kk;  // join INDEX: dense key records, read a's key o at 4 a + o (o = 0, 1 here;
+  uint64_t* join_kv;  // o = 2, 3 by k_rc_keys); the runs follow at 4 N in the flat arrays
 };
 
 // ---------------------------------------------------------------- join ---
@@ -1003,6 +1016,14 @@ __global__ __launch_bounds__(kBlock) void k_scan_reg(ScanParams p) {
   const uint64_t gw = (uint64_t)blockIdx.x * kWavesPerBlock + wv;
   const uint64_t nw = (uint64_t)gridDim.x * kWavesPerBlock;
   RunStage<MAXW> st(p, smem + (size_t)wv * kStageRing, p.runs + gw * p.run_cap, lane);
+  constexpr int kRwLoad = MAXW + 1 <= slot_words(MAXW) ? MAXW + 1 : slot_words(MAXW);
+  uint64_t nx[MAXW + 1];  // the read words of this lane's next group (software pipelined)
+  {
+    const uint64_t a = p.a_lo + gw * kWave + lane;
+    const uint64_t* gs = p.words + (a < p.a_hi && gw < ngroups ? a : 0) * slot_words(MAXW);
+#pragma unroll
+    for (int k = 0; k <= MAXW; ++k) nx[k] = k < kRwLoad ? gs[k] : 0;
+  }
 
   for (uint64_t grp = gw; grp < ngroups; grp += nw) {
     const uint64_t a = p.a_lo + grp * kWave + lane;
@@ -1019,39 +1040,15 @@ __global__ __launch_bounds__(kBlock) void k_scan_reg(ScanParams p) {
     for (int d = 32; d >= 1; d >>= 1) tmax = max(tmax, __shfl_xor(tmax, d));
     tmax = __builtin_amdgcn_readfirstlane(tmax);
     uint64_t rw[MAXW + 1];
-    {
-      constexpr int kRw = MAXW + 1 <= slot_words(MAXW) ? MAXW + 1 : slot_words(MAXW);
-      const uint64_t* gs = p.words + (a < p.a_hi ? a : 0) * slot_words(MAXW);
 #pragma unroll
-      for (int k = 0; k <= MAXW; ++k) rw[k] = k < kRw ? gs[k] : 0;
+    for (int k = 0; k <= MAXW; ++k) rw[k] = nx[k];
+    {  // the next group's words load behind this group's scan
+      const uint64_t an = a + (uint64_t)nw * kWave;
+      const uint64_t* gs = p.words + (an < p.a_hi ? an : 0) * slot_words(MAXW);
+#pragma unroll
+      for (int k = 0; k <= MAXW; ++k) nx[k] = k < kRwLoad ? gs[k] : 0;
     }
     const uint64_t a0 = p.a_lo + grp * kWave;
-    // INDEX, reverse-strand keys first (before the scan's registers are live):
-    // o = 3 (R[n-h, n) = rc F[0, h): m-mer i = rc of F's at t = w-1-i) and
-    // o = 2 (R[0, h) = rc F[n-h, n): m-mer i = rc of F's at t = n-m-i), both
-    // rolled towards smaller t, one base per step
-    uint32_t kb3 = 0xFFFFFFFFu, kb2 = 0xFFFFFFFFu;
-    uint64_t mb3 = 0, mb2 = 0;
-    if (INDEX && n) {
-      const uint64_t Aw = ext_reg<MAXW>(rw, n - h);                      // F[n-h, n-h+32)
-      uint64_t r3 = rc_word(funnel(rw[0], rw[1], 2 * (w - 1))) & mmask;  // rc(F[w-1, w-1+m))
-      uint64_t r2 = rc_word(ext_reg<MAXW>(rw, n - m)) & mmask;          // rc(F[n-m, n))
-      for (int i = 0; i < w; ++i) {
-        const uint32_t k3 = order_key(r3) | (uint32_t)i, k2 = order_key(r2) | (uint32_t)i;
-        if (k3 < kb3) { kb3 = k3; mb3 = r3; }
-        if (k2 < kb2) { kb2 = k2; mb2 = r2; }
-        const int t3 = w - 2 - i;  // F base entering the rc m-mer at t - 1 (both keys: offset w-2-i)
-        if (t3 >= 0) {
-          r3 = ((r3 << 2) | (3u - ((rw[0] >> (62 - 2 * t3)) & 3u))) & mmask;
-          r2 = ((r2 << 2) | (3u - ((Aw >> (62 - 2 * t3)) & 3u))) & mmask;  // F[n-m-1-i] = F[n-h + w-2-i]
-        }
-      }
-    }
-    if (INDEX) {  // emit them now (every lane: the flat-chunk state is wavefront-uniform)
-      const uint64_t v2 = mix64(mb2), v3 = mix64(mb3);
-      st.emit_ready(n > 0, join_k32(v2, p.join_P, 0u), join_key_val((uint32_t)a, 2, (int)(kb2 & 1023u), v2, p));
-      st.emit_ready(n > 0, join_k32(v3, p.join_P, 0u), join_key_val((uint32_t)a, 3, (int)(kb3 & 1023u), v3, p));
-    }
     uint32_t S[kRegW + 1];
 #pragma unroll
     for (int u = 0; u <= kRegW; ++u) S[u] = 0xFFFFFFFFu;
@@ -1102,15 +1099,48 @@ __global__ __launch_bounds__(kBlock) void k_scan_reg(ScanParams p) {
     }
     st.put(tend >= 0, run_meta(a, last, jlo, J));  // each read's last run
     while (st.nbuf) st.flush(st.nbuf < (uint32_t)kWave ? st.nbuf : (uint32_t)kWave, rw, a0);
-    if constexpr (INDEX) {  // (join mode only: the cell index is built by k_scan / k_index_build)
-      const int p0 = (int)(kw0 & 1023u), p1 = (int)(kw1 & 1023u);
-      uint64_t v0 = 0, v1 = 0;
-      if (n) {
-        v0 = mix64(funnel(rw[0], rw[1], p0 << 1) >> msh);  // p0 < w <= 32
-        v1 = mix64(ext_reg<MAXW>(rw, p1) >> msh);
+    if constexpr (INDEX) {  // join records of keys o = 0 / 1 (the cell index is k_scan's / k_index_build's)
+      if (a < p.a_hi) {
+        const int p0 = (int)(kw0 & 1023u), p1 = (int)(kw1 & 1023u);
+        uint32_t k0 = 0xFFFFFFFFu, k1 = 0xFFFFFFFFu;  // (no keys: holes, n <= l cannot pass setup)
+        uint64_t e0 = kFlatHole, e1 = kFlatHole;
+        if (n && p.join_P) {
+          const uint64_t v0 = mix64(funnel(rw[0], rw[1], p0 << 1) >> msh);  // p0 < w <= 32
+          const uint64_t v1 = mix64(ext_reg<MAXW>(rw, p1) >> msh);
+          k0 = join_k32(v0, p.join_P, 0u);
+          e0 = join_key_val((uint32_t)a, 0, p0, v0, p);
+          k1 = join_k32(v1, p.join_P, 0u);
+          e1 = join_key_val((uint32_t)a, 1, p1 - (n - h), v1, p);
+        }
+        if (p.join_P) {
+          p.join_kk[4 * a] = k0;
+          p.join_kv[4 * a] = e0;
+          p.join_kk[4 * a + 1] = k1;
+          p.join_kv[4 * a + 1] = e1;
+        } else {  // cell index: (bucket, entry) records, o-major (k_insert_dense / sorted_index file them)
+          const uint64_t nbm = (1ULL << p.nb_log2) - 1;
+          uint64_t c0 = kEmpty, c1 = kEmpty;
+          uint32_t b0 = 0, b1 = 0;
+          if (n) {
+            const uint64_t v0 = mix64(funnel(rw[0], rw[1], p0 << 1) >> msh);
+            const uint64_t v1 = mix64(ext_reg<MAXW>(rw, p1) >> msh);
+            b0 = (uint32_t)(v0 & nbm);
+            b1 = (uint32_t)(v1 & nbm);
+            c0 = make_entry(v0, p.nb_log2, p0, 0, (uint32_t)a);
+            c1 = make_entry(v1, p.nb_log2, p1 - (n - h), 1, (uint32_t)a);
+          }
+          if (p.key0 && n) {
+            const uint64_t v0 = mix64(funnel(rw[0], rw[1], p0 << 1) >> msh);
+            p.key0[a] = (v0 & ((1ULL << 50) - 1)) | ((uint64_t)p0 << 54);
+          } else if (p.key0) {
+            p.key0[a] = kEmpty;
+          }
+          p.key_bk[a] = b0;
+          p.key_ent[a] = c0;
+          p.key_bk[p.key_n + a] = b1;
+          p.key_ent[p.key_n + a] = c1;
+        }
       }
-      st.emit_ready(n > 0, join_k32(v0, p.join_P, 0u), join_key_val((uint32_t)a, 0, p0, v0, p));
-      st.emit_ready(n > 0, join_k32(v1, p.join_P, 0u), join_key_val((uint32_t)a, 1, p1 - (n - h), v1, p));
     }
   }
   st.finish(gw);
@@ -1134,6 +1164,50 @@ __device__ __forceinline__ void load_slot(const uint64_t* words, uint32_t bid, u
     }
     if (MAXW % 2 == 0) y[MAXW] = 0;
   }
+}
+
+// Join records of the reverse strand's keys (hashRead, HashTable.cpp:88-104),
+// one thread per read: o = 3 (R[n-h, n) = rc F[0, h): m-mer i = rc of F's at
+// t = w-1-i) and o = 2 (R[0, h) = rc F[n-h, n): m-mer i = rc of F's at
+// t = n-m-i), both rolled towards smaller t, one base per step; the same
+// minimizer rule (order_key | i, smallest wins) as key_minimizer.  Written to
+// the dense key slots 4 a + 2 / 4 a + 3 (k_scan_reg<INDEX> writes 4 a + 0 / 1).
+template <int MAXW>
+__global__ __launch_bounds__(kBlock) void k_rc_keys(ScanParams p) {
+  const uint64_t a = p.a_lo + (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (a >= p.a_hi) return;
+  const int h = p.h, m = p.m, w = p.w, n = p.len[a];
+  const uint64_t mmask = (m == 32) ? ~0ULL : ((1ULL << (2 * m)) - 1);
+  uint64_t rw[MAXW + 1];
+  load_slot<MAXW>(p.words, (uint32_t)a, rw);
+  uint32_t kb3 = 0xFFFFFFFFu, kb2 = 0xFFFFFFFFu;
+  uint64_t mb3 = 0, mb2 = 0;
+  const uint64_t Aw = ext_reg<MAXW>(rw, n - h);                      // F[n-h, n-h+32)
+  uint64_t r3 = rc_word(funnel(rw[0], rw[1], 2 * (w - 1))) & mmask;  // rc(F[w-1, w-1+m))
+  uint64_t r2 = rc_word(ext_reg<MAXW>(rw, n - m)) & mmask;          // rc(F[n-m, n))
+  for (int i = 0; i < w; ++i) {
+    const uint32_t k3 = order_key(r3) | (uint32_t)i, k2 = order_key(r2) | (uint32_t)i;
+    if (k3 < kb3) { kb3 = k3; mb3 = r3; }
+    if (k2 < kb2) { kb2 = k2; mb2 = r2; }
+    const int t3 = w - 2 - i;  // F base entering at t - 1: F[t3] (o = 3), F[n-h + t3] = F[n-m-1-i] (o = 2)
+    if (t3 >= 0) {
+      r3 = ((r3 << 2) | (3u - ((rw[0] >> (62 - 2 * t3)) & 3u))) & mmask;
+      r2 = ((r2 << 2) | (3u - ((Aw >> (62 - 2 * t3)) & 3u))) & mmask;
+    }
+  }
+  const uint64_t v2 = mix64(mb2), v3 = mix64(mb3);
+  if (!p.join_P) {  // cell index: (bucket, entry) records, o-major
+    const uint64_t nbm = (1ULL << p.nb_log2) - 1;
+    p.key_bk[2 * p.key_n + a] = n ? (uint32_t)(v2 & nbm) : 0u;
+    p.key_ent[2 * p.key_n + a] = n ? make_entry(v2, p.nb_log2, (int)(kb2 & 1023u), 2, (uint32_t)a) : kEmpty;
+    p.key_bk[3 * p.key_n + a] = n ? (uint32_t)(v3 & nbm) : 0u;
+    p.key_ent[3 * p.key_n + a] = n ? make_entry(v3, p.nb_log2, (int)(kb3 & 1023u), 3, (uint32_t)a) : kEmpty;
+    return;
+  }
+  p.join_kk[4 * a + 2] = n ? join_k32(v2, p.join_P, 0u) : 0xFFFFFFFFu;
+  p.join_kv[4 * a + 2] = n ? join_key_val((uint32_t)a, 2, (int)(kb2 & 1023u), v2, p) : kFlatHole;
+  p.join_kk[4 * a + 3] = n ? join_k32(v3, p.join_P, 0u) : 0xFFFFFFFFu;
+  p.join_kv[4 * a + 3] = n ? join_key_val((uint32_t)a, 3, (int)(kb3 & 1023u), v3, p) : kFlatHole;
 }
 
 // checkOverlap's string compare (OverlapGraph.cpp:354-383) on packed words:
@@ -1829,7 +1903,7 @@ __global__ __launch_bounds__(kJoinBlock) void k_join(JoinParams p) {
   const uint32_t seg = (uint32_t)(gw & (kSegs - 1));
   uint32_t* const region = p.rows + gw * p.reg_cap * 3;
   uint64_t cursor = 0;
-  uint32_t st_runs = 0, st_ent = 0, st_ver = 0, st_rows = 0;
+  uint32_t st_runs = 0, st_ent = 0, st_ver = 0, st_rows = 0, st_trips = 0;
   uint32_t rhead = 0, rcnt = 0;  // candidate ring (wavefront-uniform)
 
   // verify the first k (<= 64) candidates of the ring, one per lane
@@ -1976,15 +2050,29 @@ __global__ __launch_bounds__(kJoinBlock) void k_join(JoinParams p) {
       // lookups: CONTAIN prefix queries (the partition's o = 0 keys), then runs
       const uint64_t q0 = (CONTAIN && p.prefix_queries) ? kb : kr;
       const uint64_t qe = p.phase_limit <= 5 ? q0 : ke;
+      // the next batch's records load behind the current batch's lookups
+      uint64_t nv = 0;
+      uint32_t nk = 0;
+      {
+        const uint64_t i = q0 + (uint64_t)wv * kWave + lane;
+        if (i < qe) {
+          nv = p.val[i];
+          nk = p.k32[i];
+        }
+      }
       for (uint64_t i0 = q0 + (uint64_t)wv * kWave; i0 < qe; i0 += kJoinBlock) {
         const uint64_t i = i0 + lane;
         bool live = i < qe;
         const bool is_run = i >= kr;
         uint32_t H = 0, ra = 0;
         int rp = 0, jlo = 0, jhi = 0, qa = 0;
+        const uint64_t v = nv;
+        const uint32_t k = nk;
+        if (i + kJoinBlock < qe) {
+          nv = p.val[i + kJoinBlock];
+          nk = p.k32[i + kJoinBlock];
+        }
         if (live) {
-          const uint64_t v = p.val[i];
-          const uint32_t k = p.k32[i];
           ra = (uint32_t)(v & amask);
           if (is_run) {
             H = join_h32(k, v, P, run_sh);
@@ -2000,9 +2088,13 @@ __global__ __launch_bounds__(kJoinBlock) void k_join(JoinParams p) {
         }
         if (live && is_run) ++st_runs;
         const uint32_t fpr = H >> 13;
+        const bool rcs_low = p.halving_low != 0;
         uint32_t c = join_cell(H);
         while (__ballot(live)) {
           const uint32_t cnt = live ? ccnt[c] : 0u;
+          const uint32_t nv = cnt < (uint32_t)kCell ? cnt : (uint32_t)kCell;  // entries past the count are stale
+          st_ent += nv;
+          st_trips += lane == 0 ? 1u : 0u;
           uint64_t e[kCell];
           {
             const ulonglong2* cp = reinterpret_cast<const ulonglong2*>(cells + (live ? c : 0u) * kCell);
@@ -2013,34 +2105,39 @@ __global__ __launch_bounds__(kJoinBlock) void k_join(JoinParams p) {
               e[2 * s2 + 1] = x.y;
             }
           }
+          // branch-free filter of the 8 entries: fingerprint, window range, halving
+          uint32_t keepm = 0;
 #pragma unroll
           for (int sl = 0; sl < kCell; ++sl) {
-            bool keep = false;
-            uint32_t b = 0, info = 0;
-            if ((uint32_t)sl < cnt) {  // entries past the count are stale
-              ++st_ent;
-              b = (uint32_t)e[sl];
-              const uint32_t hi = (uint32_t)(e[sl] >> 32);
-              const int oo = (int)(hi >> 29), q = (int)((hi >> 19) & 1023u);
-              if ((hi & 0x7FFFFu) == fpr) {
-                if (is_run) {
-                  const int j = rp - q;
-                  keep = j >= jlo && j <= jhi;
-                  // halving: o = 1 hits are twins of the partner's o = 0
-                  // hits; an o = 2/3 pair is kept on one side only (rc_side_keeps)
-                  keep = keep && (CONTAIN || oo == 0 ||
-                                  (oo >= 2 && (p.halving_low ? b >= ra : rc_side_keeps(ra, b))));
-                  keep = keep && !(CONTAIN && p.contain_even && (oo & 1));
-                  info = ((uint32_t)oo << 10) | (uint32_t)j;
-                } else {
-                  // read b's o = 0/2 key is read1's o = 0 key (same string at the same q):
-                  // b (or its reverse strand) may be a prefix of read1 (offset j = 0)
-                  keep = q == qa && !(oo & 1) && b != ra;
-                  info = (uint32_t)oo << 10;
-                }
-              }
+            const uint32_t hi = (uint32_t)(e[sl] >> 32), b = (uint32_t)e[sl];
+            const int oo = (int)(hi >> 29), q = (int)((hi >> 19) & 1023u);
+            bool keep = ((uint32_t)sl < nv) & ((hi & 0x7FFFFu) == fpr);
+            if (is_run) {
+              const int j = rp - q;
+              // halving: o = 1 hits are twins of the partner's o = 0
+              // hits; an o = 2/3 pair is kept on one side only (rc_side_keeps)
+              const bool side = rcs_low ? (b >= ra) : ((b == ra) | ((((ra ^ b) & 1u) != 0) ? (b > ra) : (b < ra)));
+              const bool ok_o = CONTAIN ? !(p.contain_even && (oo & 1)) : ((oo == 0) | ((oo >= 2) & side));
+              keep = keep & (j >= jlo) & (j <= jhi) & ok_o;
+            } else {
+              // read b's o = 0/2 key is read1's o = 0 key (same string at the same q):
+              // b (or its reverse strand) may be a prefix of read1 (offset j = 0)
+              keep = keep & (q == qa) & !(oo & 1) & (b != ra);
             }
-            push(keep && p.phase_limit > 6, b, info, ra);
+            keepm |= (keep ? 1u : 0u) << sl;
+          }
+          if (p.phase_limit > 6) {
+            // candidates into the ring slot by slot (one push site keeps verify inlined once)
+#pragma unroll 1
+            for (int sl = 0; sl < kCell; ++sl) {
+              const bool k = (keepm >> sl) & 1u;
+              if (!__ballot(k)) continue;
+              const uint64_t es = k ? cells[c * kCell + sl] : 0ull;
+              const uint32_t hi = (uint32_t)(es >> 32);
+              const uint32_t oo = hi >> 29;
+              const uint32_t info = is_run ? ((oo << 10) | (uint32_t)(rp - (int)((hi >> 19) & 1023u))) : (oo << 10);
+              push(k, (uint32_t)es, info, ra);
+            }
           }
           live = live && cnt > (uint32_t)kCell;  // a key went past this cell: continue in the next
           c = (c + 1) & (kJoinCells - 1);
@@ -2056,6 +2153,7 @@ __global__ __launch_bounds__(kJoinBlock) void k_join(JoinParams p) {
   }
   if (!CONTAIN && lane == 0) p.reg_cnt[gw] = cursor;
   if (p.stats) {
+    if (lane == 0) atomicAdd(&p.stats[kSegs * 4], (unsigned long long)st_trips);  // wavefront lookup trips
     uint32_t vv[4] = {st_runs, st_ent, st_ver, st_rows};
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -2469,7 +2567,9 @@ inline bool use_scan_reg_w(const mg_ctx* ctx) { return ctx->w <= (uint32_t)kRegW
 inline bool use_scan_reg(const mg_ctx* ctx) { return (ctx->scan_reg || ctx->join_P) && use_scan_reg_w(ctx); }
 // the index-building scan: k_scan_reg<INDEX> writes join records only; the
 // cell index rides on k_scan<INDEX>
-inline bool use_scan_reg_index(const mg_ctx* ctx) { return ctx->join_P && use_scan_reg_w(ctx); }
+// (cell mode: option "reg_index" = 1 writes key records that k_insert_dense files;
+// measured slower than k_scan<INDEX>, whose CAS inserts hide behind its ALU work)
+inline bool use_scan_reg_index(const mg_ctx* ctx) { return (ctx->join_P || ctx->reg_index) && use_scan_reg_w(ctx); }
 inline uint32_t scan_block_waves(const mg_ctx* ctx);
 inline size_t scan_lds(const mg_ctx* ctx);
 inline uint32_t scan_wpb(uint32_t w) {
@@ -2592,9 +2692,9 @@ struct LaunchScan {
       // SoA output for the bucket sort: ~2 J / (w + 1) + 1 runs per read, sized
       // with 20 % slack (or the exact need after an overflow)
       // (join mode: + the four key records of every read)
-      const uint64_t est = ctx->flat_cap_opt ? ctx->flat_cap_opt
-                                             : (a_hi - a_lo) * (2 * J / (ctx->w + 1) + 2 + (ctx->join_P ? 4 : 0)) * 6 / 5 +
-                                                   4096;
+      const uint64_t off = (ctx->join_P && index) ? 4 * ctx->n : 0;
+      const uint64_t est = off + (ctx->flat_cap_opt ? ctx->flat_cap_opt
+                                                    : (a_hi - a_lo) * (2 * J / (ctx->w + 1) + 2) * 6 / 5 + 4096);
       const uint64_t cap = std::max<uint64_t>(ctx->flat_need, est);
       if (cap > ctx->sk_cap || (ctx->flat_cap_opt && cap < ctx->sk_cap)) {
         for (int b = 0; b < 2; ++b) {
@@ -2614,12 +2714,16 @@ struct LaunchScan {
         return -1;
       if (hipMemsetAsync(ctx->d_flat_cursor, 0, kFlatCounters * sizeof(unsigned long long), stream) != hipSuccess)
         return -1;
-      sp.flat_keys = ctx->d_sk[0];
-      sp.flat_meta = ctx->d_sm[0];
+      // join INDEX: the dense key records [0, 4 N) come first, the runs' chunks after
+      ctx->flat_off = (ctx->join_P && index) ? 4 * ctx->n : 0;
+      sp.flat_keys = reinterpret_cast<uint64_t*>(reinterpret_cast<uint32_t*>(ctx->d_sk[0]) + ctx->flat_off);
+      sp.flat_meta = ctx->d_sm[0] + ctx->flat_off;
       sp.flat_cursor = ctx->d_flat_cursor;
-      sp.flat_cap = ctx->sk_cap;
+      sp.flat_cap = ctx->sk_cap - ctx->flat_off;
       if (ctx->join_P && index) {  // join records (runs + keys), no cells
         ctx->pack_a = ctx->pack_w = 0;
+        sp.join_kk = reinterpret_cast<uint32_t*>(ctx->d_sk[0]);
+        sp.join_kv = ctx->d_sm[0];
         sp.join_P = ctx->join_P;
         sp.join_A = ctx->join_A;
         sp.join_QB = ctx->join_QB;
@@ -2633,7 +2737,8 @@ struct LaunchScan {
       ctx->pack_a = ctx->pack_w = 0;
     }
     if (index && ctx->key0_ready) sp.key0 = ctx->d_key0;  // mg_build_index allocated it (mixed lengths)
-    if (index && ctx->sorted_index) {  // key records for the sorted build (mg_build_index files them)
+    if (index && (ctx->sorted_index || (scan_is_reg(ctx, true) && !ctx->join_P))) {
+      // key records (bucket, entry), o-major: the sorted build or k_insert_dense files them
       sp.key_bk = ctx->d_kb[0];
       sp.key_ent = ctx->d_ke[0];
       sp.key_n = ctx->n;
@@ -2643,6 +2748,9 @@ struct LaunchScan {
       if (index) {
         allow_lds(k_scan_reg<W, true>, lds);
         hipLaunchKernelGGL((k_scan_reg<W, true>), dim3(sgrid), dim3(wpb * kWave), lds, stream, sp);
+        if (a_hi > a_lo)  // the reverse strand's keys (dense slots 4 a + 2, 4 a + 3)
+          hipLaunchKernelGGL((k_rc_keys<W>), dim3((uint32_t)((a_hi - a_lo + kBlock - 1) / kBlock)), dim3(kBlock), 0,
+                             stream, sp);
       } else {
         allow_lds(k_scan_reg<W, false>, lds);
         hipLaunchKernelGGL((k_scan_reg<W, false>), dim3(sgrid), dim3(wpb * kWave), lds, stream, sp);
@@ -2775,7 +2883,7 @@ struct LaunchProbe {
       bool again = false;
       if (settle_rows(ctx, &again)) return -1;
       if (!again) break;
-      if (ctx->stats && hipMemsetAsync(ctx->d_stats, 0, kSegs * 4 * sizeof(unsigned long long), ctx->stream) != hipSuccess)
+      if (ctx->stats && hipMemsetAsync(ctx->d_stats, 0, (kSegs * 4 + 1) * sizeof(unsigned long long), ctx->stream) != hipSuccess)
         return -1;  // counters of a rerun would double (the probe's are lost too: diagnostics only)
     }
     return 0;
@@ -3066,6 +3174,11 @@ int mg_set_option(mg_ctx* ctx, const char* name, int64_t value) {
     ctx->join_ready = false;
     return 0;
   }
+  if (!strcmp(name, "reg_index")) {  // 1: the cell index from the register scan's key records + k_insert_dense
+    ctx->reg_index = value != 0;
+    ctx->index_ready = false;
+    return 0;
+  }
   if (!strcmp(name, "scan_reg")) {  // 1 (default): register sliding minimum when w <= 32; 0: LDS version
     ctx->scan_reg = value != 0;
     ctx->scan_state = 0;
@@ -3318,8 +3431,8 @@ int ensure_rows(mg_ctx* ctx, uint64_t nsrc) {
     ctx->rows_cap = want;
   }
   if (ctx->stats) {
-    if (!ctx->d_stats) MG_TRY(hipMalloc(&ctx->d_stats, kSegs * 4 * sizeof(unsigned long long)));
-    MG_TRY(hipMemsetAsync(ctx->d_stats, 0, kSegs * 4 * sizeof(unsigned long long), ctx->stream));
+    if (!ctx->d_stats) MG_TRY(hipMalloc(&ctx->d_stats, (kSegs * 4 + 1) * sizeof(unsigned long long)));
+    MG_TRY(hipMemsetAsync(ctx->d_stats, 0, (kSegs * 4 + 1) * sizeof(unsigned long long), ctx->stream));
   }
   return 0;
 }
@@ -3354,7 +3467,7 @@ int settle_rows(mg_ctx* ctx, bool* again) {
 
 void read_stats(mg_ctx* ctx, uint64_t nsrc) {
   if (!ctx->stats) return;
-  std::vector<unsigned long long> st(kSegs * 4);
+  std::vector<unsigned long long> st(kSegs * 4 + 1);
   if (hipMemcpy(st.data(), ctx->d_stats, st.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost) !=
       hipSuccess)
     return;
@@ -3366,6 +3479,7 @@ void read_stats(mg_ctx* ctx, uint64_t nsrc) {
   ctx->counters.verified = acc[2];
   ctx->counters.rows = acc[3];
   ctx->counters.sources = nsrc;
+  ctx->counters.trips = st[kSegs * 4];
 }
 // The window scan of ALL sources, unfiltered (runs of contained or foreign
 // sources are dropped by the probe).  With index = true it is k_scan<INDEX>:
@@ -3398,8 +3512,8 @@ int settle_flat(mg_ctx* ctx, bool* again) {
   for (uint32_t x = 0; x < kFlatCounters; ++x)
     if (c[x]) ext = std::max<uint64_t>(ext, (c[x] - 1) * kFlatCounters + x + 1);
   const uint64_t n = ext * kFlatChunk;
-  if (n > ctx->sk_cap) {
-    ctx->flat_need = n + n / 8 + 4096;
+  if (ctx->flat_off + n > ctx->sk_cap) {
+    ctx->flat_need = ctx->flat_off + n + n / 8 + 4096;
     *again = true;
     return 0;
   }
@@ -3413,11 +3527,14 @@ int settle_flat(mg_ctx* ctx, bool* again) {
     MG_TRY(ensure(&ctx->d_holes, &ctx->holes_cap, nh));
     MG_TRY(hipMemcpyAsync(ctx->d_holes, ctx->holes_host.data(), nh * sizeof(uint64_t), hipMemcpyHostToDevice,
                           ctx->stream));
-    hipLaunchKernelGGL(k_fill_holes, dim3((uint32_t)nh), dim3(kBlock), 0, ctx->stream, ctx->d_holes, ctx->d_sk[0],
-                       ctx->d_sm[0], (ctx->pack_a || ctx->join_P) ? 1 : 0);
+    const bool packed = ctx->pack_a || ctx->join_P;
+    uint64_t* keys = packed ? reinterpret_cast<uint64_t*>(reinterpret_cast<uint32_t*>(ctx->d_sk[0]) + ctx->flat_off)
+                            : ctx->d_sk[0] + ctx->flat_off;
+    hipLaunchKernelGGL(k_fill_holes, dim3((uint32_t)nh), dim3(kBlock), 0, ctx->stream, ctx->d_holes, keys,
+                       ctx->d_sm[0] + ctx->flat_off, packed ? 1 : 0);
     MG_TRY(hipGetLastError());
   }
-  ctx->n_flat = n;
+  ctx->n_flat = ctx->flat_off + n;
   return 0;
 }
 
@@ -3687,7 +3804,7 @@ int probe_join(mg_ctx* ctx, bool contain) {
     bool again = false;
     if (settle_rows(ctx, &again)) return -1;
     if (!again) return 0;
-    if (ctx->stats) MG_TRY(hipMemsetAsync(ctx->d_stats, 0, kSegs * 4 * sizeof(unsigned long long), ctx->stream));
+    if (ctx->stats) MG_TRY(hipMemsetAsync(ctx->d_stats, 0, (kSegs * 4 + 1) * sizeof(unsigned long long), ctx->stream));
   }
   return set_err(ctx, "row buffers overflow after resize");
 }
@@ -3770,16 +3887,26 @@ int mg_build_index(mg_ctx* ctx, uint32_t min_overlap, uint32_t seed_k) {
     // mixed lengths: each read's o = 0 key for the prefix-containment kernel
     ctx->key0_ready = ctx->minlen != ctx->maxlen && ctx->prefix_contain;
     if (ctx->key0_ready) MG_TRY(ensure(&ctx->d_key0, &ctx->key0_cap, ctx->n + 1));
-    if (ctx->sorted_index) {
+    const bool reg_keys = scan_is_reg(ctx, true);  // the register scan writes key records (no CAS inside)
+    if (ctx->sorted_index || reg_keys) {
       MG_TRY(ensure(&ctx->d_kb[0], &ctx->kb_cap, 4 * ctx->n));
-      MG_TRY(ensure(&ctx->d_kb[1], &ctx->kb1_cap, 4 * ctx->n));
       MG_TRY(ensure(&ctx->d_ke[0], &ctx->ke_cap, 4 * ctx->n));
+    }
+    if (ctx->sorted_index) {
+      MG_TRY(ensure(&ctx->d_kb[1], &ctx->kb1_cap, 4 * ctx->n));
       MG_TRY(ensure(&ctx->d_ke[1], &ctx->ke1_cap, 4 * ctx->n));
     }
     if (ctx->n && dispatch_w<LaunchScanAll>(ctx->maxw, ctx, ctx->stream, true))
       return set_err(ctx, "index build launch failed");
     if (!ctx->n) ctx->nrun_reg = 0;
-    if (ctx->sorted_index && fill_sorted_index(ctx)) return -1;
+    if (ctx->sorted_index) {
+      if (fill_sorted_index(ctx)) return -1;
+    } else if (reg_keys && ctx->n) {
+      const uint64_t nk = 4 * ctx->n;
+      hipLaunchKernelGGL(k_insert_dense, dim3((uint32_t)std::min<uint64_t>((nk + kBlock - 1) / kBlock, 65536)),
+                         dim3(kBlock), 0, ctx->stream, ctx->d_kb[0], ctx->d_ke[0], nk, ctx->d_cells, ctx->cell_n);
+      MG_TRY(hipGetLastError());
+    }
     ctx->scan_state = 1;
   } else if (dispatch_w<LaunchIndex>(ctx->maxw, ctx)) {
     return set_err(ctx, "index build launch failed");

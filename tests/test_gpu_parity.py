@@ -701,19 +701,20 @@ def test_register_scan_window_extremes(engine, l, k):
             rows, sup = gpu_rows(engine, ds, l, k=k)
         finally:
             engine.set_option("scan_reg", 0)
-            engine.set_option("join", 1)
+            engine.set_option("join", 0)
         assert np.array_equal(sup.astype(np.uint64), osup), join
         assert np.array_equal(rows_to_tuples(rows), sorted_tuples(orows)), join
 
 
 @pytest.mark.parametrize("name", FIXTURES)
-def test_cell_probe_path(name):
-    """option join = 0: the cell index (CAS inserts inside the scan) + bucket-sorted
-    run probe instead of the partitioned join; same rows and superReadIDs."""
+def test_join_path(name):
+    """option join = 1: the partitioned join (keys + runs as sorted join records,
+    per-partition LDS cells, k_join) instead of the cell index + bucket-sorted
+    run probe; same rows and superReadIDs."""
     meta = load_meta(name)
     ds = Dataset.from_files([fixture_input(name)], meta["l"])
     e = OverlapEngine(0)
-    e.set_option("join", 0)
+    e.set_option("join", 1)
     rows, sup = gpu_rows(e, ds, meta["l"])
     e.close()
     assert np.array_equal(rows_to_tuples(rows), golden_rows(name))
@@ -729,6 +730,7 @@ def test_join_forced_partitions(name, parts):
     meta = load_meta(name)
     ds = Dataset.from_files([fixture_input(name)], meta["l"])
     e = OverlapEngine(0)
+    e.set_option("join", 1)
     e.set_option("join_parts_log2", parts)
     rows, sup = gpu_rows(e, ds, meta["l"])
     e.close()
@@ -744,11 +746,13 @@ def test_join_chunked_containment_vs_oracle(engine):
     seqs = seqs + synth.codes_to_strings(c, L)
     ds = Dataset.from_strings(seqs, l)
     od = OracleDataset.from_strings(seqs, l)
+    engine.set_option("join", 1)
     engine.set_option("join_parts_log2", 1)
     try:
         rows, sup = gpu_rows(engine, ds, l, k=0)
     finally:
         engine.set_option("join_parts_log2", 0)
+        engine.set_option("join", 0)
     orows, osup, _, _ = od.overlaps(l)
     assert np.array_equal(sup.astype(np.uint64), osup)
     assert np.array_equal(rows_to_tuples(rows), sorted_tuples(orows))
