@@ -670,13 +670,14 @@ def test_scan_inside_probe_path(name):
 
 
 @pytest.mark.parametrize("name", FIXTURES)
-def test_scan_register_path(name):
-    """option scan_reg = 1: the register sliding-minimum scan (k_scan_reg)
-    instead of the LDS one (k_scan); same runs, keys and rows."""
+def test_scan_register_index_path(name):
+    """option reg_index = 1: the cell index from the register scan's key records
+    (k_scan_reg<INDEX> + k_rc_keys) filed by k_insert_dense instead of the CAS
+    inserts inside k_scan<INDEX>; same keys, runs and rows."""
     meta = load_meta(name)
     ds = Dataset.from_files([fixture_input(name)], meta["l"])
     e = OverlapEngine(0)
-    e.set_option("scan_reg", 1)
+    e.set_option("reg_index", 1)
     rows, sup = gpu_rows(e, ds, meta["l"])
     e.close()
     assert np.array_equal(rows_to_tuples(rows), golden_rows(name))
@@ -694,13 +695,13 @@ def test_register_scan_window_extremes(engine, l, k):
     ds = Dataset.from_codes(c, L, l)
     od = OracleDataset.from_strings(seqs, l)
     orows, osup, _, _ = od.overlaps(l)
-    for join in (1, 0):
+    for join, reg_index in ((1, 0), (0, 1), (0, 0)):
         engine.set_option("join", join)
-        engine.set_option("scan_reg", 1)
+        engine.set_option("reg_index", reg_index)
         try:
             rows, sup = gpu_rows(engine, ds, l, k=k)
         finally:
-            engine.set_option("scan_reg", 0)
+            engine.set_option("reg_index", 0)
             engine.set_option("join", 0)
         assert np.array_equal(sup.astype(np.uint64), osup), join
         assert np.array_equal(rows_to_tuples(rows), sorted_tuples(orows)), join
@@ -756,3 +757,18 @@ def test_join_chunked_containment_vs_oracle(engine):
     orows, osup, _, _ = od.overlaps(l)
     assert np.array_equal(sup.astype(np.uint64), osup)
     assert np.array_equal(rows_to_tuples(rows), sorted_tuples(orows))
+
+
+@pytest.mark.parametrize("name", ["mixed", "tandem", "highdup", "branchy"])
+def test_scan_lds_path(name):
+    """option scan_reg = 0: the LDS sliding-minimum scan (k_scan) for the run
+    scans as well (source-range shards: a scan per probe pass)."""
+    meta = load_meta(name)
+    ds = Dataset.from_files([fixture_input(name)], meta["l"])
+    e = OverlapEngine(0)
+    e.set_option("scan_reg", 0)
+    e.set_option("overlap_scan", 0)
+    rows, sup = gpu_rows(e, ds, meta["l"])
+    e.close()
+    assert np.array_equal(rows_to_tuples(rows), golden_rows(name))
+    assert {str(i): int(s) for i, s in enumerate(sup) if s} == meta["super"]
