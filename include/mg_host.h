@@ -44,6 +44,16 @@ uint32_t mgh_frequency(const mgh_dataset* ds, uint64_t id); /* Read::getFrequenc
  * strand, 0 if absent. */
 uint64_t mgh_find_read(const mgh_dataset* ds, const char* s, uint64_t len);
 
+/* --- HashTable API values (no device counterpart) --------------------------------
+ * HashTable::getHashTableSize() after insertDataset: the first entry of the
+ * reference's prime table greater than 8 N + 1 (getPrimeLargerThanNumber,
+ * HashTable.cpp:20-29,56); N = unique reads.  HashTable::hashFunction(key)
+ * (HashTable.cpp:135-155) for a table of `table_size` entries.  The device
+ * index does not use either: its exact-key buckets do not depend on the hash
+ * (SURVEY §8(a) a8). */
+uint64_t mgh_hash_table_size(uint64_t n_unique);
+uint64_t mgh_hash_function(const char* key, uint64_t len, uint64_t table_size);
+
 /* --- record splitting -------------------------------------
  * Dataset::readDataset's record splitting (Dataset.cpp:110-193) on a
  * memory-mapped file with nthreads host threads (<= 0: all): FASTA = header

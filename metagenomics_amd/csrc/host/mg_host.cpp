@@ -249,13 +249,91 @@ std::string decode_packed(const uint64_t* w, uint16_t L, bool reverse) {
 int g_default_device = 0;
 uint32_t g_default_seed_k = 0;
 
-// getPrimeLargerThanNumber is a fixed prime list in the reference
-// (HashTable.cpp:20-29); the device index is a power-of-two directory, whose
-// size is what getHashTableSize reports here.
-uint64_t directory_size(uint64_t n) {
-  uint32_t nbl = 10;
-  while (nbl < 30 && (1ull << nbl) < n) nbl++;
-  return 1ull << nbl;
+// getPrimeLargerThanNumber (HashTable.cpp:20-29): the first entry of the
+// reference's fixed table of 450 primes that exceeds `number`, else number + 1.
+// The table is data the API reports (getHashTableSize, hashFunction's modulus);
+// the device index never uses it (its directory is a power of two).
+const uint64_t kRefPrimes[450] = {
+    1114523ULL, 1180043ULL, 1245227ULL, 1310759ULL, 1376447ULL, 1442087ULL, 1507379ULL, 1573667ULL,
+    1638899ULL, 1704023ULL, 1769627ULL, 1835027ULL, 1900667ULL, 1966127ULL, 2031839ULL, 2228483ULL,
+    2359559ULL, 2490707ULL, 2621447ULL, 2752679ULL, 2883767ULL, 3015527ULL, 3145739ULL, 3277283ULL,
+    3408323ULL, 3539267ULL, 3670259ULL, 3801143ULL, 3932483ULL, 4063559ULL, 4456643ULL, 4718699ULL,
+    4980827ULL, 5243003ULL, 5505239ULL, 5767187ULL, 6029603ULL, 6291563ULL, 6553979ULL, 6816527ULL,
+    7079159ULL, 7340639ULL, 7602359ULL, 7864799ULL, 8126747ULL, 8913119ULL, 9437399ULL, 9962207ULL,
+    10485767ULL, 11010383ULL, 11534819ULL, 12059123ULL, 12583007ULL, 13107923ULL, 13631819ULL, 14156543ULL,
+    14680067ULL, 15204467ULL, 15729647ULL, 16253423ULL, 17825999ULL, 18874379ULL, 19923227ULL, 20971799ULL,
+    22020227ULL, 23069447ULL, 24117683ULL, 25166423ULL, 26214743ULL, 27264047ULL, 28312007ULL, 29360147ULL,
+    30410483ULL, 31457627ULL, 32505983ULL, 35651783ULL, 37749983ULL, 39845987ULL, 41943347ULL, 44040383ULL,
+    46137887ULL, 48234623ULL, 50331707ULL, 52429067ULL, 54526019ULL, 56623367ULL, 58720307ULL, 60817763ULL,
+    62915459ULL, 65012279ULL, 71303567ULL, 75497999ULL, 79691867ULL, 83886983ULL, 88080527ULL, 92275307ULL,
+    96470447ULL, 100663439ULL, 104858387ULL, 109052183ULL, 113246699ULL, 117440699ULL, 121635467ULL, 125829239ULL,
+    130023683ULL, 142606379ULL, 150994979ULL, 159383759ULL, 167772239ULL, 176160779ULL, 184549559ULL, 192938003ULL,
+    201327359ULL, 209715719ULL, 218104427ULL, 226493747ULL, 234882239ULL, 243269639ULL, 251659139ULL, 260047367ULL,
+    285215507ULL, 301989959ULL, 318767927ULL, 335544323ULL, 352321643ULL, 369100463ULL, 385876703ULL, 402654059ULL,
+    419432243ULL, 436208447ULL, 452986103ULL, 469762067ULL, 486539519ULL, 503316623ULL, 520094747ULL, 570425399ULL,
+    603979919ULL, 637534763ULL, 671089283ULL, 704643287ULL, 738198347ULL, 771752363ULL, 805307963ULL, 838861103ULL,
+    872415239ULL, 905971007ULL, 939525143ULL, 973079279ULL, 1006633283ULL, 1040187419ULL, 1140852767ULL, 1207960679ULL,
+    1275069143ULL, 1342177379ULL, 1409288183ULL, 1476395699ULL, 1543504343ULL, 1610613119ULL, 1677721667ULL, 1744830587ULL,
+    1811940419ULL, 1879049087ULL, 1946157419ULL, 2013265967ULL, 2080375127ULL, 2281701827ULL, 2415920939ULL, 2550137039ULL,
+    2684355383ULL, 2818572539ULL, 2952791147ULL, 3087008663ULL, 3221226167ULL, 3355444187ULL, 3489661079ULL, 3623878823ULL,
+    3758096939ULL, 3892314659ULL, 4026532187ULL, 4160749883ULL, 4563403379ULL, 4831838783ULL, 5100273923ULL, 5368709219ULL,
+    5637144743ULL, 5905580687ULL, 6174015503ULL, 6442452119ULL, 6710886467ULL, 6979322123ULL, 7247758307ULL, 7516193123ULL,
+    7784629079ULL, 8053065599ULL, 8321499203ULL, 9126806147ULL, 9663676523ULL, 10200548819ULL, 10737418883ULL, 11274289319ULL,
+    11811160139ULL, 12348031523ULL, 12884902223ULL, 13421772839ULL, 13958645543ULL, 14495515943ULL, 15032386163ULL, 15569257247ULL,
+    16106127887ULL, 16642998803ULL, 18253612127ULL, 19327353083ULL, 20401094843ULL, 21474837719ULL, 22548578579ULL, 23622320927ULL,
+    24696062387ULL, 25769803799ULL, 26843546243ULL, 27917287907ULL, 28991030759ULL, 30064772327ULL, 31138513067ULL, 32212254947ULL,
+    33285996803ULL, 36507222923ULL, 38654706323ULL, 40802189423ULL, 42949673423ULL, 45097157927ULL, 47244640319ULL, 49392124247ULL,
+    51539607599ULL, 53687092307ULL, 55834576979ULL, 57982058579ULL, 60129542339ULL, 62277026327ULL, 64424509847ULL, 66571993199ULL,
+    73014444299ULL, 77309412407ULL, 81604379243ULL, 85899346727ULL, 90194314103ULL, 94489281203ULL, 98784255863ULL, 103079215439ULL,
+    107374183703ULL, 111669150239ULL, 115964117999ULL, 120259085183ULL, 124554051983ULL, 128849019059ULL, 133143986399ULL, 146028888179ULL,
+    154618823603ULL, 163208757527ULL, 171798693719ULL, 180388628579ULL, 188978561207ULL, 197568495647ULL, 206158430447ULL, 214748365067ULL,
+    223338303719ULL, 231928234787ULL, 240518168603ULL, 249108103547ULL, 257698038539ULL, 266287975727ULL, 292057776239ULL, 309237645803ULL,
+    326417515547ULL, 343597385507ULL, 360777253763ULL, 377957124803ULL, 395136991499ULL, 412316861267ULL, 429496730879ULL, 446676599987ULL,
+    463856468987ULL, 481036337207ULL, 498216206387ULL, 515396078039ULL, 532575944723ULL, 584115552323ULL, 618475290887ULL, 652835029643ULL,
+    687194768879ULL, 721554506879ULL, 755914244627ULL, 790273985219ULL, 824633721383ULL, 858993459587ULL, 893353198763ULL, 927712936643ULL,
+    962072674643ULL, 996432414899ULL, 1030792152539ULL, 1065151889507ULL, 1168231105859ULL, 1236950582039ULL, 1305670059983ULL, 1374389535587ULL,
+    1443109012607ULL, 1511828491883ULL, 1580547965639ULL, 1649267441747ULL, 1717986918839ULL, 1786706397767ULL, 1855425872459ULL, 1924145348627ULL,
+    1992864827099ULL, 2061584304323ULL, 2130303780503ULL, 2336462210183ULL, 2473901164367ULL, 2611340118887ULL, 2748779070239ULL, 2886218024939ULL,
+    3023656976507ULL, 3161095931639ULL, 3298534883999ULL, 3435973836983ULL, 3573412791647ULL, 3710851743923ULL, 3848290698467ULL, 3985729653707ULL,
+    4123168604483ULL, 4260607557707ULL, 4672924419707ULL, 4947802331663ULL, 5222680234139ULL, 5497558138979ULL, 5772436047947ULL, 6047313952943ULL,
+    6322191860339ULL, 6597069767699ULL, 6871947674003ULL, 7146825580703ULL, 7421703488567ULL, 7696581395627ULL, 7971459304163ULL, 8246337210659ULL,
+    8521215117407ULL, 9345848837267ULL, 9895604651243ULL, 10445360463947ULL, 10995116279639ULL, 11544872100683ULL, 12094627906847ULL, 12644383722779ULL,
+    13194139536659ULL, 13743895350023ULL, 14293651161443ULL, 14843406975659ULL, 15393162789503ULL, 15942918604343ULL, 16492674420863ULL, 17042430234443ULL,
+    18691697672867ULL, 19791209300867ULL, 20890720927823ULL, 21990232555703ULL, 23089744183799ULL, 24189255814847ULL, 25288767440099ULL, 26388279068903ULL,
+    27487790694887ULL, 28587302323787ULL, 29686813951463ULL, 30786325577867ULL, 31885837205567ULL, 32985348833687ULL, 34084860462083ULL, 37383395344739ULL,
+    39582418600883ULL, 41781441856823ULL, 43980465111383ULL, 46179488367203ULL, 48378511622303ULL, 50577534878987ULL, 52776558134423ULL, 54975581392583ULL,
+    57174604644503ULL, 59373627900407ULL, 61572651156383ULL, 63771674412287ULL, 65970697666967ULL, 68169720924167ULL, 74766790688867ULL, 79164837200927ULL,
+    83562883712027ULL, 87960930223163ULL, 92358976733483ULL, 96757023247427ULL, 101155069756823ULL, 105553116266999ULL, 109951162779203ULL, 114349209290003ULL,
+    118747255800179ULL, 123145302311783ULL, 127543348823027ULL, 131941395333479ULL, 136339441846019ULL, 149533581378263ULL, 158329674402959ULL, 167125767424739ULL,
+    175921860444599ULL, 184717953466703ULL, 193514046490343ULL, 202310139514283ULL, 211106232536699ULL, 219902325558107ULL, 228698418578879ULL, 237494511600287ULL,
+    246290604623279ULL, 255086697645023ULL, 263882790666959ULL, 272678883689987ULL, 299067162755363ULL, 316659348799919ULL, 334251534845303ULL, 351843720890723ULL,
+    369435906934019ULL, 387028092977819ULL, 404620279022447ULL, 422212465067447ULL, 439804651111103ULL, 457396837157483ULL, 474989023199423ULL, 492581209246163ULL,
+    510173395291199ULL, 527765581341227ULL, 545357767379483ULL, 598134325510343ULL, 633318697599023ULL, 668503069688723ULL, 703687441776707ULL, 738871813866287ULL,
+    774056185954967ULL, 809240558043419ULL, 844424930134187ULL, 879609302222207ULL, 914793674313899ULL, 949978046398607ULL, 985162418489267ULL, 1020346790579903ULL,
+    1055531162666507ULL, 1090715534754863ULL,
+};
+
+uint64_t prime_larger_than(uint64_t number) {
+  for (uint64_t p : kRefPrimes)
+    if (p > number) return p;
+  return number + 1;
+}
+
+// hashFunction (HashTable.cpp:135-155): 2-bit codes (c >> 1) & 3 (A0 C1 G3 T2),
+// the first 32 characters shifted into sum1, the rest into sum2, both seeded
+// with 1; the product of the residues modulo the table size, in UINT64
+// (wrapping like the reference's when the size exceeds 2^32).
+uint64_t ref_hash(const char* s, uint64_t len, uint64_t size) {
+  uint64_t sum1 = 1, sum2 = 1;
+  for (uint64_t i = 0; i < len; ++i) {
+    const uint64_t c = ((uint64_t)(int)s[i] >> 1) & 3ULL;
+    if (i < 32)
+      sum1 = (sum1 << 2) | c;
+    else
+      sum2 = (sum2 << 2) | c;
+  }
+  const uint64_t P = size ? size : 1;  // (the reference divides by zero before insertDataset)
+  return ((sum1 % P) * (sum2 % P)) % P;
 }
 
 [[noreturn]] void fail(mg_ctx* ctx, const char* what) {
@@ -401,7 +479,7 @@ bool HashTable::insertDataset(Dataset* d, UINT64 minOverlapLength) {
   // HashTable::insertDataset (HashTable.cpp:50-80) on the device
   dataSet = d;
   hashStringLength = (UINT16)(minOverlapLength - 1);
-  hashTableSize = mg::directory_size(d->getNumberOfUniqueReads());
+  hashTableSize = mg::prime_larger_than(d->getNumberOfUniqueReads() * 8 + 1);  // HashTable.cpp:56
   if (!ctx) {
     const int rc = mg_create(&ctx, mg::g_default_device);
     if (rc) {
@@ -433,19 +511,10 @@ std::vector<UINT64>* HashTable::getListOfReads(std::string subString) {
 }
 
 UINT64 HashTable::hashFunction(std::string subString) {
-  // the reference's index function (HashTable.cpp:135-155): 2-bit codes
-  // (c >> 1) & 3, first 32 characters into sum1, the rest into sum2, both
-  // seeded with 1; product of residues modulo the table size
-  UINT64 sum1 = 1, sum2 = 1;
-  for (size_t i = 0; i < subString.size(); ++i) {
-    const UINT64 c = ((UINT64)(int)subString[i] >> 1) & 3ULL;
-    if (i < 32)
-      sum1 = (sum1 << 2) | c;
-    else
-      sum2 = (sum2 << 2) | c;
-  }
-  const UINT64 P = hashTableSize ? hashTableSize : 1;
-  return ((sum1 % P) * (sum2 % P)) % P;
+  // the reference's index function (HashTable.cpp:135-155) modulo the
+  // reference's table size (HashTable.cpp:56); the device index files keys
+  // under minimizers instead, so this value only serves the API
+  return mg::ref_hash(subString.data(), subString.size(), hashTableSize);
 }
 
 // ========================================================== OverlapGraph ====
@@ -940,3 +1009,10 @@ void mgh_parse_free(void* p) { std::free(p); }
 void mgh_parse_set_min_chunk(uint64_t bytes) { mg::g_parse_min_chunk = bytes ? bytes : (1 << 20); }
 
 }  // extern "C"
+
+// ======================================================== HashTable C-ABI ====
+extern "C" uint64_t mgh_hash_table_size(uint64_t n_unique) { return mg::prime_larger_than(n_unique * 8 + 1); }
+
+extern "C" uint64_t mgh_hash_function(const char* key, uint64_t len, uint64_t table_size) {
+  return mg::ref_hash(key, len, table_size);
+}
