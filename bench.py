@@ -10,12 +10,13 @@ Default workload = BASELINE.json configs[2] (C3): 10M x 150 bp synthetic
 reads, 20x coverage of a 75 Mb random genome, 50 % reverse-complemented,
 l = 50, seed k = 31.  Multi-GPU (torchrun, one process per GPU): the same 10M
 reads on N GPUs (strong scaling), DESIGN.md §6:
-  --multi replicated (default): every rank builds the whole index and
-    discovers from its source-read range; no data-path collective (the
-    process group carries only the barrier and the step clock);
-  --multi exchange: each rank owns a bucket range of the index and a
-    source-read range; key records, window runs and rows move between ranks
-    with RCCL all-to-all(v) over xGMI (torch.distributed "nccl").
+  --multi exchange (default, north_star): each rank owns a bucket range of
+    the index and a source-read range; key records, window runs and rows move
+    between ranks with equal-split RCCL all-to-alls over xGMI
+    (torch.distributed "nccl"), ordered on the engine's HIP stream;
+  --multi replicated: every rank builds the whole index and discovers from
+    its source-read range; no data-path collective (the process group carries
+    only the barrier and the step clock).
 --sim-world P runs all P ranks of the chosen mode inside one process on one
 GPU (replicated: each rank timed alone, step = slowest rank; exchange:
 buffers exchanged on the device).
@@ -172,7 +173,8 @@ def parity_digest(engines, last, mode, dist, config):
     import torch
 
     if mode.startswith("exchange"):
-        rows = [e.rows_digest(buf.data_ptr(), n) for e, (buf, n) in zip(engines, last.rows)]
+        rows = [e.slots_digest(buf.data_ptr(), slot, rounds, cnt.data_ptr())
+                for e, (buf, cnt, slot, rounds) in zip(engines, last.rows)]
     else:
         rows = [e.rows_digest() for e in engines]
     sup = engines[0].super_digest() if engines else {"n": 0, "sum": 0, "xor": 0, "sum2": 0}
@@ -229,10 +231,11 @@ def main():
                     help="run all SIM-WORLD ranks of the exchange mode in this process on one GPU")
     ap.add_argument("--exchange", action="store_true",
                     help="use the RCCL exchange mode even with one rank (checks the torch.distributed plumbing)")
-    ap.add_argument("--multi", choices=["replicated", "exchange"], default="replicated",
-                    help="N > 1 (and --sim-world): replicated = every rank builds the whole index and probes its "
-                         "source-read range, no data-path collective (SURVEY 8(e)(ii)); exchange = bucket-range "
-                         "index shards + RCCL all-to-all of keys, runs and rows (SURVEY 8(e) main design)")
+    ap.add_argument("--multi", choices=["replicated", "exchange"], default="exchange",
+                    help="N > 1 (and --sim-world): exchange (default, north_star) = bucket-range index shards + "
+                         "RCCL all-to-all of keys, runs and rows (SURVEY 8(e) main design); replicated = every rank "
+                         "builds the whole index and probes its source-read range, no data-path collective "
+                         "(SURVEY 8(e)(ii))")
     ap.add_argument("--cpu-sample", type=int, default=200_000)
     ap.add_argument("--no-cpu-full", action="store_true", help="skip the reference's full-build timing")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -247,6 +250,12 @@ def main():
     ap.add_argument("--opt", action="append", default=[],
                     help="engine option NAME=VALUE (mg_set_option), repeatable; diagnostics / A-B runs")
     args = ap.parse_args()
+    # stdout carries exactly one JSON line: native libraries (RCCL prints its
+    # version banner at communicator creation) write to fd 1, so fd 1 goes to
+    # stderr for the whole run and the JSON line to a duplicate of the original
+    json_out = os.fdopen(os.dup(1), "w")
+    sys.stdout.flush()
+    os.dup2(2, 1)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -346,14 +355,18 @@ def main():
                 torch.cuda.synchronize(local)
                 rank_ms[i] += (time.perf_counter() - ta) * 1e3
             return tot
-        res = sharded_step(engines, xchg, l, k)
+        res = sharded_step(engines, xchg, l, k, plan=plan[0])
+        plan[0] = plan[0] or res.plan
         last_res[0] = res
         for kk, v in res.ms.items():
             phase_ms[kk] = phase_ms.get(kk, 0.0) + v
-        return sum(nr for _, nr in res.rows)
+        reruns[0] += res.reruns
+        return sum(res.n_rows)
 
     phase_ms = {}
     last_res = [None]
+    plan = [None]    # exchange stream capacities, kept from step to step
+    reruns = [0]     # exchange steps rerun after a capacity overflow (timed steps only)
 
     def sync_barrier():
         torch.cuda.synchronize(local)
@@ -377,6 +390,7 @@ def main():
     dev_ms = {"index_ms": 0.0, "contained_ms": 0.0, "overlap_ms": 0.0, "scan_ms": 0.0, "sort_ms": 0.0,
               "probe_ms": 0.0, "verify_ms": 0.0, "total_ms": 0.0}
     phase_ms.clear()
+    reruns[0] = 0
     rank_ms[:] = [0.0] * len(engines)
     sync_barrier()
     t0 = time.perf_counter()
@@ -443,7 +457,8 @@ def main():
                 "frac": achieved / HBM_PEAK_GBS, "traffic": None,
                 "kernel": ("rank 0 step kernels (whole index build, scan + probe of its source range)"
                            if mode.startswith("replicated") else
-                           "rank 0 step kernels (key records + insert, scan, probe)"),
+                           "rank 0 step device wall (scan + run sort + key exchange + insert, "
+                           "containment + discovery probes; ev0 -> discovery end on the engine's stream)"),
                 "alg_bytes_per_step": alg / P, "kernel_ms_per_step": kern_ms}
     par = {"fused": "1 GPU, fused path",
            "replicated": f"{P} ranks: whole index on every rank, source-read range shards, no data-path collective",
@@ -469,6 +484,7 @@ def main():
         "undirected_edges": edges,
         "device_ms": dev_ms,
         "phase_wall_ms": {kk: v / args.steps for kk, v in phase_ms.items()} or None,
+        "exchange_reruns": reruns[0] if mode.startswith("exchange") else None,
         "counters": cnt,
         "roofline": roof,
         "parity": parity,
@@ -498,7 +514,7 @@ def main():
             res["cpu_baseline"] = cpu_baseline(cfg, args.cpu_sample, not args.no_cpu_full)
         except Exception as e:  # report, never fake
             res["cpu_baseline"] = {"value": None, "error": str(e)}
-    print(json.dumps(res), flush=True)
+    print(json.dumps(res), file=json_out, flush=True)
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()

@@ -151,37 +151,58 @@ int mg_set_shard(mg_ctx* ctx, uint32_t rank, uint32_t nranks, uint64_t read_lo, 
  * Rank r of P (mg_set_shard(ctx, r, P, 0, 0)) owns the index buckets b with
  * floor(b P / 2^nb) == r and the source reads (IDs - 1) in
  * [floor(r N / P), floor((r+1) N / P)); every rank holds all packed reads.
- * One step (the host moves each packed buffer with an all-to-all(v), e.g.
- * torch.distributed.all_to_all_single over RCCL; metagenomics_amd/sharded.py):
- *   mg_key_records -> mg_pack(MG_KEYS) -> a2a -> mg_insert_keys     (insertDataset)
- *   mg_begin_contained(superkey buffer)
- *   [lengths differ: mg_scan_runs(1) -> mg_pack(MG_RUNS) -> a2a
- *    -> mg_probe_runs(1) -> all-reduce MAX of the superkey buffer]   (markContainedReads)
- *   mg_finalize_contained
- *   mg_scan_runs(0) -> mg_pack(MG_RUNS) -> a2a -> mg_probe_runs(0)   (insertAllEdgesOfRead)
- *   -> mg_pack(MG_ROWS) -> a2a: every rank ends with the rows whose src it owns.
- * counts[P] out-parameters give the records bound for each rank (the send
- * split sizes); mg_pack writes them grouped by destination rank, in rank order,
- * into a caller-owned device buffer.  Record sizes: mg_record_bytes(). */
+ *
+ * SLOT LAYOUT.  Records travel between ranks in caller-owned device buffers of
+ * rounds * P * slot records (slot a multiple of 64).  The records a rank sends
+ * to peer d -- or receives from peer s -- form one stream whose i-th record
+ * sits at
+ *     ((i / slot) * P + d) * slot + i % slot,      i < rounds * slot,
+ * so round t of every peer is the contiguous block [t P slot, (t+1) P slot):
+ * one equal-split all-to-all per round moves it (no split sizes on the host),
+ * and one more moves the P per-peer counts (uint64 device arrays).  A stream
+ * longer than rounds * slot is cut there but its count keeps the full length:
+ * the caller reads the counts once at the end of the step (MAX over ranks),
+ * and on an overflow grows the capacity and reruns the step.  Capacities must
+ * be the same on every rank; mg_xchg_caps gives first estimates from global
+ * quantities only.  Every call below only enqueues work on the context's
+ * stream except mg_xchg_begin (one sync: the run count) and mg_xchg_probe(0)
+ * (one sync: the row count); a caller that runs its collectives on the same
+ * stream (metagenomics_amd/sharded.py) never waits on the host in between.
+ *
+ * One step (HashTable::insertDataset + OverlapGraph markContainedReads +
+ * insertAllEdgesOfRead, distributed):
+ *   mg_xchg_begin                 one window scan of this rank's sources: their
+ *                                 4 index keys + minimizer runs, runs sorted by bucket
+ *   mg_xchg_pack(MG_KEYS) -> a2a -> mg_xchg_insert_keys        (insertDataset)
+ *   mg_xchg_pack(MG_RUNS) -> a2a   (the received runs serve both probes)
+ *   mg_begin_contained(superkey)
+ *   [lengths differ: mg_xchg_probe(1) -> all-reduce MAX of superkey]
+ *   mg_finalize_contained                                       (markContainedReads)
+ *   mg_xchg_probe(0) -> mg_xchg_pack(MG_ROWS) -> a2a             (insertAllEdgesOfRead)
+ * and every rank ends with the rows whose src it owns.  Record sizes:
+ * mg_record_bytes(): keys 16 B (bucket, index entry), runs 16 B (bucket |
+ * fingerprint << nb, run meta), rows 12 B (mg_edge). */
 enum { MG_KEYS = 0, MG_RUNS = 1, MG_ROWS = 2 };
 uint32_t mg_record_bytes(int what);
-/* Keys of this rank's source reads (hashRead, HashTable.cpp:88-104) as 16-B
- * index records; sets up (and clears) this rank's part of the index. */
-int mg_key_records(mg_ctx* ctx, uint32_t min_overlap, uint32_t seed_k, uint64_t* counts);
-/* File n received key records (device pointer) into the local index
- * (insertIntoTable, HashTable.cpp:163-195). */
-int mg_insert_keys(mg_ctx* ctx, const void* recs, uint64_t n);
-/* Minimizer runs of this rank's source reads' windows (OverlapGraph.cpp:534-537)
- * as 16-B run records; contain = 1 for the markContainedReads pass. */
-int mg_scan_runs(mg_ctx* ctx, int contain, uint64_t* counts);
-/* Probe n received run records (device pointer) against the local index;
- * contain = 0: verified rows (+ twins) stay in the context, counts[P] = rows
- * per src owner; contain = 1: containment keys (atomicMax) into the superkey
- * buffer of mg_begin_contained. */
-int mg_probe_runs(mg_ctx* ctx, int contain, const void* runs, uint64_t n, uint64_t* counts);
-/* Copy the last routable output (keys, runs or rows) grouped by destination
- * rank into dst (device pointer, capacity cap records). */
-int mg_pack(mg_ctx* ctx, int what, void* dst, uint64_t cap);
+/* First per-peer stream capacities (records) for keys, runs and rows:
+ * caps[3], identical on every rank (global read count and lengths only). */
+int mg_xchg_caps(mg_ctx* ctx, uint32_t min_overlap, uint32_t seed_k, uint64_t* caps);
+/* Set up (and clear) this rank's part of the index, then one scan of its
+ * source reads: the index keys (hashRead, HashTable.cpp:88-104) and the
+ * windows' minimizer runs (OverlapGraph.cpp:534-537), runs radix-sorted by
+ * bucket (so grouped by owning rank). */
+int mg_xchg_begin(mg_ctx* ctx, uint32_t min_overlap, uint32_t seed_k);
+/* Route what = MG_KEYS / MG_RUNS (after mg_xchg_begin) or MG_ROWS (after
+ * mg_xchg_probe(0)) into dst in the slot layout; counts = P device uint64. */
+int mg_xchg_pack(mg_ctx* ctx, int what, void* dst, uint64_t slot, uint32_t rounds, uint64_t* counts);
+/* File the received key records into the local cells (insertIntoTable,
+ * HashTable.cpp:163-195); recv / counts as the all-to-all delivered them. */
+int mg_xchg_insert_keys(mg_ctx* ctx, const void* recv, uint64_t slot, uint32_t rounds, const uint64_t* counts);
+/* Probe the received runs against the local cells: contain = 1 atomicMax-es
+ * containment keys into the buffer of mg_begin_contained; contain = 0 verifies
+ * overlaps (sources with superReadID != 0 give none) and keeps the rows
+ * (+ twins) for mg_xchg_pack(MG_ROWS). */
+int mg_xchg_probe(mg_ctx* ctx, int contain, const void* recv, uint64_t slot, uint32_t rounds, const uint64_t* counts);
 /* Containment: *needed = 1 when read lengths differ (OverlapGraph.cpp:228-233).
  * superkey = caller-owned device array of n_reads u64 (NULL: context-owned),
  * cleared here; the contain probe atomicMax-es (len << 32 | ~index) into it,
@@ -202,9 +223,12 @@ int mg_finalize_contained(mg_ctx* ctx, uint32_t* super_out);
  *   contained read id:          h = mix64((id << 32) | superReadID)
  * Digests of disjoint parts combine by adding count/sum/sum2 and xor-ing xor.
  * mg_rows_digest: rows = NULL digests the context's rows of the last
- * mg_find_overlaps / mg_probe_runs; else `rows` is a device array of n_rows
- * mg_edge records (e.g. an exchange-mode receive buffer). */
+ * mg_find_overlaps / mg_xchg_probe; else `rows` is a device array of n_rows
+ * mg_edge records.  mg_slots_digest: rows received in the slot layout of the
+ * exchange mode (counts = the P device uint64 per-peer counts). */
 int mg_rows_digest(mg_ctx* ctx, const void* rows, uint64_t n_rows, uint64_t* out);
+int mg_slots_digest(mg_ctx* ctx, const void* rows, uint64_t slot, uint32_t rounds, const uint64_t* counts,
+                    uint64_t* out);
 int mg_super_digest(mg_ctx* ctx, uint64_t* out);
 
 /* --- diagnostics ----------------------------------------------------------- */

@@ -72,15 +72,18 @@ struct mg_ctx {
   std::vector<unsigned long long> run_cnt_host;
   uint32_t* d_compact = nullptr;
   size_t compact_cap = 0;
-  // exchange mode (one process per GPU)
-  ulonglong2* d_keyrec = nullptr;   // key records of this rank's source reads
-  size_t keyrec_cap = 0;
-  uint64_t n_keyrec = 0;
-  unsigned long long* d_blk = nullptr;   // routing: per-(block, rank) counts / offsets + totals
+  // exchange mode (one process per GPU): mg_xchg_begin's scan
+  // leaves key records (d_kb[0] / d_ke[0]) and bucket-sorted runs of this
+  // rank's sources; packable = bit mask of what mg_xchg_pack can route now
+  bool xchg = false;                     // the context's current build is an exchange-mode build
+  uint64_t xchg_lo = 0, xchg_hi = 0;     // its source reads
+  unsigned long long* d_blk = nullptr;   // routing: per-(block, rank) counts / offsets
   size_t blk_cap = 0;
-  int packable = -1;                     // MG_KEYS / MG_RUNS / MG_ROWS: what mg_pack copies out
+  int packable = 0;                      // 1 << MG_KEYS | 1 << MG_RUNS | 1 << MG_ROWS
   unsigned long long* d_flat_cnt = nullptr;
   size_t flat_cnt_cap = 0;
+  unsigned long long* d_slot_cnt = nullptr;  // per-region counts of a slot-layout buffer (digest)
+  size_t slot_cnt_cap = 0;
   // timing
   hipEvent_t ev[14] = {};
   // unsharded contexts build the index inside the window scan (k_scan<INDEX>);

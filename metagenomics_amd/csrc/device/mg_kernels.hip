@@ -363,37 +363,20 @@ struct LaunchPrefixContain {
   }
 };
 
-// Exchange mode, step 1: the index records of the keys of source reads
-// [a_lo, a_hi) (16 B: x = mix64(minimizer), y = entry without fingerprint),
-// written densely in key order; k_part routes them to the bucket owners.
-template <int MAXW>
-__global__ __launch_bounds__(kBlock) void k_key_records(IndexParams p, uint64_t a_lo, uint64_t a_hi,
-                                                       ulonglong2* __restrict__ out) {
-  extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
-  const uint64_t gid = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-  const uint64_t r = a_lo + (gid >> 2);
-  const int o = (int)(gid & 3);
-  if (r >= a_hi) return;
-  uint64_t* f = smem + threadIdx.x;
-  const uint64_t* g = p.words + r * slot_words(MAXW);
-#pragma unroll
-  for (int k = 0; k < MAXW; ++k) f[k * kBlock] = g[k];
-  f[MAXW * kBlock] = 0;
-  int q;
-  const uint64_t v = key_minimizer<kBlock>(f, p.len[r], o, p.h, p.m, p.w, &q);
-  out[gid] = make_ulonglong2(v, ((unsigned long long)(((uint32_t)q << 2) | (uint32_t)o) << 32) | (uint32_t)r);
-}
-
-// Exchange mode, step 2: file the records routed to this rank.
-__global__ __launch_bounds__(kBlock) void k_insert_records(IndexParams p, const ulonglong2* __restrict__ rec,
-                                                           uint64_t n) {
-  const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (i >= n) return;
-  const ulonglong2 x = rec[i];
-  const uint64_t b = x.x & ((1ULL << p.nb_log2) - 1);
-  const uint32_t hi = (uint32_t)(x.y >> 32);
-  cell_insert(p.cells, b - p.cell_lo, p.cell_n,
-              make_entry(x.x, p.nb_log2, (int)((hi >> 2) & 1023u), (int)(hi & 3u), (uint32_t)x.y));
+// Exchange mode: file the key records this rank received, in the slot layout
+// of include/mg_overlap.h (record i of peer s at ((i / slot) P + s) slot +
+// i % slot, present while i < counts[s]); x = bucket, y = index entry.
+__global__ __launch_bounds__(kBlock) void k_insert_slots(IndexParams p, const ulonglong2* __restrict__ rec,
+                                                         uint64_t slot, uint32_t rounds,
+                                                         const unsigned long long* __restrict__ counts) {
+  const uint64_t P = p.nranks, blk = P * slot, total = (uint64_t)rounds * blk;
+  for (uint64_t idx = (uint64_t)blockIdx.x * kBlock + threadIdx.x; idx < total; idx += (uint64_t)gridDim.x * kBlock) {
+    const uint64_t t = idx / blk, rem = idx - t * blk, s = rem / slot;
+    if (t * slot + (rem - s * slot) >= counts[s]) continue;
+    const ulonglong2 x = rec[idx];
+    const uint64_t c = x.x - p.cell_lo;
+    if (c < p.cell_n) cell_insert(p.cells, c, p.cell_n, x.y);
+  }
 }
 
 // ------------------------------------------------------------- discovery ---
@@ -2195,31 +2178,40 @@ __global__ __launch_bounds__(kBlock) void k_compact_rows(const uint32_t* __restr
 }
 
 // ------------------------------------------------------- exchange routing ---
-// Records produced in per-wavefront regions (or one flat array) are routed to
-// their owning rank for one all-to-all(v), as a stable-per-block counting sort
-// by destination: pass 0 counts per (block, destination) in LDS, k_part_scan
-// turns the counts into send offsets (destination-major, so the send buffer is
-// grouped by rank in rank order), pass 1 re-walks the same regions with the
-// same grid and scatters through LDS cursors (no global atomics).  Within a
-// wavefront the lanes bound for one destination take one LDS cursor step
-// together (ballot + mbcnt); order inside a destination is irrelevant (the
-// result is a multiset).
-//   OWN_BUCKET: 16-B key/run records, owner of mix64 value x = bucket range
-//               (same rule as owned());
-//   OWN_SRC   : 12-B rows, owner of src ID = source-read range
-//               [floor(r N / P), floor((r+1) N / P)) -> (src P - 1) / N.
-enum OwnerKind { OWN_BUCKET = 0, OWN_SRC = 1 };
+// Exchange mode moves records in the SLOT LAYOUT (include/mg_overlap.h): the
+// records bound for (or received from) peer d form a stream whose i-th record
+// sits at ((i / slot) P + d) slot + i % slot, i < rounds * slot, so round t of
+// every peer is one contiguous block and one equal-split all-to-all per round
+// moves it; the per-peer counts stay on the device.
+//
+// Records produced in per-wavefront regions (rows) or o-major key arrays are
+// routed as a stable-per-block counting sort by destination: pass 0 counts per
+// (block, destination) in LDS, k_part_scan turns the counts into per-
+// destination offsets (and the totals into the caller's device counts), pass 1
+// re-walks the same records with the same grid and scatters through LDS
+// cursors (no global atomics).  Within a wavefront the lanes bound for one
+// destination take one LDS cursor step together (ballot + mbcnt); order inside
+// a destination is irrelevant (the result is a multiset).
+//   OWN_KEY: the four key records (bucket, entry) of every source read, o-major
+//            (key_ent[o key_n + a]); owner = bucket range (same rule as owned());
+//   OWN_SRC: 12-B rows, owner of src ID = source-read range
+//            [floor(r N / P), floor((r+1) N / P)) -> (src P - 1) / N.
+enum OwnerKind { OWN_KEY = 0, OWN_SRC = 1 };
 constexpr int kMaxRanks = 64;
 
 struct PartParams {
-  const void* base;                 // region r starts at base + r * cap records
+  const void* base;                 // OWN_SRC: region r starts at base + r * cap records
   uint64_t cap;                     // records per region
   const unsigned long long* cnt;    // records per region (nullptr: flat array of flat_n records)
   uint64_t nreg, flat_n;
   uint32_t nranks, nb_log2;
   uint64_t n_reads;
-  unsigned long long* blk;          // [gridDim.x * nranks]: pass 0 counts, then send offsets
-  void* out;
+  unsigned long long* blk;          // [gridDim.x * nranks]: pass 0 counts, then offsets
+  void* out;                        // slot layout
+  uint64_t slot, rounds;
+  const uint32_t* key_bk;           // OWN_KEY: sources [a_lo, a_lo + nsrc), key o of read a at o * key_n + a
+  const uint64_t* key_ent;
+  uint64_t key_n, a_lo, nsrc;
 };
 
 template <int KIND, int PASS>
@@ -2229,19 +2221,24 @@ __global__ __launch_bounds__(kBlock) void k_part(PartParams p) {
   if (threadIdx.x < kMaxRanks)
     s_cnt[threadIdx.x] = (PASS == 1 && threadIdx.x < p.nranks) ? p.blk[(uint64_t)blockIdx.x * p.nranks + threadIdx.x] : 0;
   __syncthreads();
+  const uint64_t lim = p.slot * p.rounds;
   for (uint64_t r = blockIdx.x; r < p.nreg; r += gridDim.x) {
     uint64_t c = p.cnt ? p.cnt[r] : (p.flat_n > r * p.cap ? p.flat_n - r * p.cap : 0);
     c = c < p.cap ? c : p.cap;
     for (uint64_t i0 = 0; i0 < c; i0 += kBlock) {
       const uint64_t i = i0 + threadIdx.x;
-      const bool valid = i < c;
+      bool valid = i < c;
       uint32_t d = 0;
       ulonglong2 x16 = make_ulonglong2(0, 0);
       uint3 x12 = make_uint3(0, 0, 0);
       if (valid) {
-        if (KIND == OWN_BUCKET) {
-          x16 = reinterpret_cast<const ulonglong2*>(p.base)[r * p.cap + i];
-          d = (uint32_t)(((x16.x & ((1ULL << p.nb_log2) - 1)) * p.nranks) >> p.nb_log2);
+        if (KIND == OWN_KEY) {
+          const uint64_t v = r * p.cap + i, o = v / p.nsrc, at = o * p.key_n + p.a_lo + (v - o * p.nsrc);
+          const uint64_t e = p.key_ent[at];
+          const uint32_t b = p.key_bk[at];
+          valid = e != kEmpty;  // a read without keys (never after setup_index's length check)
+          x16 = make_ulonglong2(b, e);
+          d = (uint32_t)(((uint64_t)b * p.nranks) >> p.nb_log2);
         } else {
           x12 = reinterpret_cast<const uint3*>(p.base)[r * p.cap + i];
           d = (uint32_t)(((uint64_t)x12.x * p.nranks - 1) / p.n_reads);  // src is the 1-based ID
@@ -2256,10 +2253,11 @@ __global__ __launch_bounds__(kBlock) void k_part(PartParams p) {
         if (lane == leader) at = atomicAdd(&s_cnt[dd], (unsigned long long)__popcll(m));
         if (PASS == 1) {
           at = __shfl(at, leader);
-          if (valid && d == dd) {
-            const uint64_t k = at + lane_prefix(m);
-            if (KIND == OWN_BUCKET) reinterpret_cast<ulonglong2*>(p.out)[k] = x16;
-            else reinterpret_cast<uint3*>(p.out)[k] = x12;
+          const uint64_t k = at + lane_prefix(m);
+          if (valid && d == dd && k < lim) {  // a stream cut at its capacity keeps its full count
+            const uint64_t q = k / p.slot, o = ((q * p.nranks) + dd) * p.slot + (k - q * p.slot);
+            if (KIND == OWN_KEY) reinterpret_cast<ulonglong2*>(p.out)[o] = x16;
+            else reinterpret_cast<uint3*>(p.out)[o] = x12;
           }
         }
         todo &= ~m;
@@ -2272,17 +2270,16 @@ __global__ __launch_bounds__(kBlock) void k_part(PartParams p) {
   }
 }
 
-// Per-(block, destination) counts -> send offsets, destination-major:
-// off[b][d] = sum_{d' < d} total[d'] + sum_{b' < b} cnt[b'][d].  One block;
-// totals[d] out for the host (the all-to-all split sizes).
+// Per-(block, destination) counts -> offsets within each destination's stream:
+// off[b][d] = sum_{b' < b} cnt[b'][d]; totals[d] = the stream's length (the
+// caller's device counts).  One block.
 __global__ __launch_bounds__(1024) void k_part_scan(unsigned long long* blk, uint32_t nblk, uint32_t nranks,
                                                     unsigned long long* totals) {
   __shared__ unsigned long long s_part[1024];
   __shared__ unsigned long long s_base;
-  if (threadIdx.x == 0) s_base = 0;
-  __syncthreads();
   for (uint32_t d = 0; d < nranks; ++d) {
-    const unsigned long long before = s_base;
+    if (threadIdx.x == 0) s_base = 0;
+    __syncthreads();
     for (uint32_t b0 = 0; b0 < nblk; b0 += 1024) {
       const uint32_t b = b0 + threadIdx.x;
       const unsigned long long v = b < nblk ? blk[(uint64_t)b * nranks + d] : 0;
@@ -2299,9 +2296,74 @@ __global__ __launch_bounds__(1024) void k_part_scan(unsigned long long* blk, uin
       if (threadIdx.x == 1023) s_base += s_part[1023];
       __syncthreads();
     }
-    if (threadIdx.x == 0) totals[d] = s_base - before;
+    if (threadIdx.x == 0) totals[d] = s_base;
     __syncthreads();
   }
+}
+
+// The bucket-sorted runs of this rank's sources are grouped by owning rank:
+// bnd[d] = the first record whose bucket rank d (or a later rank) owns.
+__global__ __launch_bounds__(128) void k_dest_bounds(const void* __restrict__ keys, int packed, uint64_t n,
+                                                     uint32_t nranks, uint32_t nb_log2,
+                                                     unsigned long long* __restrict__ bnd) {
+  const uint32_t d = threadIdx.x;
+  if (d > nranks) return;
+  const uint64_t nbm = (1ULL << nb_log2) - 1;
+  uint64_t lo = 0, hi = n;
+  while (lo < hi) {
+    const uint64_t mid = (lo + hi) / 2;
+    const uint64_t k = packed ? reinterpret_cast<const uint32_t*>(keys)[mid] : reinterpret_cast<const uint64_t*>(keys)[mid];
+    if ((((k & nbm) * nranks) >> nb_log2) < d) lo = mid + 1;
+    else hi = mid;
+  }
+  bnd[d] = lo;
+}
+
+// Sorted runs -> 16-B run records (x = bucket | fingerprint << nb, y = run
+// meta; holes stay all-ones, the probe skips them) in the slot layout, in
+// bucket order within each peer's stream; counts[d] = the stream lengths.
+__global__ __launch_bounds__(kBlock) void k_pack_runs(const void* __restrict__ keys, const uint64_t* __restrict__ meta,
+                                                      int pack_a, int pack_w, uint32_t nb_log2, uint64_t n,
+                                                      const unsigned long long* __restrict__ bnd, uint32_t nranks,
+                                                      uint64_t slot, uint64_t rounds, ulonglong2* __restrict__ out,
+                                                      unsigned long long* __restrict__ counts) {
+  __shared__ unsigned long long s_b[kMaxRanks + 1];
+  if (threadIdx.x <= nranks) s_b[threadIdx.x] = bnd[threadIdx.x];
+  __syncthreads();
+  if (blockIdx.x == 0 && threadIdx.x < nranks) counts[threadIdx.x] = s_b[threadIdx.x + 1] - s_b[threadIdx.x];
+  const uint64_t lim = slot * rounds;
+  uint32_t d = 0;
+  for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBlock) {
+    while (d + 1 < nranks && i >= s_b[d + 1]) ++d;  // i only grows: d only grows
+    const uint64_t j = i - s_b[d];
+    if (j >= lim) continue;
+    uint64_t x, y = meta[i];
+    if (y == kFlatHole) {
+      x = ~0ULL;
+    } else if (pack_a) {
+      uint64_t b;
+      uint32_t fp;
+      run_unpack(reinterpret_cast<const uint32_t*>(keys)[i], y, nb_log2, pack_a, pack_w, &b, &fp, &y);
+      x = b | ((uint64_t)fp << nb_log2);
+    } else {
+      x = reinterpret_cast<const uint64_t*>(keys)[i];
+    }
+    const uint64_t q = j / slot;
+    out[((q * nranks) + d) * slot + (j - q * slot)] = make_ulonglong2(x, y);
+  }
+}
+
+// Per-region counts of a slot-layout buffer cut into regions of `reg` records
+// (reg divides slot; region q covers records [q reg, q reg + reg)).
+__global__ __launch_bounds__(kBlock) void k_slot_regions(unsigned long long* __restrict__ out,
+                                                         const unsigned long long* __restrict__ counts,
+                                                         uint64_t slot, uint64_t reg, uint64_t nreg,
+                                                         uint32_t nranks) {
+  const uint64_t q = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (q >= nreg) return;
+  const uint64_t K = slot / reg, blk = q / K, k = q - blk * K, t = blk / nranks, s = blk - t * nranks;
+  const uint64_t start = t * slot + k * reg, c = counts[s];
+  out[q] = c > start ? (c - start < reg ? c - start : reg) : 0;
 }
 
 // Region counts that tile a flat array of n records (probe input in exchange mode).
@@ -2569,7 +2631,9 @@ inline bool use_scan_reg(const mg_ctx* ctx) { return (ctx->scan_reg || ctx->join
 // cell index rides on k_scan<INDEX>
 // (cell mode: option "reg_index" = 1 writes key records that k_insert_dense files;
 // measured slower than k_scan<INDEX>, whose CAS inserts hide behind its ALU work)
-inline bool use_scan_reg_index(const mg_ctx* ctx) { return (ctx->join_P || ctx->reg_index) && use_scan_reg_w(ctx); }
+inline bool use_scan_reg_index(const mg_ctx* ctx) {
+  return (ctx->join_P || ctx->reg_index || ctx->xchg) && use_scan_reg_w(ctx);
+}
 inline uint32_t scan_block_waves(const mg_ctx* ctx);
 inline size_t scan_lds(const mg_ctx* ctx);
 inline uint32_t scan_wpb(uint32_t w) {
@@ -2737,7 +2801,7 @@ struct LaunchScan {
       ctx->pack_a = ctx->pack_w = 0;
     }
     if (index && ctx->key0_ready) sp.key0 = ctx->d_key0;  // mg_build_index allocated it (mixed lengths)
-    if (index && (ctx->sorted_index || (scan_is_reg(ctx, true) && !ctx->join_P))) {
+    if (index && (ctx->sorted_index || ctx->xchg || (scan_is_reg(ctx, true) && !ctx->join_P))) {
       // key records (bucket, entry), o-major: the sorted build or k_insert_dense files them
       sp.key_bk = ctx->d_kb[0];
       sp.key_ent = ctx->d_ke[0];
@@ -3015,7 +3079,7 @@ void mg_destroy(mg_ctx* ctx) {
   (void)hipStreamSynchronize(ctx->stream);
   void* bufs[] = {ctx->d_words, ctx->d_len, ctx->d_cells,
                   ctx->d_superkey, ctx->d_super, ctx->d_any, ctx->d_rows, ctx->d_seg, ctx->d_stats,
-                  ctx->d_compact, ctx->d_runs, ctx->d_run_cnt, ctx->d_keyrec, ctx->d_blk, ctx->d_flat_cnt, ctx->d_cand, ctx->d_cand_cnt, ctx->d_freq,
+                  ctx->d_compact, ctx->d_runs, ctx->d_run_cnt, ctx->d_blk, ctx->d_flat_cnt, ctx->d_slot_cnt, ctx->d_cand, ctx->d_cand_cnt, ctx->d_freq,
                   ctx->d_sk[0], ctx->d_sk[1], ctx->d_sm[0], ctx->d_sm[1], ctx->d_sort_tmp, ctx->d_run_off,
                   ctx->d_flat_cursor, ctx->d_kb[0], ctx->d_kb[1], ctx->d_ke[0], ctx->d_ke[1], ctx->d_key0, ctx->d_holes,
                   ctx->d_digest, ctx->d_bnd, ctx->d_mid, ctx->d_queue};
@@ -3288,6 +3352,8 @@ int setup_index(mg_ctx* ctx, uint32_t min_overlap, uint32_t seed_k, bool cells =
   ctx->contained_done = false;
   ctx->super_any = false;
   ctx->key0_ready = false;  // set by the fused build when it writes the o = 0 keys
+  ctx->xchg = false;        // mg_xchg_begin sets it after this
+  ctx->packable = 0;
   return 0;
 }
 
@@ -3325,93 +3391,77 @@ void source_range(const mg_ctx* ctx, uint64_t* lo, uint64_t* hi) {
   *hi = ctx->n * (ctx->rank + 1) / ctx->nranks;
 }
 
-// Routing pass over 16-B or 12-B records (k_part): counts per destination
-// into counts[] (host) and send offsets per (block, destination) on the device,
-// which the following route_scatter over the same records consumes.
+// Routing of key records or rows (k_part) into a slot-layout buffer; the
+// per-peer stream lengths go to the caller's device counts (no host sync).
 uint32_t part_grid(uint64_t nreg) { return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(nreg, 8192)); }
 
 template <int KIND>
-PartParams part_params(mg_ctx* ctx, const void* base, uint64_t cap, const unsigned long long* cnt, uint64_t nreg,
-                       uint64_t flat_n) {
-  PartParams pp{};
-  pp.base = base;
-  pp.cap = cap;
-  pp.cnt = cnt;
-  pp.nreg = nreg;
-  pp.flat_n = flat_n;
+int route_slots(mg_ctx* ctx, PartParams pp, void* out, uint64_t slot, uint32_t rounds, unsigned long long* counts) {
+  const uint32_t grid = part_grid(pp.nreg);
+  MG_TRY(ensure(&ctx->d_blk, &ctx->blk_cap, (size_t)grid * ctx->nranks));
   pp.nranks = ctx->nranks;
   pp.nb_log2 = ctx->nb_log2;
   pp.n_reads = ctx->n;
   pp.blk = ctx->d_blk;
-  return pp;
-}
-
-template <int KIND>
-int route_count(mg_ctx* ctx, const void* base, uint64_t cap, const unsigned long long* cnt, uint64_t nreg,
-                uint64_t flat_n, uint64_t* counts) {
-  if (ctx->nranks > (uint32_t)kMaxRanks) return set_err(ctx, "at most 64 ranks");
-  const uint32_t grid = part_grid(nreg);
-  MG_TRY(ensure(&ctx->d_blk, &ctx->blk_cap, (size_t)grid * ctx->nranks + kMaxRanks));
-  unsigned long long* totals = ctx->d_blk + (size_t)grid * ctx->nranks;
-  PartParams pp = part_params<KIND>(ctx, base, cap, cnt, nreg, flat_n);
+  pp.out = out;
+  pp.slot = slot;
+  pp.rounds = rounds;
   hipLaunchKernelGGL((k_part<KIND, 0>), dim3(grid), dim3(kBlock), 0, ctx->stream, pp);
   MG_TRY(hipGetLastError());
-  hipLaunchKernelGGL(k_part_scan, dim3(1), dim3(1024), 0, ctx->stream, ctx->d_blk, grid, ctx->nranks, totals);
+  hipLaunchKernelGGL(k_part_scan, dim3(1), dim3(1024), 0, ctx->stream, ctx->d_blk, grid, ctx->nranks, counts);
   MG_TRY(hipGetLastError());
-  std::vector<unsigned long long> c(ctx->nranks);
-  MG_TRY(hipMemcpyAsync(c.data(), totals, ctx->nranks * sizeof(unsigned long long), hipMemcpyDeviceToHost,
-                        ctx->stream));
-  MG_TRY(hipStreamSynchronize(ctx->stream));
-  for (uint32_t i = 0; i < ctx->nranks; ++i) counts[i] = c[i];
-  return 0;
-}
-
-template <int KIND>
-int route_scatter(mg_ctx* ctx, const void* base, uint64_t cap, const unsigned long long* cnt, uint64_t nreg,
-                  uint64_t flat_n, void* out) {
-  PartParams pp = part_params<KIND>(ctx, base, cap, cnt, nreg, flat_n);
-  pp.out = out;
-  hipLaunchKernelGGL((k_part<KIND, 1>), dim3(part_grid(nreg)), dim3(kBlock), 0, ctx->stream, pp);
+  hipLaunchKernelGGL((k_part<KIND, 1>), dim3(grid), dim3(kBlock), 0, ctx->stream, pp);
   MG_TRY(hipGetLastError());
-  MG_TRY(hipStreamSynchronize(ctx->stream));
   return 0;
 }
 
 constexpr uint64_t kFlatRegion = 4096;  // records per routing region of a flat array
 
+// region size of a slot-layout run buffer for the probe: the largest power of
+// two <= 1024 that divides the slot (slots are multiples of 64 records)
+uint64_t slot_region(uint64_t slot) {
+  uint64_t reg = 1024;
+  while (reg > 1 && slot % reg) reg >>= 1;
+  return reg;
+}
+
+// region counts of a slot-layout buffer into *buf (grown as needed)
+int slot_regions(mg_ctx* ctx, unsigned long long** buf, size_t* cap, const unsigned long long* counts,
+                 uint64_t slot, uint64_t reg, uint64_t nreg) {
+  if (*cap < nreg) {
+    if (*buf) (void)hipFree(*buf);
+    *buf = nullptr;
+    *cap = 0;
+    MG_TRY(hipMalloc(buf, nreg * sizeof(unsigned long long)));
+    *cap = nreg;
+  }
+  if (nreg)
+    hipLaunchKernelGGL(k_slot_regions, dim3((uint32_t)((nreg + kBlock - 1) / kBlock)), dim3(kBlock), 0, ctx->stream,
+                       *buf, counts, slot, reg, nreg, ctx->nranks);
+  MG_TRY(hipGetLastError());
+  return 0;
+}
+
+// exchange-mode window scan of this rank's sources: key records + flat runs
 template <int W>
-struct LaunchKeyRecords {
-  static int run(mg_ctx* ctx, uint64_t a_lo, uint64_t a_hi) {
-    IndexParams p = index_params(ctx);
-    const uint64_t nk = 4 * (a_hi - a_lo);
-    if (!nk) return 0;
-    const size_t lds = (size_t)(W + 1) * kBlock * sizeof(uint64_t);
-    allow_lds(k_key_records<W>, lds);
-    hipLaunchKernelGGL((k_key_records<W>), dim3((uint32_t)((nk + kBlock - 1) / kBlock)), dim3(kBlock), lds,
-                       ctx->stream, p, a_lo, a_hi, ctx->d_keyrec);
-    return hipGetLastError() == hipSuccess ? 0 : -1;
+struct LaunchScanXchg {
+  static int run(mg_ctx* ctx, uint64_t lo, uint64_t hi) {
+    const uint32_t wpb = scan_block_waves(ctx, true);
+    const uint64_t groups = (hi - lo + kWave - 1) / kWave;
+    const uint32_t sgrid = scan_resident<W>(ctx, true, (groups + wpb - 1) / wpb);
+    return LaunchScan<W>::run(ctx, true, lo, hi, sgrid, false, ctx->stream, true, true, true);
   }
 };
 
-// exchange-mode probe over a flat array of n received run records
+// exchange-mode probe over received runs in the slot layout (regions of `reg`
+// records, counts in ctx->d_flat_cnt)
 template <int W>
-struct LaunchProbeFlat {
-  static int run(mg_ctx* ctx, bool contain, const ulonglong2* runs, uint64_t n) {
-    const uint64_t approx_src = std::max<uint64_t>(1, n / 8);  // grid sizing only
-    DiscGeom g = disc_geom<W>(ctx, contain, approx_src);
-    const uint64_t nw = (uint64_t)g.grid * kWavesPerBlock;
-    const uint64_t cap = std::max<uint64_t>(1, (n + nw - 1) / nw);
-    if (ctx->flat_cnt_cap < nw) {
-      if (ctx->d_flat_cnt) (void)hipFree(ctx->d_flat_cnt);
-      ctx->d_flat_cnt = nullptr;
-      if (hipMalloc(&ctx->d_flat_cnt, nw * sizeof(unsigned long long)) != hipSuccess) return -1;
-      ctx->flat_cnt_cap = nw;
-    }
-    hipLaunchKernelGGL(k_flat_counts, dim3((uint32_t)((nw + kBlock - 1) / kBlock)), dim3(kBlock), 0, ctx->stream,
-                       ctx->d_flat_cnt, nw, cap, n);
-    if (hipGetLastError() != hipSuccess) return -1;
-    (void)hipEventRecord(ctx->ev[7], ctx->stream);
-    return LaunchProbe<W>::run(ctx, contain, runs, ctx->d_flat_cnt, cap, nw, g.grid, n);
+struct LaunchProbeSlots {
+  static int run(mg_ctx* ctx, bool contain, const ulonglong2* runs, uint64_t reg, uint64_t nregions,
+                 uint64_t approx_runs) {
+    const DiscGeom g = disc_geom<W>(ctx, contain, std::max<uint64_t>(1, ctx->n / ctx->nranks));
+    const uint32_t* sup = (!contain && ctx->contained_done && ctx->super_any) ? ctx->d_super : nullptr;
+    return LaunchProbe<W>::run(ctx, contain, runs, ctx->d_flat_cnt, reg, nregions, g.grid, approx_runs, sup);
   }
 };
 
@@ -4009,7 +4059,6 @@ int mg_find_overlaps(mg_ctx* ctx, uint64_t* n_rows) {
   // device wall of the step: index build start .. last discovery kernel end
   ctx->t.total_ms = shared_scan(ctx) ? elapsed(ctx->ev[0], ctx->ev[5])
                                      : ctx->t.index_ms + ctx->t.contained_ms + ctx->t.overlap_ms;
-  ctx->packable = MG_ROWS;
   if (n_rows) *n_rows = ctx->n_rows;
   return 0;
 }
@@ -4017,136 +4066,176 @@ int mg_find_overlaps(mg_ctx* ctx, uint64_t* n_rows) {
 /* ---------------------------------------------------------- exchange mode --- */
 uint32_t mg_record_bytes(int what) { return what == MG_ROWS ? 12u : (what == MG_KEYS || what == MG_RUNS) ? 16u : 0u; }
 
-int mg_key_records(mg_ctx* ctx, uint32_t min_overlap, uint32_t seed_k, uint64_t* counts) {
-  if (!ctx || !counts) return -1;
-  MG_TRY(hipSetDevice(ctx->device));
-  MG_TRY(hipEventRecord(ctx->ev[0], ctx->stream));
-  if (setup_index(ctx, min_overlap, seed_k)) return -1;
-  uint64_t lo, hi;
-  source_range(ctx, &lo, &hi);
-  ctx->n_keyrec = 4 * (hi - lo);
-  MG_TRY(ensure(&ctx->d_keyrec, &ctx->keyrec_cap, ctx->n_keyrec));
-  if (dispatch_w<LaunchKeyRecords>(ctx->maxw, ctx, lo, hi)) return set_err(ctx, "key record launch failed");
-  if (route_count<OWN_BUCKET>(ctx, ctx->d_keyrec, kFlatRegion, nullptr, (ctx->n_keyrec + kFlatRegion - 1) / kFlatRegion,
-                              ctx->n_keyrec, counts))
-    return -1;
-  ctx->packable = MG_KEYS;
+int mg_xchg_caps(mg_ctx* ctx, uint32_t min_overlap, uint32_t seed_k, uint64_t* caps) {
+  if (!ctx || !caps) return -1;
+  if (min_overlap < 2) return set_err(ctx, "min_overlap must be >= 2");
+  const uint64_t h = min_overlap - 1, m = seed_k ? seed_k : std::min<uint64_t>(31, h);
+  if (m > 32 || m > h) return set_err(ctx, "seed k must satisfy 1 <= k <= min(32, l-1)");
+  const uint64_t w = h - m + 1, P = ctx->nranks;
+  const uint64_t src = (ctx->n + P - 1) / P;  // the most source reads a rank owns
+  const uint64_t J = ctx->maxlen > h + 1 ? ctx->maxlen - h - 1 : 1;
+  auto per_peer = [&](uint64_t total) { return P == 1 ? total : total / P + total / (4 * P); };
+  caps[0] = per_peer(4 * src) + 1024;                                // 4 keys per read, hashed buckets
+  caps[1] = per_peer(src * (2 * J / (w + 1) + 2) * 6 / 5) + 1024;   // the flat scan's run estimate
+  caps[2] = per_peer(32 * src) + 4096;                              // rows: grown from the counts seen
   return 0;
 }
 
-int mg_insert_keys(mg_ctx* ctx, const void* recs, uint64_t n) {
+int mg_xchg_begin(mg_ctx* ctx, uint32_t min_overlap, uint32_t seed_k) {
   if (!ctx) return -1;
   MG_TRY(hipSetDevice(ctx->device));
-  if (!ctx->cell_n) return set_err(ctx, "mg_key_records must run first");
-  if (n) {
+  if (ctx->nranks > (uint32_t)kMaxRanks) return set_err(ctx, "at most 64 ranks");
+  MG_TRY(hipEventRecord(ctx->ev[0], ctx->stream));
+  if (setup_index(ctx, min_overlap, seed_k)) return -1;  // this rank's (cleared) cells
+  ctx->join_P = 0;
+  ctx->xchg = true;
+  uint64_t lo, hi;
+  source_range(ctx, &lo, &hi);
+  ctx->xchg_lo = lo;
+  ctx->xchg_hi = hi;
+  MG_TRY(ensure(&ctx->d_kb[0], &ctx->kb_cap, 4 * ctx->n + 1));
+  MG_TRY(ensure(&ctx->d_ke[0], &ctx->ke_cap, 4 * ctx->n + 1));
+  ctx->scan_state = 0;
+  ctx->sorted_state = 0;
+  ctx->n_flat = ctx->n_sorted = 0;
+  ctx->shared_scan_ms = 0.f;
+  ctx->t = mg_timings{};
+  if (hi > lo) {
+    // one scan: the four keys of every source read (o-major records) + its runs
+    for (int attempt = 0;; ++attempt) {
+      if (attempt == 3) return set_err(ctx, "run buffers overflow after resize");
+      if (dispatch_w<LaunchScanXchg>(ctx->maxw, ctx, lo, hi)) return set_err(ctx, "scan launch failed");
+      bool again = false;
+      if (settle_flat(ctx, &again)) return -1;
+      if (!again) break;
+    }
+    ctx->shared_scan_ms = elapsed(ctx->ev[6], ctx->ev[7]);
+    if (sort_shared_runs(ctx)) return -1;  // bucket order = grouped by owning rank
+  } else {
+    MG_TRY(hipEventRecord(ctx->ev[12], ctx->stream));
+    MG_TRY(hipEventRecord(ctx->ev[13], ctx->stream));
+  }
+  MG_TRY(ensure(&ctx->d_bnd, &ctx->bnd_cap, (size_t)ctx->nranks + 1));
+  hipLaunchKernelGGL(k_dest_bounds, dim3(1), dim3(128), 0, ctx->stream,
+                     ctx->n_sorted ? (const void*)ctx->d_sk[ctx->sk_sel] : (const void*)ctx->d_bnd,
+                     ctx->pack_a ? 1 : 0, ctx->n_sorted, ctx->nranks, ctx->nb_log2, ctx->d_bnd);
+  MG_TRY(hipGetLastError());
+  ctx->packable = (1 << MG_KEYS) | (1 << MG_RUNS);
+  return 0;
+}
+
+int mg_xchg_pack(mg_ctx* ctx, int what, void* dst, uint64_t slot, uint32_t rounds, uint64_t* counts) {
+  if (!ctx) return -1;
+  MG_TRY(hipSetDevice(ctx->device));
+  if (what < MG_KEYS || what > MG_ROWS || !(ctx->packable & (1 << what)))
+    return set_err(ctx, "mg_xchg_pack: nothing of that kind to pack now (call order)");
+  if (!slot || !rounds || !counts || (!dst && slot)) return set_err(ctx, "mg_xchg_pack: bad slot geometry");
+  auto* cnt = reinterpret_cast<unsigned long long*>(counts);
+  const uint64_t nsrc = ctx->xchg_hi - ctx->xchg_lo;
+  if (what == MG_KEYS) {
+    PartParams pp{};
+    pp.cap = kFlatRegion;
+    pp.flat_n = 4 * nsrc;
+    pp.nreg = (pp.flat_n + kFlatRegion - 1) / kFlatRegion;
+    pp.key_bk = ctx->d_kb[0];
+    pp.key_ent = ctx->d_ke[0];
+    pp.key_n = ctx->n;
+    pp.a_lo = ctx->xchg_lo;
+    pp.nsrc = nsrc;
+    return route_slots<OWN_KEY>(ctx, pp, dst, slot, rounds, cnt);
+  }
+  if (what == MG_RUNS) {
+    const uint64_t n = ctx->n_sorted;
+    const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((n + kBlock - 1) / kBlock, 16384));
+    hipLaunchKernelGGL(k_pack_runs, dim3(grid), dim3(kBlock), 0, ctx->stream,
+                       n ? (const void*)ctx->d_sk[ctx->sk_sel] : (const void*)ctx->d_bnd,
+                       n ? ctx->d_sm[ctx->sk_sel] : nullptr, ctx->pack_a, ctx->pack_w, ctx->nb_log2, n, ctx->d_bnd,
+                       ctx->nranks, slot, (uint64_t)rounds, reinterpret_cast<ulonglong2*>(dst), cnt);
+    MG_TRY(hipGetLastError());
+    return 0;
+  }
+  PartParams pp{};
+  pp.base = ctx->d_rows;
+  pp.cap = ctx->nreg ? ctx->rows_cap / ctx->nreg : 0;
+  pp.cnt = ctx->d_seg;
+  pp.nreg = ctx->n_rows ? ctx->nreg : 0;
+  return route_slots<OWN_SRC>(ctx, pp, dst, slot, rounds, cnt);
+}
+
+int mg_xchg_insert_keys(mg_ctx* ctx, const void* recv, uint64_t slot, uint32_t rounds, const uint64_t* counts) {
+  if (!ctx) return -1;
+  MG_TRY(hipSetDevice(ctx->device));
+  if (!ctx->xchg) return set_err(ctx, "mg_xchg_begin must run first");
+  const uint64_t total = (uint64_t)rounds * ctx->nranks * slot;
+  if (total) {
+    if (!recv || !counts) return set_err(ctx, "mg_xchg_insert_keys: null buffer");
     IndexParams p = index_params(ctx);
-    hipLaunchKernelGGL(k_insert_records, dim3((uint32_t)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, ctx->stream, p,
-                       reinterpret_cast<const ulonglong2*>(recs), n);
+    const uint32_t grid = (uint32_t)std::min<uint64_t>((total + kBlock - 1) / kBlock, 65536);
+    hipLaunchKernelGGL(k_insert_slots, dim3(grid), dim3(kBlock), 0, ctx->stream, p,
+                       reinterpret_cast<const ulonglong2*>(recv), slot, rounds,
+                       reinterpret_cast<const unsigned long long*>(counts));
     MG_TRY(hipGetLastError());
   }
   MG_TRY(hipEventRecord(ctx->ev[1], ctx->stream));
-  MG_TRY(hipEventSynchronize(ctx->ev[1]));
-  ctx->t.index_ms = elapsed(ctx->ev[0], ctx->ev[1]);
   ctx->index_ready = true;
   ctx->cells_ready = true;
   return 0;
 }
 
-int mg_scan_runs(mg_ctx* ctx, int contain, uint64_t* counts) {
-  if (!ctx || !counts) return -1;
-  MG_TRY(hipSetDevice(ctx->device));
-  if (!ctx->index_ready) return set_err(ctx, "mg_insert_keys must run first");
-  if (!contain && !ctx->contained_done) return set_err(ctx, "containment must be settled first (mg_finalize_contained)");
-  uint64_t lo, hi;
-  source_range(ctx, &lo, &hi);
-  ctx->nrun_reg = 0;
-  if (hi > lo) {
-    for (int attempt = 0;; ++attempt) {
-      if (attempt == 3) return set_err(ctx, "run buffers overflow after resize");
-      uint32_t sgrid = 0;
-      switch (ctx->maxw) {
-#define MG_G(W) case W: sgrid = disc_geom<W>(ctx, contain != 0, hi - lo).sgrid; break;
-        MG_G(1) MG_G(2) MG_G(3) MG_G(4) MG_G(5) MG_G(6) MG_G(8) MG_G(12) MG_G(16) MG_G(32)
-#undef MG_G
-      }
-      if (dispatch_w<LaunchScan>(ctx->maxw, ctx, contain != 0, lo, hi, sgrid, false))
-        return set_err(ctx, "scan launch failed");
-      bool again = false;
-      if (settle_runs(ctx, &again)) return -1;
-      if (!again) break;
-    }
-  }
-  ctx->t.scan_ms = ctx->nrun_reg ? elapsed(ctx->ev[6], ctx->ev[7]) : 0.f;
-  if (route_count<OWN_BUCKET>(ctx, ctx->d_runs, ctx->run_cap, ctx->d_run_cnt, ctx->nrun_reg, 0, counts)) return -1;
-  ctx->packable = MG_RUNS;
-  return 0;
-}
-
-int mg_probe_runs(mg_ctx* ctx, int contain, const void* runs, uint64_t n, uint64_t* counts) {
+int mg_xchg_probe(mg_ctx* ctx, int contain, const void* recv, uint64_t slot, uint32_t rounds, const uint64_t* counts) {
   if (!ctx) return -1;
   MG_TRY(hipSetDevice(ctx->device));
-  if (!ctx->index_ready) return set_err(ctx, "mg_insert_keys must run first");
+  if (!ctx->xchg || !ctx->index_ready) return set_err(ctx, "mg_xchg_insert_keys must run first");
   if (contain && !ctx->superkey) return set_err(ctx, "mg_begin_contained must run first (lengths differ)");
-  if (!contain && !ctx->contained_done) return set_err(ctx, "containment must be settled first");
+  if (!contain && !ctx->contained_done) return set_err(ctx, "containment must be settled first (mg_finalize_contained)");
+  if ((uint64_t)rounds * slot && (!recv || !counts)) return set_err(ctx, "mg_xchg_probe: null buffer");
+  const uint64_t reg = slot_region(slot);
+  const uint64_t nregions = (uint64_t)rounds * ctx->nranks * (slot / reg);
+  if (slot_regions(ctx, &ctx->d_flat_cnt, &ctx->flat_cnt_cap, reinterpret_cast<const unsigned long long*>(counts),
+                   slot, reg, nregions))
+    return -1;
+  const uint64_t approx = (uint64_t)rounds * ctx->nranks * slot;  // (split probe: candidate sizing only)
+  const auto* runs = reinterpret_cast<const ulonglong2*>(recv);
   ctx->nreg = 0;
   ctx->n_rows = 0;
-  if (!contain && ensure_rows(ctx, std::max<uint64_t>(1, n / 12))) return -1;  // ~4 rows per run
+  if (contain) {
+    MG_TRY(hipEventRecord(ctx->ev[2], ctx->stream));
+    if (nregions && dispatch_w<LaunchProbeSlots>(ctx->maxw, ctx, true, runs, reg, nregions, approx))
+      return set_err(ctx, "probe launch failed");
+    MG_TRY(hipEventRecord(ctx->ev[3], ctx->stream));
+    return 0;
+  }
+  if (ensure_rows(ctx, std::max<uint64_t>(1, ctx->n / ctx->nranks))) return -1;
   for (int attempt = 0;; ++attempt) {
     if (attempt == 3) return set_err(ctx, "row buffers overflow after resize");
     MG_TRY(hipEventRecord(ctx->ev[4], ctx->stream));
-    if (n && dispatch_w<LaunchProbeFlat>(ctx->maxw, ctx, contain != 0, reinterpret_cast<const ulonglong2*>(runs), n))
+    if (nregions && dispatch_w<LaunchProbeSlots>(ctx->maxw, ctx, false, runs, reg, nregions, approx))
       return set_err(ctx, "probe launch failed");
     MG_TRY(hipEventRecord(ctx->ev[5], ctx->stream));
+    if (!nregions) break;
     bool again = false;
-    if (!contain && !ctx->split && settle_rows(ctx, &again)) return -1;
+    if (!ctx->split && settle_rows(ctx, &again)) return -1;
     if (!again) break;
   }
   MG_TRY(hipEventSynchronize(ctx->ev[5]));
+  // device times of this step (events on the context's stream; the exchanges
+  // between them ran on the same stream when the caller used it)
+  ctx->t.scan_ms = ctx->shared_scan_ms;
+  ctx->t.sort_ms = elapsed(ctx->ev[12], ctx->ev[13]);
+  ctx->t.index_ms = elapsed(ctx->ev[0], ctx->ev[1]);
+  ctx->t.contained_ms = ctx->minlen != ctx->maxlen ? elapsed(ctx->ev[2], ctx->ev[3]) : 0.f;
   if (ctx->split) {
-    ctx->t.probe_ms = n ? elapsed(ctx->ev[8], ctx->ev[9]) : 0.f;
-    ctx->t.verify_ms = n ? elapsed(ctx->ev[10], ctx->ev[11]) : 0.f;
+    ctx->t.probe_ms = elapsed(ctx->ev[8], ctx->ev[9]);
+    ctx->t.verify_ms = elapsed(ctx->ev[10], ctx->ev[11]);
   } else {
-    ctx->t.probe_ms = n ? elapsed(ctx->ev[7], ctx->ev[5]) : 0.f;
+    ctx->t.probe_ms = elapsed(ctx->ev[4], ctx->ev[5]);
     ctx->t.verify_ms = 0.f;
   }
-  if (contain) return 0;
-  ctx->t.sort_ms = (shared_scan(ctx) && ctx->sort_runs && ctx->sorted_state == 2)
-                       ? elapsed(ctx->ev[12], ctx->ev[13]) : 0.f;
-  ctx->t.overlap_ms = ctx->t.scan_ms + ctx->t.sort_ms + ctx->t.probe_ms + ctx->t.verify_ms;
-  read_stats(ctx, 0);
-  if (counts) {
-    const uint64_t reg_cap = ctx->nreg ? ctx->rows_cap / ctx->nreg : 0;
-    if (route_count<OWN_SRC>(ctx, ctx->d_rows, reg_cap, ctx->d_seg, ctx->nreg, 0, counts)) return -1;
-  }
-  ctx->packable = MG_ROWS;
+  ctx->t.overlap_ms = ctx->t.probe_ms + ctx->t.verify_ms;
+  ctx->t.total_ms = elapsed(ctx->ev[0], ctx->ev[5]);
+  read_stats(ctx, ctx->xchg_hi - ctx->xchg_lo);
+  ctx->packable |= 1 << MG_ROWS;
   return 0;
-}
-
-int mg_pack(mg_ctx* ctx, int what, void* dst, uint64_t cap) {
-  if (!ctx) return -1;
-  MG_TRY(hipSetDevice(ctx->device));
-  if (what != ctx->packable) return set_err(ctx, "mg_pack: nothing of that kind to pack (call order)");
-  std::vector<uint64_t> counts(ctx->nranks);
-  uint64_t total = 0;
-  if (what == MG_KEYS) {
-    const uint64_t nreg = (ctx->n_keyrec + kFlatRegion - 1) / kFlatRegion;
-    if (route_count<OWN_BUCKET>(ctx, ctx->d_keyrec, kFlatRegion, nullptr, nreg, ctx->n_keyrec, counts.data())) return -1;
-    for (auto c : counts) total += c;
-    if (total > cap) return set_err(ctx, "mg_pack: destination too small");
-    return route_scatter<OWN_BUCKET>(ctx, ctx->d_keyrec, kFlatRegion, nullptr, nreg, ctx->n_keyrec, dst);
-  }
-  if (what == MG_RUNS) {
-    if (route_count<OWN_BUCKET>(ctx, ctx->d_runs, ctx->run_cap, ctx->d_run_cnt, ctx->nrun_reg, 0, counts.data()))
-      return -1;
-    for (auto c : counts) total += c;
-    if (total > cap) return set_err(ctx, "mg_pack: destination too small");
-    return route_scatter<OWN_BUCKET>(ctx, ctx->d_runs, ctx->run_cap, ctx->d_run_cnt, ctx->nrun_reg, 0, dst);
-  }
-  const uint64_t reg_cap = ctx->nreg ? ctx->rows_cap / ctx->nreg : 0;
-  if (route_count<OWN_SRC>(ctx, ctx->d_rows, reg_cap, ctx->d_seg, ctx->nreg, 0, counts.data())) return -1;
-  for (auto c : counts) total += c;
-  if (total > cap) return set_err(ctx, "mg_pack: destination too small");
-  return route_scatter<OWN_SRC>(ctx, ctx->d_rows, reg_cap, ctx->d_seg, ctx->nreg, 0, dst);
 }
 
 int mg_begin_contained(mg_ctx* ctx, void* superkey, int* needed) {
@@ -4166,7 +4255,6 @@ int mg_begin_contained(mg_ctx* ctx, void* superkey, int* needed) {
       ctx->superkey = ctx->d_superkey;
     }
     MG_TRY(hipMemsetAsync(ctx->superkey, 0, ctx->n * sizeof(unsigned long long), ctx->stream));
-    MG_TRY(hipStreamSynchronize(ctx->stream));
   }
   return 0;
 }
@@ -4308,6 +4396,26 @@ int mg_rows_digest(mg_ctx* ctx, const void* rows, uint64_t n_rows, uint64_t* out
   } else if (ctx->nreg && ctx->n_rows) {
     hipLaunchKernelGGL(k_rows_digest, dim3(grid), dim3(kBlock), 0, ctx->stream, ctx->d_rows,
                        ctx->rows_cap / ctx->nreg, ctx->d_seg, ctx->nreg, (uint64_t)0, ctx->d_digest);
+  }
+  return digest_end(ctx, out);
+}
+
+int mg_slots_digest(mg_ctx* ctx, const void* rows, uint64_t slot, uint32_t rounds, const uint64_t* counts,
+                    uint64_t* out) {
+  if (!ctx || !out) return -1;
+  MG_TRY(hipSetDevice(ctx->device));
+  if (digest_begin(ctx)) return -1;
+  const uint64_t nreg = (uint64_t)rounds * ctx->nranks;
+  if (nreg && slot) {
+    if (!rows || !counts) return set_err(ctx, "mg_slots_digest: null buffer");
+    if (slot_regions(ctx, &ctx->d_slot_cnt, &ctx->slot_cnt_cap, reinterpret_cast<const unsigned long long*>(counts),
+                     slot, slot, nreg))
+      return -1;
+    const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(4096, ((uint64_t)ctx->n_cu) * 8));
+    hipLaunchKernelGGL(k_rows_digest, dim3(grid), dim3(kBlock), 0, ctx->stream,
+                       reinterpret_cast<const uint32_t*>(rows), slot, ctx->d_slot_cnt, nreg, (uint64_t)0,
+                       ctx->d_digest);
+    MG_TRY(hipGetLastError());
   }
   return digest_end(ctx, out);
 }

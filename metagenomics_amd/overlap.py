@@ -85,11 +85,12 @@ def lib() -> C.CDLL:
         "mg_ingest_codes": (i32, [vp, vp, u64, u64, vp, u32, P(u64)]),
         "mg_dataset_counts": (i32, [vp, P(u64), P(u64)]),
         "mg_download_frequency": (i32, [vp, vp]),
-        "mg_key_records": (i32, [vp, u32, u32, vp]),
-        "mg_insert_keys": (i32, [vp, vp, u64]),
-        "mg_scan_runs": (i32, [vp, i32, vp]),
-        "mg_probe_runs": (i32, [vp, i32, vp, u64, vp]),
-        "mg_pack": (i32, [vp, i32, vp, u64]),
+        "mg_xchg_caps": (i32, [vp, u32, u32, vp]),
+        "mg_xchg_begin": (i32, [vp, u32, u32]),
+        "mg_xchg_pack": (i32, [vp, i32, vp, u64, u32, vp]),
+        "mg_xchg_insert_keys": (i32, [vp, vp, u64, u32, vp]),
+        "mg_xchg_probe": (i32, [vp, i32, vp, u64, u32, vp]),
+        "mg_slots_digest": (i32, [vp, vp, u64, u32, vp, vp]),
         "mg_begin_contained": (i32, [vp, vp, P(i32)]),
         "mg_finalize_contained": (i32, [vp, vp]),
         "mg_rows_digest": (i32, [vp, vp, u64, vp]),
@@ -395,30 +396,27 @@ class OverlapEngine:
                 return [(int(x & ((1 << 62) - 1)), int(x >> 62)) for x in buf[: n.value]]
             cap = int(n.value)
 
-    # --- exchange mode (one process per GPU; metagenomics_amd/sharded.py drives it)
-    def _counts(self, nranks: int) -> np.ndarray:
-        return np.zeros(max(1, nranks), dtype=np.uint64)
-
-    def key_records(self, min_overlap: int, seed_k: int, nranks: int) -> np.ndarray:
-        c = self._counts(nranks)
-        self._check(lib().mg_key_records(self._h, min_overlap, seed_k, _ptr(c)), "key_records")
+    # --- exchange mode (one process per GPU; metagenomics_amd/sharded.py drives it).
+    # Buffers and counts are device pointers in the slot layout of include/mg_overlap.h.
+    def xchg_caps(self, min_overlap: int, seed_k: int = 0) -> np.ndarray:
+        c = np.zeros(3, dtype=np.uint64)
+        self._check(lib().mg_xchg_caps(self._h, min_overlap, seed_k, _ptr(c)), "xchg_caps")
         return c
 
-    def insert_keys(self, dptr: int, n: int):
-        self._check(lib().mg_insert_keys(self._h, C.c_void_p(dptr), n), "insert_keys")
+    def xchg_begin(self, min_overlap: int, seed_k: int = 0):
+        self._check(lib().mg_xchg_begin(self._h, min_overlap, seed_k), "xchg_begin")
 
-    def scan_runs(self, contain: bool, nranks: int) -> np.ndarray:
-        c = self._counts(nranks)
-        self._check(lib().mg_scan_runs(self._h, int(contain), _ptr(c)), "scan_runs")
-        return c
+    def xchg_pack(self, what: int, dptr: int, slot: int, rounds: int, counts_dptr: int):
+        self._check(lib().mg_xchg_pack(self._h, what, C.c_void_p(dptr), slot, rounds, C.c_void_p(counts_dptr)),
+                    "xchg_pack")
 
-    def probe_runs(self, contain: bool, dptr: int, n: int, nranks: int) -> np.ndarray:
-        c = self._counts(nranks)
-        self._check(lib().mg_probe_runs(self._h, int(contain), C.c_void_p(dptr), n, _ptr(c)), "probe_runs")
-        return c
+    def xchg_insert_keys(self, dptr: int, slot: int, rounds: int, counts_dptr: int):
+        self._check(lib().mg_xchg_insert_keys(self._h, C.c_void_p(dptr), slot, rounds, C.c_void_p(counts_dptr)),
+                    "xchg_insert_keys")
 
-    def pack(self, what: int, dptr: int, cap: int):
-        self._check(lib().mg_pack(self._h, what, C.c_void_p(dptr), cap), "pack")
+    def xchg_probe(self, contain: bool, dptr: int, slot: int, rounds: int, counts_dptr: int):
+        self._check(lib().mg_xchg_probe(self._h, int(contain), C.c_void_p(dptr), slot, rounds,
+                                        C.c_void_p(counts_dptr)), "xchg_probe")
 
     def begin_contained(self, superkey_dptr: int | None) -> bool:
         need = C.c_int()
@@ -443,6 +441,13 @@ class OverlapEngine:
         """Digest of the context's rows (dptr None) or of n mg_edge rows at device pointer dptr."""
         out = np.zeros(4, dtype=np.uint64)
         self._check(lib().mg_rows_digest(self._h, C.c_void_p(dptr or 0), n, _ptr(out)), "rows_digest")
+        return self._digest(out)
+
+    def slots_digest(self, dptr: int, slot: int, rounds: int, counts_dptr: int) -> dict:
+        """Digest of exchange-mode rows received in the slot layout."""
+        out = np.zeros(4, dtype=np.uint64)
+        self._check(lib().mg_slots_digest(self._h, C.c_void_p(dptr), slot, rounds, C.c_void_p(counts_dptr),
+                                          _ptr(out)), "slots_digest")
         return self._digest(out)
 
     def super_digest(self) -> dict:

@@ -4,23 +4,34 @@ One process per GPU. Every rank holds all packed reads. Rank r of P owns two thi
 * the index buckets b with floor(b P / 2^nb) == r (bucket-range sharding);
 * the source reads (IDs - 1) in [floor(r N / P), floor((r+1) N / P)), i.e. graph[u] of those u.
 
-One step is three all-to-all(v) exchanges of packed record buffers, plus one all-reduce when read lengths
-differ:
+One step (``sharded_step``):
 
-1. key records of the rank's source reads → bucket owners → local index (``HashTable::insertDataset``,
-   HashTable.cpp:50-80);
-2. (mixed lengths) containment runs → bucket owners → probe → all-reduce MAX of the per-read
+1. ``xchg_begin``: one window scan of the rank's source reads writes the four index keys of every
+   source read (``hashRead``, HashTable.cpp:88-104) and its minimizer runs; the runs are radix-sorted
+   by bucket, which also groups them by owning rank;
+2. keys -> bucket owners -> local cells (``HashTable::insertDataset``, HashTable.cpp:50-80);
+3. runs -> bucket owners (kept for both probes);
+4. (mixed lengths) containment probe of the received runs, all-reduce MAX of the per-read
    containment keys (``markContainedReads``, OverlapGraph.cpp:225-290);
-3. window runs of the rank's sources → bucket owners → probe + verify (``insertAllEdgesOfRead``,
-   OverlapGraph.cpp:529-565) → rows (+ twins, ``insertEdge`` :407-419) → src owners.
+5. discovery probe + verify of the received runs (``insertAllEdgesOfRead``, OverlapGraph.cpp:529-565)
+   -> rows (+ twins, ``insertEdge`` :407-419) -> src owners.
 
-The compute is the HIP library (``include/mg_overlap.h``, exchange-mode entry points). This module only
-moves the buffers between ranks. ``TorchExchange`` uses ``torch.distributed`` ``all_to_all_single`` over
-RCCL/xGMI (backend "nccl"), or gloo for CPU tests. ``LocalExchange`` drives P simulated ranks inside one
-process, for single-GPU parity tests. The step logic in :func:`sharded_step` is the same for both.
+Records travel in the library's SLOT LAYOUT (include/mg_overlap.h "exchange mode"): per peer a
+fixed-capacity stream of ``rounds * slot`` records, round t of all peers contiguous, so every round
+is ONE equal-split ``all_to_all_single`` straight from the packed buffer (no host-side split sizes,
+no per-round concatenation), and the per-peer record counts travel as a device tensor in one more
+equal-split all-to-all. Nothing in the step waits on the host for the exchange: the capacities are
+fixed up front (``XchgPlan``) and a stream that would not fit is cut; its full count comes back with
+the step's single host read (an all-reduce MAX of the send counts), and the step is rerun with the
+capacities grown. With a CUDA device the library calls, the torch copies and the RCCL collectives
+are all ordered on the engine's own HIP stream.
+
+``TorchExchange`` uses ``torch.distributed`` (backend "nccl" = RCCL over xGMI, or gloo for CPU
+tests). ``LocalExchange`` drives P simulated ranks inside one process (single-GPU parity tests).
 """
 from __future__ import annotations
 
+import contextlib
 import os
 import time
 from dataclasses import dataclass, field
@@ -29,22 +40,68 @@ import numpy as np
 
 from .overlap import EDGE_DTYPE, MG_KEYS, MG_ROWS, MG_RUNS, RECORD_BYTES
 
+SLOT_ALIGN = 64  # slots are whole multiples of this many records (the probe tiles a slot by its divisors)
+KINDS = (MG_KEYS, MG_RUNS, MG_ROWS)
+
+
+def slot_geometry(cap: int, world: int, rec_bytes: int, chunk_bytes: int):
+    """(slot, rounds) for a per-peer stream of at most ``cap`` records: one round moves
+    world * slot records per rank, at most ``chunk_bytes`` (never below one aligned slot)."""
+    per_round = max(SLOT_ALIGN, (chunk_bytes // (world * rec_bytes)) // SLOT_ALIGN * SLOT_ALIGN)
+    want = max(SLOT_ALIGN, -(-int(cap) // SLOT_ALIGN) * SLOT_ALIGN)
+    slot = min(want, per_round)
+    return slot, -(-want // slot)
+
+
+@dataclass
+class XchgPlan:
+    """Per-peer stream capacities (records) for keys, runs and rows; identical on every rank
+    (derived from global quantities only, then grown from all-reduced counts)."""
+    caps: dict = field(default_factory=dict)
+    reruns: int = 0
+
+    def geometry(self, kind: int, world: int, chunk_bytes: int):
+        return slot_geometry(self.caps[kind], world, RECORD_BYTES[kind], chunk_bytes)
+
+    def grow(self, used: dict) -> bool:
+        """Raise capacities below the counts seen; True if any stream overflowed."""
+        over = False
+        for k, c in used.items():
+            if c > self.caps[k]:
+                over = True
+                self.caps[k] = int(c * 1.15) + SLOT_ALIGN
+        return over
+
 
 class Exchange:
-    """Moves per-destination-grouped byte buffers between the ranks this process drives."""
+    """Moves slot-layout buffers between the ranks this process drives."""
 
     world: int
     ranks: list  # the ranks driven by this process
+    device = None
 
     def empty(self, nbytes: int):
-        raise NotImplementedError
+        return self.torch.empty(max(1, int(nbytes)), dtype=self.torch.uint8, device=self.device)
 
-    def all_to_all(self, sends: list, counts: list, rec_bytes: int) -> list:
-        """sends[i]: buffer of local rank i, grouped by destination, counts[i][d]
-        records for d.  Returns [(recv_buffer, n_records)] per local rank."""
+    def counts(self):
+        # no fill kernel: the library writes every entry (a fill on another stream could land after it)
+        return self.torch.empty(self.world, dtype=self.torch.int64, device=self.device)
+
+    def streams(self, engines):
+        """Context in which the step's torch work is ordered with the engines' HIP streams."""
+        return contextlib.nullcontext()
+
+    def all_to_all_slots(self, sends: list, counts: list, slot: int, rounds: int, rec_bytes: int) -> list:
+        """sends[i] / counts[i]: slot-layout buffer and per-peer counts of local rank i.
+        Returns [(recv_buffer, recv_counts)] per local rank, in the same layout."""
         raise NotImplementedError
 
     def allreduce_max(self, bufs: list) -> None:
+        raise NotImplementedError
+
+    def max_counts(self, sent: list) -> np.ndarray:
+        """sent[i] = the per-peer send counts (one tensor per kind) of local rank i: the MAX of
+        each kind over the local ranks and over all ranks, on the host."""
         raise NotImplementedError
 
     def barrier(self) -> None:
@@ -57,11 +114,10 @@ class Exchange:
 class TorchExchange(Exchange):
     """One rank per process over a torch.distributed group (nccl = RCCL on ROCm, or gloo).
 
-    Every all-to-all(v) call moves at most ``chunk_bytes`` in total per rank:
-    the torch-bundled RCCL (2.26.6, ROCm 7.0) corrupts ``all_to_all_single``
-    payloads above ~1 GiB per call (measured with one rank, every dtype:
-    tools/a2a_probe.py), so larger exchanges run in rounds of
-    per-peer slices."""
+    Each round is one equal-split ``all_to_all_single`` of world * slot records, at most
+    ``chunk_bytes`` per rank (256 MiB by default): the torch-bundled RCCL corrupted single
+    all-to-all payloads above ~1 GiB per call in round 1 (tools/a2a_probe.py), and
+    rounds of a few hundred MiB cost nothing measurable on xGMI."""
 
     def __init__(self, device=None, chunk_bytes: int = 256 << 20):
         import torch
@@ -74,59 +130,38 @@ class TorchExchange(Exchange):
         self.device = device if device is not None else torch.device("cpu")
         self.chunk_bytes = int(os.environ.get("MG_A2A_CHUNK_BYTES", chunk_bytes))
 
-    def empty(self, nbytes: int):
-        return self.torch.empty(max(1, int(nbytes)), dtype=self.torch.uint8, device=self.device)
+    def streams(self, engines):
+        if self.device.type != "cuda" or not engines or not hasattr(engines[0], "stream"):
+            return contextlib.nullcontext()
+        # the collectives and torch copies run on the library's stream: no host round trip
+        s = self.torch.cuda.ExternalStream(engines[0].stream(), device=self.device)
+        return self.torch.cuda.stream(s)
 
     def sync(self):
         if self.device.type == "cuda":
-            self.torch.cuda.synchronize(self.device)
+            self.torch.cuda.current_stream(self.device).synchronize()
 
-    def all_to_all(self, sends, counts, rec_bytes):
-        torch, dist = self.torch, self.dist
+    def all_to_all_slots(self, sends, counts, slot, rounds, rec_bytes):
         (send,), (cnt,) = sends, counts
-        P, me, rb = self.world, self.rank, rec_bytes
-        # the full P x P count matrix: M[s, d] = records s -> d
-        sc = torch.tensor([int(c) for c in cnt], dtype=torch.int64, device=self.device)
-        mat = torch.empty(P * P, dtype=torch.int64, device=self.device)
-        dist.all_gather_into_tensor(mat, sc)
-        M = mat.view(P, P).cpu().numpy()
-        scnt, rcnt = M[me, :], M[:, me]
-        soff = np.concatenate([[0], np.cumsum(scnt)])
-        roff = np.concatenate([[0], np.cumsum(rcnt)])
-        n_in = int(rcnt.sum())
-        recv = self.empty(n_in * rb)
-        per_peer = max(1, self.chunk_bytes // (P * rb))  # records per peer per round
-        rounds = max(1, -(-int(M.max()) // per_peer))
-        if rounds == 1:
-            dist.all_to_all_single(recv[: n_in * rb], send[: int(soff[-1]) * rb],
-                                   output_split_sizes=[int(c) * rb for c in rcnt],
-                                   input_split_sizes=[int(c) * rb for c in scnt])
-        else:
-            for t in range(rounds):
-                lo = t * per_peer
-                s_sz = np.clip(scnt - lo, 0, per_peer)
-                r_sz = np.clip(rcnt - lo, 0, per_peer)
-                sbuf = torch.cat([send[int(soff[d] + lo) * rb: int(soff[d] + lo + s_sz[d]) * rb] for d in range(P)])
-                rbuf = self.empty(int(r_sz.sum()) * rb)
-                dist.all_to_all_single(rbuf[: int(r_sz.sum()) * rb], sbuf,
-                                       output_split_sizes=[int(c) * rb for c in r_sz],
-                                       input_split_sizes=[int(c) * rb for c in s_sz])
-                at = 0
-                for s_ in range(P):
-                    nbytes = int(r_sz[s_]) * rb
-                    if nbytes:
-                        dst = int(roff[s_] + lo) * rb
-                        recv[dst: dst + nbytes].copy_(rbuf[at: at + nbytes])
-                    at += nbytes
-        self.sync()
-        return [(recv, n_in)]
+        blk = self.world * slot * rec_bytes
+        recv = self.empty(rounds * blk)
+        for t in range(rounds):
+            self.dist.all_to_all_single(recv[t * blk:(t + 1) * blk], send[t * blk:(t + 1) * blk])
+        rc = self.torch.empty_like(cnt)
+        self.dist.all_to_all_single(rc, cnt)
+        return [(recv, rc)]
 
     def allreduce_max(self, bufs):
         (b,) = bufs
         step = max(1, self.chunk_bytes // b.element_size())
         for i in range(0, b.numel(), step):
             self.dist.all_reduce(b[i: i + step], op=self.dist.ReduceOp.MAX)
-        self.sync()
+
+    def max_counts(self, sent):
+        (cnts,) = sent
+        v = self.torch.stack([c.max() for c in cnts])
+        self.dist.all_reduce(v, op=self.dist.ReduceOp.MAX)
+        return v.cpu().numpy()
 
     def barrier(self):
         self.sync()
@@ -134,36 +169,38 @@ class TorchExchange(Exchange):
 
 
 class LocalExchange(Exchange):
-    """P simulated ranks in one process, all buffers on one device (parity tests)."""
+    """P simulated ranks in one process, all buffers on one device (parity tests, --sim-world).
+    The engines run on separate HIP streams, so every exchange synchronizes the device."""
 
-    def __init__(self, world: int, device=None):
+    def __init__(self, world: int, device=None, chunk_bytes: int = 256 << 20):
         import torch
 
         self.torch = torch
         self.world = world
         self.ranks = list(range(world))
         self.device = device if device is not None else torch.device("cpu")
-
-    def empty(self, nbytes: int):
-        return self.torch.empty(max(1, int(nbytes)), dtype=self.torch.uint8, device=self.device)
+        self.chunk_bytes = int(os.environ.get("MG_A2A_CHUNK_BYTES", chunk_bytes))
 
     def sync(self):
         if self.device.type == "cuda":
             self.torch.cuda.synchronize(self.device)
 
-    def all_to_all(self, sends, counts, rec_bytes):
-        torch = self.torch
-        offs = [np.concatenate([[0], np.cumsum(np.asarray(c, dtype=np.int64))]) * rec_bytes for c in counts]
+    def all_to_all_slots(self, sends, counts, slot, rounds, rec_bytes):
+        P, sb = self.world, slot * rec_bytes
+        self.sync()
         out = []
-        for d in range(self.world):
-            parts = [sends[s][int(offs[s][d]): int(offs[s][d + 1])] for s in range(self.world)]
-            n = sum(int(counts[s][d]) for s in range(self.world))
-            buf = torch.cat(parts) if n else self.empty(0)
-            out.append((buf, n))
+        for d in range(P):
+            recv = self.empty(rounds * P * sb)
+            for t in range(rounds):
+                for s in range(P):
+                    recv[(t * P + s) * sb:(t * P + s + 1) * sb].copy_(sends[s][(t * P + d) * sb:(t * P + d + 1) * sb])
+            rc = self.torch.stack([counts[s][d] for s in range(P)])
+            out.append((recv, rc))
         self.sync()
         return out
 
     def allreduce_max(self, bufs):
+        self.sync()
         m = bufs[0].clone()
         for b in bufs[1:]:
             m = self.torch.maximum(m, b)
@@ -171,19 +208,36 @@ class LocalExchange(Exchange):
             b.copy_(m)
         self.sync()
 
+    def max_counts(self, sent):
+        self.sync()  # the engines wrote the counts on their own streams
+        v = self.torch.stack([self.torch.stack([c.max() for c in cnts]) for cnts in sent])
+        return v.max(dim=0).values.cpu().numpy()
+
 
 @dataclass
 class ShardResult:
-    rows: list            # per local rank: (uint8 buffer of rows, n_rows): the rows whose src it owns
+    rows: list            # per local rank: (uint8 slot buffer, counts tensor, slot, rounds): rows it owns by src
     ms: dict = field(default_factory=dict)
     contained: bool = False
     super_read_id: np.ndarray | None = None  # superReadID per ID (index 0 unused), if requested
+    n_rows: list = field(default_factory=list)  # rows held per local rank
+    reruns: int = 0       # steps rerun with grown capacities
+    plan: XchgPlan | None = None  # the capacities used (pass it to the next step)
 
     def rows_numpy(self, i: int = 0) -> np.ndarray:
-        buf, n = self.rows[i]
-        if n == 0:
-            return np.zeros(0, dtype=EDGE_DTYPE)
-        return buf[: n * 12].cpu().numpy().view(EDGE_DTYPE).copy()
+        """The rows of local rank i, compacted out of the slot layout (host copy)."""
+        buf, cnt, slot, rounds = self.rows[i]
+        c = cnt.cpu().numpy().astype(np.int64)
+        P = len(c)
+        raw = buf[: rounds * P * slot * 12].cpu().numpy().view(EDGE_DTYPE)
+        parts = []
+        for s in range(P):
+            for t in range(rounds):
+                k = min(max(0, int(c[s]) - t * slot), slot)
+                if k:
+                    at = (t * P + s) * slot
+                    parts.append(raw[at: at + k])
+        return np.concatenate(parts).copy() if parts else np.zeros(0, dtype=EDGE_DTYPE)
 
 
 def source_range(n_reads: int, rank: int, world: int):
@@ -191,54 +245,95 @@ def source_range(n_reads: int, rank: int, world: int):
     return n_reads * rank // world, n_reads * (rank + 1) // world
 
 
+def initial_plan(engine, world: int, min_overlap: int, seed_k: int) -> XchgPlan:
+    caps = engine.xchg_caps(min_overlap, seed_k)
+    return XchgPlan(caps={MG_KEYS: int(caps[0]), MG_RUNS: int(caps[1]), MG_ROWS: int(caps[2])})
+
+
 def sharded_step(engines: list, xchg: Exchange, min_overlap: int, seed_k: int = 0,
-                 want_super: bool = False) -> ShardResult:
+                 want_super: bool = False, plan: XchgPlan | None = None) -> ShardResult:
     """One exchange-mode step over the local ranks' engines (set up with
-    ``set_shard(rank, world)`` and the full read set uploaded)."""
+    ``set_shard(rank, world)`` and the full read set uploaded).  ``plan`` carries the
+    stream capacities from step to step (grown in place after an overflow)."""
+    if plan is None:
+        plan = initial_plan(engines[0], xchg.world, min_overlap, seed_k)
+    reruns = 0
+    while True:
+        res, used = _step(engines, xchg, min_overlap, seed_k, want_super, plan)
+        if not plan.grow(used):
+            res.reruns = reruns
+            res.plan = plan
+            return res
+        reruns += 1
+        plan.reruns += 1
+        if reruns > 3:
+            raise RuntimeError(f"exchange capacities still overflow after {reruns} reruns: {used}")
+
+
+def _step(engines, xchg, min_overlap, seed_k, want_super, plan):
     P = xchg.world
+    ch = getattr(xchg, "chunk_bytes", 256 << 20)
     ms = {}
-    t0 = time.perf_counter()
+    sent = {}
 
-    def route(kind, counts):
+    def route(kind):
+        slot, rounds = plan.geometry(kind, P, ch)
         rb = RECORD_BYTES[kind]
-        sends = []
-        for e, c in zip(engines, counts):
-            n = int(np.sum(c))
-            buf = xchg.empty(n * rb)
-            e.pack(kind, buf.data_ptr(), n)
+        sends, cnts = [], []
+        for e in engines:
+            buf = xchg.empty(rounds * P * slot * rb)
+            c = xchg.counts()
+            e.xchg_pack(kind, buf.data_ptr(), slot, rounds, c.data_ptr())
             sends.append(buf)
-        return xchg.all_to_all(sends, counts, rb)
+            cnts.append(c)
+        sent[kind] = cnts
+        return xchg.all_to_all_slots(sends, cnts, slot, rounds, rb), slot, rounds
 
-    # 1. HashTable::insertDataset: key records -> bucket owners -> local index
-    counts = [e.key_records(min_overlap, seed_k, P) for e in engines]
-    for e, (buf, n) in zip(engines, route(MG_KEYS, counts)):
-        e.insert_keys(buf.data_ptr(), n)
-    t1 = time.perf_counter()
-    ms["index"] = (t1 - t0) * 1e3
+    t0 = time.perf_counter()
+    with xchg.streams(engines):
+        # 1. one scan of the rank's sources: index keys + sorted runs
+        for e in engines:
+            e.xchg_begin(min_overlap, seed_k)
+        # 2. HashTable::insertDataset: key records -> bucket owners -> local cells
+        keys, ks, kr = route(MG_KEYS)
+        for e, (buf, c) in zip(engines, keys):
+            e.xchg_insert_keys(buf.data_ptr(), ks, kr, c.data_ptr())
+        # 3. runs -> bucket owners (both probes read them)
+        runs, rs, rr = route(MG_RUNS)
+        t1 = time.perf_counter()
+        ms["index"] = (t1 - t0) * 1e3
 
-    # 2. markContainedReads (only when lengths differ, OverlapGraph.cpp:228-233)
-    # keys (len << 32 | ~index) < 2^48: int64 MAX is the library's unsigned atomicMax
-    contained = bool(engines[0].lengths_differ)
-    skeys = [xchg.torch.empty(max(1, engines[0].n_reads), dtype=xchg.torch.int64, device=xchg.device)
-             if contained else None for _ in engines]
-    for e, sk in zip(engines, skeys):
-        e.begin_contained(sk.data_ptr() if sk is not None else None)
-    if contained:
-        counts = [e.scan_runs(True, P) for e in engines]
-        for e, (buf, n) in zip(engines, route(MG_RUNS, counts)):
-            e.probe_runs(True, buf.data_ptr(), n, P)
-        xchg.allreduce_max(skeys)
-    sup = None
-    for i, e in enumerate(engines):
-        s = e.finalize_contained(copy=want_super and i == 0)
-        sup = s if s is not None else sup
-    del skeys
-    t2 = time.perf_counter()
-    ms["contained"] = (t2 - t1) * 1e3
+        # 4. markContainedReads (only when lengths differ, OverlapGraph.cpp:228-233)
+        # keys (len << 32 | ~index) < 2^48: int64 MAX is the library's unsigned atomicMax
+        contained = bool(engines[0].lengths_differ)
+        skeys = [xchg.torch.empty(max(1, engines[0].n_reads), dtype=xchg.torch.int64, device=xchg.device)
+                 if contained else None for _ in engines]
+        for e, sk in zip(engines, skeys):
+            e.begin_contained(sk.data_ptr() if sk is not None else None)
+        if contained:
+            for e, (buf, c) in zip(engines, runs):
+                e.xchg_probe(True, buf.data_ptr(), rs, rr, c.data_ptr())
+            xchg.allreduce_max(skeys)
+        sup = None
+        for i, e in enumerate(engines):
+            s = e.finalize_contained(copy=want_super and i == 0)
+            sup = s if s is not None else sup
+        del skeys
+        t2 = time.perf_counter()
+        ms["contained"] = (t2 - t1) * 1e3
 
-    # 3. insertAllEdgesOfRead: window runs -> bucket owners -> rows -> src owners
-    counts = [e.scan_runs(False, P) for e in engines]
-    counts = [e.probe_runs(False, buf.data_ptr(), n, P) for e, (buf, n) in zip(engines, route(MG_RUNS, counts))]
-    rows = route(MG_ROWS, counts)
+        # 5. insertAllEdgesOfRead: probe the received runs -> rows -> src owners
+        for e, (buf, c) in zip(engines, runs):
+            e.xchg_probe(False, buf.data_ptr(), rs, rr, c.data_ptr())
+        rows, ws, wr = route(MG_ROWS)
+        # the step's one host read: MAX over ranks of every per-peer send count
+        mx = xchg.max_counts([[sent[k][i] for k in KINDS] for i in range(len(engines))])
+        n_rows = [int(c.sum().item()) for _, c in rows]
+        # (the key and run buffers stay referenced until here: with LocalExchange the
+        # engines' streams may still read them when a del would let torch reuse the memory)
+        del keys, runs
     ms["overlap"] = (time.perf_counter() - t2) * 1e3
-    return ShardResult(rows=rows, ms=ms, contained=contained, super_read_id=sup)
+    used = {k: int(v) for k, v in zip(KINDS, mx)}
+    res = ShardResult(rows=[(b, c, ws, wr) for b, c in rows], ms=ms, contained=contained, super_read_id=sup,
+                      n_rows=n_rows)
+    return res, used

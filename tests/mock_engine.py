@@ -1,11 +1,12 @@
 """TEST INFRASTRUCTURE: a CPU stand-in for the exchange-mode engine interface
-(``OverlapEngine.key_records / pack / insert_keys / scan_runs / probe_runs /
-begin_contained / finalize_contained``) so that the multi-rank orchestration
-(metagenomics_amd/sharded.py) and its all-to-all plumbing can be exercised with
-the gloo backend on CPU.  It does NOT compute overlaps: it replays a known row
-multiset (a golden fixture) under the library's routing rules
-(include/mg_overlap.h "exchange mode"), so that a test can check that every
-record reaches the rank that owns it and that the union is unchanged.
+(``OverlapEngine.xchg_caps / xchg_begin / xchg_pack / xchg_insert_keys /
+xchg_probe / begin_contained / finalize_contained``) so that the multi-rank
+orchestration (metagenomics_amd/sharded.py) and its all-to-all plumbing can be
+exercised with the gloo backend on CPU.  It does NOT compute overlaps: it
+replays a known row multiset (a golden fixture) under the library's routing
+rules and its SLOT LAYOUT (include/mg_overlap.h "exchange mode"), so that a test
+can check that every record reaches the rank that owns it, that cut streams
+are detected and the step rerun, and that the union is unchanged.
 """
 from __future__ import annotations
 
@@ -16,6 +17,7 @@ import numpy as np
 from metagenomics_amd.overlap import EDGE_DTYPE, MG_KEYS, MG_ROWS, MG_RUNS
 
 NB_LOG2 = 20
+REC_DTYPE = np.dtype([("x", "<u8"), ("y", "<u8")])  # 16-B key / run records
 
 
 def mix(x: np.ndarray) -> np.ndarray:
@@ -38,44 +40,78 @@ def src_owner(src: np.ndarray, n_reads: int, world: int) -> np.ndarray:
     return (src.astype(np.int64) * world - 1) // n_reads
 
 
-def _read(ptr: int, nbytes: int) -> bytes:
-    return ctypes.string_at(ptr, nbytes) if nbytes else b""
+def write_slots(ptr: int, recs: np.ndarray, owner: np.ndarray, world: int, slot: int, rounds: int,
+                counts_ptr: int):
+    """The library's slot layout: record i of peer d's stream at ((i // slot) * P + d) * slot + i % slot,
+    streams cut at rounds * slot, full lengths into the device (here: host) counts."""
+    rb = recs.dtype.itemsize
+    cnt = np.zeros(world, np.int64)
+    for d in range(world):
+        stream = np.ascontiguousarray(recs[owner == d])
+        cnt[d] = len(stream)
+        for t in range(rounds):
+            part = stream[t * slot:(t + 1) * slot]
+            if len(part):
+                ctypes.memmove(ptr + (t * world + d) * slot * rb, part.tobytes(), part.nbytes)
+    ctypes.memmove(counts_ptr, cnt.tobytes(), cnt.nbytes)
+
+
+def read_slots(ptr: int, dtype, world: int, slot: int, rounds: int, counts_ptr: int) -> np.ndarray:
+    cnt = np.frombuffer(ctypes.string_at(counts_ptr, 8 * world), dtype=np.int64)
+    rb = np.dtype(dtype).itemsize
+    parts = []
+    for s in range(world):
+        for t in range(rounds):
+            k = min(max(0, int(cnt[s]) - t * slot), slot)
+            if k:
+                parts.append(np.frombuffer(ctypes.string_at(ptr + (t * world + s) * slot * rb, k * rb), dtype=dtype))
+    return np.concatenate(parts) if parts else np.zeros(0, dtype)
 
 
 class MockEngine:
-    def __init__(self, rank: int, world: int, rows: np.ndarray, n_reads: int, lengths_differ: bool = True):
+    def __init__(self, rank: int, world: int, rows: np.ndarray, n_reads: int, lengths_differ: bool = True,
+                 caps=(64, 64, 64)):
         self.rank, self.world = rank, world
         self.rows = rows  # the full directed multiset (EDGE_DTYPE)
         self.n_reads = n_reads
         self.lengths_differ = lengths_differ
         self.lo, self.hi = n_reads * rank // world, n_reads * (rank + 1) // world
-        self._out = None
+        self.caps = caps  # small first capacities: the steps exercise the overflow rerun
         self.received_keys = None
         self.sk_ptr = 0
         self.super_keys = None
+        self.begins = 0
 
-    def _group(self, recs: np.ndarray, owner: np.ndarray) -> np.ndarray:
-        order = np.argsort(owner, kind="stable")
-        self._out = recs[order]
-        return np.bincount(owner, minlength=self.world).astype(np.uint64)
+    def xchg_caps(self, min_overlap, seed_k=0):
+        return np.array(self.caps, dtype=np.uint64)
 
-    # HashTable::insertDataset: 4 key records per source read
-    def key_records(self, min_overlap, seed_k, world):
+    # one scan of the rank's sources: 4 key records per read + one run per read
+    def xchg_begin(self, min_overlap, seed_k=0):
+        self.begins += 1
         idx = np.repeat(np.arange(self.lo, self.hi, dtype=np.uint64), 4)
         o = np.tile(np.arange(4, dtype=np.uint64), self.hi - self.lo)
-        v = mix(idx * np.uint64(4) + o)
-        recs = np.stack([v, (o << np.uint64(32)) | idx], axis=1) if len(idx) else np.zeros((0, 2), np.uint64)
-        return self._group(recs, bucket_owner(recs[:, 0], world) if len(idx) else np.zeros(0, np.int64))
+        self.keys = np.zeros(len(idx), REC_DTYPE)
+        self.keys["x"] = mix(idx * np.uint64(4) + o)
+        self.keys["y"] = (o << np.uint64(32)) | idx
+        a = np.arange(self.lo, self.hi, dtype=np.uint64)
+        self.runs = np.zeros(len(a), REC_DTYPE)
+        self.runs["x"] = mix(a + np.uint64(104729))
+        self.runs["y"] = a
+        self.out_rows = None
 
-    def pack(self, what, ptr, cap):
-        data = np.ascontiguousarray(self._out).tobytes()
-        assert len(data) <= max(1, cap) * (12 if what == MG_ROWS else 16)
-        if data:
-            ctypes.memmove(ptr, data, len(data))
+    def xchg_pack(self, what, ptr, slot, rounds, counts_ptr):
+        if what == MG_KEYS:
+            recs, owner = self.keys, bucket_owner(self.keys["x"], self.world)
+        elif what == MG_RUNS:
+            recs, owner = self.runs, bucket_owner(self.runs["x"], self.world)
+        else:
+            assert self.out_rows is not None, "rows before the discovery probe"
+            recs, owner = self.out_rows, src_owner(self.out_rows["src"], self.n_reads, self.world)
+        write_slots(ptr, recs, owner, self.world, slot, rounds, counts_ptr)
 
-    def insert_keys(self, ptr, n):
-        recs = np.frombuffer(_read(ptr, n * 16), dtype=np.uint64).reshape(-1, 2)
-        assert np.all(bucket_owner(recs[:, 0], self.world) == self.rank), "key record at the wrong rank"
+    def xchg_insert_keys(self, ptr, slot, rounds, counts_ptr):
+        recs = read_slots(ptr, REC_DTYPE, self.world, slot, rounds, counts_ptr)
+        assert np.all(bucket_owner(recs["x"], self.world) == self.rank), "key record at the wrong rank"
         self.received_keys = recs.copy()
 
     def begin_contained(self, ptr):
@@ -84,30 +120,22 @@ class MockEngine:
             ctypes.memset(ptr, 0, self.n_reads * 8)
         return self.lengths_differ
 
-    def scan_runs(self, contain, world):
-        a = np.arange(self.lo, self.hi, dtype=np.uint64)
-        v = mix(a + np.uint64(7919 if contain else 104729))
-        recs = np.stack([v, a], axis=1) if len(a) else np.zeros((0, 2), np.uint64)
-        return self._group(recs, bucket_owner(v, world))
-
-    def probe_runs(self, contain, ptr, n, world):
-        recs = np.frombuffer(_read(ptr, n * 16), dtype=np.uint64).reshape(-1, 2)
-        assert np.all(bucket_owner(recs[:, 0], self.world) == self.rank), "run record at the wrong rank"
-        a = recs[:, 1].astype(np.int64)
+    def xchg_probe(self, contain, ptr, slot, rounds, counts_ptr):
+        recs = read_slots(ptr, REC_DTYPE, self.world, slot, rounds, counts_ptr)
+        assert np.all(bucket_owner(recs["x"], self.world) == self.rank), "run record at the wrong rank"
+        a = recs["y"].astype(np.int64)
         if contain:  # partial maxima the all-reduce must combine
-            sk = np.frombuffer(_read(self.sk_ptr, self.n_reads * 8), dtype=np.int64).copy()
-            tgt = (a * 7) % self.n_reads
-            np.maximum.at(sk, tgt, a + 1)
+            sk = np.frombuffer(ctypes.string_at(self.sk_ptr, self.n_reads * 8), dtype=np.int64).copy()
+            np.maximum.at(sk, (a * 7) % self.n_reads, a + 1)
             ctypes.memmove(self.sk_ptr, sk.tobytes(), sk.nbytes)
-            return np.zeros(world, np.uint64)
+            return
         # every row is "discovered" by the rank that probed min(src, dst)'s run
         mine = np.isin(np.minimum(self.rows["src"], self.rows["dst"]).astype(np.int64) - 1, a)
-        out = self.rows[mine]
-        return self._group(out, src_owner(out["src"], self.n_reads, world))
+        self.out_rows = self.rows[mine]
 
     def finalize_contained(self, copy=False):
         if self.sk_ptr:
-            self.super_keys = np.frombuffer(_read(self.sk_ptr, self.n_reads * 8), dtype=np.int64).copy()
+            self.super_keys = np.frombuffer(ctypes.string_at(self.sk_ptr, self.n_reads * 8), dtype=np.int64).copy()
         self.sk_ptr = 0
         return None
 
@@ -117,7 +145,3 @@ def expected_super_keys(n_reads: int) -> np.ndarray:
     a = np.arange(n_reads, dtype=np.int64)
     np.maximum.at(sk, (a * 7) % n_reads, a + 1)
     return sk
-
-
-def rows_from_buffer(buf, n) -> np.ndarray:
-    return buf[: n * 12].numpy().view(EDGE_DTYPE).copy() if n else np.zeros(0, EDGE_DTYPE)

@@ -297,7 +297,8 @@ def exchange_rows(ds, l, world, k=0, want_super=True):
 
 
 @pytest.mark.parametrize("name,world", [("small", 2), ("mixed", 3), ("tandem", 4), ("highdup", 2),
-                                        ("dirty", 3), ("tworead", 2), ("wrapped", 5)])
+                                        ("dirty", 3), ("tworead", 2), ("wrapped", 5), ("small", 1),
+                                        ("tworead", 3)])
 def test_exchange_mode_matches_reference(name, world):
     meta = load_meta(name)
     ds = Dataset.from_files([fixture_input(name)], meta["l"])
@@ -316,6 +317,45 @@ def test_exchange_mode_random_vs_oracle(case):
     rows, sup = exchange_rows(ds, l, 3, k=k)
     assert np.array_equal(sup.astype(np.uint64), osup)
     assert np.array_equal(rows_to_tuples(rows), sorted_tuples(orows))
+
+
+def test_exchange_mode_cut_streams_rerun():
+    """Streams cut at tiny capacities (64 records per peer, rounds of 128 records):
+    the step sees the overflow in the device counts, grows the capacities and
+    reruns; the same plan then runs without a rerun.  Same rows and superReadIDs
+    as the reference; the slot-layout digest equals the digest of the rows."""
+    import torch
+
+    import digest
+    from metagenomics_amd.overlap import MG_KEYS, MG_ROWS, MG_RUNS
+    from metagenomics_amd.sharded import LocalExchange, XchgPlan, sharded_step
+
+    meta = load_meta("mixed")
+    ds = Dataset.from_files([fixture_input("mixed")], meta["l"])
+    engines = []
+    for r in range(3):
+        e = OverlapEngine(0)
+        e.set_shard(r, 3, 0, 0)
+        e.upload(ds)
+        engines.append(e)
+    xchg = LocalExchange(3, torch.device("cuda:0"), chunk_bytes=3 * 16 * 128)
+    plan = XchgPlan(caps={MG_KEYS: 64, MG_RUNS: 64, MG_ROWS: 64})
+    for attempt in range(2):
+        res = sharded_step(engines, xchg, meta["l"], 0, want_super=True, plan=plan)
+        assert (res.reruns >= 1) if attempt == 0 else (res.reruns == 0)
+        rows = np.concatenate([res.rows_numpy(r) for r in range(3)])
+        assert np.array_equal(rows_to_tuples(rows), golden_rows("mixed"))
+        assert {str(i): int(s) for i, s in enumerate(res.super_read_id) if s} == meta["super"]
+        ds_dev = [e.slots_digest(b.data_ptr(), slot, rounds, c.data_ptr())
+                  for e, (b, c, slot, rounds) in zip(engines, res.rows)]
+        tot = {"n": 0, "sum": 0, "xor": 0, "sum2": 0}
+        for d in ds_dev:
+            tot = {"n": tot["n"] + d["n"], "sum": (tot["sum"] + d["sum"]) % 2**64, "xor": tot["xor"] ^ d["xor"],
+                   "sum2": (tot["sum2"] + d["sum2"]) % 2**64}
+        g = golden_rows("mixed")
+        assert tot == digest.rows_digest(g[:, 0], g[:, 1], g[:, 2], g[:, 3])
+    for e in engines:
+        e.close()
 
 
 def test_exchange_mode_c2_scale_matches_fused(engine):

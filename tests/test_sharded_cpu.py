@@ -1,7 +1,9 @@
 """Multi-rank exchange orchestration (metagenomics_amd/sharded.py) on CPU with
 the gloo backend, world_size 2 and 3: every key/run record reaches its bucket
 owner, every row reaches its src owner, the union of the ranks' rows is the
-reference multiset, and the containment keys are MAX-reduced across ranks.
+reference multiset, the containment keys are MAX-reduced across ranks, and
+streams cut at their slot capacity are detected and the step rerun with grown
+capacities (the mock starts every stream at 64 records).
 The engine is tests/mock_engine.py (routing rules of include/mg_overlap.h); the
 GPU kernels behind the same calls are covered by tests/test_gpu_parity.py."""
 import os
@@ -46,6 +48,8 @@ def _worker(rank, world, port, name, outdir, chunk):
     eng = MockEngine(rank, world, rows, n)
     res = sharded_step([eng], TorchExchange(), lm(name)["l"], 0)
     mine = res.rows_numpy(0)
+    assert res.n_rows == [len(mine)]
+    np.save(os.path.join(outdir, f"reruns{rank}.npy"), np.array([res.reruns, eng.begins]))
     np.save(os.path.join(outdir, f"rows{rank}.npy"), mine)
     np.save(os.path.join(outdir, f"keys{rank}.npy"), eng.received_keys)
     np.save(os.path.join(outdir, f"sk{rank}.npy"), eng.super_keys)
@@ -69,7 +73,22 @@ def test_exchange_routes_every_record(tmp_path, name, world, chunk):
         keys += np.load(tmp_path / f"keys{r}.npy").shape[0]
         assert np.array_equal(np.load(tmp_path / f"sk{r}.npy"), expected_super_keys(n))
     assert keys == 4 * n
+    rr = [np.load(tmp_path / f"reruns{r}.npy") for r in range(world)]
+    assert all(x[0] == rr[0][0] for x in rr), "ranks disagree on the reruns"
+    assert all(x[1] == x[0] + 1 for x in rr)  # one begin per attempt
     allr = np.concatenate(parts)
     t = np.stack([allr["src"], allr["dst"], allr["orient"], allr["offset"]], axis=1).astype(np.int64)
     t = t[np.lexsort((t[:, 3], t[:, 2], t[:, 1], t[:, 0]))]
     assert np.array_equal(t, golden_rows(name))
+
+
+def test_slot_geometry():
+    from metagenomics_amd.sharded import SLOT_ALIGN, slot_geometry
+
+    for cap, world, rb, ch in [(1, 1, 16, 256 << 20), (10**8, 1, 16, 256 << 20), (10**8, 8, 12, 256 << 20),
+                               (1000, 2, 16, 4096), (64, 3, 12, 100), (5 * 10**6, 64, 16, 256 << 20)]:
+        slot, rounds = slot_geometry(cap, world, rb, ch)
+        assert slot % SLOT_ALIGN == 0 and slot >= SLOT_ALIGN and rounds >= 1
+        assert slot * rounds >= cap
+        assert world * slot * rb <= max(ch, world * SLOT_ALIGN * rb)  # a round stays within the chunk
+        assert world * slot * rb < 2**31  # every all-to-all call's byte count fits int32

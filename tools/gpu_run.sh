@@ -23,8 +23,8 @@ for s in $STEPS; do
     rc=$?; echo "bench rc=$rc"; cat $OUT/bench.json ;;
   sim)
     for P in 2 4 8; do
-      timeout -k 10 300 python -u bench.py --sim-world $P --multi exchange --steps 3 > $OUT/bench_sim$P.json 2> $OUT/bench_sim$P.err
-      rc=$?; echo "bench sim $P rc=$rc"; cat $OUT/bench_sim$P.json; [ $rc -ne 0 ] && break
+      timeout -k 10 300 python -u bench.py --sim-world $P --multi exchange --steps 3 --no-cpu-baseline --no-ingest > $OUT/bench_sim$P.json 2> $OUT/bench_sim$P.err
+      rc=$?; echo "bench sim $P rc=$rc"; python3 -c "import json;d=json.load(open('$OUT/bench_sim$P.json'));print('ms/step',round(d['ms_per_step'],3),'digest_ok',d['parity'].get('digest_ok'),'reruns',d.get('exchange_reruns'),d.get('phase_wall_ms'))"; [ $rc -ne 0 ] && break
     done ;;
   simrep)
     for P in 2 4 8; do
@@ -32,8 +32,15 @@ for s in $STEPS; do
       rc=$?; echo "bench sim replicated $P rc=$rc"; python3 -c "import json;d=json.load(open('$OUT/bench_simrep$P.json'));print(d['ms_per_step'], d['value'], d['undirected_edges'], d.get('sim_rank_ms'))"; [ $rc -ne 0 ] && break
     done ;;
   xchg1)
-    timeout -k 10 300 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29511 bench.py --exchange --steps 3 --no-cpu-baseline > $OUT/bench_xchg1.json 2> $OUT/bench_xchg1.err
-    rc=$?; echo "bench exchange(RCCL, 1 rank) rc=$rc"; cat $OUT/bench_xchg1.json ;;
+    timeout -k 10 300 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29511 bench.py --exchange --steps 5 --no-cpu-baseline --no-ingest > $OUT/bench_xchg1.json 2> $OUT/bench_xchg1.err
+    rc=$?; echo "bench exchange(RCCL, 1 rank) rc=$rc"; python3 -c "import json;d=json.load(open('$OUT/bench_xchg1.json'));print('ms/step',round(d['ms_per_step'],3),'edges',d['undirected_edges'],'digest_ok',d['parity'].get('digest_ok'),'reruns',d.get('exchange_reruns'),{k:round(v,3) for k,v in d['device_ms'].items()},d.get('phase_wall_ms'))" ;;
+  profxchg1)
+    export MASTER_ADDR=127.0.0.1 MASTER_PORT=29513 RANK=0 WORLD_SIZE=1 LOCAL_RANK=0
+    timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/profxchg1 -o kt -- python3 bench.py --exchange --steps 5 --no-cpu-baseline --no-ingest > $OUT/profxchg1_bench.json 2> $OUT/profxchg1_bench.err
+    rc=$?; unset MASTER_ADDR MASTER_PORT RANK WORLD_SIZE LOCAL_RANK; echo "profxchg1 rc=$rc"; cat $OUT/profxchg1_bench.json; head -24 $OUT/profxchg1/kt_kernel_stats.csv | cut -c1-160 ;;
+  xchgtests)
+    timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -x -v -m gpu -k exchange --timeout 300 --timeout-method thread > $OUT/xchg_tests.log 2>&1
+    rc=$?; echo "exchange tests rc=$rc"; grep -E "PASS|FAIL|Error" $OUT/xchg_tests.log | tail -20 ;;
   digest)
     timeout -k 10 600 python -u -m pytest tests/test_scale_digest.py -x -v -m gpu --timeout 300 --timeout-method thread > $OUT/digest_tests.log 2>&1
     rc=$?; echo "digest tests rc=$rc"; grep -E "PASS|FAIL|SKIP|Error" $OUT/digest_tests.log | tail -12 ;;
