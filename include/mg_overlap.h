@@ -193,8 +193,13 @@ int mg_xchg_caps(mg_ctx* ctx, uint32_t min_overlap, uint32_t seed_k, uint64_t* c
  * bucket (so grouped by owning rank). */
 int mg_xchg_begin(mg_ctx* ctx, uint32_t min_overlap, uint32_t seed_k);
 /* Route what = MG_KEYS / MG_RUNS (after mg_xchg_begin) or MG_ROWS (after
- * mg_xchg_probe(0)) into dst in the slot layout; counts = P device uint64. */
-int mg_xchg_pack(mg_ctx* ctx, int what, void* dst, uint64_t slot, uint32_t rounds, uint64_t* counts);
+ * mg_xchg_probe(0)) into dst in the slot layout; counts = P device uint64.
+ * self_dst (optional): the stream bound for this rank itself is written there
+ * instead -- the caller's receive buffer, whose slots for this rank sit at the
+ * same offsets -- so it never travels (the all-to-all then moves only the
+ * other peers' slots; dst may be NULL when P == 1). */
+int mg_xchg_pack(mg_ctx* ctx, int what, void* dst, uint64_t slot, uint32_t rounds, uint64_t* counts,
+                 void* self_dst);
 /* File the received key records into the local cells (insertIntoTable,
  * HashTable.cpp:163-195); recv / counts as the all-to-all delivered them. */
 int mg_xchg_insert_keys(mg_ctx* ctx, const void* recv, uint64_t slot, uint32_t rounds, const uint64_t* counts);

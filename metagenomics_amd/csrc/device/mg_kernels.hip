@@ -2208,6 +2208,8 @@ struct PartParams {
   uint64_t n_reads;
   unsigned long long* blk;          // [gridDim.x * nranks]: pass 0 counts, then offsets
   void* out;                        // slot layout
+  void* self_out;                   // non-null: the stream to this rank goes here (same offsets)
+  uint32_t self_rank;
   uint64_t slot, rounds;
   const uint32_t* key_bk;           // OWN_KEY: sources [a_lo, a_lo + nsrc), key o of read a at o * key_n + a
   const uint64_t* key_ent;
@@ -2256,8 +2258,9 @@ __global__ __launch_bounds__(kBlock) void k_part(PartParams p) {
           const uint64_t k = at + lane_prefix(m);
           if (valid && d == dd && k < lim) {  // a stream cut at its capacity keeps its full count
             const uint64_t q = k / p.slot, o = ((q * p.nranks) + dd) * p.slot + (k - q * p.slot);
-            if (KIND == OWN_KEY) reinterpret_cast<ulonglong2*>(p.out)[o] = x16;
-            else reinterpret_cast<uint3*>(p.out)[o] = x12;
+            void* dst = (p.self_out && dd == p.self_rank) ? p.self_out : p.out;
+            if (KIND == OWN_KEY) reinterpret_cast<ulonglong2*>(dst)[o] = x16;
+            else reinterpret_cast<uint3*>(dst)[o] = x12;
           }
         }
         todo &= ~m;
@@ -2325,7 +2328,8 @@ __global__ __launch_bounds__(128) void k_dest_bounds(const void* __restrict__ ke
 __global__ __launch_bounds__(kBlock) void k_pack_runs(const void* __restrict__ keys, const uint64_t* __restrict__ meta,
                                                       int pack_a, int pack_w, uint32_t nb_log2, uint64_t n,
                                                       const unsigned long long* __restrict__ bnd, uint32_t nranks,
-                                                      uint64_t slot, uint64_t rounds, ulonglong2* __restrict__ out,
+                                                      uint64_t slot, uint64_t rounds, ulonglong2* out,
+                                                      ulonglong2* self_out, uint32_t self_rank,
                                                       unsigned long long* __restrict__ counts) {
   __shared__ unsigned long long s_b[kMaxRanks + 1];
   if (threadIdx.x <= nranks) s_b[threadIdx.x] = bnd[threadIdx.x];
@@ -2349,7 +2353,7 @@ __global__ __launch_bounds__(kBlock) void k_pack_runs(const void* __restrict__ k
       x = reinterpret_cast<const uint64_t*>(keys)[i];
     }
     const uint64_t q = j / slot;
-    out[((q * nranks) + d) * slot + (j - q * slot)] = make_ulonglong2(x, y);
+    ((self_out && d == self_rank) ? self_out : out)[((q * nranks) + d) * slot + (j - q * slot)] = make_ulonglong2(x, y);
   }
 }
 
@@ -3396,7 +3400,8 @@ void source_range(const mg_ctx* ctx, uint64_t* lo, uint64_t* hi) {
 uint32_t part_grid(uint64_t nreg) { return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(nreg, 8192)); }
 
 template <int KIND>
-int route_slots(mg_ctx* ctx, PartParams pp, void* out, uint64_t slot, uint32_t rounds, unsigned long long* counts) {
+int route_slots(mg_ctx* ctx, PartParams pp, void* out, void* self_out, uint64_t slot, uint32_t rounds,
+                unsigned long long* counts) {
   const uint32_t grid = part_grid(pp.nreg);
   MG_TRY(ensure(&ctx->d_blk, &ctx->blk_cap, (size_t)grid * ctx->nranks));
   pp.nranks = ctx->nranks;
@@ -3404,6 +3409,8 @@ int route_slots(mg_ctx* ctx, PartParams pp, void* out, uint64_t slot, uint32_t r
   pp.n_reads = ctx->n;
   pp.blk = ctx->d_blk;
   pp.out = out;
+  pp.self_out = self_out;
+  pp.self_rank = ctx->rank;
   pp.slot = slot;
   pp.rounds = rounds;
   hipLaunchKernelGGL((k_part<KIND, 0>), dim3(grid), dim3(kBlock), 0, ctx->stream, pp);
@@ -4124,12 +4131,14 @@ int mg_xchg_begin(mg_ctx* ctx, uint32_t min_overlap, uint32_t seed_k) {
   return 0;
 }
 
-int mg_xchg_pack(mg_ctx* ctx, int what, void* dst, uint64_t slot, uint32_t rounds, uint64_t* counts) {
+int mg_xchg_pack(mg_ctx* ctx, int what, void* dst, uint64_t slot, uint32_t rounds, uint64_t* counts,
+                 void* self_dst) {
   if (!ctx) return -1;
   MG_TRY(hipSetDevice(ctx->device));
   if (what < MG_KEYS || what > MG_ROWS || !(ctx->packable & (1 << what)))
     return set_err(ctx, "mg_xchg_pack: nothing of that kind to pack now (call order)");
-  if (!slot || !rounds || !counts || (!dst && slot)) return set_err(ctx, "mg_xchg_pack: bad slot geometry");
+  if (!slot || !rounds || !counts || (!dst && !(self_dst && ctx->nranks == 1)))
+    return set_err(ctx, "mg_xchg_pack: bad slot geometry");
   auto* cnt = reinterpret_cast<unsigned long long*>(counts);
   const uint64_t nsrc = ctx->xchg_hi - ctx->xchg_lo;
   if (what == MG_KEYS) {
@@ -4142,7 +4151,7 @@ int mg_xchg_pack(mg_ctx* ctx, int what, void* dst, uint64_t slot, uint32_t round
     pp.key_n = ctx->n;
     pp.a_lo = ctx->xchg_lo;
     pp.nsrc = nsrc;
-    return route_slots<OWN_KEY>(ctx, pp, dst, slot, rounds, cnt);
+    return route_slots<OWN_KEY>(ctx, pp, dst, self_dst, slot, rounds, cnt);
   }
   if (what == MG_RUNS) {
     const uint64_t n = ctx->n_sorted;
@@ -4150,7 +4159,8 @@ int mg_xchg_pack(mg_ctx* ctx, int what, void* dst, uint64_t slot, uint32_t round
     hipLaunchKernelGGL(k_pack_runs, dim3(grid), dim3(kBlock), 0, ctx->stream,
                        n ? (const void*)ctx->d_sk[ctx->sk_sel] : (const void*)ctx->d_bnd,
                        n ? ctx->d_sm[ctx->sk_sel] : nullptr, ctx->pack_a, ctx->pack_w, ctx->nb_log2, n, ctx->d_bnd,
-                       ctx->nranks, slot, (uint64_t)rounds, reinterpret_cast<ulonglong2*>(dst), cnt);
+                       ctx->nranks, slot, (uint64_t)rounds, reinterpret_cast<ulonglong2*>(dst),
+                       reinterpret_cast<ulonglong2*>(self_dst), ctx->rank, cnt);
     MG_TRY(hipGetLastError());
     return 0;
   }
@@ -4159,7 +4169,7 @@ int mg_xchg_pack(mg_ctx* ctx, int what, void* dst, uint64_t slot, uint32_t round
   pp.cap = ctx->nreg ? ctx->rows_cap / ctx->nreg : 0;
   pp.cnt = ctx->d_seg;
   pp.nreg = ctx->n_rows ? ctx->nreg : 0;
-  return route_slots<OWN_SRC>(ctx, pp, dst, slot, rounds, cnt);
+  return route_slots<OWN_SRC>(ctx, pp, dst, self_dst, slot, rounds, cnt);
 }
 
 int mg_xchg_insert_keys(mg_ctx* ctx, const void* recv, uint64_t slot, uint32_t rounds, const uint64_t* counts) {

@@ -87,7 +87,7 @@ def lib() -> C.CDLL:
         "mg_download_frequency": (i32, [vp, vp]),
         "mg_xchg_caps": (i32, [vp, u32, u32, vp]),
         "mg_xchg_begin": (i32, [vp, u32, u32]),
-        "mg_xchg_pack": (i32, [vp, i32, vp, u64, u32, vp]),
+        "mg_xchg_pack": (i32, [vp, i32, vp, u64, u32, vp, vp]),
         "mg_xchg_insert_keys": (i32, [vp, vp, u64, u32, vp]),
         "mg_xchg_probe": (i32, [vp, i32, vp, u64, u32, vp]),
         "mg_slots_digest": (i32, [vp, vp, u64, u32, vp, vp]),
@@ -406,9 +406,10 @@ class OverlapEngine:
     def xchg_begin(self, min_overlap: int, seed_k: int = 0):
         self._check(lib().mg_xchg_begin(self._h, min_overlap, seed_k), "xchg_begin")
 
-    def xchg_pack(self, what: int, dptr: int, slot: int, rounds: int, counts_dptr: int):
-        self._check(lib().mg_xchg_pack(self._h, what, C.c_void_p(dptr), slot, rounds, C.c_void_p(counts_dptr)),
-                    "xchg_pack")
+    def xchg_pack(self, what: int, dptr: int, slot: int, rounds: int, counts_dptr: int, self_dptr: int = 0):
+        """self_dptr: the receive buffer; this rank's own stream is written there directly."""
+        self._check(lib().mg_xchg_pack(self._h, what, C.c_void_p(dptr or 0), slot, rounds, C.c_void_p(counts_dptr),
+                                       C.c_void_p(self_dptr or 0)), "xchg_pack")
 
     def xchg_insert_keys(self, dptr: int, slot: int, rounds: int, counts_dptr: int):
         self._check(lib().mg_xchg_insert_keys(self._h, C.c_void_p(dptr), slot, rounds, C.c_void_p(counts_dptr)),

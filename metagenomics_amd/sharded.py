@@ -18,9 +18,10 @@ One step (``sharded_step``):
 
 Records travel in the library's SLOT LAYOUT (include/mg_overlap.h "exchange mode"): per peer a
 fixed-capacity stream of ``rounds * slot`` records, round t of all peers contiguous, so every round
-is ONE equal-split ``all_to_all_single`` straight from the packed buffer (no host-side split sizes,
-no per-round concatenation), and the per-peer record counts travel as a device tensor in one more
-equal-split all-to-all. Nothing in the step waits on the host for the exchange: the capacities are
+is one group of equal-size sends/receives straight from the packed buffer (no host-side split
+sizes, no per-round concatenation), and the per-peer record counts travel as a device tensor in
+one equal-split all-to-all. A rank's stream to itself never travels: the pack writes it straight
+into the rank's receive buffer (same slot offsets), so one rank moves nothing but its counts. Nothing in the step waits on the host for the exchange: the capacities are
 fixed up front (``XchgPlan``) and a stream that would not fit is cut; its full count comes back with
 the step's single host read (an all-reduce MAX of the send counts), and the step is rerun with the
 capacities grown. With a CUDA device the library calls, the torch copies and the RCCL collectives
@@ -91,9 +92,11 @@ class Exchange:
         """Context in which the step's torch work is ordered with the engines' HIP streams."""
         return contextlib.nullcontext()
 
-    def all_to_all_slots(self, sends: list, counts: list, slot: int, rounds: int, rec_bytes: int) -> list:
-        """sends[i] / counts[i]: slot-layout buffer and per-peer counts of local rank i.
-        Returns [(recv_buffer, recv_counts)] per local rank, in the same layout."""
+    def all_to_all_slots(self, sends: list, recvs: list, counts: list, slot: int, rounds: int,
+                         rec_bytes: int) -> list:
+        """sends[i] / recvs[i] / counts[i]: slot-layout send and receive buffers and per-peer
+        counts of local rank i; its slots for itself are already in recvs[i].  Moves every other
+        slot and returns [(recv_buffer, recv_counts)] per local rank."""
         raise NotImplementedError
 
     def allreduce_max(self, bufs: list) -> None:
@@ -141,14 +144,23 @@ class TorchExchange(Exchange):
         if self.device.type == "cuda":
             self.torch.cuda.current_stream(self.device).synchronize()
 
-    def all_to_all_slots(self, sends, counts, slot, rounds, rec_bytes):
-        (send,), (cnt,) = sends, counts
-        blk = self.world * slot * rec_bytes
-        recv = self.empty(rounds * blk)
-        for t in range(rounds):
-            self.dist.all_to_all_single(recv[t * blk:(t + 1) * blk], send[t * blk:(t + 1) * blk])
+    def all_to_all_slots(self, sends, recvs, counts, slot, rounds, rec_bytes):
+        (send,), (recv,), (cnt,) = sends, recvs, counts
+        P, me, sb = self.world, self.rank, slot * rec_bytes
+        if P == 1:
+            return [(recv, cnt)]
+        dist = self.dist
+        for t in range(rounds):  # one group of sends/receives per round, none to itself
+            ops = []
+            for p in range(P):
+                if p != me:
+                    at = (t * P + p) * sb
+                    ops.append(dist.P2POp(dist.isend, send[at: at + sb], p))
+                    ops.append(dist.P2POp(dist.irecv, recv[at: at + sb], p))
+            for w in dist.batch_isend_irecv(ops):
+                w.wait()
         rc = self.torch.empty_like(cnt)
-        self.dist.all_to_all_single(rc, cnt)
+        dist.all_to_all_single(rc, cnt)
         return [(recv, rc)]
 
     def allreduce_max(self, bufs):
@@ -185,15 +197,17 @@ class LocalExchange(Exchange):
         if self.device.type == "cuda":
             self.torch.cuda.synchronize(self.device)
 
-    def all_to_all_slots(self, sends, counts, slot, rounds, rec_bytes):
+    def all_to_all_slots(self, sends, recvs, counts, slot, rounds, rec_bytes):
         P, sb = self.world, slot * rec_bytes
         self.sync()
         out = []
         for d in range(P):
-            recv = self.empty(rounds * P * sb)
+            recv = recvs[d]
             for t in range(rounds):
                 for s in range(P):
-                    recv[(t * P + s) * sb:(t * P + s + 1) * sb].copy_(sends[s][(t * P + d) * sb:(t * P + d + 1) * sb])
+                    if s != d:
+                        recv[(t * P + s) * sb:(t * P + s + 1) * sb].copy_(
+                            sends[s][(t * P + d) * sb:(t * P + d + 1) * sb])
             rc = self.torch.stack([counts[s][d] for s in range(P)])
             out.append((recv, rc))
         self.sync()
@@ -279,15 +293,18 @@ def _step(engines, xchg, min_overlap, seed_k, want_super, plan):
     def route(kind):
         slot, rounds = plan.geometry(kind, P, ch)
         rb = RECORD_BYTES[kind]
-        sends, cnts = [], []
+        sends, recvs, cnts = [], [], []
         for e in engines:
-            buf = xchg.empty(rounds * P * slot * rb)
+            recv = xchg.empty(rounds * P * slot * rb)
+            send = xchg.empty(rounds * P * slot * rb) if P > 1 else None
             c = xchg.counts()
-            e.xchg_pack(kind, buf.data_ptr(), slot, rounds, c.data_ptr())
-            sends.append(buf)
+            e.xchg_pack(kind, send.data_ptr() if send is not None else 0, slot, rounds, c.data_ptr(),
+                        recv.data_ptr())
+            sends.append(send)
+            recvs.append(recv)
             cnts.append(c)
         sent[kind] = cnts
-        return xchg.all_to_all_slots(sends, cnts, slot, rounds, rb), slot, rounds
+        return xchg.all_to_all_slots(sends, recvs, cnts, slot, rounds, rb), slot, rounds
 
     t0 = time.perf_counter()
     with xchg.streams(engines):

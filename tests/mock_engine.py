@@ -41,9 +41,10 @@ def src_owner(src: np.ndarray, n_reads: int, world: int) -> np.ndarray:
 
 
 def write_slots(ptr: int, recs: np.ndarray, owner: np.ndarray, world: int, slot: int, rounds: int,
-                counts_ptr: int):
+                counts_ptr: int, self_ptr: int = 0, me: int = -1):
     """The library's slot layout: record i of peer d's stream at ((i // slot) * P + d) * slot + i % slot,
-    streams cut at rounds * slot, full lengths into the device (here: host) counts."""
+    streams cut at rounds * slot, full lengths into the device (here: host) counts; the stream to
+    this rank itself goes to self_ptr (the receive buffer) when given."""
     rb = recs.dtype.itemsize
     cnt = np.zeros(world, np.int64)
     for d in range(world):
@@ -52,7 +53,8 @@ def write_slots(ptr: int, recs: np.ndarray, owner: np.ndarray, world: int, slot:
         for t in range(rounds):
             part = stream[t * slot:(t + 1) * slot]
             if len(part):
-                ctypes.memmove(ptr + (t * world + d) * slot * rb, part.tobytes(), part.nbytes)
+                base = self_ptr if (self_ptr and d == me) else ptr
+                ctypes.memmove(base + (t * world + d) * slot * rb, part.tobytes(), part.nbytes)
     ctypes.memmove(counts_ptr, cnt.tobytes(), cnt.nbytes)
 
 
@@ -99,7 +101,7 @@ class MockEngine:
         self.runs["y"] = a
         self.out_rows = None
 
-    def xchg_pack(self, what, ptr, slot, rounds, counts_ptr):
+    def xchg_pack(self, what, ptr, slot, rounds, counts_ptr, self_ptr=0):
         if what == MG_KEYS:
             recs, owner = self.keys, bucket_owner(self.keys["x"], self.world)
         elif what == MG_RUNS:
@@ -107,7 +109,7 @@ class MockEngine:
         else:
             assert self.out_rows is not None, "rows before the discovery probe"
             recs, owner = self.out_rows, src_owner(self.out_rows["src"], self.n_reads, self.world)
-        write_slots(ptr, recs, owner, self.world, slot, rounds, counts_ptr)
+        write_slots(ptr, recs, owner, self.world, slot, rounds, counts_ptr, self_ptr, self.rank)
 
     def xchg_insert_keys(self, ptr, slot, rounds, counts_ptr):
         recs = read_slots(ptr, REC_DTYPE, self.world, slot, rounds, counts_ptr)
