@@ -54,6 +54,7 @@ typedef struct mg_timings {
   float upload_ms;      /* H2D copy of raw reads (mg_ingest_*)        */
   float ingest_ms;      /* device Dataset ingest (mg_ingest_*)        */
   float sort_ms;        /* run records ordered by bucket (option "sort_runs"; 0 otherwise) */
+  float layout_ms;      /* device layout of the last upload / ingest (clustered slots, option "layout") */
 } mg_timings;
 
 /* Work counters of the last discovery launch (only with option "stats" = 1):
@@ -109,6 +110,10 @@ int mg_dataset_counts(const mg_ctx* ctx, uint64_t* n_good, uint64_t* n_unique);
 int mg_download_frequency(mg_ctx* ctx, uint32_t* freq);
 /* Copy back the packed reads (words_per_read words each) for inspection. */
 int mg_download_reads_packed(mg_ctx* ctx, uint64_t* words, uint16_t* lens, uint32_t* words_per_read);
+/* Device slot of every read: slot_of_id[ID - 1] (the device stores the reads
+ * clustered for locality, option "layout"; identity when it is off).  Only
+ * diagnostics need it: every result leaves the device in reference IDs. */
+int mg_read_slots(mg_ctx* ctx, uint32_t* slot_of_id);
 
 /* --- index (HashTable) ---------------------------------------------------- */
 /* HashTable::insertDataset(Dataset*, minOverlapLength) (HashTable.h:30,

@@ -30,6 +30,17 @@ struct mg_ctx {
   uint64_t* d_words = nullptr;
   uint16_t* d_len = nullptr;
   size_t words_cap = 0, len_cap = 0;
+  // device layout (option "layout"): slots clustered by each
+  // read's canonical global minimizer, so overlapping reads sit near each
+  // other; d_id[slot] = reference ID - 1, d_phys[ID - 1] = slot (both nullptr:
+  // slots in ID order).  Everything on the device works in slots; rows,
+  // superReadIDs, lookups and downloads leave in reference IDs.
+  bool layout = true;
+  uint32_t* d_id = nullptr;
+  uint32_t* d_phys = nullptr;
+  size_t id_cap = 0, phys_cap = 0;
+  uint32_t* d_tmp32 = nullptr;  // ID-order staging of per-read outputs
+  size_t tmp32_cap = 0;
   // index
   uint32_t l = 0, h = 0, m = 0, w = 0;
   uint32_t nb_log2 = 0, nb_log2_opt = 0;
@@ -85,11 +96,12 @@ struct mg_ctx {
   unsigned long long* d_slot_cnt = nullptr;  // per-region counts of a slot-layout buffer (digest)
   size_t slot_cnt_cap = 0;
   // timing
-  hipEvent_t ev[14] = {};
+  hipEvent_t ev[16] = {};  // [14], [15]: apply_layout
   // unsharded contexts build the index inside the window scan (k_scan<INDEX>);
   // its runs then serve the containment and the discovery probes
   int scan_state = 0;        // 0 none, 1 launched (not settled), 2 settled
   bool overlap_scan = true;  // option "overlap_scan" (0: separate index build, a scan per probe pass)
+  bool scan_pp = false;       // option "scan_pp": position-parallel scan (k_scan_pp) when the read fits a wavefront
   bool scan_reg = true;      // option "scan_reg": register sliding minimum (k_scan_reg) for the run scans when w <= 32
   bool reg_index = false;    // option "reg_index": also for the cell index build (key records + k_insert_dense)
   // partitioned join (option "join", default): keys + runs as sorted join
@@ -114,7 +126,7 @@ struct mg_ctx {
   std::vector<unsigned long long> cand_cnt_host;
   // bucket-ordered runs (option "sort_runs"): the shared scan's runs as SoA
   // (x, meta) sorted by bucket, so the probe meets each cell's runs together
-  bool sort_runs = true;
+  bool sort_runs = false;
   uint64_t* d_sk[2] = {nullptr, nullptr};
   uint64_t* d_sm[2] = {nullptr, nullptr};
   size_t sk_cap = 0;
@@ -135,6 +147,8 @@ struct mg_ctx {
   bool pack_runs = true;           // option "pack_runs": 12-B sort records when the widths fit
   int pack_a = 0, pack_w = 0;      // packing of the current flat runs (0: 16-B records)
   int sorted_state = 0;  // 0 none, 2 sorted (for the current scan)
+  uint64_t probe_region = 0;  // sorted probe: runs per region (0: one tile per wavefront)
+  bool xcd_map = false;       // sorted probe: regions dealt XCD by XCD
   int sort_bits = 0;     // diagnostics: sort only the top sort_bits bucket bits (0: all)
   // sorted index build (option "sorted_index", default off): k_scan<INDEX> writes
   // the 4N key records (bucket, entry), a radix sort orders them by bucket and
@@ -196,6 +210,11 @@ inline uint32_t supported_maxw(uint32_t need) {
     if (w >= need) return w;
   return 0;
 }
+
+// the device layout of freshly uploaded reads (mg_kernels.hip): clusters the
+// slots by canonical global minimizer and fills d_id / d_phys (option "layout"
+// = 0: ID order); records t.layout_ms
+int apply_layout(mg_ctx* ctx);
 
 // new reads invalidate everything derived from them
 inline void reset_derived(mg_ctx* ctx) {

@@ -302,6 +302,7 @@ struct Ingest {
     ctx->n_good = ngood;
     ctx->minlen = ngood ? lrh[0] : 0;
     ctx->maxlen = ngood ? lrh[1] : 0;
+    if (apply_layout(ctx)) return -1;
     reset_derived(ctx);
     *n_unique = nu;
     return 0;

@@ -101,6 +101,9 @@ __device__ __forceinline__ uint64_t ext_fwd(const uint64_t* f, int pos) {
 }
 
 
+// Reference ID - 1 of the read in slot x of the device layout (mg_ctx::d_id:
+// reads are stored clustered for locality; nullptr = ID order).
+__device__ __forceinline__ uint32_t rid(const uint32_t* id, uint32_t x) { return id ? id[x] : x; }
 // Number of set bits of a ballot below this lane (v_mbcnt_lo/hi).
 __device__ __forceinline__ uint32_t lane_prefix(uint64_t bal) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
@@ -160,6 +163,7 @@ struct IndexParams {
   uint32_t rank, nranks;
   uint64_t cell_lo, cell_n;  // this rank's bucket range [cell_lo, cell_lo + cell_n): local cell = bucket - cell_lo
   uint64_t* cells;   // [cell_n * kCell] entries: lo32 = read index, hi32 = chain1 | fp19 | q10 | o2
+  const uint32_t* id;  // slot -> reference ID - 1 (nullptr: ID order; lookups return IDs)
 };
 
 __device__ __forceinline__ bool owned(uint64_t bkt, uint32_t nb_log2, uint32_t rank, uint32_t nranks) {
@@ -312,7 +316,8 @@ __global__ __launch_bounds__(kBlock) void k_prefix_contain(const uint64_t* __res
                                                            const uint64_t* __restrict__ key0,
                                                            const uint64_t* __restrict__ cells, uint64_t cell_n,
                                                            uint32_t nb_log2, uint64_t n,
-                                                           unsigned long long* __restrict__ superkey) {
+                                                           unsigned long long* __restrict__ superkey,
+                                                           const uint32_t* __restrict__ id) {
   const uint64_t a = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
   if (a >= n) return;
   const uint64_t k0 = key0[a];
@@ -345,7 +350,7 @@ __global__ __launch_bounds__(kBlock) void k_prefix_contain(const uint64_t* __res
         const int rem = n2 - 32 * k;
         diff |= (f1[k] ^ bv) & (rem >= 32 ? ~0ULL : ~(~0ULL >> (2 * rem)));
       }
-      if (!diff) atomicMax(&superkey[r2], ((unsigned long long)n1 << 32) | (0xFFFFFFFFu - (uint32_t)a));
+      if (!diff) atomicMax(&superkey[r2], ((unsigned long long)n1 << 32) | (0xFFFFFFFFu - rid(id, (uint32_t)a)));
     }
     if (e[kCell - 1] == kEmpty || !(e[kCell - 1] & kChain)) break;
     c = next_cell(c, cell_n);
@@ -358,7 +363,7 @@ struct LaunchPrefixContain {
     if (!ctx->n) return 0;
     hipLaunchKernelGGL(k_prefix_contain<W>, dim3((uint32_t)((ctx->n + kBlock - 1) / kBlock)), dim3(kBlock), 0,
                        ctx->stream, ctx->d_words, ctx->d_len, ctx->d_key0, ctx->d_cells, ctx->cell_n, ctx->nb_log2,
-                       ctx->n, ctx->d_superkey);
+                       ctx->n, ctx->d_superkey, ctx->d_id);
     return hipGetLastError() == hipSuccess ? 0 : -1;
   }
 };
@@ -818,7 +823,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) voi
 // coalesced record per lane, either into this wavefront's region (16-B
 // records) or into the flat SoA arrays of the bucket sort (chunks of
 // kFlatChunk records claimed from kFlatCounters counters).
-template <int MAXW>
+template <int MAXW, int RING = kStageRing, bool FROM_MEM = false>
 struct RunStage {
   const ScanParams& p;
   uint64_t* s_buf;
@@ -834,7 +839,7 @@ struct RunStage {
 
   __device__ __forceinline__ void put(bool flag, uint64_t meta) {
     const uint64_t bal = __ballot(flag);
-    if (flag) s_buf[(head + nbuf + lane_prefix(bal)) & (kStageRing - 1)] = meta;
+    if (flag) s_buf[(head + nbuf + lane_prefix(bal)) & (RING - 1)] = meta;
     nbuf += (uint32_t)__popcll(bal);
   }
 
@@ -844,8 +849,8 @@ struct RunStage {
     wave_sync();
     bool flag = (uint32_t)lane < k;
     uint64_t v = 0, meta = 0;
-    if (flag) meta = s_buf[(head + lane) & (kStageRing - 1)];
-    if constexpr (MAXW <= 8) {
+    if (flag) meta = s_buf[(head + lane) & (RING - 1)];
+    if constexpr (MAXW <= 8 && !FROM_MEM) {
       const int pos = (int)((meta >> 32) & 1023u), wi = pos >> 5;
       const int src = flag ? (int)((uint32_t)meta - (uint32_t)a0) : lane;
       uint64_t w0 = 0, w1 = 0;
@@ -860,8 +865,8 @@ struct RunStage {
       if (flag) v = mix64(funnel(w0, w1, (pos & 31) << 1) >> msh);
     } else if (flag) {
       const uint64_t* g2 = p.words + (meta & 0xFFFFFFFFull) * slot_words(MAXW);
-      const int pos = (int)((meta >> 32) & 1023u);
-      v = mix64(funnel(g2[pos >> 5], g2[(pos >> 5) + 1], (pos & 31) << 1) >> msh);
+      const int pos = (int)((meta >> 32) & 1023u), wi = pos >> 5;
+      v = mix64(funnel(g2[wi], wi + 1 < slot_words(MAXW) ? g2[wi + 1] : 0ull, (pos & 31) << 1) >> msh);
     }
     if (flag) flag = owned(v & nbmask, p.nb_log2, p.rank, p.nranks);
     const uint64_t bal = __ballot(flag);
@@ -1193,6 +1198,237 @@ __global__ __launch_bounds__(kBlock) void k_rc_keys(ScanParams p) {
   p.join_kv[4 * a + 3] = n ? join_key_val((uint32_t)a, 3, (int)(kb3 & 1023u), v3, p) : kFlatHole;
 }
 
+// Window minimizers with LANES OVER POSITIONS (option scan_pp): a wavefront
+// takes one read at a time and lane l holds the K m-mers at positions
+// t = K l + k, each hashed independently (no serial chain, no per-position
+// branch).  Window j = m-mers [j, j + w - 1] (OverlapGraph.cpp:534-537); its
+// minimum is (suffix of lane l from k) | (lanes l+1 .. l+F, a sparse table of
+// lane minima doubled by __shfl_down) | (prefix of lane l+F+1), with the same
+// order (order_key | t, leftmost on ties) as every other scan.  Run starts
+// are ballots; a start's run ends before the next start (one scan of the
+// uniform start masks).  Runs are staged as metas in an LDS ring and hashed /
+// written 64 at a time (RunStage; the m-mer comes back from the read's slot,
+// an L1 hit).  INDEX (HashTable::insertDataset / hashRead, HashTable.cpp:
+// 50-104): o = 0 / 1 are windows j = 0 and j = n - h of this same min; o = 3 /
+// 2 are the minimum over positions [0, w) / [n - h, n - m] of the reverse
+// strand's m-mer keys (order_key(rc) | i), a wave reduction; the four entries
+// are staged and CAS-inserted 64 at a time (or written as key records).
+constexpr int kPPWords = 16;  // LDS copy of the current read's words (zero past the slot)
+constexpr int kPPKeys = 128;  // staged index entries per wavefront (inserted 64 at a time)
+template <int K>
+struct PPLds {
+  static constexpr int RING = 128 * K;  // >= 63 + the most runs one read can add (J < 64 K)
+  static constexpr size_t o_w = 0;
+  static constexpr size_t o_ring = o_w + kPPWords * 8;
+  static constexpr size_t o_kb = o_ring + (size_t)RING * 8;
+  static constexpr size_t o_ke = o_kb + kPPKeys * 8;
+  static constexpr size_t bytes = o_ke + kPPKeys * 8;
+};
+
+template <int MAXW, int K, bool INDEX>
+__global__ __launch_bounds__(kBlock) void k_scan_pp(ScanParams p) {
+  using PL = PPLds<K>;
+  extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  unsigned char* base = reinterpret_cast<unsigned char*>(smem) + (size_t)wv * PL::bytes;
+  uint64_t* s_w = reinterpret_cast<uint64_t*>(base + PL::o_w);
+  uint64_t* s_kb = reinterpret_cast<uint64_t*>(base + PL::o_kb);
+  uint64_t* s_ke = reinterpret_cast<uint64_t*>(base + PL::o_ke);
+  const int h = p.h, m = p.m, w = p.w;
+  const int msh = 64 - 2 * m;
+  const uint64_t mmask = (m == 32) ? ~0ULL : ((1ULL << (2 * m)) - 1);
+  const uint64_t nbmask = (1ULL << p.nb_log2) - 1;
+  const uint64_t gw = (uint64_t)blockIdx.x * kWavesPerBlock + wv;
+  const uint64_t nw = (uint64_t)gridDim.x * kWavesPerBlock;
+  RunStage<MAXW, PL::RING, true> st(p, reinterpret_cast<uint64_t*>(base + PL::o_ring), p.runs + gw * p.run_cap, lane);
+  // this wavefront's reads: one contiguous range (its runs stay in read order)
+  const uint64_t nrd = p.a_hi - p.a_lo, per = (nrd + nw - 1) / nw;
+  const uint64_t a_beg = p.a_lo + std::min<uint64_t>(nrd, gw * per);
+  const uint64_t a_end = p.a_lo + std::min<uint64_t>(nrd, (gw + 1) * per);
+  constexpr int kRw = MAXW + 1 <= slot_words(MAXW) ? MAXW + 1 : slot_words(MAXW);
+  uint32_t nkeys = 0;  // staged index entries (CAS mode)
+  // the staged entries, one per lane, into the cells (insertIntoTable, HashTable.cpp:163-195)
+  auto insert_keys = [&](uint32_t k) {
+    wave_sync();
+    if ((uint32_t)lane < k) cell_insert(p.cells, s_kb[lane], p.cell_n, s_ke[lane]);
+    const uint32_t rest = nkeys - k;  // < 64 + 4
+    const uint64_t b0 = (uint32_t)lane < rest ? s_kb[k + lane] : 0, e0 = (uint32_t)lane < rest ? s_ke[k + lane] : 0;
+    wave_sync();
+    if ((uint32_t)lane < rest) {
+      s_kb[lane] = b0;
+      s_ke[lane] = e0;
+    }
+    nkeys = rest;
+    wave_sync();
+  };
+  // software pipeline: the next read's words and length load behind this read
+  uint64_t wnext = 0;
+  int nnext = 0;
+  if (a_beg < a_end) {
+    wnext = lane < kRw ? p.words[a_beg * slot_words(MAXW) + lane] : 0;
+    nnext = (int)p.len[a_beg];
+  }
+  for (uint64_t a = a_beg; a < a_end; ++a) {
+    const uint64_t wcur = wnext;
+    int n = nnext;
+    if (a + 1 < a_end) {
+      wnext = lane < kRw ? p.words[(a + 1) * slot_words(MAXW) + lane] : 0;
+      nnext = (int)p.len[a + 1];
+    }
+    if (n && p.super && p.super[a]) n = 0;  // contained sources get no windows (:548)
+    n = __builtin_amdgcn_readfirstlane(n);
+    wave_sync();
+    if (lane < kPPWords) s_w[lane] = wcur;
+    wave_sync();
+    if (!n) {  // (no such read in a Dataset: every read is longer than l) key holes
+      if (INDEX && lane == 0 && p.key0) p.key0[a] = kEmpty;
+      if (INDEX && p.key_bk && lane < 4) {
+        p.key_bk[lane * p.key_n + a] = 0;
+        p.key_ent[lane * p.key_n + a] = kEmpty;
+      }
+      continue;
+    }
+    const int J = n - h - 1;  // scan windows j = 1 .. J
+    const int tl = n - m;     // last m-mer position
+    // ---- keys of this lane's positions
+    uint32_t key[K];
+    uint32_t rk2 = 0xFFFFFFFFu, rk3 = 0xFFFFFFFFu;  // INDEX: reverse-strand keys of o = 2 / 3
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const int t = K * lane + k, wi = t >> 5;
+      const uint64_t x = funnel(s_w[wi], s_w[wi + 1], (t & 31) << 1);  // bases t .. t + 31
+      key[k] = t <= tl ? (order_key(x >> msh) | (uint32_t)t) : 0xFFFFFFFFu;
+      if (INDEX) {
+        const uint32_t hr = order_key(rc_word(x) & mmask);
+        if (t < w) rk3 = min(rk3, hr | (uint32_t)(w - 1 - t));                // o = 3, i = w - 1 - t
+        if (t >= tl - w + 1 && t <= tl) rk2 = min(rk2, hr | (uint32_t)(tl - t));  // o = 2, i = n - m - t
+      }
+    }
+    // ---- sliding minimum over w positions
+    uint32_t pre[K], suf[K];
+    pre[0] = key[0];
+#pragma unroll
+    for (int k = 1; k < K; ++k) pre[k] = min(pre[k - 1], key[k]);
+    suf[K - 1] = key[K - 1];
+#pragma unroll
+    for (int k = K - 2; k >= 0; --k) suf[k] = min(suf[k + 1], key[k]);
+    // sparse table of lane minima: T[v] = min over lanes l .. l + 2^v - 1
+    const int fmax = (K - 1 + w - 1) / K - 1;  // most full lanes inside one window
+    uint32_t T[6];
+    T[0] = pre[K - 1];
+#pragma unroll
+    for (int v = 1; v < 6; ++v) T[v] = ((1 << v) <= fmax) ? min(T[v - 1], (uint32_t)__shfl_down(T[v - 1], 1 << (v - 1))) : T[v - 1];
+    uint32_t pos[K];
+    uint32_t wn0 = 0xFFFFFFFFu, wn1 = 0xFFFFFFFFu;  // INDEX: minima of windows 0 and n - h
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const int e = k + w - 1, le = e / K, ke = e % K;  // window end: lane + le, slot ke (uniform)
+      uint32_t r;
+      if (le == 0) {
+        r = 0xFFFFFFFFu;
+#pragma unroll
+        for (int kk = k; kk < K; ++kk) r = kk <= ke ? min(r, key[kk]) : r;
+      } else {
+        uint32_t pk = pre[0];
+#pragma unroll
+        for (int kk = 1; kk < K; ++kk) pk = kk == ke ? pre[kk] : pk;
+        r = min(suf[k], (uint32_t)__shfl_down(pk, le));
+        const int F = le - 1;
+        if (F > 0) {
+          const int v = 31 - __clz(F);
+          uint32_t tv = T[0];
+#pragma unroll
+          for (int vv = 1; vv < 6; ++vv) tv = vv == v ? T[vv] : tv;
+          r = min(r, min((uint32_t)__shfl_down(tv, 1), (uint32_t)__shfl_down(tv, 1 + F - (1 << v))));
+        }
+      }
+      pos[k] = r & 1023u;
+      if (INDEX) {  // o = 0: window 0 (lane 0, slot 0); o = 1: window n - h
+        const int j = K * lane + k;
+        if (j == 0) wn0 = r;
+        if (j == n - h) wn1 = r;
+      }
+    }
+    // ---- runs: starts are windows whose minimizer differs from window j - 1
+    uint64_t S[K];
+    uint64_t anyS = 0;
+    {
+      const uint32_t up = (uint32_t)__shfl_up((int)pos[K - 1], 1);
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        const int j = K * lane + k;
+        const uint32_t prev = k ? pos[k - 1] : up;
+        const bool start = j >= 1 && j <= J && (j == 1 || pos[k] != prev);
+        S[k] = __ballot(start);
+        anyS |= S[k];
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const int j = K * lane + k;
+      const bool start = (S[k] >> lane) & 1ull;
+      int jn = J + 1;  // next start (or one past the last window)
+      bool found = false;
+#pragma unroll
+      for (int kk = K - 1; kk > k; --kk)
+        if ((S[kk] >> lane) & 1ull) {
+          jn = K * lane + kk;
+          found = true;
+        }
+      if (!found) {
+        const uint64_t upper = lane == 63 ? 0ull : (anyS & (~0ull << (lane + 1)));
+        if (upper) {
+          const int l2 = __builtin_ctzll(upper);
+          int k2 = K - 1;
+#pragma unroll
+          for (int kk = K - 1; kk >= 0; --kk)
+            if ((S[kk] >> l2) & 1ull) k2 = kk;
+          jn = K * l2 + k2;
+        }
+      }
+      st.put(start, run_meta(a, (int)pos[k], j, jn - 1));
+    }
+    while (st.nbuf >= (uint32_t)kWave) st.flush(kWave, nullptr, 0);
+    if constexpr (INDEX) {
+      // the four keys' minimizers (uniform): o = 0 / 1 forward, o = 2 / 3 reverse strand
+      const uint32_t k0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)wn0);
+      const uint32_t k1 = (uint32_t)__builtin_amdgcn_readlane((int)wn1, (n - h) / K);
+#pragma unroll
+      for (int d = 32; d >= 1; d >>= 1) {
+        rk2 = min(rk2, (uint32_t)__shfl_xor((int)rk2, d));
+        rk3 = min(rk3, (uint32_t)__shfl_xor((int)rk3, d));
+      }
+      // lane o < 4 builds entry o: m-mer position t, key offset q, strand
+      const int o = lane & 3;
+      const uint32_t kk = o == 0 ? k0 : o == 1 ? k1 : o == 2 ? rk2 : rk3;
+      const int q0 = (int)(kk & 1023u);  // o < 2: window position t; o >= 2: offset i
+      const int t = o == 0 ? q0 : o == 1 ? q0 : o == 2 ? tl - q0 : w - 1 - q0;
+      const int q = o == 1 ? q0 - (n - h) : q0;
+      const int wi = t >> 5;
+      const uint64_t x = funnel(s_w[wi], s_w[wi + 1], (t & 31) << 1);
+      const uint64_t v = mix64(o < 2 ? x >> msh : rc_word(x) & mmask);
+      const unsigned long long e = make_entry(v, p.nb_log2, q, o, (uint32_t)a);
+      if (lane == 0 && p.key0) p.key0[a] = (v & ((1ULL << 50) - 1)) | ((uint64_t)q << 54);
+      if (p.key_bk) {
+        if (lane < 4) {
+          p.key_bk[o * p.key_n + a] = (uint32_t)(v & nbmask);
+          p.key_ent[o * p.key_n + a] = e;
+        }
+      } else {
+        if (lane < 4) {
+          s_kb[nkeys + lane] = v & nbmask;
+          s_ke[nkeys + lane] = e;
+        }
+        nkeys += 4;
+        if (nkeys >= (uint32_t)kWave) insert_keys(kWave);
+      }
+    }
+  }
+  while (st.nbuf) st.flush(st.nbuf < (uint32_t)kWave ? st.nbuf : (uint32_t)kWave, nullptr, 0);
+  if (INDEX && nkeys) insert_keys(nkeys);
+  st.finish(gw);
+}
+
 // checkOverlap's string compare (OverlapGraph.cpp:354-383) on packed words:
 // the L partner bases [y0, y0+L) against the source bases [x0, x0+L) of the
 // forward strand, or of the reverse strand when rcA.  Partner words are used in
@@ -1248,6 +1484,12 @@ struct ProbeParams {
   uint3* cand;                    // one region of cand_cap records per probe wavefront
   unsigned long long* cand_cnt;   // [waves] candidates written (may exceed cand_cap)
   uint64_t cand_cap;
+  // xcd_map: run regions are dealt XCD by XCD (blockIdx % 8 shares an XCD): the
+  // waves of one XCD take consecutive regions of one contiguous share of the
+  // bucket-sorted runs, so at any moment they probe one narrow bucket window
+  // whose cells and partner slots stay in that XCD's L2
+  int xcd_map;
+  const uint32_t* id;             // slot -> reference ID - 1 (nullptr: ID order); rows and superkeys carry IDs
 };
 
 // Which side of a self-symmetric (o = 2/3) discovery pair {a, b} emits it:
@@ -1357,8 +1599,15 @@ __global__ __launch_bounds__(kBlock) void k_probe(ProbeParams p) {
       }
     }
     // partner slot first (the long-latency random load: its words in 16-B
-    // pieces of one aligned line), then stage the source
-    if (cond) load_slot<MAXW>(p.words, bid, y);
+    // pieces of one aligned line) and both reference IDs, then stage the source
+    uint32_t ida = sa, idb = bid;
+    if (cond) {
+      load_slot<MAXW>(p.words, bid, y);
+      if (p.id) {
+        ida = p.id[sa];
+        idb = p.id[bid];
+      }
+    }
     if (have) {
       const uint64_t* g = p.words + (uint64_t)sa * slot_words(MAXW);
 #pragma unroll
@@ -1371,15 +1620,15 @@ __global__ __launch_bounds__(kBlock) void k_probe(ProbeParams p) {
       const uint64_t diff = overlap_diff<MAXW, kWave>(s_a + lane, n1, x0, y0, L, rcA, y);
       if (diff == 0) {
         if (CONTAIN) {
-          atomicMax(&p.superkey[bid], ((unsigned long long)n1 << 32) | (0xFFFFFFFFu - sa));
+          atomicMax(&p.superkey[bid], ((unsigned long long)n1 << 32) | (0xFFFFFFFFu - ida));
         } else if (!(p.super && p.super[bid])) {  // :548 read2 contained
           // orientation/offset switch (:550-557) and the twin (:409-412, :841-855)
           const uint32_t orient = (o == 0) ? 3u : (o == 2 ? 2u : 1u);
           const uint32_t off = (o == 3) ? (uint32_t)(n1 - h - j) : (uint32_t)j;
           const uint32_t torient = (orient == 3u) ? 0u : orient;
           const uint32_t toff = (uint16_t)(n2 + off - n1);
-          r0 = sa + 1; r1 = bid + 1; r2 = (orient << 16) | off;
-          t0 = bid + 1; t1 = sa + 1; t2 = (torient << 16) | toff;
+          r0 = ida + 1; r1 = idb + 1; r2 = (orient << 16) | off;
+          t0 = idb + 1; t1 = ida + 1; t2 = (torient << 16) | toff;
           nrec = (bid == sa && o == 0) ? 4 : 2;  // self o=0 hit also stands for its o=1 twin
           st_rows += nrec;
         }
@@ -1409,8 +1658,21 @@ __global__ __launch_bounds__(kBlock) void k_probe(ProbeParams p) {
   uint64_t rpos = 0, rcnt = 0;
   const ulonglong2* rbase = p.runs;
   uint64_t rbase_i = 0;
+  // region sequence of this wavefront: first, first + stride, ... < rlimit
+  uint64_t rfirst = gw, rstride = nwp, rlimit = p.run_regions;
+  if (p.xcd_map) {
+    const uint64_t G = gridDim.x, x = blockIdx.x & 7u;
+    const uint64_t bx = (G + 7 - x) >> 3;  // blocks sharing this XCD
+    uint64_t before = 0;                     // waves of the XCD groups before x
+    for (uint64_t y = 0; y < x; ++y) before += ((G + 7 - y) >> 3) * kWavesPerBlock;
+    const uint64_t wx = bx * kWavesPerBlock;
+    const uint64_t lo = p.run_regions * before / nwp, hi = p.run_regions * (before + wx) / nwp;
+    rfirst = lo + (blockIdx.x >> 3) * kWavesPerBlock + wv;
+    rstride = wx;
+    rlimit = hi;
+  }
   auto open_region = [&](uint32_t r) {
-    const uint64_t reg = gw + (uint64_t)r * nwp;
+    const uint64_t reg = rfirst + (uint64_t)r * rstride;
     rbase = p.runs + (p.fkeys ? 0 : reg * p.run_cap);
     rbase_i = reg * p.run_cap;
     const uint64_t c = p.run_cnt[reg];
@@ -1420,7 +1682,7 @@ __global__ __launch_bounds__(kBlock) void k_probe(ProbeParams p) {
   // skip to the next non-empty batch position; false once the regions are exhausted
   auto hbm_settle = [&]() -> bool {
     while (rpos >= rcnt) {
-      if (gw + (uint64_t)(rg + 1) * nwp >= p.run_regions) return false;
+      if (rfirst + (uint64_t)(rg + 1) * rstride >= rlimit) return false;
       open_region(++rg);
     }
     return true;
@@ -1588,7 +1850,7 @@ __global__ __launch_bounds__(kBlock) void k_probe(ProbeParams p) {
     }
   };
 
-  if (p.phase_limit > 4 && gw < p.run_regions) {
+  if (p.phase_limit > 4 && rfirst < rlimit) {
     open_region(0);
     pf_any = hbm_settle();
     hbm_fetch();
@@ -1738,7 +2000,7 @@ __global__ __launch_bounds__(kBlock) void k_verify(ProbeParams p, uint64_t cand_
     uint32_t r2 = 0, t2 = 0;
     if (ok) {
       if (CONTAIN) {
-        atomicMax(&p.superkey[k.bid], ((unsigned long long)k.n1 << 32) | (0xFFFFFFFFu - k.sa));
+        atomicMax(&p.superkey[k.bid], ((unsigned long long)k.n1 << 32) | (0xFFFFFFFFu - rid(p.id, k.sa)));
       } else if (!(p.super && p.super[k.bid])) {  // :548 read2 contained
         const uint32_t orient = (k.o == 0) ? 3u : (k.o == 2 ? 2u : 1u);
         const uint32_t off = (k.o == 3) ? (uint32_t)(k.n1 - h - k.j) : (uint32_t)k.j;
@@ -1758,8 +2020,9 @@ __global__ __launch_bounds__(kBlock) void k_verify(ProbeParams p, uint64_t cand_
         const uint32_t pr = 2u * (lane_prefix(b2) + lane_prefix(b4));
         uint3* d = reinterpret_cast<uint3*>(region + (cursor + pr) * 3);
         for (int rr = 0; rr < nrec; rr += 2) {
-          d[0] = make_uint3(k.sa + 1, k.bid + 1, r2);
-          d[1] = make_uint3(k.bid + 1, k.sa + 1, t2);
+          const uint32_t ia = rid(p.id, k.sa) + 1, ib = rid(p.id, k.bid) + 1;
+          d[0] = make_uint3(ia, ib, r2);
+          d[1] = make_uint3(ib, ia, t2);
           d += 2;
         }
       }
@@ -1836,6 +2099,7 @@ constexpr size_t kJoinLds = (size_t)kJoinCells * kCell * 8 + (size_t)kJoinCells 
 struct JoinParams {
   const uint64_t* words;
   const uint16_t* len;
+  const uint32_t* id;                // slot -> reference ID - 1 (nullptr: ID order)
   int h, P, A, QB, WB;
   const uint32_t* k32;               // sorted join records
   const uint64_t* val;
@@ -1950,7 +2214,7 @@ __global__ __launch_bounds__(kJoinBlock) void k_join(JoinParams p) {
       }
       if (diff == 0) {
         if (CONTAIN) {
-          atomicMax(&p.superkey[bid], ((unsigned long long)n1 << 32) | (0xFFFFFFFFu - sa));
+          atomicMax(&p.superkey[bid], ((unsigned long long)n1 << 32) | (0xFFFFFFFFu - rid(p.id, sa)));
         } else if (!(p.super && p.super[bid])) {  // :548 read2 contained
           // orientation/offset switch (:550-557) and the twin (:409-412, :841-855)
           const uint32_t orient = (o == 0) ? 3u : (o == 2 ? 2u : 1u);
@@ -1971,8 +2235,9 @@ __global__ __launch_bounds__(kJoinBlock) void k_join(JoinParams p) {
           const uint32_t pr = 2u * (lane_prefix(b2) + lane_prefix(b4));
           uint3* d = reinterpret_cast<uint3*>(region + (cursor + pr) * 3);
           for (int rr = 0; rr < nrec; rr += 2) {
-            d[0] = make_uint3(sa + 1, bid + 1, r2);
-            d[1] = make_uint3(bid + 1, sa + 1, t2);
+            const uint32_t ia = rid(p.id, sa) + 1, ib = rid(p.id, bid) + 1;
+            d[0] = make_uint3(ia, ib, r2);
+            d[1] = make_uint3(ib, ia, t2);
             d += 2;
           }
         }
@@ -2459,12 +2724,12 @@ __global__ __launch_bounds__(kBlock) void k_rows_digest(const uint32_t* __restri
 }
 
 __global__ __launch_bounds__(kBlock) void k_super_digest(const uint32_t* __restrict__ super, uint64_t n_reads,
-                                                         unsigned long long* acc) {
+                                                         unsigned long long* acc, const uint32_t* __restrict__ id) {
   uint64_t n = 0, s = 0, x = 0, s2 = 0;
   for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n_reads; i += (uint64_t)gridDim.x * kBlock) {
     const uint32_t sp = super[i];
     if (sp) {
-      const uint64_t g = mix64(((i + 1) << 32) | sp);
+      const uint64_t g = mix64(((uint64_t)(rid(id, (uint32_t)i) + 1) << 32) | sp);
       n += 1;
       s += g;
       x ^= g;
@@ -2525,7 +2790,7 @@ __global__ __launch_bounds__(kBlock) void k_lookup_key(IndexParams p, const uint
         }
         if (!diff) {
           const unsigned int slot = atomicAdd(nout, 1u);
-          if (slot < cap) out[slot] = ((unsigned long long)(r + 1)) | ((unsigned long long)o << 62);
+          if (slot < cap) out[slot] = ((unsigned long long)(rid(p.id, r) + 1)) | ((unsigned long long)o << 62);
         }
       }
     }
@@ -2533,6 +2798,95 @@ __global__ __launch_bounds__(kBlock) void k_lookup_key(IndexParams p, const uint
     b = next_cell(b, p.cell_n);
   }
 }
+
+}  // namespace
+
+namespace {
+// ------------------------------------------------------------ layout ---
+// Device layout of the reads.  Overlapping reads share
+// m-mers, so clustering the slots by each read's canonical global minimizer
+// (the smallest mix64 over its m-mers and their reverse complements, m =
+// min(31, n); strand-independent) puts a read's overlap partners next to it
+// in memory for about half of its discoveries: the probe's partner slots and
+// the shared minimizer cells then come from L2 instead of HBM.  Key = minimizer
+// hash (high 54 bits) | its offset, so each cluster is ordered along the
+// genome.  One thread per read.
+template <int MAXW>
+__global__ __launch_bounds__(kBlock) void k_layout_keys(const uint64_t* __restrict__ words,
+                                                       const uint16_t* __restrict__ len, uint64_t n,
+                                                       uint64_t* __restrict__ key, uint32_t* __restrict__ val) {
+  const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  const int L = len[i];
+  const int m = L < 31 ? L : 31;
+  const uint64_t* g = words + i * slot_words(MAXW);
+  const uint64_t mmask = m ? ((1ULL << (2 * m)) - 1) : 0;
+  uint64_t fw = 0, rc = 0, best = ~0ULL, cw = 0;
+  int bpos = 0;
+  for (int t = 0; t < L; ++t) {
+    if ((t & 31) == 0) cw = g[t >> 5];
+    const uint64_t b = (cw >> (62 - 2 * (t & 31))) & 3u;
+    fw = ((fw << 2) | b) & mmask;
+    rc = (rc >> 2) | ((3u - b) << (2 * m - 2));
+    if (t >= m - 1) {
+      const uint64_t hv = mix64(fw < rc ? fw : rc);
+      if (hv < best) {
+        best = hv;
+        bpos = t - m + 1;
+      }
+    }
+  }
+  key[i] = (best & ~0x3FFull) | (uint64_t)(bpos < 1023 ? bpos : 1023);
+  val[i] = (uint32_t)i;
+}
+
+// slot i of the new layout <- slot src[i] of the ID-order upload; d_id / d_phys
+template <int MAXW>
+__global__ __launch_bounds__(kBlock) void k_layout_gather(const uint64_t* __restrict__ src_words,
+                                                         const uint16_t* __restrict__ src_len,
+                                                         const uint32_t* __restrict__ order, uint64_t n,
+                                                         uint64_t* __restrict__ dst_words, uint16_t* __restrict__ dst_len,
+                                                         uint32_t* __restrict__ id, uint32_t* __restrict__ phys) {
+  constexpr int S = slot_words(MAXW);
+  const uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (t >= n * S) return;
+  const uint64_t i = t / S;
+  const int k = (int)(t - i * S);
+  const uint32_t r = order[i];
+  dst_words[t] = src_words[(uint64_t)r * S + k];
+  if (k == 0) {
+    dst_len[i] = src_len[r];
+    id[i] = r;
+    phys[r] = (uint32_t)i;
+  }
+}
+
+// per-slot values -> ID order (superReadIDs leave the device in ID order)
+__global__ __launch_bounds__(kBlock) void k_unpermute_u32(const uint32_t* __restrict__ v, const uint32_t* __restrict__ id,
+                                                         uint64_t n, uint32_t* __restrict__ out) {
+  const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i < n) out[id[i]] = v[i];
+}
+
+template <int W>
+struct LaunchLayout {
+  static int run(mg_ctx* ctx, uint64_t* key, uint32_t* val) {
+    const uint64_t n = ctx->n;
+    hipLaunchKernelGGL((k_layout_keys<W>), dim3((uint32_t)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, ctx->stream,
+                       ctx->d_words, ctx->d_len, n, key, val);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+  }
+};
+template <int W>
+struct LaunchLayoutGather {
+  static int run(mg_ctx* ctx, const uint64_t* src_words, const uint16_t* src_len, const uint32_t* order,
+                 uint64_t* dst_words, uint16_t* dst_len) {
+    const uint64_t t = ctx->n * (uint64_t)slot_words(W);
+    hipLaunchKernelGGL((k_layout_gather<W>), dim3((uint32_t)((t + kBlock - 1) / kBlock)), dim3(kBlock), 0, ctx->stream,
+                       src_words, src_len, order, ctx->n, dst_words, dst_len, ctx->d_id, ctx->d_phys);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+  }
+};
 
 }  // namespace
 
@@ -2579,6 +2933,7 @@ IndexParams index_params(mg_ctx* ctx) {
   p.cell_lo = ctx->cell_lo;
   p.cell_n = ctx->cell_n;
   p.cells = ctx->d_cells;
+  p.id = ctx->d_id;
   return p;
 }
 
@@ -2640,16 +2995,53 @@ inline bool use_scan_reg_index(const mg_ctx* ctx) {
 }
 inline uint32_t scan_block_waves(const mg_ctx* ctx);
 inline size_t scan_lds(const mg_ctx* ctx);
+// positions per lane of the position-parallel scan (option scan_pp): the
+// read's m-mer positions must fit one wavefront (0: not applicable)
+inline int pp_K(const mg_ctx* ctx) {
+  if (ctx->maxw > 8 || ctx->maxlen < ctx->m) return 0;
+  const uint64_t np = ctx->maxlen - ctx->m + 1;
+  return np <= 64 ? 1 : np <= 128 ? 2 : np <= 256 ? 4 : 0;
+}
+// the instantiated (W, K) pairs: K = 1 needs maxlen <= 63 + m (W <= 3), K = 2
+// maxlen <= 127 + m (W 3..5), K = 4 maxlen >= 129 (W 5..8)
+template <int W, int K>
+constexpr bool pp_inst() {
+  return (K == 1 && W <= 3) || (K == 2 && W >= 3 && W <= 5) || (K == 4 && W >= 5 && W <= 8);
+}
+template <int W, bool INDEX, class Op>
+int pp_visit(int K, Op op) {
+  switch (K) {
+    case 1:
+      if constexpr (pp_inst<W, 1>()) return op(k_scan_pp<W, 1, INDEX>, PPLds<1>::bytes);
+      break;
+    case 2:
+      if constexpr (pp_inst<W, 2>()) return op(k_scan_pp<W, 2, INDEX>, PPLds<2>::bytes);
+      break;
+    case 4:
+      if constexpr (pp_inst<W, 4>()) return op(k_scan_pp<W, 4, INDEX>, PPLds<4>::bytes);
+      break;
+  }
+  return -1;
+}
+inline bool use_scan_pp(const mg_ctx* ctx, bool index) {
+  return ctx->scan_pp && pp_K(ctx) && !ctx->join_P && !(index && (ctx->reg_index || ctx->xchg));
+}
 inline uint32_t scan_wpb(uint32_t w) {
   for (uint32_t wpb = kWavesPerBlock; wpb >= 1; wpb >>= 1)
     if (wpb * scan_lds_per_wave(w) <= kLdsPerCu) return wpb;
   return 0;
 }
-inline bool scan_is_reg(const mg_ctx* ctx, bool index) { return index ? use_scan_reg_index(ctx) : use_scan_reg(ctx); }
+inline bool scan_is_reg(const mg_ctx* ctx, bool index) {
+  return !use_scan_pp(ctx, index) && (index ? use_scan_reg_index(ctx) : use_scan_reg(ctx));
+}
 inline uint32_t scan_block_waves(const mg_ctx* ctx, bool index) {
-  return scan_is_reg(ctx, index) ? kWavesPerBlock : scan_wpb(ctx->w);
+  return (use_scan_pp(ctx, index) || scan_is_reg(ctx, index)) ? kWavesPerBlock : scan_wpb(ctx->w);
 }
 inline size_t scan_lds(const mg_ctx* ctx, bool index) {
+  if (use_scan_pp(ctx, index)) {
+    const int K = pp_K(ctx);
+    return (size_t)kWavesPerBlock * (K == 1 ? PPLds<1>::bytes : K == 2 ? PPLds<2>::bytes : PPLds<4>::bytes);
+  }
   return scan_is_reg(ctx, index) ? (size_t)kWavesPerBlock * kStageRing * sizeof(uint64_t)
                                  : (size_t)scan_wpb(ctx->w) * scan_lds_per_wave(ctx->w);
 }
@@ -2657,6 +3049,11 @@ template <int W>
 uint32_t scan_resident(mg_ctx* ctx, bool index, uint64_t want) {
   const size_t lds = scan_lds(ctx, index);
   const int block = (int)scan_block_waves(ctx, index) * kWave;
+  if (use_scan_pp(ctx, index)) {
+    auto op = [&](auto kern, size_t) -> int { return (int)resident_blocks(ctx, kern, lds, want, block); };
+    const int r = index ? pp_visit<W, true>(pp_K(ctx), op) : pp_visit<W, false>(pp_K(ctx), op);
+    return (uint32_t)std::max(1, r);
+  }
   if (scan_is_reg(ctx, index))
     return index ? resident_blocks(ctx, k_scan_reg<W, true>, lds, want, block)
                  : resident_blocks(ctx, k_scan_reg<W, false>, lds, want, block);
@@ -2812,7 +3209,14 @@ struct LaunchScan {
       sp.key_n = ctx->n;
     }
     (void)hipEventRecord(ctx->ev[6], stream);
-    if (scan_is_reg(ctx, index)) {
+    if (use_scan_pp(ctx, index)) {
+      auto op = [&](auto kern, size_t) -> int {
+        allow_lds(kern, lds);
+        hipLaunchKernelGGL(kern, dim3(sgrid), dim3(wpb * kWave), lds, stream, sp);
+        return 0;
+      };
+      if ((index ? pp_visit<W, true>(pp_K(ctx), op) : pp_visit<W, false>(pp_K(ctx), op)) < 0) return -1;
+    } else if (scan_is_reg(ctx, index)) {
       if (index) {
         allow_lds(k_scan_reg<W, true>, lds);
         hipLaunchKernelGGL((k_scan_reg<W, true>), dim3(sgrid), dim3(wpb * kWave), lds, stream, sp);
@@ -2846,7 +3250,7 @@ struct LaunchProbe {
                  uint64_t run_cap, uint64_t run_regions, uint32_t grid, uint64_t total_runs,
                  const uint32_t* src_super = nullptr, uint64_t src_lo = 0, uint64_t src_hi = 0,
                  const uint64_t* fkeys = nullptr, const uint64_t* fmeta = nullptr, int pack_a = 0,
-                 int pack_w = 0) {
+                 int pack_w = 0, int xcd_map = 0) {
     ctx->nreg = (uint64_t)grid * kWavesPerBlock;  // probe wavefronts = row regions
     ProbeParams pp{};
     pp.words = ctx->d_words;
@@ -2880,6 +3284,8 @@ struct LaunchProbe {
     pp.phase_limit = contain ? 99 : ctx->phase_limit;
     pp.halving_low = ctx->halving_low ? 1 : 0;
     pp.contain_even = (contain && ctx->key0_ready) ? 1 : 0;
+    pp.xcd_map = xcd_map;
+    pp.id = ctx->d_id;
     if (ctx->split) return run_split(ctx, contain, pp, grid, total_runs);
     const size_t lds = (size_t)kWavesPerBlock * ProbeLds<W>::bytes;
     if (contain)
@@ -2992,6 +3398,15 @@ struct LaunchLookup {
   }
 };
 
+// d_super in ID order (unpermuted into d_tmp32 when the slots are clustered)
+const uint32_t* super_in_id_order(mg_ctx* ctx) {
+  if (!ctx->d_id || !ctx->n) return ctx->d_super;
+  if (ensure(&ctx->d_tmp32, &ctx->tmp32_cap, ctx->n) != hipSuccess) return ctx->d_super;
+  hipLaunchKernelGGL(k_unpermute_u32, dim3((uint32_t)((ctx->n + kBlock - 1) / kBlock)), dim3(kBlock), 0, ctx->stream,
+                     ctx->d_super, ctx->d_id, ctx->n, ctx->d_tmp32);
+  return ctx->d_tmp32;
+}
+
 float elapsed(hipEvent_t a, hipEvent_t b) {
   float ms = 0.f;
   if (hipEventElapsedTime(&ms, a, b) != hipSuccess) return 0.f;
@@ -3086,7 +3501,7 @@ void mg_destroy(mg_ctx* ctx) {
                   ctx->d_compact, ctx->d_runs, ctx->d_run_cnt, ctx->d_blk, ctx->d_flat_cnt, ctx->d_slot_cnt, ctx->d_cand, ctx->d_cand_cnt, ctx->d_freq,
                   ctx->d_sk[0], ctx->d_sk[1], ctx->d_sm[0], ctx->d_sm[1], ctx->d_sort_tmp, ctx->d_run_off,
                   ctx->d_flat_cursor, ctx->d_kb[0], ctx->d_kb[1], ctx->d_ke[0], ctx->d_ke[1], ctx->d_key0, ctx->d_holes,
-                  ctx->d_digest, ctx->d_bnd, ctx->d_mid, ctx->d_queue};
+                  ctx->d_digest, ctx->d_bnd, ctx->d_mid, ctx->d_queue, ctx->d_id, ctx->d_phys, ctx->d_tmp32};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   for (auto& e : ctx->ev)
@@ -3111,6 +3526,7 @@ static int finish_upload(mg_ctx* ctx, const uint16_t* lens_host) {
   }
   ctx->minlen = ctx->n ? mn : 0;
   ctx->maxlen = mx;
+  if (apply_layout(ctx)) return -1;
   reset_derived(ctx);
   return 0;
 }
@@ -3204,6 +3620,29 @@ int mg_download_reads_packed(mg_ctx* ctx, uint64_t* words, uint16_t* lens, uint3
     MG_TRY(hipMemcpy2D(words, ctx->maxw * sizeof(uint64_t), ctx->d_words, ctx->stride * sizeof(uint64_t),
                        ctx->maxw * sizeof(uint64_t), ctx->n, hipMemcpyDeviceToHost));
   if (lens && ctx->n) MG_TRY(hipMemcpy(lens, ctx->d_len, ctx->n * sizeof(uint16_t), hipMemcpyDeviceToHost));
+  if (ctx->d_id && ctx->n && (words || lens)) {  // slots -> ID order
+    std::vector<uint32_t> id(ctx->n);
+    MG_TRY(hipMemcpy(id.data(), ctx->d_id, ctx->n * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    const size_t wr = ctx->maxw;
+    if (words) {
+      std::vector<uint64_t> tmp(words, words + ctx->n * wr);
+      for (uint64_t i = 0; i < ctx->n; ++i) std::copy(&tmp[i * wr], &tmp[i * wr] + wr, words + (size_t)id[i] * wr);
+    }
+    if (lens) {
+      std::vector<uint16_t> tmp(lens, lens + ctx->n);
+      for (uint64_t i = 0; i < ctx->n; ++i) lens[id[i]] = tmp[i];
+    }
+  }
+  return 0;
+}
+
+int mg_read_slots(mg_ctx* ctx, uint32_t* slot_of_id) {
+  if (!ctx || !slot_of_id) return -1;
+  MG_TRY(hipSetDevice(ctx->device));
+  if (ctx->d_phys && ctx->n)
+    MG_TRY(hipMemcpy(slot_of_id, ctx->d_phys, ctx->n * sizeof(uint32_t), hipMemcpyDeviceToHost));
+  else
+    for (uint64_t i = 0; i < ctx->n; ++i) slot_of_id[i] = (uint32_t)i;
   return 0;
 }
 
@@ -3247,6 +3686,17 @@ int mg_set_option(mg_ctx* ctx, const char* name, int64_t value) {
     ctx->index_ready = false;
     return 0;
   }
+  if (!strcmp(name, "layout")) {  // 1 (default): clustered slots; 0: ID order (takes effect at the next upload)
+    ctx->layout = value != 0;
+    return 0;
+  }
+  if (!strcmp(name, "scan_pp")) {  // 1: position-parallel scan (k_scan_pp) where it applies
+    ctx->scan_pp = value != 0;
+    ctx->scan_state = 0;
+    ctx->sorted_state = 0;
+    ctx->index_ready = false;
+    return 0;
+  }
   if (!strcmp(name, "scan_reg")) {  // 1 (default): register sliding minimum when w <= 32; 0: LDS version
     ctx->scan_reg = value != 0;
     ctx->scan_state = 0;
@@ -3286,6 +3736,15 @@ int mg_set_option(mg_ctx* ctx, const char* name, int64_t value) {
   if (!strcmp(name, "sort_bits")) {  // diagnostics: sort only the top sort_bits bucket bits (0: all)
     ctx->sort_bits = (int)value;
     ctx->sorted_state = 0;
+    return 0;
+  }
+  if (!strcmp(name, "probe_region")) {  // sorted probe: runs per region (0: one tile per wavefront)
+    if (value < 0 || value > (1 << 24)) return set_err(ctx, "probe_region out of range [0, 2^24]");
+    ctx->probe_region = (uint64_t)value;
+    return 0;
+  }
+  if (!strcmp(name, "xcd_map")) {  // sorted probe with probe_region: regions dealt XCD by XCD
+    ctx->xcd_map = value != 0;
     return 0;
   }
   if (!strcmp(name, "split")) {
@@ -3636,8 +4095,11 @@ struct LaunchProbeShared {
     if (ctx->sort_runs && ctx->sorted_state == 2) {
       // bucket-ordered runs: one contiguous tile per probe wavefront
       const uint64_t n = ctx->n_sorted;
-      const uint64_t nw = (uint64_t)g.grid * kWavesPerBlock;
-      const uint64_t cap = std::max<uint64_t>(1, (n + nw - 1) / nw);
+      // regions: one contiguous tile per probe wavefront, or (option
+      // probe_region = R) regions of R runs, dealt XCD by XCD (option xcd_map)
+      const uint64_t R = ctx->probe_region;
+      const uint64_t nw = R ? std::max<uint64_t>(1, (n + R - 1) / R) : (uint64_t)g.grid * kWavesPerBlock;
+      const uint64_t cap = R ? R : std::max<uint64_t>(1, (n + nw - 1) / nw);
       if (ctx->flat_cnt_cap < nw) {
         if (ctx->d_flat_cnt) (void)hipFree(ctx->d_flat_cnt);
         ctx->d_flat_cnt = nullptr;
@@ -3648,7 +4110,8 @@ struct LaunchProbeShared {
                          ctx->d_flat_cnt, nw, cap, n);
       if (hipGetLastError() != hipSuccess) return -1;
       return LaunchProbe<W>::run(ctx, contain, nullptr, ctx->d_flat_cnt, cap, nw, g.grid, n, sup, lo, hi,
-                                 ctx->d_sk[ctx->sk_sel], ctx->d_sm[ctx->sk_sel], ctx->pack_a, ctx->pack_w);
+                                 ctx->d_sk[ctx->sk_sel], ctx->d_sm[ctx->sk_sel], ctx->pack_a, ctx->pack_w,
+                                 (R && ctx->xcd_map) ? 1 : 0);
     }
     return LaunchProbe<W>::run(ctx, contain, ctx->d_runs, ctx->d_run_cnt, ctx->run_cap, ctx->nrun_reg, g.grid, total,
                                sup, lo, hi);
@@ -3810,6 +4273,7 @@ struct LaunchJoin {
     JoinParams jp{};
     jp.words = ctx->d_words;
     jp.len = ctx->d_len;
+    jp.id = ctx->d_id;
     jp.h = (int)ctx->h;
     jp.P = ctx->join_P;
     jp.A = ctx->join_A;
@@ -3875,6 +4339,61 @@ int ensure_cells(mg_ctx* ctx) {
   return 0;
 }
 }  // namespace
+
+// Device layout of freshly uploaded reads (mg_ctx.hpp): layout keys ->
+// rocprim radix sort of (key, ID - 1) -> gather into a new slot array.  The
+// scratch (keys, the old slots) is freed before returning.
+int apply_layout(mg_ctx* ctx) {
+  ctx->t.layout_ms = 0.f;
+  if (!ctx->layout || ctx->n < 2) {  // ID order
+    if (ctx->d_id) (void)hipFree(ctx->d_id);
+    if (ctx->d_phys) (void)hipFree(ctx->d_phys);
+    ctx->d_id = ctx->d_phys = nullptr;
+    ctx->id_cap = ctx->phys_cap = 0;
+    return 0;
+  }
+  const uint64_t n = ctx->n;
+  if (n >= 0xFFFFFFFFull) return set_err(ctx, "layout: too many reads");
+  struct Scratch {
+    void* p[6] = {};
+    ~Scratch() {
+      for (void* x : p)
+        if (x) (void)hipFree(x);
+    }
+  } sc;
+  MG_TRY(hipEventRecord(ctx->ev[14], ctx->stream));
+  MG_TRY(hipMalloc(&sc.p[0], n * sizeof(uint64_t)));
+  MG_TRY(hipMalloc(&sc.p[1], n * sizeof(uint64_t)));
+  MG_TRY(hipMalloc(&sc.p[2], n * sizeof(uint32_t)));
+  MG_TRY(hipMalloc(&sc.p[3], n * sizeof(uint32_t)));
+  uint64_t* k0 = static_cast<uint64_t*>(sc.p[0]);
+  uint64_t* k1 = static_cast<uint64_t*>(sc.p[1]);
+  uint32_t* v0 = static_cast<uint32_t*>(sc.p[2]);
+  uint32_t* v1 = static_cast<uint32_t*>(sc.p[3]);
+  if (dispatch_w<LaunchLayout>(ctx->maxw, ctx, k0, v0)) return set_err(ctx, "layout key launch failed");
+  size_t tb = 0;
+  MG_TRY(rocprim::radix_sort_pairs(nullptr, tb, k0, k1, v0, v1, (unsigned int)n, 0u, 64u, ctx->stream));
+  MG_TRY(hipMalloc(&sc.p[4], std::max<size_t>(tb, 1)));
+  MG_TRY(rocprim::radix_sort_pairs(sc.p[4], tb, k0, k1, v0, v1, (unsigned int)n, 0u, 64u, ctx->stream));
+  MG_TRY(ensure(&ctx->d_id, &ctx->id_cap, n));
+  MG_TRY(ensure(&ctx->d_phys, &ctx->phys_cap, n));
+  // new slot array (same size and zero pad as the upload's); the old one is freed
+  const size_t nw = ctx->words_cap;
+  uint64_t* nwords = nullptr;
+  MG_TRY(hipMalloc(&nwords, nw * sizeof(uint64_t)));
+  sc.p[5] = nwords;
+  uint16_t* nlen = reinterpret_cast<uint16_t*>(k0);  // keys are dead after the sort: reuse for the lengths
+  MG_TRY(hipMemsetAsync(nwords, 0, nw * sizeof(uint64_t), ctx->stream));
+  if (dispatch_w<LaunchLayoutGather>(ctx->maxw, ctx, ctx->d_words, ctx->d_len, v1, nwords, nlen))
+    return set_err(ctx, "layout gather launch failed");
+  MG_TRY(hipMemcpyAsync(ctx->d_len, nlen, n * sizeof(uint16_t), hipMemcpyDeviceToDevice, ctx->stream));
+  MG_TRY(hipEventRecord(ctx->ev[15], ctx->stream));
+  MG_TRY(hipStreamSynchronize(ctx->stream));
+  sc.p[5] = ctx->d_words;  // the ID-order slots go with the scratch
+  ctx->d_words = nwords;
+  ctx->t.layout_ms = elapsed(ctx->ev[14], ctx->ev[15]);
+  return 0;
+}
 
 extern "C" {
 
@@ -4024,7 +4543,7 @@ int mg_mark_contained(mg_ctx* ctx, uint32_t* super_out) {
   if (super_out) {
     super_out[0] = 0;
     if (ctx->n)
-      MG_TRY(hipMemcpyAsync(super_out + 1, ctx->d_super, ctx->n * sizeof(uint32_t), hipMemcpyDeviceToHost,
+      MG_TRY(hipMemcpyAsync(super_out + 1, super_in_id_order(ctx), ctx->n * sizeof(uint32_t), hipMemcpyDeviceToHost,
                             ctx->stream));
     MG_TRY(hipStreamSynchronize(ctx->stream));
   }
@@ -4293,7 +4812,7 @@ int mg_finalize_contained(mg_ctx* ctx, uint32_t* super_out) {
   if (super_out) {
     super_out[0] = 0;
     if (ctx->n)
-      MG_TRY(hipMemcpyAsync(super_out + 1, ctx->d_super, ctx->n * sizeof(uint32_t), hipMemcpyDeviceToHost,
+      MG_TRY(hipMemcpyAsync(super_out + 1, super_in_id_order(ctx), ctx->n * sizeof(uint32_t), hipMemcpyDeviceToHost,
                             ctx->stream));
   }
   MG_TRY(hipStreamSynchronize(ctx->stream));
@@ -4437,7 +4956,7 @@ int mg_super_digest(mg_ctx* ctx, uint64_t* out) {
   if (digest_begin(ctx)) return -1;
   if (ctx->super_any && ctx->n) {
     const uint32_t grid = (uint32_t)std::min<uint64_t>(4096, (ctx->n + kBlock - 1) / kBlock);
-    hipLaunchKernelGGL(k_super_digest, dim3(grid), dim3(kBlock), 0, ctx->stream, ctx->d_super, ctx->n, ctx->d_digest);
+    hipLaunchKernelGGL(k_super_digest, dim3(grid), dim3(kBlock), 0, ctx->stream, ctx->d_super, ctx->n, ctx->d_digest, ctx->d_id);
   }
   return digest_end(ctx, out);
 }

@@ -32,7 +32,7 @@ class _Timings(C.Structure):
     _fields_ = [("pack_ms", C.c_float), ("index_ms", C.c_float), ("contained_ms", C.c_float),
                 ("overlap_ms", C.c_float), ("total_ms", C.c_float), ("scan_ms", C.c_float),
                 ("probe_ms", C.c_float), ("verify_ms", C.c_float), ("upload_ms", C.c_float),
-                ("ingest_ms", C.c_float), ("sort_ms", C.c_float)]
+                ("ingest_ms", C.c_float), ("sort_ms", C.c_float), ("layout_ms", C.c_float)]
 
 
 class _Counters(C.Structure):
@@ -70,6 +70,7 @@ def lib() -> C.CDLL:
         "mg_upload_reads_ascii": (i32, [vp, C.c_char_p, vp, u64]),
         "mg_num_reads": (u64, [vp]),
         "mg_download_reads_packed": (i32, [vp, vp, vp, P(u32)]),
+        "mg_read_slots": (i32, [vp, vp]),
         "mg_build_index": (i32, [vp, u32, u32]),
         "mg_lookup_key": (i32, [vp, C.c_char_p, u32, vp, u64, P(u64)]),
         "mg_mark_contained": (i32, [vp, vp]),
@@ -353,6 +354,12 @@ class OverlapEngine:
         lens = np.zeros(self.n_reads, np.uint16)
         self._check(lib().mg_download_reads_packed(self._h, _ptr(words), _ptr(lens), C.byref(wpr)), "download")
         return words, lens
+
+    def slot_of_ids(self) -> np.ndarray:
+        """Device slot of each read, indexed by ID - 1 (mg_read_slots)."""
+        s = np.zeros(self.n_reads, dtype=np.uint32)
+        self._check(lib().mg_read_slots(self._h, _ptr(s)), "read_slots")
+        return s.astype(np.int64)
 
     # --- hot path
     def set_option(self, name: str, value: int):
