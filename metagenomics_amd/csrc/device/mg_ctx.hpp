@@ -101,7 +101,6 @@ struct mg_ctx {
   // its runs then serve the containment and the discovery probes
   int scan_state = 0;        // 0 none, 1 launched (not settled), 2 settled
   bool overlap_scan = true;  // option "overlap_scan" (0: separate index build, a scan per probe pass)
-  bool scan_pp = false;       // option "scan_pp": position-parallel scan (k_scan_pp) when the read fits a wavefront
   bool scan_reg = true;      // option "scan_reg": register sliding minimum (k_scan_reg) for the run scans when w <= 32
   bool reg_index = false;    // option "reg_index": also for the cell index build (key records + k_insert_dense)
   // partitioned join (option "join", default): keys + runs as sorted join
@@ -148,7 +147,9 @@ struct mg_ctx {
   int pack_a = 0, pack_w = 0;      // packing of the current flat runs (0: 16-B records)
   int sorted_state = 0;  // 0 none, 2 sorted (for the current scan)
   uint64_t probe_region = 0;  // sorted probe: runs per region (0: one tile per wavefront)
-  bool xcd_map = false;       // sorted probe: regions dealt XCD by XCD
+  bool xcd_map = true;        // probe: run regions dealt XCD by XCD (group regions, or sorted with probe_region)
+  bool group_regions = false; // option "group_regions": one run region per read group of 64 (measured slower)
+  bool group_active = false;  // the last scan wrote group regions
   int sort_bits = 0;     // diagnostics: sort only the top sort_bits bucket bits (0: all)
   // sorted index build (option "sorted_index", default off): k_scan<INDEX> writes
   // the 4N key records (bucket, entry), a radix sort orders them by bucket and

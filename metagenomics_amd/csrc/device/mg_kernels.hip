@@ -144,6 +144,8 @@ __global__ __launch_bounds__(kBlock) void k_pack_ascii(const char* __restrict__ 
 // An entry goes to the first cell of its minimizer's home cell chain that has
 // room (cell-granular linear probing), so a lookup reads the home cell's count
 // and line together and follows the chain only while count > kCell.
+// s_waitcnt immediate of gfx9/CDNA: vmcnt(0), expcnt and lgkmcnt not waited for
+constexpr int kWaitVm0 = 0x0F70;
 constexpr int kCell = 8;
 constexpr int kScanBuf = 3 * 64;  // staged run metas per scan wavefront (two puts per step: < 64 + 128)
 constexpr int kStageRing = 512;   // register scan: LDS ring of staged run metas per wavefront
@@ -398,7 +400,8 @@ struct ScanParams {
   uint64_t a_lo, a_hi;
   int h, m, w;
   uint32_t nb_log2, rank, nranks;
-  ulonglong2* runs;               // one region of run_cap records per wavefront
+  ulonglong2* runs;               // one region of run_cap records per wavefront (group_regions: per group of 64 reads)
+  int group_regions;              // 1: region g holds the runs of read group g (reads [64 g, 64 g + 64)), in read order
   unsigned long long* run_cnt;    // [waves] records produced (may exceed run_cap)
   uint64_t run_cap;
   uint64_t* cells;                // k_scan<INDEX>: the (unsharded) cell table the keys go into
@@ -533,7 +536,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) voi
   const uint64_t nw = (uint64_t)gridDim.x * wpb;
   uint64_t* s_buf = reinterpret_cast<uint64_t*>(smem) + (size_t)wpb * ((w * kWave + 1) / 2) +
                     (size_t)wv * kScanBuf;
-  ulonglong2* const region = p.runs + gw * p.run_cap;
+  ulonglong2* region = p.runs + gw * p.run_cap;
   const uint64_t nbmask = (1ULL << p.nb_log2) - 1;
   uint64_t cursor = 0;
   uint32_t nbuf = 0;  // run metas staged in s_buf (wavefront-uniform)
@@ -550,6 +553,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) voi
     const uint64_t a = p.a_lo + grp * kWave + lane;
     int n = 0;
     const uint64_t* g = p.words + a * slot_words(MAXW);
+    if (p.group_regions) {  // this group's own region
+      region = p.runs + grp * p.run_cap;
+      cursor = 0;
+    }
     if (a < p.a_hi) {
       n = (int)p.len[a];
       if (n && p.super && p.super[a]) n = 0;
@@ -569,6 +576,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) voi
 #pragma unroll
       for (int k = 0; k <= MAXW; ++k) rw[k] = k < kRw ? gs[k] : 0;
     }
+    // the words land before the base loop: otherwise the loop's first use of a
+    // word sits behind a vmcnt(0) that the compiler repeats every step (the
+    // flushes' run stores and the CAS inserts keep vmcnt open across the back
+    // edge), so each step after a flush waited for those stores to retire
+    __builtin_amdgcn_s_waitcnt(kWaitVm0);
     auto word_at = [&](int idx) {  // idx wavefront-uniform
       uint64_t v = rw[0];
 #pragma unroll
@@ -764,6 +776,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) voi
     }
     put(tend > 0, run_meta(a, last_pos, jlo, J));  // each read's last run
     while (nbuf) flush(nbuf < (uint32_t)kWave ? nbuf : (uint32_t)kWave);  // the group's runs leave with its registers
+    if (p.group_regions && lane == 0) p.run_cnt[grp] = cursor;
     if (INDEX && tend) {
       // t = n-m, one past the last window position: the rolled m-mers sit there
       const uint32_t hk = order_key(mm), hr = order_key(rcm);
@@ -812,7 +825,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) voi
       }
     }
   }
-  if (lane == 0) p.run_cnt[gw] = cursor;
+  if (lane == 0 && !p.group_regions) p.run_cnt[gw] = cursor;
 }
 
 // ---------------------------------------------------------------------------
@@ -955,7 +968,17 @@ struct RunStage {
         }
       }
     }
-    if (lane == 0) p.run_cnt[gw] = cursor;
+    if (lane == 0 && !p.group_regions) p.run_cnt[gw] = cursor;
+  }
+  // group_regions: each read group's runs go to its own region
+  __device__ __forceinline__ void begin_group(uint64_t grp) {
+    if (p.group_regions) {
+      region = p.runs + grp * p.run_cap;
+      cursor = 0;
+    }
+  }
+  __device__ __forceinline__ void end_group(uint64_t grp) {
+    if (p.group_regions && lane == 0) p.run_cnt[grp] = cursor;
   }
 };
 
@@ -1037,6 +1060,7 @@ __global__ __launch_bounds__(kBlock) void k_scan_reg(ScanParams p) {
       for (int k = 0; k <= MAXW; ++k) nx[k] = k < kRwLoad ? gs[k] : 0;
     }
     const uint64_t a0 = p.a_lo + grp * kWave;
+    st.begin_group(grp);
     uint32_t S[kRegW + 1];
 #pragma unroll
     for (int u = 0; u <= kRegW; ++u) S[u] = 0xFFFFFFFFu;
@@ -1087,6 +1111,7 @@ __global__ __launch_bounds__(kBlock) void k_scan_reg(ScanParams p) {
     }
     st.put(tend >= 0, run_meta(a, last, jlo, J));  // each read's last run
     while (st.nbuf) st.flush(st.nbuf < (uint32_t)kWave ? st.nbuf : (uint32_t)kWave, rw, a0);
+    st.end_group(grp);
     if constexpr (INDEX) {  // join records of keys o = 0 / 1 (the cell index is k_scan's / k_index_build's)
       if (a < p.a_hi) {
         const int p0 = (int)(kw0 & 1023u), p1 = (int)(kw1 & 1023u);
@@ -1196,237 +1221,6 @@ __global__ __launch_bounds__(kBlock) void k_rc_keys(ScanParams p) {
   p.join_kv[4 * a + 2] = n ? join_key_val((uint32_t)a, 2, (int)(kb2 & 1023u), v2, p) : kFlatHole;
   p.join_kk[4 * a + 3] = n ? join_k32(v3, p.join_P, 0u) : 0xFFFFFFFFu;
   p.join_kv[4 * a + 3] = n ? join_key_val((uint32_t)a, 3, (int)(kb3 & 1023u), v3, p) : kFlatHole;
-}
-
-// Window minimizers with LANES OVER POSITIONS (option scan_pp): a wavefront
-// takes one read at a time and lane l holds the K m-mers at positions
-// t = K l + k, each hashed independently (no serial chain, no per-position
-// branch).  Window j = m-mers [j, j + w - 1] (OverlapGraph.cpp:534-537); its
-// minimum is (suffix of lane l from k) | (lanes l+1 .. l+F, a sparse table of
-// lane minima doubled by __shfl_down) | (prefix of lane l+F+1), with the same
-// order (order_key | t, leftmost on ties) as every other scan.  Run starts
-// are ballots; a start's run ends before the next start (one scan of the
-// uniform start masks).  Runs are staged as metas in an LDS ring and hashed /
-// written 64 at a time (RunStage; the m-mer comes back from the read's slot,
-// an L1 hit).  INDEX (HashTable::insertDataset / hashRead, HashTable.cpp:
-// 50-104): o = 0 / 1 are windows j = 0 and j = n - h of this same min; o = 3 /
-// 2 are the minimum over positions [0, w) / [n - h, n - m] of the reverse
-// strand's m-mer keys (order_key(rc) | i), a wave reduction; the four entries
-// are staged and CAS-inserted 64 at a time (or written as key records).
-constexpr int kPPWords = 16;  // LDS copy of the current read's words (zero past the slot)
-constexpr int kPPKeys = 128;  // staged index entries per wavefront (inserted 64 at a time)
-template <int K>
-struct PPLds {
-  static constexpr int RING = 128 * K;  // >= 63 + the most runs one read can add (J < 64 K)
-  static constexpr size_t o_w = 0;
-  static constexpr size_t o_ring = o_w + kPPWords * 8;
-  static constexpr size_t o_kb = o_ring + (size_t)RING * 8;
-  static constexpr size_t o_ke = o_kb + kPPKeys * 8;
-  static constexpr size_t bytes = o_ke + kPPKeys * 8;
-};
-
-template <int MAXW, int K, bool INDEX>
-__global__ __launch_bounds__(kBlock) void k_scan_pp(ScanParams p) {
-  using PL = PPLds<K>;
-  extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  unsigned char* base = reinterpret_cast<unsigned char*>(smem) + (size_t)wv * PL::bytes;
-  uint64_t* s_w = reinterpret_cast<uint64_t*>(base + PL::o_w);
-  uint64_t* s_kb = reinterpret_cast<uint64_t*>(base + PL::o_kb);
-  uint64_t* s_ke = reinterpret_cast<uint64_t*>(base + PL::o_ke);
-  const int h = p.h, m = p.m, w = p.w;
-  const int msh = 64 - 2 * m;
-  const uint64_t mmask = (m == 32) ? ~0ULL : ((1ULL << (2 * m)) - 1);
-  const uint64_t nbmask = (1ULL << p.nb_log2) - 1;
-  const uint64_t gw = (uint64_t)blockIdx.x * kWavesPerBlock + wv;
-  const uint64_t nw = (uint64_t)gridDim.x * kWavesPerBlock;
-  RunStage<MAXW, PL::RING, true> st(p, reinterpret_cast<uint64_t*>(base + PL::o_ring), p.runs + gw * p.run_cap, lane);
-  // this wavefront's reads: one contiguous range (its runs stay in read order)
-  const uint64_t nrd = p.a_hi - p.a_lo, per = (nrd + nw - 1) / nw;
-  const uint64_t a_beg = p.a_lo + std::min<uint64_t>(nrd, gw * per);
-  const uint64_t a_end = p.a_lo + std::min<uint64_t>(nrd, (gw + 1) * per);
-  constexpr int kRw = MAXW + 1 <= slot_words(MAXW) ? MAXW + 1 : slot_words(MAXW);
-  uint32_t nkeys = 0;  // staged index entries (CAS mode)
-  // the staged entries, one per lane, into the cells (insertIntoTable, HashTable.cpp:163-195)
-  auto insert_keys = [&](uint32_t k) {
-    wave_sync();
-    if ((uint32_t)lane < k) cell_insert(p.cells, s_kb[lane], p.cell_n, s_ke[lane]);
-    const uint32_t rest = nkeys - k;  // < 64 + 4
-    const uint64_t b0 = (uint32_t)lane < rest ? s_kb[k + lane] : 0, e0 = (uint32_t)lane < rest ? s_ke[k + lane] : 0;
-    wave_sync();
-    if ((uint32_t)lane < rest) {
-      s_kb[lane] = b0;
-      s_ke[lane] = e0;
-    }
-    nkeys = rest;
-    wave_sync();
-  };
-  // software pipeline: the next read's words and length load behind this read
-  uint64_t wnext = 0;
-  int nnext = 0;
-  if (a_beg < a_end) {
-    wnext = lane < kRw ? p.words[a_beg * slot_words(MAXW) + lane] : 0;
-    nnext = (int)p.len[a_beg];
-  }
-  for (uint64_t a = a_beg; a < a_end; ++a) {
-    const uint64_t wcur = wnext;
-    int n = nnext;
-    if (a + 1 < a_end) {
-      wnext = lane < kRw ? p.words[(a + 1) * slot_words(MAXW) + lane] : 0;
-      nnext = (int)p.len[a + 1];
-    }
-    if (n && p.super && p.super[a]) n = 0;  // contained sources get no windows (:548)
-    n = __builtin_amdgcn_readfirstlane(n);
-    wave_sync();
-    if (lane < kPPWords) s_w[lane] = wcur;
-    wave_sync();
-    if (!n) {  // (no such read in a Dataset: every read is longer than l) key holes
-      if (INDEX && lane == 0 && p.key0) p.key0[a] = kEmpty;
-      if (INDEX && p.key_bk && lane < 4) {
-        p.key_bk[lane * p.key_n + a] = 0;
-        p.key_ent[lane * p.key_n + a] = kEmpty;
-      }
-      continue;
-    }
-    const int J = n - h - 1;  // scan windows j = 1 .. J
-    const int tl = n - m;     // last m-mer position
-    // ---- keys of this lane's positions
-    uint32_t key[K];
-    uint32_t rk2 = 0xFFFFFFFFu, rk3 = 0xFFFFFFFFu;  // INDEX: reverse-strand keys of o = 2 / 3
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-      const int t = K * lane + k, wi = t >> 5;
-      const uint64_t x = funnel(s_w[wi], s_w[wi + 1], (t & 31) << 1);  // bases t .. t + 31
-      key[k] = t <= tl ? (order_key(x >> msh) | (uint32_t)t) : 0xFFFFFFFFu;
-      if (INDEX) {
-        const uint32_t hr = order_key(rc_word(x) & mmask);
-        if (t < w) rk3 = min(rk3, hr | (uint32_t)(w - 1 - t));                // o = 3, i = w - 1 - t
-        if (t >= tl - w + 1 && t <= tl) rk2 = min(rk2, hr | (uint32_t)(tl - t));  // o = 2, i = n - m - t
-      }
-    }
-    // ---- sliding minimum over w positions
-    uint32_t pre[K], suf[K];
-    pre[0] = key[0];
-#pragma unroll
-    for (int k = 1; k < K; ++k) pre[k] = min(pre[k - 1], key[k]);
-    suf[K - 1] = key[K - 1];
-#pragma unroll
-    for (int k = K - 2; k >= 0; --k) suf[k] = min(suf[k + 1], key[k]);
-    // sparse table of lane minima: T[v] = min over lanes l .. l + 2^v - 1
-    const int fmax = (K - 1 + w - 1) / K - 1;  // most full lanes inside one window
-    uint32_t T[6];
-    T[0] = pre[K - 1];
-#pragma unroll
-    for (int v = 1; v < 6; ++v) T[v] = ((1 << v) <= fmax) ? min(T[v - 1], (uint32_t)__shfl_down(T[v - 1], 1 << (v - 1))) : T[v - 1];
-    uint32_t pos[K];
-    uint32_t wn0 = 0xFFFFFFFFu, wn1 = 0xFFFFFFFFu;  // INDEX: minima of windows 0 and n - h
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-      const int e = k + w - 1, le = e / K, ke = e % K;  // window end: lane + le, slot ke (uniform)
-      uint32_t r;
-      if (le == 0) {
-        r = 0xFFFFFFFFu;
-#pragma unroll
-        for (int kk = k; kk < K; ++kk) r = kk <= ke ? min(r, key[kk]) : r;
-      } else {
-        uint32_t pk = pre[0];
-#pragma unroll
-        for (int kk = 1; kk < K; ++kk) pk = kk == ke ? pre[kk] : pk;
-        r = min(suf[k], (uint32_t)__shfl_down(pk, le));
-        const int F = le - 1;
-        if (F > 0) {
-          const int v = 31 - __clz(F);
-          uint32_t tv = T[0];
-#pragma unroll
-          for (int vv = 1; vv < 6; ++vv) tv = vv == v ? T[vv] : tv;
-          r = min(r, min((uint32_t)__shfl_down(tv, 1), (uint32_t)__shfl_down(tv, 1 + F - (1 << v))));
-        }
-      }
-      pos[k] = r & 1023u;
-      if (INDEX) {  // o = 0: window 0 (lane 0, slot 0); o = 1: window n - h
-        const int j = K * lane + k;
-        if (j == 0) wn0 = r;
-        if (j == n - h) wn1 = r;
-      }
-    }
-    // ---- runs: starts are windows whose minimizer differs from window j - 1
-    uint64_t S[K];
-    uint64_t anyS = 0;
-    {
-      const uint32_t up = (uint32_t)__shfl_up((int)pos[K - 1], 1);
-#pragma unroll
-      for (int k = 0; k < K; ++k) {
-        const int j = K * lane + k;
-        const uint32_t prev = k ? pos[k - 1] : up;
-        const bool start = j >= 1 && j <= J && (j == 1 || pos[k] != prev);
-        S[k] = __ballot(start);
-        anyS |= S[k];
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-      const int j = K * lane + k;
-      const bool start = (S[k] >> lane) & 1ull;
-      int jn = J + 1;  // next start (or one past the last window)
-      bool found = false;
-#pragma unroll
-      for (int kk = K - 1; kk > k; --kk)
-        if ((S[kk] >> lane) & 1ull) {
-          jn = K * lane + kk;
-          found = true;
-        }
-      if (!found) {
-        const uint64_t upper = lane == 63 ? 0ull : (anyS & (~0ull << (lane + 1)));
-        if (upper) {
-          const int l2 = __builtin_ctzll(upper);
-          int k2 = K - 1;
-#pragma unroll
-          for (int kk = K - 1; kk >= 0; --kk)
-            if ((S[kk] >> l2) & 1ull) k2 = kk;
-          jn = K * l2 + k2;
-        }
-      }
-      st.put(start, run_meta(a, (int)pos[k], j, jn - 1));
-    }
-    while (st.nbuf >= (uint32_t)kWave) st.flush(kWave, nullptr, 0);
-    if constexpr (INDEX) {
-      // the four keys' minimizers (uniform): o = 0 / 1 forward, o = 2 / 3 reverse strand
-      const uint32_t k0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)wn0);
-      const uint32_t k1 = (uint32_t)__builtin_amdgcn_readlane((int)wn1, (n - h) / K);
-#pragma unroll
-      for (int d = 32; d >= 1; d >>= 1) {
-        rk2 = min(rk2, (uint32_t)__shfl_xor((int)rk2, d));
-        rk3 = min(rk3, (uint32_t)__shfl_xor((int)rk3, d));
-      }
-      // lane o < 4 builds entry o: m-mer position t, key offset q, strand
-      const int o = lane & 3;
-      const uint32_t kk = o == 0 ? k0 : o == 1 ? k1 : o == 2 ? rk2 : rk3;
-      const int q0 = (int)(kk & 1023u);  // o < 2: window position t; o >= 2: offset i
-      const int t = o == 0 ? q0 : o == 1 ? q0 : o == 2 ? tl - q0 : w - 1 - q0;
-      const int q = o == 1 ? q0 - (n - h) : q0;
-      const int wi = t >> 5;
-      const uint64_t x = funnel(s_w[wi], s_w[wi + 1], (t & 31) << 1);
-      const uint64_t v = mix64(o < 2 ? x >> msh : rc_word(x) & mmask);
-      const unsigned long long e = make_entry(v, p.nb_log2, q, o, (uint32_t)a);
-      if (lane == 0 && p.key0) p.key0[a] = (v & ((1ULL << 50) - 1)) | ((uint64_t)q << 54);
-      if (p.key_bk) {
-        if (lane < 4) {
-          p.key_bk[o * p.key_n + a] = (uint32_t)(v & nbmask);
-          p.key_ent[o * p.key_n + a] = e;
-        }
-      } else {
-        if (lane < 4) {
-          s_kb[nkeys + lane] = v & nbmask;
-          s_ke[nkeys + lane] = e;
-        }
-        nkeys += 4;
-        if (nkeys >= (uint32_t)kWave) insert_keys(kWave);
-      }
-    }
-  }
-  while (st.nbuf) st.flush(st.nbuf < (uint32_t)kWave ? st.nbuf : (uint32_t)kWave, nullptr, 0);
-  if (INDEX && nkeys) insert_keys(nkeys);
-  st.finish(gw);
 }
 
 // checkOverlap's string compare (OverlapGraph.cpp:354-383) on packed words:
@@ -1703,6 +1497,7 @@ __global__ __launch_bounds__(kBlock) void k_probe(ProbeParams p) {
       rec_pf = rbase[pf_ok ? k : 0];
     }
   };
+
   auto take_item = [&](uint64_t& key, uint64_t& meta, bool& valid) -> bool {
     if (npend >= (uint32_t)kWave) {
       npend -= kWave;
@@ -2995,53 +2790,16 @@ inline bool use_scan_reg_index(const mg_ctx* ctx) {
 }
 inline uint32_t scan_block_waves(const mg_ctx* ctx);
 inline size_t scan_lds(const mg_ctx* ctx);
-// positions per lane of the position-parallel scan (option scan_pp): the
-// read's m-mer positions must fit one wavefront (0: not applicable)
-inline int pp_K(const mg_ctx* ctx) {
-  if (ctx->maxw > 8 || ctx->maxlen < ctx->m) return 0;
-  const uint64_t np = ctx->maxlen - ctx->m + 1;
-  return np <= 64 ? 1 : np <= 128 ? 2 : np <= 256 ? 4 : 0;
-}
-// the instantiated (W, K) pairs: K = 1 needs maxlen <= 63 + m (W <= 3), K = 2
-// maxlen <= 127 + m (W 3..5), K = 4 maxlen >= 129 (W 5..8)
-template <int W, int K>
-constexpr bool pp_inst() {
-  return (K == 1 && W <= 3) || (K == 2 && W >= 3 && W <= 5) || (K == 4 && W >= 5 && W <= 8);
-}
-template <int W, bool INDEX, class Op>
-int pp_visit(int K, Op op) {
-  switch (K) {
-    case 1:
-      if constexpr (pp_inst<W, 1>()) return op(k_scan_pp<W, 1, INDEX>, PPLds<1>::bytes);
-      break;
-    case 2:
-      if constexpr (pp_inst<W, 2>()) return op(k_scan_pp<W, 2, INDEX>, PPLds<2>::bytes);
-      break;
-    case 4:
-      if constexpr (pp_inst<W, 4>()) return op(k_scan_pp<W, 4, INDEX>, PPLds<4>::bytes);
-      break;
-  }
-  return -1;
-}
-inline bool use_scan_pp(const mg_ctx* ctx, bool index) {
-  return ctx->scan_pp && pp_K(ctx) && !ctx->join_P && !(index && (ctx->reg_index || ctx->xchg));
-}
 inline uint32_t scan_wpb(uint32_t w) {
   for (uint32_t wpb = kWavesPerBlock; wpb >= 1; wpb >>= 1)
     if (wpb * scan_lds_per_wave(w) <= kLdsPerCu) return wpb;
   return 0;
 }
-inline bool scan_is_reg(const mg_ctx* ctx, bool index) {
-  return !use_scan_pp(ctx, index) && (index ? use_scan_reg_index(ctx) : use_scan_reg(ctx));
-}
+inline bool scan_is_reg(const mg_ctx* ctx, bool index) { return index ? use_scan_reg_index(ctx) : use_scan_reg(ctx); }
 inline uint32_t scan_block_waves(const mg_ctx* ctx, bool index) {
-  return (use_scan_pp(ctx, index) || scan_is_reg(ctx, index)) ? kWavesPerBlock : scan_wpb(ctx->w);
+  return scan_is_reg(ctx, index) ? kWavesPerBlock : scan_wpb(ctx->w);
 }
 inline size_t scan_lds(const mg_ctx* ctx, bool index) {
-  if (use_scan_pp(ctx, index)) {
-    const int K = pp_K(ctx);
-    return (size_t)kWavesPerBlock * (K == 1 ? PPLds<1>::bytes : K == 2 ? PPLds<2>::bytes : PPLds<4>::bytes);
-  }
   return scan_is_reg(ctx, index) ? (size_t)kWavesPerBlock * kStageRing * sizeof(uint64_t)
                                  : (size_t)scan_wpb(ctx->w) * scan_lds_per_wave(ctx->w);
 }
@@ -3049,11 +2807,6 @@ template <int W>
 uint32_t scan_resident(mg_ctx* ctx, bool index, uint64_t want) {
   const size_t lds = scan_lds(ctx, index);
   const int block = (int)scan_block_waves(ctx, index) * kWave;
-  if (use_scan_pp(ctx, index)) {
-    auto op = [&](auto kern, size_t) -> int { return (int)resident_blocks(ctx, kern, lds, want, block); };
-    const int r = index ? pp_visit<W, true>(pp_K(ctx), op) : pp_visit<W, false>(pp_K(ctx), op);
-    return (uint32_t)std::max(1, r);
-  }
   if (scan_is_reg(ctx, index))
     return index ? resident_blocks(ctx, k_scan_reg<W, true>, lds, want, block)
                  : resident_blocks(ctx, k_scan_reg<W, false>, lds, want, block);
@@ -3112,27 +2865,34 @@ struct LaunchScan {
                  hipStream_t stream = nullptr, bool no_super = false, bool index = false, bool flat = false) {
     if (!stream) stream = ctx->stream;
     const uint32_t wpb = scan_block_waves(ctx, index);
-    const uint64_t nw = (uint64_t)sgrid * wpb;  // scan wavefronts = run regions
-    ctx->nrun_reg = nw;
+    const uint64_t nw = (uint64_t)sgrid * wpb;  // scan wavefronts
     const uint64_t ngroups = (a_hi - a_lo + kWave - 1) / kWave;
-    // run regions: expected runs per read ~ 2 J / (w + 1) + 1 (minimizer density)
+    // run regions: one per scan wavefront, or (option group_regions) one per
+    // read group of 64, so region order is read order and the probe can sweep
+    // neighbouring reads together (the clustered layout's locality)
+    const bool group = ctx->group_regions && !flat;
+    ctx->group_active = group;
+    const uint64_t nreg = group ? ngroups : nw;
+    ctx->nrun_reg = nreg;
+    // expected runs per read ~ 2 J / (w + 1) + 1 (minimizer density)
     const uint64_t J = ctx->maxlen > ctx->h + 1 ? ctx->maxlen - ctx->h - 1 : 1;
-    const uint64_t per_read = std::min<uint64_t>(J, 3 * (2 * J / (ctx->w + 1) + 2));
-    const uint64_t groups_per_wave = (ngroups + nw - 1) / nw;
-    uint64_t run_cap = std::max<uint64_t>(ctx->run_cap_need, groups_per_wave * kWave * per_read);
-    if (run_cap * nw > ctx->runs_cap) {
+    const uint64_t per_read = group ? std::min<uint64_t>(J, 3 * (2 * J / (ctx->w + 1) + 2) / 2)
+                                    : std::min<uint64_t>(J, 3 * (2 * J / (ctx->w + 1) + 2));
+    const uint64_t groups_per_region = group ? 1 : (ngroups + nw - 1) / nw;
+    uint64_t run_cap = std::max<uint64_t>(ctx->run_cap_need, groups_per_region * kWave * per_read);
+    if (run_cap * nreg > ctx->runs_cap) {
       if (ctx->d_runs) (void)hipFree(ctx->d_runs);
       ctx->d_runs = nullptr;
-      if (hipMalloc(&ctx->d_runs, run_cap * nw * sizeof(ulonglong2)) != hipSuccess) return -1;
-      ctx->runs_cap = run_cap * nw;
+      if (hipMalloc(&ctx->d_runs, run_cap * nreg * sizeof(ulonglong2)) != hipSuccess) return -1;
+      ctx->runs_cap = run_cap * nreg;
     }
-    run_cap = ctx->runs_cap / nw;
+    run_cap = ctx->runs_cap / std::max<uint64_t>(1, nreg);
     ctx->run_cap = run_cap;
-    if (ctx->run_cnt_cap < nw) {
+    if (ctx->run_cnt_cap < nreg) {
       if (ctx->d_run_cnt) (void)hipFree(ctx->d_run_cnt);
       ctx->d_run_cnt = nullptr;
-      if (hipMalloc(&ctx->d_run_cnt, nw * sizeof(unsigned long long)) != hipSuccess) return -1;
-      ctx->run_cnt_cap = nw;
+      if (hipMalloc(&ctx->d_run_cnt, std::max<uint64_t>(1, nreg) * sizeof(unsigned long long)) != hipSuccess) return -1;
+      ctx->run_cnt_cap = nreg;
     }
     ScanParams sp{};
     sp.words = ctx->d_words;
@@ -3149,6 +2909,7 @@ struct LaunchScan {
     sp.runs = ctx->d_runs;
     sp.run_cnt = ctx->d_run_cnt;
     sp.run_cap = run_cap;
+    sp.group_regions = group ? 1 : 0;
     const size_t lds = scan_lds(ctx, index);
     sp.cells = ctx->d_cells;
     sp.cell_n = ctx->cell_n;
@@ -3209,14 +2970,7 @@ struct LaunchScan {
       sp.key_n = ctx->n;
     }
     (void)hipEventRecord(ctx->ev[6], stream);
-    if (use_scan_pp(ctx, index)) {
-      auto op = [&](auto kern, size_t) -> int {
-        allow_lds(kern, lds);
-        hipLaunchKernelGGL(kern, dim3(sgrid), dim3(wpb * kWave), lds, stream, sp);
-        return 0;
-      };
-      if ((index ? pp_visit<W, true>(pp_K(ctx), op) : pp_visit<W, false>(pp_K(ctx), op)) < 0) return -1;
-    } else if (scan_is_reg(ctx, index)) {
+    if (scan_is_reg(ctx, index)) {
       if (index) {
         allow_lds(k_scan_reg<W, true>, lds);
         hipLaunchKernelGGL((k_scan_reg<W, true>), dim3(sgrid), dim3(wpb * kWave), lds, stream, sp);
@@ -3690,13 +3444,6 @@ int mg_set_option(mg_ctx* ctx, const char* name, int64_t value) {
     ctx->layout = value != 0;
     return 0;
   }
-  if (!strcmp(name, "scan_pp")) {  // 1: position-parallel scan (k_scan_pp) where it applies
-    ctx->scan_pp = value != 0;
-    ctx->scan_state = 0;
-    ctx->sorted_state = 0;
-    ctx->index_ready = false;
-    return 0;
-  }
   if (!strcmp(name, "scan_reg")) {  // 1 (default): register sliding minimum when w <= 32; 0: LDS version
     ctx->scan_reg = value != 0;
     ctx->scan_state = 0;
@@ -3743,7 +3490,13 @@ int mg_set_option(mg_ctx* ctx, const char* name, int64_t value) {
     ctx->probe_region = (uint64_t)value;
     return 0;
   }
-  if (!strcmp(name, "xcd_map")) {  // sorted probe with probe_region: regions dealt XCD by XCD
+  if (!strcmp(name, "group_regions")) {  // 1 (default): one run region per read group (read order)
+    ctx->group_regions = value != 0;
+    ctx->scan_state = 0;
+    ctx->sorted_state = 0;
+    return 0;
+  }
+  if (!strcmp(name, "xcd_map")) {  // probe regions dealt XCD by XCD (group regions; sorted runs with probe_region)
     ctx->xcd_map = value != 0;
     return 0;
   }
@@ -4114,7 +3867,7 @@ struct LaunchProbeShared {
                                  (R && ctx->xcd_map) ? 1 : 0);
     }
     return LaunchProbe<W>::run(ctx, contain, ctx->d_runs, ctx->d_run_cnt, ctx->run_cap, ctx->nrun_reg, g.grid, total,
-                               sup, lo, hi);
+                               sup, lo, hi, nullptr, nullptr, 0, 0, (ctx->group_active && ctx->xcd_map) ? 1 : 0);
   }
 };
 

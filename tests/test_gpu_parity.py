@@ -815,53 +815,6 @@ def test_scan_lds_path(name):
 
 
 @pytest.mark.parametrize("name", FIXTURES)
-@pytest.mark.parametrize("pp", [0, 1])
-def test_scan_pp_path(name, pp):
-    """option scan_pp: the position-parallel scan (k_scan_pp, lanes over m-mer
-    positions, log-step lane minima) for the index build and the run scans,
-    against the LDS / register scans (pp = 0); same keys, runs, rows and
-    superReadIDs as the reference."""
-    meta = load_meta(name)
-    ds = Dataset.from_files([fixture_input(name)], meta["l"])
-    e = OverlapEngine(0)
-    e.set_option("scan_pp", pp)
-    for overlap_scan in (1, 0):  # shared INDEX scan, then a separate run scan per probe
-        e.set_option("overlap_scan", overlap_scan)
-        rows, sup = gpu_rows(e, ds, meta["l"])
-        assert np.array_equal(rows_to_tuples(rows), golden_rows(name)), overlap_scan
-        assert {str(i): int(s) for i, s in enumerate(sup) if s} == meta["super"]
-        if overlap_scan and "lookups" in meta:  # the index k_scan_pp<INDEX> filed
-            for key, exp in meta["lookups"].items():
-                assert [list(x) for x in e.lookup(key)] == exp, key
-    e.close()
-
-
-@pytest.mark.parametrize("l,k,lo,hi", [(33, 1, 34, 60), (40, 8, 41, 130), (50, 17, 51, 178), (20, 19, 21, 82),
-                                       (50, 31, 51, 158), (50, 31, 120, 256), (60, 32, 61, 256), (30, 12, 31, 75),
-                                       (60, 28, 61, 91)])
-def test_scan_pp_window_extremes(engine, l, k, lo, hi):
-    """k_scan_pp across its lane geometries (K = 1, 2, 4 positions per lane:
-    reads of 34-256 bp), w = l - k from 1 to 32 (windows inside one lane up to
-    windows spanning 31 lanes), mixed lengths (containment, all four keys),
-    against the oracle; also with the sorted index build (key records)."""
-    c, L = synth.uniform_read_set(3000, 0, 15000, seed=300 + k, lo=lo, hi=hi)
-    seqs = synth.codes_to_strings(c, L)
-    ds = Dataset.from_codes(c, L, l)
-    od = OracleDataset.from_strings(seqs, l)
-    orows, osup, _, _ = od.overlaps(l)
-    engine.set_option("scan_pp", 1)
-    try:
-        for sorted_index in (0, 1):
-            engine.set_option("sorted_index", sorted_index)
-            rows, sup = gpu_rows(engine, ds, l, k=k)
-            assert np.array_equal(sup.astype(np.uint64), osup), sorted_index
-            assert np.array_equal(rows_to_tuples(rows), sorted_tuples(orows)), sorted_index
-    finally:
-        engine.set_option("sorted_index", 0)
-        engine.set_option("scan_pp", 0)
-
-
-@pytest.mark.parametrize("name", FIXTURES)
 @pytest.mark.parametrize("layout,sort_runs", [(0, 0), (0, 1), (1, 1)])
 def test_layout_and_sort_options(name, layout, sort_runs):
     """option layout = 0 (slots in ID order) and the bucket-sorted run probe
