@@ -66,6 +66,8 @@ typedef struct mg_counters {
   uint64_t verified;  /* partner reads fetched and compared           */
   uint64_t rows;      /* directed rows emitted                        */
   uint64_t trips;     /* join: wavefront index-lookup trips (diagnostics) */
+  /* the last containment pass (markContainedReads), same units */
+  uint64_t c_runs, c_entries, c_verified, c_contained;
 } mg_counters;
 
 /* --- context ------------------------------------------------------------ */

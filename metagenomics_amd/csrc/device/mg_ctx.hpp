@@ -212,6 +212,19 @@ inline uint32_t supported_maxw(uint32_t need) {
   return 0;
 }
 
+// Reads longer than 1024 bp (up to 65,535, Read.h:62) take the long-read
+// kernels (mg_kernels.hip: k_index_long, k_probe_long): maxw is then the exact
+// word count and a slot holds it plus at least one zero pad word.
+inline bool long_mode(const mg_ctx* ctx) { return ctx->maxw > 32; }
+inline uint32_t long_stride(uint32_t maxw) { return (maxw + 1 + 7) & ~7u; }
+// slot width for reads of `need` words: the instantiated widths up to 32,
+// else the long-read width (maxw = need); 0 = longer than 65,535 bp
+inline uint32_t slot_maxw(uint32_t need) {
+  if (need <= 32) return supported_maxw(need < 1 ? 1 : need);
+  return need <= 2048 ? need : 0;
+}
+inline uint32_t slot_stride(uint32_t maxw) { return maxw > 32 ? long_stride(maxw) : (uint32_t)slot_words((int)maxw); }
+
 // the device layout of freshly uploaded reads (mg_kernels.hip): clusters the
 // slots by canonical global minimizer and fills d_id / d_phys (option "layout"
 // = 0: ID order); records t.layout_ms

@@ -117,13 +117,63 @@ __global__ __launch_bounds__(kThreads) void k_ingest(IngestSrc s, uint64_t n, ui
   atomicMax(&lenrange[1], (unsigned int)L);
 }
 
-// key of the current LSD pass for the order so far
+// k_ingest for reads longer than 1,024 bp (up to 65,535, Read.h:62): the same
+// filter and canonical strand, but the words are built one at a time from the
+// source (no register arrays): pass 1 testRead, pass 2 the first word where
+// the strands differ (std::lexicographical_compare), pass 3 the chosen
+// strand's CW words.
+template <bool ASCII>
+__global__ __launch_bounds__(kThreads) void k_ingest_long(IngestSrc s, uint64_t n, uint32_t min_overlap, uint32_t cw,
+                                                          uint64_t* __restrict__ canon, uint16_t* __restrict__ len_out,
+                                                          uint8_t* __restrict__ valid,
+                                                          unsigned int* __restrict__ lenrange) {
+  const uint64_t i = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t L = raw_len<ASCII>(s, i);
+  bool ok = L > min_overlap && L <= 65535 && L <= 32u * cw;  // Dataset.cpp:160; UINT16 length
+  uint32_t cnt[4] = {0, 0, 0, 0};
+  for (uint64_t p = 0; ok && p < L; ++p) {
+    const uint32_t c = base_code<ASCII>(s, i, p);
+    if (c > 3u) ok = false;
+    else cnt[c]++;
+  }
+  if (ok) {  // 80 % rule (Dataset.cpp:409-411)
+    const uint64_t thr = (uint64_t)((double)L * .8);
+    ok = cnt[0] < thr && cnt[1] < thr && cnt[2] < thr && cnt[3] < thr;
+  }
+  valid[i] = ok ? 1 : 0;
+  len_out[i] = (uint16_t)(ok ? L : 0);
+  if (!ok) return;
+  auto word = [&](uint32_t k, bool rc) {
+    uint64_t x = 0;
+    for (int t = 0; t < 32; ++t) {
+      const uint64_t p = 32u * k + t;
+      uint32_t c = 0;
+      if (p < L) c = rc ? 3u - base_code<ASCII>(s, i, L - 1 - p) : base_code<ASCII>(s, i, p);
+      x = (x << 2) | c;
+    }
+    return x;
+  };
+  bool fwd = false;
+  for (uint32_t k = 0; 32u * k < L; ++k) {
+    const uint64_t f = word(k, false), r = word(k, true);
+    if (f != r) {
+      fwd = f < r;
+      break;
+    }
+  }
+  for (uint32_t k = 0; k < cw; ++k) canon[i * cw + k] = 32u * k < L ? word(k, !fwd) : 0ull;
+  atomicMin(&lenrange[0], (unsigned int)L);
+  atomicMax(&lenrange[1], (unsigned int)L);
+}
+
+// key of the current LSD pass for the order so far (W = 0: cw words per read)
 template <int W>
 __global__ __launch_bounds__(kThreads) void k_gather_word(const uint64_t* __restrict__ canon,
                                                           const uint32_t* __restrict__ idx, uint64_t n, int k,
-                                                          uint64_t* __restrict__ key) {
+                                                          uint64_t* __restrict__ key, uint32_t cw) {
   const uint64_t i = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
-  if (i < n) key[i] = canon[(uint64_t)idx[i] * W + k];
+  if (i < n) key[i] = canon[(uint64_t)idx[i] * (W ? W : cw) + k];
 }
 
 __global__ __launch_bounds__(kThreads) void k_gather_len(const uint16_t* __restrict__ len,
@@ -138,15 +188,17 @@ template <int W>
 __global__ __launch_bounds__(kThreads) void k_dedup_flags(const uint64_t* __restrict__ canon,
                                                           const uint16_t* __restrict__ len,
                                                           const uint32_t* __restrict__ idx, uint64_t n,
-                                                          uint32_t* __restrict__ start) {
+                                                          uint32_t* __restrict__ start, uint32_t cw) {
   const uint64_t i = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
   if (i >= n) return;
+  constexpr uint32_t CW0 = W;
+  const uint32_t CW = W ? CW0 : cw;
   bool s = i == 0;
   if (!s) {
     const uint64_t a = idx[i - 1], b = idx[i];
     s = len[a] != len[b];
 #pragma unroll
-    for (int k = 0; k < W; ++k) s = s || canon[a * W + k] != canon[b * W + k];
+    for (uint32_t k = 0; k < CW; ++k) s = s || canon[a * CW + k] != canon[b * CW + k];
   }
   start[i] = s ? 1u : 0u;
 }
@@ -161,13 +213,15 @@ __global__ __launch_bounds__(kThreads) void k_dedup_write(const uint64_t* __rest
                                                           const uint32_t* __restrict__ uid, uint64_t n,
                                                           uint32_t maxw, uint32_t stride,
                                                           uint64_t* __restrict__ words, uint16_t* __restrict__ lens,
-                                                          uint32_t* __restrict__ first) {
+                                                          uint32_t* __restrict__ first, uint32_t cw) {
   const uint64_t i = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
   if (i >= n || !start[i]) return;
   const uint64_t u = uid[i], a = idx[i];
+  constexpr uint32_t CW0 = W;
+  const uint32_t CW = W ? CW0 : cw;
 #pragma unroll
-  for (int k = 0; k < W; ++k)
-    if ((uint32_t)k < maxw) words[u * stride + k] = canon[a * W + k];
+  for (uint32_t k = 0; k < CW; ++k)
+    if (k < maxw) words[u * stride + k] = canon[a * CW + k];
   lens[u] = len[a];
   first[u] = (uint32_t)i;
 }
@@ -191,15 +245,18 @@ uint32_t blocks(uint64_t n) { return (uint32_t)((n + kThreads - 1) / kThreads); 
 
 template <int W>
 struct Ingest {
-  static int run(mg_ctx* ctx, const IngestSrc& s, bool ascii, uint64_t n, uint32_t min_overlap, uint64_t* n_unique) {
+  // W = 0: reads longer than 1,024 bp, cw words per read (k_ingest_long)
+  static int run(mg_ctx* ctx, const IngestSrc& s, bool ascii, uint64_t n, uint32_t min_overlap, uint64_t* n_unique,
+                 uint32_t cw = 0) {
     hipStream_t st = ctx->stream;
+    const uint32_t CW = W ? (uint32_t)W : cw;
     DevBuf<uint64_t> canon, key_a, key_b;
     DevBuf<uint16_t> len, lkey_a, lkey_b;
     DevBuf<uint8_t> valid;
     DevBuf<uint32_t> idx_a, idx_b, start, uid, first;
     DevBuf<unsigned int> lr;
     DevBuf<unsigned long long> nsel;
-    MG_TRY(canon.alloc(n * W));
+    MG_TRY(canon.alloc(n * CW));
     MG_TRY(len.alloc(n));
     MG_TRY(valid.alloc(n));
     MG_TRY(lr.alloc(2));
@@ -207,12 +264,18 @@ struct Ingest {
     const unsigned int lr0[2] = {0xFFFFFFFFu, 0u};
     MG_TRY(hipMemcpyAsync(lr.p, lr0, sizeof(lr0), hipMemcpyHostToDevice, st));
     if (n) {
-      if (ascii)
-        hipLaunchKernelGGL((k_ingest<W, true>), dim3(blocks(n)), dim3(kThreads), 0, st, s, n, min_overlap, canon.p,
-                           len.p, valid.p, lr.p);
+      if (W == 0 && ascii)
+        hipLaunchKernelGGL((k_ingest_long<true>), dim3(blocks(n)), dim3(kThreads), 0, st, s, n, min_overlap, CW,
+                           canon.p, len.p, valid.p, lr.p);
+      else if (W == 0)
+        hipLaunchKernelGGL((k_ingest_long<false>), dim3(blocks(n)), dim3(kThreads), 0, st, s, n, min_overlap, CW,
+                           canon.p, len.p, valid.p, lr.p);
+      else if (ascii)
+        hipLaunchKernelGGL((k_ingest<(W ? W : 1), true>), dim3(blocks(n)), dim3(kThreads), 0, st, s, n, min_overlap,
+                           canon.p, len.p, valid.p, lr.p);
       else
-        hipLaunchKernelGGL((k_ingest<W, false>), dim3(blocks(n)), dim3(kThreads), 0, st, s, n, min_overlap, canon.p,
-                           len.p, valid.p, lr.p);
+        hipLaunchKernelGGL((k_ingest<(W ? W : 1), false>), dim3(blocks(n)), dim3(kThreads), 0, st, s, n, min_overlap,
+                           canon.p, len.p, valid.p, lr.p);
       MG_TRY(hipGetLastError());
     }
     // indices of the valid reads, in input order
@@ -259,7 +322,7 @@ struct Ingest {
       const uint32_t wused = (lrh[1] + 31) / 32;  // words past the longest read are all zero
       for (int k = (int)wused - 1; k >= 0; --k) {
         hipLaunchKernelGGL((k_gather_word<W>), dim3(blocks(ngood)), dim3(kThreads), 0, st, canon.p, cur, ngood, k,
-                           key_a.p);
+                           key_a.p, CW);
         tb = tmp_bytes;
         MG_TRY(hipcub::DeviceRadixSort::SortPairs(tmp.p, tb, key_a.p, key_b.p, cur, alt, (int)ngood, 0, 64, st));
         std::swap(cur, alt);
@@ -270,7 +333,7 @@ struct Ingest {
     MG_TRY(uid.alloc(ngood));
     if (ngood) {
       hipLaunchKernelGGL((k_dedup_flags<W>), dim3(blocks(ngood)), dim3(kThreads), 0, st, canon.p, len.p, cur, ngood,
-                         start.p);
+                         start.p, CW);
       tb = tmp_bytes;
       MG_TRY(hipcub::DeviceScan::ExclusiveSum(tmp.p, tb, start.p, uid.p, (int)ngood, st));
     }
@@ -282,10 +345,10 @@ struct Ingest {
     MG_TRY(hipStreamSynchronize(st));
     const uint64_t nu = ngood ? (uint64_t)last_uid + last_start : 0;
     if (nu >= 0xFFFFFFFFull) return set_err(ctx, "too many reads (max 2^32-2)");
-    const uint32_t maxw = supported_maxw(std::max<uint32_t>(1, (lrh[1] + 31) / 32));
+    const uint32_t maxw = slot_maxw(std::max<uint32_t>(1, (lrh[1] + 31) / 32));
     ctx->n = nu;
     ctx->maxw = ngood ? maxw : supported_maxw(1);
-    ctx->stride = slot_words((int)ctx->maxw);
+    ctx->stride = slot_stride(ctx->maxw);
     const size_t nw = (size_t)(nu + 2) * ctx->stride + 2;  // zero pad for over-reads
     MG_TRY(ensure(&ctx->d_words, &ctx->words_cap, nw));
     MG_TRY(ensure(&ctx->d_len, &ctx->len_cap, nu + 1));
@@ -294,7 +357,7 @@ struct Ingest {
     MG_TRY(first.alloc(nu));
     if (ngood) {
       hipLaunchKernelGGL((k_dedup_write<W>), dim3(blocks(ngood)), dim3(kThreads), 0, st, canon.p, len.p, cur, start.p,
-                         uid.p, ngood, ctx->maxw, ctx->stride, ctx->d_words, ctx->d_len, first.p);
+                         uid.p, ngood, ctx->maxw, ctx->stride, ctx->d_words, ctx->d_len, first.p, CW);
       hipLaunchKernelGGL(k_dedup_freq, dim3(blocks(nu)), dim3(kThreads), 0, st, first.p, nu, ngood, ctx->d_freq);
       MG_TRY(hipGetLastError());
     }
@@ -311,7 +374,9 @@ struct Ingest {
 
 int ingest(mg_ctx* ctx, const IngestSrc& s, bool ascii, uint64_t n, uint64_t maxlen, uint32_t min_overlap,
            uint64_t* n_unique) {
-  const uint32_t w = supported_maxw((uint32_t)std::max<uint64_t>(1, (std::min<uint64_t>(maxlen, 1024) + 31) / 32));
+  const uint64_t need = (std::min<uint64_t>(maxlen, 65535) + 31) / 32;
+  if (need > 32) return Ingest<0>::run(ctx, s, ascii, n, min_overlap, n_unique, (uint32_t)need);
+  const uint32_t w = supported_maxw((uint32_t)std::max<uint64_t>(1, need));
   switch (w) {
     case 1: return Ingest<1>::run(ctx, s, ascii, n, min_overlap, n_unique);
     case 2: return Ingest<2>::run(ctx, s, ascii, n, min_overlap, n_unique);
@@ -336,13 +401,11 @@ int mg_ingest_ascii(mg_ctx* ctx, const char* concat, const uint64_t* offsets, ui
   if (!ctx || !n_unique || (n_raw && (!concat || !offsets))) return -1;
   MG_TRY(hipSetDevice(ctx->device));
   if (n_raw >= 0xFFFFFFFFull) return set_err(ctx, "too many reads (max 2^32-2)");
-  uint64_t maxlen = 0, longest_valid_len = 0;
+  uint64_t longest_valid_len = 0;
   for (uint64_t i = 0; i < n_raw; ++i) {
     const uint64_t L = offsets[i + 1] - offsets[i];
-    maxlen = std::max(maxlen, L);
     if (L > min_overlap && L <= 65535) longest_valid_len = std::max(longest_valid_len, L);
   }
-  if (longest_valid_len > 1024) return set_err(ctx, "reads longer than 1024 bp are not supported on the device");
   const uint64_t total = n_raw ? offsets[n_raw] : 0;
   DevBuf<char> d_ascii;
   DevBuf<uint64_t> d_off;
@@ -353,7 +416,8 @@ int mg_ingest_ascii(mg_ctx* ctx, const char* concat, const uint64_t* offsets, ui
   MG_TRY(hipMemcpyAsync(d_off.p, offsets, (n_raw + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, ctx->stream));
   MG_TRY(hipEventRecord(ctx->ev[1], ctx->stream));
   IngestSrc s{d_ascii.p, d_off.p, nullptr, 0, nullptr};
-  if (ingest(ctx, s, true, n_raw, maxlen, min_overlap, n_unique)) return -1;
+  // slot width from the longest read that can pass testRead's length bounds
+  if (ingest(ctx, s, true, n_raw, longest_valid_len, min_overlap, n_unique)) return -1;
   MG_TRY(hipEventRecord(ctx->ev[2], ctx->stream));
   MG_TRY(hipEventSynchronize(ctx->ev[2]));
   float h2d = 0.f, dev = 0.f;
@@ -375,7 +439,6 @@ int mg_ingest_codes(mg_ctx* ctx, const uint8_t* codes, uint64_t n_raw, uint64_t 
     if (lens[i] > min_overlap) longest_valid_len = std::max<uint64_t>(longest_valid_len, lens[i]);
   }
   if (maxlen > stride && n_raw > 1) return set_err(ctx, "read length exceeds the row stride");
-  if (longest_valid_len > 1024) return set_err(ctx, "reads longer than 1024 bp are not supported on the device");
   DevBuf<uint8_t> d_codes;
   DevBuf<uint16_t> d_lens;
   MG_TRY(d_codes.alloc(n_raw * stride));
@@ -387,7 +450,7 @@ int mg_ingest_codes(mg_ctx* ctx, const uint8_t* codes, uint64_t n_raw, uint64_t 
   }
   MG_TRY(hipEventRecord(ctx->ev[1], ctx->stream));
   IngestSrc s{nullptr, nullptr, d_codes.p, stride, d_lens.p};
-  if (ingest(ctx, s, false, n_raw, maxlen, min_overlap, n_unique)) return -1;
+  if (ingest(ctx, s, false, n_raw, longest_valid_len, min_overlap, n_unique)) return -1;
   MG_TRY(hipEventRecord(ctx->ev[2], ctx->stream));
   MG_TRY(hipEventSynchronize(ctx->ev[2]));
   float h2d = 0.f, dev = 0.f;

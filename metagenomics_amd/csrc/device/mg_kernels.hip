@@ -166,6 +166,7 @@ struct IndexParams {
   uint64_t cell_lo, cell_n;  // this rank's bucket range [cell_lo, cell_lo + cell_n): local cell = bucket - cell_lo
   uint64_t* cells;   // [cell_n * kCell] entries: lo32 = read index, hi32 = chain1 | fp19 | q10 | o2
   const uint32_t* id;  // slot -> reference ID - 1 (nullptr: ID order; lookups return IDs)
+  uint32_t stride;     // words per slot (the long-read kernels; the templated ones use slot_words(MAXW))
 };
 
 __device__ __forceinline__ bool owned(uint64_t bkt, uint32_t nb_log2, uint32_t rank, uint32_t nranks) {
@@ -1415,6 +1416,7 @@ __global__ __launch_bounds__(kBlock) void k_probe(ProbeParams p) {
       if (diff == 0) {
         if (CONTAIN) {
           atomicMax(&p.superkey[bid], ((unsigned long long)n1 << 32) | (0xFFFFFFFFu - ida));
+          ++st_rows;
         } else if (!(p.super && p.super[bid])) {  // :548 read2 contained
           // orientation/offset switch (:550-557) and the twin (:409-412, :841-855)
           const uint32_t orient = (o == 0) ? 3u : (o == 2 ? 2u : 1u);
@@ -2563,7 +2565,7 @@ __global__ __launch_bounds__(kBlock) void k_lookup_key(IndexParams p, const uint
       if (en != kEmpty && ((hi >> 12) & kFpMask) == fp && (int)((hi >> 2) & 1023u) == qq) {
         const int o = (int)(hi & 3u);
         const uint32_t r = (uint32_t)en;
-        const uint64_t* g = p.words + (uint64_t)r * slot_words(MAXW);
+        const uint64_t* g = p.words + (uint64_t)r * (MAXW ? (uint64_t)slot_words(MAXW) : (uint64_t)p.stride);
         const int n = p.len[r];
         // key string of (r, o) vs the query, 32 bases at a time
         uint64_t diff = 0;
@@ -2592,6 +2594,181 @@ __global__ __launch_bounds__(kBlock) void k_lookup_key(IndexParams p, const uint
     if (last == kEmpty || !(last & kChain)) break;
     b = next_cell(b, p.cell_n);
   }
+}
+
+// ------------------------------------------------------------ long reads ---
+// Reads longer than 1,024 bp, up to Read::getReadLength's UINT16 (Read.h:62).
+// The templated kernels keep a read's words in registers and pack window
+// positions into 10-bit fields; these keep the words in HBM (slots of
+// mg_ctx::stride words, at least one zero pad word) and work one WINDOW per
+// lane, so positions are plain ints.  Same cell index, same entries, same
+// exactness argument as the main path: window F1[j, j+h)
+// equals key K only if both select the same minimizer at the same offset q,
+// so an entry is a candidate when its fingerprint and q match the window's,
+// and every candidate is verified over the full overlap.
+
+// HashTable::insertDataset (HashTable.cpp:50-80) for long reads: one thread
+// per key, the key's m-mers read straight from the slot.
+__global__ __launch_bounds__(kBlock) void k_index_long(IndexParams p) {
+  const uint64_t mask = (1ULL << p.nb_log2) - 1;
+  for (uint64_t gid = (uint64_t)blockIdx.x * kBlock + threadIdx.x; (gid >> 2) < p.n;
+       gid += (uint64_t)gridDim.x * kBlock) {
+    const uint64_t r = gid >> 2;
+    const int o = (int)(gid & 3);
+    int q;
+    const uint64_t v = key_minimizer<1>(p.words + r * p.stride, p.len[r], o, p.h, p.m, p.w, &q);
+    const uint64_t b = v & mask;
+    if (owned(b, p.nb_log2, p.rank, p.nranks))
+      cell_insert(p.cells, b - p.cell_lo, p.cell_n, make_entry(v, p.nb_log2, q, o, (uint32_t)r));
+  }
+}
+
+// Minimizer of the forward window F[s0, s0+h): the same rule as key_minimizer
+// (order_key | i, smallest wins), so a window and an identical key agree.
+__device__ __forceinline__ uint64_t window_minimizer(const uint64_t* f, int s0, int m, int w, int* q) {
+  const uint64_t mmask = (m == 32) ? ~0ULL : ((1ULL << (2 * m)) - 1);
+  uint64_t mm = ext_fwd<1>(f, s0) >> (64 - 2 * m);
+  uint32_t bkey = 0xFFFFFFFFu;
+  uint64_t bmm = 0;
+  for (int i = 0; i < w; ++i) {
+    const uint32_t key = order_key(mm) | (uint32_t)i;
+    if (key < bkey) {
+      bkey = key;
+      bmm = mm;
+    }
+    if (i + 1 < w) {
+      const int x = s0 + i + m;
+      mm = ((mm << 2) | ((f[x >> 5] >> (62 - 2 * (x & 31))) & 3u)) & mmask;
+    }
+  }
+  *q = (int)(bkey & 1023u);
+  return mix64(bmm);
+}
+
+// checkOverlap / checkOverlapForContainedRead's compare (OverlapGraph.cpp:
+// 302-383) for any length: partner bases [y0, y0+L) of F2 against source bases
+// [x0, x0+L) of F1, or of R1 when rcA, 32 bases per step, both from HBM.
+__device__ bool overlap_equal_long(const uint64_t* f1, int n1, const uint64_t* f2, int x0, int y0, int L, bool rcA) {
+  for (int k = y0 >> 5; 32 * k < y0 + L; ++k) {
+    const int lo = max(y0 - 32 * k, 0), hi = min(y0 + L - 32 * k, 32);
+    const int s = x0 - y0 + 32 * k;  // source position of partner base 32k
+    const uint64_t av = rcA ? rc_word(ext_fwd<1>(f1, n1 - s - 32)) : ext_fwd<1>(f1, s);
+    const uint64_t msk = (lo ? (~0ULL >> (2 * lo)) : ~0ULL) & (hi < 32 ? ~(~0ULL >> (2 * hi)) : ~0ULL);
+    if ((av ^ f2[k]) & msk) return false;
+  }
+  return true;
+}
+
+struct LongParams {
+  const uint64_t* words;
+  const uint16_t* len;
+  uint32_t stride;
+  int h, m, w;
+  uint32_t nb_log2;
+  uint64_t cell_n;
+  const uint64_t* cells;
+  uint64_t a_lo, a_hi;            // source reads
+  const uint32_t* super;          // superReadID per read (nullptr: none contained)
+  unsigned long long* superkey;   // CONTAIN: max over containers of (len << 32 | ~index)
+  uint32_t* rows;                 // one region of reg_cap rows per wavefront
+  unsigned long long* reg_cnt;
+  uint64_t reg_cap;
+  int halving_low;
+};
+
+// markContainedReads (CONTAIN) or insertAllEdgesOfRead (OverlapGraph.cpp:
+// 225-290, 529-565) for long reads: one wavefront per source read (grid-
+// stride), one window j in [1, n1-h) per lane, the window's home cell chain,
+// then the same filter, halving rule, verification and rows + twins as
+// k_probe.  Rows go to the wavefront's region through an LDS
+// cursor (the count keeps running past the capacity: the host resizes and
+// reruns).
+template <bool CONTAIN>
+__global__ __launch_bounds__(kBlock) void k_probe_long(LongParams p) {
+  __shared__ unsigned long long s_cur[kWavesPerBlock];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint64_t gw = (uint64_t)blockIdx.x * kWavesPerBlock + wv;
+  const uint64_t nw = (uint64_t)gridDim.x * kWavesPerBlock;
+  if (lane == 0) s_cur[wv] = 0;
+  __syncthreads();
+  const int h = p.h;
+  const uint64_t nbmask = (1ULL << p.nb_log2) - 1;
+  uint32_t* const region = p.rows + gw * p.reg_cap * 3;
+  for (uint64_t a = p.a_lo + gw; a < p.a_hi; a += nw) {
+    if (!CONTAIN && p.super && p.super[a]) continue;  // :548 read1 contained
+    const int n1 = p.len[a];
+    const uint64_t* f1 = p.words + a * p.stride;
+    for (int j = 1 + lane; j < n1 - h; j += kWave) {
+      int q;
+      const uint64_t v = window_minimizer(f1, j, p.m, p.w, &q);
+      const uint32_t fp = (uint32_t)(v >> p.nb_log2) & kFpMask;
+      uint64_t c = v & nbmask;
+      for (uint64_t probe = 0; probe < p.cell_n; ++probe) {
+        const uint64_t* cell = p.cells + c * kCell;
+        for (int s = 0; s < kCell; ++s) {
+          const uint64_t e = cell[s];
+          if (e == kEmpty) continue;
+          const uint32_t hi = (uint32_t)(e >> 32), bid = (uint32_t)e;
+          if (((hi >> 12) & kFpMask) != fp || (int)((hi >> 2) & 1023u) != q) continue;
+          const int o = (int)(hi & 3u);
+          const int n2 = p.len[bid];
+          const uint64_t* f2 = p.words + (uint64_t)bid * p.stride;
+          int L, x0, y0;
+          bool cond, rcA;
+          if (CONTAIN) {
+            // checkOverlapForContainedRead: o = 0/2 place read2 at s = j; o = 1/3
+            // only at s = 0 (s >= 1 is the o = 0/2 hit at window j = s, k_probe)
+            int sft;
+            cond = n1 > n2;
+            if (o == 0 || o == 2) {
+              cond = cond && j <= n1 - n2;
+              sft = j;
+            } else {
+              cond = cond && j == n2 - h;
+              sft = 0;
+            }
+            L = n2;
+            y0 = 0;
+            rcA = o >= 2;
+            x0 = rcA ? n1 - sft - n2 : sft;
+            if (cond && overlap_equal_long(f1, n1, f2, x0, y0, L, rcA))
+              atomicMax(&p.superkey[bid], ((unsigned long long)n1 << 32) | (0xFFFFFFFFu - (uint32_t)a));
+            continue;
+          }
+          // halving: o = 1 never, o = 2/3 on one side only
+          if (o == 1 || (o >= 2 && !(p.halving_low ? bid >= (uint32_t)a : rc_side_keeps((uint32_t)a, bid)))) continue;
+          if (p.super && p.super[bid]) continue;  // :548 read2 contained
+          if (o == 0) {        // F1[j, n1) == F2[0, L)
+            L = n1 - j; cond = L < n2; x0 = j; y0 = 0; rcA = false;
+          } else if (o == 2) { // F1[j, n1) == R2[0, L)  <=>  R1[0, L) == F2[n2-L, n2)
+            L = n1 - j; cond = L < n2; x0 = 0; y0 = n2 - L; rcA = true;
+          } else {             // F1[0, L) == R2[n2-L, n2)  <=>  R1[n1-L, n1) == F2[0, L)
+            L = j + h; cond = j <= n2 - h; x0 = n1 - L; y0 = 0; rcA = true;
+          }
+          if (!cond || !overlap_equal_long(f1, n1, f2, x0, y0, L, rcA)) continue;
+          // orientation/offset switch (:550-557) and the twin (:409-412, :841-855)
+          const uint32_t orient = (o == 0) ? 3u : (o == 2 ? 2u : 1u);
+          const uint32_t off = (o == 3) ? (uint32_t)(n1 - h - j) : (uint32_t)j;
+          const uint32_t torient = (orient == 3u) ? 0u : orient;
+          const uint32_t toff = (uint16_t)(n2 + off - n1);
+          const int nrec = (bid == (uint32_t)a && o == 0) ? 4 : 2;  // self o=0 hit also stands for its o=1 twin
+          const unsigned long long at = atomicAdd(&s_cur[wv], (unsigned long long)nrec);
+          if (at + nrec <= p.reg_cap) {
+            uint3* d = reinterpret_cast<uint3*>(region + at * 3);
+            for (int rr = 0; rr < nrec; rr += 2) {
+              d[rr] = make_uint3((uint32_t)a + 1, bid + 1, (orient << 16) | off);
+              d[rr + 1] = make_uint3(bid + 1, (uint32_t)a + 1, (torient << 16) | toff);
+            }
+          }
+        }
+        const uint64_t last = cell[kCell - 1];
+        if (last == kEmpty || !(last & kChain)) break;
+        c = next_cell(c, p.cell_n);
+      }
+    }
+  }
+  __syncthreads();
+  if (!CONTAIN && lane == 0) p.reg_cnt[gw] = s_cur[wv];
 }
 
 }  // namespace
@@ -2729,6 +2906,7 @@ IndexParams index_params(mg_ctx* ctx) {
   p.cell_n = ctx->cell_n;
   p.cells = ctx->d_cells;
   p.id = ctx->d_id;
+  p.stride = ctx->stride;
   return p;
 }
 
@@ -2788,8 +2966,6 @@ inline bool use_scan_reg(const mg_ctx* ctx) { return (ctx->scan_reg || ctx->join
 inline bool use_scan_reg_index(const mg_ctx* ctx) {
   return (ctx->join_P || ctx->reg_index || ctx->xchg) && use_scan_reg_w(ctx);
 }
-inline uint32_t scan_block_waves(const mg_ctx* ctx);
-inline size_t scan_lds(const mg_ctx* ctx);
 inline uint32_t scan_wpb(uint32_t w) {
   for (uint32_t wpb = kWavesPerBlock; wpb >= 1; wpb >>= 1)
     if (wpb * scan_lds_per_wave(w) <= kLdsPerCu) return wpb;
@@ -3034,7 +3210,7 @@ struct LaunchProbe {
     pp.reg_cnt = ctx->d_seg;
     pp.reg_cap = contain ? 0 : ctx->rows_cap / ctx->nreg;
     pp.uniform_len = ctx->minlen == ctx->maxlen ? (int)ctx->maxlen : 0;
-    pp.stats = contain ? nullptr : (ctx->stats ? ctx->d_stats : nullptr);
+    pp.stats = ctx->stats ? ctx->d_stats : nullptr;
     pp.phase_limit = contain ? 99 : ctx->phase_limit;
     pp.halving_low = ctx->halving_low ? 1 : 0;
     pp.contain_even = (contain && ctx->key0_ready) ? 1 : 0;
@@ -3151,6 +3327,65 @@ struct LaunchLookup {
     return hipGetLastError() == hipSuccess ? 0 : -1;
   }
 };
+
+// ---- long reads (> 1024 bp): the generic kernels behind the same entry points
+int launch_index(mg_ctx* ctx) {
+  if (!long_mode(ctx)) return dispatch_w<LaunchIndex>(ctx->maxw, ctx);
+  if (!ctx->n) return 0;
+  const uint32_t grid = (uint32_t)std::min<uint64_t>((4 * ctx->n + kBlock - 1) / kBlock, 65536);
+  hipLaunchKernelGGL(k_index_long, dim3(grid), dim3(kBlock), 0, ctx->stream, index_params(ctx));
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_lookup(mg_ctx* ctx, const uint64_t* dq, int qwords, unsigned long long* dout, uint32_t cap,
+                  unsigned int* dn) {
+  if (!long_mode(ctx)) return dispatch_w<LaunchLookup>(ctx->maxw, ctx, dq, qwords, dout, cap, dn);
+  hipLaunchKernelGGL((k_lookup_key<0>), dim3(1), dim3(kBlock), 0, ctx->stream, index_params(ctx), dq, qwords, dout,
+                     cap, dn);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// k_probe_long over sources [a_lo, a_hi): containment (atomicMax into the
+// superkeys) or discovery (rows; regions resized and rerun on overflow)
+int settle_rows(mg_ctx* ctx, bool* again);
+int long_probe(mg_ctx* ctx, bool contain, uint64_t a_lo, uint64_t a_hi) {
+  LongParams p{};
+  p.words = ctx->d_words;
+  p.len = ctx->d_len;
+  p.stride = ctx->stride;
+  p.h = (int)ctx->h;
+  p.m = (int)ctx->m;
+  p.w = (int)ctx->w;
+  p.nb_log2 = ctx->nb_log2;
+  p.cell_n = ctx->cell_n;
+  p.cells = ctx->d_cells;
+  p.a_lo = a_lo;
+  p.a_hi = a_hi;
+  p.super = (!contain && ctx->contained_done && ctx->super_any) ? ctx->d_super : nullptr;
+  p.superkey = ctx->superkey;
+  p.halving_low = ctx->halving_low ? 1 : 0;
+  const uint64_t nsrc = a_hi > a_lo ? a_hi - a_lo : 0;
+  const uint32_t grid = (uint32_t)std::max<uint64_t>(
+      1, std::min<uint64_t>({(nsrc + kWavesPerBlock - 1) / kWavesPerBlock, (uint64_t)ctx->n_cu * 8, ctx->max_blocks}));
+  if (contain) {
+    hipLaunchKernelGGL(k_probe_long<true>, dim3(grid), dim3(kBlock), 0, ctx->stream, p);
+    return hipGetLastError() == hipSuccess ? 0 : set_err(ctx, "long-read containment launch failed");
+  }
+  ctx->nreg = (uint64_t)grid * kWavesPerBlock;
+  for (int attempt = 0; attempt < 3; ++attempt) {
+    p.rows = ctx->d_rows;
+    p.reg_cnt = ctx->d_seg;
+    p.reg_cap = ctx->rows_cap / ctx->nreg;
+    MG_TRY(hipEventRecord(ctx->ev[8], ctx->stream));
+    hipLaunchKernelGGL(k_probe_long<false>, dim3(grid), dim3(kBlock), 0, ctx->stream, p);
+    MG_TRY(hipGetLastError());
+    MG_TRY(hipEventRecord(ctx->ev[9], ctx->stream));
+    bool again = false;
+    if (settle_rows(ctx, &again)) return -1;
+    if (!again) return 0;
+  }
+  return set_err(ctx, "discovery buffers overflow after resize");
+}
 
 // d_super in ID order (unpermuted into d_tmp32 when the slots are clustered)
 const uint32_t* super_in_id_order(mg_ctx* ctx) {
@@ -3293,21 +3528,23 @@ int mg_upload_reads_packed(mg_ctx* ctx, const uint64_t* words, const uint16_t* l
   uint32_t mx = 0;
   for (uint64_t i = 0; i < n_reads; i++) mx = std::max<uint32_t>(mx, lens[i]);
   if (mx > 32u * words_per_read) return set_err(ctx, "read longer than words_per_read * 32");
-  const uint32_t maxw = supported_maxw(std::max<uint32_t>(1, words_per_read));
-  if (!maxw) return set_err(ctx, "reads longer than 1024 bp are not supported");
+  // the slot width follows the longest read (words past it are zero)
+  const uint32_t maxw = slot_maxw(std::max<uint32_t>(1, (mx + 31) / 32));
+  if (!maxw) return set_err(ctx, "read longer than 65535 (Read::getReadLength is UINT16)");
   ctx->n = n_reads;
   ctx->maxw = maxw;
-  ctx->stride = slot_words((int)maxw);
+  ctx->stride = slot_stride(maxw);
   const size_t nw = (size_t)(n_reads + 2) * ctx->stride + 2;  // zero pad for over-reads
   MG_TRY(ensure(&ctx->d_words, &ctx->words_cap, nw));
   MG_TRY(ensure(&ctx->d_len, &ctx->len_cap, n_reads + 1));
   MG_TRY(hipMemsetAsync(ctx->d_words, 0, nw * sizeof(uint64_t), ctx->stream));
+  const uint32_t copy_w = std::min<uint32_t>(words_per_read, ctx->stride);
   if (n_reads && ctx->stride == words_per_read) {
     MG_TRY(hipMemcpyAsync(ctx->d_words, words, n_reads * ctx->stride * sizeof(uint64_t), hipMemcpyHostToDevice,
                           ctx->stream));
   } else if (n_reads) {
     MG_TRY(hipMemcpy2DAsync(ctx->d_words, ctx->stride * sizeof(uint64_t), words, words_per_read * sizeof(uint64_t),
-                            words_per_read * sizeof(uint64_t), n_reads, hipMemcpyHostToDevice, ctx->stream));
+                            copy_w * sizeof(uint64_t), n_reads, hipMemcpyHostToDevice, ctx->stream));
   }
   if (n_reads)
     MG_TRY(hipMemcpyAsync(ctx->d_len, lens, n_reads * sizeof(uint16_t), hipMemcpyHostToDevice, ctx->stream));
@@ -3328,11 +3565,10 @@ int mg_upload_reads_ascii(mg_ctx* ctx, const char* concat, const uint64_t* offse
     lens[i] = (uint16_t)L;
     mx = std::max(mx, L);
   }
-  const uint32_t maxw = supported_maxw((uint32_t)std::max<uint64_t>(1, (mx + 31) / 32));
-  if (!maxw) return set_err(ctx, "reads longer than 1024 bp are not supported");
+  const uint32_t maxw = slot_maxw((uint32_t)std::max<uint64_t>(1, (mx + 31) / 32));
   ctx->n = n_reads;
   ctx->maxw = maxw;
-  ctx->stride = slot_words((int)maxw);
+  ctx->stride = slot_stride(maxw);
   const uint64_t total = n_reads ? offsets[n_reads] : 0;
   // staging buffers freed on every exit path (an error return included)
   struct Staging {
@@ -4087,7 +4323,7 @@ int probe_join(mg_ctx* ctx, bool contain) {
 int ensure_cells(mg_ctx* ctx) {
   if (ctx->cells_ready) return 0;
   if (setup_cells(ctx)) return -1;
-  if (ctx->n && dispatch_w<LaunchIndex>(ctx->maxw, ctx)) return set_err(ctx, "cell index launch failed");
+  if (ctx->n && launch_index(ctx)) return set_err(ctx, "cell index launch failed");
   ctx->cells_ready = true;
   return 0;
 }
@@ -4098,7 +4334,7 @@ int ensure_cells(mg_ctx* ctx) {
 // scratch (keys, the old slots) is freed before returning.
 int apply_layout(mg_ctx* ctx) {
   ctx->t.layout_ms = 0.f;
-  if (!ctx->layout || ctx->n < 2) {  // ID order
+  if (!ctx->layout || ctx->n < 2 || long_mode(ctx)) {  // ID order (long reads: always)
     if (ctx->d_id) (void)hipFree(ctx->d_id);
     if (ctx->d_phys) (void)hipFree(ctx->d_phys);
     ctx->d_id = ctx->d_phys = nullptr;
@@ -4191,6 +4427,21 @@ int mg_build_index(mg_ctx* ctx, uint32_t min_overlap, uint32_t seed_k) {
   MG_TRY(hipSetDevice(ctx->device));
   MG_TRY(hipEventRecord(ctx->ev[0], ctx->stream));
   if (setup_index(ctx, min_overlap, seed_k, false)) return -1;
+  if (long_mode(ctx)) {  // reads > 1024 bp: k_index_long, one thread per key
+    if (ctx->nranks > 1) return set_err(ctx, "reads longer than 1024 bp: bucket-sharded index not supported");
+    if (setup_cells(ctx)) return -1;
+    ctx->scan_state = 0;
+    ctx->sorted_state = 0;
+    ctx->t.sort_ms = 0.f;
+    if (launch_index(ctx)) return set_err(ctx, "index build launch failed");
+    MG_TRY(hipEventRecord(ctx->ev[1], ctx->stream));
+    MG_TRY(hipEventSynchronize(ctx->ev[1]));
+    ctx->t.index_ms = elapsed(ctx->ev[0], ctx->ev[1]);
+    ctx->shared_scan_ms = 0.f;
+    ctx->index_ready = true;
+    ctx->cells_ready = true;
+    return 0;
+  }
   const bool join = join_geometry(ctx);
   if (!join && setup_cells(ctx)) return -1;
   ctx->scan_state = 0;
@@ -4266,11 +4517,17 @@ int mg_mark_contained(mg_ctx* ctx, uint32_t* super_out) {
     ctx->superkey = ctx->d_superkey;
     MG_TRY(hipMemsetAsync(ctx->d_superkey, 0, (ctx->n + 1) * sizeof(unsigned long long), ctx->stream));
     MG_TRY(hipMemsetAsync(ctx->d_any, 0, sizeof(unsigned int), ctx->stream));
+    if (ctx->stats) {  // containment work counters (mg_counters c_*)
+      if (!ctx->d_stats) MG_TRY(hipMalloc(&ctx->d_stats, (kSegs * 4 + 1) * sizeof(unsigned long long)));
+      MG_TRY(hipMemsetAsync(ctx->d_stats, 0, (kSegs * 4 + 1) * sizeof(unsigned long long), ctx->stream));
+    }
     MG_TRY(hipEventRecord(ctx->ev[2], ctx->stream));
     // sharded contexts still need the full superReadID vector: run over all
     // buckets (the containment pass is small, only for mixed lengths)
     if (ctx->nranks > 1) return set_err(ctx, "containment with a bucket-sharded index: use the exchange mode");
-    if (ctx->join_ready) {  // the join's prefix queries cover offset-0 containments
+    if (long_mode(ctx)) {
+      if (long_probe(ctx, true, 0, ctx->n)) return -1;
+    } else if (ctx->join_ready) {  // the join's prefix queries cover offset-0 containments
       if (probe_join(ctx, true)) return -1;
     } else {
       if (!shared_scan(ctx)) ctx->key0_ready = false;  // only the shared scan writes the o = 0 keys
@@ -4288,6 +4545,17 @@ int mg_mark_contained(mg_ctx* ctx, uint32_t* super_out) {
     MG_TRY(hipStreamSynchronize(ctx->stream));
     ctx->t.contained_ms = elapsed(ctx->ev[2], ctx->ev[3]);
     ctx->super_any = any != 0;
+    if (ctx->stats) {
+      std::vector<unsigned long long> st(kSegs * 4 + 1);
+      MG_TRY(hipMemcpy(st.data(), ctx->d_stats, st.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+      uint64_t acc[4] = {0, 0, 0, 0};
+      for (int s2 = 0; s2 < kSegs; ++s2)
+        for (int i = 0; i < 4; ++i) acc[i] += st[s2 * 4 + i];
+      ctx->counters.c_runs = acc[0];
+      ctx->counters.c_entries = acc[1];
+      ctx->counters.c_verified = acc[2];
+      ctx->counters.c_contained = acc[3];
+    }
   } else {
     MG_TRY(hipMemsetAsync(ctx->d_super, 0, (ctx->n + 1) * sizeof(uint32_t), ctx->stream));
     ctx->super_any = false;
@@ -4312,6 +4580,21 @@ int mg_find_overlaps(mg_ctx* ctx, uint64_t* n_rows) {
                         std::min(ctx->read_lo, ctx->n);
   if (ensure_rows(ctx, nsrc)) return -1;
   MG_TRY(hipEventRecord(ctx->ev[4], ctx->stream));
+  if (long_mode(ctx)) {
+    const uint64_t lo = std::min(ctx->read_lo, ctx->n), hi = ctx->read_hi ? std::min(ctx->read_hi, ctx->n) : ctx->n;
+    if (long_probe(ctx, false, lo, hi)) return -1;
+    MG_TRY(hipEventRecord(ctx->ev[5], ctx->stream));
+    MG_TRY(hipEventSynchronize(ctx->ev[5]));
+    ctx->t.scan_ms = 0.f;
+    ctx->t.sort_ms = 0.f;
+    ctx->t.verify_ms = 0.f;
+    ctx->t.probe_ms = elapsed(ctx->ev[8], ctx->ev[9]);
+    ctx->t.overlap_ms = ctx->t.probe_ms;
+    ctx->t.total_ms = ctx->t.index_ms + ctx->t.contained_ms + ctx->t.overlap_ms;
+    read_stats(ctx, nsrc);
+    if (n_rows) *n_rows = ctx->n_rows;
+    return 0;
+  }
   if (ctx->join_ready ? probe_join(ctx, false) : shared_scan(ctx) ? probe_shared(ctx, false) : run_discover(ctx, false))
     return -1;
   MG_TRY(hipEventRecord(ctx->ev[5], ctx->stream));
@@ -4364,6 +4647,7 @@ int mg_xchg_begin(mg_ctx* ctx, uint32_t min_overlap, uint32_t seed_k) {
   if (!ctx) return -1;
   MG_TRY(hipSetDevice(ctx->device));
   if (ctx->nranks > (uint32_t)kMaxRanks) return set_err(ctx, "at most 64 ranks");
+  if (long_mode(ctx)) return set_err(ctx, "reads longer than 1024 bp: exchange mode not supported (use the replicated mode)");
   MG_TRY(hipEventRecord(ctx->ev[0], ctx->stream));
   if (setup_index(ctx, min_overlap, seed_k)) return -1;  // this rank's (cleared) cells
   ctx->join_P = 0;
@@ -4630,7 +4914,7 @@ int mg_lookup_key(mg_ctx* ctx, const char* key, uint32_t key_len, uint64_t* out,
   MG_TRY(hipMalloc(&dn, sizeof(unsigned int)));
   MG_TRY(hipMemcpyAsync(dq, q.data(), (qwords + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, ctx->stream));
   MG_TRY(hipMemsetAsync(dn, 0, sizeof(unsigned int), ctx->stream));
-  if (dispatch_w<LaunchLookup>(ctx->maxw, ctx, dq, qwords, dout, dcap, dn)) return set_err(ctx, "lookup failed");
+  if (launch_lookup(ctx, dq, qwords, dout, dcap, dn)) return set_err(ctx, "lookup failed");
   unsigned int n = 0;
   MG_TRY(hipMemcpyAsync(&n, dn, sizeof(n), hipMemcpyDeviceToHost, ctx->stream));
   MG_TRY(hipStreamSynchronize(ctx->stream));

@@ -12,7 +12,7 @@ GOLDEN = os.path.join(ROOT, "tests", "golden")
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "oracle"))
 
-FIXTURES = ["small", "mixed", "highdup", "tandem", "tworead", "dirty", "wrapped", "branchy"]
+FIXTURES = ["small", "mixed", "highdup", "tandem", "tworead", "dirty", "wrapped", "branchy", "longreads"]
 
 
 def pytest_configure(config):

@@ -29,7 +29,7 @@ Only runs in the build container (the reference is not on the GPU box).
                          Dataset's unique reads (ref_harness dataset): the record
                          splitting quirks of Dataset.cpp:110-193
 
-Usage: python tests/golden/make_golden.py [--big] | --bfs | --branchy | --unitig | --parse
+Usage: python tests/golden/make_golden.py [--big] | --bfs | --branchy | --unitig | --parse | --long
 """
 from __future__ import annotations
 
@@ -170,10 +170,10 @@ def run_bfs(path: str, l: int):
     return int(nodes), int(edges), rows
 
 
-def add_bfs():
-    """Attach the reference's post-exploration graph to every fixture."""
+def add_bfs(only=None):
+    """Attach the reference's post-exploration graph to every fixture (or `only`)."""
     for fn in sorted(os.listdir(HERE)):
-        if not fn.endswith(".json"):
+        if not fn.endswith(".json") or (only and fn != only + ".json"):
             continue
         with open(os.path.join(HERE, fn)) as f:
             meta = json.load(f)
@@ -215,10 +215,10 @@ def run_unitig(path: str, l: int):
     return head, "".join(lists), unitig
 
 
-def add_unitig():
-    """Attach the reference's contracted graph and .unitig file to every fixture."""
+def add_unitig(only=None):
+    """Attach the reference's contracted graph and .unitig file to every fixture (or `only`)."""
     for fn in sorted(os.listdir(HERE)):
-        if not fn.endswith(".json"):
+        if not fn.endswith(".json") or (only and fn != only + ".json"):
             continue
         with open(os.path.join(HERE, fn)) as f:
             meta = json.load(f)
@@ -288,6 +288,31 @@ def branchy():
     emit("branchy", out, 40, lookups=True)
 
 
+def longreads():
+    """Reads longer than 1,024 bp (Read::getReadLength is UINT16, Read.h:62):
+    mostly 2.5-4.2 kb (some 1.1-9 kb) reads of a 60 kb genome, both strands, with 150 bp reads, exact
+    prefixes of long reads (offset-0 containment) and a tandem stretch, l = 60."""
+    rng = np.random.default_rng(91)
+    G = synth.codes_to_strings(synth.random_genome(60000, 92)[None, :], np.array([60000]))[0]
+    G = G[:30000] + "ACGTTGCAAGGCTTACGATCGATTACGG" * 50 + G[30000:]
+    n = len(G)
+    out = []
+    for _ in range(140):
+        L = int(rng.integers(2500, 4200)) if rng.random() < 0.9 else int(rng.integers(1100, 9000))
+        p = int(rng.integers(0, n - L))
+        r = G[p:p + L]
+        out.append(synth.revcomp_str(r) if rng.random() < 0.5 else r)
+        if rng.random() < 0.15:
+            out.append(r[:int(rng.integers(200, 1000))])
+    for _ in range(150):
+        p = int(rng.integers(0, n - 150))
+        r = G[p:p + 150]
+        out.append(synth.revcomp_str(r) if rng.random() < 0.5 else r)
+    emit("longreads", out, 60, lookups=True)
+    add_bfs("longreads")
+    add_unitig("longreads")
+
+
 PARSE_CASES = [
     # name, ext, l, text
     ("fasta_basic", ".fa", 10, ">a\nACGTACGTACGTAC\n>b desc\nTTTTGGGGCCCCAAAT\n"),
@@ -348,6 +373,9 @@ def main():
         return
     if "--branchy" in sys.argv:
         branchy()
+        return
+    if "--long" in sys.argv:
+        longreads()
         return
     big = "--big" in sys.argv
     # 1. fixed-length uniform set (SURVEY §0 "small")
