@@ -211,11 +211,13 @@ def load_pmc(path):
     tr = d.get("traffic", {})
     step = ("k_index_build", "k_scan", "k_probe")
     if any("dispatches" in v for v in tr.values()):
-        # every dispatch of the step's kernels (the bucket sort's rocprim passes
-        # included) over the number of step passes (one k_scan each)
+        # every dispatch of the step's kernels over the number of step passes
+        # (one k_scan each); the default step has no run sort since the
+        # clustered slot layout (the rocprim passes in the trace are the
+        # upload's layout sort, outside the step)
         passes = sum(v.get("dispatches", 0) for k, v in tr.items() if k.startswith("k_scan")) or 1
         tot = sum(v["traffic_bytes_per_launch"] * v.get("dispatches", 1) for k, v in tr.items()
-                  if k.startswith(step) or "radix_sort_onesweep" in k) / passes
+                  if k.startswith(step)) / passes
     else:
         tot = sum(v["traffic_bytes_per_launch"] for k, v in tr.items() if k.startswith(step))
     return tot or None
