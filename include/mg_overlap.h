@@ -254,8 +254,9 @@ int mg_get_counters(const mg_ctx* ctx, mg_counters* c);
  * 0 = separate index build and a scan per probe pass; source-range shards
  * with the whole index, bench --multi replicated, use 0),
  * "sort_runs" (1 = the shared scan's runs are radix-sorted by bucket before
- * the probes, so cell and partner loads coalesce (default); 0 = the probe
- * walks the scan's per-wavefront run regions),
+ * the probes, so cell and partner loads coalesce; 0 = the probe walks the
+ * scan's per-wavefront run regions in read order (default: the clustered
+ * slot layout, option "layout" = 1, gives it the same locality)),
  * "pack_runs" (1 = 12-byte sort records when the field widths fit (default);
  * 0 = 16-byte records),
  * "sorted_index" (1 = k_scan<INDEX> writes the key records, a bucket sort

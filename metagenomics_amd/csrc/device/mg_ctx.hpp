@@ -164,6 +164,8 @@ struct mg_ctx {
   size_t key0_cap = 0;
   bool key0_ready = false;
   bool prefix_contain = true;  // option "prefix_contain"
+  bool contain_jcut = true;    // option "contain_jcut": containment probe drops runs with jlo > n1 - minlen (C5: 60 -> 47 ms)
+  bool contain_prune = true;   // option "contain_prune": skip candidates that cannot raise the superkey (C5: 388M -> 110M compares)
   uint32_t* d_kb[2] = {nullptr, nullptr};
   uint64_t* d_ke[2] = {nullptr, nullptr};
   size_t kb_cap = 0, ke_cap = 0, kb1_cap = 0, ke1_cap = 0;

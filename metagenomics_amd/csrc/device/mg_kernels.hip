@@ -206,8 +206,24 @@ __device__ __forceinline__ uint64_t key_minimizer(const uint64_t* f, int n, int 
   return mix64(bmm);
 }
 
-// Next cell of a chain inside the rank's local range (wraps at its end).
-__device__ __forceinline__ uint64_t next_cell(uint64_t c, uint64_t n) { return c + 1 == n ? 0 : c + 1; }
+// Next cell of a chain inside the rank's local range (wraps at its end).  The
+// step is odd and depends on the entry's fingerprint (double hashing): with a
+// step of 1 (linear probing) the overflow of one heavy minimizer (a high-
+// abundance genome's m-mer in hundreds of keys) filled the neighbouring home
+// cells, and every run of those buckets walked the whole merged cluster (C5:
+// 16 entries scanned per containment run at 3.7 % fingerprint hits).  A step
+// of 1 + 2 (fp mod 1024) keeps other minimizers' chains out of the cluster;
+// an odd step visits every cell of a power-of-two table.  A rank's range of a
+// bucket-sharded table (exchange mode) need not be a power of two, and a step
+// sharing a factor with it would cycle through a fraction of the cells, so
+// those ranges keep the step of 1.  Insertion and every walk (probe, lookup,
+// prefix containment) use the same sequence.
+__device__ __forceinline__ uint64_t next_cell(uint64_t c, uint64_t n, uint32_t fp) {
+  const uint64_t x = c + ((n & (n - 1)) ? 1 : 1 + 2 * (uint64_t)(fp & 1023u));
+  return x >= n ? x % n : x;
+}
+// the fingerprint an entry was filed with (make_entry: hi32 = fp19 << 12 | q10 << 2 | o2)
+__device__ __forceinline__ uint32_t entry_fp(unsigned long long e) { return (uint32_t)(e >> 44) & ((1u << 19) - 1); }
 
 // Index entry: lo32 = read index, hi32 = fp19 << 12 | q10 << 2 | o2 (the chain
 // bit, bit 63, is set on a full cell's last slot).
@@ -238,7 +254,7 @@ __device__ __forceinline__ void cell_insert(uint64_t* cells, uint64_t c, uint64_
     if (done) return;
     // every slot is filled now: flag the chain (slot 7 holds an entry)
     if (e[kCell - 1] == kEmpty || !(e[kCell - 1] & kChain)) atomicOr(&cell[kCell - 1], (unsigned long long)kChain);
-    c = next_cell(c, cell_n);
+    c = next_cell(c, cell_n, entry_fp(entry));
   }
 }
 
@@ -356,7 +372,7 @@ __global__ __launch_bounds__(kBlock) void k_prefix_contain(const uint64_t* __res
       if (!diff) atomicMax(&superkey[r2], ((unsigned long long)n1 << 32) | (0xFFFFFFFFu - rid(id, (uint32_t)a)));
     }
     if (e[kCell - 1] == kEmpty || !(e[kCell - 1] & kChain)) break;
-    c = next_cell(c, cell_n);
+    c = next_cell(c, cell_n, fp);
   }
 }
 
@@ -1275,6 +1291,8 @@ struct ProbeParams {
   int phase_limit;                // diagnostics: 4 no probe, 5 + cell loads, 6 + filter, 7 full
   int halving_low;                // option "halving" = 1: keep o=2/3 pairs at the lower ID (else rc_side_keeps)
   int contain_even;               // CONTAIN: drop o = 1/3 hits (k_prefix_contain finds the s = 0 containments)
+  int contain_minlen;             // CONTAIN (with contain_even): drop runs whose first window jlo > n1 - minlen
+  int contain_prune;              // CONTAIN: skip a candidate whose container cannot raise the superkey
   // split path (k_probe<SPLIT=true> + k_verify): candidates {partner, source, o << 30 | j}
   uint3* cand;                    // one region of cand_cap records per probe wavefront
   unsigned long long* cand_cnt;   // [waves] candidates written (may exceed cand_cap)
@@ -1322,8 +1340,13 @@ struct ProbeLds {
 // (ballot + mbcnt per slot) and are verified one per lane against the
 // partner's slot in HBM; a full cell's chain flag turns the lane's item into a
 // pending item (LDS) that a later batch probes at the next cell.
+// MG_PROBE_WAVES: minimum waves per SIMD asked of the register allocator
+// (1 = its own choice; A/B builds, tools/ab_libs.sh)
+#ifndef MG_PROBE_WAVES
+#define MG_PROBE_WAVES 1
+#endif
 template <int MAXW, bool CONTAIN, bool SPLIT>
-__global__ __launch_bounds__(kBlock) void k_probe(ProbeParams p) {
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MG_PROBE_WAVES))) void k_probe(ProbeParams p) {
   using PL = ProbeLds<MAXW>;
   extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -1396,6 +1419,14 @@ __global__ __launch_bounds__(kBlock) void k_probe(ProbeParams p) {
     // partner slot first (the long-latency random load: its words in 16-B
     // pieces of one aligned line) and both reference IDs, then stage the source
     uint32_t ida = sa, idb = bid;
+    if (CONTAIN && p.contain_prune && cond) {
+      // atomicMax(len << 32 | ~id) would be a no-op when the partner already
+      // holds a key >= this container's: skip the slot load and the compare
+      // (keys only grow, so a stale view only prunes less)
+      const uint32_t ia = p.id ? p.id[sa] : sa;
+      const unsigned long long want = ((unsigned long long)n1 << 32) | (0xFFFFFFFFu - ia);
+      cond = __hip_atomic_load(&p.superkey[bid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want;
+    }
     if (cond) {
       load_slot<MAXW>(p.words, bid, y);
       if (p.id) {
@@ -1523,6 +1554,13 @@ __global__ __launch_bounds__(kBlock) void k_probe(ProbeParams p) {
         const uint32_t ra = (uint32_t)meta;
         if ((p.src_super && p.src_super[ra]) || (p.src_hi && (ra < p.src_lo || ra >= p.src_hi))) valid = false;
       }
+      // containment: read2 sits at s = j <= n1 - n2 <= n1 - minlen, so a run
+      // whose first window lies beyond that finds nothing (o = 1/3, the s = 0
+      // side, is k_prefix_contain's when contain_even)
+      if (CONTAIN && p.contain_minlen && valid) {
+        const int n1 = p.uniform_len ? p.uniform_len : (int)p.len[(uint32_t)meta];
+        if ((int)((meta >> 42) & 1023u) > n1 - p.contain_minlen) valid = false;
+      }
       key = (valid ? bucket - p.cell_lo : 0) | ((uint64_t)fpv << 32);
       if (valid) ++st_runs;
       rpos += kWave;
@@ -1566,7 +1604,7 @@ __global__ __launch_bounds__(kBlock) void k_probe(ProbeParams p) {
     const uint64_t cb = __ballot(chain);
     if (chain) {
       const uint32_t at = npend + lane_prefix(cb);
-      s_pk[at] = next_cell(key & 0xFFFFFFFFull, p.cell_n) | (key & 0xFFFFFFFF00000000ull);
+      s_pk[at] = next_cell(key & 0xFFFFFFFFull, p.cell_n, fp) | (key & 0xFFFFFFFF00000000ull);
       s_pm[at] = meta;
     }
     npend += (uint32_t)__popcll(cb);
@@ -2592,7 +2630,7 @@ __global__ __launch_bounds__(kBlock) void k_lookup_key(IndexParams p, const uint
       }
     }
     if (last == kEmpty || !(last & kChain)) break;
-    b = next_cell(b, p.cell_n);
+    b = next_cell(b, p.cell_n, fp);
   }
 }
 
@@ -2763,7 +2801,7 @@ __global__ __launch_bounds__(kBlock) void k_probe_long(LongParams p) {
         }
         const uint64_t last = cell[kCell - 1];
         if (last == kEmpty || !(last & kChain)) break;
-        c = next_cell(c, p.cell_n);
+        c = next_cell(c, p.cell_n, fp);
       }
     }
   }
@@ -3214,6 +3252,8 @@ struct LaunchProbe {
     pp.phase_limit = contain ? 99 : ctx->phase_limit;
     pp.halving_low = ctx->halving_low ? 1 : 0;
     pp.contain_even = (contain && ctx->key0_ready) ? 1 : 0;
+    pp.contain_minlen = (pp.contain_even && ctx->contain_jcut) ? (int)ctx->minlen : 0;
+    pp.contain_prune = (contain && ctx->contain_prune) ? 1 : 0;
     pp.xcd_map = xcd_map;
     pp.id = ctx->d_id;
     if (ctx->split) return run_split(ctx, contain, pp, grid, total_runs);
@@ -3693,6 +3733,14 @@ int mg_set_option(mg_ctx* ctx, const char* name, int64_t value) {
   if (!strcmp(name, "sort_runs")) {
     ctx->sort_runs = value != 0;
     ctx->sorted_state = 0;
+    return 0;
+  }
+  if (!strcmp(name, "contain_jcut")) {  // 1: the containment probe drops runs past j = n1 - minlen
+    ctx->contain_jcut = value != 0;
+    return 0;
+  }
+  if (!strcmp(name, "contain_prune")) {  // 1: skip candidates whose container cannot raise the superkey
+    ctx->contain_prune = value != 0;
     return 0;
   }
   if (!strcmp(name, "prefix_contain")) {  // 1 (default): k_prefix_contain + even-o containment probe

@@ -2,7 +2,7 @@
 cd $GRAFT_REPO_ROOT
 O=gpurun_out/${1:-r02ch}
 mkdir -p $O
-timeout -k 10 900 python -u -m pytest tests -x -q -m gpu --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1
+timeout -k 10 900 python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1
 rc=$?; echo "tests rc=$rc"; tail -4 $O/gpu_tests.log; [ $rc -ne 0 ] && exit $rc
 for cfg in c3 c5; do
   timeout -k 10 400 python -u bench.py --config $cfg --steps 3 --no-cpu-baseline --no-ingest > $O/$cfg.json 2> $O/$cfg.err
