@@ -199,6 +199,10 @@ def parity_digest(engines, last, mode, dist, config):
     return out
 
 
+# rocprofv3 --pmc summaries (tools/pmc_summary.py) of the default step, newest first
+PMC_FILES = {"c3": ["r02s3_pmc_c3.json", "r02s2_pmc_c3.json"], "c5": ["r02s3_pmc_c5.json"]}
+
+
 def load_pmc(path):
     """HBM traffic of one step from a committed rocprofv3 --pmc summary
     (tools/pmc_summary.py): (2 x FETCH_SIZE + WRITE_SIZE) summed over the step's
@@ -209,7 +213,7 @@ def load_pmc(path):
     except Exception:
         return None
     tr = d.get("traffic", {})
-    step = ("k_index_build", "k_scan", "k_probe")
+    step = ("k_index_build", "k_scan", "k_probe", "k_prefix_contain", "k_super_finalize")
     if any("dispatches" in v for v in tr.values()):
         # every dispatch of the step's kernels over the number of step passes
         # (one k_scan each); the default step has no run sort since the
@@ -244,7 +248,8 @@ def main():
     ap.add_argument("--no-ingest", action="store_true", help="skip the device Dataset ingest measurement")
     ap.add_argument("--replay", action="store_true",
                     help="also time the host replay of the exploration + transitive reduction + contraction on the rows")
-    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r02s2_pmc_c3.json"))
+    ap.add_argument("--pmc", default=None,
+                    help="committed rocprofv3 --pmc summary for roofline.traffic (default: profiles/PMC_FILES[config])")
     ap.add_argument("--nb-log2", type=int, default=0)
     ap.add_argument("--split-probe", action="store_true", help="probe -> candidates -> verify kernels (option split = 1)")
     ap.add_argument("--sort-runs", type=int, default=None,
@@ -447,7 +452,9 @@ def main():
     roof = None
     if mode == "fused":
         achieved = alg / (kern_ms / 1000.0) / 1e9 if kern_ms > 0 else 0.0
-        traffic = load_pmc(args.pmc) if args.config == "c3" else None
+        pmc = args.pmc or next((os.path.join(ROOT, "profiles", f) for f in PMC_FILES.get(args.config, [])
+                                if os.path.exists(os.path.join(ROOT, "profiles", f))), None)
+        traffic = load_pmc(pmc) if pmc else None
         roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                 "kernel": ("step = k_scan<INDEX> (window scan + fused index build), "

@@ -82,7 +82,10 @@ int mg_device_count(void);
 /* --- reads (Dataset / Read) ---------------------------------------------- */
 /* Upload the Dataset's unique reads, already 2-bit packed (the host mirror of
  * Dataset packs while it canonicalises/sorts, Dataset.cpp:158-202,316-345).
- * lens[i] = Read::getReadLength() of read ID i+1 (Read.h:62). */
+ * lens[i] = Read::getReadLength() of read ID i+1 (Read.h:62).  Any length up to
+ * 65,535 (UINT16): reads up to 1,024 bp take the register-resident kernels,
+ * longer ones the long-read kernels (the exchange mode refuses
+ * them).  The same holds for every upload and ingest below. */
 int mg_upload_reads_packed(mg_ctx* ctx, const uint64_t* words, const uint16_t* lens, uint64_t n_reads,
                            uint32_t words_per_read);
 /* Upload reads as ASCII (upper-case ACGT only, already filtered by

@@ -1293,6 +1293,8 @@ struct ProbeParams {
   int contain_even;               // CONTAIN: drop o = 1/3 hits (k_prefix_contain finds the s = 0 containments)
   int contain_minlen;             // CONTAIN (with contain_even): drop runs whose first window jlo > n1 - minlen
   int contain_prune;              // CONTAIN: skip a candidate whose container cannot raise the superkey
+  int contain_skip;               // CONTAIN: skip runs of sources already contained (their superkey != 0)
+  int src_len_lo, src_len_hi;     // CONTAIN: only sources with length in [lo, hi) (hi = 0: all)
   // split path (k_probe<SPLIT=true> + k_verify): candidates {partner, source, o << 30 | j}
   uint3* cand;                    // one region of cand_cap records per probe wavefront
   unsigned long long* cand_cnt;   // [waves] candidates written (may exceed cand_cap)
@@ -1557,9 +1559,17 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MG_PROBE
       // containment: read2 sits at s = j <= n1 - n2 <= n1 - minlen, so a run
       // whose first window lies beyond that finds nothing (o = 1/3, the s = 0
       // side, is k_prefix_contain's when contain_even)
-      if (CONTAIN && p.contain_minlen && valid) {
-        const int n1 = p.uniform_len ? p.uniform_len : (int)p.len[(uint32_t)meta];
-        if ((int)((meta >> 42) & 1023u) > n1 - p.contain_minlen) valid = false;
+      if (CONTAIN && valid && (p.contain_minlen || p.src_len_hi || p.contain_skip)) {
+        const uint32_t ra = (uint32_t)meta;
+        const int n1 = p.uniform_len ? p.uniform_len : (int)p.len[ra];
+        if (p.contain_minlen && (int)((meta >> 42) & 1023u) > n1 - p.contain_minlen) valid = false;
+        if (p.src_len_hi && (n1 < p.src_len_lo || n1 >= p.src_len_hi)) valid = false;
+        // a source that is itself contained (in a longer read C) never holds
+        // a partner's final superReadID: every read2 it contains is also in
+        // C, which is longer, and the longest container is never contained
+        if (p.contain_skip && valid &&
+            __hip_atomic_load(&p.superkey[ra], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0)
+          valid = false;
       }
       key = (valid ? bucket - p.cell_lo : 0) | ((uint64_t)fpv << 32);
       if (valid) ++st_runs;
@@ -3254,6 +3264,9 @@ struct LaunchProbe {
     pp.contain_even = (contain && ctx->key0_ready) ? 1 : 0;
     pp.contain_minlen = (pp.contain_even && ctx->contain_jcut) ? (int)ctx->minlen : 0;
     pp.contain_prune = (contain && ctx->contain_prune) ? 1 : 0;
+    pp.contain_skip = (contain && ctx->contain_skip) ? 1 : 0;
+    pp.src_len_lo = contain ? ctx->pass_len_lo : 0;
+    pp.src_len_hi = contain ? ctx->pass_len_hi : 0;
     pp.xcd_map = xcd_map;
     pp.id = ctx->d_id;
     if (ctx->split) return run_split(ctx, contain, pp, grid, total_runs);
@@ -3737,6 +3750,14 @@ int mg_set_option(mg_ctx* ctx, const char* name, int64_t value) {
   }
   if (!strcmp(name, "contain_jcut")) {  // 1: the containment probe drops runs past j = n1 - minlen
     ctx->contain_jcut = value != 0;
+    return 0;
+  }
+  if (!strcmp(name, "contain_skip")) {  // 1: the containment probe skips runs of already-contained sources
+    ctx->contain_skip = value != 0;
+    return 0;
+  }
+  if (!strcmp(name, "contain_passes")) {  // containment probe passes by source length, longest first
+    ctx->contain_passes = value < 1 ? 1 : value > 16 ? 16 : (int)value;
     return 0;
   }
   if (!strcmp(name, "contain_prune")) {  // 1: skip candidates whose container cannot raise the superkey
@@ -4579,9 +4600,23 @@ int mg_mark_contained(mg_ctx* ctx, uint32_t* super_out) {
       if (probe_join(ctx, true)) return -1;
     } else {
       if (!shared_scan(ctx)) ctx->key0_ready = false;  // only the shared scan writes the o = 0 keys
-      if (shared_scan(ctx) ? probe_shared(ctx, true) : run_discover(ctx, true)) return -1;
+      // prefix containments first: what they mark is skipped as a container
       if (ctx->key0_ready && dispatch_w<LaunchPrefixContain>(ctx->maxw, ctx))
         return set_err(ctx, "prefix containment launch failed");
+      // source-length passes, longest first (option contain_passes): with
+      // contain_skip, the sources the longer passes found contained probe nothing
+      const int passes = shared_scan(ctx) ? ctx->contain_passes : 1;
+      const uint32_t span = ctx->maxlen + 1 - ctx->minlen;
+      for (int k = 0; k < passes; ++k) {
+        ctx->pass_len_hi = passes > 1 ? (int)(ctx->maxlen + 1 - (uint64_t)span * k / passes) : 0;
+        ctx->pass_len_lo = passes > 1 ? (int)(ctx->maxlen + 1 - (uint64_t)span * (k + 1) / passes) : 0;
+        const int rc = shared_scan(ctx) ? probe_shared(ctx, true) : run_discover(ctx, true);
+        if (rc) {
+          ctx->pass_len_lo = ctx->pass_len_hi = 0;
+          return -1;
+        }
+      }
+      ctx->pass_len_lo = ctx->pass_len_hi = 0;
     }
     if (ctx->n)
       hipLaunchKernelGGL(k_super_finalize, dim3((uint32_t)((ctx->n + kBlock - 1) / kBlock)), dim3(kBlock), 0,

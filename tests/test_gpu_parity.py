@@ -666,6 +666,48 @@ def test_prefix_contain_off(name):
             assert {str(i): int(x) for i, x in enumerate(sup) if x} == want_sup, (join, flag)
 
 
+CONTAIN_OPTS = [
+    {"contain_jcut": 0, "contain_prune": 0, "contain_skip": 0},
+    {"contain_jcut": 1, "contain_prune": 0, "contain_skip": 0},
+    {"contain_jcut": 0, "contain_prune": 1, "contain_skip": 0},
+    {"contain_jcut": 0, "contain_prune": 0, "contain_skip": 1},
+    {"contain_skip": 1, "contain_passes": 3},
+    {"contain_skip": 1, "prefix_contain": 0},
+]
+
+
+@pytest.mark.parametrize("name", ["mixed", "dirty", "branchy", "longreads", "prefixes", "metagenome"])
+def test_containment_options(name):
+    """The containment cuts are pure pruning: runs past
+    j = n1 - minlen (contain_jcut), candidates that cannot raise the superkey
+    (contain_prune), runs of already-contained sources (contain_skip, also without
+    k_prefix_contain) and source-length passes (contain_passes): every combination
+    gives the same superReadIDs and rows."""
+    if name in ("prefixes", "metagenome"):
+        if name == "prefixes":
+            seqs, l = prefix_reads(), 40
+        else:
+            c, L = synth.metagenome_read_set(20000, 100, 250, n_genomes=20, total_len=400000, seed=51)
+            seqs, l = synth.codes_to_strings(c, L), 50
+        ds = Dataset.from_strings(seqs, l)
+        orows, osup, _, _ = OracleDataset.from_strings(seqs, l).overlaps(l)
+        want_rows, want_sup = sorted_tuples(orows), {str(i): int(x) for i, x in enumerate(osup) if x}
+    else:
+        meta = load_meta(name)
+        l = meta["l"]
+        ds = Dataset.from_files([fixture_input(name)], l)
+        want_rows, want_sup = golden_rows(name), meta["super"]
+    assert want_sup
+    for opts in CONTAIN_OPTS:
+        e = OverlapEngine(0)
+        for k, v in opts.items():
+            e.set_option(k, v)
+        rows, sup = gpu_rows(e, ds, l)
+        e.close()
+        assert {str(i): int(x) for i, x in enumerate(sup) if x} == want_sup, opts
+        assert np.array_equal(rows_to_tuples(rows), want_rows), opts
+
+
 @pytest.mark.parametrize("name", FIXTURES)
 def test_replicated_index_source_shards(name):
     """Multi-GPU replicated mode (bench --multi replicated): every rank builds

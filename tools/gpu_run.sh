@@ -98,6 +98,15 @@ for s in $STEPS; do
       rc=$?; echo "pmc $set rc=$rc"; [ $rc -ne 0 ] && break
     done
     [ $rc -eq 0 ] && python3 tools/pmc_summary.py $OUT/pmc_summary.json $OUT/pmc_* > /dev/null ;;
+  pmc5)
+    for set in "FETCH_SIZE" "WRITE_SIZE"; do
+      timeout -s KILL 400 rocprofv3 --pmc $set --kernel-trace --output-format csv -d $OUT/pmc5_$set -o p -- python3 bench.py --config c5 --steps 1 --warmup 0 --no-cpu-baseline --no-ingest > $OUT/pmc5_$set.log 2>&1
+      rc=$?; echo "pmc5 $set rc=$rc"; [ $rc -ne 0 ] && break
+    done
+    [ $rc -eq 0 ] && python3 tools/pmc_summary.py $OUT/pmc5_summary.json $OUT/pmc5_* > /dev/null ;;
+  prof5)
+    timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof5 -o kt -- python3 bench.py --config c5 --steps 2 --no-cpu-baseline --no-ingest > $OUT/prof5_bench.json 2> $OUT/prof5_bench.err
+    rc=$?; echo "prof5 rc=$rc"; head -10 $OUT/prof5/kt_kernel_stats.csv | cut -c1-160 ;;
   *) echo "unknown step $s"; rc=2 ;;
   esac
   if [ $rc -ne 0 ]; then tail -30 $OUT/*.err 2>/dev/null; exit $rc; fi
