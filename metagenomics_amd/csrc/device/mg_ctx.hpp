@@ -150,6 +150,9 @@ struct mg_ctx {
   bool xcd_map = true;        // probe: run regions dealt XCD by XCD (group regions, or sorted with probe_region)
   bool group_regions = false; // option "group_regions": one run region per read group of 64 (measured slower)
   bool group_active = false;  // the last scan wrote group regions
+  bool probe_share = true;     // option "probe_share": a discovery-probe block's 4 wavefronts share its regions
+  bool probe_compact = true;   // option "probe_compact": sparse run batches compacted in the probe (C5 probe 30.4 -> 26.8 ms)
+  bool xcd_plain = false;     // option "xcd_plain": xcd_map for the scan's per-wavefront regions too
   int sort_bits = 0;     // diagnostics: sort only the top sort_bits bucket bits (0: all)
   // sorted index build (option "sorted_index", default off): k_scan<INDEX> writes
   // the 4N key records (bucket, entry), a radix sort orders them by bucket and

@@ -1294,6 +1294,8 @@ struct ProbeParams {
   int contain_minlen;             // CONTAIN (with contain_even): drop runs whose first window jlo > n1 - minlen
   int contain_prune;              // CONTAIN: skip a candidate whose container cannot raise the superkey
   int contain_skip;               // CONTAIN: skip runs of sources already contained (their superkey != 0)
+  int compact;                    // park the live items of sparse run batches (filled batches only)
+  int share;                      // a block's wavefronts share its regions batch by batch (probe_share)
   int src_len_lo, src_len_hi;     // CONTAIN: only sources with length in [lo, hi) (hi = 0: all)
   // split path (k_probe<SPLIT=true> + k_verify): candidates {partner, source, o << 30 | j}
   uint3* cand;                    // one region of cand_cap records per probe wavefront
@@ -1500,18 +1502,28 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MG_PROBE
     rstride = wx;
     rlimit = hi;
   }
+  // share (option probe_share): the block's 4 wavefronts walk the SAME regions
+  // (4 b .. 4 b + 3, then + nwp, ...) and take every 4th batch of each, so a
+  // block probes one scan group of 64 neighbouring reads at a time and their
+  // shared cells and partner slots stay in its CU's L1 and its XCD's L2
+  const bool share = p.share && !p.xcd_map;
+  const uint64_t rstep = share ? (uint64_t)kWavesPerBlock * kWave : (uint64_t)kWave;
+  auto reg_of = [&](uint32_t r) -> uint64_t {
+    return share ? (uint64_t)(r >> 2) * nwp + (uint64_t)blockIdx.x * kWavesPerBlock + (r & 3u)
+                 : rfirst + (uint64_t)r * rstride;
+  };
   auto open_region = [&](uint32_t r) {
-    const uint64_t reg = rfirst + (uint64_t)r * rstride;
+    const uint64_t reg = reg_of(r);
     rbase = p.runs + (p.fkeys ? 0 : reg * p.run_cap);
     rbase_i = reg * p.run_cap;
     const uint64_t c = p.run_cnt[reg];
     rcnt = c < p.run_cap ? c : p.run_cap;
-    rpos = 0;
+    rpos = share ? (uint64_t)wv * kWave : 0;
   };
   // skip to the next non-empty batch position; false once the regions are exhausted
   auto hbm_settle = [&]() -> bool {
     while (rpos >= rcnt) {
-      if (rfirst + (uint64_t)(rg + 1) * rstride >= rlimit) return false;
+      if (reg_of(rg + 1) >= rlimit) return false;
       open_region(++rg);
     }
     return true;
@@ -1534,6 +1546,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MG_PROBE
   };
 
   auto take_item = [&](uint64_t& key, uint64_t& meta, bool& valid) -> bool {
+   while (true) {
     if (npend >= (uint32_t)kWave) {
       npend -= kWave;
       key = s_pk[npend + lane];
@@ -1573,8 +1586,26 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MG_PROBE
       }
       key = (valid ? bucket - p.cell_lo : 0) | ((uint64_t)fpv << 32);
       if (valid) ++st_runs;
-      rpos += kWave;
+      rpos += rstep;
       pf_any = hbm_settle();
+      if (p.compact && npend < (uint32_t)kWave) {
+        // a sparse batch (runs of contained sources dropped, containment cuts):
+        // park its live items with the pending ones and read on, so batches
+        // go out (nearly) full instead of two thirds empty (C5)
+        const uint64_t vb = __ballot(valid);
+        const uint32_t nv = (uint32_t)__popcll(vb);
+        if (nv < (uint32_t)(kWave * 3 / 4)) {
+          if (valid) {
+            const uint32_t at = npend + lane_prefix(vb);
+            s_pk[at] = key;
+            s_pm[at] = meta;
+          }
+          npend += nv;
+          wave_sync();
+          hbm_fetch();
+          continue;
+        }
+      }
       return true;
     }
     if (npend) {
@@ -1586,6 +1617,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MG_PROBE
     }
     valid = false;
     return false;
+   }
   };
   // unconditional loads (invalid lanes read cell 0 and discard it): with no
   // branch around them the compiler's vmcnt waits stay exact, so the next
@@ -1695,7 +1727,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MG_PROBE
     }
   };
 
-  if (p.phase_limit > 4 && rfirst < rlimit) {
+  if (p.phase_limit > 4 && reg_of(0) < rlimit) {
     open_region(0);
     pf_any = hbm_settle();
     hbm_fetch();
@@ -3265,6 +3297,10 @@ struct LaunchProbe {
     pp.contain_minlen = (pp.contain_even && ctx->contain_jcut) ? (int)ctx->minlen : 0;
     pp.contain_prune = (contain && ctx->contain_prune) ? 1 : 0;
     pp.contain_skip = (contain && ctx->contain_skip) ? 1 : 0;
+    pp.compact = ctx->probe_compact ? 1 : 0;
+    // shared regions help the discovery probe (C3 probe 4.56-4.57 vs 4.65-4.78 ms) but cost the
+    // containment probe (C5 35.0 vs 29.6 ms: contain_skip finds fewer containers marked in time)
+    pp.share = (!contain && ctx->probe_share) ? 1 : 0;
     pp.src_len_lo = contain ? ctx->pass_len_lo : 0;
     pp.src_len_hi = contain ? ctx->pass_len_hi : 0;
     pp.xcd_map = xcd_map;
@@ -3801,6 +3837,18 @@ int mg_set_option(mg_ctx* ctx, const char* name, int64_t value) {
     ctx->sorted_state = 0;
     return 0;
   }
+  if (!strcmp(name, "probe_share")) {  // 1: a probe block's wavefronts share its run regions batch by batch
+    ctx->probe_share = value != 0;
+    return 0;
+  }
+  if (!strcmp(name, "probe_compact")) {  // 1: sparse run batches are compacted through the pending list
+    ctx->probe_compact = value != 0;
+    return 0;
+  }
+  if (!strcmp(name, "xcd_plain")) {  // 1: the scan's own (wavefront) run regions dealt XCD by XCD too
+    ctx->xcd_plain = value != 0;
+    return 0;
+  }
   if (!strcmp(name, "xcd_map")) {  // probe regions dealt XCD by XCD (group regions; sorted runs with probe_region)
     ctx->xcd_map = value != 0;
     return 0;
@@ -4172,7 +4220,8 @@ struct LaunchProbeShared {
                                  (R && ctx->xcd_map) ? 1 : 0);
     }
     return LaunchProbe<W>::run(ctx, contain, ctx->d_runs, ctx->d_run_cnt, ctx->run_cap, ctx->nrun_reg, g.grid, total,
-                               sup, lo, hi, nullptr, nullptr, 0, 0, (ctx->group_active && ctx->xcd_map) ? 1 : 0);
+                               sup, lo, hi, nullptr, nullptr, 0, 0,
+                               ((ctx->group_active || ctx->xcd_plain) && ctx->xcd_map) ? 1 : 0);
   }
 };
 

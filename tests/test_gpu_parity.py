@@ -673,6 +673,9 @@ CONTAIN_OPTS = [
     {"contain_jcut": 0, "contain_prune": 0, "contain_skip": 1},
     {"contain_skip": 1, "contain_passes": 3},
     {"contain_skip": 1, "prefix_contain": 0},
+    {"probe_share": 0, "probe_compact": 0},
+    {"probe_share": 1, "probe_compact": 0},
+    {"probe_share": 0, "probe_compact": 1},
 ]
 
 
@@ -681,8 +684,9 @@ def test_containment_options(name):
     """The containment cuts are pure pruning: runs past
     j = n1 - minlen (contain_jcut), candidates that cannot raise the superkey
     (contain_prune), runs of already-contained sources (contain_skip, also without
-    k_prefix_contain) and source-length passes (contain_passes): every combination
-    gives the same superReadIDs and rows."""
+    k_prefix_contain) and source-length passes (contain_passes), and the probe's
+    batch compaction and block-shared regions (probe_compact, probe_share): every
+    combination gives the same superReadIDs and rows."""
     if name in ("prefixes", "metagenome"):
         if name == "prefixes":
             seqs, l = prefix_reads(), 40
