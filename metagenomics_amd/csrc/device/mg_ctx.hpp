@@ -48,6 +48,16 @@ struct mg_ctx {
   uint64_t* d_cells = nullptr;  // cells of kCell entries (this rank's bucket range)
   size_t cells_cap = 0;
   uint64_t cell_lo = 0, cell_n = 0;  // local bucket range [cell_lo, cell_lo + cell_n)
+  // ping-pong cell tables of the unsharded build (option "cell_pp", mg_kernels.hip setup_cells_pp)
+  bool cell_pp = false;  // measured slower: the side-stream fill slows the scan or the probe it overlaps
+  uint64_t* pp_buf[2] = {nullptr, nullptr};
+  size_t pp_cap = 0;
+  int pp_next = 0;
+  int pp_due = -1;  // table whose clear waits for this build's probe (-1: none)
+  bool pp_dirty[2] = {true, true}, pp_pending[2] = {false, false};
+  hipStream_t clear_stream = nullptr;
+  hipEvent_t ev_clear[2] = {nullptr, nullptr};
+  hipEvent_t ev_use = nullptr;
   // containment
   unsigned long long* d_superkey = nullptr;
   unsigned long long* superkey = nullptr;  // the containment key array in use (d_superkey or caller-owned)

@@ -666,6 +666,28 @@ def test_prefix_contain_off(name):
             assert {str(i): int(x) for i, x in enumerate(sup) if x} == want_sup, (join, flag)
 
 
+def test_cell_pingpong_rebuilds():
+    """option cell_pp: builds alternate between two cell tables, the
+    next one cleared on a side stream; repeated builds on one engine over data
+    sets of growing and shrinking table sizes (and nb_log2 changes) give the
+    golden rows every time."""
+    e = OverlapEngine(0)
+    e.set_option("cell_pp", 1)
+    seq = ["small", "highdup", "mixed", "mixed", "tworead", "branchy", "small", "tandem", "mixed"]
+    for i, name in enumerate(seq):
+        meta = load_meta(name)
+        ds = Dataset.from_files([fixture_input(name)], meta["l"])
+        rows, sup = gpu_rows(e, ds, meta["l"], nb_log2=(10 if i == 5 else 0))
+        assert np.array_equal(rows_to_tuples(rows), golden_rows(name)), (i, name)
+        assert {str(k): int(x) for k, x in enumerate(sup) if x} == meta["super"], (i, name)
+        # a second build on the same upload takes the other table
+        e.build_index(meta["l"], 0)
+        e.mark_contained()
+        rows2 = e.rows(e.find_overlaps())
+        assert np.array_equal(rows_to_tuples(rows2), golden_rows(name)), (i, name, "rebuild")
+    e.close()
+
+
 CONTAIN_OPTS = [
     {"contain_jcut": 0, "contain_prune": 0, "contain_skip": 0},
     {"contain_jcut": 1, "contain_prune": 0, "contain_skip": 0},
@@ -676,6 +698,7 @@ CONTAIN_OPTS = [
     {"probe_share": 0, "probe_compact": 0},
     {"probe_share": 1, "probe_compact": 0},
     {"probe_share": 0, "probe_compact": 1},
+    {"cell_pp": 1},
 ]
 
 
