@@ -1631,6 +1631,31 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MG_PROBE
       e[2 * s + 1] = valid ? x.y : kEmpty;
     }
   };
+  // verify the first 64 candidates and move the rest (< 128) to the front,
+  // while at least thr are listed (thr = 64: a full wavefront)
+  auto drain = [&](uint32_t thr) {
+    while (ncand >= thr) {
+      wave_sync();
+      if (p.phase_limit > 6) verify(kWave);
+      const uint32_t rest = ncand - kWave;  // < 128: move to the front
+      uint32_t mb0 = 0, mi0 = 0, ma0 = 0, mb1 = 0, mi1 = 0, ma1 = 0;
+      if ((uint32_t)lane < rest) {
+        mb0 = s_cb[kWave + lane]; mi0 = s_ci[kWave + lane]; ma0 = s_ca[kWave + lane];
+      }
+      if ((uint32_t)lane + kWave < rest) {
+        mb1 = s_cb[2 * kWave + lane]; mi1 = s_ci[2 * kWave + lane]; ma1 = s_ca[2 * kWave + lane];
+      }
+      wave_sync();
+      if ((uint32_t)lane < rest) {
+        s_cb[lane] = mb0; s_ci[lane] = mi0; s_ca[lane] = ma0;
+      }
+      if ((uint32_t)lane + kWave < rest) {
+        s_cb[kWave + lane] = mb1; s_ci[kWave + lane] = mi1; s_ca[kWave + lane] = ma1;
+      }
+      ncand = rest;
+      wave_sync();
+    }
+  };
   auto process = [&](uint64_t key, uint64_t meta, bool valid, const uint64_t* e) {
     const uint32_t ra = (uint32_t)meta;
     const int rp = (int)((meta >> 32) & 1023u);
@@ -1703,27 +1728,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MG_PROBE
           ncand += nb;
         }
       }
-      while (ncand >= (uint32_t)kWave) {
-        wave_sync();
-        if (p.phase_limit > 6) verify(kWave);
-        const uint32_t rest = ncand - kWave;  // < 128: move to the front
-        uint32_t mb0 = 0, mi0 = 0, ma0 = 0, mb1 = 0, mi1 = 0, ma1 = 0;
-        if ((uint32_t)lane < rest) {
-          mb0 = s_cb[kWave + lane]; mi0 = s_ci[kWave + lane]; ma0 = s_ca[kWave + lane];
-        }
-        if ((uint32_t)lane + kWave < rest) {
-          mb1 = s_cb[2 * kWave + lane]; mi1 = s_ci[2 * kWave + lane]; ma1 = s_ca[2 * kWave + lane];
-        }
-        wave_sync();
-        if ((uint32_t)lane < rest) {
-          s_cb[lane] = mb0; s_ci[lane] = mi0; s_ca[lane] = ma0;
-        }
-        if ((uint32_t)lane + kWave < rest) {
-          s_cb[kWave + lane] = mb1; s_ci[kWave + lane] = mi1; s_ca[kWave + lane] = ma1;
-        }
-        ncand = rest;
-        wave_sync();
-      }
+      drain(kWave);
     }
   };
 
