@@ -163,6 +163,7 @@ struct mg_ctx {
   bool probe_share = true;     // option "probe_share": a discovery-probe block's 4 wavefronts share its regions
   bool probe_compact = true;   // option "probe_compact": sparse run batches compacted in the probe (C5 probe 30.4 -> 26.8 ms)
   bool xcd_plain = false;     // option "xcd_plain": xcd_map for the scan's per-wavefront regions too
+  int xchg_sort_bits = 8;  // option "xchg_sort_bits": exchange mode (P a power of two) sorts runs on the top bits only
   int sort_bits = 0;     // diagnostics: sort only the top sort_bits bucket bits (0: all)
   // sorted index build (option "sorted_index", default off): k_scan<INDEX> writes
   // the 4N key records (bucket, entry), a radix sort orders them by bucket and
