@@ -112,6 +112,7 @@ struct mg_ctx {
   int scan_state = 0;        // 0 none, 1 launched (not settled), 2 settled
   bool overlap_scan = true;  // option "overlap_scan" (0: separate index build, a scan per probe pass)
   bool scan_reg = true;      // option "scan_reg": register sliding minimum (k_scan_reg) for the run scans when w <= 32
+  bool reg_cas = false;      // option "reg_cas": k_scan_reg<INDEX> CAS-inserts all four keys itself (no key records)
   bool reg_index = false;    // option "reg_index": also for the cell index build (key records + k_insert_dense)
   // partitioned join (option "join", default): keys + runs as sorted join
   // records, per-partition LDS tables (k_join); cells only on demand (lookups)

@@ -1147,6 +1147,36 @@ __global__ __launch_bounds__(kBlock) void k_scan_reg(ScanParams p) {
           p.join_kv[4 * a] = e0;
           p.join_kk[4 * a + 1] = k1;
           p.join_kv[4 * a + 1] = e1;
+        } else if (!p.key_bk) {  // option reg_cas: all four keys CAS-inserted here (no records, no k_rc_keys)
+          if (n) {
+            const uint64_t nbm = (1ULL << p.nb_log2) - 1;
+            const uint64_t v0 = mix64(funnel(rw[0], rw[1], p0 << 1) >> msh);
+            const uint64_t v1 = mix64(ext_reg<MAXW>(rw, p1) >> msh);
+            // the reverse strand's keys o = 3 / 2 (k_rc_keys' rolled pass, from registers)
+            uint32_t kb3 = 0xFFFFFFFFu, kb2 = 0xFFFFFFFFu;
+            uint64_t mb3 = 0, mb2 = 0;
+            const uint64_t Aw = ext_reg<MAXW>(rw, n - h);
+            uint64_t r3 = rc_word(funnel(rw[0], rw[1], 2 * (w - 1))) & mmask;
+            uint64_t r2 = rc_word(ext_reg<MAXW>(rw, n - m)) & mmask;
+            for (int i = 0; i < w; ++i) {
+              const uint32_t k3 = order_key(r3) | (uint32_t)i, k2 = order_key(r2) | (uint32_t)i;
+              if (k3 < kb3) { kb3 = k3; mb3 = r3; }
+              if (k2 < kb2) { kb2 = k2; mb2 = r2; }
+              const int t3 = w - 2 - i;
+              if (t3 >= 0) {
+                r3 = ((r3 << 2) | (3u - ((rw[0] >> (62 - 2 * t3)) & 3u))) & mmask;
+                r2 = ((r2 << 2) | (3u - ((Aw >> (62 - 2 * t3)) & 3u))) & mmask;
+              }
+            }
+            const uint64_t v2 = mix64(mb2), v3 = mix64(mb3);
+            if (p.key0) p.key0[a] = (v0 & ((1ULL << 50) - 1)) | ((uint64_t)p0 << 54);
+            cell_insert(p.cells, v0 & nbm, p.cell_n, make_entry(v0, p.nb_log2, p0, 0, (uint32_t)a));
+            cell_insert(p.cells, v1 & nbm, p.cell_n, make_entry(v1, p.nb_log2, p1 - (n - h), 1, (uint32_t)a));
+            cell_insert(p.cells, v2 & nbm, p.cell_n, make_entry(v2, p.nb_log2, (int)(kb2 & 1023u), 2, (uint32_t)a));
+            cell_insert(p.cells, v3 & nbm, p.cell_n, make_entry(v3, p.nb_log2, (int)(kb3 & 1023u), 3, (uint32_t)a));
+          } else if (p.key0) {
+            p.key0[a] = kEmpty;
+          }
         } else {  // cell index: (bucket, entry) records, o-major (k_insert_dense / sorted_index file them)
           const uint64_t nbm = (1ULL << p.nb_log2) - 1;
           uint64_t c0 = kEmpty, c1 = kEmpty;
@@ -3049,7 +3079,7 @@ inline bool use_scan_reg(const mg_ctx* ctx) { return (ctx->scan_reg || ctx->join
 // (cell mode: option "reg_index" = 1 writes key records that k_insert_dense files;
 // measured slower than k_scan<INDEX>, whose CAS inserts hide behind its ALU work)
 inline bool use_scan_reg_index(const mg_ctx* ctx) {
-  return (ctx->join_P || ctx->reg_index || ctx->xchg) && use_scan_reg_w(ctx);
+  return (ctx->join_P || ctx->reg_index || ctx->reg_cas || ctx->xchg) && use_scan_reg_w(ctx);
 }
 inline uint32_t scan_wpb(uint32_t w) {
   for (uint32_t wpb = kWavesPerBlock; wpb >= 1; wpb >>= 1)
@@ -3224,7 +3254,9 @@ struct LaunchScan {
       ctx->pack_a = ctx->pack_w = 0;
     }
     if (index && ctx->key0_ready) sp.key0 = ctx->d_key0;  // mg_build_index allocated it (mixed lengths)
-    if (index && (ctx->sorted_index || ctx->xchg || (scan_is_reg(ctx, true) && !ctx->join_P))) {
+    const bool reg_cas = index && ctx->reg_cas && !ctx->sorted_index && !ctx->xchg && !ctx->join_P &&
+                         !ctx->reg_index && scan_is_reg(ctx, true);
+    if (index && !reg_cas && (ctx->sorted_index || ctx->xchg || (scan_is_reg(ctx, true) && !ctx->join_P))) {
       // key records (bucket, entry), o-major: the sorted build or k_insert_dense files them
       sp.key_bk = ctx->d_kb[0];
       sp.key_ent = ctx->d_ke[0];
@@ -3235,7 +3267,7 @@ struct LaunchScan {
       if (index) {
         allow_lds(k_scan_reg<W, true>, lds);
         hipLaunchKernelGGL((k_scan_reg<W, true>), dim3(sgrid), dim3(wpb * kWave), lds, stream, sp);
-        if (a_hi > a_lo)  // the reverse strand's keys (dense slots 4 a + 2, 4 a + 3)
+        if (a_hi > a_lo && !reg_cas)  // the reverse strand's keys (dense slots 4 a + 2, 4 a + 3)
           hipLaunchKernelGGL((k_rc_keys<W>), dim3((uint32_t)((a_hi - a_lo + kBlock - 1) / kBlock)), dim3(kBlock), 0,
                              stream, sp);
       } else {
@@ -3832,6 +3864,11 @@ int mg_set_option(mg_ctx* ctx, const char* name, int64_t value) {
   if (!strcmp(name, "flat_cap")) {  // tests: initial capacity of the flat run arrays (0 = auto)
     ctx->flat_cap_opt = value > 0 ? (uint64_t)value : 0;
     ctx->flat_need = 0;
+    return 0;
+  }
+  if (!strcmp(name, "reg_cas")) {  // 1: the register scan builds the cell index with inline CAS inserts
+    ctx->reg_cas = value != 0;
+    ctx->index_ready = false;
     return 0;
   }
   if (!strcmp(name, "xchg_sort_bits")) {  // exchange mode, P a power of two: top bucket bits the runs are sorted on (0: all)
@@ -4680,7 +4717,8 @@ int mg_build_index(mg_ctx* ctx, uint32_t min_overlap, uint32_t seed_k) {
     // mixed lengths: each read's o = 0 key for the prefix-containment kernel
     ctx->key0_ready = ctx->minlen != ctx->maxlen && ctx->prefix_contain;
     if (ctx->key0_ready) MG_TRY(ensure(&ctx->d_key0, &ctx->key0_cap, ctx->n + 1));
-    const bool reg_keys = scan_is_reg(ctx, true);  // the register scan writes key records (no CAS inside)
+    // the register scan writes key records (no CAS inside), unless option reg_cas
+    const bool reg_keys = scan_is_reg(ctx, true) && !(ctx->reg_cas && !ctx->reg_index && !ctx->sorted_index);
     if (ctx->sorted_index || reg_keys) {
       MG_TRY(ensure(&ctx->d_kb[0], &ctx->kb_cap, 4 * ctx->n));
       MG_TRY(ensure(&ctx->d_ke[0], &ctx->ke_cap, 4 * ctx->n));

@@ -666,6 +666,22 @@ def test_prefix_contain_off(name):
             assert {str(i): int(x) for i, x in enumerate(sup) if x} == want_sup, (join, flag)
 
 
+@pytest.mark.parametrize("name", FIXTURES)
+def test_reg_cas_index(name):
+    """option reg_cas: the register scan CAS-inserts all four keys itself; the
+    same rows, superReadIDs and getListOfReads lists (incl. list order)."""
+    meta = load_meta(name)
+    ds = Dataset.from_files([fixture_input(name)], meta["l"])
+    e = OverlapEngine(0)
+    e.set_option("reg_cas", 1)
+    rows, sup = gpu_rows(e, ds, meta["l"])
+    assert np.array_equal(rows_to_tuples(rows), golden_rows(name))
+    assert {str(i): int(x) for i, x in enumerate(sup) if x} == meta["super"]
+    for key, exp in meta.get("lookups", {}).items():
+        assert [list(x) for x in e.lookup(key)] == exp, key
+    e.close()
+
+
 def test_cell_pingpong_rebuilds():
     """option cell_pp: builds alternate between two cell tables, the
     next one cleared on a side stream; repeated builds on one engine over data
@@ -699,6 +715,7 @@ CONTAIN_OPTS = [
     {"probe_share": 1, "probe_compact": 0},
     {"probe_share": 0, "probe_compact": 1},
     {"cell_pp": 1},
+    {"reg_cas": 1},
 ]
 
 
