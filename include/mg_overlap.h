@@ -273,7 +273,21 @@ int mg_get_counters(const mg_ctx* ctx, mg_counters* c);
  * "halving" (which side emits a self-symmetric o=2/3 discovery pair:
  * 0 = parity-alternating (default, even load over source IDs), 1 = lower ID),
  * "phase_limit" / "max_blocks" (diagnostics: stop the probe after a phase /
- * cap the persistent grid).  Results never depend on any option. */
+ * cap the persistent grid),
+ * containment prunes, all exact: "contain_jcut" (runs whose
+ * first window lies past n1 - minlen, default 1), "contain_prune" (candidates
+ * that cannot raise the partner's superkey, default 1), "contain_skip" (runs of
+ * sources already contained, default 1), "contain_passes" (source-length
+ * passes, longest first, default 1),
+ * probe: "probe_share" (a discovery block's 4 wavefronts share its run regions,
+ * default 1), "probe_compact" (sparse run batches compacted, default 1),
+ * "xcd_plain" / "xcd_map" (run regions dealt XCD by XCD, default 0 / 1),
+ * "layout" (clustered slot order, default 1), "cell_pp" (ping-pong cell tables
+ * cleared on a side stream, default 0), "reg_cas" (the register scan builds the
+ * index with inline CAS, default 0), "reg_index" / "scan_reg" / "join" /
+ * "group_regions" (measured alternatives),
+ * "xchg_sort_bits" (exchange mode with P a power of two: runs sorted on the top
+ * bucket bits only, default 8; 0 = all).  Results never depend on any option. */
 int mg_set_option(mg_ctx* ctx, const char* name, int64_t value);
 /* HIP stream the context launches on (hipStream_t as void*), for callers that
  * time or capture it themselves. */
