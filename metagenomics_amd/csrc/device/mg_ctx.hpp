@@ -162,6 +162,7 @@ struct mg_ctx {
   bool group_regions = false; // option "group_regions": one run region per read group of 64 (measured slower)
   bool group_active = false;  // the last scan wrote group regions
   bool probe_share = true;     // option "probe_share": a discovery-probe block's 4 wavefronts share its regions
+  bool probe_share_xcd = false;  // option "probe_share_xcd": shared probe regions dealt XCD-major
   bool probe_compact = true;   // option "probe_compact": sparse run batches compacted in the probe (C5 probe 30.4 -> 26.8 ms)
   bool xcd_plain = false;     // option "xcd_plain": xcd_map for the scan's per-wavefront regions too
   int xchg_sort_bits = 8;  // option "xchg_sort_bits": exchange mode (P a power of two) sorts runs on the top bits only

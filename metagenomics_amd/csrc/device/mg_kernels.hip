@@ -1326,6 +1326,7 @@ struct ProbeParams {
   int contain_skip;               // CONTAIN: skip runs of sources already contained (their superkey != 0)
   int compact;                    // park the live items of sparse run batches (filled batches only)
   int share;                      // a block's wavefronts share its regions batch by batch (probe_share)
+  int share_xcd;                  // with share: blocks take region quadruples XCD-major (probe_share_xcd)
   int src_len_lo, src_len_hi;     // CONTAIN: only sources with length in [lo, hi) (hi = 0: all)
   // split path (k_probe<SPLIT=true> + k_verify): candidates {partner, source, o << 30 | j}
   uint3* cand;                    // one region of cand_cap records per probe wavefront
@@ -1538,8 +1539,17 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MG_PROBE
   // shared cells and partner slots stay in its CU's L1 and its XCD's L2
   const bool share = p.share && !p.xcd_map;
   const uint64_t rstep = share ? (uint64_t)kWavesPerBlock * kWave : (uint64_t)kWave;
+  // share_xcd: blocks renumbered XCD-major (block b runs on XCD b % 8), so the
+  // blocks of one XCD take neighbouring region quadruples
+  uint64_t lblock = blockIdx.x;
+  if (share && p.share_xcd) {
+    const uint64_t G = gridDim.x, x = blockIdx.x & 7u;
+    uint64_t before = 0;
+    for (uint64_t y = 0; y < x; ++y) before += (G + 7 - y) >> 3;
+    lblock = before + (blockIdx.x >> 3);
+  }
   auto reg_of = [&](uint32_t r) -> uint64_t {
-    return share ? (uint64_t)(r >> 2) * nwp + (uint64_t)blockIdx.x * kWavesPerBlock + (r & 3u)
+    return share ? (uint64_t)(r >> 2) * nwp + lblock * kWavesPerBlock + (r & 3u)
                  : rfirst + (uint64_t)r * rstride;
   };
   auto open_region = [&](uint32_t r) {
@@ -3338,6 +3348,7 @@ struct LaunchProbe {
     // shared regions help the discovery probe (C3 probe 4.56-4.57 vs 4.65-4.78 ms) but cost the
     // containment probe (C5 35.0 vs 29.6 ms: contain_skip finds fewer containers marked in time)
     pp.share = (!contain && ctx->probe_share) ? 1 : 0;
+    pp.share_xcd = ctx->probe_share_xcd ? 1 : 0;
     pp.src_len_lo = contain ? ctx->pass_len_lo : 0;
     pp.src_len_hi = contain ? ctx->pass_len_hi : 0;
     pp.xcd_map = xcd_map;
@@ -3893,6 +3904,10 @@ int mg_set_option(mg_ctx* ctx, const char* name, int64_t value) {
   }
   if (!strcmp(name, "cell_pp")) {  // 1: ping-pong cell tables, the next build's table cleared on a side stream
     ctx->cell_pp = value != 0;
+    return 0;
+  }
+  if (!strcmp(name, "probe_share_xcd")) {  // 1: shared probe regions dealt XCD-major
+    ctx->probe_share_xcd = value != 0;
     return 0;
   }
   if (!strcmp(name, "probe_share")) {  // 1: a probe block's wavefronts share its run regions batch by batch

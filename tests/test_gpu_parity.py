@@ -716,6 +716,7 @@ CONTAIN_OPTS = [
     {"probe_share": 0, "probe_compact": 1},
     {"cell_pp": 1},
     {"reg_cas": 1},
+    {"probe_share_xcd": 1},
 ]
 
 
