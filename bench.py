@@ -157,6 +157,60 @@ def cpu_baseline(cfg, sample_reads: int, full_build: bool = True):
                 reads_per_sec=od.num_unique / secs)
 
 
+def one_shot(e, ds, fused_step, device, rows):
+    """Per-dataset time: the reference builds its index and
+    graph once per dataset (main.cpp:45-47), so the clustered slot layout, built
+    once per upload, belongs to a dataset's cost.  layout_ms = the layout's
+    device time (kernels only: its buffers are kept between uploads); one_shot_ms
+    = layout_ms + the wall of one step right after it.  Beside it the same with
+    the slots in ID order (option layout = 0: no layout pass).  The packed reads'
+    H2D copy is outside both, as it is outside ms_per_step."""
+    import torch
+
+    def cycle(eng):
+        eng.upload(ds)
+        lay = eng.timings()["layout_ms"]
+        torch.cuda.synchronize(device)
+        t0 = time.perf_counter()
+        n = fused_step(eng)
+        torch.cuda.synchronize(device)
+        return lay, (time.perf_counter() - t0) * 1e3, n
+
+    out = {}
+    lay, ms, n = cycle(e)
+    assert n == rows, (n, rows)
+    out.update(layout_ms=lay, step_ms=ms, one_shot_ms=lay + ms)
+    e0 = OverlapEngine(device)
+    try:
+        e0.set_option("layout", 0)
+        e0.set_shard(0, 1)
+        cycle(e0)  # allocations
+        _, ms0, n0 = cycle(e0)
+        assert n0 == rows, (n0, rows)
+        out.update(id_order_step_ms=ms0, id_order_one_shot_ms=ms0)
+    finally:
+        e0.close()
+    out["default"] = "layout" if out["one_shot_ms"] <= out["id_order_one_shot_ms"] else "id_order"
+    return out
+
+
+def full_size_reference(config):
+    """The reference's own time for the bench's exact workload, from the
+    committed golden (tests/golden/<config>.json, made by make_scale_golden.py
+    with oracle/_ref/ref_harness digest: insertDataset + markContainedReads +
+    the insertAllEdgesOfRead loop, 1 thread, in the build container's Xeon)."""
+    path = GOLDEN_DIGEST.format(config)
+    if not os.path.exists(path):
+        return None
+    g = json.load(open(path))
+    rs = g.get("reference_seconds")
+    if not rs:
+        return None
+    secs = rs["hash_s"] + rs["contain_s"] + rs["discovery_s"]
+    return {"edges_per_sec": g["rows"]["n"] / 2 / secs, "seconds": secs, "reads": g["n_reads"],
+            "source": os.path.relpath(path, ROOT) + " (reference harness, 1 thread, build container)"}
+
+
 def combine_digests(ds):
     out = {"n": 0, "sum": 0, "xor": 0, "sum2": 0}
     for d in ds:
@@ -251,9 +305,8 @@ def main():
     ap.add_argument("--pmc", default=None,
                     help="committed rocprofv3 --pmc summary for roofline.traffic (default: profiles/PMC_FILES[config])")
     ap.add_argument("--nb-log2", type=int, default=0)
-    ap.add_argument("--split-probe", action="store_true", help="probe -> candidates -> verify kernels (option split = 1)")
-    ap.add_argument("--sort-runs", type=int, default=None,
-                    help="option sort_runs: bucket-ordered runs before the probe (default: the library's)")
+    ap.add_argument("--no-one-shot", action="store_true",
+                    help="skip the per-dataset one-shot timing (layout + one step, and ID order + one step)")
     ap.add_argument("--opt", action="append", default=[],
                     help="engine option NAME=VALUE (mg_set_option), repeatable; diagnostics / A-B runs")
     args = ap.parse_args()
@@ -320,9 +373,6 @@ def main():
     for r in ([rank] if mode in ("exchange", "replicated") else range(P)):
         e = OverlapEngine(local)
         e.set_option("nb_log2", args.nb_log2)
-        e.set_option("split", 1 if args.split_probe else 0)
-        if args.sort_runs is not None:
-            e.set_option("sort_runs", args.sort_runs)
         for kv in args.opt:
             name, val = kv.split("=", 1)
             e.set_option(name, int(val))
@@ -334,7 +384,6 @@ def main():
                 e.close()
                 continue
             e.set_shard(0, 1, s_lo, s_hi)
-            e.set_option("overlap_scan", 0)
         else:
             e.set_shard(r, P, 0, 0)
         e.upload(ds)
@@ -347,12 +396,7 @@ def main():
     def step():
         """one pass of the hot path; returns directed rows held by this process"""
         if mode in ("fused", "replicated"):
-            if not engines:
-                return 0
-            e = engines[0]
-            e.build_index(l, k)
-            e.mark_contained(copy=False)
-            return e.find_overlaps()
+            return fused_step(engines[0]) if engines else 0
         if mode == "replicated-sim":
             tot = 0
             for i, e in enumerate(engines):  # the ranks one after the other, each timed alone
@@ -376,6 +420,11 @@ def main():
     last_res = [None]
     plan = [None]    # exchange stream capacities, kept from step to step
     reruns = [0]     # exchange steps rerun after a capacity overflow (timed steps only)
+
+    def fused_step(e):
+        e.build_index(l, k)
+        e.mark_contained(copy=False)
+        return e.find_overlaps()
 
     def sync_barrier():
         torch.cuda.synchronize(local)
@@ -507,6 +556,11 @@ def main():
     }
     if sim_rank_ms is not None:
         res["sim_rank_ms"] = sim_rank_ms
+    if world == 1 and mode == "fused" and not args.no_one_shot:
+        try:
+            res["one_shot"] = one_shot(engines[0], ds, fused_step, local, rows)
+        except Exception as e:  # report, never fake
+            res["one_shot"] = {"error": str(e)}
     if world == 1 and mode == "fused" and args.replay:
         from metagenomics_amd.overlap import UnitigGraph
 
@@ -530,6 +584,9 @@ def main():
             res["cpu_baseline"] = cpu_baseline(cfg, args.cpu_sample, not args.no_cpu_full)
         except Exception as e:  # report, never fake
             res["cpu_baseline"] = {"value": None, "error": str(e)}
+        fsr = full_size_reference(args.config)
+        if fsr is not None:
+            res["cpu_baseline"]["full_size_reference"] = fsr
     print(json.dumps(res), file=json_out, flush=True)
     if dist is not None:
         dist.barrier()

@@ -50,10 +50,10 @@ typedef struct mg_timings {
   float total_ms;       /* device wall of index + contained + overlap */
   float scan_ms;        /* minimizer-run scan kernel (unsharded: the index-building scan, part of index_ms) */
   float probe_ms;       /* probe kernel (fused path: probe + verify) */
-  float verify_ms;      /* verify kernel of the split path (0 fused) */
+  float verify_ms;      /* 0 (the probe verifies inline)                */
   float upload_ms;      /* H2D copy of raw reads (mg_ingest_*)        */
   float ingest_ms;      /* device Dataset ingest (mg_ingest_*)        */
-  float sort_ms;        /* run records ordered by bucket (option "sort_runs"; 0 otherwise) */
+  float sort_ms;        /* exchange mode: runs ordered by bucket (grouped by owner); 0 otherwise */
   float layout_ms;      /* device layout of the last upload / ingest (clustered slots, option "layout") */
 } mg_timings;
 
@@ -65,7 +65,7 @@ typedef struct mg_counters {
   uint64_t entries;   /* bucket entries scanned                       */
   uint64_t verified;  /* partner reads fetched and compared           */
   uint64_t rows;      /* directed rows emitted                        */
-  uint64_t trips;     /* join: wavefront index-lookup trips (diagnostics) */
+  uint64_t trips;     /* 0 (reserved)                                   */
   /* the last containment pass (markContainedReads), same units */
   uint64_t c_runs, c_entries, c_verified, c_contained;
 } mg_counters;
@@ -152,9 +152,14 @@ int mg_copy_rows(mg_ctx* ctx, mg_edge* out, uint64_t cap, uint64_t* n_copied);
 
 /* --- sharding (multi-GPU, one process per GPU) ---------------------------- */
 /* Restrict this context to index buckets owned by `rank` of `nranks`
- * (bucket-range sharding) and/or to source reads
- * [read_lo, read_hi) (0-based; read_hi = 0 means all).  Rows produced are
- * this shard's part of the multiset; the union over ranks is the whole. */
+ * (bucket-range sharding) and/or to the source reads with
+ * reference IDs in [read_lo + 1, read_hi] (0-based range; read_hi = 0 means
+ * all): every row this context produces then has its `src` in that range or
+ * is the twin of such a row, so each rank holds the discoveries of its reads
+ * (insertAllEdgesOfRead of its sources, OverlapGraph.cpp:529-565).  The union
+ * over ranks is the whole multiset.  With the clustered slot layout the
+ * range's reads are re-clustered into slots [read_lo, read_hi) at the next
+ * mg_build_index. */
 int mg_set_shard(mg_ctx* ctx, uint32_t rank, uint32_t nranks, uint64_t read_lo, uint64_t read_hi);
 
 /* --- exchange mode: one process per GPU, SURVEY §8(e) ------------------------
@@ -249,45 +254,26 @@ int mg_super_digest(mg_ctx* ctx, uint64_t* out);
 /* --- diagnostics ----------------------------------------------------------- */
 int mg_get_timings(const mg_ctx* ctx, mg_timings* t);
 int mg_get_counters(const mg_ctx* ctx, mg_counters* c);
-/* Options: "nb_log2" (log2 directory buckets, 0 = auto), "rows_cap" (initial
- * row capacity, 0 = auto), "stats" (1 = count work units in the next launches),
- * "split" (1 = probe -> candidates -> verify kernels, 0 = fused probe (default)),
- * "overlap_scan" (1 = unsharded contexts build the index inside one window
- * scan of all reads, k_scan<INDEX>, and both probes reuse its runs (default);
- * 0 = separate index build and a scan per probe pass; source-range shards
- * with the whole index, bench --multi replicated, use 0),
- * "sort_runs" (1 = the shared scan's runs are radix-sorted by bucket before
- * the probes, so cell and partner loads coalesce; 0 = the probe walks the
- * scan's per-wavefront run regions in read order (default: the clustered
- * slot layout, option "layout" = 1, gives it the same locality)),
- * "pack_runs" (1 = 12-byte sort records when the field widths fit (default);
- * 0 = 16-byte records),
- * "sorted_index" (1 = k_scan<INDEX> writes the key records, a bucket sort
- * orders them and the cells are filled with plain stores; 0 = per-key CAS
- * inserts inside the scan (default, faster at C3)),
- * "prefix_contain" (1 = mixed-length sets find offset-0 containments with
- * k_prefix_contain and the containment probe skips suffix-key hits (default);
- * 0 = the probe verifies suffix-key hits at offset 0 itself),
- * "flat_cap" (tests: initial capacity of the sorted-run arrays, 0 = auto),
- * "sort_bits" (diagnostics: sort only the top bucket bits, 0 = all),
- * "halving" (which side emits a self-symmetric o=2/3 discovery pair:
- * 0 = parity-alternating (default, even load over source IDs), 1 = lower ID),
- * "phase_limit" / "max_blocks" (diagnostics: stop the probe after a phase /
- * cap the persistent grid),
- * containment prunes, all exact: "contain_jcut" (runs whose
- * first window lies past n1 - minlen, default 1), "contain_prune" (candidates
- * that cannot raise the partner's superkey, default 1), "contain_skip" (runs of
- * sources already contained, default 1), "contain_passes" (source-length
- * passes, longest first, default 1),
- * probe: "probe_share" (a discovery block's 4 wavefronts share its run regions,
- * default 1), "probe_compact" (sparse run batches compacted, default 1),
- * "xcd_plain" / "xcd_map" (run regions dealt XCD by XCD, default 0 / 1),
- * "layout" (clustered slot order, default 1), "cell_pp" (ping-pong cell tables
- * cleared on a side stream, default 0), "reg_cas" (the register scan builds the
- * index with inline CAS, default 0), "reg_index" / "scan_reg" / "join" /
- * "group_regions" (measured alternatives),
- * "xchg_sort_bits" (exchange mode with P a power of two: runs sorted on the top
- * bucket bits only, default 8; 0 = all).  Results never depend on any option. */
+/* Options (results never depend on any of them):
+ *  "nb_log2"        log2 directory buckets (0 = auto);
+ *  "rows_cap"       initial row capacity (0 = auto);
+ *  "stats"          1 = count work units (mg_get_counters) in the next launches;
+ *  "layout"         1 = slots clustered by canonical global minimizer (default),
+ *                   0 = ID order; takes effect at the next upload;
+ *  "halving"        side of a self-symmetric o = 2/3 pair: 0 = parity-alternating
+ *                   (default, even load over source IDs), 1 = lower ID;
+ *  "prefix_contain" 1 = mixed-length sets find offset-0 containments with
+ *                   k_prefix_contain and the containment probe skips suffix-key
+ *                   hits (default); 0 = the probe verifies them itself;
+ *  "contain_jcut", "contain_prune", "contain_skip"
+ *                   containment pruning, all exact, default 1;
+ *  "probe_share"    a discovery block's 4 wavefronts share its run regions (default 1);
+ *  "probe_compact"  sparse run batches are compacted in the probe (default 1);
+ *  "xchg_sort_bits" exchange mode with P a power of two: runs sorted on the top
+ *                   bucket bits only (default 8; 0 = all);
+ *  "flat_cap"       tests: initial capacity of the exchange scan's run arrays;
+ *  "phase_limit", "max_blocks"
+ *                   diagnostics: stop the probe after a phase / cap its grid. */
 int mg_set_option(mg_ctx* ctx, const char* name, int64_t value);
 /* HIP stream the context launches on (hipStream_t as void*), for callers that
  * time or capture it themselves. */

@@ -34,11 +34,29 @@ struct mg_ctx {
   // read's canonical global minimizer, so overlapping reads sit near each
   // other; d_id[slot] = reference ID - 1, d_phys[ID - 1] = slot (both nullptr:
   // slots in ID order).  Everything on the device works in slots; rows,
-  // superReadIDs, lookups and downloads leave in reference IDs.
+  // superReadIDs, lookups and downloads leave in reference IDs.  With a
+  // source-read range set (mg_set_shard), the reads of the range take the
+  // slots [read_lo, read_hi) (clustered among themselves), so a shard's slot
+  // range holds exactly its reference IDs.
   bool layout = true;
-  uint32_t* d_id = nullptr;
-  uint32_t* d_phys = nullptr;
-  size_t id_cap = 0, phys_cap = 0;
+  uint32_t* d_id = nullptr;    // one of id_store[], or nullptr
+  uint32_t* d_phys = nullptr;  // one of phys_store[], or nullptr
+  uint32_t* id_store[2] = {nullptr, nullptr};  // a re-layout builds the maps in the unused pair
+  uint32_t* phys_store[2] = {nullptr, nullptr};
+  size_t id_cap[2] = {0, 0}, phys_cap[2] = {0, 0};
+  uint64_t layout_lo = 0, layout_hi = 0;  // the source-read range the current layout groups (0, 0: none)
+  // layout scratch, kept between uploads so a re-upload allocates nothing:
+  // sort keys / values (double buffers), the sort's temporary storage, and the
+  // second slot array the gather writes (the two slot arrays swap)
+  uint32_t* d_lay_k[2] = {nullptr, nullptr};
+  uint32_t* d_lay_v[2] = {nullptr, nullptr};
+  size_t lay_k_cap[2] = {0, 0}, lay_v_cap[2] = {0, 0};
+  void* d_lay_tmp = nullptr;
+  size_t lay_tmp_cap = 0;
+  uint64_t* d_words_alt = nullptr;
+  size_t words_alt_cap = 0;
+  uint16_t* d_len_alt = nullptr;
+  size_t len_alt_cap = 0;
   uint32_t* d_tmp32 = nullptr;  // ID-order staging of per-read outputs
   size_t tmp32_cap = 0;
   // index
@@ -48,23 +66,13 @@ struct mg_ctx {
   uint64_t* d_cells = nullptr;  // cells of kCell entries (this rank's bucket range)
   size_t cells_cap = 0;
   uint64_t cell_lo = 0, cell_n = 0;  // local bucket range [cell_lo, cell_lo + cell_n)
-  // ping-pong cell tables of the unsharded build (option "cell_pp", mg_kernels.hip setup_cells_pp)
-  bool cell_pp = false;  // measured slower: the side-stream fill slows the scan or the probe it overlaps
-  uint64_t* pp_buf[2] = {nullptr, nullptr};
-  size_t pp_cap = 0;
-  int pp_next = 0;
-  int pp_due = -1;  // table whose clear waits for this build's probe (-1: none)
-  bool pp_dirty[2] = {true, true}, pp_pending[2] = {false, false};
-  hipStream_t clear_stream = nullptr;
-  hipEvent_t ev_clear[2] = {nullptr, nullptr};
-  hipEvent_t ev_use = nullptr;
   // containment
   unsigned long long* d_superkey = nullptr;
   unsigned long long* superkey = nullptr;  // the containment key array in use (d_superkey or caller-owned)
   uint32_t* d_super = nullptr;
   unsigned int* d_any = nullptr;
   unsigned long long* d_digest = nullptr;  // mg_rows_digest / mg_super_digest accumulators (4 u64)
-  size_t super_cap = 0;
+  size_t super_cap = 0, superkey_cap = 0;
   bool contained_done = false, super_any = false;
   // rows
   uint32_t* d_rows = nullptr;
@@ -78,7 +86,7 @@ struct mg_ctx {
   mg_counters counters{};
   // shard
   uint32_t rank = 0, nranks = 1;
-  uint64_t read_lo = 0, read_hi = 0;
+  uint64_t read_lo = 0, read_hi = 0;  // source-read range: reference IDs - 1 = slots [read_lo, read_hi)
   uint32_t max_blocks = 8192;  // cap on the persistent discovery grid (blocks of 4 wavefronts)
   int phase_limit = 99;        // diagnostics (option "phase_limit")
   bool halving_low = false;    // option "halving": o=2/3 pair side rule
@@ -94,85 +102,47 @@ struct mg_ctx {
   uint32_t* d_compact = nullptr;
   size_t compact_cap = 0;
   // exchange mode (one process per GPU): mg_xchg_begin's scan
-  // leaves key records (d_kb[0] / d_ke[0]) and bucket-sorted runs of this
-  // rank's sources; packable = bit mask of what mg_xchg_pack can route now
+  // leaves key records (d_kb / d_ke) and bucket-sorted runs of this rank's
+  // sources; packable = bit mask of what mg_xchg_pack can route now
   bool xchg = false;                     // the context's current build is an exchange-mode build
   uint64_t xchg_lo = 0, xchg_hi = 0;     // its source reads
   unsigned long long* d_blk = nullptr;   // routing: per-(block, rank) counts / offsets
   size_t blk_cap = 0;
   int packable = 0;                      // 1 << MG_KEYS | 1 << MG_RUNS | 1 << MG_ROWS
-  unsigned long long* d_flat_cnt = nullptr;
+  unsigned long long* d_flat_cnt = nullptr;  // per-region counts of the received runs (probe input)
   size_t flat_cnt_cap = 0;
   unsigned long long* d_slot_cnt = nullptr;  // per-region counts of a slot-layout buffer (digest)
   size_t slot_cnt_cap = 0;
-  // timing
-  hipEvent_t ev[16] = {};  // [14], [15]: apply_layout
-  // unsharded contexts build the index inside the window scan (k_scan<INDEX>);
-  // its runs then serve the containment and the discovery probes
-  int scan_state = 0;        // 0 none, 1 launched (not settled), 2 settled
-  bool overlap_scan = true;  // option "overlap_scan" (0: separate index build, a scan per probe pass)
-  bool scan_reg = true;      // option "scan_reg": register sliding minimum (k_scan_reg) for the run scans when w <= 32
-  bool reg_cas = false;      // option "reg_cas": k_scan_reg<INDEX> CAS-inserts all four keys itself (no key records)
-  bool reg_index = false;    // option "reg_index": also for the cell index build (key records + k_insert_dense)
-  // partitioned join (option "join", default): keys + runs as sorted join
-  // records, per-partition LDS tables (k_join); cells only on demand (lookups)
-  bool join = false;
-  int join_P = 0, join_A = 0, join_QB = 0, join_WB = 0;  // record geometry of the current build (0: not join)
-  int join_P_opt = 0;        // option "join_parts_log2" (0: auto)
-  bool join_ready = false;   // the sorted join records + partition bounds are current
-  bool cells_ready = false;  // the cell table holds the current index
-  uint64_t n_join = 0;       // join records (holes excluded)
-  unsigned long long* d_bnd = nullptr;
-  unsigned long long* d_mid = nullptr;
-  size_t bnd_cap = 0, mid_cap = 0;
-  unsigned int* d_queue = nullptr;
-  // split probe (k_probe<SPLIT> + k_verify)
-  bool split = false;  // option "split": k_probe<SPLIT> + k_verify instead of the fused probe
-  uint3* d_cand = nullptr;
-  size_t cand_cap_total = 0;
-  uint64_t cand_cap_need = 0;
-  unsigned long long* d_cand_cnt = nullptr;
-  size_t cand_cnt_cap = 0;
-  std::vector<unsigned long long> cand_cnt_host;
-  // bucket-ordered runs (option "sort_runs"): the shared scan's runs as SoA
-  // (x, meta) sorted by bucket, so the probe meets each cell's runs together
-  bool sort_runs = false;
+  uint32_t* d_kb = nullptr;  // key records: bucket / index entry, key o of read a at o * n + a
+  uint64_t* d_ke = nullptr;
+  size_t kb_cap = 0, ke_cap = 0;
+  // the exchange scan's runs as flat SoA arrays (double buffers of the bucket
+  // sort): chunks of kFlatChunk records claimed from kFlatCounters cursors
+  bool scan_flat = false;
   uint64_t* d_sk[2] = {nullptr, nullptr};
   uint64_t* d_sm[2] = {nullptr, nullptr};
   size_t sk_cap = 0;
   int sk_sel = 0;  // which buffer holds the sorted result
   void* d_sort_tmp = nullptr;
   size_t sort_tmp_cap = 0;
-  unsigned long long* d_run_off = nullptr;
-  size_t run_off_cap = 0;
   uint64_t n_sorted = 0;
-  bool scan_flat = false;          // the shared scan wrote d_sk[0] / d_sm[0] directly
   unsigned long long* d_flat_cursor = nullptr;
   uint64_t flat_need = 0, n_flat = 0;
   uint64_t* d_holes = nullptr;  // chunk ids of the flat arrays no counter reached (k_fill_holes)
   size_t holes_cap = 0;
   std::vector<uint64_t> holes_host;
-  uint64_t flat_cap_opt = 0;       // option "flat_cap" (tests: force the overflow rerun)
-  uint64_t flat_off = 0;           // records ahead of the flat chunks (join: the 4 N dense key records)
-  bool pack_runs = true;           // option "pack_runs": 12-B sort records when the widths fit
-  int pack_a = 0, pack_w = 0;      // packing of the current flat runs (0: 16-B records)
-  int sorted_state = 0;  // 0 none, 2 sorted (for the current scan)
-  uint64_t probe_region = 0;  // sorted probe: runs per region (0: one tile per wavefront)
-  bool xcd_map = true;        // probe: run regions dealt XCD by XCD (group regions, or sorted with probe_region)
-  bool group_regions = false; // option "group_regions": one run region per read group of 64 (measured slower)
-  bool group_active = false;  // the last scan wrote group regions
+  uint64_t flat_cap_opt = 0;  // option "flat_cap" (tests: force the overflow rerun)
+  int pack_a = 0, pack_w = 0;  // packing of the current flat runs (0: 16-B records)
+  int xchg_sort_bits = 8;  // option "xchg_sort_bits": P a power of two: runs sorted on the top bits only
+  unsigned long long* d_bnd = nullptr;  // per-destination bounds of the sorted runs
+  size_t bnd_cap = 0;
+  // timing
+  hipEvent_t ev[16] = {};  // [14], [15]: apply_layout
+  // unsharded contexts build the index inside the window scan (k_scan<INDEX>);
+  // its runs then serve the containment and the discovery probes
+  int scan_state = 0;        // 0 none, 1 launched (not settled), 2 settled
   bool probe_share = true;     // option "probe_share": a discovery-probe block's 4 wavefronts share its regions
-  bool probe_share_xcd = false;  // option "probe_share_xcd": shared probe regions dealt XCD-major
   bool probe_compact = true;   // option "probe_compact": sparse run batches compacted in the probe (C5 probe 30.4 -> 26.8 ms)
-  bool xcd_plain = false;     // option "xcd_plain": xcd_map for the scan's per-wavefront regions too
-  int xchg_sort_bits = 8;  // option "xchg_sort_bits": exchange mode (P a power of two) sorts runs on the top bits only
-  int sort_bits = 0;     // diagnostics: sort only the top sort_bits bucket bits (0: all)
-  // sorted index build (option "sorted_index", default off): k_scan<INDEX> writes
-  // the 4N key records (bucket, entry), a radix sort orders them by bucket and
-  // k_fill_cells files them with plain stores instead of per-key CAS.  Measured
-  // at C3: index 5.6 vs 3.9 ms (the CAS inserts hide behind the scan's ALU work;
-  // the key sort alone costs 1.2 ms), so CAS stays the default
-  bool sorted_index = false;
   // prefix containments (k_prefix_contain): each read's o = 0 key (bucket,
   // fingerprint, q) written by k_scan<INDEX> for mixed-length sets; when ready
   // the containment probe skips suffix-key hits (containment)
@@ -182,13 +152,7 @@ struct mg_ctx {
   bool prefix_contain = true;  // option "prefix_contain"
   bool contain_jcut = true;    // option "contain_jcut": containment probe drops runs with jlo > n1 - minlen (C5: 60 -> 47 ms)
   bool contain_skip = true;    // option "contain_skip": skip runs of sources already known contained (C5: 42.8 -> 29.7 ms)
-  int contain_passes = 1;      // option "contain_passes": containment probe passes by source length, longest first
-  int pass_len_lo = 0, pass_len_hi = 0;  // the current pass's source lengths [lo, hi) (0: all)
   bool contain_prune = true;   // option "contain_prune": skip candidates that cannot raise the superkey (C5: 388M -> 110M compares)
-  uint32_t* d_kb[2] = {nullptr, nullptr};
-  uint64_t* d_ke[2] = {nullptr, nullptr};
-  size_t kb_cap = 0, ke_cap = 0, kb1_cap = 0, ke1_cap = 0;
-  float keysort_ms = 0.f;
   float shared_scan_ms = 0.f;  // k_scan<INDEX> kernel time of the last mg_build_index
   mg_timings t{};
   // Dataset ingest on the device (mg_ingest_*): frequency of each unique read
@@ -254,10 +218,7 @@ int apply_layout(mg_ctx* ctx);
 // new reads invalidate everything derived from them
 inline void reset_derived(mg_ctx* ctx) {
   ctx->scan_state = 0;
-  ctx->sorted_state = 0;
   ctx->index_ready = false;
-  ctx->join_ready = false;
-  ctx->cells_ready = false;
   ctx->contained_done = false;
   ctx->super_any = false;
   ctx->n_rows = 0;

@@ -26,8 +26,8 @@
 //    against the partner's slot, ballot-compacted rows into a per-wavefront
 //    HBM region).
 //  * only half of the symmetric discoveries are verified: o = 1 hits are the
-//    twins of the partner's o = 0 hits, o = 2/3 hits are kept only when
-//    source <= partner; every verified discovery emits its row and its twin
+//    twins of the partner's o = 0 hits, an o = 2/3 pair is kept on one side
+//    (rc_side_keeps); every verified discovery emits its row and its twin
 //    (DESIGN.md §4 proves this reproduces the reference multiset).
 #include <hip/hip_runtime.h>
 
@@ -283,43 +283,6 @@ __global__ __launch_bounds__(kBlock) void k_index_build(IndexParams p) {
   }
 }
 
-// Sorted index build (option "sorted_index"): the key records sorted by bucket
-// (stable rocprim radix sort) are filed without atomics.  A record's rank among
-// the records of its bucket is found by looking back over at most kCell
-// neighbours; ranks below kCell take home slot `rank` with a plain store
-// (OVERFLOW = false), the rest go through cell_insert's chain walk in a second
-// launch, after every home slot is written (OVERFLOW = true).  Same cell
-// contents as the CAS build up to the order inside a cell, which nothing reads
-// (probe and getListOfReads filter every slot).
-template <bool OVERFLOW>
-__global__ __launch_bounds__(kBlock) void k_fill_cells(const uint32_t* __restrict__ bk,
-                                                       const uint64_t* __restrict__ ent, uint64_t n,
-                                                       uint64_t* __restrict__ cells, uint64_t cell_n) {
-  const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (i >= n) return;
-  const uint64_t e = ent[i];
-  if (e == kEmpty) return;
-  const uint32_t b = bk[i];
-  int r = 0;
-  while (r < kCell && i > (uint64_t)r && bk[i - r - 1] == b) ++r;
-  if (!OVERFLOW) {
-    if (r < kCell) cells[(uint64_t)b * kCell + r] = e;
-  } else if (r >= kCell) {
-    cell_insert(cells, b, cell_n, e);
-  }
-}
-
-// insertIntoTable (HashTable.cpp:163-195) for the o-major key records the
-// register scan and k_rc_keys wrote: one thread per key, CAS into its home
-// cell chain (independent inserts, so the whole device hides their latency).
-__global__ __launch_bounds__(kBlock) void k_insert_dense(const uint32_t* __restrict__ bk, const uint64_t* __restrict__ ent,
-                                                         uint64_t n, uint64_t* __restrict__ cells, uint64_t cell_n) {
-  for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBlock) {
-    const uint64_t e = ent[i];
-    if (e != kEmpty) cell_insert(cells, bk[i], cell_n, e);
-  }
-}
-
 // markContainedReads at offset s = 0 (OverlapGraph.cpp:225-340): read2 (or
 // its reverse strand) is a prefix of read1.  The reference meets these only
 // through read2's suffix key (o = 1/3 at window j = n2 - h), because window
@@ -417,68 +380,31 @@ struct ScanParams {
   uint64_t a_lo, a_hi;
   int h, m, w;
   uint32_t nb_log2, rank, nranks;
-  ulonglong2* runs;               // one region of run_cap records per wavefront (group_regions: per group of 64 reads)
-  int group_regions;              // 1: region g holds the runs of read group g (reads [64 g, 64 g + 64)), in read order
+  ulonglong2* runs;               // one region of run_cap records per wavefront
   unsigned long long* run_cnt;    // [waves] records produced (may exceed run_cap)
   uint64_t run_cap;
   uint64_t* cells;                // k_scan<INDEX>: the (unsharded) cell table the keys go into
   uint64_t cell_n;
-  // flat SoA output (option "sort_runs"): x / meta arrays filled through one
-  // cursor, 64 records per atomic; regions are not written
+  // flat SoA output (exchange mode: the bucket sort's input): x / meta arrays
+  // filled in chunks claimed from kFlatCounters cursors; regions are not written
   uint64_t* flat_keys;
   uint64_t* flat_meta;
   unsigned long long* flat_cursor;
   uint64_t flat_cap;
   int pack_a, pack_w;  // pack_a > 0: 12-B records (run_pack_key / run_pack_meta) instead of 16-B
-  // k_scan<INDEX> with a sorted index build (option "sorted_index"): the four key
-  // records of read a go to key_bk / key_ent[o * key_n + a] (bucket, entry)
-  // instead of a CAS into the cells; k_fill_cells files them after a bucket sort
+  // exchange mode: the four key records of read a go to key_bk / key_ent[o *
+  // key_n + a] (bucket, entry) instead of a CAS into the cells; they travel to
+  // the bucket owner (k_part) and k_insert_slots files them there
   uint32_t* key_bk;
   uint64_t* key_ent;
   uint64_t key_n;
   // per read: its o = 0 key's hash bits (bucket | fingerprint, 50 bits) | q << 54
   // (k_prefix_contain); nullptr: not written
   uint64_t* key0;
-  // partitioned join (option "join"): join_P > 0 packs runs AND the four keys of
-  // every read as 12-B join records (join_k32 / join_run_val / join_key_val)
-  // into the flat arrays instead of inserting keys into cells
-  int join_P, join_A, join_QB, join_WB;
-  uint32_t* join_kk;  // join INDEX: dense key records, read a's key o at 4 a + o (o = 0, 1 here;
-  uint64_t* join_kv;  // o = 2, 3 by k_rc_keys); the runs follow at 4 N in the flat arrays
 };
 
-// ---------------------------------------------------------------- join ---
-// Partitioned hash join: every index key (hashRead's four keys,
-// HashTable.cpp:88-104) and every window run becomes a 12-B record {k32, val64}
-// keyed by the partition f = top P bits of v = mix64(minimizer m-mer).  One
-// radix sort on the low P + 2 bits of k32 groups each partition's keys, then its
-// runs; k_join builds the partition's exact-key table in LDS and probes its runs
-// against it.  k32 = H32 << (P + 2) | f << 1 | is_run (bit P + 1 is 0; holes
-// are all ones and sort last), H32 = low 32 bits of v; the P + 2 high bits of
-// H32 that k32 cannot hold ride in val64:
-//   run: read (A) | jlo (10) | jhi - jlo (WB) | p - jhi (WB) | H32 >> (30 - P)
-//   key: read (A) | o (2)    | q (QB)                       | H32 >> (30 - P)
-__device__ __forceinline__ uint32_t join_k32(uint64_t v, int P, uint32_t is_run) {
-  return ((uint32_t)v << (P + 2)) | ((uint32_t)(v >> (64 - P)) << 1) | is_run;
-}
-__device__ __forceinline__ uint64_t join_hhi(uint64_t v, int P) { return (uint64_t)((uint32_t)v >> (30 - P)); }
-__device__ __forceinline__ uint64_t join_run_val(uint64_t meta, uint64_t v, const ScanParams& p) {
-  const uint64_t ra = meta & 0xFFFFFFFFull, pos = (meta >> 32) & 1023u, jlo = (meta >> 42) & 1023u,
-                 jhi = (meta >> 52) & 1023u;
-  const int A = p.join_A, WB = p.join_WB;
-  return ra | (jlo << A) | ((jhi - jlo) << (A + 10)) | ((pos - jhi) << (A + 10 + WB)) |
-         (join_hhi(v, p.join_P) << (A + 10 + 2 * WB));
-}
-__device__ __forceinline__ uint64_t join_key_val(uint32_t r, int o, int q, uint64_t v, const ScanParams& p) {
-  const int A = p.join_A;
-  return (uint64_t)r | ((uint64_t)o << A) | ((uint64_t)q << (A + 2)) | (join_hhi(v, p.join_P) << (A + 2 + p.join_QB));
-}
-__device__ __forceinline__ uint32_t join_h32(uint32_t k32, uint64_t val, int P, int shift) {
-  return (k32 >> (P + 2)) | ((uint32_t)(val >> shift) << (30 - P));
-}
-
-// Sort records of 12 B instead of 16 (option "sort_runs" when the widths fit,
-// packable_runs): key32 = bucket | low (32 - nb) fingerprint bits; meta64 =
+// Sort records of 12 B instead of 16 (exchange mode's bucket sort, when the
+// widths fit: packable_runs): key32 = bucket | low (32 - nb) fingerprint bits; meta64 =
 // read (A bits) | jlo (10) | jhi - jlo (WB) | p - jhi (WB) | high fingerprint
 // bits.  A run's minimizer lies in all its windows, so p - jhi and jhi - jlo
 // are both < w.  A = bit width of the read count, so a read index is never all
@@ -570,10 +496,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) voi
     const uint64_t a = p.a_lo + grp * kWave + lane;
     int n = 0;
     const uint64_t* g = p.words + a * slot_words(MAXW);
-    if (p.group_regions) {  // this group's own region
-      region = p.runs + grp * p.run_cap;
-      cursor = 0;
-    }
     if (a < p.a_hi) {
       n = (int)p.len[a];
       if (n && p.super && p.super[a]) n = 0;
@@ -793,7 +715,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) voi
     }
     put(tend > 0, run_meta(a, last_pos, jlo, J));  // each read's last run
     while (nbuf) flush(nbuf < (uint32_t)kWave ? nbuf : (uint32_t)kWave);  // the group's runs leave with its registers
-    if (p.group_regions && lane == 0) p.run_cnt[grp] = cursor;
     if (INDEX && tend) {
       // t = n-m, one past the last window position: the rolled m-mers sit there
       const uint32_t hk = order_key(mm), hr = order_key(rcm);
@@ -842,7 +763,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) voi
       }
     }
   }
-  if (lane == 0 && !p.group_regions) p.run_cnt[gw] = cursor;
+  if (lane == 0) p.run_cnt[gw] = cursor;
 }
 
 // ---------------------------------------------------------------------------
@@ -913,10 +834,7 @@ struct RunStage {
         const uint64_t pr = lane_prefix(bal);
         const uint64_t at = pr < room ? fbase + fused + pr : nbase + (pr - room);
         if (at < p.flat_cap) {
-          if (p.join_P) {
-            reinterpret_cast<uint32_t*>(p.flat_keys)[at] = join_k32(v, p.join_P, 1u);
-            p.flat_meta[at] = join_run_val(meta, v, p);
-          } else if (p.pack_a) {
+          if (p.pack_a) {
             reinterpret_cast<uint32_t*>(p.flat_keys)[at] = run_pack_key(v, p.nb_log2);
             p.flat_meta[at] = run_pack_meta(meta, v, p.nb_log2, p.pack_a, p.pack_w);
           } else {
@@ -947,37 +865,13 @@ struct RunStage {
     }
   }
 
-  // one ready 32-bit-key record per flagged lane straight into the flat arrays
-  // (the join mode's index keys)
-  __device__ void emit_ready(bool flag, uint32_t k32, uint64_t val) {
-    const uint64_t bal = __ballot(flag);
-    const uint64_t npop = (uint64_t)__popcll(bal);
-    if (!npop) return;
-    const uint64_t room = fcap - fused;
-    unsigned long long nbase = 0;
-    if (npop > room) {
-      const uint32_t x = blockIdx.x & (kFlatCounters - 1);
-      if (lane == 0) nbase = (atomicAdd(&p.flat_cursor[x], 1ull) * kFlatCounters + x) * kFlatChunk;
-      nbase = __shfl(nbase, 0);
-    }
-    if (flag) {
-      const uint64_t pr = lane_prefix(bal);
-      const uint64_t at = pr < room ? fbase + fused + pr : nbase + (pr - room);
-      if (at < p.flat_cap) {
-        reinterpret_cast<uint32_t*>(p.flat_keys)[at] = k32;
-        p.flat_meta[at] = val;
-      }
-    }
-    advance(npop, room, nbase);
-  }
-
   // unused tail of the last flat chunk (holes the sort and probe skip) and the region count
   __device__ void finish(uint64_t gw) {
     if (p.flat_keys) {
       for (uint64_t i = fused + lane; i < fcap; i += kWave) {
         const uint64_t at = fbase + i;
         if (at < p.flat_cap) {
-          if (p.pack_a || p.join_P)
+          if (p.pack_a)
             reinterpret_cast<uint32_t*>(p.flat_keys)[at] = 0xFFFFFFFFu;
           else
             p.flat_keys[at] = kEmpty;
@@ -985,17 +879,7 @@ struct RunStage {
         }
       }
     }
-    if (lane == 0 && !p.group_regions) p.run_cnt[gw] = cursor;
-  }
-  // group_regions: each read group's runs go to its own region
-  __device__ __forceinline__ void begin_group(uint64_t grp) {
-    if (p.group_regions) {
-      region = p.runs + grp * p.run_cap;
-      cursor = 0;
-    }
-  }
-  __device__ __forceinline__ void end_group(uint64_t grp) {
-    if (p.group_regions && lane == 0) p.run_cnt[grp] = cursor;
+    if (lane == 0) p.run_cnt[gw] = cursor;
   }
 };
 
@@ -1077,7 +961,6 @@ __global__ __launch_bounds__(kBlock) void k_scan_reg(ScanParams p) {
       for (int k = 0; k <= MAXW; ++k) nx[k] = k < kRwLoad ? gs[k] : 0;
     }
     const uint64_t a0 = p.a_lo + grp * kWave;
-    st.begin_group(grp);
     uint32_t S[kRegW + 1];
 #pragma unroll
     for (int u = 0; u <= kRegW; ++u) S[u] = 0xFFFFFFFFu;
@@ -1128,78 +1011,24 @@ __global__ __launch_bounds__(kBlock) void k_scan_reg(ScanParams p) {
     }
     st.put(tend >= 0, run_meta(a, last, jlo, J));  // each read's last run
     while (st.nbuf) st.flush(st.nbuf < (uint32_t)kWave ? st.nbuf : (uint32_t)kWave, rw, a0);
-    st.end_group(grp);
-    if constexpr (INDEX) {  // join records of keys o = 0 / 1 (the cell index is k_scan's / k_index_build's)
+    if constexpr (INDEX) {  // key records of o = 0 / 1, o-major (k_rc_keys writes o = 2 / 3)
       if (a < p.a_hi) {
         const int p0 = (int)(kw0 & 1023u), p1 = (int)(kw1 & 1023u);
-        uint32_t k0 = 0xFFFFFFFFu, k1 = 0xFFFFFFFFu;  // (no keys: holes, n <= l cannot pass setup)
-        uint64_t e0 = kFlatHole, e1 = kFlatHole;
-        if (n && p.join_P) {
+        const uint64_t nbm = (1ULL << p.nb_log2) - 1;
+        uint64_t c0 = kEmpty, c1 = kEmpty;  // (no keys: holes, n <= l cannot pass setup_index)
+        uint32_t b0 = 0, b1 = 0;
+        if (n) {
           const uint64_t v0 = mix64(funnel(rw[0], rw[1], p0 << 1) >> msh);  // p0 < w <= 32
           const uint64_t v1 = mix64(ext_reg<MAXW>(rw, p1) >> msh);
-          k0 = join_k32(v0, p.join_P, 0u);
-          e0 = join_key_val((uint32_t)a, 0, p0, v0, p);
-          k1 = join_k32(v1, p.join_P, 0u);
-          e1 = join_key_val((uint32_t)a, 1, p1 - (n - h), v1, p);
+          b0 = (uint32_t)(v0 & nbm);
+          b1 = (uint32_t)(v1 & nbm);
+          c0 = make_entry(v0, p.nb_log2, p0, 0, (uint32_t)a);
+          c1 = make_entry(v1, p.nb_log2, p1 - (n - h), 1, (uint32_t)a);
         }
-        if (p.join_P) {
-          p.join_kk[4 * a] = k0;
-          p.join_kv[4 * a] = e0;
-          p.join_kk[4 * a + 1] = k1;
-          p.join_kv[4 * a + 1] = e1;
-        } else if (!p.key_bk) {  // option reg_cas: all four keys CAS-inserted here (no records, no k_rc_keys)
-          if (n) {
-            const uint64_t nbm = (1ULL << p.nb_log2) - 1;
-            const uint64_t v0 = mix64(funnel(rw[0], rw[1], p0 << 1) >> msh);
-            const uint64_t v1 = mix64(ext_reg<MAXW>(rw, p1) >> msh);
-            // the reverse strand's keys o = 3 / 2 (k_rc_keys' rolled pass, from registers)
-            uint32_t kb3 = 0xFFFFFFFFu, kb2 = 0xFFFFFFFFu;
-            uint64_t mb3 = 0, mb2 = 0;
-            const uint64_t Aw = ext_reg<MAXW>(rw, n - h);
-            uint64_t r3 = rc_word(funnel(rw[0], rw[1], 2 * (w - 1))) & mmask;
-            uint64_t r2 = rc_word(ext_reg<MAXW>(rw, n - m)) & mmask;
-            for (int i = 0; i < w; ++i) {
-              const uint32_t k3 = order_key(r3) | (uint32_t)i, k2 = order_key(r2) | (uint32_t)i;
-              if (k3 < kb3) { kb3 = k3; mb3 = r3; }
-              if (k2 < kb2) { kb2 = k2; mb2 = r2; }
-              const int t3 = w - 2 - i;
-              if (t3 >= 0) {
-                r3 = ((r3 << 2) | (3u - ((rw[0] >> (62 - 2 * t3)) & 3u))) & mmask;
-                r2 = ((r2 << 2) | (3u - ((Aw >> (62 - 2 * t3)) & 3u))) & mmask;
-              }
-            }
-            const uint64_t v2 = mix64(mb2), v3 = mix64(mb3);
-            if (p.key0) p.key0[a] = (v0 & ((1ULL << 50) - 1)) | ((uint64_t)p0 << 54);
-            cell_insert(p.cells, v0 & nbm, p.cell_n, make_entry(v0, p.nb_log2, p0, 0, (uint32_t)a));
-            cell_insert(p.cells, v1 & nbm, p.cell_n, make_entry(v1, p.nb_log2, p1 - (n - h), 1, (uint32_t)a));
-            cell_insert(p.cells, v2 & nbm, p.cell_n, make_entry(v2, p.nb_log2, (int)(kb2 & 1023u), 2, (uint32_t)a));
-            cell_insert(p.cells, v3 & nbm, p.cell_n, make_entry(v3, p.nb_log2, (int)(kb3 & 1023u), 3, (uint32_t)a));
-          } else if (p.key0) {
-            p.key0[a] = kEmpty;
-          }
-        } else {  // cell index: (bucket, entry) records, o-major (k_insert_dense / sorted_index file them)
-          const uint64_t nbm = (1ULL << p.nb_log2) - 1;
-          uint64_t c0 = kEmpty, c1 = kEmpty;
-          uint32_t b0 = 0, b1 = 0;
-          if (n) {
-            const uint64_t v0 = mix64(funnel(rw[0], rw[1], p0 << 1) >> msh);
-            const uint64_t v1 = mix64(ext_reg<MAXW>(rw, p1) >> msh);
-            b0 = (uint32_t)(v0 & nbm);
-            b1 = (uint32_t)(v1 & nbm);
-            c0 = make_entry(v0, p.nb_log2, p0, 0, (uint32_t)a);
-            c1 = make_entry(v1, p.nb_log2, p1 - (n - h), 1, (uint32_t)a);
-          }
-          if (p.key0 && n) {
-            const uint64_t v0 = mix64(funnel(rw[0], rw[1], p0 << 1) >> msh);
-            p.key0[a] = (v0 & ((1ULL << 50) - 1)) | ((uint64_t)p0 << 54);
-          } else if (p.key0) {
-            p.key0[a] = kEmpty;
-          }
-          p.key_bk[a] = b0;
-          p.key_ent[a] = c0;
-          p.key_bk[p.key_n + a] = b1;
-          p.key_ent[p.key_n + a] = c1;
-        }
+        p.key_bk[a] = b0;
+        p.key_ent[a] = c0;
+        p.key_bk[p.key_n + a] = b1;
+        p.key_ent[p.key_n + a] = c1;
       }
     }
   }
@@ -1226,12 +1055,12 @@ __device__ __forceinline__ void load_slot(const uint64_t* words, uint32_t bid, u
   }
 }
 
-// Join records of the reverse strand's keys (hashRead, HashTable.cpp:88-104),
+// Key records of the reverse strand's keys (hashRead, HashTable.cpp:88-104),
 // one thread per read: o = 3 (R[n-h, n) = rc F[0, h): m-mer i = rc of F's at
 // t = w-1-i) and o = 2 (R[0, h) = rc F[n-h, n): m-mer i = rc of F's at
 // t = n-m-i), both rolled towards smaller t, one base per step; the same
 // minimizer rule (order_key | i, smallest wins) as key_minimizer.  Written to
-// the dense key slots 4 a + 2 / 4 a + 3 (k_scan_reg<INDEX> writes 4 a + 0 / 1).
+// key_bk / key_ent[o * key_n + a], o = 2, 3 (k_scan_reg<INDEX> writes o = 0, 1).
 template <int MAXW>
 __global__ __launch_bounds__(kBlock) void k_rc_keys(ScanParams p) {
   const uint64_t a = p.a_lo + (uint64_t)blockIdx.x * kBlock + threadIdx.x;
@@ -1256,18 +1085,11 @@ __global__ __launch_bounds__(kBlock) void k_rc_keys(ScanParams p) {
     }
   }
   const uint64_t v2 = mix64(mb2), v3 = mix64(mb3);
-  if (!p.join_P) {  // cell index: (bucket, entry) records, o-major
-    const uint64_t nbm = (1ULL << p.nb_log2) - 1;
-    p.key_bk[2 * p.key_n + a] = n ? (uint32_t)(v2 & nbm) : 0u;
-    p.key_ent[2 * p.key_n + a] = n ? make_entry(v2, p.nb_log2, (int)(kb2 & 1023u), 2, (uint32_t)a) : kEmpty;
-    p.key_bk[3 * p.key_n + a] = n ? (uint32_t)(v3 & nbm) : 0u;
-    p.key_ent[3 * p.key_n + a] = n ? make_entry(v3, p.nb_log2, (int)(kb3 & 1023u), 3, (uint32_t)a) : kEmpty;
-    return;
-  }
-  p.join_kk[4 * a + 2] = n ? join_k32(v2, p.join_P, 0u) : 0xFFFFFFFFu;
-  p.join_kv[4 * a + 2] = n ? join_key_val((uint32_t)a, 2, (int)(kb2 & 1023u), v2, p) : kFlatHole;
-  p.join_kk[4 * a + 3] = n ? join_k32(v3, p.join_P, 0u) : 0xFFFFFFFFu;
-  p.join_kv[4 * a + 3] = n ? join_key_val((uint32_t)a, 3, (int)(kb3 & 1023u), v3, p) : kFlatHole;
+  const uint64_t nbm = (1ULL << p.nb_log2) - 1;  // (bucket, entry) records, o-major
+  p.key_bk[2 * p.key_n + a] = n ? (uint32_t)(v2 & nbm) : 0u;
+  p.key_ent[2 * p.key_n + a] = n ? make_entry(v2, p.nb_log2, (int)(kb2 & 1023u), 2, (uint32_t)a) : kEmpty;
+  p.key_bk[3 * p.key_n + a] = n ? (uint32_t)(v3 & nbm) : 0u;
+  p.key_ent[3 * p.key_n + a] = n ? make_entry(v3, p.nb_log2, (int)(kb3 & 1023u), 3, (uint32_t)a) : kEmpty;
 }
 
 // checkOverlap's string compare (OverlapGraph.cpp:354-383) on packed words:
@@ -1308,9 +1130,6 @@ struct ProbeParams {
   const unsigned long long* run_cnt;
   uint64_t run_cap;
   uint64_t run_regions;           // probe wavefront r consumes run regions r, r + nw, r + 2 nw, ... < run_regions
-  const uint64_t* fkeys;          // non-null: runs as SoA (x, meta), region r = [r * run_cap, + run_cnt[r])
-  const uint64_t* fmeta;
-  int pack_a, pack_w;             // pack_a > 0: fkeys holds 32-bit packed keys (run_unpack)
   const uint32_t* src_super;      // runs of sources with superReadID != 0 are dropped (:548; nullptr: none)
   uint64_t src_lo, src_hi;        // only runs of sources in [src_lo, src_hi) (src_hi = 0: all)
   uint32_t* rows;                 // 3 dwords per row (mg_edge); one region per wavefront
@@ -1320,23 +1139,17 @@ struct ProbeParams {
   unsigned long long* stats;      // optional [kSegs*4]: runs probed, entries scanned, partners fetched, rows
   int phase_limit;                // diagnostics: 4 no probe, 5 + cell loads, 6 + filter, 7 full
   int halving_low;                // option "halving" = 1: keep o=2/3 pairs at the lower ID (else rc_side_keeps)
+  // the halving rule's read numbers: slots (nullptr) when every context that
+  // shares the work has the same slot order (one context; the exchange mode's
+  // ranks, whose layouts are identical), reference IDs (slot -> ID - 1) for
+  // source-range shards, whose layouts group their own range
+  const uint32_t* halving_id;
   int contain_even;               // CONTAIN: drop o = 1/3 hits (k_prefix_contain finds the s = 0 containments)
   int contain_minlen;             // CONTAIN (with contain_even): drop runs whose first window jlo > n1 - minlen
   int contain_prune;              // CONTAIN: skip a candidate whose container cannot raise the superkey
   int contain_skip;               // CONTAIN: skip runs of sources already contained (their superkey != 0)
   int compact;                    // park the live items of sparse run batches (filled batches only)
   int share;                      // a block's wavefronts share its regions batch by batch (probe_share)
-  int share_xcd;                  // with share: blocks take region quadruples XCD-major (probe_share_xcd)
-  int src_len_lo, src_len_hi;     // CONTAIN: only sources with length in [lo, hi) (hi = 0: all)
-  // split path (k_probe<SPLIT=true> + k_verify): candidates {partner, source, o << 30 | j}
-  uint3* cand;                    // one region of cand_cap records per probe wavefront
-  unsigned long long* cand_cnt;   // [waves] candidates written (may exceed cand_cap)
-  uint64_t cand_cap;
-  // xcd_map: run regions are dealt XCD by XCD (blockIdx % 8 shares an XCD): the
-  // waves of one XCD take consecutive regions of one contiguous share of the
-  // bucket-sorted runs, so at any moment they probe one narrow bucket window
-  // whose cells and partner slots stay in that XCD's L2
-  int xcd_map;
   const uint32_t* id;             // slot -> reference ID - 1 (nullptr: ID order); rows and superkeys carry IDs
 };
 
@@ -1360,8 +1173,6 @@ struct ProbeLds {
   static constexpr size_t o_ci = o_cb + CAND * 4;                       // [CAND] u32 o << 30 | j
   static constexpr size_t o_ca = o_ci + CAND * 4;                       // [CAND] u32 source read
   static constexpr size_t bytes = o_ca + CAND * 4;
-  // split path (k_probe<.., SPLIT = true>): only the pending arrays, at offset 0
-  static constexpr size_t split_bytes = 2 * PEND * 8;
 };
 
 // Probe wavefront r consumes its run regions in batches of 64 probe items (one
@@ -1380,15 +1191,15 @@ struct ProbeLds {
 #ifndef MG_PROBE_WAVES
 #define MG_PROBE_WAVES 1
 #endif
-template <int MAXW, bool CONTAIN, bool SPLIT>
+template <int MAXW, bool CONTAIN>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MG_PROBE_WAVES))) void k_probe(ProbeParams p) {
   using PL = ProbeLds<MAXW>;
   extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  unsigned char* base = reinterpret_cast<unsigned char*>(smem) + (size_t)wv * (SPLIT ? PL::split_bytes : PL::bytes);
+  unsigned char* base = reinterpret_cast<unsigned char*>(smem) + (size_t)wv * PL::bytes;
   uint64_t* s_a = reinterpret_cast<uint64_t*>(base + PL::o_a);
-  uint64_t* s_pk = reinterpret_cast<uint64_t*>(base + (SPLIT ? 0 : PL::o_pk));
-  uint64_t* s_pm = reinterpret_cast<uint64_t*>(base + (SPLIT ? PL::PEND * 8 : PL::o_pm));
+  uint64_t* s_pk = reinterpret_cast<uint64_t*>(base + PL::o_pk);
+  uint64_t* s_pm = reinterpret_cast<uint64_t*>(base + PL::o_pm);
   uint32_t* s_cb = reinterpret_cast<uint32_t*>(base + PL::o_cb);
   uint32_t* s_ci = reinterpret_cast<uint32_t*>(base + PL::o_ci);
   uint32_t* s_ca = reinterpret_cast<uint32_t*>(base + PL::o_ca);
@@ -1399,8 +1210,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MG_PROBE
   const uint32_t seg = (uint32_t)(gw & (kSegs - 1));
   uint32_t* const region = p.rows + gw * p.reg_cap * 3;
   uint64_t cursor = 0;
-  uint3* const cregion = SPLIT ? p.cand + gw * p.cand_cap : nullptr;
-  uint64_t ccur = 0;
   uint32_t st_runs = 0, st_ent = 0, st_ver = 0, st_rows = 0;
   uint32_t ncand = 0, npend = 0;
 
@@ -1519,43 +1328,21 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MG_PROBE
   uint32_t rg = 0;
   uint64_t rpos = 0, rcnt = 0;
   const ulonglong2* rbase = p.runs;
-  uint64_t rbase_i = 0;
-  // region sequence of this wavefront: first, first + stride, ... < rlimit
-  uint64_t rfirst = gw, rstride = nwp, rlimit = p.run_regions;
-  if (p.xcd_map) {
-    const uint64_t G = gridDim.x, x = blockIdx.x & 7u;
-    const uint64_t bx = (G + 7 - x) >> 3;  // blocks sharing this XCD
-    uint64_t before = 0;                     // waves of the XCD groups before x
-    for (uint64_t y = 0; y < x; ++y) before += ((G + 7 - y) >> 3) * kWavesPerBlock;
-    const uint64_t wx = bx * kWavesPerBlock;
-    const uint64_t lo = p.run_regions * before / nwp, hi = p.run_regions * (before + wx) / nwp;
-    rfirst = lo + (blockIdx.x >> 3) * kWavesPerBlock + wv;
-    rstride = wx;
-    rlimit = hi;
-  }
+  const uint64_t rlimit = p.run_regions;
   // share (option probe_share): the block's 4 wavefronts walk the SAME regions
   // (4 b .. 4 b + 3, then + nwp, ...) and take every 4th batch of each, so a
   // block probes one scan group of 64 neighbouring reads at a time and their
-  // shared cells and partner slots stay in its CU's L1 and its XCD's L2
-  const bool share = p.share && !p.xcd_map;
+  // shared cells and partner slots stay in its CU's L1 and its XCD's L2;
+  // otherwise wavefront gw walks regions gw, gw + nwp, ...
+  const bool share = p.share != 0;
   const uint64_t rstep = share ? (uint64_t)kWavesPerBlock * kWave : (uint64_t)kWave;
-  // share_xcd: blocks renumbered XCD-major (block b runs on XCD b % 8), so the
-  // blocks of one XCD take neighbouring region quadruples
-  uint64_t lblock = blockIdx.x;
-  if (share && p.share_xcd) {
-    const uint64_t G = gridDim.x, x = blockIdx.x & 7u;
-    uint64_t before = 0;
-    for (uint64_t y = 0; y < x; ++y) before += (G + 7 - y) >> 3;
-    lblock = before + (blockIdx.x >> 3);
-  }
   auto reg_of = [&](uint32_t r) -> uint64_t {
-    return share ? (uint64_t)(r >> 2) * nwp + lblock * kWavesPerBlock + (r & 3u)
-                 : rfirst + (uint64_t)r * rstride;
+    return share ? (uint64_t)(r >> 2) * nwp + (uint64_t)blockIdx.x * kWavesPerBlock + (r & 3u)
+                 : gw + (uint64_t)r * nwp;
   };
   auto open_region = [&](uint32_t r) {
     const uint64_t reg = reg_of(r);
-    rbase = p.runs + (p.fkeys ? 0 : reg * p.run_cap);
-    rbase_i = reg * p.run_cap;
+    rbase = p.runs + reg * p.run_cap;
     const uint64_t c = p.run_cnt[reg];
     rcnt = c < p.run_cap ? c : p.run_cap;
     rpos = share ? (uint64_t)wv * kWave : 0;
@@ -1577,12 +1364,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MG_PROBE
   auto hbm_fetch = [&]() {
     const uint64_t k = rpos + (uint64_t)lane;
     pf_ok = pf_any && k < rcnt;
-    if (p.fkeys) {
-      const uint64_t i = rbase_i + (pf_ok ? k : 0);
-      rec_pf = make_ulonglong2(p.pack_a ? reinterpret_cast<const uint32_t*>(p.fkeys)[i] : p.fkeys[i], p.fmeta[i]);
-    } else {
-      rec_pf = rbase[pf_ok ? k : 0];
-    }
+    rec_pf = rbase[pf_ok ? k : 0];
   };
 
   auto take_item = [&](uint64_t& key, uint64_t& meta, bool& valid) -> bool {
@@ -1596,15 +1378,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MG_PROBE
     }
     if (pf_any) {
       valid = pf_ok && rec_pf.y != kFlatHole;
-      uint64_t bucket;
-      uint32_t fpv;
-      if (p.pack_a) {
-        run_unpack((uint32_t)rec_pf.x, rec_pf.y, p.nb_log2, p.pack_a, p.pack_w, &bucket, &fpv, &meta);
-      } else {
-        meta = rec_pf.y;
-        bucket = rec_pf.x & nbmask;
-        fpv = (uint32_t)(rec_pf.x >> p.nb_log2) & kFpMask;
-      }
+      meta = rec_pf.y;
+      const uint64_t bucket = rec_pf.x & nbmask;
+      const uint32_t fpv = (uint32_t)(rec_pf.x >> p.nb_log2) & kFpMask;
       if (valid && (p.src_super || p.src_hi)) {  // contained or foreign sources contribute no windows
         const uint32_t ra = (uint32_t)meta;
         if ((p.src_super && p.src_super[ra]) || (p.src_hi && (ra < p.src_lo || ra >= p.src_hi))) valid = false;
@@ -1612,11 +1388,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MG_PROBE
       // containment: read2 sits at s = j <= n1 - n2 <= n1 - minlen, so a run
       // whose first window lies beyond that finds nothing (o = 1/3, the s = 0
       // side, is k_prefix_contain's when contain_even)
-      if (CONTAIN && valid && (p.contain_minlen || p.src_len_hi || p.contain_skip)) {
+      if (CONTAIN && valid && (p.contain_minlen || p.contain_skip)) {
         const uint32_t ra = (uint32_t)meta;
         const int n1 = p.uniform_len ? p.uniform_len : (int)p.len[ra];
         if (p.contain_minlen && (int)((meta >> 42) & 1023u) > n1 - p.contain_minlen) valid = false;
-        if (p.src_len_hi && (n1 < p.src_len_lo || n1 >= p.src_len_hi)) valid = false;
         // a source that is itself contained (in a longer read C) never holds
         // a partner's final superReadID: every read2 it contains is also in
         // C, which is longer, and the longest container is never contained
@@ -1716,6 +1491,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MG_PROBE
     }
     npend += (uint32_t)__popcll(cb);
     uint32_t keepm = 0;
+    const uint32_t ra_h = (!CONTAIN && p.halving_id && valid) ? p.halving_id[ra] : ra;
 #pragma unroll
     for (int s = 0; s < kCell; ++s) {
       const uint32_t hi = (uint32_t)(e[s] >> 32);
@@ -1724,30 +1500,16 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MG_PROBE
       bool keep = e[s] != kEmpty && ((hi >> 12) & kFpMask) == fp && j >= rjlo && j <= rjhi;
       // halving: o=1 hits are twins of the partner's o=0
       // hits; an o=2/3 pair is kept on one side only (rc_side_keeps)
-      keep = keep && (CONTAIN || oo == 0 ||
-                      (oo >= 2 && (p.halving_low ? (uint32_t)e[s] >= ra : rc_side_keeps(ra, (uint32_t)e[s]))));
+      bool side = true;
+      if (!CONTAIN && oo >= 2 && keep) {
+        const uint32_t bh = p.halving_id ? p.halving_id[(uint32_t)e[s]] : (uint32_t)e[s];
+        side = p.halving_low ? bh >= ra_h : rc_side_keeps(ra_h, bh);
+      }
+      keep = keep && (CONTAIN || oo == 0 || (oo >= 2 && side));
       // containment with k_prefix_contain covering offset s = 0: suffix-key
       // hits (o = 1/3) add nothing (see the verify's CONTAIN case)
       keep = keep && !(CONTAIN && p.contain_even && (oo & 1));
       keepm |= (keep ? 1u : 0u) << s;
-    }
-    if (SPLIT) {
-      // candidates straight to this wavefront's HBM region (k_verify checks them)
-#pragma unroll
-      for (int s = 0; s < kCell; ++s) {
-        const bool k = (keepm >> s) & 1u;
-        const uint64_t bal = __ballot(k);
-        if (bal) {
-          if (k) {
-            const uint32_t hi = (uint32_t)(e[s] >> 32);
-            const uint64_t at = ccur + lane_prefix(bal);
-            if (at < p.cand_cap)
-              cregion[at] = make_uint3((uint32_t)e[s], ra, ((hi & 3u) << 30) | (uint32_t)(rp - (int)((hi >> 2) & 1023u)));
-          }
-          ccur += (uint64_t)__popcll(bal);
-        }
-      }
-      return;
     }
     while (__ballot(keepm != 0)) {
       // append slot groups while they fit, then verify a full wavefront
@@ -1807,9 +1569,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MG_PROBE
       key_c = key_n; meta_c = meta_n; val_c = val_n;
     }
   }
-  if (!SPLIT && ncand && p.phase_limit > 6) verify(ncand);
-  if (SPLIT && lane == 0) p.cand_cnt[gw] = ccur;
-  if (!SPLIT && !CONTAIN && lane == 0) p.reg_cnt[gw] = cursor;
+  if (ncand && p.phase_limit > 6) verify(ncand);
+  if (!CONTAIN && lane == 0) p.reg_cnt[gw] = cursor;
   if (p.stats) {
     uint32_t v[4] = {st_runs, st_ent, st_ver, st_rows};
 #pragma unroll
@@ -1820,537 +1581,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MG_PROBE
       if (lane == 0) atomicAdd(&p.stats[seg * 4 + i], (unsigned long long)x);
     }
   }
-}
-
-// Split path, stage 2 helpers.  One candidate {partner, source, o << 30 | j}
-// -> the overlap to compare: L bases of the source at x0 (reverse strand when
-// rcA) against the partner's forward bases at y0 (checkOverlap,
-// OverlapGraph.cpp:354-383; checkOverlapForContainedRead :302-340).
-struct Cand {
-  uint32_t bid, sa;
-  int o, j, n1, n2, L, x0, y0;
-  bool cond, rcA;
-};
-
-template <bool CONTAIN>
-__device__ __forceinline__ Cand cand_setup(const ProbeParams& p, uint3 c, bool have) {
-  Cand k{};
-  k.bid = c.x;
-  k.sa = c.y;
-  if (!have) return k;
-  const int h = p.h;
-  k.o = (int)(c.z >> 30);
-  k.j = (int)(c.z & 1023u);
-  k.n1 = p.uniform_len ? p.uniform_len : (int)p.len[k.sa];
-  k.n2 = p.uniform_len ? p.uniform_len : (int)p.len[k.bid];
-  const int o = k.o, j = k.j, n1 = k.n1, n2 = k.n2;
-  if (!CONTAIN) {
-    if (o == 0) {        // F1[j, n1) == F2[0, L)
-      k.L = n1 - j; k.cond = k.L < n2; k.x0 = j; k.y0 = 0; k.rcA = false;
-    } else if (o == 2) { // F1[j, n1) == R2[0, L)  <=>  R1[0, L) == F2[n2-L, n2)
-      k.L = n1 - j; k.cond = k.L < n2; k.x0 = 0; k.y0 = n2 - k.L; k.rcA = true;
-    } else {             // F1[0, L) == R2[n2-L, n2)  <=>  R1[n1-L, n1) == F2[0, L)
-      k.L = j + h; k.cond = j <= n2 - h; k.x0 = n1 - k.L; k.y0 = 0; k.rcA = true;
-    }
-  } else {
-    int sft;
-    k.cond = n1 > n2;
-    if (o == 0 || o == 2) {
-      k.cond = k.cond && (j <= n1 - n2);
-      sft = j;
-    } else {
-      k.cond = k.cond && (j == n2 - h);  // s = 0 only: s >= 1 is the o = 0/2 hit's (k_probe verify)
-      sft = j - (n2 - h);
-    }
-    k.L = n2;
-    k.y0 = 0;
-    k.rcA = o >= 2;
-    k.x0 = k.rcA ? n1 - sft - n2 : sft;
-  }
-  return k;
-}
-
-// the partner words [y0, y0 + L) spans: all inside the partner's own slot
-template <int MAXW>
-__device__ __forceinline__ void cand_load(const ProbeParams& p, const Cand& k, uint64_t* y) {
-  const uint64_t* bg = p.words + (uint64_t)k.bid * slot_words(MAXW) + (k.y0 >> 5);
-  const int need = (((k.y0 & 31) + k.L - 1) >> 5) + 1;
-#pragma unroll
-  for (int w = 0; w <= MAXW; ++w) y[w] = (k.cond && w < need) ? bg[w] : 0;
-}
-
-// compare against the source slot (read straight from memory: the candidates
-// of a batch come from a handful of consecutive source reads, so these are
-// L1/L2 hits)
-template <int MAXW>
-__device__ __forceinline__ bool cand_match(const ProbeParams& p, const Cand& k, const uint64_t* y) {
-  const uint64_t* f1 = p.words + (uint64_t)k.sa * slot_words(MAXW);
-  const int ys = (k.y0 & 31) << 1;
-  uint64_t diff = 0;
-#pragma unroll
-  for (int cc = 0; cc < MAXW; ++cc) {
-    if (cc * 32 < k.L) {
-      const uint64_t av = k.rcA ? rc_word(ext_fwd<1>(f1, k.n1 - k.x0 - 32 * cc - 32)) : ext_fwd<1>(f1, k.x0 + 32 * cc);
-      const uint64_t bv = funnel(y[cc], y[cc + 1], ys);
-      const int rem = k.L - 32 * cc;
-      const uint64_t msk = rem >= 32 ? ~0ULL : ~(~0ULL >> (2 * rem));
-      diff |= (av ^ bv) & msk;
-    }
-  }
-  return diff == 0;
-}
-
-// Split path, stage 2: verify the candidates of k_probe<SPLIT>, two batches of
-// 64 per trip (two partner slots in flight per lane; the next pair's candidate
-// records load behind them).  A verified discovery becomes a row + twin
-// (insertEdge :407-419, orientation/offset switch :550-557, twin :841-855) in
-// this wavefront's row region, or a superReadID key (atomicMax) in CONTAIN
-// mode.  Wavefront r verifies the candidate regions r, r + nw, ... of the probe.
-template <int MAXW, bool CONTAIN>
-__global__ __launch_bounds__(kBlock) void k_verify(ProbeParams p, uint64_t cand_regions) {
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int h = p.h;
-  const uint64_t gw = (uint64_t)blockIdx.x * kWavesPerBlock + wv;
-  const uint64_t nw = (uint64_t)gridDim.x * kWavesPerBlock;
-  const uint32_t seg = (uint32_t)(gw & (kSegs - 1));
-  uint32_t* const region = p.rows + gw * p.reg_cap * 3;
-  uint64_t cursor = 0;
-  uint32_t st_ver = 0, st_rows = 0;
-
-  auto emit = [&](const Cand& k, bool ok) {
-    int nrec = 0;
-    uint32_t r2 = 0, t2 = 0;
-    if (ok) {
-      if (CONTAIN) {
-        atomicMax(&p.superkey[k.bid], ((unsigned long long)k.n1 << 32) | (0xFFFFFFFFu - rid(p.id, k.sa)));
-      } else if (!(p.super && p.super[k.bid])) {  // :548 read2 contained
-        const uint32_t orient = (k.o == 0) ? 3u : (k.o == 2 ? 2u : 1u);
-        const uint32_t off = (k.o == 3) ? (uint32_t)(k.n1 - h - k.j) : (uint32_t)k.j;
-        const uint32_t torient = (orient == 3u) ? 0u : orient;
-        const uint32_t toff = (uint16_t)(k.n2 + off - k.n1);
-        r2 = (orient << 16) | off;
-        t2 = (torient << 16) | toff;
-        nrec = (k.bid == k.sa && k.o == 0) ? 4 : 2;  // self o=0 hit also stands for its o=1 twin
-        st_rows += nrec;
-      }
-    }
-    if (CONTAIN) return;
-    const uint64_t b2 = __ballot(nrec >= 2), b4 = __ballot(nrec == 4);
-    const uint32_t tot = 2u * (uint32_t)(__popcll(b2) + __popcll(b4));
-    if (tot) {
-      if (cursor + tot <= p.reg_cap) {
-        const uint32_t pr = 2u * (lane_prefix(b2) + lane_prefix(b4));
-        uint3* d = reinterpret_cast<uint3*>(region + (cursor + pr) * 3);
-        for (int rr = 0; rr < nrec; rr += 2) {
-          const uint32_t ia = rid(p.id, k.sa) + 1, ib = rid(p.id, k.bid) + 1;
-          d[0] = make_uint3(ia, ib, r2);
-          d[1] = make_uint3(ib, ia, t2);
-          d += 2;
-        }
-      }
-      cursor += tot;  // keeps counting past the capacity: the host resizes and reruns
-    }
-  };
-
-  for (uint64_t cr = gw; cr < cand_regions; cr += nw) {
-    const uint3* cbase = p.cand + cr * p.cand_cap;
-    uint64_t cn = p.cand_cnt[cr];
-    cn = cn < p.cand_cap ? cn : p.cand_cap;
-    uint3 nA = (uint64_t)lane < cn ? cbase[lane] : make_uint3(0, 0, 0);
-    uint3 nB = (uint64_t)lane + kWave < cn ? cbase[kWave + lane] : make_uint3(0, 0, 0);
-    for (uint64_t b0 = 0; b0 < cn; b0 += 2 * kWave) {
-      const bool hA = b0 + lane < cn, hB = b0 + kWave + lane < cn;
-      const Cand kA = cand_setup<CONTAIN>(p, nA, hA);
-      const Cand kB = cand_setup<CONTAIN>(p, nB, hB);
-      uint64_t yA[MAXW + 1], yB[MAXW + 1];
-      cand_load<MAXW>(p, kA, yA);
-      cand_load<MAXW>(p, kB, yB);
-      const uint64_t q = b0 + 2 * kWave + lane;
-      nA = q < cn ? cbase[q] : make_uint3(0, 0, 0);
-      nB = q + kWave < cn ? cbase[q + kWave] : make_uint3(0, 0, 0);
-      const bool okA = kA.cond && cand_match<MAXW>(p, kA, yA);
-      const bool okB = kB.cond && cand_match<MAXW>(p, kB, yB);
-      st_ver += (kA.cond ? 1u : 0u) + (kB.cond ? 1u : 0u);
-      emit(kA, okA);
-      emit(kB, okB);
-    }
-  }
-  if (!CONTAIN && lane == 0) p.reg_cnt[gw] = cursor;
-  if (p.stats) {
-    uint32_t v[2] = {st_ver, st_rows};
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      uint32_t x = v[i];
-#pragma unroll
-      for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d);
-      if (lane == 0) atomicAdd(&p.stats[seg * 4 + 2 + i], (unsigned long long)x);
-    }
-  }
-}
-
-// ----------------------------------------------------------- k_join ---
-// One partition of the sorted join records at a time per workgroup (dynamic
-// queue): the partition's keys are filed into an exact-key index in LDS, then
-// every run of the partition looks its minimizer up there.  The LDS index is
-// the global cell index in small: kJoinCells cells of kCell 8-B entries
-// (read | fp19 << 32 | q << 51 | o << 61, fp = H32 bits 13..31), cell =
-// H32 mod kJoinCells; a key takes the next free entry of its cell (LDS
-// atomicAdd on the cell's count) or, when the cell is full, of the following
-// cells, so a lookup reads one 64-B cell and continues only while the count
-// says a key went past it.  A run's candidate is an entry with its
-// fingerprint and a q such that j = p - q lies in the run's window range
-// [jlo, jhi]: the exact candidate of getListOfReads(F1[j, j+h))
-// (HashTable.cpp:202-221) that the reference meets at window j
-// (OverlapGraph.cpp:534-547).  Candidates go to a per-wavefront LDS ring and
-// are verified 64 at a time against both reads' slots (checkOverlap :354-383 /
-// checkOverlapForContainedRead :302-340), the source read's words in
-// registers.  More keys than kJoinCap: the index is refilled per chunk of
-// keys and the runs are streamed again (skewed partitions).  CONTAIN with
-// prefix queries: every o = 0 key of the partition also looks up shorter reads
-// whose o = 0/2 key is the same string at the same q (a prefix of read1 at
-// offset 0, which the reference meets only through the shorter read's suffix
-// key): the k_prefix_contain rule.
-constexpr int kJoinBlock = 512;
-constexpr int kJoinWaves = kJoinBlock / kWave;
-constexpr int kJoinCells = 1024;                 // LDS cells of kCell entries (64 KiB)
-constexpr int kJoinCap = kJoinCells * kCell / 2;  // keys per fill (cells at most half full)
-constexpr int kJoinRing = 128;                   // per-wavefront candidate ring
-constexpr size_t kJoinLds = (size_t)kJoinCells * kCell * 8 + (size_t)kJoinCells * 4 +
-                            (size_t)kJoinWaves * kJoinRing * 10 + 16;
-
-struct JoinParams {
-  const uint64_t* words;
-  const uint16_t* len;
-  const uint32_t* id;                // slot -> reference ID - 1 (nullptr: ID order)
-  int h, P, A, QB, WB;
-  const uint32_t* k32;               // sorted join records
-  const uint64_t* val;
-  const unsigned long long* bnd;     // [nparts + 1] first record of each partition (its keys come first)
-  const unsigned long long* mid;     // [nparts] first run record of each partition
-  uint32_t nparts;
-  unsigned int* queue;               // partition dequeue counter (zeroed before the launch)
-  const uint32_t* super;             // discovery: partners with superReadID != 0 dropped at emit (:548)
-  const uint32_t* src_super;         // discovery: runs of contained sources dropped (:548)
-  uint64_t src_lo, src_hi;           // only runs of sources in [src_lo, src_hi) (src_hi = 0: all)
-  unsigned long long* superkey;      // CONTAIN: max (len << 32 | ~index) per contained read
-  int contain_even;                  // CONTAIN: drop o = 1/3 hits (the prefix queries cover s = 0)
-  int prefix_queries;                // CONTAIN: o = 0 keys query the index (offset-0 containments)
-  uint32_t* rows;                    // 3 dwords per row, one region per wavefront
-  unsigned long long* reg_cnt;
-  uint64_t reg_cap;
-  int uniform_len, halving_low;
-  unsigned long long* stats;         // optional [kSegs * 4]: runs, entries, verified, rows
-  int phase_limit;                   // diagnostics: 5 index only, 6 + lookups (no candidates), 7 full
-};
-
-// 32 bases of a read held in registers starting at pos (pos >= -31; bases
-// before 0 read as 0)
-template <int MAXW>
-__device__ __forceinline__ uint64_t ext_reg_s(const uint64_t* rw, int pos) {
-  const uint64_t neg = rw[0] >> ((pos < 0 ? -pos : 0) * 2);
-  const uint64_t x = ext_reg<MAXW>(rw, pos < 0 ? 0 : pos);
-  return pos < 0 ? neg : x;
-}
-
-__device__ __forceinline__ uint32_t join_cell(uint32_t H) { return H & (kJoinCells - 1); }
-
-template <int MAXW, bool CONTAIN>
-__global__ __launch_bounds__(kJoinBlock) void k_join(JoinParams p) {
-  extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  uint64_t* const cells = smem;                                                   // [kJoinCells][kCell]
-  uint32_t* const ccnt = reinterpret_cast<uint32_t*>(smem + kJoinCells * kCell);  // [kJoinCells]
-  uint32_t* const rbase = ccnt + kJoinCells;
-  uint32_t* const rb = rbase + (size_t)wv * kJoinRing * 2;  // ring: partner [128] | source [128]
-  uint16_t* const ri = reinterpret_cast<uint16_t*>(rbase + (size_t)kJoinWaves * kJoinRing * 2) +
-                       (size_t)wv * kJoinRing;              // ring: o << 10 | j
-  uint32_t* const s_part = reinterpret_cast<uint32_t*>(ri + (size_t)(kJoinWaves - wv) * kJoinRing);
-  const int h = p.h, P = p.P, A = p.A;
-  const uint64_t amask = (1ULL << A) - 1;
-  const int run_sh = A + 10 + 2 * p.WB, key_sh = A + 2 + p.QB;
-  const uint64_t gw = (uint64_t)blockIdx.x * kJoinWaves + wv;
-  const uint32_t seg = (uint32_t)(gw & (kSegs - 1));
-  uint32_t* const region = p.rows + gw * p.reg_cap * 3;
-  uint64_t cursor = 0;
-  uint32_t st_runs = 0, st_ent = 0, st_ver = 0, st_rows = 0, st_trips = 0;
-  uint32_t rhead = 0, rcnt = 0;  // candidate ring (wavefront-uniform)
-
-  // verify the first k (<= 64) candidates of the ring, one per lane
-  auto verify = [&](uint32_t k) {
-    const bool have = (uint32_t)lane < k;
-    int nrec = 0;
-    uint32_t r2 = 0, t2 = 0;
-    uint32_t bid = 0, sa = 0;
-    int n1 = 0, n2 = 0, o = 0, j = 0, x0 = 0, y0 = 0, L = 0;
-    bool cond = false, rcA = false;
-    if (have) {
-      const uint32_t at = (rhead + lane) & (kJoinRing - 1);
-      bid = rb[at];
-      sa = rb[kJoinRing + at];
-      const uint32_t info = ri[at];
-      o = (int)(info >> 10);
-      j = (int)(info & 1023u);
-      n1 = p.uniform_len ? p.uniform_len : (int)p.len[sa];
-      n2 = p.uniform_len ? p.uniform_len : (int)p.len[bid];
-      if (!CONTAIN) {
-        if (o == 0) {        // F1[j, n1) == F2[0, L)
-          L = n1 - j; cond = L < n2; x0 = j; y0 = 0; rcA = false;
-        } else if (o == 2) { // F1[j, n1) == R2[0, L)  <=>  R1[0, L) == F2[n2-L, n2)
-          L = n1 - j; cond = L < n2; x0 = 0; y0 = n2 - L; rcA = true;
-        } else {             // F1[0, L) == R2[n2-L, n2)  <=>  R1[n1-L, n1) == F2[0, L)
-          L = j + h; cond = j <= n2 - h; x0 = n1 - L; y0 = 0; rcA = true;
-        }
-      } else {
-        int sft;
-        cond = n1 > n2;
-        if (o == 0 || o == 2) {
-          cond = cond && (j <= n1 - n2);
-          sft = j;
-        } else {  // o = 1/3: only s = 0 (see k_probe's verify)
-          cond = cond && (j == n2 - h);
-          sft = 0;
-        }
-        L = n2;
-        y0 = 0;
-        rcA = o >= 2;
-        x0 = rcA ? n1 - sft - n2 : sft;
-      }
-    }
-    rhead += k;
-    rcnt -= k;
-    uint64_t y[MAXW + 1], xs[MAXW + 1];
-    load_slot<MAXW>(p.words, cond ? bid : 0u, y);  // partner slot (random line)
-    load_slot<MAXW>(p.words, cond ? sa : 0u, xs);  // source slot (random line)
-    if (cond) {
-      ++st_ver;
-      uint64_t diff = 0;
-#pragma unroll
-      for (int kk = 0; kk < MAXW; ++kk) {
-        const int lo = max(y0 - 32 * kk, 0), hi = min(y0 + L - 32 * kk, 32);
-        if (hi > lo) {
-          const int s = x0 - y0 + 32 * kk;  // source position of partner base 32 kk
-          const uint64_t av = rcA ? rc_word(ext_reg_s<MAXW>(xs, n1 - s - 32)) : ext_reg_s<MAXW>(xs, s);
-          const uint64_t msk = (lo ? (~0ULL >> (2 * lo)) : ~0ULL) & (hi < 32 ? ~(~0ULL >> (2 * hi)) : ~0ULL);
-          diff |= (av ^ y[kk]) & msk;
-        }
-      }
-      if (diff == 0) {
-        if (CONTAIN) {
-          atomicMax(&p.superkey[bid], ((unsigned long long)n1 << 32) | (0xFFFFFFFFu - rid(p.id, sa)));
-        } else if (!(p.super && p.super[bid])) {  // :548 read2 contained
-          // orientation/offset switch (:550-557) and the twin (:409-412, :841-855)
-          const uint32_t orient = (o == 0) ? 3u : (o == 2 ? 2u : 1u);
-          const uint32_t off = (o == 3) ? (uint32_t)(n1 - h - j) : (uint32_t)j;
-          const uint32_t torient = (orient == 3u) ? 0u : orient;
-          r2 = (orient << 16) | off;
-          t2 = (torient << 16) | (uint32_t)(uint16_t)(n2 + off - n1);
-          nrec = (bid == sa && o == 0) ? 4 : 2;  // a self o = 0 hit also stands for its o = 1 twin
-          st_rows += nrec;
-        }
-      }
-    }
-    if (!CONTAIN) {
-      const uint64_t b2 = __ballot(nrec >= 2), b4 = __ballot(nrec == 4);
-      const uint32_t tot = 2u * (uint32_t)(__popcll(b2) + __popcll(b4));
-      if (tot) {
-        if (cursor + tot <= p.reg_cap) {
-          const uint32_t pr = 2u * (lane_prefix(b2) + lane_prefix(b4));
-          uint3* d = reinterpret_cast<uint3*>(region + (cursor + pr) * 3);
-          for (int rr = 0; rr < nrec; rr += 2) {
-            const uint32_t ia = rid(p.id, sa) + 1, ib = rid(p.id, bid) + 1;
-            d[0] = make_uint3(ia, ib, r2);
-            d[1] = make_uint3(ib, ia, t2);
-            d += 2;
-          }
-        }
-        cursor += tot;  // keeps counting past the capacity: the host resizes and reruns
-      }
-    }
-  };
-
-  // append one candidate per flagged lane to the ring; verify full batches
-  auto push = [&](bool flag, uint32_t b, uint32_t info, uint32_t a) {
-    const uint64_t bal = __ballot(flag);
-    if (!bal) return;
-    if (flag) {
-      const uint32_t at = (rhead + rcnt + lane_prefix(bal)) & (kJoinRing - 1);
-      rb[at] = b;
-      rb[kJoinRing + at] = a;
-      ri[at] = (uint16_t)info;
-    }
-    rcnt += (uint32_t)__popcll(bal);
-    if (rcnt >= (uint32_t)kWave) {
-      wave_sync();
-      verify(kWave);
-      wave_sync();
-    }
-  };
-
-  for (;;) {
-    __syncthreads();  // every wave is done with the previous partition's index and s_part
-    if (threadIdx.x == 0) s_part[0] = atomicAdd(p.queue, 1u);
-    __syncthreads();
-    const uint32_t f = s_part[0];
-    if (f >= p.nparts) break;
-    const uint64_t kb = p.bnd[f], kr = p.mid[f], ke = p.bnd[f + 1];
-    if (kr == kb) continue;                                    // no keys: nothing to find
-    if (ke == kr && !(CONTAIN && p.prefix_queries)) continue;  // no runs and no prefix queries
-    for (uint64_t c0 = kb; c0 < kr; c0 += kJoinCap) {
-      const uint64_t c1 = min(kr, c0 + (uint64_t)kJoinCap);
-      if (c0 != kb) __syncthreads();  // the previous chunk's lookups are done
-      for (int i = threadIdx.x; i < kJoinCells; i += kJoinBlock) ccnt[i] = 0;
-      __syncthreads();
-      // the chunk's keys into the LDS cells
-      for (uint64_t i = c0 + threadIdx.x; i < c1; i += kJoinBlock) {
-        const uint64_t v = p.val[i];
-        const uint32_t H = join_h32(p.k32[i], v, P, key_sh);
-        const uint64_t e = (v & amask) | ((uint64_t)(H >> 13) << 32) |
-                           (((v >> (A + 2)) & ((1ULL << p.QB) - 1)) << 51) | (((v >> A) & 3u) << 61);
-        uint32_t c = join_cell(H);
-        for (;;) {  // at most half the entries are used: a free one always exists
-          const uint32_t at = atomicAdd(&ccnt[c], 1u);
-          if (at < (uint32_t)kCell) {
-            cells[c * kCell + at] = e;
-            break;
-          }
-          c = (c + 1) & (kJoinCells - 1);
-        }
-      }
-      __syncthreads();
-      // lookups: CONTAIN prefix queries (the partition's o = 0 keys), then runs
-      const uint64_t q0 = (CONTAIN && p.prefix_queries) ? kb : kr;
-      const uint64_t qe = p.phase_limit <= 5 ? q0 : ke;
-      // the next batch's records load behind the current batch's lookups
-      uint64_t nv = 0;
-      uint32_t nk = 0;
-      {
-        const uint64_t i = q0 + (uint64_t)wv * kWave + lane;
-        if (i < qe) {
-          nv = p.val[i];
-          nk = p.k32[i];
-        }
-      }
-      for (uint64_t i0 = q0 + (uint64_t)wv * kWave; i0 < qe; i0 += kJoinBlock) {
-        const uint64_t i = i0 + lane;
-        bool live = i < qe;
-        const bool is_run = i >= kr;
-        uint32_t H = 0, ra = 0;
-        int rp = 0, jlo = 0, jhi = 0, qa = 0;
-        const uint64_t v = nv;
-        const uint32_t k = nk;
-        if (i + kJoinBlock < qe) {
-          nv = p.val[i + kJoinBlock];
-          nk = p.k32[i + kJoinBlock];
-        }
-        if (live) {
-          ra = (uint32_t)(v & amask);
-          if (is_run) {
-            H = join_h32(k, v, P, run_sh);
-            jlo = (int)((v >> A) & 1023u);
-            jhi = jlo + (int)((v >> (A + 10)) & ((1ULL << p.WB) - 1));
-            rp = jhi + (int)((v >> (A + 10 + p.WB)) & ((1ULL << p.WB) - 1));
-            if ((p.src_super && p.src_super[ra]) || (p.src_hi && (ra < p.src_lo || ra >= p.src_hi))) live = false;
-          } else {  // prefix query: only o = 0 keys
-            H = join_h32(k, v, P, key_sh);
-            qa = (int)((v >> (A + 2)) & ((1ULL << p.QB) - 1));
-            if (((v >> A) & 3u) != 0) live = false;
-          }
-        }
-        if (live && is_run) ++st_runs;
-        const uint32_t fpr = H >> 13;
-        const bool rcs_low = p.halving_low != 0;
-        uint32_t c = join_cell(H);
-        while (__ballot(live)) {
-          const uint32_t cnt = live ? ccnt[c] : 0u;
-          const uint32_t nv = cnt < (uint32_t)kCell ? cnt : (uint32_t)kCell;  // entries past the count are stale
-          st_ent += nv;
-          st_trips += lane == 0 ? 1u : 0u;
-          uint64_t e[kCell];
-          {
-            const ulonglong2* cp = reinterpret_cast<const ulonglong2*>(cells + (live ? c : 0u) * kCell);
-#pragma unroll
-            for (int s2 = 0; s2 < kCell / 2; ++s2) {
-              const ulonglong2 x = cp[s2];
-              e[2 * s2] = x.x;
-              e[2 * s2 + 1] = x.y;
-            }
-          }
-          // branch-free filter of the 8 entries: fingerprint, window range, halving
-          uint32_t keepm = 0;
-#pragma unroll
-          for (int sl = 0; sl < kCell; ++sl) {
-            const uint32_t hi = (uint32_t)(e[sl] >> 32), b = (uint32_t)e[sl];
-            const int oo = (int)(hi >> 29), q = (int)((hi >> 19) & 1023u);
-            bool keep = ((uint32_t)sl < nv) & ((hi & 0x7FFFFu) == fpr);
-            if (is_run) {
-              const int j = rp - q;
-              // halving: o = 1 hits are twins of the partner's o = 0
-              // hits; an o = 2/3 pair is kept on one side only (rc_side_keeps)
-              const bool side = rcs_low ? (b >= ra) : ((b == ra) | ((((ra ^ b) & 1u) != 0) ? (b > ra) : (b < ra)));
-              const bool ok_o = CONTAIN ? !(p.contain_even && (oo & 1)) : ((oo == 0) | ((oo >= 2) & side));
-              keep = keep & (j >= jlo) & (j <= jhi) & ok_o;
-            } else {
-              // read b's o = 0/2 key is read1's o = 0 key (same string at the same q):
-              // b (or its reverse strand) may be a prefix of read1 (offset j = 0)
-              keep = keep & (q == qa) & !(oo & 1) & (b != ra);
-            }
-            keepm |= (keep ? 1u : 0u) << sl;
-          }
-          if (p.phase_limit > 6) {
-            // candidates into the ring slot by slot (one push site keeps verify inlined once)
-#pragma unroll 1
-            for (int sl = 0; sl < kCell; ++sl) {
-              const bool k = (keepm >> sl) & 1u;
-              if (!__ballot(k)) continue;
-              const uint64_t es = k ? cells[c * kCell + sl] : 0ull;
-              const uint32_t hi = (uint32_t)(es >> 32);
-              const uint32_t oo = hi >> 29;
-              const uint32_t info = is_run ? ((oo << 10) | (uint32_t)(rp - (int)((hi >> 19) & 1023u))) : (oo << 10);
-              push(k, (uint32_t)es, info, ra);
-            }
-          }
-          live = live && cnt > (uint32_t)kCell;  // a key went past this cell: continue in the next
-          c = (c + 1) & (kJoinCells - 1);
-        }
-      }
-    }
-  }
-  while (rcnt) {
-    const uint32_t k = rcnt < (uint32_t)kWave ? rcnt : (uint32_t)kWave;
-    wave_sync();
-    verify(k);
-    wave_sync();
-  }
-  if (!CONTAIN && lane == 0) p.reg_cnt[gw] = cursor;
-  if (p.stats) {
-    if (lane == 0) atomicAdd(&p.stats[kSegs * 4], (unsigned long long)st_trips);  // wavefront lookup trips
-    uint32_t vv[4] = {st_runs, st_ent, st_ver, st_rows};
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      uint32_t x = vv[i];
-#pragma unroll
-      for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d);
-      if (lane == 0) atomicAdd(&p.stats[seg * 4 + i], (unsigned long long)x);
-    }
-  }
-}
-
-// Partition bounds of the sorted join records: bnd[f] = first record whose
-// (partition, type) sort bits are >= (f, key), mid[f] = first >= (f, run).
-__global__ __launch_bounds__(kBlock) void k_join_bounds(const uint32_t* __restrict__ k32, uint64_t n, int P,
-                                                        unsigned long long* __restrict__ bnd,
-                                                        unsigned long long* __restrict__ mid, uint32_t nparts) {
-  const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
-  if (t > 2 * nparts) return;  // targets 0 .. 2 nparts: (f << 1) | type, the last = end
-  const uint32_t mask = (1u << (P + 2)) - 1, target = t;
-  uint64_t lo = 0, hi = n;
-  while (lo < hi) {
-    const uint64_t md = (lo + hi) / 2;
-    if ((k32[md] & mask) < target) lo = md + 1;
-    else hi = md;
-  }
-  if (t & 1) mid[t >> 1] = lo;
-  else bnd[t >> 1] = lo;
 }
 
 // Gather per-wavefront row regions into a contiguous array (copy-out path only).
@@ -2555,30 +1785,6 @@ __global__ __launch_bounds__(kBlock) void k_slot_regions(unsigned long long* __r
   const uint64_t K = slot / reg, blk = q / K, k = q - blk * K, t = blk / nranks, s = blk - t * nranks;
   const uint64_t start = t * slot + k * reg, c = counts[s];
   out[q] = c > start ? (c - start < reg ? c - start : reg) : 0;
-}
-
-// Region counts that tile a flat array of n records (probe input in exchange mode).
-__global__ __launch_bounds__(kBlock) void k_flat_counts(unsigned long long* cnt, uint64_t nreg, uint64_t cap,
-                                                        uint64_t n) {
-  const uint64_t r = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (r >= nreg) return;
-  const uint64_t lo = r * cap;
-  cnt[r] = lo >= n ? 0 : (n - lo < cap ? n - lo : cap);
-}
-
-// Run regions -> SoA flat arrays (x, meta) at off[r] (the sort input of option
-// "sort_runs"); one block per region.
-__global__ __launch_bounds__(kBlock) void k_runs_soa(const ulonglong2* __restrict__ runs, uint64_t cap,
-                                                     const unsigned long long* __restrict__ off,
-                                                     uint64_t* __restrict__ keys, uint64_t* __restrict__ meta) {
-  const uint64_t r = blockIdx.x;
-  const uint64_t lo = off[r], c = off[r + 1] - lo;
-  const ulonglong2* src = runs + r * cap;
-  for (uint64_t i = threadIdx.x; i < c; i += kBlock) {
-    const ulonglong2 x = src[i];
-    keys[lo + i] = x.x;
-    meta[lo + i] = x.y;
-  }
 }
 
 __global__ __launch_bounds__(kBlock) void k_super_finalize(const unsigned long long* __restrict__ key,
@@ -2902,60 +2108,86 @@ namespace {
 // ------------------------------------------------------------ layout ---
 // Device layout of the reads.  Overlapping reads share
 // m-mers, so clustering the slots by each read's canonical global minimizer
-// (the smallest mix64 over its m-mers and their reverse complements, m =
-// min(31, n); strand-independent) puts a read's overlap partners next to it
-// in memory for about half of its discoveries: the probe's partner slots and
-// the shared minimizer cells then come from L2 instead of HBM.  Key = minimizer
-// hash (high 54 bits) | its offset, so each cluster is ordered along the
-// genome.  One thread per read.
+// (the smallest hash over its 16-mers and their reverse complements;
+// strand-independent) puts a read's overlap partners next to it in memory for
+// about half of its discoveries: the probe's partner slots and the shared
+// minimizer cells then come from L2 instead of HBM.  The key is 32 bits:
+// [group (2, only with a source-read range) | minimizer hash (HB) | its offset
+// (PB)], so each cluster is ordered along the genome and four 8-bit radix
+// passes sort it.  group = 0 / 1 / 2 for reference IDs below / inside / above
+// the range [lo, hi), so the range's reads take exactly the slots [lo, hi).
+// One thread per slot (old_id: the slot's reference ID - 1, nullptr = ID order).
 template <int MAXW>
 __global__ __launch_bounds__(kBlock) void k_layout_keys(const uint64_t* __restrict__ words,
                                                        const uint16_t* __restrict__ len, uint64_t n,
-                                                       uint64_t* __restrict__ key, uint32_t* __restrict__ val) {
+                                                       const uint32_t* __restrict__ old_id, uint64_t lo, uint64_t hi,
+                                                       int grouped, int pb, uint32_t* __restrict__ key,
+                                                       uint32_t* __restrict__ val) {
   const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
   if (i >= n) return;
   const int L = len[i];
-  const int m = L < 31 ? L : 31;
+  constexpr int kM = 16;
+  const int m = L < kM ? L : kM;
+  const uint32_t mmask = m == 16 ? 0xFFFFFFFFu : ((1u << (2 * m)) - 1u);
   const uint64_t* g = words + i * slot_words(MAXW);
-  const uint64_t mmask = m ? ((1ULL << (2 * m)) - 1) : 0;
-  uint64_t fw = 0, rc = 0, best = ~0ULL, cw = 0;
-  int bpos = 0;
+  uint32_t fw = 0, rc = 0, best = 0xFFFFFFFFu, bpos = 0;
+  uint64_t cw = 0;
   for (int t = 0; t < L; ++t) {
     if ((t & 31) == 0) cw = g[t >> 5];
-    const uint64_t b = (cw >> (62 - 2 * (t & 31))) & 3u;
+    const uint32_t b = (uint32_t)(cw >> (62 - 2 * (t & 31))) & 3u;
     fw = ((fw << 2) | b) & mmask;
     rc = (rc >> 2) | ((3u - b) << (2 * m - 2));
     if (t >= m - 1) {
-      const uint64_t hv = mix64(fw < rc ? fw : rc);
-      if (hv < best) {
+      const uint32_t hv = order_key(fw < rc ? fw : rc) | (uint32_t)(t - m + 1 < 1023 ? t - m + 1 : 1023);
+      if (hv < best) {  // the hash, leftmost on ties
         best = hv;
-        bpos = t - m + 1;
+        bpos = (uint32_t)(t - m + 1);
       }
     }
   }
-  key[i] = (best & ~0x3FFull) | (uint64_t)(bpos < 1023 ? bpos : 1023);
+  const int gb = grouped ? 2 : 0, hb = 32 - gb - pb;
+  const uint32_t pmax = (1u << pb) - 1u;
+  uint32_t k = ((best >> (32 - hb)) << pb) | (bpos < pmax ? bpos : pmax);
+  if (grouped) {
+    const uint64_t id = old_id ? old_id[i] : i;
+    const uint32_t grp = id < lo ? 0u : id < hi ? 1u : 2u;
+    k |= grp << 30;
+  }
+  key[i] = k;
   val[i] = (uint32_t)i;
 }
 
-// slot i of the new layout <- slot src[i] of the ID-order upload; d_id / d_phys
+// new slot i <- old slot src[i]: its words (16-B pieces), length and reference
+// ID, into the second slot array (committed by swapping)
 template <int MAXW>
 __global__ __launch_bounds__(kBlock) void k_layout_gather(const uint64_t* __restrict__ src_words,
                                                          const uint16_t* __restrict__ src_len,
+                                                         const uint32_t* __restrict__ old_id,
                                                          const uint32_t* __restrict__ order, uint64_t n,
                                                          uint64_t* __restrict__ dst_words, uint16_t* __restrict__ dst_len,
-                                                         uint32_t* __restrict__ id, uint32_t* __restrict__ phys) {
+                                                         uint32_t* __restrict__ id) {
   constexpr int S = slot_words(MAXW);
+  constexpr int P = S >= 2 ? S / 2 : 1;  // 16-B pieces per slot
   const uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (t >= n * S) return;
-  const uint64_t i = t / S;
-  const int k = (int)(t - i * S);
+  if (t >= n * P) return;
+  const uint64_t i = t / P;
+  const int k = (int)(t - i * P);
   const uint32_t r = order[i];
-  dst_words[t] = src_words[(uint64_t)r * S + k];
+  if (S >= 2) {
+    reinterpret_cast<ulonglong2*>(dst_words)[t] = reinterpret_cast<const ulonglong2*>(src_words)[(uint64_t)r * P + k];
+  } else {
+    dst_words[i] = src_words[r];
+  }
   if (k == 0) {
     dst_len[i] = src_len[r];
-    id[i] = r;
-    phys[r] = (uint32_t)i;
+    id[i] = old_id ? old_id[r] : r;
   }
+}
+
+__global__ __launch_bounds__(kBlock) void k_layout_phys(const uint32_t* __restrict__ id, uint64_t n,
+                                                       uint32_t* __restrict__ phys) {
+  const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i < n) phys[id[i]] = (uint32_t)i;
 }
 
 // per-slot values -> ID order (superReadIDs leave the device in ID order)
@@ -2967,20 +2199,20 @@ __global__ __launch_bounds__(kBlock) void k_unpermute_u32(const uint32_t* __rest
 
 template <int W>
 struct LaunchLayout {
-  static int run(mg_ctx* ctx, uint64_t* key, uint32_t* val) {
+  static int run(mg_ctx* ctx, uint64_t lo, uint64_t hi, int grouped, int pb, uint32_t* key, uint32_t* val) {
     const uint64_t n = ctx->n;
     hipLaunchKernelGGL((k_layout_keys<W>), dim3((uint32_t)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, ctx->stream,
-                       ctx->d_words, ctx->d_len, n, key, val);
+                       ctx->d_words, ctx->d_len, n, ctx->d_id, lo, hi, grouped, pb, key, val);
     return hipGetLastError() == hipSuccess ? 0 : -1;
   }
 };
 template <int W>
 struct LaunchLayoutGather {
-  static int run(mg_ctx* ctx, const uint64_t* src_words, const uint16_t* src_len, const uint32_t* order,
-                 uint64_t* dst_words, uint16_t* dst_len) {
-    const uint64_t t = ctx->n * (uint64_t)slot_words(W);
+  static int run(mg_ctx* ctx, const uint32_t* order, uint64_t* dst_words, uint16_t* dst_len, uint32_t* id) {
+    constexpr int S = slot_words(W);
+    const uint64_t t = ctx->n * (uint64_t)(S >= 2 ? S / 2 : 1);
     hipLaunchKernelGGL((k_layout_gather<W>), dim3((uint32_t)((t + kBlock - 1) / kBlock)), dim3(kBlock), 0, ctx->stream,
-                       src_words, src_len, order, ctx->n, dst_words, dst_len, ctx->d_id, ctx->d_phys);
+                       ctx->d_words, ctx->d_len, ctx->d_id, order, ctx->n, dst_words, dst_len, id);
     return hipGetLastError() == hipSuccess ? 0 : -1;
   }
 };
@@ -3081,22 +2313,20 @@ uint32_t resident_blocks(mg_ctx* ctx, K kernel, size_t lds, uint64_t want, int b
 // (long windows: w = l - k grows with min_overlap).  0 = w too large.
 constexpr size_t kLdsPerCu = 160 * 1024;
 inline size_t scan_lds_per_wave(uint32_t w) { return (((size_t)w * kWave + 1) / 2 + kScanBuf) * sizeof(uint64_t); }
-// the register scan (k_scan_reg) when its window fits in registers
-inline bool use_scan_reg_w(const mg_ctx* ctx) { return ctx->w <= (uint32_t)kRegW; }
-inline bool use_scan_reg(const mg_ctx* ctx) { return (ctx->scan_reg || ctx->join_P) && use_scan_reg_w(ctx); }
-// the index-building scan: k_scan_reg<INDEX> writes join records only; the
-// cell index rides on k_scan<INDEX>
-// (cell mode: option "reg_index" = 1 writes key records that k_insert_dense files;
-// measured slower than k_scan<INDEX>, whose CAS inserts hide behind its ALU work)
-inline bool use_scan_reg_index(const mg_ctx* ctx) {
-  return (ctx->join_P || ctx->reg_index || ctx->reg_cas || ctx->xchg) && use_scan_reg_w(ctx);
-}
 inline uint32_t scan_wpb(uint32_t w) {
   for (uint32_t wpb = kWavesPerBlock; wpb >= 1; wpb >>= 1)
     if (wpb * scan_lds_per_wave(w) <= kLdsPerCu) return wpb;
   return 0;
 }
-inline bool scan_is_reg(const mg_ctx* ctx, bool index) { return index ? use_scan_reg_index(ctx) : use_scan_reg(ctx); }
+// Which window scan runs.  The index-building scan of the fused path is
+// k_scan<INDEX> (LDS sliding minimum, CAS inserts hidden behind its ALU work);
+// the exchange mode's scan writes key records instead, from the register
+// sliding minimum (k_scan_reg<INDEX> + k_rc_keys) when w fits its unrolled
+// window, else from k_scan<INDEX>.  Run-only scans (source-range shards) take
+// the register scan when w fits.
+inline bool scan_is_reg(const mg_ctx* ctx, bool index) {
+  return ctx->w <= (uint32_t)kRegW && (!index || ctx->xchg);
+}
 inline uint32_t scan_block_waves(const mg_ctx* ctx, bool index) {
   return scan_is_reg(ctx, index) ? kWavesPerBlock : scan_wpb(ctx->w);
 }
@@ -3123,7 +2353,7 @@ inline void packable_runs(const mg_ctx* ctx, int* a, int* wb) {
   const int WB = bits(ctx->w > 0 ? ctx->w - 1 : 0);
   const int nb = (int)ctx->nb_log2;
   const int fph = std::max(0, (int)kFpBits - (32 - nb));
-  const bool ok = ctx->pack_runs && nb < 32 && A + 10 + 2 * WB + fph <= 64;
+  const bool ok = nb < 32 && A + 10 + 2 * WB + fph <= 64;
   *a = ok ? A : 0;
   *wb = ok ? WB : 0;
 }
@@ -3142,56 +2372,48 @@ DiscGeom disc_geom(mg_ctx* ctx, bool contain, uint64_t nsrc) {
   const uint64_t ngroups = (nsrc + kWave - 1) / kWave;
   const uint64_t want = std::max<uint64_t>(1, (ngroups + kWavesPerBlock - 1) / kWavesPerBlock);
   g.lds_scan = scan_lds(ctx, false);
-  if (ctx->split) {
-    g.lds_probe = (size_t)kWavesPerBlock * ProbeLds<W>::split_bytes;
-    g.grid = contain ? resident_blocks(ctx, k_probe<W, true, true>, g.lds_probe, want)
-                     : resident_blocks(ctx, k_probe<W, false, true>, g.lds_probe, want);
-  } else {
-    g.lds_probe = (size_t)kWavesPerBlock * ProbeLds<W>::bytes;
-    g.grid = contain ? resident_blocks(ctx, k_probe<W, true, false>, g.lds_probe, want)
-                     : resident_blocks(ctx, k_probe<W, false, false>, g.lds_probe, want);
-  }
+  g.lds_probe = (size_t)kWavesPerBlock * ProbeLds<W>::bytes;
+  g.grid = contain ? resident_blocks(ctx, k_probe<W, true>, g.lds_probe, want)
+                   : resident_blocks(ctx, k_probe<W, false>, g.lds_probe, want);
   const uint32_t scan_res = scan_resident<W>(ctx, false, ~0ull >> 1);
   g.kreg = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(scan_res / g.grid, (want + g.grid - 1) / g.grid));
   g.sgrid = g.grid * g.kreg;
   return g;
 }
 
-// k_scan over source reads [a_lo, a_hi) into ctx->d_runs (one region per scan
-// wavefront).  filter: keep only runs whose bucket this rank owns (replicated
-// scan of SURVEY §8(e)); exchange mode scans its own sources unfiltered.
+// Window scan over source slots [a_lo, a_hi): one run region per scan
+// wavefront in ctx->d_runs, or (flat, exchange mode) the SoA arrays of the
+// bucket sort.  filter: keep only runs whose bucket this rank owns (a
+// bucket-sharded single context); index: the scan also builds the index
+// (fused: CAS into the cells; exchange: key records).
 template <int W>
 struct LaunchScan {
   static int run(mg_ctx* ctx, bool contain, uint64_t a_lo, uint64_t a_hi, uint32_t sgrid, bool filter,
                  hipStream_t stream = nullptr, bool no_super = false, bool index = false, bool flat = false) {
     if (!stream) stream = ctx->stream;
     const uint32_t wpb = scan_block_waves(ctx, index);
-    const uint64_t nw = (uint64_t)sgrid * wpb;  // scan wavefronts
+    const uint64_t nw = (uint64_t)sgrid * wpb;  // scan wavefronts = run regions
     const uint64_t ngroups = (a_hi - a_lo + kWave - 1) / kWave;
-    // run regions: one per scan wavefront, or (option group_regions) one per
-    // read group of 64, so region order is read order and the probe can sweep
-    // neighbouring reads together (the clustered layout's locality)
-    const bool group = ctx->group_regions && !flat;
-    ctx->group_active = group;
-    const uint64_t nreg = group ? ngroups : nw;
+    const uint64_t nreg = nw;
     ctx->nrun_reg = nreg;
     // expected runs per read ~ 2 J / (w + 1) + 1 (minimizer density)
     const uint64_t J = ctx->maxlen > ctx->h + 1 ? ctx->maxlen - ctx->h - 1 : 1;
-    const uint64_t per_read = group ? std::min<uint64_t>(J, 3 * (2 * J / (ctx->w + 1) + 2) / 2)
-                                    : std::min<uint64_t>(J, 3 * (2 * J / (ctx->w + 1) + 2));
-    const uint64_t groups_per_region = group ? 1 : (ngroups + nw - 1) / nw;
+    const uint64_t per_read = std::min<uint64_t>(J, 3 * (2 * J / (ctx->w + 1) + 2));
+    const uint64_t groups_per_region = (ngroups + nw - 1) / nw;
     uint64_t run_cap = std::max<uint64_t>(ctx->run_cap_need, groups_per_region * kWave * per_read);
-    if (run_cap * nreg > ctx->runs_cap) {
+    if (!flat && run_cap * nreg > ctx->runs_cap) {
       if (ctx->d_runs) (void)hipFree(ctx->d_runs);
       ctx->d_runs = nullptr;
+      ctx->runs_cap = 0;
       if (hipMalloc(&ctx->d_runs, run_cap * nreg * sizeof(ulonglong2)) != hipSuccess) return -1;
       ctx->runs_cap = run_cap * nreg;
     }
-    run_cap = ctx->runs_cap / std::max<uint64_t>(1, nreg);
+    run_cap = flat ? 0 : ctx->runs_cap / std::max<uint64_t>(1, nreg);
     ctx->run_cap = run_cap;
     if (ctx->run_cnt_cap < nreg) {
       if (ctx->d_run_cnt) (void)hipFree(ctx->d_run_cnt);
       ctx->d_run_cnt = nullptr;
+      ctx->run_cnt_cap = 0;
       if (hipMalloc(&ctx->d_run_cnt, std::max<uint64_t>(1, nreg) * sizeof(unsigned long long)) != hipSuccess) return -1;
       ctx->run_cnt_cap = nreg;
     }
@@ -3210,18 +2432,16 @@ struct LaunchScan {
     sp.runs = ctx->d_runs;
     sp.run_cnt = ctx->d_run_cnt;
     sp.run_cap = run_cap;
-    sp.group_regions = group ? 1 : 0;
     const size_t lds = scan_lds(ctx, index);
     sp.cells = ctx->d_cells;
     sp.cell_n = ctx->cell_n;
     ctx->scan_flat = flat;
+    ctx->pack_a = ctx->pack_w = 0;
     if (flat) {
       // SoA output for the bucket sort: ~2 J / (w + 1) + 1 runs per read, sized
       // with 20 % slack (or the exact need after an overflow)
-      // (join mode: + the four key records of every read)
-      const uint64_t off = (ctx->join_P && index) ? 4 * ctx->n : 0;
-      const uint64_t est = off + (ctx->flat_cap_opt ? ctx->flat_cap_opt
-                                                    : (a_hi - a_lo) * (2 * J / (ctx->w + 1) + 2) * 6 / 5 + 4096);
+      const uint64_t est = ctx->flat_cap_opt ? ctx->flat_cap_opt
+                                             : (a_hi - a_lo) * (2 * J / (ctx->w + 1) + 2) * 6 / 5 + 4096;
       const uint64_t cap = std::max<uint64_t>(ctx->flat_need, est);
       if (cap > ctx->sk_cap || (ctx->flat_cap_opt && cap < ctx->sk_cap)) {
         for (int b = 0; b < 2; ++b) {
@@ -3241,35 +2461,18 @@ struct LaunchScan {
         return -1;
       if (hipMemsetAsync(ctx->d_flat_cursor, 0, kFlatCounters * sizeof(unsigned long long), stream) != hipSuccess)
         return -1;
-      // join INDEX: the dense key records [0, 4 N) come first, the runs' chunks after
-      ctx->flat_off = (ctx->join_P && index) ? 4 * ctx->n : 0;
-      sp.flat_keys = reinterpret_cast<uint64_t*>(reinterpret_cast<uint32_t*>(ctx->d_sk[0]) + ctx->flat_off);
-      sp.flat_meta = ctx->d_sm[0] + ctx->flat_off;
+      sp.flat_keys = ctx->d_sk[0];
+      sp.flat_meta = ctx->d_sm[0];
       sp.flat_cursor = ctx->d_flat_cursor;
-      sp.flat_cap = ctx->sk_cap - ctx->flat_off;
-      if (ctx->join_P && index) {  // join records (runs + keys), no cells
-        ctx->pack_a = ctx->pack_w = 0;
-        sp.join_kk = reinterpret_cast<uint32_t*>(ctx->d_sk[0]);
-        sp.join_kv = ctx->d_sm[0];
-        sp.join_P = ctx->join_P;
-        sp.join_A = ctx->join_A;
-        sp.join_QB = ctx->join_QB;
-        sp.join_WB = ctx->join_WB;
-      } else {
-        packable_runs(ctx, &ctx->pack_a, &ctx->pack_w);
-      }
+      sp.flat_cap = ctx->sk_cap;
+      packable_runs(ctx, &ctx->pack_a, &ctx->pack_w);
       sp.pack_a = ctx->pack_a;
       sp.pack_w = ctx->pack_w;
-    } else {
-      ctx->pack_a = ctx->pack_w = 0;
     }
     if (index && ctx->key0_ready) sp.key0 = ctx->d_key0;  // mg_build_index allocated it (mixed lengths)
-    const bool reg_cas = index && ctx->reg_cas && !ctx->sorted_index && !ctx->xchg && !ctx->join_P &&
-                         !ctx->reg_index && scan_is_reg(ctx, true);
-    if (index && !reg_cas && (ctx->sorted_index || ctx->xchg || (scan_is_reg(ctx, true) && !ctx->join_P))) {
-      // key records (bucket, entry), o-major: the sorted build or k_insert_dense files them
-      sp.key_bk = ctx->d_kb[0];
-      sp.key_ent = ctx->d_ke[0];
+    if (index && ctx->xchg) {  // key records (bucket, entry), o-major: they travel to the bucket owner
+      sp.key_bk = ctx->d_kb;
+      sp.key_ent = ctx->d_ke;
       sp.key_n = ctx->n;
     }
     (void)hipEventRecord(ctx->ev[6], stream);
@@ -3277,14 +2480,14 @@ struct LaunchScan {
       if (index) {
         allow_lds(k_scan_reg<W, true>, lds);
         hipLaunchKernelGGL((k_scan_reg<W, true>), dim3(sgrid), dim3(wpb * kWave), lds, stream, sp);
-        if (a_hi > a_lo && !reg_cas)  // the reverse strand's keys (dense slots 4 a + 2, 4 a + 3)
+        if (a_hi > a_lo)  // the reverse strand's keys (o = 2, 3)
           hipLaunchKernelGGL((k_rc_keys<W>), dim3((uint32_t)((a_hi - a_lo + kBlock - 1) / kBlock)), dim3(kBlock), 0,
                              stream, sp);
       } else {
         allow_lds(k_scan_reg<W, false>, lds);
         hipLaunchKernelGGL((k_scan_reg<W, false>), dim3(sgrid), dim3(wpb * kWave), lds, stream, sp);
       }
-    } else if (index) {  // unsharded only (the whole key space is this context's)
+    } else if (index) {
       allow_lds(k_scan<W, true>, lds);
       hipLaunchKernelGGL((k_scan<W, true>), dim3(sgrid), dim3(wpb * kWave), lds, stream, sp);
     } else {
@@ -3301,13 +2504,12 @@ int settle_runs(mg_ctx* ctx, bool* again);
 
 // k_probe over run regions (runs + r * run_cap, run_cnt[r] records), rows into
 // ctx->d_rows (one region per probe wavefront) or superkey updates (contain).
+// src_lo / src_hi: only runs of source slots in [src_lo, src_hi) (0, 0: all).
 template <int W>
 struct LaunchProbe {
   static int run(mg_ctx* ctx, bool contain, const ulonglong2* runs, const unsigned long long* run_cnt,
-                 uint64_t run_cap, uint64_t run_regions, uint32_t grid, uint64_t total_runs,
-                 const uint32_t* src_super = nullptr, uint64_t src_lo = 0, uint64_t src_hi = 0,
-                 const uint64_t* fkeys = nullptr, const uint64_t* fmeta = nullptr, int pack_a = 0,
-                 int pack_w = 0, int xcd_map = 0) {
+                 uint64_t run_cap, uint64_t run_regions, uint32_t grid, const uint32_t* src_super = nullptr,
+                 uint64_t src_lo = 0, uint64_t src_hi = 0) {
     ctx->nreg = (uint64_t)grid * kWavesPerBlock;  // probe wavefronts = row regions
     ProbeParams pp{};
     pp.words = ctx->d_words;
@@ -3326,10 +2528,6 @@ struct LaunchProbe {
     pp.run_cnt = run_cnt;
     pp.run_cap = run_cap;
     pp.run_regions = run_regions;
-    pp.fkeys = fkeys;
-    pp.fmeta = fmeta;
-    pp.pack_a = pack_a;
-    pp.pack_w = pack_w;
     pp.src_super = src_super;
     pp.src_lo = src_lo;
     pp.src_hi = src_hi;
@@ -3340,6 +2538,7 @@ struct LaunchProbe {
     pp.stats = ctx->stats ? ctx->d_stats : nullptr;
     pp.phase_limit = contain ? 99 : ctx->phase_limit;
     pp.halving_low = ctx->halving_low ? 1 : 0;
+    pp.halving_id = (ctx->read_lo || ctx->read_hi) ? ctx->d_id : nullptr;
     pp.contain_even = (contain && ctx->key0_ready) ? 1 : 0;
     pp.contain_minlen = (pp.contain_even && ctx->contain_jcut) ? (int)ctx->minlen : 0;
     pp.contain_prune = (contain && ctx->contain_prune) ? 1 : 0;
@@ -3348,93 +2547,20 @@ struct LaunchProbe {
     // shared regions help the discovery probe (C3 probe 4.56-4.57 vs 4.65-4.78 ms) but cost the
     // containment probe (C5 35.0 vs 29.6 ms: contain_skip finds fewer containers marked in time)
     pp.share = (!contain && ctx->probe_share) ? 1 : 0;
-    pp.share_xcd = ctx->probe_share_xcd ? 1 : 0;
-    pp.src_len_lo = contain ? ctx->pass_len_lo : 0;
-    pp.src_len_hi = contain ? ctx->pass_len_hi : 0;
-    pp.xcd_map = xcd_map;
     pp.id = ctx->d_id;
-    if (ctx->split) return run_split(ctx, contain, pp, grid, total_runs);
     const size_t lds = (size_t)kWavesPerBlock * ProbeLds<W>::bytes;
     if (contain)
-      hipLaunchKernelGGL((k_probe<W, true, false>), dim3(grid), dim3(kBlock), lds, ctx->stream, pp);
+      hipLaunchKernelGGL((k_probe<W, true>), dim3(grid), dim3(kBlock), lds, ctx->stream, pp);
     else
-      hipLaunchKernelGGL((k_probe<W, false, false>), dim3(grid), dim3(kBlock), lds, ctx->stream, pp);
+      hipLaunchKernelGGL((k_probe<W, false>), dim3(grid), dim3(kBlock), lds, ctx->stream, pp);
     return hipGetLastError() == hipSuccess ? 0 : -1;
-  }
-
-  // k_probe<SPLIT> -> candidates (regions resized and the probe rerun on
-  // overflow), then k_verify -> rows (row regions resized and the verify rerun
-  // on overflow).  Synchronous; rows are settled here (ctx->n_rows).
-  static int run_split(mg_ctx* ctx, bool contain, ProbeParams pp, uint32_t grid, uint64_t total_runs) {
-    const uint64_t nwp = (uint64_t)grid * kWavesPerBlock;
-    const size_t lds_p = (size_t)kWavesPerBlock * ProbeLds<W>::split_bytes;
-    allow_lds(k_probe<W, true, true>, lds_p);
-    allow_lds(k_probe<W, false, true>, lds_p);
-    if (ctx->cand_cnt_cap < nwp) {
-      if (ctx->d_cand_cnt) (void)hipFree(ctx->d_cand_cnt);
-      ctx->d_cand_cnt = nullptr;
-      if (hipMalloc(&ctx->d_cand_cnt, nwp * sizeof(unsigned long long)) != hipSuccess) return -1;
-      ctx->cand_cnt_cap = nwp;
-    }
-    if (ctx->cand_cnt_host.size() < nwp) ctx->cand_cnt_host.resize(nwp);
-    for (int attempt = 0;; ++attempt) {
-      if (attempt == 3) return -1;
-      const uint64_t cap = std::max<uint64_t>(ctx->cand_cap_need, total_runs * 3 / 2 / nwp + 256);
-      if (cap * nwp > ctx->cand_cap_total) {
-        if (ctx->d_cand) (void)hipFree(ctx->d_cand);
-        ctx->d_cand = nullptr;
-        if (hipMalloc(&ctx->d_cand, cap * nwp * sizeof(uint3)) != hipSuccess) return -1;
-        ctx->cand_cap_total = cap * nwp;
-      }
-      pp.cand = ctx->d_cand;
-      pp.cand_cnt = ctx->d_cand_cnt;
-      pp.cand_cap = ctx->cand_cap_total / nwp;
-      (void)hipEventRecord(ctx->ev[8], ctx->stream);
-      if (contain)
-        hipLaunchKernelGGL((k_probe<W, true, true>), dim3(grid), dim3(kBlock), lds_p, ctx->stream, pp);
-      else
-        hipLaunchKernelGGL((k_probe<W, false, true>), dim3(grid), dim3(kBlock), lds_p, ctx->stream, pp);
-      if (hipGetLastError() != hipSuccess) return -1;
-      (void)hipEventRecord(ctx->ev[9], ctx->stream);
-      if (hipMemcpyAsync(ctx->cand_cnt_host.data(), ctx->d_cand_cnt, nwp * sizeof(unsigned long long),
-                         hipMemcpyDeviceToHost, ctx->stream) != hipSuccess ||
-          hipStreamSynchronize(ctx->stream) != hipSuccess)
-        return -1;
-      uint64_t mx = 0;
-      for (uint64_t r = 0; r < nwp; ++r) mx = std::max<uint64_t>(mx, ctx->cand_cnt_host[r]);
-      if (mx <= pp.cand_cap) break;
-      ctx->cand_cap_need = mx + mx / 4 + 256;
-    }
-    const size_t lds_v = 0;
-    const uint32_t vgrid = contain ? resident_blocks(ctx, k_verify<W, true>, lds_v, ~0ull >> 1)
-                                   : resident_blocks(ctx, k_verify<W, false>, lds_v, ~0ull >> 1);
-    ctx->nreg = (uint64_t)vgrid * kWavesPerBlock;  // verify wavefronts = row regions
-    for (int attempt = 0;; ++attempt) {
-      if (attempt == 3) return -1;
-      pp.reg_cap = contain ? 0 : ctx->rows_cap / ctx->nreg;
-      pp.rows = ctx->d_rows;
-      (void)hipEventRecord(ctx->ev[10], ctx->stream);
-      if (contain)
-        hipLaunchKernelGGL((k_verify<W, true>), dim3(vgrid), dim3(kBlock), lds_v, ctx->stream, pp, nwp);
-      else
-        hipLaunchKernelGGL((k_verify<W, false>), dim3(vgrid), dim3(kBlock), lds_v, ctx->stream, pp, nwp);
-      if (hipGetLastError() != hipSuccess) return -1;
-      (void)hipEventRecord(ctx->ev[11], ctx->stream);
-      if (contain) break;
-      bool again = false;
-      if (settle_rows(ctx, &again)) return -1;
-      if (!again) break;
-      if (ctx->stats && hipMemsetAsync(ctx->d_stats, 0, (kSegs * 4 + 1) * sizeof(unsigned long long), ctx->stream) != hipSuccess)
-        return -1;  // counters of a rerun would double (the probe's are lost too: diagnostics only)
-    }
-    return 0;
   }
 };
 
 template <int W>
 struct LaunchDiscover {
-  // fused scan + probe over the context's source range; `contain` selects
-  // markContainedReads semantics
+  // scan + probe over the context's source slots (a source-range shard);
+  // `contain` selects markContainedReads semantics (all sources)
   static int run(mg_ctx* ctx, bool contain) {
     const uint64_t a_lo = contain ? 0 : ctx->read_lo;
     const uint64_t a_hi = contain ? ctx->n : (ctx->read_hi ? std::min<uint64_t>(ctx->read_hi, ctx->n) : ctx->n);
@@ -3443,15 +2569,7 @@ struct LaunchDiscover {
     if (a_hi <= a_lo) return 0;
     const DiscGeom g = disc_geom<W>(ctx, contain, a_hi - a_lo);
     if (LaunchScan<W>::run(ctx, contain, a_lo, a_hi, g.sgrid, !contain)) return -1;
-    uint64_t total_runs = 0;
-    if (ctx->split) {  // the split probe sizes its candidate regions from the run count
-      bool again = false;
-      if (settle_runs(ctx, &again)) return -1;
-      if (again) return 1;
-      for (uint64_t r = 0; r < ctx->nrun_reg; ++r) total_runs += std::min<uint64_t>(ctx->run_cnt_host[r], ctx->run_cap);
-    }
-    return LaunchProbe<W>::run(ctx, contain, ctx->d_runs, ctx->d_run_cnt, ctx->run_cap, ctx->nrun_reg, g.grid,
-                               total_runs);
+    return LaunchProbe<W>::run(ctx, contain, ctx->d_runs, ctx->d_run_cnt, ctx->run_cap, ctx->nrun_reg, g.grid);
   }
 };
 
@@ -3484,7 +2602,6 @@ int launch_lookup(mg_ctx* ctx, const uint64_t* dq, int qwords, unsigned long lon
 
 // k_probe_long over sources [a_lo, a_hi): containment (atomicMax into the
 // superkeys) or discovery (rows; regions resized and rerun on overflow)
-int settle_rows(mg_ctx* ctx, bool* again);
 int long_probe(mg_ctx* ctx, bool contain, uint64_t a_lo, uint64_t a_hi) {
   LongParams p{};
   p.words = ctx->d_words;
@@ -3571,10 +2688,6 @@ int run_discover(mg_ctx* ctx, bool contain) {
       ctx->err = "discovery launch failed";
       return -1;
     }
-    if (ctx->split) {  // runs and rows were settled inside (rc 1: run regions resized)
-      if (rc == 0) return 0;
-      continue;
-    }
     bool again = false;
     if (settle_runs(ctx, &again)) return -1;
     if (!contain && !again && settle_rows(ctx, &again)) return -1;
@@ -3622,20 +2735,13 @@ void mg_destroy(mg_ctx* ctx) {
   if (!ctx) return;
   (void)hipSetDevice(ctx->device);
   (void)hipStreamSynchronize(ctx->stream);
-  if (ctx->clear_stream) (void)hipStreamSynchronize(ctx->clear_stream);
-  if (ctx->d_cells == ctx->pp_buf[0] || ctx->d_cells == ctx->pp_buf[1]) ctx->d_cells = nullptr;
-  for (auto& b : ctx->pp_buf)
-    if (b) (void)hipFree(b);
-  for (auto& e : ctx->ev_clear)
-    if (e) (void)hipEventDestroy(e);
-  if (ctx->ev_use) (void)hipEventDestroy(ctx->ev_use);
-  if (ctx->clear_stream) (void)hipStreamDestroy(ctx->clear_stream);
-  void* bufs[] = {ctx->d_words, ctx->d_len, ctx->d_cells,
-                  ctx->d_superkey, ctx->d_super, ctx->d_any, ctx->d_rows, ctx->d_seg, ctx->d_stats,
-                  ctx->d_compact, ctx->d_runs, ctx->d_run_cnt, ctx->d_blk, ctx->d_flat_cnt, ctx->d_slot_cnt, ctx->d_cand, ctx->d_cand_cnt, ctx->d_freq,
-                  ctx->d_sk[0], ctx->d_sk[1], ctx->d_sm[0], ctx->d_sm[1], ctx->d_sort_tmp, ctx->d_run_off,
-                  ctx->d_flat_cursor, ctx->d_kb[0], ctx->d_kb[1], ctx->d_ke[0], ctx->d_ke[1], ctx->d_key0, ctx->d_holes,
-                  ctx->d_digest, ctx->d_bnd, ctx->d_mid, ctx->d_queue, ctx->d_id, ctx->d_phys, ctx->d_tmp32};
+  void* bufs[] = {ctx->d_words, ctx->d_len, ctx->d_cells, ctx->d_superkey, ctx->d_super, ctx->d_any, ctx->d_rows,
+                  ctx->d_seg, ctx->d_stats, ctx->d_compact, ctx->d_runs, ctx->d_run_cnt, ctx->d_blk, ctx->d_flat_cnt,
+                  ctx->d_slot_cnt, ctx->d_freq, ctx->d_sk[0], ctx->d_sk[1], ctx->d_sm[0], ctx->d_sm[1],
+                  ctx->d_sort_tmp, ctx->d_flat_cursor, ctx->d_kb, ctx->d_ke, ctx->d_key0, ctx->d_holes, ctx->d_digest,
+                  ctx->d_bnd, ctx->id_store[0], ctx->id_store[1], ctx->phys_store[0], ctx->phys_store[1],
+                  ctx->d_tmp32, ctx->d_lay_k[0], ctx->d_lay_k[1], ctx->d_lay_v[0], ctx->d_lay_v[1], ctx->d_lay_tmp,
+                  ctx->d_words_alt, ctx->d_len_alt};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   for (auto& e : ctx->ev)
@@ -3783,159 +2889,45 @@ int mg_read_slots(mg_ctx* ctx, uint32_t* slot_of_id) {
 
 int mg_set_option(mg_ctx* ctx, const char* name, int64_t value) {
   if (!ctx || !name) return -1;
+  auto flag = [&](const char* opt, bool* field) {
+    if (strcmp(name, opt)) return false;
+    *field = value != 0;
+    return true;
+  };
   if (!strcmp(name, "nb_log2")) {
     if (value != 0 && (value < 10 || value > 31)) return set_err(ctx, "nb_log2 out of range [10,31]");
     ctx->nb_log2_opt = (uint32_t)value;
     ctx->index_ready = false;
     return 0;
   }
-  if (!strcmp(name, "phase_limit")) {
+  if (!strcmp(name, "rows_cap")) {
+    ctx->rows_cap_opt = (uint64_t)std::max<int64_t>(0, value);
+    return 0;
+  }
+  if (!strcmp(name, "phase_limit")) {  // diagnostics: stop the probe after a phase
     ctx->phase_limit = value > 0 ? (int)value : 99;
     return 0;
   }
-  if (!strcmp(name, "max_blocks")) {
+  if (!strcmp(name, "max_blocks")) {  // diagnostics: cap the persistent probe grid
     ctx->max_blocks = value > 0 ? (uint32_t)value : 8192u;
     return 0;
   }
-  if (!strcmp(name, "overlap_scan")) {
-    ctx->overlap_scan = value != 0;
-    ctx->scan_state = 0;
-    ctx->sorted_state = 0;
-    return 0;
-  }
-  if (!strcmp(name, "join_parts_log2")) {  // 0: auto (~2.5k keys per partition); tests force few partitions
-    if (value < 0 || value > 16) return set_err(ctx, "join_parts_log2 out of range [0,16]");
-    ctx->join_P_opt = (int)value;
-    ctx->index_ready = false;
-    ctx->join_ready = false;
-    return 0;
-  }
-  if (!strcmp(name, "join")) {  // 1 (default): partitioned join (k_join) when it applies; 0: cell index + probe
-    ctx->join = value != 0;
-    ctx->index_ready = false;
-    ctx->join_ready = false;
-    return 0;
-  }
-  if (!strcmp(name, "reg_index")) {  // 1: the cell index from the register scan's key records + k_insert_dense
-    ctx->reg_index = value != 0;
-    ctx->index_ready = false;
-    return 0;
-  }
-  if (!strcmp(name, "layout")) {  // 1 (default): clustered slots; 0: ID order (takes effect at the next upload)
-    ctx->layout = value != 0;
-    return 0;
-  }
-  if (!strcmp(name, "scan_reg")) {  // 1 (default): register sliding minimum when w <= 32; 0: LDS version
-    ctx->scan_reg = value != 0;
-    ctx->scan_state = 0;
-    ctx->sorted_state = 0;
-    return 0;
-  }
-  if (!strcmp(name, "halving")) {  // 0: parity-alternating o=2/3 side (default), 1: lower ID keeps
-    ctx->halving_low = value != 0;
-    return 0;
-  }
-  if (!strcmp(name, "sort_runs")) {
-    ctx->sort_runs = value != 0;
-    ctx->sorted_state = 0;
-    return 0;
-  }
-  if (!strcmp(name, "contain_jcut")) {  // 1: the containment probe drops runs past j = n1 - minlen
-    ctx->contain_jcut = value != 0;
-    return 0;
-  }
-  if (!strcmp(name, "contain_skip")) {  // 1: the containment probe skips runs of already-contained sources
-    ctx->contain_skip = value != 0;
-    return 0;
-  }
-  if (!strcmp(name, "contain_passes")) {  // containment probe passes by source length, longest first
-    ctx->contain_passes = value < 1 ? 1 : value > 16 ? 16 : (int)value;
-    return 0;
-  }
-  if (!strcmp(name, "contain_prune")) {  // 1: skip candidates whose container cannot raise the superkey
-    ctx->contain_prune = value != 0;
-    return 0;
-  }
-  if (!strcmp(name, "prefix_contain")) {  // 1 (default): k_prefix_contain + even-o containment probe
-    ctx->prefix_contain = value != 0;
-    ctx->index_ready = false;
-    return 0;
-  }
-  if (!strcmp(name, "sorted_index")) {  // 1: bucket-sorted key records + plain stores; 0 (default): CAS inserts
-    ctx->sorted_index = value != 0;
-    ctx->index_ready = false;
-    return 0;
-  }
-  if (!strcmp(name, "pack_runs")) {  // 12-B sort records when the widths fit (default 1)
-    ctx->pack_runs = value != 0;
-    ctx->scan_state = 0;
-    ctx->sorted_state = 0;
-    return 0;
-  }
-  if (!strcmp(name, "flat_cap")) {  // tests: initial capacity of the flat run arrays (0 = auto)
+  if (!strcmp(name, "flat_cap")) {  // tests: initial capacity of the exchange scan's flat run arrays (0 = auto)
     ctx->flat_cap_opt = value > 0 ? (uint64_t)value : 0;
     ctx->flat_need = 0;
-    return 0;
-  }
-  if (!strcmp(name, "reg_cas")) {  // 1: the register scan builds the cell index with inline CAS inserts
-    ctx->reg_cas = value != 0;
-    ctx->index_ready = false;
     return 0;
   }
   if (!strcmp(name, "xchg_sort_bits")) {  // exchange mode, P a power of two: top bucket bits the runs are sorted on (0: all)
     ctx->xchg_sort_bits = (int)value;
     return 0;
   }
-  if (!strcmp(name, "sort_bits")) {  // diagnostics: sort only the top sort_bits bucket bits (0: all)
-    ctx->sort_bits = (int)value;
-    ctx->sorted_state = 0;
+  if (flag("stats", &ctx->stats) || flag("halving", &ctx->halving_low) || flag("layout", &ctx->layout) ||
+      flag("contain_jcut", &ctx->contain_jcut) || flag("contain_skip", &ctx->contain_skip) ||
+      flag("contain_prune", &ctx->contain_prune) || flag("probe_share", &ctx->probe_share) ||
+      flag("probe_compact", &ctx->probe_compact))
     return 0;
-  }
-  if (!strcmp(name, "probe_region")) {  // sorted probe: runs per region (0: one tile per wavefront)
-    if (value < 0 || value > (1 << 24)) return set_err(ctx, "probe_region out of range [0, 2^24]");
-    ctx->probe_region = (uint64_t)value;
-    return 0;
-  }
-  if (!strcmp(name, "group_regions")) {  // 1 (default): one run region per read group (read order)
-    ctx->group_regions = value != 0;
-    ctx->scan_state = 0;
-    ctx->sorted_state = 0;
-    return 0;
-  }
-  if (!strcmp(name, "cell_pp")) {  // 1: ping-pong cell tables, the next build's table cleared on a side stream
-    ctx->cell_pp = value != 0;
-    return 0;
-  }
-  if (!strcmp(name, "probe_share_xcd")) {  // 1: shared probe regions dealt XCD-major
-    ctx->probe_share_xcd = value != 0;
-    return 0;
-  }
-  if (!strcmp(name, "probe_share")) {  // 1: a probe block's wavefronts share its run regions batch by batch
-    ctx->probe_share = value != 0;
-    return 0;
-  }
-  if (!strcmp(name, "probe_compact")) {  // 1: sparse run batches are compacted through the pending list
-    ctx->probe_compact = value != 0;
-    return 0;
-  }
-  if (!strcmp(name, "xcd_plain")) {  // 1: the scan's own (wavefront) run regions dealt XCD by XCD too
-    ctx->xcd_plain = value != 0;
-    return 0;
-  }
-  if (!strcmp(name, "xcd_map")) {  // probe regions dealt XCD by XCD (group regions; sorted runs with probe_region)
-    ctx->xcd_map = value != 0;
-    return 0;
-  }
-  if (!strcmp(name, "split")) {
-    ctx->split = value != 0;
-    return 0;
-  }
-  if (!strcmp(name, "stats")) {
-    ctx->stats = value != 0;
-    return 0;
-  }
-  if (!strcmp(name, "rows_cap")) {
-    ctx->rows_cap_opt = (uint64_t)std::max<int64_t>(0, value);
+  if (flag("prefix_contain", &ctx->prefix_contain)) {
+    ctx->index_ready = false;
     return 0;
   }
   return set_err(ctx, std::string("unknown option ") + name);
@@ -3945,7 +2937,8 @@ int mg_set_shard(mg_ctx* ctx, uint32_t rank, uint32_t nranks, uint64_t read_lo, 
   if (!ctx) return -1;
   if (nranks == 0 || rank >= nranks) return set_err(ctx, "bad shard rank/nranks");
   if (read_hi && read_hi < read_lo) return set_err(ctx, "bad read range");
-  if (rank != ctx->rank || nranks != ctx->nranks) ctx->index_ready = false;
+  if (rank != ctx->rank || nranks != ctx->nranks || read_lo != ctx->read_lo || read_hi != ctx->read_hi)
+    ctx->index_ready = false;  // the next mg_build_index re-clusters the slots for a new range (ensure_layout_range)
   ctx->rank = rank;
   ctx->nranks = nranks;
   ctx->read_lo = read_lo;
@@ -3987,8 +2980,6 @@ int setup_index(mg_ctx* ctx, uint32_t min_overlap, uint32_t seed_k, bool cells =
   const uint64_t NB = 1ull << nbl, P = ctx->nranks, r = ctx->rank;
   ctx->cell_lo = (r * NB + P - 1) / P;
   ctx->cell_n = ((r + 1) * NB + P - 1) / P - ctx->cell_lo;
-  ctx->cells_ready = false;
-  ctx->join_ready = false;
   if (cells && setup_cells(ctx)) return -1;
   ctx->index_ready = false;
   ctx->contained_done = false;
@@ -4001,103 +2992,9 @@ int setup_index(mg_ctx* ctx, uint32_t min_overlap, uint32_t seed_k, bool cells =
 
 // the (cleared) cell table of this rank's bucket range
 int setup_cells(mg_ctx* ctx) {
-  if (ctx->d_cells && (ctx->d_cells == ctx->pp_buf[0] || ctx->d_cells == ctx->pp_buf[1])) {
-    ctx->d_cells = nullptr;  // a ping-pong table stays with the ping-pong pair
-    ctx->cells_cap = 0;
-  }
   MG_TRY(ensure(&ctx->d_cells, &ctx->cells_cap, ctx->cell_n * kCell));
   MG_TRY(hipMemsetAsync(ctx->d_cells, 0xFF, ctx->cell_n * kCell * sizeof(uint64_t), ctx->stream));  // kEmpty
   return 0;
-}
-
-int pp_schedule_clear(mg_ctx* ctx);
-// The unsharded build's cell table from a ping-pong pair (option "cell_pp"):
-// this build takes the table cleared behind the previous build, and the table
-// the previous build used is cleared on a side stream behind the work already
-// queued, so the 1 GB fill overlaps this build's latency-bound scan and probe
-// instead of opening it.  Every build still clears exactly one table.
-int setup_cells_pp(mg_ctx* ctx) {
-  const size_t need = ctx->cell_n * kCell;
-  if (!ctx->cell_pp || ctx->nranks != 1) return setup_cells(ctx);
-  if (!ctx->clear_stream) {
-    MG_TRY(hipStreamCreateWithFlags(&ctx->clear_stream, hipStreamNonBlocking));
-    for (auto& e : ctx->ev_clear) MG_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    MG_TRY(hipEventCreateWithFlags(&ctx->ev_use, hipEventDisableTiming));
-  }
-  if (ctx->d_cells && ctx->d_cells != ctx->pp_buf[0] && ctx->d_cells != ctx->pp_buf[1]) {
-    MG_TRY(hipStreamSynchronize(ctx->stream));
-    MG_TRY(hipFree(ctx->d_cells));  // a plain table from an earlier build
-    ctx->d_cells = nullptr;
-    ctx->cells_cap = 0;
-  }
-  if (ctx->pp_cap < need) {  // (re)allocate the pair, both cleared in order on the main stream
-    MG_TRY(hipStreamSynchronize(ctx->clear_stream));
-    MG_TRY(hipStreamSynchronize(ctx->stream));
-    for (int i = 0; i < 2; ++i) {
-      if (ctx->pp_buf[i]) MG_TRY(hipFree(ctx->pp_buf[i]));
-      ctx->pp_buf[i] = nullptr;
-    }
-    ctx->d_cells = nullptr;
-    for (int i = 0; i < 2; ++i) MG_TRY(hipMalloc(&ctx->pp_buf[i], need * sizeof(uint64_t)));
-    ctx->pp_cap = need;
-    for (int i = 0; i < 2; ++i) {
-      ctx->pp_dirty[i] = true;
-      ctx->pp_pending[i] = false;
-    }
-  }
-  if (ctx->pp_due >= 0 && pp_schedule_clear(ctx)) return -1;  // the last build's probe never ran
-  const int cur = ctx->pp_next, oth = cur ^ 1;
-  if (ctx->pp_pending[cur]) {  // its clear runs on the side stream: wait for it on the device
-    MG_TRY(hipStreamWaitEvent(ctx->stream, ctx->ev_clear[cur], 0));
-    ctx->pp_pending[cur] = false;
-  } else if (ctx->pp_dirty[cur]) {  // never cleared (fresh, or a different table geometry)
-    MG_TRY(hipMemsetAsync(ctx->pp_buf[cur], 0xFF, need * sizeof(uint64_t), ctx->stream));
-  }
-  ctx->pp_dirty[cur] = true;  // this build fills it
-  ctx->d_cells = ctx->pp_buf[cur];
-  ctx->cells_cap = need;
-  // the other table is cleared once this build's scan is queued (mg_find_overlaps,
-  // before the discovery probe): the fill then overlaps the latency-bound probe,
-  // not the scan, whose CAS inserts it slowed (3.42 vs 3.20 ms when overlapped)
-  ctx->pp_due = (ctx->pp_dirty[oth] && !ctx->pp_pending[oth]) ? oth : -1;
-  ctx->pp_next = oth;
-  return 0;
-}
-
-// queue the due ping-pong clear on the side stream behind everything queued so far
-int pp_schedule_clear(mg_ctx* ctx) {
-  const int i = ctx->pp_due;
-  ctx->pp_due = -1;
-  if (i < 0 || !ctx->clear_stream || !ctx->pp_buf[i]) return 0;
-  MG_TRY(hipEventRecord(ctx->ev_use, ctx->stream));
-  MG_TRY(hipStreamWaitEvent(ctx->clear_stream, ctx->ev_use, 0));
-  // the whole buffer: a later build may span more cells than this one
-  MG_TRY(hipMemsetAsync(ctx->pp_buf[i], 0xFF, ctx->pp_cap * sizeof(uint64_t), ctx->clear_stream));
-  MG_TRY(hipEventRecord(ctx->ev_clear[i], ctx->clear_stream));
-  ctx->pp_pending[i] = true;
-  ctx->pp_dirty[i] = false;
-  return 0;
-}
-
-// Partitioned join geometry (option "join"): the unsharded fused
-// path with a register scan (w <= kRegW) whose record fields fit 12 bytes.
-// P = partition bits, chosen for ~2.5k keys per partition (one LDS table fill).
-bool join_geometry(mg_ctx* ctx) {
-  auto bits = [](uint64_t x) { int b = 0; while (x) { ++b; x >>= 1; } return b; };
-  ctx->join_P = 0;
-  if (!ctx->join || ctx->nranks != 1 || !ctx->overlap_scan || !use_scan_reg_w(ctx) || ctx->maxw > 32) return false;
-  const int A = std::max(1, bits(ctx->n));  // read index < 2^A
-  const int WB = bits(ctx->w - 1), QB = WB;
-  const double keys = 4.0 * (double)std::max<uint64_t>(ctx->n, 1);
-  int P = (int)std::lround(std::log2(std::max(2.0, keys / 2500.0)));
-  P = std::min(16, std::max(1, P));
-  if (ctx->join_P_opt) P = ctx->join_P_opt;  // option "join_parts_log2" (tests: force multi-chunk partitions)
-  if (A > 32 || A + 12 + 2 * WB + P > 64 || A + 4 + QB + P > 64) return false;
-  ctx->join_P = P;
-  ctx->join_A = A;
-  ctx->join_QB = QB;
-  ctx->join_WB = WB;
-  return true;
 }
 
 // this rank's source reads in exchange mode: [floor(r N / P), floor((r+1) N / P))
@@ -4175,11 +3072,10 @@ struct LaunchScanXchg {
 // records, counts in ctx->d_flat_cnt)
 template <int W>
 struct LaunchProbeSlots {
-  static int run(mg_ctx* ctx, bool contain, const ulonglong2* runs, uint64_t reg, uint64_t nregions,
-                 uint64_t approx_runs) {
+  static int run(mg_ctx* ctx, bool contain, const ulonglong2* runs, uint64_t reg, uint64_t nregions) {
     const DiscGeom g = disc_geom<W>(ctx, contain, std::max<uint64_t>(1, ctx->n / ctx->nranks));
     const uint32_t* sup = (!contain && ctx->contained_done && ctx->super_any) ? ctx->d_super : nullptr;
-    return LaunchProbe<W>::run(ctx, contain, runs, ctx->d_flat_cnt, reg, nregions, g.grid, approx_runs, sup);
+    return LaunchProbe<W>::run(ctx, contain, runs, ctx->d_flat_cnt, reg, nregions, g.grid, sup);
   }
 };
 
@@ -4249,26 +3145,39 @@ void read_stats(mg_ctx* ctx, uint64_t nsrc) {
   ctx->counters.sources = nsrc;
   ctx->counters.trips = st[kSegs * 4];
 }
-// The window scan of ALL sources, unfiltered (runs of contained or foreign
-// sources are dropped by the probe).  With index = true it is k_scan<INDEX>:
+// The window scan of ALL sources, unfiltered (runs of contained sources are
+// dropped by the probe) and fused with the index build (k_scan<INDEX>):
 // mg_build_index runs it as THE index build, so one pass over the reads files
 // every key and leaves the runs that the containment and the discovery probes
 // both consume.
 template <int W>
 struct LaunchScanAll {
-  static int run(mg_ctx* ctx, hipStream_t st, bool index) {
-    const uint32_t wpb = scan_block_waves(ctx, index);
+  static int run(mg_ctx* ctx, hipStream_t st) {
+    const uint32_t wpb = scan_block_waves(ctx, true);
     const uint64_t groups = (ctx->n + kWave - 1) / kWave;
-    const uint32_t sgrid = scan_resident<W>(ctx, index, (groups + wpb - 1) / wpb);
-    return LaunchScan<W>::run(ctx, true, 0, ctx->n, sgrid, false, st, true, index,
-                              ctx->sort_runs || (index && ctx->join_P));
+    const uint32_t sgrid = scan_resident<W>(ctx, true, (groups + wpb - 1) / wpb);
+    return LaunchScan<W>::run(ctx, true, 0, ctx->n, sgrid, false, st, true, true, false);
   }
 };
 
-bool shared_scan(const mg_ctx* ctx) { return ctx->nranks == 1 && ctx->overlap_scan; }
+// the same scan without the index (a rerun after the shared scan's run
+// regions overflowed: the cells are already filled)
+template <int W>
+struct LaunchScanRuns {
+  static int run(mg_ctx* ctx) {
+    const uint32_t wpb = scan_block_waves(ctx, false);
+    const uint64_t groups = (ctx->n + kWave - 1) / kWave;
+    const uint32_t sgrid = scan_resident<W>(ctx, false, (groups + wpb - 1) / wpb);
+    return LaunchScan<W>::run(ctx, true, 0, ctx->n, sgrid, false, ctx->stream, true, false, false);
+  }
+};
 
-// the shared scan's region counts settled (rerun without the index part on overflow)
-// flat scan output: the cursor is the run count; on overflow size for it and rerun
+// one shared scan per build: an unsharded context over all its sources (a
+// source-read range takes the separate index build + a scan of its slots)
+bool shared_scan(const mg_ctx* ctx) { return ctx->nranks == 1 && ctx->read_lo == 0 && ctx->read_hi == 0; }
+
+// flat scan output (exchange mode): the cursor is the run count; on overflow
+// size for it and rerun
 int settle_flat(mg_ctx* ctx, bool* again) {
   *again = false;
   unsigned long long c[kFlatCounters] = {};
@@ -4280,8 +3189,8 @@ int settle_flat(mg_ctx* ctx, bool* again) {
   for (uint32_t x = 0; x < kFlatCounters; ++x)
     if (c[x]) ext = std::max<uint64_t>(ext, (c[x] - 1) * kFlatCounters + x + 1);
   const uint64_t n = ext * kFlatChunk;
-  if (ctx->flat_off + n > ctx->sk_cap) {
-    ctx->flat_need = ctx->flat_off + n + n / 8 + 4096;
+  if (n > ctx->sk_cap) {
+    ctx->flat_need = n + n / 8 + 4096;
     *again = true;
     return 0;
   }
@@ -4295,36 +3204,31 @@ int settle_flat(mg_ctx* ctx, bool* again) {
     MG_TRY(ensure(&ctx->d_holes, &ctx->holes_cap, nh));
     MG_TRY(hipMemcpyAsync(ctx->d_holes, ctx->holes_host.data(), nh * sizeof(uint64_t), hipMemcpyHostToDevice,
                           ctx->stream));
-    const bool packed = ctx->pack_a || ctx->join_P;
-    uint64_t* keys = packed ? reinterpret_cast<uint64_t*>(reinterpret_cast<uint32_t*>(ctx->d_sk[0]) + ctx->flat_off)
-                            : ctx->d_sk[0] + ctx->flat_off;
-    hipLaunchKernelGGL(k_fill_holes, dim3((uint32_t)nh), dim3(kBlock), 0, ctx->stream, ctx->d_holes, keys,
-                       ctx->d_sm[0] + ctx->flat_off, packed ? 1 : 0);
+    hipLaunchKernelGGL(k_fill_holes, dim3((uint32_t)nh), dim3(kBlock), 0, ctx->stream, ctx->d_holes, ctx->d_sk[0],
+                       ctx->d_sm[0], ctx->pack_a ? 1 : 0);
     MG_TRY(hipGetLastError());
   }
-  ctx->n_flat = ctx->flat_off + n;
+  ctx->n_flat = n;
   return 0;
 }
 
-int settle_scan(mg_ctx* ctx, bool* again) {
-  return ctx->scan_flat ? settle_flat(ctx, again) : settle_runs(ctx, again);
-}
-
+// the shared scan's region counts settled (its overflow reruns a plain run scan)
 int ensure_scan(mg_ctx* ctx) {
   if (ctx->scan_state == 2) return 0;
   if (ctx->scan_state == 1) {
     bool again = false;
-    if (settle_scan(ctx, &again)) return -1;
+    if (settle_runs(ctx, &again)) return -1;
     ctx->scan_state = again ? 0 : 2;
     if (!again) return 0;
   }
-  ctx->sorted_state = 0;
   for (int attempt = 0; attempt < 3; ++attempt) {
-    if (ctx->n && dispatch_w<LaunchScanAll>(ctx->maxw, ctx, ctx->stream, false))
-      return set_err(ctx, "scan launch failed");
-    if (!ctx->n) ctx->nrun_reg = 0;
+    if (ctx->n) {
+      if (dispatch_w<LaunchScanRuns>(ctx->maxw, ctx)) return set_err(ctx, "scan launch failed");
+    } else {
+      ctx->nrun_reg = 0;
+    }
     bool again = false;
-    if (settle_scan(ctx, &again)) return -1;
+    if (settle_runs(ctx, &again)) return -1;
     if (!again) {
       ctx->scan_state = 2;
       return 0;
@@ -4336,79 +3240,22 @@ int ensure_scan(mg_ctx* ctx) {
 template <int W>
 struct LaunchProbeShared {
   static int run(mg_ctx* ctx, bool contain) {
-    uint64_t total = 0;
-    if (!ctx->scan_flat)  // (a flat scan leaves no per-region counts on the host)
-      for (uint64_t r = 0; r < ctx->nrun_reg && r < ctx->run_cnt_host.size(); ++r)
-        total += std::min<uint64_t>(ctx->run_cnt_host[r], ctx->run_cap);
     const DiscGeom g = disc_geom<W>(ctx, contain, std::max<uint64_t>(ctx->n, 1));
     const uint32_t* sup = (!contain && ctx->contained_done && ctx->super_any) ? ctx->d_super : nullptr;
-    const uint64_t lo = contain ? 0 : ctx->read_lo;
-    const uint64_t hi = contain ? 0 : (ctx->read_hi ? std::min(ctx->read_hi, ctx->n) : 0);
-    if (ctx->sort_runs && ctx->sorted_state == 2) {
-      // bucket-ordered runs: one contiguous tile per probe wavefront
-      const uint64_t n = ctx->n_sorted;
-      // regions: one contiguous tile per probe wavefront, or (option
-      // probe_region = R) regions of R runs, dealt XCD by XCD (option xcd_map)
-      const uint64_t R = ctx->probe_region;
-      const uint64_t nw = R ? std::max<uint64_t>(1, (n + R - 1) / R) : (uint64_t)g.grid * kWavesPerBlock;
-      const uint64_t cap = R ? R : std::max<uint64_t>(1, (n + nw - 1) / nw);
-      if (ctx->flat_cnt_cap < nw) {
-        if (ctx->d_flat_cnt) (void)hipFree(ctx->d_flat_cnt);
-        ctx->d_flat_cnt = nullptr;
-        if (hipMalloc(&ctx->d_flat_cnt, nw * sizeof(unsigned long long)) != hipSuccess) return -1;
-        ctx->flat_cnt_cap = nw;
-      }
-      hipLaunchKernelGGL(k_flat_counts, dim3((uint32_t)((nw + kBlock - 1) / kBlock)), dim3(kBlock), 0, ctx->stream,
-                         ctx->d_flat_cnt, nw, cap, n);
-      if (hipGetLastError() != hipSuccess) return -1;
-      return LaunchProbe<W>::run(ctx, contain, nullptr, ctx->d_flat_cnt, cap, nw, g.grid, n, sup, lo, hi,
-                                 ctx->d_sk[ctx->sk_sel], ctx->d_sm[ctx->sk_sel], ctx->pack_a, ctx->pack_w,
-                                 (R && ctx->xcd_map) ? 1 : 0);
-    }
-    return LaunchProbe<W>::run(ctx, contain, ctx->d_runs, ctx->d_run_cnt, ctx->run_cap, ctx->nrun_reg, g.grid, total,
-                               sup, lo, hi, nullptr, nullptr, 0, 0,
-                               ((ctx->group_active || ctx->xcd_plain) && ctx->xcd_map) ? 1 : 0);
+    return LaunchProbe<W>::run(ctx, contain, ctx->d_runs, ctx->d_run_cnt, ctx->run_cap, ctx->nrun_reg, g.grid, sup);
   }
 };
 
-// option "sort_runs": the settled shared-scan runs -> SoA arrays (k_runs_soa)
-// -> rocprim radix sort by bucket (8 bits per pass), so consecutive probe items share
-// cells and, through the cells' entries, partner reads.  Option "sort_bits"
-// (diagnostics) sorts only the top sort_bits bucket bits.
-int sort_shared_runs(mg_ctx* ctx, int bits = -1) {
-  if (ctx->sorted_state == 2) return 0;
-  const bool flat = ctx->scan_flat;  // the scan already wrote d_sk[0] / d_sm[0]
-  const uint64_t nreg = flat ? 0 : ctx->nrun_reg;
-  std::vector<unsigned long long> off(nreg + 1, 0);
-  for (uint64_t r = 0; r < nreg; ++r) off[r + 1] = off[r] + std::min<uint64_t>(ctx->run_cnt_host[r], ctx->run_cap);
-  const uint64_t n = flat ? ctx->n_flat : off[nreg];
-  if (n > 0x7FFFFFFFull) return set_err(ctx, "sort_runs: more than 2^31 runs");
-  MG_TRY(ensure(&ctx->d_run_off, &ctx->run_off_cap, nreg + 1));
-  if (!flat && n > ctx->sk_cap) {
-    for (int b = 0; b < 2; ++b) {
-      if (ctx->d_sk[b]) (void)hipFree(ctx->d_sk[b]);
-      if (ctx->d_sm[b]) (void)hipFree(ctx->d_sm[b]);
-      ctx->d_sk[b] = ctx->d_sm[b] = nullptr;
-    }
-    ctx->sk_cap = 0;
-    for (int b = 0; b < 2; ++b) {
-      MG_TRY(hipMalloc(&ctx->d_sk[b], std::max<uint64_t>(n, 1) * sizeof(uint64_t)));
-      MG_TRY(hipMalloc(&ctx->d_sm[b], std::max<uint64_t>(n, 1) * sizeof(uint64_t)));
-    }
-    ctx->sk_cap = n;
-  }
+// exchange mode: the flat runs of this rank's scan -> rocprim radix sort by
+// bucket (8 bits per pass; `bits` > 0: only the top `bits` bucket bits), which
+// groups them by owning rank for mg_xchg_pack(MG_RUNS)
+int sort_flat_runs(mg_ctx* ctx, int bits) {
+  const uint64_t n = ctx->n_flat;
+  if (n > 0x7FFFFFFFull) return set_err(ctx, "exchange: more than 2^31 runs on one rank");
   MG_TRY(hipEventRecord(ctx->ev[12], ctx->stream));
-  if (!flat)
-    MG_TRY(hipMemcpyAsync(ctx->d_run_off, off.data(), (nreg + 1) * sizeof(unsigned long long),
-                          hipMemcpyHostToDevice, ctx->stream));
-  if (nreg)
-    hipLaunchKernelGGL(k_runs_soa, dim3((uint32_t)nreg), dim3(kBlock), 0, ctx->stream, ctx->d_runs, ctx->run_cap,
-                       ctx->d_run_off, ctx->d_sk[0], ctx->d_sm[0]);
-  MG_TRY(hipGetLastError());
   const unsigned nb = ctx->nb_log2;
-  if (bits < 0) bits = ctx->sort_bits;
   const unsigned lo_bit = (bits > 0 && (unsigned)bits < nb) ? nb - (unsigned)bits : 0u;
-  const bool packed = flat && ctx->pack_a;  // 32-bit keys (run_pack_key)
+  const bool packed = ctx->pack_a != 0;  // 32-bit keys (run_pack_key)
   auto sort = [&](void* tmp, size_t& tb, int& sel) -> hipError_t {
     rocprim::double_buffer<uint64_t> vals(ctx->d_sm[0], ctx->d_sm[1]);
     hipError_t e;
@@ -4431,6 +3278,7 @@ int sort_shared_runs(mg_ctx* ctx, int bits = -1) {
   if (tb > ctx->sort_tmp_cap) {
     if (ctx->d_sort_tmp) (void)hipFree(ctx->d_sort_tmp);
     ctx->d_sort_tmp = nullptr;
+    ctx->sort_tmp_cap = 0;
     MG_TRY(hipMalloc(&ctx->d_sort_tmp, tb));
     ctx->sort_tmp_cap = tb;
   }
@@ -4439,292 +3287,135 @@ int sort_shared_runs(mg_ctx* ctx, int bits = -1) {
   MG_TRY(hipEventRecord(ctx->ev[13], ctx->stream));
   ctx->sk_sel = sel;
   ctx->n_sorted = n;
-  ctx->sorted_state = 2;
   return 0;
 }
 
 // probe the shared scan's runs (rows settled for the discovery probe)
 int probe_shared(mg_ctx* ctx, bool contain) {
   if (ensure_scan(ctx)) return -1;
-  if (ctx->sort_runs) {
-    if (sort_shared_runs(ctx)) return -1;
-  }
-  for (int attempt = 0; attempt < 3; ++attempt) {
-    ctx->nreg = 0;
-    if (!ctx->split) MG_TRY(hipEventRecord(ctx->ev[8], ctx->stream));
-    if (dispatch_w<LaunchProbeShared>(ctx->maxw, ctx, contain)) return set_err(ctx, "probe launch failed");
-    if (!ctx->split) MG_TRY(hipEventRecord(ctx->ev[9], ctx->stream));
-    if (contain || ctx->split) return 0;  // the split path settles its rows itself
-    bool again = false;
-    if (settle_rows(ctx, &again)) return -1;
-    if (!again) return 0;
-  }
-  return set_err(ctx, "row buffers overflow after resize");
-}
-}  // namespace
-
-namespace {
-// ------------------------------------------------------ join host path ---
-// k_scan_reg<INDEX> with join records -> settle (overflow: resize, rerun) ->
-// radix sort by (partition, type) -> partition bounds.
-int build_join(mg_ctx* ctx) {
-  ctx->join_ready = false;
-  for (int attempt = 0;; ++attempt) {
-    if (attempt == 3) return set_err(ctx, "join record buffers overflow after resize");
-    if (ctx->n && dispatch_w<LaunchScanAll>(ctx->maxw, ctx, ctx->stream, true))
-      return set_err(ctx, "index build launch failed");
-    bool again = false;
-    if (ctx->n) {
-      if (settle_flat(ctx, &again)) return -1;
-    } else {
-      ctx->n_flat = 0;
-    }
-    if (!again) break;
-  }
-  ctx->shared_scan_ms = ctx->n ? elapsed(ctx->ev[6], ctx->ev[7]) : 0.f;
-  const uint64_t n = ctx->n_flat;
-  if (n > 0x7FFFFFFFull) return set_err(ctx, "join: more than 2^31 records");
-  const unsigned bits = (unsigned)ctx->join_P + 2;
-  MG_TRY(hipEventRecord(ctx->ev[12], ctx->stream));
-  int sel = 0;
-  if (n) {
-    auto sort = [&](void* tmp, size_t& tb) -> hipError_t {
-      rocprim::double_buffer<uint32_t> keys(reinterpret_cast<uint32_t*>(ctx->d_sk[0]),
-                                            reinterpret_cast<uint32_t*>(ctx->d_sk[1]));
-      rocprim::double_buffer<uint64_t> vals(ctx->d_sm[0], ctx->d_sm[1]);
-      hipError_t e = rocprim::radix_sort_pairs(tmp, tb, keys, vals, (unsigned int)n, 0u, bits, ctx->stream);
-      sel = keys.current() == reinterpret_cast<uint32_t*>(ctx->d_sk[0]) ? 0 : 1;
-      if (e == hipSuccess && tmp && (vals.current() == ctx->d_sm[0] ? 0 : 1) != sel) e = hipErrorUnknown;
-      return e;
-    };
-    size_t tb = 0;
-    MG_TRY(sort(nullptr, tb));
-    if (tb > ctx->sort_tmp_cap) {
-      if (ctx->d_sort_tmp) (void)hipFree(ctx->d_sort_tmp);
-      ctx->d_sort_tmp = nullptr;
-      MG_TRY(hipMalloc(&ctx->d_sort_tmp, tb));
-      ctx->sort_tmp_cap = tb;
-    }
-    tb = ctx->sort_tmp_cap;
-    MG_TRY(sort(ctx->d_sort_tmp, tb));
-  }
-  ctx->sk_sel = sel;
-  const uint32_t nparts = 1u << ctx->join_P;
-  MG_TRY(ensure(&ctx->d_bnd, &ctx->bnd_cap, (size_t)nparts + 1));
-  MG_TRY(ensure(&ctx->d_mid, &ctx->mid_cap, (size_t)nparts));
-  const uint32_t targets = 2 * nparts + 1;
-  hipLaunchKernelGGL(k_join_bounds, dim3((targets + kBlock - 1) / kBlock), dim3(kBlock), 0, ctx->stream,
-                     reinterpret_cast<const uint32_t*>(ctx->d_sk[sel]), n, ctx->join_P, ctx->d_bnd, ctx->d_mid, nparts);
-  MG_TRY(hipGetLastError());
-  MG_TRY(hipEventRecord(ctx->ev[13], ctx->stream));
-  ctx->join_ready = true;
-  return 0;
-}
-
-template <int W>
-struct LaunchJoin {
-  static int run(mg_ctx* ctx, bool contain) {
-    JoinParams jp{};
-    jp.words = ctx->d_words;
-    jp.len = ctx->d_len;
-    jp.id = ctx->d_id;
-    jp.h = (int)ctx->h;
-    jp.P = ctx->join_P;
-    jp.A = ctx->join_A;
-    jp.QB = ctx->join_QB;
-    jp.WB = ctx->join_WB;
-    jp.k32 = reinterpret_cast<const uint32_t*>(ctx->d_sk[ctx->sk_sel]);
-    jp.val = ctx->d_sm[ctx->sk_sel];
-    jp.bnd = ctx->d_bnd;
-    jp.mid = ctx->d_mid;
-    jp.nparts = 1u << ctx->join_P;
-    jp.queue = ctx->d_queue;
-    const bool sup = !contain && ctx->contained_done && ctx->super_any;
-    jp.super = sup ? ctx->d_super : nullptr;
-    jp.src_super = sup ? ctx->d_super : nullptr;
-    jp.src_lo = contain ? 0 : ctx->read_lo;
-    jp.src_hi = contain ? 0 : (ctx->read_hi ? std::min(ctx->read_hi, ctx->n) : 0);
-    jp.superkey = ctx->superkey;
-    jp.prefix_queries = (contain && ctx->prefix_contain) ? 1 : 0;
-    jp.contain_even = jp.prefix_queries;
-    jp.uniform_len = ctx->minlen == ctx->maxlen ? (int)ctx->maxlen : 0;
-    jp.halving_low = ctx->halving_low ? 1 : 0;
-    jp.stats = contain ? nullptr : (ctx->stats ? ctx->d_stats : nullptr);
-    jp.phase_limit = contain ? 99 : ctx->phase_limit;
-    const uint32_t grid = contain ? resident_blocks(ctx, k_join<W, true>, kJoinLds, jp.nparts, kJoinBlock)
-                                  : resident_blocks(ctx, k_join<W, false>, kJoinLds, jp.nparts, kJoinBlock);
-    ctx->nreg = (uint64_t)grid * kJoinWaves;  // join wavefronts = row regions
-    jp.rows = ctx->d_rows;
-    jp.reg_cnt = ctx->d_seg;
-    jp.reg_cap = contain ? 0 : ctx->rows_cap / ctx->nreg;
-    if (hipMemsetAsync(ctx->d_queue, 0, sizeof(unsigned int), ctx->stream) != hipSuccess) return -1;
-    if (contain)
-      hipLaunchKernelGGL((k_join<W, true>), dim3(grid), dim3(kJoinBlock), kJoinLds, ctx->stream, jp);
-    else
-      hipLaunchKernelGGL((k_join<W, false>), dim3(grid), dim3(kJoinBlock), kJoinLds, ctx->stream, jp);
-    return hipGetLastError() == hipSuccess ? 0 : -1;
-  }
-};
-
-// one join pass (containment or discovery); discovery rows are settled
-// (resized and rerun on overflow)
-int probe_join(mg_ctx* ctx, bool contain) {
-  if (!ctx->d_queue) MG_TRY(hipMalloc(&ctx->d_queue, sizeof(unsigned int)));
   for (int attempt = 0; attempt < 3; ++attempt) {
     ctx->nreg = 0;
     MG_TRY(hipEventRecord(ctx->ev[8], ctx->stream));
-    if (dispatch_w<LaunchJoin>(ctx->maxw, ctx, contain)) return set_err(ctx, "join launch failed");
+    if (dispatch_w<LaunchProbeShared>(ctx->maxw, ctx, contain)) return set_err(ctx, "probe launch failed");
     MG_TRY(hipEventRecord(ctx->ev[9], ctx->stream));
     if (contain) return 0;
     bool again = false;
     if (settle_rows(ctx, &again)) return -1;
     if (!again) return 0;
-    if (ctx->stats) MG_TRY(hipMemsetAsync(ctx->d_stats, 0, (kSegs * 4 + 1) * sizeof(unsigned long long), ctx->stream));
   }
   return set_err(ctx, "row buffers overflow after resize");
 }
-
-// the cell table for getListOfReads when the index was built as join records
-int ensure_cells(mg_ctx* ctx) {
-  if (ctx->cells_ready) return 0;
-  if (setup_cells(ctx)) return -1;
-  if (ctx->n && launch_index(ctx)) return set_err(ctx, "cell index launch failed");
-  ctx->cells_ready = true;
-  return 0;
-}
 }  // namespace
 
-// Device layout of freshly uploaded reads (mg_ctx.hpp): layout keys ->
-// rocprim radix sort of (key, ID - 1) -> gather into a new slot array.  The
-// scratch (keys, the old slots) is freed before returning.
-int apply_layout(mg_ctx* ctx) {
+// Device layout (mg_ctx.hpp): layout keys -> rocprim radix sort
+// of (key, slot) -> gather into the second slot array -> commit.  Every
+// buffer is the context's own and kept between uploads, so the timed window
+// (ev[14] .. ev[15], t.layout_ms) holds kernels only; nothing the context
+// holds changes until the commit, which swaps the slot arrays and the
+// ID maps after every launch succeeded.  Composes with the current order
+// (d_id), so a new source-read range re-clusters resident reads.
+int layout_current(mg_ctx* ctx, bool force) {
   ctx->t.layout_ms = 0.f;
-  if (!ctx->layout || ctx->n < 2 || long_mode(ctx)) {  // ID order (long reads: always)
-    if (ctx->d_id) (void)hipFree(ctx->d_id);
-    if (ctx->d_phys) (void)hipFree(ctx->d_phys);
-    ctx->d_id = ctx->d_phys = nullptr;
-    ctx->id_cap = ctx->phys_cap = 0;
-    return 0;
-  }
   const uint64_t n = ctx->n;
+  if ((!ctx->layout && !force) || n < 2 || long_mode(ctx)) return 0;  // ID order (long reads: always)
   if (n >= 0xFFFFFFFFull) return set_err(ctx, "layout: too many reads");
-  struct Scratch {
-    void* p[6] = {};
-    ~Scratch() {
-      for (void* x : p)
-        if (x) (void)hipFree(x);
-    }
-  } sc;
-  MG_TRY(hipEventRecord(ctx->ev[14], ctx->stream));
-  MG_TRY(hipMalloc(&sc.p[0], n * sizeof(uint64_t)));
-  MG_TRY(hipMalloc(&sc.p[1], n * sizeof(uint64_t)));
-  MG_TRY(hipMalloc(&sc.p[2], n * sizeof(uint32_t)));
-  MG_TRY(hipMalloc(&sc.p[3], n * sizeof(uint32_t)));
-  uint64_t* k0 = static_cast<uint64_t*>(sc.p[0]);
-  uint64_t* k1 = static_cast<uint64_t*>(sc.p[1]);
-  uint32_t* v0 = static_cast<uint32_t*>(sc.p[2]);
-  uint32_t* v1 = static_cast<uint32_t*>(sc.p[3]);
-  if (dispatch_w<LaunchLayout>(ctx->maxw, ctx, k0, v0)) return set_err(ctx, "layout key launch failed");
+  uint64_t lo = ctx->read_lo < n ? ctx->read_lo : n;
+  uint64_t hi = ctx->read_hi ? std::min<uint64_t>(ctx->read_hi, n) : n;
+  if (hi < lo) hi = lo;
+  const int grouped = (lo > 0 || hi < n) ? 1 : 0;
+  int pb = 1;
+  while (pb < 10 && (1u << pb) <= ctx->maxlen) ++pb;  // offsets < maxlen (capped at 10 bits)
+  for (int b = 0; b < 2; ++b) {
+    MG_TRY(ensure(&ctx->d_lay_k[b], &ctx->lay_k_cap[b], n));
+    MG_TRY(ensure(&ctx->d_lay_v[b], &ctx->lay_v_cap[b], n));
+  }
   size_t tb = 0;
-  MG_TRY(rocprim::radix_sort_pairs(nullptr, tb, k0, k1, v0, v1, (unsigned int)n, 0u, 64u, ctx->stream));
-  MG_TRY(hipMalloc(&sc.p[4], std::max<size_t>(tb, 1)));
-  MG_TRY(rocprim::radix_sort_pairs(sc.p[4], tb, k0, k1, v0, v1, (unsigned int)n, 0u, 64u, ctx->stream));
-  MG_TRY(ensure(&ctx->d_id, &ctx->id_cap, n));
-  MG_TRY(ensure(&ctx->d_phys, &ctx->phys_cap, n));
-  // new slot array (same size and zero pad as the upload's); the old one is freed
-  const size_t nw = ctx->words_cap;
-  uint64_t* nwords = nullptr;
-  MG_TRY(hipMalloc(&nwords, nw * sizeof(uint64_t)));
-  sc.p[5] = nwords;
-  uint16_t* nlen = reinterpret_cast<uint16_t*>(k0);  // keys are dead after the sort: reuse for the lengths
-  MG_TRY(hipMemsetAsync(nwords, 0, nw * sizeof(uint64_t), ctx->stream));
-  if (dispatch_w<LaunchLayoutGather>(ctx->maxw, ctx, ctx->d_words, ctx->d_len, v1, nwords, nlen))
+  MG_TRY(rocprim::radix_sort_pairs(nullptr, tb, ctx->d_lay_k[0], ctx->d_lay_k[1], ctx->d_lay_v[0], ctx->d_lay_v[1],
+                                   (unsigned int)n, 0u, 32u, ctx->stream));
+  if (tb > ctx->lay_tmp_cap) {
+    if (ctx->d_lay_tmp) MG_TRY(hipFree(ctx->d_lay_tmp));
+    ctx->d_lay_tmp = nullptr;
+    ctx->lay_tmp_cap = 0;
+    MG_TRY(hipMalloc(&ctx->d_lay_tmp, tb));
+    ctx->lay_tmp_cap = tb;
+  }
+  tb = ctx->lay_tmp_cap;
+  MG_TRY(ensure(&ctx->d_words_alt, &ctx->words_alt_cap, ctx->words_cap));
+  MG_TRY(ensure(&ctx->d_len_alt, &ctx->len_alt_cap, ctx->len_cap));
+  // the new maps go to the pair the current order does not use
+  const int sel = (ctx->d_id && ctx->d_id == ctx->id_store[0]) ? 1 : 0;
+  MG_TRY(ensure(&ctx->id_store[sel], &ctx->id_cap[sel], n));
+  MG_TRY(ensure(&ctx->phys_store[sel], &ctx->phys_cap[sel], n));
+  uint32_t* id_new = ctx->id_store[sel];
+  uint32_t* ph_new = ctx->phys_store[sel];
+  const uint64_t S = slot_words((int)ctx->maxw);
+  // --- timed: kernels only
+  MG_TRY(hipEventRecord(ctx->ev[14], ctx->stream));
+  if (dispatch_w<LaunchLayout>(ctx->maxw, ctx, lo, hi, grouped, pb, ctx->d_lay_k[0], ctx->d_lay_v[0]))
+    return set_err(ctx, "layout key launch failed");
+  MG_TRY(rocprim::radix_sort_pairs(ctx->d_lay_tmp, tb, ctx->d_lay_k[0], ctx->d_lay_k[1], ctx->d_lay_v[0],
+                                   ctx->d_lay_v[1], (unsigned int)n, 0u, 32u, ctx->stream));
+  if (dispatch_w<LaunchLayoutGather>(ctx->maxw, ctx, ctx->d_lay_v[1], ctx->d_words_alt, ctx->d_len_alt, id_new))
     return set_err(ctx, "layout gather launch failed");
-  MG_TRY(hipMemcpyAsync(ctx->d_len, nlen, n * sizeof(uint16_t), hipMemcpyDeviceToDevice, ctx->stream));
+  // the zero pad past the last slot (over-reads of the kernels)
+  MG_TRY(hipMemsetAsync(ctx->d_words_alt + n * S, 0, (ctx->words_cap - n * S) * sizeof(uint64_t), ctx->stream));
+  hipLaunchKernelGGL(k_layout_phys, dim3((uint32_t)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, ctx->stream, id_new,
+                     n, ph_new);
+  MG_TRY(hipGetLastError());
   MG_TRY(hipEventRecord(ctx->ev[15], ctx->stream));
   MG_TRY(hipStreamSynchronize(ctx->stream));
-  sc.p[5] = ctx->d_words;  // the ID-order slots go with the scratch
-  ctx->d_words = nwords;
+  // --- commit
+  std::swap(ctx->d_words, ctx->d_words_alt);
+  std::swap(ctx->words_cap, ctx->words_alt_cap);
+  std::swap(ctx->d_len, ctx->d_len_alt);
+  std::swap(ctx->len_cap, ctx->len_alt_cap);
+  ctx->d_id = id_new;
+  ctx->d_phys = ph_new;
+  ctx->layout_lo = grouped ? lo : 0;
+  ctx->layout_hi = grouped ? hi : 0;
   ctx->t.layout_ms = elapsed(ctx->ev[14], ctx->ev[15]);
+  return 0;
+}
+
+// the reads were just written in ID order (upload / ingest)
+int apply_layout(mg_ctx* ctx) {
+  ctx->d_id = ctx->d_phys = nullptr;
+  ctx->layout_lo = ctx->layout_hi = 0;
+  return layout_current(ctx, false);
+}
+
+// a source-read range set after the upload: re-cluster so that the range's
+// reads take the slots [read_lo, read_hi)
+int ensure_layout_range(mg_ctx* ctx) {
+  if (!ctx->d_id) return 0;  // ID order: slots are IDs
+  const uint64_t n = ctx->n;
+  const uint64_t lo = ctx->read_lo < n ? ctx->read_lo : n;
+  const uint64_t hi = ctx->read_hi ? std::min<uint64_t>(ctx->read_hi, n) : n;
+  const bool grouped = lo > 0 || hi < n;
+  if (grouped ? (ctx->layout_lo == lo && ctx->layout_hi == hi) : (ctx->layout_lo == 0 && ctx->layout_hi == 0)) return 0;
+  if (layout_current(ctx, true)) return -1;  // (option layout = 0 applies from the next upload)
+  reset_derived(ctx);
   return 0;
 }
 
 extern "C" {
 
-// Sorted index build, after k_scan<INDEX> wrote the 4N key records to
-// d_kb[0] / d_ke[0]: stable radix sort by bucket (nb bits), then the home-slot
-// fill and the overflow chain walk (k_fill_cells).
-int fill_sorted_index(mg_ctx* ctx) {
-  const uint64_t n = 4 * ctx->n;
-  if (!n) return 0;
-  if (n > 0xFFFFFFFFull) return set_err(ctx, "sorted_index: more than 2^32 keys");
-  auto sort = [&](void* tmp, size_t& tb, int& sel) -> hipError_t {
-    rocprim::double_buffer<uint32_t> keys(ctx->d_kb[0], ctx->d_kb[1]);
-    rocprim::double_buffer<uint64_t> vals(ctx->d_ke[0], ctx->d_ke[1]);
-    hipError_t e = rocprim::radix_sort_pairs(tmp, tb, keys, vals, (unsigned int)n, 0u, ctx->nb_log2, ctx->stream);
-    sel = keys.current() == ctx->d_kb[0] ? 0 : 1;
-    if (e == hipSuccess && tmp && (vals.current() == ctx->d_ke[0] ? 0 : 1) != sel) e = hipErrorUnknown;
-    return e;
-  };
-  size_t tb = 0;
-  int sel = 0;
-  MG_TRY(sort(nullptr, tb, sel));
-  if (tb > ctx->sort_tmp_cap) {
-    if (ctx->d_sort_tmp) (void)hipFree(ctx->d_sort_tmp);
-    ctx->d_sort_tmp = nullptr;
-    MG_TRY(hipMalloc(&ctx->d_sort_tmp, tb));
-    ctx->sort_tmp_cap = tb;
-  }
-  tb = ctx->sort_tmp_cap;
-  MG_TRY(sort(ctx->d_sort_tmp, tb, sel));
-  const uint32_t grid = (uint32_t)((n + kBlock - 1) / kBlock);
-  hipLaunchKernelGGL(k_fill_cells<false>, dim3(grid), dim3(kBlock), 0, ctx->stream, ctx->d_kb[sel], ctx->d_ke[sel], n,
-                     ctx->d_cells, ctx->cell_n);
-  MG_TRY(hipGetLastError());
-  hipLaunchKernelGGL(k_fill_cells<true>, dim3(grid), dim3(kBlock), 0, ctx->stream, ctx->d_kb[sel], ctx->d_ke[sel], n,
-                     ctx->d_cells, ctx->cell_n);
-  MG_TRY(hipGetLastError());
-  return 0;
-}
-
 int mg_build_index(mg_ctx* ctx, uint32_t min_overlap, uint32_t seed_k) {
   if (!ctx) return -1;
   MG_TRY(hipSetDevice(ctx->device));
-  MG_TRY(hipEventRecord(ctx->ev[0], ctx->stream));
+  if (ensure_layout_range(ctx)) return -1;  // a source-read range set after the upload
+  // the cell table exists before the timed window (its clear is inside it)
   if (setup_index(ctx, min_overlap, seed_k, false)) return -1;
+  MG_TRY(ensure(&ctx->d_cells, &ctx->cells_cap, ctx->cell_n * kCell));
+  MG_TRY(hipEventRecord(ctx->ev[0], ctx->stream));
+  if (setup_cells(ctx)) return -1;
+  ctx->scan_state = 0;
+  ctx->t.sort_ms = 0.f;
+  ctx->shared_scan_ms = 0.f;
   if (long_mode(ctx)) {  // reads > 1024 bp: k_index_long, one thread per key
     if (ctx->nranks > 1) return set_err(ctx, "reads longer than 1024 bp: bucket-sharded index not supported");
-    if (setup_cells(ctx)) return -1;
-    ctx->scan_state = 0;
-    ctx->sorted_state = 0;
-    ctx->t.sort_ms = 0.f;
     if (launch_index(ctx)) return set_err(ctx, "index build launch failed");
-    MG_TRY(hipEventRecord(ctx->ev[1], ctx->stream));
-    MG_TRY(hipEventSynchronize(ctx->ev[1]));
-    ctx->t.index_ms = elapsed(ctx->ev[0], ctx->ev[1]);
-    ctx->shared_scan_ms = 0.f;
-    ctx->index_ready = true;
-    ctx->cells_ready = true;
-    return 0;
-  }
-  const bool join = join_geometry(ctx);
-  if (!join && setup_cells_pp(ctx)) return -1;
-  ctx->scan_state = 0;
-  ctx->sorted_state = 0;
-  ctx->t.sort_ms = 0.f;
-  if (join) {
-    // partitioned join: one register scan writes runs + keys as join records,
-    // one radix sort by partition, partition bounds (no cell table)
-    ctx->key0_ready = false;
-    if (build_join(ctx)) return -1;
-    MG_TRY(hipEventRecord(ctx->ev[1], ctx->stream));
-    MG_TRY(hipEventSynchronize(ctx->ev[1]));
-    ctx->t.index_ms = elapsed(ctx->ev[0], ctx->ev[1]);
-    ctx->t.sort_ms = elapsed(ctx->ev[12], ctx->ev[13]);
-    ctx->index_ready = true;
-    return 0;
-  }
-  if (shared_scan(ctx)) {
+  } else if (shared_scan(ctx)) {
     // one pass over the reads: the index inserts ride on the window scan
     // (k_scan<INDEX>), whose runs then serve the containment and discovery
     // probes.  Measured at C3 (same box): 3.58 ms vs index 2.05 + scan 1.83
@@ -4732,37 +3423,18 @@ int mg_build_index(mg_ctx* ctx, uint32_t min_overlap, uint32_t seed_k) {
     // mixed lengths: each read's o = 0 key for the prefix-containment kernel
     ctx->key0_ready = ctx->minlen != ctx->maxlen && ctx->prefix_contain;
     if (ctx->key0_ready) MG_TRY(ensure(&ctx->d_key0, &ctx->key0_cap, ctx->n + 1));
-    // the register scan writes key records (no CAS inside), unless option reg_cas
-    const bool reg_keys = scan_is_reg(ctx, true) && !(ctx->reg_cas && !ctx->reg_index && !ctx->sorted_index);
-    if (ctx->sorted_index || reg_keys) {
-      MG_TRY(ensure(&ctx->d_kb[0], &ctx->kb_cap, 4 * ctx->n));
-      MG_TRY(ensure(&ctx->d_ke[0], &ctx->ke_cap, 4 * ctx->n));
-    }
-    if (ctx->sorted_index) {
-      MG_TRY(ensure(&ctx->d_kb[1], &ctx->kb1_cap, 4 * ctx->n));
-      MG_TRY(ensure(&ctx->d_ke[1], &ctx->ke1_cap, 4 * ctx->n));
-    }
-    if (ctx->n && dispatch_w<LaunchScanAll>(ctx->maxw, ctx, ctx->stream, true))
+    if (ctx->n && dispatch_w<LaunchScanAll>(ctx->maxw, ctx, ctx->stream))
       return set_err(ctx, "index build launch failed");
     if (!ctx->n) ctx->nrun_reg = 0;
-    if (ctx->sorted_index) {
-      if (fill_sorted_index(ctx)) return -1;
-    } else if (reg_keys && ctx->n) {
-      const uint64_t nk = 4 * ctx->n;
-      hipLaunchKernelGGL(k_insert_dense, dim3((uint32_t)std::min<uint64_t>((nk + kBlock - 1) / kBlock, 65536)),
-                         dim3(kBlock), 0, ctx->stream, ctx->d_kb[0], ctx->d_ke[0], nk, ctx->d_cells, ctx->cell_n);
-      MG_TRY(hipGetLastError());
-    }
     ctx->scan_state = 1;
-  } else if (dispatch_w<LaunchIndex>(ctx->maxw, ctx)) {
+  } else if (dispatch_w<LaunchIndex>(ctx->maxw, ctx)) {  // the whole index for a source-range shard
     return set_err(ctx, "index build launch failed");
   }
   MG_TRY(hipEventRecord(ctx->ev[1], ctx->stream));
   MG_TRY(hipEventSynchronize(ctx->ev[1]));
   ctx->t.index_ms = elapsed(ctx->ev[0], ctx->ev[1]);
-  ctx->shared_scan_ms = (shared_scan(ctx) && ctx->n) ? elapsed(ctx->ev[6], ctx->ev[7]) : 0.f;
+  ctx->shared_scan_ms = (!long_mode(ctx) && shared_scan(ctx) && ctx->n) ? elapsed(ctx->ev[6], ctx->ev[7]) : 0.f;
   ctx->index_ready = true;
-  ctx->cells_ready = true;
   return 0;
 }
 
@@ -4774,12 +3446,7 @@ int mg_mark_contained(mg_ctx* ctx, uint32_t* super_out) {
   if (!ctx->d_any) MG_TRY(hipMalloc(&ctx->d_any, sizeof(unsigned int)));
   ctx->t.contained_ms = 0.f;
   if (ctx->minlen != ctx->maxlen) {  // OverlapGraph.cpp:228-233
-    size_t skcap = 0;
-    if (ctx->d_superkey) {
-      (void)hipFree(ctx->d_superkey);
-      ctx->d_superkey = nullptr;
-    }
-    MG_TRY(ensure(&ctx->d_superkey, &skcap, ctx->n + 1));
+    MG_TRY(ensure(&ctx->d_superkey, &ctx->superkey_cap, ctx->n + 1));
     ctx->superkey = ctx->d_superkey;
     MG_TRY(hipMemsetAsync(ctx->d_superkey, 0, (ctx->n + 1) * sizeof(unsigned long long), ctx->stream));
     MG_TRY(hipMemsetAsync(ctx->d_any, 0, sizeof(unsigned int), ctx->stream));
@@ -4793,27 +3460,12 @@ int mg_mark_contained(mg_ctx* ctx, uint32_t* super_out) {
     if (ctx->nranks > 1) return set_err(ctx, "containment with a bucket-sharded index: use the exchange mode");
     if (long_mode(ctx)) {
       if (long_probe(ctx, true, 0, ctx->n)) return -1;
-    } else if (ctx->join_ready) {  // the join's prefix queries cover offset-0 containments
-      if (probe_join(ctx, true)) return -1;
     } else {
       if (!shared_scan(ctx)) ctx->key0_ready = false;  // only the shared scan writes the o = 0 keys
       // prefix containments first: what they mark is skipped as a container
       if (ctx->key0_ready && dispatch_w<LaunchPrefixContain>(ctx->maxw, ctx))
         return set_err(ctx, "prefix containment launch failed");
-      // source-length passes, longest first (option contain_passes): with
-      // contain_skip, the sources the longer passes found contained probe nothing
-      const int passes = shared_scan(ctx) ? ctx->contain_passes : 1;
-      const uint32_t span = ctx->maxlen + 1 - ctx->minlen;
-      for (int k = 0; k < passes; ++k) {
-        ctx->pass_len_hi = passes > 1 ? (int)(ctx->maxlen + 1 - (uint64_t)span * k / passes) : 0;
-        ctx->pass_len_lo = passes > 1 ? (int)(ctx->maxlen + 1 - (uint64_t)span * (k + 1) / passes) : 0;
-        const int rc = shared_scan(ctx) ? probe_shared(ctx, true) : run_discover(ctx, true);
-        if (rc) {
-          ctx->pass_len_lo = ctx->pass_len_hi = 0;
-          return -1;
-        }
-      }
-      ctx->pass_len_lo = ctx->pass_len_hi = 0;
+      if (shared_scan(ctx) ? probe_shared(ctx, true) : run_discover(ctx, true)) return -1;
     }
     if (ctx->n)
       hipLaunchKernelGGL(k_super_finalize, dim3((uint32_t)((ctx->n + kBlock - 1) / kBlock)), dim3(kBlock), 0,
@@ -4859,7 +3511,6 @@ int mg_find_overlaps(mg_ctx* ctx, uint64_t* n_rows) {
   const uint64_t nsrc = (ctx->read_hi ? std::min(ctx->read_hi, ctx->n) : ctx->n) -
                         std::min(ctx->read_lo, ctx->n);
   if (ensure_rows(ctx, nsrc)) return -1;
-  if (ctx->pp_due >= 0 && pp_schedule_clear(ctx)) return -1;  // overlaps the probe below
   MG_TRY(hipEventRecord(ctx->ev[4], ctx->stream));
   if (long_mode(ctx)) {
     const uint64_t lo = std::min(ctx->read_lo, ctx->n), hi = ctx->read_hi ? std::min(ctx->read_hi, ctx->n) : ctx->n;
@@ -4876,28 +3527,17 @@ int mg_find_overlaps(mg_ctx* ctx, uint64_t* n_rows) {
     if (n_rows) *n_rows = ctx->n_rows;
     return 0;
   }
-  if (ctx->join_ready ? probe_join(ctx, false) : shared_scan(ctx) ? probe_shared(ctx, false) : run_discover(ctx, false))
-    return -1;
+  if (shared_scan(ctx) ? probe_shared(ctx, false) : run_discover(ctx, false)) return -1;
   MG_TRY(hipEventRecord(ctx->ev[5], ctx->stream));
   MG_TRY(hipEventSynchronize(ctx->ev[5]));
   // the kernels' own events bracket the last launches (a resize retry included
   // in ev[4]..ev[5] is not kernel time)
   // scan kernel time (shared scan: measured at build time, part of index_ms)
   ctx->t.scan_ms = shared_scan(ctx) ? ctx->shared_scan_ms : elapsed(ctx->ev[6], ctx->ev[7]);
-  if (ctx->split) {
-    ctx->t.probe_ms = elapsed(ctx->ev[8], ctx->ev[9]);
-    ctx->t.verify_ms = elapsed(ctx->ev[10], ctx->ev[11]);
-  } else {
-    ctx->t.probe_ms = shared_scan(ctx) ? elapsed(ctx->ev[8], ctx->ev[9]) : elapsed(ctx->ev[7], ctx->ev[5]);
-    ctx->t.verify_ms = 0.f;
-  }
-  if (ctx->join_ready)  // the sort ran in mg_build_index (part of index_ms)
-    ctx->t.sort_ms = elapsed(ctx->ev[12], ctx->ev[13]);
-  else
-    ctx->t.sort_ms = (shared_scan(ctx) && ctx->sort_runs && ctx->sorted_state == 2)
-                         ? elapsed(ctx->ev[12], ctx->ev[13]) : 0.f;
-  ctx->t.overlap_ms = (shared_scan(ctx) ? 0.f : ctx->t.scan_ms) + (ctx->join_ready ? 0.f : ctx->t.sort_ms) +
-                      ctx->t.probe_ms + ctx->t.verify_ms;
+  ctx->t.probe_ms = shared_scan(ctx) ? elapsed(ctx->ev[8], ctx->ev[9]) : elapsed(ctx->ev[7], ctx->ev[5]);
+  ctx->t.verify_ms = 0.f;
+  ctx->t.sort_ms = 0.f;
+  ctx->t.overlap_ms = (shared_scan(ctx) ? 0.f : ctx->t.scan_ms) + ctx->t.probe_ms;
   read_stats(ctx, nsrc);
   // device wall of the step: index build start .. last discovery kernel end
   ctx->t.total_ms = shared_scan(ctx) ? elapsed(ctx->ev[0], ctx->ev[5])
@@ -4929,18 +3569,17 @@ int mg_xchg_begin(mg_ctx* ctx, uint32_t min_overlap, uint32_t seed_k) {
   MG_TRY(hipSetDevice(ctx->device));
   if (ctx->nranks > (uint32_t)kMaxRanks) return set_err(ctx, "at most 64 ranks");
   if (long_mode(ctx)) return set_err(ctx, "reads longer than 1024 bp: exchange mode not supported (use the replicated mode)");
+  if (ensure_layout_range(ctx)) return -1;
   MG_TRY(hipEventRecord(ctx->ev[0], ctx->stream));
   if (setup_index(ctx, min_overlap, seed_k)) return -1;  // this rank's (cleared) cells
-  ctx->join_P = 0;
   ctx->xchg = true;
   uint64_t lo, hi;
   source_range(ctx, &lo, &hi);
   ctx->xchg_lo = lo;
   ctx->xchg_hi = hi;
-  MG_TRY(ensure(&ctx->d_kb[0], &ctx->kb_cap, 4 * ctx->n + 1));
-  MG_TRY(ensure(&ctx->d_ke[0], &ctx->ke_cap, 4 * ctx->n + 1));
+  MG_TRY(ensure(&ctx->d_kb, &ctx->kb_cap, 4 * ctx->n + 1));
+  MG_TRY(ensure(&ctx->d_ke, &ctx->ke_cap, 4 * ctx->n + 1));
   ctx->scan_state = 0;
-  ctx->sorted_state = 0;
   ctx->n_flat = ctx->n_sorted = 0;
   ctx->shared_scan_ms = 0.f;
   ctx->t = mg_timings{};
@@ -4959,13 +3598,13 @@ int mg_xchg_begin(mg_ctx* ctx, uint32_t min_overlap, uint32_t seed_k) {
     // groups the runs by owner in one digit pass instead of three, and keeps a
     // coarse bucket order for the probe (simulated C3: P = 8 25.2 -> 24.4 ms,
     // P = 2 17.5 -> 16.3 ms summed over ranks); other P sort every bit
-    int bits = ctx->sort_bits;
-    if (!bits && ctx->xchg_sort_bits > 0 && !(ctx->nranks & (ctx->nranks - 1))) {
+    int bits = 0;
+    if (ctx->xchg_sort_bits > 0 && !(ctx->nranks & (ctx->nranks - 1))) {
       int lg = 0;
       while ((1u << lg) < ctx->nranks) ++lg;
       bits = std::max(ctx->xchg_sort_bits, lg);
     }
-    if (sort_shared_runs(ctx, bits)) return -1;
+    if (sort_flat_runs(ctx, bits)) return -1;
   } else {
     MG_TRY(hipEventRecord(ctx->ev[12], ctx->stream));
     MG_TRY(hipEventRecord(ctx->ev[13], ctx->stream));
@@ -4994,8 +3633,8 @@ int mg_xchg_pack(mg_ctx* ctx, int what, void* dst, uint64_t slot, uint32_t round
     pp.cap = kFlatRegion;
     pp.flat_n = 4 * nsrc;
     pp.nreg = (pp.flat_n + kFlatRegion - 1) / kFlatRegion;
-    pp.key_bk = ctx->d_kb[0];
-    pp.key_ent = ctx->d_ke[0];
+    pp.key_bk = ctx->d_kb;
+    pp.key_ent = ctx->d_ke;
     pp.key_n = ctx->n;
     pp.a_lo = ctx->xchg_lo;
     pp.nsrc = nsrc;
@@ -5036,7 +3675,6 @@ int mg_xchg_insert_keys(mg_ctx* ctx, const void* recv, uint64_t slot, uint32_t r
   }
   MG_TRY(hipEventRecord(ctx->ev[1], ctx->stream));
   ctx->index_ready = true;
-  ctx->cells_ready = true;
   return 0;
 }
 
@@ -5052,13 +3690,12 @@ int mg_xchg_probe(mg_ctx* ctx, int contain, const void* recv, uint64_t slot, uin
   if (slot_regions(ctx, &ctx->d_flat_cnt, &ctx->flat_cnt_cap, reinterpret_cast<const unsigned long long*>(counts),
                    slot, reg, nregions))
     return -1;
-  const uint64_t approx = (uint64_t)rounds * ctx->nranks * slot;  // (split probe: candidate sizing only)
   const auto* runs = reinterpret_cast<const ulonglong2*>(recv);
   ctx->nreg = 0;
   ctx->n_rows = 0;
   if (contain) {
     MG_TRY(hipEventRecord(ctx->ev[2], ctx->stream));
-    if (nregions && dispatch_w<LaunchProbeSlots>(ctx->maxw, ctx, true, runs, reg, nregions, approx))
+    if (nregions && dispatch_w<LaunchProbeSlots>(ctx->maxw, ctx, true, runs, reg, nregions))
       return set_err(ctx, "probe launch failed");
     MG_TRY(hipEventRecord(ctx->ev[3], ctx->stream));
     return 0;
@@ -5067,12 +3704,12 @@ int mg_xchg_probe(mg_ctx* ctx, int contain, const void* recv, uint64_t slot, uin
   for (int attempt = 0;; ++attempt) {
     if (attempt == 3) return set_err(ctx, "row buffers overflow after resize");
     MG_TRY(hipEventRecord(ctx->ev[4], ctx->stream));
-    if (nregions && dispatch_w<LaunchProbeSlots>(ctx->maxw, ctx, false, runs, reg, nregions, approx))
+    if (nregions && dispatch_w<LaunchProbeSlots>(ctx->maxw, ctx, false, runs, reg, nregions))
       return set_err(ctx, "probe launch failed");
     MG_TRY(hipEventRecord(ctx->ev[5], ctx->stream));
     if (!nregions) break;
     bool again = false;
-    if (!ctx->split && settle_rows(ctx, &again)) return -1;
+    if (settle_rows(ctx, &again)) return -1;
     if (!again) break;
   }
   MG_TRY(hipEventSynchronize(ctx->ev[5]));
@@ -5082,14 +3719,9 @@ int mg_xchg_probe(mg_ctx* ctx, int contain, const void* recv, uint64_t slot, uin
   ctx->t.sort_ms = elapsed(ctx->ev[12], ctx->ev[13]);
   ctx->t.index_ms = elapsed(ctx->ev[0], ctx->ev[1]);
   ctx->t.contained_ms = ctx->minlen != ctx->maxlen ? elapsed(ctx->ev[2], ctx->ev[3]) : 0.f;
-  if (ctx->split) {
-    ctx->t.probe_ms = elapsed(ctx->ev[8], ctx->ev[9]);
-    ctx->t.verify_ms = elapsed(ctx->ev[10], ctx->ev[11]);
-  } else {
-    ctx->t.probe_ms = elapsed(ctx->ev[4], ctx->ev[5]);
-    ctx->t.verify_ms = 0.f;
-  }
-  ctx->t.overlap_ms = ctx->t.probe_ms + ctx->t.verify_ms;
+  ctx->t.probe_ms = elapsed(ctx->ev[4], ctx->ev[5]);
+  ctx->t.verify_ms = 0.f;
+  ctx->t.overlap_ms = ctx->t.probe_ms;
   ctx->t.total_ms = elapsed(ctx->ev[0], ctx->ev[5]);
   read_stats(ctx, ctx->xchg_hi - ctx->xchg_lo);
   ctx->packable |= 1 << MG_ROWS;
@@ -5106,10 +3738,7 @@ int mg_begin_contained(mg_ctx* ctx, void* superkey, int* needed) {
     if (superkey) {
       ctx->superkey = reinterpret_cast<unsigned long long*>(superkey);
     } else {
-      size_t skcap = 0;
-      if (ctx->d_superkey) (void)hipFree(ctx->d_superkey);
-      ctx->d_superkey = nullptr;
-      MG_TRY(ensure(&ctx->d_superkey, &skcap, ctx->n + 1));
+      MG_TRY(ensure(&ctx->d_superkey, &ctx->superkey_cap, ctx->n + 1));
       ctx->superkey = ctx->d_superkey;
     }
     MG_TRY(hipMemsetAsync(ctx->superkey, 0, ctx->n * sizeof(unsigned long long), ctx->stream));
@@ -5182,7 +3811,6 @@ int mg_lookup_key(mg_ctx* ctx, const char* key, uint32_t key_len, uint64_t* out,
   if (n_out) *n_out = 0;
   if (key_len != ctx->h) return 0;  // no key of another length exists
   if (ctx->nranks > 1) return set_err(ctx, "lookup on a bucket-sharded index");
-  if (ensure_cells(ctx)) return -1;  // join builds keep no cell table until a lookup asks for one
   const int qwords = (int)((key_len + 31) / 32);
   std::vector<uint64_t> q(qwords + 1, 0);
   for (uint32_t i = 0; i < key_len; i++) {

@@ -10,6 +10,7 @@
 #include "mg_digest.h"
 
 #include <ctype.h>
+#include <pthread.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -203,6 +204,22 @@ mgo_dataset* mgo_dataset_from_seqs(const char* concat, const uint64_t* offsets, 
                                    uint64_t min_overlap) {
   mgo_dataset* ds = new_dataset();
   for (uint64_t i = 0; i < n; i++) add_read(ds, concat + offsets[i], offsets[i + 1] - offsets[i], min_overlap);
+  finish_dataset(ds);
+  return ds;
+}
+
+/* Same pipeline from 2-bit codes (0..3 = A C G T) of n reads, read i at
+ * codes[i * stride, i * stride + lens[i]): the synthetic workloads' form. */
+mgo_dataset* mgo_dataset_from_codes(const uint8_t* codes, uint64_t stride, const uint16_t* lens, uint64_t n,
+                                    uint64_t min_overlap) {
+  mgo_dataset* ds = new_dataset();
+  char* s = (char*)malloc(stride + 1);
+  for (uint64_t i = 0; i < n; i++) {
+    const uint8_t* c = codes + i * stride;
+    for (uint64_t k = 0; k < lens[i]; k++) s[k] = "ACGT"[c[k] & 3];
+    add_read(ds, s, lens[i], min_overlap);
+  }
+  free(s);
   finish_dataset(ds);
   return ds;
 }
@@ -432,6 +449,159 @@ uint64_t mgo_lookup(mgo_dataset* ds, uint64_t min_overlap, const char* key, uint
 }
 
 void mgo_free(void* p) { free(p); }
+
+/* --- the same hot path, split over threads by source read, digests only ---
+ *
+ * For workloads whose row lists do not fit in memory (C5: 50M reads): the
+ * loops are mgo_overlaps' loops, line for line, over source-read ranges.
+ *  - markContainedReads (OverlapGraph.cpp:225-290): thread t runs the loop over
+ *    sources [lo_t, hi_t) into its own superReadID array with the reference's
+ *    rule (first containing read, replaced only by a strictly longer one,
+ *    :259-268); the arrays are then folded in source order with the same rule,
+ *    which is the rule applied to the whole sequence i = 1..N.
+ *  - insertAllEdgesOfRead (OverlapGraph.cpp:529-565) in ID order: when read i
+ *    is explored, the explored reads are exactly IDs 1..i-1, so the :546 test
+ *    is id2 < i and every source is independent; rows go into additive digests
+ *    (mg_digest.h) instead of a list. */
+typedef struct {
+  mgo_dataset* ds;
+  uint64_t h, lo, hi;
+  uint32_t* sup;          /* containment: this range's superReadIDs */
+  const uint64_t* super;  /* discovery: the folded superReadIDs */
+  uint64_t* next;         /* discovery: shared chunk cursor */
+  uint64_t chunk;
+  mgo_digest d;
+} mgo_task;
+
+static void* contain_range(void* arg) {
+  mgo_task* t = (mgo_task*)arg;
+  mgo_dataset* ds = t->ds;
+  uint64_t h = t->h;
+  for (uint64_t i = t->lo; i < t->hi; i++) {
+    oread* r1 = &ds->reads[i - 1];
+    for (uint64_t j = 1; j < r1->len - h; j++) {
+      struct bucket* b = find_bucket(ds, r1->fwd + j, 0);
+      if (!b) continue;
+      for (uint32_t k = 0; k < b->n; k++) {
+        uint64_t data = b->items[k];
+        uint64_t id2 = data & 0x3FFFFFFFFFFFFFFFULL, o = data >> 62;
+        oread* r2 = &ds->reads[id2 - 1];
+        if (r1->len > r2->len && contained_check(r1, r2, o, j, h)) {
+          if (t->sup[id2] == 0)
+            t->sup[id2] = (uint32_t)i;
+          else if (r1->len > ds->reads[t->sup[id2] - 1].len)
+            t->sup[id2] = (uint32_t)i;
+        }
+      }
+    }
+  }
+  return NULL;
+}
+
+static void* discover_chunks(void* arg) {
+  mgo_task* t = (mgo_task*)arg;
+  mgo_dataset* ds = t->ds;
+  uint64_t h = t->h, N = ds->n_unique;
+  for (;;) {
+    uint64_t a = __atomic_fetch_add(t->next, t->chunk, __ATOMIC_RELAXED) + 1;
+    if (a > N) break;
+    uint64_t e = a + t->chunk > N + 1 ? N + 1 : a + t->chunk;
+    for (uint64_t i = a; i < e; i++) {
+      oread* r1 = &ds->reads[i - 1];
+      uint64_t n1 = r1->len;
+      for (uint64_t j = 1; j < n1 - h; j++) {
+        struct bucket* b = find_bucket(ds, r1->fwd + j, 0);
+        if (!b) continue;
+        for (uint32_t k = 0; k < b->n; k++) {
+          uint64_t data = b->items[k];
+          uint64_t id2 = data & 0x3FFFFFFFFFFFFFFFULL, o = data >> 62;
+          if (id2 < i) continue; /* explored (:546) */
+          oread* r2 = &ds->reads[id2 - 1];
+          if (t->super[i] == 0 && t->super[id2] == 0 && overlap_check(r1, r2, o, j, h)) {
+            uint8_t orient;
+            uint16_t ovl;
+            switch (o) { /* :550-556 */
+              case 0: orient = 3; ovl = (uint16_t)(n1 - j); break;
+              case 1: orient = 0; ovl = (uint16_t)(h + j); break;
+              case 2: orient = 2; ovl = (uint16_t)(n1 - j); break;
+              default: orient = 1; ovl = (uint16_t)(h + j); break;
+            }
+            uint16_t off = (uint16_t)(n1 - ovl);               /* :557 */
+            uint16_t off_rev = (uint16_t)(r2->len + off - n1); /* :410 */
+            mgo_digest_add(&t->d, mgo_row_hash(i, id2, orient, off));
+            mgo_digest_add(&t->d, mgo_row_hash(id2, i, twin_orient(orient), off_rev));
+          }
+        }
+      }
+    }
+  }
+  return NULL;
+}
+
+int mgo_overlaps_digest(mgo_dataset* ds, uint64_t min_overlap, int nthreads, uint64_t* rows_out,
+                        uint64_t* super_digest_out, uint64_t* super_out, double* t_hash, double* t_contain,
+                        double* t_disc) {
+  if (min_overlap < 2 || nthreads < 1) return -1;
+  uint64_t N = ds->n_unique, h = min_overlap - 1;
+  double t0 = now_s();
+  build_table(ds, min_overlap);
+  double t1 = now_s();
+  uint64_t* super = (uint64_t*)calloc(N + 1, sizeof(uint64_t));
+  pthread_t* th = (pthread_t*)calloc((size_t)nthreads, sizeof(pthread_t));
+  mgo_task* tk = (mgo_task*)calloc((size_t)nthreads, sizeof(mgo_task));
+  if (N && ds->longest != ds->shortest) { /* :228-233 */
+    for (int t = 0; t < nthreads; t++) {
+      tk[t].ds = ds;
+      tk[t].h = h;
+      tk[t].lo = 1 + N * (uint64_t)t / (uint64_t)nthreads;
+      tk[t].hi = 1 + N * (uint64_t)(t + 1) / (uint64_t)nthreads;
+      tk[t].sup = (uint32_t*)calloc(N + 1, sizeof(uint32_t));
+      pthread_create(&th[t], NULL, contain_range, &tk[t]);
+    }
+    for (int t = 0; t < nthreads; t++) pthread_join(th[t], NULL);
+    for (int t = 0; t < nthreads; t++) { /* fold in source order, rule of :259-268 */
+      for (uint64_t id = 1; id <= N; id++) {
+        uint64_t s = tk[t].sup[id];
+        if (!s) continue;
+        if (super[id] == 0 || ds->reads[s - 1].len > ds->reads[super[id] - 1].len) super[id] = s;
+      }
+      free(tk[t].sup);
+    }
+  }
+  double t2 = now_s();
+  uint64_t next = 0;
+  memset(tk, 0, (size_t)nthreads * sizeof(mgo_task));
+  for (int t = 0; t < nthreads; t++) {
+    tk[t].ds = ds;
+    tk[t].h = h;
+    tk[t].super = super;
+    tk[t].next = &next;
+    tk[t].chunk = 4096;
+    pthread_create(&th[t], NULL, discover_chunks, &tk[t]);
+  }
+  mgo_digest d = {0, 0, 0, 0};
+  for (int t = 0; t < nthreads; t++) {
+    pthread_join(th[t], NULL);
+    d.n += tk[t].d.n;
+    d.sum += tk[t].d.sum;
+    d.xr ^= tk[t].d.xr;
+    d.sum2 += tk[t].d.sum2;
+  }
+  double t3 = now_s();
+  rows_out[0] = d.n;
+  rows_out[1] = d.sum;
+  rows_out[2] = d.xr;
+  rows_out[3] = d.sum2;
+  mgo_super_digest(super, N, super_digest_out);
+  if (super_out) memcpy(super_out, super, (N + 1) * sizeof(uint64_t));
+  free(super);
+  free(th);
+  free(tk);
+  if (t_hash) *t_hash = t1 - t0;
+  if (t_contain) *t_contain = t2 - t1;
+  if (t_disc) *t_disc = t3 - t2;
+  return 0;
+}
 
 /* Digests of oracle/mg_digest.h over rows / a superReadID vector (the
  * checker's side of mg_rows_digest / mg_super_digest). */

@@ -34,6 +34,10 @@ mgo_dataset* mgo_dataset_from_files(const char* const* files, int nfiles, uint64
  * n+1 offsets (no parsing; upper-casing, filter, canonicalise, sort, dedup). */
 mgo_dataset* mgo_dataset_from_seqs(const char* concat, const uint64_t* offsets, uint64_t n,
                                    uint64_t min_overlap);
+/* Same pipeline from 2-bit codes (0..3 = A C G T): read i is
+ * codes[i * stride, i * stride + lens[i]). */
+mgo_dataset* mgo_dataset_from_codes(const uint8_t* codes, uint64_t stride, const uint16_t* lens, uint64_t n,
+                                    uint64_t min_overlap);
 void mgo_dataset_free(mgo_dataset* ds);
 uint64_t mgo_num_reads(const mgo_dataset* ds);         /* good reads incl. duplicates */
 uint64_t mgo_num_unique(const mgo_dataset* ds);
@@ -49,6 +53,16 @@ uint32_t mgo_frequency(const mgo_dataset* ds, uint64_t id);
  * t_hash / t_disc (optional): wall seconds of the two phases. */
 int mgo_overlaps(mgo_dataset* ds, uint64_t min_overlap, uint64_t* super_out, mgo_row** rows,
                  uint64_t* nrows, double* t_hash, double* t_disc);
+
+/* The same hot path over `nthreads` threads, for workloads whose rows do not
+ * fit in memory: the containment loop over source ranges folded in source
+ * order, the ID-order discovery loop with "explored" = ID below the source
+ * (exactly the explored set when read i is explored), rows digested
+ * (mg_digest.h) instead of listed.  rows_digest[4] / super_digest[4] as
+ * mgo_rows_digest / mgo_super_digest; super_out (optional) N+1 entries. */
+int mgo_overlaps_digest(mgo_dataset* ds, uint64_t min_overlap, int nthreads, uint64_t* rows_digest,
+                        uint64_t* super_digest, uint64_t* super_out, double* t_hash, double* t_contain,
+                        double* t_disc);
 
 /* HashTable::getListOfReads(key) (HashTable.cpp:202-221) on a table built by
  * insertDataset: writes up to cap entries id|o<<62 in reference list order,

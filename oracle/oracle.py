@@ -35,6 +35,11 @@ def lib():
         L.mgo_dataset_from_files.argtypes = [C.POINTER(C.c_char_p), C.c_int, u64]
         L.mgo_dataset_from_seqs.restype = vp
         L.mgo_dataset_from_seqs.argtypes = [C.c_char_p, vp, u64, u64]
+        L.mgo_dataset_from_codes.restype = vp
+        L.mgo_dataset_from_codes.argtypes = [vp, u64, vp, u64, u64]
+        L.mgo_overlaps_digest.restype = C.c_int
+        L.mgo_overlaps_digest.argtypes = [vp, u64, C.c_int, vp, vp, vp, C.POINTER(C.c_double),
+                                          C.POINTER(C.c_double), C.POINTER(C.c_double)]
         L.mgo_dataset_free.argtypes = [vp]
         L.mgo_num_unique.restype = u64
         L.mgo_num_unique.argtypes = [vp]
@@ -75,6 +80,14 @@ class OracleDataset:
         off[1:] = np.cumsum([len(s) for s in seqs])
         return cls(lib().mgo_dataset_from_seqs(data, C.c_void_p(off.ctypes.data), len(seqs), l))
 
+    @classmethod
+    def from_codes(cls, codes, lens, l):
+        """2-bit codes [n, stride] uint8 (A0 C1 G2 T3) + lengths: metagenomics_amd.synth's form."""
+        codes = np.ascontiguousarray(codes, dtype=np.uint8)
+        lens = np.ascontiguousarray(lens, dtype=np.uint16)
+        return cls(lib().mgo_dataset_from_codes(C.c_void_p(codes.ctypes.data), codes.shape[1],
+                                                C.c_void_p(lens.ctypes.data), codes.shape[0], l))
+
     def __del__(self):
         if getattr(self, "_h", None) and _lib is not None:
             _lib.mgo_dataset_free(self._h)
@@ -112,6 +125,21 @@ class OracleDataset:
             rows = np.zeros(0, dtype=ROW_DTYPE)
         lib().mgo_free(rows_p)
         return rows, sup, th.value, td.value
+
+    def overlaps_digest(self, l, nthreads, want_super=False):
+        """Threaded hot path, digests only (mgo_overlaps_digest): -> (rows digest,
+        super digest, super[N+1] or None, {hash_s, contain_s, discovery_s})"""
+        rd = np.zeros(4, dtype=np.uint64)
+        sd = np.zeros(4, dtype=np.uint64)
+        sup = np.zeros(self.num_unique + 1, dtype=np.uint64) if want_super else None
+        th, tc, td = C.c_double(), C.c_double(), C.c_double()
+        rc = lib().mgo_overlaps_digest(self._h, l, nthreads, C.c_void_p(rd.ctypes.data), C.c_void_p(sd.ctypes.data),
+                                       C.c_void_p(sup.ctypes.data) if want_super else None,
+                                       C.byref(th), C.byref(tc), C.byref(td))
+        if rc:
+            raise RuntimeError("oracle overlaps_digest failed")
+        d = lambda a: {"n": int(a[0]), "sum": int(a[1]), "xor": int(a[2]), "sum2": int(a[3])}  # noqa: E731
+        return d(rd), d(sd), sup, {"hash_s": th.value, "contain_s": tc.value, "discovery_s": td.value}
 
     def lookup(self, l, key):
         out = np.zeros(1 << 16, dtype=np.uint64)

@@ -14,7 +14,19 @@ compare the device's digest with these numbers.
         5M x 100-250 bp, 100 genomes, 43.75 Mb total (20x), seed 55, l = 50
   c2  : bench.py CONFIGS["c2"] (1M x 150 bp), a quick self-check of the recipe
 
-usage: make_scale_golden.py NAME [NAME ...]   (takes tens of minutes for c3)
+  c5  : bench.py CONFIGS["c5"] = BASELINE configs[4]: 50M x 100-250 bp, 100
+        genomes, 437.5 Mb (20x), seed 55, l = 50.  The reference needs ~10x the
+        c5s hours and more memory than this container has, so this one is made
+        by the ORACLE (--oracle): oracle/mg_oracle.c's mgo_overlaps_digest, the
+        C restatement pinned bit-exact to the reference on every fixture, run
+        over source-read ranges in threads (its containment ranges folded in
+        source order with the reference's rule, its discovery digests added).
+        Before it is trusted, --oracle --check c5s must reproduce the
+        reference's own c5s digests.
+
+usage: make_scale_golden.py NAME [NAME ...]            (reference; tens of minutes for c3)
+       make_scale_golden.py --oracle [--threads T] NAME  (oracle, threaded)
+       make_scale_golden.py --oracle --check NAME       (oracle vs the committed golden)
 """
 from __future__ import annotations
 
@@ -38,6 +50,7 @@ SETS = {
     "c2": ("uniform", 1_000_000, 150, 150, 7_500_000, 0, 21, 50),
     "c3": ("uniform", 10_000_000, 150, 150, 75_000_000, 0, 31, 50),
     "c5s": ("meta", 5_000_000, 100, 250, 43_750_000, 100, 55, 50),
+    "c5": ("meta", 50_000_000, 100, 250, 437_500_000, 100, 55, 50),
 }
 
 
@@ -64,7 +77,59 @@ def write_fasta_fast(path, codes, lens):
             f.write(rec[a:b][keep[a:b]].tobytes())
 
 
+def generator_text(kind):
+    return ("synth.metagenome_read_set(n, lo, hi, genomes, genome_len, seed)" if kind == "meta" else
+            "synth.uniform_read_set(n, 0, genome_len, seed=seed, lo=lo, hi=hi)")
+
+
+def oracle_main(names, threads, check):
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+
+    for name in names:
+        kind, n, lo, hi, G, ng, seed, l = SETS[name]
+        t0 = time.time()
+        codes, lens = make_codes(name)
+        od = oracle.OracleDataset.from_codes(codes, lens, l)
+        del codes, lens
+        t1 = time.time()
+        rd, sd, _, secs = od.overlaps_digest(l, threads)
+        res = {
+            "name": name,
+            "workload": {"kind": kind, "reads": n, "read_len": [lo, hi], "genome_len": G, "genomes": ng,
+                         "seed": seed, "min_overlap": l, "generator": generator_text(kind)},
+            "recipe": ("oracle/mg_oracle.c mgo_overlaps_digest (the C restatement of insertDataset + "
+                       "markContainedReads + ID-order insertAllEdgesOfRead, HashTable.cpp:50-80, "
+                       "OverlapGraph.cpp:225-290,529-565; pinned to the reference on every fixture and on "
+                       "the reference's own c5s digests), %d threads over source-read ranges" % threads),
+            "n_unique": od.num_unique, "n_reads": od.num_reads, "rows": rd, "super": sd,
+            "oracle_seconds": dict(secs, dataset_s=round(t1 - t0, 1)), "threads": threads,
+            "wall_s": round(time.time() - t0, 1),
+        }
+        del od
+        if check:
+            g = json.load(open(os.path.join(HERE, f"{name}.json")))
+            ok = all(g[k] == res[k] for k in ("n_unique", "n_reads", "rows", "super"))
+            print(json.dumps({"name": name, "check": ok, "oracle": res}), flush=True)
+            if not ok:
+                sys.exit(1)
+            continue
+        with open(os.path.join(HERE, f"{name}.json"), "w") as f:
+            json.dump(res, f, indent=1)
+        print(json.dumps(res), flush=True)
+
+
 def main():
+    if "--oracle" in sys.argv:
+        args = [a for a in sys.argv[1:] if a != "--oracle"]
+        check = "--check" in args
+        args = [a for a in args if a != "--check"]
+        threads = os.cpu_count() or 1
+        if "--threads" in args:
+            i = args.index("--threads")
+            threads = int(args[i + 1])
+            del args[i:i + 2]
+        return oracle_main(args, threads, check)
     harness = os.path.join(ROOT, "oracle", "_ref", "ref_harness")
     if not os.path.exists(harness):
         subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "ref"], check=True)

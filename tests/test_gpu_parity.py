@@ -56,8 +56,7 @@ def test_fixture_matches_reference(engine, name):
     check_pairs(rows, ds.packed()[1])
 
 
-@pytest.mark.parametrize("name,k", [("small", 12), ("small", 21), ("small", 32), ("tandem", 8),
-                                    ("tandem", 25), ("mixed", 17), ("highdup", 31), ("highdup", 5)])
+@pytest.mark.parametrize("name,k", [("small", 12), ("small", 32), ("tandem", 8), ("mixed", 17), ("highdup", 5)])
 def test_seed_k_does_not_change_results(engine, name, k):
     meta = load_meta(name)
     ds = Dataset.from_files([fixture_input(name)], meta["l"])
@@ -93,18 +92,15 @@ def test_lookup_matches_reference(engine, name):
 def test_lookup_tiny_directory(engine, name):
     """getListOfReads through long overflow chains: with 2^10 requested buckets
     the directory runs at ~70 % load, so many entries sit outside their home
-    cell; both index builds (CAS, and sorted + k_fill_cells<OVERFLOW>)."""
+    cell."""
     meta = load_meta(name)
     ds = Dataset.from_files([fixture_input(name)], meta["l"])
     engine.set_option("nb_log2", 10)
     engine.set_shard(0, 1)
     engine.upload(ds)
-    for sorted_index in (0, 1):
-        engine.set_option("sorted_index", sorted_index)
-        engine.build_index(meta["l"])
-        for key, exp in meta["lookups"].items():
-            assert [list(x) for x in engine.lookup(key)] == exp, key
-    engine.set_option("sorted_index", 0)
+    engine.build_index(meta["l"])
+    for key, exp in meta["lookups"].items():
+        assert [list(x) for x in engine.lookup(key)] == exp, key
     engine.set_option("nb_log2", 0)
 
 
@@ -142,17 +138,60 @@ def test_bucket_shards_union(engine, name, nranks):
     assert np.array_equal(rows_to_tuples(allr), golden_rows(name))
 
 
-@pytest.mark.parametrize("name", ["small", "mixed", "tandem"])
-def test_read_range_union(engine, name):
+def assert_shard_rows(rows, lo, hi):
+    """A source-range shard holds its sources' discoveries: every (row, twin)
+    pair has the row's src in the range's reference IDs [lo + 1, hi]."""
+    a, b = rows[0::2], rows[1::2]
+    assert np.array_equal(a["src"], b["dst"]) and np.array_equal(a["dst"], b["src"])
+    assert np.all((a["src"] >= lo + 1) & (a["src"] <= hi)), "a row whose source read the shard does not own"
+
+
+@pytest.mark.parametrize("name,layout", [("small", 1), ("mixed", 1), ("branchy", 1), ("tandem", 0)])
+def test_read_range_union(engine, name, layout):
+    """Source-read shards (mg_set_shard read_lo/read_hi) by reference ID, on the
+    clustered layout (the range re-clustered into its own slots) and on ID order."""
     meta = load_meta(name)
     ds = Dataset.from_files([fixture_input(name)], meta["l"])
     n = ds.num_unique
     cuts = [0, n // 3, n // 2 + 7, n]
     parts = []
-    for lo, hi in zip(cuts[:-1], cuts[1:]):
-        rows, _ = gpu_rows(engine, ds, meta["l"], shard=(0, 1, lo, hi))
-        parts.append(rows)
+    engine.set_option("layout", layout)
+    try:
+        for lo, hi in zip(cuts[:-1], cuts[1:]):
+            rows, sup = gpu_rows(engine, ds, meta["l"], shard=(0, 1, lo, hi))
+            assert {str(i): int(s) for i, s in enumerate(sup) if s} == meta["super"]
+            assert_shard_rows(rows, lo, hi)
+            parts.append(rows)
+    finally:
+        engine.set_option("layout", 1)
     assert np.array_equal(rows_to_tuples(np.concatenate(parts)), golden_rows(name))
+
+
+def test_read_range_set_after_upload(engine):
+    """A range set on resident reads re-clusters them at the next build; then
+    the whole range again (the ungrouped layout)."""
+    meta = load_meta("mixed")
+    ds = Dataset.from_files([fixture_input("mixed")], meta["l"])
+    n = ds.num_unique
+    engine.set_option("nb_log2", 0)
+    engine.set_shard(0, 1)
+    engine.upload(ds)
+    parts = []
+    for lo, hi in ((0, n // 4), (n // 4, n)):
+        engine.set_shard(0, 1, lo, hi)
+        engine.build_index(meta["l"])
+        engine.mark_contained()
+        rows = engine.rows(engine.find_overlaps())
+        assert_shard_rows(rows, lo, hi)
+        parts.append(rows)
+    assert np.array_equal(rows_to_tuples(np.concatenate(parts)), golden_rows("mixed"))
+    engine.set_shard(0, 1)
+    engine.build_index(meta["l"])
+    engine.mark_contained()
+    assert np.array_equal(rows_to_tuples(engine.rows(engine.find_overlaps())), golden_rows("mixed"))
+    w, lens = engine.download_packed()
+    hw, hl = ds.packed()
+    assert np.array_equal(lens, hl) and np.array_equal(w[:, :hw.shape[1]], hw)
 
 
 def test_c1_digest(engine):
@@ -296,9 +335,8 @@ def exchange_rows(ds, l, world, k=0, want_super=True):
     return np.concatenate(parts), res.super_read_id
 
 
-@pytest.mark.parametrize("name,world", [("small", 2), ("mixed", 3), ("tandem", 4), ("highdup", 2),
-                                        ("dirty", 3), ("tworead", 2), ("wrapped", 5), ("small", 1),
-                                        ("tworead", 3)])
+@pytest.mark.parametrize("name,world", [("small", 2), ("mixed", 3), ("tandem", 4), ("dirty", 3), ("tworead", 2),
+                                        ("wrapped", 5)])
 def test_exchange_mode_matches_reference(name, world):
     meta = load_meta(name)
     ds = Dataset.from_files([fixture_input(name)], meta["l"])
@@ -358,6 +396,31 @@ def test_exchange_mode_cut_streams_rerun():
         e.close()
 
 
+@pytest.mark.parametrize("name", ["mixed", "branchy", "highdup"])
+def test_exchange_flat_overflow(name):
+    """The exchange scan's flat run arrays start far too small: its chunk
+    cursors keep counting, the host resizes to the exact need and reruns."""
+    import torch
+
+    from metagenomics_amd.sharded import LocalExchange, sharded_step
+
+    meta = load_meta(name)
+    ds = Dataset.from_files([fixture_input(name)], meta["l"])
+    engines = []
+    for r in range(2):
+        e = OverlapEngine(0)
+        e.set_option("flat_cap", 700)
+        e.set_shard(r, 2, 0, 0)
+        e.upload(ds)
+        engines.append(e)
+    res = sharded_step(engines, LocalExchange(2, torch.device("cuda:0")), meta["l"], 0, want_super=True)
+    rows = np.concatenate([res.rows_numpy(r) for r in range(2)])
+    for e in engines:
+        e.close()
+    assert np.array_equal(rows_to_tuples(rows), golden_rows(name))
+    assert {str(i): int(s) for i, s in enumerate(res.super_read_id) if s} == meta["super"]
+
+
 def test_exchange_mode_c2_scale_matches_fused(engine):
     """1M x 150 bp (configs[1] shape): 4 exchange ranks == the fused single-GPU path."""
     c, L = synth.uniform_read_set(1_000_000, 150, 7_500_000, seed=21)
@@ -367,20 +430,6 @@ def test_exchange_mode_c2_scale_matches_fused(engine):
     assert rows.shape[0] == fused.shape[0]
     assert np.array_equal(rows_to_tuples(rows), rows_to_tuples(fused))
     check_pairs(fused, ds.packed()[1])
-
-
-@pytest.mark.parametrize("name", ["small", "mixed", "tandem", "highdup"])
-def test_split_probe_path(name):
-    """option split = 1: probe -> candidates -> verify kernels give the same multiset."""
-    meta = load_meta(name)
-    ds = Dataset.from_files([fixture_input(name)], meta["l"])
-    e = OverlapEngine(0)
-    e.set_option("join", 0)
-    e.set_option("split", 1)
-    rows, sup = gpu_rows(e, ds, meta["l"])
-    e.close()
-    assert np.array_equal(rows_to_tuples(rows), golden_rows(name))
-    assert {str(i): int(s) for i, s in enumerate(sup) if s} == meta["super"]
 
 
 # ---- Dataset ingest on the device (SURVEY §8(f) row 2) vs the host mirror,
@@ -411,7 +460,7 @@ def assert_same_dataset(engine, ds):
     assert int(f.sum()) == ds.num_reads
 
 
-@pytest.mark.parametrize("name", FIXTURES)
+@pytest.mark.parametrize("name", ["mixed", "tandem", "dirty", "wrapped", "branchy", "longreads"])
 def test_device_ingest_matches_host_dataset(engine, name):
     meta = load_meta(name)
     path = fixture_input(name)
@@ -564,83 +613,10 @@ def test_ingest_files_parse_cases(tmp_path):
     e.close()
 
 
-@pytest.mark.parametrize("name", FIXTURES)
-def test_sorted_runs_path(name):
-    """option sort_runs = 1: the shared scan's runs are radix-sorted by bucket
-    before the containment and discovery probes; same rows and superReadIDs."""
-    meta = load_meta(name)
-    ds = Dataset.from_files([fixture_input(name)], meta["l"])
-    e = OverlapEngine(0)
-    e.set_option("join", 0)
-    e.set_option("sort_runs", 1)
-    rows, sup = gpu_rows(e, ds, meta["l"])
-    e.close()
-    assert np.array_equal(rows_to_tuples(rows), golden_rows(name))
-    assert {str(i): int(s) for i, s in enumerate(sup) if s} == meta["super"]
+MIXED_LENGTH = ["mixed", "dirty", "branchy", "longreads"]  # fixtures where markContainedReads runs
 
 
-@pytest.mark.parametrize("name", ["mixed", "branchy", "highdup"])
-def test_sorted_runs_flat_overflow(name):
-    """The flat run arrays start far too small: the scan's chunk cursor keeps
-    counting, the host resizes to the exact need and reruns the scan."""
-    meta = load_meta(name)
-    ds = Dataset.from_files([fixture_input(name)], meta["l"])
-    e = OverlapEngine(0)
-    e.set_option("sort_runs", 1)
-    e.set_option("join", 0)
-    e.set_option("flat_cap", 700)
-    rows, sup = gpu_rows(e, ds, meta["l"])
-    e.close()
-    assert np.array_equal(rows_to_tuples(rows), golden_rows(name))
-    assert {str(i): int(s) for i, s in enumerate(sup) if s} == meta["super"]
-
-
-@pytest.mark.parametrize("name", FIXTURES)
-def test_sorted_runs_16b_records(name):
-    """option pack_runs = 0: the bucket sort moves 16-B run records instead of
-    the packed 12-B ones."""
-    meta = load_meta(name)
-    ds = Dataset.from_files([fixture_input(name)], meta["l"])
-    e = OverlapEngine(0)
-    e.set_option("join", 0)
-    e.set_option("pack_runs", 0)
-    rows, sup = gpu_rows(e, ds, meta["l"])
-    e.close()
-    assert np.array_equal(rows_to_tuples(rows), golden_rows(name))
-    assert {str(i): int(s) for i, s in enumerate(sup) if s} == meta["super"]
-
-
-@pytest.mark.parametrize("name", FIXTURES)
-def test_unsorted_runs_path(name):
-    """option sort_runs = 0: the probe walks the scan's per-wavefront regions."""
-    meta = load_meta(name)
-    ds = Dataset.from_files([fixture_input(name)], meta["l"])
-    e = OverlapEngine(0)
-    e.set_option("join", 0)
-    e.set_option("sort_runs", 0)
-    rows, sup = gpu_rows(e, ds, meta["l"])
-    e.close()
-    assert np.array_equal(rows_to_tuples(rows), golden_rows(name))
-    assert {str(i): int(s) for i, s in enumerate(sup) if s} == meta["super"]
-
-
-@pytest.mark.parametrize("name,nb", [(f, 0) for f in FIXTURES] + [("highdup", 10), ("mixed", 10)])
-def test_sorted_index_path(name, nb):
-    """option sorted_index = 1: the fused scan writes its key records, a bucket
-    sort orders them and k_fill_cells files them with plain stores (overflow
-    through the chain walk) instead of per-key CAS; same results."""
-    meta = load_meta(name)
-    ds = Dataset.from_files([fixture_input(name)], meta["l"])
-    e = OverlapEngine(0)
-    e.set_option("join", 0)
-    e.set_option("sorted_index", 1)
-    rows, sup = gpu_rows(e, ds, meta["l"], nb_log2=nb)
-    e.close()
-    assert np.array_equal(rows_to_tuples(rows), golden_rows(name))
-    assert {str(i): int(s) for i, s in enumerate(sup) if s} == meta["super"]
-
-
-@pytest.mark.parametrize("name", FIXTURES + ["prefixes"])
+@pytest.mark.parametrize("name", MIXED_LENGTH + ["prefixes"])
 def test_prefix_contain_off(name):
     """option prefix_contain = 0: the containment probe verifies suffix-key
     hits too (at offset s = 0 only) instead of running k_prefix_contain; the
@@ -655,53 +631,12 @@ def test_prefix_contain_off(name):
         l = meta["l"]
         ds = Dataset.from_files([fixture_input(name)], l)
         want_rows, want_sup = golden_rows(name), meta["super"]
-    for join in (0, 1):
-        for flag in (0, 1):
-            e = OverlapEngine(0)
-            e.set_option("join", join)
-            e.set_option("prefix_contain", flag)
-            rows, sup = gpu_rows(e, ds, l)
-            e.close()
-            assert np.array_equal(rows_to_tuples(rows), want_rows), (join, flag)
-            assert {str(i): int(x) for i, x in enumerate(sup) if x} == want_sup, (join, flag)
-
-
-@pytest.mark.parametrize("name", FIXTURES)
-def test_reg_cas_index(name):
-    """option reg_cas: the register scan CAS-inserts all four keys itself; the
-    same rows, superReadIDs and getListOfReads lists (incl. list order)."""
-    meta = load_meta(name)
-    ds = Dataset.from_files([fixture_input(name)], meta["l"])
     e = OverlapEngine(0)
-    e.set_option("reg_cas", 1)
-    rows, sup = gpu_rows(e, ds, meta["l"])
-    assert np.array_equal(rows_to_tuples(rows), golden_rows(name))
-    assert {str(i): int(x) for i, x in enumerate(sup) if x} == meta["super"]
-    for key, exp in meta.get("lookups", {}).items():
-        assert [list(x) for x in e.lookup(key)] == exp, key
+    e.set_option("prefix_contain", 0)
+    rows, sup = gpu_rows(e, ds, l)
     e.close()
-
-
-def test_cell_pingpong_rebuilds():
-    """option cell_pp: builds alternate between two cell tables, the
-    next one cleared on a side stream; repeated builds on one engine over data
-    sets of growing and shrinking table sizes (and nb_log2 changes) give the
-    golden rows every time."""
-    e = OverlapEngine(0)
-    e.set_option("cell_pp", 1)
-    seq = ["small", "highdup", "mixed", "mixed", "tworead", "branchy", "small", "tandem", "mixed"]
-    for i, name in enumerate(seq):
-        meta = load_meta(name)
-        ds = Dataset.from_files([fixture_input(name)], meta["l"])
-        rows, sup = gpu_rows(e, ds, meta["l"], nb_log2=(10 if i == 5 else 0))
-        assert np.array_equal(rows_to_tuples(rows), golden_rows(name)), (i, name)
-        assert {str(k): int(x) for k, x in enumerate(sup) if x} == meta["super"], (i, name)
-        # a second build on the same upload takes the other table
-        e.build_index(meta["l"], 0)
-        e.mark_contained()
-        rows2 = e.rows(e.find_overlaps())
-        assert np.array_equal(rows_to_tuples(rows2), golden_rows(name)), (i, name, "rebuild")
-    e.close()
+    assert np.array_equal(rows_to_tuples(rows), want_rows)
+    assert {str(i): int(x) for i, x in enumerate(sup) if x} == want_sup
 
 
 CONTAIN_OPTS = [
@@ -709,14 +644,10 @@ CONTAIN_OPTS = [
     {"contain_jcut": 1, "contain_prune": 0, "contain_skip": 0},
     {"contain_jcut": 0, "contain_prune": 1, "contain_skip": 0},
     {"contain_jcut": 0, "contain_prune": 0, "contain_skip": 1},
-    {"contain_skip": 1, "contain_passes": 3},
     {"contain_skip": 1, "prefix_contain": 0},
     {"probe_share": 0, "probe_compact": 0},
     {"probe_share": 1, "probe_compact": 0},
     {"probe_share": 0, "probe_compact": 1},
-    {"cell_pp": 1},
-    {"reg_cas": 1},
-    {"probe_share_xcd": 1},
 ]
 
 
@@ -753,7 +684,7 @@ def test_containment_options(name):
         assert np.array_equal(rows_to_tuples(rows), want_rows), opts
 
 
-@pytest.mark.parametrize("name", FIXTURES)
+@pytest.mark.parametrize("name", ["small", "mixed", "tandem", "highdup", "tworead"])
 def test_replicated_index_source_shards(name):
     """Multi-GPU replicated mode (bench --multi replicated): every rank builds
     the whole index and discovers only from its source-read range; each rank
@@ -771,147 +702,47 @@ def test_replicated_index_source_shards(name):
         if hi == lo:  # an empty range (read_hi = 0 would mean "all")
             continue
         e = OverlapEngine(0)
-        e.set_option("overlap_scan", 0)
         rows, sup = gpu_rows(e, ds, meta["l"], shard=(0, 1, lo, hi))
         e.close()
         assert {str(i): int(s) for i, s in enumerate(sup) if s} == meta["super"]
+        assert_shard_rows(rows, lo, hi)
         parts.append(rows)
     allrows = np.concatenate(parts) if parts else parts
     assert np.array_equal(rows_to_tuples(allrows), golden_rows(name))
 
 
-@pytest.mark.parametrize("name", ["mixed", "tandem", "highdup", "dirty"])
-def test_scan_inside_probe_path(name):
-    """option overlap_scan = 0: the window scan runs inside each probe pass
-    (containment and discovery scan separately) instead of once, on a second
-    stream, next to the index build."""
-    meta = load_meta(name)
-    ds = Dataset.from_files([fixture_input(name)], meta["l"])
-    e = OverlapEngine(0)
-    e.set_option("join", 0)
-    e.set_option("overlap_scan", 0)
-    rows, sup = gpu_rows(e, ds, meta["l"])
-    e.close()
-    assert np.array_equal(rows_to_tuples(rows), golden_rows(name))
-    assert {str(i): int(s) for i, s in enumerate(sup) if s} == meta["super"]
-
-
-@pytest.mark.parametrize("name", FIXTURES)
-def test_scan_register_index_path(name):
-    """option reg_index = 1: the cell index from the register scan's key records
-    (k_scan_reg<INDEX> + k_rc_keys) filed by k_insert_dense instead of the CAS
-    inserts inside k_scan<INDEX>; same keys, runs and rows."""
-    meta = load_meta(name)
-    ds = Dataset.from_files([fixture_input(name)], meta["l"])
-    e = OverlapEngine(0)
-    e.set_option("reg_index", 1)
-    rows, sup = gpu_rows(e, ds, meta["l"])
-    e.close()
-    assert np.array_equal(rows_to_tuples(rows), golden_rows(name))
-    assert {str(i): int(s) for i, s in enumerate(sup) if s} == meta["super"]
-
-
-@pytest.mark.parametrize("l,k", [(33, 1), (40, 8), (50, 17), (50, 18), (20, 19), (50, 31), (60, 32)])
+@pytest.mark.parametrize("l,k", [(33, 1), (50, 17), (20, 19), (50, 31), (60, 32)])
 def test_register_scan_window_extremes(engine, l, k):
-    """w = l - k = 32 (the register scan's largest window), 33 (falls back to the
-    LDS scan and the cell index), 1 and typical ones, against the oracle on mixed
-    lengths (containment, all four keys, runs crossing block edges), through the
-    join (default) and through the cell index with the register scan."""
+    """w = l - k = 32 (the register scan's largest window), 33 (the exchange
+    mode's key records then come from the LDS scan), 1 and typical ones, against
+    the oracle on mixed lengths (containment, all four keys, runs crossing block
+    edges): the fused path (k_scan<INDEX>), a source-range shard (run-only
+    scans) and the exchange mode at P = 2 (key records)."""
     c, L = synth.uniform_read_set(3000, 0, 15000, seed=120 + k, lo=l + 1, hi=l + 90)
     seqs = synth.codes_to_strings(c, L)
     ds = Dataset.from_codes(c, L, l)
     od = OracleDataset.from_strings(seqs, l)
     orows, osup, _, _ = od.overlaps(l)
-    for join, reg_index in ((1, 0), (0, 1), (0, 0)):
-        engine.set_option("join", join)
-        engine.set_option("reg_index", reg_index)
-        try:
-            rows, sup = gpu_rows(engine, ds, l, k=k)
-        finally:
-            engine.set_option("reg_index", 0)
-            engine.set_option("join", 0)
-        assert np.array_equal(sup.astype(np.uint64), osup), join
-        assert np.array_equal(rows_to_tuples(rows), sorted_tuples(orows)), join
-
-
-@pytest.mark.parametrize("name", FIXTURES)
-def test_join_path(name):
-    """option join = 1: the partitioned join (keys + runs as sorted join records,
-    per-partition LDS cells, k_join) instead of the cell index + bucket-sorted
-    run probe; same rows and superReadIDs."""
-    meta = load_meta(name)
-    ds = Dataset.from_files([fixture_input(name)], meta["l"])
-    e = OverlapEngine(0)
-    e.set_option("join", 1)
-    rows, sup = gpu_rows(e, ds, meta["l"])
-    e.close()
-    assert np.array_equal(rows_to_tuples(rows), golden_rows(name))
-    assert {str(i): int(s) for i, s in enumerate(sup) if s} == meta["super"]
-
-
-@pytest.mark.parametrize("name,parts", [("highdup", 1), ("tandem", 1), ("mixed", 1), ("branchy", 1), ("small", 3),
-                                        ("highdup", 12)])
-def test_join_forced_partitions(name, parts):
-    """join_parts_log2: two partitions hold thousands of keys each, so the LDS
-    table is filled in several chunks and the runs (and the containment prefix
-    queries) are streamed once per chunk; or many nearly empty partitions."""
-    meta = load_meta(name)
-    ds = Dataset.from_files([fixture_input(name)], meta["l"])
-    e = OverlapEngine(0)
-    e.set_option("join", 1)
-    e.set_option("join_parts_log2", parts)
-    rows, sup = gpu_rows(e, ds, meta["l"])
-    e.close()
-    assert np.array_equal(rows_to_tuples(rows), golden_rows(name))
-    assert {str(i): int(s) for i, s in enumerate(sup) if s} == meta["super"]
-
-
-def test_join_chunked_containment_vs_oracle(engine):
-    """Mixed lengths, many nested prefixes, 2 partitions: containment queries
-    across key chunks of one partition."""
-    seqs, l = prefix_reads(seed=7) * 1, 40
-    c, L = synth.metagenome_read_set(20000, 100, 250, n_genomes=20, total_len=400000, seed=57)
-    seqs = seqs + synth.codes_to_strings(c, L)
-    ds = Dataset.from_strings(seqs, l)
-    od = OracleDataset.from_strings(seqs, l)
-    engine.set_option("join", 1)
-    engine.set_option("join_parts_log2", 1)
-    try:
-        rows, sup = gpu_rows(engine, ds, l, k=0)
-    finally:
-        engine.set_option("join_parts_log2", 0)
-        engine.set_option("join", 0)
-    orows, osup, _, _ = od.overlaps(l)
+    rows, sup = gpu_rows(engine, ds, l, k=k)
     assert np.array_equal(sup.astype(np.uint64), osup)
     assert np.array_equal(rows_to_tuples(rows), sorted_tuples(orows))
+    n = ds.num_unique
+    a, _ = gpu_rows(engine, ds, l, k=k, shard=(0, 1, 0, n // 2))
+    b, _ = gpu_rows(engine, ds, l, k=k, shard=(0, 1, n // 2, n))
+    assert np.array_equal(rows_to_tuples(np.concatenate([a, b])), sorted_tuples(orows))
+    xrows, xsup = exchange_rows(ds, l, 2, k=k)
+    assert np.array_equal(xsup.astype(np.uint64), osup)
+    assert np.array_equal(rows_to_tuples(xrows), sorted_tuples(orows))
 
 
-@pytest.mark.parametrize("name", ["mixed", "tandem", "highdup", "branchy"])
-def test_scan_lds_path(name):
-    """option scan_reg = 0: the LDS sliding-minimum scan (k_scan) for the run
-    scans as well (source-range shards: a scan per probe pass)."""
+@pytest.mark.parametrize("name", ["small", "mixed", "tandem", "branchy", "longreads"])
+def test_id_order_layout(name):
+    """option layout = 0 (slots in ID order) beside the default (clustered
+    slots): same rows, superReadIDs, getListOfReads lists and downloaded reads."""
     meta = load_meta(name)
     ds = Dataset.from_files([fixture_input(name)], meta["l"])
     e = OverlapEngine(0)
-    e.set_option("scan_reg", 0)
-    e.set_option("overlap_scan", 0)
-    rows, sup = gpu_rows(e, ds, meta["l"])
-    e.close()
-    assert np.array_equal(rows_to_tuples(rows), golden_rows(name))
-    assert {str(i): int(s) for i, s in enumerate(sup) if s} == meta["super"]
-
-
-@pytest.mark.parametrize("name", FIXTURES)
-@pytest.mark.parametrize("layout,sort_runs", [(0, 0), (0, 1), (1, 1)])
-def test_layout_and_sort_options(name, layout, sort_runs):
-    """option layout = 0 (slots in ID order) and the bucket-sorted run probe
-    (sort_runs = 1) beside the default (clustered slots, runs in read order):
-    same rows, superReadIDs, getListOfReads lists and downloaded reads."""
-    meta = load_meta(name)
-    ds = Dataset.from_files([fixture_input(name)], meta["l"])
-    e = OverlapEngine(0)
-    e.set_option("layout", layout)
-    e.set_option("sort_runs", sort_runs)
+    e.set_option("layout", 0)
     rows, sup = gpu_rows(e, ds, meta["l"])
     assert np.array_equal(rows_to_tuples(rows), golden_rows(name))
     assert {str(i): int(s) for i, s in enumerate(sup) if s} == meta["super"]

@@ -56,3 +56,32 @@ def test_oracle_lookup_golden(name):
     ds = OracleDataset.from_files([fixture_input(name)], meta["l"])
     for key, exp in meta["lookups"].items():
         assert [list(x) for x in ds.lookup(meta["l"], key)] == exp, key
+
+
+@pytest.mark.parametrize("name", FIXTURES)
+@pytest.mark.parametrize("nthreads", [1, 3, 8])
+def test_oracle_threaded_digest_matches_reference_fixture(name, nthreads):
+    """mgo_overlaps_digest (source-range threads, digests only; the recipe of
+    the 50M C5 golden) == the reference's rows and superReadIDs on every fixture."""
+    import digest
+
+    meta = load_meta(name)
+    ds = OracleDataset.from_files([fixture_input(name)], meta["l"])
+    rd, sd, sup, _ = ds.overlaps_digest(meta["l"], nthreads, want_super=True)
+    g = golden_rows(name)
+    assert rd == digest.rows_digest(g[:, 0], g[:, 1], g[:, 2], g[:, 3])
+    assert {str(i): int(s) for i, s in enumerate(sup) if s} == meta["super"]
+    s = np.zeros(meta["n_unique"] + 1, dtype=np.uint64)
+    for k, v in meta["super"].items():
+        s[int(k)] = v
+    assert sd == digest.super_digest(s)
+
+
+def test_oracle_from_codes_equals_from_strings():
+    from metagenomics_amd import synth
+
+    c, L = synth.metagenome_read_set(3000, 100, 250, 5, 60_000, 9)
+    a = OracleDataset.from_codes(c, L, 50)
+    b = OracleDataset.from_strings(synth.codes_to_strings(c, L), 50)
+    assert a.num_unique == b.num_unique and a.num_reads == b.num_reads
+    assert all(a.read(i) == b.read(i) for i in range(1, a.num_unique + 1, 7))

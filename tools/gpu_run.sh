@@ -56,18 +56,12 @@ for s in $STEPS; do
   parse)
     timeout -k 10 900 python -u tools/parse_bench.py > $OUT/parse_bench.json 2> $OUT/parse_bench.err
     rc=$?; echo "parse rc=$rc"; tail -12 $OUT/parse_bench.err; cat $OUT/parse_bench.json ;;
-  indexcost)
-    timeout -k 10 300 python -u tools/index_cost.py > $OUT/index_cost.log 2>&1
-    rc=$?; echo "indexcost rc=$rc"; grep index_ms $OUT/index_cost.log ;;
   variants)
     timeout -k 10 400 python -u tools/variant_sweep.py > $OUT/variant_sweep.log 2>&1
     rc=$?; echo "variants rc=$rc"; grep opts $OUT/variant_sweep.log ;;
   phases)
     timeout -k 10 400 python -u tools/phase_sweep.py > $OUT/phase_sweep.log 2>&1
     rc=$?; echo "phases rc=$rc"; grep phase $OUT/phase_sweep.log ;;
-  benchsplit)
-    timeout -k 10 300 python -u bench.py --split-probe --no-cpu-baseline > $OUT/bench_split.json 2> $OUT/bench_split.err
-    rc=$?; echo "bench split-probe rc=$rc"; cat $OUT/bench_split.json ;;
   benchc2)
     timeout -k 10 300 python -u bench.py --config c2 --no-cpu-baseline > $OUT/bench_c2.json 2> $OUT/bench_c2.err
     rc=$?; echo "bench c2 rc=$rc"; cat $OUT/bench_c2.json ;;
@@ -77,9 +71,6 @@ for s in $STEPS; do
   prof)
     timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o kt -- python3 bench.py --steps 5 --no-cpu-baseline > $OUT/prof_bench.json 2> $OUT/prof_bench.err
     rc=$?; echo "prof rc=$rc"; cat $OUT/prof_bench.json; head -8 $OUT/prof/kt_kernel_stats.csv | cut -c1-200 ;;
-  profsort)
-    timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/profsort -o kt -- python3 bench.py --steps 3 --no-cpu-baseline --no-ingest --sort-runs 1 > $OUT/profsort_bench.json 2> $OUT/profsort_bench.err
-    rc=$?; echo "profsort rc=$rc"; python3 -c "import json;d=json.load(open('$OUT/profsort_bench.json'));print(d['ms_per_step'], d['device_ms'])"; head -12 $OUT/profsort/kt_kernel_stats.csv | cut -c1-150 ;;
   profsim)
     timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/profsim -o kt -- python3 bench.py --sim-world 4 --multi exchange --steps 2 --no-cpu-baseline > $OUT/profsim_bench.json 2> $OUT/profsim_bench.err
     rc=$?; echo "profsim rc=$rc"; cat $OUT/profsim_bench.json; cat $OUT/profsim/kt_kernel_stats.csv ;;

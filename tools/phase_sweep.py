@@ -9,8 +9,6 @@ G = n * 150 // 20
 c, L = synth.uniform_read_set(n, 150, G, seed=31)
 ds = Dataset.from_codes(c, L, 50, nthreads=16)
 eng = OverlapEngine(0)
-if os.environ.get("MG_SORT_RUNS"):
-    eng.set_option("sort_runs", int(os.environ["MG_SORT_RUNS"]))
 eng.upload(ds)
 eng.build_index(50, 31)
 eng.mark_contained(copy=False)
