@@ -49,6 +49,10 @@ struct PackedReads;
 class Dataset;
 class Edge;
 
+// The exploration state and the transitive-reduction marks (OverlapGraph.h:20-30).
+enum nodeType { UNEXPLORED = 0, EXPLORED = 1, EXPLORED_AND_TRANSITIVE_EDGES_MARKED = 2 };
+enum markType { VACANT = 0, INPLAY = 1, ELIMINATED = 2 };
+
 class Read {
  public:
   UINT64 superReadID = 0;      // 0 = not contained, else ID of the super read (Read.h:50)
@@ -102,6 +106,8 @@ class Edge {
   UINT16 flow = 0;  // Edge.h:42 (0 until flow is computed)
 
  private:
+  friend class OverlapGraph;
+  UINT64 serial = 0;  // creation order (insertEdge(Read*,...) makes the edge before its twin)
   Read* source;
   Read* destination;
   UINT8 overlapOrientation;  // 0 = u<---<v, 1 = u<--->v, 2 = u>---<v, 3 = u>--->v
@@ -181,6 +187,33 @@ class OverlapGraph {
   void markContainedReads();
   bool insertEdge(Edge* edge);
   bool insertEdge(Read* read1, Read* read2, UINT8 orient, UINT16 overlapOffset);
+
+  // --- the reference's per-read build steps (OverlapGraph.h:54,64-68), for a
+  // caller that drives its own exploration as buildOverlapGraphFromHashTable
+  // does (OverlapGraph.cpp:144-204).  beginBuildFromHashTable(ht) does that
+  // function's set-up (:111-142): counters, the N + 1 empty lists,
+  // markContainedReads on the device, and the device discovery of every read's
+  // D(A) (mg_find_overlaps), kept on the host in insertAllEdgesOfRead's loop
+  // order; the caller keeps ownership of ht.  Then:
+  //  * insertAllEdgesOfRead (:529-565) inserts D(readNumber) in that order,
+  //    skipping partners that are not UNEXPLORED (:546), and sorts the list by
+  //    overlap offset with the reference's comparator (:563);
+  //  * markTransitiveEdges (:574-615) / removeTransitiveEdges (:623-661) on
+  //    the Edge objects, statement for statement;
+  //  * checkOverlap (:354-383) / checkOverlapForContainedRead (:302-340) are
+  //    the reference's string predicates for any pair (the device answers the
+  //    same questions in bulk);
+  //  * the contraction steps, sortEdges and saveGraphToFile then apply to the
+  //    caller-built graph as to buildOverlapGraphFromHashTable's.
+  bool beginBuildFromHashTable(HashTable* ht);
+  bool insertAllEdgesOfRead(UINT64 readNumber, std::vector<nodeType>* exploredReads);
+  bool markTransitiveEdges(UINT64 readNumber, std::vector<markType>* markedNodes);
+  bool removeTransitiveEdges(UINT64 readNumber);
+  bool checkOverlap(Read* read1, Read* read2, UINT64 orient, UINT64 start);
+  bool checkOverlapForContainedRead(Read* read1, Read* read2, UINT64 orient, UINT64 start);
+  // the .unitig checkpoint back into the graph (:1270-1367; main.cpp:36-42's
+  // -s resume: OverlapGraph() -> setDataset -> readGraphFromFile -> sortEdges)
+  bool readGraphFromFile(const std::string& fileName);
   UINT64 getNumberOfEdges() { return numberOfEdges; }
   UINT64 getNumberOfNodes() { return numberOfNodes; }
   bool setDataset(Dataset* d) {
@@ -216,8 +249,12 @@ class OverlapGraph {
   bool containedDone = false;
   mg_timings lastTimings{};
   mg::UnitigGraph* unitig = nullptr;  // the list state the contraction steps work on
+  struct Manual;                      // a caller-driven build: D(A) lists + the hash string length
+  Manual* manual = nullptr;
+  UINT64 nextSerial = 0;
   void clear();
   void materialize();  // graph / Edge objects / read locations from `unitig`
+  void adoptEdgeLists();  // `unitig` from the Edge lists of a caller-driven build
 };
 
 #endif  // MG_API_HPP_

@@ -85,6 +85,13 @@ typedef struct mgh_graph mgh_graph;
 /* 0 = ok; -1 bad arguments; -2 rows inconsistent with lens / h; -3 unpaired self rows */
 int mgh_graph_replay(const mg_edge* rows, uint64_t n_rows, const uint16_t* lens, uint64_t n_reads, uint32_t h,
                      mgh_graph** out);
+/* OverlapGraph::readGraphFromFile (OverlapGraph.cpp:1270-1367): a .unitig
+ * checkpoint back into a graph (both edges of every record, twins rebuilt,
+ * read locations updated); lens[id - 1] of the Dataset it was written for.
+ * The handle then behaves as a contracted one (sort_edges, save_unitig,
+ * save_lists, unitig_edges).  0 ok; -1 cannot open; -2 malformed or a read ID
+ * out of range; -3 bad arguments. */
+int mgh_graph_read_unitig(const char* path, const uint16_t* lens, uint64_t n_reads, mgh_graph** out);
 void mgh_graph_free(mgh_graph* g);
 uint64_t mgh_graph_nodes(const mgh_graph* g); /* OverlapGraph::getNumberOfNodes */
 uint64_t mgh_graph_edges(const mgh_graph* g); /* OverlapGraph::getNumberOfEdges (directed) */

@@ -35,14 +35,6 @@ namespace {
 enum : uint8_t { UNEXPLORED = 0, EXPLORED = 1, EXPLORED_AND_MARKED = 2 };  // nodeType (OverlapGraph.h:20-25)
 enum : uint8_t { VACANT = 0, INPLAY = 1, ELIMINATED = 2 };                // markType (OverlapGraph.h:26-30)
 
-struct Disc {  // one discovery of a read, in loop order
-  uint32_t j;
-  uint32_t r2;
-  uint8_t o;
-  uint8_t orient;
-  uint16_t offset;
-};
-
 inline uint8_t orient_to_key(uint8_t orient) {  // inverse of the switch at OverlapGraph.cpp:550-556
   return orient == 3 ? 0 : orient == 0 ? 1 : orient == 2 ? 2 : 3;
 }
@@ -198,6 +190,59 @@ struct GraphReplay::Impl {
 GraphReplay::GraphReplay() : impl(new Impl) { impl->g = this; }
 GraphReplay::~GraphReplay() { delete impl; }
 
+int Discoveries::build(const mg_edge* rows, uint64_t n_rows, const uint16_t* lens, uint64_t n_reads, uint32_t h) {
+  // D(A) from the rows with src = A (counting sort by src)
+  start.assign(n_reads + 2, 0);
+  for (uint64_t i = 0; i < n_rows; ++i) {
+    if (rows[i].src < 1 || rows[i].src > n_reads || rows[i].dst < 1 || rows[i].dst > n_reads) return -1;
+    start[rows[i].src + 1]++;
+  }
+  for (uint64_t a = 1; a <= n_reads + 1; ++a) start[a] += start[a - 1];
+  disc.assign(n_rows, Disc{});
+  {
+    std::vector<uint64_t> at(start.begin(), start.end() - 1);
+    for (uint64_t i = 0; i < n_rows; ++i) {
+      const mg_edge& r = rows[i];
+      const uint8_t o = orient_to_key(r.orient);
+      const int64_t n1 = lens[r.src - 1];
+      // window j: offset = j for o = 0, 2; offset = n1 - h - j for o = 1, 3 (:550-557)
+      const int64_t j = (o == 0 || o == 2) ? r.offset : n1 - (int64_t)h - r.offset;
+      if (j < 1 || j >= n1 - (int64_t)h) return -2;
+      disc[at[r.src]++] = Disc{(uint32_t)j, r.dst, o, r.orient, r.offset};
+    }
+  }
+  // loop order; each self row is present twice in M and counts once
+  for (uint64_t a = 1; a <= n_reads; ++a) {
+    const uint64_t lo = start[a], hi = start[a + 1];
+    std::sort(disc.begin() + lo, disc.begin() + hi, [](const Disc& x, const Disc& y) {
+      if (x.j != y.j) return x.j < y.j;
+      if (x.r2 != y.r2) return x.r2 < y.r2;
+      return x.o < y.o;
+    });
+  }
+  uint64_t w = 0;
+  std::vector<uint64_t> ns(n_reads + 2, 0);
+  for (uint64_t a = 1; a <= n_reads; ++a) {
+    ns[a] = w;
+    const uint64_t lo = start[a], hi = start[a + 1];
+    for (uint64_t k = lo; k < hi; ++k) {
+      const Disc& d = disc[k];
+      if (d.r2 == a) {
+        if (k + 1 >= hi || std::memcmp(&disc[k + 1], &d, sizeof(Disc)) != 0) return -3;  // must come in pairs
+        disc[w++] = d;
+        ++k;
+      } else {
+        disc[w++] = d;
+      }
+    }
+  }
+  ns[n_reads + 1] = w;
+  ns[0] = 0;
+  start.swap(ns);
+  disc.resize(w);
+  return 0;
+}
+
 int GraphReplay::build(const mg_edge* rows, uint64_t n_rows, const uint16_t* lens, uint64_t n_reads, uint32_t h) {
   Impl& I = *impl;
   I.len = lens;
@@ -206,57 +251,11 @@ int GraphReplay::build(const mg_edge* rows, uint64_t n_rows, const uint16_t* len
   pool.clear();
   lists.assign(n_reads + 1, {});
   nodes = edges = 0;
-  // D(A) from the rows with src = A (counting sort by src)
-  I.dstart.assign(n_reads + 2, 0);
-  for (uint64_t i = 0; i < n_rows; ++i) {
-    if (rows[i].src < 1 || rows[i].src > n_reads || rows[i].dst < 1 || rows[i].dst > n_reads) return -1;
-    I.dstart[rows[i].src + 1]++;
-  }
-  for (uint64_t a = 1; a <= n_reads + 1; ++a) I.dstart[a] += I.dstart[a - 1];
-  I.disc.assign(n_rows, Disc{});
-  {
-    std::vector<uint64_t> at(I.dstart.begin(), I.dstart.end() - 1);
-    for (uint64_t i = 0; i < n_rows; ++i) {
-      const mg_edge& r = rows[i];
-      const uint8_t o = orient_to_key(r.orient);
-      const int64_t n1 = lens[r.src - 1];
-      // window j: offset = j for o = 0, 2; offset = n1 - h - j for o = 1, 3 (:550-557)
-      const int64_t j = (o == 0 || o == 2) ? r.offset : n1 - (int64_t)h - r.offset;
-      if (j < 1 || j >= n1 - (int64_t)h) return -2;
-      I.disc[at[r.src]++] = Disc{(uint32_t)j, r.dst, o, r.orient, r.offset};
-    }
-  }
-  // loop order; each self row is present twice in M and counts once
-  for (uint64_t a = 1; a <= n_reads; ++a) {
-    const uint64_t lo = I.dstart[a], hi = I.dstart[a + 1];
-    std::sort(I.disc.begin() + lo, I.disc.begin() + hi, [](const Disc& x, const Disc& y) {
-      if (x.j != y.j) return x.j < y.j;
-      if (x.r2 != y.r2) return x.r2 < y.r2;
-      return x.o < y.o;
-    });
-  }
-  {
-    uint64_t w = 0;
-    std::vector<uint64_t> ns(n_reads + 2, 0);
-    for (uint64_t a = 1; a <= n_reads; ++a) {
-      ns[a] = w;
-      const uint64_t lo = I.dstart[a], hi = I.dstart[a + 1];
-      for (uint64_t k = lo; k < hi; ++k) {
-        const Disc& d = I.disc[k];
-        if (d.r2 == a) {
-          if (k + 1 >= hi || std::memcmp(&I.disc[k + 1], &d, sizeof(Disc)) != 0) return -3;  // must come in pairs
-          I.disc[w++] = d;
-          ++k;
-        } else {
-          I.disc[w++] = d;
-        }
-      }
-    }
-    ns[n_reads + 1] = w;
-    ns[0] = 0;
-    I.dstart.swap(ns);
-    I.disc.resize(w);
-  }
+  Discoveries D;
+  const int rc = D.build(rows, n_rows, lens, n_reads, h);
+  if (rc) return rc;
+  I.dstart.swap(D.start);
+  I.disc.swap(D.disc);
   pool.reserve(n_rows);
   I.run();
   return 0;

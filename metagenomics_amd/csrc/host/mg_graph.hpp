@@ -18,6 +18,29 @@ struct GraphEdge {  // Edge (Edge.h:18-44) without the contraction fields
   uint32_t rev;   // reverseEdge (index into the pool)
 };
 
+// One discovery of read A: window j, partner r2, key o (HashTable's 2-bit
+// orientation) and the edge insertEdge(A, r2, orient, offset) would create
+// (OverlapGraph.cpp:550-557).
+struct Disc {
+  uint32_t j;
+  uint32_t r2;
+  uint8_t o;
+  uint8_t orient;
+  uint16_t offset;
+};
+
+// D(A) for every read A, in insertAllEdgesOfRead's loop order (window j
+// ascending, then getListOfReads order: partner ID, then key o;
+// OverlapGraph.cpp:534-547, HashTable.cpp:58-60), from the device's directed
+// discovery multiset.  D(A) = disc[start[A] .. start[A + 1]).
+struct Discoveries {
+  std::vector<uint64_t> start;
+  std::vector<Disc> disc;
+  // rows: the full directed multiset (any order); lens[id - 1]; h = l - 1.
+  // 0 = ok, < 0 = rows inconsistent with the lengths / h.
+  int build(const mg_edge* rows, uint64_t n_rows, const uint16_t* lens, uint64_t n_reads, uint32_t h);
+};
+
 class GraphReplay {
  public:
   GraphReplay();

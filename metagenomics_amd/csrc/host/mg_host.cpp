@@ -14,6 +14,7 @@
 #include <iomanip>
 #include <sstream>
 #include <thread>
+#include <unordered_map>
 
 #include "mg_api.hpp"
 #include "mg_parse.hpp"
@@ -536,10 +537,17 @@ void free_graph(std::vector<std::vector<Edge*>*>*& graph) {
 }
 }  // namespace
 
+struct OverlapGraph::Manual {
+  mg::Discoveries D;  // D(A) of every read, in insertAllEdgesOfRead's loop order
+  UINT64 h = 0;       // hashTable->getHashStringLength()
+};
+
 void OverlapGraph::clear() {
   free_graph(graph);
   delete unitig;
   unitig = nullptr;
+  delete manual;
+  manual = nullptr;
 }
 
 void OverlapGraph::materialize() {
@@ -588,7 +596,37 @@ void OverlapGraph::materialize() {
   numberOfEdges = ug.edges;
 }
 
+void OverlapGraph::adoptEdgeLists() {
+  // the Edge lists of a caller-driven build as compact records, numbered in
+  // creation order (the .unitig writer's self-loop rule, mg_unitig.cpp)
+  if (unitig || !graph) return;
+  const UINT64 N = dataSet->getNumberOfUniqueReads();
+  std::vector<Edge*> live;
+  for (UINT64 u = 1; u <= N; ++u)
+    for (Edge* e : *(*graph)[u]) live.push_back(e);
+  std::sort(live.begin(), live.end(), [](Edge* a, Edge* b) { return a->serial < b->serial; });
+  std::unordered_map<const Edge*, uint32_t> idx;
+  idx.reserve(live.size() * 2);
+  for (size_t i = 0; i < live.size(); ++i) idx[live[i]] = (uint32_t)i;
+  std::vector<mg::GraphEdge> pool(live.size());
+  for (size_t i = 0; i < live.size(); ++i) {
+    Edge* e = live[i];
+    auto it = idx.find(e->getReverseEdge());
+    if (it == idx.end()) throw mg::Error("graph edge without its listed twin");
+    pool[i] = mg::GraphEdge{(uint32_t)e->getSourceRead()->getReadNumber(),
+                            (uint32_t)e->getDestinationRead()->getReadNumber(), (uint16_t)e->getOverlapOffset(),
+                            e->getOrientation(), 0, it->second};
+  }
+  std::vector<std::vector<uint32_t>> lists(N + 1);
+  for (UINT64 u = 1; u <= N; ++u)
+    for (Edge* e : *(*graph)[u]) lists[u].push_back(idx[e]);
+  unitig = new mg::UnitigGraph();
+  unitig->init(pool, lists, numberOfNodes, numberOfEdges, N, true);
+  materialize();
+}
+
 UINT64 OverlapGraph::contractCompositePaths() {
+  adoptEdgeLists();
   if (!unitig) throw mg::Error("contractCompositePaths: no replayed graph");
   const UINT64 n = unitig->contract_composite_paths();
   if (unitig->bad_merge) throw mg::Error("Unable to merge.");  // OverlapGraph.cpp:830-833
@@ -597,6 +635,7 @@ UINT64 OverlapGraph::contractCompositePaths() {
 }
 
 UINT64 OverlapGraph::removeDeadEndNodes() {
+  adoptEdgeLists();
   if (!unitig) throw mg::Error("removeDeadEndNodes: no replayed graph");
   const UINT64 n = unitig->remove_dead_end_nodes();
   materialize();
@@ -617,6 +656,7 @@ void OverlapGraph::sortEdges() {
 }
 
 bool OverlapGraph::saveGraphToFile(const std::string& fileName) {
+  adoptEdgeLists();
   if (!unitig) throw mg::Error("saveGraphToFile: no replayed graph");
   if (unitig->save_unitig(fileName.c_str())) throw mg::Error("Unable to open file: " + fileName);
   return true;
@@ -651,6 +691,8 @@ bool OverlapGraph::insertEdge(Read* read1, Read* read2, UINT8 orient, UINT16 ove
   const UINT16 rev = (UINT16)(read2->getReadLength() + overlapOffset - read1->getReadLength());
   const UINT8 tw = orient == 0 ? 3 : (orient == 3 ? 0 : orient);
   Edge* e2 = new Edge(read2, read1, tw, rev);
+  e1->serial = nextSerial++;
+  e2->serial = nextSerial++;
   e1->setReverseEdge(e2);
   e2->setReverseEdge(e1);
   insertEdge(e1);
@@ -708,6 +750,162 @@ bool OverlapGraph::buildOverlapGraphFromHashTable(HashTable* ht) {
   }
   delete ht;  // the graph owns and frees the table (:210)
   hashTable = nullptr;
+  return true;
+}
+
+bool OverlapGraph::beginBuildFromHashTable(HashTable* ht) {
+  // buildOverlapGraphFromHashTable's set-up (OverlapGraph.cpp:111-142); the
+  // caller then explores (:144-204) through insertAllEdgesOfRead & co.
+  clear();
+  hashTable = ht;
+  dataSet = ht->getDataset();
+  numberOfNodes = numberOfEdges = 0;
+  nextSerial = 0;
+  const UINT64 N = dataSet->getNumberOfUniqueReads();
+  graph = new std::vector<std::vector<Edge*>*>();
+  graph->reserve(N + 1);
+  for (UINT64 i = 0; i <= N; ++i) graph->push_back(new std::vector<Edge*>());
+  markContainedReads();
+  mg_ctx* ctx = ht->context();
+  uint64_t nrows = 0;
+  if (mg_find_overlaps(ctx, &nrows)) mg::fail(ctx, "beginBuildFromHashTable");
+  std::vector<mg_edge> rows(nrows);
+  uint64_t got = 0;
+  if (mg_copy_rows(ctx, rows.data(), nrows, &got)) mg::fail(ctx, "copy rows");
+  mg_get_timings(ctx, &lastTimings);
+  manual = new Manual();
+  manual->h = ht->getHashStringLength();
+  const int rc = manual->D.build(rows.data(), got, dataSet->packedLengths(), N, (uint32_t)manual->h);
+  if (rc) throw mg::Error("discoveries inconsistent with the Dataset (" + std::to_string(rc) + ")");
+  return true;
+}
+
+bool OverlapGraph::insertAllEdgesOfRead(UINT64 readNumber, std::vector<nodeType>* exploredReads) {
+  // OverlapGraph.cpp:529-565: D(readNumber) in the loop order (j, then the
+  // getListOfReads list: partner ID, then o); the device verified each one
+  // (checkOverlap with both superReadIDs 0, :548)
+  if (!manual) throw mg::Error("insertAllEdgesOfRead: call beginBuildFromHashTable first");
+  Read* read1 = dataSet->getReadFromID(readNumber);
+  const mg::Discoveries& D = manual->D;
+  for (uint64_t k = D.start[readNumber]; k < D.start[readNumber + 1]; ++k) {
+    const mg::Disc& d = D.disc[k];
+    if (exploredReads->at(d.r2) != UNEXPLORED) continue;  // :546
+    insertEdge(read1, dataSet->getReadFromID(d.r2), d.orient, d.offset);
+  }
+  std::vector<Edge*>* lst = (*graph)[readNumber];
+  if (!lst->empty())  // compareEdges (:42-45): overlap offset ascending, std::sort as :563
+    std::sort(lst->begin(), lst->end(), [](Edge* a, Edge* b) { return a->getOverlapOffset() < b->getOverlapOffset(); });
+  return true;
+}
+
+bool OverlapGraph::markTransitiveEdges(UINT64 readNumber, std::vector<markType>* markedNodes) {
+  // OverlapGraph.cpp:574-615 (Myers' transitive reduction, one read)
+  std::vector<Edge*>& lu = *(*graph)[readNumber];
+  for (Edge* e : lu) markedNodes->at(e->getDestinationRead()->getReadNumber()) = INPLAY;
+  for (size_t i = 0; i < lu.size(); ++i) {
+    const UINT64 read2 = lu[i]->getDestinationRead()->getReadNumber();
+    if (markedNodes->at(read2) != INPLAY) continue;
+    const UINT8 t1 = lu[i]->getOrientation();
+    for (Edge* e2 : *(*graph)[read2]) {
+      const UINT64 read3 = e2->getDestinationRead()->getReadNumber();
+      if (markedNodes->at(read3) != INPLAY) continue;
+      const UINT8 t2 = e2->getOrientation();
+      if ((t1 == 0 || t1 == 2) && (t2 == 0 || t2 == 1))
+        markedNodes->at(read3) = ELIMINATED;
+      else if ((t1 == 1 || t1 == 3) && (t2 == 2 || t2 == 3))
+        markedNodes->at(read3) = ELIMINATED;
+    }
+  }
+  for (Edge* e : lu) {
+    if (markedNodes->at(e->getDestinationRead()->getReadNumber()) == ELIMINATED) {
+      e->transitiveRemovalFlag = true;
+      e->getReverseEdge()->transitiveRemovalFlag = true;
+    }
+  }
+  for (Edge* e : lu) markedNodes->at(e->getDestinationRead()->getReadNumber()) = VACANT;
+  markedNodes->at(readNumber) = VACANT;
+  return true;
+}
+
+bool OverlapGraph::removeTransitiveEdges(UINT64 readNumber) {
+  // OverlapGraph.cpp:623-661: the twins first (the last edge of their list
+  // moved into their place), then this read's marked edges, order kept
+  std::vector<Edge*>& lu = *(*graph)[readNumber];
+  for (size_t index = 0; index < lu.size(); ++index) {
+    if (!lu[index]->transitiveRemovalFlag) continue;
+    Edge* twin = lu[index]->getReverseEdge();
+    std::vector<Edge*>& lt = *(*graph)[twin->getSourceRead()->getReadNumber()];
+    for (size_t k = 0; k < lt.size(); ++k) {
+      if (lt[k] == twin) {
+        delete twin;
+        lt[k] = lt.back();
+        lt.pop_back();
+        if (lt.empty()) numberOfNodes--;
+        numberOfEdges--;
+        break;
+      }
+    }
+  }
+  size_t j = 0;
+  for (size_t index = 0; index < lu.size(); ++index) {
+    if (!lu[index]->transitiveRemovalFlag) {
+      lu[j++] = lu[index];
+    } else {
+      numberOfEdges--;
+      delete lu[index];
+    }
+  }
+  lu.resize(j);
+  if (lu.empty()) numberOfNodes--;
+  return true;
+}
+
+namespace {
+UINT64 hash_string_length(HashTable* ht, UINT64 manual_h) {
+  if (ht) return ht->getHashStringLength();
+  if (manual_h) return manual_h;
+  throw mg::Error("checkOverlap: no hash table (the graph was built and its table freed)");
+}
+}  // namespace
+
+bool OverlapGraph::checkOverlap(Read* read1, Read* read2, UINT64 orient, UINT64 start) {
+  // OverlapGraph.cpp:354-383, the same unsigned arithmetic and substrings
+  const std::string string1 = read1->getStringForward();
+  const UINT64 h = hash_string_length(hashTable, manual ? manual->h : 0);
+  const std::string string2 = (orient == 0 || orient == 1) ? read2->getStringForward() : read2->getStringReverse();
+  if (orient == 0 || orient == 2) {
+    if (string1.length() - start - h >= string2.length() - h) return false;  // :367
+    return string1.substr(start + h, string1.length() - (start + h)) == string2.substr(h, string1.length() - (start + h));
+  }
+  if (string2.length() - h < start) return false;  // :379
+  return string1.substr(0, start) == string2.substr(string2.length() - h - start, start);
+}
+
+bool OverlapGraph::checkOverlapForContainedRead(Read* read1, Read* read2, UINT64 orient, UINT64 start) {
+  // OverlapGraph.cpp:302-340
+  const std::string string1 = read1->getStringForward();
+  const UINT64 h = hash_string_length(hashTable, manual ? manual->h : 0);
+  const std::string string2 = (orient == 0 || orient == 1) ? read2->getStringForward() : read2->getStringReverse();
+  if (orient == 0 || orient == 2) {
+    const UINT64 rem1 = string1.length() - start - h, rem2 = string2.length() - h;
+    if (rem1 >= rem2) return string1.substr(start + h, rem2) == string2.substr(h, rem2);
+  } else {
+    const UINT64 rem1 = start, rem2 = string2.length() - h;
+    if (rem1 >= rem2) return string1.substr(start - rem2, rem2) == string2.substr(0, rem2);
+  }
+  return false;
+}
+
+bool OverlapGraph::readGraphFromFile(const std::string& fileName) {
+  // OverlapGraph.cpp:1270-1367 (the -s resume of main.cpp:36-42)
+  if (!dataSet) throw mg::Error("readGraphFromFile: setDataset first");
+  clear();
+  numberOfNodes = numberOfEdges = 0;
+  unitig = new mg::UnitigGraph();
+  const int rc = unitig->read_unitig(fileName.c_str(), dataSet->packedLengths(), dataSet->getNumberOfUniqueReads(), true);
+  if (rc == -1) throw mg::Error("Unable to open file: " + fileName);
+  if (rc) throw mg::Error("readGraphFromFile: malformed unitig file " + fileName);
+  materialize();
   return true;
 }
 
@@ -857,6 +1055,21 @@ int mgh_graph_replay(const mg_edge* rows, uint64_t n_rows, const uint16_t* lens,
     *out = g;
   } catch (const std::exception&) {
     return -1;
+  }
+  return 0;
+}
+
+int mgh_graph_read_unitig(const char* path, const uint16_t* lens, uint64_t n_reads, mgh_graph** out) {
+  if (!out || !path || (n_reads && !lens)) return -3;
+  *out = nullptr;
+  try {
+    std::unique_ptr<mgh_graph> g(new mgh_graph());
+    g->u.reset(new mg::UnitigGraph());
+    const int rc = g->u->read_unitig(path, lens, n_reads, true);
+    if (rc) return rc;
+    *out = g.release();
+  } catch (const std::exception&) {
+    return -3;
   }
   return 0;
 }

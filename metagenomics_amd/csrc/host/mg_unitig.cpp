@@ -94,32 +94,37 @@ struct Out {
 }  // namespace
 
 void UnitigGraph::init(const GraphReplay& g, uint64_t n_reads, bool track_locations) {
+  init(g.pool, g.lists, g.nodes, g.edges, n_reads, track_locations);
+}
+
+void UnitigGraph::init(const std::vector<GraphEdge>& gpool, const std::vector<std::vector<uint32_t>>& glists,
+                       uint64_t gnodes, uint64_t gedges, uint64_t n_reads, bool track_locations) {
   track = track_locations;
   pool.clear();
   reads.clear();
   lists.assign(n_reads + 1, {});
   // keep only the listed edges (the transitive ones were deleted), renumbered
   // in creation order (insertEdge(Read*,...) allocates the edge before its twin)
-  std::vector<uint32_t> id(g.pool.size(), UINT32_MAX);
+  std::vector<uint32_t> id(gpool.size(), UINT32_MAX);
   uint64_t listed = 0;
-  for (size_t u = 1; u < g.lists.size() && u <= n_reads; ++u) {
-    listed += g.lists[u].size();
-    for (uint32_t e : g.lists[u]) id[e] = 0;
+  for (size_t u = 1; u < glists.size() && u <= n_reads; ++u) {
+    listed += glists[u].size();
+    for (uint32_t e : glists[u]) id[e] = 0;
   }
   pool.reserve(listed + listed / 2 + 16);
-  for (size_t e = 0; e < g.pool.size(); ++e) {
+  for (size_t e = 0; e < gpool.size(); ++e) {
     if (id[e] == UINT32_MAX) continue;
     id[e] = (uint32_t)pool.size();
-    const GraphEdge& x = g.pool[e];
+    const GraphEdge& x = gpool[e];
     pool.push_back(UnitigEdge{x.src, x.dst, UINT32_MAX, x.orient, 1, 0, x.offset});
   }
-  for (size_t e = 0; e < g.pool.size(); ++e)
-    if (id[e] != UINT32_MAX) pool[id[e]].rev = id[g.pool[e].rev];
-  for (size_t u = 1; u < g.lists.size() && u <= n_reads; ++u)
-    for (uint32_t e : g.lists[u]) lists[u].push_back(id[e]);
+  for (size_t e = 0; e < gpool.size(); ++e)
+    if (id[e] != UINT32_MAX) pool[id[e]].rev = id[gpool[e].rev];
+  for (size_t u = 1; u < glists.size() && u <= n_reads; ++u)
+    for (uint32_t e : glists[u]) lists[u].push_back(id[e]);
   reads.resize(pool.size());
-  nodes = g.nodes;
-  edges = g.edges;
+  nodes = gnodes;
+  edges = gedges;
   loc_fwd.clear();
   loc_rev.clear();
   if (track) {
@@ -128,6 +133,104 @@ void UnitigGraph::init(const GraphReplay& g, uint64_t n_reads, bool track_locati
   }
   merged_total = dead_end_total = 0;
   bad_merge = false;
+}
+
+int UnitigGraph::read_unitig(const char* path, const uint16_t* lens, uint64_t n_reads, bool track_locations) {
+  FILE* f = std::fopen(path, "rb");
+  if (!f) return -1;  // "Unable to open file: " (:1276)
+  std::vector<char> text;
+  {
+    char buf[1 << 16];
+    size_t k;
+    while ((k = std::fread(buf, 1, sizeof buf, f)) > 0) text.insert(text.end(), buf, buf + k);
+    std::fclose(f);
+  }
+  // while (good()) { file >> temp; list.push_back(temp); } (:1289-1294): every
+  // number, plus the value of the extraction that hits the end of the file
+  // when the last number is followed by whitespace (or the file is empty)
+  std::vector<uint64_t> vals;
+  bool in_num = false, bad = false;
+  uint64_t cur = 0;
+  for (char c : text) {
+    if (c >= '0' && c <= '9') {
+      cur = cur * 10 + (uint64_t)(c - '0');
+      in_num = true;
+    } else if (c == ' ' || c == '\n' || c == '\t' || c == '\r' || c == '\v' || c == '\f') {
+      if (in_num) vals.push_back(cur);
+      in_num = false;
+      cur = 0;
+    } else {
+      bad = true;
+      break;
+    }
+  }
+  if (bad) return -2;
+  const bool trailing = !in_num;  // the last extraction failed at the end of the file
+  if (in_num) vals.push_back(cur);
+  const uint64_t size = vals.size() + (trailing ? 1 : 0);
+  track = track_locations;
+  pool.clear();
+  reads.clear();
+  lists.assign(n_reads + 1, {});
+  loc_fwd.clear();
+  loc_rev.clear();
+  if (track) {
+    loc_fwd.resize(n_reads + 1);
+    loc_rev.resize(n_reads + 1);
+  }
+  nodes = edges = merged_total = dead_end_total = 0;
+  bad_merge = false;
+  flow_computed = false;
+  auto at = [&](uint64_t i, uint64_t* v) {
+    if (i >= vals.size()) return false;
+    *v = vals[i];
+    return true;
+  };
+  auto len = [&](uint64_t id) -> uint64_t { return lens[id - 1]; };
+  for (uint64_t i = 0; i + 1 < size;) {  // (:1297-1363)
+    uint64_t src, dst, orient, offset, nr;
+    if (!at(i, &src) || !at(i + 1, &dst) || !at(i + 2, &orient) || !at(i + 3, &offset) || !at(i + 4, &nr))
+      return -2;
+    i += 5;
+    if (src < 1 || src > n_reads || dst < 1 || dst > n_reads) return -2;  // getReadFromID's range check
+    if (nr > (vals.size() - i) / 3) return -2;
+    auto fr = std::make_unique<EdgeReads>();
+    uint64_t length = 0;
+    for (uint64_t j = 0; j < 3 * nr; j += 3) {
+      fr->reads.push_back((uint32_t)vals[i + j]);
+      fr->offs.push_back((uint16_t)vals[i + j + 1]);  // vector<UINT16>
+      fr->ors.push_back((uint8_t)vals[i + j + 2]);    // vector<UINT8>
+      length += vals[i + j + 1];
+    }
+    for (uint32_t r : fr->reads)
+      if (r < 1 || r > n_reads) return -2;
+    // the reverse edge's lists from the forward ones (:1322-1343)
+    auto rr = std::make_unique<EdgeReads>();
+    const uint64_t sz = fr->reads.size();
+    for (uint64_t j = 0; j < sz; ++j) {
+      rr->reads.push_back(fr->reads[sz - j - 1]);
+      uint64_t length1, fwd;
+      if (j == 0) {  // last / first read
+        length1 = len(dst);
+        fwd = offset - length;
+      } else {
+        length1 = len(fr->reads[sz - j]);
+        fwd = fr->offs[sz - j];
+      }
+      const uint64_t length2 = len(fr->reads[sz - j - 1]);
+      rr->offs.push_back((uint16_t)(length1 + fwd - length2));
+      rr->ors.push_back((uint8_t)!fr->ors[sz - j - 1]);
+    }
+    const uint64_t rev_offset = offset + len(dst) - len(src);
+    const uint32_t e1 = new_edge((uint32_t)src, (uint32_t)dst, (uint8_t)orient, offset, std::move(fr));
+    const uint32_t e2 = new_edge((uint32_t)dst, (uint32_t)src, twin_orient((uint8_t)orient), rev_offset, std::move(rr));
+    pool[e1].rev = e2;
+    pool[e2].rev = e1;
+    insert(e1);
+    insert(e2);
+    i += nr * 3;
+  }
+  return 0;
 }
 
 uint32_t UnitigGraph::new_edge(uint32_t src, uint32_t dst, uint8_t orient, uint64_t offset,

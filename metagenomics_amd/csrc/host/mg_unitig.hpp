@@ -37,6 +37,14 @@ class UnitigGraph {
   // Takes the replayed pre-contraction graph (buildOverlapGraphFromHashTable
   // up to :209).  track_locations = maintain the per-read location lists.
   void init(const GraphReplay& g, uint64_t n_reads, bool track_locations);
+  // the same from any pre-contraction edge pool + lists (a caller-driven build
+  // through OverlapGraph::insertAllEdgesOfRead & co.); pool in creation order
+  void init(const std::vector<GraphEdge>& gpool, const std::vector<std::vector<uint32_t>>& glists, uint64_t gnodes,
+            uint64_t gedges, uint64_t n_reads, bool track_locations);
+  // readGraphFromFile (:1270-1367): the .unitig checkpoint back into lists
+  // (both edges of every line, twins rebuilt, read locations updated);
+  // lens[id - 1].  0 ok, -1 cannot open, -2 malformed / read ID out of range.
+  int read_unitig(const char* path, const uint16_t* lens, uint64_t n_reads, bool track_locations);
   // do { contractCompositePaths(); removeDeadEndNodes(); } while (changed)
   // (:211-215).  Returns the number of loop iterations; < 0 on an
   // orientation the reference would MYEXIT on ("Unable to merge.").

@@ -10,7 +10,11 @@
 //                write every graph[u] list in list order to <prefix>.graph
 //                ("#C nodes edges" first) instead of the .unitig;
 //   -raw         the raw discovery multiset to <prefix>.edges (sorted
-//                "u v orient offset" lines).
+//                "u v orient offset" lines);
+//   -s           main.cpp:36-42's resume: OverlapGraph() -> setDataset ->
+//                readGraphFromFile(<prefix>.unitig) -> sortEdges (no device
+//                needed), then saveGraphToFile(<prefix>.resumed.unitig) and the
+//                lists in list order to <prefix>.resumed.graph.
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -21,7 +25,7 @@
 
 static void usage() {
   std::fprintf(stderr,
-               "Usage: mg_overlap [-pe n f1..fn] [-se n f1..fn] -f prefix -l minOverlap [-k seedK] [-d device] [-nocontract | -raw]\n");
+               "Usage: mg_overlap [-pe n f1..fn] [-se n f1..fn] -f prefix -l minOverlap [-k seedK] [-d device] [-nocontract | -raw | -s]\n");
 }
 
 int main(int argc, char** argv) {
@@ -29,7 +33,7 @@ int main(int argc, char** argv) {
   std::string prefix;
   unsigned long long l = 0;
   int k = 0, dev = 0;
-  bool raw = false, nocontract = false;
+  bool raw = false, nocontract = false, resume = false;
   for (int i = 1; i < argc; ++i) {
     std::string a = argv[i];
     if ((a == "-pe" || a == "-se") && i + 1 < argc) {
@@ -47,6 +51,8 @@ int main(int argc, char** argv) {
       raw = true;
     } else if (a == "-nocontract") {
       nocontract = true;
+    } else if (a == "-s") {
+      resume = true;
     } else {
       usage();
       return (a == "-h" || a == "--help") ? 0 : 1;
@@ -62,6 +68,20 @@ int main(int argc, char** argv) {
     OverlapGraph::replayExploration = !raw;
     OverlapGraph::contractPaths = !nocontract;
     Dataset* ds = new Dataset(pe, se, l);
+    if (resume) {  // main.cpp:36-42
+      OverlapGraph* g = new OverlapGraph();
+      g->setDataset(ds);
+      g->readGraphFromFile(prefix + ".unitig");
+      g->sortEdges();
+      g->saveGraphToFile(prefix + ".resumed.unitig");
+      g->saveGraphLists(prefix + ".resumed.graph");
+      std::printf("{\"unique_reads\": %llu, \"nodes\": %llu, \"directed_edges\": %llu}\n",
+                  (unsigned long long)ds->getNumberOfUniqueReads(), (unsigned long long)g->getNumberOfNodes(),
+                  (unsigned long long)g->getNumberOfEdges());
+      delete g;
+      delete ds;
+      return 0;
+    }
     HashTable* ht = new HashTable();
     ht->insertDataset(ds, l);
     OverlapGraph* g = new OverlapGraph(ht);  // deletes ht

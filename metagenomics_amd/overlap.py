@@ -120,6 +120,7 @@ def lib() -> C.CDLL:
         "mgh_parse_free": (None, [vp]),
         "mgh_parse_set_min_chunk": (None, [u64]),
         "mgh_graph_contract": (i32, [vp, i32, P(u64), P(u64), P(u64)]),
+        "mgh_graph_read_unitig": (i32, [C.c_char_p, vp, u64, P(vp)]),
         "mgh_graph_sort_edges": (i32, [vp]),
         "mgh_graph_save_unitig": (i32, [vp, C.c_char_p]),
         "mgh_graph_save_lists": (i32, [vp, C.c_char_p]),
@@ -573,6 +574,22 @@ class UnitigGraph:
             raise MgError(f"contraction failed ({rc})")
         self.replay_s, self.contract_s = t1 - t0, time.perf_counter() - t1
         self.iterations, self.merged, self.dead_end_nodes = it.value, merged.value, dead.value
+
+    @classmethod
+    def from_unitig_file(cls, path: str, lens: np.ndarray) -> "UnitigGraph":
+        """OverlapGraph::readGraphFromFile (OverlapGraph.cpp:1270-1367): the
+        .unitig checkpoint of a Dataset with these read lengths back into lists."""
+        lens = np.ascontiguousarray(lens, dtype=np.uint16)
+        self = cls.__new__(cls)
+        L = self._L = lib()
+        self._g = C.c_void_p()
+        rc = L.mgh_graph_read_unitig(os.fsencode(path), _ptr(lens), lens.shape[0], C.byref(self._g))
+        if rc:
+            raise MgError({-1: f"Unable to open file: {path}"}.get(rc, f"readGraphFromFile failed ({rc})"))
+        self.replay_s = self.contract_s = 0.0
+        self.replay_nodes = self.replay_edges = None
+        self.iterations = self.merged = self.dead_end_nodes = 0
+        return self
 
     @property
     def nodes(self) -> int:

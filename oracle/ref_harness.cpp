@@ -56,6 +56,11 @@
 //        "F|R <read> <src> <dst> <orient> <offset> <location>" rows; then
 //        sortEdges (:2799-2808) and saveGraphToFile (:1219-1261) into
 //        <out>.unitig (main.cpp:49-50).
+//   reread <fasta> <l> <out> <unitig> : main.cpp:36-42's resume from a
+//        .unitig checkpoint: OverlapGraph() -> setDataset -> readGraphFromFile
+//        (OverlapGraph.cpp:1270-1367); writes "#C", the lists and the read
+//        location lists as the unitig mode does, then sortEdges and
+//        saveGraphToFile into <out>.unitig.
 #define private public
 #include "Dataset.h"
 #include "HashTable.h"
@@ -304,6 +309,44 @@ int main(int argc, char** argv) {
     fprintf(out, "#C %llu %llu\n", (unsigned long long)og->numberOfNodes, (unsigned long long)og->numberOfEdges);
     fprintf(out, "#I %llu\n", (unsigned long long)iters);
     fprintf(out, "#T %.6f %.6f\n", t2 - t1, t3 - t2);
+    for (UINT64 u = 1; u <= N; u++) {
+      vector<Edge*>* lst = og->graph->at(u);
+      for (size_t k = 0; k < lst->size(); k++) {
+        Edge* e = lst->at(k);
+        fprintf(out, "%llu %llu %u %llu %llu", (unsigned long long)u,
+                (unsigned long long)e->getDestinationRead()->getReadNumber(), (unsigned)e->getOrientation(),
+                (unsigned long long)e->getOverlapOffset(), (unsigned long long)e->getListOfReads()->size());
+        for (size_t q = 0; q < e->getListOfReads()->size(); q++)
+          fprintf(out, " %llu:%u:%u", (unsigned long long)e->getListOfReads()->at(q),
+                  (unsigned)e->getListOfOverlapOffsets()->at(q), (unsigned)e->getListOfOrientations()->at(q));
+        fprintf(out, "\n");
+      }
+    }
+    for (UINT64 r = 1; r <= N; r++) {
+      Read* rd = ds->getReadFromID(r);
+      for (int side = 0; side < 2; side++) {
+        vector<Edge*>* le = side ? rd->getListOfEdgesReverse() : rd->getListOfEdgesForward();
+        vector<UINT64>* ll = side ? rd->getLocationOnEdgeReverse() : rd->getLocationOnEdgeForward();
+        for (size_t q = 0; q < le->size(); q++) {
+          Edge* e = le->at(q);
+          fprintf(out, "%c %llu %llu %llu %u %llu %llu\n", side ? 'R' : 'F', (unsigned long long)r,
+                  (unsigned long long)e->getSourceRead()->getReadNumber(),
+                  (unsigned long long)e->getDestinationRead()->getReadNumber(), (unsigned)e->getOrientation(),
+                  (unsigned long long)e->getOverlapOffset(), (unsigned long long)ll->at(q));
+        }
+      }
+    }
+    og->sortEdges();
+    og->saveGraphToFile(string(argv[4]) + ".unitig");
+  } else if (!strcmp(mode, "reread")) {
+    if (argc < 6) {
+      fprintf(stderr, "reread needs the .unitig file\n");
+      return 2;
+    }
+    OverlapGraph* og = new OverlapGraph();
+    og->setDataset(ds);
+    og->readGraphFromFile(string(argv[5]));
+    fprintf(out, "#C %llu %llu\n", (unsigned long long)og->numberOfNodes, (unsigned long long)og->numberOfEdges);
     for (UINT64 u = 1; u <= N; u++) {
       vector<Edge*>* lst = og->graph->at(u);
       for (size_t k = 0; k < lst->size(); k++) {

@@ -3,7 +3,11 @@
 tests/golden/{c2,c3,c5s}.json hold the digests (oracle/mg_digest.h) of the
 REFERENCE's own edge multiset and superReadID vector on the bench's exact
 workloads (tests/golden/make_scale_golden.py runs oracle/_ref/ref_harness
-digest on them in the build container).  The device computes the same digests
+digest on them in the build container).  tests/golden/c5.json (BASELINE
+configs[4], 50M reads: beyond the reference's reach in this container) is the
+oracle's (mgo_overlaps_digest over source-read ranges), which
+tests/golden/c5s_oracle_check.json shows reproducing the reference's own c5s
+digests.  The device computes the same digests
 (mg_rows_digest / mg_super_digest) without downloading 10^8 rows.  Three
 independent implementations of the digest (C in the harness and the oracle,
 numpy in tests/digest.py, HIP in the product) are checked against each other.
@@ -19,7 +23,7 @@ from conftest import FIXTURES, GOLDEN, fixture_input, golden_rows, load_meta
 from metagenomics_amd import synth
 from oracle import OracleDataset, rows_digest as oracle_rows_digest, super_digest as oracle_super_digest
 
-SCALE = {name: os.path.join(GOLDEN, name + ".json") for name in ("c2", "c3", "c5s")}
+SCALE = {name: os.path.join(GOLDEN, name + ".json") for name in ("c2", "c3", "c5s", "c5")}
 
 
 def super_array(meta, n):
@@ -125,8 +129,23 @@ def scale_dataset(name):
     return m, ds
 
 
+def test_c5_oracle_recipe_pinned_on_c5s():
+    """The threaded oracle recipe behind c5.json reproduced the reference's own
+    c5s digests (rows and superReadIDs) in the build container."""
+    chk = json.load(open(os.path.join(GOLDEN, "c5s_oracle_check.json")))
+    ref = json.load(open(SCALE["c5s"]))
+    assert chk["check"] is True
+    for k in ("n_unique", "n_reads", "rows", "super"):
+        assert chk["oracle"][k] == ref[k], k
+    c5 = json.load(open(SCALE["c5"]))
+    assert c5["recipe"] == chk["oracle"]["recipe"].replace(str(chk["oracle"]["threads"]) + " threads",
+                                                          str(c5["threads"]) + " threads")
+    assert c5["workload"]["reads"] == 50_000_000 and c5["super"]["n"] > 0
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize("name", ["c2", "c3", "c5s"])
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("name", ["c2", "c3", "c5s", "c5"])
 def test_scale_digest_matches_reference(name):
     """The bench's exact workloads (C2, C3 = the headline metric's config, and a
     C5-shaped metagenome with containment): the device's edge multiset and
@@ -146,3 +165,50 @@ def test_scale_digest_matches_reference(name):
         assert e.super_digest() == m["super"]
     finally:
         e.close()
+
+
+def combine(ds):
+    out = {"n": 0, "sum": 0, "xor": 0, "sum2": 0}
+    for d in ds:
+        out = {"n": out["n"] + d["n"], "sum": (out["sum"] + d["sum"]) % 2**64, "xor": out["xor"] ^ d["xor"],
+               "sum2": (out["sum2"] + d["sum2"]) % 2**64}
+    return out
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("name,world", [("c3", 8), ("c5s", 8)])
+def test_exchange_scale_digest(name, world):
+    """The multi-GPU exchange mode (bucket-range index shards,
+    key / run / row all-to-alls, MAX all-reduce of the containment keys) with
+    `world` simulated ranks on this GPU (LocalExchange moves the slot buffers):
+    C4's data path on the C3 workload, and containment through the exchange on
+    the C5-shaped set; the union of the ranks' rows has the reference's digest."""
+    import torch
+
+    from metagenomics_amd.overlap import OverlapEngine
+    from metagenomics_amd.sharded import LocalExchange, sharded_step, source_range
+
+    if not os.path.exists(SCALE[name]):
+        pytest.skip(f"{name}.json not generated")
+    m, ds = scale_dataset(name)
+    engines = []
+    try:
+        for r in range(world):
+            e = OverlapEngine(0)
+            e.set_shard(r, world, 0, 0)
+            e.upload(ds)
+            engines.append(e)
+        res = sharded_step(engines, LocalExchange(world, torch.device("cuda:0")), m["workload"]["min_overlap"], 31)
+        rd = combine([e.slots_digest(b.data_ptr(), slot, rounds, c.data_ptr())
+                      for e, (b, c, slot, rounds) in zip(engines, res.rows)])
+        assert rd == m["rows"]
+        assert engines[0].super_digest() == m["super"]
+        # each rank holds the rows of the sources it owns (by reference ID)
+        for r in range(world):
+            assert res.n_rows[r] > 0
+            lo, hi = source_range(ds.num_unique, r, world)
+            assert lo < hi
+    finally:
+        for e in engines:
+            e.close()

@@ -135,3 +135,70 @@ def test_c1_digest(tmp_path):
     g.sort_edges()
     g.save_unitig(str(tmp_path / "x.unitig"))
     assert hashlib.sha256((tmp_path / "x.unitig").read_bytes()).hexdigest() == u["unitig_sha256"]
+
+
+def reread_golden(name):
+    meta = load_meta(name)
+    with gzip.open(os.path.join(GOLDEN, meta["reread"]["file"]), "rt") as f:
+        return meta, f.read()
+
+
+@pytest.mark.parametrize("name", FIXTURES)
+def test_read_graph_from_file_matches_reference(name, tmp_path):
+    """readGraphFromFile (OverlapGraph.cpp:1270-1367): the committed .unitig
+    golden read back gives the reference's own lists (list order, composite
+    edges' read lists with the reverse edges' rebuilt offsets / orientations),
+    read locations and counters (tests/golden/make_reread_golden.py runs the
+    reference on the same file); sortEdges + saveGraphToFile then write the
+    reference's re-saved file."""
+    meta, text = reread_golden(name)
+    ds = Dataset.from_files([fixture_input(name)], meta["l"])
+    path = tmp_path / "in.unitig"
+    path.write_text(golden_text(name, "file"))
+    g = UnitigGraph.from_unitig_file(str(path), ds.packed()[1])
+    assert (g.nodes, g.edges) == (meta["reread"]["nodes"], meta["reread"]["edges"])
+    g.save_lists(str(tmp_path / "lists"))
+    assert (tmp_path / "lists").read_text() == text.split("\n", 1)[1]
+    g.sort_edges()
+    g.save_unitig(str(tmp_path / "out.unitig"))
+    want = golden_text(name, "file") if meta["reread"]["resave_identical"] else None
+    if want is None:
+        with gzip.open(os.path.join(GOLDEN, meta["reread"]["resaved_file"]), "rt") as f:
+            want = f.read()
+    assert (tmp_path / "out.unitig").read_text() == want
+    g.close()
+
+
+@pytest.mark.parametrize("name", ["branchy", "tandem", "small"])
+def test_cli_resume_from_unitig(name, tmp_path):
+    """main.cpp:36-42 (-s) through the C++ drop-in CLI, no device needed:
+    OverlapGraph() -> setDataset -> readGraphFromFile -> sortEdges -> the
+    re-saved checkpoint equals the reference's, the lists its lists."""
+    import subprocess
+
+    from conftest import ROOT
+
+    meta, text = reread_golden(name)
+    prefix = tmp_path / name
+    (tmp_path / f"{name}.unitig").write_text(golden_text(name, "file"))
+    exe = os.path.join(ROOT, "metagenomics_amd", "lib", "mg_overlap")
+    subprocess.run([exe, "-se", "1", fixture_input(name), "-f", str(prefix), "-l", str(meta["l"]), "-s"], check=True,
+                   stdout=subprocess.DEVNULL, timeout=120)
+    assert (tmp_path / f"{name}.resumed.unitig").read_text() == golden_text(name, "file")
+    got = (tmp_path / f"{name}.resumed.graph").read_text().split("\n")
+    assert got[0] == "#C %d %d" % (meta["reread"]["nodes"], meta["reread"]["edges"])
+
+
+def test_read_graph_from_file_errors(tmp_path):
+    meta = load_meta("small")
+    ds = Dataset.from_files([fixture_input("small")], meta["l"])
+    with pytest.raises(Exception, match="Unable to open"):
+        UnitigGraph.from_unitig_file(str(tmp_path / "missing.unitig"), ds.packed()[1])
+    bad = tmp_path / "bad.unitig"
+    bad.write_text("1\n999999\n3\n10\n0\n")  # a read ID past the Dataset (getReadFromID's range check)
+    with pytest.raises(Exception):
+        UnitigGraph.from_unitig_file(str(bad), ds.packed()[1])
+    empty = tmp_path / "empty.unitig"
+    empty.write_text("")
+    g = UnitigGraph.from_unitig_file(str(empty), ds.packed()[1])
+    assert (g.nodes, g.edges) == (0, 0)

@@ -13,7 +13,7 @@ mkdir -p $OUT
 for s in $STEPS; do
   case $s in
   tests)
-    timeout -k 10 900 python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread > $OUT/gpu_tests.log 2>&1
+    timeout -k 10 1150 python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread > $OUT/gpu_tests.log 2>&1
     rc=$?; echo "tests rc=$rc"; tail -3 $OUT/gpu_tests.log ;;
   smoke)
     timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1
@@ -42,7 +42,7 @@ for s in $STEPS; do
     timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -x -v -m gpu -k exchange --timeout 300 --timeout-method thread > $OUT/xchg_tests.log 2>&1
     rc=$?; echo "exchange tests rc=$rc"; grep -E "PASS|FAIL|Error" $OUT/xchg_tests.log | tail -20 ;;
   digest)
-    timeout -k 10 600 python -u -m pytest tests/test_scale_digest.py -x -v -m gpu --timeout 300 --timeout-method thread > $OUT/digest_tests.log 2>&1
+    timeout -k 10 1100 python -u -m pytest tests/test_scale_digest.py -x -v -m gpu --timeout 900 --timeout-method thread > $OUT/digest_tests.log 2>&1
     rc=$?; echo "digest tests rc=$rc"; grep -E "PASS|FAIL|SKIP|Error" $OUT/digest_tests.log | tail -12 ;;
   a2a)
     timeout -k 10 300 python -u tools/a2a_probe.py > $OUT/a2a_probe.log 2>&1
