@@ -48,7 +48,7 @@ struct mg_ctx {
   // layout scratch, kept between uploads so a re-upload allocates nothing:
   // sort keys / values (double buffers), the sort's temporary storage, and the
   // second slot array the gather writes (the two slot arrays swap)
-  uint32_t* d_lay_k[2] = {nullptr, nullptr};
+  uint64_t* d_lay_k[2] = {nullptr, nullptr};
   uint32_t* d_lay_v[2] = {nullptr, nullptr};
   size_t lay_k_cap[2] = {0, 0}, lay_v_cap[2] = {0, 0};
   void* d_lay_tmp = nullptr;

@@ -2111,47 +2111,59 @@ namespace {
 // (the smallest hash over its 16-mers and their reverse complements;
 // strand-independent) puts a read's overlap partners next to it in memory for
 // about half of its discoveries: the probe's partner slots and the shared
-// minimizer cells then come from L2 instead of HBM.  The key is 32 bits:
-// [group (2, only with a source-read range) | minimizer hash (HB) | its offset
-// (PB)], so each cluster is ordered along the genome and four 8-bit radix
-// passes sort it.  group = 0 / 1 / 2 for reference IDs below / inside / above
-// the range [lo, hi), so the range's reads take exactly the slots [lo, hi).
-// One thread per slot (old_id: the slot's reference ID - 1, nullptr = ID order).
+// minimizer cells then come from L2 instead of HBM.  The key is
+// [group (2, only with a source-read range) | minimizer hash (32) | its offset
+// (pb)], so each cluster is ordered along the genome; the radix sort runs over
+// those 32 + pb (+ 2) bits only.  A 22-bit hash (order_key) merged too many
+// clusters: C3 probe 4.9 vs 4.6 ms.  group = 0 / 1 / 2 for reference IDs
+// below / inside / above the range [lo, hi), so the range's reads take exactly
+// the slots [lo, hi).  One thread per slot (old_id: the slot's reference
+// ID - 1, nullptr = ID order).
+__device__ __forceinline__ uint32_t fmix32(uint32_t x) {  // murmur3 finaliser (bijective)
+  x ^= x >> 16;
+  x *= 0x85ebca6bu;
+  x ^= x >> 13;
+  x *= 0xc2b2ae35u;
+  x ^= x >> 16;
+  return x;
+}
+
 template <int MAXW>
 __global__ __launch_bounds__(kBlock) void k_layout_keys(const uint64_t* __restrict__ words,
                                                        const uint16_t* __restrict__ len, uint64_t n,
                                                        const uint32_t* __restrict__ old_id, uint64_t lo, uint64_t hi,
-                                                       int grouped, int pb, uint32_t* __restrict__ key,
+                                                       int grouped, int pb, uint64_t* __restrict__ key,
                                                        uint32_t* __restrict__ val) {
   const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
   if (i >= n) return;
   const int L = len[i];
+  using mer_t = uint32_t;  // (31-mers hashed by mix64: same probe time, layout 2.3 vs 1.85 ms at C3)
   constexpr int kM = 16;
   const int m = L < kM ? L : kM;
-  const uint32_t mmask = m == 16 ? 0xFFFFFFFFu : ((1u << (2 * m)) - 1u);
+  const mer_t mmask = 2 * m == 8 * (int)sizeof(mer_t) ? ~(mer_t)0 : (((mer_t)1 << (2 * m)) - 1);
   const uint64_t* g = words + i * slot_words(MAXW);
-  uint32_t fw = 0, rc = 0, best = 0xFFFFFFFFu, bpos = 0;
+  mer_t fw = 0, rc = 0;
+  uint32_t best = 0xFFFFFFFFu, bpos = 0;
   uint64_t cw = 0;
   for (int t = 0; t < L; ++t) {
     if ((t & 31) == 0) cw = g[t >> 5];
     const uint32_t b = (uint32_t)(cw >> (62 - 2 * (t & 31))) & 3u;
     fw = ((fw << 2) | b) & mmask;
-    rc = (rc >> 2) | ((3u - b) << (2 * m - 2));
+    rc = (rc >> 2) | ((mer_t)(3u - b) << (2 * m - 2));
     if (t >= m - 1) {
-      const uint32_t hv = order_key(fw < rc ? fw : rc) | (uint32_t)(t - m + 1 < 1023 ? t - m + 1 : 1023);
+      const uint32_t hv = fmix32(fw < rc ? fw : rc);
       if (hv < best) {  // the hash, leftmost on ties
         best = hv;
         bpos = (uint32_t)(t - m + 1);
       }
     }
   }
-  const int gb = grouped ? 2 : 0, hb = 32 - gb - pb;
   const uint32_t pmax = (1u << pb) - 1u;
-  uint32_t k = ((best >> (32 - hb)) << pb) | (bpos < pmax ? bpos : pmax);
+  uint64_t k = ((uint64_t)best << pb) | (bpos < pmax ? bpos : pmax);
   if (grouped) {
     const uint64_t id = old_id ? old_id[i] : i;
-    const uint32_t grp = id < lo ? 0u : id < hi ? 1u : 2u;
-    k |= grp << 30;
+    const uint64_t grp = id < lo ? 0u : id < hi ? 1u : 2u;
+    k |= grp << (32 + pb);
   }
   key[i] = k;
   val[i] = (uint32_t)i;
@@ -2199,7 +2211,7 @@ __global__ __launch_bounds__(kBlock) void k_unpermute_u32(const uint32_t* __rest
 
 template <int W>
 struct LaunchLayout {
-  static int run(mg_ctx* ctx, uint64_t lo, uint64_t hi, int grouped, int pb, uint32_t* key, uint32_t* val) {
+  static int run(mg_ctx* ctx, uint64_t lo, uint64_t hi, int grouped, int pb, uint64_t* key, uint32_t* val) {
     const uint64_t n = ctx->n;
     hipLaunchKernelGGL((k_layout_keys<W>), dim3((uint32_t)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, ctx->stream,
                        ctx->d_words, ctx->d_len, n, ctx->d_id, lo, hi, grouped, pb, key, val);
@@ -3329,9 +3341,10 @@ int layout_current(mg_ctx* ctx, bool force) {
     MG_TRY(ensure(&ctx->d_lay_k[b], &ctx->lay_k_cap[b], n));
     MG_TRY(ensure(&ctx->d_lay_v[b], &ctx->lay_v_cap[b], n));
   }
+  const unsigned kbits = 32u + (unsigned)pb + (grouped ? 2u : 0u);  // the key's significant bits
   size_t tb = 0;
   MG_TRY(rocprim::radix_sort_pairs(nullptr, tb, ctx->d_lay_k[0], ctx->d_lay_k[1], ctx->d_lay_v[0], ctx->d_lay_v[1],
-                                   (unsigned int)n, 0u, 32u, ctx->stream));
+                                   (unsigned int)n, 0u, kbits, ctx->stream));
   if (tb > ctx->lay_tmp_cap) {
     if (ctx->d_lay_tmp) MG_TRY(hipFree(ctx->d_lay_tmp));
     ctx->d_lay_tmp = nullptr;
@@ -3354,7 +3367,7 @@ int layout_current(mg_ctx* ctx, bool force) {
   if (dispatch_w<LaunchLayout>(ctx->maxw, ctx, lo, hi, grouped, pb, ctx->d_lay_k[0], ctx->d_lay_v[0]))
     return set_err(ctx, "layout key launch failed");
   MG_TRY(rocprim::radix_sort_pairs(ctx->d_lay_tmp, tb, ctx->d_lay_k[0], ctx->d_lay_k[1], ctx->d_lay_v[0],
-                                   ctx->d_lay_v[1], (unsigned int)n, 0u, 32u, ctx->stream));
+                                   ctx->d_lay_v[1], (unsigned int)n, 0u, kbits, ctx->stream));
   if (dispatch_w<LaunchLayoutGather>(ctx->maxw, ctx, ctx->d_lay_v[1], ctx->d_words_alt, ctx->d_len_alt, id_new))
     return set_err(ctx, "layout gather launch failed");
   // the zero pad past the last slot (over-reads of the kernels)

@@ -6,7 +6,7 @@ cd $GRAFT_REPO_ROOT
 TAG=${1:-ab}
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
-export MG_VARIANTS='[{}, {}, {}]'
+export MG_VARIANTS=${MG_VARIANTS:-'[{}, {}]'}
 for rep in 1 2; do
   for L in default metagenomics_amd/lib/variants/*.so; do
     if [ "$L" = default ]; then unset MG_LIB; else export MG_LIB=$PWD/$L; fi

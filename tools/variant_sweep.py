@@ -13,13 +13,15 @@ from metagenomics_amd.overlap import Dataset, OverlapEngine  # noqa: E402
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 10_000_000
 c, L = synth.uniform_read_set(n, 150, n * 150 // 20, seed=31)
 ds = Dataset.from_codes(c, L, 50, nthreads=16)
-VARIANTS = json.loads(os.environ["MG_VARIANTS"]) if os.environ.get("MG_VARIANTS") else [{"split": i % 2} for i in range(6)]
+VARIANTS = json.loads(os.environ["MG_VARIANTS"]) if os.environ.get("MG_VARIANTS") else [{}, {}]
 res = []
 for opts in VARIANTS:
     e = OverlapEngine(0)
     for k, v in opts.items():
         e.set_option(k, v)
     e.upload(ds)
+    e.upload(ds)  # the second upload: layout buffers and kernels warm
+    lay = e.timings()["layout_ms"]
     ts = []
     rows = 0
     for _ in range(6):
@@ -30,7 +32,7 @@ for opts in VARIANTS:
         ts.append((t["total_ms"], t["index_ms"], t["scan_ms"], t["probe_ms"], t["sort_ms"], t["verify_ms"]))
     e.close()
     best = min(ts[1:])
-    r = {"opts": opts, "rows": rows, "total_ms": round(best[0], 3), "index_ms": round(best[1], 3),
+    r = {"opts": opts, "rows": rows, "layout_ms": round(lay, 3), "total_ms": round(best[0], 3), "index_ms": round(best[1], 3),
          "scan_ms": round(best[2], 3), "probe_ms": round(best[3], 3), "sort_ms": round(best[4], 3), "verify_ms": round(best[5], 3)}
     res.append(r)
     print(json.dumps(r), flush=True)
