@@ -503,9 +503,17 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) voi
     const int J = n - h - 1;                 // windows j = 1 .. J (:534)
     const int tend = J >= 1 ? J + w - 1 : 0;  // last m-mer position a window uses
     int tmax = tend;
+    // INDEX: the keys' windows are t < w (o = 0, 3) and t >= n - h (o = 1, 2);
+    // t_tail = the wavefront's first t >= n - h, so the steps between the two
+    // (most of them) skip the key work behind a uniform branch
+    int t_tail = tend ? n - h : 0x7FFFFFFF;
 #pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) tmax = max(tmax, __shfl_xor(tmax, d));
+    for (int d = 32; d >= 1; d >>= 1) {
+      tmax = max(tmax, __shfl_xor(tmax, d));
+      if (INDEX) t_tail = min(t_tail, __shfl_xor(t_tail, d));
+    }
     tmax = __builtin_amdgcn_readfirstlane(tmax);  // wavefront-uniform loop bound
+    if (INDEX) t_tail = __builtin_amdgcn_readfirstlane(t_tail);
     // the read's words in registers (no global load inside the base loop); the
     // word holding base t + m is picked by a wavefront-uniform index
     constexpr int kRw = MAXW + 1 <= slot_words(MAXW) ? MAXW + 1 : slot_words(MAXW);
@@ -634,7 +642,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) voi
       if (t <= tend) {
         const uint32_t hk = order_key(mm);
         const uint32_t key = hk | (uint32_t)t;
-        if (INDEX) {
+        if (INDEX && (t < w || t >= t_tail)) {  // wavefront-uniform
+          // the reverse-strand m-mer is rolled only inside the key windows: at
+          // the tail's first step it is derived from the forward one
+          if (t == t_tail) rcm = rc_word(mm << msh) & mmask;
           const int i1 = t - (n - h);
           if (t < w && key < kb0) {  // o = 0, i = t
             kb0 = key;
@@ -716,7 +727,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) voi
     put(tend > 0, run_meta(a, last_pos, jlo, J));  // each read's last run
     while (nbuf) flush(nbuf < (uint32_t)kWave ? nbuf : (uint32_t)kWave);  // the group's runs leave with its registers
     if (INDEX && tend) {
-      // t = n-m, one past the last window position: the rolled m-mers sit there
+      // t = n-m, one past the last window position: the rolled m-mer sits there
+      // (the reverse one is derived: the lane's tail may have been cut short)
+      rcm = rc_word(mm << msh) & mmask;
       const uint32_t hk = order_key(mm), hr = order_key(rcm);
       if ((hk | (uint32_t)(w - 1)) < kb1) {
         kb1 = hk | (uint32_t)(w - 1);
@@ -738,7 +751,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) voi
           p.key_bk[o * p.key_n + a] = (uint32_t)(v & nbm);
           p.key_ent[o * p.key_n + a] = e;
         } else {
+#ifndef MG_X_NOCAS
           cell_insert(p.cells, v & nbm, p.cell_n, e);
+#else
+          if (e == 1) p.cells[0] = v;
+#endif
         }
       }
     } else if (INDEX && a < p.a_hi) {  // no keys (n <= l cannot pass setup_index): holes
@@ -2373,6 +2390,9 @@ inline void packable_runs(const mg_ctx* ctx, int* a, int* wb) {
 // Geometry of one discovery pass over source reads [a_lo, a_hi): probe grid =
 // its resident blocks; the scan (fewer registers) runs kreg times as many
 // wavefronts and probe wavefront r consumes scan regions r + i * (probe waves).
+#ifndef MG_X_NOIDX
+#define MG_X_NOIDX 0
+#endif
 struct DiscGeom {
   uint32_t grid = 0, sgrid = 0, kreg = 1;
   size_t lds_scan = 0, lds_probe = 0;
@@ -2499,7 +2519,7 @@ struct LaunchScan {
         allow_lds(k_scan_reg<W, false>, lds);
         hipLaunchKernelGGL((k_scan_reg<W, false>), dim3(sgrid), dim3(wpb * kWave), lds, stream, sp);
       }
-    } else if (index) {
+    } else if (index && !MG_X_NOIDX) {
       allow_lds(k_scan<W, true>, lds);
       hipLaunchKernelGGL((k_scan<W, true>), dim3(sgrid), dim3(wpb * kWave), lds, stream, sp);
     } else {

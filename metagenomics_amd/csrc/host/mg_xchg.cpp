@@ -1,0 +1,284 @@
+// mg_xchg.cpp — see mg_xchg.hpp.  The step mirrors metagenomics_amd/sharded.py
+// _step over the C-ABI of include/mg_overlap.h:
+//   mg_xchg_begin                          one window scan of this rank's sources
+//   mg_xchg_pack(KEYS) -> RCCL -> mg_xchg_insert_keys     HashTable::insertDataset
+//   mg_xchg_pack(RUNS) -> RCCL
+//   mg_begin_contained; [mg_xchg_probe(1); ncclAllReduce MAX]; mg_finalize_contained
+//                                                          markContainedReads
+//   mg_xchg_probe(0) -> mg_xchg_pack(ROWS) -> RCCL        insertAllEdgesOfRead
+// Every library call and every collective is enqueued on the context's HIP
+// stream (mg_stream); the step reads the host only for the run and row counts
+// inside the library and once at its end (the MAX over ranks of the send
+// counts, to detect a stream cut at its capacity).
+#include "mg_xchg.hpp"
+
+#include <arpa/inet.h>
+#include <netinet/in.h>
+#include <sys/socket.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstring>
+#include <stdexcept>
+#include <thread>
+
+namespace mg {
+
+namespace {
+constexpr size_t kChunkBytes = 256ull << 20;
+void nccl_check(ncclResult_t r, const char* what) {
+  if (r != ncclSuccess) throw std::runtime_error(std::string(what) + ": " + ncclGetErrorString(r));
+}
+void hip_check(hipError_t e, const char* what) {
+  if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+bool send_all(int fd, const void* p, size_t n) {
+  const char* c = static_cast<const char*>(p);
+  while (n) {
+    const ssize_t k = ::send(fd, c, n, 0);
+    if (k <= 0) return false;
+    c += k;
+    n -= (size_t)k;
+  }
+  return true;
+}
+bool recv_all(int fd, void* p, size_t n) {
+  char* c = static_cast<char*>(p);
+  while (n) {
+    const ssize_t k = ::recv(fd, c, n, 0);
+    if (k <= 0) return false;
+    c += k;
+    n -= (size_t)k;
+  }
+  return true;
+}
+
+// rank 0 creates the id and serves it to world - 1 connections
+ncclUniqueId rendezvous(int rank, int world, const std::string& addr, int port) {
+  ncclUniqueId id;
+  if (world == 1) {
+    nccl_check(ncclGetUniqueId(&id), "ncclGetUniqueId");
+    return id;
+  }
+  sockaddr_in sa{};
+  sa.sin_family = AF_INET;
+  sa.sin_port = htons((uint16_t)port);
+  if (inet_pton(AF_INET, addr.c_str(), &sa.sin_addr) != 1) throw std::runtime_error("bad MASTER_ADDR " + addr);
+  if (rank == 0) {
+    nccl_check(ncclGetUniqueId(&id), "ncclGetUniqueId");
+    const int fd = ::socket(AF_INET, SOCK_STREAM, 0);
+    const int one = 1;
+    ::setsockopt(fd, SOL_SOCKET, SO_REUSEADDR, &one, sizeof one);
+    if (::bind(fd, reinterpret_cast<sockaddr*>(&sa), sizeof sa) || ::listen(fd, world))
+      throw std::runtime_error("rendezvous: cannot listen on port " + std::to_string(port));
+    for (int i = 1; i < world; ++i) {
+      const int c = ::accept(fd, nullptr, nullptr);
+      if (c < 0 || !send_all(c, &id, sizeof id)) throw std::runtime_error("rendezvous: send failed");
+      ::close(c);
+    }
+    ::close(fd);
+    return id;
+  }
+  for (int attempt = 0; attempt < 600; ++attempt) {  // rank 0 may not listen yet: retry for 60 s
+    const int fd = ::socket(AF_INET, SOCK_STREAM, 0);
+    if (::connect(fd, reinterpret_cast<sockaddr*>(&sa), sizeof sa) == 0) {
+      const bool ok = recv_all(fd, &id, sizeof id);
+      ::close(fd);
+      if (!ok) throw std::runtime_error("rendezvous: receive failed");
+      return id;
+    }
+    ::close(fd);
+    std::this_thread::sleep_for(std::chrono::milliseconds(100));
+  }
+  throw std::runtime_error("rendezvous: rank 0 unreachable");
+}
+}  // namespace
+
+RcclExchange::RcclExchange(int rank, int world, int device, const std::string& addr, int port)
+    : rank_(rank), world_(world) {
+  hip_check(hipSetDevice(device), "hipSetDevice");
+  const ncclUniqueId id = rendezvous(rank, world, addr, port);
+  nccl_check(ncclCommInitRank(&comm_, world, id, rank), "ncclCommInitRank");
+}
+
+RcclExchange::~RcclExchange() {
+  if (flag_) (void)hipFree(flag_);
+  if (comm_) ncclCommDestroy(comm_);
+}
+
+void RcclExchange::all_to_all_slots(const uint8_t* send, uint8_t* recv, uint64_t sb, uint32_t rounds,
+                                    hipStream_t s) {
+  if (world_ == 1) return;
+  for (uint32_t t = 0; t < rounds; ++t) {  // one group of point-to-point transfers per round, none to itself
+    nccl_check(ncclGroupStart(), "ncclGroupStart");
+    for (int p = 0; p < world_; ++p) {
+      if (p == rank_) continue;
+      const uint64_t at = ((uint64_t)t * world_ + p) * sb;
+      nccl_check(ncclSend(send + at, sb, ncclUint8, p, comm_, s), "ncclSend");
+      nccl_check(ncclRecv(recv + at, sb, ncclUint8, p, comm_, s), "ncclRecv");
+    }
+    nccl_check(ncclGroupEnd(), "ncclGroupEnd");
+  }
+}
+
+void RcclExchange::all_to_all_u64(const uint64_t* send, uint64_t* recv, hipStream_t s) {
+  if (world_ == 1) {
+    hip_check(hipMemcpyAsync(recv, send, sizeof(uint64_t), hipMemcpyDeviceToDevice, s), "counts copy");
+    return;
+  }
+  nccl_check(ncclGroupStart(), "ncclGroupStart");
+  for (int p = 0; p < world_; ++p) {
+    nccl_check(ncclSend(send + p, 1, ncclUint64, p, comm_, s), "ncclSend");
+    nccl_check(ncclRecv(recv + p, 1, ncclUint64, p, comm_, s), "ncclRecv");
+  }
+  nccl_check(ncclGroupEnd(), "ncclGroupEnd");
+}
+
+void RcclExchange::allreduce_max_u64(uint64_t* buf, size_t n, hipStream_t s) {
+  if (world_ == 1) return;
+  const size_t step = kChunkBytes / sizeof(uint64_t);  // bounded payload per collective
+  for (size_t i = 0; i < n; i += step)
+    nccl_check(ncclAllReduce(buf + i, buf + i, std::min(step, n - i), ncclUint64, ncclMax, comm_, s), "ncclAllReduce");
+}
+
+void RcclExchange::allreduce_max_f64(double* buf, size_t n, hipStream_t s) {
+  if (world_ > 1) nccl_check(ncclAllReduce(buf, buf, n, ncclFloat64, ncclMax, comm_, s), "ncclAllReduce");
+}
+
+void RcclExchange::barrier(hipStream_t s) {
+  if (world_ > 1) {
+    if (!flag_) hip_check(hipMalloc(&flag_, sizeof(double)), "hipMalloc");
+    allreduce_max_f64(flag_, 1, s);
+  }
+  hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
+}
+
+void RcclExchange::allgather_u64(const uint64_t* send, uint64_t* recv, size_t n, hipStream_t s) {
+  if (world_ == 1) {
+    hip_check(hipMemcpyAsync(recv, send, n * sizeof(uint64_t), hipMemcpyDeviceToDevice, s), "allgather copy");
+    return;
+  }
+  nccl_check(ncclAllGather(send, recv, n, ncclUint64, comm_, s), "ncclAllGather");
+}
+
+void slot_geometry(uint64_t cap, int world, uint32_t rec, uint64_t chunk, uint64_t* slot, uint32_t* rounds) {
+  constexpr uint64_t kAlign = 64;  // the probe tiles a slot by its divisors
+  const uint64_t per_round = std::max<uint64_t>(kAlign, (chunk / ((uint64_t)world * rec)) / kAlign * kAlign);
+  const uint64_t want = std::max<uint64_t>(kAlign, (cap + kAlign - 1) / kAlign * kAlign);
+  *slot = std::min(want, per_round);
+  *rounds = (uint32_t)((want + *slot - 1) / *slot);
+}
+
+XchgStep::XchgStep(mg_ctx* ctx, RcclExchange& x, uint32_t l, uint32_t k, uint64_t chunk)
+    : ctx_(ctx), x_(x), l_(l), k_(k), chunk_(chunk), s_((hipStream_t)mg_stream(ctx)) {
+  check(mg_xchg_caps(ctx_, l_, k_, caps_), "mg_xchg_caps");
+}
+
+XchgStep::~XchgStep() {
+  for (Stream& st : st_)
+    for (void* p : {(void*)st.send, (void*)st.recv, (void*)st.counts, (void*)st.rcounts})
+      if (p) (void)hipFree(p);
+  if (superkey_) (void)hipFree(superkey_);
+  if (maxbuf_) (void)hipFree(maxbuf_);
+}
+
+void XchgStep::check(int rc, const char* what) {
+  if (rc) throw std::runtime_error(std::string(what) + ": " + mg_last_error(ctx_));
+}
+
+void XchgStep::ensure(Stream& st, int kind) {
+  const int P = x_.world();
+  slot_geometry(caps_[kind], P, mg_record_bytes(kind), chunk_, &st.slot, &st.rounds);
+  const size_t bytes = (size_t)st.rounds * P * st.slot * mg_record_bytes(kind);
+  if (bytes > st.bytes) {
+    for (uint8_t** p : {&st.send, &st.recv})
+      if (*p) hip_check(hipFree(*p), "hipFree");
+    st.send = st.recv = nullptr;
+    hip_check(hipMalloc(&st.recv, bytes), "hipMalloc");
+    if (P > 1) hip_check(hipMalloc(&st.send, bytes), "hipMalloc");
+    st.bytes = bytes;
+  }
+  if (!st.counts) {
+    hip_check(hipMalloc(&st.counts, P * sizeof(uint64_t)), "hipMalloc");
+    hip_check(hipMalloc(&st.rcounts, P * sizeof(uint64_t)), "hipMalloc");
+  }
+}
+
+void XchgStep::route(int kind) {
+  Stream& st = st_[kind];
+  ensure(st, kind);
+  check(mg_xchg_pack(ctx_, kind, st.send, st.slot, st.rounds, st.counts, st.recv), "mg_xchg_pack");
+  x_.all_to_all_slots(st.send, st.recv, st.slot * mg_record_bytes(kind), st.rounds, s_);
+  x_.all_to_all_u64(st.counts, st.rcounts, s_);
+}
+
+int XchgStep::run() {
+  const int P = x_.world();
+  for (int reruns = 0;; ++reruns) {
+    if (reruns > 3) throw std::runtime_error("exchange capacities still overflow after 3 reruns");
+    // 1. one scan of this rank's sources: index keys + bucket-sorted runs
+    check(mg_xchg_begin(ctx_, l_, k_), "mg_xchg_begin");
+    // 2. HashTable::insertDataset: keys -> bucket owners -> local cells
+    route(MG_KEYS);
+    const Stream& ks = st_[MG_KEYS];
+    check(mg_xchg_insert_keys(ctx_, ks.recv, ks.slot, ks.rounds, ks.rcounts), "mg_xchg_insert_keys");
+    // 3. runs -> bucket owners (both probes read them)
+    route(MG_RUNS);
+    const Stream& rs = st_[MG_RUNS];
+    // 4. markContainedReads (lengths differ, OverlapGraph.cpp:228-233): MAX of the keys over ranks
+    const uint64_t n = mg_num_reads(ctx_);
+    if (n > superkey_n_) {
+      if (superkey_) hip_check(hipFree(superkey_), "hipFree");
+      hip_check(hipMalloc(&superkey_, std::max<uint64_t>(n, 1) * sizeof(unsigned long long)), "hipMalloc");
+      superkey_n_ = n;
+    }
+    int needed = 0;
+    check(mg_begin_contained(ctx_, superkey_, &needed), "mg_begin_contained");
+    contained_ = needed != 0;
+    if (needed) {
+      check(mg_xchg_probe(ctx_, 1, rs.recv, rs.slot, rs.rounds, rs.rcounts), "mg_xchg_probe(contain)");
+      x_.allreduce_max_u64(reinterpret_cast<uint64_t*>(superkey_), n, s_);
+    }
+    check(mg_finalize_contained(ctx_, nullptr), "mg_finalize_contained");
+    // 5. insertAllEdgesOfRead: probe -> rows -> src owners
+    check(mg_xchg_probe(ctx_, 0, rs.recv, rs.slot, rs.rounds, rs.rcounts), "mg_xchg_probe");
+    route(MG_ROWS);
+    // the step's one host read: the MAX over ranks of every per-peer send count
+    std::vector<uint64_t> c(3 * P);
+    for (int kind = 0; kind < 3; ++kind)
+      hip_check(hipMemcpyAsync(c.data() + kind * P, st_[kind].counts, P * sizeof(uint64_t), hipMemcpyDeviceToHost, s_),
+                "counts D2H");
+    std::vector<uint64_t> rc(P);
+    hip_check(hipMemcpyAsync(rc.data(), st_[MG_ROWS].rcounts, P * sizeof(uint64_t), hipMemcpyDeviceToHost, s_),
+              "counts D2H");
+    hip_check(hipStreamSynchronize(s_), "hipStreamSynchronize");
+    uint64_t mx[3] = {0, 0, 0};
+    for (int kind = 0; kind < 3; ++kind)
+      for (int p = 0; p < P; ++p) mx[kind] = std::max(mx[kind], c[kind * P + p]);
+    if (!maxbuf_) hip_check(hipMalloc(&maxbuf_, sizeof mx), "hipMalloc");
+    uint64_t* dmx = maxbuf_;
+    hip_check(hipMemcpyAsync(dmx, mx, sizeof mx, hipMemcpyHostToDevice, s_), "max H2D");
+    x_.allreduce_max_u64(dmx, 3, s_);
+    hip_check(hipMemcpyAsync(mx, dmx, sizeof mx, hipMemcpyDeviceToHost, s_), "max D2H");
+    hip_check(hipStreamSynchronize(s_), "hipStreamSynchronize");
+    bool over = false;
+    for (int kind = 0; kind < 3; ++kind) {
+      if (mx[kind] > caps_[kind]) {
+        caps_[kind] = mx[kind] + mx[kind] * 15 / 100 + 64;
+        over = true;
+      }
+    }
+    rows_held_ = 0;
+    for (int p = 0; p < P; ++p) rows_held_ += rc[p];
+    if (!over) return reruns;
+  }
+}
+
+void XchgStep::rows_digest(uint64_t out[4]) {
+  const Stream& ws = st_[MG_ROWS];
+  check(mg_slots_digest(ctx_, ws.recv, ws.slot, ws.rounds, ws.rcounts, out), "mg_slots_digest");
+}
+
+}  // namespace mg

@@ -27,6 +27,7 @@ compare the device's digest with these numbers.
 usage: make_scale_golden.py NAME [NAME ...]            (reference; tens of minutes for c3)
        make_scale_golden.py --oracle [--threads T] NAME  (oracle, threaded)
        make_scale_golden.py --oracle --check NAME       (oracle vs the committed golden)
+       make_scale_golden.py --fasta NAME PATH           (only write the workload's FASTA)
 """
 from __future__ import annotations
 
@@ -120,6 +121,9 @@ def oracle_main(names, threads, check):
 
 
 def main():
+    if sys.argv[1:2] == ["--fasta"]:
+        codes, lens = make_codes(sys.argv[2])
+        return write_fasta_fast(sys.argv[3], codes, lens)
     if "--oracle" in sys.argv:
         args = [a for a in sys.argv[1:] if a != "--oracle"]
         check = "--check" in args

@@ -19,7 +19,7 @@ import numpy as np
 import pytest
 
 import digest
-from conftest import FIXTURES, GOLDEN, fixture_input, golden_rows, load_meta
+from conftest import FIXTURES, GOLDEN, ROOT, fixture_input, golden_rows, load_meta
 from metagenomics_amd import synth
 from oracle import OracleDataset, rows_digest as oracle_rows_digest, super_digest as oracle_super_digest
 
@@ -212,3 +212,35 @@ def test_exchange_scale_digest(name, world):
     finally:
         for e in engines:
             e.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("name,launcher", [("c3", "direct"), ("c5s", "torchrun")])
+def test_cli_exchange_over_rccl(name, launcher, tmp_path):
+    """The C++ host's exchange mode (mg_overlap -xchg, metagenomics_amd/csrc/host/
+    mg_xchg.cpp: collectives issued by C++ over RCCL on the library's stream) at
+    world 1 on the workload's FASTA: the reference's row and superReadID digests.
+    c5s goes through torchrun --no-python, the launcher of the N-GPU runs."""
+    import subprocess
+    import sys
+
+    if not os.path.exists(SCALE[name]):
+        pytest.skip(f"{name}.json not generated")
+    m = json.load(open(SCALE[name]))
+    fa = str(tmp_path / f"{name}.fa")
+    subprocess.run([sys.executable, os.path.join(GOLDEN, "make_scale_golden.py"), "--fasta", name, fa],
+                   check=True, timeout=600)
+    cli = os.path.join(ROOT, "metagenomics_amd", "lib", "mg_overlap")
+    args = [cli, "-se", "1", fa, "-f", str(tmp_path / "x"), "-l", str(m["workload"]["min_overlap"]), "-k", "31",
+            "-xchg", "3"]
+    if launcher == "torchrun":
+        args = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+                "--master-addr", "127.0.0.1", "--master-port", "29731", "--no-python"] + args
+    out = subprocess.run(args, capture_output=True, text=True, timeout=600)
+    assert out.returncode == 0, out.stderr[-3000:]
+    r = json.loads([x for x in out.stdout.splitlines() if x.startswith("{")][-1])
+    assert r["world"] == 1 and r["unique_reads"] == m["n_unique"]
+    assert r["rows"] == m["rows"]
+    assert r["super"] == m["super"]
+    assert r["contained"] == (m["super"]["n"] > 0)

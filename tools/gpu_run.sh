@@ -44,6 +44,22 @@ for s in $STEPS; do
   digest)
     timeout -k 10 1100 python -u -m pytest tests/test_scale_digest.py -x -v -m gpu --timeout 900 --timeout-method thread > $OUT/digest_tests.log 2>&1
     rc=$?; echo "digest tests rc=$rc"; grep -E "PASS|FAIL|SKIP|Error" $OUT/digest_tests.log | tail -12 ;;
+  parity)
+    timeout -k 10 900 python -u -m pytest tests/test_gpu_parity.py -x -q -m gpu --timeout 300 --timeout-method thread > $OUT/parity_tests.log 2>&1
+    rc=$?; echo "parity tests rc=$rc"; tail -3 $OUT/parity_tests.log ;;
+  c3digest)
+    timeout -k 10 900 python -u -m pytest tests/test_scale_digest.py -x -v -m gpu -k "c3 or c5s" --timeout 900 --timeout-method thread > $OUT/c3digest_tests.log 2>&1
+    rc=$?; echo "c3/c5s digest tests rc=$rc"; grep -E "PASS|FAIL|SKIP|Error" $OUT/c3digest_tests.log | tail -12 ;;
+  clixchg)
+    timeout -k 10 1000 python -u -m pytest tests/test_scale_digest.py -x -v -m gpu -k cli_exchange --timeout 900 --timeout-method thread > $OUT/clixchg_tests.log 2>&1
+    rc=$?; echo "cli exchange tests rc=$rc"; grep -E "PASS|FAIL|SKIP|Error|assert" $OUT/clixchg_tests.log | tail -12 ;;
+  profsim8)
+    # per-rank kernel tables of the exchange mode at P=8 (simulated ranks), C3 then C5
+    for C in c3 c5; do
+      timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/profsim8_$C -o kt -- python3 bench.py --config $C --sim-world 8 --multi exchange --steps 2 --no-cpu-baseline --no-ingest > $OUT/profsim8_${C}_bench.json 2> $OUT/profsim8_${C}_bench.err
+      rc=$?; echo "profsim8 $C rc=$rc"; [ $rc -ne 0 ] && break
+      python3 tools/rank_table.py $OUT/profsim8_$C/kt_kernel_stats.csv 8 4 "$C exchange-sim" | tee $OUT/profsim8_${C}_ranks.md | tail -14
+    done ;;
   a2a)
     timeout -k 10 300 python -u tools/a2a_probe.py > $OUT/a2a_probe.log 2>&1
     rc=$?; echo "a2a_probe rc=$rc"; grep MB $OUT/a2a_probe.log ;;

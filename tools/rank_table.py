@@ -1,0 +1,36 @@
+"""Per-rank kernel table of a simulated-world run (bench.py --sim-world P):
+the P simulated ranks' kernels all land in one rocprofv3 kernel_stats.csv, and
+every rank runs the same kernels on its own share, so a kernel's per-rank cost
+is its total duration / P, and per step / (P * S) for S step executions in the
+run (bench: 1 counting pass + warmup + steps).  Upload-time kernels (packing,
+layout) run once per rank and are divided by S all the same: read them as such.
+usage: rank_table.py kernel_stats.csv P S [title]"""
+import csv
+import re
+import sys
+
+
+def short(name: str) -> str:
+    name = re.sub(r"\(anonymous namespace\)::", "", name)
+    name = re.sub(r"rocprim::ROCPRIM_\w+::detail::", "rocprim::", name)
+    m = re.match(r"(?:void )?([\w:]+(?:<[^()]*?>)?)", name)
+    s = m.group(1) if m else name
+    return s[:90]
+
+
+def main():
+    path, P, S = sys.argv[1], int(sys.argv[2]), int(sys.argv[3])
+    title = sys.argv[4] if len(sys.argv) > 4 else path
+    rows = list(csv.DictReader(open(path)))
+    tot = sum(float(r["TotalDurationNs"]) for r in rows)
+    print(f"### {title}: kernel time per rank per step at P={P} (total / (P x {S}))\n")
+    print("| kernel | calls/rank/step | ms/rank/step | share |")
+    print("|---|---:|---:|---:|")
+    for r in sorted(rows, key=lambda r: -float(r["TotalDurationNs"])):
+        t = float(r["TotalDurationNs"])
+        print(f"| `{short(r['Name'])}` | {int(r['Calls']) / P / S:.2f} | {t / P / S / 1e6:.3f} | {100 * t / tot:.1f}% |")
+    print(f"| **all kernels** | | **{tot / P / S / 1e6:.3f}** | |")
+
+
+if __name__ == "__main__":
+    main()
