@@ -550,6 +550,10 @@ def main():
         "layout_ms": layout_ms,
         "phase_wall_ms": {kk: v / args.steps for kk, v in phase_ms.items()} or None,
         "exchange_reruns": reruns[0] if mode.startswith("exchange") else None,
+        # slot-layout padding: records moved between ranks vs records sent (rank 0's, or all
+        # simulated ranks'), from the last step's counts
+        "exchange_padding": (last_res[0].padding(P, [rank] if mode == "exchange" else list(range(P)))
+                             if mode.startswith("exchange") and last_res[0] is not None and P > 1 else None),
         "counters": cnt,
         "roofline": roof,
         "parity": parity,

@@ -53,7 +53,7 @@ typedef struct mg_timings {
   float verify_ms;      /* 0 (the probe verifies inline)                */
   float upload_ms;      /* H2D copy of raw reads (mg_ingest_*)        */
   float ingest_ms;      /* device Dataset ingest (mg_ingest_*)        */
-  float sort_ms;        /* exchange mode: runs ordered by bucket (grouped by owner); 0 otherwise */
+  float sort_ms;        /* always 0 (no run sort since the clustered layout; field kept for ABI) */
   float layout_ms;      /* device layout of the last upload / ingest (clustered slots, option "layout") */
 } mg_timings;
 
@@ -221,8 +221,9 @@ int mg_xchg_insert_keys(mg_ctx* ctx, const void* recv, uint64_t slot, uint32_t r
 /* Probe the received runs against the local cells: contain = 1 atomicMax-es
  * containment keys into the buffer of mg_begin_contained; contain = 0 verifies
  * overlaps (sources with superReadID != 0 give none) and keeps the rows
- * (+ twins) for mg_xchg_pack(MG_ROWS). */
-int mg_xchg_probe(mg_ctx* ctx, int contain, const void* recv, uint64_t slot, uint32_t rounds, const uint64_t* counts);
+ * (+ twins) for mg_xchg_pack(MG_ROWS).  With contained reads, contain = 0
+ * first drops their runs from recv IN PLACE (recv is not reusable after). */
+int mg_xchg_probe(mg_ctx* ctx, int contain, void* recv, uint64_t slot, uint32_t rounds, const uint64_t* counts);
 /* Containment: *needed = 1 when read lengths differ (OverlapGraph.cpp:228-233).
  * superkey = caller-owned device array of n_reads u64 (NULL: context-owned),
  * cleared here; the contain probe atomicMax-es (len << 32 | ~index) into it,
@@ -269,9 +270,8 @@ int mg_get_counters(const mg_ctx* ctx, mg_counters* c);
  *                   containment pruning, all exact, default 1;
  *  "probe_share"    a discovery block's 4 wavefronts share its run regions (default 1);
  *  "probe_compact"  sparse run batches are compacted in the probe (default 1);
- *  "xchg_sort_bits" exchange mode with P a power of two: runs sorted on the top
- *                   bucket bits only (default 8; 0 = all);
- *  "flat_cap"       tests: initial capacity of the exchange scan's run arrays;
+ *  "run_cap"        tests: initial run records per scan region (0 = sized from
+ *                   the reads; overflowing regions are resized and rescanned);
  *  "phase_limit", "max_blocks"
  *                   diagnostics: stop the probe after a phase / cap its grid. */
 int mg_set_option(mg_ctx* ctx, const char* name, int64_t value);

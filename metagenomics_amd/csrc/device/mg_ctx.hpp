@@ -95,14 +95,14 @@ struct mg_ctx {
   uint64_t nrun_reg = 0;       // run regions (one per scan wavefront)
   ulonglong2* d_runs = nullptr;  // run records, one region per wavefront
   size_t runs_cap = 0;
-  uint64_t run_cap = 0, run_cap_need = 0;
+  uint64_t run_cap = 0, run_cap_need = 0, run_cap_opt = 0;  // run_cap_opt: option "run_cap" (tests)
   unsigned long long* d_run_cnt = nullptr;
   size_t run_cnt_cap = 0;
   std::vector<unsigned long long> run_cnt_host;
   uint32_t* d_compact = nullptr;
   size_t compact_cap = 0;
   // exchange mode (one process per GPU): mg_xchg_begin's scan
-  // leaves key records (d_kb / d_ke) and bucket-sorted runs of this rank's
+  // leaves key records (d_kb / d_ke) and the run regions of this rank's
   // sources; packable = bit mask of what mg_xchg_pack can route now
   bool xchg = false;                     // the context's current build is an exchange-mode build
   uint64_t xchg_lo = 0, xchg_hi = 0;     // its source reads
@@ -116,31 +116,12 @@ struct mg_ctx {
   uint32_t* d_kb = nullptr;  // key records: bucket / index entry, key o of read a at o * n + a
   uint64_t* d_ke = nullptr;
   size_t kb_cap = 0, ke_cap = 0;
-  // the exchange scan's runs as flat SoA arrays (double buffers of the bucket
-  // sort): chunks of kFlatChunk records claimed from kFlatCounters cursors
-  bool scan_flat = false;
-  uint64_t* d_sk[2] = {nullptr, nullptr};
-  uint64_t* d_sm[2] = {nullptr, nullptr};
-  size_t sk_cap = 0;
-  int sk_sel = 0;  // which buffer holds the sorted result
-  void* d_sort_tmp = nullptr;
-  size_t sort_tmp_cap = 0;
-  uint64_t n_sorted = 0;
-  unsigned long long* d_flat_cursor = nullptr;
-  uint64_t flat_need = 0, n_flat = 0;
-  uint64_t* d_holes = nullptr;  // chunk ids of the flat arrays no counter reached (k_fill_holes)
-  size_t holes_cap = 0;
-  std::vector<uint64_t> holes_host;
-  uint64_t flat_cap_opt = 0;  // option "flat_cap" (tests: force the overflow rerun)
-  int pack_a = 0, pack_w = 0;  // packing of the current flat runs (0: 16-B records)
-  int xchg_sort_bits = 8;  // option "xchg_sort_bits": P a power of two: runs sorted on the top bits only
-  unsigned long long* d_bnd = nullptr;  // per-destination bounds of the sorted runs
-  size_t bnd_cap = 0;
   // timing
   hipEvent_t ev[16] = {};  // [14], [15]: apply_layout
   // unsharded contexts build the index inside the window scan (k_scan<INDEX>);
   // its runs then serve the containment and the discovery probes
   int scan_state = 0;        // 0 none, 1 launched (not settled), 2 settled
+  bool runs_live = false;    // the run regions hold only runs of uncontained sources (k_live_runs)
   bool probe_share = true;     // option "probe_share": a discovery-probe block's 4 wavefronts share its regions
   bool probe_compact = true;   // option "probe_compact": sparse run batches compacted in the probe (C5 probe 30.4 -> 26.8 ms)
   // prefix containments (k_prefix_contain): each read's o = 0 key (bucket,
@@ -148,6 +129,13 @@ struct mg_ctx {
   // the containment probe skips suffix-key hits (containment)
   uint64_t* d_key0 = nullptr;
   size_t key0_cap = 0;
+  // exchange mode, mixed lengths: the o = 0 key records this rank filed
+  // (k_insert_slots), walked by k_prefix_contain_rec before the containment
+  // probe, which then drops o = 1/3 hits like the fused path (xchg_prefix)
+  ulonglong2* d_k0rec = nullptr;
+  size_t k0rec_cap = 0;
+  unsigned long long* d_k0n = nullptr;
+  bool xchg_prefix = false;
   bool key0_ready = false;
   bool prefix_contain = true;  // option "prefix_contain"
   bool contain_jcut = true;    // option "contain_jcut": containment probe drops runs with jlo > n1 - minlen (C5: 60 -> 47 ms)

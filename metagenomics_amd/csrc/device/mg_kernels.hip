@@ -152,9 +152,7 @@ constexpr int kStageRing = 512;   // register scan: LDS ring of staged run metas
 constexpr uint64_t kEmpty = ~0ULL;       // free slot (a read index is never 0xFFFFFFFF)
 constexpr uint64_t kChain = 1ULL << 63;  // on a cell's last slot: the chain continues in the next cell
 constexpr uint32_t kFpMask = (1u << kFpBits) - 1;
-constexpr uint64_t kFlatChunk = 512;   // flat scan output: records per wavefront chunk
-constexpr uint32_t kFlatCounters = 8;  // chunk counters (one per XCD: one counter serialised at 0.2 ms)
-constexpr uint64_t kFlatHole = ~0ULL;  // meta of an unused flat slot (a run meta never has bit 63)
+constexpr uint64_t kFlatHole = ~0ULL;  // meta of a dead run record (a run meta never has bit 63)
 
 struct IndexParams {
   const uint64_t* words;
@@ -292,23 +290,19 @@ __global__ __launch_bounds__(kBlock) void k_index_build(IndexParams p) {
 // fingerprint and offset q, a shorter read2 and F1[0, n2) == F2 (o = 0) or R2
 // (o = 2) -> the same atomicMax as the probe.  With this kernel the
 // containment probe drops all o = 1/3 hits (ProbeParams::contain_even).
+// read1 = slot a with its o = 0 key filed at local cell c (fingerprint fp,
+// offset q): walk the chain for shorter reads whose o = 0/2 key is the same
+// string at the same offset, compare the whole of read2 (or its reverse
+// strand) with F1[0, n2), atomicMax the container key into read2's superkey
 template <int MAXW>
-__global__ __launch_bounds__(kBlock) void k_prefix_contain(const uint64_t* __restrict__ words,
-                                                           const uint16_t* __restrict__ len,
-                                                           const uint64_t* __restrict__ key0,
-                                                           const uint64_t* __restrict__ cells, uint64_t cell_n,
-                                                           uint32_t nb_log2, uint64_t n,
-                                                           unsigned long long* __restrict__ superkey,
-                                                           const uint32_t* __restrict__ id) {
-  const uint64_t a = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (a >= n) return;
-  const uint64_t k0 = key0[a];
-  if (k0 == kEmpty) return;
+__device__ __forceinline__ void prefix_contain_walk(const uint64_t* __restrict__ words,
+                                                    const uint16_t* __restrict__ len,
+                                                    const uint64_t* __restrict__ cells, uint64_t cell_n, uint64_t c,
+                                                    uint32_t a, uint32_t fp, uint32_t q,
+                                                    unsigned long long* __restrict__ superkey,
+                                                    const uint32_t* __restrict__ id) {
   const int n1 = len[a];
-  const uint32_t fp = (uint32_t)(k0 >> nb_log2) & kFpMask;
-  const uint32_t q = (uint32_t)(k0 >> 54);
-  const uint64_t* f1 = words + a * slot_words(MAXW);
-  uint64_t c = k0 & ((1ULL << nb_log2) - 1);
+  const uint64_t* f1 = words + (uint64_t)a * slot_words(MAXW);
   for (uint64_t probe = 0; probe < cell_n; ++probe) {
     const ulonglong2* cp = reinterpret_cast<const ulonglong2*>(cells + c * kCell);
     uint64_t e[kCell];
@@ -322,7 +316,7 @@ __global__ __launch_bounds__(kBlock) void k_prefix_contain(const uint64_t* __res
       if (e[s] == kEmpty) continue;
       const uint32_t hi = (uint32_t)(e[s] >> 32), r2 = (uint32_t)e[s];
       const int o = (int)(hi & 3u);
-      if ((o & 1) || r2 == (uint32_t)a || ((hi >> 12) & kFpMask) != fp || ((hi >> 2) & 1023u) != q) continue;
+      if ((o & 1) || r2 == a || ((hi >> 12) & kFpMask) != fp || ((hi >> 2) & 1023u) != q) continue;
       const int n2 = len[r2];
       if (n2 >= n1) continue;
       const uint64_t* f2 = words + (uint64_t)r2 * slot_words(MAXW);
@@ -332,12 +326,58 @@ __global__ __launch_bounds__(kBlock) void k_prefix_contain(const uint64_t* __res
         const int rem = n2 - 32 * k;
         diff |= (f1[k] ^ bv) & (rem >= 32 ? ~0ULL : ~(~0ULL >> (2 * rem)));
       }
-      if (!diff) atomicMax(&superkey[r2], ((unsigned long long)n1 << 32) | (0xFFFFFFFFu - rid(id, (uint32_t)a)));
+      if (!diff) atomicMax(&superkey[r2], ((unsigned long long)n1 << 32) | (0xFFFFFFFFu - rid(id, a)));
     }
     if (e[kCell - 1] == kEmpty || !(e[kCell - 1] & kChain)) break;
     c = next_cell(c, cell_n, fp);
   }
 }
+
+template <int MAXW>
+__global__ __launch_bounds__(kBlock) void k_prefix_contain(const uint64_t* __restrict__ words,
+                                                           const uint16_t* __restrict__ len,
+                                                           const uint64_t* __restrict__ key0,
+                                                           const uint64_t* __restrict__ cells, uint64_t cell_n,
+                                                           uint32_t nb_log2, uint64_t n,
+                                                           unsigned long long* __restrict__ superkey,
+                                                           const uint32_t* __restrict__ id) {
+  const uint64_t a = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (a >= n) return;
+  const uint64_t k0 = key0[a];
+  if (k0 == kEmpty) return;
+  prefix_contain_walk<MAXW>(words, len, cells, cell_n, k0 & ((1ULL << nb_log2) - 1), (uint32_t)a,
+                            (uint32_t)(k0 >> nb_log2) & kFpMask, (uint32_t)(k0 >> 54), superkey, id);
+}
+
+// Exchange mode: the same walk from the o = 0 key records this rank filed
+// (k_insert_slots kept them: x = bucket, y = entry), over its own cells
+template <int MAXW>
+__global__ __launch_bounds__(kBlock) void k_prefix_contain_rec(const uint64_t* __restrict__ words,
+                                                               const uint16_t* __restrict__ len,
+                                                               const ulonglong2* __restrict__ rec,
+                                                               const unsigned long long* __restrict__ nrec,
+                                                               const uint64_t* __restrict__ cells, uint64_t cell_lo,
+                                                               uint64_t cell_n, unsigned long long* __restrict__ superkey,
+                                                               const uint32_t* __restrict__ id) {
+  const uint64_t nr = *nrec;
+  for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < nr; i += (uint64_t)gridDim.x * kBlock) {
+    const ulonglong2 x = rec[i];
+    const uint32_t hi = (uint32_t)(x.y >> 32);
+    prefix_contain_walk<MAXW>(words, len, cells, cell_n, x.x - cell_lo, (uint32_t)x.y, (hi >> 12) & kFpMask,
+                              (hi >> 2) & 1023u, superkey, id);
+  }
+}
+
+template <int W>
+struct LaunchPrefixContainRec {
+  static int run(mg_ctx* ctx) {
+    const uint32_t grid = (uint32_t)std::max<uint64_t>(
+        1, std::min<uint64_t>((ctx->n + kBlock - 1) / kBlock, (uint64_t)ctx->n_cu * 16));
+    hipLaunchKernelGGL(k_prefix_contain_rec<W>, dim3(grid), dim3(kBlock), 0, ctx->stream, ctx->d_words, ctx->d_len,
+                       ctx->d_k0rec, ctx->d_k0n, ctx->d_cells, ctx->cell_lo, ctx->cell_n, ctx->superkey, ctx->d_id);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+  }
+};
 
 template <int W>
 struct LaunchPrefixContain {
@@ -353,16 +393,39 @@ struct LaunchPrefixContain {
 // Exchange mode: file the key records this rank received, in the slot layout
 // of include/mg_overlap.h (record i of peer s at ((i / slot) P + s) slot +
 // i % slot, present while i < counts[s]); x = bucket, y = index entry.
+// Neighbouring records are keys of neighbouring (clustered) reads and often
+// share a minimizer cell, so the lanes of a wavefront take records 64 apart
+// (a 64 x 64 transpose of each 4096-record tile): CAS on one cell from many
+// lanes at once retries serially.
+// k0out (mixed lengths): the o = 0 records are also kept for k_prefix_contain_rec.
 __global__ __launch_bounds__(kBlock) void k_insert_slots(IndexParams p, const ulonglong2* __restrict__ rec,
                                                          uint64_t slot, uint32_t rounds,
-                                                         const unsigned long long* __restrict__ counts) {
+                                                         const unsigned long long* __restrict__ counts,
+                                                         ulonglong2* __restrict__ k0out,
+                                                         unsigned long long* __restrict__ k0n) {
   const uint64_t P = p.nranks, blk = P * slot, total = (uint64_t)rounds * blk;
-  for (uint64_t idx = (uint64_t)blockIdx.x * kBlock + threadIdx.x; idx < total; idx += (uint64_t)gridDim.x * kBlock) {
+  const uint64_t tiles_end = total & ~(uint64_t)(kWave * kWave - 1);  // whole 4096-record tiles
+  for (uint64_t j = (uint64_t)blockIdx.x * kBlock + threadIdx.x; j < total; j += (uint64_t)gridDim.x * kBlock) {
+    const uint64_t u = j & (kWave * kWave - 1);
+    const uint64_t idx = j < tiles_end ? (j - u) + (u & (kWave - 1)) * kWave + (u >> 6) : j;
     const uint64_t t = idx / blk, rem = idx - t * blk, s = rem / slot;
-    if (t * slot + (rem - s * slot) >= counts[s]) continue;
-    const ulonglong2 x = rec[idx];
-    const uint64_t c = x.x - p.cell_lo;
-    if (c < p.cell_n) cell_insert(p.cells, c, p.cell_n, x.y);
+    bool k0 = false;
+    ulonglong2 x = make_ulonglong2(0, 0);
+    if (t * slot + (rem - s * slot) < counts[s]) {
+      x = rec[idx];
+      const uint64_t c = x.x - p.cell_lo;
+      if (c < p.cell_n) {
+        cell_insert(p.cells, c, p.cell_n, x.y);
+        k0 = k0out && ((x.y >> 32) & 3u) == 0;
+      }
+    }
+    if (k0out) {  // wavefront-aggregated append (every lane of the wavefront reaches here)
+      const uint64_t bal = __ballot(k0);
+      unsigned long long base = 0;
+      if ((threadIdx.x & 63) == 0 && bal) base = atomicAdd(k0n, (unsigned long long)__popcll(bal));
+      base = __shfl(base, 0);
+      if (k0) k0out[base + lane_prefix(bal)] = x;
+    }
   }
 }
 
@@ -385,13 +448,6 @@ struct ScanParams {
   uint64_t run_cap;
   uint64_t* cells;                // k_scan<INDEX>: the (unsharded) cell table the keys go into
   uint64_t cell_n;
-  // flat SoA output (exchange mode: the bucket sort's input): x / meta arrays
-  // filled in chunks claimed from kFlatCounters cursors; regions are not written
-  uint64_t* flat_keys;
-  uint64_t* flat_meta;
-  unsigned long long* flat_cursor;
-  uint64_t flat_cap;
-  int pack_a, pack_w;  // pack_a > 0: 12-B records (run_pack_key / run_pack_meta) instead of 16-B
   // exchange mode: the four key records of read a go to key_bk / key_ent[o *
   // key_n + a] (bucket, entry) instead of a CAS into the cells; they travel to
   // the bucket owner (k_part) and k_insert_slots files them there
@@ -402,34 +458,6 @@ struct ScanParams {
   // (k_prefix_contain); nullptr: not written
   uint64_t* key0;
 };
-
-// Sort records of 12 B instead of 16 (exchange mode's bucket sort, when the
-// widths fit: packable_runs): key32 = bucket | low (32 - nb) fingerprint bits; meta64 =
-// read (A bits) | jlo (10) | jhi - jlo (WB) | p - jhi (WB) | high fingerprint
-// bits.  A run's minimizer lies in all its windows, so p - jhi and jhi - jlo
-// are both < w.  A = bit width of the read count, so a read index is never all
-// ones and an all-ones meta stays free for holes.
-__device__ __forceinline__ uint32_t run_pack_key(uint64_t v, uint32_t nb) {
-  const uint32_t fp = (uint32_t)(v >> nb) & kFpMask;
-  return (uint32_t)(v & ((1ULL << nb) - 1)) | (fp << nb);
-}
-__device__ __forceinline__ uint64_t run_pack_meta(uint64_t meta, uint64_t v, uint32_t nb, int a, int wb) {
-  const uint64_t ra = meta & 0xFFFFFFFFull, pos = (meta >> 32) & 1023u, jlo = (meta >> 42) & 1023u,
-                 jhi = (meta >> 52) & 1023u;
-  const uint64_t fph = (uint64_t)(((uint32_t)(v >> nb) & kFpMask) >> (32 - nb));
-  return ra | (jlo << a) | ((jhi - jlo) << (a + 10)) | ((pos - jhi) << (a + 10 + wb)) | (fph << (a + 10 + 2 * wb));
-}
-// back to the bucket, fingerprint and 64-bit run meta the probe works on
-__device__ __forceinline__ void run_unpack(uint32_t k32, uint64_t m, uint32_t nb, int a, int wb, uint64_t* bucket,
-                                           uint32_t* fp, uint64_t* meta) {
-  const uint64_t amask = (1ULL << a) - 1, wmask = (1ULL << wb) - 1;
-  const uint64_t ra = m & amask, jlo = (m >> a) & 1023u, djh = (m >> (a + 10)) & wmask,
-                 dp = (m >> (a + 10 + wb)) & wmask, fph = m >> (a + 10 + 2 * wb);
-  const uint64_t jhi = jlo + djh, pos = jhi + dp;
-  *bucket = k32 & (uint32_t)((1ULL << nb) - 1);
-  *fp = ((k32 >> nb) | (uint32_t)(fph << (32 - nb))) & kFpMask;
-  *meta = ra | (pos << 32) | (jlo << 42) | (jhi << 52);
-}
 
 __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -483,7 +511,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) voi
   const uint64_t nbmask = (1ULL << p.nb_log2) - 1;
   uint64_t cursor = 0;
   uint32_t nbuf = 0;  // run metas staged in s_buf (wavefront-uniform)
-  uint64_t fbase = 0, fused = 0, fcap = 0;  // flat output: current chunk, records used, chunk size
 
   // close the run of minimizer position pos over windows [jlo, jhi]: stage its
   // meta in LDS (the hashing and the HBM write happen 64 at a time in flush)
@@ -568,39 +595,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) voi
         flag = owned(v & nbmask, p.nb_log2, p.rank, p.nranks);
       }
       const uint64_t bal = __ballot(flag);
-      if (p.flat_keys) {
-        // this wavefront's current chunk of the flat arrays; a new chunk (one
-        // atomic per kFlatChunk records: a cursor bumped per flush serialised at
-        // 20 ms) takes whatever does not fit in the current one
-        const uint64_t npop = (uint64_t)__popcll(bal);
-        const uint64_t room = fcap - fused;
-        unsigned long long nbase = 0;
-        if (npop > room) {  // chunk ids x, x + 8, x + 16, ... belong to counter x = blockIdx % 8
-          const uint32_t x = blockIdx.x & (kFlatCounters - 1);
-          if (lane == 0) nbase = (atomicAdd(&p.flat_cursor[x], 1ull) * kFlatCounters + x) * kFlatChunk;
-          nbase = __shfl(nbase, 0);
-        }
-        if (flag) {
-          const uint64_t pr = lane_prefix(bal);
-          const uint64_t at = pr < room ? fbase + fused + pr : nbase + (pr - room);
-          if (at < p.flat_cap) {
-            if (p.pack_a) {
-              reinterpret_cast<uint32_t*>(p.flat_keys)[at] = run_pack_key(v, p.nb_log2);
-              p.flat_meta[at] = run_pack_meta(meta, v, p.nb_log2, p.pack_a, p.pack_w);
-            } else {
-              p.flat_keys[at] = v;
-              p.flat_meta[at] = meta;
-            }
-          }
-        }
-        if (npop > room) {
-          fbase = nbase;
-          fused = npop - room;
-          fcap = kFlatChunk;
-        } else {
-          fused += npop;
-        }
-      } else if (flag) {
+      if (flag) {
         const uint64_t at = cursor + lane_prefix(bal);
         if (at < p.run_cap) region[at] = make_ulonglong2(v, meta);
       }
@@ -751,11 +746,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) voi
           p.key_bk[o * p.key_n + a] = (uint32_t)(v & nbm);
           p.key_ent[o * p.key_n + a] = e;
         } else {
-#ifndef MG_X_NOCAS
           cell_insert(p.cells, v & nbm, p.cell_n, e);
-#else
-          if (e == 1) p.cells[0] = v;
-#endif
         }
       }
     } else if (INDEX && a < p.a_hi) {  // no keys (n <= l cannot pass setup_index): holes
@@ -768,18 +759,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) voi
       }
     }
   }
-  if (p.flat_keys) {  // the unused tail of the last chunk: records the probe skips
-    for (uint64_t i = fused + lane; i < fcap; i += kWave) {
-      const uint64_t at = fbase + i;
-      if (at < p.flat_cap) {
-        if (p.pack_a)
-          reinterpret_cast<uint32_t*>(p.flat_keys)[at] = 0xFFFFFFFFu;
-        else
-          p.flat_keys[at] = kEmpty;
-        p.flat_meta[at] = kFlatHole;
-      }
-    }
-  }
   if (lane == 0) p.run_cnt[gw] = cursor;
 }
 
@@ -788,9 +767,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) voi
 // metas (ballot + mbcnt), then flushed 64 at a time with every lane busy: the
 // minimizer m-mer is re-extracted from the owner lane's registers
 // (ds_bpermute), hashed (mix64 -> bucket | fingerprint) and written as one
-// coalesced record per lane, either into this wavefront's region (16-B
-// records) or into the flat SoA arrays of the bucket sort (chunks of
-// kFlatChunk records claimed from kFlatCounters counters).
+// coalesced 16-B record per lane into this wavefront's region.
 template <int MAXW, int RING = kStageRing, bool FROM_MEM = false>
 struct RunStage {
   const ScanParams& p;
@@ -799,8 +776,7 @@ struct RunStage {
   int lane, msh;
   uint64_t nbmask;
   uint64_t cursor = 0;
-  uint32_t head = 0, nbuf = 0;              // staged metas: ring [head, head + nbuf) (wavefront-uniform)
-  uint64_t fbase = 0, fused = 0, fcap = 0;  // flat output: chunk base, used, size
+  uint32_t head = 0, nbuf = 0;  // staged metas: ring [head, head + nbuf) (wavefront-uniform)
 
   __device__ RunStage(const ScanParams& pp, uint64_t* buf, ulonglong2* reg, int ln)
       : p(pp), s_buf(buf), region(reg), lane(ln), msh(64 - 2 * pp.m), nbmask((1ULL << pp.nb_log2) - 1) {}
@@ -838,30 +814,7 @@ struct RunStage {
     }
     if (flag) flag = owned(v & nbmask, p.nb_log2, p.rank, p.nranks);
     const uint64_t bal = __ballot(flag);
-    if (p.flat_keys) {
-      const uint64_t npop = (uint64_t)__popcll(bal);
-      const uint64_t room = fcap - fused;
-      unsigned long long nbase = 0;
-      if (npop > room) {  // chunk ids x, x + 8, ... belong to counter x = blockIdx % 8
-        const uint32_t x = blockIdx.x & (kFlatCounters - 1);
-        if (lane == 0) nbase = (atomicAdd(&p.flat_cursor[x], 1ull) * kFlatCounters + x) * kFlatChunk;
-        nbase = __shfl(nbase, 0);
-      }
-      if (flag) {
-        const uint64_t pr = lane_prefix(bal);
-        const uint64_t at = pr < room ? fbase + fused + pr : nbase + (pr - room);
-        if (at < p.flat_cap) {
-          if (p.pack_a) {
-            reinterpret_cast<uint32_t*>(p.flat_keys)[at] = run_pack_key(v, p.nb_log2);
-            p.flat_meta[at] = run_pack_meta(meta, v, p.nb_log2, p.pack_a, p.pack_w);
-          } else {
-            p.flat_keys[at] = v;
-            p.flat_meta[at] = meta;
-          }
-        }
-      }
-      advance(npop, room, nbase);
-    } else if (flag) {
+    if (flag) {
       const uint64_t at = cursor + lane_prefix(bal);
       if (at < p.run_cap) region[at] = make_ulonglong2(v, meta);
     }
@@ -871,31 +824,8 @@ struct RunStage {
     wave_sync();
   }
 
-  // flat chunk bookkeeping after npop records were placed (room = what the old chunk had left)
-  __device__ __forceinline__ void advance(uint64_t npop, uint64_t room, uint64_t nbase) {
-    if (npop > room) {
-      fbase = nbase;
-      fused = npop - room;
-      fcap = kFlatChunk;
-    } else {
-      fused += npop;
-    }
-  }
-
-  // unused tail of the last flat chunk (holes the sort and probe skip) and the region count
+  // the region count
   __device__ void finish(uint64_t gw) {
-    if (p.flat_keys) {
-      for (uint64_t i = fused + lane; i < fcap; i += kWave) {
-        const uint64_t at = fbase + i;
-        if (at < p.flat_cap) {
-          if (p.pack_a)
-            reinterpret_cast<uint32_t*>(p.flat_keys)[at] = 0xFFFFFFFFu;
-          else
-            p.flat_keys[at] = kEmpty;
-          p.flat_meta[at] = kFlatHole;
-        }
-      }
-    }
     if (lane == 0) p.run_cnt[gw] = cursor;
   }
 };
@@ -1629,8 +1559,10 @@ __global__ __launch_bounds__(kBlock) void k_compact_rows(const uint32_t* __restr
 //   OWN_KEY: the four key records (bucket, entry) of every source read, o-major
 //            (key_ent[o key_n + a]); owner = bucket range (same rule as owned());
 //   OWN_SRC: 12-B rows, owner of src ID = source-read range
-//            [floor(r N / P), floor((r+1) N / P)) -> (src P - 1) / N.
-enum OwnerKind { OWN_KEY = 0, OWN_SRC = 1 };
+//            [floor(r N / P), floor((r+1) N / P)) -> (src P - 1) / N;
+//   OWN_BUCKET: 16-B run records of the scan's regions (x = bucket |
+//            fingerprint, y = run meta), owner = the bucket's rank.
+enum OwnerKind { OWN_KEY = 0, OWN_SRC = 1, OWN_BUCKET = 2 };
 constexpr int kMaxRanks = 64;
 
 struct PartParams {
@@ -1675,29 +1607,36 @@ __global__ __launch_bounds__(kBlock) void k_part(PartParams p) {
           valid = e != kEmpty;  // a read without keys (never after setup_index's length check)
           x16 = make_ulonglong2(b, e);
           d = (uint32_t)(((uint64_t)b * p.nranks) >> p.nb_log2);
+        } else if (KIND == OWN_BUCKET) {
+          x16 = reinterpret_cast<const ulonglong2*>(p.base)[r * p.cap + i];
+          d = (uint32_t)(((x16.x & ((1ULL << p.nb_log2) - 1)) * p.nranks) >> p.nb_log2);
         } else {
           x12 = reinterpret_cast<const uint3*>(p.base)[r * p.cap + i];
           d = (uint32_t)(((uint64_t)x12.x * p.nranks - 1) / p.n_reads);  // src is the 1-based ID
         }
       }
-      uint64_t todo = __ballot(valid);
-      while (todo) {
-        const int leader = __ffsll((unsigned long long)todo) - 1;
-        const uint32_t dd = (uint32_t)__shfl((int)d, leader);
+      // wavefront multi-split: one ballot per destination; lane dd then holds
+      // destination dd's count and takes its LDS cursor step, all
+      // destinations in one LDS atomic (no loop serialised per destination)
+      uint64_t mine = 0;
+      uint32_t cnt_d = 0;
+      for (uint32_t dd = 0; dd < p.nranks; ++dd) {
         const uint64_t m = __ballot(valid && d == dd);
-        unsigned long long at = 0;
-        if (lane == leader) at = atomicAdd(&s_cnt[dd], (unsigned long long)__popcll(m));
-        if (PASS == 1) {
-          at = __shfl(at, leader);
-          const uint64_t k = at + lane_prefix(m);
-          if (valid && d == dd && k < lim) {  // a stream cut at its capacity keeps its full count
-            const uint64_t q = k / p.slot, o = ((q * p.nranks) + dd) * p.slot + (k - q * p.slot);
-            void* dst = (p.self_out && dd == p.self_rank) ? p.self_out : p.out;
-            if (KIND == OWN_KEY) reinterpret_cast<ulonglong2*>(dst)[o] = x16;
-            else reinterpret_cast<uint3*>(dst)[o] = x12;
-          }
+        if (valid && d == dd) mine = m;
+        if ((uint32_t)lane == dd) cnt_d = (uint32_t)__popcll(m);
+      }
+      unsigned long long at = 0;
+      if (cnt_d) at = atomicAdd(&s_cnt[lane], (unsigned long long)cnt_d);
+      if (PASS == 1) {
+        const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)at, (int)d);
+        const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(at >> 32), (int)d);
+        const uint64_t k = (((uint64_t)hi << 32) | lo) + lane_prefix(mine);
+        if (valid && k < lim) {  // a stream cut at its capacity keeps its full count
+          const uint64_t q = k / p.slot, o = ((q * p.nranks) + d) * p.slot + (k - q * p.slot);
+          void* dst = (p.self_out && d == p.self_rank) ? p.self_out : p.out;
+          if (KIND != OWN_SRC) reinterpret_cast<ulonglong2*>(dst)[o] = x16;
+          else reinterpret_cast<uint3*>(dst)[o] = x12;
         }
-        todo &= ~m;
       }
     }
   }
@@ -1738,59 +1677,6 @@ __global__ __launch_bounds__(1024) void k_part_scan(unsigned long long* blk, uin
   }
 }
 
-// The bucket-sorted runs of this rank's sources are grouped by owning rank:
-// bnd[d] = the first record whose bucket rank d (or a later rank) owns.
-__global__ __launch_bounds__(128) void k_dest_bounds(const void* __restrict__ keys, int packed, uint64_t n,
-                                                     uint32_t nranks, uint32_t nb_log2,
-                                                     unsigned long long* __restrict__ bnd) {
-  const uint32_t d = threadIdx.x;
-  if (d > nranks) return;
-  const uint64_t nbm = (1ULL << nb_log2) - 1;
-  uint64_t lo = 0, hi = n;
-  while (lo < hi) {
-    const uint64_t mid = (lo + hi) / 2;
-    const uint64_t k = packed ? reinterpret_cast<const uint32_t*>(keys)[mid] : reinterpret_cast<const uint64_t*>(keys)[mid];
-    if ((((k & nbm) * nranks) >> nb_log2) < d) lo = mid + 1;
-    else hi = mid;
-  }
-  bnd[d] = lo;
-}
-
-// Sorted runs -> 16-B run records (x = bucket | fingerprint << nb, y = run
-// meta; holes stay all-ones, the probe skips them) in the slot layout, in
-// bucket order within each peer's stream; counts[d] = the stream lengths.
-__global__ __launch_bounds__(kBlock) void k_pack_runs(const void* __restrict__ keys, const uint64_t* __restrict__ meta,
-                                                      int pack_a, int pack_w, uint32_t nb_log2, uint64_t n,
-                                                      const unsigned long long* __restrict__ bnd, uint32_t nranks,
-                                                      uint64_t slot, uint64_t rounds, ulonglong2* out,
-                                                      ulonglong2* self_out, uint32_t self_rank,
-                                                      unsigned long long* __restrict__ counts) {
-  __shared__ unsigned long long s_b[kMaxRanks + 1];
-  if (threadIdx.x <= nranks) s_b[threadIdx.x] = bnd[threadIdx.x];
-  __syncthreads();
-  if (blockIdx.x == 0 && threadIdx.x < nranks) counts[threadIdx.x] = s_b[threadIdx.x + 1] - s_b[threadIdx.x];
-  const uint64_t lim = slot * rounds;
-  uint32_t d = 0;
-  for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBlock) {
-    while (d + 1 < nranks && i >= s_b[d + 1]) ++d;  // i only grows: d only grows
-    const uint64_t j = i - s_b[d];
-    if (j >= lim) continue;
-    uint64_t x, y = meta[i];
-    if (y == kFlatHole) {
-      x = ~0ULL;
-    } else if (pack_a) {
-      uint64_t b;
-      uint32_t fp;
-      run_unpack(reinterpret_cast<const uint32_t*>(keys)[i], y, nb_log2, pack_a, pack_w, &b, &fp, &y);
-      x = b | ((uint64_t)fp << nb_log2);
-    } else {
-      x = reinterpret_cast<const uint64_t*>(keys)[i];
-    }
-    const uint64_t q = j / slot;
-    ((self_out && d == self_rank) ? self_out : out)[((q * nranks) + d) * slot + (j - q * slot)] = make_ulonglong2(x, y);
-  }
-}
-
 // Per-region counts of a slot-layout buffer cut into regions of `reg` records
 // (reg divides slot; region q covers records [q reg, q reg + reg)).
 __global__ __launch_bounds__(kBlock) void k_slot_regions(unsigned long long* __restrict__ out,
@@ -1802,6 +1688,44 @@ __global__ __launch_bounds__(kBlock) void k_slot_regions(unsigned long long* __r
   const uint64_t K = slot / reg, blk = q / K, k = q - blk * K, t = blk / nranks, s = blk - t * nranks;
   const uint64_t start = t * slot + k * reg, c = counts[s];
   out[q] = c > start ? (c - start < reg ? c - start : reg) : 0;
+}
+
+// After markContainedReads: sources with superReadID != 0 contribute no
+// windows (OverlapGraph.cpp:548), so their runs (about two thirds of them at
+// C5) are dropped from every run region before the discovery probe, which
+// then streams and batches live runs only.  One wavefront per region, stable
+// in-place ballot compaction (a write never passes the batch being read), four
+// batches in flight; run_cnt[r] becomes the live count.
+__global__ __launch_bounds__(kBlock) void k_live_runs(ulonglong2* __restrict__ runs,
+                                                     unsigned long long* __restrict__ run_cnt, uint64_t run_cap,
+                                                     uint64_t nreg, const uint32_t* __restrict__ super) {
+  const int lane = threadIdx.x & 63;
+  const uint64_t nw = (uint64_t)gridDim.x * kWavesPerBlock;
+  constexpr int kDepth = 4;
+  for (uint64_t r = (uint64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6); r < nreg; r += nw) {
+    ulonglong2* reg = runs + r * run_cap;
+    const uint64_t c = run_cnt[r] < run_cap ? run_cnt[r] : run_cap;
+    uint64_t out = 0;
+    for (uint64_t b = 0; b < c; b += kDepth * kWave) {
+      ulonglong2 rec[kDepth];
+      bool live[kDepth];
+#pragma unroll
+      for (int d = 0; d < kDepth; ++d) {
+        const uint64_t i = b + (uint64_t)d * kWave + lane;
+        rec[d] = i < c ? reg[i] : make_ulonglong2(0, kFlatHole);
+      }
+#pragma unroll
+      for (int d = 0; d < kDepth; ++d) live[d] = rec[d].y != kFlatHole && super[(uint32_t)rec[d].y] == 0;
+      wave_sync();
+#pragma unroll
+      for (int d = 0; d < kDepth; ++d) {
+        const uint64_t bal = __ballot(live[d]);
+        if (live[d]) reg[out + lane_prefix(bal)] = rec[d];
+        out += (uint64_t)__popcll(bal);
+      }
+    }
+    if (lane == 0) run_cnt[r] = out;
+  }
 }
 
 __global__ __launch_bounds__(kBlock) void k_super_finalize(const unsigned long long* __restrict__ key,
@@ -2213,6 +2137,48 @@ __global__ __launch_bounds__(kBlock) void k_layout_gather(const uint64_t* __rest
   }
 }
 
+// Mixed lengths: within each aligned window of kLenWin consecutive slots of
+// the clustered order (windows restart at the group bounds lo and hi), order
+// the reads by length (stable).  A scan wavefront's 64 lanes then hold reads
+// of similar length, so fewer lanes idle to the longest read of the group,
+// while a window (one scan block's four groups, which the probe's shared
+// regions also walk together) keeps the same reads and so the same cells and
+// partner slots.  One block per window: rank = number of (len, position)
+// keys below the thread's own.
+constexpr int kLenWin = kBlock;
+__global__ __launch_bounds__(kBlock) void k_layout_lensort(const uint32_t* __restrict__ order,
+                                                          const uint16_t* __restrict__ len, uint64_t lo,
+                                                          uint64_t hi, uint64_t n, uint32_t* __restrict__ out) {
+  __shared__ uint32_t s_key[kLenWin];
+  const uint64_t w0 = (lo + kLenWin - 1) / kLenWin, w1 = (hi - lo + kLenWin - 1) / kLenWin;
+  const uint64_t b = blockIdx.x;
+  uint64_t beg, end;
+  if (b < w0) {
+    beg = b * kLenWin;
+    end = lo;
+  } else if (b < w0 + w1) {
+    beg = lo + (b - w0) * kLenWin;
+    end = hi;
+  } else {
+    beg = hi + (b - w0 - w1) * kLenWin;
+    end = n;
+  }
+  end = end < beg + kLenWin ? end : beg + kLenWin;
+  const int cnt = (int)(end - beg), i = threadIdx.x;
+  uint32_t o = 0, key = 0xFFFFFFFFu;
+  if (i < cnt) {
+    o = order[beg + i];
+    key = ((uint32_t)len[o] << 8) | (uint32_t)i;  // length, then position (stable; kLenWin <= 256)
+  }
+  s_key[i] = key;
+  __syncthreads();
+  if (i < cnt) {
+    int rank = 0;
+    for (int j = 0; j < cnt; ++j) rank += s_key[j] < key ? 1 : 0;
+    out[beg + rank] = o;
+  }
+}
+
 __global__ __launch_bounds__(kBlock) void k_layout_phys(const uint32_t* __restrict__ id, uint64_t n,
                                                        uint32_t* __restrict__ phys) {
   const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
@@ -2309,22 +2275,6 @@ struct LaunchIndex {
   }
 };
 
-// Flat scan output: chunk ids below the extent that no counter reached hold
-// nothing; one block per such chunk marks its records as holes (all-ones key
-// and meta) that the sort moves to the end and the probe skips.  One launch
-// instead of two memsets per chunk (~40 per C3 step, ~0.4 ms of launches).
-__global__ __launch_bounds__(kBlock) void k_fill_holes(const uint64_t* __restrict__ ids, uint64_t* keys,
-                                                       uint64_t* meta, int packed) {
-  const uint64_t base = ids[blockIdx.x] * kFlatChunk;
-  for (uint32_t i = threadIdx.x; i < kFlatChunk; i += kBlock) {
-    if (packed)
-      reinterpret_cast<uint32_t*>(keys)[base + i] = 0xFFFFFFFFu;
-    else
-      keys[base + i] = kEmpty;
-    meta[base + i] = kFlatHole;
-  }
-}
-
 // Persistent grids: exactly the resident blocks (a larger grid would run a
 // second, partly idle round of wavefronts).  Scan and probe use the same
 // wavefront count: probe wavefront r consumes scan region r.
@@ -2374,25 +2324,9 @@ uint32_t scan_resident(mg_ctx* ctx, bool index, uint64_t want) {
                : resident_blocks(ctx, k_scan<W, false>, lds, want, block);
 }
 
-// 12-B sort records fit when read index, jlo, two window deltas and the
-// fingerprint bits the 32-bit key cannot hold share 64 bits (run_pack_meta).
-inline void packable_runs(const mg_ctx* ctx, int* a, int* wb) {
-  auto bits = [](uint64_t x) { int b = 0; while (x) { ++b; x >>= 1; } return b; };
-  const int A = std::max(1, bits(ctx->n));  // n < 2^A: an index is never all ones
-  const int WB = bits(ctx->w > 0 ? ctx->w - 1 : 0);
-  const int nb = (int)ctx->nb_log2;
-  const int fph = std::max(0, (int)kFpBits - (32 - nb));
-  const bool ok = nb < 32 && A + 10 + 2 * WB + fph <= 64;
-  *a = ok ? A : 0;
-  *wb = ok ? WB : 0;
-}
-
 // Geometry of one discovery pass over source reads [a_lo, a_hi): probe grid =
 // its resident blocks; the scan (fewer registers) runs kreg times as many
 // wavefronts and probe wavefront r consumes scan regions r + i * (probe waves).
-#ifndef MG_X_NOIDX
-#define MG_X_NOIDX 0
-#endif
 struct DiscGeom {
   uint32_t grid = 0, sgrid = 0, kreg = 1;
   size_t lds_scan = 0, lds_probe = 0;
@@ -2414,14 +2348,13 @@ DiscGeom disc_geom(mg_ctx* ctx, bool contain, uint64_t nsrc) {
 }
 
 // Window scan over source slots [a_lo, a_hi): one run region per scan
-// wavefront in ctx->d_runs, or (flat, exchange mode) the SoA arrays of the
-// bucket sort.  filter: keep only runs whose bucket this rank owns (a
+// wavefront in ctx->d_runs.  filter: keep only runs whose bucket this rank owns (a
 // bucket-sharded single context); index: the scan also builds the index
 // (fused: CAS into the cells; exchange: key records).
 template <int W>
 struct LaunchScan {
   static int run(mg_ctx* ctx, bool contain, uint64_t a_lo, uint64_t a_hi, uint32_t sgrid, bool filter,
-                 hipStream_t stream = nullptr, bool no_super = false, bool index = false, bool flat = false) {
+                 hipStream_t stream = nullptr, bool no_super = false, bool index = false) {
     if (!stream) stream = ctx->stream;
     const uint32_t wpb = scan_block_waves(ctx, index);
     const uint64_t nw = (uint64_t)sgrid * wpb;  // scan wavefronts = run regions
@@ -2432,15 +2365,16 @@ struct LaunchScan {
     const uint64_t J = ctx->maxlen > ctx->h + 1 ? ctx->maxlen - ctx->h - 1 : 1;
     const uint64_t per_read = std::min<uint64_t>(J, 3 * (2 * J / (ctx->w + 1) + 2));
     const uint64_t groups_per_region = (ngroups + nw - 1) / nw;
-    uint64_t run_cap = std::max<uint64_t>(ctx->run_cap_need, groups_per_region * kWave * per_read);
-    if (!flat && run_cap * nreg > ctx->runs_cap) {
+    uint64_t run_cap = std::max<uint64_t>(
+        ctx->run_cap_need, ctx->run_cap_opt ? ctx->run_cap_opt : groups_per_region * kWave * per_read);
+    if (run_cap * nreg > ctx->runs_cap) {
       if (ctx->d_runs) (void)hipFree(ctx->d_runs);
       ctx->d_runs = nullptr;
       ctx->runs_cap = 0;
       if (hipMalloc(&ctx->d_runs, run_cap * nreg * sizeof(ulonglong2)) != hipSuccess) return -1;
       ctx->runs_cap = run_cap * nreg;
     }
-    run_cap = flat ? 0 : ctx->runs_cap / std::max<uint64_t>(1, nreg);
+    if (!ctx->run_cap_opt) run_cap = ctx->runs_cap / std::max<uint64_t>(1, nreg);
     ctx->run_cap = run_cap;
     if (ctx->run_cnt_cap < nreg) {
       if (ctx->d_run_cnt) (void)hipFree(ctx->d_run_cnt);
@@ -2449,6 +2383,7 @@ struct LaunchScan {
       if (hipMalloc(&ctx->d_run_cnt, std::max<uint64_t>(1, nreg) * sizeof(unsigned long long)) != hipSuccess) return -1;
       ctx->run_cnt_cap = nreg;
     }
+    ctx->runs_live = false;
     ScanParams sp{};
     sp.words = ctx->d_words;
     sp.len = ctx->d_len;
@@ -2467,40 +2402,6 @@ struct LaunchScan {
     const size_t lds = scan_lds(ctx, index);
     sp.cells = ctx->d_cells;
     sp.cell_n = ctx->cell_n;
-    ctx->scan_flat = flat;
-    ctx->pack_a = ctx->pack_w = 0;
-    if (flat) {
-      // SoA output for the bucket sort: ~2 J / (w + 1) + 1 runs per read, sized
-      // with 20 % slack (or the exact need after an overflow)
-      const uint64_t est = ctx->flat_cap_opt ? ctx->flat_cap_opt
-                                             : (a_hi - a_lo) * (2 * J / (ctx->w + 1) + 2) * 6 / 5 + 4096;
-      const uint64_t cap = std::max<uint64_t>(ctx->flat_need, est);
-      if (cap > ctx->sk_cap || (ctx->flat_cap_opt && cap < ctx->sk_cap)) {
-        for (int b = 0; b < 2; ++b) {
-          if (ctx->d_sk[b]) (void)hipFree(ctx->d_sk[b]);
-          if (ctx->d_sm[b]) (void)hipFree(ctx->d_sm[b]);
-          ctx->d_sk[b] = ctx->d_sm[b] = nullptr;
-        }
-        ctx->sk_cap = 0;
-        for (int b = 0; b < 2; ++b) {
-          if (hipMalloc(&ctx->d_sk[b], cap * sizeof(uint64_t)) != hipSuccess) return -1;
-          if (hipMalloc(&ctx->d_sm[b], cap * sizeof(uint64_t)) != hipSuccess) return -1;
-        }
-        ctx->sk_cap = cap;
-      }
-      if (!ctx->d_flat_cursor &&
-          hipMalloc(&ctx->d_flat_cursor, kFlatCounters * sizeof(unsigned long long)) != hipSuccess)
-        return -1;
-      if (hipMemsetAsync(ctx->d_flat_cursor, 0, kFlatCounters * sizeof(unsigned long long), stream) != hipSuccess)
-        return -1;
-      sp.flat_keys = ctx->d_sk[0];
-      sp.flat_meta = ctx->d_sm[0];
-      sp.flat_cursor = ctx->d_flat_cursor;
-      sp.flat_cap = ctx->sk_cap;
-      packable_runs(ctx, &ctx->pack_a, &ctx->pack_w);
-      sp.pack_a = ctx->pack_a;
-      sp.pack_w = ctx->pack_w;
-    }
     if (index && ctx->key0_ready) sp.key0 = ctx->d_key0;  // mg_build_index allocated it (mixed lengths)
     if (index && ctx->xchg) {  // key records (bucket, entry), o-major: they travel to the bucket owner
       sp.key_bk = ctx->d_kb;
@@ -2519,7 +2420,7 @@ struct LaunchScan {
         allow_lds(k_scan_reg<W, false>, lds);
         hipLaunchKernelGGL((k_scan_reg<W, false>), dim3(sgrid), dim3(wpb * kWave), lds, stream, sp);
       }
-    } else if (index && !MG_X_NOIDX) {
+    } else if (index) {
       allow_lds(k_scan<W, true>, lds);
       hipLaunchKernelGGL((k_scan<W, true>), dim3(sgrid), dim3(wpb * kWave), lds, stream, sp);
     } else {
@@ -2571,7 +2472,7 @@ struct LaunchProbe {
     pp.phase_limit = contain ? 99 : ctx->phase_limit;
     pp.halving_low = ctx->halving_low ? 1 : 0;
     pp.halving_id = (ctx->read_lo || ctx->read_hi) ? ctx->d_id : nullptr;
-    pp.contain_even = (contain && ctx->key0_ready) ? 1 : 0;
+    pp.contain_even = (contain && (ctx->xchg ? ctx->xchg_prefix : ctx->key0_ready)) ? 1 : 0;
     pp.contain_minlen = (pp.contain_even && ctx->contain_jcut) ? (int)ctx->minlen : 0;
     pp.contain_prune = (contain && ctx->contain_prune) ? 1 : 0;
     pp.contain_skip = (contain && ctx->contain_skip) ? 1 : 0;
@@ -2769,9 +2670,8 @@ void mg_destroy(mg_ctx* ctx) {
   (void)hipStreamSynchronize(ctx->stream);
   void* bufs[] = {ctx->d_words, ctx->d_len, ctx->d_cells, ctx->d_superkey, ctx->d_super, ctx->d_any, ctx->d_rows,
                   ctx->d_seg, ctx->d_stats, ctx->d_compact, ctx->d_runs, ctx->d_run_cnt, ctx->d_blk, ctx->d_flat_cnt,
-                  ctx->d_slot_cnt, ctx->d_freq, ctx->d_sk[0], ctx->d_sk[1], ctx->d_sm[0], ctx->d_sm[1],
-                  ctx->d_sort_tmp, ctx->d_flat_cursor, ctx->d_kb, ctx->d_ke, ctx->d_key0, ctx->d_holes, ctx->d_digest,
-                  ctx->d_bnd, ctx->id_store[0], ctx->id_store[1], ctx->phys_store[0], ctx->phys_store[1],
+                  ctx->d_slot_cnt, ctx->d_freq, ctx->d_kb, ctx->d_ke, ctx->d_key0, ctx->d_k0rec, ctx->d_k0n,
+                  ctx->d_digest, ctx->id_store[0], ctx->id_store[1], ctx->phys_store[0], ctx->phys_store[1],
                   ctx->d_tmp32, ctx->d_lay_k[0], ctx->d_lay_k[1], ctx->d_lay_v[0], ctx->d_lay_v[1], ctx->d_lay_tmp,
                   ctx->d_words_alt, ctx->d_len_alt};
   for (void* b : bufs)
@@ -2944,13 +2844,9 @@ int mg_set_option(mg_ctx* ctx, const char* name, int64_t value) {
     ctx->max_blocks = value > 0 ? (uint32_t)value : 8192u;
     return 0;
   }
-  if (!strcmp(name, "flat_cap")) {  // tests: initial capacity of the exchange scan's flat run arrays (0 = auto)
-    ctx->flat_cap_opt = value > 0 ? (uint64_t)value : 0;
-    ctx->flat_need = 0;
-    return 0;
-  }
-  if (!strcmp(name, "xchg_sort_bits")) {  // exchange mode, P a power of two: top bucket bits the runs are sorted on (0: all)
-    ctx->xchg_sort_bits = (int)value;
+  if (!strcmp(name, "run_cap")) {  // tests: initial run records per scan region (0 = sized from the reads)
+    ctx->run_cap_opt = (uint64_t)std::max<int64_t>(0, value);
+    ctx->run_cap_need = 0;
     return 0;
   }
   if (flag("stats", &ctx->stats) || flag("halving", &ctx->halving_low) || flag("layout", &ctx->layout) ||
@@ -3096,7 +2992,7 @@ struct LaunchScanXchg {
     const uint32_t wpb = scan_block_waves(ctx, true);
     const uint64_t groups = (hi - lo + kWave - 1) / kWave;
     const uint32_t sgrid = scan_resident<W>(ctx, true, (groups + wpb - 1) / wpb);
-    return LaunchScan<W>::run(ctx, true, lo, hi, sgrid, false, ctx->stream, true, true, true);
+    return LaunchScan<W>::run(ctx, true, lo, hi, sgrid, false, ctx->stream, true, true);
   }
 };
 
@@ -3106,7 +3002,8 @@ template <int W>
 struct LaunchProbeSlots {
   static int run(mg_ctx* ctx, bool contain, const ulonglong2* runs, uint64_t reg, uint64_t nregions) {
     const DiscGeom g = disc_geom<W>(ctx, contain, std::max<uint64_t>(1, ctx->n / ctx->nranks));
-    const uint32_t* sup = (!contain && ctx->contained_done && ctx->super_any) ? ctx->d_super : nullptr;
+    const uint32_t* sup =
+        (!contain && ctx->contained_done && ctx->super_any && !ctx->runs_live) ? ctx->d_super : nullptr;
     return LaunchProbe<W>::run(ctx, contain, runs, ctx->d_flat_cnt, reg, nregions, g.grid, sup);
   }
 };
@@ -3188,7 +3085,7 @@ struct LaunchScanAll {
     const uint32_t wpb = scan_block_waves(ctx, true);
     const uint64_t groups = (ctx->n + kWave - 1) / kWave;
     const uint32_t sgrid = scan_resident<W>(ctx, true, (groups + wpb - 1) / wpb);
-    return LaunchScan<W>::run(ctx, true, 0, ctx->n, sgrid, false, st, true, true, false);
+    return LaunchScan<W>::run(ctx, true, 0, ctx->n, sgrid, false, st, true, true);
   }
 };
 
@@ -3200,49 +3097,13 @@ struct LaunchScanRuns {
     const uint32_t wpb = scan_block_waves(ctx, false);
     const uint64_t groups = (ctx->n + kWave - 1) / kWave;
     const uint32_t sgrid = scan_resident<W>(ctx, false, (groups + wpb - 1) / wpb);
-    return LaunchScan<W>::run(ctx, true, 0, ctx->n, sgrid, false, ctx->stream, true, false, false);
+    return LaunchScan<W>::run(ctx, true, 0, ctx->n, sgrid, false, ctx->stream, true, false);
   }
 };
 
 // one shared scan per build: an unsharded context over all its sources (a
 // source-read range takes the separate index build + a scan of its slots)
 bool shared_scan(const mg_ctx* ctx) { return ctx->nranks == 1 && ctx->read_lo == 0 && ctx->read_hi == 0; }
-
-// flat scan output (exchange mode): the cursor is the run count; on overflow
-// size for it and rerun
-int settle_flat(mg_ctx* ctx, bool* again) {
-  *again = false;
-  unsigned long long c[kFlatCounters] = {};
-  if (ctx->n)
-    MG_TRY(hipMemcpyAsync(c, ctx->d_flat_cursor, sizeof(c), hipMemcpyDeviceToHost, ctx->stream));
-  MG_TRY(hipStreamSynchronize(ctx->stream));
-  // chunk ids claimed: x + 8 k for k < c[x]; the array extends to the highest one
-  uint64_t ext = 0;
-  for (uint32_t x = 0; x < kFlatCounters; ++x)
-    if (c[x]) ext = std::max<uint64_t>(ext, (c[x] - 1) * kFlatCounters + x + 1);
-  const uint64_t n = ext * kFlatChunk;
-  if (n > ctx->sk_cap) {
-    ctx->flat_need = n + n / 8 + 4096;
-    *again = true;
-    return 0;
-  }
-  // ids below the extent that a counter never reached hold nothing: mark them
-  // as holes (all-ones key and meta) so the sort and the probe skip them
-  ctx->holes_host.clear();
-  for (uint32_t x = 0; x < kFlatCounters; ++x)
-    for (uint64_t id = c[x] * kFlatCounters + x; id < ext; id += kFlatCounters) ctx->holes_host.push_back(id);
-  if (!ctx->holes_host.empty()) {
-    const size_t nh = ctx->holes_host.size();
-    MG_TRY(ensure(&ctx->d_holes, &ctx->holes_cap, nh));
-    MG_TRY(hipMemcpyAsync(ctx->d_holes, ctx->holes_host.data(), nh * sizeof(uint64_t), hipMemcpyHostToDevice,
-                          ctx->stream));
-    hipLaunchKernelGGL(k_fill_holes, dim3((uint32_t)nh), dim3(kBlock), 0, ctx->stream, ctx->d_holes, ctx->d_sk[0],
-                       ctx->d_sm[0], ctx->pack_a ? 1 : 0);
-    MG_TRY(hipGetLastError());
-  }
-  ctx->n_flat = n;
-  return 0;
-}
 
 // the shared scan's region counts settled (its overflow reruns a plain run scan)
 int ensure_scan(mg_ctx* ctx) {
@@ -3273,54 +3134,12 @@ template <int W>
 struct LaunchProbeShared {
   static int run(mg_ctx* ctx, bool contain) {
     const DiscGeom g = disc_geom<W>(ctx, contain, std::max<uint64_t>(ctx->n, 1));
-    const uint32_t* sup = (!contain && ctx->contained_done && ctx->super_any) ? ctx->d_super : nullptr;
+    // (after k_live_runs every run's source is uncontained: no per-run check)
+    const uint32_t* sup =
+        (!contain && ctx->contained_done && ctx->super_any && !ctx->runs_live) ? ctx->d_super : nullptr;
     return LaunchProbe<W>::run(ctx, contain, ctx->d_runs, ctx->d_run_cnt, ctx->run_cap, ctx->nrun_reg, g.grid, sup);
   }
 };
-
-// exchange mode: the flat runs of this rank's scan -> rocprim radix sort by
-// bucket (8 bits per pass; `bits` > 0: only the top `bits` bucket bits), which
-// groups them by owning rank for mg_xchg_pack(MG_RUNS)
-int sort_flat_runs(mg_ctx* ctx, int bits) {
-  const uint64_t n = ctx->n_flat;
-  if (n > 0x7FFFFFFFull) return set_err(ctx, "exchange: more than 2^31 runs on one rank");
-  MG_TRY(hipEventRecord(ctx->ev[12], ctx->stream));
-  const unsigned nb = ctx->nb_log2;
-  const unsigned lo_bit = (bits > 0 && (unsigned)bits < nb) ? nb - (unsigned)bits : 0u;
-  const bool packed = ctx->pack_a != 0;  // 32-bit keys (run_pack_key)
-  auto sort = [&](void* tmp, size_t& tb, int& sel) -> hipError_t {
-    rocprim::double_buffer<uint64_t> vals(ctx->d_sm[0], ctx->d_sm[1]);
-    hipError_t e;
-    if (packed) {
-      rocprim::double_buffer<uint32_t> keys(reinterpret_cast<uint32_t*>(ctx->d_sk[0]),
-                                            reinterpret_cast<uint32_t*>(ctx->d_sk[1]));
-      e = rocprim::radix_sort_pairs(tmp, tb, keys, vals, n, lo_bit, nb, ctx->stream);
-      sel = keys.current() == reinterpret_cast<uint32_t*>(ctx->d_sk[0]) ? 0 : 1;
-    } else {
-      rocprim::double_buffer<uint64_t> keys(ctx->d_sk[0], ctx->d_sk[1]);
-      e = rocprim::radix_sort_pairs(tmp, tb, keys, vals, n, lo_bit, nb, ctx->stream);
-      sel = keys.current() == ctx->d_sk[0] ? 0 : 1;
-    }
-    if (e == hipSuccess && tmp && (vals.current() == ctx->d_sm[0] ? 0 : 1) != sel) e = hipErrorUnknown;
-    return e;
-  };
-  size_t tb = 0;
-  int sel = 0;
-  MG_TRY(sort(nullptr, tb, sel));
-  if (tb > ctx->sort_tmp_cap) {
-    if (ctx->d_sort_tmp) (void)hipFree(ctx->d_sort_tmp);
-    ctx->d_sort_tmp = nullptr;
-    ctx->sort_tmp_cap = 0;
-    MG_TRY(hipMalloc(&ctx->d_sort_tmp, tb));
-    ctx->sort_tmp_cap = tb;
-  }
-  tb = ctx->sort_tmp_cap;
-  MG_TRY(sort(ctx->d_sort_tmp, tb, sel));
-  MG_TRY(hipEventRecord(ctx->ev[13], ctx->stream));
-  ctx->sk_sel = sel;
-  ctx->n_sorted = n;
-  return 0;
-}
 
 // probe the shared scan's runs (rows settled for the discovery probe)
 int probe_shared(mg_ctx* ctx, bool contain) {
@@ -3328,6 +3147,14 @@ int probe_shared(mg_ctx* ctx, bool contain) {
   for (int attempt = 0; attempt < 3; ++attempt) {
     ctx->nreg = 0;
     MG_TRY(hipEventRecord(ctx->ev[8], ctx->stream));
+    if (!contain && ctx->contained_done && ctx->super_any && !ctx->runs_live && ctx->nrun_reg) {
+      const uint32_t grid = (uint32_t)std::min<uint64_t>((ctx->nrun_reg + kWavesPerBlock - 1) / kWavesPerBlock,
+                                                         (uint64_t)ctx->n_cu * 8);
+      hipLaunchKernelGGL(k_live_runs, dim3(grid), dim3(kBlock), 0, ctx->stream, ctx->d_runs, ctx->d_run_cnt,
+                         ctx->run_cap, ctx->nrun_reg, ctx->d_super);
+      MG_TRY(hipGetLastError());
+      ctx->runs_live = true;
+    }
     if (dispatch_w<LaunchProbeShared>(ctx->maxw, ctx, contain)) return set_err(ctx, "probe launch failed");
     MG_TRY(hipEventRecord(ctx->ev[9], ctx->stream));
     if (contain) return 0;
@@ -3388,7 +3215,16 @@ int layout_current(mg_ctx* ctx, bool force) {
     return set_err(ctx, "layout key launch failed");
   MG_TRY(rocprim::radix_sort_pairs(ctx->d_lay_tmp, tb, ctx->d_lay_k[0], ctx->d_lay_k[1], ctx->d_lay_v[0],
                                    ctx->d_lay_v[1], (unsigned int)n, 0u, kbits, ctx->stream));
-  if (dispatch_w<LaunchLayoutGather>(ctx->maxw, ctx, ctx->d_lay_v[1], ctx->d_words_alt, ctx->d_len_alt, id_new))
+  const uint32_t* order = ctx->d_lay_v[1];
+  if (ctx->minlen != ctx->maxlen) {  // similar lengths side by side (k_layout_lensort)
+    const uint64_t nwin = (lo + kLenWin - 1) / kLenWin + (hi - lo + kLenWin - 1) / kLenWin +
+                          (n - hi + kLenWin - 1) / kLenWin;
+    hipLaunchKernelGGL(k_layout_lensort, dim3((uint32_t)nwin), dim3(kLenWin), 0, ctx->stream, order, ctx->d_len, lo,
+                       hi, n, ctx->d_lay_v[0]);
+    MG_TRY(hipGetLastError());
+    order = ctx->d_lay_v[0];
+  }
+  if (dispatch_w<LaunchLayoutGather>(ctx->maxw, ctx, order, ctx->d_words_alt, ctx->d_len_alt, id_new))
     return set_err(ctx, "layout gather launch failed");
   // the zero pad past the last slot (over-reads of the kernels)
   MG_TRY(hipMemsetAsync(ctx->d_words_alt + n * S, 0, (ctx->words_cap - n * S) * sizeof(uint64_t), ctx->stream));
@@ -3606,6 +3442,7 @@ int mg_xchg_begin(mg_ctx* ctx, uint32_t min_overlap, uint32_t seed_k) {
   MG_TRY(hipEventRecord(ctx->ev[0], ctx->stream));
   if (setup_index(ctx, min_overlap, seed_k)) return -1;  // this rank's (cleared) cells
   ctx->xchg = true;
+  ctx->xchg_prefix = ctx->minlen != ctx->maxlen && ctx->prefix_contain;
   uint64_t lo, hi;
   source_range(ctx, &lo, &hi);
   ctx->xchg_lo = lo;
@@ -3613,40 +3450,22 @@ int mg_xchg_begin(mg_ctx* ctx, uint32_t min_overlap, uint32_t seed_k) {
   MG_TRY(ensure(&ctx->d_kb, &ctx->kb_cap, 4 * ctx->n + 1));
   MG_TRY(ensure(&ctx->d_ke, &ctx->ke_cap, 4 * ctx->n + 1));
   ctx->scan_state = 0;
-  ctx->n_flat = ctx->n_sorted = 0;
   ctx->shared_scan_ms = 0.f;
   ctx->t = mg_timings{};
   if (hi > lo) {
-    // one scan: the four keys of every source read (o-major records) + its runs
+    // one scan: the four keys of every source read (o-major records) + its
+    // runs in per-wavefront regions, as the fused path writes them
     for (int attempt = 0;; ++attempt) {
       if (attempt == 3) return set_err(ctx, "run buffers overflow after resize");
       if (dispatch_w<LaunchScanXchg>(ctx->maxw, ctx, lo, hi)) return set_err(ctx, "scan launch failed");
       bool again = false;
-      if (settle_flat(ctx, &again)) return -1;
+      if (settle_runs(ctx, &again)) return -1;
       if (!again) break;
     }
     ctx->shared_scan_ms = elapsed(ctx->ev[6], ctx->ev[7]);
-    // bucket order = grouped by owning rank.  With P a power of two the owner is
-    // the top log2 P bucket bits, so sorting the top 8 (option xchg_sort_bits)
-    // groups the runs by owner in one digit pass instead of three, and keeps a
-    // coarse bucket order for the probe (simulated C3: P = 8 25.2 -> 24.4 ms,
-    // P = 2 17.5 -> 16.3 ms summed over ranks); other P sort every bit
-    int bits = 0;
-    if (ctx->xchg_sort_bits > 0 && !(ctx->nranks & (ctx->nranks - 1))) {
-      int lg = 0;
-      while ((1u << lg) < ctx->nranks) ++lg;
-      bits = std::max(ctx->xchg_sort_bits, lg);
-    }
-    if (sort_flat_runs(ctx, bits)) return -1;
   } else {
-    MG_TRY(hipEventRecord(ctx->ev[12], ctx->stream));
-    MG_TRY(hipEventRecord(ctx->ev[13], ctx->stream));
+    ctx->nrun_reg = 0;
   }
-  MG_TRY(ensure(&ctx->d_bnd, &ctx->bnd_cap, (size_t)ctx->nranks + 1));
-  hipLaunchKernelGGL(k_dest_bounds, dim3(1), dim3(128), 0, ctx->stream,
-                     ctx->n_sorted ? (const void*)ctx->d_sk[ctx->sk_sel] : (const void*)ctx->d_bnd,
-                     ctx->pack_a ? 1 : 0, ctx->n_sorted, ctx->nranks, ctx->nb_log2, ctx->d_bnd);
-  MG_TRY(hipGetLastError());
   ctx->packable = (1 << MG_KEYS) | (1 << MG_RUNS);
   return 0;
 }
@@ -3673,16 +3492,13 @@ int mg_xchg_pack(mg_ctx* ctx, int what, void* dst, uint64_t slot, uint32_t round
     pp.nsrc = nsrc;
     return route_slots<OWN_KEY>(ctx, pp, dst, self_dst, slot, rounds, cnt);
   }
-  if (what == MG_RUNS) {
-    const uint64_t n = ctx->n_sorted;
-    const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((n + kBlock - 1) / kBlock, 16384));
-    hipLaunchKernelGGL(k_pack_runs, dim3(grid), dim3(kBlock), 0, ctx->stream,
-                       n ? (const void*)ctx->d_sk[ctx->sk_sel] : (const void*)ctx->d_bnd,
-                       n ? ctx->d_sm[ctx->sk_sel] : nullptr, ctx->pack_a, ctx->pack_w, ctx->nb_log2, n, ctx->d_bnd,
-                       ctx->nranks, slot, (uint64_t)rounds, reinterpret_cast<ulonglong2*>(dst),
-                       reinterpret_cast<ulonglong2*>(self_dst), ctx->rank, cnt);
-    MG_TRY(hipGetLastError());
-    return 0;
+  if (what == MG_RUNS) {  // the scan's run regions, each run to its bucket's owner
+    PartParams pp{};
+    pp.base = ctx->d_runs;
+    pp.cap = ctx->run_cap;
+    pp.cnt = ctx->d_run_cnt;
+    pp.nreg = ctx->nrun_reg;
+    return route_slots<OWN_BUCKET>(ctx, pp, dst, self_dst, slot, rounds, cnt);
   }
   PartParams pp{};
   pp.base = ctx->d_rows;
@@ -3700,18 +3516,27 @@ int mg_xchg_insert_keys(mg_ctx* ctx, const void* recv, uint64_t slot, uint32_t r
   if (total) {
     if (!recv || !counts) return set_err(ctx, "mg_xchg_insert_keys: null buffer");
     IndexParams p = index_params(ctx);
+    if (ctx->xchg_prefix) {  // every read has one o = 0 key: n records at most
+      MG_TRY(ensure(&ctx->d_k0rec, &ctx->k0rec_cap, std::max<uint64_t>(1, ctx->n)));
+      if (!ctx->d_k0n) MG_TRY(hipMalloc(&ctx->d_k0n, sizeof(unsigned long long)));
+      MG_TRY(hipMemsetAsync(ctx->d_k0n, 0, sizeof(unsigned long long), ctx->stream));
+    }
     const uint32_t grid = (uint32_t)std::min<uint64_t>((total + kBlock - 1) / kBlock, 65536);
     hipLaunchKernelGGL(k_insert_slots, dim3(grid), dim3(kBlock), 0, ctx->stream, p,
                        reinterpret_cast<const ulonglong2*>(recv), slot, rounds,
-                       reinterpret_cast<const unsigned long long*>(counts));
+                       reinterpret_cast<const unsigned long long*>(counts),
+                       ctx->xchg_prefix ? ctx->d_k0rec : nullptr, ctx->xchg_prefix ? ctx->d_k0n : nullptr);
     MG_TRY(hipGetLastError());
+  } else if (ctx->xchg_prefix) {
+    if (!ctx->d_k0n) MG_TRY(hipMalloc(&ctx->d_k0n, sizeof(unsigned long long)));
+    MG_TRY(hipMemsetAsync(ctx->d_k0n, 0, sizeof(unsigned long long), ctx->stream));
   }
   MG_TRY(hipEventRecord(ctx->ev[1], ctx->stream));
   ctx->index_ready = true;
   return 0;
 }
 
-int mg_xchg_probe(mg_ctx* ctx, int contain, const void* recv, uint64_t slot, uint32_t rounds, const uint64_t* counts) {
+int mg_xchg_probe(mg_ctx* ctx, int contain, void* recv, uint64_t slot, uint32_t rounds, const uint64_t* counts) {
   if (!ctx) return -1;
   MG_TRY(hipSetDevice(ctx->device));
   if (!ctx->xchg || !ctx->index_ready) return set_err(ctx, "mg_xchg_insert_keys must run first");
@@ -3723,11 +3548,14 @@ int mg_xchg_probe(mg_ctx* ctx, int contain, const void* recv, uint64_t slot, uin
   if (slot_regions(ctx, &ctx->d_flat_cnt, &ctx->flat_cnt_cap, reinterpret_cast<const unsigned long long*>(counts),
                    slot, reg, nregions))
     return -1;
-  const auto* runs = reinterpret_cast<const ulonglong2*>(recv);
+  auto* runs = reinterpret_cast<ulonglong2*>(recv);
   ctx->nreg = 0;
   ctx->n_rows = 0;
   if (contain) {
     MG_TRY(hipEventRecord(ctx->ev[2], ctx->stream));
+    // prefix containments first (what they mark is skipped as a container)
+    if (ctx->xchg_prefix && ctx->n && dispatch_w<LaunchPrefixContainRec>(ctx->maxw, ctx))
+      return set_err(ctx, "prefix containment launch failed");
     if (nregions && dispatch_w<LaunchProbeSlots>(ctx->maxw, ctx, true, runs, reg, nregions))
       return set_err(ctx, "probe launch failed");
     MG_TRY(hipEventRecord(ctx->ev[3], ctx->stream));
@@ -3737,6 +3565,17 @@ int mg_xchg_probe(mg_ctx* ctx, int contain, const void* recv, uint64_t slot, uin
   for (int attempt = 0;; ++attempt) {
     if (attempt == 3) return set_err(ctx, "row buffers overflow after resize");
     MG_TRY(hipEventRecord(ctx->ev[4], ctx->stream));
+    if (attempt == 0 && nregions && ctx->contained_done && ctx->super_any) {
+      // runs of contained sources contribute nothing (:548): drop them from the
+      // received regions in place (the caller's buffer; the containment probe
+      // has read it already) so the probe batches live runs only
+      const uint32_t grid = (uint32_t)std::min<uint64_t>((nregions + kWavesPerBlock - 1) / kWavesPerBlock,
+                                                         (uint64_t)ctx->n_cu * 8);
+      hipLaunchKernelGGL(k_live_runs, dim3(grid), dim3(kBlock), 0, ctx->stream, runs, ctx->d_flat_cnt, reg,
+                         nregions, ctx->d_super);
+      MG_TRY(hipGetLastError());
+      ctx->runs_live = true;
+    }
     if (nregions && dispatch_w<LaunchProbeSlots>(ctx->maxw, ctx, false, runs, reg, nregions))
       return set_err(ctx, "probe launch failed");
     MG_TRY(hipEventRecord(ctx->ev[5], ctx->stream));
@@ -3749,7 +3588,7 @@ int mg_xchg_probe(mg_ctx* ctx, int contain, const void* recv, uint64_t slot, uin
   // device times of this step (events on the context's stream; the exchanges
   // between them ran on the same stream when the caller used it)
   ctx->t.scan_ms = ctx->shared_scan_ms;
-  ctx->t.sort_ms = elapsed(ctx->ev[12], ctx->ev[13]);
+  ctx->t.sort_ms = 0.f;
   ctx->t.index_ms = elapsed(ctx->ev[0], ctx->ev[1]);
   ctx->t.contained_ms = ctx->minlen != ctx->maxlen ? elapsed(ctx->ev[2], ctx->ev[3]) : 0.f;
   ctx->t.probe_ms = elapsed(ctx->ev[4], ctx->ev[5]);

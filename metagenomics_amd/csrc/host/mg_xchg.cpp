@@ -263,12 +263,12 @@ int XchgStep::run() {
     x_.allreduce_max_u64(dmx, 3, s_);
     hip_check(hipMemcpyAsync(mx, dmx, sizeof mx, hipMemcpyDeviceToHost, s_), "max D2H");
     hip_check(hipStreamSynchronize(s_), "hipStreamSynchronize");
+    // fit the capacities to what was sent (grow: rerun; shrink: less padding
+    // on the links from the next step on), identically on every rank
     bool over = false;
     for (int kind = 0; kind < 3; ++kind) {
-      if (mx[kind] > caps_[kind]) {
-        caps_[kind] = mx[kind] + mx[kind] * 15 / 100 + 64;
-        over = true;
-      }
+      if (mx[kind] > caps_[kind]) over = true;
+      caps_[kind] = mx[kind] + mx[kind] * 15 / 100 + 64;
     }
     rows_held_ = 0;
     for (int p = 0; p < P; ++p) rows_held_ += rc[p];

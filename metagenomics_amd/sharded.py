@@ -65,12 +65,16 @@ class XchgPlan:
         return slot_geometry(self.caps[kind], world, RECORD_BYTES[kind], chunk_bytes)
 
     def grow(self, used: dict) -> bool:
-        """Raise capacities below the counts seen; True if any stream overflowed."""
+        """Fit the capacities to the counts seen (MAX over ranks and peers, identical on every
+        rank): streams that overflowed grow (True: rerun the step), the others shrink, so from
+        the second step on the slot layout moves ~15 % more than the largest stream instead of
+        the first guess (rows: 32 per source read, ~10x C5's)."""
         over = False
         for k, c in used.items():
+            want = int(c * 1.15) + SLOT_ALIGN
             if c > self.caps[k]:
                 over = True
-                self.caps[k] = int(c * 1.15) + SLOT_ALIGN
+            self.caps[k] = want
         return over
 
 
@@ -184,11 +188,15 @@ class LocalExchange(Exchange):
     """P simulated ranks in one process, all buffers on one device (parity tests, --sim-world).
     The engines run on separate HIP streams, so every exchange synchronizes the device."""
 
-    def __init__(self, world: int, device=None, chunk_bytes: int = 256 << 20):
+    def __init__(self, world: int, device=None, chunk_bytes: int = 256 << 20, serial: bool | None = None):
         import torch
 
         self.torch = torch
         self.world = world
+        # serial: every library call of a simulated rank completes before the next starts, so
+        # a kernel trace times each rank's kernels alone (the engines' streams otherwise overlap
+        # on the one GPU and every duration includes the other ranks' work; MG_SIM_SERIAL=1)
+        self.serial = bool(int(os.environ.get("MG_SIM_SERIAL", "0"))) if serial is None else serial
         self.ranks = list(range(world))
         self.device = device if device is not None else torch.device("cpu")
         self.chunk_bytes = int(os.environ.get("MG_A2A_CHUNK_BYTES", chunk_bytes))
@@ -237,6 +245,26 @@ class ShardResult:
     n_rows: list = field(default_factory=list)  # rows held per local rank
     reruns: int = 0       # steps rerun with grown capacities
     plan: XchgPlan | None = None  # the capacities used (pass it to the next step)
+    # kind -> (slot, rounds, [per local rank: per-peer send counts]): the slot layout moves
+    # rounds * slot records to every peer whatever the count (padding(), outside the timed step)
+    streams: dict = field(default_factory=dict)
+
+    def padding(self, world: int, rank_ids: list) -> dict:
+        """Per stream kind: records the slot layout moved between ranks vs the records sent
+        (own slots excluded; they never travel), summed over the local ranks."""
+        out = {}
+        for kind, (slot, rounds, cnts) in self.streams.items():
+            moved = sent = 0
+            for r, c in zip(rank_ids, cnts):
+                v = c.cpu().numpy().astype(np.int64)
+                for p in range(world):
+                    if p != r:
+                        moved += slot * rounds
+                        sent += int(v[p])
+            out[{MG_KEYS: "keys", MG_RUNS: "runs", MG_ROWS: "rows"}[kind]] = {
+                "moved_records": moved, "sent_records": sent,
+                "padding_frac": (1.0 - sent / moved) if moved else 0.0}
+        return out
 
     def rows_numpy(self, i: int = 0) -> np.ndarray:
         """The rows of local rank i, compacted out of the slot layout (host copy)."""
@@ -286,9 +314,15 @@ def sharded_step(engines: list, xchg: Exchange, min_overlap: int, seed_k: int = 
 
 def _step(engines, xchg, min_overlap, seed_k, want_super, plan):
     P = xchg.world
+    serial = getattr(xchg, "serial", False)
+
+    def done():  # (serial simulated ranks: one rank's call at a time on the device)
+        if serial:
+            xchg.sync()
     ch = getattr(xchg, "chunk_bytes", 256 << 20)
     ms = {}
     sent = {}
+    geo = {}
 
     def route(kind):
         slot, rounds = plan.geometry(kind, P, ch)
@@ -300,10 +334,12 @@ def _step(engines, xchg, min_overlap, seed_k, want_super, plan):
             c = xchg.counts()
             e.xchg_pack(kind, send.data_ptr() if send is not None else 0, slot, rounds, c.data_ptr(),
                         recv.data_ptr())
+            done()
             sends.append(send)
             recvs.append(recv)
             cnts.append(c)
         sent[kind] = cnts
+        geo[kind] = (slot, rounds)
         return xchg.all_to_all_slots(sends, recvs, cnts, slot, rounds, rb), slot, rounds
 
     t0 = time.perf_counter()
@@ -311,10 +347,12 @@ def _step(engines, xchg, min_overlap, seed_k, want_super, plan):
         # 1. one scan of the rank's sources: index keys + sorted runs
         for e in engines:
             e.xchg_begin(min_overlap, seed_k)
+            done()
         # 2. HashTable::insertDataset: key records -> bucket owners -> local cells
         keys, ks, kr = route(MG_KEYS)
         for e, (buf, c) in zip(engines, keys):
             e.xchg_insert_keys(buf.data_ptr(), ks, kr, c.data_ptr())
+            done()
         # 3. runs -> bucket owners (both probes read them)
         runs, rs, rr = route(MG_RUNS)
         t1 = time.perf_counter()
@@ -330,6 +368,7 @@ def _step(engines, xchg, min_overlap, seed_k, want_super, plan):
         if contained:
             for e, (buf, c) in zip(engines, runs):
                 e.xchg_probe(True, buf.data_ptr(), rs, rr, c.data_ptr())
+                done()
             xchg.allreduce_max(skeys)
         sup = None
         for i, e in enumerate(engines):
@@ -342,6 +381,7 @@ def _step(engines, xchg, min_overlap, seed_k, want_super, plan):
         # 5. insertAllEdgesOfRead: probe the received runs -> rows -> src owners
         for e, (buf, c) in zip(engines, runs):
             e.xchg_probe(False, buf.data_ptr(), rs, rr, c.data_ptr())
+            done()
         rows, ws, wr = route(MG_ROWS)
         # the step's one host read: MAX over ranks of every per-peer send count
         mx = xchg.max_counts([[sent[k][i] for k in KINDS] for i in range(len(engines))])
@@ -352,5 +392,5 @@ def _step(engines, xchg, min_overlap, seed_k, want_super, plan):
     ms["overlap"] = (time.perf_counter() - t2) * 1e3
     used = {k: int(v) for k, v in zip(KINDS, mx)}
     res = ShardResult(rows=[(b, c, ws, wr) for b, c in rows], ms=ms, contained=contained, super_read_id=sup,
-                      n_rows=n_rows)
+                      n_rows=n_rows, streams={k: geo[k] + (sent[k],) for k in KINDS})
     return res, used

@@ -312,7 +312,7 @@ def test_repeatable(engine):
 
 # ---- exchange mode: P simulated ranks in this process, buffers
 # moved by LocalExchange on the device; the same sharded_step drives RCCL ranks
-def exchange_rows(ds, l, world, k=0, want_super=True):
+def exchange_rows(ds, l, world, k=0, want_super=True, opts=None):
     import torch
 
     from metagenomics_amd.sharded import LocalExchange, sharded_step, source_range
@@ -320,6 +320,8 @@ def exchange_rows(ds, l, world, k=0, want_super=True):
     engines = []
     for r in range(world):
         e = OverlapEngine(0)
+        for kk, v in (opts or {}).items():
+            e.set_option(kk, v)
         e.set_shard(r, world, 0, 0)
         e.upload(ds)
         engines.append(e)
@@ -342,6 +344,18 @@ def test_exchange_mode_matches_reference(name, world):
     ds = Dataset.from_files([fixture_input(name)], meta["l"])
     rows, sup = exchange_rows(ds, meta["l"], world)
     assert np.array_equal(rows_to_tuples(rows), golden_rows(name))
+    assert {str(i): int(s) for i, s in enumerate(sup) if s} == meta["super"]
+
+
+@pytest.mark.parametrize("prefix", [0, 1])
+def test_exchange_mode_containment_paths(prefix):
+    """Exchange-mode markContainedReads (OverlapGraph.cpp:225-340) both ways:
+    prefix = 1 walks the o = 0 key records each rank filed (k_prefix_contain_rec)
+    and the probe drops suffix-key hits; prefix = 0 verifies them in the probe."""
+    meta = load_meta("mixed")
+    ds = Dataset.from_files([fixture_input("mixed")], meta["l"])
+    rows, sup = exchange_rows(ds, meta["l"], 3, opts={"prefix_contain": prefix})
+    assert np.array_equal(rows_to_tuples(rows), golden_rows("mixed"))
     assert {str(i): int(s) for i, s in enumerate(sup) if s} == meta["super"]
 
 
@@ -397,9 +411,10 @@ def test_exchange_mode_cut_streams_rerun():
 
 
 @pytest.mark.parametrize("name", ["mixed", "branchy", "highdup"])
-def test_exchange_flat_overflow(name):
-    """The exchange scan's flat run arrays start far too small: its chunk
-    cursors keep counting, the host resizes to the exact need and reruns."""
+def test_exchange_run_region_overflow(name):
+    """The exchange scan's run regions start far too small (option run_cap):
+    the scan keeps counting past them, the host resizes to the exact need and
+    rescans before the runs are routed."""
     import torch
 
     from metagenomics_amd.sharded import LocalExchange, sharded_step
@@ -409,7 +424,7 @@ def test_exchange_flat_overflow(name):
     engines = []
     for r in range(2):
         e = OverlapEngine(0)
-        e.set_option("flat_cap", 700)
+        e.set_option("run_cap", 8)
         e.set_shard(r, 2, 0, 0)
         e.upload(ds)
         engines.append(e)

@@ -49,6 +49,10 @@ def _worker(rank, world, port, name, outdir, chunk):
     res = sharded_step([eng], TorchExchange(), lm(name)["l"], 0)
     mine = res.rows_numpy(0)
     assert res.n_rows == [len(mine)]
+    pad = res.padding(world, [rank])  # bench.py's exchange_padding
+    assert set(pad) == {"keys", "runs", "rows"}
+    for v in pad.values():
+        assert 0 <= v["sent_records"] <= v["moved_records"] and 0.0 <= v["padding_frac"] <= 1.0
     np.save(os.path.join(outdir, f"reruns{rank}.npy"), np.array([res.reruns, eng.begins]))
     np.save(os.path.join(outdir, f"rows{rank}.npy"), mine)
     np.save(os.path.join(outdir, f"keys{rank}.npy"), eng.received_keys)

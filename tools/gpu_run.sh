@@ -54,9 +54,10 @@ for s in $STEPS; do
     timeout -k 10 1000 python -u -m pytest tests/test_scale_digest.py -x -v -m gpu -k cli_exchange --timeout 900 --timeout-method thread > $OUT/clixchg_tests.log 2>&1
     rc=$?; echo "cli exchange tests rc=$rc"; grep -E "PASS|FAIL|SKIP|Error|assert" $OUT/clixchg_tests.log | tail -12 ;;
   profsim8)
-    # per-rank kernel tables of the exchange mode at P=8 (simulated ranks), C3 then C5
+    # per-rank kernel tables of the exchange mode at P=8 (simulated ranks, one rank's call at a
+    # time: MG_SIM_SERIAL), C3 then C5
     for C in c3 c5; do
-      timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/profsim8_$C -o kt -- python3 bench.py --config $C --sim-world 8 --multi exchange --steps 2 --no-cpu-baseline --no-ingest > $OUT/profsim8_${C}_bench.json 2> $OUT/profsim8_${C}_bench.err
+      MG_SIM_SERIAL=1 timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/profsim8_$C -o kt -- python3 bench.py --config $C --sim-world 8 --multi exchange --steps 2 --no-cpu-baseline --no-ingest > $OUT/profsim8_${C}_bench.json 2> $OUT/profsim8_${C}_bench.err
       rc=$?; echo "profsim8 $C rc=$rc"; [ $rc -ne 0 ] && break
       python3 tools/rank_table.py $OUT/profsim8_$C/kt_kernel_stats.csv 8 4 "$C exchange-sim" | tee $OUT/profsim8_${C}_ranks.md | tail -14
     done ;;
@@ -81,6 +82,9 @@ for s in $STEPS; do
   benchc2)
     timeout -k 10 300 python -u bench.py --config c2 --no-cpu-baseline > $OUT/bench_c2.json 2> $OUT/bench_c2.err
     rc=$?; echo "bench c2 rc=$rc"; cat $OUT/bench_c2.json ;;
+  benchc5)
+    timeout -k 10 600 python -u bench.py --config c5 --no-ingest > $OUT/bench_c5.json 2> $OUT/bench_c5.err
+    rc=$?; echo "bench c5 rc=$rc"; cat $OUT/bench_c5.json ;;
   benchc5s)
     timeout -k 10 300 python -u bench.py --config c5s --no-cpu-baseline --no-ingest > $OUT/bench_c5s.json 2> $OUT/bench_c5s.err
     rc=$?; echo "bench c5s rc=$rc"; cat $OUT/bench_c5s.json ;;

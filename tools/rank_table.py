@@ -18,6 +18,10 @@ def short(name: str) -> str:
     return s[:90]
 
 
+# kernels that run once per upload or only for the parity check, not in the step
+OUTSIDE = ("k_layout_", "k_rows_digest", "k_super_digest", "k_ingest", "k_pack_ascii")
+
+
 def main():
     path, P, S = sys.argv[1], int(sys.argv[2]), int(sys.argv[3])
     title = sys.argv[4] if len(sys.argv) > 4 else path
@@ -26,10 +30,18 @@ def main():
     print(f"### {title}: kernel time per rank per step at P={P} (total / (P x {S}))\n")
     print("| kernel | calls/rank/step | ms/rank/step | share |")
     print("|---|---:|---:|---:|")
+    step = 0.0
     for r in sorted(rows, key=lambda r: -float(r["TotalDurationNs"])):
         t = float(r["TotalDurationNs"])
-        print(f"| `{short(r['Name'])}` | {int(r['Calls']) / P / S:.2f} | {t / P / S / 1e6:.3f} | {100 * t / tot:.1f}% |")
+        name = short(r["Name"])
+        out = name.startswith(OUTSIDE)
+        if not out:
+            step += t
+        print(f"| `{name}`{' (not in the step)' if out else ''} | {int(r['Calls']) / P / S:.2f} | "
+              f"{t / P / S / 1e6:.3f} | {100 * t / tot:.1f}% |")
     print(f"| **all kernels** | | **{tot / P / S / 1e6:.3f}** | |")
+    print(f"| **step kernels** (upload / parity kernels excluded; rocprim sorts of the layout included) | | "
+          f"**{step / P / S / 1e6:.3f}** | |")
 
 
 if __name__ == "__main__":
