@@ -179,7 +179,9 @@ def one_shot(e, ds, fused_step, device, rows):
     out = {}
     lay, ms, n = cycle(e)
     assert n == rows, (n, rows)
-    out.update(layout_ms=lay, step_ms=ms, one_shot_ms=lay + ms)
+    t = e.timings()
+    out.update(layout_ms=lay, step_ms=ms, one_shot_ms=lay + ms,
+               step_device_ms={k: round(t[k], 3) for k in ("total_ms", "index_ms", "scan_ms", "probe_ms")})
     e0 = OverlapEngine(device)
     try:
         e0.set_option("layout", 0)

@@ -221,9 +221,10 @@ int mg_xchg_insert_keys(mg_ctx* ctx, const void* recv, uint64_t slot, uint32_t r
 /* Probe the received runs against the local cells: contain = 1 atomicMax-es
  * containment keys into the buffer of mg_begin_contained; contain = 0 verifies
  * overlaps (sources with superReadID != 0 give none) and keeps the rows
- * (+ twins) for mg_xchg_pack(MG_ROWS).  With contained reads, contain = 0
- * first drops their runs from recv IN PLACE (recv is not reusable after). */
-int mg_xchg_probe(mg_ctx* ctx, int contain, void* recv, uint64_t slot, uint32_t rounds, const uint64_t* counts);
+ * (+ twins) for mg_xchg_pack(MG_ROWS).  The first probe of a step orders the
+ * received runs by bucket into the context's own array (one host read of the
+ * counts); a second call reuses that order (pass the same recv / counts). */
+int mg_xchg_probe(mg_ctx* ctx, int contain, const void* recv, uint64_t slot, uint32_t rounds, const uint64_t* counts);
 /* Containment: *needed = 1 when read lengths differ (OverlapGraph.cpp:228-233).
  * superkey = caller-owned device array of n_reads u64 (NULL: context-owned),
  * cleared here; the contain probe atomicMax-es (len << 32 | ~index) into it,

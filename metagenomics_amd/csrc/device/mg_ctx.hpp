@@ -132,6 +132,16 @@ struct mg_ctx {
   // exchange mode, mixed lengths: the o = 0 key records this rank filed
   // (k_insert_slots), walked by k_prefix_contain_rec before the containment
   // probe, which then drops o = 1/3 hits like the fused path (xchg_prefix)
+  // exchange mode: the received runs ordered by local bucket (sort_xruns), the
+  // input of both probes; xruns_ready until the next mg_xchg_begin
+  uint32_t* d_xk[2] = {nullptr, nullptr};
+  ulonglong2* d_xv[2] = {nullptr, nullptr};
+  size_t xk_cap[2] = {0, 0}, xv_cap[2] = {0, 0};
+  void* d_xsort_tmp = nullptr;
+  size_t xsort_tmp_cap = 0;
+  int xv_sel = 0;
+  uint64_t xruns_n = 0;
+  bool xruns_ready = false;
   ulonglong2* d_k0rec = nullptr;
   size_t k0rec_cap = 0;
   unsigned long long* d_k0n = nullptr;

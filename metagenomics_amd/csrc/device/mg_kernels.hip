@@ -493,7 +493,10 @@ __device__ __forceinline__ uint64_t run_meta(uint64_t a, int p, int jlo, int jhi
 // 6 waves per SIMD (the LDS limit: 6 blocks of 4 wavefronts per CU): 80 VGPRs
 // with a 12-B spill beat 83 VGPRs / 5 waves, index 3.72 vs 3.93 ms at C3
 // (profiles/r01s5_ab_scan_waves.log)
-template <int MAXW, bool INDEX>
+// KEYREC (exchange mode with w > 32, INDEX only): key records for the bucket
+// owners instead of CAS inserts.  Each instantiation references only the
+// parameters it uses, which keeps its scalar registers below the limit.
+template <int MAXW, bool INDEX, bool KEYREC = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) void k_scan(ScanParams p) {
   extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -525,7 +528,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) voi
     const uint64_t* g = p.words + a * slot_words(MAXW);
     if (a < p.a_hi) {
       n = (int)p.len[a];
-      if (n && p.super && p.super[a]) n = 0;
+      if (!INDEX && n && p.super && p.super[a]) n = 0;  // (an index scan covers every source)
     }
     const int J = n - h - 1;                 // windows j = 1 .. J (:534)
     const int tend = J >= 1 ? J + w - 1 : 0;  // last m-mer position a window uses
@@ -586,13 +589,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) voi
         }
         if (flag) {
           v = mix64(funnel(w0, w1, (pos & 31) << 1) >> msh);
-          flag = owned(v & nbmask, p.nb_log2, p.rank, p.nranks);
+          if (!INDEX) flag = owned(v & nbmask, p.nb_log2, p.rank, p.nranks);  // (index scans: all buckets)
         }
       } else if (flag) {
         const uint64_t* g2 = p.words + (meta & 0xFFFFFFFFull) * slot_words(MAXW);
         const int pos = (int)((meta >> 32) & 1023u);
         v = mix64(funnel(g2[pos >> 5], g2[(pos >> 5) + 1], (pos & 31) << 1) >> msh);
-        flag = owned(v & nbmask, p.nb_log2, p.rank, p.nranks);
+        if (!INDEX) flag = owned(v & nbmask, p.nb_log2, p.rank, p.nranks);
       }
       const uint64_t bal = __ballot(flag);
       if (flag) {
@@ -704,7 +707,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) voi
     if constexpr (MAXW <= 8) {
       // one loop per read word (t + m <= n - 1 < 32 MAXW): the word is a
       // compile-time register, so rw[] never goes to scratch and no vmcnt wait
-      // (which would also wait for the flushes' stores) sits in the loop
+      // (which would also wait for the flushes' stores) sits in the loop.  (A
+      // specialised body for the steps every lane covers, outside the key
+      // windows, measured slower: scan 3.55 vs 2.95 ms at 6 waves, its extra
+      // registers spill; 3.06 ms at 5 waves.)
 #pragma unroll
       for (int k = 0; k < MAXW; ++k) {
         const int t0 = max(1, 32 * k - m), t1 = min(tmax, 32 * k + 31 - m);
@@ -742,7 +748,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) voi
         const uint64_t v = mix64(mb[o]);
         const unsigned long long e = make_entry(v, p.nb_log2, (int)(kb[o] & 1023u), o, (uint32_t)a);
         if (o == 0 && p.key0) p.key0[a] = (v & ((1ULL << 50) - 1)) | ((uint64_t)(kb[0] & 1023u) << 54);
-        if (p.key_bk) {  // o-major: each store is one coalesced wavefront line
+        if constexpr (KEYREC) {  // o-major: each store is one coalesced wavefront line
           p.key_bk[o * p.key_n + a] = (uint32_t)(v & nbm);
           p.key_ent[o * p.key_n + a] = e;
         } else {
@@ -751,7 +757,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) voi
       }
     } else if (INDEX && a < p.a_hi) {  // no keys (n <= l cannot pass setup_index): holes
       if (p.key0) p.key0[a] = kEmpty;
-      if (p.key_bk) {
+      if constexpr (KEYREC) {
         for (int o = 0; o < 4; ++o) {
           p.key_bk[o * p.key_n + a] = 0;
           p.key_ent[o * p.key_n + a] = kEmpty;
@@ -1690,6 +1696,36 @@ __global__ __launch_bounds__(kBlock) void k_slot_regions(unsigned long long* __r
   out[q] = c > start ? (c - start < reg ? c - start : reg) : 0;
 }
 
+// Exchange mode: the received runs (slot layout, one stream per peer) ->
+// one compact array with a sort key = the top 8 bits of the run's bucket
+// within this rank's range.  Record j of peer s goes to position
+// sum_{s' < s} counts[s'] + j, so no atomics and the array is dense.
+// A stream cut at its capacity (count > rounds * slot, the step reruns)
+// contributes the rounds * slot records that arrived.
+__global__ __launch_bounds__(kBlock) void k_xruns_keys(const ulonglong2* __restrict__ recv, uint64_t slot,
+                                                      uint32_t nranks, uint64_t total,
+                                                      const unsigned long long* __restrict__ counts,
+                                                      uint64_t nbmask, uint64_t cell_lo, uint32_t shift,
+                                                      uint32_t* __restrict__ key, ulonglong2* __restrict__ val) {
+  const uint64_t blk = (uint64_t)nranks * slot, lim = total / nranks;  // records per peer stream
+  for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < total; i += (uint64_t)gridDim.x * kBlock) {
+    const uint64_t t = i / blk, rem = i - t * blk, sp = rem / slot, j = t * slot + (rem - sp * slot);
+    if (j >= counts[sp]) continue;  // (j < lim always)
+    uint64_t at = j;
+    for (uint64_t q = 0; q < sp; ++q) at += counts[q] < lim ? counts[q] : lim;
+    const ulonglong2 x = recv[i];
+    key[at] = (uint32_t)((((x.x & nbmask) - cell_lo) >> shift) & 0xFFu);
+    val[at] = x;
+  }
+}
+
+// run regions of R records over a dense array of n records
+__global__ __launch_bounds__(kBlock) void k_fixed_regions(unsigned long long* __restrict__ out, uint64_t n,
+                                                          uint64_t R, uint64_t nreg) {
+  const uint64_t q = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (q < nreg) out[q] = n > q * R ? (n - q * R < R ? n - q * R : R) : 0;
+}
+
 // After markContainedReads: sources with superReadID != 0 contribute no
 // windows (OverlapGraph.cpp:548), so their runs (about two thirds of them at
 // C5) are dropped from every run region before the discovery probe, which
@@ -2137,48 +2173,6 @@ __global__ __launch_bounds__(kBlock) void k_layout_gather(const uint64_t* __rest
   }
 }
 
-// Mixed lengths: within each aligned window of kLenWin consecutive slots of
-// the clustered order (windows restart at the group bounds lo and hi), order
-// the reads by length (stable).  A scan wavefront's 64 lanes then hold reads
-// of similar length, so fewer lanes idle to the longest read of the group,
-// while a window (one scan block's four groups, which the probe's shared
-// regions also walk together) keeps the same reads and so the same cells and
-// partner slots.  One block per window: rank = number of (len, position)
-// keys below the thread's own.
-constexpr int kLenWin = kBlock;
-__global__ __launch_bounds__(kBlock) void k_layout_lensort(const uint32_t* __restrict__ order,
-                                                          const uint16_t* __restrict__ len, uint64_t lo,
-                                                          uint64_t hi, uint64_t n, uint32_t* __restrict__ out) {
-  __shared__ uint32_t s_key[kLenWin];
-  const uint64_t w0 = (lo + kLenWin - 1) / kLenWin, w1 = (hi - lo + kLenWin - 1) / kLenWin;
-  const uint64_t b = blockIdx.x;
-  uint64_t beg, end;
-  if (b < w0) {
-    beg = b * kLenWin;
-    end = lo;
-  } else if (b < w0 + w1) {
-    beg = lo + (b - w0) * kLenWin;
-    end = hi;
-  } else {
-    beg = hi + (b - w0 - w1) * kLenWin;
-    end = n;
-  }
-  end = end < beg + kLenWin ? end : beg + kLenWin;
-  const int cnt = (int)(end - beg), i = threadIdx.x;
-  uint32_t o = 0, key = 0xFFFFFFFFu;
-  if (i < cnt) {
-    o = order[beg + i];
-    key = ((uint32_t)len[o] << 8) | (uint32_t)i;  // length, then position (stable; kLenWin <= 256)
-  }
-  s_key[i] = key;
-  __syncthreads();
-  if (i < cnt) {
-    int rank = 0;
-    for (int j = 0; j < cnt; ++j) rank += s_key[j] < key ? 1 : 0;
-    out[beg + rank] = o;
-  }
-}
-
 __global__ __launch_bounds__(kBlock) void k_layout_phys(const uint32_t* __restrict__ id, uint64_t n,
                                                        uint32_t* __restrict__ phys) {
   const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
@@ -2420,6 +2414,9 @@ struct LaunchScan {
         allow_lds(k_scan_reg<W, false>, lds);
         hipLaunchKernelGGL((k_scan_reg<W, false>), dim3(sgrid), dim3(wpb * kWave), lds, stream, sp);
       }
+    } else if (index && ctx->xchg) {
+      allow_lds(k_scan<W, true, true>, lds);
+      hipLaunchKernelGGL((k_scan<W, true, true>), dim3(sgrid), dim3(wpb * kWave), lds, stream, sp);
     } else if (index) {
       allow_lds(k_scan<W, true>, lds);
       hipLaunchKernelGGL((k_scan<W, true>), dim3(sgrid), dim3(wpb * kWave), lds, stream, sp);
@@ -2671,6 +2668,7 @@ void mg_destroy(mg_ctx* ctx) {
   void* bufs[] = {ctx->d_words, ctx->d_len, ctx->d_cells, ctx->d_superkey, ctx->d_super, ctx->d_any, ctx->d_rows,
                   ctx->d_seg, ctx->d_stats, ctx->d_compact, ctx->d_runs, ctx->d_run_cnt, ctx->d_blk, ctx->d_flat_cnt,
                   ctx->d_slot_cnt, ctx->d_freq, ctx->d_kb, ctx->d_ke, ctx->d_key0, ctx->d_k0rec, ctx->d_k0n,
+                  ctx->d_xk[0], ctx->d_xk[1], ctx->d_xv[0], ctx->d_xv[1], ctx->d_xsort_tmp,
                   ctx->d_digest, ctx->id_store[0], ctx->id_store[1], ctx->phys_store[0], ctx->phys_store[1],
                   ctx->d_tmp32, ctx->d_lay_k[0], ctx->d_lay_k[1], ctx->d_lay_v[0], ctx->d_lay_v[1], ctx->d_lay_tmp,
                   ctx->d_words_alt, ctx->d_len_alt};
@@ -2959,6 +2957,7 @@ int route_slots(mg_ctx* ctx, PartParams pp, void* out, void* self_out, uint64_t 
 }
 
 constexpr uint64_t kFlatRegion = 4096;  // records per routing region of a flat array
+constexpr uint64_t kXRegion = 1024;     // records per probe region of the ordered received runs
 
 // region size of a slot-layout run buffer for the probe: the largest power of
 // two <= 1024 that divides the slot (slots are multiples of 64 records)
@@ -3166,6 +3165,64 @@ int probe_shared(mg_ctx* ctx, bool contain) {
 }
 }  // namespace
 
+// Exchange mode: the runs this rank received (every peer's stream in the slot
+// layout) -> one dense array ordered by the top 8 bits of the bucket within
+// this rank's range (one onesweep pass; a 1/256 slice of the cell range then
+// probes together, so consecutive items share cell lines in L2).  Its run
+// regions (kXRegion records) feed both probes; the containment probe's order
+// and the discovery probe's live-run compaction work on this array, never on
+// the caller's buffer.  One host read: the received total.
+static int sort_xruns(mg_ctx* ctx, const ulonglong2* recv, uint64_t slot, uint32_t rounds,
+               const unsigned long long* counts) {
+  const uint32_t P = ctx->nranks;
+  std::vector<unsigned long long> c(P, 0);
+  if ((uint64_t)rounds * slot) {
+    MG_TRY(hipMemcpyAsync(c.data(), counts, P * sizeof(unsigned long long), hipMemcpyDeviceToHost, ctx->stream));
+    MG_TRY(hipStreamSynchronize(ctx->stream));
+  }
+  uint64_t n = 0;
+  for (uint32_t s = 0; s < P; ++s) n += std::min<uint64_t>(c[s], (uint64_t)rounds * slot);  // cut streams: what arrived
+  if (n > 0x7FFFFFFFull) return set_err(ctx, "exchange: more than 2^31 runs received on one rank");
+  for (int b = 0; b < 2; ++b) {
+    MG_TRY(ensure(&ctx->d_xk[b], &ctx->xk_cap[b], std::max<uint64_t>(n, 1)));
+    MG_TRY(ensure(&ctx->d_xv[b], &ctx->xv_cap[b], std::max<uint64_t>(n, 1)));
+  }
+  int hb = 1;
+  while (hb < 40 && (1ULL << hb) < ctx->cell_n) ++hb;  // bits of a local bucket index
+  const uint32_t shift = hb > 8 ? (uint32_t)(hb - 8) : 0u;
+  ctx->xv_sel = 0;
+  if (n) {
+    const uint64_t total = (uint64_t)rounds * P * slot;
+    const uint32_t grid = (uint32_t)std::min<uint64_t>((total + kBlock - 1) / kBlock, 65536);
+    hipLaunchKernelGGL(k_xruns_keys, dim3(grid), dim3(kBlock), 0, ctx->stream, recv, slot, P, total, counts,
+                       (1ULL << ctx->nb_log2) - 1, ctx->cell_lo, shift, ctx->d_xk[0], ctx->d_xv[0]);
+    MG_TRY(hipGetLastError());
+    rocprim::double_buffer<uint32_t> keys(ctx->d_xk[0], ctx->d_xk[1]);
+    rocprim::double_buffer<ulonglong2> vals(ctx->d_xv[0], ctx->d_xv[1]);
+    size_t tb = 0;
+    MG_TRY(rocprim::radix_sort_pairs(nullptr, tb, keys, vals, (unsigned int)n, 0u, 8u, ctx->stream));
+    if (tb > ctx->xsort_tmp_cap) {
+      if (ctx->d_xsort_tmp) MG_TRY(hipFree(ctx->d_xsort_tmp));
+      ctx->d_xsort_tmp = nullptr;
+      ctx->xsort_tmp_cap = 0;
+      MG_TRY(hipMalloc(&ctx->d_xsort_tmp, tb));
+      ctx->xsort_tmp_cap = tb;
+    }
+    tb = ctx->xsort_tmp_cap;
+    MG_TRY(rocprim::radix_sort_pairs(ctx->d_xsort_tmp, tb, keys, vals, (unsigned int)n, 0u, 8u, ctx->stream));
+    ctx->xv_sel = vals.current() == ctx->d_xv[0] ? 0 : 1;
+  }
+  const uint64_t nreg = (n + kXRegion - 1) / kXRegion;
+  MG_TRY(ensure(&ctx->d_flat_cnt, &ctx->flat_cnt_cap, std::max<uint64_t>(nreg, 1)));
+  if (nreg)
+    hipLaunchKernelGGL(k_fixed_regions, dim3((uint32_t)((nreg + kBlock - 1) / kBlock)), dim3(kBlock), 0, ctx->stream,
+                       ctx->d_flat_cnt, n, kXRegion, nreg);
+  MG_TRY(hipGetLastError());
+  ctx->xruns_n = n;
+  ctx->xruns_ready = true;
+  return 0;
+}
+
 // Device layout (mg_ctx.hpp): layout keys -> rocprim radix sort
 // of (key, slot) -> gather into the second slot array -> commit.  Every
 // buffer is the context's own and kept between uploads, so the timed window
@@ -3215,16 +3272,7 @@ int layout_current(mg_ctx* ctx, bool force) {
     return set_err(ctx, "layout key launch failed");
   MG_TRY(rocprim::radix_sort_pairs(ctx->d_lay_tmp, tb, ctx->d_lay_k[0], ctx->d_lay_k[1], ctx->d_lay_v[0],
                                    ctx->d_lay_v[1], (unsigned int)n, 0u, kbits, ctx->stream));
-  const uint32_t* order = ctx->d_lay_v[1];
-  if (ctx->minlen != ctx->maxlen) {  // similar lengths side by side (k_layout_lensort)
-    const uint64_t nwin = (lo + kLenWin - 1) / kLenWin + (hi - lo + kLenWin - 1) / kLenWin +
-                          (n - hi + kLenWin - 1) / kLenWin;
-    hipLaunchKernelGGL(k_layout_lensort, dim3((uint32_t)nwin), dim3(kLenWin), 0, ctx->stream, order, ctx->d_len, lo,
-                       hi, n, ctx->d_lay_v[0]);
-    MG_TRY(hipGetLastError());
-    order = ctx->d_lay_v[0];
-  }
-  if (dispatch_w<LaunchLayoutGather>(ctx->maxw, ctx, order, ctx->d_words_alt, ctx->d_len_alt, id_new))
+  if (dispatch_w<LaunchLayoutGather>(ctx->maxw, ctx, ctx->d_lay_v[1], ctx->d_words_alt, ctx->d_len_alt, id_new))
     return set_err(ctx, "layout gather launch failed");
   // the zero pad past the last slot (over-reads of the kernels)
   MG_TRY(hipMemsetAsync(ctx->d_words_alt + n * S, 0, (ctx->words_cap - n * S) * sizeof(uint64_t), ctx->stream));
@@ -3442,6 +3490,7 @@ int mg_xchg_begin(mg_ctx* ctx, uint32_t min_overlap, uint32_t seed_k) {
   MG_TRY(hipEventRecord(ctx->ev[0], ctx->stream));
   if (setup_index(ctx, min_overlap, seed_k)) return -1;  // this rank's (cleared) cells
   ctx->xchg = true;
+  ctx->xruns_ready = false;
   ctx->xchg_prefix = ctx->minlen != ctx->maxlen && ctx->prefix_contain;
   uint64_t lo, hi;
   source_range(ctx, &lo, &hi);
@@ -3536,19 +3585,20 @@ int mg_xchg_insert_keys(mg_ctx* ctx, const void* recv, uint64_t slot, uint32_t r
   return 0;
 }
 
-int mg_xchg_probe(mg_ctx* ctx, int contain, void* recv, uint64_t slot, uint32_t rounds, const uint64_t* counts) {
+int mg_xchg_probe(mg_ctx* ctx, int contain, const void* recv, uint64_t slot, uint32_t rounds, const uint64_t* counts) {
   if (!ctx) return -1;
   MG_TRY(hipSetDevice(ctx->device));
   if (!ctx->xchg || !ctx->index_ready) return set_err(ctx, "mg_xchg_insert_keys must run first");
   if (contain && !ctx->superkey) return set_err(ctx, "mg_begin_contained must run first (lengths differ)");
   if (!contain && !ctx->contained_done) return set_err(ctx, "containment must be settled first (mg_finalize_contained)");
   if ((uint64_t)rounds * slot && (!recv || !counts)) return set_err(ctx, "mg_xchg_probe: null buffer");
-  const uint64_t reg = slot_region(slot);
-  const uint64_t nregions = (uint64_t)rounds * ctx->nranks * (slot / reg);
-  if (slot_regions(ctx, &ctx->d_flat_cnt, &ctx->flat_cnt_cap, reinterpret_cast<const unsigned long long*>(counts),
-                   slot, reg, nregions))
+  // the first probe of the step orders the received runs (both probes read them)
+  if (!ctx->xruns_ready && sort_xruns(ctx, reinterpret_cast<const ulonglong2*>(recv), slot, rounds,
+                                      reinterpret_cast<const unsigned long long*>(counts)))
     return -1;
-  auto* runs = reinterpret_cast<ulonglong2*>(recv);
+  const uint64_t reg = kXRegion;
+  const uint64_t nregions = (ctx->xruns_n + reg - 1) / reg;
+  ulonglong2* runs = ctx->d_xv[ctx->xv_sel];
   ctx->nreg = 0;
   ctx->n_rows = 0;
   if (contain) {
@@ -3567,8 +3617,8 @@ int mg_xchg_probe(mg_ctx* ctx, int contain, void* recv, uint64_t slot, uint32_t 
     MG_TRY(hipEventRecord(ctx->ev[4], ctx->stream));
     if (attempt == 0 && nregions && ctx->contained_done && ctx->super_any) {
       // runs of contained sources contribute nothing (:548): drop them from the
-      // received regions in place (the caller's buffer; the containment probe
-      // has read it already) so the probe batches live runs only
+      // ordered regions in place (the containment probe has read them already)
+      // so the probe batches live runs only
       const uint32_t grid = (uint32_t)std::min<uint64_t>((nregions + kWavesPerBlock - 1) / kWavesPerBlock,
                                                          (uint64_t)ctx->n_cu * 8);
       hipLaunchKernelGGL(k_live_runs, dim3(grid), dim3(kBlock), 0, ctx->stream, runs, ctx->d_flat_cnt, reg,
