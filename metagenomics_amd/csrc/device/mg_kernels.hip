@@ -1654,12 +1654,13 @@ __global__ __launch_bounds__(kBlock) void k_part(PartParams p) {
 
 // Per-(block, destination) counts -> offsets within each destination's stream:
 // off[b][d] = sum_{b' < b} cnt[b'][d]; totals[d] = the stream's length (the
-// caller's device counts).  One block.
+// caller's device counts).  One block per destination.
 __global__ __launch_bounds__(1024) void k_part_scan(unsigned long long* blk, uint32_t nblk, uint32_t nranks,
                                                     unsigned long long* totals) {
   __shared__ unsigned long long s_part[1024];
   __shared__ unsigned long long s_base;
-  for (uint32_t d = 0; d < nranks; ++d) {
+  {
+    const uint32_t d = blockIdx.x;
     if (threadIdx.x == 0) s_base = 0;
     __syncthreads();
     for (uint32_t b0 = 0; b0 < nblk; b0 += 1024) {
@@ -2949,7 +2950,8 @@ int route_slots(mg_ctx* ctx, PartParams pp, void* out, void* self_out, uint64_t 
   pp.rounds = rounds;
   hipLaunchKernelGGL((k_part<KIND, 0>), dim3(grid), dim3(kBlock), 0, ctx->stream, pp);
   MG_TRY(hipGetLastError());
-  hipLaunchKernelGGL(k_part_scan, dim3(1), dim3(1024), 0, ctx->stream, ctx->d_blk, grid, ctx->nranks, counts);
+  hipLaunchKernelGGL(k_part_scan, dim3(ctx->nranks), dim3(1024), 0, ctx->stream, ctx->d_blk, grid, ctx->nranks,
+                     counts);
   MG_TRY(hipGetLastError());
   hipLaunchKernelGGL((k_part<KIND, 1>), dim3(grid), dim3(kBlock), 0, ctx->stream, pp);
   MG_TRY(hipGetLastError());
@@ -3165,15 +3167,13 @@ int probe_shared(mg_ctx* ctx, bool contain) {
 }
 }  // namespace
 
-// Exchange mode: the runs this rank received (every peer's stream in the slot
-// layout) -> one dense array ordered by the top 8 bits of the bucket within
-// this rank's range (one onesweep pass; a 1/256 slice of the cell range then
-// probes together, so consecutive items share cell lines in L2).  Its run
-// regions (kXRegion records) feed both probes; the containment probe's order
-// and the discovery probe's live-run compaction work on this array, never on
-// the caller's buffer.  One host read: the received total.
-static int sort_xruns(mg_ctx* ctx, const ulonglong2* recv, uint64_t slot, uint32_t rounds,
-               const unsigned long long* counts) {
+// Exchange mode: records this rank received (every peer's stream in the slot
+// layout; key records or runs, x = bucket [| fingerprint]) -> one dense array
+// in the context ordered by the top 8 bits of the bucket within this rank's
+// range (one onesweep pass): consecutive consumers then work in a 1/256 slice
+// of the cell range, which stays in L2.  One host read: the received total.
+static int sort_xrecs(mg_ctx* ctx, const ulonglong2* recv, uint64_t slot, uint32_t rounds,
+                      const unsigned long long* counts, uint64_t* n_out) {
   const uint32_t P = ctx->nranks;
   std::vector<unsigned long long> c(P, 0);
   if ((uint64_t)rounds * slot) {
@@ -3182,7 +3182,7 @@ static int sort_xruns(mg_ctx* ctx, const ulonglong2* recv, uint64_t slot, uint32
   }
   uint64_t n = 0;
   for (uint32_t s = 0; s < P; ++s) n += std::min<uint64_t>(c[s], (uint64_t)rounds * slot);  // cut streams: what arrived
-  if (n > 0x7FFFFFFFull) return set_err(ctx, "exchange: more than 2^31 runs received on one rank");
+  if (n > 0x7FFFFFFFull) return set_err(ctx, "exchange: more than 2^31 records received on one rank");
   for (int b = 0; b < 2; ++b) {
     MG_TRY(ensure(&ctx->d_xk[b], &ctx->xk_cap[b], std::max<uint64_t>(n, 1)));
     MG_TRY(ensure(&ctx->d_xv[b], &ctx->xv_cap[b], std::max<uint64_t>(n, 1)));
@@ -3212,6 +3212,16 @@ static int sort_xruns(mg_ctx* ctx, const ulonglong2* recv, uint64_t slot, uint32
     MG_TRY(rocprim::radix_sort_pairs(ctx->d_xsort_tmp, tb, keys, vals, (unsigned int)n, 0u, 8u, ctx->stream));
     ctx->xv_sel = vals.current() == ctx->d_xv[0] ? 0 : 1;
   }
+  *n_out = n;
+  return 0;
+}
+
+// the received runs, ordered, and their probe regions (kXRegion records);
+// both probes of the step read them, never the caller's buffer
+static int sort_xruns(mg_ctx* ctx, const ulonglong2* recv, uint64_t slot, uint32_t rounds,
+                      const unsigned long long* counts) {
+  uint64_t n = 0;
+  if (sort_xrecs(ctx, recv, slot, rounds, counts, &n)) return -1;
   const uint64_t nreg = (n + kXRegion - 1) / kXRegion;
   MG_TRY(ensure(&ctx->d_flat_cnt, &ctx->flat_cnt_cap, std::max<uint64_t>(nreg, 1)));
   if (nreg)

@@ -410,7 +410,7 @@ def test_exchange_mode_cut_streams_rerun():
         e.close()
 
 
-@pytest.mark.parametrize("name", ["mixed", "branchy", "highdup"])
+@pytest.mark.parametrize("name", ["mixed"])
 def test_exchange_run_region_overflow(name):
     """The exchange scan's run regions start far too small (option run_cap):
     the scan keeps counting past them, the host resizes to the exact need and
@@ -750,7 +750,7 @@ def test_register_scan_window_extremes(engine, l, k):
     assert np.array_equal(rows_to_tuples(xrows), sorted_tuples(orows))
 
 
-@pytest.mark.parametrize("name", ["small", "mixed", "tandem", "branchy", "longreads"])
+@pytest.mark.parametrize("name", ["mixed", "tandem", "longreads"])
 def test_id_order_layout(name):
     """option layout = 0 (slots in ID order) beside the default (clustered
     slots): same rows, superReadIDs, getListOfReads lists and downloaded reads."""
