@@ -340,9 +340,11 @@ def main():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29517")
         backend = os.environ.get("MG_BENCH_PG_BACKEND", "nccl")
-        if backend == "gloo" and args.multi == "replicated" and not args.exchange:
-            # rehearsal of the replicated mode with several ranks on fewer GPUs:
-            # it has no data-path collective, so gloo carries the barrier and the clocks
+        if backend == "gloo":
+            # rehearsal with several ranks on fewer GPUs (RCCL refuses two ranks on one
+            # device): replicated mode has no data-path collective, so gloo carries the
+            # barrier and the clocks; the exchange mode stages its all-to-alls through
+            # host copies (TorchExchange.staged), so its timing is not a measurement
             local = local % max(1, torch.cuda.device_count())
             torch.cuda.set_device(local)
             dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -548,8 +550,12 @@ def main():
         "undirected_edges": edges,
         "device_ms": dev_ms,
         # the device Dataset's slot layout (reads clustered by canonical global
-        # minimizer), built once per upload like the packing: not in ms_per_step
+        # minimizer), built once per upload like the packing: not in
+        # ms_per_step.  layout_ms = its kernels on a context that already holds the
+        # layout's buffers (one_shot re-upload, below, when it runs); the first
+        # upload also allocates them (layout_first_upload_ms)
         "layout_ms": layout_ms,
+        "layout_first_upload_ms": layout_ms,
         "phase_wall_ms": {kk: v / args.steps for kk, v in phase_ms.items()} or None,
         "exchange_reruns": reruns[0] if mode.startswith("exchange") else None,
         # slot-layout padding: records moved between ranks vs records sent (rank 0's, or all
@@ -565,6 +571,7 @@ def main():
     if world == 1 and mode == "fused" and not args.no_one_shot:
         try:
             res["one_shot"] = one_shot(engines[0], ds, fused_step, local, rows)
+            res["layout_ms"] = res["one_shot"]["layout_ms"]
         except Exception as e:  # report, never fake
             res["one_shot"] = {"error": str(e)}
     if world == 1 and mode == "fused" and args.replay:

@@ -136,6 +136,10 @@ class TorchExchange(Exchange):
         self.ranks = [self.rank]
         self.device = device if device is not None else torch.device("cpu")
         self.chunk_bytes = int(os.environ.get("MG_A2A_CHUNK_BYTES", chunk_bytes))
+        # gloo moves host tensors only: device buffers are staged through host copies.  This
+        # is the multi-process rehearsal of the real library path on a box with fewer GPUs
+        # than ranks (RCCL refuses two ranks on one device); with "nccl" nothing is staged.
+        self.staged = self.device.type == "cuda" and dist.get_backend() == "gloo"
 
     def streams(self, engines):
         if self.device.type != "cuda" or not engines or not hasattr(engines[0], "stream"):
@@ -154,6 +158,9 @@ class TorchExchange(Exchange):
         if P == 1:
             return [(recv, cnt)]
         dist = self.dist
+        dev_recv = recv
+        if self.staged:  # (.cpu() waits for the library's pack on this stream)
+            send, recv, cnt = send.cpu(), recv.cpu(), cnt.cpu()
         for t in range(rounds):  # one group of sends/receives per round, none to itself
             ops = []
             for p in range(P):
@@ -165,17 +172,25 @@ class TorchExchange(Exchange):
                 w.wait()
         rc = self.torch.empty_like(cnt)
         dist.all_to_all_single(rc, cnt)
+        if self.staged:
+            dev_recv.copy_(recv)
+            return [(dev_recv, rc.to(self.device))]
         return [(recv, rc)]
 
     def allreduce_max(self, bufs):
         (b,) = bufs
-        step = max(1, self.chunk_bytes // b.element_size())
-        for i in range(0, b.numel(), step):
-            self.dist.all_reduce(b[i: i + step], op=self.dist.ReduceOp.MAX)
+        h = b.cpu() if self.staged else b
+        step = max(1, self.chunk_bytes // h.element_size())
+        for i in range(0, h.numel(), step):
+            self.dist.all_reduce(h[i: i + step], op=self.dist.ReduceOp.MAX)
+        if self.staged:
+            b.copy_(h)
 
     def max_counts(self, sent):
         (cnts,) = sent
         v = self.torch.stack([c.max() for c in cnts])
+        if self.staged:
+            v = v.cpu()
         self.dist.all_reduce(v, op=self.dist.ReduceOp.MAX)
         return v.cpu().numpy()
 

@@ -44,9 +44,10 @@ def fixture_input(name, tmp_path_factory=None):
     os.makedirs(d, exist_ok=True)
     dst = os.path.join(d, meta["input"][:-3])
     if not os.path.exists(dst):
-        with gzip.open(src, "rb") as f, open(dst + ".part", "wb") as g:
+        part = "%s.%d.part" % (dst, os.getpid())  # parallel workers (pytest -n) each write their own
+        with gzip.open(src, "rb") as f, open(part, "wb") as g:
             g.write(f.read())
-        os.replace(dst + ".part", dst)
+        os.replace(part, dst)
     return dst
 
 

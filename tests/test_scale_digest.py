@@ -244,3 +244,31 @@ def test_cli_exchange_over_rccl(name, launcher, tmp_path):
     assert r["rows"] == m["rows"]
     assert r["super"] == m["super"]
     assert r["contained"] == (m["super"]["n"] > 0)
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("name", ["c2", "c5s"])
+def test_exchange_two_processes(name):
+    """The exchange mode as the N-GPU bench runs it -- one process per rank under
+    torchrun, bench.py's TorchExchange, each rank's own context -- with two ranks
+    on this one GPU.  RCCL refuses two ranks on one device, so the process group
+    is gloo and the all-to-alls stage the device buffers through host copies;
+    everything else (routing kernels, slot layout, counts, capacity reruns, MAX
+    all-reduce of the containment keys, rows digest over ranks) is the N-GPU
+    path.  The union of the two ranks' rows has the reference's digest."""
+    import subprocess
+    import sys
+
+    if not os.path.exists(SCALE[name]):
+        pytest.skip(f"{name}.json not generated")
+    env = dict(os.environ, MG_BENCH_PG_BACKEND="gloo")
+    args = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+            "--master-addr", "127.0.0.1", "--master-port", "29733", os.path.join(ROOT, "bench.py"),
+            "--gpus", "2", "--config", name, "--multi", "exchange", "--steps", "1", "--warmup", "1",
+            "--no-cpu-baseline", "--no-ingest"]
+    out = subprocess.run(args, capture_output=True, text=True, timeout=800, env=env)
+    assert out.returncode == 0, out.stderr[-3000:]
+    r = json.loads([x for x in out.stdout.splitlines() if x.startswith("{")][-1])
+    assert r["n_gpus"] == 2 and r["config"]["parallelism"].startswith("2 ranks")
+    assert r["parity"]["golden"] and r["parity"]["digest_ok"] is True, r["parity"]
