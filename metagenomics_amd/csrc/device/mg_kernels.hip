@@ -471,6 +471,29 @@ __device__ __forceinline__ uint64_t run_meta(uint64_t a, int p, int jlo, int jhi
   return (a & 0xFFFFFFFFull) | ((uint64_t)p << 32) | ((uint64_t)jlo << 42) | ((uint64_t)jhi << 52);
 }
 
+// 32 bases of a lane's read starting at base `pos` (per-lane), from its words
+// in registers (pos >> 5 selected by a compare chain, not a register index,
+// which would go through scratch)
+// the same from the read's slot in HBM (no read past the slot's last word)
+template <int MAXW>
+__device__ __forceinline__ uint64_t ext_slot(const uint64_t* g, int pos) {
+  const int wi = pos >> 5;
+  return funnel(g[wi], wi + 1 < slot_words(MAXW) ? g[wi + 1] : 0ull, (pos & 31) << 1);
+}
+
+template <int MAXW>
+__device__ __forceinline__ uint64_t ext_reg(const uint64_t* rw, int pos) {
+  const int wi = pos >> 5;
+  uint64_t w0 = rw[0], w1 = rw[1];
+#pragma unroll
+  for (int k = 1; k <= MAXW; ++k) {
+    w0 = wi == k ? rw[k] : w0;
+    w1 = wi + 1 == k ? rw[k] : w1;
+  }
+  if (wi + 1 > MAXW) w1 = 0;
+  return funnel(w0, w1, (pos & 31) << 1);
+}
+
 // Window minimizers of every source read (the windows of insertAllEdgesOfRead,
 // OverlapGraph.cpp:534-537), one read per lane.  Rolling 2-bit m-mer and the
 // van Herk / Gil-Werman sliding minimum over blocks of w positions: prefix
@@ -532,18 +555,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) voi
     }
     const int J = n - h - 1;                 // windows j = 1 .. J (:534)
     const int tend = J >= 1 ? J + w - 1 : 0;  // last m-mer position a window uses
-    int tmax = tend;
-    // INDEX: the keys' windows are t < w (o = 0, 3) and t >= n - h (o = 1, 2);
-    // t_tail = the wavefront's first t >= n - h, so the steps between the two
-    // (most of them) skip the key work behind a uniform branch
-    int t_tail = tend ? n - h : 0x7FFFFFFF;
+    // INDEX: one more step, t = n - m: its window j = n - h is key o = 1's
+    const int tlast = (INDEX && tend) ? tend + 1 : tend;
+    int tmax = tlast;
 #pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) {
-      tmax = max(tmax, __shfl_xor(tmax, d));
-      if (INDEX) t_tail = min(t_tail, __shfl_xor(t_tail, d));
-    }
+    for (int d = 32; d >= 1; d >>= 1) tmax = max(tmax, __shfl_xor(tmax, d));
     tmax = __builtin_amdgcn_readfirstlane(tmax);  // wavefront-uniform loop bound
-    if (INDEX) t_tail = __builtin_amdgcn_readfirstlane(t_tail);
     // the read's words in registers (no global load inside the base loop); the
     // word holding base t + m is picked by a wavefront-uniform index
     constexpr int kRw = MAXW + 1 <= slot_words(MAXW) ? MAXW + 1 : slot_words(MAXW);
@@ -614,19 +631,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) voi
     };
     uint64_t mm = 0;
     if (tend) mm = funnel(rw[0], rw[1], 2) >> msh;  // m-mer at t = 1
-    // INDEX: best (order_key | i) and m-mer of keys o = 0..3; rcm = reverse-strand m-mer
-    uint32_t kb0 = 0xFFFFFFFFu, kb1 = 0xFFFFFFFFu, kb2 = 0xFFFFFFFFu, kb3 = 0xFFFFFFFFu;
-    uint64_t mb0 = 0, mb1 = 0, mb2 = 0, mb3 = 0, rcm = 0;
-    if (INDEX && tend) {
-      const uint64_t m0 = rw[0] >> msh;  // t = 0 (window j = 0 is no scan window)
-      rcm = rc_word(rw[0]) & mmask;
-      kb0 = order_key(m0);
-      mb0 = m0;
-      kb3 = order_key(rcm) | (uint32_t)(w - 1);
-      mb3 = rcm;
-      const uint64_t b = (((m >> 5) ? rw[1] : rw[0]) >> (62 - 2 * (m & 31))) & 3u;  // base at 0 + m (m <= 32)
-      rcm = (rcm >> 2) | ((3u - b) << (2 * m - 2));
-    }
+    // INDEX: best (order_key | i) of the keys o = 0 / 1 (hashRead's forward
+    // keys = the windows j = 0 and j = n - h of this same scan: key offset i is
+    // t shifted by a constant, so the argmin is the scan's); o = 2 / 3 come from
+    // a w-step pass over the reverse strand after the read's scan
+    uint32_t kb0 = 0xFFFFFFFFu, kb1 = 0xFFFFFFFFu;
+    if (INDEX && tend) kb0 = order_key(rw[0] >> msh);  // t = 0 (window j = 0 is no scan window)
     uint32_t pmin = 0xFFFFFFFFu;
     int last_pos = 0, jlo = 1;
     int u = 0;  // offset of t in its block of w positions
@@ -637,48 +647,25 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) voi
     auto step = [&](int t, uint64_t cw) {
       bool emit = false;
       uint64_t e_meta = 0;
-      if (t <= tend) {
-        const uint32_t hk = order_key(mm);
-        const uint32_t key = hk | (uint32_t)t;
-        if (INDEX && (t < w || t >= t_tail)) {  // wavefront-uniform
-          // the reverse-strand m-mer is rolled only inside the key windows: at
-          // the tail's first step it is derived from the forward one
-          if (t == t_tail) rcm = rc_word(mm << msh) & mmask;
-          const int i1 = t - (n - h);
-          if (t < w && key < kb0) {  // o = 0, i = t
-            kb0 = key;
-            mb0 = mm;
-          }
-          if (i1 >= 0 && (hk | (uint32_t)i1) < kb1) {  // o = 1
-            kb1 = hk | (uint32_t)i1;
-            mb1 = mm;
-          }
-          if (t < w || i1 >= 0) {
-            const uint32_t hr = order_key(rcm);
-            if (t < w && (hr | (uint32_t)(w - 1 - t)) < kb3) {  // o = 3
-              kb3 = hr | (uint32_t)(w - 1 - t);
-              mb3 = rcm;
-            }
-            if (i1 >= 0 && (hr | (uint32_t)(n - m - t)) < kb2) {  // o = 2
-              kb2 = hr | (uint32_t)(n - m - t);
-              mb2 = rcm;
-            }
-          }
-          const uint64_t b = (cw >> (62 - 2 * ((t + m) & 31))) & 3u;
-          rcm = (rcm >> 2) | ((3u - b) << (2 * m - 2));
-        }
+      if (t <= tlast) {
+        const uint32_t key = order_key(mm) | (uint32_t)t;
         pmin = (u == 0 || key < pmin) ? key : pmin;
+        if (INDEX && t == w - 1) kb0 = min(kb0, pmin);  // o = 0: t in [0, w) (wavefront-uniform)
         if (t >= w) {  // window j = t - w + 1
           const int j = t - w + 1;
           uint32_t mn = pmin;
           if (u != w - 1) mn = sv_pf < mn ? sv_pf : mn;
           const int pos = (int)(mn & 1023u);
-          if (j > 1 && pos != last_pos) {
-            emit = true;
-            e_meta = run_meta(a, last_pos, jlo, j - 1);
-            jlo = j;
+          if (INDEX && t > tend) {
+            kb1 = mn - (uint32_t)(n - h);  // o = 1: window j = n - h, i = t - (n - h)
+          } else {
+            if (j > 1 && pos != last_pos) {
+              emit = true;
+              e_meta = run_meta(a, last_pos, jlo, j - 1);
+              jlo = j;
+            }
+            last_pos = pos;
           }
-          last_pos = pos;
         }
         s_keys[u * kWave] = key;
         const int x = t + m;  // roll in the base at t + m
@@ -712,7 +699,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) voi
       // windows, measured slower: scan 3.55 vs 2.95 ms at 6 waves, its extra
       // registers spill; 3.06 ms at 5 waves.)
 #pragma unroll
-      for (int k = 0; k < MAXW; ++k) {
+      for (int k = 0; k < MAXW + (INDEX ? 1 : 0); ++k) {  // (INDEX's step t = n - m rolls in base n)
         const int t0 = max(1, 32 * k - m), t1 = min(tmax, 32 * k + 31 - m);
         for (int t = t0; t <= t1; ++t) step(t, rw[k]);
       }
@@ -728,21 +715,42 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) voi
     put(tend > 0, run_meta(a, last_pos, jlo, J));  // each read's last run
     while (nbuf) flush(nbuf < (uint32_t)kWave ? nbuf : (uint32_t)kWave);  // the group's runs leave with its registers
     if (INDEX && tend) {
-      // t = n-m, one past the last window position: the rolled m-mer sits there
-      // (the reverse one is derived: the lane's tail may have been cut short)
-      rcm = rc_word(mm << msh) & mmask;
-      const uint32_t hk = order_key(mm), hr = order_key(rcm);
-      if ((hk | (uint32_t)(w - 1)) < kb1) {
-        kb1 = hk | (uint32_t)(w - 1);
-        mb1 = mm;
+      // o = 3 (R[n-h, n) = rc F[0, h): m-mer i = rc of F's at t = w-1-i) and
+      // o = 2 (R[0, h) = rc F[n-h, n): m-mer i = rc of F's at t = n-m-i), both
+      // rolled towards smaller t, one base per step, w steps for every lane
+      uint32_t kb2 = 0xFFFFFFFFu, kb3 = 0xFFFFFFFFu;
+      const bool w32 = w <= 32;  // (wavefront-uniform) every key base within 32 of its start
+      if (w32) {
+        const uint64_t Aw = ext_reg<MAXW>(rw, n - h);                      // F[n-h, n-h+32)
+        uint64_t r3 = rc_word(funnel(rw[0], rw[1], 2 * (w - 1))) & mmask;  // rc(F[w-1, w-1+m))
+        uint64_t r2 = rc_word(ext_reg<MAXW>(rw, n - m)) & mmask;          // rc(F[n-m, n))
+        for (int i = 0; i < w; ++i) {
+          kb3 = min(kb3, order_key(r3) | (uint32_t)i);
+          kb2 = min(kb2, order_key(r2) | (uint32_t)i);
+          const int t3 = w - 2 - i;  // the base entering: F[t3] (o = 3), F[n-h + t3] (o = 2)
+          if (t3 >= 0) {
+            r3 = ((r3 << 2) | (3u - ((rw[0] >> (62 - 2 * t3)) & 3u))) & mmask;
+            r2 = ((r2 << 2) | (3u - ((Aw >> (62 - 2 * t3)) & 3u))) & mmask;
+          }
+        }
+      } else {  // long keys: each m-mer read from the slot (slow, correct; off the hot path)
+        const uint64_t* gk = p.words + a * slot_words(MAXW);
+        for (int i = 0; i < w; ++i) {
+          kb3 = min(kb3, order_key(rc_word(ext_slot<MAXW>(gk, w - 1 - i)) & mmask) | (uint32_t)i);
+          kb2 = min(kb2, order_key(rc_word(ext_slot<MAXW>(gk, n - m - i)) & mmask) | (uint32_t)i);
+        }
       }
-      if (hr < kb2) {  // i = 0
-        kb2 = hr;
-        mb2 = rcm;
-      }
+      // the minimizer m-mers from their offsets: o = 0 / 3 at forward t = i /
+      // w - 1 - i, o = 1 / 2 at n - h + i / n - m - i
       const uint64_t nbm = (1ULL << p.nb_log2) - 1;
       const uint32_t kb[4] = {kb0, kb1, kb2, kb3};
-      const uint64_t mb[4] = {mb0, mb1, mb2, mb3};
+      const int i0 = (int)(kb0 & 1023u), i1 = (int)(kb1 & 1023u), i2 = (int)(kb2 & 1023u), i3 = (int)(kb3 & 1023u);
+      const uint64_t f0 = w32 ? funnel(rw[0], rw[1], i0 << 1) : ext_reg<MAXW>(rw, i0);
+      const uint64_t f3 = w32 ? funnel(rw[0], rw[1], (w - 1 - i3) << 1) : ext_reg<MAXW>(rw, w - 1 - i3);
+      const uint64_t mb[4] = {f0 >> msh, ext_reg<MAXW>(rw, n - h + i1) >> msh,
+                              rc_word(ext_reg<MAXW>(rw, n - m - i2)) & mmask, rc_word(f3) & mmask};
+      uint64_t cb[4];
+      unsigned long long ce[4];
 #pragma unroll
       for (int o = 0; o < 4; ++o) {
         const uint64_t v = mix64(mb[o]);
@@ -751,9 +759,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) voi
         if constexpr (KEYREC) {  // o-major: each store is one coalesced wavefront line
           p.key_bk[o * p.key_n + a] = (uint32_t)(v & nbm);
           p.key_ent[o * p.key_n + a] = e;
-        } else {
-          cell_insert(p.cells, v & nbm, p.cell_n, e);
         }
+        cb[o] = v & nbm;
+        ce[o] = e;
+      }
+      // (the four inserts with their cell loads and CASes in flight together
+      // measured slower: scan 3.06-3.13 vs 2.92-2.94 ms at C3, profiles/r03y_ab_scan.txt)
+      if constexpr (!KEYREC) {
+#pragma unroll
+        for (int o = 0; o < 4; ++o) cell_insert(p.cells, cb[o], p.cell_n, ce[o]);
       }
     } else if (INDEX && a < p.a_hi) {  // no keys (n <= l cannot pass setup_index): holes
       if (p.key0) p.key0[a] = kEmpty;
@@ -835,22 +849,6 @@ struct RunStage {
     if (lane == 0) p.run_cnt[gw] = cursor;
   }
 };
-
-// 32 bases of a lane's read starting at base `pos` (per-lane), from its words
-// in registers (pos >> 5 selected by a compare chain, not a register index,
-// which would go through scratch)
-template <int MAXW>
-__device__ __forceinline__ uint64_t ext_reg(const uint64_t* rw, int pos) {
-  const int wi = pos >> 5;
-  uint64_t w0 = rw[0], w1 = rw[1];
-#pragma unroll
-  for (int k = 1; k <= MAXW; ++k) {
-    w0 = wi == k ? rw[k] : w0;
-    w1 = wi + 1 == k ? rw[k] : w1;
-  }
-  if (wi + 1 > MAXW) w1 = 0;
-  return funnel(w0, w1, (pos & 31) << 1);
-}
 
 constexpr int kRegW = 32;       // largest w (= h - m + 1) of the register scan
 constexpr int kStageEvery = 6;  // register scan: flush check every kStageEvery bases (< 64 + 6 * 64 staged)
@@ -1231,10 +1229,19 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MG_PROBE
         idb = p.id[bid];
       }
     }
-    if (have) {
+    if (have) {  // the source's words, 16 B per load where the slot allows
       const uint64_t* g = p.words + (uint64_t)sa * slot_words(MAXW);
+      if constexpr (slot_words(MAXW) < 2) {
+        s_a[lane] = g[0];
+      } else {
+        const ulonglong2* gp = reinterpret_cast<const ulonglong2*>(g);
 #pragma unroll
-      for (int k = 0; k < MAXW; ++k) s_a[k * kWave + lane] = g[k];
+        for (int k = 0; k < (MAXW + 1) / 2; ++k) {
+          const ulonglong2 x = gp[k];
+          s_a[2 * k * kWave + lane] = x.x;
+          if (2 * k + 1 < MAXW) s_a[(2 * k + 1) * kWave + lane] = x.y;
+        }
+      }
       s_a[MAXW * kWave + lane] = 0;
     }
     wave_sync();
