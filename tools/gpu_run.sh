@@ -89,7 +89,7 @@ for s in $STEPS; do
     timeout -k 10 300 python -u bench.py --config c5s --no-cpu-baseline --no-ingest > $OUT/bench_c5s.json 2> $OUT/bench_c5s.err
     rc=$?; echo "bench c5s rc=$rc"; cat $OUT/bench_c5s.json ;;
   prof)
-    timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o kt -- python3 bench.py --steps 5 --no-cpu-baseline > $OUT/prof_bench.json 2> $OUT/prof_bench.err
+    timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o kt -- python3 bench.py --steps 5 --no-cpu-baseline --no-ingest --no-one-shot > $OUT/prof_bench.json 2> $OUT/prof_bench.err
     rc=$?; echo "prof rc=$rc"; cat $OUT/prof_bench.json; head -8 $OUT/prof/kt_kernel_stats.csv | cut -c1-200 ;;
   profsim)
     timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/profsim -o kt -- python3 bench.py --sim-world 4 --multi exchange --steps 2 --no-cpu-baseline > $OUT/profsim_bench.json 2> $OUT/profsim_bench.err
@@ -99,24 +99,24 @@ for s in $STEPS; do
     for set in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY SQ_INSTS_VALU SQ_INSTS_VMEM_RD" \
                "SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_WR SQ_LDS_BANK_CONFLICT TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE"; do
       i=$((i+1))
-      timeout -s KILL 300 rocprofv3 --pmc $set --kernel-trace --output-format csv -d $OUT/pmcsq_$i -o p -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline > $OUT/pmcsq_$i.log 2>&1
+      timeout -s KILL 300 rocprofv3 --pmc $set --kernel-trace --output-format csv -d $OUT/pmcsq_$i -o p -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-ingest --no-one-shot > $OUT/pmcsq_$i.log 2>&1
       rc=$?; echo "pmcsq $i rc=$rc"; [ $rc -ne 0 ] && break
     done
     [ $rc -eq 0 ] && python3 tools/pmc_summary.py $OUT/pmcsq_summary.json $OUT/pmcsq_* > /dev/null ;;
   pmc)
     for set in "FETCH_SIZE" "WRITE_SIZE"; do
-      timeout -s KILL 300 rocprofv3 --pmc $set --kernel-trace --output-format csv -d $OUT/pmc_$set -o p -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-ingest > $OUT/pmc_$set.log 2>&1
+      timeout -s KILL 300 rocprofv3 --pmc $set --kernel-trace --output-format csv -d $OUT/pmc_$set -o p -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-ingest --no-one-shot > $OUT/pmc_$set.log 2>&1
       rc=$?; echo "pmc $set rc=$rc"; [ $rc -ne 0 ] && break
     done
     [ $rc -eq 0 ] && python3 tools/pmc_summary.py $OUT/pmc_summary.json $OUT/pmc_* > /dev/null ;;
   pmc5)
     for set in "FETCH_SIZE" "WRITE_SIZE"; do
-      timeout -s KILL 400 rocprofv3 --pmc $set --kernel-trace --output-format csv -d $OUT/pmc5_$set -o p -- python3 bench.py --config c5 --steps 1 --warmup 0 --no-cpu-baseline --no-ingest > $OUT/pmc5_$set.log 2>&1
+      timeout -s KILL 400 rocprofv3 --pmc $set --kernel-trace --output-format csv -d $OUT/pmc5_$set -o p -- python3 bench.py --config c5 --steps 1 --warmup 0 --no-cpu-baseline --no-ingest --no-one-shot > $OUT/pmc5_$set.log 2>&1
       rc=$?; echo "pmc5 $set rc=$rc"; [ $rc -ne 0 ] && break
     done
     [ $rc -eq 0 ] && python3 tools/pmc_summary.py $OUT/pmc5_summary.json $OUT/pmc5_* > /dev/null ;;
   prof5)
-    timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof5 -o kt -- python3 bench.py --config c5 --steps 2 --no-cpu-baseline --no-ingest > $OUT/prof5_bench.json 2> $OUT/prof5_bench.err
+    timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof5 -o kt -- python3 bench.py --config c5 --steps 2 --no-cpu-baseline --no-ingest --no-one-shot > $OUT/prof5_bench.json 2> $OUT/prof5_bench.err
     rc=$?; echo "prof5 rc=$rc"; head -10 $OUT/prof5/kt_kernel_stats.csv | cut -c1-160 ;;
   *) echo "unknown step $s"; rc=2 ;;
   esac
