@@ -505,14 +505,17 @@ __device__ __forceinline__ uint64_t ext_reg(const uint64_t* rw, int pos) {
 // control flow is uniform across lanes.  A run ends where the minimizer
 // position changes; its record goes straight to HBM (ballot-compacted).
 // INDEX: the same pass also builds the index (HashTable::insertDataset,
-// HashTable.cpp:50-80): the four keys of every read (hashRead :88-104) are the
-// windows at the ends of the read on both strands, so their minimizers come
-// from the m-mers this loop already rolls (plus the reverse-strand m-mer rolled
-// alongside): o=0 forward t in [0, w), i = t; o=1 forward t in [n-h, n-m],
-// i = t-(n-h); o=2 reverse t in [n-h, n-m], i = n-m-t; o=3 reverse t in
-// [0, w), i = w-1-t.  Same keys (order_key | i) as key_minimizer, so lookups
-// and the exchange mode's k_key_records agree.  The CAS inserts of a read's
-// four keys overlap the ALU-bound scan of the other wavefronts.
+// HashTable.cpp:50-80).  The four keys of a read (hashRead :88-104) are the
+// windows at its two ends on both strands: o = 0 is window j = 0 (its prefix
+// minimum at t = w - 1 and the m-mer at t = 0), o = 1 is window j = n - h (one
+// extra step, t = n - m, that emits no run), each with the key offset i = t
+// shifted by a constant, so the argmin is the scan's; o = 2 / 3 come from a
+// w-step pass over the reverse strand's m-mers after the read (uniform trip
+// count, no per-step key work in the base loop: C5's mixed lengths kept the
+// key branch of the old in-step version open for most steps).  Same keys
+// (order_key | i) as key_minimizer, so lookups and the exchange mode's key
+// records agree.  The CAS inserts of a read's four keys overlap the ALU-bound
+// scan of the other wavefronts.
 // 6 waves per SIMD (the LDS limit: 6 blocks of 4 wavefronts per CU): 80 VGPRs
 // with a 12-B spill beat 83 VGPRs / 5 waves, index 3.72 vs 3.93 ms at C3
 // (profiles/r01s5_ab_scan_waves.log)
@@ -1137,10 +1140,11 @@ struct ProbeLds {
 // (ballot + mbcnt per slot) and are verified one per lane against the
 // partner's slot in HBM; a full cell's chain flag turns the lane's item into a
 // pending item (LDS) that a later batch probes at the next cell.
-// MG_PROBE_WAVES: minimum waves per SIMD asked of the register allocator
-// (1 = its own choice; A/B builds, tools/ab_libs.sh)
+// Waves per SIMD asked of the register allocator: 4 (128 VGPRs) where the
+// probe fits them without spilling (reads up to 5 words), else its own choice
+// (3 waves at 129-143 VGPRs).  MG_PROBE_WAVES overrides (A/B builds).
 #ifndef MG_PROBE_WAVES
-#define MG_PROBE_WAVES 1
+#define MG_PROBE_WAVES (MAXW <= 5 ? 4 : 1)
 #endif
 template <int MAXW, bool CONTAIN>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MG_PROBE_WAVES))) void k_probe(ProbeParams p) {
@@ -1161,8 +1165,17 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MG_PROBE
   const uint32_t seg = (uint32_t)(gw & (kSegs - 1));
   uint32_t* const region = p.rows + gw * p.reg_cap * 3;
   uint64_t cursor = 0;
-  uint32_t st_runs = 0, st_ent = 0, st_ver = 0, st_rows = 0;
   uint32_t ncand = 0, npend = 0;
+  // diagnostics (p.stats): wavefront sum of a per-lane count into counter i
+  // (runs probed, entries scanned, partners fetched, rows); call converged.
+  // No per-lane counters stay live across the loop (registers: occupancy)
+  auto stat = [&](int i, uint32_t v) {
+    if (p.stats) {
+#pragma unroll
+      for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d);
+      if (lane == 0) atomicAdd(&p.stats[seg * 4 + i], (unsigned long long)v);
+    }
+  };
 
   // verify the first nc (<= 64) candidates of the list, one per lane
   auto verify = [&](uint32_t nc) {
@@ -1245,13 +1258,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MG_PROBE
       s_a[MAXW * kWave + lane] = 0;
     }
     wave_sync();
+    uint32_t nhit = 0;
     if (cond) {
-      ++st_ver;
       const uint64_t diff = overlap_diff<MAXW, kWave>(s_a + lane, n1, x0, y0, L, rcA, y);
       if (diff == 0) {
         if (CONTAIN) {
           atomicMax(&p.superkey[bid], ((unsigned long long)n1 << 32) | (0xFFFFFFFFu - ida));
-          ++st_rows;
+          nhit = 1;
         } else if (!(p.super && p.super[bid])) {  // :548 read2 contained
           // orientation/offset switch (:550-557) and the twin (:409-412, :841-855)
           const uint32_t orient = (o == 0) ? 3u : (o == 2 ? 2u : 1u);
@@ -1261,10 +1274,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MG_PROBE
           r0 = ida + 1; r1 = idb + 1; r2 = (orient << 16) | off;
           t0 = idb + 1; t1 = ida + 1; t2 = (torient << 16) | toff;
           nrec = (bid == sa && o == 0) ? 4 : 2;  // self o=0 hit also stands for its o=1 twin
-          st_rows += nrec;
+          nhit = (uint32_t)nrec;
         }
       }
     }
+    stat(2, cond ? 1u : 0u);
+    stat(3, nhit);
     if (!CONTAIN) {
       const uint64_t b2 = __ballot(nrec >= 2), b4 = __ballot(nrec == 4);
       const uint32_t tot = 2u * (uint32_t)(__popcll(b2) + __popcll(b4));
@@ -1360,7 +1375,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MG_PROBE
           valid = false;
       }
       key = (valid ? bucket - p.cell_lo : 0) | ((uint64_t)fpv << 32);
-      if (valid) ++st_runs;
+      stat(0, valid ? 1u : 0u);
       rpos += rstep;
       pf_any = hbm_settle();
       if (p.compact && npend < (uint32_t)kWave) {
@@ -1437,8 +1452,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MG_PROBE
     const int rjlo = (int)((meta >> 42) & 1023u), rjhi = (int)((meta >> 52) & 1023u);
     const uint32_t fp = (uint32_t)(key >> 32);
     if (p.stats) {
+      uint32_t ne = 0;
 #pragma unroll
-      for (int s = 0; s < kCell; ++s) st_ent += e[s] != kEmpty ? 1u : 0u;
+      for (int s = 0; s < kCell; ++s) ne += e[s] != kEmpty ? 1u : 0u;
+      stat(1, ne);
     }
     if (p.phase_limit <= 5) return;
     // a full cell's chain flag: probe the next cell in a later batch
@@ -1531,16 +1548,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MG_PROBE
   }
   if (ncand && p.phase_limit > 6) verify(ncand);
   if (!CONTAIN && lane == 0) p.reg_cnt[gw] = cursor;
-  if (p.stats) {
-    uint32_t v[4] = {st_runs, st_ent, st_ver, st_rows};
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      uint32_t x = v[i];
-#pragma unroll
-      for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d);
-      if (lane == 0) atomicAdd(&p.stats[seg * 4 + i], (unsigned long long)x);
-    }
-  }
 }
 
 // Gather per-wavefront row regions into a contiguous array (copy-out path only).
