@@ -3211,6 +3211,14 @@ static int sort_xrecs(mg_ctx* ctx, const ulonglong2* recv, uint64_t slot, uint32
     hipLaunchKernelGGL(k_xruns_keys, dim3(grid), dim3(kBlock), 0, ctx->stream, recv, slot, P, total, counts,
                        (1ULL << ctx->nb_log2) - 1, ctx->cell_lo, shift, ctx->d_xk[0], ctx->d_xv[0]);
     MG_TRY(hipGetLastError());
+    // one rank: its one stream is its own scan's runs in scan order, which the
+    // fused path probes unsorted (the clustered layout's locality); a bucket
+    // order only pays for merging the streams of several senders (one RCCL
+    // rank at C3: 15.0 -> 13.8 ms per step)
+    if (P == 1) {
+      *n_out = n;
+      return 0;
+    }
     rocprim::double_buffer<uint32_t> keys(ctx->d_xk[0], ctx->d_xk[1]);
     rocprim::double_buffer<ulonglong2> vals(ctx->d_xv[0], ctx->d_xv[1]);
     size_t tb = 0;
