@@ -192,7 +192,10 @@ def one_shot(e, ds, fused_step, device, rows):
         out.update(id_order_step_ms=ms0, id_order_one_shot_ms=ms0)
     finally:
         e0.close()
-    out["default"] = "layout" if out["one_shot_ms"] <= out["id_order_one_shot_ms"] else "id_order"
+    # which one-shot is faster here, beside the library's default slot order
+    # (clustered: every later step over the same upload runs ~25 % faster)
+    out["faster_one_shot"] = "layout" if out["one_shot_ms"] <= out["id_order_one_shot_ms"] else "id_order"
+    out["default"] = "layout"
     return out
 
 

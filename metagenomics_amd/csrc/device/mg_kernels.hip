@@ -3726,8 +3726,10 @@ int mg_finalize_contained(mg_ctx* ctx, uint32_t* super_out) {
     if (ctx->n)
       MG_TRY(hipMemcpyAsync(super_out + 1, super_in_id_order(ctx), ctx->n * sizeof(uint32_t), hipMemcpyDeviceToHost,
                             ctx->stream));
+    MG_TRY(hipStreamSynchronize(ctx->stream));
   }
-  MG_TRY(hipStreamSynchronize(ctx->stream));
+  // (equal lengths and no copy: nothing to wait for; the exchange step keeps
+  // its queue full through this call)
   return 0;
 }
 
