@@ -148,6 +148,12 @@ __global__ __launch_bounds__(kBlock) void k_pack_ascii(const char* __restrict__ 
 constexpr int kWaitVm0 = 0x0F70;
 constexpr int kCell = 8;
 constexpr int kScanBuf = 3 * 64;  // staged run metas per scan wavefront (two puts per step: < 64 + 128)
+// k_scan<..., G> takes its reads in windows of G groups of 64 consecutive
+// slots, one pass of 64 reads of similar length at a time (longest first); the
+// runs of group j of a window go to the wavefront's run region j (G regions
+// per wave).  G = kWinGroups for the fused index scan of mixed lengths, 1
+// (one group, no sort) otherwise.
+constexpr int kWinGroups = 4;
 constexpr int kStageRing = 512;   // register scan: LDS ring of staged run metas per wavefront
 constexpr uint64_t kEmpty = ~0ULL;       // free slot (a read index is never 0xFFFFFFFF)
 constexpr uint64_t kChain = 1ULL << 63;  // on a cell's last slot: the chain continues in the next cell
@@ -522,7 +528,7 @@ __device__ __forceinline__ uint64_t ext_reg(const uint64_t* rw, int pos) {
 // KEYREC (exchange mode with w > 32, INDEX only): key records for the bucket
 // owners instead of CAS inserts.  Each instantiation references only the
 // parameters it uses, which keeps its scalar registers below the limit.
-template <int MAXW, bool INDEX, bool KEYREC = false>
+template <int MAXW, bool INDEX, bool KEYREC = false, int G = 1>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) void k_scan(ScanParams p) {
   extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -536,26 +542,88 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) voi
   const uint64_t nw = (uint64_t)gridDim.x * wpb;
   uint64_t* s_buf = reinterpret_cast<uint64_t*>(smem) + (size_t)wpb * ((w * kWave + 1) / 2) +
                     (size_t)wv * kScanBuf;
-  ulonglong2* region = p.runs + gw * p.run_cap;
+  // region j of this wavefront (= run region G gw + j) holds the runs
+  // of group j of each of its windows: a probe block's share of G
+  // consecutive regions then covers consecutive slots, as with one group per
+  // region
+  ulonglong2* const region = p.runs + gw * G * p.run_cap;
   const uint64_t nbmask = (1ULL << p.nb_log2) - 1;
-  uint64_t cursor = 0;
+  uint64_t cur[G] = {};  // records per region (wavefront-uniform)
   uint32_t nbuf = 0;  // run metas staged in s_buf (wavefront-uniform)
 
   // close the run of minimizer position pos over windows [jlo, jhi]: stage its
-  // meta in LDS (the hashing and the HBM write happen 64 at a time in flush)
+  // meta in LDS (the hashing and the HBM write happen 64 at a time in flush);
+  // staged metas carry (owner lane << 8 | slot within the window) where the
+  // record will carry the read index
   auto put = [&](bool flag, uint64_t meta) {
     const uint64_t bal = __ballot(flag);
     if (flag) s_buf[nbuf + lane_prefix(bal)] = meta;
     nbuf += (uint32_t)__popcll(bal);
   };
-  for (uint64_t grp = gw; grp < ngroups; grp += nw) {
-    const uint64_t a = p.a_lo + grp * kWave + lane;
-    int n = 0;
-    const uint64_t* g = p.words + a * slot_words(MAXW);
-    if (a < p.a_hi) {
-      n = (int)p.len[a];
-      if (!INDEX && n && p.super && p.super[a]) n = 0;  // (an index scan covers every source)
+  const uint64_t nwin = (ngroups + G - 1) / G;
+  for (uint64_t win = gw; win < nwin; win += nw) {
+   const uint64_t A0 = p.a_lo + win * (G * kWave);  // the window's first slot
+   // (length, slot) of the window's reads, ascending: pass q takes ranks
+   // [64 q, 64 q + 64), so each pass's base loop runs to about its own
+   // longest read instead of every group's (mixed lengths: lanes idle less)
+   uint32_t wk[G];
+   uint32_t lmin = 0xFFFFFFFFu, lmax = 0;
+#pragma unroll
+   for (int q = 0; q < G; ++q) {
+     const uint32_t idx = (uint32_t)(lane + kWave * q);
+     const uint64_t a = A0 + idx;
+     uint32_t n = 0;
+     if (a < p.a_hi) {
+       n = p.len[a];
+       if (!INDEX && n && p.super && p.super[a]) n = 0;  // (an index scan covers every source)
+     }
+     wk[q] = ((0x7FFu - n) << 8) | idx;  // longest first: containers before their contents
+     lmin = min(lmin, n);
+     lmax = max(lmax, n);
+   }
+   if constexpr (G > 1) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+      lmin = min(lmin, (uint32_t)__shfl_xor((int)lmin, d));
+      lmax = max(lmax, (uint32_t)__shfl_xor((int)lmax, d));
     }
+   }
+   if (G > 1 && __builtin_amdgcn_readfirstlane(lmin) != __builtin_amdgcn_readfirstlane(lmax)) {
+     // bitonic sort of the 256 keys, element e = lane + 64 q in wk[q]
+#pragma unroll
+     for (int k = 2; k <= G * kWave; k <<= 1) {
+#pragma unroll
+       for (int j = k >> 1; j > 0; j >>= 1) {
+#pragma unroll
+         for (int q = 0; q < G; ++q) {
+           const int e = lane + kWave * q;
+           const bool up = (e & k) == 0;
+           if (j >= kWave) {  // partner in this lane's own registers
+             const int q2 = q ^ (j / kWave);
+             if (q < q2) {
+               const uint32_t x = wk[q], y = wk[q2];
+               const bool sw = up ? x > y : x < y;
+               wk[q] = sw ? y : x;
+               wk[q2] = sw ? x : y;
+             }
+           } else {
+             const uint32_t o = (uint32_t)__shfl_xor((int)wk[q], j);
+             const bool low = (e & j) == 0;
+             wk[q] = (low == up) ? min(wk[q], o) : max(wk[q], o);
+           }
+         }
+       }
+     }
+   }
+   for (int q = 0; q < G; ++q) {  // one pass of 64 reads (not unrolled: code size)
+    uint32_t key = wk[0];
+#pragma unroll
+    for (int qq = 1; qq < G; ++qq) key = q == qq ? wk[qq] : key;
+    const uint32_t wslot = key & 255u;
+    const uint64_t a = A0 + wslot;
+    const int n = (int)(0x7FFu - (key >> 8));
+    const uint64_t own = G > 1 ? ((uint64_t)lane << 8) | wslot : a;  // a staged run's read (see put)
+    const uint64_t* g = p.words + a * slot_words(MAXW);
     const int J = n - h - 1;                 // windows j = 1 .. J (:534)
     const int tend = J >= 1 ? J + w - 1 : 0;  // last m-mer position a window uses
     // INDEX: one more step, t = n - m: its window j = n - h is key o = 1's
@@ -584,20 +652,23 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) voi
       for (int k = 1; k <= MAXW; ++k) v = idx == k ? rw[k] : v;
       return v;
     };
-    const uint64_t a0 = p.a_lo + grp * kWave;  // lane l holds read a0 + l
     // hash the first k (<= 64) staged runs with every lane busy, drop runs whose
-    // bucket another rank owns, write full-wavefront 16-B records
+    // bucket another rank owns, write full-wavefront 16-B records into the
+    // region of each run's group
     auto flush = [&](uint32_t k) {
       wave_sync();
       bool flag = (uint32_t)lane < k;
       uint64_t v = 0, meta = 0;
       if (flag) meta = s_buf[lane];
+      // slot within the window; G > 1 stages (lane << 8 | slot) for the read index
+      const uint32_t ws = G > 1 ? (uint32_t)meta & 255u : (uint32_t)meta - (uint32_t)A0;
+      if (G > 1) meta = (meta & ~0xFFFFFFFFull) | (uint32_t)(A0 + ws);
       if constexpr (MAXW <= 8) {
-        // every staged run belongs to a read of this group (flushed before the
-        // next group): its words come from the owner lane's registers, not HBM
+        // every staged run belongs to a read of this pass (flushed before the
+        // next pass): its words come from the owner lane's registers, not HBM
         // (a global load here made every flush wait for the earlier stores)
         const int pos = (int)((meta >> 32) & 1023u), wi = pos >> 5;
-        const int src = flag ? (int)((uint32_t)meta - (uint32_t)a0) : lane;
+        const int src = !flag ? lane : G > 1 ? (int)((uint32_t)s_buf[lane] >> 8 & 63u) : (int)ws;
         uint64_t w0 = 0, w1 = 0;
   #pragma unroll
         for (int kk = 0; kk <= MAXW; ++kk) {
@@ -617,12 +688,22 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) voi
         v = mix64(funnel(g2[pos >> 5], g2[(pos >> 5) + 1], (pos & 31) << 1) >> msh);
         if (!INDEX) flag = owned(v & nbmask, p.nb_log2, p.rank, p.nranks);
       }
-      const uint64_t bal = __ballot(flag);
-      if (flag) {
-        const uint64_t at = cursor + lane_prefix(bal);
-        if (at < p.run_cap) region[at] = make_ulonglong2(v, meta);
+      if constexpr (G == 1) {
+        const uint64_t bal = __ballot(flag);
+        const uint64_t at = cur[0] + lane_prefix(bal);
+        if (flag && at < p.run_cap) region[at] = make_ulonglong2(v, meta);
+        cur[0] += (uint64_t)__popcll(bal);
+      } else {
+        const uint32_t grp = ws >> 6;  // the run's group in the window
+        uint64_t at = 0;
+#pragma unroll
+        for (int j = 0; j < G; ++j) {
+          const uint64_t bal = __ballot(flag && grp == (uint32_t)j);
+          if (grp == (uint32_t)j) at = cur[j] + lane_prefix(bal);
+          cur[j] += (uint64_t)__popcll(bal);
+        }
+        if (flag && at < p.run_cap) region[grp * p.run_cap + at] = make_ulonglong2(v, meta);
       }
-      cursor += (uint64_t)__popcll(bal);
       const uint32_t rest = nbuf - k;  // < 128 left: move them to the front
       const uint64_t m0 = (uint32_t)lane < rest ? s_buf[k + lane] : 0;
       const uint64_t m1 = (uint32_t)lane + kWave < rest ? s_buf[k + kWave + lane] : 0;
@@ -664,7 +745,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) voi
           } else {
             if (j > 1 && pos != last_pos) {
               emit = true;
-              e_meta = run_meta(a, last_pos, jlo, j - 1);
+              e_meta = run_meta(own, last_pos, jlo, j - 1);
               jlo = j;
             }
             last_pos = pos;
@@ -715,7 +796,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) voi
         if ((xu & 31) == 31) cw = word_at((xu + 1) >> 5);  // next word (don't-care past a read's end)
       }
     }
-    put(tend > 0, run_meta(a, last_pos, jlo, J));  // each read's last run
+    put(tend > 0, run_meta(own, last_pos, jlo, J));  // each read's last run
     while (nbuf) flush(nbuf < (uint32_t)kWave ? nbuf : (uint32_t)kWave);  // the group's runs leave with its registers
     if (INDEX && tend) {
       // o = 3 (R[n-h, n) = rc F[0, h): m-mer i = rc of F's at t = w-1-i) and
@@ -781,8 +862,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) voi
         }
       }
     }
+   }
   }
-  if (lane == 0) p.run_cnt[gw] = cursor;
+  uint64_t c = cur[0];
+#pragma unroll
+  for (int j = 1; j < G; ++j) c = lane == j ? cur[j] : c;
+  if (lane < G) p.run_cnt[gw * G + lane] = c;
 }
 
 // ---------------------------------------------------------------------------
@@ -2315,6 +2400,11 @@ inline uint32_t scan_wpb(uint32_t w) {
 inline bool scan_is_reg(const mg_ctx* ctx, bool index) {
   return ctx->w <= (uint32_t)kRegW && (!index || ctx->xchg);
 }
+// groups per k_scan window (one run region each): the fused index scan of
+// mixed lengths ranks each window's reads by length (kWinGroups); else 1
+inline int scan_windows(const mg_ctx* ctx, bool index) {
+  return (index && !ctx->xchg && ctx->minlen != ctx->maxlen && !scan_is_reg(ctx, index)) ? kWinGroups : 1;
+}
 inline uint32_t scan_block_waves(const mg_ctx* ctx, bool index) {
   return scan_is_reg(ctx, index) ? kWavesPerBlock : scan_wpb(ctx->w);
 }
@@ -2329,7 +2419,8 @@ uint32_t scan_resident(mg_ctx* ctx, bool index, uint64_t want) {
   if (scan_is_reg(ctx, index))
     return index ? resident_blocks(ctx, k_scan_reg<W, true>, lds, want, block)
                  : resident_blocks(ctx, k_scan_reg<W, false>, lds, want, block);
-  return index ? resident_blocks(ctx, k_scan<W, true>, lds, want, block)
+  return index ? (scan_windows(ctx, index) > 1 ? resident_blocks(ctx, k_scan<W, true, false, kWinGroups>, lds, want, block)
+                                                : resident_blocks(ctx, k_scan<W, true>, lds, want, block))
                : resident_blocks(ctx, k_scan<W, false>, lds, want, block);
 }
 
@@ -2366,14 +2457,16 @@ struct LaunchScan {
                  hipStream_t stream = nullptr, bool no_super = false, bool index = false) {
     if (!stream) stream = ctx->stream;
     const uint32_t wpb = scan_block_waves(ctx, index);
-    const uint64_t nw = (uint64_t)sgrid * wpb;  // scan wavefronts = run regions
+    const uint64_t nw = (uint64_t)sgrid * wpb;  // scan wavefronts
     const uint64_t ngroups = (a_hi - a_lo + kWave - 1) / kWave;
-    const uint64_t nreg = nw;
+    // run regions: one per register-scan wavefront, one per window group of k_scan's
+    const uint64_t G = scan_is_reg(ctx, index) ? 1 : (uint64_t)scan_windows(ctx, index);
+    const uint64_t nreg = nw * G;
     ctx->nrun_reg = nreg;
     // expected runs per read ~ 2 J / (w + 1) + 1 (minimizer density)
     const uint64_t J = ctx->maxlen > ctx->h + 1 ? ctx->maxlen - ctx->h - 1 : 1;
     const uint64_t per_read = std::min<uint64_t>(J, 3 * (2 * J / (ctx->w + 1) + 2));
-    const uint64_t groups_per_region = (ngroups + nw - 1) / nw;
+    const uint64_t groups_per_region = ((ngroups + G - 1) / G + nw - 1) / nw;  // windows per wave
     uint64_t run_cap = std::max<uint64_t>(
         ctx->run_cap_need, ctx->run_cap_opt ? ctx->run_cap_opt : groups_per_region * kWave * per_read);
     if (run_cap * nreg > ctx->runs_cap) {
@@ -2432,6 +2525,9 @@ struct LaunchScan {
     } else if (index && ctx->xchg) {
       allow_lds(k_scan<W, true, true>, lds);
       hipLaunchKernelGGL((k_scan<W, true, true>), dim3(sgrid), dim3(wpb * kWave), lds, stream, sp);
+    } else if (index && G > 1) {
+      allow_lds(k_scan<W, true, false, kWinGroups>, lds);
+      hipLaunchKernelGGL((k_scan<W, true, false, kWinGroups>), dim3(sgrid), dim3(wpb * kWave), lds, stream, sp);
     } else if (index) {
       allow_lds(k_scan<W, true>, lds);
       hipLaunchKernelGGL((k_scan<W, true>), dim3(sgrid), dim3(wpb * kWave), lds, stream, sp);
