@@ -70,6 +70,11 @@ struct mg_ctx {
   unsigned long long* d_superkey = nullptr;
   unsigned long long* superkey = nullptr;  // the containment key array in use (d_superkey or caller-owned)
   uint32_t* d_super = nullptr;
+  // contained slots as a bitmap (bit a of word a / 32 = d_super[a] != 0,
+  // k_super_finalize): the discovery probe drops contained partners before
+  // they take a verification (:548), from a 1/32-size array that stays in cache
+  uint32_t* d_cbits = nullptr;
+  size_t cbits_cap = 0;
   unsigned int* d_any = nullptr;
   unsigned long long* d_digest = nullptr;  // mg_rows_digest / mg_super_digest accumulators (4 u64)
   size_t super_cap = 0, superkey_cap = 0;

@@ -1163,7 +1163,7 @@ struct ProbeParams {
   uint32_t rank, nranks;
   uint64_t cell_lo, cell_n;       // local bucket range of the cell table (IndexParams)
   const uint64_t* cells;
-  const uint32_t* super;          // superReadID per read index (nullptr: none contained)
+  const uint32_t* cbits;          // discovery: contained slots as bits (mg_ctx::d_cbits; nullptr: none contained)
   unsigned long long* superkey;   // CONTAIN: max over containers of (len << 32 | ~index)
   const ulonglong2* runs;
   const unsigned long long* run_cnt;
@@ -1350,7 +1350,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MG_PROBE
         if (CONTAIN) {
           atomicMax(&p.superkey[bid], ((unsigned long long)n1 << 32) | (0xFFFFFFFFu - ida));
           nhit = 1;
-        } else if (!(p.super && p.super[bid])) {  // :548 read2 contained
+        } else {  // (:548 a contained read2 was dropped at listing, p.cbits)
           // orientation/offset switch (:550-557) and the twin (:409-412, :841-855)
           const uint32_t orient = (o == 0) ? 3u : (o == 2 ? 2u : 1u);
           const uint32_t off = (o == 3) ? (uint32_t)(n1 - h - j) : (uint32_t)j;
@@ -1572,6 +1572,21 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MG_PROBE
       // hits (o = 1/3) add nothing (see the verify's CONTAIN case)
       keep = keep && !(CONTAIN && p.contain_even && (oo & 1));
       keepm |= (keep ? 1u : 0u) << s;
+    }
+    if (!CONTAIN && p.cbits) {
+      // :548 a contained read2 is never inserted: drop it before it takes a
+      // candidate slot, a partner-slot load and a compare (C5: most
+      // candidates), from the bitmap (1/32 of d_super, mostly cache hits);
+      // half a cell's lookups in flight together (registers: occupancy)
+#pragma unroll
+      for (int s0 = 0; s0 < kCell; s0 += kCell / 2) {
+        uint32_t cw[kCell / 2];
+#pragma unroll
+        for (int s = 0; s < kCell / 2; ++s)
+          cw[s] = ((keepm >> (s0 + s)) & 1u) ? p.cbits[(uint32_t)e[s0 + s] >> 5] : 0u;
+#pragma unroll
+        for (int s = 0; s < kCell / 2; ++s) keepm &= ~(((cw[s] >> ((uint32_t)e[s0 + s] & 31u)) & 1u) << (s0 + s));
+      }
     }
     while (__ballot(keepm != 0)) {
       // append slot groups while they fit, then verify a full wavefront
@@ -1866,7 +1881,8 @@ __global__ __launch_bounds__(kBlock) void k_live_runs(ulonglong2* __restrict__ r
 
 __global__ __launch_bounds__(kBlock) void k_super_finalize(const unsigned long long* __restrict__ key,
                                                           uint64_t n, uint32_t* __restrict__ super,
-                                                          unsigned int* __restrict__ any) {
+                                                          unsigned int* __restrict__ any,
+                                                          uint32_t* __restrict__ cbits) {
   const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
   uint32_t s = 0;
   if (i < n) {
@@ -1874,9 +1890,13 @@ __global__ __launch_bounds__(kBlock) void k_super_finalize(const unsigned long l
     s = k ? (0xFFFFFFFFu - (uint32_t)k) + 1u : 0u;  // container index -> ID
     super[i] = s;
   }
+  // the wavefront's 64 contained bits as two bitmap words (i is 64-aligned at lane 0)
+  const uint64_t bal = __ballot(s != 0);
+  const int lane = (int)(threadIdx.x & 63);
+  if (lane < 2 && i - lane < n) cbits[(i - lane) / 32 + lane] = (uint32_t)(bal >> (32 * lane));
   // the flag is set once: waves that already see it set skip the atomic
   // (an atomic per contained read on one address serialised: 8.9 ms at C5)
-  if (__ballot(s != 0) && (threadIdx.x & 63) == 0 && __hip_atomic_load(any, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u)
+  if (bal && lane == 0 && __hip_atomic_load(any, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u)
     atomicOr(any, 1u);
 }
 
@@ -2563,7 +2583,7 @@ struct LaunchProbe {
     pp.cell_lo = ctx->cell_lo;
     pp.cell_n = ctx->cell_n;
     pp.cells = ctx->d_cells;
-    pp.super = (!contain && ctx->contained_done && ctx->super_any) ? ctx->d_super : nullptr;
+    pp.cbits = (!contain && ctx->contained_done && ctx->super_any) ? ctx->d_cbits : nullptr;
     pp.superkey = ctx->superkey;
     pp.runs = runs;
     pp.run_cnt = run_cnt;
@@ -2782,7 +2802,7 @@ void mg_destroy(mg_ctx* ctx) {
                   ctx->d_xk[0], ctx->d_xk[1], ctx->d_xv[0], ctx->d_xv[1], ctx->d_xsort_tmp,
                   ctx->d_digest, ctx->id_store[0], ctx->id_store[1], ctx->phys_store[0], ctx->phys_store[1],
                   ctx->d_tmp32, ctx->d_lay_k[0], ctx->d_lay_k[1], ctx->d_lay_v[0], ctx->d_lay_v[1], ctx->d_lay_tmp,
-                  ctx->d_words_alt, ctx->d_len_alt};
+                  ctx->d_words_alt, ctx->d_len_alt, ctx->d_cbits};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   for (auto& e : ctx->ev)
@@ -3488,6 +3508,7 @@ int mg_mark_contained(mg_ctx* ctx, uint32_t* super_out) {
   MG_TRY(hipSetDevice(ctx->device));
   if (!ctx->index_ready) return set_err(ctx, "mg_build_index must run first");
   MG_TRY(ensure(&ctx->d_super, &ctx->super_cap, ctx->n + 1));
+  MG_TRY(ensure(&ctx->d_cbits, &ctx->cbits_cap, (ctx->n + 63) / 64 * 2));
   if (!ctx->d_any) MG_TRY(hipMalloc(&ctx->d_any, sizeof(unsigned int)));
   ctx->t.contained_ms = 0.f;
   if (ctx->minlen != ctx->maxlen) {  // OverlapGraph.cpp:228-233
@@ -3514,7 +3535,7 @@ int mg_mark_contained(mg_ctx* ctx, uint32_t* super_out) {
     }
     if (ctx->n)
       hipLaunchKernelGGL(k_super_finalize, dim3((uint32_t)((ctx->n + kBlock - 1) / kBlock)), dim3(kBlock), 0,
-                         ctx->stream, ctx->d_superkey, ctx->n, ctx->d_super, ctx->d_any);
+                         ctx->stream, ctx->d_superkey, ctx->n, ctx->d_super, ctx->d_any, ctx->d_cbits);
     MG_TRY(hipGetLastError());
     MG_TRY(hipEventRecord(ctx->ev[3], ctx->stream));
     unsigned int any = 0;
@@ -3800,13 +3821,14 @@ int mg_finalize_contained(mg_ctx* ctx, uint32_t* super_out) {
   if (!ctx) return -1;
   MG_TRY(hipSetDevice(ctx->device));
   MG_TRY(ensure(&ctx->d_super, &ctx->super_cap, ctx->n + 1));
+  MG_TRY(ensure(&ctx->d_cbits, &ctx->cbits_cap, (ctx->n + 63) / 64 * 2));
   if (!ctx->d_any) MG_TRY(hipMalloc(&ctx->d_any, sizeof(unsigned int)));
   ctx->super_any = false;
   if (ctx->minlen != ctx->maxlen && ctx->superkey) {
     MG_TRY(hipMemsetAsync(ctx->d_any, 0, sizeof(unsigned int), ctx->stream));
     if (ctx->n)
       hipLaunchKernelGGL(k_super_finalize, dim3((uint32_t)((ctx->n + kBlock - 1) / kBlock)), dim3(kBlock), 0,
-                         ctx->stream, ctx->superkey, ctx->n, ctx->d_super, ctx->d_any);
+                         ctx->stream, ctx->superkey, ctx->n, ctx->d_super, ctx->d_any, ctx->d_cbits);
     MG_TRY(hipGetLastError());
     unsigned int any = 0;
     MG_TRY(hipMemcpyAsync(&any, ctx->d_any, sizeof(any), hipMemcpyDeviceToHost, ctx->stream));
