@@ -528,8 +528,11 @@ __device__ __forceinline__ uint64_t ext_reg(const uint64_t* rw, int pos) {
 // KEYREC (exchange mode with w > 32, INDEX only): key records for the bucket
 // owners instead of CAS inserts.  Each instantiation references only the
 // parameters it uses, which keeps its scalar registers below the limit.
+#ifndef MG_SCAN_WAVES_G
+#define MG_SCAN_WAVES_G 6  // waves/SIMD of the length-ranked (G > 1) scan (A/B builds override)
+#endif
 template <int MAXW, bool INDEX, bool KEYREC = false, int G = 1>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) void k_scan(ScanParams p) {
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(G > 1 ? MG_SCAN_WAVES_G : 6))) void k_scan(ScanParams p) {
   extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int h = p.h, m = p.m, w = p.w;
@@ -1572,6 +1575,27 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MG_PROBE
       // hits (o = 1/3) add nothing (see the verify's CONTAIN case)
       keep = keep && !(CONTAIN && p.contain_even && (oo & 1));
       keepm |= (keep ? 1u : 0u) << s;
+    }
+    if (CONTAIN && valid) {
+      // the verify's length conditions (checkOverlapForContainedRead, :302-340:
+      // read2 strictly shorter, at offset s = j <= n1 - n2, or s = 0 for a
+      // suffix-key hit) at listing time, so a candidate that cannot be
+      // contained takes no candidate slot and no verification round
+      const int n1 = p.uniform_len ? p.uniform_len : (int)p.len[ra];
+#pragma unroll
+      for (int s0 = 0; s0 < kCell; s0 += kCell / 2) {
+        uint32_t n2v[kCell / 2];
+#pragma unroll
+        for (int s = 0; s < kCell / 2; ++s)
+          n2v[s] = ((keepm >> (s0 + s)) & 1u) ? (uint32_t)p.len[(uint32_t)e[s0 + s]] : 0u;
+#pragma unroll
+        for (int s = 0; s < kCell / 2; ++s) {
+          const uint32_t hi = (uint32_t)(e[s0 + s] >> 32);
+          const int j = rp - (int)((hi >> 2) & 1023u), n2 = (int)n2v[s];
+          const bool ok = n1 > n2 && ((hi & 1u) ? j == n2 - h : j <= n1 - n2);
+          if (!ok) keepm &= ~(1u << (s0 + s));
+        }
+      }
     }
     if (!CONTAIN && p.cbits) {
       // :548 a contained read2 is never inserted: drop it before it takes a
