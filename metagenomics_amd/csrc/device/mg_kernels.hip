@@ -1869,14 +1869,14 @@ __global__ __launch_bounds__(kBlock) void k_fixed_regions(unsigned long long* __
 // windows (OverlapGraph.cpp:548), so their runs (about two thirds of them at
 // C5) are dropped from every run region before the discovery probe, which
 // then streams and batches live runs only.  One wavefront per region, stable
-// in-place ballot compaction (a write never passes the batch being read), four
+// in-place ballot compaction (a write never passes the batch being read), eight
 // batches in flight; run_cnt[r] becomes the live count.
 __global__ __launch_bounds__(kBlock) void k_live_runs(ulonglong2* __restrict__ runs,
                                                      unsigned long long* __restrict__ run_cnt, uint64_t run_cap,
-                                                     uint64_t nreg, const uint32_t* __restrict__ super) {
+                                                     uint64_t nreg, const uint32_t* __restrict__ cbits) {
   const int lane = threadIdx.x & 63;
   const uint64_t nw = (uint64_t)gridDim.x * kWavesPerBlock;
-  constexpr int kDepth = 4;
+  constexpr int kDepth = 8;
   for (uint64_t r = (uint64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6); r < nreg; r += nw) {
     ulonglong2* reg = runs + r * run_cap;
     const uint64_t c = run_cnt[r] < run_cap ? run_cnt[r] : run_cap;
@@ -1890,7 +1890,10 @@ __global__ __launch_bounds__(kBlock) void k_live_runs(ulonglong2* __restrict__ r
         rec[d] = i < c ? reg[i] : make_ulonglong2(0, kFlatHole);
       }
 #pragma unroll
-      for (int d = 0; d < kDepth; ++d) live[d] = rec[d].y != kFlatHole && super[(uint32_t)rec[d].y] == 0;
+      for (int d = 0; d < kDepth; ++d) {
+        const uint32_t ra = (uint32_t)rec[d].y;  // (the bitmap of contained slots, k_super_finalize)
+        live[d] = rec[d].y != kFlatHole && !((cbits[ra >> 5] >> (ra & 31u)) & 1u);
+      }
       wave_sync();
 #pragma unroll
       for (int d = 0; d < kDepth; ++d) {
@@ -3306,7 +3309,7 @@ int probe_shared(mg_ctx* ctx, bool contain) {
       const uint32_t grid = (uint32_t)std::min<uint64_t>((ctx->nrun_reg + kWavesPerBlock - 1) / kWavesPerBlock,
                                                          (uint64_t)ctx->n_cu * 8);
       hipLaunchKernelGGL(k_live_runs, dim3(grid), dim3(kBlock), 0, ctx->stream, ctx->d_runs, ctx->d_run_cnt,
-                         ctx->run_cap, ctx->nrun_reg, ctx->d_super);
+                         ctx->run_cap, ctx->nrun_reg, ctx->d_cbits);
       MG_TRY(hipGetLastError());
       ctx->runs_live = true;
     }
@@ -3795,7 +3798,7 @@ int mg_xchg_probe(mg_ctx* ctx, int contain, const void* recv, uint64_t slot, uin
       const uint32_t grid = (uint32_t)std::min<uint64_t>((nregions + kWavesPerBlock - 1) / kWavesPerBlock,
                                                          (uint64_t)ctx->n_cu * 8);
       hipLaunchKernelGGL(k_live_runs, dim3(grid), dim3(kBlock), 0, ctx->stream, runs, ctx->d_flat_cnt, reg,
-                         nregions, ctx->d_super);
+                         nregions, ctx->d_cbits);
       MG_TRY(hipGetLastError());
       ctx->runs_live = true;
     }
