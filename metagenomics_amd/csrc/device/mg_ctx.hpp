@@ -75,6 +75,18 @@ struct mg_ctx {
   // they take a verification (:548), from a 1/32-size array that stays in cache
   uint32_t* d_cbits = nullptr;
   size_t cbits_cap = 0;
+  // contained reads counted by k_super_finalize (64 counters, one per 64-B line)
+  unsigned int* d_ccnt = nullptr;
+  uint64_t n_contained = 0;
+  // discovery index (option "live_index", unsharded fused path, mixed lengths):
+  // after markContainedReads the discovery probe only needs the keys of
+  // uncontained reads (:548 drops contained partners), so it probes a table of
+  // those alone, sized for them (C5: a quarter of the entries and chains)
+  bool live_index = true;
+  bool live_ready = false;
+  uint64_t* d_lcells = nullptr;
+  size_t lcells_cap = 0;
+  uint32_t lnb_log2 = 0;
   unsigned int* d_any = nullptr;
   unsigned long long* d_digest = nullptr;  // mg_rows_digest / mg_super_digest accumulators (4 u64)
   size_t super_cap = 0, superkey_cap = 0;
@@ -224,6 +236,7 @@ inline void reset_derived(mg_ctx* ctx) {
   ctx->index_ready = false;
   ctx->contained_done = false;
   ctx->super_any = false;
+  ctx->live_ready = false;
   ctx->n_rows = 0;
 }
 

@@ -171,6 +171,7 @@ struct IndexParams {
   uint64_t* cells;   // [cell_n * kCell] entries: lo32 = read index, hi32 = chain1 | fp19 | q10 | o2
   const uint32_t* id;  // slot -> reference ID - 1 (nullptr: ID order; lookups return IDs)
   uint32_t stride;     // words per slot (the long-read kernels; the templated ones use slot_words(MAXW))
+  const uint32_t* cbits;  // k_index_build: skip the keys of contained slots (the discovery index; nullptr: none)
 };
 
 __device__ __forceinline__ bool owned(uint64_t bkt, uint32_t nb_log2, uint32_t rank, uint32_t nranks) {
@@ -274,6 +275,7 @@ __global__ __launch_bounds__(kBlock) void k_index_build(IndexParams p) {
        gid += (uint64_t)gridDim.x * kBlock) {
     const uint64_t r = gid >> 2;
     const int o = (int)(gid & 3);
+    if (p.cbits && ((p.cbits[r >> 5] >> (r & 31)) & 1u)) continue;
     const uint64_t* g = p.words + r * slot_words(MAXW);
 #pragma unroll
     for (int k = 0; k < MAXW; ++k) f[k * kBlock] = g[k];
@@ -1909,7 +1911,8 @@ __global__ __launch_bounds__(kBlock) void k_live_runs(ulonglong2* __restrict__ r
 __global__ __launch_bounds__(kBlock) void k_super_finalize(const unsigned long long* __restrict__ key,
                                                           uint64_t n, uint32_t* __restrict__ super,
                                                           unsigned int* __restrict__ any,
-                                                          uint32_t* __restrict__ cbits) {
+                                                          uint32_t* __restrict__ cbits,
+                                                          unsigned int* __restrict__ ccnt) {
   const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
   uint32_t s = 0;
   if (i < n) {
@@ -1921,6 +1924,7 @@ __global__ __launch_bounds__(kBlock) void k_super_finalize(const unsigned long l
   const uint64_t bal = __ballot(s != 0);
   const int lane = (int)(threadIdx.x & 63);
   if (lane < 2 && i - lane < n) cbits[(i - lane) / 32 + lane] = (uint32_t)(bal >> (32 * lane));
+  if (ccnt && bal && lane == 0) atomicAdd(&ccnt[(blockIdx.x & 63u) * 16], (unsigned int)__popcll(bal));
   // the flag is set once: waves that already see it set skip the atomic
   // (an atomic per contained read on one address serialised: 8.9 ms at C5)
   if (bal && lane == 0 && __hip_atomic_load(any, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u)
@@ -2405,8 +2409,8 @@ IndexParams index_params(mg_ctx* ctx) {
 
 template <int W>
 struct LaunchIndex {
-  static int run(mg_ctx* ctx) {
-    IndexParams p = index_params(ctx);
+  static int run(mg_ctx* ctx, const IndexParams* over = nullptr) {  // over: another table (build_live_index)
+    IndexParams p = over ? *over : index_params(ctx);
     uint32_t grid = (uint32_t)((4 * ctx->n + kBlock - 1) / kBlock);  // one thread per key
     const size_t lds = (size_t)(W + 1) * kBlock * sizeof(uint64_t);
     if (grid == 0) return 0;
@@ -2610,6 +2614,12 @@ struct LaunchProbe {
     pp.cell_lo = ctx->cell_lo;
     pp.cell_n = ctx->cell_n;
     pp.cells = ctx->d_cells;
+    if (!contain && ctx->live_ready) {  // the discovery index of uncontained reads (build_live_index)
+      pp.nb_log2 = ctx->lnb_log2;
+      pp.cell_lo = 0;
+      pp.cell_n = 1ull << ctx->lnb_log2;
+      pp.cells = ctx->d_lcells;
+    }
     pp.cbits = (!contain && ctx->contained_done && ctx->super_any) ? ctx->d_cbits : nullptr;
     pp.superkey = ctx->superkey;
     pp.runs = runs;
@@ -2829,7 +2839,7 @@ void mg_destroy(mg_ctx* ctx) {
                   ctx->d_xk[0], ctx->d_xk[1], ctx->d_xv[0], ctx->d_xv[1], ctx->d_xsort_tmp,
                   ctx->d_digest, ctx->id_store[0], ctx->id_store[1], ctx->phys_store[0], ctx->phys_store[1],
                   ctx->d_tmp32, ctx->d_lay_k[0], ctx->d_lay_k[1], ctx->d_lay_v[0], ctx->d_lay_v[1], ctx->d_lay_tmp,
-                  ctx->d_words_alt, ctx->d_len_alt, ctx->d_cbits};
+                  ctx->d_words_alt, ctx->d_len_alt, ctx->d_cbits, ctx->d_ccnt, ctx->d_lcells};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   for (auto& e : ctx->ev)
@@ -3008,7 +3018,7 @@ int mg_set_option(mg_ctx* ctx, const char* name, int64_t value) {
   if (flag("stats", &ctx->stats) || flag("halving", &ctx->halving_low) || flag("layout", &ctx->layout) ||
       flag("contain_jcut", &ctx->contain_jcut) || flag("contain_skip", &ctx->contain_skip) ||
       flag("contain_prune", &ctx->contain_prune) || flag("probe_share", &ctx->probe_share) ||
-      flag("probe_compact", &ctx->probe_compact))
+      flag("probe_compact", &ctx->probe_compact) || flag("live_index", &ctx->live_index))
     return 0;
   if (flag("prefix_contain", &ctx->prefix_contain)) {
     ctx->index_ready = false;
@@ -3068,6 +3078,7 @@ int setup_index(mg_ctx* ctx, uint32_t min_overlap, uint32_t seed_k, bool cells =
   ctx->index_ready = false;
   ctx->contained_done = false;
   ctx->super_any = false;
+  ctx->live_ready = false;
   ctx->key0_ready = false;  // set by the fused build when it writes the o = 0 keys
   ctx->xchg = false;        // mg_xchg_begin sets it after this
   ctx->packable = 0;
@@ -3300,11 +3311,40 @@ struct LaunchProbeShared {
 };
 
 // probe the shared scan's runs (rows settled for the discovery probe)
+// The discovery index (option live_index): the keys of the uncontained reads
+// only, in a table sized for them (same minimizer keys and entries as the
+// full index, so the runs probe it unchanged; the full table keeps serving
+// getListOfReads and containment)
+int build_live_index(mg_ctx* ctx) {
+  ctx->live_ready = false;
+  if (!ctx->live_index || !ctx->super_any || ctx->nranks > 1 || ctx->xchg || long_mode(ctx)) return 0;
+  const uint64_t live = ctx->n > ctx->n_contained ? ctx->n - ctx->n_contained : 1;
+  uint32_t nbl = 10;  // setup_index's rule for `live` reads
+  while (nbl < 31 && (1ull << nbl) < live) nbl++;
+  while (nbl < 31 && (1ull << nbl) * kCell < 5 * live) nbl++;
+  if (nbl >= ctx->nb_log2) return 0;  // no smaller than the full table: probe that
+  MG_TRY(ensure(&ctx->d_lcells, &ctx->lcells_cap, (1ull << nbl) * kCell));
+  MG_TRY(hipMemsetAsync(ctx->d_lcells, 0xFF, (1ull << nbl) * kCell * sizeof(uint64_t), ctx->stream));
+  IndexParams p = index_params(ctx);
+  p.nb_log2 = nbl;
+  p.rank = 0;
+  p.nranks = 1;
+  p.cell_lo = 0;
+  p.cell_n = 1ull << nbl;
+  p.cells = ctx->d_lcells;
+  p.cbits = ctx->d_cbits;
+  if (dispatch_w<LaunchIndex>(ctx->maxw, ctx, &p)) return set_err(ctx, "live index launch failed");
+  ctx->lnb_log2 = nbl;
+  ctx->live_ready = true;
+  return 0;
+}
+
 int probe_shared(mg_ctx* ctx, bool contain) {
   if (ensure_scan(ctx)) return -1;
   for (int attempt = 0; attempt < 3; ++attempt) {
     ctx->nreg = 0;
     MG_TRY(hipEventRecord(ctx->ev[8], ctx->stream));
+    if (!contain && attempt == 0 && ctx->contained_done && build_live_index(ctx)) return -1;
     if (!contain && ctx->contained_done && ctx->super_any && !ctx->runs_live && ctx->nrun_reg) {
       const uint32_t grid = (uint32_t)std::min<uint64_t>((ctx->nrun_reg + kWavesPerBlock - 1) / kWavesPerBlock,
                                                          (uint64_t)ctx->n_cu * 8);
@@ -3543,6 +3583,8 @@ int mg_mark_contained(mg_ctx* ctx, uint32_t* super_out) {
     ctx->superkey = ctx->d_superkey;
     MG_TRY(hipMemsetAsync(ctx->d_superkey, 0, (ctx->n + 1) * sizeof(unsigned long long), ctx->stream));
     MG_TRY(hipMemsetAsync(ctx->d_any, 0, sizeof(unsigned int), ctx->stream));
+    if (!ctx->d_ccnt) MG_TRY(hipMalloc(&ctx->d_ccnt, 64 * 16 * sizeof(unsigned int)));
+    MG_TRY(hipMemsetAsync(ctx->d_ccnt, 0, 64 * 16 * sizeof(unsigned int), ctx->stream));
     if (ctx->stats) {  // containment work counters (mg_counters c_*)
       if (!ctx->d_stats) MG_TRY(hipMalloc(&ctx->d_stats, (kSegs * 4 + 1) * sizeof(unsigned long long)));
       MG_TRY(hipMemsetAsync(ctx->d_stats, 0, (kSegs * 4 + 1) * sizeof(unsigned long long), ctx->stream));
@@ -3562,14 +3604,19 @@ int mg_mark_contained(mg_ctx* ctx, uint32_t* super_out) {
     }
     if (ctx->n)
       hipLaunchKernelGGL(k_super_finalize, dim3((uint32_t)((ctx->n + kBlock - 1) / kBlock)), dim3(kBlock), 0,
-                         ctx->stream, ctx->d_superkey, ctx->n, ctx->d_super, ctx->d_any, ctx->d_cbits);
+                         ctx->stream, ctx->d_superkey, ctx->n, ctx->d_super, ctx->d_any, ctx->d_cbits, ctx->d_ccnt);
     MG_TRY(hipGetLastError());
     MG_TRY(hipEventRecord(ctx->ev[3], ctx->stream));
     unsigned int any = 0;
+    unsigned int ccnt[64 * 16];
     MG_TRY(hipMemcpyAsync(&any, ctx->d_any, sizeof(any), hipMemcpyDeviceToHost, ctx->stream));
+    MG_TRY(hipMemcpyAsync(ccnt, ctx->d_ccnt, sizeof(ccnt), hipMemcpyDeviceToHost, ctx->stream));
     MG_TRY(hipStreamSynchronize(ctx->stream));
     ctx->t.contained_ms = elapsed(ctx->ev[2], ctx->ev[3]);
     ctx->super_any = any != 0;
+    ctx->n_contained = 0;
+    for (int c = 0; c < 64; ++c) ctx->n_contained += ccnt[c * 16];
+    ctx->live_ready = false;
     if (ctx->stats) {
       std::vector<unsigned long long> st(kSegs * 4 + 1);
       MG_TRY(hipMemcpy(st.data(), ctx->d_stats, st.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
@@ -3831,6 +3878,7 @@ int mg_begin_contained(mg_ctx* ctx, void* superkey, int* needed) {
   MG_TRY(hipSetDevice(ctx->device));
   *needed = ctx->minlen != ctx->maxlen;  // OverlapGraph.cpp:228-233
   ctx->contained_done = false;
+  ctx->live_ready = false;
   ctx->superkey = nullptr;
   if (*needed) {
     if (superkey) {
@@ -3855,7 +3903,7 @@ int mg_finalize_contained(mg_ctx* ctx, uint32_t* super_out) {
     MG_TRY(hipMemsetAsync(ctx->d_any, 0, sizeof(unsigned int), ctx->stream));
     if (ctx->n)
       hipLaunchKernelGGL(k_super_finalize, dim3((uint32_t)((ctx->n + kBlock - 1) / kBlock)), dim3(kBlock), 0,
-                         ctx->stream, ctx->superkey, ctx->n, ctx->d_super, ctx->d_any, ctx->d_cbits);
+                         ctx->stream, ctx->superkey, ctx->n, ctx->d_super, ctx->d_any, ctx->d_cbits, nullptr);
     MG_TRY(hipGetLastError());
     unsigned int any = 0;
     MG_TRY(hipMemcpyAsync(&any, ctx->d_any, sizeof(any), hipMemcpyDeviceToHost, ctx->stream));

@@ -656,6 +656,7 @@ def test_prefix_contain_off(name):
 
 CONTAIN_OPTS = [
     {"contain_jcut": 0, "contain_prune": 0, "contain_skip": 0},
+    {"live_index": 0},
     {"contain_jcut": 1, "contain_prune": 0, "contain_skip": 0},
     {"contain_jcut": 0, "contain_prune": 1, "contain_skip": 0},
     {"contain_jcut": 0, "contain_prune": 0, "contain_skip": 1},
@@ -672,8 +673,9 @@ def test_containment_options(name):
     j = n1 - minlen (contain_jcut), candidates that cannot raise the superkey
     (contain_prune), runs of already-contained sources (contain_skip, also without
     k_prefix_contain) and source-length passes (contain_passes), and the probe's
-    batch compaction and block-shared regions (probe_compact, probe_share): every
-    combination gives the same superReadIDs and rows."""
+    batch compaction and block-shared regions (probe_compact, probe_share), and the
+    discovery probe on the full index instead of the uncontained reads' index
+    (live_index = 0): every combination gives the same superReadIDs and rows."""
     if name in ("prefixes", "metagenome"):
         if name == "prefixes":
             seqs, l = prefix_reads(), 40
