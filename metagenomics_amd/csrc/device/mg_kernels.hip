@@ -171,7 +171,7 @@ struct IndexParams {
   uint64_t* cells;   // [cell_n * kCell] entries: lo32 = read index, hi32 = chain1 | fp19 | q10 | o2
   const uint32_t* id;  // slot -> reference ID - 1 (nullptr: ID order; lookups return IDs)
   uint32_t stride;     // words per slot (the long-read kernels; the templated ones use slot_words(MAXW))
-  const uint32_t* cbits;  // k_index_build: skip the keys of contained slots (the discovery index; nullptr: none)
+  const uint32_t* cbits;  // k_index_live: the contained slots (bitmap, k_super_finalize)
 };
 
 __device__ __forceinline__ bool owned(uint64_t bkt, uint32_t nb_log2, uint32_t rank, uint32_t nranks) {
@@ -275,7 +275,6 @@ __global__ __launch_bounds__(kBlock) void k_index_build(IndexParams p) {
        gid += (uint64_t)gridDim.x * kBlock) {
     const uint64_t r = gid >> 2;
     const int o = (int)(gid & 3);
-    if (p.cbits && ((p.cbits[r >> 5] >> (r & 31)) & 1u)) continue;
     const uint64_t* g = p.words + r * slot_words(MAXW);
 #pragma unroll
     for (int k = 0; k < MAXW; ++k) f[k * kBlock] = g[k];
@@ -286,6 +285,53 @@ __global__ __launch_bounds__(kBlock) void k_index_build(IndexParams p) {
     const uint64_t b = v & mask;
     if (owned(b, p.nb_log2, p.rank, p.nranks))
       cell_insert(p.cells, b - p.cell_lo, p.cell_n, make_entry(v, p.nb_log2, q, o, (uint32_t)r));
+  }
+}
+
+// The discovery index of the uncontained reads (build_live_index): the same
+// entries as k_index_build for the live slots only.  A wavefront takes 64
+// consecutive slots, reads their contained bits (p.cbits, two words) and
+// deals the 4 keys of each live slot to consecutive lanes, so no lane is
+// spent on a contained read (C5: three quarters of them).
+__device__ __forceinline__ uint32_t nth_set_bit(uint64_t x, uint32_t k) {  // position of set bit k (0-based)
+  uint32_t pos = 0;
+#pragma unroll
+  for (int s = 32; s >= 1; s >>= 1) {
+    const uint32_t c = (uint32_t)__popcll(x & ((1ull << s) - 1));
+    if (k >= c) {
+      k -= c;
+      x >>= s;
+      pos += (uint32_t)s;
+    }
+  }
+  return pos;
+}
+
+template <int MAXW>
+__global__ __launch_bounds__(kBlock) void k_index_live(IndexParams p) {
+  extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
+  uint64_t* f = smem + threadIdx.x;  // word k at f[k * kBlock]
+  const int lane = threadIdx.x & 63;
+  const uint64_t mask = (1ULL << p.nb_log2) - 1;
+  const uint64_t ngrp = (p.n + kWave - 1) / kWave, nw = (uint64_t)gridDim.x * kWavesPerBlock;
+  for (uint64_t g = (uint64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6); g < ngrp; g += nw) {
+    const uint64_t r0 = g * kWave;
+    uint64_t live = ~((uint64_t)p.cbits[2 * g] | ((uint64_t)p.cbits[2 * g + 1] << 32));
+    if (p.n - r0 < (uint64_t)kWave) live &= (1ull << (p.n - r0)) - 1;
+    const uint32_t nk = 4u * (uint32_t)__popcll(live);
+    for (uint32_t k0 = 0; k0 < nk; k0 += kWave) {
+      const uint32_t k = k0 + (uint32_t)lane;
+      if (k >= nk) continue;
+      const uint64_t r = r0 + nth_set_bit(live, k >> 2);
+      const int o = (int)(k & 3u);
+      const uint64_t* gw = p.words + r * slot_words(MAXW);
+#pragma unroll
+      for (int kk = 0; kk < MAXW; ++kk) f[kk * kBlock] = gw[kk];
+      f[MAXW * kBlock] = 0;
+      int q;
+      const uint64_t v = key_minimizer<kBlock>(f, p.len[r], o, p.h, p.m, p.w, &q);
+      cell_insert(p.cells, v & mask, p.cell_n, make_entry(v, p.nb_log2, q, o, (uint32_t)r));
+    }
   }
 }
 
@@ -2408,9 +2454,21 @@ IndexParams index_params(mg_ctx* ctx) {
 }
 
 template <int W>
+struct LaunchIndexLive {
+  static int run(mg_ctx* ctx, const IndexParams* p) {
+    const uint32_t grid = (uint32_t)(((ctx->n + kWave - 1) / kWave + kWavesPerBlock - 1) / kWavesPerBlock);
+    const size_t lds = (size_t)(W + 1) * kBlock * sizeof(uint64_t);
+    if (grid == 0) return 0;
+    allow_lds(k_index_live<W>, lds);
+    hipLaunchKernelGGL((k_index_live<W>), dim3(grid), dim3(kBlock), lds, ctx->stream, *p);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+  }
+};
+
+template <int W>
 struct LaunchIndex {
-  static int run(mg_ctx* ctx, const IndexParams* over = nullptr) {  // over: another table (build_live_index)
-    IndexParams p = over ? *over : index_params(ctx);
+  static int run(mg_ctx* ctx) {
+    IndexParams p = index_params(ctx);
     uint32_t grid = (uint32_t)((4 * ctx->n + kBlock - 1) / kBlock);  // one thread per key
     const size_t lds = (size_t)(W + 1) * kBlock * sizeof(uint64_t);
     if (grid == 0) return 0;
@@ -3333,7 +3391,7 @@ int build_live_index(mg_ctx* ctx) {
   p.cell_n = 1ull << nbl;
   p.cells = ctx->d_lcells;
   p.cbits = ctx->d_cbits;
-  if (dispatch_w<LaunchIndex>(ctx->maxw, ctx, &p)) return set_err(ctx, "live index launch failed");
+  if (dispatch_w<LaunchIndexLive>(ctx->maxw, ctx, &p)) return set_err(ctx, "live index launch failed");
   ctx->lnb_log2 = nbl;
   ctx->live_ready = true;
   return 0;
