@@ -259,7 +259,7 @@ def parity_digest(engines, last, mode, dist, config):
 
 
 # rocprofv3 --pmc summaries (tools/pmc_summary.py) of the default step, newest first
-PMC_FILES = {"c3": ["r03q_pmc_c3.json", "r02s3_pmc_c3.json"], "c5": ["r03q_pmc_c5.json", "r02s3_pmc_c5.json"]}
+PMC_FILES = {"c3": ["r03q_pmc_c3.json", "r02s3_pmc_c3.json"], "c5": ["r03g_pmc_c5.json", "r03q_pmc_c5.json"]}
 
 
 def load_pmc(path):
@@ -272,7 +272,8 @@ def load_pmc(path):
     except Exception:
         return None
     tr = d.get("traffic", {})
-    step = ("k_index_build", "k_scan", "k_probe", "k_prefix_contain", "k_live_runs", "k_super_finalize")
+    step = ("k_index_build", "k_index_live", "k_scan", "k_probe", "k_prefix_contain", "k_live_runs",
+            "k_super_finalize")
     if any("dispatches" in v for v in tr.values()):
         # every dispatch of the step's kernels over the number of step passes
         # (one k_scan each); the default step has no run sort since the
