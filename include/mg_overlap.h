@@ -271,6 +271,9 @@ int mg_get_counters(const mg_ctx* ctx, mg_counters* c);
  *                   containment pruning, all exact, default 1;
  *  "probe_share"    a discovery block's 4 wavefronts share its run regions (default 1);
  *  "probe_compact"  sparse run batches are compacted in the probe (default 1);
+ *  "live_index"     mixed lengths, one rank: after mg_mark_contained the
+ *                   discovery probe walks an index of the uncontained reads'
+ *                   keys only (OverlapGraph.cpp:548; exact, default 1);
  *  "run_cap"        tests: initial run records per scan region (0 = sized from
  *                   the reads; overflowing regions are resized and rescanned);
  *  "phase_limit", "max_blocks"
