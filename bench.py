@@ -199,6 +199,33 @@ def one_shot(e, ds, fused_step, device, rows):
     return out
 
 
+def d2h_rows(e, rows):
+    """SURVEY §8(d) "H2D/D2H reported separately": the drop-in's caller reads
+    graph[u] on the host (OverlapGraph.cpp:390-419), so the rows leave the device
+    through mg_copy_rows (region compaction on the device + one D2H copy).
+    Timed into a pinned buffer (the rate a caller that pins its buffer sees)
+    and into pageable memory; not part of ms_per_step (inputs and outputs
+    resident in HBM), reported beside it."""
+    import torch
+
+    out = {"rows": rows, "bytes": rows * 12}
+    pinned = torch.empty(max(1, rows * 12), dtype=torch.uint8, pin_memory=True)
+    e.copy_rows_to(pinned.data_ptr(), rows)  # first call sizes the compaction buffer
+    t0 = time.perf_counter()
+    got = e.copy_rows_to(pinned.data_ptr(), rows)
+    ms = (time.perf_counter() - t0) * 1e3
+    assert got == rows, (got, rows)
+    out.update(pinned_ms=ms, pinned_gbs=rows * 12 / ms / 1e6)
+    del pinned
+    page = np.empty(rows * 12, dtype=np.uint8)
+    page[:: 4096] = 0  # fault the pages in before timing
+    t0 = time.perf_counter()
+    e.copy_rows_to(page.ctypes.data, rows)
+    ms = (time.perf_counter() - t0) * 1e3
+    out.update(pageable_ms=ms, pageable_gbs=rows * 12 / ms / 1e6)
+    return out
+
+
 def full_size_reference(config):
     """The reference's own time for the bench's exact workload, from the
     committed golden (tests/golden/<config>.json, made by make_scale_golden.py
@@ -231,7 +258,7 @@ def parity_digest(engines, last, mode, dist, config):
     workload (tests/golden/<config>.json, made by oracle/_ref/ref_harness)."""
     import torch
 
-    if mode.startswith("exchange"):
+    if mode.startswith("exchange") and last.host_rows is None:
         rows = [e.slots_digest(buf.data_ptr(), slot, rounds, cnt.data_ptr())
                 for e, (buf, cnt, slot, rounds) in zip(engines, last.rows)]
     else:
@@ -311,6 +338,7 @@ def main():
     ap.add_argument("--pmc", default=None,
                     help="committed rocprofv3 --pmc summary for roofline.traffic (default: profiles/PMC_FILES[config])")
     ap.add_argument("--nb-log2", type=int, default=0)
+    ap.add_argument("--no-d2h", action="store_true", help="skip the rows' D2H timing (mg_copy_rows)")
     ap.add_argument("--no-one-shot", action="store_true",
                     help="skip the per-dataset one-shot timing (layout + one step, and ID order + one step)")
     ap.add_argument("--opt", action="append", default=[],
@@ -572,10 +600,21 @@ def main():
     }
     if sim_rank_ms is not None:
         res["sim_rank_ms"] = sim_rank_ms
+    if world == 1 and mode == "fused" and not args.no_d2h:
+        try:
+            d2h = d2h_rows(engines[0], rows)
+            res["d2h_rows"] = d2h
+            res["d2h_rows_ms"] = d2h["pinned_ms"]
+            # PCIe-inclusive rate (never `value`): the step plus the rows' copy to pinned host memory
+            res["edges_per_sec_with_d2h"] = edges / ((ms_step + d2h["pinned_ms"]) / 1000.0)
+        except Exception as e:  # report, never fake
+            res["d2h_rows"] = {"error": str(e)}
     if world == 1 and mode == "fused" and not args.no_one_shot:
         try:
             res["one_shot"] = one_shot(engines[0], ds, fused_step, local, rows)
             res["layout_ms"] = res["one_shot"]["layout_ms"]
+            res["one_shot_ms"] = res["one_shot"]["one_shot_ms"]
+            res["one_shot_edges_per_sec"] = edges / (res["one_shot"]["one_shot_ms"] / 1000.0)
         except Exception as e:  # report, never fake
             res["one_shot"] = {"error": str(e)}
     if world == 1 and mode == "fused" and args.replay:

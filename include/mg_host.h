@@ -74,6 +74,16 @@ void mgh_parse_free(void* p);
 /* smallest chunk one thread splits (default 1 MiB; 0 restores it) */
 void mgh_parse_set_min_chunk(uint64_t bytes);
 
+/* --- multi-process rendezvous (exchange mode over RCCL) ---------
+ * Rank 0 serves the n-byte blob (the RCCL unique id) to the world - 1 other
+ * ranks over TCP at addr:port; the others receive it into blob.  addr is a
+ * dotted address or a host name (torchrun's MASTER_ADDR, e.g. "localhost").
+ * Every wait is bounded by timeout_ms (<= 0: 10 minutes).  0 = ok, -1 bad
+ * arguments, -2 addr does not resolve, -3 cannot listen (rank 0), -4 deadline
+ * passed (a peer never connected / rank 0 never reachable), -5 I/O error.
+ * Replaces torch.distributed's store for the C++ host (mg_overlap -xchg). */
+int mgh_rendezvous(int rank, int world, const char* addr, int port, void* blob, uint64_t n, int timeout_ms);
+
 /* --- graph construction order ----------------------------
  * Replays OverlapGraph::buildOverlapGraphFromHashTable's exploration and
  * transitive reduction (OverlapGraph.cpp:144-204, 574-661) on the device's

@@ -65,7 +65,8 @@ typedef struct mg_counters {
   uint64_t entries;   /* bucket entries scanned                       */
   uint64_t verified;  /* partner reads fetched and compared           */
   uint64_t rows;      /* directed rows emitted                        */
-  uint64_t trips;     /* 0 (reserved)                                   */
+  uint64_t live_cells; /* cells of the discovery index of uncontained reads the probe
+                          walked (option live_index); 0 = the full table */
   /* the last containment pass (markContainedReads), same units */
   uint64_t c_runs, c_entries, c_verified, c_contained;
 } mg_counters;

@@ -87,6 +87,7 @@ struct mg_ctx {
   uint64_t* d_lcells = nullptr;
   size_t lcells_cap = 0;
   uint32_t lnb_log2 = 0;
+  uint64_t live_cells = 0;  // cells of the discovery index (mg_counters::live_cells)
   unsigned int* d_any = nullptr;
   unsigned long long* d_digest = nullptr;  // mg_rows_digest / mg_super_digest accumulators (4 u64)
   size_t super_cap = 0, superkey_cap = 0;
@@ -237,6 +238,7 @@ inline void reset_derived(mg_ctx* ctx) {
   ctx->contained_done = false;
   ctx->super_any = false;
   ctx->live_ready = false;
+  ctx->n_contained = 0;
   ctx->n_rows = 0;
 }
 

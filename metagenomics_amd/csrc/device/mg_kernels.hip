@@ -3299,7 +3299,7 @@ void read_stats(mg_ctx* ctx, uint64_t nsrc) {
   ctx->counters.verified = acc[2];
   ctx->counters.rows = acc[3];
   ctx->counters.sources = nsrc;
-  ctx->counters.trips = st[kSegs * 4];
+  ctx->counters.live_cells = ctx->live_ready ? ctx->live_cells : 0;
 }
 // The window scan of ALL sources, unfiltered (runs of contained sources are
 // dropped by the probe) and fused with the index build (k_scan<INDEX>):
@@ -3393,6 +3393,7 @@ int build_live_index(mg_ctx* ctx) {
   p.cbits = ctx->d_cbits;
   if (dispatch_w<LaunchIndexLive>(ctx->maxw, ctx, &p)) return set_err(ctx, "live index launch failed");
   ctx->lnb_log2 = nbl;
+  ctx->live_cells = 1ull << nbl;
   ctx->live_ready = true;
   return 0;
 }
@@ -3937,6 +3938,7 @@ int mg_begin_contained(mg_ctx* ctx, void* superkey, int* needed) {
   *needed = ctx->minlen != ctx->maxlen;  // OverlapGraph.cpp:228-233
   ctx->contained_done = false;
   ctx->live_ready = false;
+  ctx->n_contained = 0;
   ctx->superkey = nullptr;
   if (*needed) {
     if (superkey) {
@@ -3959,14 +3961,20 @@ int mg_finalize_contained(mg_ctx* ctx, uint32_t* super_out) {
   ctx->super_any = false;
   if (ctx->minlen != ctx->maxlen && ctx->superkey) {
     MG_TRY(hipMemsetAsync(ctx->d_any, 0, sizeof(unsigned int), ctx->stream));
+    if (!ctx->d_ccnt) MG_TRY(hipMalloc(&ctx->d_ccnt, 64 * 16 * sizeof(unsigned int)));
+    MG_TRY(hipMemsetAsync(ctx->d_ccnt, 0, 64 * 16 * sizeof(unsigned int), ctx->stream));
     if (ctx->n)
       hipLaunchKernelGGL(k_super_finalize, dim3((uint32_t)((ctx->n + kBlock - 1) / kBlock)), dim3(kBlock), 0,
-                         ctx->stream, ctx->superkey, ctx->n, ctx->d_super, ctx->d_any, ctx->d_cbits, nullptr);
+                         ctx->stream, ctx->superkey, ctx->n, ctx->d_super, ctx->d_any, ctx->d_cbits, ctx->d_ccnt);
     MG_TRY(hipGetLastError());
     unsigned int any = 0;
+    unsigned int ccnt[64 * 16];
     MG_TRY(hipMemcpyAsync(&any, ctx->d_any, sizeof(any), hipMemcpyDeviceToHost, ctx->stream));
+    MG_TRY(hipMemcpyAsync(ccnt, ctx->d_ccnt, sizeof(ccnt), hipMemcpyDeviceToHost, ctx->stream));
     MG_TRY(hipStreamSynchronize(ctx->stream));
     ctx->super_any = any != 0;
+    ctx->n_contained = 0;
+    for (int c = 0; c < 64; ++c) ctx->n_contained += ccnt[c * 16];
   } else {
     MG_TRY(hipMemsetAsync(ctx->d_super, 0, (ctx->n + 1) * sizeof(uint32_t), ctx->stream));
   }

@@ -664,6 +664,7 @@ bool OverlapGraph::saveGraphToFile(const std::string& fileName) {
 
 void OverlapGraph::markContainedReads() {
   // OverlapGraph.cpp:225-290 on the device; superReadID written back to Read
+  if (!hashTable) throw mg::Error("markContainedReads: no hash table (the build released it)");
   mg_ctx* ctx = hashTable->context();
   const UINT64 N = dataSet->getNumberOfUniqueReads();
   std::vector<uint32_t> super(N + 1, 0);
@@ -777,6 +778,9 @@ bool OverlapGraph::beginBuildFromHashTable(HashTable* ht) {
   manual->h = ht->getHashStringLength();
   const int rc = manual->D.build(rows.data(), got, dataSet->packedLengths(), N, (uint32_t)manual->h);
   if (rc) throw mg::Error("discoveries inconsistent with the Dataset (" + std::to_string(rc) + ")");
+  // the table stays the caller's, who frees it after the build as the reference
+  // does (:210, mg_explore_main.cpp): nothing here reads it again (h is captured)
+  hashTable = nullptr;
   return true;
 }
 
@@ -862,8 +866,8 @@ bool OverlapGraph::removeTransitiveEdges(UINT64 readNumber) {
 
 namespace {
 UINT64 hash_string_length(HashTable* ht, UINT64 manual_h) {
+  if (manual_h) return manual_h;  // captured by beginBuildFromHashTable (the table may be freed since)
   if (ht) return ht->getHashStringLength();
-  if (manual_h) return manual_h;
   throw mg::Error("checkOverlap: no hash table (the graph was built and its table freed)");
 }
 }  // namespace

@@ -12,21 +12,19 @@
 // counts, to detect a stream cut at its capacity).
 #include "mg_xchg.hpp"
 
-#include <arpa/inet.h>
-#include <netinet/in.h>
-#include <sys/socket.h>
-#include <unistd.h>
-
 #include <algorithm>
 #include <chrono>
 #include <cstring>
 #include <stdexcept>
 #include <thread>
 
+#include "mg_host.h"
+
 namespace mg {
 
 namespace {
 constexpr size_t kChunkBytes = 256ull << 20;
+constexpr int kRendezvousMs = 300000;  // every rank of the job connects within 5 minutes
 void nccl_check(ncclResult_t r, const char* what) {
   if (r != ncclSuccess) throw std::runtime_error(std::string(what) + ": " + ncclGetErrorString(r));
 }
@@ -34,65 +32,18 @@ void hip_check(hipError_t e, const char* what) {
   if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
 }
 
-bool send_all(int fd, const void* p, size_t n) {
-  const char* c = static_cast<const char*>(p);
-  while (n) {
-    const ssize_t k = ::send(fd, c, n, 0);
-    if (k <= 0) return false;
-    c += k;
-    n -= (size_t)k;
-  }
-  return true;
-}
-bool recv_all(int fd, void* p, size_t n) {
-  char* c = static_cast<char*>(p);
-  while (n) {
-    const ssize_t k = ::recv(fd, c, n, 0);
-    if (k <= 0) return false;
-    c += k;
-    n -= (size_t)k;
-  }
-  return true;
-}
-
-// rank 0 creates the id and serves it to world - 1 connections
+// rank 0 creates the id and serves it to the other ranks (mgh_rendezvous:
+// host names resolve, every wait has a deadline, descriptors never leak)
 ncclUniqueId rendezvous(int rank, int world, const std::string& addr, int port) {
   ncclUniqueId id;
-  if (world == 1) {
-    nccl_check(ncclGetUniqueId(&id), "ncclGetUniqueId");
-    return id;
-  }
-  sockaddr_in sa{};
-  sa.sin_family = AF_INET;
-  sa.sin_port = htons((uint16_t)port);
-  if (inet_pton(AF_INET, addr.c_str(), &sa.sin_addr) != 1) throw std::runtime_error("bad MASTER_ADDR " + addr);
-  if (rank == 0) {
-    nccl_check(ncclGetUniqueId(&id), "ncclGetUniqueId");
-    const int fd = ::socket(AF_INET, SOCK_STREAM, 0);
-    const int one = 1;
-    ::setsockopt(fd, SOL_SOCKET, SO_REUSEADDR, &one, sizeof one);
-    if (::bind(fd, reinterpret_cast<sockaddr*>(&sa), sizeof sa) || ::listen(fd, world))
-      throw std::runtime_error("rendezvous: cannot listen on port " + std::to_string(port));
-    for (int i = 1; i < world; ++i) {
-      const int c = ::accept(fd, nullptr, nullptr);
-      if (c < 0 || !send_all(c, &id, sizeof id)) throw std::runtime_error("rendezvous: send failed");
-      ::close(c);
-    }
-    ::close(fd);
-    return id;
-  }
-  for (int attempt = 0; attempt < 600; ++attempt) {  // rank 0 may not listen yet: retry for 60 s
-    const int fd = ::socket(AF_INET, SOCK_STREAM, 0);
-    if (::connect(fd, reinterpret_cast<sockaddr*>(&sa), sizeof sa) == 0) {
-      const bool ok = recv_all(fd, &id, sizeof id);
-      ::close(fd);
-      if (!ok) throw std::runtime_error("rendezvous: receive failed");
-      return id;
-    }
-    ::close(fd);
-    std::this_thread::sleep_for(std::chrono::milliseconds(100));
-  }
-  throw std::runtime_error("rendezvous: rank 0 unreachable");
+  if (rank == 0) nccl_check(ncclGetUniqueId(&id), "ncclGetUniqueId");
+  if (world == 1) return id;
+  const int rc = mgh_rendezvous(rank, world, addr.c_str(), port, &id, sizeof id, kRendezvousMs);
+  if (rc)
+    throw std::runtime_error("rendezvous with rank 0 at " + addr + ":" + std::to_string(port) + " failed (" +
+                             (rc == -2 ? "address does not resolve" : rc == -3 ? "cannot listen" :
+                              rc == -4 ? "deadline passed: a rank never connected" : "I/O error") + ")");
+  return id;
 }
 }  // namespace
 

@@ -37,7 +37,7 @@ class _Timings(C.Structure):
 
 class _Counters(C.Structure):
     _fields_ = [("sources", C.c_uint64), ("runs", C.c_uint64), ("entries", C.c_uint64),
-                ("verified", C.c_uint64), ("rows", C.c_uint64), ("trips", C.c_uint64),
+                ("verified", C.c_uint64), ("rows", C.c_uint64), ("live_cells", C.c_uint64),
                 ("c_runs", C.c_uint64), ("c_entries", C.c_uint64), ("c_verified", C.c_uint64),
                 ("c_contained", C.c_uint64)]
 
@@ -247,6 +247,7 @@ class OverlapEngine:
         self._h = h
         self.n_reads = 0
         self.lengths_differ = False
+        self.max_len = 0  # longest uploaded read (> 1024 bp: long-read kernels, no exchange mode)
 
     def close(self):
         if getattr(self, "_h", None):
@@ -272,6 +273,7 @@ class OverlapEngine:
         self._check(lib().mg_upload_reads_packed(self._h, _ptr(words), _ptr(lens), lens.shape[0], wpr), "upload")
         self.n_reads = int(lens.shape[0])
         self.lengths_differ = bool(lens.shape[0]) and int(lens.min()) != int(lens.max())
+        self.max_len = int(lens.max()) if lens.shape[0] else 0
 
     def upload_ascii(self, seqs: Sequence[str]):
         data = "".join(seqs).encode()
@@ -280,6 +282,7 @@ class OverlapEngine:
         self._check(lib().mg_upload_reads_ascii(self._h, data, _ptr(off), len(seqs)), "upload_ascii")
         self.n_reads = len(seqs)
         self.lengths_differ = len({len(x) for x in seqs}) > 1
+        self.max_len = max((len(x) for x in seqs), default=0)
 
     def ingest_ascii(self, seqs: Sequence[str] | None = None, min_overlap: int = 0, text: bytes | None = None,
                      offsets: np.ndarray | None = None) -> int:
@@ -337,8 +340,10 @@ class OverlapEngine:
         if self.n_reads:
             _, lens = self.download_packed()
             self.lengths_differ = int(lens.min()) != int(lens.max())
+            self.max_len = int(lens.max())
         else:
             self.lengths_differ = False
+            self.max_len = 0
 
     def dataset_counts(self):
         g, u = C.c_uint64(), C.c_uint64()
@@ -395,6 +400,12 @@ class OverlapEngine:
         got = C.c_uint64()
         self._check(lib().mg_copy_rows(self._h, _ptr(out), n_rows, C.byref(got)), "copy_rows")
         return out[: got.value]
+
+    def copy_rows_to(self, host_ptr: int, cap: int) -> int:
+        """mg_copy_rows into caller-owned host memory (e.g. a pinned buffer of cap * 12 bytes)."""
+        got = C.c_uint64()
+        self._check(lib().mg_copy_rows(self._h, C.c_void_p(host_ptr), cap, C.byref(got)), "copy_rows")
+        return int(got.value)
 
     def lookup(self, key: str):
         n = C.c_uint64()

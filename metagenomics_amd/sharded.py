@@ -42,6 +42,9 @@ import numpy as np
 from .overlap import EDGE_DTYPE, MG_KEYS, MG_ROWS, MG_RUNS, RECORD_BYTES
 
 SLOT_ALIGN = 64  # slots are whole multiples of this many records (the probe tiles a slot by its divisors)
+# the exchange mode's kernels keep a read in registers and pack window
+# positions into 10 bits: reads up to 1,024 bp (longer ones: replicated mode)
+EXCHANGE_MAX_BP = 1024
 KINDS = (MG_KEYS, MG_RUNS, MG_ROWS)
 
 
@@ -263,6 +266,9 @@ class ShardResult:
     # kind -> (slot, rounds, [per local rank: per-peer send counts]): the slot layout moves
     # rounds * slot records to every peer whatever the count (padding(), outside the timed step)
     streams: dict = field(default_factory=dict)
+    # long-read fallback (replicated mode): per local rank the rows it holds, on the host
+    host_rows: list | None = None
+    mode: str = "exchange"
 
     def padding(self, world: int, rank_ids: list) -> dict:
         """Per stream kind: records the slot layout moved between ranks vs the records sent
@@ -283,6 +289,8 @@ class ShardResult:
 
     def rows_numpy(self, i: int = 0) -> np.ndarray:
         """The rows of local rank i, compacted out of the slot layout (host copy)."""
+        if self.host_rows is not None:
+            return self.host_rows[i]
         buf, cnt, slot, rounds = self.rows[i]
         c = cnt.cpu().numpy().astype(np.int64)
         P = len(c)
@@ -312,6 +320,8 @@ def sharded_step(engines: list, xchg: Exchange, min_overlap: int, seed_k: int = 
     """One exchange-mode step over the local ranks' engines (set up with
     ``set_shard(rank, world)`` and the full read set uploaded).  ``plan`` carries the
     stream capacities from step to step (grown in place after an overflow)."""
+    if any(e.max_len > EXCHANGE_MAX_BP for e in engines):
+        return _replicated_step(engines, xchg, min_overlap, seed_k, want_super)
     if plan is None:
         plan = initial_plan(engines[0], xchg.world, min_overlap, seed_k)
     reruns = 0
@@ -325,6 +335,39 @@ def sharded_step(engines: list, xchg: Exchange, min_overlap: int, seed_k: int = 
         plan.reruns += 1
         if reruns > 3:
             raise RuntimeError(f"exchange capacities still overflow after {reruns} reruns: {used}")
+
+
+_warned_long = [False]
+
+
+def _replicated_step(engines, xchg, min_overlap, seed_k, want_super):
+    """Reads longer than EXCHANGE_MAX_BP (Read::getReadLength is UINT16, Read.h:62):
+    the step runs the replicated mode instead (every rank builds the
+    whole index with the long-read kernels and discovers from its source-read
+    range; no data-path collective).  Every rank holds the rows + twins of its
+    sources' discoveries; their union is the reference multiset.  The engines
+    are re-sharded to their source ranges (set_shard(0, 1, lo, hi))."""
+    if not _warned_long[0]:
+        print(f"[sharded] reads longer than {EXCHANGE_MAX_BP} bp: the exchange mode's kernels stop there; "
+              "this step runs the replicated mode (whole index per rank, source-read shards, no data-path "
+              "collective)", flush=True)
+        _warned_long[0] = True
+    P = xchg.world
+    t0 = time.perf_counter()
+    host_rows, n_rows, sup = [], [], None
+    for i, (e, r) in enumerate(zip(engines, xchg.ranks)):
+        lo, hi = source_range(e.n_reads, r, P)
+        e.set_shard(0, 1, lo, hi if hi > lo else lo)
+        e.build_index(min_overlap, seed_k)
+        s = e.mark_contained(copy=want_super and i == 0)
+        sup = s if s is not None else sup
+        n = e.find_overlaps() if hi > lo else 0  # (read_hi == read_lo == 0 would mean "all")
+        host_rows.append(e.rows(n) if n else np.zeros(0, dtype=EDGE_DTYPE))
+        n_rows.append(n)
+    xchg.barrier()
+    ms = {"index": 0.0, "contained": 0.0, "overlap": (time.perf_counter() - t0) * 1e3}
+    return ShardResult(rows=[], ms=ms, contained=bool(engines[0].lengths_differ), super_read_id=sup,
+                       n_rows=n_rows, host_rows=host_rows, mode="replicated")
 
 
 def _step(engines, xchg, min_overlap, seed_k, want_super, plan):

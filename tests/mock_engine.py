@@ -77,6 +77,7 @@ class MockEngine:
         self.rows = rows  # the full directed multiset (EDGE_DTYPE)
         self.n_reads = n_reads
         self.lengths_differ = lengths_differ
+        self.max_len = 150  # (reads <= 1024 bp: the exchange path, not the long-read fallback)
         self.lo, self.hi = n_reads * rank // world, n_reads * (rank + 1) // world
         self.caps = caps  # small first capacities: the steps exercise the overflow rerun
         self.received_keys = None

@@ -701,6 +701,41 @@ def test_containment_options(name):
         assert np.array_equal(rows_to_tuples(rows), want_rows), opts
 
 
+@pytest.mark.parametrize("name", ["mixed", "dirty", "branchy", "prefixes", "metagenome"])
+def test_live_index_forced(name):
+    """The discovery index of the uncontained reads (option live_index) against
+    the goldens with the live table really in use: a large directory (nb_log2 =
+    16) makes the live reads' table smaller than the full one even on the small
+    fixtures, and counters().live_cells proves the probe walked it (on the
+    default directory of a small set both tables get 2^10 cells, the live build
+    is skipped, and a live_index on/off comparison would be vacuous)."""
+    if name in ("prefixes", "metagenome"):
+        if name == "prefixes":
+            seqs, l = prefix_reads(), 40
+        else:
+            c, L = synth.metagenome_read_set(20000, 100, 250, n_genomes=20, total_len=400000, seed=51)
+            seqs, l = synth.codes_to_strings(c, L), 50
+        ds = Dataset.from_strings(seqs, l)
+        orows, osup, _, _ = OracleDataset.from_strings(seqs, l).overlaps(l)
+        want_rows, want_sup = sorted_tuples(orows), {str(i): int(x) for i, x in enumerate(osup) if x}
+    else:
+        meta = load_meta(name)
+        l = meta["l"]
+        ds = Dataset.from_files([fixture_input(name)], l)
+        want_rows, want_sup = golden_rows(name), meta["super"]
+    assert want_sup
+    for live in (1, 0):
+        e = OverlapEngine(0)
+        e.set_option("live_index", live)
+        e.set_option("stats", 1)
+        rows, sup = gpu_rows(e, ds, l, nb_log2=16)
+        cells = e.counters()["live_cells"]
+        e.close()
+        assert (cells > 0) == bool(live) and cells < (1 << 16), (live, cells)
+        assert {str(i): int(x) for i, x in enumerate(sup) if x} == want_sup, live
+        assert np.array_equal(rows_to_tuples(rows), want_rows), live
+
+
 @pytest.mark.parametrize("name", ["small", "mixed", "tandem", "highdup", "tworead"])
 def test_replicated_index_source_shards(name):
     """Multi-GPU replicated mode (bench --multi replicated): every rank builds

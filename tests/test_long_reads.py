@@ -174,10 +174,43 @@ def test_long_reads_device_ingest(engine):
 
 
 def test_long_reads_exchange_refused(engine):
-    """The bucket-sharded exchange mode is for reads <= 1 kb: a clear error."""
+    """The bucket-sharded exchange kernels are for reads <= 1 kb: at the C-ABI a
+    clear error (sharded_step falls back to the replicated mode, below)."""
     seqs = long_set(20, 1500, 2000, 20_000, 206)
     ds = Dataset.from_strings(seqs, 50)
     engine.set_shard(0, 1)
     engine.upload(ds)
     with pytest.raises(RuntimeError, match="1024"):
         engine.xchg_begin(50, 31)
+
+
+@pytest.mark.parametrize("world", [1, 3])
+def test_long_reads_exchange_step_falls_back(world):
+    """sharded_step (the multi-GPU default, bench --gpus N) on a set with reads
+    over 1,024 bp runs the replicated mode (whole index per rank, source-range
+    shards) and says so: the union over the simulated ranks is the reference's
+    multiset (the reference-generated longreads fixture: 150 bp-9 kb reads) and
+    the superReadIDs are the reference's."""
+    import torch
+
+    from conftest import fixture_input, golden_rows, load_meta
+    from metagenomics_amd.sharded import LocalExchange, sharded_step
+
+    meta = load_meta("longreads")
+    l = meta["l"]
+    ds = Dataset.from_files([fixture_input("longreads")], l)
+    engines = []
+    for r in range(world):
+        e = OverlapEngine(0)
+        e.set_shard(r, world, 0, 0)
+        e.upload(ds)
+        engines.append(e)
+    assert max(e.max_len for e in engines) > 1024
+    res = sharded_step(engines, LocalExchange(world, torch.device("cuda:0")), l, 0, want_super=True)
+    assert res.mode == "replicated"
+    rows = np.concatenate([res.rows_numpy(r) for r in range(world)])
+    assert sum(res.n_rows) == rows.shape[0]
+    for e in engines:
+        e.close()
+    assert np.array_equal(rows_to_tuples(rows), golden_rows("longreads"))
+    assert {str(i): int(x) for i, x in enumerate(res.super_read_id) if x} == meta["super"]
