@@ -147,9 +147,6 @@ struct mg_ctx {
   // the containment probe skips suffix-key hits (containment)
   uint64_t* d_key0 = nullptr;
   size_t key0_cap = 0;
-  // exchange mode, mixed lengths: the o = 0 key records this rank filed
-  // (k_insert_slots), walked by k_prefix_contain_rec before the containment
-  // probe, which then drops o = 1/3 hits like the fused path (xchg_prefix)
   // exchange mode: the received runs ordered by local bucket (sort_xruns), the
   // input of both probes; xruns_ready until the next mg_xchg_begin
   uint32_t* d_xk[2] = {nullptr, nullptr};
@@ -160,9 +157,26 @@ struct mg_ctx {
   int xv_sel = 0;
   uint64_t xruns_n = 0;
   bool xruns_ready = false;
-  ulonglong2* d_k0rec = nullptr;
-  size_t k0rec_cap = 0;
-  unsigned long long* d_k0n = nullptr;
+  // exchange mode: the key records this rank received, dense and grouped by
+  // bin of home cells (mg_xchg_insert_keys: key = local home cell, ent = index
+  // entry); they build the cells, the o = 0 ones drive the prefix containments
+  // (k_prefix_contain_keys, xchg_prefix) and the live ones the discovery index
+  uint32_t* d_xkk[2] = {nullptr, nullptr};
+  uint64_t* d_xke[2] = {nullptr, nullptr};
+  size_t xkk_cap[2] = {0, 0}, xke_cap[2] = {0, 0};
+  int xkey_sel = 0;
+  uint64_t xkeys_n = 0;
+  // overflow list of k_cells_build (a cell's entries past its 8 slots)
+  uint32_t* d_ovf_c = nullptr;
+  uint64_t* d_ovf_e = nullptr;
+  size_t ovf_c_cap = 0, ovf_e_cap = 0;
+  unsigned long long* d_novf = nullptr;
+  // the exchange mode's discovery index coarsens the rank's cells (cell =
+  // local home cell >> live_shift) instead of rebuilding entries
+  bool live_coarse = false;
+  uint32_t live_shift = 0;
+  bool xchg_sort_runs = true;  // option "xchg_sort_runs": received runs ordered by bucket before the probes
+  bool layout_scratch = true;  // option "layout_scratch" = 0: free the layout's double buffers after each layout
   bool xchg_prefix = false;
   bool key0_ready = false;
   bool prefix_contain = true;  // option "prefix_contain"
@@ -238,6 +252,7 @@ inline void reset_derived(mg_ctx* ctx) {
   ctx->contained_done = false;
   ctx->super_any = false;
   ctx->live_ready = false;
+  ctx->live_coarse = false;
   ctx->n_contained = 0;
   ctx->n_rows = 0;
 }

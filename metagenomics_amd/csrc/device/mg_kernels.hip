@@ -403,32 +403,37 @@ __global__ __launch_bounds__(kBlock) void k_prefix_contain(const uint64_t* __res
                             (uint32_t)(k0 >> nb_log2) & kFpMask, (uint32_t)(k0 >> 54), superkey, id);
 }
 
-// Exchange mode: the same walk from the o = 0 key records this rank filed
-// (k_insert_slots kept them: x = bucket, y = entry), over its own cells
+// Exchange mode: the same walk from the o = 0 records among the key records
+// this rank received (dense and grouped by bin, mg_xchg_insert_keys: key[i] =
+// local home cell, ent[i] = index entry), over its own cells; consecutive
+// records walk neighbouring cells
 template <int MAXW>
-__global__ __launch_bounds__(kBlock) void k_prefix_contain_rec(const uint64_t* __restrict__ words,
-                                                               const uint16_t* __restrict__ len,
-                                                               const ulonglong2* __restrict__ rec,
-                                                               const unsigned long long* __restrict__ nrec,
-                                                               const uint64_t* __restrict__ cells, uint64_t cell_lo,
-                                                               uint64_t cell_n, unsigned long long* __restrict__ superkey,
-                                                               const uint32_t* __restrict__ id) {
-  const uint64_t nr = *nrec;
-  for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < nr; i += (uint64_t)gridDim.x * kBlock) {
-    const ulonglong2 x = rec[i];
-    const uint32_t hi = (uint32_t)(x.y >> 32);
-    prefix_contain_walk<MAXW>(words, len, cells, cell_n, x.x - cell_lo, (uint32_t)x.y, (hi >> 12) & kFpMask,
-                              (hi >> 2) & 1023u, superkey, id);
+__global__ __launch_bounds__(kBlock) void k_prefix_contain_keys(const uint64_t* __restrict__ words,
+                                                                const uint16_t* __restrict__ len,
+                                                                const uint32_t* __restrict__ key,
+                                                                const uint64_t* __restrict__ ent, uint64_t n,
+                                                                const uint64_t* __restrict__ cells, uint64_t cell_n,
+                                                                unsigned long long* __restrict__ superkey,
+                                                                const uint32_t* __restrict__ id) {
+  for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBlock) {
+    const uint64_t e = ent[i];
+    const uint32_t hi = (uint32_t)(e >> 32);
+    if (hi & 3u) continue;  // o = 0 keys only
+    prefix_contain_walk<MAXW>(words, len, cells, cell_n, key[i], (uint32_t)e, (hi >> 12) & kFpMask, (hi >> 2) & 1023u,
+                              superkey, id);
   }
 }
 
 template <int W>
-struct LaunchPrefixContainRec {
+struct LaunchPrefixContainKeys {
   static int run(mg_ctx* ctx) {
+    const uint64_t n = ctx->xkeys_n;
+    if (!n) return 0;
     const uint32_t grid = (uint32_t)std::max<uint64_t>(
-        1, std::min<uint64_t>((ctx->n + kBlock - 1) / kBlock, (uint64_t)ctx->n_cu * 16));
-    hipLaunchKernelGGL(k_prefix_contain_rec<W>, dim3(grid), dim3(kBlock), 0, ctx->stream, ctx->d_words, ctx->d_len,
-                       ctx->d_k0rec, ctx->d_k0n, ctx->d_cells, ctx->cell_lo, ctx->cell_n, ctx->superkey, ctx->d_id);
+        1, std::min<uint64_t>((n + kBlock - 1) / kBlock, (uint64_t)ctx->n_cu * 16));
+    hipLaunchKernelGGL(k_prefix_contain_keys<W>, dim3(grid), dim3(kBlock), 0, ctx->stream, ctx->d_words, ctx->d_len,
+                       ctx->d_xkk[ctx->xkey_sel], ctx->d_xke[ctx->xkey_sel], n, ctx->d_cells, ctx->cell_n,
+                       ctx->superkey, ctx->d_id);
     return hipGetLastError() == hipSuccess ? 0 : -1;
   }
 };
@@ -444,43 +449,127 @@ struct LaunchPrefixContain {
   }
 };
 
-// Exchange mode: file the key records this rank received, in the slot layout
-// of include/mg_overlap.h (record i of peer s at ((i / slot) P + s) slot +
-// i % slot, present while i < counts[s]); x = bucket, y = index entry.
-// Neighbouring records are keys of neighbouring (clustered) reads and often
-// share a minimizer cell, so the lanes of a wavefront take records 64 apart
-// (a 64 x 64 transpose of each 4096-record tile): CAS on one cell from many
-// lanes at once retries serially.
-// k0out (mixed lengths): the o = 0 records are also kept for k_prefix_contain_rec.
-__global__ __launch_bounds__(kBlock) void k_insert_slots(IndexParams p, const ulonglong2* __restrict__ rec,
-                                                         uint64_t slot, uint32_t rounds,
-                                                         const unsigned long long* __restrict__ counts,
-                                                         ulonglong2* __restrict__ k0out,
-                                                         unsigned long long* __restrict__ k0n) {
-  const uint64_t P = p.nranks, blk = P * slot, total = (uint64_t)rounds * blk;
-  const uint64_t tiles_end = total & ~(uint64_t)(kWave * kWave - 1);  // whole 4096-record tiles
-  for (uint64_t j = (uint64_t)blockIdx.x * kBlock + threadIdx.x; j < total; j += (uint64_t)gridDim.x * kBlock) {
-    const uint64_t u = j & (kWave * kWave - 1);
-    const uint64_t idx = j < tiles_end ? (j - u) + (u & (kWave - 1)) * kWave + (u >> 6) : j;
-    const uint64_t t = idx / blk, rem = idx - t * blk, s = rem / slot;
-    bool k0 = false;
-    ulonglong2 x = make_ulonglong2(0, 0);
-    if (t * slot + (rem - s * slot) < counts[s]) {
-      x = rec[idx];
-      const uint64_t c = x.x - p.cell_lo;
-      if (c < p.cell_n) {
-        cell_insert(p.cells, c, p.cell_n, x.y);
-        k0 = k0out && ((x.y >> 32) & 3u) == 0;
+// ---- exchange mode: the received key records filed without global atomics
+// (HashTable::insertDataset / insertIntoTable, HashTable.cpp:50-80,163-195).
+// mg_xchg_insert_keys makes the records dense (k_xkeys_dense: local home cell +
+// entry) and groups them by BIN (kBinCells consecutive cells, one radix sort
+// over the bin bits); k_cells_build then builds each bin's cells in LDS: LDS
+// atomics deal the slots, a cell with more entries than slots gets the chain
+// flag, and the bin leaves as whole 64-B lines (every cell of the table is
+// written, so the table needs no clear).  A cell's 9th and later entries go to
+// an overflow list that k_cells_overflow files with cell_insert after the build
+// (the chain starts at the flagged home cell, so insertion and every walk
+// follow the same sequence).  CAS inserts of received keys (k_insert_slots)
+// cost ~7 G keys/s of memory-side atomics on the step's critical path; the
+// fused path hides the same CASes behind its scan.  The same build over the
+// same records, filtered to the uncontained reads and with cells coarsened by
+// `shift`, is the exchange mode's discovery index (build_live_index_xchg).
+constexpr int kBinLog2 = 9;
+constexpr uint32_t kBinCells = 1u << kBinLog2;  // 512 cells = 32 KiB of LDS per bin
+
+__global__ __launch_bounds__(kBlock) void k_xkeys_dense(const ulonglong2* __restrict__ recv, uint64_t slot,
+                                                       uint32_t nranks, uint64_t total,
+                                                       const unsigned long long* __restrict__ counts,
+                                                       uint64_t cell_lo, uint32_t* __restrict__ key,
+                                                       uint64_t* __restrict__ ent) {
+  const uint64_t blk = (uint64_t)nranks * slot, lim = total / nranks;  // records per peer stream
+  for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < total; i += (uint64_t)gridDim.x * kBlock) {
+    const uint64_t t = i / blk, rem = i - t * blk, sp = rem / slot, j = t * slot + (rem - sp * slot);
+    if (j >= counts[sp]) continue;
+    uint64_t at = j;
+    for (uint64_t q = 0; q < sp; ++q) at += counts[q] < lim ? counts[q] : lim;
+    const ulonglong2 x = recv[i];  // x = global bucket, y = entry
+    key[at] = (uint32_t)(x.x - cell_lo);
+    ent[at] = x.y;
+  }
+}
+
+struct CellBuild {
+  const uint32_t* key;        // home cell (full table) of each record, grouped by key >> kBinLog2
+  const uint64_t* ent;
+  uint64_t n;
+  uint32_t shift;             // cell of the table built = key >> shift
+  uint64_t cell_n;            // cells of the table built
+  uint64_t* cells;
+  const uint32_t* cbits;      // non-null: only entries of uncontained reads (discovery index)
+  uint32_t* ovf_cell;         // overflow list (capacity n)
+  uint64_t* ovf_ent;
+  unsigned long long* novf;
+};
+
+// first record whose bin (key >> sh) is >= bin
+__device__ __forceinline__ uint64_t bin_lower_bound(const uint32_t* __restrict__ key, uint64_t n, uint32_t sh,
+                                                    uint64_t bin) {
+  uint64_t lo = 0, hi = n;
+  while (lo < hi) {
+    const uint64_t mid = (lo + hi) >> 1;
+    if ((uint64_t)(key[mid] >> sh) < bin) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+
+__global__ __launch_bounds__(kBlock) void k_cells_build(CellBuild p) {
+  __shared__ __attribute__((aligned(16))) unsigned long long s_cell[kBinCells * kCell];
+  __shared__ uint32_t s_cnt[kBinCells];
+  __shared__ uint64_t s_rng[2];
+  const int lane = threadIdx.x & 63;
+  const uint32_t sh = kBinLog2 + p.shift;
+  const uint64_t nbins = (p.cell_n + kBinCells - 1) >> kBinLog2;
+  for (uint64_t bin = blockIdx.x; bin < nbins; bin += gridDim.x) {
+    for (uint32_t i = threadIdx.x; i < kBinCells * kCell; i += kBlock) s_cell[i] = kEmpty;
+    for (uint32_t i = threadIdx.x; i < kBinCells; i += kBlock) s_cnt[i] = 0;
+    if (threadIdx.x < 2) s_rng[threadIdx.x] = bin_lower_bound(p.key, p.n, sh, bin + threadIdx.x);
+    __syncthreads();
+    const uint64_t lo = s_rng[0], hi = s_rng[1];
+    for (uint64_t i0 = lo; i0 < hi; i0 += kBlock) {  // (uniform trip count: the ballot below)
+      const uint64_t i = i0 + threadIdx.x;
+      bool ov = false;
+      uint32_t c = 0;
+      uint64_t e = 0;
+      if (i < hi) {
+        e = p.ent[i];
+        c = p.key[i] >> p.shift;
+        const uint32_t r = (uint32_t)e;
+        if (!p.cbits || !((p.cbits[r >> 5] >> (r & 31u)) & 1u)) {
+          const uint32_t lc = c & (kBinCells - 1);
+          const uint32_t k = atomicAdd(&s_cnt[lc], 1u);
+          if (k < (uint32_t)kCell) s_cell[lc * kCell + k] = e;
+          else ov = true;
+        }
+      }
+      const uint64_t bal = __ballot(ov);
+      if (bal) {  // wavefront-aggregated append to the overflow list
+        unsigned long long base = 0;
+        if (lane == 0) base = atomicAdd(p.novf, (unsigned long long)__popcll(bal));
+        base = __shfl(base, 0);
+        if (ov) {
+          const uint64_t at = base + lane_prefix(bal);
+          p.ovf_cell[at] = c;
+          p.ovf_ent[at] = e;
+        }
       }
     }
-    if (k0out) {  // wavefront-aggregated append (every lane of the wavefront reaches here)
-      const uint64_t bal = __ballot(k0);
-      unsigned long long base = 0;
-      if ((threadIdx.x & 63) == 0 && bal) base = atomicAdd(k0n, (unsigned long long)__popcll(bal));
-      base = __shfl(base, 0);
-      if (k0) k0out[base + lane_prefix(bal)] = x;
-    }
+    __syncthreads();
+    const uint64_t c0 = bin << kBinLog2;
+    const uint32_t nc = (uint32_t)(p.cell_n - c0 < kBinCells ? p.cell_n - c0 : kBinCells);
+    for (uint32_t c = threadIdx.x; c < nc; c += kBlock)
+      if (s_cnt[c] > (uint32_t)kCell) s_cell[c * kCell + kCell - 1] |= kChain;
+    __syncthreads();
+    ulonglong2* dst = reinterpret_cast<ulonglong2*>(p.cells + c0 * kCell);
+    const ulonglong2* src = reinterpret_cast<const ulonglong2*>(s_cell);
+    for (uint32_t i = threadIdx.x; i < nc * (kCell / 2); i += kBlock) dst[i] = src[i];
+    __syncthreads();
   }
+}
+
+__global__ __launch_bounds__(kBlock) void k_cells_overflow(uint64_t* cells, uint64_t cell_n,
+                                                          const uint32_t* __restrict__ ovf_cell,
+                                                          const uint64_t* __restrict__ ovf_ent,
+                                                          const unsigned long long* __restrict__ novf) {
+  const uint64_t n = *novf;
+  for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBlock)
+    cell_insert(cells, ovf_cell[i], cell_n, ovf_ent[i]);
 }
 
 // ------------------------------------------------------------- discovery ---
@@ -504,10 +593,10 @@ struct ScanParams {
   uint64_t cell_n;
   // exchange mode: the four key records of read a go to key_bk / key_ent[o *
   // key_n + a] (bucket, entry) instead of a CAS into the cells; they travel to
-  // the bucket owner (k_part) and k_insert_slots files them there
+  // the bucket owner (k_part) and mg_xchg_insert_keys files them there
   uint32_t* key_bk;
   uint64_t* key_ent;
-  uint64_t key_n;
+  uint64_t key_n, key_lo;       // key o of source read a at o * key_n + (a - key_lo)
   // per read: its o = 0 key's hash bits (bucket | fingerprint, 50 bits) | q << 54
   // (k_prefix_contain); nullptr: not written
   uint64_t* key0;
@@ -892,8 +981,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(G > 1 ? 
         const unsigned long long e = make_entry(v, p.nb_log2, (int)(kb[o] & 1023u), o, (uint32_t)a);
         if (o == 0 && p.key0) p.key0[a] = (v & ((1ULL << 50) - 1)) | ((uint64_t)(kb[0] & 1023u) << 54);
         if constexpr (KEYREC) {  // o-major: each store is one coalesced wavefront line
-          p.key_bk[o * p.key_n + a] = (uint32_t)(v & nbm);
-          p.key_ent[o * p.key_n + a] = e;
+          p.key_bk[o * p.key_n + a - p.key_lo] = (uint32_t)(v & nbm);
+          p.key_ent[o * p.key_n + a - p.key_lo] = e;
         }
         cb[o] = v & nbm;
         ce[o] = e;
@@ -908,8 +997,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(G > 1 ? 
       if (p.key0) p.key0[a] = kEmpty;
       if constexpr (KEYREC) {
         for (int o = 0; o < 4; ++o) {
-          p.key_bk[o * p.key_n + a] = 0;
-          p.key_ent[o * p.key_n + a] = kEmpty;
+          p.key_bk[o * p.key_n + a - p.key_lo] = 0;
+          p.key_ent[o * p.key_n + a - p.key_lo] = kEmpty;
         }
       }
     }
@@ -1115,10 +1204,11 @@ __global__ __launch_bounds__(kBlock) void k_scan_reg(ScanParams p) {
           c0 = make_entry(v0, p.nb_log2, p0, 0, (uint32_t)a);
           c1 = make_entry(v1, p.nb_log2, p1 - (n - h), 1, (uint32_t)a);
         }
-        p.key_bk[a] = b0;
-        p.key_ent[a] = c0;
-        p.key_bk[p.key_n + a] = b1;
-        p.key_ent[p.key_n + a] = c1;
+        const uint64_t ka = a - p.key_lo;
+        p.key_bk[ka] = b0;
+        p.key_ent[ka] = c0;
+        p.key_bk[p.key_n + ka] = b1;
+        p.key_ent[p.key_n + ka] = c1;
       }
     }
   }
@@ -1176,10 +1266,11 @@ __global__ __launch_bounds__(kBlock) void k_rc_keys(ScanParams p) {
   }
   const uint64_t v2 = mix64(mb2), v3 = mix64(mb3);
   const uint64_t nbm = (1ULL << p.nb_log2) - 1;  // (bucket, entry) records, o-major
-  p.key_bk[2 * p.key_n + a] = n ? (uint32_t)(v2 & nbm) : 0u;
-  p.key_ent[2 * p.key_n + a] = n ? make_entry(v2, p.nb_log2, (int)(kb2 & 1023u), 2, (uint32_t)a) : kEmpty;
-  p.key_bk[3 * p.key_n + a] = n ? (uint32_t)(v3 & nbm) : 0u;
-  p.key_ent[3 * p.key_n + a] = n ? make_entry(v3, p.nb_log2, (int)(kb3 & 1023u), 3, (uint32_t)a) : kEmpty;
+  const uint64_t ka = a - p.key_lo;
+  p.key_bk[2 * p.key_n + ka] = n ? (uint32_t)(v2 & nbm) : 0u;
+  p.key_ent[2 * p.key_n + ka] = n ? make_entry(v2, p.nb_log2, (int)(kb2 & 1023u), 2, (uint32_t)a) : kEmpty;
+  p.key_bk[3 * p.key_n + ka] = n ? (uint32_t)(v3 & nbm) : 0u;
+  p.key_ent[3 * p.key_n + ka] = n ? make_entry(v3, p.nb_log2, (int)(kb3 & 1023u), 3, (uint32_t)a) : kEmpty;
 }
 
 // checkOverlap's string compare (OverlapGraph.cpp:354-383) on packed words:
@@ -1213,6 +1304,7 @@ struct ProbeParams {
   uint32_t nb_log2;
   uint32_t rank, nranks;
   uint64_t cell_lo, cell_n;       // local bucket range of the cell table (IndexParams)
+  uint32_t cell_shift;            // cell = (bucket - cell_lo) >> cell_shift (the exchange mode's discovery index)
   const uint64_t* cells;
   const uint32_t* cbits;          // discovery: contained slots as bits (mg_ctx::d_cbits; nullptr: none contained)
   unsigned long long* superkey;   // CONTAIN: max over containers of (len << 32 | ~index)
@@ -1510,7 +1602,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MG_PROBE
             __hip_atomic_load(&p.superkey[ra], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0)
           valid = false;
       }
-      key = (valid ? bucket - p.cell_lo : 0) | ((uint64_t)fpv << 32);
+      key = (valid ? (bucket - p.cell_lo) >> p.cell_shift : 0) | ((uint64_t)fpv << 32);
       stat(0, valid ? 1u : 0u);
       rpos += rstep;
       pf_any = hbm_settle();
@@ -2617,7 +2709,8 @@ struct LaunchScan {
     if (index && ctx->xchg) {  // key records (bucket, entry), o-major: they travel to the bucket owner
       sp.key_bk = ctx->d_kb;
       sp.key_ent = ctx->d_ke;
-      sp.key_n = ctx->n;
+      sp.key_n = a_hi - a_lo;  // the rank's sources only
+      sp.key_lo = a_lo;
     }
     (void)hipEventRecord(ctx->ev[6], stream);
     if (scan_is_reg(ctx, index)) {
@@ -2672,7 +2765,11 @@ struct LaunchProbe {
     pp.cell_lo = ctx->cell_lo;
     pp.cell_n = ctx->cell_n;
     pp.cells = ctx->d_cells;
-    if (!contain && ctx->live_ready) {  // the discovery index of uncontained reads (build_live_index)
+    if (!contain && ctx->live_ready && ctx->live_coarse) {  // exchange mode (build_live_index_xchg)
+      pp.cell_shift = ctx->live_shift;
+      pp.cell_n = ctx->live_cells;
+      pp.cells = ctx->d_lcells;
+    } else if (!contain && ctx->live_ready) {  // the discovery index of uncontained reads (build_live_index)
       pp.nb_log2 = ctx->lnb_log2;
       pp.cell_lo = 0;
       pp.cell_n = 1ull << ctx->lnb_log2;
@@ -2893,7 +2990,8 @@ void mg_destroy(mg_ctx* ctx) {
   (void)hipStreamSynchronize(ctx->stream);
   void* bufs[] = {ctx->d_words, ctx->d_len, ctx->d_cells, ctx->d_superkey, ctx->d_super, ctx->d_any, ctx->d_rows,
                   ctx->d_seg, ctx->d_stats, ctx->d_compact, ctx->d_runs, ctx->d_run_cnt, ctx->d_blk, ctx->d_flat_cnt,
-                  ctx->d_slot_cnt, ctx->d_freq, ctx->d_kb, ctx->d_ke, ctx->d_key0, ctx->d_k0rec, ctx->d_k0n,
+                  ctx->d_slot_cnt, ctx->d_freq, ctx->d_kb, ctx->d_ke, ctx->d_key0, ctx->d_xkk[0], ctx->d_xkk[1], ctx->d_xke[0], ctx->d_xke[1],
+                  ctx->d_ovf_c, ctx->d_ovf_e, ctx->d_novf,
                   ctx->d_xk[0], ctx->d_xk[1], ctx->d_xv[0], ctx->d_xv[1], ctx->d_xsort_tmp,
                   ctx->d_digest, ctx->id_store[0], ctx->id_store[1], ctx->phys_store[0], ctx->phys_store[1],
                   ctx->d_tmp32, ctx->d_lay_k[0], ctx->d_lay_k[1], ctx->d_lay_v[0], ctx->d_lay_v[1], ctx->d_lay_tmp,
@@ -3076,7 +3174,8 @@ int mg_set_option(mg_ctx* ctx, const char* name, int64_t value) {
   if (flag("stats", &ctx->stats) || flag("halving", &ctx->halving_low) || flag("layout", &ctx->layout) ||
       flag("contain_jcut", &ctx->contain_jcut) || flag("contain_skip", &ctx->contain_skip) ||
       flag("contain_prune", &ctx->contain_prune) || flag("probe_share", &ctx->probe_share) ||
-      flag("probe_compact", &ctx->probe_compact) || flag("live_index", &ctx->live_index))
+      flag("probe_compact", &ctx->probe_compact) || flag("live_index", &ctx->live_index) ||
+      flag("xchg_sort_runs", &ctx->xchg_sort_runs) || flag("layout_scratch", &ctx->layout_scratch))
     return 0;
   if (flag("prefix_contain", &ctx->prefix_contain)) {
     ctx->index_ready = false;
@@ -3186,14 +3285,6 @@ int route_slots(mg_ctx* ctx, PartParams pp, void* out, void* self_out, uint64_t 
 
 constexpr uint64_t kFlatRegion = 4096;  // records per routing region of a flat array
 constexpr uint64_t kXRegion = 1024;     // records per probe region of the ordered received runs
-
-// region size of a slot-layout run buffer for the probe: the largest power of
-// two <= 1024 that divides the slot (slots are multiples of 64 records)
-uint64_t slot_region(uint64_t slot) {
-  uint64_t reg = 1024;
-  while (reg > 1 && slot % reg) reg >>= 1;
-  return reg;
-}
 
 // region counts of a slot-layout buffer into *buf (grown as needed)
 int slot_regions(mg_ctx* ctx, unsigned long long** buf, size_t* cap, const unsigned long long* counts,
@@ -3394,6 +3485,90 @@ int build_live_index(mg_ctx* ctx) {
   if (dispatch_w<LaunchIndexLive>(ctx->maxw, ctx, &p)) return set_err(ctx, "live index launch failed");
   ctx->lnb_log2 = nbl;
   ctx->live_cells = 1ull << nbl;
+  ctx->live_coarse = false;
+  ctx->live_ready = true;
+  return 0;
+}
+
+// the cell table `cells` of cell_n cells from the rank's dense received key
+// records (k_cells_build + k_cells_overflow): cell = home cell >> shift; cbits
+// non-null = only the uncontained reads' entries
+int build_cells(mg_ctx* ctx, uint64_t* cells, uint64_t cell_n, uint32_t shift, const uint32_t* cbits) {
+  const uint64_t n = ctx->xkeys_n;
+  MG_TRY(ensure(&ctx->d_ovf_c, &ctx->ovf_c_cap, std::max<uint64_t>(n, 1)));
+  MG_TRY(ensure(&ctx->d_ovf_e, &ctx->ovf_e_cap, std::max<uint64_t>(n, 1)));
+  if (!ctx->d_novf) MG_TRY(hipMalloc(&ctx->d_novf, sizeof(unsigned long long)));
+  MG_TRY(hipMemsetAsync(ctx->d_novf, 0, sizeof(unsigned long long), ctx->stream));
+  CellBuild b{};
+  b.key = ctx->d_xkk[ctx->xkey_sel];
+  b.ent = ctx->d_xke[ctx->xkey_sel];
+  b.n = n;
+  b.shift = shift;
+  b.cell_n = cell_n;
+  b.cells = cells;
+  b.cbits = cbits;
+  b.ovf_cell = ctx->d_ovf_c;
+  b.ovf_ent = ctx->d_ovf_e;
+  b.novf = ctx->d_novf;
+  const uint64_t nbins = (cell_n + kBinCells - 1) / kBinCells;
+  if (nbins) {
+    hipLaunchKernelGGL(k_cells_build, dim3((uint32_t)std::min<uint64_t>(nbins, 1u << 20)), dim3(kBlock), 0,
+                       ctx->stream, b);
+    MG_TRY(hipGetLastError());
+    if (getenv("MG_DEBUG_OVF")) {  // TEMP diagnostics: overflow and bin size distribution
+      unsigned long long no = 0;
+      MG_TRY(hipMemcpyAsync(&no, ctx->d_novf, 8, hipMemcpyDeviceToHost, ctx->stream));
+      MG_TRY(hipStreamSynchronize(ctx->stream));
+      std::vector<uint32_t> oc(no), kk(n);
+      if (no) MG_TRY(hipMemcpy(oc.data(), ctx->d_ovf_c, no * 4, hipMemcpyDeviceToHost));
+      if (n) MG_TRY(hipMemcpy(kk.data(), b.key, n * 4, hipMemcpyDeviceToHost));
+      std::sort(oc.begin(), oc.end());
+      std::vector<uint64_t> g;
+      for (size_t i = 0; i < oc.size();) { size_t j = i; while (j < oc.size() && oc[j] == oc[i]) ++j; g.push_back(j - i); i = j; }
+      std::sort(g.rbegin(), g.rend());
+      std::vector<uint64_t> bc(nbins, 0);
+      for (uint64_t i = 0; i < n; ++i) { uint64_t bb = (kk[i] >> shift) >> kBinLog2; if (bb < nbins) bc[bb]++; }
+      std::sort(bc.rbegin(), bc.rend());
+      fprintf(stderr, "[ovf] rank %u shift %u records %lu cells %lu bins %lu overflow %llu groups %zu top groups:", ctx->rank, shift,
+              (unsigned long)n, (unsigned long)cell_n, (unsigned long)nbins, no, g.size());
+      for (size_t i = 0; i < g.size() && i < 12; ++i) fprintf(stderr, " %lu", (unsigned long)g[i]);
+      fprintf(stderr, " | top bins:");
+      for (size_t i = 0; i < bc.size() && i < 8; ++i) fprintf(stderr, " %lu", (unsigned long)bc[i]);
+      fprintf(stderr, " median %lu\n", (unsigned long)bc[bc.size() / 2]);
+    }
+    hipLaunchKernelGGL(k_cells_overflow, dim3((uint32_t)std::max(1, ctx->n_cu * 4)), dim3(kBlock), 0, ctx->stream,
+                       cells, cell_n, ctx->d_ovf_c, ctx->d_ovf_e, ctx->d_novf);
+    MG_TRY(hipGetLastError());
+  }
+  return 0;
+}
+
+// The exchange mode's discovery index (option live_index): after
+// markContainedReads the discovery probe only lists uncontained partners
+// (:548), so it walks a table of the uncontained reads' entries only.  The
+// rank's cells are coarsened (cell = home cell >> s), which keeps every bucket
+// on its owner, and the entries stay as they are (their fingerprints are the
+// bits above the full bucket): entries of 2^s buckets share a cell, and a
+// fingerprint or offset collision between them is a false candidate that the
+// full-overlap verification rejects.  s is the largest shift that keeps one
+// cell per live read of the rank (the full table's sizing rule).
+int build_live_index_xchg(mg_ctx* ctx) {
+  ctx->live_ready = false;
+  ctx->live_coarse = false;
+  if (!ctx->live_index || !ctx->super_any || !ctx->cell_n) return 0;
+  const double frac = (double)ctx->cell_n / (double)(1ull << ctx->nb_log2);
+  const uint64_t live_reads = ctx->n > ctx->n_contained ? ctx->n - ctx->n_contained : 1;
+  const uint64_t live_local = (uint64_t)((double)live_reads * frac) + 1;
+  uint32_t sft = 0;
+  while (sft < 24 && (ctx->cell_n >> (sft + 1)) >= live_local && (ctx->cell_n >> (sft + 1)) * kCell >= 5 * live_local)
+    ++sft;
+  if (!sft) return 0;  // no smaller than the full table: probe that
+  const uint64_t live_n = (ctx->cell_n + (1ull << sft) - 1) >> sft;
+  MG_TRY(ensure(&ctx->d_lcells, &ctx->lcells_cap, live_n * kCell));
+  if (build_cells(ctx, ctx->d_lcells, live_n, sft, ctx->d_cbits)) return -1;
+  ctx->live_shift = sft;
+  ctx->live_cells = live_n;
+  ctx->live_coarse = true;
   ctx->live_ready = true;
   return 0;
 }
@@ -3457,7 +3632,7 @@ static int sort_xrecs(mg_ctx* ctx, const ulonglong2* recv, uint64_t slot, uint32
     // fused path probes unsorted (the clustered layout's locality); a bucket
     // order only pays for merging the streams of several senders (one RCCL
     // rank at C3: 15.0 -> 13.8 ms per step)
-    if (P == 1) {
+    if (P == 1 || !ctx->xchg_sort_runs) {
       *n_out = n;
       return 0;
     }
@@ -3565,6 +3740,18 @@ int layout_current(mg_ctx* ctx, bool force) {
   ctx->layout_lo = grouped ? lo : 0;
   ctx->layout_hi = grouped ? hi : 0;
   ctx->t.layout_ms = elapsed(ctx->ev[14], ctx->ev[15]);
+  if (!ctx->layout_scratch) {  // (option layout_scratch = 0: many contexts on one device, the simulated ranks)
+    for (void** b : {(void**)&ctx->d_words_alt, (void**)&ctx->d_len_alt, (void**)&ctx->d_lay_k[0], (void**)&ctx->d_lay_k[1],
+                     (void**)&ctx->d_lay_v[0], (void**)&ctx->d_lay_v[1], &ctx->d_lay_tmp,
+                     (void**)&ctx->id_store[1 - sel], (void**)&ctx->phys_store[1 - sel]})
+      if (*b) {
+        MG_TRY(hipFree(*b));
+        *b = nullptr;
+      }
+    ctx->words_alt_cap = ctx->len_alt_cap = ctx->lay_tmp_cap = 0;
+    ctx->lay_k_cap[0] = ctx->lay_k_cap[1] = ctx->lay_v_cap[0] = ctx->lay_v_cap[1] = 0;
+    ctx->id_cap[1 - sel] = ctx->phys_cap[1 - sel] = 0;
+  }
   return 0;
 }
 
@@ -3770,7 +3957,9 @@ int mg_xchg_begin(mg_ctx* ctx, uint32_t min_overlap, uint32_t seed_k) {
   if (long_mode(ctx)) return set_err(ctx, "reads longer than 1024 bp: exchange mode not supported (use the replicated mode)");
   if (ensure_layout_range(ctx)) return -1;
   MG_TRY(hipEventRecord(ctx->ev[0], ctx->stream));
-  if (setup_index(ctx, min_overlap, seed_k)) return -1;  // this rank's (cleared) cells
+  if (setup_index(ctx, min_overlap, seed_k, false)) return -1;
+  // this rank's cells: mg_xchg_insert_keys writes every one of them (no clear)
+  MG_TRY(ensure(&ctx->d_cells, &ctx->cells_cap, ctx->cell_n * kCell));
   ctx->xchg = true;
   ctx->xruns_ready = false;
   ctx->xchg_prefix = ctx->minlen != ctx->maxlen && ctx->prefix_contain;
@@ -3778,8 +3967,8 @@ int mg_xchg_begin(mg_ctx* ctx, uint32_t min_overlap, uint32_t seed_k) {
   source_range(ctx, &lo, &hi);
   ctx->xchg_lo = lo;
   ctx->xchg_hi = hi;
-  MG_TRY(ensure(&ctx->d_kb, &ctx->kb_cap, 4 * ctx->n + 1));
-  MG_TRY(ensure(&ctx->d_ke, &ctx->ke_cap, 4 * ctx->n + 1));
+  MG_TRY(ensure(&ctx->d_kb, &ctx->kb_cap, 4 * (hi - lo) + 1));
+  MG_TRY(ensure(&ctx->d_ke, &ctx->ke_cap, 4 * (hi - lo) + 1));
   ctx->scan_state = 0;
   ctx->shared_scan_ms = 0.f;
   ctx->t = mg_timings{};
@@ -3818,8 +4007,8 @@ int mg_xchg_pack(mg_ctx* ctx, int what, void* dst, uint64_t slot, uint32_t round
     pp.nreg = (pp.flat_n + kFlatRegion - 1) / kFlatRegion;
     pp.key_bk = ctx->d_kb;
     pp.key_ent = ctx->d_ke;
-    pp.key_n = ctx->n;
-    pp.a_lo = ctx->xchg_lo;
+    pp.key_n = nsrc;  // (key o of source a - xchg_lo at o * nsrc + a - xchg_lo)
+    pp.a_lo = 0;
     pp.nsrc = nsrc;
     return route_slots<OWN_KEY>(ctx, pp, dst, self_dst, slot, rounds, cnt);
   }
@@ -3843,25 +4032,52 @@ int mg_xchg_insert_keys(mg_ctx* ctx, const void* recv, uint64_t slot, uint32_t r
   if (!ctx) return -1;
   MG_TRY(hipSetDevice(ctx->device));
   if (!ctx->xchg) return set_err(ctx, "mg_xchg_begin must run first");
-  const uint64_t total = (uint64_t)rounds * ctx->nranks * slot;
+  const uint32_t P = ctx->nranks;
+  const uint64_t total = (uint64_t)rounds * P * slot;
+  uint64_t n = 0;
   if (total) {
     if (!recv || !counts) return set_err(ctx, "mg_xchg_insert_keys: null buffer");
-    IndexParams p = index_params(ctx);
-    if (ctx->xchg_prefix) {  // every read has one o = 0 key: n records at most
-      MG_TRY(ensure(&ctx->d_k0rec, &ctx->k0rec_cap, std::max<uint64_t>(1, ctx->n)));
-      if (!ctx->d_k0n) MG_TRY(hipMalloc(&ctx->d_k0n, sizeof(unsigned long long)));
-      MG_TRY(hipMemsetAsync(ctx->d_k0n, 0, sizeof(unsigned long long), ctx->stream));
-    }
-    const uint32_t grid = (uint32_t)std::min<uint64_t>((total + kBlock - 1) / kBlock, 65536);
-    hipLaunchKernelGGL(k_insert_slots, dim3(grid), dim3(kBlock), 0, ctx->stream, p,
-                       reinterpret_cast<const ulonglong2*>(recv), slot, rounds,
-                       reinterpret_cast<const unsigned long long*>(counts),
-                       ctx->xchg_prefix ? ctx->d_k0rec : nullptr, ctx->xchg_prefix ? ctx->d_k0n : nullptr);
-    MG_TRY(hipGetLastError());
-  } else if (ctx->xchg_prefix) {
-    if (!ctx->d_k0n) MG_TRY(hipMalloc(&ctx->d_k0n, sizeof(unsigned long long)));
-    MG_TRY(hipMemsetAsync(ctx->d_k0n, 0, sizeof(unsigned long long), ctx->stream));
+    std::vector<unsigned long long> c(P, 0);
+    MG_TRY(hipMemcpyAsync(c.data(), counts, P * sizeof(unsigned long long), hipMemcpyDeviceToHost, ctx->stream));
+    MG_TRY(hipStreamSynchronize(ctx->stream));
+    for (uint32_t q = 0; q < P; ++q) n += std::min<uint64_t>(c[q], (uint64_t)rounds * slot);  // cut streams: what arrived
   }
+  if (n > 0x7FFFFFFFull) return set_err(ctx, "exchange: more than 2^31 key records received on one rank");
+  for (int b = 0; b < 2; ++b) {
+    MG_TRY(ensure(&ctx->d_xkk[b], &ctx->xkk_cap[b], std::max<uint64_t>(n, 1)));
+    MG_TRY(ensure(&ctx->d_xke[b], &ctx->xke_cap[b], std::max<uint64_t>(n, 1)));
+  }
+  ctx->xkey_sel = 0;
+  if (n) {
+    const uint32_t grid = (uint32_t)std::min<uint64_t>((total + kBlock - 1) / kBlock, 65536);
+    hipLaunchKernelGGL(k_xkeys_dense, dim3(grid), dim3(kBlock), 0, ctx->stream,
+                       reinterpret_cast<const ulonglong2*>(recv), slot, P, total,
+                       reinterpret_cast<const unsigned long long*>(counts), ctx->cell_lo, ctx->d_xkk[0],
+                       ctx->d_xke[0]);
+    MG_TRY(hipGetLastError());
+    int hb = 0;
+    while (hb < 32 && (1ull << hb) < ctx->cell_n) ++hb;  // bits of a local cell index
+    if (hb > kBinLog2 && n > 1) {  // group the records by bin (the build's unit), not by cell
+      rocprim::double_buffer<uint32_t> keys(ctx->d_xkk[0], ctx->d_xkk[1]);
+      rocprim::double_buffer<uint64_t> vals(ctx->d_xke[0], ctx->d_xke[1]);
+      size_t tb = 0;
+      MG_TRY(rocprim::radix_sort_pairs(nullptr, tb, keys, vals, (unsigned int)n, (unsigned)kBinLog2, (unsigned)hb,
+                                       ctx->stream));
+      if (tb > ctx->xsort_tmp_cap) {
+        if (ctx->d_xsort_tmp) MG_TRY(hipFree(ctx->d_xsort_tmp));
+        ctx->d_xsort_tmp = nullptr;
+        ctx->xsort_tmp_cap = 0;
+        MG_TRY(hipMalloc(&ctx->d_xsort_tmp, tb));
+        ctx->xsort_tmp_cap = tb;
+      }
+      tb = ctx->xsort_tmp_cap;
+      MG_TRY(rocprim::radix_sort_pairs(ctx->d_xsort_tmp, tb, keys, vals, (unsigned int)n, (unsigned)kBinLog2,
+                                       (unsigned)hb, ctx->stream));
+      ctx->xkey_sel = keys.current() == ctx->d_xkk[0] ? 0 : 1;
+    }
+  }
+  ctx->xkeys_n = n;
+  if (build_cells(ctx, ctx->d_cells, ctx->cell_n, 0, nullptr)) return -1;
   MG_TRY(hipEventRecord(ctx->ev[1], ctx->stream));
   ctx->index_ready = true;
   return 0;
@@ -3886,7 +4102,7 @@ int mg_xchg_probe(mg_ctx* ctx, int contain, const void* recv, uint64_t slot, uin
   if (contain) {
     MG_TRY(hipEventRecord(ctx->ev[2], ctx->stream));
     // prefix containments first (what they mark is skipped as a container)
-    if (ctx->xchg_prefix && ctx->n && dispatch_w<LaunchPrefixContainRec>(ctx->maxw, ctx))
+    if (ctx->xchg_prefix && ctx->n && dispatch_w<LaunchPrefixContainKeys>(ctx->maxw, ctx))
       return set_err(ctx, "prefix containment launch failed");
     if (nregions && dispatch_w<LaunchProbeSlots>(ctx->maxw, ctx, true, runs, reg, nregions))
       return set_err(ctx, "probe launch failed");
@@ -3897,6 +4113,7 @@ int mg_xchg_probe(mg_ctx* ctx, int contain, const void* recv, uint64_t slot, uin
   for (int attempt = 0;; ++attempt) {
     if (attempt == 3) return set_err(ctx, "row buffers overflow after resize");
     MG_TRY(hipEventRecord(ctx->ev[4], ctx->stream));
+    if (attempt == 0 && ctx->contained_done && ctx->super_any && build_live_index_xchg(ctx)) return -1;
     if (attempt == 0 && nregions && ctx->contained_done && ctx->super_any) {
       // runs of contained sources contribute nothing (:548): drop them from the
       // ordered regions in place (the containment probe has read them already)

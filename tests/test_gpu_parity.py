@@ -326,6 +326,7 @@ def exchange_rows(ds, l, world, k=0, want_super=True, opts=None):
         e.upload(ds)
         engines.append(e)
     res = sharded_step(engines, LocalExchange(world, torch.device("cuda:0")), l, k, want_super=want_super)
+    exchange_rows.counters = [e.counters() for e in engines]
     parts = []
     for r in range(world):
         rows = res.rows_numpy(r)
@@ -350,13 +351,50 @@ def test_exchange_mode_matches_reference(name, world):
 @pytest.mark.parametrize("prefix", [0, 1])
 def test_exchange_mode_containment_paths(prefix):
     """Exchange-mode markContainedReads (OverlapGraph.cpp:225-340) both ways:
-    prefix = 1 walks the o = 0 key records each rank filed (k_prefix_contain_rec)
+    prefix = 1 walks the o = 0 key records each rank received (k_prefix_contain_keys)
     and the probe drops suffix-key hits; prefix = 0 verifies them in the probe."""
     meta = load_meta("mixed")
     ds = Dataset.from_files([fixture_input("mixed")], meta["l"])
     rows, sup = exchange_rows(ds, meta["l"], 3, opts={"prefix_contain": prefix})
     assert np.array_equal(rows_to_tuples(rows), golden_rows("mixed"))
     assert {str(i): int(s) for i, s in enumerate(sup) if s} == meta["super"]
+
+
+@pytest.mark.parametrize("name,world,opts", [
+    ("mixed", 3, {"nb_log2": 16}), ("dirty", 4, {"nb_log2": 16}), ("branchy", 2, {"nb_log2": 16}),
+    ("mixed", 4, {"nb_log2": 16, "live_index": 0}), ("mixed", 3, {"xchg_sort_runs": 0}),
+    ("tandem", 4, {"xchg_sort_runs": 0}), ("highdup", 8, {"nb_log2": 16, "xchg_sort_runs": 0})])
+def test_exchange_mode_options(name, world, opts):
+    """Exchange-mode variants against the reference: the discovery index of the
+    uncontained reads (build_live_index_xchg: the rank's cells coarsened, live
+    entries only; forced on the small fixtures by a large directory, and its
+    use checked through counters().live_cells), the full table instead
+    (live_index = 0), and the received runs probed in arrival order
+    (xchg_sort_runs = 0)."""
+    meta = load_meta(name)
+    ds = Dataset.from_files([fixture_input(name)], meta["l"])
+    rows, sup = exchange_rows(ds, meta["l"], world, opts=dict(opts, stats=1))
+    assert np.array_equal(rows_to_tuples(rows), golden_rows(name))
+    assert {str(i): int(s) for i, s in enumerate(sup) if s} == meta["super"]
+    live = [c["live_cells"] for c in exchange_rows.counters]
+    if meta["super"] and opts.get("live_index", 1) and opts.get("nb_log2"):
+        assert all(0 < x < (1 << 16) // world + 1 for x in live), live
+    elif not opts.get("live_index", 1) or not meta["super"]:
+        assert not any(live), live
+
+
+def test_exchange_mode_metagenome_vs_oracle():
+    """A 20k-read metagenome (mixed lengths, log-normal abundance: heavy
+    minimizers overflow their home cells, so k_cells_build's overflow list and
+    chains are exercised) through 4 exchange ranks with the live discovery
+    index, against the oracle."""
+    c, L = synth.metagenome_read_set(20000, 100, 250, n_genomes=20, total_len=400000, seed=51)
+    seqs = synth.codes_to_strings(c, L)
+    ds = Dataset.from_strings(seqs, 50)
+    orows, osup, _, _ = OracleDataset.from_strings(seqs, 50).overlaps(50)
+    rows, sup = exchange_rows(ds, 50, 4, opts={"nb_log2": 15})
+    assert np.array_equal(sup.astype(np.uint64), osup)
+    assert np.array_equal(rows_to_tuples(rows), sorted_tuples(orows))
 
 
 @pytest.mark.parametrize("case", RANDOM_CASES[:4])

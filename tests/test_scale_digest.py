@@ -177,13 +177,16 @@ def combine(ds):
 
 @pytest.mark.gpu
 @pytest.mark.timeout(900)
-@pytest.mark.parametrize("name,world", [("c3", 8), ("c5s", 8)])
+@pytest.mark.parametrize("name,world", [("c3", 8), ("c5s", 8), ("c5", 8)])
 def test_exchange_scale_digest(name, world):
     """The multi-GPU exchange mode (bucket-range index shards,
     key / run / row all-to-alls, MAX all-reduce of the containment keys) with
     `world` simulated ranks on this GPU (LocalExchange moves the slot buffers):
-    C4's data path on the C3 workload, and containment through the exchange on
-    the C5-shaped set; the union of the ranks' rows has the reference's digest."""
+    C4's data path on the C3 workload, containment through the exchange on the
+    C5-shaped set, and BASELINE configs[4] itself (50M mixed reads, 8 ranks:
+    the 8 contexts share the one 288 GB device, so each frees its layout's
+    double buffers); the union of the ranks' rows has the reference's digest
+    (c5: the pinned oracle's, tests/golden/c5s_oracle_check.json)."""
     import torch
 
     from metagenomics_amd.overlap import OverlapEngine
@@ -196,9 +199,11 @@ def test_exchange_scale_digest(name, world):
     try:
         for r in range(world):
             e = OverlapEngine(0)
+            e.set_option("layout_scratch", 0)
             e.set_shard(r, world, 0, 0)
             e.upload(ds)
             engines.append(e)
+        del ds  # (the host Dataset: 50M reads at c5)
         res = sharded_step(engines, LocalExchange(world, torch.device("cuda:0")), m["workload"]["min_overlap"], 31)
         rd = combine([e.slots_digest(b.data_ptr(), slot, rounds, c.data_ptr())
                       for e, (b, c, slot, rounds) in zip(engines, res.rows)])
@@ -207,7 +212,7 @@ def test_exchange_scale_digest(name, world):
         # each rank holds the rows of the sources it owns (by reference ID)
         for r in range(world):
             assert res.n_rows[r] > 0
-            lo, hi = source_range(ds.num_unique, r, world)
+            lo, hi = source_range(m["n_unique"], r, world)
             assert lo < hi
     finally:
         for e in engines:

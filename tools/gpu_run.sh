@@ -38,6 +38,12 @@ for s in $STEPS; do
     export MASTER_ADDR=127.0.0.1 MASTER_PORT=29513 RANK=0 WORLD_SIZE=1 LOCAL_RANK=0
     timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/profxchg1 -o kt -- python3 bench.py --exchange --steps 5 --no-cpu-baseline --no-ingest > $OUT/profxchg1_bench.json 2> $OUT/profxchg1_bench.err
     rc=$?; unset MASTER_ADDR MASTER_PORT RANK WORLD_SIZE LOCAL_RANK; echo "profxchg1 rc=$rc"; cat $OUT/profxchg1_bench.json; head -24 $OUT/profxchg1/kt_kernel_stats.csv | cut -c1-160 ;;
+  newtests)
+    timeout -k 10 900 python -u -m pytest tests/test_gpu_parity.py tests/test_long_reads.py -x -v -m gpu -k "exchange or live_index or falls_back" --timeout 300 --timeout-method thread > $OUT/new_tests.log 2>&1
+    rc=$?; echo "new tests rc=$rc"; grep -E "PASS|FAIL|Error" $OUT/new_tests.log | tail -40 ;;
+  xdigest)
+    timeout -k 10 1100 python -u -m pytest tests/test_scale_digest.py -x -v -m gpu -k "exchange_scale" --timeout 1000 --timeout-method thread > $OUT/xdigest_tests.log 2>&1
+    rc=$?; echo "exchange digest tests rc=$rc"; grep -E "PASS|FAIL|SKIP|Error" $OUT/xdigest_tests.log | tail -12 ;;
   xchgtests)
     timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -x -v -m gpu -k exchange --timeout 300 --timeout-method thread > $OUT/xchg_tests.log 2>&1
     rc=$?; echo "exchange tests rc=$rc"; grep -E "PASS|FAIL|Error" $OUT/xchg_tests.log | tail -20 ;;
@@ -57,7 +63,7 @@ for s in $STEPS; do
     # per-rank kernel tables of the exchange mode at P=8 (simulated ranks, one rank's call at a
     # time: MG_SIM_SERIAL), C3 then C5
     for C in c3 c5; do
-      MG_SIM_SERIAL=1 timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/profsim8_$C -o kt -- python3 bench.py --config $C --sim-world 8 --multi exchange --steps 2 --no-cpu-baseline --no-ingest > $OUT/profsim8_${C}_bench.json 2> $OUT/profsim8_${C}_bench.err
+      MG_SIM_SERIAL=1 timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/profsim8_$C -o kt -- python3 bench.py --config $C --sim-world 8 --multi exchange --steps 2 --no-cpu-baseline --no-ingest --opt layout_scratch=0 $SIMOPTS > $OUT/profsim8_${C}_bench.json 2> $OUT/profsim8_${C}_bench.err
       rc=$?; echo "profsim8 $C rc=$rc"; [ $rc -ne 0 ] && break
       python3 tools/rank_table.py $OUT/profsim8_$C/kt_kernel_stats.csv 8 4 "$C exchange-sim" | tee $OUT/profsim8_${C}_ranks.md | tail -14
     done ;;
