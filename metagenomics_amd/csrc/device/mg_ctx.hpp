@@ -65,6 +65,15 @@ struct mg_ctx {
   bool index_ready = false;
   uint64_t* d_cells = nullptr;  // cells of kCell entries (this rank's bucket range)
   size_t cells_cap = 0;
+  // the index holds the o = 1 keys (suffix keys of the forward strand) only
+  // when a probe reads them: discovery never does (an o = 1 hit is the twin of
+  // the partner's o = 0 hit) and containment only without the
+  // prefix-containment kernel; getListOfReads then takes a lookup table of all
+  // four keys, built on the first lookup after a build (d_lkcells)
+  bool index_o1 = true;
+  uint64_t* d_lkcells = nullptr;
+  size_t lkcells_cap = 0;
+  bool lookup_ready = false;
   uint64_t cell_lo = 0, cell_n = 0;  // local bucket range [cell_lo, cell_lo + cell_n)
   // containment
   unsigned long long* d_superkey = nullptr;
@@ -249,6 +258,7 @@ int apply_layout(mg_ctx* ctx);
 inline void reset_derived(mg_ctx* ctx) {
   ctx->scan_state = 0;
   ctx->index_ready = false;
+  ctx->lookup_ready = false;
   ctx->contained_done = false;
   ctx->super_any = false;
   ctx->live_ready = false;

@@ -172,6 +172,7 @@ struct IndexParams {
   const uint32_t* id;  // slot -> reference ID - 1 (nullptr: ID order; lookups return IDs)
   uint32_t stride;     // words per slot (the long-read kernels; the templated ones use slot_words(MAXW))
   const uint32_t* cbits;  // k_index_live: the contained slots (bitmap, k_super_finalize)
+  int skip_o1;         // leave out the o = 1 keys (index_o1: nothing on this path reads them)
 };
 
 __device__ __forceinline__ bool owned(uint64_t bkt, uint32_t nb_log2, uint32_t rank, uint32_t nranks) {
@@ -275,6 +276,7 @@ __global__ __launch_bounds__(kBlock) void k_index_build(IndexParams p) {
        gid += (uint64_t)gridDim.x * kBlock) {
     const uint64_t r = gid >> 2;
     const int o = (int)(gid & 3);
+    if (o == 1 && p.skip_o1) continue;
     const uint64_t* g = p.words + r * slot_words(MAXW);
 #pragma unroll
     for (int k = 0; k < MAXW; ++k) f[k * kBlock] = g[k];
@@ -289,10 +291,12 @@ __global__ __launch_bounds__(kBlock) void k_index_build(IndexParams p) {
 }
 
 // The discovery index of the uncontained reads (build_live_index): the same
-// entries as k_index_build for the live slots only.  A wavefront takes 64
-// consecutive slots, reads their contained bits (p.cbits, two words) and
-// deals the 4 keys of each live slot to consecutive lanes, so no lane is
-// spent on a contained read (C5: three quarters of them).
+// entries as k_index_build for the live slots only, and only the keys the
+// discovery lists (o = 0, 2, 3: an o = 1 hit is the twin of the partner's
+// o = 0 hit).  A wavefront takes 64 consecutive slots, reads
+// their contained bits (p.cbits, two words) and deals the 3 keys of each live
+// slot to consecutive lanes, so no lane is spent on a contained read (C5:
+// three quarters of them).
 __device__ __forceinline__ uint32_t nth_set_bit(uint64_t x, uint32_t k) {  // position of set bit k (0-based)
   uint32_t pos = 0;
 #pragma unroll
@@ -318,12 +322,13 @@ __global__ __launch_bounds__(kBlock) void k_index_live(IndexParams p) {
     const uint64_t r0 = g * kWave;
     uint64_t live = ~((uint64_t)p.cbits[2 * g] | ((uint64_t)p.cbits[2 * g + 1] << 32));
     if (p.n - r0 < (uint64_t)kWave) live &= (1ull << (p.n - r0)) - 1;
-    const uint32_t nk = 4u * (uint32_t)__popcll(live);
+    const uint32_t nk = 3u * (uint32_t)__popcll(live);
     for (uint32_t k0 = 0; k0 < nk; k0 += kWave) {
       const uint32_t k = k0 + (uint32_t)lane;
       if (k >= nk) continue;
-      const uint64_t r = r0 + nth_set_bit(live, k >> 2);
-      const int o = (int)(k & 3u);
+      const uint32_t kq = k / 3u, km = k - 3u * kq;
+      const uint64_t r = r0 + nth_set_bit(live, kq);
+      const int o = km ? (int)km + 1 : 0;  // 0, 2, 3
       const uint64_t* gw = p.words + r * slot_words(MAXW);
 #pragma unroll
       for (int kk = 0; kk < MAXW; ++kk) f[kk * kBlock] = gw[kk];
@@ -600,6 +605,7 @@ struct ScanParams {
   // per read: its o = 0 key's hash bits (bucket | fingerprint, 50 bits) | q << 54
   // (k_prefix_contain); nullptr: not written
   uint64_t* key0;
+  int skip_o1;                    // INDEX: leave out the o = 1 keys (mg_ctx::index_o1)
 };
 
 __device__ __forceinline__ void wave_sync() {
@@ -982,7 +988,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(G > 1 ? 
         if (o == 0 && p.key0) p.key0[a] = (v & ((1ULL << 50) - 1)) | ((uint64_t)(kb[0] & 1023u) << 54);
         if constexpr (KEYREC) {  // o-major: each store is one coalesced wavefront line
           p.key_bk[o * p.key_n + a - p.key_lo] = (uint32_t)(v & nbm);
-          p.key_ent[o * p.key_n + a - p.key_lo] = e;
+          p.key_ent[o * p.key_n + a - p.key_lo] = (o == 1 && p.skip_o1) ? kEmpty : e;  // (a hole: not routed)
         }
         cb[o] = v & nbm;
         ce[o] = e;
@@ -991,7 +997,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(G > 1 ? 
       // measured slower: scan 3.06-3.13 vs 2.92-2.94 ms at C3, profiles/r03y_ab_scan.txt)
       if constexpr (!KEYREC) {
 #pragma unroll
-        for (int o = 0; o < 4; ++o) cell_insert(p.cells, cb[o], p.cell_n, ce[o]);
+        for (int o = 0; o < 4; ++o)
+          if (o != 1 || !p.skip_o1) cell_insert(p.cells, cb[o], p.cell_n, ce[o]);
       }
     } else if (INDEX && a < p.a_hi) {  // no keys (n <= l cannot pass setup_index): holes
       if (p.key0) p.key0[a] = kEmpty;
@@ -1202,7 +1209,7 @@ __global__ __launch_bounds__(kBlock) void k_scan_reg(ScanParams p) {
           b0 = (uint32_t)(v0 & nbm);
           b1 = (uint32_t)(v1 & nbm);
           c0 = make_entry(v0, p.nb_log2, p0, 0, (uint32_t)a);
-          c1 = make_entry(v1, p.nb_log2, p1 - (n - h), 1, (uint32_t)a);
+          c1 = p.skip_o1 ? kEmpty : make_entry(v1, p.nb_log2, p1 - (n - h), 1, (uint32_t)a);
         }
         const uint64_t ka = a - p.key_lo;
         p.key_bk[ka] = b0;
@@ -2559,8 +2566,10 @@ struct LaunchIndexLive {
 
 template <int W>
 struct LaunchIndex {
-  static int run(mg_ctx* ctx) {
+  static int run(mg_ctx* ctx, uint64_t* cells = nullptr, bool all_keys = false) {
     IndexParams p = index_params(ctx);
+    if (cells) p.cells = cells;
+    p.skip_o1 = (!all_keys && !ctx->index_o1) ? 1 : 0;
     uint32_t grid = (uint32_t)((4 * ctx->n + kBlock - 1) / kBlock);  // one thread per key
     const size_t lds = (size_t)(W + 1) * kBlock * sizeof(uint64_t);
     if (grid == 0) return 0;
@@ -2706,6 +2715,7 @@ struct LaunchScan {
     sp.cells = ctx->d_cells;
     sp.cell_n = ctx->cell_n;
     if (index && ctx->key0_ready) sp.key0 = ctx->d_key0;  // mg_build_index allocated it (mixed lengths)
+    sp.skip_o1 = (index && !ctx->index_o1) ? 1 : 0;
     if (index && ctx->xchg) {  // key records (bucket, entry), o-major: they travel to the bucket owner
       sp.key_bk = ctx->d_kb;
       sp.key_ent = ctx->d_ke;
@@ -2826,11 +2836,18 @@ struct LaunchDiscover {
   }
 };
 
+// getListOfReads reads all four keys: the lookup table when the index left out o = 1
+IndexParams lookup_params(mg_ctx* ctx) {
+  IndexParams p = index_params(ctx);
+  if (!ctx->index_o1 && !long_mode(ctx)) p.cells = ctx->d_lkcells;
+  return p;
+}
+
 template <int W>
 struct LaunchLookup {
   static int run(mg_ctx* ctx, const uint64_t* dq, int qwords, unsigned long long* dout, uint32_t cap,
                  unsigned int* dn) {
-    IndexParams p = index_params(ctx);
+    IndexParams p = lookup_params(ctx);
     hipLaunchKernelGGL((k_lookup_key<W>), dim3(1), dim3(kBlock), 0, ctx->stream, p, dq, qwords, dout, cap, dn);
     return hipGetLastError() == hipSuccess ? 0 : -1;
   }
@@ -2848,7 +2865,7 @@ int launch_index(mg_ctx* ctx) {
 int launch_lookup(mg_ctx* ctx, const uint64_t* dq, int qwords, unsigned long long* dout, uint32_t cap,
                   unsigned int* dn) {
   if (!long_mode(ctx)) return dispatch_w<LaunchLookup>(ctx->maxw, ctx, dq, qwords, dout, cap, dn);
-  hipLaunchKernelGGL((k_lookup_key<0>), dim3(1), dim3(kBlock), 0, ctx->stream, index_params(ctx), dq, qwords, dout,
+  hipLaunchKernelGGL((k_lookup_key<0>), dim3(1), dim3(kBlock), 0, ctx->stream, lookup_params(ctx), dq, qwords, dout,
                      cap, dn);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
@@ -2995,7 +3012,7 @@ void mg_destroy(mg_ctx* ctx) {
                   ctx->d_xk[0], ctx->d_xk[1], ctx->d_xv[0], ctx->d_xv[1], ctx->d_xsort_tmp,
                   ctx->d_digest, ctx->id_store[0], ctx->id_store[1], ctx->phys_store[0], ctx->phys_store[1],
                   ctx->d_tmp32, ctx->d_lay_k[0], ctx->d_lay_k[1], ctx->d_lay_v[0], ctx->d_lay_v[1], ctx->d_lay_tmp,
-                  ctx->d_words_alt, ctx->d_len_alt, ctx->d_cbits, ctx->d_ccnt, ctx->d_lcells};
+                  ctx->d_words_alt, ctx->d_len_alt, ctx->d_cbits, ctx->d_ccnt, ctx->d_lcells, ctx->d_lkcells};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   for (auto& e : ctx->ev)
@@ -3233,6 +3250,7 @@ int setup_index(mg_ctx* ctx, uint32_t min_overlap, uint32_t seed_k, bool cells =
   ctx->cell_n = ((r + 1) * NB + P - 1) / P - ctx->cell_lo;
   if (cells && setup_cells(ctx)) return -1;
   ctx->index_ready = false;
+  ctx->lookup_ready = false;
   ctx->contained_done = false;
   ctx->super_any = false;
   ctx->live_ready = false;
@@ -3790,7 +3808,9 @@ int mg_build_index(mg_ctx* ctx, uint32_t min_overlap, uint32_t seed_k) {
   ctx->scan_state = 0;
   ctx->t.sort_ms = 0.f;
   ctx->shared_scan_ms = 0.f;
+  const bool mixed = ctx->minlen != ctx->maxlen;
   if (long_mode(ctx)) {  // reads > 1024 bp: k_index_long, one thread per key
+    ctx->index_o1 = true;
     if (ctx->nranks > 1) return set_err(ctx, "reads longer than 1024 bp: bucket-sharded index not supported");
     if (launch_index(ctx)) return set_err(ctx, "index build launch failed");
   } else if (shared_scan(ctx)) {
@@ -3799,14 +3819,17 @@ int mg_build_index(mg_ctx* ctx, uint32_t min_overlap, uint32_t seed_k) {
     // probes.  Measured at C3 (same box): 3.58 ms vs index 2.05 + scan 1.83
     // separately; a concurrent scan on a second stream did not overlap (3.95).
     // mixed lengths: each read's o = 0 key for the prefix-containment kernel
-    ctx->key0_ready = ctx->minlen != ctx->maxlen && ctx->prefix_contain;
+    ctx->key0_ready = mixed && ctx->prefix_contain;
+    // o = 1 keys: only the containment probe without k_prefix_contain reads them
+    ctx->index_o1 = mixed && !ctx->key0_ready;
     if (ctx->key0_ready) MG_TRY(ensure(&ctx->d_key0, &ctx->key0_cap, ctx->n + 1));
     if (ctx->n && dispatch_w<LaunchScanAll>(ctx->maxw, ctx, ctx->stream))
       return set_err(ctx, "index build launch failed");
     if (!ctx->n) ctx->nrun_reg = 0;
     ctx->scan_state = 1;
-  } else if (dispatch_w<LaunchIndex>(ctx->maxw, ctx)) {  // the whole index for a source-range shard
-    return set_err(ctx, "index build launch failed");
+  } else {  // the whole index for a source-range shard (its containment probe reads suffix-key hits)
+    ctx->index_o1 = mixed;
+    if (dispatch_w<LaunchIndex>(ctx->maxw, ctx)) return set_err(ctx, "index build launch failed");
   }
   MG_TRY(hipEventRecord(ctx->ev[1], ctx->stream));
   MG_TRY(hipEventSynchronize(ctx->ev[1]));
@@ -3963,6 +3986,7 @@ int mg_xchg_begin(mg_ctx* ctx, uint32_t min_overlap, uint32_t seed_k) {
   ctx->xchg = true;
   ctx->xruns_ready = false;
   ctx->xchg_prefix = ctx->minlen != ctx->maxlen && ctx->prefix_contain;
+  ctx->index_o1 = ctx->minlen != ctx->maxlen && !ctx->xchg_prefix;  // (key records of o = 1: holes otherwise)
   uint64_t lo, hi;
   source_range(ctx, &lo, &hi);
   ctx->xchg_lo = lo;
@@ -4243,6 +4267,14 @@ int mg_lookup_key(mg_ctx* ctx, const char* key, uint32_t key_len, uint64_t* out,
   if (n_out) *n_out = 0;
   if (key_len != ctx->h) return 0;  // no key of another length exists
   if (ctx->nranks > 1) return set_err(ctx, "lookup on a bucket-sharded index");
+  if (!ctx->index_o1 && !long_mode(ctx) && !ctx->lookup_ready) {
+    // the step's index has no o = 1 keys: file all four once into the lookup table
+    MG_TRY(ensure(&ctx->d_lkcells, &ctx->lkcells_cap, ctx->cell_n * kCell));
+    MG_TRY(hipMemsetAsync(ctx->d_lkcells, 0xFF, ctx->cell_n * kCell * sizeof(uint64_t), ctx->stream));
+    if (ctx->n && dispatch_w<LaunchIndex>(ctx->maxw, ctx, ctx->d_lkcells, true))
+      return set_err(ctx, "lookup table build failed");
+    ctx->lookup_ready = true;
+  }
   const int qwords = (int)((key_len + 31) / 32);
   std::vector<uint64_t> q(qwords + 1, 0);
   for (uint32_t i = 0; i < key_len; i++) {
