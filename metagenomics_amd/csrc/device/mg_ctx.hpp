@@ -166,8 +166,8 @@ struct mg_ctx {
   int xv_sel = 0;
   uint64_t xruns_n = 0;
   bool xruns_ready = false;
-  // exchange mode: the key records this rank received, dense and grouped by
-  // bin of home cells (mg_xchg_insert_keys: key = local home cell, ent = index
+  // exchange mode: the key records this rank received, dense and sorted by
+  // home cell (mg_xchg_insert_keys: key = local home cell, ent = index
   // entry); they build the cells, the o = 0 ones drive the prefix containments
   // (k_prefix_contain_keys, xchg_prefix) and the live ones the discovery index
   uint32_t* d_xkk[2] = {nullptr, nullptr};
@@ -175,11 +175,10 @@ struct mg_ctx {
   size_t xkk_cap[2] = {0, 0}, xke_cap[2] = {0, 0};
   int xkey_sel = 0;
   uint64_t xkeys_n = 0;
-  // overflow list of k_cells_build (a cell's entries past its 8 slots)
-  uint32_t* d_ovf_c = nullptr;
-  uint64_t* d_ovf_e = nullptr;
-  size_t ovf_c_cap = 0, ovf_e_cap = 0;
-  unsigned long long* d_novf = nullptr;
+  // the live records' in-order compaction (build_live_index_xchg)
+  uint8_t* d_xflag = nullptr;
+  size_t xflag_cap = 0;
+  unsigned long long* d_nlive = nullptr;
   // the exchange mode's discovery index coarsens the rank's cells (cell =
   // local home cell >> live_shift) instead of rebuilding entries
   bool live_coarse = false;

@@ -454,24 +454,24 @@ struct LaunchPrefixContain {
   }
 };
 
-// ---- exchange mode: the received key records filed without global atomics
+// ---- exchange mode: the received key records filed without CAS inserts
 // (HashTable::insertDataset / insertIntoTable, HashTable.cpp:50-80,163-195).
-// mg_xchg_insert_keys makes the records dense (k_xkeys_dense: local home cell +
-// entry) and groups them by BIN (kBinCells consecutive cells, one radix sort
-// over the bin bits); k_cells_build then builds each bin's cells in LDS: LDS
-// atomics deal the slots, a cell with more entries than slots gets the chain
-// flag, and the bin leaves as whole 64-B lines (every cell of the table is
-// written, so the table needs no clear).  A cell's 9th and later entries go to
-// an overflow list that k_cells_overflow files with cell_insert after the build
-// (the chain starts at the flagged home cell, so insertion and every walk
-// follow the same sequence).  CAS inserts of received keys (k_insert_slots)
-// cost ~7 G keys/s of memory-side atomics on the step's critical path; the
-// fused path hides the same CASes behind its scan.  The same build over the
-// same records, filtered to the uncontained reads and with cells coarsened by
-// `shift`, is the exchange mode's discovery index (build_live_index_xchg).
-constexpr int kBinLog2 = 9;
-constexpr uint32_t kBinCells = 1u << kBinLog2;  // 512 cells = 32 KiB of LDS per bin
-
+// mg_xchg_insert_keys makes the records dense (k_xkeys_dense: local home cell
+// + entry) and radix-sorts them by home cell, so a cell's entries are
+// consecutive.  k_cells_fill then files every record with one plain store: its
+// slot is its rank among the equal keys before it (a look back over at most 8
+// neighbours, cache hits), and the 8th entry of a cell that has more carries
+// the chain flag.  A cell's 9th and later entries (heavy minimizers: a
+// metagenome's abundant genomes put dozens of keys under one minimizer, 26 %
+// of the records at C5) are placed by k_cells_chain once the homes are filled:
+// the record of rank 8 walks the chain for its whole group, resuming each
+// entry where the previous one with the same fingerprint went, so a group of g
+// entries costs ~g/8 cell visits instead of the ~g^2/16 of one walk per entry.
+// CAS inserts of received keys (k_insert_slots) ran at ~7 G keys/s of
+// memory-side atomics on the step's critical path; the fused path hides the
+// same CASes behind its scan.  The same two kernels over the uncontained
+// reads' records (compacted in order) with cells coarsened by `shift` build
+// the exchange mode's discovery index (build_live_index_xchg).
 __global__ __launch_bounds__(kBlock) void k_xkeys_dense(const ulonglong2* __restrict__ recv, uint64_t slot,
                                                        uint32_t nranks, uint64_t total,
                                                        const unsigned long long* __restrict__ counts,
@@ -489,92 +489,79 @@ __global__ __launch_bounds__(kBlock) void k_xkeys_dense(const ulonglong2* __rest
   }
 }
 
-struct CellBuild {
-  const uint32_t* key;        // home cell (full table) of each record, grouped by key >> kBinLog2
-  const uint64_t* ent;
-  uint64_t n;
-  uint32_t shift;             // cell of the table built = key >> shift
-  uint64_t cell_n;            // cells of the table built
-  uint64_t* cells;
-  const uint32_t* cbits;      // non-null: only entries of uncontained reads (discovery index)
-  uint32_t* ovf_cell;         // overflow list (capacity n)
-  uint64_t* ovf_ent;
-  unsigned long long* novf;
-};
-
-// first record whose bin (key >> sh) is >= bin
-__device__ __forceinline__ uint64_t bin_lower_bound(const uint32_t* __restrict__ key, uint64_t n, uint32_t sh,
-                                                    uint64_t bin) {
-  uint64_t lo = 0, hi = n;
-  while (lo < hi) {
-    const uint64_t mid = (lo + hi) >> 1;
-    if ((uint64_t)(key[mid] >> sh) < bin) lo = mid + 1;
-    else hi = mid;
-  }
-  return lo;
+// number of records equal to key c (>> shift) directly before record i, capped at kCell
+__device__ __forceinline__ int rank_in_cell(const uint32_t* __restrict__ key, uint64_t i, uint32_t shift, uint32_t c) {
+  bool eq[kCell + 1];
+#pragma unroll
+  for (int k = 1; k <= kCell; ++k) eq[k] = i >= (uint64_t)k && (key[i - k] >> shift) == c;
+  int r = 0;
+#pragma unroll
+  for (int k = 1; k <= kCell; ++k) r = (r == k - 1 && eq[k]) ? k : r;
+  return r;
 }
 
-__global__ __launch_bounds__(kBlock) void k_cells_build(CellBuild p) {
-  __shared__ __attribute__((aligned(16))) unsigned long long s_cell[kBinCells * kCell];
-  __shared__ uint32_t s_cnt[kBinCells];
-  __shared__ uint64_t s_rng[2];
-  const int lane = threadIdx.x & 63;
-  const uint32_t sh = kBinLog2 + p.shift;
-  const uint64_t nbins = (p.cell_n + kBinCells - 1) >> kBinLog2;
-  for (uint64_t bin = blockIdx.x; bin < nbins; bin += gridDim.x) {
-    for (uint32_t i = threadIdx.x; i < kBinCells * kCell; i += kBlock) s_cell[i] = kEmpty;
-    for (uint32_t i = threadIdx.x; i < kBinCells; i += kBlock) s_cnt[i] = 0;
-    if (threadIdx.x < 2) s_rng[threadIdx.x] = bin_lower_bound(p.key, p.n, sh, bin + threadIdx.x);
-    __syncthreads();
-    const uint64_t lo = s_rng[0], hi = s_rng[1];
-    for (uint64_t i0 = lo; i0 < hi; i0 += kBlock) {  // (uniform trip count: the ballot below)
-      const uint64_t i = i0 + threadIdx.x;
-      bool ov = false;
-      uint32_t c = 0;
-      uint64_t e = 0;
-      if (i < hi) {
-        e = p.ent[i];
-        c = p.key[i] >> p.shift;
-        const uint32_t r = (uint32_t)e;
-        if (!p.cbits || !((p.cbits[r >> 5] >> (r & 31u)) & 1u)) {
-          const uint32_t lc = c & (kBinCells - 1);
-          const uint32_t k = atomicAdd(&s_cnt[lc], 1u);
-          if (k < (uint32_t)kCell) s_cell[lc * kCell + k] = e;
-          else ov = true;
+// n_dev non-null: the record count is on the device (a compaction's output)
+__global__ __launch_bounds__(kBlock) void k_cells_fill(const uint32_t* __restrict__ key,
+                                                      const uint64_t* __restrict__ ent,
+                                                      const unsigned long long* __restrict__ n_dev, uint64_t n_host,
+                                                      uint32_t shift, uint64_t* __restrict__ cells) {
+  const uint64_t n = n_dev ? *n_dev : n_host;
+  for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBlock) {
+    const uint32_t c = key[i] >> shift;
+    const int r = rank_in_cell(key, i, shift, c);
+    if (r < kCell) {
+      const bool more = r == kCell - 1 && i + 1 < n && (key[i + 1] >> shift) == c;
+      cells[(uint64_t)c * kCell + r] = more ? (ent[i] | kChain) : ent[i];
+    }
+  }
+}
+
+// the 9th+ entries of each cell, one thread per group (the group's record of rank 8)
+__global__ __launch_bounds__(kBlock) void k_cells_chain(const uint32_t* __restrict__ key,
+                                                       const uint64_t* __restrict__ ent,
+                                                       const unsigned long long* __restrict__ n_dev, uint64_t n_host,
+                                                       uint32_t shift, uint64_t* cells, uint64_t cell_n) {
+  const uint64_t n = n_dev ? *n_dev : n_host;
+  for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBlock) {
+    const uint32_t c = key[i] >> shift;
+    if (rank_in_cell(key, i, shift, c) != kCell || (i >= kCell + 1 && (key[i - kCell - 1] >> shift) == c)) continue;
+    uint32_t last_fp = ~0u;
+    uint64_t at = c;
+    for (uint64_t j = i; j < n && (key[j] >> shift) == c; ++j) {
+      const unsigned long long e = ent[j];
+      const uint32_t fp = entry_fp(e);
+      if (fp != last_fp) at = next_cell(c, cell_n, fp);  // the home is full: its chain starts at the next cell
+      last_fp = fp;
+      // cell_insert from `at`, leaving `at` at the cell that took the entry
+      for (uint64_t probe = 0; probe < cell_n; ++probe) {
+        unsigned long long* cell = reinterpret_cast<unsigned long long*>(cells + at * kCell);
+        uint64_t ev[kCell];
+        const ulonglong2* cp = reinterpret_cast<const ulonglong2*>(cell);
+#pragma unroll
+        for (int s2 = 0; s2 < kCell / 2; ++s2) {
+          const ulonglong2 x = cp[s2];
+          ev[2 * s2] = x.x;
+          ev[2 * s2 + 1] = x.y;
         }
-      }
-      const uint64_t bal = __ballot(ov);
-      if (bal) {  // wavefront-aggregated append to the overflow list
-        unsigned long long base = 0;
-        if (lane == 0) base = atomicAdd(p.novf, (unsigned long long)__popcll(bal));
-        base = __shfl(base, 0);
-        if (ov) {
-          const uint64_t at = base + lane_prefix(bal);
-          p.ovf_cell[at] = c;
-          p.ovf_ent[at] = e;
-        }
+        bool done = false;
+#pragma unroll
+        for (int s2 = 0; s2 < kCell; ++s2)
+          if (!done && ev[s2] == kEmpty) done = atomicCAS(&cell[s2], kEmpty, e) == kEmpty;
+        if (done) break;
+        if (ev[kCell - 1] == kEmpty || !(ev[kCell - 1] & kChain)) atomicOr(&cell[kCell - 1], (unsigned long long)kChain);
+        at = next_cell(at, cell_n, fp);
       }
     }
-    __syncthreads();
-    const uint64_t c0 = bin << kBinLog2;
-    const uint32_t nc = (uint32_t)(p.cell_n - c0 < kBinCells ? p.cell_n - c0 : kBinCells);
-    for (uint32_t c = threadIdx.x; c < nc; c += kBlock)
-      if (s_cnt[c] > (uint32_t)kCell) s_cell[c * kCell + kCell - 1] |= kChain;
-    __syncthreads();
-    ulonglong2* dst = reinterpret_cast<ulonglong2*>(p.cells + c0 * kCell);
-    const ulonglong2* src = reinterpret_cast<const ulonglong2*>(s_cell);
-    for (uint32_t i = threadIdx.x; i < nc * (kCell / 2); i += kBlock) dst[i] = src[i];
-    __syncthreads();
   }
 }
 
-__global__ __launch_bounds__(kBlock) void k_cells_overflow(uint64_t* cells, uint64_t cell_n,
-                                                          const uint32_t* __restrict__ ovf_cell,
-                                                          const uint64_t* __restrict__ ovf_ent,
-                                                          const unsigned long long* __restrict__ novf) {
-  const uint64_t n = *novf;
-  for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBlock)
-    cell_insert(cells, ovf_cell[i], cell_n, ovf_ent[i]);
+// the uncontained reads' records (cbits clear), flagged for the in-order compaction
+__global__ __launch_bounds__(kBlock) void k_live_flags(const uint64_t* __restrict__ ent, uint64_t n,
+                                                      const uint32_t* __restrict__ cbits, uint8_t* __restrict__ flag) {
+  const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t r = (uint32_t)ent[i];
+  flag[i] = ((cbits[r >> 5] >> (r & 31u)) & 1u) ? 0 : 1;
 }
 
 // ------------------------------------------------------------- discovery ---
@@ -3008,7 +2995,7 @@ void mg_destroy(mg_ctx* ctx) {
   void* bufs[] = {ctx->d_words, ctx->d_len, ctx->d_cells, ctx->d_superkey, ctx->d_super, ctx->d_any, ctx->d_rows,
                   ctx->d_seg, ctx->d_stats, ctx->d_compact, ctx->d_runs, ctx->d_run_cnt, ctx->d_blk, ctx->d_flat_cnt,
                   ctx->d_slot_cnt, ctx->d_freq, ctx->d_kb, ctx->d_ke, ctx->d_key0, ctx->d_xkk[0], ctx->d_xkk[1], ctx->d_xke[0], ctx->d_xke[1],
-                  ctx->d_ovf_c, ctx->d_ovf_e, ctx->d_novf,
+                  ctx->d_xflag, ctx->d_nlive,
                   ctx->d_xk[0], ctx->d_xk[1], ctx->d_xv[0], ctx->d_xv[1], ctx->d_xsort_tmp,
                   ctx->d_digest, ctx->id_store[0], ctx->id_store[1], ctx->phys_store[0], ctx->phys_store[1],
                   ctx->d_tmp32, ctx->d_lay_k[0], ctx->d_lay_k[1], ctx->d_lay_v[0], ctx->d_lay_v[1], ctx->d_lay_tmp,
@@ -3508,56 +3495,21 @@ int build_live_index(mg_ctx* ctx) {
   return 0;
 }
 
-// the cell table `cells` of cell_n cells from the rank's dense received key
-// records (k_cells_build + k_cells_overflow): cell = home cell >> shift; cbits
-// non-null = only the uncontained reads' entries
-int build_cells(mg_ctx* ctx, uint64_t* cells, uint64_t cell_n, uint32_t shift, const uint32_t* cbits) {
-  const uint64_t n = ctx->xkeys_n;
-  MG_TRY(ensure(&ctx->d_ovf_c, &ctx->ovf_c_cap, std::max<uint64_t>(n, 1)));
-  MG_TRY(ensure(&ctx->d_ovf_e, &ctx->ovf_e_cap, std::max<uint64_t>(n, 1)));
-  if (!ctx->d_novf) MG_TRY(hipMalloc(&ctx->d_novf, sizeof(unsigned long long)));
-  MG_TRY(hipMemsetAsync(ctx->d_novf, 0, sizeof(unsigned long long), ctx->stream));
-  CellBuild b{};
-  b.key = ctx->d_xkk[ctx->xkey_sel];
-  b.ent = ctx->d_xke[ctx->xkey_sel];
-  b.n = n;
-  b.shift = shift;
-  b.cell_n = cell_n;
-  b.cells = cells;
-  b.cbits = cbits;
-  b.ovf_cell = ctx->d_ovf_c;
-  b.ovf_ent = ctx->d_ovf_e;
-  b.novf = ctx->d_novf;
-  const uint64_t nbins = (cell_n + kBinCells - 1) / kBinCells;
-  if (nbins) {
-    hipLaunchKernelGGL(k_cells_build, dim3((uint32_t)std::min<uint64_t>(nbins, 1u << 20)), dim3(kBlock), 0,
-                       ctx->stream, b);
-    MG_TRY(hipGetLastError());
-    if (getenv("MG_DEBUG_OVF")) {  // TEMP diagnostics: overflow and bin size distribution
-      unsigned long long no = 0;
-      MG_TRY(hipMemcpyAsync(&no, ctx->d_novf, 8, hipMemcpyDeviceToHost, ctx->stream));
-      MG_TRY(hipStreamSynchronize(ctx->stream));
-      std::vector<uint32_t> oc(no), kk(n);
-      if (no) MG_TRY(hipMemcpy(oc.data(), ctx->d_ovf_c, no * 4, hipMemcpyDeviceToHost));
-      if (n) MG_TRY(hipMemcpy(kk.data(), b.key, n * 4, hipMemcpyDeviceToHost));
-      std::sort(oc.begin(), oc.end());
-      std::vector<uint64_t> g;
-      for (size_t i = 0; i < oc.size();) { size_t j = i; while (j < oc.size() && oc[j] == oc[i]) ++j; g.push_back(j - i); i = j; }
-      std::sort(g.rbegin(), g.rend());
-      std::vector<uint64_t> bc(nbins, 0);
-      for (uint64_t i = 0; i < n; ++i) { uint64_t bb = (kk[i] >> shift) >> kBinLog2; if (bb < nbins) bc[bb]++; }
-      std::sort(bc.rbegin(), bc.rend());
-      fprintf(stderr, "[ovf] rank %u shift %u records %lu cells %lu bins %lu overflow %llu groups %zu top groups:", ctx->rank, shift,
-              (unsigned long)n, (unsigned long)cell_n, (unsigned long)nbins, no, g.size());
-      for (size_t i = 0; i < g.size() && i < 12; ++i) fprintf(stderr, " %lu", (unsigned long)g[i]);
-      fprintf(stderr, " | top bins:");
-      for (size_t i = 0; i < bc.size() && i < 8; ++i) fprintf(stderr, " %lu", (unsigned long)bc[i]);
-      fprintf(stderr, " median %lu\n", (unsigned long)bc[bc.size() / 2]);
-    }
-    hipLaunchKernelGGL(k_cells_overflow, dim3((uint32_t)std::max(1, ctx->n_cu * 4)), dim3(kBlock), 0, ctx->stream,
-                       cells, cell_n, ctx->d_ovf_c, ctx->d_ovf_e, ctx->d_novf);
-    MG_TRY(hipGetLastError());
-  }
+// the cell table `cells` of cell_n cells from sorted records key / ent (count
+// n_host, or on the device at n_dev): clear, one store per record, then the
+// chains of the cells with more than kCell entries
+int build_cells(mg_ctx* ctx, const uint32_t* key, const uint64_t* ent, const unsigned long long* n_dev,
+                uint64_t n_host, uint64_t* cells, uint64_t cell_n, uint32_t shift) {
+  MG_TRY(hipMemsetAsync(cells, 0xFF, cell_n * kCell * sizeof(uint64_t), ctx->stream));  // kEmpty
+  const uint64_t cap = n_host;  // (n_dev <= n_host)
+  if (!cap) return 0;
+  const uint32_t grid = (uint32_t)std::max<uint64_t>(
+      1, std::min<uint64_t>((cap + kBlock - 1) / kBlock, (uint64_t)ctx->n_cu * 32));
+  hipLaunchKernelGGL(k_cells_fill, dim3(grid), dim3(kBlock), 0, ctx->stream, key, ent, n_dev, n_host, shift, cells);
+  MG_TRY(hipGetLastError());
+  hipLaunchKernelGGL(k_cells_chain, dim3(grid), dim3(kBlock), 0, ctx->stream, key, ent, n_dev, n_host, shift, cells,
+                     cell_n);
+  MG_TRY(hipGetLastError());
   return 0;
 }
 
@@ -3583,7 +3535,39 @@ int build_live_index_xchg(mg_ctx* ctx) {
   if (!sft) return 0;  // no smaller than the full table: probe that
   const uint64_t live_n = (ctx->cell_n + (1ull << sft) - 1) >> sft;
   MG_TRY(ensure(&ctx->d_lcells, &ctx->lcells_cap, live_n * kCell));
-  if (build_cells(ctx, ctx->d_lcells, live_n, sft, ctx->d_cbits)) return -1;
+  // the live reads' records, compacted in order into the sort's other buffers
+  const uint64_t n = ctx->xkeys_n;
+  const int sel = ctx->xkey_sel;
+  uint32_t* lk = ctx->d_xkk[1 - sel];
+  uint64_t* le = ctx->d_xke[1 - sel];
+  MG_TRY(ensure(&ctx->d_xflag, &ctx->xflag_cap, std::max<uint64_t>(n, 1)));
+  if (!ctx->d_nlive) MG_TRY(hipMalloc(&ctx->d_nlive, sizeof(unsigned long long)));
+  MG_TRY(hipMemsetAsync(ctx->d_nlive, 0, sizeof(unsigned long long), ctx->stream));
+  if (n) {
+    hipLaunchKernelGGL(k_live_flags, dim3((uint32_t)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, ctx->stream,
+                       ctx->d_xke[sel], n, ctx->d_cbits, ctx->d_xflag);
+    MG_TRY(hipGetLastError());
+    for (int pass = 0; pass < 2; ++pass) {
+      size_t tb = 0;
+      MG_TRY(pass ? hipcub::DeviceSelect::Flagged(nullptr, tb, ctx->d_xke[sel], ctx->d_xflag, le, ctx->d_nlive, (int)n,
+                                                  ctx->stream)
+                  : hipcub::DeviceSelect::Flagged(nullptr, tb, ctx->d_xkk[sel], ctx->d_xflag, lk, ctx->d_nlive, (int)n,
+                                                  ctx->stream));
+      if (tb > ctx->xsort_tmp_cap) {
+        if (ctx->d_xsort_tmp) MG_TRY(hipFree(ctx->d_xsort_tmp));
+        ctx->d_xsort_tmp = nullptr;
+        ctx->xsort_tmp_cap = 0;
+        MG_TRY(hipMalloc(&ctx->d_xsort_tmp, tb));
+        ctx->xsort_tmp_cap = tb;
+      }
+      tb = ctx->xsort_tmp_cap;
+      MG_TRY(pass ? hipcub::DeviceSelect::Flagged(ctx->d_xsort_tmp, tb, ctx->d_xke[sel], ctx->d_xflag, le, ctx->d_nlive,
+                                                  (int)n, ctx->stream)
+                  : hipcub::DeviceSelect::Flagged(ctx->d_xsort_tmp, tb, ctx->d_xkk[sel], ctx->d_xflag, lk, ctx->d_nlive,
+                                                  (int)n, ctx->stream));
+    }
+  }
+  if (build_cells(ctx, lk, le, ctx->d_nlive, n, ctx->d_lcells, live_n, sft)) return -1;
   ctx->live_shift = sft;
   ctx->live_cells = live_n;
   ctx->live_coarse = true;
@@ -4081,12 +4065,11 @@ int mg_xchg_insert_keys(mg_ctx* ctx, const void* recv, uint64_t slot, uint32_t r
     MG_TRY(hipGetLastError());
     int hb = 0;
     while (hb < 32 && (1ull << hb) < ctx->cell_n) ++hb;  // bits of a local cell index
-    if (hb > kBinLog2 && n > 1) {  // group the records by bin (the build's unit), not by cell
+    if (hb > 0 && n > 1) {  // a cell's records consecutive
       rocprim::double_buffer<uint32_t> keys(ctx->d_xkk[0], ctx->d_xkk[1]);
       rocprim::double_buffer<uint64_t> vals(ctx->d_xke[0], ctx->d_xke[1]);
       size_t tb = 0;
-      MG_TRY(rocprim::radix_sort_pairs(nullptr, tb, keys, vals, (unsigned int)n, (unsigned)kBinLog2, (unsigned)hb,
-                                       ctx->stream));
+      MG_TRY(rocprim::radix_sort_pairs(nullptr, tb, keys, vals, (unsigned int)n, 0u, (unsigned)hb, ctx->stream));
       if (tb > ctx->xsort_tmp_cap) {
         if (ctx->d_xsort_tmp) MG_TRY(hipFree(ctx->d_xsort_tmp));
         ctx->d_xsort_tmp = nullptr;
@@ -4095,13 +4078,14 @@ int mg_xchg_insert_keys(mg_ctx* ctx, const void* recv, uint64_t slot, uint32_t r
         ctx->xsort_tmp_cap = tb;
       }
       tb = ctx->xsort_tmp_cap;
-      MG_TRY(rocprim::radix_sort_pairs(ctx->d_xsort_tmp, tb, keys, vals, (unsigned int)n, (unsigned)kBinLog2,
-                                       (unsigned)hb, ctx->stream));
+      MG_TRY(rocprim::radix_sort_pairs(ctx->d_xsort_tmp, tb, keys, vals, (unsigned int)n, 0u, (unsigned)hb,
+                                       ctx->stream));
       ctx->xkey_sel = keys.current() == ctx->d_xkk[0] ? 0 : 1;
     }
   }
   ctx->xkeys_n = n;
-  if (build_cells(ctx, ctx->d_cells, ctx->cell_n, 0, nullptr)) return -1;
+  if (build_cells(ctx, ctx->d_xkk[ctx->xkey_sel], ctx->d_xke[ctx->xkey_sel], nullptr, n, ctx->d_cells, ctx->cell_n, 0))
+    return -1;
   MG_TRY(hipEventRecord(ctx->ev[1], ctx->stream));
   ctx->index_ready = true;
   return 0;
