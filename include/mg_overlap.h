@@ -188,7 +188,7 @@ int mg_set_shard(mg_ctx* ctx, uint32_t rank, uint32_t nranks, uint64_t read_lo, 
  * One step (HashTable::insertDataset + OverlapGraph markContainedReads +
  * insertAllEdgesOfRead, distributed):
  *   mg_xchg_begin                 one window scan of this rank's sources: their
- *                                 4 index keys + minimizer runs, runs sorted by bucket
+ *                                 index keys + minimizer runs (in scan order)
  *   mg_xchg_pack(MG_KEYS) -> a2a -> mg_xchg_insert_keys        (insertDataset)
  *   mg_xchg_pack(MG_RUNS) -> a2a   (the received runs serve both probes)
  *   mg_begin_contained(superkey)
@@ -203,10 +203,10 @@ uint32_t mg_record_bytes(int what);
 /* First per-peer stream capacities (records) for keys, runs and rows:
  * caps[3], identical on every rank (global read count and lengths only). */
 int mg_xchg_caps(mg_ctx* ctx, uint32_t min_overlap, uint32_t seed_k, uint64_t* caps);
-/* Set up (and clear) this rank's part of the index, then one scan of its
- * source reads: the index keys (hashRead, HashTable.cpp:88-104) and the
- * windows' minimizer runs (OverlapGraph.cpp:534-537), runs radix-sorted by
- * bucket (so grouped by owning rank). */
+/* Set up this rank's part of the index, then one scan of its source reads:
+ * the index keys (hashRead, HashTable.cpp:88-104; the o = 1 key only when the
+ * containment probe reads it) and the windows' minimizer runs
+ * (OverlapGraph.cpp:534-537), in the scan's order. */
 int mg_xchg_begin(mg_ctx* ctx, uint32_t min_overlap, uint32_t seed_k);
 /* Route what = MG_KEYS / MG_RUNS (after mg_xchg_begin) or MG_ROWS (after
  * mg_xchg_probe(0)) into dst in the slot layout; counts = P device uint64.
@@ -217,14 +217,18 @@ int mg_xchg_begin(mg_ctx* ctx, uint32_t min_overlap, uint32_t seed_k);
 int mg_xchg_pack(mg_ctx* ctx, int what, void* dst, uint64_t slot, uint32_t rounds, uint64_t* counts,
                  void* self_dst);
 /* File the received key records into the local cells (insertIntoTable,
- * HashTable.cpp:163-195); recv / counts as the all-to-all delivered them. */
+ * HashTable.cpp:163-195); recv / counts as the all-to-all delivered them.  The
+ * records are sorted by home cell and stored without atomics (a cell's 9th+
+ * entries chain on); one host read of the counts. */
 int mg_xchg_insert_keys(mg_ctx* ctx, const void* recv, uint64_t slot, uint32_t rounds, const uint64_t* counts);
 /* Probe the received runs against the local cells: contain = 1 atomicMax-es
  * containment keys into the buffer of mg_begin_contained; contain = 0 verifies
  * overlaps (sources with superReadID != 0 give none) and keeps the rows
- * (+ twins) for mg_xchg_pack(MG_ROWS).  The first probe of a step orders the
- * received runs by bucket into the context's own array (one host read of the
- * counts); a second call reuses that order (pass the same recv / counts). */
+ * (+ twins) for mg_xchg_pack(MG_ROWS).  The probes read the runs in place in
+ * recv (pass the same recv / counts to both calls of a step); contain = 0
+ * first compacts away, in place, the runs of contained sources, so recv is
+ * the library's scratch until the step ends.  (Option xchg_sort_runs = 1: the
+ * first call orders them by bucket into the context's own array instead.) */
 int mg_xchg_probe(mg_ctx* ctx, int contain, const void* recv, uint64_t slot, uint32_t rounds, const uint64_t* counts);
 /* Containment: *needed = 1 when read lengths differ (OverlapGraph.cpp:228-233).
  * superkey = caller-owned device array of n_reads u64 (NULL: context-owned),

@@ -166,6 +166,8 @@ struct mg_ctx {
   int xv_sel = 0;
   uint64_t xruns_n = 0;
   bool xruns_ready = false;
+  ulonglong2* xruns_base = nullptr;  // the probes' run regions: d_xv (sorted) or the receive buffer
+  uint64_t xruns_reg = 0, xruns_nreg = 0;
   // exchange mode: the key records this rank received, dense and sorted by
   // home cell (mg_xchg_insert_keys: key = local home cell, ent = index
   // entry); they build the cells, the o = 0 ones drive the prefix containments
@@ -183,7 +185,8 @@ struct mg_ctx {
   // local home cell >> live_shift) instead of rebuilding entries
   bool live_coarse = false;
   uint32_t live_shift = 0;
-  bool xchg_sort_runs = true;  // option "xchg_sort_runs": received runs ordered by bucket before the probes
+  bool xchg_sort_runs = false;  // option "xchg_sort_runs": received runs ordered by bucket before the probes
+  bool xchg_windows = true;    // option "xchg_windows": the exchange scan of mixed lengths in length-ranked windows
   bool layout_scratch = true;  // option "layout_scratch" = 0: free the layout's double buffers after each layout
   bool xchg_prefix = false;
   bool key0_ready = false;

@@ -2594,13 +2594,16 @@ inline uint32_t scan_wpb(uint32_t w) {
 // sliding minimum (k_scan_reg<INDEX> + k_rc_keys) when w fits its unrolled
 // window, else from k_scan<INDEX>.  Run-only scans (source-range shards) take
 // the register scan when w fits.
+// The exchange mode's index scan of mixed lengths takes k_scan's length-ranked
+// windows too (option xchg_windows): one read per lane idles the lanes of
+// shorter reads, and longest first scans containers before their contents.
 inline bool scan_is_reg(const mg_ctx* ctx, bool index) {
-  return ctx->w <= (uint32_t)kRegW && (!index || ctx->xchg);
+  return ctx->w <= (uint32_t)kRegW && (!index || (ctx->xchg && !(ctx->xchg_windows && ctx->minlen != ctx->maxlen)));
 }
-// groups per k_scan window (one run region each): the fused index scan of
-// mixed lengths ranks each window's reads by length (kWinGroups); else 1
+// groups per k_scan window (one run region each): the index scan of mixed
+// lengths ranks each window's reads by length (kWinGroups); else 1
 inline int scan_windows(const mg_ctx* ctx, bool index) {
-  return (index && !ctx->xchg && ctx->minlen != ctx->maxlen && !scan_is_reg(ctx, index)) ? kWinGroups : 1;
+  return (index && ctx->minlen != ctx->maxlen && !scan_is_reg(ctx, index)) ? kWinGroups : 1;
 }
 inline uint32_t scan_block_waves(const mg_ctx* ctx, bool index) {
   return scan_is_reg(ctx, index) ? kWavesPerBlock : scan_wpb(ctx->w);
@@ -2616,6 +2619,9 @@ uint32_t scan_resident(mg_ctx* ctx, bool index, uint64_t want) {
   if (scan_is_reg(ctx, index))
     return index ? resident_blocks(ctx, k_scan_reg<W, true>, lds, want, block)
                  : resident_blocks(ctx, k_scan_reg<W, false>, lds, want, block);
+  if (index && ctx->xchg)
+    return scan_windows(ctx, index) > 1 ? resident_blocks(ctx, k_scan<W, true, true, kWinGroups>, lds, want, block)
+                                        : resident_blocks(ctx, k_scan<W, true, true>, lds, want, block);
   return index ? (scan_windows(ctx, index) > 1 ? resident_blocks(ctx, k_scan<W, true, false, kWinGroups>, lds, want, block)
                                                 : resident_blocks(ctx, k_scan<W, true>, lds, want, block))
                : resident_blocks(ctx, k_scan<W, false>, lds, want, block);
@@ -2721,6 +2727,9 @@ struct LaunchScan {
         allow_lds(k_scan_reg<W, false>, lds);
         hipLaunchKernelGGL((k_scan_reg<W, false>), dim3(sgrid), dim3(wpb * kWave), lds, stream, sp);
       }
+    } else if (index && ctx->xchg && G > 1) {
+      allow_lds(k_scan<W, true, true, kWinGroups>, lds);
+      hipLaunchKernelGGL((k_scan<W, true, true, kWinGroups>), dim3(sgrid), dim3(wpb * kWave), lds, stream, sp);
     } else if (index && ctx->xchg) {
       allow_lds(k_scan<W, true, true>, lds);
       hipLaunchKernelGGL((k_scan<W, true, true>), dim3(sgrid), dim3(wpb * kWave), lds, stream, sp);
@@ -3179,7 +3188,8 @@ int mg_set_option(mg_ctx* ctx, const char* name, int64_t value) {
       flag("contain_jcut", &ctx->contain_jcut) || flag("contain_skip", &ctx->contain_skip) ||
       flag("contain_prune", &ctx->contain_prune) || flag("probe_share", &ctx->probe_share) ||
       flag("probe_compact", &ctx->probe_compact) || flag("live_index", &ctx->live_index) ||
-      flag("xchg_sort_runs", &ctx->xchg_sort_runs) || flag("layout_scratch", &ctx->layout_scratch))
+      flag("xchg_sort_runs", &ctx->xchg_sort_runs) || flag("layout_scratch", &ctx->layout_scratch) ||
+      flag("xchg_windows", &ctx->xchg_windows))
     return 0;
   if (flag("prefix_contain", &ctx->prefix_contain)) {
     ctx->index_ready = false;
@@ -3674,6 +3684,34 @@ static int sort_xruns(mg_ctx* ctx, const ulonglong2* recv, uint64_t slot, uint32
   return 0;
 }
 
+// The received runs as probe regions: by default the receive buffer itself
+// (slot layout, compacted in place by k_live_runs before the discovery probe),
+// regions of the largest power of two <= kXRegion records dividing the slot,
+// with device-side counts (no host read).  Each peer's stream keeps its
+// sender's scan order, i.e. the clustered slot order, so consecutive runs
+// share cells and partners as in the fused path; ordering them by bucket
+// (option xchg_sort_runs) measured slower: C3 simulated P = 8 step 20.5 vs
+// 18.4 ms, C5 133.8 vs 123.0 ms (profiles/r04e_ab_xchg_sort_runs.txt).
+static int prepare_xruns(mg_ctx* ctx, const void* recv, uint64_t slot, uint32_t rounds,
+                         const unsigned long long* counts) {
+  if (ctx->xchg_sort_runs) {
+    if (sort_xruns(ctx, reinterpret_cast<const ulonglong2*>(recv), slot, rounds, counts)) return -1;
+    ctx->xruns_base = ctx->d_xv[ctx->xv_sel];
+    ctx->xruns_reg = kXRegion;
+    ctx->xruns_nreg = (ctx->xruns_n + kXRegion - 1) / kXRegion;
+    return 0;
+  }
+  uint64_t reg = kXRegion;
+  while (reg > 1 && slot % reg) reg >>= 1;
+  const uint64_t nreg = slot ? (uint64_t)rounds * ctx->nranks * (slot / reg) : 0;
+  if (slot_regions(ctx, &ctx->d_flat_cnt, &ctx->flat_cnt_cap, counts, slot, reg, nreg)) return -1;
+  ctx->xruns_base = reinterpret_cast<ulonglong2*>(const_cast<void*>(recv));
+  ctx->xruns_reg = reg;
+  ctx->xruns_nreg = nreg;
+  ctx->xruns_ready = true;
+  return 0;
+}
+
 // Device layout (mg_ctx.hpp): layout keys -> rocprim radix sort
 // of (key, slot) -> gather into the second slot array -> commit.  Every
 // buffer is the context's own and kept between uploads, so the timed window
@@ -4098,13 +4136,12 @@ int mg_xchg_probe(mg_ctx* ctx, int contain, const void* recv, uint64_t slot, uin
   if (contain && !ctx->superkey) return set_err(ctx, "mg_begin_contained must run first (lengths differ)");
   if (!contain && !ctx->contained_done) return set_err(ctx, "containment must be settled first (mg_finalize_contained)");
   if ((uint64_t)rounds * slot && (!recv || !counts)) return set_err(ctx, "mg_xchg_probe: null buffer");
-  // the first probe of the step orders the received runs (both probes read them)
-  if (!ctx->xruns_ready && sort_xruns(ctx, reinterpret_cast<const ulonglong2*>(recv), slot, rounds,
-                                      reinterpret_cast<const unsigned long long*>(counts)))
+  // the first probe of the step sets up the received runs (both probes read them)
+  if (!ctx->xruns_ready && prepare_xruns(ctx, recv, slot, rounds, reinterpret_cast<const unsigned long long*>(counts)))
     return -1;
-  const uint64_t reg = kXRegion;
-  const uint64_t nregions = (ctx->xruns_n + reg - 1) / reg;
-  ulonglong2* runs = ctx->d_xv[ctx->xv_sel];
+  const uint64_t reg = ctx->xruns_reg;
+  const uint64_t nregions = ctx->xruns_nreg;
+  ulonglong2* runs = ctx->xruns_base;
   ctx->nreg = 0;
   ctx->n_rows = 0;
   if (contain) {
@@ -4124,8 +4161,8 @@ int mg_xchg_probe(mg_ctx* ctx, int contain, const void* recv, uint64_t slot, uin
     if (attempt == 0 && ctx->contained_done && ctx->super_any && build_live_index_xchg(ctx)) return -1;
     if (attempt == 0 && nregions && ctx->contained_done && ctx->super_any) {
       // runs of contained sources contribute nothing (:548): drop them from the
-      // ordered regions in place (the containment probe has read them already)
-      // so the probe batches live runs only
+      // run regions in place (the containment probe has read them already), so
+      // the probe batches live runs only
       const uint32_t grid = (uint32_t)std::min<uint64_t>((nregions + kWavesPerBlock - 1) / kWavesPerBlock,
                                                          (uint64_t)ctx->n_cu * 8);
       hipLaunchKernelGGL(k_live_runs, dim3(grid), dim3(kBlock), 0, ctx->stream, runs, ctx->d_flat_cnt, reg,

@@ -115,7 +115,8 @@ void RcclExchange::allgather_u64(const uint64_t* send, uint64_t* recv, size_t n,
 }
 
 void slot_geometry(uint64_t cap, int world, uint32_t rec, uint64_t chunk, uint64_t* slot, uint32_t* rounds) {
-  constexpr uint64_t kAlign = 64;  // the probe tiles a slot by its divisors
+  // the probe tiles a slot by its divisors: large streams take whole 1024-record regions
+  const uint64_t kAlign = cap >= 64 * 1024 ? 1024 : 64;
   const uint64_t per_round = std::max<uint64_t>(kAlign, (chunk / ((uint64_t)world * rec)) / kAlign * kAlign);
   const uint64_t want = std::max<uint64_t>(kAlign, (cap + kAlign - 1) / kAlign * kAlign);
   *slot = std::min(want, per_round);

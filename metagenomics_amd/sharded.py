@@ -42,6 +42,7 @@ import numpy as np
 from .overlap import EDGE_DTYPE, MG_KEYS, MG_ROWS, MG_RUNS, RECORD_BYTES
 
 SLOT_ALIGN = 64  # slots are whole multiples of this many records (the probe tiles a slot by its divisors)
+BIG_SLOT_ALIGN = 1024
 # the exchange mode's kernels keep a read in registers and pack window
 # positions into 10 bits: reads up to 1,024 bp (longer ones: replicated mode)
 EXCHANGE_MAX_BP = 1024
@@ -50,9 +51,12 @@ KINDS = (MG_KEYS, MG_RUNS, MG_ROWS)
 
 def slot_geometry(cap: int, world: int, rec_bytes: int, chunk_bytes: int):
     """(slot, rounds) for a per-peer stream of at most ``cap`` records: one round moves
-    world * slot records per rank, at most ``chunk_bytes`` (never below one aligned slot)."""
-    per_round = max(SLOT_ALIGN, (chunk_bytes // (world * rec_bytes)) // SLOT_ALIGN * SLOT_ALIGN)
-    want = max(SLOT_ALIGN, -(-int(cap) // SLOT_ALIGN) * SLOT_ALIGN)
+    world * slot records per rank, at most ``chunk_bytes`` (never below one aligned slot).
+    Large streams take slots of whole 1024-record regions (the probe's region size over
+    the received runs is the largest power of two <= 1024 dividing the slot)."""
+    align = BIG_SLOT_ALIGN if cap >= 64 * BIG_SLOT_ALIGN else SLOT_ALIGN
+    per_round = max(align, (chunk_bytes // (world * rec_bytes)) // align * align)
+    want = max(align, -(-int(cap) // align) * align)
     slot = min(want, per_round)
     return slot, -(-want // slot)
 

@@ -87,12 +87,14 @@ def test_exchange_routes_every_record(tmp_path, name, world, chunk):
 
 
 def test_slot_geometry():
-    from metagenomics_amd.sharded import SLOT_ALIGN, slot_geometry
+    from metagenomics_amd.sharded import BIG_SLOT_ALIGN, SLOT_ALIGN, slot_geometry
 
     for cap, world, rb, ch in [(1, 1, 16, 256 << 20), (10**8, 1, 16, 256 << 20), (10**8, 8, 12, 256 << 20),
                                (1000, 2, 16, 4096), (64, 3, 12, 100), (5 * 10**6, 64, 16, 256 << 20)]:
         slot, rounds = slot_geometry(cap, world, rb, ch)
         assert slot % SLOT_ALIGN == 0 and slot >= SLOT_ALIGN and rounds >= 1
+        if cap >= 64 * BIG_SLOT_ALIGN:  # whole 1024-record probe regions
+            assert slot % BIG_SLOT_ALIGN == 0
         assert slot * rounds >= cap
         assert world * slot * rb <= max(ch, world * SLOT_ALIGN * rb)  # a round stays within the chunk
         assert world * slot * rb < 2**31  # every all-to-all call's byte count fits int32

@@ -67,6 +67,18 @@ for s in $STEPS; do
       rc=$?; echo "profsim8 $C rc=$rc"; [ $rc -ne 0 ] && break
       python3 tools/rank_table.py $OUT/profsim8_$C/kt_kernel_stats.csv 8 4 "$C exchange-sim" | tee $OUT/profsim8_${C}_ranks.md | tail -14
     done ;;
+  simab)
+    # wall of the simulated exchange step (serial ranks) for option A/B pairs: MG_AB="opt=v ..." vs default
+    for C in ${SIMAB_CONFIGS:-c3 c5}; do
+      for rep in 1 2; do
+        for V in "" "$MG_AB"; do
+          o=""; for kv in $V; do o="$o --opt $kv"; done
+          MG_SIM_SERIAL=1 timeout -k 10 400 python -u bench.py --config $C --sim-world 8 --multi exchange --steps 3 --no-cpu-baseline --no-ingest --opt layout_scratch=0 $o > $OUT/simab.json 2> $OUT/simab.err
+          rc=$?; [ $rc -ne 0 ] && break 3
+          python3 -c "import json;d=json.load(open('$OUT/simab.json'));print('$C','[$V]','ms/step',round(d['ms_per_step'],3),'digest_ok',d['parity'].get('digest_ok'),{k:round(v,2) for k,v in (d.get('phase_wall_ms') or {}).items()})" | tee -a $OUT/simab.log
+        done
+      done
+    done ;;
   a2a)
     timeout -k 10 300 python -u tools/a2a_probe.py > $OUT/a2a_probe.log 2>&1
     rc=$?; echo "a2a_probe rc=$rc"; grep MB $OUT/a2a_probe.log ;;
