@@ -258,7 +258,7 @@ def parity_digest(engines, last, mode, dist, config):
     workload (tests/golden/<config>.json, made by oracle/_ref/ref_harness)."""
     import torch
 
-    if mode.startswith("exchange") and last.host_rows is None:
+    if mode.startswith("exchange") and last.rows_in_slots:
         rows = [e.slots_digest(buf.data_ptr(), slot, rounds, cnt.data_ptr())
                 for e, (buf, cnt, slot, rounds) in zip(engines, last.rows)]
     else:

@@ -150,6 +150,9 @@ int mg_find_overlaps(mg_ctx* ctx, uint64_t* n_rows);
 /* Copy the rows to the host (any order; the multiset is what the reference
  * defines).  cap in rows; returns rows copied via *n_copied. */
 int mg_copy_rows(mg_ctx* ctx, mg_edge* out, uint64_t cap, uint64_t* n_copied);
+/* Rows held by the context after the last mg_find_overlaps / mg_xchg_probe(0)
+ * (the count mg_copy_rows copies and mg_rows_digest(rows = NULL) digests). */
+uint64_t mg_num_rows(const mg_ctx* ctx);
 
 /* --- sharding (multi-GPU, one process per GPU) ---------------------------- */
 /* Restrict this context to index buckets owned by `rank` of `nranks`
@@ -210,6 +213,10 @@ int mg_xchg_caps(mg_ctx* ctx, uint32_t min_overlap, uint32_t seed_k, uint64_t* c
 int mg_xchg_begin(mg_ctx* ctx, uint32_t min_overlap, uint32_t seed_k);
 /* Route what = MG_KEYS / MG_RUNS (after mg_xchg_begin) or MG_ROWS (after
  * mg_xchg_probe(0)) into dst in the slot layout; counts = P device uint64.
+ * With one rank (P = 1) every stream is the rank's own: nothing is copied and
+ * counts[0] = 0; mg_xchg_insert_keys and mg_xchg_probe then read the
+ * context's own key records and run regions (recv / counts ignored), and the
+ * rows stay in the context (mg_num_rows, mg_rows_digest, mg_copy_rows).
  * self_dst (optional): the stream bound for this rank itself is written there
  * instead -- the caller's receive buffer, whose slots for this rank sit at the
  * same offsets -- so it never travels (the all-to-all then moves only the

@@ -166,7 +166,8 @@ struct mg_ctx {
   int xv_sel = 0;
   uint64_t xruns_n = 0;
   bool xruns_ready = false;
-  ulonglong2* xruns_base = nullptr;  // the probes' run regions: d_xv (sorted) or the receive buffer
+  ulonglong2* xruns_base = nullptr;  // the probes' run regions: d_xv (sorted), the receive buffer, or (one rank) d_runs
+  unsigned long long* xruns_cnt = nullptr;  // their per-region counts
   uint64_t xruns_reg = 0, xruns_nreg = 0;
   // exchange mode: the key records this rank received, dense and sorted by
   // home cell (mg_xchg_insert_keys: key = local home cell, ent = index
@@ -175,8 +176,15 @@ struct mg_ctx {
   uint32_t* d_xkk[2] = {nullptr, nullptr};
   uint64_t* d_xke[2] = {nullptr, nullptr};
   size_t xkk_cap[2] = {0, 0}, xke_cap[2] = {0, 0};
-  int xkey_sel = 0;
   uint64_t xkeys_n = 0;
+  uint32_t* xkey_k = nullptr;  // the sorted records (one of d_xkk[] / d_kb) and the other buffer pair
+  uint64_t* xkey_e = nullptr;
+  uint32_t* xkey_k_alt = nullptr;
+  uint64_t* xkey_e_alt = nullptr;
+  // group leaders of the cell build (k_cells_fill -> k_cells_chain)
+  uint64_t* d_lead = nullptr;
+  size_t lead_cap = 0;
+  unsigned long long* d_nlead = nullptr;
   // the live records' in-order compaction (build_live_index_xchg)
   uint8_t* d_xflag = nullptr;
   size_t xflag_cap = 0;

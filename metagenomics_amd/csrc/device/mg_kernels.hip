@@ -437,7 +437,7 @@ struct LaunchPrefixContainKeys {
     const uint32_t grid = (uint32_t)std::max<uint64_t>(
         1, std::min<uint64_t>((n + kBlock - 1) / kBlock, (uint64_t)ctx->n_cu * 16));
     hipLaunchKernelGGL(k_prefix_contain_keys<W>, dim3(grid), dim3(kBlock), 0, ctx->stream, ctx->d_words, ctx->d_len,
-                       ctx->d_xkk[ctx->xkey_sel], ctx->d_xke[ctx->xkey_sel], n, ctx->d_cells, ctx->cell_n,
+                       ctx->xkey_k, ctx->xkey_e, n, ctx->d_cells, ctx->cell_n,
                        ctx->superkey, ctx->d_id);
     return hipGetLastError() == hipSuccess ? 0 : -1;
   }
@@ -489,42 +489,66 @@ __global__ __launch_bounds__(kBlock) void k_xkeys_dense(const ulonglong2* __rest
   }
 }
 
-// number of records equal to key c (>> shift) directly before record i, capped at kCell
-__device__ __forceinline__ int rank_in_cell(const uint32_t* __restrict__ key, uint64_t i, uint32_t shift, uint32_t c) {
-  bool eq[kCell + 1];
-#pragma unroll
-  for (int k = 1; k <= kCell; ++k) eq[k] = i >= (uint64_t)k && (key[i - k] >> shift) == c;
-  int r = 0;
-#pragma unroll
-  for (int k = 1; k <= kCell; ++k) r = (r == k - 1 && eq[k]) ? k : r;
-  return r;
-}
-
-// n_dev non-null: the record count is on the device (a compaction's output)
+// One plain store per record: its slot is the number of equal keys (>> shift)
+// right before it, from the block's tile of keys in LDS (kCell keys of look-
+// back before the tile, one of look-ahead after it).  The 8th entry of a cell
+// that has more carries the chain flag; the record of rank 8 (the first that
+// does not fit) is a group leader, appended to `lead` for k_cells_chain.
+// n_dev non-null: the record count is on the device (a compaction's output).
 __global__ __launch_bounds__(kBlock) void k_cells_fill(const uint32_t* __restrict__ key,
                                                       const uint64_t* __restrict__ ent,
                                                       const unsigned long long* __restrict__ n_dev, uint64_t n_host,
-                                                      uint32_t shift, uint64_t* __restrict__ cells) {
+                                                      uint32_t shift, uint64_t* __restrict__ cells,
+                                                      uint64_t* __restrict__ lead, unsigned long long* __restrict__ nlead) {
+  __shared__ uint32_t s_key[kCell + kBlock + 1];
   const uint64_t n = n_dev ? *n_dev : n_host;
-  for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBlock) {
-    const uint32_t c = key[i] >> shift;
-    const int r = rank_in_cell(key, i, shift, c);
-    if (r < kCell) {
-      const bool more = r == kCell - 1 && i + 1 < n && (key[i + 1] >> shift) == c;
-      cells[(uint64_t)c * kCell + r] = more ? (ent[i] | kChain) : ent[i];
+  const int lane = threadIdx.x & 63;
+  for (uint64_t i0 = (uint64_t)blockIdx.x * kBlock; i0 < n; i0 += (uint64_t)gridDim.x * kBlock) {
+    // tile [i0 - kCell, i0 + kBlock + 1) of the cell keys; out of range = a key no cell has
+    for (int t = threadIdx.x; t < kCell + kBlock + 1; t += kBlock) {
+      const int64_t j = (int64_t)i0 - kCell + t;
+      s_key[t] = (j >= 0 && (uint64_t)j < n) ? key[j] >> shift : 0xFFFFFFFFu;
     }
+    __syncthreads();
+    const uint64_t i = i0 + threadIdx.x;
+    bool leader = false;
+    if (i < n) {
+      const uint32_t c = s_key[kCell + threadIdx.x];
+      int r = 0;
+#pragma unroll
+      for (int k = 1; k <= kCell; ++k) r = (r == k - 1 && s_key[kCell + threadIdx.x - k] == c) ? k : r;
+      if (r < kCell) {
+        const bool more = r == kCell - 1 && s_key[kCell + threadIdx.x + 1] == c;
+        const uint64_t e = ent[i];
+        cells[(uint64_t)c * kCell + r] = more ? (e | kChain) : e;
+      } else {  // rank >= kCell: the group's leader if the key kCell + 1 back differs
+        const uint32_t back = threadIdx.x ? s_key[threadIdx.x - 1]
+                                          : (i >= kCell + 1 ? key[i - kCell - 1] >> shift : 0xFFFFFFFFu);
+        leader = back != c;
+      }
+    }
+    const uint64_t bal = __ballot(leader);
+    if (bal) {
+      unsigned long long base = 0;
+      if (lane == 0) base = atomicAdd(nlead, (unsigned long long)__popcll(bal));
+      base = __shfl(base, 0);
+      if (leader) lead[base + lane_prefix(bal)] = i;
+    }
+    __syncthreads();
   }
 }
 
-// the 9th+ entries of each cell, one thread per group (the group's record of rank 8)
+// The 9th+ entries of each cell, one thread per group (its leader: rank 8)
 __global__ __launch_bounds__(kBlock) void k_cells_chain(const uint32_t* __restrict__ key,
                                                        const uint64_t* __restrict__ ent,
                                                        const unsigned long long* __restrict__ n_dev, uint64_t n_host,
-                                                       uint32_t shift, uint64_t* cells, uint64_t cell_n) {
-  const uint64_t n = n_dev ? *n_dev : n_host;
-  for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBlock) {
+                                                       uint32_t shift, uint64_t* cells, uint64_t cell_n,
+                                                       const uint64_t* __restrict__ lead,
+                                                       const unsigned long long* __restrict__ nlead) {
+  const uint64_t n = n_dev ? *n_dev : n_host, nl = *nlead;
+  for (uint64_t g = (uint64_t)blockIdx.x * kBlock + threadIdx.x; g < nl; g += (uint64_t)gridDim.x * kBlock) {
+    const uint64_t i = lead[g];
     const uint32_t c = key[i] >> shift;
-    if (rank_in_cell(key, i, shift, c) != kCell || (i >= kCell + 1 && (key[i - kCell - 1] >> shift) == c)) continue;
     uint32_t last_fp = ~0u;
     uint64_t at = c;
     for (uint64_t j = i; j < n && (key[j] >> shift) == c; ++j) {
@@ -532,7 +556,8 @@ __global__ __launch_bounds__(kBlock) void k_cells_chain(const uint32_t* __restri
       const uint32_t fp = entry_fp(e);
       if (fp != last_fp) at = next_cell(c, cell_n, fp);  // the home is full: its chain starts at the next cell
       last_fp = fp;
-      // cell_insert from `at`, leaving `at` at the cell that took the entry
+      // cell_insert from `at`, leaving `at` at the cell that took the entry (the
+      // group's next entry with this fingerprint resumes there)
       for (uint64_t probe = 0; probe < cell_n; ++probe) {
         unsigned long long* cell = reinterpret_cast<unsigned long long*>(cells + at * kCell);
         uint64_t ev[kCell];
@@ -594,6 +619,11 @@ struct ScanParams {
   uint64_t* key0;
   int skip_o1;                    // INDEX: leave out the o = 1 keys (mg_ctx::index_o1)
 };
+
+// Exchange-mode key records are o-major in the order o = 0, 2, 3, 1: when the
+// index leaves out the o = 1 keys, the valid records are the first three
+// segments (one rank: mg_xchg_insert_keys sorts them in place)
+__device__ __forceinline__ int key_seg(int o) { return o == 0 ? 0 : (o == 1 ? 3 : o - 1); }
 
 __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -974,8 +1004,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(G > 1 ? 
         const unsigned long long e = make_entry(v, p.nb_log2, (int)(kb[o] & 1023u), o, (uint32_t)a);
         if (o == 0 && p.key0) p.key0[a] = (v & ((1ULL << 50) - 1)) | ((uint64_t)(kb[0] & 1023u) << 54);
         if constexpr (KEYREC) {  // o-major: each store is one coalesced wavefront line
-          p.key_bk[o * p.key_n + a - p.key_lo] = (uint32_t)(v & nbm);
-          p.key_ent[o * p.key_n + a - p.key_lo] = (o == 1 && p.skip_o1) ? kEmpty : e;  // (a hole: not routed)
+          p.key_bk[key_seg(o) * p.key_n + a - p.key_lo] = (uint32_t)(v & nbm);
+          p.key_ent[key_seg(o) * p.key_n + a - p.key_lo] = (o == 1 && p.skip_o1) ? kEmpty : e;  // (a hole: not routed)
         }
         cb[o] = v & nbm;
         ce[o] = e;
@@ -991,8 +1021,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(G > 1 ? 
       if (p.key0) p.key0[a] = kEmpty;
       if constexpr (KEYREC) {
         for (int o = 0; o < 4; ++o) {
-          p.key_bk[o * p.key_n + a - p.key_lo] = 0;
-          p.key_ent[o * p.key_n + a - p.key_lo] = kEmpty;
+          p.key_bk[key_seg(o) * p.key_n + a - p.key_lo] = 0;
+          p.key_ent[key_seg(o) * p.key_n + a - p.key_lo] = kEmpty;
         }
       }
     }
@@ -1201,8 +1231,8 @@ __global__ __launch_bounds__(kBlock) void k_scan_reg(ScanParams p) {
         const uint64_t ka = a - p.key_lo;
         p.key_bk[ka] = b0;
         p.key_ent[ka] = c0;
-        p.key_bk[p.key_n + ka] = b1;
-        p.key_ent[p.key_n + ka] = c1;
+        p.key_bk[3 * p.key_n + ka] = b1;  // (key_seg(1) = 3)
+        p.key_ent[3 * p.key_n + ka] = c1;
       }
     }
   }
@@ -1234,7 +1264,7 @@ __device__ __forceinline__ void load_slot(const uint64_t* words, uint32_t bid, u
 // t = w-1-i) and o = 2 (R[0, h) = rc F[n-h, n): m-mer i = rc of F's at
 // t = n-m-i), both rolled towards smaller t, one base per step; the same
 // minimizer rule (order_key | i, smallest wins) as key_minimizer.  Written to
-// key_bk / key_ent[o * key_n + a], o = 2, 3 (k_scan_reg<INDEX> writes o = 0, 1).
+// key_bk / key_ent[key_seg(o) * key_n + a], o = 2, 3 (k_scan_reg<INDEX> writes o = 0, 1).
 template <int MAXW>
 __global__ __launch_bounds__(kBlock) void k_rc_keys(ScanParams p) {
   const uint64_t a = p.a_lo + (uint64_t)blockIdx.x * kBlock + threadIdx.x;
@@ -1261,10 +1291,10 @@ __global__ __launch_bounds__(kBlock) void k_rc_keys(ScanParams p) {
   const uint64_t v2 = mix64(mb2), v3 = mix64(mb3);
   const uint64_t nbm = (1ULL << p.nb_log2) - 1;  // (bucket, entry) records, o-major
   const uint64_t ka = a - p.key_lo;
-  p.key_bk[2 * p.key_n + ka] = n ? (uint32_t)(v2 & nbm) : 0u;
-  p.key_ent[2 * p.key_n + ka] = n ? make_entry(v2, p.nb_log2, (int)(kb2 & 1023u), 2, (uint32_t)a) : kEmpty;
-  p.key_bk[3 * p.key_n + ka] = n ? (uint32_t)(v3 & nbm) : 0u;
-  p.key_ent[3 * p.key_n + ka] = n ? make_entry(v3, p.nb_log2, (int)(kb3 & 1023u), 3, (uint32_t)a) : kEmpty;
+  p.key_bk[p.key_n + ka] = n ? (uint32_t)(v2 & nbm) : 0u;  // (key_seg(2) = 1, key_seg(3) = 2)
+  p.key_ent[p.key_n + ka] = n ? make_entry(v2, p.nb_log2, (int)(kb2 & 1023u), 2, (uint32_t)a) : kEmpty;
+  p.key_bk[2 * p.key_n + ka] = n ? (uint32_t)(v3 & nbm) : 0u;
+  p.key_ent[2 * p.key_n + ka] = n ? make_entry(v3, p.nb_log2, (int)(kb3 & 1023u), 3, (uint32_t)a) : kEmpty;
 }
 
 // checkOverlap's string compare (OverlapGraph.cpp:354-383) on packed words:
@@ -1879,7 +1909,7 @@ __global__ __launch_bounds__(kBlock) void k_part(PartParams p) {
       uint3 x12 = make_uint3(0, 0, 0);
       if (valid) {
         if (KIND == OWN_KEY) {
-          const uint64_t v = r * p.cap + i, o = v / p.nsrc, at = o * p.key_n + p.a_lo + (v - o * p.nsrc);
+          const uint64_t at = r * p.cap + i;  // (the rank's records are contiguous, key_seg order)
           const uint64_t e = p.key_ent[at];
           const uint32_t b = p.key_bk[at];
           valid = e != kEmpty;  // a read without keys (never after setup_index's length check)
@@ -3003,7 +3033,7 @@ void mg_destroy(mg_ctx* ctx) {
   (void)hipStreamSynchronize(ctx->stream);
   void* bufs[] = {ctx->d_words, ctx->d_len, ctx->d_cells, ctx->d_superkey, ctx->d_super, ctx->d_any, ctx->d_rows,
                   ctx->d_seg, ctx->d_stats, ctx->d_compact, ctx->d_runs, ctx->d_run_cnt, ctx->d_blk, ctx->d_flat_cnt,
-                  ctx->d_slot_cnt, ctx->d_freq, ctx->d_kb, ctx->d_ke, ctx->d_key0, ctx->d_xkk[0], ctx->d_xkk[1], ctx->d_xke[0], ctx->d_xke[1],
+                  ctx->d_slot_cnt, ctx->d_freq, ctx->d_kb, ctx->d_ke, ctx->d_key0, ctx->d_xkk[0], ctx->d_xkk[1], ctx->d_xke[0], ctx->d_xke[1], ctx->d_lead, ctx->d_nlead,
                   ctx->d_xflag, ctx->d_nlive,
                   ctx->d_xk[0], ctx->d_xk[1], ctx->d_xv[0], ctx->d_xv[1], ctx->d_xsort_tmp,
                   ctx->d_digest, ctx->id_store[0], ctx->id_store[1], ctx->phys_store[0], ctx->phys_store[1],
@@ -3022,6 +3052,8 @@ const char* mg_last_error(const mg_ctx* ctx) { return ctx ? ctx->err.c_str() : "
 void* mg_stream(mg_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
 
 uint64_t mg_num_reads(const mg_ctx* ctx) { return ctx ? ctx->n : 0; }
+
+uint64_t mg_num_rows(const mg_ctx* ctx) { return ctx ? ctx->n_rows : 0; }
 
 
 static int finish_upload(mg_ctx* ctx, const uint16_t* lens_host) {
@@ -3337,7 +3369,7 @@ struct LaunchProbeSlots {
     const DiscGeom g = disc_geom<W>(ctx, contain, std::max<uint64_t>(1, ctx->n / ctx->nranks));
     const uint32_t* sup =
         (!contain && ctx->contained_done && ctx->super_any && !ctx->runs_live) ? ctx->d_super : nullptr;
-    return LaunchProbe<W>::run(ctx, contain, runs, ctx->d_flat_cnt, reg, nregions, g.grid, sup);
+    return LaunchProbe<W>::run(ctx, contain, runs, ctx->xruns_cnt, reg, nregions, g.grid, sup);
   }
 };
 
@@ -3506,19 +3538,22 @@ int build_live_index(mg_ctx* ctx) {
 }
 
 // the cell table `cells` of cell_n cells from sorted records key / ent (count
-// n_host, or on the device at n_dev): clear, one store per record, then the
-// chains of the cells with more than kCell entries
+// n_host, or on the device at n_dev <= n_host): clear, one store per record,
+// then the chains of the cells with more than kCell entries (their leaders)
 int build_cells(mg_ctx* ctx, const uint32_t* key, const uint64_t* ent, const unsigned long long* n_dev,
                 uint64_t n_host, uint64_t* cells, uint64_t cell_n, uint32_t shift) {
   MG_TRY(hipMemsetAsync(cells, 0xFF, cell_n * kCell * sizeof(uint64_t), ctx->stream));  // kEmpty
-  const uint64_t cap = n_host;  // (n_dev <= n_host)
-  if (!cap) return 0;
+  if (!n_host) return 0;
+  MG_TRY(ensure(&ctx->d_lead, &ctx->lead_cap, n_host / (kCell + 1) + 1));  // a leader per kCell + 1 records at most
+  if (!ctx->d_nlead) MG_TRY(hipMalloc(&ctx->d_nlead, sizeof(unsigned long long)));
+  MG_TRY(hipMemsetAsync(ctx->d_nlead, 0, sizeof(unsigned long long), ctx->stream));
   const uint32_t grid = (uint32_t)std::max<uint64_t>(
-      1, std::min<uint64_t>((cap + kBlock - 1) / kBlock, (uint64_t)ctx->n_cu * 32));
-  hipLaunchKernelGGL(k_cells_fill, dim3(grid), dim3(kBlock), 0, ctx->stream, key, ent, n_dev, n_host, shift, cells);
+      1, std::min<uint64_t>((n_host + kBlock - 1) / kBlock, (uint64_t)ctx->n_cu * 32));
+  hipLaunchKernelGGL(k_cells_fill, dim3(grid), dim3(kBlock), 0, ctx->stream, key, ent, n_dev, n_host, shift, cells,
+                     ctx->d_lead, ctx->d_nlead);
   MG_TRY(hipGetLastError());
-  hipLaunchKernelGGL(k_cells_chain, dim3(grid), dim3(kBlock), 0, ctx->stream, key, ent, n_dev, n_host, shift, cells,
-                     cell_n);
+  hipLaunchKernelGGL(k_cells_chain, dim3((uint32_t)std::max(1, ctx->n_cu * 4)), dim3(kBlock), 0, ctx->stream, key,
+                     ent, n_dev, n_host, shift, cells, cell_n, ctx->d_lead, ctx->d_nlead);
   MG_TRY(hipGetLastError());
   return 0;
 }
@@ -3547,21 +3582,20 @@ int build_live_index_xchg(mg_ctx* ctx) {
   MG_TRY(ensure(&ctx->d_lcells, &ctx->lcells_cap, live_n * kCell));
   // the live reads' records, compacted in order into the sort's other buffers
   const uint64_t n = ctx->xkeys_n;
-  const int sel = ctx->xkey_sel;
-  uint32_t* lk = ctx->d_xkk[1 - sel];
-  uint64_t* le = ctx->d_xke[1 - sel];
+  uint32_t* lk = ctx->xkey_k_alt;
+  uint64_t* le = ctx->xkey_e_alt;
   MG_TRY(ensure(&ctx->d_xflag, &ctx->xflag_cap, std::max<uint64_t>(n, 1)));
   if (!ctx->d_nlive) MG_TRY(hipMalloc(&ctx->d_nlive, sizeof(unsigned long long)));
   MG_TRY(hipMemsetAsync(ctx->d_nlive, 0, sizeof(unsigned long long), ctx->stream));
   if (n) {
     hipLaunchKernelGGL(k_live_flags, dim3((uint32_t)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, ctx->stream,
-                       ctx->d_xke[sel], n, ctx->d_cbits, ctx->d_xflag);
+                       ctx->xkey_e, n, ctx->d_cbits, ctx->d_xflag);
     MG_TRY(hipGetLastError());
     for (int pass = 0; pass < 2; ++pass) {
       size_t tb = 0;
-      MG_TRY(pass ? hipcub::DeviceSelect::Flagged(nullptr, tb, ctx->d_xke[sel], ctx->d_xflag, le, ctx->d_nlive, (int)n,
+      MG_TRY(pass ? hipcub::DeviceSelect::Flagged(nullptr, tb, ctx->xkey_e, ctx->d_xflag, le, ctx->d_nlive, (int)n,
                                                   ctx->stream)
-                  : hipcub::DeviceSelect::Flagged(nullptr, tb, ctx->d_xkk[sel], ctx->d_xflag, lk, ctx->d_nlive, (int)n,
+                  : hipcub::DeviceSelect::Flagged(nullptr, tb, ctx->xkey_k, ctx->d_xflag, lk, ctx->d_nlive, (int)n,
                                                   ctx->stream));
       if (tb > ctx->xsort_tmp_cap) {
         if (ctx->d_xsort_tmp) MG_TRY(hipFree(ctx->d_xsort_tmp));
@@ -3571,9 +3605,9 @@ int build_live_index_xchg(mg_ctx* ctx) {
         ctx->xsort_tmp_cap = tb;
       }
       tb = ctx->xsort_tmp_cap;
-      MG_TRY(pass ? hipcub::DeviceSelect::Flagged(ctx->d_xsort_tmp, tb, ctx->d_xke[sel], ctx->d_xflag, le, ctx->d_nlive,
+      MG_TRY(pass ? hipcub::DeviceSelect::Flagged(ctx->d_xsort_tmp, tb, ctx->xkey_e, ctx->d_xflag, le, ctx->d_nlive,
                                                   (int)n, ctx->stream)
-                  : hipcub::DeviceSelect::Flagged(ctx->d_xsort_tmp, tb, ctx->d_xkk[sel], ctx->d_xflag, lk, ctx->d_nlive,
+                  : hipcub::DeviceSelect::Flagged(ctx->d_xsort_tmp, tb, ctx->xkey_k, ctx->d_xflag, lk, ctx->d_nlive,
                                                   (int)n, ctx->stream));
     }
   }
@@ -3694,6 +3728,15 @@ static int sort_xruns(mg_ctx* ctx, const ulonglong2* recv, uint64_t slot, uint32
 // 18.4 ms, C5 133.8 vs 123.0 ms (profiles/r04e_ab_xchg_sort_runs.txt).
 static int prepare_xruns(mg_ctx* ctx, const void* recv, uint64_t slot, uint32_t rounds,
                          const unsigned long long* counts) {
+  if (ctx->nranks == 1) {  // one rank: the scan's own run regions, as the fused path probes them
+    ctx->xruns_base = ctx->d_runs;
+    ctx->xruns_cnt = ctx->d_run_cnt;
+    ctx->xruns_reg = ctx->run_cap;
+    ctx->xruns_nreg = ctx->nrun_reg;
+    ctx->xruns_ready = true;
+    return 0;
+  }
+  ctx->xruns_cnt = ctx->d_flat_cnt;
   if (ctx->xchg_sort_runs) {
     if (sort_xruns(ctx, reinterpret_cast<const ulonglong2*>(recv), slot, rounds, counts)) return -1;
     ctx->xruns_base = ctx->d_xv[ctx->xv_sel];
@@ -3705,6 +3748,7 @@ static int prepare_xruns(mg_ctx* ctx, const void* recv, uint64_t slot, uint32_t 
   while (reg > 1 && slot % reg) reg >>= 1;
   const uint64_t nreg = slot ? (uint64_t)rounds * ctx->nranks * (slot / reg) : 0;
   if (slot_regions(ctx, &ctx->d_flat_cnt, &ctx->flat_cnt_cap, counts, slot, reg, nreg)) return -1;
+  ctx->xruns_cnt = ctx->d_flat_cnt;
   ctx->xruns_base = reinterpret_cast<ulonglong2*>(const_cast<void*>(recv));
   ctx->xruns_reg = reg;
   ctx->xruns_nreg = nreg;
@@ -4042,6 +4086,15 @@ int mg_xchg_pack(mg_ctx* ctx, int what, void* dst, uint64_t slot, uint32_t round
   MG_TRY(hipSetDevice(ctx->device));
   if (what < MG_KEYS || what > MG_ROWS || !(ctx->packable & (1 << what)))
     return set_err(ctx, "mg_xchg_pack: nothing of that kind to pack now (call order)");
+  if (ctx->nranks == 1) {
+    // one rank: every stream is its own, so nothing is routed or copied; the
+    // consumers (mg_xchg_insert_keys, mg_xchg_probe) read the context's key
+    // records and run regions, and the rows stay in the context
+    // (mg_num_rows, mg_rows_digest, mg_copy_rows); counts = 0
+    if (!counts) return set_err(ctx, "mg_xchg_pack: null counts");
+    MG_TRY(hipMemsetAsync(counts, 0, sizeof(uint64_t), ctx->stream));
+    return 0;
+  }
   if (!slot || !rounds || !counts || (!dst && !(self_dst && ctx->nranks == 1)))
     return set_err(ctx, "mg_xchg_pack: bad slot geometry");
   auto* cnt = reinterpret_cast<unsigned long long*>(counts);
@@ -4079,51 +4132,68 @@ int mg_xchg_insert_keys(mg_ctx* ctx, const void* recv, uint64_t slot, uint32_t r
   MG_TRY(hipSetDevice(ctx->device));
   if (!ctx->xchg) return set_err(ctx, "mg_xchg_begin must run first");
   const uint32_t P = ctx->nranks;
-  const uint64_t total = (uint64_t)rounds * P * slot;
   uint64_t n = 0;
-  if (total) {
-    if (!recv || !counts) return set_err(ctx, "mg_xchg_insert_keys: null buffer");
-    std::vector<unsigned long long> c(P, 0);
-    MG_TRY(hipMemcpyAsync(c.data(), counts, P * sizeof(unsigned long long), hipMemcpyDeviceToHost, ctx->stream));
-    MG_TRY(hipStreamSynchronize(ctx->stream));
-    for (uint32_t q = 0; q < P; ++q) n += std::min<uint64_t>(c[q], (uint64_t)rounds * slot);  // cut streams: what arrived
-  }
-  if (n > 0x7FFFFFFFull) return set_err(ctx, "exchange: more than 2^31 key records received on one rank");
-  for (int b = 0; b < 2; ++b) {
-    MG_TRY(ensure(&ctx->d_xkk[b], &ctx->xkk_cap[b], std::max<uint64_t>(n, 1)));
-    MG_TRY(ensure(&ctx->d_xke[b], &ctx->xke_cap[b], std::max<uint64_t>(n, 1)));
-  }
-  ctx->xkey_sel = 0;
-  if (n) {
-    const uint32_t grid = (uint32_t)std::min<uint64_t>((total + kBlock - 1) / kBlock, 65536);
-    hipLaunchKernelGGL(k_xkeys_dense, dim3(grid), dim3(kBlock), 0, ctx->stream,
-                       reinterpret_cast<const ulonglong2*>(recv), slot, P, total,
-                       reinterpret_cast<const unsigned long long*>(counts), ctx->cell_lo, ctx->d_xkk[0],
-                       ctx->d_xke[0]);
-    MG_TRY(hipGetLastError());
-    int hb = 0;
-    while (hb < 32 && (1ull << hb) < ctx->cell_n) ++hb;  // bits of a local cell index
-    if (hb > 0 && n > 1) {  // a cell's records consecutive
-      rocprim::double_buffer<uint32_t> keys(ctx->d_xkk[0], ctx->d_xkk[1]);
-      rocprim::double_buffer<uint64_t> vals(ctx->d_xke[0], ctx->d_xke[1]);
-      size_t tb = 0;
-      MG_TRY(rocprim::radix_sort_pairs(nullptr, tb, keys, vals, (unsigned int)n, 0u, (unsigned)hb, ctx->stream));
-      if (tb > ctx->xsort_tmp_cap) {
-        if (ctx->d_xsort_tmp) MG_TRY(hipFree(ctx->d_xsort_tmp));
-        ctx->d_xsort_tmp = nullptr;
-        ctx->xsort_tmp_cap = 0;
-        MG_TRY(hipMalloc(&ctx->d_xsort_tmp, tb));
-        ctx->xsort_tmp_cap = tb;
-      }
-      tb = ctx->xsort_tmp_cap;
-      MG_TRY(rocprim::radix_sort_pairs(ctx->d_xsort_tmp, tb, keys, vals, (unsigned int)n, 0u, (unsigned)hb,
-                                       ctx->stream));
-      ctx->xkey_sel = keys.current() == ctx->d_xkk[0] ? 0 : 1;
+  uint32_t* k0 = nullptr;
+  uint64_t* e0 = nullptr;
+  if (P == 1) {
+    // one rank: its own key records are the input (mg_xchg_pack packed nothing);
+    // without o = 1 keys they are the first three segments (key_seg)
+    n = (ctx->index_o1 ? 4 : 3) * (ctx->xchg_hi - ctx->xchg_lo);
+    k0 = ctx->d_kb;
+    e0 = ctx->d_ke;
+    MG_TRY(ensure(&ctx->d_xkk[1], &ctx->xkk_cap[1], std::max<uint64_t>(n, 1)));
+    MG_TRY(ensure(&ctx->d_xke[1], &ctx->xke_cap[1], std::max<uint64_t>(n, 1)));
+  } else {
+    const uint64_t total = (uint64_t)rounds * P * slot;
+    if (total) {
+      if (!recv || !counts) return set_err(ctx, "mg_xchg_insert_keys: null buffer");
+      std::vector<unsigned long long> c(P, 0);
+      MG_TRY(hipMemcpyAsync(c.data(), counts, P * sizeof(unsigned long long), hipMemcpyDeviceToHost, ctx->stream));
+      MG_TRY(hipStreamSynchronize(ctx->stream));
+      for (uint32_t q = 0; q < P; ++q) n += std::min<uint64_t>(c[q], (uint64_t)rounds * slot);  // cut streams: what arrived
+    }
+    for (int b = 0; b < 2; ++b) {
+      MG_TRY(ensure(&ctx->d_xkk[b], &ctx->xkk_cap[b], std::max<uint64_t>(n, 1)));
+      MG_TRY(ensure(&ctx->d_xke[b], &ctx->xke_cap[b], std::max<uint64_t>(n, 1)));
+    }
+    k0 = ctx->d_xkk[0];
+    e0 = ctx->d_xke[0];
+    if (n) {
+      const uint32_t grid = (uint32_t)std::min<uint64_t>((total + kBlock - 1) / kBlock, 65536);
+      hipLaunchKernelGGL(k_xkeys_dense, dim3(grid), dim3(kBlock), 0, ctx->stream,
+                         reinterpret_cast<const ulonglong2*>(recv), slot, P, total,
+                         reinterpret_cast<const unsigned long long*>(counts), ctx->cell_lo, k0, e0);
+      MG_TRY(hipGetLastError());
     }
   }
+  if (n > 0x7FFFFFFFull) return set_err(ctx, "exchange: more than 2^31 key records on one rank");
+  ctx->xkey_k = k0;
+  ctx->xkey_e = e0;
+  ctx->xkey_k_alt = ctx->d_xkk[1];
+  ctx->xkey_e_alt = ctx->d_xke[1];
+  int hb = 0;
+  while (hb < 32 && (1ull << hb) < ctx->cell_n) ++hb;  // bits of a local cell index
+  if (hb > 0 && n > 1) {  // a cell's records consecutive
+    rocprim::double_buffer<uint32_t> keys(k0, ctx->d_xkk[1]);
+    rocprim::double_buffer<uint64_t> vals(e0, ctx->d_xke[1]);
+    size_t tb = 0;
+    MG_TRY(rocprim::radix_sort_pairs(nullptr, tb, keys, vals, (unsigned int)n, 0u, (unsigned)hb, ctx->stream));
+    if (tb > ctx->xsort_tmp_cap) {
+      if (ctx->d_xsort_tmp) MG_TRY(hipFree(ctx->d_xsort_tmp));
+      ctx->d_xsort_tmp = nullptr;
+      ctx->xsort_tmp_cap = 0;
+      MG_TRY(hipMalloc(&ctx->d_xsort_tmp, tb));
+      ctx->xsort_tmp_cap = tb;
+    }
+    tb = ctx->xsort_tmp_cap;
+    MG_TRY(rocprim::radix_sort_pairs(ctx->d_xsort_tmp, tb, keys, vals, (unsigned int)n, 0u, (unsigned)hb, ctx->stream));
+    ctx->xkey_k = keys.current();
+    ctx->xkey_e = vals.current();
+    ctx->xkey_k_alt = keys.alternate();
+    ctx->xkey_e_alt = vals.alternate();
+  }
   ctx->xkeys_n = n;
-  if (build_cells(ctx, ctx->d_xkk[ctx->xkey_sel], ctx->d_xke[ctx->xkey_sel], nullptr, n, ctx->d_cells, ctx->cell_n, 0))
-    return -1;
+  if (build_cells(ctx, ctx->xkey_k, ctx->xkey_e, nullptr, n, ctx->d_cells, ctx->cell_n, 0)) return -1;
   MG_TRY(hipEventRecord(ctx->ev[1], ctx->stream));
   ctx->index_ready = true;
   return 0;
@@ -4135,7 +4205,7 @@ int mg_xchg_probe(mg_ctx* ctx, int contain, const void* recv, uint64_t slot, uin
   if (!ctx->xchg || !ctx->index_ready) return set_err(ctx, "mg_xchg_insert_keys must run first");
   if (contain && !ctx->superkey) return set_err(ctx, "mg_begin_contained must run first (lengths differ)");
   if (!contain && !ctx->contained_done) return set_err(ctx, "containment must be settled first (mg_finalize_contained)");
-  if ((uint64_t)rounds * slot && (!recv || !counts)) return set_err(ctx, "mg_xchg_probe: null buffer");
+  if (ctx->nranks > 1 && (uint64_t)rounds * slot && (!recv || !counts)) return set_err(ctx, "mg_xchg_probe: null buffer");
   // the first probe of the step sets up the received runs (both probes read them)
   if (!ctx->xruns_ready && prepare_xruns(ctx, recv, slot, rounds, reinterpret_cast<const unsigned long long*>(counts)))
     return -1;
@@ -4165,7 +4235,7 @@ int mg_xchg_probe(mg_ctx* ctx, int contain, const void* recv, uint64_t slot, uin
       // the probe batches live runs only
       const uint32_t grid = (uint32_t)std::min<uint64_t>((nregions + kWavesPerBlock - 1) / kWavesPerBlock,
                                                          (uint64_t)ctx->n_cu * 8);
-      hipLaunchKernelGGL(k_live_runs, dim3(grid), dim3(kBlock), 0, ctx->stream, runs, ctx->d_flat_cnt, reg,
+      hipLaunchKernelGGL(k_live_runs, dim3(grid), dim3(kBlock), 0, ctx->stream, runs, ctx->xruns_cnt, reg,
                          nregions, ctx->d_cbits);
       MG_TRY(hipGetLastError());
       ctx->runs_live = true;

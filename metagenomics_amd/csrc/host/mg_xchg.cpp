@@ -160,6 +160,15 @@ void XchgStep::ensure(Stream& st, int kind) {
 
 void XchgStep::route(int kind) {
   Stream& st = st_[kind];
+  if (x_.world() == 1) {  // one rank: nothing is packed (mg_xchg_pack at P = 1), the consumers read the context
+    if (!st.counts) {
+      hip_check(hipMalloc(&st.counts, sizeof(uint64_t)), "hipMalloc");
+      hip_check(hipMalloc(&st.rcounts, sizeof(uint64_t)), "hipMalloc");
+    }
+    check(mg_xchg_pack(ctx_, kind, nullptr, 1, 1, st.counts, nullptr), "mg_xchg_pack");
+    x_.all_to_all_u64(st.counts, st.rcounts, s_);
+    return;
+  }
   ensure(st, kind);
   check(mg_xchg_pack(ctx_, kind, st.send, st.slot, st.rounds, st.counts, st.recv), "mg_xchg_pack");
   x_.all_to_all_slots(st.send, st.recv, st.slot * mg_record_bytes(kind), st.rounds, s_);
@@ -224,11 +233,16 @@ int XchgStep::run() {
     }
     rows_held_ = 0;
     for (int p = 0; p < P; ++p) rows_held_ += rc[p];
+    if (P == 1) rows_held_ = mg_num_rows(ctx_);  // (the rows stay in the context)
     if (!over) return reruns;
   }
 }
 
 void XchgStep::rows_digest(uint64_t out[4]) {
+  if (x_.world() == 1) {
+    check(mg_rows_digest(ctx_, nullptr, 0, out), "mg_rows_digest");
+    return;
+  }
   const Stream& ws = st_[MG_ROWS];
   check(mg_slots_digest(ctx_, ws.recv, ws.slot, ws.rounds, ws.rcounts, out), "mg_slots_digest");
 }

@@ -71,6 +71,7 @@ def lib() -> C.CDLL:
         "mg_upload_reads_packed": (i32, [vp, vp, vp, u64, u32]),
         "mg_upload_reads_ascii": (i32, [vp, C.c_char_p, vp, u64]),
         "mg_num_reads": (u64, [vp]),
+        "mg_num_rows": (u64, [vp]),
         "mg_download_reads_packed": (i32, [vp, vp, vp, P(u32)]),
         "mg_read_slots": (i32, [vp, vp]),
         "mg_build_index": (i32, [vp, u32, u32]),
@@ -400,6 +401,10 @@ class OverlapEngine:
         got = C.c_uint64()
         self._check(lib().mg_copy_rows(self._h, _ptr(out), n_rows, C.byref(got)), "copy_rows")
         return out[: got.value]
+
+    def num_rows(self) -> int:
+        """Rows held after the last find_overlaps / xchg_probe(0) (mg_num_rows)."""
+        return int(lib().mg_num_rows(self._h))
 
     def copy_rows_to(self, host_ptr: int, cap: int) -> int:
         """mg_copy_rows into caller-owned host memory (e.g. a pinned buffer of cap * 12 bytes)."""

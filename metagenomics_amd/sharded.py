@@ -272,7 +272,14 @@ class ShardResult:
     streams: dict = field(default_factory=dict)
     # long-read fallback (replicated mode): per local rank the rows it holds, on the host
     host_rows: list | None = None
+    # one rank: nothing is routed, the rows stay in the engine (mg_xchg_pack at P = 1)
+    engine_rows: list | None = None
     mode: str = "exchange"
+
+    @property
+    def rows_in_slots(self) -> bool:
+        """The rows are in slot-layout receive buffers (self.rows)."""
+        return self.host_rows is None and self.engine_rows is None
 
     def padding(self, world: int, rank_ids: list) -> dict:
         """Per stream kind: records the slot layout moved between ranks vs the records sent
@@ -295,6 +302,8 @@ class ShardResult:
         """The rows of local rank i, compacted out of the slot layout (host copy)."""
         if self.host_rows is not None:
             return self.host_rows[i]
+        if self.engine_rows is not None:
+            return self.engine_rows[i].rows(self.n_rows[i])
         buf, cnt, slot, rounds = self.rows[i]
         c = cnt.cpu().numpy().astype(np.int64)
         P = len(c)
@@ -387,6 +396,16 @@ def _step(engines, xchg, min_overlap, seed_k, want_super, plan):
     geo = {}
 
     def route(kind):
+        if P == 1:  # one rank: every stream is its own, nothing is packed (counts = 0)
+            cnts = []
+            for e in engines:
+                c = xchg.counts()
+                e.xchg_pack(kind, 0, 1, 1, c.data_ptr(), 0)
+                done()
+                cnts.append(c)
+            sent[kind] = cnts
+            geo[kind] = (0, 0)
+            return [(None, c) for c in cnts], 0, 0
         slot, rounds = plan.geometry(kind, P, ch)
         rb = RECORD_BYTES[kind]
         sends, recvs, cnts = [], [], []
@@ -413,7 +432,7 @@ def _step(engines, xchg, min_overlap, seed_k, want_super, plan):
         # 2. HashTable::insertDataset: key records -> bucket owners -> local cells
         keys, ks, kr = route(MG_KEYS)
         for e, (buf, c) in zip(engines, keys):
-            e.xchg_insert_keys(buf.data_ptr(), ks, kr, c.data_ptr())
+            e.xchg_insert_keys(buf.data_ptr() if buf is not None else 0, ks, kr, c.data_ptr())
             done()
         # 3. runs -> bucket owners (both probes read them)
         runs, rs, rr = route(MG_RUNS)
@@ -429,7 +448,7 @@ def _step(engines, xchg, min_overlap, seed_k, want_super, plan):
             e.begin_contained(sk.data_ptr() if sk is not None else None)
         if contained:
             for e, (buf, c) in zip(engines, runs):
-                e.xchg_probe(True, buf.data_ptr(), rs, rr, c.data_ptr())
+                e.xchg_probe(True, buf.data_ptr() if buf is not None else 0, rs, rr, c.data_ptr())
                 done()
             xchg.allreduce_max(skeys)
         sup = None
@@ -442,17 +461,18 @@ def _step(engines, xchg, min_overlap, seed_k, want_super, plan):
 
         # 5. insertAllEdgesOfRead: probe the received runs -> rows -> src owners
         for e, (buf, c) in zip(engines, runs):
-            e.xchg_probe(False, buf.data_ptr(), rs, rr, c.data_ptr())
+            e.xchg_probe(False, buf.data_ptr() if buf is not None else 0, rs, rr, c.data_ptr())
             done()
         rows, ws, wr = route(MG_ROWS)
         # the step's one host read: MAX over ranks of every per-peer send count
         mx = xchg.max_counts([[sent[k][i] for k in KINDS] for i in range(len(engines))])
-        n_rows = [int(c.sum().item()) for _, c in rows]
+        n_rows = [e.num_rows() for e in engines] if P == 1 else [int(c.sum().item()) for _, c in rows]
         # (the key and run buffers stay referenced until here: with LocalExchange the
         # engines' streams may still read them when a del would let torch reuse the memory)
         del keys, runs
     ms["overlap"] = (time.perf_counter() - t2) * 1e3
     used = {k: int(v) for k, v in zip(KINDS, mx)}
     res = ShardResult(rows=[(b, c, ws, wr) for b, c in rows], ms=ms, contained=contained, super_read_id=sup,
-                      n_rows=n_rows, streams={k: geo[k] + (sent[k],) for k in KINDS})
+                      n_rows=n_rows, streams={k: geo[k] + (sent[k],) for k in KINDS},
+                      engine_rows=list(engines) if P == 1 else None)
     return res, used

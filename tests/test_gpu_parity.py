@@ -339,7 +339,7 @@ def exchange_rows(ds, l, world, k=0, want_super=True, opts=None):
 
 
 @pytest.mark.parametrize("name,world", [("small", 2), ("mixed", 3), ("tandem", 4), ("dirty", 3), ("tworead", 2),
-                                        ("wrapped", 5)])
+                                        ("wrapped", 5), ("mixed", 1), ("highdup", 1)])
 def test_exchange_mode_matches_reference(name, world):
     meta = load_meta(name)
     ds = Dataset.from_files([fixture_input(name)], meta["l"])
