@@ -181,10 +181,6 @@ struct mg_ctx {
   uint64_t* xkey_e = nullptr;
   uint32_t* xkey_k_alt = nullptr;
   uint64_t* xkey_e_alt = nullptr;
-  // group leaders of the cell build (k_cells_fill -> k_cells_chain)
-  uint64_t* d_lead = nullptr;
-  size_t lead_cap = 0;
-  unsigned long long* d_nlead = nullptr;
   // the live records' in-order compaction (build_live_index_xchg)
   uint8_t* d_xflag = nullptr;
   size_t xflag_cap = 0;

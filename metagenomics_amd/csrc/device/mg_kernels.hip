@@ -489,66 +489,46 @@ __global__ __launch_bounds__(kBlock) void k_xkeys_dense(const ulonglong2* __rest
   }
 }
 
-// One plain store per record: its slot is the number of equal keys (>> shift)
-// right before it, from the block's tile of keys in LDS (kCell keys of look-
-// back before the tile, one of look-ahead after it).  The 8th entry of a cell
-// that has more carries the chain flag; the record of rank 8 (the first that
-// does not fit) is a group leader, appended to `lead` for k_cells_chain.
+// number of records equal to key c (>> shift) directly before record i, capped at kCell
+__device__ __forceinline__ int rank_in_cell(const uint32_t* __restrict__ key, uint64_t i, uint32_t shift, uint32_t c) {
+  bool eq[kCell + 1];
+#pragma unroll
+  for (int k = 1; k <= kCell; ++k) eq[k] = i >= (uint64_t)k && (key[i - k] >> shift) == c;
+  int r = 0;
+#pragma unroll
+  for (int k = 1; k <= kCell; ++k) r = (r == k - 1 && eq[k]) ? k : r;
+  return r;
+}
+
 // n_dev non-null: the record count is on the device (a compaction's output).
+// (Appending each group's leader to a list here, for k_cells_chain to visit
+// only those, made this kernel 15x slower -- C3 simulated P = 8: 0.42 vs
+// 0.028 ms per rank, profiles/r04i_sim8_c3_ranks_leader_list_rejected.md --
+// against 0.02 ms saved in the chain kernel.)
 __global__ __launch_bounds__(kBlock) void k_cells_fill(const uint32_t* __restrict__ key,
                                                       const uint64_t* __restrict__ ent,
                                                       const unsigned long long* __restrict__ n_dev, uint64_t n_host,
-                                                      uint32_t shift, uint64_t* __restrict__ cells,
-                                                      uint64_t* __restrict__ lead, unsigned long long* __restrict__ nlead) {
-  __shared__ uint32_t s_key[kCell + kBlock + 1];
+                                                      uint32_t shift, uint64_t* __restrict__ cells) {
   const uint64_t n = n_dev ? *n_dev : n_host;
-  const int lane = threadIdx.x & 63;
-  for (uint64_t i0 = (uint64_t)blockIdx.x * kBlock; i0 < n; i0 += (uint64_t)gridDim.x * kBlock) {
-    // tile [i0 - kCell, i0 + kBlock + 1) of the cell keys; out of range = a key no cell has
-    for (int t = threadIdx.x; t < kCell + kBlock + 1; t += kBlock) {
-      const int64_t j = (int64_t)i0 - kCell + t;
-      s_key[t] = (j >= 0 && (uint64_t)j < n) ? key[j] >> shift : 0xFFFFFFFFu;
+  for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBlock) {
+    const uint32_t c = key[i] >> shift;
+    const int r = rank_in_cell(key, i, shift, c);
+    if (r < kCell) {
+      const bool more = r == kCell - 1 && i + 1 < n && (key[i + 1] >> shift) == c;
+      cells[(uint64_t)c * kCell + r] = more ? (ent[i] | kChain) : ent[i];
     }
-    __syncthreads();
-    const uint64_t i = i0 + threadIdx.x;
-    bool leader = false;
-    if (i < n) {
-      const uint32_t c = s_key[kCell + threadIdx.x];
-      int r = 0;
-#pragma unroll
-      for (int k = 1; k <= kCell; ++k) r = (r == k - 1 && s_key[kCell + threadIdx.x - k] == c) ? k : r;
-      if (r < kCell) {
-        const bool more = r == kCell - 1 && s_key[kCell + threadIdx.x + 1] == c;
-        const uint64_t e = ent[i];
-        cells[(uint64_t)c * kCell + r] = more ? (e | kChain) : e;
-      } else {  // rank >= kCell: the group's leader if the key kCell + 1 back differs
-        const uint32_t back = threadIdx.x ? s_key[threadIdx.x - 1]
-                                          : (i >= kCell + 1 ? key[i - kCell - 1] >> shift : 0xFFFFFFFFu);
-        leader = back != c;
-      }
-    }
-    const uint64_t bal = __ballot(leader);
-    if (bal) {
-      unsigned long long base = 0;
-      if (lane == 0) base = atomicAdd(nlead, (unsigned long long)__popcll(bal));
-      base = __shfl(base, 0);
-      if (leader) lead[base + lane_prefix(bal)] = i;
-    }
-    __syncthreads();
   }
 }
 
-// The 9th+ entries of each cell, one thread per group (its leader: rank 8)
+// the 9th+ entries of each cell, one thread per group (the group's record of rank 8)
 __global__ __launch_bounds__(kBlock) void k_cells_chain(const uint32_t* __restrict__ key,
                                                        const uint64_t* __restrict__ ent,
                                                        const unsigned long long* __restrict__ n_dev, uint64_t n_host,
-                                                       uint32_t shift, uint64_t* cells, uint64_t cell_n,
-                                                       const uint64_t* __restrict__ lead,
-                                                       const unsigned long long* __restrict__ nlead) {
-  const uint64_t n = n_dev ? *n_dev : n_host, nl = *nlead;
-  for (uint64_t g = (uint64_t)blockIdx.x * kBlock + threadIdx.x; g < nl; g += (uint64_t)gridDim.x * kBlock) {
-    const uint64_t i = lead[g];
+                                                       uint32_t shift, uint64_t* cells, uint64_t cell_n) {
+  const uint64_t n = n_dev ? *n_dev : n_host;
+  for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBlock) {
     const uint32_t c = key[i] >> shift;
+    if (rank_in_cell(key, i, shift, c) != kCell || (i >= kCell + 1 && (key[i - kCell - 1] >> shift) == c)) continue;
     uint32_t last_fp = ~0u;
     uint64_t at = c;
     for (uint64_t j = i; j < n && (key[j] >> shift) == c; ++j) {
@@ -556,8 +536,7 @@ __global__ __launch_bounds__(kBlock) void k_cells_chain(const uint32_t* __restri
       const uint32_t fp = entry_fp(e);
       if (fp != last_fp) at = next_cell(c, cell_n, fp);  // the home is full: its chain starts at the next cell
       last_fp = fp;
-      // cell_insert from `at`, leaving `at` at the cell that took the entry (the
-      // group's next entry with this fingerprint resumes there)
+      // cell_insert from `at`, leaving `at` at the cell that took the entry
       for (uint64_t probe = 0; probe < cell_n; ++probe) {
         unsigned long long* cell = reinterpret_cast<unsigned long long*>(cells + at * kCell);
         uint64_t ev[kCell];
@@ -3033,7 +3012,7 @@ void mg_destroy(mg_ctx* ctx) {
   (void)hipStreamSynchronize(ctx->stream);
   void* bufs[] = {ctx->d_words, ctx->d_len, ctx->d_cells, ctx->d_superkey, ctx->d_super, ctx->d_any, ctx->d_rows,
                   ctx->d_seg, ctx->d_stats, ctx->d_compact, ctx->d_runs, ctx->d_run_cnt, ctx->d_blk, ctx->d_flat_cnt,
-                  ctx->d_slot_cnt, ctx->d_freq, ctx->d_kb, ctx->d_ke, ctx->d_key0, ctx->d_xkk[0], ctx->d_xkk[1], ctx->d_xke[0], ctx->d_xke[1], ctx->d_lead, ctx->d_nlead,
+                  ctx->d_slot_cnt, ctx->d_freq, ctx->d_kb, ctx->d_ke, ctx->d_key0, ctx->d_xkk[0], ctx->d_xkk[1], ctx->d_xke[0], ctx->d_xke[1], 
                   ctx->d_xflag, ctx->d_nlive,
                   ctx->d_xk[0], ctx->d_xk[1], ctx->d_xv[0], ctx->d_xv[1], ctx->d_xsort_tmp,
                   ctx->d_digest, ctx->id_store[0], ctx->id_store[1], ctx->phys_store[0], ctx->phys_store[1],
@@ -3544,16 +3523,12 @@ int build_cells(mg_ctx* ctx, const uint32_t* key, const uint64_t* ent, const uns
                 uint64_t n_host, uint64_t* cells, uint64_t cell_n, uint32_t shift) {
   MG_TRY(hipMemsetAsync(cells, 0xFF, cell_n * kCell * sizeof(uint64_t), ctx->stream));  // kEmpty
   if (!n_host) return 0;
-  MG_TRY(ensure(&ctx->d_lead, &ctx->lead_cap, n_host / (kCell + 1) + 1));  // a leader per kCell + 1 records at most
-  if (!ctx->d_nlead) MG_TRY(hipMalloc(&ctx->d_nlead, sizeof(unsigned long long)));
-  MG_TRY(hipMemsetAsync(ctx->d_nlead, 0, sizeof(unsigned long long), ctx->stream));
   const uint32_t grid = (uint32_t)std::max<uint64_t>(
       1, std::min<uint64_t>((n_host + kBlock - 1) / kBlock, (uint64_t)ctx->n_cu * 32));
-  hipLaunchKernelGGL(k_cells_fill, dim3(grid), dim3(kBlock), 0, ctx->stream, key, ent, n_dev, n_host, shift, cells,
-                     ctx->d_lead, ctx->d_nlead);
+  hipLaunchKernelGGL(k_cells_fill, dim3(grid), dim3(kBlock), 0, ctx->stream, key, ent, n_dev, n_host, shift, cells);
   MG_TRY(hipGetLastError());
-  hipLaunchKernelGGL(k_cells_chain, dim3((uint32_t)std::max(1, ctx->n_cu * 4)), dim3(kBlock), 0, ctx->stream, key,
-                     ent, n_dev, n_host, shift, cells, cell_n, ctx->d_lead, ctx->d_nlead);
+  hipLaunchKernelGGL(k_cells_chain, dim3(grid), dim3(kBlock), 0, ctx->stream, key, ent, n_dev, n_host, shift, cells,
+                     cell_n);
   MG_TRY(hipGetLastError());
   return 0;
 }
