@@ -69,6 +69,8 @@ typedef struct mg_counters {
                           walked (option live_index); 0 = the full table */
   /* the last containment pass (markContainedReads), same units */
   uint64_t c_runs, c_entries, c_verified, c_contained;
+  uint64_t deferred;  /* keys the last fused index build found their home cell full for
+                         and placed after the scan (option scan_defer); 0 otherwise */
 } mg_counters;
 
 /* --- context ------------------------------------------------------------ */
@@ -283,9 +285,17 @@ int mg_get_counters(const mg_ctx* ctx, mg_counters* c);
  *                   containment pruning, all exact, default 1;
  *  "probe_share"    a discovery block's 4 wavefronts share its run regions (default 1);
  *  "probe_compact"  sparse run batches are compacted in the probe (default 1);
- *  "live_index"     mixed lengths, one rank: after mg_mark_contained the
- *                   discovery probe walks an index of the uncontained reads'
- *                   keys only (OverlapGraph.cpp:548; exact, default 1);
+ *  "live_index"     mixed lengths: after mg_mark_contained the discovery probe
+ *                   walks an index of the uncontained reads' keys only
+ *                   (OverlapGraph.cpp:548; exact, default 1; the exchange mode
+ *                   coarsens the rank's cells for it); with it, the full index
+ *                   of a mixed-length set holds the o = 0 / 2 keys only;
+ *  "xchg_sort_runs" exchange mode: order the received runs by bucket before
+ *                   the probes (default 0: probed in place, arrival order);
+ *  "xchg_windows"   exchange mode, mixed lengths: the scan takes length-ranked
+ *                   windows of 256 reads (default 1);
+ *  "layout_scratch" 0 = free the layout's double buffers after each layout
+ *                   (many contexts on one device); default 1 keeps them;
  *  "run_cap"        tests: initial run records per scan region (0 = sized from
  *                   the reads; overflowing regions are resized and rescanned);
  *  "phase_limit", "max_blocks"

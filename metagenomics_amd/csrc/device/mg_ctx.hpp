@@ -71,6 +71,10 @@ struct mg_ctx {
   // prefix-containment kernel; getListOfReads then takes a lookup table of all
   // four keys, built on the first lookup after a build (d_lkcells)
   bool index_o1 = true;
+  // the o = 3 keys likewise (fused mixed lengths with k_prefix_contain and the
+  // live discovery index: containment drops o = 1/3 hits, discovery walks the
+  // live table, which has them)
+  bool index_o3 = true;
   uint64_t* d_lkcells = nullptr;
   size_t lkcells_cap = 0;
   bool lookup_ready = false;
@@ -177,6 +181,8 @@ struct mg_ctx {
   uint64_t* d_xke[2] = {nullptr, nullptr};
   size_t xkk_cap[2] = {0, 0}, xke_cap[2] = {0, 0};
   uint64_t xkeys_n = 0;
+  uint32_t xkey_cls = 0;       // 1: key = home cell << 1 | (o == 3) (the full table leaves out o = 3)
+  uint32_t xkey_fs = 0;        // low fingerprint bits below the cell / class bits (chain_par)
   uint32_t* xkey_k = nullptr;  // the sorted records (one of d_xkk[] / d_kb) and the other buffer pair
   uint64_t* xkey_e = nullptr;
   uint32_t* xkey_k_alt = nullptr;
@@ -192,6 +198,28 @@ struct mg_ctx {
   bool xchg_sort_runs = false;  // option "xchg_sort_runs": received runs ordered by bucket before the probes
   bool xchg_windows = true;    // option "xchg_windows": the exchange scan of mixed lengths in length-ranked windows
   bool layout_scratch = true;  // option "layout_scratch" = 0: free the layout's double buffers after each layout
+  // option "chain_par": build_cells places a cell's overflow records in
+  // parallel by their index in their fingerprint's run (k_cells_place; else one
+  // thread per overflowing cell, k_cells_chain); d_rhead / d_rstart: run heads
+  // and their max-scan
+  bool chain_par = true;
+  uint32_t* d_rhead = nullptr;
+  uint32_t* d_rstart = nullptr;
+  size_t rhead_cap = 0, rstart_cap = 0;
+  // option "scan_defer": the fused index scan files each key into its home
+  // cell only and leaves a full home's keys in per-lane overflow lists
+  // ([wave][k][lane], ovf_cap per lane), placed after the scan by one sort and
+  // build_cells instead of a chain walk per key
+  bool scan_defer = false;
+  uint32_t* d_ovf_key = nullptr;
+  uint64_t* d_ovf_ent = nullptr;
+  uint32_t* d_ovf_cnt = nullptr;
+  unsigned long long* d_ovf_off = nullptr;
+  size_t ovf_key_cap = 0, ovf_ent_cap = 0, ovf_cnt_cap = 0, ovf_off_cap = 0;
+  uint32_t ovf_cap = 0;       // records per lane of the last deferred scan
+  uint64_t ovf_lanes = 0;     // its wavefronts x 64 (0: the last scan deferred nothing)
+  uint32_t ovf_fs = 0;        // low fingerprint bits below the home cell in the sort key
+  uint64_t ovf_n = 0;         // deferred records of the last build (counters)
   bool xchg_prefix = false;
   bool key0_ready = false;
   bool prefix_contain = true;  // option "prefix_contain"

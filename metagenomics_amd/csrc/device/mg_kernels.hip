@@ -264,6 +264,36 @@ __device__ __forceinline__ void cell_insert(uint64_t* cells, uint64_t c, uint64_
   }
 }
 
+// cell_insert's first step only (the deferred build, option scan_defer): true
+// when the entry took a slot of its home cell; a full home gets its chain flag
+// and the entry is left to the caller (an overflow list, placed after the scan
+// by build_cells in one sorted pass instead of a walk per entry)
+__device__ __forceinline__ bool cell_insert_home(uint64_t* cells, uint64_t c, unsigned long long entry) {
+  unsigned long long* cell = reinterpret_cast<unsigned long long*>(cells + c * kCell);
+  uint64_t e[kCell];
+  const ulonglong2* cp = reinterpret_cast<const ulonglong2*>(cell);
+#pragma unroll
+  for (int s = 0; s < kCell / 2; ++s) {
+    const ulonglong2 x = cp[s];
+    e[2 * s] = x.x;
+    e[2 * s + 1] = x.y;
+  }
+  bool done = false;
+#pragma unroll
+  for (int s = 0; s < kCell; ++s)
+    if (!done && e[s] == kEmpty) done = atomicCAS(&cell[s], kEmpty, entry) == kEmpty;
+  if (!done && (e[kCell - 1] == kEmpty || !(e[kCell - 1] & kChain)))
+    atomicOr(&cell[kCell - 1], (unsigned long long)kChain);
+  return done;
+}
+
+// cell s steps along the chain of fingerprint fp from c (next_cell applied s
+// times: every step adds the same stride modulo the range)
+__device__ __forceinline__ uint64_t chain_cell(uint64_t c, uint64_t n, uint32_t fp, uint64_t s) {
+  const uint64_t step = (n & (n - 1)) ? 1 : 1 + 2 * (uint64_t)(fp & 1023u);
+  return (c + s * step) % n;
+}
+
 // HashTable::insertDataset (HashTable.cpp:50-80): one thread per key (read r,
 // key o = hashRead's four strings, HashTable.cpp:88-104) finds the key's
 // minimizer and files the entry in its home cell (this rank's buckets only).
@@ -417,6 +447,7 @@ __global__ __launch_bounds__(kBlock) void k_prefix_contain_keys(const uint64_t* 
                                                                 const uint16_t* __restrict__ len,
                                                                 const uint32_t* __restrict__ key,
                                                                 const uint64_t* __restrict__ ent, uint64_t n,
+                                                                uint32_t cshift,
                                                                 const uint64_t* __restrict__ cells, uint64_t cell_n,
                                                                 unsigned long long* __restrict__ superkey,
                                                                 const uint32_t* __restrict__ id) {
@@ -424,7 +455,8 @@ __global__ __launch_bounds__(kBlock) void k_prefix_contain_keys(const uint64_t* 
     const uint64_t e = ent[i];
     const uint32_t hi = (uint32_t)(e >> 32);
     if (hi & 3u) continue;  // o = 0 keys only
-    prefix_contain_walk<MAXW>(words, len, cells, cell_n, key[i], (uint32_t)e, (hi >> 12) & kFpMask, (hi >> 2) & 1023u,
+    prefix_contain_walk<MAXW>(words, len, cells, cell_n, key[i] >> cshift, (uint32_t)e, (hi >> 12) & kFpMask,
+                              (hi >> 2) & 1023u,
                               superkey, id);
   }
 }
@@ -437,7 +469,7 @@ struct LaunchPrefixContainKeys {
     const uint32_t grid = (uint32_t)std::max<uint64_t>(
         1, std::min<uint64_t>((n + kBlock - 1) / kBlock, (uint64_t)ctx->n_cu * 16));
     hipLaunchKernelGGL(k_prefix_contain_keys<W>, dim3(grid), dim3(kBlock), 0, ctx->stream, ctx->d_words, ctx->d_len,
-                       ctx->xkey_k, ctx->xkey_e, n, ctx->d_cells, ctx->cell_n,
+                       ctx->xkey_k, ctx->xkey_e, n, ctx->xkey_cls + ctx->xkey_fs, ctx->d_cells, ctx->cell_n,
                        ctx->superkey, ctx->d_id);
     return hipGetLastError() == hipSuccess ? 0 : -1;
   }
@@ -505,17 +537,25 @@ __device__ __forceinline__ int rank_in_cell(const uint32_t* __restrict__ key, ui
 // only those, made this kernel 15x slower -- C3 simulated P = 8: 0.42 vs
 // 0.028 ms per rank, profiles/r04i_sim8_c3_ranks_leader_list_rejected.md --
 // against 0.02 ms saved in the chain kernel.)
+// Records group by key >> gshift (equal group = one cell's entries) and file
+// into cell key >> cshift; skip_odd: records whose group has bit 0 set (the
+// o = 3 class of a classed key, build_cells) are not filed here.  The bits
+// below gshift hold low fingerprint bits (build_cells: a group's records of one
+// fingerprint adjacent after the sort, for k_cells_place).
 __global__ __launch_bounds__(kBlock) void k_cells_fill(const uint32_t* __restrict__ key,
                                                       const uint64_t* __restrict__ ent,
                                                       const unsigned long long* __restrict__ n_dev, uint64_t n_host,
-                                                      uint32_t shift, uint64_t* __restrict__ cells) {
+                                                      uint32_t gshift, uint32_t cshift, int skip_odd,
+                                                      uint64_t* __restrict__ cells) {
   const uint64_t n = n_dev ? *n_dev : n_host;
   for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBlock) {
-    const uint32_t c = key[i] >> shift;
-    const int r = rank_in_cell(key, i, shift, c);
+    const uint32_t k = key[i];
+    const uint32_t g = k >> gshift;
+    if (skip_odd && (g & 1u)) continue;
+    const int r = rank_in_cell(key, i, gshift, g);
     if (r < kCell) {
-      const bool more = r == kCell - 1 && i + 1 < n && (key[i + 1] >> shift) == c;
-      cells[(uint64_t)c * kCell + r] = more ? (ent[i] | kChain) : ent[i];
+      const bool more = r == kCell - 1 && i + 1 < n && (key[i + 1] >> gshift) == g;
+      cells[(uint64_t)(k >> cshift) * kCell + r] = more ? (ent[i] | kChain) : ent[i];
     }
   }
 }
@@ -524,14 +564,17 @@ __global__ __launch_bounds__(kBlock) void k_cells_fill(const uint32_t* __restric
 __global__ __launch_bounds__(kBlock) void k_cells_chain(const uint32_t* __restrict__ key,
                                                        const uint64_t* __restrict__ ent,
                                                        const unsigned long long* __restrict__ n_dev, uint64_t n_host,
-                                                       uint32_t shift, uint64_t* cells, uint64_t cell_n) {
+                                                       uint32_t gshift, uint32_t cshift, int skip_odd, uint64_t* cells,
+                                                       uint64_t cell_n) {
   const uint64_t n = n_dev ? *n_dev : n_host;
   for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBlock) {
-    const uint32_t c = key[i] >> shift;
-    if (rank_in_cell(key, i, shift, c) != kCell || (i >= kCell + 1 && (key[i - kCell - 1] >> shift) == c)) continue;
+    const uint32_t k = key[i];
+    const uint32_t g = k >> gshift, c = k >> cshift;
+    if (skip_odd && (g & 1u)) continue;
+    if (rank_in_cell(key, i, gshift, g) != kCell || (i >= kCell + 1 && (key[i - kCell - 1] >> gshift) == g)) continue;
     uint32_t last_fp = ~0u;
     uint64_t at = c;
-    for (uint64_t j = i; j < n && (key[j] >> shift) == c; ++j) {
+    for (uint64_t j = i; j < n && (key[j] >> gshift) == g; ++j) {
       const unsigned long long e = ent[j];
       const uint32_t fp = entry_fp(e);
       if (fp != last_fp) at = next_cell(c, cell_n, fp);  // the home is full: its chain starts at the next cell
@@ -556,6 +599,123 @@ __global__ __launch_bounds__(kBlock) void k_cells_chain(const uint32_t* __restri
         at = next_cell(at, cell_n, fp);
       }
     }
+  }
+}
+
+// Chain records placed in parallel (k_over_heads, a max-scan, k_cells_place):
+// an overflow record is one past its home's kCell (all_over: every record, the
+// deferred inserts of the fused scan, whose homes filled during the scan).  A
+// RUN is a group's overflow records of one fingerprint, adjacent after the
+// sort; the run's record of index x goes straight to slot x % kCell of the
+// cell 1 + x / kCell steps along the fingerprint's chain, so a heavy minimizer's
+// hundreds of entries take one CAS each instead of one thread walking them all
+// (k_cells_chain).  A slot already taken (another group's entries crossing the
+// chain, or a run of a second fingerprint on the same chain) sends its record
+// walking on from there, as cell_insert walks.  Chain flags: a run's slot-
+// (kCell - 1) record carries the flag when the run goes on; if that record
+// was displaced, the cell held more than kCell claimants, so one of them
+// walked through it full and set the flag.  Every entry stays reachable from
+// its home along its fingerprint's chain, which is all a walk needs (the order
+// inside a chain is not an output).
+__device__ __forceinline__ bool over_rec(const uint32_t* __restrict__ key, uint64_t i, uint32_t gshift, uint32_t g,
+                                         int all_over, bool* first) {
+  if (all_over) {
+    *first = i == 0 || (key[i - 1] >> gshift) != g;
+    return true;
+  }
+  if (rank_in_cell(key, i, gshift, g) != kCell) return false;
+  *first = !(i >= kCell + 1 && (key[i - kCell - 1] >> gshift) == g);
+  return true;
+}
+
+// head[i] = i at the first record of each run, else 0 (the max-scan then gives
+// every overflow record its run's start)
+__global__ __launch_bounds__(kBlock) void k_over_heads(const uint32_t* __restrict__ key,
+                                                      const uint64_t* __restrict__ ent,
+                                                      const unsigned long long* __restrict__ n_dev, uint64_t n_host,
+                                                      uint32_t gshift, int skip_odd, int all_over,
+                                                      uint32_t* __restrict__ head) {
+  const uint64_t n = n_dev ? *n_dev : n_host;
+  for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBlock) {
+    const uint32_t g = key[i] >> gshift;
+    bool first = false;
+    const bool over = !(skip_odd && (g & 1u)) && over_rec(key, i, gshift, g, all_over, &first);
+    head[i] = (over && (first || entry_fp(ent[i]) != entry_fp(ent[i - 1]))) ? (uint32_t)i : 0u;
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_cells_place(const uint32_t* __restrict__ key,
+                                                       const uint64_t* __restrict__ ent,
+                                                       const uint32_t* __restrict__ start,
+                                                       const unsigned long long* __restrict__ n_dev, uint64_t n_host,
+                                                       uint32_t gshift, uint32_t cshift, int skip_odd, int all_over,
+                                                       uint64_t* cells, uint64_t cell_n) {
+  const uint64_t n = n_dev ? *n_dev : n_host;
+  for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBlock) {
+    const uint32_t k = key[i];
+    const uint32_t g = k >> gshift;
+    bool first = false;
+    if ((skip_odd && (g & 1u)) || !over_rec(key, i, gshift, g, all_over, &first)) continue;
+    const unsigned long long e = ent[i];
+    const uint32_t fp = entry_fp(e);
+    const uint64_t x = i - start[i];  // index in the run
+    const int slot = (int)(x % kCell);
+    const bool more = slot == kCell - 1 && i + 1 < n && (key[i + 1] >> gshift) == g && entry_fp(ent[i + 1]) == fp;
+    uint64_t at = chain_cell(k >> cshift, cell_n, fp, 1 + x / kCell);
+    unsigned long long* cell = reinterpret_cast<unsigned long long*>(cells + at * kCell);
+    if (atomicCAS(&cell[slot], kEmpty, more ? (e | kChain) : e) == kEmpty) continue;
+    // taken: cell_insert from this cell on
+    for (uint64_t probe = 0; probe < cell_n; ++probe) {
+      cell = reinterpret_cast<unsigned long long*>(cells + at * kCell);
+      uint64_t ev[kCell];
+      const ulonglong2* cp = reinterpret_cast<const ulonglong2*>(cell);
+#pragma unroll
+      for (int s2 = 0; s2 < kCell / 2; ++s2) {
+        const ulonglong2 y = cp[s2];
+        ev[2 * s2] = y.x;
+        ev[2 * s2 + 1] = y.y;
+      }
+      bool done = false;
+#pragma unroll
+      for (int s2 = 0; s2 < kCell; ++s2)
+        if (!done && ev[s2] == kEmpty) done = atomicCAS(&cell[s2], kEmpty, e) == kEmpty;
+      if (done) break;
+      if (ev[kCell - 1] == kEmpty || !(ev[kCell - 1] & kChain)) atomicOr(&cell[kCell - 1], (unsigned long long)kChain);
+      at = next_cell(at, cell_n, fp);
+    }
+  }
+}
+
+// Gather the fused scan's deferred inserts (option scan_defer: per lane, records
+// [wave][k][lane], ovf_cnt[wave * 64 + lane] of them) to off[...] onwards, for
+// the sort; one block of 64 threads per wavefront region
+__global__ __launch_bounds__(kWave) void k_ovf_gather(const uint32_t* __restrict__ okey,
+                                                     const uint64_t* __restrict__ oent,
+                                                     const uint32_t* __restrict__ cnt,
+                                                     const unsigned long long* __restrict__ off, uint32_t cap,
+                                                     uint32_t* __restrict__ key, uint64_t* __restrict__ ent) {
+  const uint64_t wv = blockIdx.x, lane = threadIdx.x;
+  const uint32_t c = cnt[wv * kWave + lane];
+  const uint64_t o = off[wv * kWave + lane];
+  for (uint32_t k = 0; k < c; ++k) {
+    const uint64_t at = ((wv * cap + k) << 6) + lane;
+    key[o + k] = okey[at];
+    ent[o + k] = oent[at];
+  }
+}
+
+// Sort keys of the exchange mode's received records: ((home cell << cls | c) <<
+// fs) | the fingerprint's low fs bits.  A classed build (cls = 1) leaves out the
+// o = 3 records from the full table: c = (o == 3), so a cell's o = 0 / 2 records
+// group apart from its o = 3 ones (build_cells, index_o3); the fingerprint bits
+// put a group's records of one fingerprint next to each other (k_cells_place)
+__global__ __launch_bounds__(kBlock) void k_key_class(uint32_t* __restrict__ key, const uint64_t* __restrict__ ent,
+                                                     uint64_t n, uint32_t cls, uint32_t fs) {
+  const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i < n) {
+    const uint64_t e = ent[i];
+    const uint32_t c = (cls && ((uint32_t)(e >> 32) & 3u) == 3u) ? 1u : 0u;
+    key[i] = (((key[i] << cls) | c) << fs) | (entry_fp(e) & ((1u << fs) - 1u));
   }
 }
 
@@ -597,6 +757,16 @@ struct ScanParams {
   // (k_prefix_contain); nullptr: not written
   uint64_t* key0;
   int skip_o1;                    // INDEX: leave out the o = 1 keys (mg_ctx::index_o1)
+  int skip_o3;                    // INDEX (fused): leave out the o = 3 keys (mg_ctx::index_o3)
+  int no_insert;                  // diagnostics (phase_limit = 1): the index scan files no keys (timing only)
+  // INDEX (fused, option scan_defer): a key whose home cell is full goes to its
+  // lane's overflow list, record k of lane l of wavefront gw at (gw ovf_cap +
+  // k) 64 + l, key = home cell << ovf_fs | low fingerprint bits; the lane's
+  // count to ovf_cnt[gw 64 + l] (a full list falls back to the walk)
+  uint32_t* ovf_key;
+  uint64_t* ovf_ent;
+  uint32_t* ovf_cnt;
+  uint32_t ovf_cap, ovf_fs;
 };
 
 // Exchange-mode key records are o-major in the order o = 0, 2, 3, 1: when the
@@ -692,6 +862,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(G > 1 ? 
   const uint64_t nbmask = (1ULL << p.nb_log2) - 1;
   uint64_t cur[G] = {};  // records per region (wavefront-uniform)
   uint32_t nbuf = 0;  // run metas staged in s_buf (wavefront-uniform)
+  uint32_t novf = 0;  // this lane's deferred inserts (ScanParams::ovf_ent)
 
   // close the run of minimizer position pos over windows [jlo, jhi]: stage its
   // meta in LDS (the hashing and the HBM write happen 64 at a time in flush);
@@ -993,8 +1164,20 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(G > 1 ? 
       // measured slower: scan 3.06-3.13 vs 2.92-2.94 ms at C3, profiles/r03y_ab_scan.txt)
       if constexpr (!KEYREC) {
 #pragma unroll
-        for (int o = 0; o < 4; ++o)
-          if (o != 1 || !p.skip_o1) cell_insert(p.cells, cb[o], p.cell_n, ce[o]);
+        for (int o = 0; o < 4; ++o) {
+          if ((o == 1 && p.skip_o1) || (o == 3 && p.skip_o3) || p.no_insert) continue;
+          if (p.ovf_ent) {
+            if (cell_insert_home(p.cells, cb[o], ce[o])) continue;
+            if (novf < p.ovf_cap) {
+              const uint64_t at = (((uint64_t)gw * p.ovf_cap + novf) << 6) + (uint64_t)lane;
+              p.ovf_key[at] = ((uint32_t)cb[o] << p.ovf_fs) | (entry_fp(ce[o]) & ((1u << p.ovf_fs) - 1u));
+              p.ovf_ent[at] = ce[o];
+              ++novf;
+              continue;
+            }
+          }
+          cell_insert(p.cells, cb[o], p.cell_n, ce[o]);
+        }
       }
     } else if (INDEX && a < p.a_hi) {  // no keys (n <= l cannot pass setup_index): holes
       if (p.key0) p.key0[a] = kEmpty;
@@ -1011,6 +1194,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(G > 1 ? 
 #pragma unroll
   for (int j = 1; j < G; ++j) c = lane == j ? cur[j] : c;
   if (lane < G) p.run_cnt[gw * G + lane] = c;
+  if (INDEX && !KEYREC && p.ovf_cnt) p.ovf_cnt[gw * kWave + lane] = novf;
 }
 
 // ---------------------------------------------------------------------------
@@ -2663,6 +2847,17 @@ DiscGeom disc_geom(mg_ctx* ctx, bool contain, uint64_t nsrc) {
 // wavefront in ctx->d_runs.  filter: keep only runs whose bucket this rank owns (a
 // bucket-sharded single context); index: the scan also builds the index
 // (fused: CAS into the cells; exchange: key records).
+// Low fingerprint bits appended below hb bits of cell index in a sort key:
+// the rest of the sort's last 8-bit digit, or one more digit when that leaves
+// fewer than 4 (a cell's records of one fingerprint then sort together,
+// k_cells_place); at most kFpBits, and the key stays within 32 bits
+uint32_t fp_sort_bits(uint32_t hb) {
+  if (hb >= 32) return 0;
+  uint32_t fs = (hb + 7) / 8 * 8 - hb;
+  if (fs < 4 && hb + fs + 8 <= 32) fs += 8;
+  return std::min<uint32_t>(fs, kFpBits);
+}
+
 template <int W>
 struct LaunchScan {
   static int run(mg_ctx* ctx, bool contain, uint64_t a_lo, uint64_t a_hi, uint32_t sgrid, bool filter,
@@ -2718,6 +2913,30 @@ struct LaunchScan {
     sp.cell_n = ctx->cell_n;
     if (index && ctx->key0_ready) sp.key0 = ctx->d_key0;  // mg_build_index allocated it (mixed lengths)
     sp.skip_o1 = (index && !ctx->index_o1) ? 1 : 0;
+    sp.skip_o3 = (index && !ctx->index_o3 && !ctx->xchg) ? 1 : 0;
+    sp.no_insert = (index && ctx->phase_limit == 1) ? 1 : 0;
+    if (index && !ctx->xchg) {
+      ctx->ovf_lanes = 0;
+      if (ctx->scan_defer && !scan_is_reg(ctx, index)) {
+        // per lane at most 4 keys of each read it scans (G per window)
+        const uint64_t cap = 4 * G * ((((ngroups + G - 1) / G) + nw - 1) / nw);
+        const uint64_t lanes = nw * kWave;
+        if (cap <= 0xFFFFFFFFull) {
+          if (ensure(&ctx->d_ovf_key, &ctx->ovf_key_cap, lanes * cap) ||
+              ensure(&ctx->d_ovf_ent, &ctx->ovf_ent_cap, lanes * cap) ||
+              ensure(&ctx->d_ovf_cnt, &ctx->ovf_cnt_cap, lanes))
+            return -1;
+          ctx->ovf_cap = (uint32_t)cap;
+          ctx->ovf_lanes = lanes;
+          ctx->ovf_fs = fp_sort_bits(ctx->nb_log2);
+          sp.ovf_key = ctx->d_ovf_key;
+          sp.ovf_ent = ctx->d_ovf_ent;
+          sp.ovf_cnt = ctx->d_ovf_cnt;
+          sp.ovf_cap = ctx->ovf_cap;
+          sp.ovf_fs = ctx->ovf_fs;
+        }
+      }
+    }
     if (index && ctx->xchg) {  // key records (bucket, entry), o-major: they travel to the bucket owner
       sp.key_bk = ctx->d_kb;
       sp.key_ent = ctx->d_ke;
@@ -2844,7 +3063,7 @@ struct LaunchDiscover {
 // getListOfReads reads all four keys: the lookup table when the index left out o = 1
 IndexParams lookup_params(mg_ctx* ctx) {
   IndexParams p = index_params(ctx);
-  if (!ctx->index_o1 && !long_mode(ctx)) p.cells = ctx->d_lkcells;
+  if ((!ctx->index_o1 || !ctx->index_o3) && !long_mode(ctx)) p.cells = ctx->d_lkcells;
   return p;
 }
 
@@ -3017,7 +3236,8 @@ void mg_destroy(mg_ctx* ctx) {
                   ctx->d_xk[0], ctx->d_xk[1], ctx->d_xv[0], ctx->d_xv[1], ctx->d_xsort_tmp,
                   ctx->d_digest, ctx->id_store[0], ctx->id_store[1], ctx->phys_store[0], ctx->phys_store[1],
                   ctx->d_tmp32, ctx->d_lay_k[0], ctx->d_lay_k[1], ctx->d_lay_v[0], ctx->d_lay_v[1], ctx->d_lay_tmp,
-                  ctx->d_words_alt, ctx->d_len_alt, ctx->d_cbits, ctx->d_ccnt, ctx->d_lcells, ctx->d_lkcells};
+                  ctx->d_words_alt, ctx->d_len_alt, ctx->d_cbits, ctx->d_ccnt, ctx->d_lcells, ctx->d_lkcells,
+                  ctx->d_rhead, ctx->d_rstart, ctx->d_ovf_key, ctx->d_ovf_ent, ctx->d_ovf_cnt, ctx->d_ovf_off};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   for (auto& e : ctx->ev)
@@ -3182,7 +3402,7 @@ int mg_set_option(mg_ctx* ctx, const char* name, int64_t value) {
     ctx->rows_cap_opt = (uint64_t)std::max<int64_t>(0, value);
     return 0;
   }
-  if (!strcmp(name, "phase_limit")) {  // diagnostics: stop the probe after a phase
+  if (!strcmp(name, "phase_limit")) {  // diagnostics: stop the probe after a phase (1: the scan files no keys)
     ctx->phase_limit = value > 0 ? (int)value : 99;
     return 0;
   }
@@ -3200,7 +3420,8 @@ int mg_set_option(mg_ctx* ctx, const char* name, int64_t value) {
       flag("contain_prune", &ctx->contain_prune) || flag("probe_share", &ctx->probe_share) ||
       flag("probe_compact", &ctx->probe_compact) || flag("live_index", &ctx->live_index) ||
       flag("xchg_sort_runs", &ctx->xchg_sort_runs) || flag("layout_scratch", &ctx->layout_scratch) ||
-      flag("xchg_windows", &ctx->xchg_windows))
+      flag("xchg_windows", &ctx->xchg_windows) || flag("chain_par", &ctx->chain_par) ||
+      flag("scan_defer", &ctx->scan_defer))
     return 0;
   if (flag("prefix_contain", &ctx->prefix_contain)) {
     ctx->index_ready = false;
@@ -3492,12 +3713,15 @@ struct LaunchProbeShared {
 // getListOfReads and containment)
 int build_live_index(mg_ctx* ctx) {
   ctx->live_ready = false;
-  if (!ctx->live_index || !ctx->super_any || ctx->nranks > 1 || ctx->xchg || long_mode(ctx)) return 0;
+  // (forced when the full table has no o = 3 keys: discovery needs them)
+  const bool force = !ctx->index_o3;
+  if (!force && (!ctx->live_index || !ctx->super_any || ctx->nranks > 1 || ctx->xchg || long_mode(ctx))) return 0;
   const uint64_t live = ctx->n > ctx->n_contained ? ctx->n - ctx->n_contained : 1;
   uint32_t nbl = 10;  // setup_index's rule for `live` reads
   while (nbl < 31 && (1ull << nbl) < live) nbl++;
   while (nbl < 31 && (1ull << nbl) * kCell < 5 * live) nbl++;
-  if (nbl >= ctx->nb_log2) return 0;  // no smaller than the full table: probe that
+  if (nbl >= ctx->nb_log2 && !force) return 0;  // no smaller than the full table: probe that
+  nbl = std::min(nbl, ctx->nb_log2);
   MG_TRY(ensure(&ctx->d_lcells, &ctx->lcells_cap, (1ull << nbl) * kCell));
   MG_TRY(hipMemsetAsync(ctx->d_lcells, 0xFF, (1ull << nbl) * kCell * sizeof(uint64_t), ctx->stream));
   IndexParams p = index_params(ctx);
@@ -3516,19 +3740,65 @@ int build_live_index(mg_ctx* ctx) {
   return 0;
 }
 
+// the sort / scan scratch of the exchange build and the deferred inserts
+// (d_xsort_tmp), grown to tb bytes
+hipError_t grow_tmp(mg_ctx* ctx, size_t tb) {
+  if (tb > ctx->xsort_tmp_cap) {
+    if (ctx->d_xsort_tmp) {
+      const hipError_t e = hipFree(ctx->d_xsort_tmp);
+      if (e != hipSuccess) return e;
+    }
+    ctx->d_xsort_tmp = nullptr;
+    ctx->xsort_tmp_cap = 0;
+    const hipError_t e = hipMalloc(&ctx->d_xsort_tmp, tb);
+    if (e != hipSuccess) return e;
+    ctx->xsort_tmp_cap = tb;
+  }
+  return hipSuccess;
+}
+
 // the cell table `cells` of cell_n cells from sorted records key / ent (count
 // n_host, or on the device at n_dev <= n_host): clear, one store per record,
-// then the chains of the cells with more than kCell entries (their leaders)
+// then the records past their home's kCell: placed in parallel by their index
+// in their fingerprint's run (option chain_par, k_cells_place), or walked by
+// one thread per overflowing cell (k_cells_chain)
+// gshift / cshift / skip_odd: as k_cells_fill (classed keys: the full table
+// groups and skips by class, the coarse live table merges the classes).
+// all_over: every record overflows a full home (the fused scan's deferred
+// inserts: the table is not cleared, nothing goes to the homes)
 int build_cells(mg_ctx* ctx, const uint32_t* key, const uint64_t* ent, const unsigned long long* n_dev,
-                uint64_t n_host, uint64_t* cells, uint64_t cell_n, uint32_t shift) {
-  MG_TRY(hipMemsetAsync(cells, 0xFF, cell_n * kCell * sizeof(uint64_t), ctx->stream));  // kEmpty
+                uint64_t n_host, uint64_t* cells, uint64_t cell_n, uint32_t gshift, uint32_t cshift, int skip_odd,
+                int all_over) {
+  if (!all_over) MG_TRY(hipMemsetAsync(cells, 0xFF, cell_n * kCell * sizeof(uint64_t), ctx->stream));  // kEmpty
   if (!n_host) return 0;
   const uint32_t grid = (uint32_t)std::max<uint64_t>(
       1, std::min<uint64_t>((n_host + kBlock - 1) / kBlock, (uint64_t)ctx->n_cu * 32));
-  hipLaunchKernelGGL(k_cells_fill, dim3(grid), dim3(kBlock), 0, ctx->stream, key, ent, n_dev, n_host, shift, cells);
+  if (!all_over) {
+    hipLaunchKernelGGL(k_cells_fill, dim3(grid), dim3(kBlock), 0, ctx->stream, key, ent, n_dev, n_host, gshift,
+                       cshift, skip_odd, cells);
+    MG_TRY(hipGetLastError());
+  }
+  if (!ctx->chain_par && !all_over) {
+    hipLaunchKernelGGL(k_cells_chain, dim3(grid), dim3(kBlock), 0, ctx->stream, key, ent, n_dev, n_host, gshift,
+                       cshift, skip_odd, cells, cell_n);
+    MG_TRY(hipGetLastError());
+    return 0;
+  }
+  if (n_host > 0xFFFFFFFFull) return set_err(ctx, "cell build: more than 2^32 records");
+  MG_TRY(ensure(&ctx->d_rhead, &ctx->rhead_cap, n_host));
+  MG_TRY(ensure(&ctx->d_rstart, &ctx->rstart_cap, n_host));
+  hipLaunchKernelGGL(k_over_heads, dim3(grid), dim3(kBlock), 0, ctx->stream, key, ent, n_dev, n_host, gshift, skip_odd,
+                     all_over, ctx->d_rhead);
   MG_TRY(hipGetLastError());
-  hipLaunchKernelGGL(k_cells_chain, dim3(grid), dim3(kBlock), 0, ctx->stream, key, ent, n_dev, n_host, shift, cells,
-                     cell_n);
+  size_t tb = 0;
+  MG_TRY(rocprim::inclusive_scan(nullptr, tb, ctx->d_rhead, ctx->d_rstart, (size_t)n_host,
+                                 rocprim::maximum<uint32_t>(), ctx->stream));
+  MG_TRY(grow_tmp(ctx, tb));
+  tb = ctx->xsort_tmp_cap;
+  MG_TRY(rocprim::inclusive_scan(ctx->d_xsort_tmp, tb, ctx->d_rhead, ctx->d_rstart, (size_t)n_host,
+                                 rocprim::maximum<uint32_t>(), ctx->stream));
+  hipLaunchKernelGGL(k_cells_place, dim3(grid), dim3(kBlock), 0, ctx->stream, key, ent, ctx->d_rstart, n_dev, n_host,
+                     gshift, cshift, skip_odd, all_over, cells, cell_n);
   MG_TRY(hipGetLastError());
   return 0;
 }
@@ -3545,14 +3815,15 @@ int build_cells(mg_ctx* ctx, const uint32_t* key, const uint64_t* ent, const uns
 int build_live_index_xchg(mg_ctx* ctx) {
   ctx->live_ready = false;
   ctx->live_coarse = false;
-  if (!ctx->live_index || !ctx->super_any || !ctx->cell_n) return 0;
+  const bool force = !ctx->index_o3;  // (discovery needs the o = 3 keys the full table left out)
+  if (!ctx->cell_n || (!force && (!ctx->live_index || !ctx->super_any))) return 0;
   const double frac = (double)ctx->cell_n / (double)(1ull << ctx->nb_log2);
   const uint64_t live_reads = ctx->n > ctx->n_contained ? ctx->n - ctx->n_contained : 1;
   const uint64_t live_local = (uint64_t)((double)live_reads * frac) + 1;
   uint32_t sft = 0;
   while (sft < 24 && (ctx->cell_n >> (sft + 1)) >= live_local && (ctx->cell_n >> (sft + 1)) * kCell >= 5 * live_local)
     ++sft;
-  if (!sft) return 0;  // no smaller than the full table: probe that
+  if (!sft && !force) return 0;  // no smaller than the full table: probe that
   const uint64_t live_n = (ctx->cell_n + (1ull << sft) - 1) >> sft;
   MG_TRY(ensure(&ctx->d_lcells, &ctx->lcells_cap, live_n * kCell));
   // the live reads' records, compacted in order into the sort's other buffers
@@ -3572,13 +3843,7 @@ int build_live_index_xchg(mg_ctx* ctx) {
                                                   ctx->stream)
                   : hipcub::DeviceSelect::Flagged(nullptr, tb, ctx->xkey_k, ctx->d_xflag, lk, ctx->d_nlive, (int)n,
                                                   ctx->stream));
-      if (tb > ctx->xsort_tmp_cap) {
-        if (ctx->d_xsort_tmp) MG_TRY(hipFree(ctx->d_xsort_tmp));
-        ctx->d_xsort_tmp = nullptr;
-        ctx->xsort_tmp_cap = 0;
-        MG_TRY(hipMalloc(&ctx->d_xsort_tmp, tb));
-        ctx->xsort_tmp_cap = tb;
-      }
+      MG_TRY(grow_tmp(ctx, tb));
       tb = ctx->xsort_tmp_cap;
       MG_TRY(pass ? hipcub::DeviceSelect::Flagged(ctx->d_xsort_tmp, tb, ctx->xkey_e, ctx->d_xflag, le, ctx->d_nlive,
                                                   (int)n, ctx->stream)
@@ -3586,7 +3851,8 @@ int build_live_index_xchg(mg_ctx* ctx) {
                                                   (int)n, ctx->stream));
     }
   }
-  if (build_cells(ctx, lk, le, ctx->d_nlive, n, ctx->d_lcells, live_n, sft)) return -1;
+  const uint32_t lsh = sft + ctx->xkey_cls + ctx->xkey_fs;  // (classes merged)
+  if (build_cells(ctx, lk, le, ctx->d_nlive, n, ctx->d_lcells, live_n, lsh, lsh, 0, 0)) return -1;
   ctx->live_shift = sft;
   ctx->live_cells = live_n;
   ctx->live_coarse = true;
@@ -3837,6 +4103,50 @@ int ensure_layout_range(mg_ctx* ctx) {
 
 extern "C" {
 
+// The fused scan's deferred inserts (option scan_defer): gather the per-lane
+// overflow lists, sort them by (home cell, low fingerprint bits) and place them
+// along their chains (build_cells, every record past a full home)
+int place_deferred(mg_ctx* ctx) {
+  ctx->ovf_n = 0;
+  ctx->counters.deferred = 0;
+  const uint64_t L = ctx->ovf_lanes;
+  if (!L) return 0;
+  MG_TRY(ensure(&ctx->d_ovf_off, &ctx->ovf_off_cap, L + 1));
+  MG_TRY(hipMemsetAsync(ctx->d_ovf_off, 0, sizeof(unsigned long long), ctx->stream));
+  size_t tb = 0;
+  MG_TRY(rocprim::inclusive_scan(nullptr, tb, ctx->d_ovf_cnt, ctx->d_ovf_off + 1, (size_t)L,
+                                 rocprim::plus<unsigned long long>(), ctx->stream));
+  MG_TRY(grow_tmp(ctx, tb));
+  tb = ctx->xsort_tmp_cap;
+  MG_TRY(rocprim::inclusive_scan(ctx->d_xsort_tmp, tb, ctx->d_ovf_cnt, ctx->d_ovf_off + 1, (size_t)L,
+                                 rocprim::plus<unsigned long long>(), ctx->stream));
+  unsigned long long total = 0;
+  MG_TRY(hipMemcpyAsync(&total, ctx->d_ovf_off + L, sizeof(total), hipMemcpyDeviceToHost, ctx->stream));
+  MG_TRY(hipStreamSynchronize(ctx->stream));
+  ctx->ovf_n = total;
+  ctx->counters.deferred = total;
+  if (!total) return 0;
+  if (total > 0xFFFFFFFFull) return set_err(ctx, "deferred inserts: more than 2^32 records");
+  for (int b = 0; b < 2; ++b) {
+    MG_TRY(ensure(&ctx->d_xkk[b], &ctx->xkk_cap[b], total));
+    MG_TRY(ensure(&ctx->d_xke[b], &ctx->xke_cap[b], total));
+  }
+  hipLaunchKernelGGL(k_ovf_gather, dim3((uint32_t)(L / kWave)), dim3(kWave), 0, ctx->stream, ctx->d_ovf_key,
+                     ctx->d_ovf_ent, ctx->d_ovf_cnt, ctx->d_ovf_off, ctx->ovf_cap, ctx->d_xkk[0], ctx->d_xke[0]);
+  MG_TRY(hipGetLastError());
+  const uint32_t fs = ctx->ovf_fs, bits = ctx->nb_log2 + fs;
+  rocprim::double_buffer<uint32_t> keys(ctx->d_xkk[0], ctx->d_xkk[1]);
+  rocprim::double_buffer<uint64_t> vals(ctx->d_xke[0], ctx->d_xke[1]);
+  if (total > 1) {
+    tb = 0;
+    MG_TRY(rocprim::radix_sort_pairs(nullptr, tb, keys, vals, (unsigned int)total, 0u, bits, ctx->stream));
+    MG_TRY(grow_tmp(ctx, tb));
+    tb = ctx->xsort_tmp_cap;
+    MG_TRY(rocprim::radix_sort_pairs(ctx->d_xsort_tmp, tb, keys, vals, (unsigned int)total, 0u, bits, ctx->stream));
+  }
+  return build_cells(ctx, keys.current(), vals.current(), nullptr, total, ctx->d_cells, ctx->cell_n, fs, fs, 0, 1);
+}
+
 int mg_build_index(mg_ctx* ctx, uint32_t min_overlap, uint32_t seed_k) {
   if (!ctx) return -1;
   MG_TRY(hipSetDevice(ctx->device));
@@ -3850,6 +4160,7 @@ int mg_build_index(mg_ctx* ctx, uint32_t min_overlap, uint32_t seed_k) {
   ctx->t.sort_ms = 0.f;
   ctx->shared_scan_ms = 0.f;
   const bool mixed = ctx->minlen != ctx->maxlen;
+  ctx->index_o3 = true;
   if (long_mode(ctx)) {  // reads > 1024 bp: k_index_long, one thread per key
     ctx->index_o1 = true;
     if (ctx->nranks > 1) return set_err(ctx, "reads longer than 1024 bp: bucket-sharded index not supported");
@@ -3863,9 +4174,14 @@ int mg_build_index(mg_ctx* ctx, uint32_t min_overlap, uint32_t seed_k) {
     ctx->key0_ready = mixed && ctx->prefix_contain;
     // o = 1 keys: only the containment probe without k_prefix_contain reads them
     ctx->index_o1 = mixed && !ctx->key0_ready;
+    // o = 3 keys: with k_prefix_contain the containment probe drops them, and
+    // the discovery probe then walks the live reads' table (always built,
+    // build_live_index), so this table holds o = 0 / 2 only
+    ctx->index_o3 = !(ctx->key0_ready && ctx->live_index);
     if (ctx->key0_ready) MG_TRY(ensure(&ctx->d_key0, &ctx->key0_cap, ctx->n + 1));
     if (ctx->n && dispatch_w<LaunchScanAll>(ctx->maxw, ctx, ctx->stream))
       return set_err(ctx, "index build launch failed");
+    if (ctx->n && place_deferred(ctx)) return -1;
     if (!ctx->n) ctx->nrun_reg = 0;
     ctx->scan_state = 1;
   } else {  // the whole index for a source-range shard (its containment probe reads suffix-key hits)
@@ -4028,6 +4344,9 @@ int mg_xchg_begin(mg_ctx* ctx, uint32_t min_overlap, uint32_t seed_k) {
   ctx->xruns_ready = false;
   ctx->xchg_prefix = ctx->minlen != ctx->maxlen && ctx->prefix_contain;
   ctx->index_o1 = ctx->minlen != ctx->maxlen && !ctx->xchg_prefix;  // (key records of o = 1: holes otherwise)
+  // the full table leaves out o = 3 as the fused path does (containment drops
+  // them; discovery walks the coarse live table, built from all received records)
+  ctx->index_o3 = !(ctx->xchg_prefix && ctx->live_index);
   uint64_t lo, hi;
   source_range(ctx, &lo, &hi);
   ctx->xchg_lo = lo;
@@ -4148,18 +4467,26 @@ int mg_xchg_insert_keys(mg_ctx* ctx, const void* recv, uint64_t slot, uint32_t r
   ctx->xkey_e_alt = ctx->d_xke[1];
   int hb = 0;
   while (hb < 32 && (1ull << hb) < ctx->cell_n) ++hb;  // bits of a local cell index
+  ctx->xkey_cls = (!ctx->index_o3 && hb < 31) ? 1 : 0;
+  if (!ctx->index_o3 && !ctx->xkey_cls) return set_err(ctx, "exchange: local cell index too wide for the o = 3 class bit");
+  hb += (int)ctx->xkey_cls;
+  // low fingerprint bits below the cell (chain_par: a group's records of one
+  // fingerprint adjacent), filling the sort's last 8-bit digit, or one more
+  // digit when that leaves fewer than 4
+  const uint32_t fs = ctx->chain_par ? fp_sort_bits((uint32_t)hb) : 0u;
+  ctx->xkey_fs = fs;
+  if ((ctx->xkey_cls || fs) && n) {
+    hipLaunchKernelGGL(k_key_class, dim3((uint32_t)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, ctx->stream, k0, e0,
+                       n, ctx->xkey_cls, fs);
+    MG_TRY(hipGetLastError());
+  }
+  hb += (int)fs;
   if (hb > 0 && n > 1) {  // a cell's records consecutive
     rocprim::double_buffer<uint32_t> keys(k0, ctx->d_xkk[1]);
     rocprim::double_buffer<uint64_t> vals(e0, ctx->d_xke[1]);
     size_t tb = 0;
     MG_TRY(rocprim::radix_sort_pairs(nullptr, tb, keys, vals, (unsigned int)n, 0u, (unsigned)hb, ctx->stream));
-    if (tb > ctx->xsort_tmp_cap) {
-      if (ctx->d_xsort_tmp) MG_TRY(hipFree(ctx->d_xsort_tmp));
-      ctx->d_xsort_tmp = nullptr;
-      ctx->xsort_tmp_cap = 0;
-      MG_TRY(hipMalloc(&ctx->d_xsort_tmp, tb));
-      ctx->xsort_tmp_cap = tb;
-    }
+    MG_TRY(grow_tmp(ctx, tb));
     tb = ctx->xsort_tmp_cap;
     MG_TRY(rocprim::radix_sort_pairs(ctx->d_xsort_tmp, tb, keys, vals, (unsigned int)n, 0u, (unsigned)hb, ctx->stream));
     ctx->xkey_k = keys.current();
@@ -4168,7 +4495,9 @@ int mg_xchg_insert_keys(mg_ctx* ctx, const void* recv, uint64_t slot, uint32_t r
     ctx->xkey_e_alt = vals.alternate();
   }
   ctx->xkeys_n = n;
-  if (build_cells(ctx, ctx->xkey_k, ctx->xkey_e, nullptr, n, ctx->d_cells, ctx->cell_n, 0)) return -1;
+  if (build_cells(ctx, ctx->xkey_k, ctx->xkey_e, nullptr, n, ctx->d_cells, ctx->cell_n, fs, fs + ctx->xkey_cls,
+                  ctx->xkey_cls, 0))
+    return -1;
   MG_TRY(hipEventRecord(ctx->ev[1], ctx->stream));
   ctx->index_ready = true;
   return 0;
@@ -4203,7 +4532,8 @@ int mg_xchg_probe(mg_ctx* ctx, int contain, const void* recv, uint64_t slot, uin
   for (int attempt = 0;; ++attempt) {
     if (attempt == 3) return set_err(ctx, "row buffers overflow after resize");
     MG_TRY(hipEventRecord(ctx->ev[4], ctx->stream));
-    if (attempt == 0 && ctx->contained_done && ctx->super_any && build_live_index_xchg(ctx)) return -1;
+    if (attempt == 0 && ctx->contained_done && (ctx->super_any || !ctx->index_o3) && build_live_index_xchg(ctx))
+      return -1;
     if (attempt == 0 && nregions && ctx->contained_done && ctx->super_any) {
       // runs of contained sources contribute nothing (:548): drop them from the
       // run regions in place (the containment probe has read them already), so
@@ -4333,7 +4663,7 @@ int mg_lookup_key(mg_ctx* ctx, const char* key, uint32_t key_len, uint64_t* out,
   if (n_out) *n_out = 0;
   if (key_len != ctx->h) return 0;  // no key of another length exists
   if (ctx->nranks > 1) return set_err(ctx, "lookup on a bucket-sharded index");
-  if (!ctx->index_o1 && !long_mode(ctx) && !ctx->lookup_ready) {
+  if ((!ctx->index_o1 || !ctx->index_o3) && !long_mode(ctx) && !ctx->lookup_ready) {
     // the step's index has no o = 1 keys: file all four once into the lookup table
     MG_TRY(ensure(&ctx->d_lkcells, &ctx->lkcells_cap, ctx->cell_n * kCell));
     MG_TRY(hipMemsetAsync(ctx->d_lkcells, 0xFF, ctx->cell_n * kCell * sizeof(uint64_t), ctx->stream));

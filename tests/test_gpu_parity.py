@@ -362,15 +362,21 @@ def test_exchange_mode_containment_paths(prefix):
 
 @pytest.mark.parametrize("name,world,opts", [
     ("mixed", 3, {"nb_log2": 16}), ("dirty", 4, {"nb_log2": 16}), ("branchy", 2, {"nb_log2": 16}),
-    ("mixed", 4, {"nb_log2": 16, "live_index": 0}), ("mixed", 3, {"xchg_sort_runs": 0}),
-    ("tandem", 4, {"xchg_sort_runs": 0}), ("highdup", 8, {"nb_log2": 16, "xchg_sort_runs": 0})])
+    ("mixed", 4, {"nb_log2": 16, "live_index": 0}), ("mixed", 3, {"xchg_sort_runs": 1}),
+    ("tandem", 4, {"xchg_sort_runs": 1}), ("highdup", 8, {"nb_log2": 16, "xchg_sort_runs": 1}),
+    ("mixed", 3, {"xchg_windows": 0}), ("dirty", 2, {"xchg_windows": 0, "prefix_contain": 0}),
+    ("highdup", 4, {"nb_log2": 16, "chain_par": 0}), ("mixed", 3, {"chain_par": 0}),
+    ("highdup", 2, {"nb_log2": 10}), ("tandem", 3, {"nb_log2": 10})])
 def test_exchange_mode_options(name, world, opts):
     """Exchange-mode variants against the reference: the discovery index of the
     uncontained reads (build_live_index_xchg: the rank's cells coarsened, live
     entries only; forced on the small fixtures by a large directory, and its
     use checked through counters().live_cells), the full table instead
-    (live_index = 0), and the received runs probed in arrival order
-    (xchg_sort_runs = 0)."""
+    (live_index = 0, the full table then keeps the o = 3 keys), the received
+    runs ordered by bucket (xchg_sort_runs = 1; default: probed in place), the
+    register scan for mixed lengths (xchg_windows = 0), the overflow records
+    walked by one thread per cell instead of placed in parallel (chain_par = 0),
+    and small directories whose chains run long (nb_log2 = 10)."""
     meta = load_meta(name)
     ds = Dataset.from_files([fixture_input(name)], meta["l"])
     rows, sup = exchange_rows(ds, meta["l"], world, opts=dict(opts, stats=1))
@@ -379,7 +385,7 @@ def test_exchange_mode_options(name, world, opts):
     live = [c["live_cells"] for c in exchange_rows.counters]
     if meta["super"] and opts.get("live_index", 1) and opts.get("nb_log2"):
         assert all(0 < x < (1 << 16) // world + 1 for x in live), live
-    elif not opts.get("live_index", 1) or not meta["super"]:
+    elif not opts.get("live_index", 1):
         assert not any(live), live
 
 
@@ -772,6 +778,41 @@ def test_live_index_forced(name):
         assert (cells > 0) == bool(live) and cells < (1 << 16), (live, cells)
         assert {str(i): int(x) for i, x in enumerate(sup) if x} == want_sup, live
         assert np.array_equal(rows_to_tuples(rows), want_rows), live
+
+
+@pytest.mark.parametrize("name", ["small", "mixed", "tandem", "highdup", "dirty", "branchy", "metagenome"])
+def test_deferred_index_build(name):
+    """Option scan_defer: the fused scan files each key into its home cell only;
+    the keys of full homes wait in per-lane lists and are sorted and placed along
+    their fingerprints' chains after the scan (place_deferred, k_cells_place).
+    Rows and superReadIDs equal the goldens on the default directory and on the
+    smallest one the load bound allows (nb_log2 = 10: long chains, runs of
+    several fingerprints crossing), counters().deferred shows the path ran,
+    and the lookups read the deferred table too."""
+    if name == "metagenome":
+        c, L = synth.metagenome_read_set(20000, 100, 250, n_genomes=20, total_len=400000, seed=51)
+        seqs, l = synth.codes_to_strings(c, L), 50
+        ds = Dataset.from_strings(seqs, l)
+        orows, osup, _, _ = OracleDataset.from_strings(seqs, l).overlaps(l)
+        want_rows, want_sup, lookups = sorted_tuples(orows), {str(i): int(x) for i, x in enumerate(osup) if x}, {}
+    else:
+        meta = load_meta(name)
+        l = meta["l"]
+        ds = Dataset.from_files([fixture_input(name)], l)
+        want_rows, want_sup, lookups = golden_rows(name), meta["super"], meta.get("lookups", {})
+    for nb in (0, 10):
+        e = OverlapEngine(0)
+        e.set_option("scan_defer", 1)
+        e.set_option("stats", 1)
+        rows, sup = gpu_rows(e, ds, l, nb_log2=nb)
+        deferred = e.counters()["deferred"]
+        assert {str(i): int(x) for i, x in enumerate(sup) if x} == want_sup, nb
+        assert np.array_equal(rows_to_tuples(rows), want_rows), nb
+        for key, exp in lookups.items():
+            assert [list(x) for x in e.lookup(key)] == exp, (nb, key)
+        e.close()
+        if nb == 10 and name in ("highdup", "tandem", "metagenome"):
+            assert deferred > 0, (name, nb)
 
 
 @pytest.mark.parametrize("name", ["small", "mixed", "tandem", "highdup", "tworead"])

@@ -41,6 +41,9 @@ for s in $STEPS; do
   newtests)
     timeout -k 10 900 python -u -m pytest tests/test_gpu_parity.py tests/test_long_reads.py -x -v -m gpu -k "exchange or live_index or falls_back" --timeout 300 --timeout-method thread > $OUT/new_tests.log 2>&1
     rc=$?; echo "new tests rc=$rc"; grep -E "PASS|FAIL|Error" $OUT/new_tests.log | tail -40 ;;
+  defer)
+    timeout -k 10 1100 python -u -m pytest tests/test_gpu_parity.py tests/test_scale_digest.py -x -v -m gpu -k "deferred or exchange_mode_options" --timeout 900 --timeout-method thread > $OUT/defer_tests.log 2>&1
+    rc=$?; echo "deferred-build tests rc=$rc"; grep -E "PASS|FAIL|SKIP|Error" $OUT/defer_tests.log | tail -30 ;;
   xdigest)
     timeout -k 10 1100 python -u -m pytest tests/test_scale_digest.py -x -v -m gpu -k "exchange_scale" --timeout 1000 --timeout-method thread > $OUT/xdigest_tests.log 2>&1
     rc=$?; echo "exchange digest tests rc=$rc"; grep -E "PASS|FAIL|SKIP|Error" $OUT/xdigest_tests.log | tail -12 ;;
@@ -91,6 +94,9 @@ for s in $STEPS; do
   parse)
     timeout -k 10 900 python -u tools/parse_bench.py > $OUT/parse_bench.json 2> $OUT/parse_bench.err
     rc=$?; echo "parse rc=$rc"; tail -12 $OUT/parse_bench.err; cat $OUT/parse_bench.json ;;
+  sweep)
+    timeout -k 10 600 python -u tools/variant_sweep.py > $OUT/sweep_${MG_SWEEP_CONFIG:-c3}.log 2>&1
+    rc=$?; echo "sweep rc=$rc"; grep opts $OUT/sweep_${MG_SWEEP_CONFIG:-c3}.log ;;
   variants)
     timeout -k 10 400 python -u tools/variant_sweep.py > $OUT/variant_sweep.log 2>&1
     rc=$?; echo "variants rc=$rc"; grep opts $OUT/variant_sweep.log ;;
