@@ -3977,9 +3977,9 @@ static int prepare_xruns(mg_ctx* ctx, const void* recv, uint64_t slot, uint32_t 
     ctx->xruns_ready = true;
     return 0;
   }
-  ctx->xruns_cnt = ctx->d_flat_cnt;
   if (ctx->xchg_sort_runs) {
     if (sort_xruns(ctx, reinterpret_cast<const ulonglong2*>(recv), slot, rounds, counts)) return -1;
+    ctx->xruns_cnt = ctx->d_flat_cnt;  // (after sort_xruns: it may have grown the counts)
     ctx->xruns_base = ctx->d_xv[ctx->xv_sel];
     ctx->xruns_reg = kXRegion;
     ctx->xruns_nreg = (ctx->xruns_n + kXRegion - 1) / kXRegion;
