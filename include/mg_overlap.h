@@ -69,8 +69,6 @@ typedef struct mg_counters {
                           walked (option live_index); 0 = the full table */
   /* the last containment pass (markContainedReads), same units */
   uint64_t c_runs, c_entries, c_verified, c_contained;
-  uint64_t deferred;  /* keys the last fused index build found their home cell full for
-                         and placed after the scan (option scan_defer); 0 otherwise */
 } mg_counters;
 
 /* --- context ------------------------------------------------------------ */

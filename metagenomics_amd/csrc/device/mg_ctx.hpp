@@ -206,20 +206,6 @@ struct mg_ctx {
   uint32_t* d_rhead = nullptr;
   uint32_t* d_rstart = nullptr;
   size_t rhead_cap = 0, rstart_cap = 0;
-  // option "scan_defer": the fused index scan files each key into its home
-  // cell only and leaves a full home's keys in per-lane overflow lists
-  // ([wave][k][lane], ovf_cap per lane), placed after the scan by one sort and
-  // build_cells instead of a chain walk per key
-  bool scan_defer = false;
-  uint32_t* d_ovf_key = nullptr;
-  uint64_t* d_ovf_ent = nullptr;
-  uint32_t* d_ovf_cnt = nullptr;
-  unsigned long long* d_ovf_off = nullptr;
-  size_t ovf_key_cap = 0, ovf_ent_cap = 0, ovf_cnt_cap = 0, ovf_off_cap = 0;
-  uint32_t ovf_cap = 0;       // records per lane of the last deferred scan
-  uint64_t ovf_lanes = 0;     // its wavefronts x 64 (0: the last scan deferred nothing)
-  uint32_t ovf_fs = 0;        // low fingerprint bits below the home cell in the sort key
-  uint64_t ovf_n = 0;         // deferred records of the last build (counters)
   bool xchg_prefix = false;
   bool key0_ready = false;
   bool prefix_contain = true;  // option "prefix_contain"

@@ -264,29 +264,6 @@ __device__ __forceinline__ void cell_insert(uint64_t* cells, uint64_t c, uint64_
   }
 }
 
-// cell_insert's first step only (the deferred build, option scan_defer): true
-// when the entry took a slot of its home cell; a full home gets its chain flag
-// and the entry is left to the caller (an overflow list, placed after the scan
-// by build_cells in one sorted pass instead of a walk per entry)
-__device__ __forceinline__ bool cell_insert_home(uint64_t* cells, uint64_t c, unsigned long long entry) {
-  unsigned long long* cell = reinterpret_cast<unsigned long long*>(cells + c * kCell);
-  uint64_t e[kCell];
-  const ulonglong2* cp = reinterpret_cast<const ulonglong2*>(cell);
-#pragma unroll
-  for (int s = 0; s < kCell / 2; ++s) {
-    const ulonglong2 x = cp[s];
-    e[2 * s] = x.x;
-    e[2 * s + 1] = x.y;
-  }
-  bool done = false;
-#pragma unroll
-  for (int s = 0; s < kCell; ++s)
-    if (!done && e[s] == kEmpty) done = atomicCAS(&cell[s], kEmpty, entry) == kEmpty;
-  if (!done && (e[kCell - 1] == kEmpty || !(e[kCell - 1] & kChain)))
-    atomicOr(&cell[kCell - 1], (unsigned long long)kChain);
-  return done;
-}
-
 // cell s steps along the chain of fingerprint fp from c (next_cell applied s
 // times: every step adds the same stride modulo the range)
 __device__ __forceinline__ uint64_t chain_cell(uint64_t c, uint64_t n, uint32_t fp, uint64_t s) {
@@ -603,8 +580,7 @@ __global__ __launch_bounds__(kBlock) void k_cells_chain(const uint32_t* __restri
 }
 
 // Chain records placed in parallel (k_over_heads, a max-scan, k_cells_place):
-// an overflow record is one past its home's kCell (all_over: every record, the
-// deferred inserts of the fused scan, whose homes filled during the scan).  A
+// an overflow record is one past its home's kCell.  A
 // RUN is a group's overflow records of one fingerprint, adjacent after the
 // sort; the run's record of index x goes straight to slot x % kCell of the
 // cell 1 + x / kCell steps along the fingerprint's chain, so a heavy minimizer's
@@ -618,11 +594,7 @@ __global__ __launch_bounds__(kBlock) void k_cells_chain(const uint32_t* __restri
 // its home along its fingerprint's chain, which is all a walk needs (the order
 // inside a chain is not an output).
 __device__ __forceinline__ bool over_rec(const uint32_t* __restrict__ key, uint64_t i, uint32_t gshift, uint32_t g,
-                                         int all_over, bool* first) {
-  if (all_over) {
-    *first = i == 0 || (key[i - 1] >> gshift) != g;
-    return true;
-  }
+                                         bool* first) {
   if (rank_in_cell(key, i, gshift, g) != kCell) return false;
   *first = !(i >= kCell + 1 && (key[i - kCell - 1] >> gshift) == g);
   return true;
@@ -633,13 +605,13 @@ __device__ __forceinline__ bool over_rec(const uint32_t* __restrict__ key, uint6
 __global__ __launch_bounds__(kBlock) void k_over_heads(const uint32_t* __restrict__ key,
                                                       const uint64_t* __restrict__ ent,
                                                       const unsigned long long* __restrict__ n_dev, uint64_t n_host,
-                                                      uint32_t gshift, int skip_odd, int all_over,
+                                                      uint32_t gshift, int skip_odd,
                                                       uint32_t* __restrict__ head) {
   const uint64_t n = n_dev ? *n_dev : n_host;
   for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBlock) {
     const uint32_t g = key[i] >> gshift;
     bool first = false;
-    const bool over = !(skip_odd && (g & 1u)) && over_rec(key, i, gshift, g, all_over, &first);
+    const bool over = !(skip_odd && (g & 1u)) && over_rec(key, i, gshift, g, &first);
     head[i] = (over && (first || entry_fp(ent[i]) != entry_fp(ent[i - 1]))) ? (uint32_t)i : 0u;
   }
 }
@@ -648,14 +620,14 @@ __global__ __launch_bounds__(kBlock) void k_cells_place(const uint32_t* __restri
                                                        const uint64_t* __restrict__ ent,
                                                        const uint32_t* __restrict__ start,
                                                        const unsigned long long* __restrict__ n_dev, uint64_t n_host,
-                                                       uint32_t gshift, uint32_t cshift, int skip_odd, int all_over,
+                                                       uint32_t gshift, uint32_t cshift, int skip_odd,
                                                        uint64_t* cells, uint64_t cell_n) {
   const uint64_t n = n_dev ? *n_dev : n_host;
   for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBlock) {
     const uint32_t k = key[i];
     const uint32_t g = k >> gshift;
     bool first = false;
-    if ((skip_odd && (g & 1u)) || !over_rec(key, i, gshift, g, all_over, &first)) continue;
+    if ((skip_odd && (g & 1u)) || !over_rec(key, i, gshift, g, &first)) continue;
     const unsigned long long e = ent[i];
     const uint32_t fp = entry_fp(e);
     const uint64_t x = i - start[i];  // index in the run
@@ -683,24 +655,6 @@ __global__ __launch_bounds__(kBlock) void k_cells_place(const uint32_t* __restri
       if (ev[kCell - 1] == kEmpty || !(ev[kCell - 1] & kChain)) atomicOr(&cell[kCell - 1], (unsigned long long)kChain);
       at = next_cell(at, cell_n, fp);
     }
-  }
-}
-
-// Gather the fused scan's deferred inserts (option scan_defer: per lane, records
-// [wave][k][lane], ovf_cnt[wave * 64 + lane] of them) to off[...] onwards, for
-// the sort; one block of 64 threads per wavefront region
-__global__ __launch_bounds__(kWave) void k_ovf_gather(const uint32_t* __restrict__ okey,
-                                                     const uint64_t* __restrict__ oent,
-                                                     const uint32_t* __restrict__ cnt,
-                                                     const unsigned long long* __restrict__ off, uint32_t cap,
-                                                     uint32_t* __restrict__ key, uint64_t* __restrict__ ent) {
-  const uint64_t wv = blockIdx.x, lane = threadIdx.x;
-  const uint32_t c = cnt[wv * kWave + lane];
-  const uint64_t o = off[wv * kWave + lane];
-  for (uint32_t k = 0; k < c; ++k) {
-    const uint64_t at = ((wv * cap + k) << 6) + lane;
-    key[o + k] = okey[at];
-    ent[o + k] = oent[at];
   }
 }
 
@@ -759,14 +713,6 @@ struct ScanParams {
   int skip_o1;                    // INDEX: leave out the o = 1 keys (mg_ctx::index_o1)
   int skip_o3;                    // INDEX (fused): leave out the o = 3 keys (mg_ctx::index_o3)
   int no_insert;                  // diagnostics (phase_limit = 1): the index scan files no keys (timing only)
-  // INDEX (fused, option scan_defer): a key whose home cell is full goes to its
-  // lane's overflow list, record k of lane l of wavefront gw at (gw ovf_cap +
-  // k) 64 + l, key = home cell << ovf_fs | low fingerprint bits; the lane's
-  // count to ovf_cnt[gw 64 + l] (a full list falls back to the walk)
-  uint32_t* ovf_key;
-  uint64_t* ovf_ent;
-  uint32_t* ovf_cnt;
-  uint32_t ovf_cap, ovf_fs;
 };
 
 // Exchange-mode key records are o-major in the order o = 0, 2, 3, 1: when the
@@ -862,7 +808,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(G > 1 ? 
   const uint64_t nbmask = (1ULL << p.nb_log2) - 1;
   uint64_t cur[G] = {};  // records per region (wavefront-uniform)
   uint32_t nbuf = 0;  // run metas staged in s_buf (wavefront-uniform)
-  uint32_t novf = 0;  // this lane's deferred inserts (ScanParams::ovf_ent)
 
   // close the run of minimizer position pos over windows [jlo, jhi]: stage its
   // meta in LDS (the hashing and the HBM write happen 64 at a time in flush);
@@ -1164,20 +1109,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(G > 1 ? 
       // measured slower: scan 3.06-3.13 vs 2.92-2.94 ms at C3, profiles/r03y_ab_scan.txt)
       if constexpr (!KEYREC) {
 #pragma unroll
-        for (int o = 0; o < 4; ++o) {
-          if ((o == 1 && p.skip_o1) || (o == 3 && p.skip_o3) || p.no_insert) continue;
-          if (p.ovf_ent) {
-            if (cell_insert_home(p.cells, cb[o], ce[o])) continue;
-            if (novf < p.ovf_cap) {
-              const uint64_t at = (((uint64_t)gw * p.ovf_cap + novf) << 6) + (uint64_t)lane;
-              p.ovf_key[at] = ((uint32_t)cb[o] << p.ovf_fs) | (entry_fp(ce[o]) & ((1u << p.ovf_fs) - 1u));
-              p.ovf_ent[at] = ce[o];
-              ++novf;
-              continue;
-            }
-          }
-          cell_insert(p.cells, cb[o], p.cell_n, ce[o]);
-        }
+        for (int o = 0; o < 4; ++o)
+          if ((o != 1 || !p.skip_o1) && (o != 3 || !p.skip_o3) && !p.no_insert) cell_insert(p.cells, cb[o], p.cell_n, ce[o]);
       }
     } else if (INDEX && a < p.a_hi) {  // no keys (n <= l cannot pass setup_index): holes
       if (p.key0) p.key0[a] = kEmpty;
@@ -1194,7 +1127,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(G > 1 ? 
 #pragma unroll
   for (int j = 1; j < G; ++j) c = lane == j ? cur[j] : c;
   if (lane < G) p.run_cnt[gw * G + lane] = c;
-  if (INDEX && !KEYREC && p.ovf_cnt) p.ovf_cnt[gw * kWave + lane] = novf;
 }
 
 // ---------------------------------------------------------------------------
@@ -2848,14 +2780,13 @@ DiscGeom disc_geom(mg_ctx* ctx, bool contain, uint64_t nsrc) {
 // bucket-sharded single context); index: the scan also builds the index
 // (fused: CAS into the cells; exchange: key records).
 // Low fingerprint bits appended below hb bits of cell index in a sort key:
-// the rest of the sort's last 8-bit digit, or one more digit when that leaves
-// fewer than 4 (a cell's records of one fingerprint then sort together,
-// k_cells_place); at most kFpBits, and the key stays within 32 bits
+// the rest of the sort's last 8-bit digit (a cell's records of one
+// fingerprint then mostly sort together, k_cells_place, at no extra pass; a
+// whole extra digit cost C3 at P = 8 0.05 ms per rank for nothing, where few
+// cells overflow: profiles/r04m_sim8_c3_ranks_fs_extra_digit.md)
 uint32_t fp_sort_bits(uint32_t hb) {
   if (hb >= 32) return 0;
-  uint32_t fs = (hb + 7) / 8 * 8 - hb;
-  if (fs < 4 && hb + fs + 8 <= 32) fs += 8;
-  return std::min<uint32_t>(fs, kFpBits);
+  return std::min<uint32_t>((hb + 7) / 8 * 8 - hb, kFpBits);
 }
 
 template <int W>
@@ -2915,28 +2846,6 @@ struct LaunchScan {
     sp.skip_o1 = (index && !ctx->index_o1) ? 1 : 0;
     sp.skip_o3 = (index && !ctx->index_o3 && !ctx->xchg) ? 1 : 0;
     sp.no_insert = (index && ctx->phase_limit == 1) ? 1 : 0;
-    if (index && !ctx->xchg) {
-      ctx->ovf_lanes = 0;
-      if (ctx->scan_defer && !scan_is_reg(ctx, index)) {
-        // per lane at most 4 keys of each read it scans (G per window)
-        const uint64_t cap = 4 * G * ((((ngroups + G - 1) / G) + nw - 1) / nw);
-        const uint64_t lanes = nw * kWave;
-        if (cap <= 0xFFFFFFFFull) {
-          if (ensure(&ctx->d_ovf_key, &ctx->ovf_key_cap, lanes * cap) ||
-              ensure(&ctx->d_ovf_ent, &ctx->ovf_ent_cap, lanes * cap) ||
-              ensure(&ctx->d_ovf_cnt, &ctx->ovf_cnt_cap, lanes))
-            return -1;
-          ctx->ovf_cap = (uint32_t)cap;
-          ctx->ovf_lanes = lanes;
-          ctx->ovf_fs = fp_sort_bits(ctx->nb_log2);
-          sp.ovf_key = ctx->d_ovf_key;
-          sp.ovf_ent = ctx->d_ovf_ent;
-          sp.ovf_cnt = ctx->d_ovf_cnt;
-          sp.ovf_cap = ctx->ovf_cap;
-          sp.ovf_fs = ctx->ovf_fs;
-        }
-      }
-    }
     if (index && ctx->xchg) {  // key records (bucket, entry), o-major: they travel to the bucket owner
       sp.key_bk = ctx->d_kb;
       sp.key_ent = ctx->d_ke;
@@ -3237,7 +3146,7 @@ void mg_destroy(mg_ctx* ctx) {
                   ctx->d_digest, ctx->id_store[0], ctx->id_store[1], ctx->phys_store[0], ctx->phys_store[1],
                   ctx->d_tmp32, ctx->d_lay_k[0], ctx->d_lay_k[1], ctx->d_lay_v[0], ctx->d_lay_v[1], ctx->d_lay_tmp,
                   ctx->d_words_alt, ctx->d_len_alt, ctx->d_cbits, ctx->d_ccnt, ctx->d_lcells, ctx->d_lkcells,
-                  ctx->d_rhead, ctx->d_rstart, ctx->d_ovf_key, ctx->d_ovf_ent, ctx->d_ovf_cnt, ctx->d_ovf_off};
+                  ctx->d_rhead, ctx->d_rstart};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   for (auto& e : ctx->ev)
@@ -3420,8 +3329,7 @@ int mg_set_option(mg_ctx* ctx, const char* name, int64_t value) {
       flag("contain_prune", &ctx->contain_prune) || flag("probe_share", &ctx->probe_share) ||
       flag("probe_compact", &ctx->probe_compact) || flag("live_index", &ctx->live_index) ||
       flag("xchg_sort_runs", &ctx->xchg_sort_runs) || flag("layout_scratch", &ctx->layout_scratch) ||
-      flag("xchg_windows", &ctx->xchg_windows) || flag("chain_par", &ctx->chain_par) ||
-      flag("scan_defer", &ctx->scan_defer))
+      flag("xchg_windows", &ctx->xchg_windows) || flag("chain_par", &ctx->chain_par))
     return 0;
   if (flag("prefix_contain", &ctx->prefix_contain)) {
     ctx->index_ready = false;
@@ -3740,8 +3648,7 @@ int build_live_index(mg_ctx* ctx) {
   return 0;
 }
 
-// the sort / scan scratch of the exchange build and the deferred inserts
-// (d_xsort_tmp), grown to tb bytes
+// the sort / scan scratch of the exchange build (d_xsort_tmp), grown to tb bytes
 hipError_t grow_tmp(mg_ctx* ctx, size_t tb) {
   if (tb > ctx->xsort_tmp_cap) {
     if (ctx->d_xsort_tmp) {
@@ -3763,22 +3670,17 @@ hipError_t grow_tmp(mg_ctx* ctx, size_t tb) {
 // in their fingerprint's run (option chain_par, k_cells_place), or walked by
 // one thread per overflowing cell (k_cells_chain)
 // gshift / cshift / skip_odd: as k_cells_fill (classed keys: the full table
-// groups and skips by class, the coarse live table merges the classes).
-// all_over: every record overflows a full home (the fused scan's deferred
-// inserts: the table is not cleared, nothing goes to the homes)
+// groups and skips by class, the coarse live table merges the classes)
 int build_cells(mg_ctx* ctx, const uint32_t* key, const uint64_t* ent, const unsigned long long* n_dev,
-                uint64_t n_host, uint64_t* cells, uint64_t cell_n, uint32_t gshift, uint32_t cshift, int skip_odd,
-                int all_over) {
-  if (!all_over) MG_TRY(hipMemsetAsync(cells, 0xFF, cell_n * kCell * sizeof(uint64_t), ctx->stream));  // kEmpty
+                uint64_t n_host, uint64_t* cells, uint64_t cell_n, uint32_t gshift, uint32_t cshift, int skip_odd) {
+  MG_TRY(hipMemsetAsync(cells, 0xFF, cell_n * kCell * sizeof(uint64_t), ctx->stream));  // kEmpty
   if (!n_host) return 0;
   const uint32_t grid = (uint32_t)std::max<uint64_t>(
       1, std::min<uint64_t>((n_host + kBlock - 1) / kBlock, (uint64_t)ctx->n_cu * 32));
-  if (!all_over) {
-    hipLaunchKernelGGL(k_cells_fill, dim3(grid), dim3(kBlock), 0, ctx->stream, key, ent, n_dev, n_host, gshift,
-                       cshift, skip_odd, cells);
-    MG_TRY(hipGetLastError());
-  }
-  if (!ctx->chain_par && !all_over) {
+  hipLaunchKernelGGL(k_cells_fill, dim3(grid), dim3(kBlock), 0, ctx->stream, key, ent, n_dev, n_host, gshift, cshift,
+                     skip_odd, cells);
+  MG_TRY(hipGetLastError());
+  if (!ctx->chain_par) {
     hipLaunchKernelGGL(k_cells_chain, dim3(grid), dim3(kBlock), 0, ctx->stream, key, ent, n_dev, n_host, gshift,
                        cshift, skip_odd, cells, cell_n);
     MG_TRY(hipGetLastError());
@@ -3788,7 +3690,7 @@ int build_cells(mg_ctx* ctx, const uint32_t* key, const uint64_t* ent, const uns
   MG_TRY(ensure(&ctx->d_rhead, &ctx->rhead_cap, n_host));
   MG_TRY(ensure(&ctx->d_rstart, &ctx->rstart_cap, n_host));
   hipLaunchKernelGGL(k_over_heads, dim3(grid), dim3(kBlock), 0, ctx->stream, key, ent, n_dev, n_host, gshift, skip_odd,
-                     all_over, ctx->d_rhead);
+                     ctx->d_rhead);
   MG_TRY(hipGetLastError());
   size_t tb = 0;
   MG_TRY(rocprim::inclusive_scan(nullptr, tb, ctx->d_rhead, ctx->d_rstart, (size_t)n_host,
@@ -3798,7 +3700,7 @@ int build_cells(mg_ctx* ctx, const uint32_t* key, const uint64_t* ent, const uns
   MG_TRY(rocprim::inclusive_scan(ctx->d_xsort_tmp, tb, ctx->d_rhead, ctx->d_rstart, (size_t)n_host,
                                  rocprim::maximum<uint32_t>(), ctx->stream));
   hipLaunchKernelGGL(k_cells_place, dim3(grid), dim3(kBlock), 0, ctx->stream, key, ent, ctx->d_rstart, n_dev, n_host,
-                     gshift, cshift, skip_odd, all_over, cells, cell_n);
+                     gshift, cshift, skip_odd, cells, cell_n);
   MG_TRY(hipGetLastError());
   return 0;
 }
@@ -3852,7 +3754,7 @@ int build_live_index_xchg(mg_ctx* ctx) {
     }
   }
   const uint32_t lsh = sft + ctx->xkey_cls + ctx->xkey_fs;  // (classes merged)
-  if (build_cells(ctx, lk, le, ctx->d_nlive, n, ctx->d_lcells, live_n, lsh, lsh, 0, 0)) return -1;
+  if (build_cells(ctx, lk, le, ctx->d_nlive, n, ctx->d_lcells, live_n, lsh, lsh, 0)) return -1;
   ctx->live_shift = sft;
   ctx->live_cells = live_n;
   ctx->live_coarse = true;
@@ -4103,50 +4005,6 @@ int ensure_layout_range(mg_ctx* ctx) {
 
 extern "C" {
 
-// The fused scan's deferred inserts (option scan_defer): gather the per-lane
-// overflow lists, sort them by (home cell, low fingerprint bits) and place them
-// along their chains (build_cells, every record past a full home)
-int place_deferred(mg_ctx* ctx) {
-  ctx->ovf_n = 0;
-  ctx->counters.deferred = 0;
-  const uint64_t L = ctx->ovf_lanes;
-  if (!L) return 0;
-  MG_TRY(ensure(&ctx->d_ovf_off, &ctx->ovf_off_cap, L + 1));
-  MG_TRY(hipMemsetAsync(ctx->d_ovf_off, 0, sizeof(unsigned long long), ctx->stream));
-  size_t tb = 0;
-  MG_TRY(rocprim::inclusive_scan(nullptr, tb, ctx->d_ovf_cnt, ctx->d_ovf_off + 1, (size_t)L,
-                                 rocprim::plus<unsigned long long>(), ctx->stream));
-  MG_TRY(grow_tmp(ctx, tb));
-  tb = ctx->xsort_tmp_cap;
-  MG_TRY(rocprim::inclusive_scan(ctx->d_xsort_tmp, tb, ctx->d_ovf_cnt, ctx->d_ovf_off + 1, (size_t)L,
-                                 rocprim::plus<unsigned long long>(), ctx->stream));
-  unsigned long long total = 0;
-  MG_TRY(hipMemcpyAsync(&total, ctx->d_ovf_off + L, sizeof(total), hipMemcpyDeviceToHost, ctx->stream));
-  MG_TRY(hipStreamSynchronize(ctx->stream));
-  ctx->ovf_n = total;
-  ctx->counters.deferred = total;
-  if (!total) return 0;
-  if (total > 0xFFFFFFFFull) return set_err(ctx, "deferred inserts: more than 2^32 records");
-  for (int b = 0; b < 2; ++b) {
-    MG_TRY(ensure(&ctx->d_xkk[b], &ctx->xkk_cap[b], total));
-    MG_TRY(ensure(&ctx->d_xke[b], &ctx->xke_cap[b], total));
-  }
-  hipLaunchKernelGGL(k_ovf_gather, dim3((uint32_t)(L / kWave)), dim3(kWave), 0, ctx->stream, ctx->d_ovf_key,
-                     ctx->d_ovf_ent, ctx->d_ovf_cnt, ctx->d_ovf_off, ctx->ovf_cap, ctx->d_xkk[0], ctx->d_xke[0]);
-  MG_TRY(hipGetLastError());
-  const uint32_t fs = ctx->ovf_fs, bits = ctx->nb_log2 + fs;
-  rocprim::double_buffer<uint32_t> keys(ctx->d_xkk[0], ctx->d_xkk[1]);
-  rocprim::double_buffer<uint64_t> vals(ctx->d_xke[0], ctx->d_xke[1]);
-  if (total > 1) {
-    tb = 0;
-    MG_TRY(rocprim::radix_sort_pairs(nullptr, tb, keys, vals, (unsigned int)total, 0u, bits, ctx->stream));
-    MG_TRY(grow_tmp(ctx, tb));
-    tb = ctx->xsort_tmp_cap;
-    MG_TRY(rocprim::radix_sort_pairs(ctx->d_xsort_tmp, tb, keys, vals, (unsigned int)total, 0u, bits, ctx->stream));
-  }
-  return build_cells(ctx, keys.current(), vals.current(), nullptr, total, ctx->d_cells, ctx->cell_n, fs, fs, 0, 1);
-}
-
 int mg_build_index(mg_ctx* ctx, uint32_t min_overlap, uint32_t seed_k) {
   if (!ctx) return -1;
   MG_TRY(hipSetDevice(ctx->device));
@@ -4181,7 +4039,6 @@ int mg_build_index(mg_ctx* ctx, uint32_t min_overlap, uint32_t seed_k) {
     if (ctx->key0_ready) MG_TRY(ensure(&ctx->d_key0, &ctx->key0_cap, ctx->n + 1));
     if (ctx->n && dispatch_w<LaunchScanAll>(ctx->maxw, ctx, ctx->stream))
       return set_err(ctx, "index build launch failed");
-    if (ctx->n && place_deferred(ctx)) return -1;
     if (!ctx->n) ctx->nrun_reg = 0;
     ctx->scan_state = 1;
   } else {  // the whole index for a source-range shard (its containment probe reads suffix-key hits)
@@ -4496,7 +4353,7 @@ int mg_xchg_insert_keys(mg_ctx* ctx, const void* recv, uint64_t slot, uint32_t r
   }
   ctx->xkeys_n = n;
   if (build_cells(ctx, ctx->xkey_k, ctx->xkey_e, nullptr, n, ctx->d_cells, ctx->cell_n, fs, fs + ctx->xkey_cls,
-                  ctx->xkey_cls, 0))
+                  ctx->xkey_cls))
     return -1;
   MG_TRY(hipEventRecord(ctx->ev[1], ctx->stream));
   ctx->index_ready = true;

@@ -39,7 +39,7 @@ class _Counters(C.Structure):
     _fields_ = [("sources", C.c_uint64), ("runs", C.c_uint64), ("entries", C.c_uint64),
                 ("verified", C.c_uint64), ("rows", C.c_uint64), ("live_cells", C.c_uint64),
                 ("c_runs", C.c_uint64), ("c_entries", C.c_uint64), ("c_verified", C.c_uint64),
-                ("c_contained", C.c_uint64), ("deferred", C.c_uint64)]
+                ("c_contained", C.c_uint64)]
 
 
 _lib = None

@@ -1,14 +1,12 @@
 """A step-level model of the cell table's parallel chain placement
-(build_cells: k_cells_fill, k_over_heads + max-scan, k_cells_place; the fused
-scan's deferred inserts use the same placement with every record past a full
-home).  Every record's atomic steps run in a random interleaving with the
+(build_cells: k_cells_fill, k_over_heads + max-scan, k_cells_place).  Every record's atomic steps run in a random interleaving with the
 others', including records whose runs share a chain (equal fingerprint low bits,
 equal stride) and entries of other homes sitting in the chain cells.  The check
 is the probe's walk rule (k_probe, prefix_contain_walk, k_lookup_key): every
 record is found from its home cell, moving to the next cell of its
 fingerprint's chain while the current one is full with the chain flag on its
 last slot.  Kernel-level parity runs on the GPU (test_gpu_parity
-test_deferred_index_build, test_exchange_mode_options chain_par)."""
+test_exchange_mode_options, the exchange scale digests)."""
 import random
 
 import pytest
@@ -32,7 +30,7 @@ class TableFull(Exception):
     pass
 
 
-def place(n_cells, recs, all_over, foreign, rnd):
+def place(n_cells, recs, foreign, rnd):
     """recs: (home, fp, tag); returns the cells and their chain flags."""
     cells = [[None] * K for _ in range(n_cells)]
     flag = [False] * n_cells
@@ -43,9 +41,6 @@ def place(n_cells, recs, all_over, foreign, rnd):
     n = len(recs)
     over, first = [False] * n, [False] * n
     for i, (c, fp, _) in enumerate(recs):
-        if all_over:  # deferred inserts: the scan filled and flagged every home
-            over[i], first[i] = True, i == 0 or recs[i - 1][0] != c
-            continue
         r = 0
         while r < K and i - r - 1 >= 0 and recs[i - r - 1][0] == c:
             r += 1
@@ -55,10 +50,6 @@ def place(n_cells, recs, all_over, foreign, rnd):
         else:
             over[i] = True
             first[i] = not (i >= K + 1 and recs[i - K - 1][0] == c)
-    if all_over:
-        for c, _, _ in recs:
-            cells[c] = [x if x is not None else ("home", c) for x in cells[c]]
-            flag[c] = True
     head = [i if over[i] and (first[i] or recs[i][1] != recs[i - 1][1]) else 0 for i in range(n)]
     start, m = [], 0
     for h in head:  # inclusive max-scan
@@ -123,12 +114,13 @@ def test_parallel_chain_placement_keeps_every_record_reachable():
                 recs.append((rnd.randrange(2), rnd.choice([5, 1029, 7, 29]), k))
             else:
                 recs.append((rnd.randrange(n_cells), rnd.randrange(1 << 19), k))
-        all_over = rnd.random() < 0.5
+        # entries of other homes in the chain cells (not in any home of recs:
+        # k_cells_fill owns those)
         homes = {r[0] for r in recs}
         foreign = [(c, ("f", k)) for k, c in enumerate(rnd.randrange(n_cells) for _ in range(n_cells // 2))
-                   if all_over and c not in homes]
+                   if c not in homes]
         try:
-            placed, cells, flag = place(n_cells, recs, all_over, foreign, rnd)
+            placed, cells, flag = place(n_cells, recs, foreign, rnd)
         except TableFull:
             continue
         for r in placed:

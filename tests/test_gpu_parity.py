@@ -780,41 +780,6 @@ def test_live_index_forced(name):
         assert np.array_equal(rows_to_tuples(rows), want_rows), live
 
 
-@pytest.mark.parametrize("name", ["small", "mixed", "tandem", "highdup", "dirty", "branchy", "metagenome"])
-def test_deferred_index_build(name):
-    """Option scan_defer: the fused scan files each key into its home cell only;
-    the keys of full homes wait in per-lane lists and are sorted and placed along
-    their fingerprints' chains after the scan (place_deferred, k_cells_place).
-    Rows and superReadIDs equal the goldens on the default directory and on the
-    smallest one the load bound allows (nb_log2 = 10: long chains, runs of
-    several fingerprints crossing), counters().deferred shows the path ran,
-    and the lookups read the deferred table too."""
-    if name == "metagenome":
-        c, L = synth.metagenome_read_set(20000, 100, 250, n_genomes=20, total_len=400000, seed=51)
-        seqs, l = synth.codes_to_strings(c, L), 50
-        ds = Dataset.from_strings(seqs, l)
-        orows, osup, _, _ = OracleDataset.from_strings(seqs, l).overlaps(l)
-        want_rows, want_sup, lookups = sorted_tuples(orows), {str(i): int(x) for i, x in enumerate(osup) if x}, {}
-    else:
-        meta = load_meta(name)
-        l = meta["l"]
-        ds = Dataset.from_files([fixture_input(name)], l)
-        want_rows, want_sup, lookups = golden_rows(name), meta["super"], meta.get("lookups", {})
-    for nb in (0, 10):
-        e = OverlapEngine(0)
-        e.set_option("scan_defer", 1)
-        e.set_option("stats", 1)
-        rows, sup = gpu_rows(e, ds, l, nb_log2=nb)
-        deferred = e.counters()["deferred"]
-        assert {str(i): int(x) for i, x in enumerate(sup) if x} == want_sup, nb
-        assert np.array_equal(rows_to_tuples(rows), want_rows), nb
-        for key, exp in lookups.items():
-            assert [list(x) for x in e.lookup(key)] == exp, (nb, key)
-        e.close()
-        if nb == 10 and name in ("highdup", "tandem", "metagenome"):
-            assert deferred > 0, (name, nb)
-
-
 @pytest.mark.parametrize("name", ["small", "mixed", "tandem", "highdup", "tworead"])
 def test_replicated_index_source_shards(name):
     """Multi-GPU replicated mode (bench --multi replicated): every rank builds

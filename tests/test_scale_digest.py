@@ -167,32 +167,6 @@ def test_scale_digest_matches_reference(name):
         e.close()
 
 
-@pytest.mark.gpu
-@pytest.mark.timeout(900)
-@pytest.mark.parametrize("name", ["c3", "c5s", "c5"])
-def test_scale_digest_deferred_index(name):
-    """The same digests with the fused scan's deferred inserts (option
-    scan_defer: home cells only during the scan, the full homes' keys sorted and
-    placed along their chains afterwards; C5's heavy minimizers overflow a
-    quarter of the homes)."""
-    from metagenomics_amd.overlap import OverlapEngine
-
-    if not os.path.exists(SCALE[name]):
-        pytest.skip(f"{name}.json not generated")
-    m, ds = scale_dataset(name)
-    e = OverlapEngine(0)
-    try:
-        e.set_option("scan_defer", 1)
-        e.set_option("stats", 1)
-        n = _engine_rows(e, ds, m["workload"]["min_overlap"], 31)
-        assert e.counters()["deferred"] > 0
-        assert n == m["rows"]["n"]
-        assert e.rows_digest() == m["rows"]
-        assert e.super_digest() == m["super"]
-    finally:
-        e.close()
-
-
 def combine(ds):
     out = {"n": 0, "sum": 0, "xor": 0, "sum2": 0}
     for d in ds:

@@ -41,9 +41,6 @@ for s in $STEPS; do
   newtests)
     timeout -k 10 900 python -u -m pytest tests/test_gpu_parity.py tests/test_long_reads.py -x -v -m gpu -k "exchange or live_index or falls_back" --timeout 300 --timeout-method thread > $OUT/new_tests.log 2>&1
     rc=$?; echo "new tests rc=$rc"; grep -E "PASS|FAIL|Error" $OUT/new_tests.log | tail -40 ;;
-  defer)
-    timeout -k 10 1100 python -u -m pytest tests/test_gpu_parity.py tests/test_scale_digest.py -x -v -m gpu -k "deferred or exchange_mode_options" --timeout 900 --timeout-method thread > $OUT/defer_tests.log 2>&1
-    rc=$?; echo "deferred-build tests rc=$rc"; grep -E "PASS|FAIL|SKIP|Error" $OUT/defer_tests.log | tail -30 ;;
   xdigest)
     timeout -k 10 1100 python -u -m pytest tests/test_scale_digest.py -x -v -m gpu -k "exchange_scale" --timeout 1000 --timeout-method thread > $OUT/xdigest_tests.log 2>&1
     rc=$?; echo "exchange digest tests rc=$rc"; grep -E "PASS|FAIL|SKIP|Error" $OUT/xdigest_tests.log | tail -12 ;;
