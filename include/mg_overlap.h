@@ -294,6 +294,13 @@ int mg_get_counters(const mg_ctx* ctx, mg_counters* c);
  *                   windows of 256 reads (default 1);
  *  "layout_scratch" 0 = free the layout's double buffers after each layout
  *                   (many contexts on one device); default 1 keeps them;
+ *  "chain_par"      sorted cell builds (exchange mode): records past their home
+ *                   cell placed in parallel by their index in their fingerprint's
+ *                   run (default 1); 0 = one thread walks each overflowing cell;
+ *  "check_cells"    diagnostics: after each sorted cell build, walk every record
+ *                   from its home and fail the call if one is not found;
+ *  "xchg_fs"        diagnostics: fingerprint bits in the exchange sort key
+ *                   (-1 = auto: what fills the sort's last 8-bit digit);
  *  "run_cap"        tests: initial run records per scan region (0 = sized from
  *                   the reads; overflowing regions are resized and rescanned);
  *  "phase_limit", "max_blocks"

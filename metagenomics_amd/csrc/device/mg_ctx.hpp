@@ -203,6 +203,8 @@ struct mg_ctx {
   // thread per overflowing cell, k_cells_chain); d_rhead / d_rstart: run heads
   // and their max-scan
   bool chain_par = true;
+  bool check_cells = false;  // diagnostics (option "check_cells"): verify each sorted cell build
+  int xchg_fs = -1;  // diagnostics (option "xchg_fs"): fingerprint bits in the exchange sort key (-1: fp_sort_bits)
   uint32_t* d_rhead = nullptr;
   uint32_t* d_rstart = nullptr;
   size_t rhead_cap = 0, rstart_cap = 0;

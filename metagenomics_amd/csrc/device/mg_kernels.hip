@@ -612,7 +612,12 @@ __global__ __launch_bounds__(kBlock) void k_over_heads(const uint32_t* __restric
     const uint32_t g = key[i] >> gshift;
     bool first = false;
     const bool over = !(skip_odd && (g & 1u)) && over_rec(key, i, gshift, g, &first);
-    head[i] = (over && (first || entry_fp(ent[i]) != entry_fp(ent[i - 1]))) ? (uint32_t)i : 0u;
+    // both fingerprints loaded unconditionally and the head formed by a
+    // multiply: the nested-select form of this expression was miscompiled
+    // (ROCm 7.2 hipcc, gfx950: every record past index 8 stored 0)
+    const uint32_t fp_prev = entry_fp(ent[i ? i - 1 : 0]), fp_cur = entry_fp(ent[i]);
+    const uint32_t hd = (over ? 1u : 0u) & ((first ? 1u : 0u) | (fp_prev != fp_cur ? 1u : 0u));
+    head[i] = (uint32_t)i * hd;
   }
 }
 
@@ -654,6 +659,44 @@ __global__ __launch_bounds__(kBlock) void k_cells_place(const uint32_t* __restri
       if (done) break;
       if (ev[kCell - 1] == kEmpty || !(ev[kCell - 1] & kChain)) atomicOr(&cell[kCell - 1], (unsigned long long)kChain);
       at = next_cell(at, cell_n, fp);
+    }
+  }
+}
+
+// Diagnostics (option check_cells): every filed record must be found by the
+// probes' walk (home cell, then the next cell of its fingerprint's chain while
+// the current one is full with the chain flag on its last slot); bad[0] counts
+// the records that are not, bad[1..] describes the first ones
+__global__ __launch_bounds__(kBlock) void k_check_cells(const uint32_t* __restrict__ key,
+                                                       const uint64_t* __restrict__ ent,
+                                                       const uint32_t* __restrict__ start,
+                                                       const unsigned long long* __restrict__ n_dev, uint64_t n_host,
+                                                       uint32_t gshift, uint32_t cshift, int skip_odd,
+                                                       const uint64_t* __restrict__ cells, uint64_t cell_n,
+                                                       unsigned long long* __restrict__ bad) {
+  const uint64_t n = n_dev ? *n_dev : n_host;
+  for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBlock) {
+    const uint32_t k = key[i];
+    if (skip_odd && ((k >> gshift) & 1u)) continue;
+    const uint64_t e = ent[i];
+    const uint32_t fp = entry_fp(e);
+    uint64_t at = k >> cshift;
+    bool found = false;
+    uint64_t steps = 0;
+    for (; steps <= cell_n; ++steps) {
+      const uint64_t* c = cells + at * kCell;
+      for (int s = 0; s < kCell; ++s) found = found || ((c[s] & ~kChain) == e);
+      if (found || c[kCell - 1] == kEmpty || !(c[kCell - 1] & kChain)) break;
+      at = next_cell(at, cell_n, fp);
+    }
+    if (!found) {
+      const unsigned long long q = atomicAdd(&bad[0], 1ull);
+      if (q < 8) {
+        bad[1 + q * 4] = i;
+        bad[2 + q * 4] = ((uint64_t)(k >> cshift) << 32) | steps;
+        bad[3 + q * 4] = start ? (uint64_t)start[i] : ~0ull;
+        bad[4 + q * 4] = e;
+      }
     }
   }
 }
@@ -3315,6 +3358,14 @@ int mg_set_option(mg_ctx* ctx, const char* name, int64_t value) {
     ctx->phase_limit = value > 0 ? (int)value : 99;
     return 0;
   }
+  if (!strcmp(name, "check_cells")) {  // diagnostics: verify every sorted cell build (build_cells)
+    ctx->check_cells = value != 0;
+    return 0;
+  }
+  if (!strcmp(name, "xchg_fs")) {  // diagnostics: fingerprint bits of the exchange sort key (-1: auto)
+    ctx->xchg_fs = (int)std::max<int64_t>(-1, std::min<int64_t>(value, kFpBits));
+    return 0;
+  }
   if (!strcmp(name, "max_blocks")) {  // diagnostics: cap the persistent probe grid
     ctx->max_blocks = value > 0 ? (uint32_t)value : 8192u;
     return 0;
@@ -3664,6 +3715,50 @@ hipError_t grow_tmp(mg_ctx* ctx, size_t tb) {
   return hipSuccess;
 }
 
+// option check_cells: fail the build when a filed record cannot be walked to
+int check_cells(mg_ctx* ctx, const uint32_t* key, const uint64_t* ent, const uint32_t* start,
+                const unsigned long long* n_dev, uint64_t n_host, const uint64_t* cells, uint64_t cell_n,
+                uint32_t gshift, uint32_t cshift, int skip_odd) {
+  if (!ctx->check_cells || !n_host) return 0;
+  unsigned long long* d_bad = nullptr;
+  MG_TRY(hipMalloc(&d_bad, 33 * sizeof(unsigned long long)));
+  MG_TRY(hipMemsetAsync(d_bad, 0, 33 * sizeof(unsigned long long), ctx->stream));
+  hipLaunchKernelGGL(k_check_cells, dim3((uint32_t)std::min<uint64_t>((n_host + kBlock - 1) / kBlock, 4096)),
+                     dim3(kBlock), 0, ctx->stream, key, ent, start, n_dev, n_host, gshift, cshift, skip_odd, cells,
+                     cell_n, d_bad);
+  unsigned long long h[33];
+  MG_TRY(hipMemcpyAsync(h, d_bad, sizeof(h), hipMemcpyDeviceToHost, ctx->stream));
+  MG_TRY(hipStreamSynchronize(ctx->stream));
+  (void)hipFree(d_bad);
+  std::string scan_note;
+  if (start && n_host <= (1u << 22)) {  // the max-scan against the host's
+    std::vector<uint32_t> hh(n_host), hs(n_host);
+    MG_TRY(hipMemcpy(hh.data(), ctx->d_rhead, n_host * 4, hipMemcpyDeviceToHost));
+    MG_TRY(hipMemcpy(hs.data(), start, n_host * 4, hipMemcpyDeviceToHost));
+    uint32_t mx = 0;
+    uint64_t heads = 0, bad_scan = 0, first_bad = 0;
+    for (uint64_t i = 0; i < n_host; ++i) {
+      heads += hh[i] != 0;
+      mx = std::max(mx, hh[i]);
+      if (hs[i] != mx && !bad_scan++) first_bad = i;
+    }
+    scan_note = " heads " + std::to_string(heads) + " scan mismatches " + std::to_string(bad_scan) + " first at " +
+                std::to_string(first_bad) + " (head " + std::to_string(hh[first_bad]) + " start " +
+                std::to_string(hs[first_bad]) + ")";
+  }
+  if (!h[0]) return 0;
+  std::string m = scan_note + " check_cells: " + std::to_string(h[0]) + " of " + std::to_string(n_host) +
+                  " records unreachable (gshift " + std::to_string(gshift) + ", cshift " + std::to_string(cshift) +
+                  ", cell_n " + std::to_string(cell_n) + "):";
+  for (int q = 0; q < 8 && q < (int)h[0]; ++q) {
+    char b[160];
+    snprintf(b, sizeof(b), " [i %llu home %llu steps %llu start %lld ent %016llx]", h[1 + 4 * q], h[2 + 4 * q] >> 32,
+             h[2 + 4 * q] & 0xFFFFFFFFull, (long long)h[3 + 4 * q], h[4 + 4 * q]);
+    m += b;
+  }
+  return set_err(ctx, m);
+}
+
 // the cell table `cells` of cell_n cells from sorted records key / ent (count
 // n_host, or on the device at n_dev <= n_host): clear, one store per record,
 // then the records past their home's kCell: placed in parallel by their index
@@ -3684,7 +3779,7 @@ int build_cells(mg_ctx* ctx, const uint32_t* key, const uint64_t* ent, const uns
     hipLaunchKernelGGL(k_cells_chain, dim3(grid), dim3(kBlock), 0, ctx->stream, key, ent, n_dev, n_host, gshift,
                        cshift, skip_odd, cells, cell_n);
     MG_TRY(hipGetLastError());
-    return 0;
+    return check_cells(ctx, key, ent, nullptr, n_dev, n_host, cells, cell_n, gshift, cshift, skip_odd);
   }
   if (n_host > 0xFFFFFFFFull) return set_err(ctx, "cell build: more than 2^32 records");
   MG_TRY(ensure(&ctx->d_rhead, &ctx->rhead_cap, n_host));
@@ -3702,7 +3797,7 @@ int build_cells(mg_ctx* ctx, const uint32_t* key, const uint64_t* ent, const uns
   hipLaunchKernelGGL(k_cells_place, dim3(grid), dim3(kBlock), 0, ctx->stream, key, ent, ctx->d_rstart, n_dev, n_host,
                      gshift, cshift, skip_odd, cells, cell_n);
   MG_TRY(hipGetLastError());
-  return 0;
+  return check_cells(ctx, key, ent, ctx->d_rstart, n_dev, n_host, cells, cell_n, gshift, cshift, skip_odd);
 }
 
 // The exchange mode's discovery index (option live_index): after
@@ -4330,7 +4425,8 @@ int mg_xchg_insert_keys(mg_ctx* ctx, const void* recv, uint64_t slot, uint32_t r
   // low fingerprint bits below the cell (chain_par: a group's records of one
   // fingerprint adjacent), filling the sort's last 8-bit digit, or one more
   // digit when that leaves fewer than 4
-  const uint32_t fs = ctx->chain_par ? fp_sort_bits((uint32_t)hb) : 0u;
+  uint32_t fs = ctx->chain_par ? fp_sort_bits((uint32_t)hb) : 0u;
+  if (ctx->xchg_fs >= 0) fs = std::min<uint32_t>((uint32_t)ctx->xchg_fs, hb < 32 ? 32u - (uint32_t)hb : 0u);
   ctx->xkey_fs = fs;
   if ((ctx->xkey_cls || fs) && n) {
     hipLaunchKernelGGL(k_key_class, dim3((uint32_t)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, ctx->stream, k0, e0,

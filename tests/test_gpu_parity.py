@@ -366,7 +366,9 @@ def test_exchange_mode_containment_paths(prefix):
     ("tandem", 4, {"xchg_sort_runs": 1}), ("highdup", 8, {"nb_log2": 16, "xchg_sort_runs": 1}),
     ("mixed", 3, {"xchg_windows": 0}), ("dirty", 2, {"xchg_windows": 0, "prefix_contain": 0}),
     ("highdup", 4, {"nb_log2": 16, "chain_par": 0}), ("mixed", 3, {"chain_par": 0}),
-    ("highdup", 2, {"nb_log2": 10}), ("tandem", 3, {"nb_log2": 10})])
+    ("highdup", 2, {"nb_log2": 10}), ("tandem", 3, {"nb_log2": 10}),
+    ("small", 2, {"check_cells": 1}), ("highdup", 3, {"check_cells": 1, "nb_log2": 10}),
+    ("mixed", 3, {"check_cells": 1, "nb_log2": 16}), ("highdup", 2, {"check_cells": 1, "xchg_fs": 0})])
 def test_exchange_mode_options(name, world, opts):
     """Exchange-mode variants against the reference: the discovery index of the
     uncontained reads (build_live_index_xchg: the rank's cells coarsened, live
@@ -376,7 +378,10 @@ def test_exchange_mode_options(name, world, opts):
     runs ordered by bucket (xchg_sort_runs = 1; default: probed in place), the
     register scan for mixed lengths (xchg_windows = 0), the overflow records
     walked by one thread per cell instead of placed in parallel (chain_par = 0),
-    and small directories whose chains run long (nb_log2 = 10)."""
+    small directories whose chains run long (nb_log2 = 10), and the table
+    checker (check_cells: every record found from its home, for the full table
+    and the coarse live table; xchg_fs = 0: no fingerprint bits in the sort, the
+    runs of different fingerprints interleave)."""
     meta = load_meta(name)
     ds = Dataset.from_files([fixture_input(name)], meta["l"])
     rows, sup = exchange_rows(ds, meta["l"], world, opts=dict(opts, stats=1))
