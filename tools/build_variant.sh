@@ -11,4 +11,4 @@ mkdir -p $B $ROOT/metagenomics_amd/lib/variants
   -c $ROOT/metagenomics_amd/csrc/device/mg_kernels.hip -o $B/mg_kernels.o
 O=$ROOT/metagenomics_amd/build
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -pthread -o $ROOT/metagenomics_amd/lib/variants/$NAME.so \
-  $B/mg_kernels.o $O/mg_dataset.o $O/mg_host.o $O/mg_graph.o $O/mg_unitig.o $O/mg_parse.o
+  $B/mg_kernels.o $O/mg_dataset.o $O/mg_host.o $O/mg_graph.o $O/mg_unitig.o $O/mg_parse.o $O/mg_rdzv.o
