@@ -139,6 +139,12 @@ struct mg_ctx {
   uint64_t xchg_lo = 0, xchg_hi = 0;     // its source reads
   unsigned long long* d_blk = nullptr;   // routing: per-(block, rank) counts / offsets
   size_t blk_cap = 0;
+  // exchange mode, equal lengths: the register scan counts its runs per
+  // destination rank (one row of nranks per run region), so routing the runs
+  // skips k_part's count pass (runs_counted: valid for the last scan)
+  unsigned long long* d_rcnt = nullptr;
+  size_t rcnt_cap = 0;
+  bool runs_counted = false;
   int packable = 0;                      // 1 << MG_KEYS | 1 << MG_RUNS | 1 << MG_ROWS
   unsigned long long* d_flat_cnt = nullptr;  // per-region counts of the received runs (probe input)
   size_t flat_cnt_cap = 0;

@@ -756,6 +756,10 @@ struct ScanParams {
   int skip_o1;                    // INDEX: leave out the o = 1 keys (mg_ctx::index_o1)
   int skip_o3;                    // INDEX (fused): leave out the o = 3 keys (mg_ctx::index_o3)
   int no_insert;                  // diagnostics (phase_limit = 1): the index scan files no keys (timing only)
+  // k_scan_reg (exchange mode): runs stored per destination rank, dst_cnt[gw *
+  // dst_ranks + d] (nullptr: not counted; k_part's count pass does it)
+  unsigned long long* dst_cnt;
+  uint32_t dst_ranks;
 };
 
 // Exchange-mode key records are o-major in the order o = 0, 2, 3, 1: when the
@@ -1187,6 +1191,7 @@ struct RunStage {
   uint64_t nbmask;
   uint64_t cursor = 0;
   uint32_t head = 0, nbuf = 0;  // staged metas: ring [head, head + nbuf) (wavefront-uniform)
+  uint32_t dcnt = 0;            // p.dst_cnt: lane d counts the stored runs bound for rank d
 
   __device__ RunStage(const ScanParams& pp, uint64_t* buf, ulonglong2* reg, int ln)
       : p(pp), s_buf(buf), region(reg), lane(ln), msh(64 - 2 * pp.m), nbmask((1ULL << pp.nb_log2) - 1) {}
@@ -1224,19 +1229,29 @@ struct RunStage {
     }
     if (flag) flag = owned(v & nbmask, p.nb_log2, p.rank, p.nranks);
     const uint64_t bal = __ballot(flag);
+    bool stored = false;
     if (flag) {
       const uint64_t at = cursor + lane_prefix(bal);
-      if (at < p.run_cap) region[at] = make_ulonglong2(v, meta);
+      stored = at < p.run_cap;
+      if (stored) region[at] = make_ulonglong2(v, meta);
     }
     cursor += (uint64_t)__popcll(bal);
+    if (p.dst_cnt) {  // k_part's destination rule (OWN_BUCKET), one ballot per rank
+      const uint32_t d = (uint32_t)(((v & nbmask) * p.dst_ranks) >> p.nb_log2);
+      for (uint32_t dd = 0; dd < p.dst_ranks; ++dd) {
+        const uint32_t c = (uint32_t)__popcll(__ballot(stored && d == dd));
+        dcnt += (uint32_t)lane == dd ? c : 0u;
+      }
+    }
     head += k;
     nbuf -= k;
     wave_sync();
   }
 
-  // the region count
+  // the region count (and its per-rank split)
   __device__ void finish(uint64_t gw) {
     if (lane == 0) p.run_cnt[gw] = cursor;
+    if (p.dst_cnt && (uint32_t)lane < p.dst_ranks) p.dst_cnt[gw * p.dst_ranks + lane] = dcnt;
   }
 };
 
@@ -2889,6 +2904,13 @@ struct LaunchScan {
     sp.skip_o1 = (index && !ctx->index_o1) ? 1 : 0;
     sp.skip_o3 = (index && !ctx->index_o3 && !ctx->xchg) ? 1 : 0;
     sp.no_insert = (index && ctx->phase_limit == 1) ? 1 : 0;
+    if (index && ctx->xchg) ctx->runs_counted = false;
+    if (index && ctx->xchg && scan_is_reg(ctx, index) && ctx->nranks > 1 && ctx->nranks <= kWave) {
+      if (ensure(&ctx->d_rcnt, &ctx->rcnt_cap, nreg * ctx->nranks)) return -1;
+      sp.dst_cnt = ctx->d_rcnt;
+      sp.dst_ranks = ctx->nranks;
+      ctx->runs_counted = true;
+    }
     if (index && ctx->xchg) {  // key records (bucket, entry), o-major: they travel to the bucket owner
       sp.key_bk = ctx->d_kb;
       sp.key_ent = ctx->d_ke;
@@ -3189,7 +3211,7 @@ void mg_destroy(mg_ctx* ctx) {
                   ctx->d_digest, ctx->id_store[0], ctx->id_store[1], ctx->phys_store[0], ctx->phys_store[1],
                   ctx->d_tmp32, ctx->d_lay_k[0], ctx->d_lay_k[1], ctx->d_lay_v[0], ctx->d_lay_v[1], ctx->d_lay_tmp,
                   ctx->d_words_alt, ctx->d_len_alt, ctx->d_cbits, ctx->d_ccnt, ctx->d_lcells, ctx->d_lkcells,
-                  ctx->d_rhead, ctx->d_rstart};
+                  ctx->d_rhead, ctx->d_rstart, ctx->d_rcnt};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   for (auto& e : ctx->ev)
@@ -3465,23 +3487,27 @@ void source_range(const mg_ctx* ctx, uint64_t* lo, uint64_t* hi) {
 // per-peer stream lengths go to the caller's device counts (no host sync).
 uint32_t part_grid(uint64_t nreg) { return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(nreg, 8192)); }
 
+// precounted: per-(region, rank) counts the producer wrote (k_scan_reg's
+// dst_cnt); then one block per region and no count pass
 template <int KIND>
 int route_slots(mg_ctx* ctx, PartParams pp, void* out, void* self_out, uint64_t slot, uint32_t rounds,
-                unsigned long long* counts) {
-  const uint32_t grid = part_grid(pp.nreg);
-  MG_TRY(ensure(&ctx->d_blk, &ctx->blk_cap, (size_t)grid * ctx->nranks));
+                unsigned long long* counts, unsigned long long* precounted = nullptr) {
+  const uint32_t grid = precounted ? (uint32_t)pp.nreg : part_grid(pp.nreg);
+  if (!precounted) MG_TRY(ensure(&ctx->d_blk, &ctx->blk_cap, (size_t)grid * ctx->nranks));
   pp.nranks = ctx->nranks;
   pp.nb_log2 = ctx->nb_log2;
   pp.n_reads = ctx->n;
-  pp.blk = ctx->d_blk;
+  pp.blk = precounted ? precounted : ctx->d_blk;
   pp.out = out;
   pp.self_out = self_out;
   pp.self_rank = ctx->rank;
   pp.slot = slot;
   pp.rounds = rounds;
-  hipLaunchKernelGGL((k_part<KIND, 0>), dim3(grid), dim3(kBlock), 0, ctx->stream, pp);
-  MG_TRY(hipGetLastError());
-  hipLaunchKernelGGL(k_part_scan, dim3(ctx->nranks), dim3(1024), 0, ctx->stream, ctx->d_blk, grid, ctx->nranks,
+  if (!precounted) {
+    hipLaunchKernelGGL((k_part<KIND, 0>), dim3(grid), dim3(kBlock), 0, ctx->stream, pp);
+    MG_TRY(hipGetLastError());
+  }
+  hipLaunchKernelGGL(k_part_scan, dim3(ctx->nranks), dim3(1024), 0, ctx->stream, pp.blk, grid, ctx->nranks,
                      counts);
   MG_TRY(hipGetLastError());
   hipLaunchKernelGGL((k_part<KIND, 1>), dim3(grid), dim3(kBlock), 0, ctx->stream, pp);
@@ -4348,7 +4374,7 @@ int mg_xchg_pack(mg_ctx* ctx, int what, void* dst, uint64_t slot, uint32_t round
   if (what == MG_KEYS) {
     PartParams pp{};
     pp.cap = kFlatRegion;
-    pp.flat_n = 4 * nsrc;
+    pp.flat_n = (ctx->index_o1 ? 4 : 3) * nsrc;  // (no o = 1 keys: the last segment is holes, key_seg)
     pp.nreg = (pp.flat_n + kFlatRegion - 1) / kFlatRegion;
     pp.key_bk = ctx->d_kb;
     pp.key_ent = ctx->d_ke;
@@ -4363,6 +4389,8 @@ int mg_xchg_pack(mg_ctx* ctx, int what, void* dst, uint64_t slot, uint32_t round
     pp.cap = ctx->run_cap;
     pp.cnt = ctx->d_run_cnt;
     pp.nreg = ctx->nrun_reg;
+    if (ctx->runs_counted && pp.nreg)  // the scan counted them per rank: one block per region, no count pass
+      return route_slots<OWN_BUCKET>(ctx, pp, dst, self_dst, slot, rounds, cnt, ctx->d_rcnt);
     return route_slots<OWN_BUCKET>(ctx, pp, dst, self_dst, slot, rounds, cnt);
   }
   PartParams pp{};
