@@ -2833,10 +2833,6 @@ DiscGeom disc_geom(mg_ctx* ctx, bool contain, uint64_t nsrc) {
   return g;
 }
 
-// Window scan over source slots [a_lo, a_hi): one run region per scan
-// wavefront in ctx->d_runs.  filter: keep only runs whose bucket this rank owns (a
-// bucket-sharded single context); index: the scan also builds the index
-// (fused: CAS into the cells; exchange: key records).
 // Low fingerprint bits appended below hb bits of cell index in a sort key:
 // the rest of the sort's last 8-bit digit (a cell's records of one
 // fingerprint then mostly sort together, k_cells_place, at no extra pass; a
@@ -2847,6 +2843,10 @@ uint32_t fp_sort_bits(uint32_t hb) {
   return std::min<uint32_t>((hb + 7) / 8 * 8 - hb, kFpBits);
 }
 
+// Window scan over source slots [a_lo, a_hi): one run region per scan
+// wavefront in ctx->d_runs.  filter: keep only runs whose bucket this rank owns (a
+// bucket-sharded single context); index: the scan also builds the index
+// (fused: CAS into the cells; exchange: key records).
 template <int W>
 struct LaunchScan {
   static int run(mg_ctx* ctx, bool contain, uint64_t a_lo, uint64_t a_hi, uint32_t sgrid, bool filter,
