@@ -145,6 +145,11 @@ struct mg_ctx {
   unsigned long long* d_rcnt = nullptr;
   size_t rcnt_cap = 0;
   bool runs_counted = false;
+  // exchange-mode discovery probe: rows per (probe wavefront, destination
+  // rank), so routing the rows skips k_part's count pass (rows_counted)
+  unsigned long long* d_dcnt = nullptr;
+  size_t dcnt_cap = 0;
+  bool rows_counted = false;
   int packable = 0;                      // 1 << MG_KEYS | 1 << MG_RUNS | 1 << MG_ROWS
   unsigned long long* d_flat_cnt = nullptr;  // per-region counts of the received runs (probe input)
   size_t flat_cnt_cap = 0;

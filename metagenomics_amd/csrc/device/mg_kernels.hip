@@ -1510,6 +1510,12 @@ struct ProbeParams {
   int compact;                    // park the live items of sparse run batches (filled batches only)
   int share;                      // a block's wavefronts share its regions batch by batch (probe_share)
   const uint32_t* id;             // slot -> reference ID - 1 (nullptr: ID order); rows and superkeys carry IDs
+  // DCNT (exchange-mode discovery): rows stored per destination rank (the
+  // source ID's owner, k_part's OWN_SRC rule) into dst_cnt[gw * dst_ranks + d]
+  unsigned long long* dst_cnt;
+  uint32_t dst_ranks;
+  uint64_t n_ids;
+  double inv_n_ids;
 };
 
 // Which side of a self-symmetric (o = 2/3) discovery pair {a, b} emits it:
@@ -1551,11 +1557,26 @@ struct ProbeLds {
 #ifndef MG_PROBE_WAVES
 #define MG_PROBE_WAVES (MAXW <= 5 ? 4 : 1)
 #endif
-template <int MAXW, bool CONTAIN>
+// the owner rank of 1-based reference ID x1 (k_part's OWN_SRC rule,
+// (x1 P - 1) / n), the quotient estimated in double and corrected
+__device__ __forceinline__ uint32_t id_owner(uint32_t x1, uint32_t P, uint64_t n, double inv_n) {
+  const uint64_t x = (uint64_t)x1 * P - 1;
+  uint64_t q = (uint64_t)((double)x * inv_n);
+  while (q * n > x) --q;
+  while ((q + 1) * n <= x) ++q;
+  return (uint32_t)q;
+}
+
+// DCNT (exchange mode, P > 1): the rows each wavefront stores are also counted
+// per destination rank, so their routing needs no count pass (a separate
+// instantiation: the fused path's probe keeps its registers)
+template <int MAXW, bool CONTAIN, bool DCNT = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MG_PROBE_WAVES))) void k_probe(ProbeParams p) {
   using PL = ProbeLds<MAXW>;
   extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
+  __shared__ unsigned int s_dc[DCNT ? kWavesPerBlock * kWave : 1];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if constexpr (DCNT) s_dc[wv * kWave + lane] = 0u;
   unsigned char* base = reinterpret_cast<unsigned char*>(smem) + (size_t)wv * PL::bytes;
   uint64_t* s_a = reinterpret_cast<uint64_t*>(base + PL::o_a);
   uint64_t* s_pk = reinterpret_cast<uint64_t*>(base + PL::o_pk);
@@ -1690,6 +1711,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MG_PROBE
       const uint32_t tot = 2u * (uint32_t)(__popcll(b2) + __popcll(b4));
       if (tot) {
         if (cursor + tot <= p.reg_cap) {
+          if constexpr (DCNT) {
+            if (nrec) {  // nrec / 2 rows to the source's owner, as many twins to the partner's
+              atomicAdd(&s_dc[wv * kWave + id_owner(r0, p.dst_ranks, p.n_ids, p.inv_n_ids)], (unsigned)nrec / 2);
+              atomicAdd(&s_dc[wv * kWave + id_owner(t0, p.dst_ranks, p.n_ids, p.inv_n_ids)], (unsigned)nrec / 2);
+            }
+          }
           const uint32_t pr = 2u * (lane_prefix(b2) + lane_prefix(b4));
           uint3* d = reinterpret_cast<uint3*>(region + (cursor + pr) * 3);
           for (int rr = 0; rr < nrec; rr += 2) {
@@ -1989,6 +2016,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MG_PROBE
   }
   if (ncand && p.phase_limit > 6) verify(ncand);
   if (!CONTAIN && lane == 0) p.reg_cnt[gw] = cursor;
+  if constexpr (DCNT) {
+    wave_sync();
+    if ((uint32_t)lane < p.dst_ranks) p.dst_cnt[gw * p.dst_ranks + lane] = s_dc[wv * kWave + lane];
+  }
 }
 
 // Gather per-wavefront row regions into a contiguous array (copy-out path only).
@@ -3010,10 +3041,22 @@ struct LaunchProbe {
     pp.share = (!contain && ctx->probe_share) ? 1 : 0;
     pp.id = ctx->d_id;
     const size_t lds = (size_t)kWavesPerBlock * ProbeLds<W>::bytes;
-    if (contain)
+    const bool dcnt = !contain && ctx->xchg && ctx->nranks > 1 && ctx->nranks <= (uint32_t)kWave && ctx->n;
+    if (!contain) ctx->rows_counted = false;
+    if (dcnt) {  // the rows' routing takes these counts (mg_xchg_pack, MG_ROWS)
+      if (ensure(&ctx->d_dcnt, &ctx->dcnt_cap, ctx->nreg * ctx->nranks)) return -1;
+      pp.dst_cnt = ctx->d_dcnt;
+      pp.dst_ranks = ctx->nranks;
+      pp.n_ids = ctx->n;
+      pp.inv_n_ids = 1.0 / (double)ctx->n;
+      ctx->rows_counted = true;
+      allow_lds(k_probe<W, false, true>, lds);
+      hipLaunchKernelGGL((k_probe<W, false, true>), dim3(grid), dim3(kBlock), lds, ctx->stream, pp);
+    } else if (contain) {
       hipLaunchKernelGGL((k_probe<W, true>), dim3(grid), dim3(kBlock), lds, ctx->stream, pp);
-    else
+    } else {
       hipLaunchKernelGGL((k_probe<W, false>), dim3(grid), dim3(kBlock), lds, ctx->stream, pp);
+    }
     return hipGetLastError() == hipSuccess ? 0 : -1;
   }
 };
@@ -3211,7 +3254,7 @@ void mg_destroy(mg_ctx* ctx) {
                   ctx->d_digest, ctx->id_store[0], ctx->id_store[1], ctx->phys_store[0], ctx->phys_store[1],
                   ctx->d_tmp32, ctx->d_lay_k[0], ctx->d_lay_k[1], ctx->d_lay_v[0], ctx->d_lay_v[1], ctx->d_lay_tmp,
                   ctx->d_words_alt, ctx->d_len_alt, ctx->d_cbits, ctx->d_ccnt, ctx->d_lcells, ctx->d_lkcells,
-                  ctx->d_rhead, ctx->d_rstart, ctx->d_rcnt};
+                  ctx->d_rhead, ctx->d_rstart, ctx->d_rcnt, ctx->d_dcnt};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   for (auto& e : ctx->ev)
@@ -4398,6 +4441,8 @@ int mg_xchg_pack(mg_ctx* ctx, int what, void* dst, uint64_t slot, uint32_t round
   pp.cap = ctx->nreg ? ctx->rows_cap / ctx->nreg : 0;
   pp.cnt = ctx->d_seg;
   pp.nreg = ctx->n_rows ? ctx->nreg : 0;
+  if (ctx->rows_counted && pp.nreg)  // the probe counted them per rank: no count pass
+    return route_slots<OWN_SRC>(ctx, pp, dst, self_dst, slot, rounds, cnt, ctx->d_dcnt);
   return route_slots<OWN_SRC>(ctx, pp, dst, self_dst, slot, rounds, cnt);
 }
 
