@@ -145,6 +145,10 @@ struct mg_ctx {
   unsigned long long* d_rcnt = nullptr;
   size_t rcnt_cap = 0;
   bool runs_counted = false;
+  // mg_build_index leaves its timings (index_ms, shared_scan_ms) to be read once
+  // its events have completed (settle_index_times): no host round trip between
+  // the build and the probe
+  bool index_times_pending = false;
   // exchange-mode discovery probe: rows per (probe wavefront, destination
   // rank), so routing the rows skips k_part's count pass (rows_counted)
   unsigned long long* d_dcnt = nullptr;

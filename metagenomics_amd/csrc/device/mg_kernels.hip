@@ -3698,8 +3698,19 @@ struct LaunchScanRuns {
 // source-read range takes the separate index build + a scan of its slots)
 bool shared_scan(const mg_ctx* ctx) { return ctx->nranks == 1 && ctx->read_lo == 0 && ctx->read_hi == 0; }
 
+// mg_build_index's timings from its events (before a rescan records ev[6] / ev[7] again)
+int settle_index_times(mg_ctx* ctx) {
+  if (!ctx->index_times_pending) return 0;
+  MG_TRY(hipEventSynchronize(ctx->ev[1]));
+  ctx->t.index_ms = elapsed(ctx->ev[0], ctx->ev[1]);
+  ctx->shared_scan_ms = (!long_mode(ctx) && shared_scan(ctx) && ctx->n) ? elapsed(ctx->ev[6], ctx->ev[7]) : 0.f;
+  ctx->index_times_pending = false;
+  return 0;
+}
+
 // the shared scan's region counts settled (its overflow reruns a plain run scan)
 int ensure_scan(mg_ctx* ctx) {
+  if (settle_index_times(ctx)) return -1;
   if (ctx->scan_state == 2) return 0;
   if (ctx->scan_state == 1) {
     bool again = false;
@@ -3926,9 +3937,14 @@ int build_live_index_xchg(mg_ctx* ctx) {
   return 0;
 }
 
+// Discovery as the shared scan's first reader (equal lengths: no containment
+// pass ran) goes out before the scan's run counts are read: the probe reads at
+// most run_cap records of a region, and a region that overflowed is found with
+// the row counts, after which scan and probe rerun.  One host round trip per
+// step instead of two.
 int probe_shared(mg_ctx* ctx, bool contain) {
-  if (ensure_scan(ctx)) return -1;
-  for (int attempt = 0; attempt < 3; ++attempt) {
+  if (!(!contain && ctx->scan_state == 1) && ensure_scan(ctx)) return -1;
+  for (int attempt = 0; attempt < 4; ++attempt) {
     ctx->nreg = 0;
     MG_TRY(hipEventRecord(ctx->ev[8], ctx->stream));
     if (!contain && attempt == 0 && ctx->contained_done && build_live_index(ctx)) return -1;
@@ -3943,6 +3959,16 @@ int probe_shared(mg_ctx* ctx, bool contain) {
     if (dispatch_w<LaunchProbeShared>(ctx->maxw, ctx, contain)) return set_err(ctx, "probe launch failed");
     MG_TRY(hipEventRecord(ctx->ev[9], ctx->stream));
     if (contain) return 0;
+    if (ctx->scan_state == 1) {  // the scan's regions, settled now (the probe above may have cut them)
+      bool cut = false;
+      if (settle_runs(ctx, &cut)) return -1;
+      if (settle_index_times(ctx)) return -1;
+      ctx->scan_state = cut ? 0 : 2;
+      if (cut) {
+        if (ensure_scan(ctx)) return -1;
+        continue;
+      }
+    }
     bool again = false;
     if (settle_rows(ctx, &again)) return -1;
     if (!again) return 0;
@@ -4210,9 +4236,7 @@ int mg_build_index(mg_ctx* ctx, uint32_t min_overlap, uint32_t seed_k) {
     if (dispatch_w<LaunchIndex>(ctx->maxw, ctx)) return set_err(ctx, "index build launch failed");
   }
   MG_TRY(hipEventRecord(ctx->ev[1], ctx->stream));
-  MG_TRY(hipEventSynchronize(ctx->ev[1]));
-  ctx->t.index_ms = elapsed(ctx->ev[0], ctx->ev[1]);
-  ctx->shared_scan_ms = (!long_mode(ctx) && shared_scan(ctx) && ctx->n) ? elapsed(ctx->ev[6], ctx->ev[7]) : 0.f;
+  ctx->index_times_pending = true;  // (read by settle_index_times once the events completed)
   ctx->index_ready = true;
   return 0;
 }
@@ -4304,6 +4328,7 @@ int mg_find_overlaps(mg_ctx* ctx, uint64_t* n_rows) {
     if (long_probe(ctx, false, lo, hi)) return -1;
     MG_TRY(hipEventRecord(ctx->ev[5], ctx->stream));
     MG_TRY(hipEventSynchronize(ctx->ev[5]));
+    if (settle_index_times(ctx)) return -1;
     ctx->t.scan_ms = 0.f;
     ctx->t.sort_ms = 0.f;
     ctx->t.verify_ms = 0.f;
@@ -4317,6 +4342,7 @@ int mg_find_overlaps(mg_ctx* ctx, uint64_t* n_rows) {
   if (shared_scan(ctx) ? probe_shared(ctx, false) : run_discover(ctx, false)) return -1;
   MG_TRY(hipEventRecord(ctx->ev[5], ctx->stream));
   MG_TRY(hipEventSynchronize(ctx->ev[5]));
+  if (settle_index_times(ctx)) return -1;
   // the kernels' own events bracket the last launches (a resize retry included
   // in ev[4]..ev[5] is not kernel time)
   // scan kernel time (shared scan: measured at build time, part of index_ms)
@@ -4806,6 +4832,7 @@ int mg_super_digest(mg_ctx* ctx, uint64_t* out) {
 
 int mg_get_timings(const mg_ctx* ctx, mg_timings* t) {
   if (!ctx || !t) return -1;
+  if (settle_index_times(const_cast<mg_ctx*>(ctx))) return -1;
   *t = ctx->t;
   return 0;
 }

@@ -785,6 +785,29 @@ def test_live_index_forced(name):
         assert np.array_equal(rows_to_tuples(rows), want_rows), live
 
 
+@pytest.mark.parametrize("name", ["small", "tandem", "highdup", "mixed", "branchy"])
+def test_fused_run_region_overflow(name):
+    """The fused scan's run regions start far too small (option run_cap = 8):
+    equal lengths send the discovery probe out before the run counts are read
+    (probe_shared), so the cut regions are found with the row counts and scan
+    + probe rerun; mixed lengths settle the regions before the containment
+    probe.  Rows and superReadIDs equal the goldens on both steps of an engine
+    (the second step starts from the grown capacity)."""
+    meta = load_meta(name)
+    ds = Dataset.from_files([fixture_input(name)], meta["l"])
+    e = OverlapEngine(0)
+    try:
+        e.set_option("run_cap", 8)
+        for _ in range(2):
+            rows, sup = gpu_rows(e, ds, meta["l"])
+            assert np.array_equal(rows_to_tuples(rows), golden_rows(name))
+            assert {str(i): int(x) for i, x in enumerate(sup) if x} == meta["super"]
+        t = e.timings()
+        assert t["index_ms"] > 0 and t["probe_ms"] > 0
+    finally:
+        e.close()
+
+
 @pytest.mark.parametrize("name", ["small", "mixed", "tandem", "highdup", "tworead"])
 def test_replicated_index_source_shards(name):
     """Multi-GPU replicated mode (bench --multi replicated): every rank builds
