@@ -198,6 +198,7 @@ struct mg_ctx {
   uint64_t xkeys_n = 0;
   uint32_t xkey_cls = 0;       // 1: key = home cell << 1 | (o == 3) (the full table leaves out o = 3)
   uint32_t xkey_fs = 0;        // low fingerprint bits below the cell / class bits (chain_par)
+  bool xkey_par = false;       // the received records' cells are built by the parallel placement
   uint32_t* xkey_k = nullptr;  // the sorted records (one of d_xkk[] / d_kb) and the other buffer pair
   uint64_t* xkey_e = nullptr;
   uint32_t* xkey_k_alt = nullptr;

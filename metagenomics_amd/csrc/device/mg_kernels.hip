@@ -3847,7 +3847,8 @@ int check_cells(mg_ctx* ctx, const uint32_t* key, const uint64_t* ent, const uin
 // gshift / cshift / skip_odd: as k_cells_fill (classed keys: the full table
 // groups and skips by class, the coarse live table merges the classes)
 int build_cells(mg_ctx* ctx, const uint32_t* key, const uint64_t* ent, const unsigned long long* n_dev,
-                uint64_t n_host, uint64_t* cells, uint64_t cell_n, uint32_t gshift, uint32_t cshift, int skip_odd) {
+                uint64_t n_host, uint64_t* cells, uint64_t cell_n, uint32_t gshift, uint32_t cshift, int skip_odd,
+                bool par) {
   MG_TRY(hipMemsetAsync(cells, 0xFF, cell_n * kCell * sizeof(uint64_t), ctx->stream));  // kEmpty
   if (!n_host) return 0;
   const uint32_t grid = (uint32_t)std::max<uint64_t>(
@@ -3855,7 +3856,7 @@ int build_cells(mg_ctx* ctx, const uint32_t* key, const uint64_t* ent, const uns
   hipLaunchKernelGGL(k_cells_fill, dim3(grid), dim3(kBlock), 0, ctx->stream, key, ent, n_dev, n_host, gshift, cshift,
                      skip_odd, cells);
   MG_TRY(hipGetLastError());
-  if (!ctx->chain_par) {
+  if (!par) {
     hipLaunchKernelGGL(k_cells_chain, dim3(grid), dim3(kBlock), 0, ctx->stream, key, ent, n_dev, n_host, gshift,
                        cshift, skip_odd, cells, cell_n);
     MG_TRY(hipGetLastError());
@@ -3929,7 +3930,7 @@ int build_live_index_xchg(mg_ctx* ctx) {
     }
   }
   const uint32_t lsh = sft + ctx->xkey_cls + ctx->xkey_fs;  // (classes merged)
-  if (build_cells(ctx, lk, le, ctx->d_nlive, n, ctx->d_lcells, live_n, lsh, lsh, 0)) return -1;
+  if (build_cells(ctx, lk, le, ctx->d_nlive, n, ctx->d_lcells, live_n, lsh, lsh, 0, ctx->xkey_par)) return -1;
   ctx->live_shift = sft;
   ctx->live_cells = live_n;
   ctx->live_coarse = true;
@@ -4527,6 +4528,11 @@ int mg_xchg_insert_keys(mg_ctx* ctx, const void* recv, uint64_t slot, uint32_t r
   uint32_t fs = ctx->chain_par ? fp_sort_bits((uint32_t)hb) : 0u;
   if (ctx->xchg_fs >= 0) fs = std::min<uint32_t>((uint32_t)ctx->xchg_fs, hb < 32 ? 32u - (uint32_t)hb : 0u);
   ctx->xkey_fs = fs;
+  // the parallel placement needs a group's fingerprints mostly sorted: with
+  // fewer than 3 spare bits in the last digit (one rank at C3: none) runs of
+  // different fingerprints interleave, and one walk per group is faster (one
+  // RCCL rank, index 4.50 vs 4.68-4.75 ms, profiles/r04x2_ab_chain_par_xchg1.txt)
+  ctx->xkey_par = ctx->chain_par && (fs >= 3 || ctx->xchg_fs >= 0);
   if ((ctx->xkey_cls || fs) && n) {
     hipLaunchKernelGGL(k_key_class, dim3((uint32_t)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, ctx->stream, k0, e0,
                        n, ctx->xkey_cls, fs);
@@ -4548,7 +4554,7 @@ int mg_xchg_insert_keys(mg_ctx* ctx, const void* recv, uint64_t slot, uint32_t r
   }
   ctx->xkeys_n = n;
   if (build_cells(ctx, ctx->xkey_k, ctx->xkey_e, nullptr, n, ctx->d_cells, ctx->cell_n, fs, fs + ctx->xkey_cls,
-                  ctx->xkey_cls))
+                  ctx->xkey_cls, ctx->xkey_par))
     return -1;
   MG_TRY(hipEventRecord(ctx->ev[1], ctx->stream));
   ctx->index_ready = true;
