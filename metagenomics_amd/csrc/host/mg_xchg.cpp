@@ -114,6 +114,116 @@ void RcclExchange::allgather_u64(const uint64_t* send, uint64_t* recv, size_t n,
   nccl_check(ncclAllGather(send, recv, n, ncclUint64, comm_, s), "ncclAllGather");
 }
 
+LocalGroup::LocalGroup(int world, int timeout_ms)
+    : world_(world), timeout_ms_(timeout_ms), ptrs_(world, nullptr), dbl_(world, 0.0) {}
+
+void LocalGroup::barrier() {
+  std::unique_lock<std::mutex> lk(mu_);
+  if (failed_) throw std::runtime_error("a peer rank failed");
+  const uint64_t gen = gen_;
+  if (++arrived_ == world_) {
+    arrived_ = 0;
+    ++gen_;
+    cv_.notify_all();
+    return;
+  }
+  if (!cv_.wait_for(lk, std::chrono::milliseconds(timeout_ms_), [&] { return gen_ != gen || failed_; })) {
+    failed_ = true;
+    cv_.notify_all();
+    throw std::runtime_error("local barrier: a rank never arrived");
+  }
+  if (gen_ == gen) throw std::runtime_error("a peer rank failed");
+}
+
+void LocalGroup::abort() {
+  std::lock_guard<std::mutex> lk(mu_);
+  failed_ = true;
+  cv_.notify_all();
+}
+
+std::vector<const void*> LocalTransport::exchange_ptr(const void* p, hipStream_t s) {
+  hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");  // p's producer (the pack) is done
+  g_.slot(rank_) = p;
+  g_.barrier();
+  std::vector<const void*> v(g_.world());
+  for (int r = 0; r < g_.world(); ++r) v[r] = g_.slot(r);
+  return v;
+}
+
+void LocalTransport::finish(hipStream_t s) {
+  hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
+  g_.barrier();  // no rank reuses a buffer a peer may still be reading
+}
+
+void LocalTransport::all_to_all_slots(const uint8_t* send, uint8_t* recv, uint64_t sb, uint32_t rounds,
+                                      hipStream_t s) {
+  const int P = g_.world();
+  if (P == 1) return;
+  const std::vector<const void*> peer = exchange_ptr(send, s);
+  for (int p = 0; p < P; ++p) {  // pull peer p's stream to this rank: its round t slot sits at (t P + me) sb
+    if (p == rank_) continue;
+    const uint8_t* src = static_cast<const uint8_t*>(peer[p]);
+    for (uint32_t t = 0; t < rounds; ++t)
+      hip_check(hipMemcpyAsync(recv + ((uint64_t)t * P + p) * sb, src + ((uint64_t)t * P + rank_) * sb, sb,
+                               hipMemcpyDeviceToDevice, s),
+                "slot copy");
+  }
+  finish(s);
+}
+
+void LocalTransport::all_to_all_u64(const uint64_t* send, uint64_t* recv, hipStream_t s) {
+  const int P = g_.world();
+  const std::vector<const void*> peer = exchange_ptr(send, s);
+  for (int p = 0; p < P; ++p)
+    hip_check(hipMemcpyAsync(recv + p, static_cast<const uint64_t*>(peer[p]) + rank_, sizeof(uint64_t),
+                             hipMemcpyDeviceToDevice, s),
+              "count copy");
+  finish(s);
+}
+
+void LocalTransport::allreduce_max_u64(uint64_t* buf, size_t n, hipStream_t s) {
+  const int P = g_.world();
+  if (P == 1) return;
+  const std::vector<const void*> peer = exchange_ptr(buf, s);
+  std::vector<uint64_t*> ptrs(P);
+  for (int r = 0; r < P; ++r) ptrs[r] = const_cast<uint64_t*>(static_cast<const uint64_t*>(peer[r]));
+  // this rank reduces its slice of every array and writes the maximum to all of them
+  local_max_u64(ptrs.data(), P, (uint64_t)n * rank_ / P, (uint64_t)n * (rank_ + 1) / P, s);
+  finish(s);
+}
+
+void LocalTransport::allreduce_max_f64(double* buf, size_t n, hipStream_t s) {
+  const int P = g_.world();
+  if (P == 1) return;
+  std::vector<double> h(n);
+  hip_check(hipMemcpyAsync(h.data(), buf, n * sizeof(double), hipMemcpyDeviceToHost, s), "D2H");
+  hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
+  for (size_t i = 0; i < n; ++i) {
+    g_.scalars()[rank_] = h[i];
+    g_.barrier();
+    double m = g_.scalars()[0];
+    for (int r = 1; r < P; ++r) m = std::max(m, g_.scalars()[r]);
+    g_.barrier();
+    h[i] = m;
+  }
+  hip_check(hipMemcpyAsync(buf, h.data(), n * sizeof(double), hipMemcpyHostToDevice, s), "H2D");
+  hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
+}
+
+void LocalTransport::allgather_u64(const uint64_t* send, uint64_t* recv, size_t n, hipStream_t s) {
+  const int P = g_.world();
+  const std::vector<const void*> peer = exchange_ptr(send, s);
+  for (int r = 0; r < P; ++r)
+    hip_check(hipMemcpyAsync(recv + (size_t)r * n, peer[r], n * sizeof(uint64_t), hipMemcpyDeviceToDevice, s),
+              "allgather copy");
+  finish(s);
+}
+
+void LocalTransport::barrier(hipStream_t s) {
+  hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
+  g_.barrier();
+}
+
 void slot_geometry(uint64_t cap, int world, uint32_t rec, uint64_t chunk, uint64_t* slot, uint32_t* rounds) {
   // the probe tiles a slot by its divisors: large streams take whole 1024-record regions
   const uint64_t kAlign = cap >= 64 * 1024 ? 1024 : 64;
@@ -123,7 +233,7 @@ void slot_geometry(uint64_t cap, int world, uint32_t rec, uint64_t chunk, uint64
   *rounds = (uint32_t)((want + *slot - 1) / *slot);
 }
 
-XchgStep::XchgStep(mg_ctx* ctx, RcclExchange& x, uint32_t l, uint32_t k, uint64_t chunk)
+XchgStep::XchgStep(mg_ctx* ctx, Transport& x, uint32_t l, uint32_t k, uint64_t chunk)
     : ctx_(ctx), x_(x), l_(l), k_(k), chunk_(chunk), s_((hipStream_t)mg_stream(ctx)) {
   check(mg_xchg_caps(ctx_, l_, k_, caps_), "mg_xchg_caps");
 }
@@ -134,6 +244,10 @@ XchgStep::~XchgStep() {
       if (p) (void)hipFree(p);
   if (superkey_) (void)hipFree(superkey_);
   if (maxbuf_) (void)hipFree(maxbuf_);
+}
+
+void XchgStep::scale_caps(double f) {
+  for (uint64_t& c : caps_) c = std::max<uint64_t>(1, (uint64_t)((double)c * f));
 }
 
 void XchgStep::check(int rc, const char* what) {

@@ -1,15 +1,24 @@
 // mg_xchg.hpp — the exchange mode driven from
-// C++ over RCCL: one process per GPU, the same step as
-// metagenomics_amd/sharded.py (bucket-range index, key / run / row streams in
-// the slot layout of include/mg_overlap.h, MAX all-reduce of the containment
-// keys), with the collectives issued by this host code on the context's own
-// HIP stream.  Linked into the mg_overlap CLI (-xchg), not into libmgovl.so.
+// C++: one rank per GPU, the same step as metagenomics_amd/sharded.py
+// (bucket-range index, key / run / row streams in the slot layout of
+// include/mg_overlap.h, MAX all-reduce of the containment keys), with the
+// collectives issued by this host code on the context's own HIP stream.
+// Linked into the mg_overlap CLI (-xchg), not into libmgovl.so.
+//
+// The step talks to its peers through a Transport:
+//   RcclExchange    one process per GPU over RCCL (xGMI): the N-GPU runs;
+//   LocalTransport  P ranks as threads of one process, each with its own
+//                   mg_ctx on one device, slots moved by device copies between
+//                   the contexts' buffers (mg_xchg_local.hip): runs the same
+//                   XchgStep code at P > 1 on a one-GPU box (-xchg-sim P).
 #ifndef MG_XCHG_HPP_
 #define MG_XCHG_HPP_
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <condition_variable>
 #include <cstdint>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -17,30 +26,98 @@
 
 namespace mg {
 
-// One RCCL communicator over the ranks of one node.  The unique id travels
-// over TCP: rank 0 listens on addr:port and hands it to the others.
-class RcclExchange {
+// The collectives the exchange step needs.  Every call is enqueued on (or
+// synchronises) the caller's stream s; buffers are device memory.
+class Transport {
  public:
-  RcclExchange(int rank, int world, int device, const std::string& addr, int port);
-  ~RcclExchange();
-  int rank() const { return rank_; }
-  int world() const { return world_; }
+  virtual ~Transport() = default;
+  virtual int rank() const = 0;
+  virtual int world() const = 0;
   // every peer's slot of every round (slot_bytes each) from send to recv;
   // this rank's own slots are already in recv (mg_xchg_pack's self_dst)
-  void all_to_all_slots(const uint8_t* send, uint8_t* recv, uint64_t slot_bytes, uint32_t rounds, hipStream_t s);
+  virtual void all_to_all_slots(const uint8_t* send, uint8_t* recv, uint64_t slot_bytes, uint32_t rounds,
+                                hipStream_t s) = 0;
   // recv[s] = what rank s sent to this rank (send[r] = what this rank sends to r)
-  void all_to_all_u64(const uint64_t* send, uint64_t* recv, hipStream_t s);
-  void allreduce_max_u64(uint64_t* buf, size_t n, hipStream_t s);
-  void allreduce_max_f64(double* buf, size_t n, hipStream_t s);
-  void allgather_u64(const uint64_t* send, uint64_t* recv, size_t n, hipStream_t s);
+  virtual void all_to_all_u64(const uint64_t* send, uint64_t* recv, hipStream_t s) = 0;
+  virtual void allreduce_max_u64(uint64_t* buf, size_t n, hipStream_t s) = 0;
+  virtual void allreduce_max_f64(double* buf, size_t n, hipStream_t s) = 0;
+  // recv[r * n + i] = rank r's send[i]
+  virtual void allgather_u64(const uint64_t* send, uint64_t* recv, size_t n, hipStream_t s) = 0;
   // every rank's work on s done
-  void barrier(hipStream_t s);
+  virtual void barrier(hipStream_t s) = 0;
+};
+
+// One RCCL communicator over the ranks of one node.  The unique id travels
+// over TCP: rank 0 listens on addr:port and hands it to the others.
+class RcclExchange : public Transport {
+ public:
+  RcclExchange(int rank, int world, int device, const std::string& addr, int port);
+  ~RcclExchange() override;
+  int rank() const override { return rank_; }
+  int world() const override { return world_; }
+  void all_to_all_slots(const uint8_t* send, uint8_t* recv, uint64_t slot_bytes, uint32_t rounds,
+                        hipStream_t s) override;
+  void all_to_all_u64(const uint64_t* send, uint64_t* recv, hipStream_t s) override;
+  void allreduce_max_u64(uint64_t* buf, size_t n, hipStream_t s) override;
+  void allreduce_max_f64(double* buf, size_t n, hipStream_t s) override;
+  void allgather_u64(const uint64_t* send, uint64_t* recv, size_t n, hipStream_t s) override;
+  void barrier(hipStream_t s) override;
 
  private:
   int rank_, world_;
   ncclComm_t comm_ = nullptr;
   double* flag_ = nullptr;
 };
+
+// The ranks of one process (threads), sharing one device.  A collective is
+// "publish my buffer; barrier; pull from the peers' buffers on my stream;
+// synchronise; barrier", so a buffer is never reused while a peer reads it.
+// A rank that fails calls abort(): every rank blocked in (or later entering) a
+// barrier then throws instead of waiting for it.
+class LocalGroup {
+ public:
+  explicit LocalGroup(int world, int timeout_ms = 600000);
+  int world() const { return world_; }
+  void barrier();  // throws on abort() or after timeout_ms
+  void abort();
+  const void*& slot(int rank) { return ptrs_[rank]; }
+  std::vector<double>& scalars() { return dbl_; }
+
+ private:
+  int world_, timeout_ms_;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  int arrived_ = 0;
+  uint64_t gen_ = 0;
+  bool failed_ = false;
+  std::vector<const void*> ptrs_;
+  std::vector<double> dbl_;
+};
+
+class LocalTransport : public Transport {
+ public:
+  LocalTransport(LocalGroup& g, int rank) : g_(g), rank_(rank) {}
+  int rank() const override { return rank_; }
+  int world() const override { return g_.world(); }
+  void all_to_all_slots(const uint8_t* send, uint8_t* recv, uint64_t slot_bytes, uint32_t rounds,
+                        hipStream_t s) override;
+  void all_to_all_u64(const uint64_t* send, uint64_t* recv, hipStream_t s) override;
+  void allreduce_max_u64(uint64_t* buf, size_t n, hipStream_t s) override;
+  void allreduce_max_f64(double* buf, size_t n, hipStream_t s) override;
+  void allgather_u64(const uint64_t* send, uint64_t* recv, size_t n, hipStream_t s) override;
+  void barrier(hipStream_t s) override;
+
+ private:
+  // publish p, wait for every rank, return the peers' pointers
+  std::vector<const void*> exchange_ptr(const void* p, hipStream_t s);
+  void finish(hipStream_t s);  // own copies done, then every rank's
+  LocalGroup& g_;
+  int rank_;
+};
+
+// dst[i] = src[i] = max over the P arrays ptrs[r][i] for i in [lo, hi) (every
+// array gets the maximum); enqueued on s (mg_xchg_local.hip)
+void local_max_u64(uint64_t* const* ptrs, int P, uint64_t lo, uint64_t hi, hipStream_t s);
 
 // Slot geometry of one stream kind (sharded.py slot_geometry): slot records
 // per peer per round (a multiple of 64) and the number of rounds for `cap`
@@ -52,8 +129,11 @@ void slot_geometry(uint64_t cap, int world, uint32_t rec_bytes, uint64_t chunk_b
 // (identical on every rank, grown after an overflow) persist from step to step.
 class XchgStep {
  public:
-  XchgStep(mg_ctx* ctx, RcclExchange& x, uint32_t min_overlap, uint32_t seed_k, uint64_t chunk_bytes = 256ull << 20);
+  XchgStep(mg_ctx* ctx, Transport& x, uint32_t min_overlap, uint32_t seed_k, uint64_t chunk_bytes = 256ull << 20);
   ~XchgStep();
+  // scale the first capacity estimates (tests: a small factor forces a cut
+  // stream and the rerun path); call before the first run()
+  void scale_caps(double f);
   // runs the step (rerun with grown capacities after an overflow); rows owned
   // by this rank (by src ID) stay in the rows receive buffer.  Returns the
   // number of reruns; throws std::runtime_error on a library error.
@@ -62,6 +142,7 @@ class XchgStep {
   // digest (mg_rows_digest formula) of this rank's rows
   void rows_digest(uint64_t out[4]);
   bool contained() const { return contained_; }
+  const uint64_t* caps() const { return caps_; }
 
  private:
   struct Stream {
@@ -77,7 +158,7 @@ class XchgStep {
   void ensure(Stream& st, int kind);
   void check(int rc, const char* what);
   mg_ctx* ctx_;
-  RcclExchange& x_;
+  Transport& x_;
   uint32_t l_, k_;
   uint64_t chunk_;
   hipStream_t s_;
