@@ -136,6 +136,10 @@ struct mg_ctx {
   // leaves key records (d_kb / d_ke) and the run regions of this rank's
   // sources; packable = bit mask of what mg_xchg_pack can route now
   bool xchg = false;                     // the context's current build is an exchange-mode build
+  // one rank (P = 1, no source range): mg_xchg_begin runs the fused build and
+  // the exchange calls delegate to the fused probes (option "xchg_fused1")
+  bool xchg_fused = false;
+  bool xchg_fused1 = true;
   uint64_t xchg_lo = 0, xchg_hi = 0;     // its source reads
   unsigned long long* d_blk = nullptr;   // routing: per-(block, rank) counts / offsets
   size_t blk_cap = 0;

@@ -458,7 +458,7 @@ struct LaunchPrefixContain {
     if (!ctx->n) return 0;
     hipLaunchKernelGGL(k_prefix_contain<W>, dim3((uint32_t)((ctx->n + kBlock - 1) / kBlock)), dim3(kBlock), 0,
                        ctx->stream, ctx->d_words, ctx->d_len, ctx->d_key0, ctx->d_cells, ctx->cell_n, ctx->nb_log2,
-                       ctx->n, ctx->d_superkey, ctx->d_id);
+                       ctx->n, ctx->superkey, ctx->d_id);
     return hipGetLastError() == hipSuccess ? 0 : -1;
   }
 };
@@ -2992,6 +2992,10 @@ struct LaunchProbe {
   static int run(mg_ctx* ctx, bool contain, const ulonglong2* runs, const unsigned long long* run_cnt,
                  uint64_t run_cap, uint64_t run_regions, uint32_t grid, const uint32_t* src_super = nullptr,
                  uint64_t src_lo = 0, uint64_t src_hi = 0) {
+    // discovery reads the o = 3 keys: a full table built without them (index_o3
+    // = false) is only exact behind the live index that has them
+    if (!contain && !ctx->index_o3 && !ctx->live_ready)
+      return set_err(ctx, "discovery probe: the full index leaves out the o = 3 keys and no live index was built");
     ctx->nreg = (uint64_t)grid * kWavesPerBlock;  // probe wavefronts = row regions
     ProbeParams pp{};
     pp.words = ctx->d_words;
@@ -3421,6 +3425,10 @@ int mg_set_option(mg_ctx* ctx, const char* name, int64_t value) {
   }
   if (!strcmp(name, "phase_limit")) {  // diagnostics: stop the probe after a phase (1: the scan files no keys)
     ctx->phase_limit = value > 0 ? (int)value : 99;
+    return 0;
+  }
+  if (!strcmp(name, "xchg_fused1")) {  // exchange mode at one rank: the fused build (default 1)
+    ctx->xchg_fused1 = value != 0;
     return 0;
   }
   if (!strcmp(name, "check_cells")) {  // diagnostics: verify every sorted cell build (build_cells)
@@ -4384,6 +4392,17 @@ int mg_xchg_begin(mg_ctx* ctx, uint32_t min_overlap, uint32_t seed_k) {
   if (ctx->nranks > (uint32_t)kMaxRanks) return set_err(ctx, "at most 64 ranks");
   if (long_mode(ctx)) return set_err(ctx, "reads longer than 1024 bp: exchange mode not supported (use the replicated mode)");
   if (ensure_layout_range(ctx)) return -1;
+  ctx->xchg_fused = false;
+  if (ctx->nranks == 1 && shared_scan(ctx) && ctx->xchg_fused1) {
+    // one rank: no key leaves it, so the step is the fused path's (the CAS
+    // inserts ride on the window scan, k_scan<INDEX>, instead of key records
+    // sorted and filed by mg_xchg_insert_keys); the mg_xchg_* calls that
+    // follow delegate to its containment and discovery
+    if (mg_build_index(ctx, min_overlap, seed_k)) return -1;
+    ctx->xchg_fused = true;
+    ctx->packable = (1 << MG_KEYS) | (1 << MG_RUNS);
+    return 0;
+  }
   MG_TRY(hipEventRecord(ctx->ev[0], ctx->stream));
   if (setup_index(ctx, min_overlap, seed_k, false)) return -1;
   // this rank's cells: mg_xchg_insert_keys writes every one of them (no clear)
@@ -4476,7 +4495,8 @@ int mg_xchg_pack(mg_ctx* ctx, int what, void* dst, uint64_t slot, uint32_t round
 int mg_xchg_insert_keys(mg_ctx* ctx, const void* recv, uint64_t slot, uint32_t rounds, const uint64_t* counts) {
   if (!ctx) return -1;
   MG_TRY(hipSetDevice(ctx->device));
-  if (!ctx->xchg) return set_err(ctx, "mg_xchg_begin must run first");
+  if (!ctx->xchg && !ctx->xchg_fused) return set_err(ctx, "mg_xchg_begin must run first");
+  if (ctx->xchg_fused) return 0;  // one rank: the fused build filed the keys already
   const uint32_t P = ctx->nranks;
   uint64_t n = 0;
   uint32_t* k0 = nullptr;
@@ -4561,12 +4581,46 @@ int mg_xchg_insert_keys(mg_ctx* ctx, const void* recv, uint64_t slot, uint32_t r
   return 0;
 }
 
+// One rank's exchange step on the fused build (mg_xchg_begin, xchg_fused): the
+// probes of mg_mark_contained / mg_find_overlaps over the scan's own run
+// regions; the superkey array is mg_begin_contained's, and mg_finalize_contained
+// turns it into superReadIDs as in the exchange step
+static int xchg_fused_probe(mg_ctx* ctx, bool contain) {
+  if (contain) {
+    MG_TRY(hipEventRecord(ctx->ev[2], ctx->stream));
+    if (!ctx->n) return 0;
+    // prefix containments first: what they mark is skipped as a container
+    if (ctx->key0_ready && dispatch_w<LaunchPrefixContain>(ctx->maxw, ctx))
+      return set_err(ctx, "prefix containment launch failed");
+    if (probe_shared(ctx, true)) return -1;
+    MG_TRY(hipEventRecord(ctx->ev[3], ctx->stream));
+    return 0;
+  }
+  if (ensure_rows(ctx, ctx->n)) return -1;
+  MG_TRY(hipEventRecord(ctx->ev[4], ctx->stream));
+  if (probe_shared(ctx, false)) return -1;
+  MG_TRY(hipEventRecord(ctx->ev[5], ctx->stream));
+  MG_TRY(hipEventSynchronize(ctx->ev[5]));
+  if (settle_index_times(ctx)) return -1;
+  ctx->t.scan_ms = ctx->shared_scan_ms;
+  ctx->t.sort_ms = 0.f;
+  ctx->t.contained_ms = ctx->minlen != ctx->maxlen ? elapsed(ctx->ev[2], ctx->ev[3]) : 0.f;
+  ctx->t.probe_ms = elapsed(ctx->ev[8], ctx->ev[9]);
+  ctx->t.verify_ms = 0.f;
+  ctx->t.overlap_ms = ctx->t.probe_ms;
+  ctx->t.total_ms = elapsed(ctx->ev[0], ctx->ev[5]);
+  read_stats(ctx, ctx->n);
+  ctx->packable |= 1 << MG_ROWS;
+  return 0;
+}
+
 int mg_xchg_probe(mg_ctx* ctx, int contain, const void* recv, uint64_t slot, uint32_t rounds, const uint64_t* counts) {
   if (!ctx) return -1;
   MG_TRY(hipSetDevice(ctx->device));
-  if (!ctx->xchg || !ctx->index_ready) return set_err(ctx, "mg_xchg_insert_keys must run first");
+  if ((!ctx->xchg && !ctx->xchg_fused) || !ctx->index_ready) return set_err(ctx, "mg_xchg_insert_keys must run first");
   if (contain && !ctx->superkey) return set_err(ctx, "mg_begin_contained must run first (lengths differ)");
   if (!contain && !ctx->contained_done) return set_err(ctx, "containment must be settled first (mg_finalize_contained)");
+  if (ctx->xchg_fused) return xchg_fused_probe(ctx, contain != 0);
   if (ctx->nranks > 1 && (uint64_t)rounds * slot && (!recv || !counts)) return set_err(ctx, "mg_xchg_probe: null buffer");
   // the first probe of the step sets up the received runs (both probes read them)
   if (!ctx->xruns_ready && prepare_xruns(ctx, recv, slot, rounds, reinterpret_cast<const unsigned long long*>(counts)))

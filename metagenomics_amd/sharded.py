@@ -359,26 +359,41 @@ def _replicated_step(engines, xchg, min_overlap, seed_k, want_super):
     whole index with the long-read kernels and discovers from its source-read
     range; no data-path collective).  Every rank holds the rows + twins of its
     sources' discoveries; their union is the reference multiset.  The engines
-    are re-sharded to their source ranges (set_shard(0, 1, lo, hi))."""
+    run this step on their source ranges (set_shard(0, 1, lo, hi)) and get their
+    bucket-range shards (set_shard(rank, world)) back at its end.  ms splits the
+    wall into index / contained / overlap like the exchange step's."""
     if not _warned_long[0]:
         print(f"[sharded] reads longer than {EXCHANGE_MAX_BP} bp: the exchange mode's kernels stop there; "
               "this step runs the replicated mode (whole index per rank, source-read shards, no data-path "
               "collective)", flush=True)
         _warned_long[0] = True
     P = xchg.world
-    t0 = time.perf_counter()
-    host_rows, n_rows, sup = [], [], None
-    for i, (e, r) in enumerate(zip(engines, xchg.ranks)):
-        lo, hi = source_range(e.n_reads, r, P)
-        e.set_shard(0, 1, lo, hi if hi > lo else lo)
-        e.build_index(min_overlap, seed_k)
-        s = e.mark_contained(copy=want_super and i == 0)
-        sup = s if s is not None else sup
-        n = e.find_overlaps() if hi > lo else 0  # (read_hi == read_lo == 0 would mean "all")
-        host_rows.append(e.rows(n) if n else np.zeros(0, dtype=EDGE_DTYPE))
-        n_rows.append(n)
-    xchg.barrier()
-    ms = {"index": 0.0, "contained": 0.0, "overlap": (time.perf_counter() - t0) * 1e3}
+    ranges = [source_range(e.n_reads, r, P) for e, r in zip(engines, xchg.ranks)]
+    ms = {}
+    sup = None
+    try:
+        t0 = time.perf_counter()
+        for e, (lo, hi) in zip(engines, ranges):
+            e.set_shard(0, 1, lo, hi if hi > lo else lo)
+            e.build_index(min_overlap, seed_k)
+        xchg.sync()
+        t1 = time.perf_counter()
+        for i, e in enumerate(engines):
+            s = e.mark_contained(copy=want_super and i == 0)
+            sup = s if s is not None else sup
+        xchg.sync()
+        t2 = time.perf_counter()
+        n_rows = [e.find_overlaps() if hi > lo else 0  # (read_hi == read_lo == 0 would mean "all")
+                  for e, (lo, hi) in zip(engines, ranges)]
+        xchg.barrier()
+        t3 = time.perf_counter()
+        host_rows = [e.rows(n) if n else np.zeros(0, dtype=EDGE_DTYPE) for e, n in zip(engines, n_rows)]
+    finally:
+        # give the engines back the bucket-range shards the caller set up (set_shard(rank, world)),
+        # so a later step with short reads runs the exchange mode with the right routing
+        for e, r in zip(engines, xchg.ranks):
+            e.set_shard(r, P, 0, 0)
+    ms = {"index": (t1 - t0) * 1e3, "contained": (t2 - t1) * 1e3, "overlap": (t3 - t2) * 1e3}
     return ShardResult(rows=[], ms=ms, contained=bool(engines[0].lengths_differ), super_read_id=sup,
                        n_rows=n_rows, host_rows=host_rows, mode="replicated")
 

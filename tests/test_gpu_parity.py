@@ -368,7 +368,8 @@ def test_exchange_mode_containment_paths(prefix):
     ("highdup", 4, {"nb_log2": 16, "chain_par": 0}), ("mixed", 3, {"chain_par": 0}),
     ("highdup", 2, {"nb_log2": 10}), ("tandem", 3, {"nb_log2": 10}),
     ("small", 2, {"check_cells": 1}), ("highdup", 3, {"check_cells": 1, "nb_log2": 10}),
-    ("mixed", 3, {"check_cells": 1, "nb_log2": 16}), ("highdup", 2, {"check_cells": 1, "xchg_fs": 0})])
+    ("mixed", 3, {"check_cells": 1, "nb_log2": 16}), ("highdup", 2, {"check_cells": 1, "xchg_fs": 0}),
+    ("mixed", 1, {"xchg_fused1": 0}), ("highdup", 1, {"xchg_fused1": 0}), ("dirty", 1, {"xchg_fused1": 0})])
 def test_exchange_mode_options(name, world, opts):
     """Exchange-mode variants against the reference: the discovery index of the
     uncontained reads (build_live_index_xchg: the rank's cells coarsened, live
@@ -381,7 +382,9 @@ def test_exchange_mode_options(name, world, opts):
     small directories whose chains run long (nb_log2 = 10), and the table
     checker (check_cells: every record found from its home, for the full table
     and the coarse live table; xchg_fs = 0: no fingerprint bits in the sort, the
-    runs of different fingerprints interleave)."""
+    runs of different fingerprints interleave), and one rank on the exchange
+    path's own key build (xchg_fused1 = 0; by default one rank takes the fused
+    build: no key leaves it)."""
     meta = load_meta(name)
     ds = Dataset.from_files([fixture_input(name)], meta["l"])
     rows, sup = exchange_rows(ds, meta["l"], world, opts=dict(opts, stats=1))

@@ -206,11 +206,24 @@ def test_long_reads_exchange_step_falls_back(world):
         e.upload(ds)
         engines.append(e)
     assert max(e.max_len for e in engines) > 1024
-    res = sharded_step(engines, LocalExchange(world, torch.device("cuda:0")), l, 0, want_super=True)
+    xchg = LocalExchange(world, torch.device("cuda:0"))
+    res = sharded_step(engines, xchg, l, 0, want_super=True)
     assert res.mode == "replicated"
+    assert set(res.ms) == {"index", "contained", "overlap"} and res.ms["index"] > 0
     rows = np.concatenate([res.rows_numpy(r) for r in range(world)])
     assert sum(res.n_rows) == rows.shape[0]
-    for e in engines:
-        e.close()
     assert np.array_equal(rows_to_tuples(rows), golden_rows("longreads"))
     assert {str(i): int(x) for i, x in enumerate(res.super_read_id) if x} == meta["super"]
+    # the same engines then take a short-read set: the fallback gave them their
+    # bucket-range shards back, so this step is a real exchange step
+    m2 = load_meta("mixed")
+    ds2 = Dataset.from_files([fixture_input("mixed")], m2["l"])
+    for e in engines:
+        e.upload(ds2)
+    res2 = sharded_step(engines, xchg, m2["l"], 0, want_super=True)
+    assert res2.mode == "exchange"
+    rows2 = np.concatenate([res2.rows_numpy(r) for r in range(world)])
+    for e in engines:
+        e.close()
+    assert np.array_equal(rows_to_tuples(rows2), golden_rows("mixed"))
+    assert {str(i): int(x) for i, x in enumerate(res2.super_read_id) if x} == m2["super"]

@@ -87,3 +87,61 @@ def test_rendezvous_missing_peer_times_out():
 def test_rendezvous_missing_rank0_times_out():
     rcs, _ = _run(2, "127.0.0.1", os.urandom(32), timeout_ms=1000, skip=(0,))
     assert rcs[1] == -4
+
+
+def _strays(port, stop, kinds):
+    """Connections to rank 0's port that are not ranks: silent, garbage, a duplicate rank."""
+    import struct
+
+    socks = []
+    while not stop.is_set() and len(socks) < len(kinds):
+        k = kinds[len(socks)]
+        try:
+            s = socket.create_connection(("127.0.0.1", port), timeout=0.2)
+        except OSError:
+            time.sleep(0.02)
+            continue
+        if k == "garbage":
+            s.sendall(b"GET / HTTP/1.0\r\n\r\n")
+        elif k == "dup":
+            s.sendall(struct.pack("<II", 0x4D47525A, 1))
+        elif k == "rank0":
+            s.sendall(struct.pack("<II", 0x4D47525A, 0))
+        socks.append(s)
+    stop.wait(10)
+    for s in socks:
+        s.close()
+
+
+@pytest.mark.parametrize("kinds", [("silent",), ("garbage", "rank0"), ("dup", "silent", "garbage")])
+def test_rendezvous_ignores_stray_connections(kinds):
+    """A port probe or a health check that connects before the ranks does not use
+    up a rank's place (rank 0 checks each peer's header and serves every rank once)."""
+    f = _lib()
+    world, payload = 3, os.urandom(128)
+    port = _free_port()
+    bufs = [C.create_string_buffer(payload if r == 0 else b"\0" * len(payload), len(payload)) for r in range(world)]
+    rcs = [None] * world
+    stop = threading.Event()
+
+    def go(r):
+        rcs[r] = f(r, world, b"127.0.0.1", port, C.cast(bufs[r], C.c_void_p), len(payload), 20000)
+
+    t0 = threading.Thread(target=go, args=(0,))
+    t0.start()
+    ts = threading.Thread(target=_strays, args=(port, stop, kinds))
+    ts.start()
+    time.sleep(0.5)  # the strays reach rank 0 first
+    peers = [threading.Thread(target=go, args=(r,)) for r in range(1, world)]
+    for t in peers:
+        t.start()
+    for t in [t0] + peers:
+        t.join(60)
+    stop.set()
+    ts.join(30)
+    if "dup" in kinds:  # the duplicate may have taken rank 1's place before it came: then rank 1 is refused
+        assert rcs[0] == 0 and rcs[2] == 0 and rcs[1] in (0, -5)
+        assert bufs[2].raw == payload
+    else:
+        assert rcs == [0] * world
+        assert all(b.raw == payload for b in bufs)

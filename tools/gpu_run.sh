@@ -139,6 +139,12 @@ for s in $STEPS; do
   prof5)
     timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof5 -o kt -- python3 bench.py --config c5 --steps 2 --no-cpu-baseline --no-ingest --no-one-shot > $OUT/prof5_bench.json 2> $OUT/prof5_bench.err
     rc=$?; echo "prof5 rc=$rc"; head -10 $OUT/prof5/kt_kernel_stats.csv | cut -c1-160 ;;
+  xhost)
+    timeout -k 10 900 python -u -m pytest tests/test_xchg_host.py -x -v -m gpu --timeout 700 --timeout-method thread > $OUT/xhost_tests.log 2>&1
+    rc=$?; echo "C++ exchange host tests rc=$rc"; grep -E "PASS|FAIL|Error" $OUT/xhost_tests.log | tail -30 ;;
+  repro)
+    make -s -C tools/micro over_heads_repro > $OUT/repro_build.log 2>&1 && timeout -k 10 120 tools/micro/over_heads_repro > $OUT/over_heads_repro.json 2>&1
+    rc=$?; echo "over_heads repro rc=$rc"; cat $OUT/over_heads_repro.json ;;
   *) echo "unknown step $s"; rc=2 ;;
   esac
   if [ $rc -ne 0 ]; then tail -30 $OUT/*.err 2>/dev/null; exit $rc; fi
