@@ -147,7 +147,17 @@ __global__ __launch_bounds__(kBlock) void k_pack_ascii(const char* __restrict__ 
 // s_waitcnt immediate of gfx9/CDNA: vmcnt(0), expcnt and lgkmcnt not waited for
 constexpr int kWaitVm0 = 0x0F70;
 constexpr int kCell = 8;
-constexpr int kScanBuf = 3 * 64;  // staged run metas per scan wavefront (two puts per step: < 64 + 128)
+// staged run metas per scan wavefront: a put finds fewer than 64 staged (every
+// step flushes at 64), so valid metas stay below 128 and [128, 192) takes the
+// stores of the lanes that put nothing (k_scan's put: one unconditional store)
+constexpr int kScanBuf = 3 * 64;
+#ifndef MG_SCAN_V1
+// k_scan keeps a +inf sentinel in key slot w of each lane (the window that is
+// exactly the current block reads it as its previous-block suffix)
+constexpr int kScanKeyPad = 1;
+#else
+constexpr int kScanKeyPad = 0;
+#endif
 // k_scan<..., G> takes its reads in windows of G groups of 64 consecutive
 // slots, one pass of 64 reads of similar length at a time (longest first); the
 // runs of group j of a window go to the wavefront's run region j (G regions
@@ -838,15 +848,16 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(G > 1 ? 
   extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int h = p.h, m = p.m, w = p.w;
-  uint32_t* s_keys = reinterpret_cast<uint32_t*>(smem) + (size_t)wv * w * kWave + lane;  // slot u at [u*64]
+  uint32_t* s_keys = reinterpret_cast<uint32_t*>(smem) + (size_t)wv * (w + kScanKeyPad) * kWave + lane;  // slot u at [u*64]
   const int msh = 64 - 2 * m;
   const uint64_t mmask = (m == 32) ? ~0ULL : ((1ULL << (2 * m)) - 1);
   const uint64_t ngroups = (p.a_hi - p.a_lo + kWave - 1) / kWave;
   const int wpb = (int)(blockDim.x >> 6);  // 4, or fewer when w's LDS arrays need it (scan_wpb)
   const uint64_t gw = (uint64_t)blockIdx.x * wpb + wv;
   const uint64_t nw = (uint64_t)gridDim.x * wpb;
-  uint64_t* s_buf = reinterpret_cast<uint64_t*>(smem) + (size_t)wpb * ((w * kWave + 1) / 2) +
+  uint64_t* s_buf = reinterpret_cast<uint64_t*>(smem) + (size_t)wpb * (((w + kScanKeyPad) * kWave + 1) / 2) +
                     (size_t)wv * kScanBuf;
+  if (kScanKeyPad) s_keys[w * kWave] = 0xFFFFFFFFu;  // the sentinel (never overwritten)
   // region j of this wavefront (= run region G gw + j) holds the runs
   // of group j of each of its windows: a probe block's share of G
   // consecutive regions then covers consecutive slots, as with one group per
@@ -862,7 +873,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(G > 1 ? 
   // record will carry the read index
   auto put = [&](bool flag, uint64_t meta) {
     const uint64_t bal = __ballot(flag);
+#ifndef MG_SCAN_V1
+    // every lane stores (no exec-mask branch: the scalar unit is the scan's
+    // tightest issue port); lanes without a run write their spare slot
+    s_buf[flag ? nbuf + lane_prefix(bal) : 2 * kWave + lane] = meta;
+#else
     if (flag) s_buf[nbuf + lane_prefix(bal)] = meta;
+#endif
     nbuf += (uint32_t)__popcll(bal);
   };
   const uint64_t nwin = (ngroups + G - 1) / G;
@@ -1033,6 +1050,58 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(G > 1 ? 
     // LDS latency hides behind the step's ALU work
     uint32_t sv_pf = s_keys[kWave];
     // one base step t; cw = the read word holding base t + m
+#ifndef MG_SCAN_V1
+    // one base step t, without a per-lane branch: a lane past its read's end
+    // (t > tlast) keeps computing, and only its run state and keys are held
+    // (selects); the block's prefix minimum restarts at +inf after each block,
+    // and the suffix minimum past the block (u = w - 1) is the sentinel slot.
+    // (The branchy step issued ~37 scalar instructions per step for the exec
+    // masks and flow blocks: 0.90 G SALU vs 1.07 G VALU per C3 launch, ~3/4 of
+    // the CU's one scalar unit.)
+    auto step = [&](int t, uint64_t cw) {
+      const bool act = t <= tlast;
+      const uint32_t key = order_key(mm) | (uint32_t)t;
+      pmin = min(pmin, key);
+      if (INDEX && t == w - 1) kb0 = min(kb0, pmin);  // o = 0: t in [0, w) (wavefront-uniform)
+      bool emit = false;
+      uint64_t e_meta = 0;
+      if (t >= w) {  // window j = t - w + 1 (wavefront-uniform)
+        const int j = t - w + 1;
+        const uint32_t mn = min(sv_pf, pmin);
+        const int pos = (int)(mn & 1023u);
+        const bool keyw = INDEX && t > tend;  // o = 1: window j = n - h, i = t - (n - h)
+        if (INDEX) kb1 = (act && keyw) ? mn - (uint32_t)(n - h) : kb1;
+        const bool live = act && !keyw;
+        emit = live && j > 1 && pos != last_pos;
+        e_meta = run_meta(own, last_pos, jlo, j - 1);
+        jlo = emit ? j : jlo;
+        last_pos = live ? pos : last_pos;
+      }
+      s_keys[u * kWave] = key;
+      const int x = t + m;  // roll in the base at t + m
+      mm = ((mm << 2) | ((cw >> (62 - 2 * (x & 31))) & 3u)) & mmask;
+      if (u == w - 1) {  // block complete: suffix minima in place, 8 reads in flight at a time
+        uint32_t run = 0xFFFFFFFFu;
+        for (int v0 = w - 1; v0 >= 0; v0 -= 8) {
+          uint32_t x8[8];
+#pragma unroll
+          for (int k = 0; k < 8; ++k) x8[k] = v0 - k >= 0 ? s_keys[(v0 - k) * kWave] : 0xFFFFFFFFu;
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            run = x8[k] < run ? x8[k] : run;
+            if (v0 - k >= 0) s_keys[(v0 - k) * kWave] = run;
+          }
+        }
+        u = 0;
+        pmin = 0xFFFFFFFFu;
+      } else {
+        ++u;
+      }
+      sv_pf = s_keys[(u + 1) * kWave];  // (u + 1 = w: the sentinel)
+      put(emit, e_meta);
+      while (nbuf >= (uint32_t)kWave) flush(kWave);
+    };
+#else
     auto step = [&](int t, uint64_t cw) {
       bool emit = false;
       uint64_t e_meta = 0;
@@ -1080,6 +1149,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(G > 1 ? 
       put(emit, e_meta);
       while (nbuf >= (uint32_t)kWave) flush(kWave);
     };
+#endif
     if constexpr (MAXW <= 8) {
       // one loop per read word (t + m <= n - 1 < 32 MAXW): the word is a
       // compile-time register, so rw[] never goes to scratch and no vmcnt wait
@@ -2796,7 +2866,9 @@ uint32_t resident_blocks(mg_ctx* ctx, K kernel, size_t lds, uint64_t want, int b
 // run metas; blocks carry 4 wavefronts, or 2 / 1 when that does not fit
 // (long windows: w = l - k grows with min_overlap).  0 = w too large.
 constexpr size_t kLdsPerCu = 160 * 1024;
-inline size_t scan_lds_per_wave(uint32_t w) { return (((size_t)w * kWave + 1) / 2 + kScanBuf) * sizeof(uint64_t); }
+inline size_t scan_lds_per_wave(uint32_t w) {
+  return (((size_t)(w + kScanKeyPad) * kWave + 1) / 2 + kScanBuf) * sizeof(uint64_t);
+}
 inline uint32_t scan_wpb(uint32_t w) {
   for (uint32_t wpb = kWavesPerBlock; wpb >= 1; wpb >>= 1)
     if (wpb * scan_lds_per_wave(w) <= kLdsPerCu) return wpb;
