@@ -151,13 +151,9 @@ constexpr int kCell = 8;
 // step flushes at 64), so valid metas stay below 128 and [128, 192) takes the
 // stores of the lanes that put nothing (k_scan's put: one unconditional store)
 constexpr int kScanBuf = 3 * 64;
-#ifndef MG_SCAN_V1
 // k_scan keeps a +inf sentinel in key slot w of each lane (the window that is
 // exactly the current block reads it as its previous-block suffix)
 constexpr int kScanKeyPad = 1;
-#else
-constexpr int kScanKeyPad = 0;
-#endif
 // k_scan<..., G> takes its reads in windows of G groups of 64 consecutive
 // slots, one pass of 64 reads of similar length at a time (longest first); the
 // runs of group j of a window go to the wavefront's run region j (G regions
@@ -857,7 +853,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(G > 1 ? 
   const uint64_t nw = (uint64_t)gridDim.x * wpb;
   uint64_t* s_buf = reinterpret_cast<uint64_t*>(smem) + (size_t)wpb * (((w + kScanKeyPad) * kWave + 1) / 2) +
                     (size_t)wv * kScanBuf;
-  if (kScanKeyPad) s_keys[w * kWave] = 0xFFFFFFFFu;  // the sentinel (never overwritten)
+  s_keys[w * kWave] = 0xFFFFFFFFu;  // the sentinel (never overwritten)
   // region j of this wavefront (= run region G gw + j) holds the runs
   // of group j of each of its windows: a probe block's share of G
   // consecutive regions then covers consecutive slots, as with one group per
@@ -873,13 +869,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(G > 1 ? 
   // record will carry the read index
   auto put = [&](bool flag, uint64_t meta) {
     const uint64_t bal = __ballot(flag);
-#ifndef MG_SCAN_V1
     // every lane stores (no exec-mask branch: the scalar unit is the scan's
     // tightest issue port); lanes without a run write their spare slot
     s_buf[flag ? nbuf + lane_prefix(bal) : 2 * kWave + lane] = meta;
-#else
-    if (flag) s_buf[nbuf + lane_prefix(bal)] = meta;
-#endif
     nbuf += (uint32_t)__popcll(bal);
   };
   const uint64_t nwin = (ngroups + G - 1) / G;
@@ -1034,6 +1026,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(G > 1 ? 
       if ((uint32_t)lane + kWave < rest) s_buf[kWave + lane] = m1;
       nbuf = rest;
       wave_sync();
+      // the flush's LDS traffic retired here, on its own (rare) path: otherwise
+      // the step after it, reusing those registers, waits on lgkmcnt(0) for every
+      // LDS op in flight, the prefetched suffix minimum included, on every step
+      __builtin_amdgcn_s_waitcnt(0xC07F);
     };
     uint64_t mm = 0;
     if (tend) mm = funnel(rw[0], rw[1], 2) >> msh;  // m-mer at t = 1
@@ -1049,34 +1045,16 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(G > 1 ? 
     // previous block's suffix minimum at u + 1, read one step ahead so the
     // LDS latency hides behind the step's ALU work
     uint32_t sv_pf = s_keys[kWave];
-    // one base step t; cw = the read word holding base t + m
-#ifndef MG_SCAN_V1
-    // one base step t, without a per-lane branch: a lane past its read's end
-    // (t > tlast) keeps computing, and only its run state and keys are held
-    // (selects); the block's prefix minimum restarts at +inf after each block,
+    // The base steps (cw = the read word holding base t + m), without a per-lane branch (selects only: the CU's one
+    // scalar unit is the scan's tightest issue port -- the branchy step issued
+    // ~37 scalar instructions per step for its exec masks and flow blocks, 0.90 G
+    // SALU vs 1.07 G VALU per C3 launch), in two loops with no per-step test of
+    // the phase: the first block t = 1 .. w (window j = 1 at t = w, key o = 0's
+    // prefix at t = w - 1), then t > w, where every step is a window j >= 2.  A
+    // lane past its read (t > tend) keeps computing; only its run state and keys
+    // are held.  The block's prefix minimum restarts at +inf after each block,
     // and the suffix minimum past the block (u = w - 1) is the sentinel slot.
-    // (The branchy step issued ~37 scalar instructions per step for the exec
-    // masks and flow blocks: 0.90 G SALU vs 1.07 G VALU per C3 launch, ~3/4 of
-    // the CU's one scalar unit.)
-    auto step = [&](int t, uint64_t cw) {
-      const bool act = t <= tlast;
-      const uint32_t key = order_key(mm) | (uint32_t)t;
-      pmin = min(pmin, key);
-      if (INDEX && t == w - 1) kb0 = min(kb0, pmin);  // o = 0: t in [0, w) (wavefront-uniform)
-      bool emit = false;
-      uint64_t e_meta = 0;
-      if (t >= w) {  // window j = t - w + 1 (wavefront-uniform)
-        const int j = t - w + 1;
-        const uint32_t mn = min(sv_pf, pmin);
-        const int pos = (int)(mn & 1023u);
-        const bool keyw = INDEX && t > tend;  // o = 1: window j = n - h, i = t - (n - h)
-        if (INDEX) kb1 = (act && keyw) ? mn - (uint32_t)(n - h) : kb1;
-        const bool live = act && !keyw;
-        emit = live && j > 1 && pos != last_pos;
-        e_meta = run_meta(own, last_pos, jlo, j - 1);
-        jlo = emit ? j : jlo;
-        last_pos = live ? pos : last_pos;
-      }
+    auto roll_and_advance = [&](int t, uint32_t key, uint64_t cw) {
       s_keys[u * kWave] = key;
       const int x = t + m;  // roll in the base at t + m
       mm = ((mm << 2) | ((cw >> (62 - 2 * (x & 31))) & 3u)) & mmask;
@@ -1098,75 +1076,47 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(G > 1 ? 
         ++u;
       }
       sv_pf = s_keys[(u + 1) * kWave];  // (u + 1 = w: the sentinel)
-      put(emit, e_meta);
-      while (nbuf >= (uint32_t)kWave) flush(kWave);
     };
-#else
+    // t = 1 .. w: the first block; t = w is window j = 1 (no run closes there)
+    auto step_first = [&](int t, uint64_t cw) {
+      const uint32_t key = order_key(mm) | (uint32_t)t;
+      pmin = min(pmin, key);
+      if (INDEX && t == w - 1) kb0 = min(kb0, pmin);  // o = 0: t in [0, w)
+      if (t == w) last_pos = (int)(min(sv_pf, pmin) & 1023u);
+      roll_and_advance(t, key, cw);
+    };
+    // t > w: window j = t - w + 1 >= 2 (a run closes where its minimizer moves)
     auto step = [&](int t, uint64_t cw) {
-      bool emit = false;
-      uint64_t e_meta = 0;
-      if (t <= tlast) {
-        const uint32_t key = order_key(mm) | (uint32_t)t;
-        pmin = (u == 0 || key < pmin) ? key : pmin;
-        if (INDEX && t == w - 1) kb0 = min(kb0, pmin);  // o = 0: t in [0, w) (wavefront-uniform)
-        if (t >= w) {  // window j = t - w + 1
-          const int j = t - w + 1;
-          uint32_t mn = pmin;
-          if (u != w - 1) mn = sv_pf < mn ? sv_pf : mn;
-          const int pos = (int)(mn & 1023u);
-          if (INDEX && t > tend) {
-            kb1 = mn - (uint32_t)(n - h);  // o = 1: window j = n - h, i = t - (n - h)
-          } else {
-            if (j > 1 && pos != last_pos) {
-              emit = true;
-              e_meta = run_meta(own, last_pos, jlo, j - 1);
-              jlo = j;
-            }
-            last_pos = pos;
-          }
-        }
-        s_keys[u * kWave] = key;
-        const int x = t + m;  // roll in the base at t + m
-        mm = ((mm << 2) | ((cw >> (62 - 2 * (x & 31))) & 3u)) & mmask;
-      }
-      if (u == w - 1) {  // block complete: suffix minima in place, 8 reads in flight at a time
-        uint32_t run = 0xFFFFFFFFu;
-        for (int v0 = w - 1; v0 >= 0; v0 -= 8) {
-          uint32_t x8[8];
-#pragma unroll
-          for (int k = 0; k < 8; ++k) x8[k] = v0 - k >= 0 ? s_keys[(v0 - k) * kWave] : 0xFFFFFFFFu;
-#pragma unroll
-          for (int k = 0; k < 8; ++k) {
-            run = x8[k] < run ? x8[k] : run;
-            if (v0 - k >= 0) s_keys[(v0 - k) * kWave] = run;
-          }
-        }
-        u = 0;
-      } else {
-        ++u;
-      }
-      sv_pf = s_keys[(u + 1 < w ? u + 1 : 0) * kWave];
+      const uint32_t key = order_key(mm) | (uint32_t)t;
+      pmin = min(pmin, key);
+      const uint32_t mn = min(sv_pf, pmin);
+      const int pos = (int)(mn & 1023u);
+      if (INDEX) kb1 = t == tlast ? mn - (uint32_t)(n - h) : kb1;  // o = 1: window j = n - h, i = t - (n - h)
+      const bool live = t <= tend;
+      const bool emit = live && pos != last_pos;
+      const uint64_t e_meta = run_meta(own, last_pos, jlo, t - w);
+      jlo = emit ? t - w + 1 : jlo;
+      last_pos = live ? pos : last_pos;
+      roll_and_advance(t, key, cw);
       put(emit, e_meta);
-      while (nbuf >= (uint32_t)kWave) flush(kWave);
+      if (nbuf >= (uint32_t)kWave) flush(kWave);  // (< 64 staged before the put: one flush at most)
     };
-#endif
     if constexpr (MAXW <= 8) {
-      // one loop per read word (t + m <= n - 1 < 32 MAXW): the word is a
-      // compile-time register, so rw[] never goes to scratch and no vmcnt wait
-      // (which would also wait for the flushes' stores) sits in the loop.  (A
-      // specialised body for the steps every lane covers, outside the key
-      // windows, measured slower: scan 3.55 vs 2.95 ms at 6 waves, its extra
-      // registers spill; 3.06 ms at 5 waves.)
+      // one loop per read word and phase (t + m <= n - 1 < 32 MAXW): the word is
+      // a compile-time register, so rw[] never goes to scratch and no vmcnt wait
+      // (which would also wait for the flushes' stores) sits in the loop
 #pragma unroll
       for (int k = 0; k < MAXW + (INDEX ? 1 : 0); ++k) {  // (INDEX's step t = n - m rolls in base n)
         const int t0 = max(1, 32 * k - m), t1 = min(tmax, 32 * k + 31 - m);
-        for (int t = t0; t <= t1; ++t) step(t, rw[k]);
+        const int tf = min(t1, w);
+        for (int t = t0; t <= tf; ++t) step_first(t, rw[k]);
+        for (int t = max(t0, w + 1); t <= t1; ++t) step(t, rw[k]);
       }
     } else {
       int cwi = __builtin_amdgcn_readfirstlane((1 + m) >> 5);
       uint64_t cw = word_at(cwi);
       for (int t = 1; t <= tmax; ++t) {
-        step(t, cw);
+        if (t <= w) step_first(t, cw); else step(t, cw);
         const int xu = __builtin_amdgcn_readfirstlane(t + m);
         if ((xu & 31) == 31) cw = word_at((xu + 1) >> 5);  // next word (don't-care past a read's end)
       }
