@@ -871,7 +871,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(G > 1 ? 
     const uint64_t bal = __ballot(flag);
     // every lane stores (no exec-mask branch: the scalar unit is the scan's
     // tightest issue port); lanes without a run write their spare slot
-    s_buf[flag ? nbuf + lane_prefix(bal) : 2 * kWave + lane] = meta;
+    uint32_t at = nbuf + lane_prefix(bal);
+    __asm__ volatile("" : "+v"(at));  // (computed by every lane: a select below, not an exec-mask region)
+    s_buf[flag ? at : 2 * kWave + lane] = meta;
     nbuf += (uint32_t)__popcll(bal);
   };
   const uint64_t nwin = (ngroups + G - 1) / G;
@@ -1054,11 +1056,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(G > 1 ? 
     // lane past its read (t > tend) keeps computing; only its run state and keys
     // are held.  The block's prefix minimum restarts at +inf after each block,
     // and the suffix minimum past the block (u = w - 1) is the sentinel slot.
-    auto roll_and_advance = [&](int t, uint32_t key, uint64_t cw) {
+    // sh = 62 - 2 ((t + m) & 31): the shift that brings base t + m of cw down
+    // (kept by the loops, wavefront-uniform)
+    auto roll_and_advance = [&](uint32_t key, uint64_t cw, int sh) {
       s_keys[u * kWave] = key;
-      const int x = t + m;  // roll in the base at t + m
-      mm = ((mm << 2) | ((cw >> (62 - 2 * (x & 31))) & 3u)) & mmask;
-      if (u == w - 1) {  // block complete: suffix minima in place, 8 reads in flight at a time
+      mm = ((mm << 2) | ((cw >> sh) & 3u)) & mmask;  // roll in the base at t + m
+      if (++u == w) {  // block complete: suffix minima in place, 8 reads in flight at a time
         uint32_t run = 0xFFFFFFFFu;
         for (int v0 = w - 1; v0 >= 0; v0 -= 8) {
           uint32_t x8[8];
@@ -1072,21 +1075,19 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(G > 1 ? 
         }
         u = 0;
         pmin = 0xFFFFFFFFu;
-      } else {
-        ++u;
       }
       sv_pf = s_keys[(u + 1) * kWave];  // (u + 1 = w: the sentinel)
     };
     // t = 1 .. w: the first block; t = w is window j = 1 (no run closes there)
-    auto step_first = [&](int t, uint64_t cw) {
+    auto step_first = [&](int t, uint64_t cw, int sh) {
       const uint32_t key = order_key(mm) | (uint32_t)t;
       pmin = min(pmin, key);
       if (INDEX && t == w - 1) kb0 = min(kb0, pmin);  // o = 0: t in [0, w)
       if (t == w) last_pos = (int)(min(sv_pf, pmin) & 1023u);
-      roll_and_advance(t, key, cw);
+      roll_and_advance(key, cw, sh);
     };
     // t > w: window j = t - w + 1 >= 2 (a run closes where its minimizer moves)
-    auto step = [&](int t, uint64_t cw) {
+    auto step = [&](int t, uint64_t cw, int sh) {
       const uint32_t key = order_key(mm) | (uint32_t)t;
       pmin = min(pmin, key);
       const uint32_t mn = min(sv_pf, pmin);
@@ -1097,7 +1098,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(G > 1 ? 
       const uint64_t e_meta = run_meta(own, last_pos, jlo, t - w);
       jlo = emit ? t - w + 1 : jlo;
       last_pos = live ? pos : last_pos;
-      roll_and_advance(t, key, cw);
+      roll_and_advance(key, cw, sh);
       put(emit, e_meta);
       if (nbuf >= (uint32_t)kWave) flush(kWave);  // (< 64 staged before the put: one flush at most)
     };
@@ -1109,14 +1110,21 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(G > 1 ? 
       for (int k = 0; k < MAXW + (INDEX ? 1 : 0); ++k) {  // (INDEX's step t = n - m rolls in base n)
         const int t0 = max(1, 32 * k - m), t1 = min(tmax, 32 * k + 31 - m);
         const int tf = min(t1, w);
-        for (int t = t0; t <= tf; ++t) step_first(t, rw[k]);
-        for (int t = max(t0, w + 1); t <= t1; ++t) step(t, rw[k]);
+        for (int t = t0, sh = 62 - 2 * ((t0 + m) & 31); t <= tf; ++t, sh -= 2) step_first(t, rw[k], sh);
+        int t = max(t0, w + 1), sh = 62 - 2 * ((t + m) & 31);
+        if (t <= t1) {
+          do {  // (bottom-tested: one compare and branch per step)
+            step(t, rw[k], sh);
+            sh -= 2;
+          } while (++t <= t1);
+        }
       }
     } else {
       int cwi = __builtin_amdgcn_readfirstlane((1 + m) >> 5);
       uint64_t cw = word_at(cwi);
       for (int t = 1; t <= tmax; ++t) {
-        if (t <= w) step_first(t, cw); else step(t, cw);
+        const int sh = 62 - 2 * ((t + m) & 31);
+        if (t <= w) step_first(t, cw, sh); else step(t, cw, sh);
         const int xu = __builtin_amdgcn_readfirstlane(t + m);
         if ((xu & 31) == 31) cw = word_at((xu + 1) >> 5);  // next word (don't-care past a read's end)
       }
