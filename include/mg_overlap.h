@@ -69,6 +69,9 @@ typedef struct mg_counters {
                           walked (option live_index); 0 = the full table */
   /* the last containment pass (markContainedReads), same units */
   uint64_t c_runs, c_entries, c_verified, c_contained;
+  /* run records the last window scan wrote (every source read's windows; kept
+   * without option "stats") */
+  uint64_t scan_runs;
 } mg_counters;
 
 /* --- context ------------------------------------------------------------ */
@@ -195,7 +198,8 @@ int mg_set_shard(mg_ctx* ctx, uint32_t rank, uint32_t nranks, uint64_t read_lo, 
  *   mg_xchg_pack(MG_KEYS) -> a2a -> mg_xchg_insert_keys        (insertDataset)
  *   mg_xchg_pack(MG_RUNS) -> a2a   (the received runs serve both probes)
  *   mg_begin_contained(superkey)
- *   [lengths differ: mg_xchg_probe(1) -> all-reduce MAX of superkey]
+ *   [lengths differ: (mg_xchg_prefix_marks -> all-reduce MAX of the marks)
+ *                    mg_xchg_probe(1) -> all-reduce MAX of superkey]
  *   mg_finalize_contained                                       (markContainedReads)
  *   mg_xchg_probe(0) -> mg_xchg_pack(MG_ROWS) -> a2a             (insertAllEdgesOfRead)
  * and every rank ends with the rows whose src it owns.  Record sizes:
@@ -243,6 +247,16 @@ int mg_xchg_probe(mg_ctx* ctx, int contain, const void* recv, uint64_t slot, uin
  * the host all-reduces it with MAX over the ranks, and mg_finalize_contained
  * turns it into superReadID (super_out optional, n_reads + 1 entries). */
 int mg_begin_contained(mg_ctx* ctx, void* superkey, int* needed);
+/* Optional, between mg_begin_contained and mg_xchg_probe(1) (lengths differ):
+ * run this rank's offset-0 containments (checkOverlapForContainedRead at s = 0,
+ * OverlapGraph.cpp:302-340, over the o = 0 key records it received) now and
+ * write marks[i] = 1 for every read they found contained (n_reads bytes,
+ * device; NULL: no marks).  The caller all-reduces marks with MAX over the
+ * ranks on the context's stream; mg_xchg_probe(1) then folds them into the
+ * key array, so that its contained-source skip (contain_skip) sees every
+ * rank's offset-0 containments, not only this rank's.  marks stays the
+ * caller's and must stay valid until mg_xchg_probe(1) is enqueued. */
+int mg_xchg_prefix_marks(mg_ctx* ctx, void* marks);
 int mg_finalize_contained(mg_ctx* ctx, uint32_t* super_out);
 
 /* --- parity digests (no reference counterpart: test/bench support) ----------

@@ -140,6 +140,12 @@ struct mg_ctx {
   // the exchange calls delegate to the fused probes (option "xchg_fused1")
   bool xchg_fused = false;
   bool xchg_fused1 = true;
+  bool index_keys = true;  // option "index_keys": LaunchIndex takes k_index_keys (0: k_index_build)
+  // mg_xchg_prefix_marks ran this step's offset-0 containments; xmarks = the
+  // caller's marks (all-reduced before mg_xchg_probe(1) folds them in)
+  uint64_t scan_runs = 0;  // run records of the last window scan (settle_runs)
+  bool xmarks_done = false;
+  uint8_t* xmarks = nullptr;
   uint64_t xchg_lo = 0, xchg_hi = 0;     // its source reads
   unsigned long long* d_blk = nullptr;   // routing: per-(block, rank) counts / offsets
   size_t blk_cap = 0;

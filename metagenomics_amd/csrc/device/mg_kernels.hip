@@ -1010,7 +1010,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(G > 1 ? 
         if (flag && at < p.run_cap) region[at] = make_ulonglong2(v, meta);
         cur[0] += (uint64_t)__popcll(bal);
       } else {
+#ifdef MG_DIAG_ONE_REGION  // (diagnostics build: every run of a window into its first region)
+        const uint32_t grp = 0;
+#else
         const uint32_t grp = ws >> 6;  // the run's group in the window
+#endif
         uint64_t at = 0;
 #pragma unroll
         for (int j = 0; j < G; ++j) {
@@ -1172,7 +1176,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(G > 1 ? 
       for (int o = 0; o < 4; ++o) {
         const uint64_t v = mix64(mb[o]);
         const unsigned long long e = make_entry(v, p.nb_log2, (int)(kb[o] & 1023u), o, (uint32_t)a);
+#ifndef MG_DIAG_NO_KEY0  // (diagnostics build: no o = 0 key records)
         if (o == 0 && p.key0) p.key0[a] = (v & ((1ULL << 50) - 1)) | ((uint64_t)(kb[0] & 1023u) << 54);
+#endif
         if constexpr (KEYREC) {  // o-major: each store is one coalesced wavefront line
           p.key_bk[key_seg(o) * p.key_n + a - p.key_lo] = (uint32_t)(v & nbm);
           p.key_ent[key_seg(o) * p.key_n + a - p.key_lo] = (o == 1 && p.skip_o1) ? kEmpty : e;  // (a hole: not routed)
@@ -2287,22 +2293,51 @@ __global__ __launch_bounds__(kBlock) void k_super_finalize(const unsigned long l
                                                           unsigned int* __restrict__ any,
                                                           uint32_t* __restrict__ cbits,
                                                           unsigned int* __restrict__ ccnt) {
-  const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-  uint32_t s = 0;
-  if (i < n) {
-    const unsigned long long k = key[i];
-    s = k ? (0xFFFFFFFFu - (uint32_t)k) + 1u : 0u;  // container index -> ID
-    super[i] = s;
-  }
-  // the wavefront's 64 contained bits as two bitmap words (i is 64-aligned at lane 0)
-  const uint64_t bal = __ballot(s != 0);
+  // grid-stride over 64-read tiles (i is 64-aligned at lane 0); the wavefront
+  // counts its contained reads in a register and adds them once at the end
+  // (one add per tile on 64 counters serialised at C5: 0.32 ms per pass)
   const int lane = (int)(threadIdx.x & 63);
-  if (lane < 2 && i - lane < n) cbits[(i - lane) / 32 + lane] = (uint32_t)(bal >> (32 * lane));
-  if (ccnt && bal && lane == 0) atomicAdd(&ccnt[(blockIdx.x & 63u) * 16], (unsigned int)__popcll(bal));
-  // the flag is set once: waves that already see it set skip the atomic
-  // (an atomic per contained read on one address serialised: 8.9 ms at C5)
-  if (bal && lane == 0 && __hip_atomic_load(any, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u)
-    atomicOr(any, 1u);
+  uint32_t cnt = 0;
+  for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i - lane < n; i += (uint64_t)gridDim.x * kBlock) {
+    uint32_t s = 0;
+    if (i < n) {
+      const unsigned long long k = key[i];
+      s = k ? (0xFFFFFFFFu - (uint32_t)k) + 1u : 0u;  // container index -> ID
+      super[i] = s;
+    }
+    // the tile's 64 contained bits as two bitmap words
+    const uint64_t bal = __ballot(s != 0);
+    if (lane < 2) cbits[(i - lane) / 32 + lane] = (uint32_t)(bal >> (32 * lane));
+    cnt += (uint32_t)__popcll(bal);
+  }
+  if (cnt && lane == 0) {
+    if (ccnt) atomicAdd(&ccnt[(blockIdx.x & 63u) * 16], cnt);
+    // the flag is set once: waves that already see it set skip the atomic
+    if (__hip_atomic_load(any, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) atomicOr(any, 1u);
+  }
+}
+
+inline uint32_t super_grid(const mg_ctx* ctx) {
+  return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((ctx->n + kBlock - 1) / kBlock, (uint64_t)ctx->n_cu * 8));
+}
+
+// Exchange mode, cross-rank prefix marks (mg_xchg_prefix_marks): marks[i] = 1
+// for every read whose containment key is set after this rank's offset-0
+// containments; after the caller's MAX all-reduce, the marks fold back into
+// the key array as key = max(key, mark), so contain_skip (the probe's
+// "source already contained" test, superkey != 0) sees every rank's prefix
+// containments.  A folded 1 never survives: the rank that set the mark holds
+// the read's real key (len << 32 | ~id > 1), and the MAX all-reduce of the keys
+// after the probe keeps the larger.
+__global__ __launch_bounds__(kBlock) void k_prefix_marks(const unsigned long long* __restrict__ key, uint64_t n,
+                                                        uint8_t* __restrict__ marks) {
+  for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBlock)
+    marks[i] = key[i] ? 1 : 0;
+}
+__global__ __launch_bounds__(kBlock) void k_fold_marks(unsigned long long* __restrict__ key, uint64_t n,
+                                                      const uint8_t* __restrict__ marks) {
+  for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBlock)
+    if (marks[i] && !key[i]) key[i] = 1ull;
 }
 
 // Order-independent digests (include/mg_overlap.h, mg_rows_digest): per row
@@ -2793,12 +2828,75 @@ struct LaunchIndexLive {
   }
 };
 
+// HashTable::insertDataset without a window scan (HashTable.cpp:50-80): the
+// index of the replicated mode and of source-range shards, and the all-keys
+// lookup table.  One read per lane with its words in registers; the four keys
+// (hashRead, :88-104) in two passes of w steps over F[0, h) and F[n-h, n), each
+// rolling the forward m-mer and its reverse complement on the same incoming
+// base: F[0, h) gives o = 0 (offset t) and o = 3 (R[n-h, n) = rc F[0, h), offset
+// w-1-t), F[n-h, n) gives o = 1 and o = 2 (R[0, h) = rc F[n-h, n)).  Same
+// (order_key | offset) rule as key_minimizer and k_scan, so the entries equal
+// k_index_build's; then one CAS insert per key.  (k_index_build -- a thread per
+// key, the read staged in LDS, one LDS read per base -- took 2.0 ms at C3.)
+template <int MAXW>
+__global__ __launch_bounds__(kBlock) void k_index_keys(IndexParams p) {
+  const int h = p.h, m = p.m, w = p.w;
+  const int msh = 64 - 2 * m;
+  const uint64_t mmask = (m == 32) ? ~0ULL : ((1ULL << (2 * m)) - 1);
+  const uint64_t nbm = (1ULL << p.nb_log2) - 1;
+  for (uint64_t a = (uint64_t)blockIdx.x * kBlock + threadIdx.x; a < p.n; a += (uint64_t)gridDim.x * kBlock) {
+    uint64_t rw[MAXW + 1];
+    load_slot<MAXW>(p.words, (uint32_t)a, rw);
+    const int n = p.len[a];
+    uint32_t kf[2], kr[2];  // per pass: best forward (o = 0 / 1) and reverse (o = 3 / 2) key
+#pragma unroll
+    for (int pass = 0; pass < 2; ++pass) {
+      const int s0 = pass ? n - h : 0;
+      uint64_t f = ext_reg<MAXW>(rw, s0) >> msh;       // F[s0, s0 + m)
+      uint64_t r = rc_word(f << msh) & mmask;          // its reverse complement
+      const uint64_t nx = ext_reg<MAXW>(rw, s0 + m);   // the bases rolled in (w <= 32)
+      uint32_t bf = order_key(f), br = order_key(r) | (uint32_t)(w - 1);
+      for (int t = 1; t < w; ++t) {
+        const uint64_t b = w <= 32 ? (nx >> (62 - 2 * (t - 1))) & 3u
+                                   : (ext_reg<MAXW>(rw, s0 + m - 1 + t) >> 62) & 3u;
+        f = ((f << 2) | b) & mmask;
+        r = (r >> 2) | ((uint64_t)(3u - b) << (2 * m - 2));
+        bf = min(bf, order_key(f) | (uint32_t)t);
+        br = min(br, order_key(r) | (uint32_t)(w - 1 - t));
+      }
+      kf[pass] = bf;
+      kr[pass] = br;
+    }
+    const uint32_t kb[4] = {kf[0], kf[1], kr[1], kr[0]};
+    const int i0 = (int)(kb[0] & 1023u), i1 = (int)(kb[1] & 1023u), i2 = (int)(kb[2] & 1023u),
+              i3 = (int)(kb[3] & 1023u);
+    const uint64_t mb[4] = {ext_reg<MAXW>(rw, i0) >> msh, ext_reg<MAXW>(rw, n - h + i1) >> msh,
+                            rc_word(ext_reg<MAXW>(rw, n - m - i2)) & mmask,
+                            rc_word(ext_reg<MAXW>(rw, w - 1 - i3)) & mmask};
+#pragma unroll
+    for (int o = 0; o < 4; ++o) {
+      if (o == 1 && p.skip_o1) continue;
+      const uint64_t v = mix64(mb[o]);
+      const uint64_t b = v & nbm;
+      if (owned(b, p.nb_log2, p.rank, p.nranks))
+        cell_insert(p.cells, b - p.cell_lo, p.cell_n, make_entry(v, p.nb_log2, (int)(kb[o] & 1023u), o, (uint32_t)a));
+    }
+  }
+}
+
 template <int W>
 struct LaunchIndex {
   static int run(mg_ctx* ctx, uint64_t* cells = nullptr, bool all_keys = false) {
     IndexParams p = index_params(ctx);
     if (cells) p.cells = cells;
     p.skip_o1 = (!all_keys && !ctx->index_o1) ? 1 : 0;
+    if (ctx->index_keys) {  // one read per lane (k_index_keys)
+      const uint32_t grid = (uint32_t)std::max<uint64_t>(
+          1, std::min<uint64_t>((ctx->n + kBlock - 1) / kBlock, (uint64_t)ctx->n_cu * 16));
+      if (!ctx->n) return 0;
+      hipLaunchKernelGGL((k_index_keys<W>), dim3(grid), dim3(kBlock), 0, ctx->stream, p);
+      return hipGetLastError() == hipSuccess ? 0 : -1;
+    }
     uint32_t grid = (uint32_t)((4 * ctx->n + kBlock - 1) / kBlock);  // one thread per key
     const size_t lds = (size_t)(W + 1) * kBlock * sizeof(uint64_t);
     if (grid == 0) return 0;
@@ -3213,8 +3311,12 @@ int settle_runs(mg_ctx* ctx, bool* again) {
     MG_TRY(hipMemcpyAsync(ctx->run_cnt_host.data(), ctx->d_run_cnt, ctx->nrun_reg * sizeof(unsigned long long),
                           hipMemcpyDeviceToHost, ctx->stream));
   MG_TRY(hipStreamSynchronize(ctx->stream));
-  uint64_t run_max = 0;
-  for (uint64_t r = 0; r < ctx->nrun_reg; ++r) run_max = std::max<uint64_t>(run_max, ctx->run_cnt_host[r]);
+  uint64_t run_max = 0, total = 0;
+  for (uint64_t r = 0; r < ctx->nrun_reg; ++r) {
+    run_max = std::max<uint64_t>(run_max, ctx->run_cnt_host[r]);
+    total += std::min<uint64_t>(ctx->run_cnt_host[r], ctx->run_cap);
+  }
+  ctx->scan_runs = total;
   if (run_max > ctx->run_cap) {
     ctx->run_cap_need = run_max + run_max / 8 + 64;
     *again = true;
@@ -3455,6 +3557,10 @@ int mg_set_option(mg_ctx* ctx, const char* name, int64_t value) {
   }
   if (!strcmp(name, "phase_limit")) {  // diagnostics: stop the probe after a phase (1: the scan files no keys)
     ctx->phase_limit = value > 0 ? (int)value : 99;
+    return 0;
+  }
+  if (!strcmp(name, "index_keys")) {  // index builds without a scan: one read per lane (default 1)
+    ctx->index_keys = value != 0;
     return 0;
   }
   if (!strcmp(name, "xchg_fused1")) {  // exchange mode at one rank: the fused build (default 1)
@@ -4313,7 +4419,7 @@ int mg_mark_contained(mg_ctx* ctx, uint32_t* super_out) {
       if (shared_scan(ctx) ? probe_shared(ctx, true) : run_discover(ctx, true)) return -1;
     }
     if (ctx->n)
-      hipLaunchKernelGGL(k_super_finalize, dim3((uint32_t)((ctx->n + kBlock - 1) / kBlock)), dim3(kBlock), 0,
+      hipLaunchKernelGGL(k_super_finalize, dim3(super_grid(ctx)), dim3(kBlock), 0,
                          ctx->stream, ctx->d_superkey, ctx->n, ctx->d_super, ctx->d_any, ctx->d_cbits, ctx->d_ccnt);
     MG_TRY(hipGetLastError());
     MG_TRY(hipEventRecord(ctx->ev[3], ctx->stream));
@@ -4617,11 +4723,14 @@ int mg_xchg_insert_keys(mg_ctx* ctx, const void* recv, uint64_t slot, uint32_t r
 // turns it into superReadIDs as in the exchange step
 static int xchg_fused_probe(mg_ctx* ctx, bool contain) {
   if (contain) {
-    MG_TRY(hipEventRecord(ctx->ev[2], ctx->stream));
+    if (!ctx->xmarks_done) MG_TRY(hipEventRecord(ctx->ev[2], ctx->stream));
     if (!ctx->n) return 0;
     // prefix containments first: what they mark is skipped as a container
-    if (ctx->key0_ready && dispatch_w<LaunchPrefixContain>(ctx->maxw, ctx))
+    // (one rank: mg_xchg_prefix_marks ran them already, its marks are its own)
+    if (!ctx->xmarks_done && ctx->key0_ready && dispatch_w<LaunchPrefixContain>(ctx->maxw, ctx))
       return set_err(ctx, "prefix containment launch failed");
+    ctx->xmarks_done = false;
+    ctx->xmarks = nullptr;
     if (probe_shared(ctx, true)) return -1;
     MG_TRY(hipEventRecord(ctx->ev[3], ctx->stream));
     return 0;
@@ -4661,10 +4770,21 @@ int mg_xchg_probe(mg_ctx* ctx, int contain, const void* recv, uint64_t slot, uin
   ctx->nreg = 0;
   ctx->n_rows = 0;
   if (contain) {
-    MG_TRY(hipEventRecord(ctx->ev[2], ctx->stream));
-    // prefix containments first (what they mark is skipped as a container)
-    if (ctx->xchg_prefix && ctx->n && dispatch_w<LaunchPrefixContainKeys>(ctx->maxw, ctx))
+    if (!ctx->xmarks_done) MG_TRY(hipEventRecord(ctx->ev[2], ctx->stream));
+    // prefix containments first (what they mark is skipped as a container);
+    // after mg_xchg_prefix_marks they ran already, and the all-reduced marks
+    // of every rank fold into the keys here
+    if (ctx->xmarks_done) {
+      if (ctx->xmarks && ctx->n) {
+        const uint32_t grid = (uint32_t)std::min<uint64_t>((ctx->n + kBlock - 1) / kBlock, (uint64_t)ctx->n_cu * 16);
+        hipLaunchKernelGGL(k_fold_marks, dim3(grid), dim3(kBlock), 0, ctx->stream, ctx->superkey, ctx->n, ctx->xmarks);
+        MG_TRY(hipGetLastError());
+      }
+    } else if (ctx->xchg_prefix && ctx->n && dispatch_w<LaunchPrefixContainKeys>(ctx->maxw, ctx)) {
       return set_err(ctx, "prefix containment launch failed");
+    }
+    ctx->xmarks_done = false;
+    ctx->xmarks = nullptr;
     if (nregions && dispatch_w<LaunchProbeSlots>(ctx->maxw, ctx, true, runs, reg, nregions))
       return set_err(ctx, "probe launch failed");
     MG_TRY(hipEventRecord(ctx->ev[3], ctx->stream));
@@ -4711,6 +4831,28 @@ int mg_xchg_probe(mg_ctx* ctx, int contain, const void* recv, uint64_t slot, uin
   return 0;
 }
 
+int mg_xchg_prefix_marks(mg_ctx* ctx, void* marks) {
+  if (!ctx) return -1;
+  MG_TRY(hipSetDevice(ctx->device));
+  if ((!ctx->xchg && !ctx->xchg_fused) || !ctx->index_ready) return set_err(ctx, "mg_xchg_insert_keys must run first");
+  if (!ctx->superkey) return set_err(ctx, "mg_begin_contained must run first (lengths differ)");
+  MG_TRY(hipEventRecord(ctx->ev[2], ctx->stream));
+  if (ctx->xchg_fused) {  // one rank on the fused build: its own o = 0 keys
+    if (ctx->key0_ready && ctx->n && dispatch_w<LaunchPrefixContain>(ctx->maxw, ctx))
+      return set_err(ctx, "prefix containment launch failed");
+  } else if (ctx->xchg_prefix && ctx->n && dispatch_w<LaunchPrefixContainKeys>(ctx->maxw, ctx)) {
+    return set_err(ctx, "prefix containment launch failed");
+  }
+  ctx->xmarks = reinterpret_cast<uint8_t*>(marks);
+  if (marks && ctx->n) {
+    const uint32_t grid = (uint32_t)std::min<uint64_t>((ctx->n + kBlock - 1) / kBlock, (uint64_t)ctx->n_cu * 16);
+    hipLaunchKernelGGL(k_prefix_marks, dim3(grid), dim3(kBlock), 0, ctx->stream, ctx->superkey, ctx->n, ctx->xmarks);
+    MG_TRY(hipGetLastError());
+  }
+  ctx->xmarks_done = true;
+  return 0;
+}
+
 int mg_begin_contained(mg_ctx* ctx, void* superkey, int* needed) {
   if (!ctx || !needed) return -1;
   MG_TRY(hipSetDevice(ctx->device));
@@ -4719,6 +4861,8 @@ int mg_begin_contained(mg_ctx* ctx, void* superkey, int* needed) {
   ctx->live_ready = false;
   ctx->n_contained = 0;
   ctx->superkey = nullptr;
+  ctx->xmarks_done = false;
+  ctx->xmarks = nullptr;
   if (*needed) {
     if (superkey) {
       ctx->superkey = reinterpret_cast<unsigned long long*>(superkey);
@@ -4743,7 +4887,7 @@ int mg_finalize_contained(mg_ctx* ctx, uint32_t* super_out) {
     if (!ctx->d_ccnt) MG_TRY(hipMalloc(&ctx->d_ccnt, 64 * 16 * sizeof(unsigned int)));
     MG_TRY(hipMemsetAsync(ctx->d_ccnt, 0, 64 * 16 * sizeof(unsigned int), ctx->stream));
     if (ctx->n)
-      hipLaunchKernelGGL(k_super_finalize, dim3((uint32_t)((ctx->n + kBlock - 1) / kBlock)), dim3(kBlock), 0,
+      hipLaunchKernelGGL(k_super_finalize, dim3(super_grid(ctx)), dim3(kBlock), 0,
                          ctx->stream, ctx->superkey, ctx->n, ctx->d_super, ctx->d_any, ctx->d_cbits, ctx->d_ccnt);
     MG_TRY(hipGetLastError());
     unsigned int any = 0;
@@ -4930,6 +5074,7 @@ int mg_get_timings(const mg_ctx* ctx, mg_timings* t) {
 int mg_get_counters(const mg_ctx* ctx, mg_counters* c) {
   if (!ctx || !c) return -1;
   *c = ctx->counters;
+  c->scan_runs = ctx->scan_runs;
   return 0;
 }
 

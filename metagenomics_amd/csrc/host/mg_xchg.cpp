@@ -3,7 +3,8 @@
 //   mg_xchg_begin                          one window scan of this rank's sources
 //   mg_xchg_pack(KEYS) -> RCCL -> mg_xchg_insert_keys     HashTable::insertDataset
 //   mg_xchg_pack(RUNS) -> RCCL
-//   mg_begin_contained; [mg_xchg_probe(1); ncclAllReduce MAX]; mg_finalize_contained
+//   mg_begin_contained; [mg_xchg_prefix_marks; ncclAllReduce MAX (u8);
+//                        mg_xchg_probe(1); ncclAllReduce MAX]; mg_finalize_contained
 //                                                          markContainedReads
 //   mg_xchg_probe(0) -> mg_xchg_pack(ROWS) -> RCCL        insertAllEdgesOfRead
 // Every library call and every collective is enqueued on the context's HIP
@@ -14,6 +15,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <stdexcept>
 #include <thread>
@@ -92,6 +94,13 @@ void RcclExchange::allreduce_max_u64(uint64_t* buf, size_t n, hipStream_t s) {
   const size_t step = kChunkBytes / sizeof(uint64_t);  // bounded payload per collective
   for (size_t i = 0; i < n; i += step)
     nccl_check(ncclAllReduce(buf + i, buf + i, std::min(step, n - i), ncclUint64, ncclMax, comm_, s), "ncclAllReduce");
+}
+
+void RcclExchange::allreduce_max_u8(uint8_t* buf, size_t n, hipStream_t s) {
+  if (world_ == 1) return;
+  for (size_t i = 0; i < n; i += kChunkBytes)
+    nccl_check(ncclAllReduce(buf + i, buf + i, std::min(kChunkBytes, n - i), ncclUint8, ncclMax, comm_, s),
+               "ncclAllReduce");
 }
 
 void RcclExchange::allreduce_max_f64(double* buf, size_t n, hipStream_t s) {
@@ -192,6 +201,16 @@ void LocalTransport::allreduce_max_u64(uint64_t* buf, size_t n, hipStream_t s) {
   finish(s);
 }
 
+void LocalTransport::allreduce_max_u8(uint8_t* buf, size_t n, hipStream_t s) {
+  const int P = g_.world();
+  if (P == 1) return;
+  const std::vector<const void*> peer = exchange_ptr(buf, s);
+  std::vector<uint8_t*> ptrs(P);
+  for (int r = 0; r < P; ++r) ptrs[r] = const_cast<uint8_t*>(static_cast<const uint8_t*>(peer[r]));
+  local_max_u8(ptrs.data(), P, (uint64_t)n * rank_ / P, (uint64_t)n * (rank_ + 1) / P, s);
+  finish(s);
+}
+
 void LocalTransport::allreduce_max_f64(double* buf, size_t n, hipStream_t s) {
   const int P = g_.world();
   if (P == 1) return;
@@ -229,13 +248,20 @@ void slot_geometry(uint64_t cap, int world, uint32_t rec, uint64_t chunk, uint64
   const uint64_t kAlign = cap >= 64 * 1024 ? 1024 : 64;
   const uint64_t per_round = std::max<uint64_t>(kAlign, (chunk / ((uint64_t)world * rec)) / kAlign * kAlign);
   const uint64_t want = std::max<uint64_t>(kAlign, (cap + kAlign - 1) / kAlign * kAlign);
-  *slot = std::min(want, per_round);
-  *rounds = (uint32_t)((want + *slot - 1) / *slot);
+  // the rounds share the stream evenly (sharded.py slot_geometry)
+  *rounds = (uint32_t)((want + per_round - 1) / per_round);
+  const uint64_t even = (want + *rounds - 1) / *rounds;
+  *slot = (even + kAlign - 1) / kAlign * kAlign;
 }
 
 XchgStep::XchgStep(mg_ctx* ctx, Transport& x, uint32_t l, uint32_t k, uint64_t chunk)
     : ctx_(ctx), x_(x), l_(l), k_(k), chunk_(chunk), s_((hipStream_t)mg_stream(ctx)) {
   check(mg_xchg_caps(ctx_, l_, k_, caps_), "mg_xchg_caps");
+  const char* mk = std::getenv("MG_XCHG_MARKS");
+  use_marks_ = mk && mk[0] == '1';  // (off by default: DESIGN.md §6a, measured)
+  hip_check(hipStreamCreateWithFlags(&s2_, hipStreamNonBlocking), "hipStreamCreate");
+  hip_check(hipEventCreateWithFlags(&ev_packed_, hipEventDisableTiming), "hipEventCreate");
+  hip_check(hipEventCreateWithFlags(&ev_runs_, hipEventDisableTiming), "hipEventCreate");
 }
 
 XchgStep::~XchgStep() {
@@ -244,6 +270,10 @@ XchgStep::~XchgStep() {
       if (p) (void)hipFree(p);
   if (superkey_) (void)hipFree(superkey_);
   if (maxbuf_) (void)hipFree(maxbuf_);
+  if (marks_) (void)hipFree(marks_);
+  if (ev_packed_) (void)hipEventDestroy(ev_packed_);
+  if (ev_runs_) (void)hipEventDestroy(ev_runs_);
+  if (s2_) (void)hipStreamDestroy(s2_);
 }
 
 void XchgStep::scale_caps(double f) {
@@ -272,7 +302,9 @@ void XchgStep::ensure(Stream& st, int kind) {
   }
 }
 
-void XchgStep::route(int kind) {
+// pack `kind` on the context's stream, then exchange it on stream s (s_ or the
+// run exchange's s2_, which waits for the pack first)
+void XchgStep::route(int kind, hipStream_t s) {
   Stream& st = st_[kind];
   if (x_.world() == 1) {  // one rank: nothing is packed (mg_xchg_pack at P = 1), the consumers read the context
     if (!st.counts) {
@@ -285,8 +317,12 @@ void XchgStep::route(int kind) {
   }
   ensure(st, kind);
   check(mg_xchg_pack(ctx_, kind, st.send, st.slot, st.rounds, st.counts, st.recv), "mg_xchg_pack");
-  x_.all_to_all_slots(st.send, st.recv, st.slot * mg_record_bytes(kind), st.rounds, s_);
-  x_.all_to_all_u64(st.counts, st.rcounts, s_);
+  if (s != s_) {
+    hip_check(hipEventRecord(ev_packed_, s_), "hipEventRecord");
+    hip_check(hipStreamWaitEvent(s, ev_packed_, 0), "hipStreamWaitEvent");
+  }
+  x_.all_to_all_slots(st.send, st.recv, st.slot * mg_record_bytes(kind), st.rounds, s);
+  x_.all_to_all_u64(st.counts, st.rcounts, s);
 }
 
 int XchgStep::run() {
@@ -295,12 +331,15 @@ int XchgStep::run() {
     if (reruns > 3) throw std::runtime_error("exchange capacities still overflow after 3 reruns");
     // 1. one scan of this rank's sources: index keys + bucket-sorted runs
     check(mg_xchg_begin(ctx_, l_, k_), "mg_xchg_begin");
-    // 2. HashTable::insertDataset: keys -> bucket owners -> local cells
-    route(MG_KEYS);
+    // 2. keys -> bucket owners; 3. runs -> bucket owners (both probes read
+    // them) on the second stream, in flight while 4. the received keys are
+    // sorted and filed into the local cells (HashTable::insertDataset)
+    route(MG_KEYS, s_);
+    route(MG_RUNS, P > 1 ? s2_ : s_);
+    if (P > 1) hip_check(hipEventRecord(ev_runs_, s2_), "hipEventRecord");
     const Stream& ks = st_[MG_KEYS];
     check(mg_xchg_insert_keys(ctx_, ks.recv, ks.slot, ks.rounds, ks.rcounts), "mg_xchg_insert_keys");
-    // 3. runs -> bucket owners (both probes read them)
-    route(MG_RUNS);
+    if (P > 1) hip_check(hipStreamWaitEvent(s_, ev_runs_, 0), "hipStreamWaitEvent");
     const Stream& rs = st_[MG_RUNS];
     // 4. markContainedReads (lengths differ, OverlapGraph.cpp:228-233): MAX of the keys over ranks
     const uint64_t n = mg_num_reads(ctx_);
@@ -312,6 +351,17 @@ int XchgStep::run() {
     int needed = 0;
     check(mg_begin_contained(ctx_, superkey_, &needed), "mg_begin_contained");
     contained_ = needed != 0;
+    if (needed && P > 1 && use_marks_) {
+      // every rank's offset-0 containments first, their marks MAX-reduced: the
+      // probe then skips the sources any rank found contained (contain_skip)
+      if (n > marks_n_) {
+        if (marks_) hip_check(hipFree(marks_), "hipFree");
+        hip_check(hipMalloc(&marks_, std::max<uint64_t>(n, 1)), "hipMalloc");
+        marks_n_ = n;
+      }
+      check(mg_xchg_prefix_marks(ctx_, marks_), "mg_xchg_prefix_marks");
+      x_.allreduce_max_u8(marks_, n, s_);
+    }
     if (needed) {
       check(mg_xchg_probe(ctx_, 1, rs.recv, rs.slot, rs.rounds, rs.rcounts), "mg_xchg_probe(contain)");
       x_.allreduce_max_u64(reinterpret_cast<uint64_t*>(superkey_), n, s_);
@@ -319,7 +369,7 @@ int XchgStep::run() {
     check(mg_finalize_contained(ctx_, nullptr), "mg_finalize_contained");
     // 5. insertAllEdgesOfRead: probe -> rows -> src owners
     check(mg_xchg_probe(ctx_, 0, rs.recv, rs.slot, rs.rounds, rs.rcounts), "mg_xchg_probe");
-    route(MG_ROWS);
+    route(MG_ROWS, s_);
     // the step's one host read: the MAX over ranks of every per-peer send count
     std::vector<uint64_t> c(3 * P);
     for (int kind = 0; kind < 3; ++kind)

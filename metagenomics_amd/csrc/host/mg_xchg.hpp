@@ -40,6 +40,7 @@ class Transport {
   // recv[s] = what rank s sent to this rank (send[r] = what this rank sends to r)
   virtual void all_to_all_u64(const uint64_t* send, uint64_t* recv, hipStream_t s) = 0;
   virtual void allreduce_max_u64(uint64_t* buf, size_t n, hipStream_t s) = 0;
+  virtual void allreduce_max_u8(uint8_t* buf, size_t n, hipStream_t s) = 0;
   virtual void allreduce_max_f64(double* buf, size_t n, hipStream_t s) = 0;
   // recv[r * n + i] = rank r's send[i]
   virtual void allgather_u64(const uint64_t* send, uint64_t* recv, size_t n, hipStream_t s) = 0;
@@ -59,6 +60,7 @@ class RcclExchange : public Transport {
                         hipStream_t s) override;
   void all_to_all_u64(const uint64_t* send, uint64_t* recv, hipStream_t s) override;
   void allreduce_max_u64(uint64_t* buf, size_t n, hipStream_t s) override;
+  void allreduce_max_u8(uint8_t* buf, size_t n, hipStream_t s) override;
   void allreduce_max_f64(double* buf, size_t n, hipStream_t s) override;
   void allgather_u64(const uint64_t* send, uint64_t* recv, size_t n, hipStream_t s) override;
   void barrier(hipStream_t s) override;
@@ -103,6 +105,7 @@ class LocalTransport : public Transport {
                         hipStream_t s) override;
   void all_to_all_u64(const uint64_t* send, uint64_t* recv, hipStream_t s) override;
   void allreduce_max_u64(uint64_t* buf, size_t n, hipStream_t s) override;
+  void allreduce_max_u8(uint8_t* buf, size_t n, hipStream_t s) override;
   void allreduce_max_f64(double* buf, size_t n, hipStream_t s) override;
   void allgather_u64(const uint64_t* send, uint64_t* recv, size_t n, hipStream_t s) override;
   void barrier(hipStream_t s) override;
@@ -118,6 +121,7 @@ class LocalTransport : public Transport {
 // dst[i] = src[i] = max over the P arrays ptrs[r][i] for i in [lo, hi) (every
 // array gets the maximum); enqueued on s (mg_xchg_local.hip)
 void local_max_u64(uint64_t* const* ptrs, int P, uint64_t lo, uint64_t hi, hipStream_t s);
+void local_max_u8(uint8_t* const* ptrs, int P, uint64_t lo, uint64_t hi, hipStream_t s);
 
 // Slot geometry of one stream kind (sharded.py slot_geometry): slot records
 // per peer per round (a multiple of 64) and the number of rounds for `cap`
@@ -154,7 +158,7 @@ class XchgStep {
     uint64_t slot = 0;
     uint32_t rounds = 0;
   };
-  void route(int kind);
+  void route(int kind, hipStream_t s);
   void ensure(Stream& st, int kind);
   void check(int rc, const char* what);
   mg_ctx* ctx_;
@@ -162,11 +166,18 @@ class XchgStep {
   uint32_t l_, k_;
   uint64_t chunk_;
   hipStream_t s_;
+  // the run exchange's own stream: its all-to-all overlaps the received keys'
+  // sort and cell fill on s_ (runs packed -> ev_packed_; runs in -> ev_runs_)
+  hipStream_t s2_ = nullptr;
+  hipEvent_t ev_packed_ = nullptr, ev_runs_ = nullptr;
   uint64_t caps_[3];
   Stream st_[3];
   unsigned long long* superkey_ = nullptr;
   size_t superkey_n_ = 0;
   uint64_t* maxbuf_ = nullptr;  // the three stream maxima, all-reduced
+  uint8_t* marks_ = nullptr;     // cross-rank prefix marks (mg_xchg_prefix_marks), n_reads bytes
+  size_t marks_n_ = 0;
+  bool use_marks_ = true;        // MG_XCHG_MARKS=0: off
   uint64_t rows_held_ = 0;
   bool contained_ = false;
 };

@@ -39,7 +39,7 @@ class _Counters(C.Structure):
     _fields_ = [("sources", C.c_uint64), ("runs", C.c_uint64), ("entries", C.c_uint64),
                 ("verified", C.c_uint64), ("rows", C.c_uint64), ("live_cells", C.c_uint64),
                 ("c_runs", C.c_uint64), ("c_entries", C.c_uint64), ("c_verified", C.c_uint64),
-                ("c_contained", C.c_uint64)]
+                ("c_contained", C.c_uint64), ("scan_runs", C.c_uint64)]
 
 
 _lib = None
@@ -96,6 +96,7 @@ def lib() -> C.CDLL:
         "mg_xchg_probe": (i32, [vp, i32, vp, u64, u32, vp]),
         "mg_slots_digest": (i32, [vp, vp, u64, u32, vp, vp]),
         "mg_begin_contained": (i32, [vp, vp, P(i32)]),
+        "mg_xchg_prefix_marks": (i32, [vp, vp]),
         "mg_finalize_contained": (i32, [vp, vp]),
         "mg_rows_digest": (i32, [vp, vp, u64, vp]),
         "mg_super_digest": (i32, [vp, vp]),
@@ -444,6 +445,11 @@ class OverlapEngine:
     def xchg_probe(self, contain: bool, dptr: int, slot: int, rounds: int, counts_dptr: int):
         self._check(lib().mg_xchg_probe(self._h, int(contain), C.c_void_p(dptr), slot, rounds,
                                         C.c_void_p(counts_dptr)), "xchg_probe")
+
+    def xchg_prefix_marks(self, marks_dptr: int | None):
+        """mg_xchg_prefix_marks: this rank's offset-0 containments now, their marks
+        (n_reads bytes) for the caller's MAX all-reduce before xchg_probe(True)."""
+        self._check(lib().mg_xchg_prefix_marks(self._h, C.c_void_p(marks_dptr or 0)), "xchg_prefix_marks")
 
     def begin_contained(self, superkey_dptr: int | None) -> bool:
         need = C.c_int()

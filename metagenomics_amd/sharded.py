@@ -11,8 +11,10 @@ One step (``sharded_step``):
    by bucket, which also groups them by owning rank;
 2. keys -> bucket owners -> local cells (``HashTable::insertDataset``, HashTable.cpp:50-80);
 3. runs -> bucket owners (kept for both probes);
-4. (mixed lengths) containment probe of the received runs, all-reduce MAX of the per-read
-   containment keys (``markContainedReads``, OverlapGraph.cpp:225-290);
+4. (mixed lengths) [MG_XCHG_MARKS=1: each rank's offset-0 containments and an all-reduce MAX
+   of their marks, so every rank's probe skips sources any rank found contained] the
+   containment probe of the received runs, all-reduce MAX of the per-read containment keys
+   (``markContainedReads``, OverlapGraph.cpp:225-290);
 5. discovery probe + verify of the received runs (``insertAllEdgesOfRead``, OverlapGraph.cpp:529-565)
    -> rows (+ twins, ``insertEdge`` :407-419) -> src owners.
 
@@ -57,8 +59,11 @@ def slot_geometry(cap: int, world: int, rec_bytes: int, chunk_bytes: int):
     align = BIG_SLOT_ALIGN if cap >= 64 * BIG_SLOT_ALIGN else SLOT_ALIGN
     per_round = max(align, (chunk_bytes // (world * rec_bytes)) // align * align)
     want = max(align, -(-int(cap) // align) * align)
-    slot = min(want, per_round)
-    return slot, -(-want // slot)
+    rounds = -(-want // per_round)
+    # the rounds share the stream evenly: a stream just past one round's size
+    # moves ~2x its records with full-size rounds, ~cap with even ones
+    slot = -(-(-(-want // rounds)) // align) * align
+    return slot, rounds
 
 
 @dataclass
@@ -400,6 +405,10 @@ def _replicated_step(engines, xchg, min_overlap, seed_k, want_super):
 
 def _step(engines, xchg, min_overlap, seed_k, want_super, plan):
     P = xchg.world
+    # cross-rank prefix marks (mg_xchg_prefix_marks): off by default -- at C5,
+    # P = 8 the containment probe gained 0.14 ms per rank and the marks cost 0.21 ms plus a
+    # 50 MB all-reduce; MG_XCHG_MARKS=1 turns them on
+    prefix_marks = os.environ.get("MG_XCHG_MARKS", "0") == "1"
     serial = getattr(xchg, "serial", False)
 
     def done():  # (serial simulated ranks: one rank's call at a time on the device)
@@ -461,11 +470,23 @@ def _step(engines, xchg, min_overlap, seed_k, want_super, plan):
                  if contained else None for _ in engines]
         for e, sk in zip(engines, skeys):
             e.begin_contained(sk.data_ptr() if sk is not None else None)
+        if contained and P > 1 and prefix_marks:
+            # every rank's offset-0 containments before the probe: the all-reduced
+            # marks let each rank's probe skip sources another rank found contained
+            marks = [xchg.torch.empty(max(1, engines[0].n_reads), dtype=xchg.torch.uint8, device=xchg.device)
+                     for _ in engines]
+            for e, mk in zip(engines, marks):
+                e.xchg_prefix_marks(mk.data_ptr())
+                done()
+            xchg.allreduce_max(marks)
+        else:
+            marks = None
         if contained:
             for e, (buf, c) in zip(engines, runs):
                 e.xchg_probe(True, buf.data_ptr() if buf is not None else 0, rs, rr, c.data_ptr())
                 done()
             xchg.allreduce_max(skeys)
+        del marks  # (read by the probes above, on the engines' streams: after the all-reduce's sync)
         sup = None
         for i, e in enumerate(engines):
             s = e.finalize_contained(copy=want_super and i == 0)

@@ -84,6 +84,8 @@ class MockEngine:
         self.sk_ptr = 0
         self.super_keys = None
         self.begins = 0
+        self.marks_ptr = 0
+        self.marks_seen = False
 
     def xchg_caps(self, min_overlap, seed_k=0):
         return np.array(self.caps, dtype=np.uint64)
@@ -117,7 +119,18 @@ class MockEngine:
         assert np.all(bucket_owner(recs["x"], self.world) == self.rank), "key record at the wrong rank"
         self.received_keys = recs.copy()
 
+    def xchg_prefix_marks(self, ptr):
+        """marks of this rank's own "offset-0 containments": read (3 a + 1) mod n for
+        every source a; xchg_probe(contain) checks that the caller all-reduced them"""
+        self.marks_ptr = ptr or 0
+        if ptr:
+            m = np.zeros(self.n_reads, np.uint8)  # (the library writes every read's mark)
+            a = np.arange(self.lo, self.hi, dtype=np.int64)
+            m[(3 * a + 1) % self.n_reads] = 1
+            ctypes.memmove(ptr, m.tobytes(), m.nbytes)
+
     def begin_contained(self, ptr):
+        self.marks_ptr = 0
         self.sk_ptr = ptr or 0
         if ptr:
             ctypes.memset(ptr, 0, self.n_reads * 8)
@@ -127,6 +140,12 @@ class MockEngine:
         recs = read_slots(ptr, REC_DTYPE, self.world, slot, rounds, counts_ptr)
         assert np.all(bucket_owner(recs["x"], self.world) == self.rank), "run record at the wrong rank"
         a = recs["y"].astype(np.int64)
+        if contain and self.marks_ptr:  # every rank's marks, MAX-all-reduced by the caller
+            m = np.frombuffer(ctypes.string_at(self.marks_ptr, self.n_reads), dtype=np.uint8)
+            want = np.zeros(self.n_reads, np.uint8)
+            want[(3 * np.arange(self.n_reads, dtype=np.int64) + 1) % self.n_reads] = 1
+            assert np.array_equal(m, want), "prefix marks not all-reduced over the ranks"
+            self.marks_seen = True
         if contain:  # partial maxima the all-reduce must combine
             sk = np.frombuffer(ctypes.string_at(self.sk_ptr, self.n_reads * 8), dtype=np.int64).copy()
             np.maximum.at(sk, (a * 7) % self.n_reads, a + 1)

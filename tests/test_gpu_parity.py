@@ -348,6 +348,19 @@ def test_exchange_mode_matches_reference(name, world):
     assert {str(i): int(s) for i, s in enumerate(sup) if s} == meta["super"]
 
 
+@pytest.mark.parametrize("name,world", [("mixed", 3), ("dirty", 2), ("mixed", 1)])
+def test_exchange_mode_prefix_marks(name, world, monkeypatch):
+    """MG_XCHG_MARKS=1: the cross-rank offset-0 containment marks
+    (mg_xchg_prefix_marks + MAX all-reduce + fold into the keys) before the
+    containment probe; at one rank the fused build's own prefix pass."""
+    monkeypatch.setenv("MG_XCHG_MARKS", "1")
+    meta = load_meta(name)
+    ds = Dataset.from_files([fixture_input(name)], meta["l"])
+    rows, sup = exchange_rows(ds, meta["l"], world)
+    assert np.array_equal(rows_to_tuples(rows), golden_rows(name))
+    assert {str(i): int(s) for i, s in enumerate(sup) if s} == meta["super"]
+
+
 @pytest.mark.parametrize("prefix", [0, 1])
 def test_exchange_mode_containment_paths(prefix):
     """Exchange-mode markContainedReads (OverlapGraph.cpp:225-340) both ways:

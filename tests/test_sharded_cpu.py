@@ -1,7 +1,8 @@
 """Multi-rank exchange orchestration (metagenomics_amd/sharded.py) on CPU with
 the gloo backend, world_size 2 and 3: every key/run record reaches its bucket
 owner, every row reaches its src owner, the union of the ranks' rows is the
-reference multiset, the containment keys are MAX-reduced across ranks, and
+reference multiset, the containment keys (and the prefix marks before the
+containment probe) are MAX-reduced across ranks, and
 streams cut at their slot capacity are detected and the step rerun with grown
 capacities (the mock starts every stream at 64 records).
 The engine is tests/mock_engine.py (routing rules of include/mg_overlap.h); the
@@ -31,6 +32,7 @@ def _worker(rank, world, port, name, outdir, chunk):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
     if chunk:
         os.environ["MG_A2A_CHUNK_BYTES"] = str(chunk)  # force the multi-round exchange
+    os.environ["MG_XCHG_MARKS"] = "1"  # the cross-rank prefix marks' all-reduce (off by default)
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import torch.distributed as dist
@@ -57,6 +59,7 @@ def _worker(rank, world, port, name, outdir, chunk):
     np.save(os.path.join(outdir, f"rows{rank}.npy"), mine)
     np.save(os.path.join(outdir, f"keys{rank}.npy"), eng.received_keys)
     np.save(os.path.join(outdir, f"sk{rank}.npy"), eng.super_keys)
+    np.save(os.path.join(outdir, f"marks{rank}.npy"), np.array([eng.marks_seen, eng.lengths_differ]))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -76,6 +79,8 @@ def test_exchange_routes_every_record(tmp_path, name, world, chunk):
         parts.append(rows)
         keys += np.load(tmp_path / f"keys{r}.npy").shape[0]
         assert np.array_equal(np.load(tmp_path / f"sk{r}.npy"), expected_super_keys(n))
+        seen, differ = np.load(tmp_path / f"marks{r}.npy")
+        assert seen == differ  # the cross-rank prefix marks: made, all-reduced, seen by the containment probe
     assert keys == 4 * n
     rr = [np.load(tmp_path / f"reruns{r}.npy") for r in range(world)]
     assert all(x[0] == rr[0][0] for x in rr), "ranks disagree on the reruns"

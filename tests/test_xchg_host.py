@@ -34,7 +34,7 @@ def golden_super_digest(meta):
     return digest.super_digest(s)
 
 
-def run_cli(inp, l, world, steps=1, k=None, caps=None, timeout=600):
+def run_cli(inp, l, world, steps=1, k=None, caps=None, timeout=600, env=None):
     args = [CLI, "-se", "1", inp, "-f", "/tmp/mg_xchg_host_unused", "-l", str(l), "-xchg", str(steps),
             "-xchg-sim", str(world)]
     if k is not None:
@@ -42,7 +42,7 @@ def run_cli(inp, l, world, steps=1, k=None, caps=None, timeout=600):
     if caps is not None:
         args += ["-xchg-caps", str(caps)]
     out = subprocess.run(["timeout", "-k", "10", str(timeout)] + args, capture_output=True, text=True,
-                         timeout=timeout + 30)
+                         timeout=timeout + 30, env=dict(os.environ, **(env or {})))
     assert out.returncode == 0, out.stderr[-3000:]
     lines = [x for x in out.stdout.splitlines() if x.startswith("{")]
     assert len(lines) == 1, out.stdout[-2000:]
@@ -138,3 +138,17 @@ def test_xchg_host_scale_digest(name, world, caps, tmp_path):
     assert all(h > 0 for h in r["rows_held"])
     if caps is not None:
         assert r["reruns"] >= 1
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,world", [("mixed", 3), ("dirty", 4), ("branchy", 2)])
+def test_xchg_host_prefix_marks(name, world):
+    """MG_XCHG_MARKS=1: each rank's offset-0 containments run first and their
+    marks are MAX-all-reduced (mg_xchg_prefix_marks, RcclExchange /
+    LocalTransport allreduce_max_u8) before the containment probe; same rows and
+    superReadIDs as the reference."""
+    meta = load_meta(name)
+    r = run_cli(fixture_input(name), meta["l"], world, env={"MG_XCHG_MARKS": "1"})
+    g = golden_rows(name)
+    assert r["rows"] == digest.rows_digest(g[:, 0], g[:, 1], g[:, 2], g[:, 3])
+    assert r["super"] == golden_super_digest(meta)

@@ -28,8 +28,8 @@ for s in $STEPS; do
     done ;;
   simrep)
     for P in 2 4 8; do
-      timeout -k 10 300 python -u bench.py --sim-world $P --multi replicated --steps 3 --no-cpu-baseline --no-ingest > $OUT/bench_simrep$P.json 2> $OUT/bench_simrep$P.err
-      rc=$?; echo "bench sim replicated $P rc=$rc"; python3 -c "import json;d=json.load(open('$OUT/bench_simrep$P.json'));print(d['ms_per_step'], d['value'], d['undirected_edges'], d.get('sim_rank_ms'))"; [ $rc -ne 0 ] && break
+      timeout -k 10 300 python -u bench.py --sim-world $P --multi replicated --steps 3 --no-cpu-baseline --no-ingest $SIMOPTS > $OUT/bench_simrep$P.json 2> $OUT/bench_simrep$P.err
+      rc=$?; echo "bench sim replicated $P rc=$rc"; python3 -c "import json;d=json.load(open('$OUT/bench_simrep$P.json'));print(round(d['ms_per_step'],3), d['value'], d['undirected_edges'], d['parity'].get('digest_ok'), [round(x,3) for x in d.get('sim_rank_ms')], {k:round(v,3) for k,v in d['device_ms'].items()})"; [ $rc -ne 0 ] && break
     done ;;
   xchg1)
     timeout -k 10 300 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29511 bench.py --exchange --steps 5 --no-cpu-baseline --no-ingest > $OUT/bench_xchg1.json 2> $OUT/bench_xchg1.err
@@ -51,7 +51,7 @@ for s in $STEPS; do
     timeout -k 10 1100 python -u -m pytest tests/test_scale_digest.py -x -v -m gpu --timeout 900 --timeout-method thread > $OUT/digest_tests.log 2>&1
     rc=$?; echo "digest tests rc=$rc"; grep -E "PASS|FAIL|SKIP|Error" $OUT/digest_tests.log | tail -12 ;;
   parity)
-    timeout -k 10 900 python -u -m pytest tests/test_gpu_parity.py -x -q -m gpu --timeout 300 --timeout-method thread > $OUT/parity_tests.log 2>&1
+    timeout -k 10 900 python -u -m pytest tests/test_gpu_parity.py tests/test_hashtable_api.py -x -q -m gpu --timeout 300 --timeout-method thread > $OUT/parity_tests.log 2>&1
     rc=$?; echo "parity tests rc=$rc"; tail -3 $OUT/parity_tests.log ;;
   c3digest)
     timeout -k 10 900 python -u -m pytest tests/test_scale_digest.py -x -v -m gpu -k "c3 or c5s" --timeout 900 --timeout-method thread > $OUT/c3digest_tests.log 2>&1
@@ -139,6 +139,33 @@ for s in $STEPS; do
   prof5)
     timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof5 -o kt -- python3 bench.py --config c5 --steps 2 --no-cpu-baseline --no-ingest --no-one-shot > $OUT/prof5_bench.json 2> $OUT/prof5_bench.err
     rc=$?; echo "prof5 rc=$rc"; head -10 $OUT/prof5/kt_kernel_stats.csv | cut -c1-160 ;;
+  profsimP)
+    # per-rank kernel tables of the exchange mode at P in $SIMP (default 2 4 8), configs in
+    # $SIMC (default c3 c5), simulated ranks one call at a time (MG_SIM_SERIAL)
+    for C in ${SIMC:-c3 c5}; do
+      for P in ${SIMP:-2 4 8}; do
+        MG_SIM_SERIAL=1 timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/profsim${P}_$C -o kt -- python3 bench.py --config $C --sim-world $P --multi exchange --steps 2 --no-cpu-baseline --no-ingest --opt layout_scratch=0 $SIMOPTS > $OUT/profsim${P}_${C}_bench.json 2> $OUT/profsim${P}_${C}_bench.err
+        rc=$?; echo "profsim $P $C rc=$rc"; [ $rc -ne 0 ] && break 2
+        python3 tools/rank_table.py $OUT/profsim${P}_$C/kt_kernel_stats.csv $P 4 "$C exchange-sim" > $OUT/profsim${P}_${C}_ranks.md
+        tail -3 $OUT/profsim${P}_${C}_ranks.md
+      done
+    done ;;
+  wattr)
+    # C5 k_scan<INDEX> write attribution: WRITE_SIZE of the default build,
+    # of the same build with no index inserts (option phase_limit=1), and of the 4-wave
+    # spill-free variant (metagenomics_amd/lib/variants/scan_w4.so)
+    for V in ${WATTR:-default noins w4}; do
+      case $V in
+        default) o=""; lib="" ;;
+        noins) o="--opt phase_limit=1"; lib="" ;;
+        w4) o=""; lib=$PWD/metagenomics_amd/lib/variants/scan_w4.so ;;
+        *) o="--opt phase_limit=1"; lib=$PWD/metagenomics_amd/lib/variants/$V.so ;;  # diagnostics builds, inserts off
+      esac
+      MG_LIB=$lib timeout -s KILL 400 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $OUT/wattr_$V -o p -- python3 bench.py --config c5 --steps 1 --warmup 0 --no-cpu-baseline --no-ingest --no-one-shot --no-d2h $o > $OUT/wattr_$V.log 2>&1
+      rc=$?; echo "wattr $V rc=$rc"; [ $rc -ne 0 ] && break
+      python3 tools/pmc_summary.py $OUT/wattr_$V.json $OUT/wattr_$V > /dev/null
+      python3 -c "import json;d=json.load(open('$OUT/wattr_$V.json'))['kernels'];[print('  ',k,round(v.get('WRITE_SIZE',0)/2**20,3),'GiB') for k,v in d.items() if k.startswith('k_scan') or k.startswith('k_probe')]"
+    done ;;
   xhost)
     timeout -k 10 900 python -u -m pytest tests/test_xchg_host.py -x -v -m gpu --timeout 700 --timeout-method thread > $OUT/xhost_tests.log 2>&1
     rc=$?; echo "C++ exchange host tests rc=$rc"; grep -E "PASS|FAIL|Error" $OUT/xhost_tests.log | tail -30 ;;

@@ -8,7 +8,9 @@
 //   head[i] = (over && (first || fp(ent[i]) != fp(ent[i - 1]))) ? i : 0;
 // and the shipped source forms it with a multiply over unconditional loads.
 // This program runs three forms on the same sorted records and checks each
-// against a host restatement:
+// against a host restatement (and a fourth, FLAGS, that audits the helpers the
+// forms share: rank_in_cell and over_rec's over / first flags, whose own
+// short-circuit guards i >= k && key[i - k] are the same pattern):
 //   SELECT  the round-4 expression, verbatim;
 //   MUL     the shipped expression;
 //   GUARD   the nested select with the i - 1 load guarded (ent[i ? i - 1 : 0]).
@@ -63,7 +65,7 @@ __device__ __forceinline__ bool over_rec(const uint32_t* __restrict__ key, uint6
   return true;
 }
 
-enum Form { SELECT = 0, MUL = 1, GUARD = 2 };
+enum Form { SELECT = 0, MUL = 1, GUARD = 2, FLAGS = 3 };
 
 template <int F>
 __global__ __launch_bounds__(kBlock) void k_over_heads(const uint32_t* __restrict__ key,
@@ -75,7 +77,9 @@ __global__ __launch_bounds__(kBlock) void k_over_heads(const uint32_t* __restric
     const uint32_t g = key[i] >> gshift;
     bool first = false;
     const bool over = !(skip_odd && (g & 1u)) && over_rec(key, i, gshift, g, &first);
-    if (F == SELECT) {
+    if (F == FLAGS) {  // the audit of the helpers themselves: rank | over << 4 | first << 5
+      head[i] = (uint32_t)rank_in_cell(key, i, gshift, g) | (over ? 16u : 0u) | (first ? 32u : 0u);
+    } else if (F == SELECT) {
       head[i] = (over && (first || entry_fp(ent[i]) != entry_fp(ent[i - 1]))) ? (uint32_t)i : 0u;
     } else if (F == GUARD) {
       head[i] = (over && (first || entry_fp(ent[i]) != entry_fp(ent[i ? i - 1 : 0]))) ? (uint32_t)i : 0u;
@@ -117,6 +121,16 @@ int main(int argc, char** argv) {
     const bool first = !(i >= kCell + 1 && (key[i - kCell - 1] >> gshift) == g);
     if (first || entry_fp(ent[i]) != entry_fp(ent[i - 1])) want[i] = (uint32_t)i;
   }
+  // the helpers' own outputs (rank_in_cell, over_rec's over and first), as FLAGS writes them
+  std::vector<uint32_t> want_flags(n, 0);
+  for (uint64_t i = 0; i < n; ++i) {
+    const uint32_t g = key[i] >> gshift;
+    int r = 0;
+    for (int k = 1; k <= kCell; ++k) r = (r == k - 1 && i >= (uint64_t)k && (key[i - k] >> gshift) == g) ? k : r;
+    const bool over = r == kCell;
+    const bool first = over && !(i >= kCell + 1 && (key[i - kCell - 1] >> gshift) == g);
+    want_flags[i] = (uint32_t)r | (over ? 16u : 0u) | (first ? 32u : 0u);
+  }
   uint32_t *dk = nullptr, *dh = nullptr;
   uint64_t* de = nullptr;
   unsigned long long* dn = nullptr;
@@ -138,26 +152,28 @@ int main(int argc, char** argv) {
   std::printf("{\"records\": %llu, \"heads\": %llu, \"grid\": %u}\n", (unsigned long long)n,
               (unsigned long long)heads, grid);
   std::vector<uint32_t> got(n);
-  const char* names[3] = {"select", "mul", "guard"};
-  for (int f = 0; f < 3; ++f)
+  const char* names[4] = {"select", "mul", "guard", "flags"};
+  for (int f = 0; f < 4; ++f)
     for (int use_dev = 0; use_dev < 2; ++use_dev) {
       CK(hipMemset(dh, 0xAB, n * 4));
       const unsigned long long* ndp = use_dev ? dn : nullptr;
       if (f == SELECT) hipLaunchKernelGGL(k_over_heads<SELECT>, dim3(grid), dim3(kBlock), 0, 0, dk, de, ndp, n, gshift, 1, dh);
       if (f == MUL) hipLaunchKernelGGL(k_over_heads<MUL>, dim3(grid), dim3(kBlock), 0, 0, dk, de, ndp, n, gshift, 1, dh);
       if (f == GUARD) hipLaunchKernelGGL(k_over_heads<GUARD>, dim3(grid), dim3(kBlock), 0, 0, dk, de, ndp, n, gshift, 1, dh);
+      if (f == FLAGS) hipLaunchKernelGGL(k_over_heads<FLAGS>, dim3(grid), dim3(kBlock), 0, 0, dk, de, ndp, n, gshift, 1, dh);
+      const std::vector<uint32_t>& ref = f == FLAGS ? want_flags : want;
       CK(hipGetLastError());
       CK(hipDeviceSynchronize());
       CK(hipMemcpy(got.data(), dh, n * 4, hipMemcpyDeviceToHost));
       uint64_t bad = 0, bad_head = 0, bad_zero = 0;
       std::string first_bad;
       for (uint64_t i = 0; i < n; ++i)
-        if (got[i] != want[i]) {
+        if (got[i] != ref[i]) {
           ++bad;
           (want[i] ? bad_head : bad_zero) += 1;
           if (bad <= 5)
             first_bad += (bad > 1 ? ", " : "") + std::string("[") + std::to_string(i) + ", " +
-                         std::to_string(want[i]) + ", " + std::to_string(got[i]) + "]";
+                         std::to_string(ref[i]) + ", " + std::to_string(got[i]) + "]";
         }
       std::printf(
           "{\"form\": \"%s\", \"n_dev\": %d, \"wrong\": %llu, \"wrong_at_heads\": %llu, \"wrong_elsewhere\": %llu, "
