@@ -96,6 +96,7 @@ struct mg_ctx {
   // uncontained reads (:548 drops contained partners), so it probes a table of
   // those alone, sized for them (C5: a quarter of the entries and chains)
   bool live_index = true;
+  bool live_runs = true;          // option live_runs: k_live_runs compacts the runs of contained sources before discovery
   bool live_ready = false;
   uint64_t* d_lcells = nullptr;
   size_t lcells_cap = 0;
@@ -120,6 +121,7 @@ struct mg_ctx {
   uint64_t read_lo = 0, read_hi = 0;  // source-read range: reference IDs - 1 = slots [read_lo, read_hi)
   uint32_t max_blocks = 8192;  // cap on the persistent discovery grid (blocks of 4 wavefronts)
   int phase_limit = 99;        // diagnostics (option "phase_limit")
+  int contain_phase_limit = 99;  // diagnostics (option "contain_phase_limit")
   bool halving_low = false;    // option "halving": o=2/3 pair side rule
   int n_cu = 256;              // compute units of the device
   uint64_t nreg = 0;           // row regions of the last discovery launch (one per probe wavefront)
@@ -127,6 +129,7 @@ struct mg_ctx {
   ulonglong2* d_runs = nullptr;  // run records, one region per wavefront
   size_t runs_cap = 0;
   uint64_t run_cap = 0, run_cap_need = 0, run_cap_opt = 0;  // run_cap_opt: option "run_cap" (tests)
+  bool run_skew = true;  // option run_skew: run regions an odd number of 128-B lines apart
   unsigned long long* d_run_cnt = nullptr;
   size_t run_cnt_cap = 0;
   std::vector<unsigned long long> run_cnt_host;

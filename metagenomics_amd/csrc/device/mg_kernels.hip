@@ -159,7 +159,10 @@ constexpr int kScanKeyPad = 1;
 // runs of group j of a window go to the wavefront's run region j (G regions
 // per wave).  G = kWinGroups for the fused index scan of mixed lengths, 1
 // (one group, no sort) otherwise.
-constexpr int kWinGroups = 4;
+#ifndef MG_WIN_GROUPS
+#define MG_WIN_GROUPS 4  // (A/B and diagnostics builds override)
+#endif
+constexpr int kWinGroups = MG_WIN_GROUPS;
 constexpr int kStageRing = 512;   // register scan: LDS ring of staged run metas per wavefront
 constexpr uint64_t kEmpty = ~0ULL;       // free slot (a read index is never 0xFFFFFFFF)
 constexpr uint64_t kChain = 1ULL << 63;  // on a cell's last slot: the chain continues in the next cell
@@ -1007,7 +1010,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(G > 1 ? 
       if constexpr (G == 1) {
         const uint64_t bal = __ballot(flag);
         const uint64_t at = cur[0] + lane_prefix(bal);
+#if defined(MG_DIAG_STORE_NEVER)
+        if (flag && at < p.run_cap && v == 0x0123456789ABCDEFull) region[at] = make_ulonglong2(v, meta);
+#elif !defined(MG_DIAG_NO_RUNSTORE)
         if (flag && at < p.run_cap) region[at] = make_ulonglong2(v, meta);
+#endif
         cur[0] += (uint64_t)__popcll(bal);
       } else {
 #ifdef MG_DIAG_ONE_REGION  // (diagnostics build: every run of a window into its first region)
@@ -1022,7 +1029,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(G > 1 ? 
           if (grp == (uint32_t)j) at = cur[j] + lane_prefix(bal);
           cur[j] += (uint64_t)__popcll(bal);
         }
+#if defined(MG_DIAG_STORE_NEVER)  // (diagnostics build: runs hashed and placed, but (practically) never stored)
+        if (flag && at < p.run_cap && v == 0x0123456789ABCDEFull) region[grp * p.run_cap + at] = make_ulonglong2(v, meta);
+#elif !defined(MG_DIAG_NO_RUNSTORE)  // (diagnostics build: the window scan stores no runs)
         if (flag && at < p.run_cap) region[grp * p.run_cap + at] = make_ulonglong2(v, meta);
+#endif
       }
       const uint32_t rest = nbuf - k;  // < 128 left: move them to the front
       const uint64_t m0 = (uint32_t)lane < rest ? s_buf[k + lane] : 0;
@@ -3024,6 +3035,10 @@ struct LaunchScan {
     const uint64_t groups_per_region = ((ngroups + G - 1) / G + nw - 1) / nw;  // windows per wave
     uint64_t run_cap = std::max<uint64_t>(
         ctx->run_cap_need, ctx->run_cap_opt ? ctx->run_cap_opt : groups_per_region * kWave * per_read);
+    // regions an odd number of 128-B lines apart (run_skew): the scan's write
+    // fronts advance through their regions at about the same rate, and a stride
+    // with a large power-of-two factor put them all on the same L2 sets
+    if (ctx->run_skew && !ctx->run_cap_opt) run_cap = ((run_cap + 7) / 8 | 1) * 8;
     if (run_cap * nreg > ctx->runs_cap) {
       if (ctx->d_runs) (void)hipFree(ctx->d_runs);
       ctx->d_runs = nullptr;
@@ -3031,7 +3046,10 @@ struct LaunchScan {
       if (hipMalloc(&ctx->d_runs, run_cap * nreg * sizeof(ulonglong2)) != hipSuccess) return -1;
       ctx->runs_cap = run_cap * nreg;
     }
-    if (!ctx->run_cap_opt) run_cap = ctx->runs_cap / std::max<uint64_t>(1, nreg);
+    if (!ctx->run_cap_opt) {
+      run_cap = ctx->runs_cap / std::max<uint64_t>(1, nreg);
+      if (ctx->run_skew && run_cap >= 8) run_cap = ((run_cap / 8 - 1) | 1) * 8;  // (<= the capacity, 8 x odd)
+    }
     ctx->run_cap = run_cap;
     if (ctx->run_cnt_cap < nreg) {
       if (ctx->d_run_cnt) (void)hipFree(ctx->d_run_cnt);
@@ -3160,7 +3178,7 @@ struct LaunchProbe {
     pp.reg_cap = contain ? 0 : ctx->rows_cap / ctx->nreg;
     pp.uniform_len = ctx->minlen == ctx->maxlen ? (int)ctx->maxlen : 0;
     pp.stats = ctx->stats ? ctx->d_stats : nullptr;
-    pp.phase_limit = contain ? 99 : ctx->phase_limit;
+    pp.phase_limit = contain ? ctx->contain_phase_limit : ctx->phase_limit;
     pp.halving_low = ctx->halving_low ? 1 : 0;
     pp.halving_id = (ctx->read_lo || ctx->read_hi) ? ctx->d_id : nullptr;
     pp.contain_even = (contain && (ctx->xchg ? ctx->xchg_prefix : ctx->key0_ready)) ? 1 : 0;
@@ -3559,6 +3577,10 @@ int mg_set_option(mg_ctx* ctx, const char* name, int64_t value) {
     ctx->phase_limit = value > 0 ? (int)value : 99;
     return 0;
   }
+  if (!strcmp(name, "contain_phase_limit")) {  // diagnostics: stop the containment probe after a phase
+    ctx->contain_phase_limit = value > 0 ? (int)value : 99;
+    return 0;
+  }
   if (!strcmp(name, "index_keys")) {  // index builds without a scan: one read per lane (default 1)
     ctx->index_keys = value != 0;
     return 0;
@@ -3589,7 +3611,8 @@ int mg_set_option(mg_ctx* ctx, const char* name, int64_t value) {
       flag("contain_prune", &ctx->contain_prune) || flag("probe_share", &ctx->probe_share) ||
       flag("probe_compact", &ctx->probe_compact) || flag("live_index", &ctx->live_index) ||
       flag("xchg_sort_runs", &ctx->xchg_sort_runs) || flag("layout_scratch", &ctx->layout_scratch) ||
-      flag("xchg_windows", &ctx->xchg_windows) || flag("chain_par", &ctx->chain_par))
+      flag("xchg_windows", &ctx->xchg_windows) || flag("chain_par", &ctx->chain_par) ||
+      flag("live_runs", &ctx->live_runs) || flag("run_skew", &ctx->run_skew))
     return 0;
   if (flag("prefix_contain", &ctx->prefix_contain)) {
     ctx->index_ready = false;
@@ -4093,7 +4116,7 @@ int probe_shared(mg_ctx* ctx, bool contain) {
     ctx->nreg = 0;
     MG_TRY(hipEventRecord(ctx->ev[8], ctx->stream));
     if (!contain && attempt == 0 && ctx->contained_done && build_live_index(ctx)) return -1;
-    if (!contain && ctx->contained_done && ctx->super_any && !ctx->runs_live && ctx->nrun_reg) {
+    if (!contain && ctx->contained_done && ctx->super_any && !ctx->runs_live && ctx->nrun_reg && ctx->live_runs) {
       const uint32_t grid = (uint32_t)std::min<uint64_t>((ctx->nrun_reg + kWavesPerBlock - 1) / kWavesPerBlock,
                                                          (uint64_t)ctx->n_cu * 8);
       hipLaunchKernelGGL(k_live_runs, dim3(grid), dim3(kBlock), 0, ctx->stream, ctx->d_runs, ctx->d_run_cnt,

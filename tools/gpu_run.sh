@@ -79,6 +79,28 @@ for s in $STEPS; do
         done
       done
     done ;;
+  fusedab)
+    # fused-path option A/B pairs (alternating processes, one box): MG_AB="opt=v ..." vs default,
+    # configs in FUSEDAB_CONFIGS (default c5)
+    for C in ${FUSEDAB_CONFIGS:-c5}; do
+      for rep in 1 2; do
+        for V in "" "$MG_AB"; do
+          o=""; for kv in $V; do o="$o --opt $kv"; done
+          timeout -k 10 400 python -u bench.py --config $C --steps 5 --no-cpu-baseline --no-ingest --no-one-shot --no-d2h $o > $OUT/fusedab.json 2> $OUT/fusedab.err
+          rc=$?; [ $rc -ne 0 ] && break 3
+          python3 -c "import json;d=json.load(open('$OUT/fusedab.json'));print('$C','[$V]','ms/step',round(d['ms_per_step'],3),'digest_ok',d['parity'].get('digest_ok'),{k:round(v,3) for k,v in d['device_ms'].items() if v})" | tee -a $OUT/fusedab.log
+        done
+      done
+    done ;;
+  optsweep)
+    # one fused bench per option set: OPTSETS="a=1 b=2;c=3;..." ("" = default), config SWEEP_CONFIG (c5)
+    IFS=';' read -ra sets <<< "${OPTSETS}"
+    for V in "" "${sets[@]}"; do
+      o=""; for kv in $V; do o="$o --opt $kv"; done
+      timeout -k 10 400 python -u bench.py --config ${SWEEP_CONFIG:-c5} --steps 3 --no-cpu-baseline --no-ingest --no-one-shot --no-d2h $o > $OUT/optsweep.json 2> $OUT/optsweep.err
+      rc=$?; [ $rc -ne 0 ] && break
+      python3 -c "import json;d=json.load(open('$OUT/optsweep.json'));print('${SWEEP_CONFIG:-c5}','[$V]','ms/step',round(d['ms_per_step'],3),'digest_ok',d['parity'].get('digest_ok'),{k:round(v,3) for k,v in d['device_ms'].items() if v},{k:v for k,v in d['counters'].items() if v})" | tee -a $OUT/optsweep.log
+    done ;;
   a2a)
     timeout -k 10 300 python -u tools/a2a_probe.py > $OUT/a2a_probe.log 2>&1
     rc=$?; echo "a2a_probe rc=$rc"; grep MB $OUT/a2a_probe.log ;;
@@ -161,10 +183,10 @@ for s in $STEPS; do
         w4) o=""; lib=$PWD/metagenomics_amd/lib/variants/scan_w4.so ;;
         *) o="--opt phase_limit=1"; lib=$PWD/metagenomics_amd/lib/variants/$V.so ;;  # diagnostics builds, inserts off
       esac
-      MG_LIB=$lib timeout -s KILL 400 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $OUT/wattr_$V -o p -- python3 bench.py --config c5 --steps 1 --warmup 0 --no-cpu-baseline --no-ingest --no-one-shot --no-d2h $o > $OUT/wattr_$V.log 2>&1
+      MG_LIB=$lib timeout -s KILL 400 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $OUT/wattr_${WATTR_CONFIG:-c5}_$V -o p -- python3 bench.py --config ${WATTR_CONFIG:-c5} --steps 1 --warmup 0 --no-cpu-baseline --no-ingest --no-one-shot --no-d2h $o > $OUT/wattr_$V.log 2>&1
       rc=$?; echo "wattr $V rc=$rc"; [ $rc -ne 0 ] && break
-      python3 tools/pmc_summary.py $OUT/wattr_$V.json $OUT/wattr_$V > /dev/null
-      python3 -c "import json;d=json.load(open('$OUT/wattr_$V.json'))['kernels'];[print('  ',k,round(v.get('WRITE_SIZE',0)/2**20,3),'GiB') for k,v in d.items() if k.startswith('k_scan') or k.startswith('k_probe')]"
+      python3 tools/pmc_summary.py $OUT/wattr_${WATTR_CONFIG:-c5}_$V.json $OUT/wattr_${WATTR_CONFIG:-c5}_$V > /dev/null
+      python3 -c "import json;d=json.load(open('$OUT/wattr_${WATTR_CONFIG:-c5}_$V.json'))['kernels'];[print('  ',k,round(v.get('WRITE_SIZE',0)/2**20,3),'GiB') for k,v in d.items() if k.startswith('k_scan') or k.startswith('k_probe')]"
     done ;;
   xhost)
     timeout -k 10 900 python -u -m pytest tests/test_xchg_host.py -x -v -m gpu --timeout 700 --timeout-method thread > $OUT/xhost_tests.log 2>&1
