@@ -10,13 +10,19 @@ Default workload = BASELINE.json configs[2] (C3): 10M x 150 bp synthetic
 reads, 20x coverage of a 75 Mb random genome, 50 % reverse-complemented,
 l = 50, seed k = 31.  Multi-GPU (torchrun, one process per GPU): the same 10M
 reads on N GPUs (strong scaling), DESIGN.md §6:
-  --multi exchange (default, north_star): each rank owns a bucket range of
-    the index and a source-read range; key records, window runs and rows move
-    between ranks with equal-split RCCL all-to-alls over xGMI
-    (torch.distributed "nccl"), ordered on the engine's HIP stream;
+  --multi auto (default): replicated when every read has one length (no
+    containment pass), exchange when lengths differ (DESIGN.md §6c);
   --multi replicated: every rank builds the whole index and discovers from
     its source-read range; no data-path collective (the process group carries
-    only the barrier and the step clock).
+    only the barrier and the step clock).  At C3 its modelled wall beats the
+    exchange mode's at P = 2, 4 and 8 on xGMI's per-link rate
+    (profiles/r05k_xchg_model_c3.md); its containment pass does not divide, so
+    mixed lengths take the exchange mode;
+  --multi exchange (north_star's bucket-range design, BASELINE configs[3]):
+    each rank owns a bucket range of the index and a source-read range; key
+    records, window runs and rows move between ranks with equal-split RCCL
+    all-to-alls over xGMI (torch.distributed "nccl"), ordered on the engine's
+    HIP stream.
 --sim-world P runs all P ranks of the chosen mode inside one process on one
 GPU (replicated: each rank timed alone, step = slowest rank; exchange:
 buffers exchanged on the device).
@@ -324,11 +330,12 @@ def main():
                     help="run all SIM-WORLD ranks of the exchange mode in this process on one GPU")
     ap.add_argument("--exchange", action="store_true",
                     help="use the RCCL exchange mode even with one rank (checks the torch.distributed plumbing)")
-    ap.add_argument("--multi", choices=["replicated", "exchange"], default="exchange",
-                    help="N > 1 (and --sim-world): exchange (default, north_star) = bucket-range index shards + "
-                         "RCCL all-to-all of keys, runs and rows (SURVEY 8(e) main design); replicated = every rank "
-                         "builds the whole index and probes its source-read range, no data-path collective "
-                         "(SURVEY 8(e)(ii))")
+    ap.add_argument("--multi", choices=["auto", "replicated", "exchange"], default="auto",
+                    help="N > 1 (and --sim-world): auto (default) = replicated for one read length, exchange for "
+                         "mixed lengths; replicated = every rank builds the whole index and "
+                         "probes its source-read range, no data-path collective (SURVEY 8(e)(ii)); exchange "
+                         "(north_star, BASELINE configs[3]) = bucket-range index shards + RCCL all-to-all of keys, "
+                         "runs and rows (SURVEY 8(e) main design).  DESIGN.md 6c: per-rank tables + xGMI model")
     ap.add_argument("--cpu-sample", type=int, default=200_000)
     ap.add_argument("--no-cpu-full", action="store_true", help="skip the reference's full-build timing")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -356,6 +363,8 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     cfg = CONFIGS[args.config]
     n, lo, hi, G, l, k, seed, desc = cfg
+    if args.multi == "auto":  # the replicated mode's containment pass does not divide by P
+        args.multi = "replicated" if lo == hi else "exchange"
     nthreads = max(2, 16 // max(1, world))
     ds, codes, lens, host_ingest_s = make_dataset(cfg, nthreads, args.config)
     N = ds.num_unique

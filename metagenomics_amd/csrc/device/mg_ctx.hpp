@@ -129,7 +129,6 @@ struct mg_ctx {
   ulonglong2* d_runs = nullptr;  // run records, one region per wavefront
   size_t runs_cap = 0;
   uint64_t run_cap = 0, run_cap_need = 0, run_cap_opt = 0;  // run_cap_opt: option "run_cap" (tests)
-  bool run_skew = true;  // option run_skew: run regions an odd number of 128-B lines apart
   unsigned long long* d_run_cnt = nullptr;
   size_t run_cnt_cap = 0;
   std::vector<unsigned long long> run_cnt_host;

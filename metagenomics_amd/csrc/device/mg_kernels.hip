@@ -3035,10 +3035,6 @@ struct LaunchScan {
     const uint64_t groups_per_region = ((ngroups + G - 1) / G + nw - 1) / nw;  // windows per wave
     uint64_t run_cap = std::max<uint64_t>(
         ctx->run_cap_need, ctx->run_cap_opt ? ctx->run_cap_opt : groups_per_region * kWave * per_read);
-    // regions an odd number of 128-B lines apart (run_skew): the scan's write
-    // fronts advance through their regions at about the same rate, and a stride
-    // with a large power-of-two factor put them all on the same L2 sets
-    if (ctx->run_skew && !ctx->run_cap_opt) run_cap = ((run_cap + 7) / 8 | 1) * 8;
     if (run_cap * nreg > ctx->runs_cap) {
       if (ctx->d_runs) (void)hipFree(ctx->d_runs);
       ctx->d_runs = nullptr;
@@ -3046,10 +3042,7 @@ struct LaunchScan {
       if (hipMalloc(&ctx->d_runs, run_cap * nreg * sizeof(ulonglong2)) != hipSuccess) return -1;
       ctx->runs_cap = run_cap * nreg;
     }
-    if (!ctx->run_cap_opt) {
-      run_cap = ctx->runs_cap / std::max<uint64_t>(1, nreg);
-      if (ctx->run_skew && run_cap >= 8) run_cap = ((run_cap / 8 - 1) | 1) * 8;  // (<= the capacity, 8 x odd)
-    }
+    if (!ctx->run_cap_opt) run_cap = ctx->runs_cap / std::max<uint64_t>(1, nreg);
     ctx->run_cap = run_cap;
     if (ctx->run_cnt_cap < nreg) {
       if (ctx->d_run_cnt) (void)hipFree(ctx->d_run_cnt);
@@ -3612,7 +3605,7 @@ int mg_set_option(mg_ctx* ctx, const char* name, int64_t value) {
       flag("probe_compact", &ctx->probe_compact) || flag("live_index", &ctx->live_index) ||
       flag("xchg_sort_runs", &ctx->xchg_sort_runs) || flag("layout_scratch", &ctx->layout_scratch) ||
       flag("xchg_windows", &ctx->xchg_windows) || flag("chain_par", &ctx->chain_par) ||
-      flag("live_runs", &ctx->live_runs) || flag("run_skew", &ctx->run_skew))
+      flag("live_runs", &ctx->live_runs))
     return 0;
   if (flag("prefix_contain", &ctx->prefix_contain)) {
     ctx->index_ready = false;

@@ -277,3 +277,28 @@ def test_exchange_two_processes(name):
     r = json.loads([x for x in out.stdout.splitlines() if x.startswith("{")][-1])
     assert r["n_gpus"] == 2 and r["config"]["parallelism"].startswith("2 ranks")
     assert r["parity"]["golden"] and r["parity"]["digest_ok"] is True, r["parity"]
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("name,mode", [("c2", "whole index on every rank"), ("c5s", "bucket-range index")])
+def test_two_processes_default_mode(name, mode):
+    """bench.py --gpus N with no --multi (auto: the replicated mode for one read
+    length, the exchange mode for mixed lengths) as the driver's
+    N-GPU runs launch it: two torchrun processes, each rank's own context; gloo
+    for the barrier and the clocks (two ranks share this one GPU).  The rows and
+    superReadIDs over both ranks have the reference's digests."""
+    import subprocess
+    import sys
+
+    if not os.path.exists(SCALE[name]):
+        pytest.skip(f"{name}.json not generated")
+    env = dict(os.environ, MG_BENCH_PG_BACKEND="gloo")
+    args = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+            "--master-addr", "127.0.0.1", "--master-port", "29735", os.path.join(ROOT, "bench.py"),
+            "--gpus", "2", "--config", name, "--steps", "1", "--warmup", "1", "--no-cpu-baseline", "--no-ingest"]
+    out = subprocess.run(args, capture_output=True, text=True, timeout=800, env=env)
+    assert out.returncode == 0, out.stderr[-3000:]
+    r = json.loads([x for x in out.stdout.splitlines() if x.startswith("{")][-1])
+    assert r["n_gpus"] == 2 and mode in r["config"]["parallelism"]
+    assert r["parity"]["golden"] and r["parity"]["digest_ok"] is True, r["parity"]

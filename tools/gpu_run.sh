@@ -28,8 +28,8 @@ for s in $STEPS; do
     done ;;
   simrep)
     for P in 2 4 8; do
-      timeout -k 10 300 python -u bench.py --sim-world $P --multi replicated --steps 3 --no-cpu-baseline --no-ingest $SIMOPTS > $OUT/bench_simrep$P.json 2> $OUT/bench_simrep$P.err
-      rc=$?; echo "bench sim replicated $P rc=$rc"; python3 -c "import json;d=json.load(open('$OUT/bench_simrep$P.json'));print(round(d['ms_per_step'],3), d['value'], d['undirected_edges'], d['parity'].get('digest_ok'), [round(x,3) for x in d.get('sim_rank_ms')], {k:round(v,3) for k,v in d['device_ms'].items()})"; [ $rc -ne 0 ] && break
+      timeout -k 10 600 python -u bench.py --config ${SIMREP_CONFIG:-c3} --sim-world $P --multi replicated --steps 3 --no-cpu-baseline --no-ingest $SIMOPTS > $OUT/bench_simrep${P}_${SIMREP_CONFIG:-c3}.json 2> $OUT/bench_simrep$P.err
+      rc=$?; echo "bench sim replicated $P rc=$rc"; python3 -c "import json;d=json.load(open('$OUT/bench_simrep${P}_${SIMREP_CONFIG:-c3}.json'));print(round(d['ms_per_step'],3), d['value'], d['undirected_edges'], d['parity'].get('digest_ok'), [round(x,3) for x in d.get('sim_rank_ms')], {k:round(v,3) for k,v in d['device_ms'].items()})"; [ $rc -ne 0 ] && break
     done ;;
   xchg1)
     timeout -k 10 300 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29511 bench.py --exchange --steps 5 --no-cpu-baseline --no-ingest > $OUT/bench_xchg1.json 2> $OUT/bench_xchg1.err
@@ -100,6 +100,17 @@ for s in $STEPS; do
       timeout -k 10 400 python -u bench.py --config ${SWEEP_CONFIG:-c5} --steps 3 --no-cpu-baseline --no-ingest --no-one-shot --no-d2h $o > $OUT/optsweep.json 2> $OUT/optsweep.err
       rc=$?; [ $rc -ne 0 ] && break
       python3 -c "import json;d=json.load(open('$OUT/optsweep.json'));print('${SWEEP_CONFIG:-c5}','[$V]','ms/step',round(d['ms_per_step'],3),'digest_ok',d['parity'].get('digest_ok'),{k:round(v,3) for k,v in d['device_ms'].items() if v},{k:v for k,v in d['counters'].items() if v})" | tee -a $OUT/optsweep.log
+    done ;;
+  libab)
+    # variant libraries (metagenomics_amd/lib/variants/NAME.so, LIBS="a b") against the default
+    # build, alternating processes, config LIBAB_CONFIG (c5)
+    for rep in 1 2; do
+      for L in default $LIBS; do
+        if [ "$L" = default ]; then lib=""; else lib=$PWD/metagenomics_amd/lib/variants/$L.so; fi
+        MG_LIB=$lib timeout -k 10 400 python -u bench.py --config ${LIBAB_CONFIG:-c5} --steps 5 --no-cpu-baseline --no-ingest --no-one-shot --no-d2h > $OUT/libab.json 2> $OUT/libab.err
+        rc=$?; [ $rc -ne 0 ] && break 2
+        python3 -c "import json;d=json.load(open('$OUT/libab.json'));print('${LIBAB_CONFIG:-c5}','$L','ms/step',round(d['ms_per_step'],3),'digest_ok',d['parity'].get('digest_ok'),{k:round(v,3) for k,v in d['device_ms'].items() if v})" | tee -a $OUT/libab.log
+      done
     done ;;
   a2a)
     timeout -k 10 300 python -u tools/a2a_probe.py > $OUT/a2a_probe.log 2>&1

@@ -24,7 +24,7 @@ the rows' behind nothing (what the C++ host's side stream can reach).
 
 usage: xchg_model.py OUT.md FUSED_BENCH.json CONFIG DIR
   DIR holds profsim{P}_{CONFIG}_ranks.md, profsim{P}_{CONFIG}_bench.json and
-  bench_simrep{P}.json (replicated, C3 only) for P in 2 4 8."""
+  bench_simrep{P}_{CONFIG}.json (replicated; bench_simrep{P}.json for c3) for P in 2 4 8."""
 import json
 import os
 import re
@@ -87,7 +87,9 @@ def main():
                                     "bytes_by_kind": per_kind, "allreduce_bytes": ar, "link_gbs": B,
                                     "transfer_ms": xfer, "wall_serial_ms": serial, "wall_overlap_ms": overlap,
                                     "key_build_ms": keybuild})
-        rj = os.path.join(d, f"bench_simrep{P}.json")
+        rj = os.path.join(d, f"bench_simrep{P}_{cfg}.json")
+        if not os.path.exists(rj) and cfg == "c3":
+            rj = os.path.join(d, f"bench_simrep{P}.json")
         if os.path.exists(rj):
             r = json.load(open(rj))
             w = max(r["sim_rank_ms"])
