@@ -187,6 +187,15 @@ struct mg_ctx {
   // the containment probe skips suffix-key hits (containment)
   uint64_t* d_key0 = nullptr;
   size_t key0_cap = 0;
+  // offset-0 containments through the containment probe (option prefix_probe,
+  // default): the fused scan writes each read's window-0 run (its o = 0 key's
+  // minimizer, window range [0, 0]) here, one 16-B record per slot, and the
+  // probe takes them first in fixed regions of d_p0cnt records
+  bool prefix_probe = true;
+  ulonglong2* d_p0runs = nullptr;
+  size_t p0runs_cap = 0;
+  unsigned long long* d_p0cnt = nullptr;
+  size_t p0cnt_cap = 0;
   // exchange mode: the received runs ordered by local bucket (sort_xruns), the
   // input of both probes; xruns_ready until the next mg_xchg_begin
   uint32_t* d_xk[2] = {nullptr, nullptr};

@@ -762,6 +762,9 @@ struct ScanParams {
   // per read: its o = 0 key's hash bits (bucket | fingerprint, 50 bits) | q << 54
   // (k_prefix_contain); nullptr: not written
   uint64_t* key0;
+  // per read: its window-0 run (x = mix64 of the o = 0 key's minimizer, window
+  // range [0, 0]) for the containment probe's offset-0 pass; nullptr: not written
+  ulonglong2* p0runs;
   int skip_o1;                    // INDEX: leave out the o = 1 keys (mg_ctx::index_o1)
   int skip_o3;                    // INDEX (fused): leave out the o = 3 keys (mg_ctx::index_o3)
   int no_insert;                  // diagnostics (phase_limit = 1): the index scan files no keys (timing only)
@@ -1189,6 +1192,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(G > 1 ? 
         const unsigned long long e = make_entry(v, p.nb_log2, (int)(kb[o] & 1023u), o, (uint32_t)a);
 #ifndef MG_DIAG_NO_KEY0  // (diagnostics build: no o = 0 key records)
         if (o == 0 && p.key0) p.key0[a] = (v & ((1ULL << 50) - 1)) | ((uint64_t)(kb[0] & 1023u) << 54);
+        if constexpr (G > 1 || kWinGroups == 1) {  // (mixed lengths only: the length-ranked windows)
+          if (o == 0 && p.p0runs) p.p0runs[a] = make_ulonglong2(v, run_meta(a, (int)(kb[0] & 1023u), 0, 0));
+        }
 #endif
         if constexpr (KEYREC) {  // o-major: each store is one coalesced wavefront line
           p.key_bk[key_seg(o) * p.key_n + a - p.key_lo] = (uint32_t)(v & nbm);
@@ -1206,6 +1212,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(G > 1 ? 
       }
     } else if (INDEX && a < p.a_hi) {  // no keys (n <= l cannot pass setup_index): holes
       if (p.key0) p.key0[a] = kEmpty;
+      if constexpr (G > 1 || kWinGroups == 1) {
+        if (p.p0runs) p.p0runs[a] = make_ulonglong2(0, kFlatHole);
+      }
       if constexpr (KEYREC) {
         for (int o = 0; o < 4; ++o) {
           p.key_bk[key_seg(o) * p.key_n + a - p.key_lo] = 0;
@@ -3070,7 +3079,12 @@ struct LaunchScan {
     const size_t lds = scan_lds(ctx, index);
     sp.cells = ctx->d_cells;
     sp.cell_n = ctx->cell_n;
-    if (index && ctx->key0_ready) sp.key0 = ctx->d_key0;  // mg_build_index allocated it (mixed lengths)
+    if (index && ctx->key0_ready) {  // mg_build_index allocated it (mixed lengths)
+      if (ctx->prefix_probe)
+        sp.p0runs = ctx->d_p0runs;
+      else
+        sp.key0 = ctx->d_key0;
+    }
     sp.skip_o1 = (index && !ctx->index_o1) ? 1 : 0;
     sp.skip_o3 = (index && !ctx->index_o3 && !ctx->xchg) ? 1 : 0;
     sp.no_insert = (index && ctx->phase_limit == 1) ? 1 : 0;
@@ -3219,6 +3233,39 @@ struct LaunchDiscover {
     return LaunchProbe<W>::run(ctx, contain, ctx->d_runs, ctx->d_run_cnt, ctx->run_cap, ctx->nrun_reg, g.grid);
   }
 };
+
+// markContainedReads at offset 0 (s = 0: read2 or its reverse strand a prefix
+// of read1, OverlapGraph.cpp:302-340) through the containment probe: each
+// read's window-0 run (written by the fused scan) finds, in its o = 0 key's
+// cell chain, the o = 0 / 2 entries of shorter reads with the same minimizer
+// offset (j = 0 in [0, 0]), and the probe's containment verify at s = 0 is
+// k_prefix_contain's compare.  Batched like every other run (the cell line of
+// the next batch in flight), where k_prefix_contain walked one chain per
+// thread.  Runs before the main containment probe, so its contain_skip sees
+// these marks; the window-0 runs never reach the discovery probe (the
+// reference scans no window 0).
+template <int W>
+struct LaunchPrefixProbe {
+  static int run(mg_ctx* ctx) {
+    if (!ctx->n) return 0;
+    constexpr uint64_t kR = 512;  // records per fixed region (consecutive slots)
+    const uint64_t nreg = (ctx->n + kR - 1) / kR;
+    if (ensure(&ctx->d_p0cnt, &ctx->p0cnt_cap, nreg)) return -1;
+    hipLaunchKernelGGL(k_fixed_regions, dim3((uint32_t)((nreg + kBlock - 1) / kBlock)), dim3(kBlock), 0, ctx->stream,
+                       ctx->d_p0cnt, ctx->n, kR, nreg);
+    const DiscGeom g = disc_geom<W>(ctx, true, ctx->n);
+    return LaunchProbe<W>::run(ctx, true, ctx->d_p0runs, ctx->d_p0cnt, kR, nreg, g.grid);
+  }
+};
+
+// the offset-0 containments of a fused build (key0_ready): the window-0 runs
+// through the containment probe (option prefix_probe, default), else k_prefix_contain
+int prefix_contain_pass(mg_ctx* ctx) {
+  if (!ctx->key0_ready) return 0;
+  if (ctx->prefix_probe ? dispatch_w<LaunchPrefixProbe>(ctx->maxw, ctx) : dispatch_w<LaunchPrefixContain>(ctx->maxw, ctx))
+    return set_err(ctx, "prefix containment launch failed");
+  return 0;
+}
 
 // getListOfReads reads all four keys: the lookup table when the index left out o = 1
 IndexParams lookup_params(mg_ctx* ctx) {
@@ -3401,7 +3448,7 @@ void mg_destroy(mg_ctx* ctx) {
                   ctx->d_digest, ctx->id_store[0], ctx->id_store[1], ctx->phys_store[0], ctx->phys_store[1],
                   ctx->d_tmp32, ctx->d_lay_k[0], ctx->d_lay_k[1], ctx->d_lay_v[0], ctx->d_lay_v[1], ctx->d_lay_tmp,
                   ctx->d_words_alt, ctx->d_len_alt, ctx->d_cbits, ctx->d_ccnt, ctx->d_lcells, ctx->d_lkcells,
-                  ctx->d_rhead, ctx->d_rstart, ctx->d_rcnt, ctx->d_dcnt};
+                  ctx->d_rhead, ctx->d_rstart, ctx->d_rcnt, ctx->d_dcnt, ctx->d_p0runs, ctx->d_p0cnt};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   for (auto& e : ctx->ev)
@@ -3607,7 +3654,7 @@ int mg_set_option(mg_ctx* ctx, const char* name, int64_t value) {
       flag("xchg_windows", &ctx->xchg_windows) || flag("chain_par", &ctx->chain_par) ||
       flag("live_runs", &ctx->live_runs))
     return 0;
-  if (flag("prefix_contain", &ctx->prefix_contain)) {
+  if (flag("prefix_contain", &ctx->prefix_contain) || flag("prefix_probe", &ctx->prefix_probe)) {
     ctx->index_ready = false;
     return 0;
   }
@@ -4387,7 +4434,8 @@ int mg_build_index(mg_ctx* ctx, uint32_t min_overlap, uint32_t seed_k) {
     // the discovery probe then walks the live reads' table (always built,
     // build_live_index), so this table holds o = 0 / 2 only
     ctx->index_o3 = !(ctx->key0_ready && ctx->live_index);
-    if (ctx->key0_ready) MG_TRY(ensure(&ctx->d_key0, &ctx->key0_cap, ctx->n + 1));
+    if (ctx->key0_ready && ctx->prefix_probe) MG_TRY(ensure(&ctx->d_p0runs, &ctx->p0runs_cap, ctx->n + 1));
+    if (ctx->key0_ready && !ctx->prefix_probe) MG_TRY(ensure(&ctx->d_key0, &ctx->key0_cap, ctx->n + 1));
     if (ctx->n && dispatch_w<LaunchScanAll>(ctx->maxw, ctx, ctx->stream))
       return set_err(ctx, "index build launch failed");
     if (!ctx->n) ctx->nrun_reg = 0;
@@ -4430,8 +4478,7 @@ int mg_mark_contained(mg_ctx* ctx, uint32_t* super_out) {
     } else {
       if (!shared_scan(ctx)) ctx->key0_ready = false;  // only the shared scan writes the o = 0 keys
       // prefix containments first: what they mark is skipped as a container
-      if (ctx->key0_ready && dispatch_w<LaunchPrefixContain>(ctx->maxw, ctx))
-        return set_err(ctx, "prefix containment launch failed");
+      if (prefix_contain_pass(ctx)) return -1;
       if (shared_scan(ctx) ? probe_shared(ctx, true) : run_discover(ctx, true)) return -1;
     }
     if (ctx->n)
@@ -4743,8 +4790,7 @@ static int xchg_fused_probe(mg_ctx* ctx, bool contain) {
     if (!ctx->n) return 0;
     // prefix containments first: what they mark is skipped as a container
     // (one rank: mg_xchg_prefix_marks ran them already, its marks are its own)
-    if (!ctx->xmarks_done && ctx->key0_ready && dispatch_w<LaunchPrefixContain>(ctx->maxw, ctx))
-      return set_err(ctx, "prefix containment launch failed");
+    if (!ctx->xmarks_done && prefix_contain_pass(ctx)) return -1;
     ctx->xmarks_done = false;
     ctx->xmarks = nullptr;
     if (probe_shared(ctx, true)) return -1;
@@ -4854,8 +4900,7 @@ int mg_xchg_prefix_marks(mg_ctx* ctx, void* marks) {
   if (!ctx->superkey) return set_err(ctx, "mg_begin_contained must run first (lengths differ)");
   MG_TRY(hipEventRecord(ctx->ev[2], ctx->stream));
   if (ctx->xchg_fused) {  // one rank on the fused build: its own o = 0 keys
-    if (ctx->key0_ready && ctx->n && dispatch_w<LaunchPrefixContain>(ctx->maxw, ctx))
-      return set_err(ctx, "prefix containment launch failed");
+    if (ctx->n && prefix_contain_pass(ctx)) return -1;
   } else if (ctx->xchg_prefix && ctx->n && dispatch_w<LaunchPrefixContainKeys>(ctx->maxw, ctx)) {
     return set_err(ctx, "prefix containment launch failed");
   }
