@@ -729,6 +729,9 @@ CONTAIN_OPTS = [
     {"probe_share": 0, "probe_compact": 0},
     {"probe_share": 1, "probe_compact": 0},
     {"probe_share": 0, "probe_compact": 1},
+    # offset-0 containments by k_prefix_contain's chain walk instead of the window-0 runs
+    {"prefix_probe": 0},
+    {"prefix_probe": 0, "contain_skip": 0, "contain_prune": 0},
 ]
 
 
@@ -737,7 +740,8 @@ def test_containment_options(name):
     """The containment cuts are pure pruning: runs past
     j = n1 - minlen (contain_jcut), candidates that cannot raise the superkey
     (contain_prune), runs of already-contained sources (contain_skip, also without
-    k_prefix_contain) and source-length passes (contain_passes), and the probe's
+    k_prefix_contain) and source-length passes (contain_passes), the offset-0
+    containments by k_prefix_contain instead of the window-0 runs (prefix_probe = 0), and the probe's
     batch compaction and block-shared regions (probe_compact, probe_share), and the
     discovery probe on the full index instead of the uncontained reads' index
     (live_index = 0): every combination gives the same superReadIDs and rows."""
