@@ -49,7 +49,7 @@ constexpr int kWave = 64;
 constexpr int kBlock = 256;
 constexpr int kWavesPerBlock = kBlock / kWave;
 constexpr int kSegs = 64;                   // diagnostic counter shards
-constexpr uint32_t kFpBits = 19;
+constexpr uint32_t kFpBits = 9;
 
 // ---------------------------------------------------------------- helpers ---
 // Invertible 64-bit mixer: x -> minimizer order and bucket.  Bijective, so
@@ -237,15 +237,26 @@ __device__ __forceinline__ uint64_t next_cell(uint64_t c, uint64_t n, uint32_t f
   const uint64_t x = c + ((n & (n - 1)) ? 1 : 1 + 2 * (uint64_t)(fp & 1023u));
   return x >= n ? x % n : x;
 }
-// the fingerprint an entry was filed with (make_entry: hi32 = fp19 << 12 | q10 << 2 | o2)
-__device__ __forceinline__ uint32_t entry_fp(unsigned long long e) { return (uint32_t)(e >> 44) & ((1u << 19) - 1); }
+// the fingerprint an entry was filed with (make_entry: hi32 = len10 << 21 | fp9 << 12 | q10 << 2 | o2)
+__device__ __forceinline__ uint32_t entry_fp(unsigned long long e) { return (uint32_t)(e >> 44) & kFpMask; }
 
-// Index entry: lo32 = read index, hi32 = fp19 << 12 | q10 << 2 | o2 (the chain
-// bit, bit 63, is set on a full cell's last slot).
-__device__ __forceinline__ unsigned long long make_entry(uint64_t v, uint32_t nb_log2, int q, int o, uint32_t r) {
+// Index entry: lo32 = read index, hi32 = len10 << 21 | fp9 << 12 | q10 << 2 |
+// o2 (the chain bit, bit 63, is set on a full cell's last slot).  len10 = the
+// read's length - 1 (the templated kernels take reads up to 1,024 bp; longer
+// reads, whose kernels read the lengths array, store 1,023): the containment
+// probe's length conditions (read2 shorter, placed inside read1) are then
+// register work instead of one random 2-B load per listed entry (C5: 554 M
+// per step).  The fingerprint has 9 bits: an entry of another minimizer in the
+// same cell passes it 1 time in 512 and then fails the window-range test or
+// the verification, which compares the whole overlap, so results never depend on it.
+__device__ __forceinline__ unsigned long long make_entry(uint64_t v, uint32_t nb_log2, int q, int o, uint32_t r,
+                                                         int n) {
   const uint32_t fp = (uint32_t)(v >> nb_log2) & kFpMask;
-  return ((unsigned long long)((fp << 12) | ((uint32_t)q << 2) | (uint32_t)o) << 32) | r;
+  const uint32_t ln = (uint32_t)(n < 1 ? 0 : n > 1024 ? 1023 : n - 1);
+  return ((unsigned long long)((ln << 21) | (fp << 12) | ((uint32_t)q << 2) | (uint32_t)o) << 32) | r;
 }
+// the length of the read an entry belongs to (reads up to 1,024 bp)
+__device__ __forceinline__ int entry_len(uint32_t hi) { return (int)((hi >> 21) & 1023u) + 1; }
 
 // insertIntoTable (HashTable.cpp:163-195) for one entry: one 64-B cell load,
 // then CAS into the slots that looked empty (slots only ever go from empty to
@@ -302,7 +313,7 @@ __global__ __launch_bounds__(kBlock) void k_index_build(IndexParams p) {
     const uint64_t v = key_minimizer<kBlock>(f, n, o, p.h, p.m, p.w, &q);
     const uint64_t b = v & mask;
     if (owned(b, p.nb_log2, p.rank, p.nranks))
-      cell_insert(p.cells, b - p.cell_lo, p.cell_n, make_entry(v, p.nb_log2, q, o, (uint32_t)r));
+      cell_insert(p.cells, b - p.cell_lo, p.cell_n, make_entry(v, p.nb_log2, q, o, (uint32_t)r, n));
   }
 }
 
@@ -351,7 +362,7 @@ __global__ __launch_bounds__(kBlock) void k_index_live(IndexParams p) {
       f[MAXW * kBlock] = 0;
       int q;
       const uint64_t v = key_minimizer<kBlock>(f, p.len[r], o, p.h, p.m, p.w, &q);
-      cell_insert(p.cells, v & mask, p.cell_n, make_entry(v, p.nb_log2, q, o, (uint32_t)r));
+      cell_insert(p.cells, v & mask, p.cell_n, make_entry(v, p.nb_log2, q, o, (uint32_t)r, p.len[r]));
     }
   }
 }
@@ -1189,7 +1200,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(G > 1 ? 
 #pragma unroll
       for (int o = 0; o < 4; ++o) {
         const uint64_t v = mix64(mb[o]);
-        const unsigned long long e = make_entry(v, p.nb_log2, (int)(kb[o] & 1023u), o, (uint32_t)a);
+        const unsigned long long e = make_entry(v, p.nb_log2, (int)(kb[o] & 1023u), o, (uint32_t)a, n);
 #ifndef MG_DIAG_NO_KEY0  // (diagnostics build: no o = 0 key records)
         if (o == 0 && p.key0) p.key0[a] = (v & ((1ULL << 50) - 1)) | ((uint64_t)(kb[0] & 1023u) << 54);
         if constexpr (G > 1 || kWinGroups == 1) {  // (mixed lengths only: the length-ranked windows)
@@ -1432,8 +1443,8 @@ __global__ __launch_bounds__(kBlock) void k_scan_reg(ScanParams p) {
           const uint64_t v1 = mix64(ext_reg<MAXW>(rw, p1) >> msh);
           b0 = (uint32_t)(v0 & nbm);
           b1 = (uint32_t)(v1 & nbm);
-          c0 = make_entry(v0, p.nb_log2, p0, 0, (uint32_t)a);
-          c1 = p.skip_o1 ? kEmpty : make_entry(v1, p.nb_log2, p1 - (n - h), 1, (uint32_t)a);
+          c0 = make_entry(v0, p.nb_log2, p0, 0, (uint32_t)a, n);
+          c1 = p.skip_o1 ? kEmpty : make_entry(v1, p.nb_log2, p1 - (n - h), 1, (uint32_t)a, n);
         }
         const uint64_t ka = a - p.key_lo;
         p.key_bk[ka] = b0;
@@ -1499,9 +1510,9 @@ __global__ __launch_bounds__(kBlock) void k_rc_keys(ScanParams p) {
   const uint64_t nbm = (1ULL << p.nb_log2) - 1;  // (bucket, entry) records, o-major
   const uint64_t ka = a - p.key_lo;
   p.key_bk[p.key_n + ka] = n ? (uint32_t)(v2 & nbm) : 0u;  // (key_seg(2) = 1, key_seg(3) = 2)
-  p.key_ent[p.key_n + ka] = n ? make_entry(v2, p.nb_log2, (int)(kb2 & 1023u), 2, (uint32_t)a) : kEmpty;
+  p.key_ent[p.key_n + ka] = n ? make_entry(v2, p.nb_log2, (int)(kb2 & 1023u), 2, (uint32_t)a, n) : kEmpty;
   p.key_bk[2 * p.key_n + ka] = n ? (uint32_t)(v3 & nbm) : 0u;
-  p.key_ent[2 * p.key_n + ka] = n ? make_entry(v3, p.nb_log2, (int)(kb3 & 1023u), 3, (uint32_t)a) : kEmpty;
+  p.key_ent[2 * p.key_n + ka] = n ? make_entry(v3, p.nb_log2, (int)(kb3 & 1023u), 3, (uint32_t)a, n) : kEmpty;
 }
 
 // checkOverlap's string compare (OverlapGraph.cpp:354-383) on packed words:
@@ -1937,12 +1948,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MG_PROBE
     const int rp = (int)((meta >> 32) & 1023u);
     const int rjlo = (int)((meta >> 42) & 1023u), rjhi = (int)((meta >> 52) & 1023u);
     const uint32_t fp = (uint32_t)(key >> 32);
+#ifndef MG_DIAG_STAT_FPJ
     if (p.stats) {
       uint32_t ne = 0;
 #pragma unroll
       for (int s = 0; s < kCell; ++s) ne += e[s] != kEmpty ? 1u : 0u;
       stat(1, ne);
     }
+#endif
     if (p.phase_limit <= 5) return;
     // a full cell's chain flag: probe the next cell in a later batch
     const bool chain = valid && e[kCell - 1] != kEmpty && (e[kCell - 1] & kChain);
@@ -1974,25 +1987,22 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MG_PROBE
       keep = keep && !(CONTAIN && p.contain_even && (oo & 1));
       keepm |= (keep ? 1u : 0u) << s;
     }
+#ifdef MG_DIAG_STAT_FPJ  // (diagnostics build: counter 1 = entries past the fingerprint / window / o filter)
+    stat(1, (uint32_t)__popc(keepm));
+#endif
     if (CONTAIN && valid) {
       // the verify's length conditions (checkOverlapForContainedRead, :302-340:
       // read2 strictly shorter, at offset s = j <= n1 - n2, or s = 0 for a
       // suffix-key hit) at listing time, so a candidate that cannot be
       // contained takes no candidate slot and no verification round
+      // (read2's length from its entry, make_entry: no load per listed entry)
       const int n1 = p.uniform_len ? p.uniform_len : (int)p.len[ra];
 #pragma unroll
-      for (int s0 = 0; s0 < kCell; s0 += kCell / 2) {
-        uint32_t n2v[kCell / 2];
-#pragma unroll
-        for (int s = 0; s < kCell / 2; ++s)
-          n2v[s] = ((keepm >> (s0 + s)) & 1u) ? (uint32_t)p.len[(uint32_t)e[s0 + s]] : 0u;
-#pragma unroll
-        for (int s = 0; s < kCell / 2; ++s) {
-          const uint32_t hi = (uint32_t)(e[s0 + s] >> 32);
-          const int j = rp - (int)((hi >> 2) & 1023u), n2 = (int)n2v[s];
-          const bool ok = n1 > n2 && ((hi & 1u) ? j == n2 - h : j <= n1 - n2);
-          if (!ok) keepm &= ~(1u << (s0 + s));
-        }
+      for (int s = 0; s < kCell; ++s) {
+        const uint32_t hi = (uint32_t)(e[s] >> 32);
+        const int j = rp - (int)((hi >> 2) & 1023u), n2 = entry_len(hi);
+        const bool ok = n1 > n2 && ((hi & 1u) ? j == n2 - h : j <= n1 - n2);
+        if (!ok) keepm &= ~(1u << s);
       }
     }
     if (!CONTAIN && p.cbits) {
@@ -2507,7 +2517,7 @@ __global__ __launch_bounds__(kBlock) void k_index_long(IndexParams p) {
     const uint64_t v = key_minimizer<1>(p.words + r * p.stride, p.len[r], o, p.h, p.m, p.w, &q);
     const uint64_t b = v & mask;
     if (owned(b, p.nb_log2, p.rank, p.nranks))
-      cell_insert(p.cells, b - p.cell_lo, p.cell_n, make_entry(v, p.nb_log2, q, o, (uint32_t)r));
+      cell_insert(p.cells, b - p.cell_lo, p.cell_n, make_entry(v, p.nb_log2, q, o, (uint32_t)r, p.len[r]));
   }
 }
 
@@ -2899,7 +2909,7 @@ __global__ __launch_bounds__(kBlock) void k_index_keys(IndexParams p) {
       const uint64_t v = mix64(mb[o]);
       const uint64_t b = v & nbm;
       if (owned(b, p.nb_log2, p.rank, p.nranks))
-        cell_insert(p.cells, b - p.cell_lo, p.cell_n, make_entry(v, p.nb_log2, (int)(kb[o] & 1023u), o, (uint32_t)a));
+        cell_insert(p.cells, b - p.cell_lo, p.cell_n, make_entry(v, p.nb_log2, (int)(kb[o] & 1023u), o, (uint32_t)a, n));
     }
   }
 }
@@ -3257,6 +3267,57 @@ struct LaunchPrefixProbe {
     return LaunchProbe<W>::run(ctx, true, ctx->d_p0runs, ctx->d_p0cnt, kR, nreg, g.grid);
   }
 };
+
+// Exchange mode: the window-0 runs of the o = 0 key records this rank received
+// (dense, sorted by local home cell, mg_xchg_insert_keys): x = bucket |
+// fingerprint << nb_log2 (what the probe reads of a run's hash), meta = the
+// record's read with window range [0, 0] at its key offset q; the other
+// records become holes, so the array keeps the cell order
+__global__ __launch_bounds__(kBlock) void k_p0_from_keys(const uint32_t* __restrict__ key,
+                                                        const uint64_t* __restrict__ ent, uint64_t n, uint32_t cshift,
+                                                        uint64_t cell_lo, uint32_t nb_log2,
+                                                        ulonglong2* __restrict__ out) {
+  for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBlock) {
+    const uint64_t e = ent[i];
+    const uint32_t hi = (uint32_t)(e >> 32);
+    ulonglong2 r = make_ulonglong2(0, kFlatHole);
+    if (e != kEmpty && !(hi & 3u))
+      r = make_ulonglong2((cell_lo + (key[i] >> cshift)) | ((uint64_t)((hi >> 12) & kFpMask) << nb_log2),
+                          run_meta((uint32_t)e, (int)((hi >> 2) & 1023u), 0, 0));
+    out[i] = r;
+  }
+}
+
+template <int W>
+struct LaunchPrefixProbeKeys {
+  static int run(mg_ctx* ctx) {
+    const uint64_t n = ctx->xkeys_n;
+    if (!n) return 0;
+    if (ensure(&ctx->d_p0runs, &ctx->p0runs_cap, n)) return -1;
+    const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((n + kBlock - 1) / kBlock,
+                                                                           (uint64_t)ctx->n_cu * 16));
+    hipLaunchKernelGGL(k_p0_from_keys, dim3(grid), dim3(kBlock), 0, ctx->stream, ctx->xkey_k, ctx->xkey_e, n,
+                       ctx->xkey_cls + ctx->xkey_fs, ctx->cell_lo, ctx->nb_log2, ctx->d_p0runs);
+    constexpr uint64_t kR = 512;
+    const uint64_t nreg = (n + kR - 1) / kR;
+    if (ensure(&ctx->d_p0cnt, &ctx->p0cnt_cap, nreg)) return -1;
+    hipLaunchKernelGGL(k_fixed_regions, dim3((uint32_t)((nreg + kBlock - 1) / kBlock)), dim3(kBlock), 0, ctx->stream,
+                       ctx->d_p0cnt, n, kR, nreg);
+    const DiscGeom g = disc_geom<W>(ctx, true, std::max<uint64_t>(1, n / 3));
+    return LaunchProbe<W>::run(ctx, true, ctx->d_p0runs, ctx->d_p0cnt, kR, nreg, g.grid);
+  }
+};
+
+// the exchange mode's offset-0 containments from the received o = 0 key records:
+// their window-0 runs through the containment probe (option prefix_probe), else
+// k_prefix_contain_keys' chain walk per record
+int prefix_contain_keys_pass(mg_ctx* ctx) {
+  if (!ctx->xchg_prefix || !ctx->n) return 0;
+  if (ctx->prefix_probe ? dispatch_w<LaunchPrefixProbeKeys>(ctx->maxw, ctx)
+                        : dispatch_w<LaunchPrefixContainKeys>(ctx->maxw, ctx))
+    return set_err(ctx, "prefix containment launch failed");
+  return 0;
+}
 
 // the offset-0 containments of a fused build (key0_ready): the window-0 runs
 // through the containment probe (option prefix_probe, default), else k_prefix_contain
@@ -4842,8 +4903,8 @@ int mg_xchg_probe(mg_ctx* ctx, int contain, const void* recv, uint64_t slot, uin
         hipLaunchKernelGGL(k_fold_marks, dim3(grid), dim3(kBlock), 0, ctx->stream, ctx->superkey, ctx->n, ctx->xmarks);
         MG_TRY(hipGetLastError());
       }
-    } else if (ctx->xchg_prefix && ctx->n && dispatch_w<LaunchPrefixContainKeys>(ctx->maxw, ctx)) {
-      return set_err(ctx, "prefix containment launch failed");
+    } else if (prefix_contain_keys_pass(ctx)) {
+      return -1;
     }
     ctx->xmarks_done = false;
     ctx->xmarks = nullptr;
@@ -4901,8 +4962,8 @@ int mg_xchg_prefix_marks(mg_ctx* ctx, void* marks) {
   MG_TRY(hipEventRecord(ctx->ev[2], ctx->stream));
   if (ctx->xchg_fused) {  // one rank on the fused build: its own o = 0 keys
     if (ctx->n && prefix_contain_pass(ctx)) return -1;
-  } else if (ctx->xchg_prefix && ctx->n && dispatch_w<LaunchPrefixContainKeys>(ctx->maxw, ctx)) {
-    return set_err(ctx, "prefix containment launch failed");
+  } else if (prefix_contain_keys_pass(ctx)) {
+    return -1;
   }
   ctx->xmarks = reinterpret_cast<uint8_t*>(marks);
   if (marks && ctx->n) {
