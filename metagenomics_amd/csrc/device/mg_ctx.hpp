@@ -97,6 +97,10 @@ struct mg_ctx {
   // those alone, sized for them (C5: a quarter of the entries and chains)
   bool live_index = true;
   bool live_runs = true;          // option live_runs: k_live_runs compacts the runs of contained sources before discovery
+  // option live_overlap: k_live_runs (HBM streaming) on a side stream beside the
+  // live index build (memory-side atomics), both before the discovery probe
+  bool live_overlap = true;
+  hipStream_t side = nullptr;
   bool live_ready = false;
   uint64_t* d_lcells = nullptr;
   size_t lcells_cap = 0;

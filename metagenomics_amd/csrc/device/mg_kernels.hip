@@ -3181,7 +3181,9 @@ struct LaunchProbe {
       pp.cell_n = 1ull << ctx->lnb_log2;
       pp.cells = ctx->d_lcells;
     }
-    pp.cbits = (!contain && ctx->contained_done && ctx->super_any) ? ctx->d_cbits : nullptr;
+    // contained partners are dropped at listing (:548), except from the live
+    // index, which holds the uncontained reads' keys only
+    pp.cbits = (!contain && ctx->contained_done && ctx->super_any && !ctx->live_ready) ? ctx->d_cbits : nullptr;
     pp.superkey = ctx->superkey;
     pp.runs = runs;
     pp.run_cnt = run_cnt;
@@ -3514,6 +3516,7 @@ void mg_destroy(mg_ctx* ctx) {
     if (b) (void)hipFree(b);
   for (auto& e : ctx->ev)
     if (e) (void)hipEventDestroy(e);
+  if (ctx->side) (void)hipStreamDestroy(ctx->side);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
 }
@@ -3713,7 +3716,7 @@ int mg_set_option(mg_ctx* ctx, const char* name, int64_t value) {
       flag("probe_compact", &ctx->probe_compact) || flag("live_index", &ctx->live_index) ||
       flag("xchg_sort_runs", &ctx->xchg_sort_runs) || flag("layout_scratch", &ctx->layout_scratch) ||
       flag("xchg_windows", &ctx->xchg_windows) || flag("chain_par", &ctx->chain_par) ||
-      flag("live_runs", &ctx->live_runs))
+      flag("live_runs", &ctx->live_runs) || flag("live_overlap", &ctx->live_overlap))
     return 0;
   if (flag("prefix_contain", &ctx->prefix_contain) || flag("prefix_probe", &ctx->prefix_probe)) {
     ctx->index_ready = false;
@@ -4206,6 +4209,35 @@ int build_live_index_xchg(mg_ctx* ctx) {
   return 0;
 }
 
+// k_live_runs over the run regions: on a side stream (option live_overlap) it
+// overlaps the live index build that the caller launches next on the main
+// stream (the compaction streams HBM, the build waits on memory-side CAS), and
+// live_runs_join() orders the discovery probe after it; else in line
+int live_runs_launch(mg_ctx* ctx, ulonglong2* runs, unsigned long long* cnt, uint64_t cap, uint64_t nreg,
+                     bool* on_side) {
+  *on_side = false;
+  uint32_t grid = (uint32_t)std::min<uint64_t>((nreg + kWavesPerBlock - 1) / kWavesPerBlock, (uint64_t)ctx->n_cu * 8);
+  hipStream_t st = ctx->stream;
+  if (ctx->live_overlap) {
+    if (!ctx->side) MG_TRY(hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking));
+    MG_TRY(hipEventRecord(ctx->ev[10], ctx->stream));
+    MG_TRY(hipStreamWaitEvent(ctx->side, ctx->ev[10], 0));
+    // 8 wavefronts per CU keep 16 MB of loads in flight, enough for HBM, and
+    // leave the CUs' other slots to the live index build
+    grid = std::min<uint32_t>(grid, (uint32_t)ctx->n_cu * 2);
+    st = ctx->side;
+    *on_side = true;
+  }
+  hipLaunchKernelGGL(k_live_runs, dim3(grid), dim3(kBlock), 0, st, runs, cnt, cap, nreg, ctx->d_cbits);
+  MG_TRY(hipGetLastError());
+  if (*on_side) MG_TRY(hipEventRecord(ctx->ev[11], ctx->side));
+  return 0;
+}
+int live_runs_join(mg_ctx* ctx, bool on_side) {
+  if (on_side) MG_TRY(hipStreamWaitEvent(ctx->stream, ctx->ev[11], 0));
+  return 0;
+}
+
 // Discovery as the shared scan's first reader (equal lengths: no containment
 // pass ran) goes out before the scan's run counts are read: the probe reads at
 // most run_cap records of a region, and a region that overflowed is found with
@@ -4216,15 +4248,13 @@ int probe_shared(mg_ctx* ctx, bool contain) {
   for (int attempt = 0; attempt < 4; ++attempt) {
     ctx->nreg = 0;
     MG_TRY(hipEventRecord(ctx->ev[8], ctx->stream));
-    if (!contain && attempt == 0 && ctx->contained_done && build_live_index(ctx)) return -1;
+    bool side = false;
     if (!contain && ctx->contained_done && ctx->super_any && !ctx->runs_live && ctx->nrun_reg && ctx->live_runs) {
-      const uint32_t grid = (uint32_t)std::min<uint64_t>((ctx->nrun_reg + kWavesPerBlock - 1) / kWavesPerBlock,
-                                                         (uint64_t)ctx->n_cu * 8);
-      hipLaunchKernelGGL(k_live_runs, dim3(grid), dim3(kBlock), 0, ctx->stream, ctx->d_runs, ctx->d_run_cnt,
-                         ctx->run_cap, ctx->nrun_reg, ctx->d_cbits);
-      MG_TRY(hipGetLastError());
+      if (live_runs_launch(ctx, ctx->d_runs, ctx->d_run_cnt, ctx->run_cap, ctx->nrun_reg, &side)) return -1;
       ctx->runs_live = true;
     }
+    if (!contain && attempt == 0 && ctx->contained_done && build_live_index(ctx)) return -1;
+    if (live_runs_join(ctx, side)) return -1;
     if (dispatch_w<LaunchProbeShared>(ctx->maxw, ctx, contain)) return set_err(ctx, "probe launch failed");
     MG_TRY(hipEventRecord(ctx->ev[9], ctx->stream));
     if (contain) return 0;
@@ -4917,19 +4947,17 @@ int mg_xchg_probe(mg_ctx* ctx, int contain, const void* recv, uint64_t slot, uin
   for (int attempt = 0;; ++attempt) {
     if (attempt == 3) return set_err(ctx, "row buffers overflow after resize");
     MG_TRY(hipEventRecord(ctx->ev[4], ctx->stream));
-    if (attempt == 0 && ctx->contained_done && (ctx->super_any || !ctx->index_o3) && build_live_index_xchg(ctx))
-      return -1;
+    bool side = false;
     if (attempt == 0 && nregions && ctx->contained_done && ctx->super_any) {
       // runs of contained sources contribute nothing (:548): drop them from the
       // run regions in place (the containment probe has read them already), so
       // the probe batches live runs only
-      const uint32_t grid = (uint32_t)std::min<uint64_t>((nregions + kWavesPerBlock - 1) / kWavesPerBlock,
-                                                         (uint64_t)ctx->n_cu * 8);
-      hipLaunchKernelGGL(k_live_runs, dim3(grid), dim3(kBlock), 0, ctx->stream, runs, ctx->xruns_cnt, reg,
-                         nregions, ctx->d_cbits);
-      MG_TRY(hipGetLastError());
+      if (live_runs_launch(ctx, runs, ctx->xruns_cnt, reg, nregions, &side)) return -1;
       ctx->runs_live = true;
     }
+    if (attempt == 0 && ctx->contained_done && (ctx->super_any || !ctx->index_o3) && build_live_index_xchg(ctx))
+      return -1;
+    if (live_runs_join(ctx, side)) return -1;
     if (nregions && dispatch_w<LaunchProbeSlots>(ctx->maxw, ctx, false, runs, reg, nregions))
       return set_err(ctx, "probe launch failed");
     MG_TRY(hipEventRecord(ctx->ev[5], ctx->stream));
