@@ -1600,7 +1600,7 @@ struct ProbeLds {
   static constexpr size_t o_pk = o_a + (size_t)(MAXW + 1) * kWave * 8;  // [PEND] u64 bucket | fp << 32
   static constexpr size_t o_pm = o_pk + PEND * 8;                       // [PEND] u64 run meta
   static constexpr size_t o_cb = o_pm + PEND * 8;                       // [CAND] u32 partner
-  static constexpr size_t o_ci = o_cb + CAND * 4;                       // [CAND] u32 o << 30 | j
+  static constexpr size_t o_ci = o_cb + CAND * 4;                       // [CAND] u32 o << 30 | (n2 - 1) << 10 | j
   static constexpr size_t o_ca = o_ci + CAND * 4;                       // [CAND] u32 source read
   static constexpr size_t bytes = o_ca + CAND * 4;
 };
@@ -1685,7 +1685,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MG_PROBE
       o = (int)(info >> 30);
       j = (int)(info & 1023u);
       n1 = p.uniform_len ? p.uniform_len : (int)p.len[sa];
-      n2 = p.uniform_len ? p.uniform_len : (int)p.len[bid];
+      n2 = p.uniform_len ? p.uniform_len : (int)((info >> 10) & 1023u) + 1;
       if (!CONTAIN) {
         if (o == 0) {        // F1[j, n1) == F2[0, L)
           L = n1 - j; cond = L < n2; x0 = j; y0 = 0; rcA = false;
@@ -2032,7 +2032,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MG_PROBE
             const uint32_t hi = (uint32_t)(e[s] >> 32);
             const uint32_t at = ncand + lane_prefix(bal);
             s_cb[at] = (uint32_t)e[s];
-            s_ci[at] = ((hi & 3u) << 30) | (uint32_t)(rp - (int)((hi >> 2) & 1023u));
+            // o | partner length - 1 (from its entry) | j: the verify loads no length
+            s_ci[at] = ((hi & 3u) << 30) | (((hi >> 21) & 1023u) << 10) | (uint32_t)(rp - (int)((hi >> 2) & 1023u));
             s_ca[at] = ra;
             keepm &= ~(1u << s);
           }
