@@ -292,7 +292,7 @@ def parity_digest(engines, last, mode, dist, config):
 
 
 # rocprofv3 --pmc summaries (tools/pmc_summary.py) of the default step, newest first
-PMC_FILES = {"c3": ["r05m_pmc_c3.json", "r04v_pmc_c3.json"], "c5": ["r04v_pmc_c5.json", "r03g_pmc_c5.json"]}
+PMC_FILES = {"c3": ["r05t_pmc_c3.json", "r05m_pmc_c3.json"], "c5": ["r05t_pmc_c5.json", "r04v_pmc_c5.json"]}
 
 
 def load_pmc(path):

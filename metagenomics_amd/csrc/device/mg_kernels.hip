@@ -3486,7 +3486,10 @@ int mg_create(mg_ctx** out, int device) {
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
     ctx->n_cu = prop.multiProcessorCount;
-  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
+  // (the side stream of live_runs_launch is made here: its first creation costs milliseconds)
+  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking) != hipSuccess) {
+    if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
     return -1;
   }
