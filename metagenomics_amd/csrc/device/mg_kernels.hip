@@ -177,7 +177,7 @@ struct IndexParams {
   uint32_t nb_log2;
   uint32_t rank, nranks;
   uint64_t cell_lo, cell_n;  // this rank's bucket range [cell_lo, cell_lo + cell_n): local cell = bucket - cell_lo
-  uint64_t* cells;   // [cell_n * kCell] entries: lo32 = read index, hi32 = chain1 | fp19 | q10 | o2
+  uint64_t* cells;   // [cell_n * kCell] entries: lo32 = read index, hi32 = chain1 | len10 | fp9 | q10 | o2 (make_entry)
   const uint32_t* id;  // slot -> reference ID - 1 (nullptr: ID order; lookups return IDs)
   uint32_t stride;     // words per slot (the long-read kernels; the templated ones use slot_words(MAXW))
   const uint32_t* cbits;  // k_index_live: the contained slots (bitmap, k_super_finalize)
@@ -227,7 +227,7 @@ __device__ __forceinline__ uint64_t key_minimizer(const uint64_t* f, int n, int 
 // abundance genome's m-mer in hundreds of keys) filled the neighbouring home
 // cells, and every run of those buckets walked the whole merged cluster (C5:
 // 16 entries scanned per containment run at 3.7 % fingerprint hits).  A step
-// of 1 + 2 (fp mod 1024) keeps other minimizers' chains out of the cluster;
+// of 1 + 2 (fp mod 1024) (512 strides with the 9-bit fingerprint) keeps other minimizers' chains out of the cluster;
 // an odd step visits every cell of a power-of-two table.  A rank's range of a
 // bucket-sharded table (exchange mode) need not be a power of two, and a step
 // sharing a factor with it would cycle through a fraction of the cells, so
