@@ -291,19 +291,58 @@ def parity_digest(engines, last, mode, dist, config):
     return out
 
 
-# rocprofv3 --pmc summaries (tools/pmc_summary.py) of the default step, newest first
-PMC_FILES = {"c3": ["r05t_pmc_c3.json", "r05m_pmc_c3.json"], "c5": ["r05t_pmc_c5.json", "r04v_pmc_c5.json"]}
+# rocprofv3 --pmc summaries (tools/pmc_summary.py) of the default step: profiles/*_pmc_<config>.json
 
 
-def load_pmc(path):
+def find_pmc(explicit, config, lib_sha):
+    """(traffic bytes, source note) from the newest committed PMC summary of this
+    config that was captured on the library this run loaded (or the explicit
+    --pmc file); none matching -> (None, why)."""
+    import glob
+
+    if explicit:
+        return load_pmc(explicit, lib_sha)
+    cands = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_pmc_{config}.json")), key=os.path.getmtime,
+                   reverse=True)
+    first_note = None
+    for p in cands:
+        t, note = load_pmc(p, lib_sha)
+        if t is not None:
+            return t, note
+        first_note = first_note or note
+    return None, first_note or "no PMC summary for this config"
+
+
+def library_sha16():
+    """sha256 (16 hex digits) of the native library this process loaded."""
+    import hashlib
+
+    from metagenomics_amd import overlap
+
+    try:
+        with open(overlap.LIB_PATH, "rb") as f:
+            return hashlib.sha256(f.read()).hexdigest()[:16]
+    except OSError:
+        return None
+
+
+def load_pmc(path, lib_sha=None):
     """HBM traffic of one step from a committed rocprofv3 --pmc summary
     (tools/pmc_summary.py): (2 x FETCH_SIZE + WRITE_SIZE) summed over the step's
-    kernels, per launch (MI355X_MICROARCH.md §HBM gfx950 correction)."""
+    kernels, per launch (MI355X_MICROARCH.md §HBM gfx950 correction).
+    Returns (bytes or None, note): a summary captured on another build of the
+    library (its recorded sha256 differs from lib_sha), or one without that
+    record, gives no traffic -- counters of other kernels are not this run's."""
     try:
         with open(path) as f:
             d = json.load(f)
     except Exception:
-        return None
+        return None, f"unreadable PMC summary {path}"
+    prov = (d.get("library") or {}).get("sha256_16")
+    if prov is None:
+        return None, f"{os.path.basename(path)} records no library build: not quoted"
+    if lib_sha is not None and prov != lib_sha:
+        return None, f"{os.path.basename(path)} was captured on library {prov}, this run loaded {lib_sha}: not quoted"
     tr = d.get("traffic", {})
     step = ("k_index_build", "k_index_live", "k_scan", "k_probe", "k_prefix_contain", "k_live_runs",
             "k_super_finalize")
@@ -317,7 +356,7 @@ def load_pmc(path):
                   if k.startswith(step)) / passes
     else:
         tot = sum(v["traffic_bytes_per_launch"] for k, v in tr.items() if k.startswith(step))
-    return tot or None
+    return (tot or None), f"{os.path.basename(path)} (library {prov})"
 
 
 def main():
@@ -336,6 +375,9 @@ def main():
                          "probes its source-read range, no data-path collective (SURVEY 8(e)(ii)); exchange "
                          "(north_star, BASELINE configs[3]) = bucket-range index shards + RCCL all-to-all of keys, "
                          "runs and rows (SURVEY 8(e) main design).  DESIGN.md 6c: per-rank tables + xGMI model")
+    ap.add_argument("--route-rows", action="store_true",
+                    help="exchange mode: route every row to the owner of its src after discovery (graph[u] by "
+                         "source range; one more all-to-all); default: each rank keeps the rows it verified")
     ap.add_argument("--cpu-sample", type=int, default=200_000)
     ap.add_argument("--no-cpu-full", action="store_true", help="skip the reference's full-build timing")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -343,7 +385,8 @@ def main():
     ap.add_argument("--replay", action="store_true",
                     help="also time the host replay of the exploration + transitive reduction + contraction on the rows")
     ap.add_argument("--pmc", default=None,
-                    help="committed rocprofv3 --pmc summary for roofline.traffic (default: profiles/PMC_FILES[config])")
+                    help="committed rocprofv3 --pmc summary for roofline.traffic (default: the newest profiles/*_pmc_<config>.json "
+                         "captured on this build of the library)")
     ap.add_argument("--nb-log2", type=int, default=0)
     ap.add_argument("--no-d2h", action="store_true", help="skip the rows' D2H timing (mg_copy_rows)")
     ap.add_argument("--no-one-shot", action="store_true",
@@ -453,7 +496,7 @@ def main():
                 torch.cuda.synchronize(local)
                 rank_ms[i] += (time.perf_counter() - ta) * 1e3
             return tot
-        res = sharded_step(engines, xchg, l, k, plan=plan[0])
+        res = sharded_step(engines, xchg, l, k, plan=plan[0], route_rows=args.route_rows)
         plan[0] = plan[0] or res.plan
         last_res[0] = res
         for kk, v in res.ms.items():
@@ -544,13 +587,12 @@ def main():
     kern_ms = dev_ms["total_ms"] if dev_ms.get("total_ms") else (
         dev_ms["index_ms"] + dev_ms["contained_ms"] + dev_ms["overlap_ms"])
     roof = None
+    lib_sha = library_sha16()
     if mode == "fused":
         achieved = alg / (kern_ms / 1000.0) / 1e9 if kern_ms > 0 else 0.0
-        pmc = args.pmc or next((os.path.join(ROOT, "profiles", f) for f in PMC_FILES.get(args.config, [])
-                                if os.path.exists(os.path.join(ROOT, "profiles", f))), None)
-        traffic = load_pmc(pmc) if pmc else None
+        traffic, traffic_src = find_pmc(args.pmc, args.config, lib_sha)
         roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                 "kernel": ("step = k_scan<INDEX> (window scan + fused index build), "
                            + ("bucket sort of the runs (rocprim onesweep), " if dev_ms.get("sort_ms") else
                               "runs in read order on the clustered slot layout, ")
@@ -570,7 +612,8 @@ def main():
     par = {"fused": "1 GPU, fused path",
            "replicated": f"{P} ranks: whole index on every rank, source-read range shards, no data-path collective",
            "replicated-sim": f"{P} simulated ranks on 1 GPU (whole index each, source-read shards; step = slowest rank)",
-           "exchange": f"{P} ranks: bucket-range index + source-range shards, RCCL all-to-all",
+           "exchange": f"{P} ranks: bucket-range index + source-range shards, RCCL all-to-all of 8-B key and "
+                       f"run records" + (" and of the rows" if args.route_rows else ""),
            "exchange-sim": f"{P} simulated ranks on 1 GPU (device-local exchange)"}[mode]
     res = {
         "metric": "overlap edges/sec",
@@ -599,11 +642,15 @@ def main():
         "layout_first_upload_ms": layout_ms,
         "phase_wall_ms": {kk: v / args.steps for kk, v in phase_ms.items()} or None,
         "exchange_reruns": reruns[0] if mode.startswith("exchange") else None,
+        "exchange_rows": (("routed to their src owners" if args.route_rows and P > 1 else
+                           "held by the rank that verified them (union = the multiset)")
+                          if mode.startswith("exchange") else None),
         # slot-layout padding: records moved between ranks vs records sent (rank 0's, or all
         # simulated ranks'), from the last step's counts
         "exchange_padding": (last_res[0].padding(P, [rank] if mode == "exchange" else list(range(P)))
                              if mode.startswith("exchange") and last_res[0] is not None and P > 1 else None),
         "counters": cnt,
+        "library_sha16": lib_sha,
         "roofline": roof,
         "parity": parity,
     }

@@ -202,9 +202,13 @@ int mg_set_shard(mg_ctx* ctx, uint32_t rank, uint32_t nranks, uint64_t read_lo, 
  *                    mg_xchg_probe(1) -> all-reduce MAX of superkey]
  *   mg_finalize_contained                                       (markContainedReads)
  *   mg_xchg_probe(0) -> mg_xchg_pack(MG_ROWS) -> a2a             (insertAllEdgesOfRead)
- * and every rank ends with the rows whose src it owns.  Record sizes:
- * mg_record_bytes(): keys 16 B (bucket, index entry), runs 16 B (bucket |
- * fingerprint << nb, run meta), rows 12 B (mg_edge). */
+ * and every rank ends with the rows whose src it owns (or, when the host skips
+ * the last pack, with the rows it verified: the union over the ranks is the
+ * same multiset).  Record sizes, mg_record_bytes(): keys 8 B (the index entry:
+ * read slot | o | q | fingerprint | length), runs 8 B (the run meta: read slot
+ * | minimizer position p | window range); the receiver recomputes the bucket
+ * and fingerprint by hashing the minimizer m-mer of its own copy of the read
+ * (every rank holds all reads), so they never travel; rows 12 B (mg_edge). */
 enum { MG_KEYS = 0, MG_RUNS = 1, MG_ROWS = 2 };
 uint32_t mg_record_bytes(int what);
 /* First per-peer stream capacities (records) for keys, runs and rows:
@@ -304,6 +308,9 @@ int mg_get_counters(const mg_ctx* ctx, mg_counters* c);
  *                   of a mixed-length set holds the o = 0 / 2 keys only;
  *  "xchg_sort_runs" exchange mode: order the received runs by bucket before
  *                   the probes (default 0: probed in place, arrival order);
+ *  "xchg_route_rows" exchange mode: the discovery probe counts its rows per src
+ *                   owner for mg_xchg_pack(MG_ROWS) (default 1); 0 when the
+ *                   host keeps the rows where they were verified;
  *  "xchg_windows"   exchange mode, mixed lengths: the scan takes length-ranked
  *                   windows of 256 reads (default 1);
  *  "layout_scratch" 0 = free the layout's double buffers after each layout
@@ -315,6 +322,9 @@ int mg_get_counters(const mg_ctx* ctx, mg_counters* c);
  *                   from its home and fail the call if one is not found;
  *  "xchg_fs"        diagnostics: fingerprint bits in the exchange sort key
  *                   (-1 = auto: what fills the sort's last 8-bit digit);
+ *  "alloc_cap"      tests: a device allocation above this many bytes fails as
+ *                   out of memory (0 = no cap); every failed allocation leaves
+ *                   the buffer's name, its size and the HIP error in mg_last_error;
  *  "run_cap"        tests: initial run records per scan region (0 = sized from
  *                   the reads; overflowing regions are resized and rescanned);
  *  "phase_limit", "max_blocks"

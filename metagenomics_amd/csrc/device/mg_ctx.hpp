@@ -170,6 +170,13 @@ struct mg_ctx {
   unsigned long long* d_dcnt = nullptr;
   size_t dcnt_cap = 0;
   bool rows_counted = false;
+  // option "xchg_route_rows" (default 1): the exchange-mode discovery probe
+  // counts its rows per src owner for mg_xchg_pack(MG_ROWS); a host that keeps
+  // the rows where they were verified sets 0 and the probe counts nothing
+  bool xchg_route_rows = true;
+  // option "xchg_scan_lds": the exchange scan of equal lengths takes k_scan<KEYREC>
+  // (LDS sliding minimum, all four keys in one pass) instead of k_scan_reg + k_rc_keys
+  bool xchg_scan_lds = false;
   int packable = 0;                      // 1 << MG_KEYS | 1 << MG_RUNS | 1 << MG_ROWS
   unsigned long long* d_flat_cnt = nullptr;  // per-region counts of the received runs (probe input)
   size_t flat_cnt_cap = 0;
@@ -209,6 +216,9 @@ struct mg_ctx {
   size_t xsort_tmp_cap = 0;
   int xv_sel = 0;
   uint64_t xruns_n = 0;
+  // the received runs expanded to 16-B probe records (k_xruns_expand), slot layout
+  ulonglong2* d_xexp = nullptr;
+  size_t xexp_cap = 0;
   bool xruns_ready = false;
   ulonglong2* xruns_base = nullptr;  // the probes' run regions: d_xv (sorted), the receive buffer, or (one rank) d_runs
   unsigned long long* xruns_cnt = nullptr;  // their per-region counts
@@ -261,6 +271,9 @@ struct mg_ctx {
   uint32_t* d_freq = nullptr;
   size_t freq_cap = 0;
   uint64_t n_good = 0;  // reads that passed testRead (Dataset::getNumberOfReads)
+  // option "alloc_cap" (tests): a device allocation above this many bytes fails
+  // as out of memory (0 = no cap), so the error path is exercised on purpose
+  uint64_t alloc_cap = 0;
 };
 
 #define MG_TRY(expr)                                                                  \
@@ -277,18 +290,46 @@ inline int set_err(mg_ctx* ctx, const std::string& s) {
   return -1;
 }
 
+// Every device buffer of a context is allocated here.  A failure -- or, with
+// option "alloc_cap" (tests), a request above that many bytes, reported as
+// out of memory -- leaves the buffer's name, the bytes asked for and the HIP
+// error in ctx->err, so no later message has to guess the cause.
+inline hipError_t ctx_malloc(mg_ctx* ctx, void** p, size_t bytes, const char* what) {
+  *p = nullptr;
+  const hipError_t e =
+      (ctx->alloc_cap && bytes > ctx->alloc_cap) ? hipErrorOutOfMemory : hipMalloc(p, std::max<size_t>(bytes, 1));
+  if (e != hipSuccess) {
+    *p = nullptr;
+    ctx->err = std::string("device allocation of ") + what + " (" + std::to_string(bytes) + " B) failed: " +
+               hipGetErrorString(e) + (ctx->alloc_cap && bytes > ctx->alloc_cap ? " (option alloc_cap)" : "");
+  }
+  return e;
+}
+
+// grow *p to at least `count` elements (contents not kept)
 template <typename T>
-inline hipError_t ensure(T** p, size_t* cap, size_t count) {
+inline hipError_t ensure(mg_ctx* ctx, T** p, size_t* cap, size_t count, const char* what) {
   if (*cap >= count && *p) return hipSuccess;
   if (*p) {
     hipError_t e = hipFree(*p);
     if (e != hipSuccess) return e;
     *p = nullptr;
+    *cap = 0;
   }
   const size_t c = std::max<size_t>(count, 1);
-  hipError_t e = hipMalloc(reinterpret_cast<void**>(p), c * sizeof(T));
+  hipError_t e = ctx_malloc(ctx, reinterpret_cast<void**>(p), c * sizeof(T), what);
   if (e == hipSuccess) *cap = c;
   return e;
+}
+// ensure() of a context field; returns -1 from the caller with ctx->err set
+#define MG_ENSURE(field, capf, count)                                                            \
+  do {                                                                                          \
+    if (ensure(ctx, &ctx->field, &ctx->capf, (count), #field) != hipSuccess) return -1;         \
+  } while (0)
+// a launch wrapper that failed: keep the cause a callee left in ctx->err
+inline int launch_fail(mg_ctx* ctx, const std::string& what) {
+  ctx->err = ctx->err.empty() ? what : what + ": " + ctx->err;
+  return -1;
 }
 
 // word counts the kernels are instantiated for (reads up to 1024 bp)

@@ -350,9 +350,9 @@ struct Ingest {
     ctx->maxw = ngood ? maxw : supported_maxw(1);
     ctx->stride = slot_stride(ctx->maxw);
     const size_t nw = (size_t)(nu + 2) * ctx->stride + 2;  // zero pad for over-reads
-    MG_TRY(ensure(&ctx->d_words, &ctx->words_cap, nw));
-    MG_TRY(ensure(&ctx->d_len, &ctx->len_cap, nu + 1));
-    MG_TRY(ensure(&ctx->d_freq, &ctx->freq_cap, nu + 1));
+    MG_ENSURE(d_words, words_cap, nw);
+    MG_ENSURE(d_len, len_cap, nu + 1);
+    MG_ENSURE(d_freq, freq_cap, nu + 1);
     MG_TRY(hipMemsetAsync(ctx->d_words, 0, nw * sizeof(uint64_t), st));
     MG_TRY(first.alloc(nu));
     if (ngood) {

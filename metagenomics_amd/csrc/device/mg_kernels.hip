@@ -100,6 +100,14 @@ __device__ __forceinline__ uint64_t ext_fwd(const uint64_t* f, int pos) {
   return funnel(f[w * S], f[(w + 1) * S], s);
 }
 
+// 32 bases of a read's slot in HBM starting at base pos (no read past the
+// slot's last word)
+template <int MAXW>
+__device__ __forceinline__ uint64_t ext_slot(const uint64_t* g, int pos) {
+  const int wi = pos >> 5;
+  return funnel(g[wi], wi + 1 < slot_words(MAXW) ? g[wi + 1] : 0ull, (pos & 31) << 1);
+}
+
 
 // Reference ID - 1 of the read in slot x of the device layout (mg_ctx::d_id:
 // reads are stored clustered for locality; nullptr = ID order).
@@ -501,22 +509,93 @@ struct LaunchPrefixContain {
 // same CASes behind its scan.  The same two kernels over the uncontained
 // reads' records (compacted in order) with cells coarsened by `shift` build
 // the exchange mode's discovery index (build_live_index_xchg).
-__global__ __launch_bounds__(kBlock) void k_xkeys_dense(const ulonglong2* __restrict__ recv, uint64_t slot,
+// mix64 of the minimizer m-mer of index entry e (read slot r, key o, minimizer
+// offset q): the m-mer hashRead's key o (HashTable.cpp:88-104) has at offset q,
+// re-extracted from the read's slot -- F[q..] (o = 0), F[n-h+q..] (o = 1),
+// rc F[n-m-q..] (o = 2), rc F[w-1-q..] (o = 3), as k_scan / k_rc_keys take
+// them -- so its bucket and fingerprint are the sender's.  The exchange
+// mode's key records travel as the 8-B entry alone, and every rank holds the reads.
+template <int MAXW>
+__device__ __forceinline__ uint64_t entry_hash(const uint64_t* __restrict__ words, const uint16_t* __restrict__ len,
+                                               uint64_t e, int h, int m, int w) {
+  const uint32_t r = (uint32_t)e, hi = (uint32_t)(e >> 32);
+  const int o = (int)(hi & 3u), q = (int)((hi >> 2) & 1023u), n = len[r];
+  const uint64_t* g = words + (uint64_t)r * slot_words(MAXW);
+  const uint64_t mmask = (m == 32) ? ~0ULL : ((1ULL << (2 * m)) - 1);
+  const int pos = o == 0 ? q : o == 1 ? n - h + q : o == 2 ? n - m - q : w - 1 - q;
+  const uint64_t x = ext_slot<MAXW>(g, pos);
+  return mix64(o < 2 ? x >> (64 - 2 * m) : rc_word(x) & mmask);
+}
+
+// the received key records (8-B entries in the slot layout) -> dense (local
+// home cell, entry) pairs for the sort, the home cell recomputed from the read
+template <int MAXW>
+__global__ __launch_bounds__(kBlock) void k_xkeys_dense(const uint64_t* __restrict__ recv, uint64_t slot,
                                                        uint32_t nranks, uint64_t total,
                                                        const unsigned long long* __restrict__ counts,
-                                                       uint64_t cell_lo, uint32_t* __restrict__ key,
+                                                       const uint64_t* __restrict__ words,
+                                                       const uint16_t* __restrict__ len, int h, int m, int w,
+                                                       uint32_t nb_log2, uint64_t cell_lo, uint32_t* __restrict__ key,
                                                        uint64_t* __restrict__ ent) {
   const uint64_t blk = (uint64_t)nranks * slot, lim = total / nranks;  // records per peer stream
+  const uint64_t nbmask = (1ULL << nb_log2) - 1;
   for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < total; i += (uint64_t)gridDim.x * kBlock) {
     const uint64_t t = i / blk, rem = i - t * blk, sp = rem / slot, j = t * slot + (rem - sp * slot);
     if (j >= counts[sp]) continue;
     uint64_t at = j;
     for (uint64_t q = 0; q < sp; ++q) at += counts[q] < lim ? counts[q] : lim;
-    const ulonglong2 x = recv[i];  // x = global bucket, y = entry
-    key[at] = (uint32_t)(x.x - cell_lo);
-    ent[at] = x.y;
+    const uint64_t e = recv[i];
+    key[at] = (uint32_t)((entry_hash<MAXW>(words, len, e, h, m, w) & nbmask) - cell_lo);
+    ent[at] = e;
   }
 }
+
+// the received runs (8-B metas in the slot layout) -> 16-B probe records at
+// the same positions: x = mix64 of the minimizer m-mer at p of the run's read
+// (bucket | fingerprint, what the sender's scan hashed), y = the meta
+template <int MAXW>
+__global__ __launch_bounds__(kBlock) void k_xruns_expand(const uint64_t* __restrict__ recv, uint64_t slot,
+                                                        uint32_t nranks, uint64_t total,
+                                                        const unsigned long long* __restrict__ counts,
+                                                        const uint64_t* __restrict__ words, int m,
+                                                        ulonglong2* __restrict__ out) {
+  const uint64_t blk = (uint64_t)nranks * slot;
+  const int msh = 64 - 2 * m;
+  for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < total; i += (uint64_t)gridDim.x * kBlock) {
+    const uint64_t t = i / blk, rem = i - t * blk, sp = rem / slot, j = t * slot + (rem - sp * slot);
+    if (j >= counts[sp]) continue;  // (the probe's regions stop at the counts)
+    const uint64_t meta = recv[i];
+    uint64_t x = 0;
+    if (meta != kFlatHole) {
+      const uint64_t* g = words + (meta & 0xFFFFFFFFull) * slot_words(MAXW);
+      x = mix64(ext_slot<MAXW>(g, (int)((meta >> 32) & 1023u)) >> msh);
+    }
+    out[i] = make_ulonglong2(x, meta);
+  }
+}
+
+template <int W>
+struct LaunchXkeysDense {
+  static int run(mg_ctx* ctx, const uint64_t* recv, uint64_t slot, uint64_t total, const unsigned long long* counts,
+                 uint32_t* key, uint64_t* ent) {
+    const uint32_t grid = (uint32_t)std::min<uint64_t>((total + kBlock - 1) / kBlock, 65536);
+    hipLaunchKernelGGL(k_xkeys_dense<W>, dim3(grid), dim3(kBlock), 0, ctx->stream, recv, slot, ctx->nranks, total, counts,
+                       ctx->d_words, ctx->d_len, (int)ctx->h, (int)ctx->m, (int)ctx->w, ctx->nb_log2, ctx->cell_lo, key,
+                       ent);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+  }
+};
+
+template <int W>
+struct LaunchXrunsExpand {
+  static int run(mg_ctx* ctx, const uint64_t* recv, uint64_t slot, uint64_t total, const unsigned long long* counts,
+                 ulonglong2* out) {
+    const uint32_t grid = (uint32_t)std::min<uint64_t>((total + kBlock - 1) / kBlock, 65536);
+    hipLaunchKernelGGL(k_xruns_expand<W>, dim3(grid), dim3(kBlock), 0, ctx->stream, recv, slot, ctx->nranks, total,
+                       counts, ctx->d_words, (int)ctx->m, out);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+  }
+};
 
 // number of records equal to key c (>> shift) directly before record i, capped at kCell
 __device__ __forceinline__ int rank_in_cell(const uint32_t* __restrict__ key, uint64_t i, uint32_t shift, uint32_t c) {
@@ -805,12 +884,6 @@ __device__ __forceinline__ uint64_t run_meta(uint64_t a, int p, int jlo, int jhi
 // 32 bases of a lane's read starting at base `pos` (per-lane), from its words
 // in registers (pos >> 5 selected by a compare chain, not a register index,
 // which would go through scratch)
-// the same from the read's slot in HBM (no read past the slot's last word)
-template <int MAXW>
-__device__ __forceinline__ uint64_t ext_slot(const uint64_t* g, int pos) {
-  const int wi = pos >> 5;
-  return funnel(g[wi], wi + 1 < slot_words(MAXW) ? g[wi + 1] : 0ull, (pos & 31) << 1);
-}
 
 template <int MAXW>
 __device__ __forceinline__ uint64_t ext_reg(const uint64_t* rw, int pos) {
@@ -878,6 +951,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(G > 1 ? 
   ulonglong2* const region = p.runs + gw * G * p.run_cap;
   const uint64_t nbmask = (1ULL << p.nb_log2) - 1;
   uint64_t cur[G] = {};  // records per region (wavefront-uniform)
+  // KEYREC with p.dst_cnt: lane j P + d counts the stored runs of region j bound
+  // for rank d (k_part's OWN_BUCKET rule), so routing them needs no count pass
+  uint32_t dcnt = 0;
   uint32_t nbuf = 0;  // run metas staged in s_buf (wavefront-uniform)
 
   // close the run of minimizer position pos over windows [jlo, jhi]: stage its
@@ -1021,9 +1097,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(G > 1 ? 
         v = mix64(funnel(g2[pos >> 5], g2[(pos >> 5) + 1], (pos & 31) << 1) >> msh);
         if (!INDEX) flag = owned(v & nbmask, p.nb_log2, p.rank, p.nranks);
       }
+      uint64_t at_rec = 0;  // the record's index in its region
+      uint32_t grp_rec = 0;
       if constexpr (G == 1) {
         const uint64_t bal = __ballot(flag);
         const uint64_t at = cur[0] + lane_prefix(bal);
+        at_rec = at;
 #if defined(MG_DIAG_STORE_NEVER)
         if (flag && at < p.run_cap && v == 0x0123456789ABCDEFull) region[at] = make_ulonglong2(v, meta);
 #elif !defined(MG_DIAG_NO_RUNSTORE)
@@ -1043,11 +1122,24 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(G > 1 ? 
           if (grp == (uint32_t)j) at = cur[j] + lane_prefix(bal);
           cur[j] += (uint64_t)__popcll(bal);
         }
+        at_rec = at;
+        grp_rec = grp;
 #if defined(MG_DIAG_STORE_NEVER)  // (diagnostics build: runs hashed and placed, but (practically) never stored)
         if (flag && at < p.run_cap && v == 0x0123456789ABCDEFull) region[grp * p.run_cap + at] = make_ulonglong2(v, meta);
 #elif !defined(MG_DIAG_NO_RUNSTORE)  // (diagnostics build: the window scan stores no runs)
         if (flag && at < p.run_cap) region[grp * p.run_cap + at] = make_ulonglong2(v, meta);
 #endif
+      }
+      if constexpr (KEYREC) {
+        if (p.dst_cnt) {
+          const bool st = flag && at_rec < p.run_cap;  // (k_part routes the stored records of a region)
+          const uint32_t d = st ? (uint32_t)(((v & nbmask) * p.dst_ranks) >> p.nb_log2) : 0u;
+          for (uint32_t jj = 0; jj < (uint32_t)G; ++jj)
+            for (uint32_t dd = 0; dd < p.dst_ranks; ++dd) {
+              const uint32_t cc = (uint32_t)__popcll(__ballot(st && grp_rec == jj && d == dd));
+              dcnt += (uint32_t)lane == jj * p.dst_ranks + dd ? cc : 0u;
+            }
+        }
       }
       const uint32_t rest = nbuf - k;  // < 128 left: move them to the front
       const uint64_t m0 = (uint32_t)lane < rest ? s_buf[k + lane] : 0;
@@ -1239,6 +1331,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(G > 1 ? 
 #pragma unroll
   for (int j = 1; j < G; ++j) c = lane == j ? cur[j] : c;
   if (lane < G) p.run_cnt[gw * G + lane] = c;
+  if constexpr (KEYREC) {
+    if (p.dst_cnt && (uint32_t)lane < (uint32_t)G * p.dst_ranks)  // region gw G + j, rank d at [(gw G + j) P + d]
+      p.dst_cnt[(gw * G + lane / p.dst_ranks) * p.dst_ranks + lane % p.dst_ranks] = dcnt;
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -2032,8 +2128,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MG_PROBE
             const uint32_t hi = (uint32_t)(e[s] >> 32);
             const uint32_t at = ncand + lane_prefix(bal);
             s_cb[at] = (uint32_t)e[s];
-            // o | partner length - 1 (from its entry) | j: the verify loads no length
-            s_ci[at] = ((hi & 3u) << 30) | (((hi >> 21) & 1023u) << 10) | (uint32_t)(rp - (int)((hi >> 2) & 1023u));
+            // o | partner length - 1 (from its entry) | j: the verify loads no length.  j lies in
+            // the run's window range [jlo, jhi] (keep above), so 0 <= j < 1024; the templated
+            // probe only runs with reads up to 1,024 bp (LaunchProbe checks maxlen)
+            s_ci[at] = ((hi & 3u) << 30) | (((hi >> 21) & 1023u) << 10) |
+                       ((uint32_t)(rp - (int)((hi >> 2) & 1023u)) & 1023u);
             s_ca[at] = ra;
             keepm &= ~(1u << s);
           }
@@ -2115,10 +2214,16 @@ __global__ __launch_bounds__(kBlock) void k_compact_rows(const uint32_t* __restr
 // a destination is irrelevant (the result is a multiset).
 //   OWN_KEY: the four key records (bucket, entry) of every source read, o-major
 //            (key_ent[o key_n + a]); owner = bucket range (same rule as owned());
+//            what travels is the 8-B entry alone (read slot | o | q | fp |
+//            length): the owner recomputes the bucket from the read, which it
+//            holds (k_xkeys_dense);
 //   OWN_SRC: 12-B rows, owner of src ID = source-read range
 //            [floor(r N / P), floor((r+1) N / P)) -> (src P - 1) / N;
 //   OWN_BUCKET: 16-B run records of the scan's regions (x = bucket |
-//            fingerprint, y = run meta), owner = the bucket's rank.
+//            fingerprint, y = run meta), owner = the bucket's rank; what
+//            travels is the 8-B meta alone (read slot | p | jlo | jhi): the owner
+//            re-hashes the minimizer m-mer at p of its copy of the read
+//            (k_xruns_expand), so a run costs 8 B on xGMI instead of 16.
 enum OwnerKind { OWN_KEY = 0, OWN_SRC = 1, OWN_BUCKET = 2 };
 constexpr int kMaxRanks = 64;
 
@@ -2191,7 +2296,7 @@ __global__ __launch_bounds__(kBlock) void k_part(PartParams p) {
         if (valid && k < lim) {  // a stream cut at its capacity keeps its full count
           const uint64_t q = k / p.slot, o = ((q * p.nranks) + d) * p.slot + (k - q * p.slot);
           void* dst = (p.self_out && d == p.self_rank) ? p.self_out : p.out;
-          if (KIND != OWN_SRC) reinterpret_cast<ulonglong2*>(dst)[o] = x16;
+          if (KIND != OWN_SRC) reinterpret_cast<uint64_t*>(dst)[o] = x16.y;  // entry / run meta (8 B)
           else reinterpret_cast<uint3*>(dst)[o] = x12;
         }
       }
@@ -2971,7 +3076,8 @@ inline uint32_t scan_wpb(uint32_t w) {
 // windows too (option xchg_windows): one read per lane idles the lanes of
 // shorter reads, and longest first scans containers before their contents.
 inline bool scan_is_reg(const mg_ctx* ctx, bool index) {
-  return ctx->w <= (uint32_t)kRegW && (!index || (ctx->xchg && !(ctx->xchg_windows && ctx->minlen != ctx->maxlen)));
+  return ctx->w <= (uint32_t)kRegW &&
+         (!index || (ctx->xchg && !ctx->xchg_scan_lds && !(ctx->xchg_windows && ctx->minlen != ctx->maxlen)));
 }
 // groups per k_scan window (one run region each): the index scan of mixed
 // lengths ranks each window's reads by length (kWinGroups); else 1
@@ -3059,7 +3165,7 @@ struct LaunchScan {
       if (ctx->d_runs) (void)hipFree(ctx->d_runs);
       ctx->d_runs = nullptr;
       ctx->runs_cap = 0;
-      if (hipMalloc(&ctx->d_runs, run_cap * nreg * sizeof(ulonglong2)) != hipSuccess) return -1;
+      if (ctx_malloc(ctx, (void**)&ctx->d_runs, run_cap * nreg * sizeof(ulonglong2), "d_runs (run regions)")) return -1;
       ctx->runs_cap = run_cap * nreg;
     }
     if (!ctx->run_cap_opt) run_cap = ctx->runs_cap / std::max<uint64_t>(1, nreg);
@@ -3068,7 +3174,8 @@ struct LaunchScan {
       if (ctx->d_run_cnt) (void)hipFree(ctx->d_run_cnt);
       ctx->d_run_cnt = nullptr;
       ctx->run_cnt_cap = 0;
-      if (hipMalloc(&ctx->d_run_cnt, std::max<uint64_t>(1, nreg) * sizeof(unsigned long long)) != hipSuccess) return -1;
+      if (ctx_malloc(ctx, (void**)&ctx->d_run_cnt, std::max<uint64_t>(1, nreg) * sizeof(unsigned long long), "d_run_cnt"))
+        return -1;
       ctx->run_cnt_cap = nreg;
     }
     ctx->runs_live = false;
@@ -3100,8 +3207,10 @@ struct LaunchScan {
     sp.skip_o3 = (index && !ctx->index_o3 && !ctx->xchg) ? 1 : 0;
     sp.no_insert = (index && ctx->phase_limit == 1) ? 1 : 0;
     if (index && ctx->xchg) ctx->runs_counted = false;
-    if (index && ctx->xchg && scan_is_reg(ctx, index) && ctx->nranks > 1 && ctx->nranks <= kWave) {
-      if (ensure(&ctx->d_rcnt, &ctx->rcnt_cap, nreg * ctx->nranks)) return -1;
+    // the exchange scan counts its runs per destination rank as it stores them
+    // (the register scan per region, k_scan<KEYREC> per region and group: G P <= 64)
+    if (index && ctx->xchg && ctx->nranks > 1 && G * ctx->nranks <= (uint64_t)kWave) {
+      MG_ENSURE(d_rcnt, rcnt_cap, nreg * ctx->nranks);
       sp.dst_cnt = ctx->d_rcnt;
       sp.dst_ranks = ctx->nranks;
       ctx->runs_counted = true;
@@ -3160,6 +3269,10 @@ struct LaunchProbe {
     // = false) is only exact behind the live index that has them
     if (!contain && !ctx->index_o3 && !ctx->live_ready)
       return set_err(ctx, "discovery probe: the full index leaves out the o = 3 keys and no live index was built");
+    // the candidate word packs j and the partner's length - 1 into 10 bits each
+    // (and entries clamp lengths at 1,024): longer reads take k_probe_long
+    if (ctx->maxlen > 1024)
+      return set_err(ctx, "templated probe: reads longer than 1,024 bp must take the long-read kernels");
     ctx->nreg = (uint64_t)grid * kWavesPerBlock;  // probe wavefronts = row regions
     ProbeParams pp{};
     pp.words = ctx->d_words;
@@ -3211,10 +3324,11 @@ struct LaunchProbe {
     pp.share = (!contain && ctx->probe_share) ? 1 : 0;
     pp.id = ctx->d_id;
     const size_t lds = (size_t)kWavesPerBlock * ProbeLds<W>::bytes;
-    const bool dcnt = !contain && ctx->xchg && ctx->nranks > 1 && ctx->nranks <= (uint32_t)kWave && ctx->n;
+    const bool dcnt = !contain && ctx->xchg && ctx->xchg_route_rows && ctx->nranks > 1 &&
+                      ctx->nranks <= (uint32_t)kWave && ctx->n;
     if (!contain) ctx->rows_counted = false;
     if (dcnt) {  // the rows' routing takes these counts (mg_xchg_pack, MG_ROWS)
-      if (ensure(&ctx->d_dcnt, &ctx->dcnt_cap, ctx->nreg * ctx->nranks)) return -1;
+      MG_ENSURE(d_dcnt, dcnt_cap, ctx->nreg * ctx->nranks);
       pp.dst_cnt = ctx->d_dcnt;
       pp.dst_ranks = ctx->nranks;
       pp.n_ids = ctx->n;
@@ -3263,7 +3377,7 @@ struct LaunchPrefixProbe {
     if (!ctx->n) return 0;
     constexpr uint64_t kR = 512;  // records per fixed region (consecutive slots)
     const uint64_t nreg = (ctx->n + kR - 1) / kR;
-    if (ensure(&ctx->d_p0cnt, &ctx->p0cnt_cap, nreg)) return -1;
+    MG_ENSURE(d_p0cnt, p0cnt_cap, nreg);
     hipLaunchKernelGGL(k_fixed_regions, dim3((uint32_t)((nreg + kBlock - 1) / kBlock)), dim3(kBlock), 0, ctx->stream,
                        ctx->d_p0cnt, ctx->n, kR, nreg);
     const DiscGeom g = disc_geom<W>(ctx, true, ctx->n);
@@ -3296,14 +3410,14 @@ struct LaunchPrefixProbeKeys {
   static int run(mg_ctx* ctx) {
     const uint64_t n = ctx->xkeys_n;
     if (!n) return 0;
-    if (ensure(&ctx->d_p0runs, &ctx->p0runs_cap, n)) return -1;
+    MG_ENSURE(d_p0runs, p0runs_cap, n);
     const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((n + kBlock - 1) / kBlock,
                                                                            (uint64_t)ctx->n_cu * 16));
     hipLaunchKernelGGL(k_p0_from_keys, dim3(grid), dim3(kBlock), 0, ctx->stream, ctx->xkey_k, ctx->xkey_e, n,
                        ctx->xkey_cls + ctx->xkey_fs, ctx->cell_lo, ctx->nb_log2, ctx->d_p0runs);
     constexpr uint64_t kR = 512;
     const uint64_t nreg = (n + kR - 1) / kR;
-    if (ensure(&ctx->d_p0cnt, &ctx->p0cnt_cap, nreg)) return -1;
+    MG_ENSURE(d_p0cnt, p0cnt_cap, nreg);
     hipLaunchKernelGGL(k_fixed_regions, dim3((uint32_t)((nreg + kBlock - 1) / kBlock)), dim3(kBlock), 0, ctx->stream,
                        ctx->d_p0cnt, n, kR, nreg);
     const DiscGeom g = disc_geom<W>(ctx, true, std::max<uint64_t>(1, n / 3));
@@ -3318,7 +3432,7 @@ int prefix_contain_keys_pass(mg_ctx* ctx) {
   if (!ctx->xchg_prefix || !ctx->n) return 0;
   if (ctx->prefix_probe ? dispatch_w<LaunchPrefixProbeKeys>(ctx->maxw, ctx)
                         : dispatch_w<LaunchPrefixContainKeys>(ctx->maxw, ctx))
-    return set_err(ctx, "prefix containment launch failed");
+    return launch_fail(ctx, "prefix containment launch failed");
   return 0;
 }
 
@@ -3327,7 +3441,7 @@ int prefix_contain_keys_pass(mg_ctx* ctx) {
 int prefix_contain_pass(mg_ctx* ctx) {
   if (!ctx->key0_ready) return 0;
   if (ctx->prefix_probe ? dispatch_w<LaunchPrefixProbe>(ctx->maxw, ctx) : dispatch_w<LaunchPrefixContain>(ctx->maxw, ctx))
-    return set_err(ctx, "prefix containment launch failed");
+    return launch_fail(ctx, "prefix containment launch failed");
   return 0;
 }
 
@@ -3388,7 +3502,7 @@ int long_probe(mg_ctx* ctx, bool contain, uint64_t a_lo, uint64_t a_hi) {
       1, std::min<uint64_t>({(nsrc + kWavesPerBlock - 1) / kWavesPerBlock, (uint64_t)ctx->n_cu * 8, ctx->max_blocks}));
   if (contain) {
     hipLaunchKernelGGL(k_probe_long<true>, dim3(grid), dim3(kBlock), 0, ctx->stream, p);
-    return hipGetLastError() == hipSuccess ? 0 : set_err(ctx, "long-read containment launch failed");
+    return hipGetLastError() == hipSuccess ? 0 : launch_fail(ctx, "long-read containment launch failed");
   }
   ctx->nreg = (uint64_t)grid * kWavesPerBlock;
   for (int attempt = 0; attempt < 3; ++attempt) {
@@ -3409,7 +3523,7 @@ int long_probe(mg_ctx* ctx, bool contain, uint64_t a_lo, uint64_t a_hi) {
 // d_super in ID order (unpermuted into d_tmp32 when the slots are clustered)
 const uint32_t* super_in_id_order(mg_ctx* ctx) {
   if (!ctx->d_id || !ctx->n) return ctx->d_super;
-  if (ensure(&ctx->d_tmp32, &ctx->tmp32_cap, ctx->n) != hipSuccess) return ctx->d_super;
+  if (ensure(ctx, &ctx->d_tmp32, &ctx->tmp32_cap, ctx->n, "d_tmp32") != hipSuccess) return ctx->d_super;
   hipLaunchKernelGGL(k_unpermute_u32, dim3((uint32_t)((ctx->n + kBlock - 1) / kBlock)), dim3(kBlock), 0, ctx->stream,
                      ctx->d_super, ctx->d_id, ctx->n, ctx->d_tmp32);
   return ctx->d_tmp32;
@@ -3453,10 +3567,7 @@ int settle_rows(mg_ctx* ctx, bool* again);
 int run_discover(mg_ctx* ctx, bool contain) {
   for (int attempt = 0; attempt < 3; ++attempt) {
     const int rc = dispatch_w<LaunchDiscover>(ctx->maxw, ctx, contain);
-    if (rc < 0) {
-      ctx->err = "discovery launch failed";
-      return -1;
-    }
+    if (rc < 0) return launch_fail(ctx, "discovery launch failed");  // (keeps the callee's cause)
     bool again = false;
     if (settle_runs(ctx, &again)) return -1;
     if (!contain && !again && settle_rows(ctx, &again)) return -1;
@@ -3515,7 +3626,7 @@ void mg_destroy(mg_ctx* ctx) {
                   ctx->d_digest, ctx->id_store[0], ctx->id_store[1], ctx->phys_store[0], ctx->phys_store[1],
                   ctx->d_tmp32, ctx->d_lay_k[0], ctx->d_lay_k[1], ctx->d_lay_v[0], ctx->d_lay_v[1], ctx->d_lay_tmp,
                   ctx->d_words_alt, ctx->d_len_alt, ctx->d_cbits, ctx->d_ccnt, ctx->d_lcells, ctx->d_lkcells,
-                  ctx->d_rhead, ctx->d_rstart, ctx->d_rcnt, ctx->d_dcnt, ctx->d_p0runs, ctx->d_p0cnt};
+                  ctx->d_rhead, ctx->d_rstart, ctx->d_rcnt, ctx->d_dcnt, ctx->d_p0runs, ctx->d_p0cnt, ctx->d_xexp};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   for (auto& e : ctx->ev)
@@ -3551,6 +3662,7 @@ static int finish_upload(mg_ctx* ctx, const uint16_t* lens_host) {
 int mg_upload_reads_packed(mg_ctx* ctx, const uint64_t* words, const uint16_t* lens, uint64_t n_reads,
                            uint32_t words_per_read) {
   if (!ctx) return -1;
+  ctx->err.clear();  // (a message left by an earlier failed call is not this call's cause)
   MG_TRY(hipSetDevice(ctx->device));
   if (n_reads >= 0xFFFFFFFFull) return set_err(ctx, "too many reads (max 2^32-2)");
   uint32_t mx = 0;
@@ -3563,8 +3675,8 @@ int mg_upload_reads_packed(mg_ctx* ctx, const uint64_t* words, const uint16_t* l
   ctx->maxw = maxw;
   ctx->stride = slot_stride(maxw);
   const size_t nw = (size_t)(n_reads + 2) * ctx->stride + 2;  // zero pad for over-reads
-  MG_TRY(ensure(&ctx->d_words, &ctx->words_cap, nw));
-  MG_TRY(ensure(&ctx->d_len, &ctx->len_cap, n_reads + 1));
+  MG_ENSURE(d_words, words_cap, nw);
+  MG_ENSURE(d_len, len_cap, n_reads + 1);
   MG_TRY(hipMemsetAsync(ctx->d_words, 0, nw * sizeof(uint64_t), ctx->stream));
   const uint32_t copy_w = std::min<uint32_t>(words_per_read, ctx->stride);
   if (n_reads && ctx->stride == words_per_read) {
@@ -3583,6 +3695,7 @@ int mg_upload_reads_packed(mg_ctx* ctx, const uint64_t* words, const uint16_t* l
 
 int mg_upload_reads_ascii(mg_ctx* ctx, const char* concat, const uint64_t* offsets, uint64_t n_reads) {
   if (!ctx) return -1;
+  ctx->err.clear();  // (a message left by an earlier failed call is not this call's cause)
   MG_TRY(hipSetDevice(ctx->device));
   if (n_reads >= 0xFFFFFFFFull) return set_err(ctx, "too many reads (max 2^32-2)");
   std::vector<uint16_t> lens(n_reads);
@@ -3612,8 +3725,8 @@ int mg_upload_reads_ascii(mg_ctx* ctx, const char* concat, const uint64_t* offse
   char* const d_ascii = st.ascii;
   uint64_t* const d_off = st.off;
   const size_t nw = (size_t)(n_reads + 2) * ctx->stride + 2;
-  MG_TRY(ensure(&ctx->d_words, &ctx->words_cap, nw));
-  MG_TRY(ensure(&ctx->d_len, &ctx->len_cap, n_reads + 1));
+  MG_ENSURE(d_words, words_cap, nw);
+  MG_ENSURE(d_len, len_cap, n_reads + 1);
   MG_TRY(hipMemsetAsync(ctx->d_words, 0, nw * sizeof(uint64_t), ctx->stream));
   if (total) MG_TRY(hipMemcpyAsync(d_ascii, concat, total, hipMemcpyHostToDevice, ctx->stream));
   MG_TRY(hipMemcpyAsync(d_off, offsets, (n_reads + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, ctx->stream));
@@ -3632,6 +3745,7 @@ int mg_upload_reads_ascii(mg_ctx* ctx, const char* concat, const uint64_t* offse
 
 int mg_download_reads_packed(mg_ctx* ctx, uint64_t* words, uint16_t* lens, uint32_t* words_per_read) {
   if (!ctx) return -1;
+  ctx->err.clear();  // (a message left by an earlier failed call is not this call's cause)
   MG_TRY(hipSetDevice(ctx->device));
   if (words_per_read) *words_per_read = ctx->maxw;
   if (words && ctx->n)
@@ -3709,6 +3823,10 @@ int mg_set_option(mg_ctx* ctx, const char* name, int64_t value) {
     ctx->max_blocks = value > 0 ? (uint32_t)value : 8192u;
     return 0;
   }
+  if (!strcmp(name, "alloc_cap")) {  // tests: device allocations above this many bytes fail (0 = no cap)
+    ctx->alloc_cap = (uint64_t)std::max<int64_t>(0, value);
+    return 0;
+  }
   if (!strcmp(name, "run_cap")) {  // tests: initial run records per scan region (0 = sized from the reads)
     ctx->run_cap_opt = (uint64_t)std::max<int64_t>(0, value);
     ctx->run_cap_need = 0;
@@ -3720,7 +3838,8 @@ int mg_set_option(mg_ctx* ctx, const char* name, int64_t value) {
       flag("probe_compact", &ctx->probe_compact) || flag("live_index", &ctx->live_index) ||
       flag("xchg_sort_runs", &ctx->xchg_sort_runs) || flag("layout_scratch", &ctx->layout_scratch) ||
       flag("xchg_windows", &ctx->xchg_windows) || flag("chain_par", &ctx->chain_par) ||
-      flag("live_runs", &ctx->live_runs) || flag("live_overlap", &ctx->live_overlap))
+      flag("live_runs", &ctx->live_runs) || flag("live_overlap", &ctx->live_overlap) ||
+      flag("xchg_route_rows", &ctx->xchg_route_rows) || flag("xchg_scan_lds", &ctx->xchg_scan_lds))
     return 0;
   if (flag("prefix_contain", &ctx->prefix_contain) || flag("prefix_probe", &ctx->prefix_probe)) {
     ctx->index_ready = false;
@@ -3733,8 +3852,15 @@ int mg_set_shard(mg_ctx* ctx, uint32_t rank, uint32_t nranks, uint64_t read_lo, 
   if (!ctx) return -1;
   if (nranks == 0 || rank >= nranks) return set_err(ctx, "bad shard rank/nranks");
   if (read_hi && read_hi < read_lo) return set_err(ctx, "bad read range");
-  if (rank != ctx->rank || nranks != ctx->nranks || read_lo != ctx->read_lo || read_hi != ctx->read_hi)
+  if (rank != ctx->rank || nranks != ctx->nranks || read_lo != ctx->read_lo || read_hi != ctx->read_hi) {
     ctx->index_ready = false;  // the next mg_build_index re-clusters the slots for a new range (ensure_layout_range)
+    // a new shard starts a new build: no exchange state of the last one carries over
+    ctx->xchg = false;
+    ctx->xchg_fused = false;
+    ctx->xmarks_done = false;
+    ctx->xmarks = nullptr;
+    ctx->packable = 0;
+  }
   ctx->rank = rank;
   ctx->nranks = nranks;
   ctx->read_lo = read_lo;
@@ -3784,13 +3910,16 @@ int setup_index(mg_ctx* ctx, uint32_t min_overlap, uint32_t seed_k, bool cells =
   ctx->live_ready = false;
   ctx->key0_ready = false;  // set by the fused build when it writes the o = 0 keys
   ctx->xchg = false;        // mg_xchg_begin sets it after this
+  ctx->xchg_fused = false;  // (a plain build after a one-rank exchange step takes no exchange shortcut)
+  ctx->xmarks_done = false;
+  ctx->xmarks = nullptr;
   ctx->packable = 0;
   return 0;
 }
 
 // the (cleared) cell table of this rank's bucket range
 int setup_cells(mg_ctx* ctx) {
-  MG_TRY(ensure(&ctx->d_cells, &ctx->cells_cap, ctx->cell_n * kCell));
+  MG_ENSURE(d_cells, cells_cap, ctx->cell_n * kCell);
   MG_TRY(hipMemsetAsync(ctx->d_cells, 0xFF, ctx->cell_n * kCell * sizeof(uint64_t), ctx->stream));  // kEmpty
   return 0;
 }
@@ -3811,7 +3940,7 @@ template <int KIND>
 int route_slots(mg_ctx* ctx, PartParams pp, void* out, void* self_out, uint64_t slot, uint32_t rounds,
                 unsigned long long* counts, unsigned long long* precounted = nullptr) {
   const uint32_t grid = precounted ? (uint32_t)pp.nreg : part_grid(pp.nreg);
-  if (!precounted) MG_TRY(ensure(&ctx->d_blk, &ctx->blk_cap, (size_t)grid * ctx->nranks));
+  if (!precounted) MG_ENSURE(d_blk, blk_cap, (size_t)grid * ctx->nranks);
   pp.nranks = ctx->nranks;
   pp.nb_log2 = ctx->nb_log2;
   pp.n_reads = ctx->n;
@@ -3881,14 +4010,16 @@ int ensure_rows(mg_ctx* ctx, uint64_t nsrc) {
   if (ctx->seg_cap_regions < max_regions) {
     if (ctx->d_seg) (void)hipFree(ctx->d_seg);
     ctx->d_seg = nullptr;
-    MG_TRY(hipMalloc(&ctx->d_seg, max_regions * sizeof(unsigned long long)));
+    ctx->seg_cap_regions = 0;
+    if (ctx_malloc(ctx, (void**)&ctx->d_seg, max_regions * sizeof(unsigned long long), "d_seg")) return -1;
     ctx->seg_cap_regions = max_regions;
   }
   const uint64_t want = ctx->rows_cap_opt ? ctx->rows_cap_opt : std::max<uint64_t>(1u << 20, 48 * nsrc);
   if (want > ctx->rows_cap) {
     if (ctx->d_rows) (void)hipFree(ctx->d_rows);
     ctx->d_rows = nullptr;
-    MG_TRY(hipMalloc(&ctx->d_rows, want * 3 * sizeof(uint32_t)));
+    ctx->rows_cap = 0;
+    if (ctx_malloc(ctx, (void**)&ctx->d_rows, want * 3 * sizeof(uint32_t), "d_rows (row regions)")) return -1;
     ctx->rows_cap = want;
   }
   if (ctx->stats) {
@@ -3917,7 +4048,8 @@ int settle_rows(mg_ctx* ctx, bool* again) {
     const uint64_t want = (row_max + row_max / 4 + 1024) * ctx->nreg;
     if (ctx->d_rows) (void)hipFree(ctx->d_rows);
     ctx->d_rows = nullptr;
-    MG_TRY(hipMalloc(&ctx->d_rows, want * 3 * sizeof(uint32_t)));
+    ctx->rows_cap = 0;
+    if (ctx_malloc(ctx, (void**)&ctx->d_rows, want * 3 * sizeof(uint32_t), "d_rows (row regions)")) return -1;
     ctx->rows_cap = want;
     *again = true;
     return 0;
@@ -3995,7 +4127,7 @@ int ensure_scan(mg_ctx* ctx) {
   }
   for (int attempt = 0; attempt < 3; ++attempt) {
     if (ctx->n) {
-      if (dispatch_w<LaunchScanRuns>(ctx->maxw, ctx)) return set_err(ctx, "scan launch failed");
+      if (dispatch_w<LaunchScanRuns>(ctx->maxw, ctx)) return launch_fail(ctx, "scan launch failed");
     } else {
       ctx->nrun_reg = 0;
     }
@@ -4036,7 +4168,7 @@ int build_live_index(mg_ctx* ctx) {
   while (nbl < 31 && (1ull << nbl) * kCell < 5 * live) nbl++;
   if (nbl >= ctx->nb_log2 && !force) return 0;  // no smaller than the full table: probe that
   nbl = std::min(nbl, ctx->nb_log2);
-  MG_TRY(ensure(&ctx->d_lcells, &ctx->lcells_cap, (1ull << nbl) * kCell));
+  MG_ENSURE(d_lcells, lcells_cap, (1ull << nbl) * kCell);
   MG_TRY(hipMemsetAsync(ctx->d_lcells, 0xFF, (1ull << nbl) * kCell * sizeof(uint64_t), ctx->stream));
   IndexParams p = index_params(ctx);
   p.nb_log2 = nbl;
@@ -4046,7 +4178,7 @@ int build_live_index(mg_ctx* ctx) {
   p.cell_n = 1ull << nbl;
   p.cells = ctx->d_lcells;
   p.cbits = ctx->d_cbits;
-  if (dispatch_w<LaunchIndexLive>(ctx->maxw, ctx, &p)) return set_err(ctx, "live index launch failed");
+  if (dispatch_w<LaunchIndexLive>(ctx->maxw, ctx, &p)) return launch_fail(ctx, "live index launch failed");
   ctx->lnb_log2 = nbl;
   ctx->live_cells = 1ull << nbl;
   ctx->live_coarse = false;
@@ -4063,7 +4195,7 @@ hipError_t grow_tmp(mg_ctx* ctx, size_t tb) {
     }
     ctx->d_xsort_tmp = nullptr;
     ctx->xsort_tmp_cap = 0;
-    const hipError_t e = hipMalloc(&ctx->d_xsort_tmp, tb);
+    const hipError_t e = ctx_malloc(ctx, &ctx->d_xsort_tmp, tb, "d_xsort_tmp (sort scratch)");
     if (e != hipSuccess) return e;
     ctx->xsort_tmp_cap = tb;
   }
@@ -4138,8 +4270,8 @@ int build_cells(mg_ctx* ctx, const uint32_t* key, const uint64_t* ent, const uns
     return check_cells(ctx, key, ent, nullptr, n_dev, n_host, cells, cell_n, gshift, cshift, skip_odd);
   }
   if (n_host > 0xFFFFFFFFull) return set_err(ctx, "cell build: more than 2^32 records");
-  MG_TRY(ensure(&ctx->d_rhead, &ctx->rhead_cap, n_host));
-  MG_TRY(ensure(&ctx->d_rstart, &ctx->rstart_cap, n_host));
+  MG_ENSURE(d_rhead, rhead_cap, n_host);
+  MG_ENSURE(d_rstart, rstart_cap, n_host);
   hipLaunchKernelGGL(k_over_heads, dim3(grid), dim3(kBlock), 0, ctx->stream, key, ent, n_dev, n_host, gshift, skip_odd,
                      ctx->d_rhead);
   MG_TRY(hipGetLastError());
@@ -4178,12 +4310,12 @@ int build_live_index_xchg(mg_ctx* ctx) {
     ++sft;
   if (!sft && !force) return 0;  // no smaller than the full table: probe that
   const uint64_t live_n = (ctx->cell_n + (1ull << sft) - 1) >> sft;
-  MG_TRY(ensure(&ctx->d_lcells, &ctx->lcells_cap, live_n * kCell));
+  MG_ENSURE(d_lcells, lcells_cap, live_n * kCell);
   // the live reads' records, compacted in order into the sort's other buffers
   const uint64_t n = ctx->xkeys_n;
   uint32_t* lk = ctx->xkey_k_alt;
   uint64_t* le = ctx->xkey_e_alt;
-  MG_TRY(ensure(&ctx->d_xflag, &ctx->xflag_cap, std::max<uint64_t>(n, 1)));
+  MG_ENSURE(d_xflag, xflag_cap, std::max<uint64_t>(n, 1));
   if (!ctx->d_nlive) MG_TRY(hipMalloc(&ctx->d_nlive, sizeof(unsigned long long)));
   MG_TRY(hipMemsetAsync(ctx->d_nlive, 0, sizeof(unsigned long long), ctx->stream));
   if (n) {
@@ -4259,7 +4391,7 @@ int probe_shared(mg_ctx* ctx, bool contain) {
     }
     if (!contain && attempt == 0 && ctx->contained_done && build_live_index(ctx)) return -1;
     if (live_runs_join(ctx, side)) return -1;
-    if (dispatch_w<LaunchProbeShared>(ctx->maxw, ctx, contain)) return set_err(ctx, "probe launch failed");
+    if (dispatch_w<LaunchProbeShared>(ctx->maxw, ctx, contain)) return launch_fail(ctx, "probe launch failed");
     MG_TRY(hipEventRecord(ctx->ev[9], ctx->stream));
     if (contain) return 0;
     if (ctx->scan_state == 1) {  // the scan's regions, settled now (the probe above may have cut them)
@@ -4297,8 +4429,8 @@ static int sort_xrecs(mg_ctx* ctx, const ulonglong2* recv, uint64_t slot, uint32
   for (uint32_t s = 0; s < P; ++s) n += std::min<uint64_t>(c[s], (uint64_t)rounds * slot);  // cut streams: what arrived
   if (n > 0x7FFFFFFFull) return set_err(ctx, "exchange: more than 2^31 records received on one rank");
   for (int b = 0; b < 2; ++b) {
-    MG_TRY(ensure(&ctx->d_xk[b], &ctx->xk_cap[b], std::max<uint64_t>(n, 1)));
-    MG_TRY(ensure(&ctx->d_xv[b], &ctx->xv_cap[b], std::max<uint64_t>(n, 1)));
+    MG_ENSURE(d_xk[b], xk_cap[b], std::max<uint64_t>(n, 1));
+    MG_ENSURE(d_xv[b], xv_cap[b], std::max<uint64_t>(n, 1));
   }
   int hb = 1;
   while (hb < 40 && (1ULL << hb) < ctx->cell_n) ++hb;  // bits of a local bucket index
@@ -4326,7 +4458,7 @@ static int sort_xrecs(mg_ctx* ctx, const ulonglong2* recv, uint64_t slot, uint32
       if (ctx->d_xsort_tmp) MG_TRY(hipFree(ctx->d_xsort_tmp));
       ctx->d_xsort_tmp = nullptr;
       ctx->xsort_tmp_cap = 0;
-      MG_TRY(hipMalloc(&ctx->d_xsort_tmp, tb));
+      if (ctx_malloc(ctx, &ctx->d_xsort_tmp, tb, "d_xsort_tmp (sort scratch)")) return -1;
       ctx->xsort_tmp_cap = tb;
     }
     tb = ctx->xsort_tmp_cap;
@@ -4344,7 +4476,7 @@ static int sort_xruns(mg_ctx* ctx, const ulonglong2* recv, uint64_t slot, uint32
   uint64_t n = 0;
   if (sort_xrecs(ctx, recv, slot, rounds, counts, &n)) return -1;
   const uint64_t nreg = (n + kXRegion - 1) / kXRegion;
-  MG_TRY(ensure(&ctx->d_flat_cnt, &ctx->flat_cnt_cap, std::max<uint64_t>(nreg, 1)));
+  MG_ENSURE(d_flat_cnt, flat_cnt_cap, std::max<uint64_t>(nreg, 1));
   if (nreg)
     hipLaunchKernelGGL(k_fixed_regions, dim3((uint32_t)((nreg + kBlock - 1) / kBlock)), dim3(kBlock), 0, ctx->stream,
                        ctx->d_flat_cnt, n, kXRegion, nreg);
@@ -4362,7 +4494,7 @@ static int sort_xruns(mg_ctx* ctx, const ulonglong2* recv, uint64_t slot, uint32
 // share cells and partners as in the fused path; ordering them by bucket
 // (option xchg_sort_runs) measured slower: C3 simulated P = 8 step 20.5 vs
 // 18.4 ms, C5 133.8 vs 123.0 ms (profiles/r04e_ab_xchg_sort_runs.txt).
-static int prepare_xruns(mg_ctx* ctx, const void* recv, uint64_t slot, uint32_t rounds,
+static int prepare_xruns(mg_ctx* ctx, const void* recv8, uint64_t slot, uint32_t rounds,
                          const unsigned long long* counts) {
   if (ctx->nranks == 1) {  // one rank: the scan's own run regions, as the fused path probes them
     ctx->xruns_base = ctx->d_runs;
@@ -4372,6 +4504,15 @@ static int prepare_xruns(mg_ctx* ctx, const void* recv, uint64_t slot, uint32_t 
     ctx->xruns_ready = true;
     return 0;
   }
+  // the 8-B metas that arrived -> 16-B probe records (x = the minimizer's
+  // mix64, re-hashed from this rank's copy of the read) in the context's own
+  // buffer, same slot positions, so the slot regions below apply unchanged
+  const uint64_t total = (uint64_t)rounds * ctx->nranks * slot;
+  MG_ENSURE(d_xexp, xexp_cap, std::max<uint64_t>(total, 1));
+  if (total && dispatch_w<LaunchXrunsExpand>(ctx->maxw, ctx, reinterpret_cast<const uint64_t*>(recv8), slot, total,
+                                             counts, ctx->d_xexp))
+    return launch_fail(ctx, "run records launch failed");
+  const void* recv = ctx->d_xexp;
   if (ctx->xchg_sort_runs) {
     if (sort_xruns(ctx, reinterpret_cast<const ulonglong2*>(recv), slot, rounds, counts)) return -1;
     ctx->xruns_cnt = ctx->d_flat_cnt;  // (after sort_xruns: it may have grown the counts)
@@ -4411,8 +4552,8 @@ int layout_current(mg_ctx* ctx, bool force) {
   int pb = 1;
   while (pb < 10 && (1u << pb) <= ctx->maxlen) ++pb;  // offsets < maxlen (capped at 10 bits)
   for (int b = 0; b < 2; ++b) {
-    MG_TRY(ensure(&ctx->d_lay_k[b], &ctx->lay_k_cap[b], n));
-    MG_TRY(ensure(&ctx->d_lay_v[b], &ctx->lay_v_cap[b], n));
+    MG_ENSURE(d_lay_k[b], lay_k_cap[b], n);
+    MG_ENSURE(d_lay_v[b], lay_v_cap[b], n);
   }
   const unsigned kbits = 32u + (unsigned)pb + (grouped ? 2u : 0u);  // the key's significant bits
   size_t tb = 0;
@@ -4422,27 +4563,27 @@ int layout_current(mg_ctx* ctx, bool force) {
     if (ctx->d_lay_tmp) MG_TRY(hipFree(ctx->d_lay_tmp));
     ctx->d_lay_tmp = nullptr;
     ctx->lay_tmp_cap = 0;
-    MG_TRY(hipMalloc(&ctx->d_lay_tmp, tb));
+    if (ctx_malloc(ctx, &ctx->d_lay_tmp, tb, "d_lay_tmp (layout sort scratch)")) return -1;
     ctx->lay_tmp_cap = tb;
   }
   tb = ctx->lay_tmp_cap;
-  MG_TRY(ensure(&ctx->d_words_alt, &ctx->words_alt_cap, ctx->words_cap));
-  MG_TRY(ensure(&ctx->d_len_alt, &ctx->len_alt_cap, ctx->len_cap));
+  MG_ENSURE(d_words_alt, words_alt_cap, ctx->words_cap);
+  MG_ENSURE(d_len_alt, len_alt_cap, ctx->len_cap);
   // the new maps go to the pair the current order does not use
   const int sel = (ctx->d_id && ctx->d_id == ctx->id_store[0]) ? 1 : 0;
-  MG_TRY(ensure(&ctx->id_store[sel], &ctx->id_cap[sel], n));
-  MG_TRY(ensure(&ctx->phys_store[sel], &ctx->phys_cap[sel], n));
+  MG_ENSURE(id_store[sel], id_cap[sel], n);
+  MG_ENSURE(phys_store[sel], phys_cap[sel], n);
   uint32_t* id_new = ctx->id_store[sel];
   uint32_t* ph_new = ctx->phys_store[sel];
   const uint64_t S = slot_words((int)ctx->maxw);
   // --- timed: kernels only
   MG_TRY(hipEventRecord(ctx->ev[14], ctx->stream));
   if (dispatch_w<LaunchLayout>(ctx->maxw, ctx, lo, hi, grouped, pb, ctx->d_lay_k[0], ctx->d_lay_v[0]))
-    return set_err(ctx, "layout key launch failed");
+    return launch_fail(ctx, "layout key launch failed");
   MG_TRY(rocprim::radix_sort_pairs(ctx->d_lay_tmp, tb, ctx->d_lay_k[0], ctx->d_lay_k[1], ctx->d_lay_v[0],
                                    ctx->d_lay_v[1], (unsigned int)n, 0u, kbits, ctx->stream));
   if (dispatch_w<LaunchLayoutGather>(ctx->maxw, ctx, ctx->d_lay_v[1], ctx->d_words_alt, ctx->d_len_alt, id_new))
-    return set_err(ctx, "layout gather launch failed");
+    return launch_fail(ctx, "layout gather launch failed");
   // the zero pad past the last slot (over-reads of the kernels)
   MG_TRY(hipMemsetAsync(ctx->d_words_alt + n * S, 0, (ctx->words_cap - n * S) * sizeof(uint64_t), ctx->stream));
   hipLaunchKernelGGL(k_layout_phys, dim3((uint32_t)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, ctx->stream, id_new,
@@ -4500,11 +4641,12 @@ extern "C" {
 
 int mg_build_index(mg_ctx* ctx, uint32_t min_overlap, uint32_t seed_k) {
   if (!ctx) return -1;
+  ctx->err.clear();  // (a message left by an earlier failed call is not this call's cause)
   MG_TRY(hipSetDevice(ctx->device));
   if (ensure_layout_range(ctx)) return -1;  // a source-read range set after the upload
   // the cell table exists before the timed window (its clear is inside it)
   if (setup_index(ctx, min_overlap, seed_k, false)) return -1;
-  MG_TRY(ensure(&ctx->d_cells, &ctx->cells_cap, ctx->cell_n * kCell));
+  MG_ENSURE(d_cells, cells_cap, ctx->cell_n * kCell);
   MG_TRY(hipEventRecord(ctx->ev[0], ctx->stream));
   if (setup_cells(ctx)) return -1;
   ctx->scan_state = 0;
@@ -4515,7 +4657,7 @@ int mg_build_index(mg_ctx* ctx, uint32_t min_overlap, uint32_t seed_k) {
   if (long_mode(ctx)) {  // reads > 1024 bp: k_index_long, one thread per key
     ctx->index_o1 = true;
     if (ctx->nranks > 1) return set_err(ctx, "reads longer than 1024 bp: bucket-sharded index not supported");
-    if (launch_index(ctx)) return set_err(ctx, "index build launch failed");
+    if (launch_index(ctx)) return launch_fail(ctx, "index build launch failed");
   } else if (shared_scan(ctx)) {
     // one pass over the reads: the index inserts ride on the window scan
     // (k_scan<INDEX>), whose runs then serve the containment and discovery
@@ -4529,15 +4671,15 @@ int mg_build_index(mg_ctx* ctx, uint32_t min_overlap, uint32_t seed_k) {
     // the discovery probe then walks the live reads' table (always built,
     // build_live_index), so this table holds o = 0 / 2 only
     ctx->index_o3 = !(ctx->key0_ready && ctx->live_index);
-    if (ctx->key0_ready && ctx->prefix_probe) MG_TRY(ensure(&ctx->d_p0runs, &ctx->p0runs_cap, ctx->n + 1));
-    if (ctx->key0_ready && !ctx->prefix_probe) MG_TRY(ensure(&ctx->d_key0, &ctx->key0_cap, ctx->n + 1));
+    if (ctx->key0_ready && ctx->prefix_probe) MG_ENSURE(d_p0runs, p0runs_cap, ctx->n + 1);
+    if (ctx->key0_ready && !ctx->prefix_probe) MG_ENSURE(d_key0, key0_cap, ctx->n + 1);
     if (ctx->n && dispatch_w<LaunchScanAll>(ctx->maxw, ctx, ctx->stream))
-      return set_err(ctx, "index build launch failed");
+      return launch_fail(ctx, "index build launch failed");
     if (!ctx->n) ctx->nrun_reg = 0;
     ctx->scan_state = 1;
   } else {  // the whole index for a source-range shard (its containment probe reads suffix-key hits)
     ctx->index_o1 = mixed;
-    if (dispatch_w<LaunchIndex>(ctx->maxw, ctx)) return set_err(ctx, "index build launch failed");
+    if (dispatch_w<LaunchIndex>(ctx->maxw, ctx)) return launch_fail(ctx, "index build launch failed");
   }
   MG_TRY(hipEventRecord(ctx->ev[1], ctx->stream));
   ctx->index_times_pending = true;  // (read by settle_index_times once the events completed)
@@ -4547,14 +4689,15 @@ int mg_build_index(mg_ctx* ctx, uint32_t min_overlap, uint32_t seed_k) {
 
 int mg_mark_contained(mg_ctx* ctx, uint32_t* super_out) {
   if (!ctx) return -1;
+  ctx->err.clear();  // (a message left by an earlier failed call is not this call's cause)
   MG_TRY(hipSetDevice(ctx->device));
   if (!ctx->index_ready) return set_err(ctx, "mg_build_index must run first");
-  MG_TRY(ensure(&ctx->d_super, &ctx->super_cap, ctx->n + 1));
-  MG_TRY(ensure(&ctx->d_cbits, &ctx->cbits_cap, (ctx->n + 63) / 64 * 2));
+  MG_ENSURE(d_super, super_cap, ctx->n + 1);
+  MG_ENSURE(d_cbits, cbits_cap, (ctx->n + 63) / 64 * 2);
   if (!ctx->d_any) MG_TRY(hipMalloc(&ctx->d_any, sizeof(unsigned int)));
   ctx->t.contained_ms = 0.f;
   if (ctx->minlen != ctx->maxlen) {  // OverlapGraph.cpp:228-233
-    MG_TRY(ensure(&ctx->d_superkey, &ctx->superkey_cap, ctx->n + 1));
+    MG_ENSURE(d_superkey, superkey_cap, ctx->n + 1);
     ctx->superkey = ctx->d_superkey;
     MG_TRY(hipMemsetAsync(ctx->d_superkey, 0, (ctx->n + 1) * sizeof(unsigned long long), ctx->stream));
     MG_TRY(hipMemsetAsync(ctx->d_any, 0, sizeof(unsigned int), ctx->stream));
@@ -4619,6 +4762,7 @@ int mg_mark_contained(mg_ctx* ctx, uint32_t* super_out) {
 
 int mg_find_overlaps(mg_ctx* ctx, uint64_t* n_rows) {
   if (!ctx) return -1;
+  ctx->err.clear();  // (a message left by an earlier failed call is not this call's cause)
   MG_TRY(hipSetDevice(ctx->device));
   if (!ctx->index_ready) return set_err(ctx, "mg_build_index must run first");
   if (!ctx->contained_done && mg_mark_contained(ctx, nullptr)) return -1;
@@ -4663,7 +4807,7 @@ int mg_find_overlaps(mg_ctx* ctx, uint64_t* n_rows) {
 }
 
 /* ---------------------------------------------------------- exchange mode --- */
-uint32_t mg_record_bytes(int what) { return what == MG_ROWS ? 12u : (what == MG_KEYS || what == MG_RUNS) ? 16u : 0u; }
+uint32_t mg_record_bytes(int what) { return what == MG_ROWS ? 12u : (what == MG_KEYS || what == MG_RUNS) ? 8u : 0u; }
 
 int mg_xchg_caps(mg_ctx* ctx, uint32_t min_overlap, uint32_t seed_k, uint64_t* caps) {
   if (!ctx || !caps) return -1;
@@ -4682,6 +4826,7 @@ int mg_xchg_caps(mg_ctx* ctx, uint32_t min_overlap, uint32_t seed_k, uint64_t* c
 
 int mg_xchg_begin(mg_ctx* ctx, uint32_t min_overlap, uint32_t seed_k) {
   if (!ctx) return -1;
+  ctx->err.clear();  // (a message left by an earlier failed call is not this call's cause)
   MG_TRY(hipSetDevice(ctx->device));
   if (ctx->nranks > (uint32_t)kMaxRanks) return set_err(ctx, "at most 64 ranks");
   if (long_mode(ctx)) return set_err(ctx, "reads longer than 1024 bp: exchange mode not supported (use the replicated mode)");
@@ -4700,7 +4845,7 @@ int mg_xchg_begin(mg_ctx* ctx, uint32_t min_overlap, uint32_t seed_k) {
   MG_TRY(hipEventRecord(ctx->ev[0], ctx->stream));
   if (setup_index(ctx, min_overlap, seed_k, false)) return -1;
   // this rank's cells: mg_xchg_insert_keys writes every one of them (no clear)
-  MG_TRY(ensure(&ctx->d_cells, &ctx->cells_cap, ctx->cell_n * kCell));
+  MG_ENSURE(d_cells, cells_cap, ctx->cell_n * kCell);
   ctx->xchg = true;
   ctx->xruns_ready = false;
   ctx->xchg_prefix = ctx->minlen != ctx->maxlen && ctx->prefix_contain;
@@ -4712,8 +4857,8 @@ int mg_xchg_begin(mg_ctx* ctx, uint32_t min_overlap, uint32_t seed_k) {
   source_range(ctx, &lo, &hi);
   ctx->xchg_lo = lo;
   ctx->xchg_hi = hi;
-  MG_TRY(ensure(&ctx->d_kb, &ctx->kb_cap, 4 * (hi - lo) + 1));
-  MG_TRY(ensure(&ctx->d_ke, &ctx->ke_cap, 4 * (hi - lo) + 1));
+  MG_ENSURE(d_kb, kb_cap, 4 * (hi - lo) + 1);
+  MG_ENSURE(d_ke, ke_cap, 4 * (hi - lo) + 1);
   ctx->scan_state = 0;
   ctx->shared_scan_ms = 0.f;
   ctx->t = mg_timings{};
@@ -4722,7 +4867,7 @@ int mg_xchg_begin(mg_ctx* ctx, uint32_t min_overlap, uint32_t seed_k) {
     // runs in per-wavefront regions, as the fused path writes them
     for (int attempt = 0;; ++attempt) {
       if (attempt == 3) return set_err(ctx, "run buffers overflow after resize");
-      if (dispatch_w<LaunchScanXchg>(ctx->maxw, ctx, lo, hi)) return set_err(ctx, "scan launch failed");
+      if (dispatch_w<LaunchScanXchg>(ctx->maxw, ctx, lo, hi)) return launch_fail(ctx, "scan launch failed");
       bool again = false;
       if (settle_runs(ctx, &again)) return -1;
       if (!again) break;
@@ -4738,6 +4883,7 @@ int mg_xchg_begin(mg_ctx* ctx, uint32_t min_overlap, uint32_t seed_k) {
 int mg_xchg_pack(mg_ctx* ctx, int what, void* dst, uint64_t slot, uint32_t rounds, uint64_t* counts,
                  void* self_dst) {
   if (!ctx) return -1;
+  ctx->err.clear();  // (a message left by an earlier failed call is not this call's cause)
   MG_TRY(hipSetDevice(ctx->device));
   if (what < MG_KEYS || what > MG_ROWS || !(ctx->packable & (1 << what)))
     return set_err(ctx, "mg_xchg_pack: nothing of that kind to pack now (call order)");
@@ -4788,6 +4934,7 @@ int mg_xchg_pack(mg_ctx* ctx, int what, void* dst, uint64_t slot, uint32_t round
 
 int mg_xchg_insert_keys(mg_ctx* ctx, const void* recv, uint64_t slot, uint32_t rounds, const uint64_t* counts) {
   if (!ctx) return -1;
+  ctx->err.clear();  // (a message left by an earlier failed call is not this call's cause)
   MG_TRY(hipSetDevice(ctx->device));
   if (!ctx->xchg && !ctx->xchg_fused) return set_err(ctx, "mg_xchg_begin must run first");
   if (ctx->xchg_fused) return 0;  // one rank: the fused build filed the keys already
@@ -4801,8 +4948,8 @@ int mg_xchg_insert_keys(mg_ctx* ctx, const void* recv, uint64_t slot, uint32_t r
     n = (ctx->index_o1 ? 4 : 3) * (ctx->xchg_hi - ctx->xchg_lo);
     k0 = ctx->d_kb;
     e0 = ctx->d_ke;
-    MG_TRY(ensure(&ctx->d_xkk[1], &ctx->xkk_cap[1], std::max<uint64_t>(n, 1)));
-    MG_TRY(ensure(&ctx->d_xke[1], &ctx->xke_cap[1], std::max<uint64_t>(n, 1)));
+    MG_ENSURE(d_xkk[1], xkk_cap[1], std::max<uint64_t>(n, 1));
+    MG_ENSURE(d_xke[1], xke_cap[1], std::max<uint64_t>(n, 1));
   } else {
     const uint64_t total = (uint64_t)rounds * P * slot;
     if (total) {
@@ -4813,18 +4960,14 @@ int mg_xchg_insert_keys(mg_ctx* ctx, const void* recv, uint64_t slot, uint32_t r
       for (uint32_t q = 0; q < P; ++q) n += std::min<uint64_t>(c[q], (uint64_t)rounds * slot);  // cut streams: what arrived
     }
     for (int b = 0; b < 2; ++b) {
-      MG_TRY(ensure(&ctx->d_xkk[b], &ctx->xkk_cap[b], std::max<uint64_t>(n, 1)));
-      MG_TRY(ensure(&ctx->d_xke[b], &ctx->xke_cap[b], std::max<uint64_t>(n, 1)));
+      MG_ENSURE(d_xkk[b], xkk_cap[b], std::max<uint64_t>(n, 1));
+      MG_ENSURE(d_xke[b], xke_cap[b], std::max<uint64_t>(n, 1));
     }
     k0 = ctx->d_xkk[0];
     e0 = ctx->d_xke[0];
-    if (n) {
-      const uint32_t grid = (uint32_t)std::min<uint64_t>((total + kBlock - 1) / kBlock, 65536);
-      hipLaunchKernelGGL(k_xkeys_dense, dim3(grid), dim3(kBlock), 0, ctx->stream,
-                         reinterpret_cast<const ulonglong2*>(recv), slot, P, total,
-                         reinterpret_cast<const unsigned long long*>(counts), ctx->cell_lo, k0, e0);
-      MG_TRY(hipGetLastError());
-    }
+    if (n && dispatch_w<LaunchXkeysDense>(ctx->maxw, ctx, reinterpret_cast<const uint64_t*>(recv), slot, total,
+                                          reinterpret_cast<const unsigned long long*>(counts), k0, e0))
+      return launch_fail(ctx, "key records launch failed");
   }
   if (n > 0x7FFFFFFFull) return set_err(ctx, "exchange: more than 2^31 key records on one rank");
   ctx->xkey_k = k0;
@@ -4912,6 +5055,7 @@ static int xchg_fused_probe(mg_ctx* ctx, bool contain) {
 
 int mg_xchg_probe(mg_ctx* ctx, int contain, const void* recv, uint64_t slot, uint32_t rounds, const uint64_t* counts) {
   if (!ctx) return -1;
+  ctx->err.clear();  // (a message left by an earlier failed call is not this call's cause)
   MG_TRY(hipSetDevice(ctx->device));
   if ((!ctx->xchg && !ctx->xchg_fused) || !ctx->index_ready) return set_err(ctx, "mg_xchg_insert_keys must run first");
   if (contain && !ctx->superkey) return set_err(ctx, "mg_begin_contained must run first (lengths differ)");
@@ -4943,7 +5087,7 @@ int mg_xchg_probe(mg_ctx* ctx, int contain, const void* recv, uint64_t slot, uin
     ctx->xmarks_done = false;
     ctx->xmarks = nullptr;
     if (nregions && dispatch_w<LaunchProbeSlots>(ctx->maxw, ctx, true, runs, reg, nregions))
-      return set_err(ctx, "probe launch failed");
+      return launch_fail(ctx, "probe launch failed");
     MG_TRY(hipEventRecord(ctx->ev[3], ctx->stream));
     return 0;
   }
@@ -4963,7 +5107,7 @@ int mg_xchg_probe(mg_ctx* ctx, int contain, const void* recv, uint64_t slot, uin
       return -1;
     if (live_runs_join(ctx, side)) return -1;
     if (nregions && dispatch_w<LaunchProbeSlots>(ctx->maxw, ctx, false, runs, reg, nregions))
-      return set_err(ctx, "probe launch failed");
+      return launch_fail(ctx, "probe launch failed");
     MG_TRY(hipEventRecord(ctx->ev[5], ctx->stream));
     if (!nregions) break;
     bool again = false;
@@ -4988,6 +5132,7 @@ int mg_xchg_probe(mg_ctx* ctx, int contain, const void* recv, uint64_t slot, uin
 
 int mg_xchg_prefix_marks(mg_ctx* ctx, void* marks) {
   if (!ctx) return -1;
+  ctx->err.clear();  // (a message left by an earlier failed call is not this call's cause)
   MG_TRY(hipSetDevice(ctx->device));
   if ((!ctx->xchg && !ctx->xchg_fused) || !ctx->index_ready) return set_err(ctx, "mg_xchg_insert_keys must run first");
   if (!ctx->superkey) return set_err(ctx, "mg_begin_contained must run first (lengths differ)");
@@ -5021,7 +5166,7 @@ int mg_begin_contained(mg_ctx* ctx, void* superkey, int* needed) {
     if (superkey) {
       ctx->superkey = reinterpret_cast<unsigned long long*>(superkey);
     } else {
-      MG_TRY(ensure(&ctx->d_superkey, &ctx->superkey_cap, ctx->n + 1));
+      MG_ENSURE(d_superkey, superkey_cap, ctx->n + 1);
       ctx->superkey = ctx->d_superkey;
     }
     MG_TRY(hipMemsetAsync(ctx->superkey, 0, ctx->n * sizeof(unsigned long long), ctx->stream));
@@ -5031,9 +5176,10 @@ int mg_begin_contained(mg_ctx* ctx, void* superkey, int* needed) {
 
 int mg_finalize_contained(mg_ctx* ctx, uint32_t* super_out) {
   if (!ctx) return -1;
+  ctx->err.clear();  // (a message left by an earlier failed call is not this call's cause)
   MG_TRY(hipSetDevice(ctx->device));
-  MG_TRY(ensure(&ctx->d_super, &ctx->super_cap, ctx->n + 1));
-  MG_TRY(ensure(&ctx->d_cbits, &ctx->cbits_cap, (ctx->n + 63) / 64 * 2));
+  MG_ENSURE(d_super, super_cap, ctx->n + 1);
+  MG_ENSURE(d_cbits, cbits_cap, (ctx->n + 63) / 64 * 2);
   if (!ctx->d_any) MG_TRY(hipMalloc(&ctx->d_any, sizeof(unsigned int)));
   ctx->super_any = false;
   if (ctx->minlen != ctx->maxlen && ctx->superkey) {
@@ -5071,6 +5217,7 @@ int mg_finalize_contained(mg_ctx* ctx, uint32_t* super_out) {
 
 int mg_copy_rows(mg_ctx* ctx, mg_edge* out, uint64_t cap, uint64_t* n_copied) {
   if (!ctx) return -1;
+  ctx->err.clear();  // (a message left by an earlier failed call is not this call's cause)
   MG_TRY(hipSetDevice(ctx->device));
   if (n_copied) *n_copied = 0;
   if (!ctx->nreg || !ctx->n_rows) return 0;
@@ -5084,7 +5231,7 @@ int mg_copy_rows(mg_ctx* ctx, mg_edge* out, uint64_t cap, uint64_t* n_copied) {
   MG_TRY(hipMalloc(&d_prefix, prefix.size() * sizeof(uint64_t)));
   MG_TRY(hipMemcpyAsync(d_prefix, prefix.data(), prefix.size() * sizeof(uint64_t), hipMemcpyHostToDevice,
                         ctx->stream));
-  MG_TRY(ensure(&ctx->d_compact, &ctx->compact_cap, total * 3));
+  MG_ENSURE(d_compact, compact_cap, total * 3);
   hipLaunchKernelGGL(k_compact_rows, dim3((uint32_t)ctx->nreg), dim3(kBlock), 0, ctx->stream, ctx->d_rows, reg_cap,
                      d_prefix, ctx->d_compact);
   MG_TRY(hipGetLastError());
@@ -5098,6 +5245,7 @@ int mg_copy_rows(mg_ctx* ctx, mg_edge* out, uint64_t cap, uint64_t* n_copied) {
 
 int mg_lookup_key(mg_ctx* ctx, const char* key, uint32_t key_len, uint64_t* out, uint64_t cap, uint64_t* n_out) {
   if (!ctx) return -1;
+  ctx->err.clear();  // (a message left by an earlier failed call is not this call's cause)
   MG_TRY(hipSetDevice(ctx->device));
   if (!ctx->index_ready) return set_err(ctx, "mg_build_index must run first");
   if (n_out) *n_out = 0;
@@ -5105,7 +5253,7 @@ int mg_lookup_key(mg_ctx* ctx, const char* key, uint32_t key_len, uint64_t* out,
   if (ctx->nranks > 1) return set_err(ctx, "lookup on a bucket-sharded index");
   if ((!ctx->index_o1 || !ctx->index_o3) && !long_mode(ctx) && !ctx->lookup_ready) {
     // the step's index has no o = 1 keys: file all four once into the lookup table
-    MG_TRY(ensure(&ctx->d_lkcells, &ctx->lkcells_cap, ctx->cell_n * kCell));
+    MG_ENSURE(d_lkcells, lkcells_cap, ctx->cell_n * kCell);
     MG_TRY(hipMemsetAsync(ctx->d_lkcells, 0xFF, ctx->cell_n * kCell * sizeof(uint64_t), ctx->stream));
     if (ctx->n && dispatch_w<LaunchIndex>(ctx->maxw, ctx, ctx->d_lkcells, true))
       return set_err(ctx, "lookup table build failed");

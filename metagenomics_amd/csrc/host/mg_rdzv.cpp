@@ -6,8 +6,12 @@
 // connects are non-blocking too, so an address that drops SYNs cannot hold a
 // rank past its deadline), and every descriptor is closed on every path (RAII).
 // A peer opens with a header (magic, its rank); rank 0 serves each rank 1..P-1
-// exactly once and drops any other connection (a port probe, a health check,
-// a duplicate), so a stray client cannot take a real rank's place.
+// exactly once and drops a connection that sends no header, a wrong magic,
+// rank 0, an out-of-range rank or a rank already served (a port probe, a
+// health check, a duplicate).  It does not authenticate: a client that sends
+// the magic and a rank not yet served is served as that rank, and the real
+// rank is then dropped and ends with -4 / -5 at its deadline.  The id only
+// names a communicator; the job is expected to run on one trusted node.
 #include <netdb.h>
 #include <poll.h>
 #include <sys/socket.h>

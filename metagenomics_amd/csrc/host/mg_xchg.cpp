@@ -6,7 +6,10 @@
 //   mg_begin_contained; [mg_xchg_prefix_marks; ncclAllReduce MAX (u8);
 //                        mg_xchg_probe(1); ncclAllReduce MAX]; mg_finalize_contained
 //                                                          markContainedReads
-//   mg_xchg_probe(0) -> mg_xchg_pack(ROWS) -> RCCL        insertAllEdgesOfRead
+//   mg_xchg_probe(0) [-> mg_xchg_pack(ROWS) -> RCCL]      insertAllEdgesOfRead
+// Keys and runs travel as 8-B records (mg_record_bytes); the rows move to
+// their src owners only with MG_XCHG_ROUTE_ROWS=1, else each rank keeps the
+// rows it verified (the union is the multiset).
 // Every library call and every collective is enqueued on the context's HIP
 // stream (mg_stream); the step reads the host only for the run and row counts
 // inside the library and once at its end (the MAX over ranks of the send
@@ -259,6 +262,9 @@ XchgStep::XchgStep(mg_ctx* ctx, Transport& x, uint32_t l, uint32_t k, uint64_t c
   check(mg_xchg_caps(ctx_, l_, k_, caps_), "mg_xchg_caps");
   const char* mk = std::getenv("MG_XCHG_MARKS");
   use_marks_ = mk && mk[0] == '1';  // (off by default: DESIGN.md §6a, measured)
+  const char* rr = std::getenv("MG_XCHG_ROUTE_ROWS");
+  route_rows_ = rr && rr[0] == '1' && x.world() > 1;  // (off by default: rows held where verified)
+  check(mg_set_option(ctx_, "xchg_route_rows", route_rows_ ? 1 : 0), "mg_set_option");
   hip_check(hipStreamCreateWithFlags(&s2_, hipStreamNonBlocking), "hipStreamCreate");
   hip_check(hipEventCreateWithFlags(&ev_packed_, hipEventDisableTiming), "hipEventCreate");
   hip_check(hipEventCreateWithFlags(&ev_runs_, hipEventDisableTiming), "hipEventCreate");
@@ -367,17 +373,19 @@ int XchgStep::run() {
       x_.allreduce_max_u64(reinterpret_cast<uint64_t*>(superkey_), n, s_);
     }
     check(mg_finalize_contained(ctx_, nullptr), "mg_finalize_contained");
-    // 5. insertAllEdgesOfRead: probe -> rows -> src owners
+    // 5. insertAllEdgesOfRead: probe -> rows [-> src owners]
     check(mg_xchg_probe(ctx_, 0, rs.recv, rs.slot, rs.rounds, rs.rcounts), "mg_xchg_probe");
-    route(MG_ROWS, s_);
+    const int nk = route_rows_ ? 3 : 2;  // the stream kinds that moved
+    if (route_rows_) route(MG_ROWS, s_);
     // the step's one host read: the MAX over ranks of every per-peer send count
-    std::vector<uint64_t> c(3 * P);
-    for (int kind = 0; kind < 3; ++kind)
+    std::vector<uint64_t> c(3 * P, 0);
+    for (int kind = 0; kind < nk; ++kind)
       hip_check(hipMemcpyAsync(c.data() + kind * P, st_[kind].counts, P * sizeof(uint64_t), hipMemcpyDeviceToHost, s_),
                 "counts D2H");
-    std::vector<uint64_t> rc(P);
-    hip_check(hipMemcpyAsync(rc.data(), st_[MG_ROWS].rcounts, P * sizeof(uint64_t), hipMemcpyDeviceToHost, s_),
-              "counts D2H");
+    std::vector<uint64_t> rc(P, 0);
+    if (route_rows_)
+      hip_check(hipMemcpyAsync(rc.data(), st_[MG_ROWS].rcounts, P * sizeof(uint64_t), hipMemcpyDeviceToHost, s_),
+                "counts D2H");
     hip_check(hipStreamSynchronize(s_), "hipStreamSynchronize");
     uint64_t mx[3] = {0, 0, 0};
     for (int kind = 0; kind < 3; ++kind)
@@ -391,19 +399,19 @@ int XchgStep::run() {
     // fit the capacities to what was sent (grow: rerun; shrink: less padding
     // on the links from the next step on), identically on every rank
     bool over = false;
-    for (int kind = 0; kind < 3; ++kind) {
+    for (int kind = 0; kind < nk; ++kind) {
       if (mx[kind] > caps_[kind]) over = true;
       caps_[kind] = mx[kind] + mx[kind] * 15 / 100 + 64;
     }
     rows_held_ = 0;
     for (int p = 0; p < P; ++p) rows_held_ += rc[p];
-    if (P == 1) rows_held_ = mg_num_rows(ctx_);  // (the rows stay in the context)
+    if (!route_rows_) rows_held_ = mg_num_rows(ctx_);  // (the rows stay in the context)
     if (!over) return reruns;
   }
 }
 
 void XchgStep::rows_digest(uint64_t out[4]) {
-  if (x_.world() == 1) {
+  if (!route_rows_) {
     check(mg_rows_digest(ctx_, nullptr, 0, out), "mg_rows_digest");
     return;
   }

@@ -138,14 +138,16 @@ class XchgStep {
   // scale the first capacity estimates (tests: a small factor forces a cut
   // stream and the rerun path); call before the first run()
   void scale_caps(double f);
-  // runs the step (rerun with grown capacities after an overflow); rows owned
-  // by this rank (by src ID) stay in the rows receive buffer.  Returns the
+  // runs the step (rerun with grown capacities after an overflow); the rows
+  // this rank verified stay in the context, or with MG_XCHG_ROUTE_ROWS=1 the
+  // rows it owns by src ID end in the rows receive buffer.  Returns the
   // number of reruns; throws std::runtime_error on a library error.
   int run();
   uint64_t rows_held() const { return rows_held_; }
   // digest (mg_rows_digest formula) of this rank's rows
   void rows_digest(uint64_t out[4]);
   bool contained() const { return contained_; }
+  bool rows_routed() const { return route_rows_; }
   const uint64_t* caps() const { return caps_; }
 
  private:
@@ -177,7 +179,8 @@ class XchgStep {
   uint64_t* maxbuf_ = nullptr;  // the three stream maxima, all-reduced
   uint8_t* marks_ = nullptr;     // cross-rank prefix marks (mg_xchg_prefix_marks), n_reads bytes
   size_t marks_n_ = 0;
-  bool use_marks_ = true;        // MG_XCHG_MARKS=0: off
+  bool use_marks_ = false;       // MG_XCHG_MARKS=1: on (off by default)
+  bool route_rows_ = false;      // MG_XCHG_ROUTE_ROWS=1 (P > 1): rows to their src owners (off by default)
   uint64_t rows_held_ = 0;
   bool contained_ = false;
 };

@@ -90,7 +90,7 @@ static void run_rank(mg::Transport& x, Dataset* ds, int device, const XchgOpts& 
   int reruns = 0;
   std::vector<double> ms;
   uint64_t mine[4] = {0, 0, 0, 0}, sup[4] = {0, 0, 0, 0}, held = 0;
-  bool contained = false;
+  bool contained = false, rows_routed = false;
   std::vector<uint64_t> caps(3, 0);
   {
     mg::XchgStep step(ctx, x, (uint32_t)o.l, (uint32_t)o.k);
@@ -131,6 +131,7 @@ static void run_rank(mg::Transport& x, Dataset* ds, int device, const XchgOpts& 
       contained = step.contained();
       held = step.rows_held();
       for (int kind = 0; kind < 3; ++kind) caps[kind] = step.caps()[kind];
+      rows_routed = step.rows_routed();
     }
     if (contained) ok(mg_super_digest(ctx, sup), "mg_super_digest");
   }
@@ -164,13 +165,13 @@ static void run_rank(mg::Transport& x, Dataset* ds, int device, const XchgOpts& 
         "{\"mode\": \"%s\", \"world\": %d, \"unique_reads\": %llu, \"rows\": {\"n\": %llu, \"sum\": %llu, "
         "\"xor\": %llu, \"sum2\": %llu}, \"super\": {\"n\": %llu, \"sum\": %llu, \"xor\": %llu, \"sum2\": %llu}, "
         "\"contained\": %s, \"steps\": %d, \"best_ms\": %.3f, \"median_ms\": %.3f, \"reruns\": %d, "
-        "\"rows_rank0\": %llu, \"rows_held\": [%s], \"caps\": [%llu, %llu, %llu]}\n",
+        "\"rows_rank0\": %llu, \"rows_held\": [%s], \"caps\": [%llu, %llu, %llu], \"rows_routed\": %s}\n",
         replicated ? "replicated" : "xchg", world, (unsigned long long)n, (unsigned long long)dg[0],
         (unsigned long long)dg[1], (unsigned long long)dg[2], (unsigned long long)dg[3],
         (unsigned long long)sup[0], (unsigned long long)sup[1], (unsigned long long)sup[2],
         (unsigned long long)sup[3], contained ? "true" : "false", o.steps, best, med, reruns,
         (unsigned long long)held, held_list.c_str(), (unsigned long long)caps[0], (unsigned long long)caps[1],
-        (unsigned long long)caps[2]);
+        (unsigned long long)caps[2], rows_routed ? "true" : "false");
     std::fflush(stdout);
   }
 }

@@ -17,9 +17,9 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MG_LIB") or os.path.join(_HERE, "lib", "libmgovl.so")  # MG_LIB: A/B builds (tools/)
 
-# exchange-mode record kinds (include/mg_overlap.h)
+# exchange-mode record kinds (include/mg_overlap.h); their sizes on the wire
+# come from the library (mg_record_bytes: keys and runs 8 B, rows 12 B)
 MG_KEYS, MG_RUNS, MG_ROWS = 0, 1, 2
-RECORD_BYTES = {MG_KEYS: 16, MG_RUNS: 16, MG_ROWS: 12}
 
 EDGE_DTYPE = np.dtype([("src", "<u4"), ("dst", "<u4"), ("offset", "<u2"), ("orient", "u1"), ("flags", "u1")])
 
@@ -429,6 +429,11 @@ class OverlapEngine:
         c = np.zeros(3, dtype=np.uint64)
         self._check(lib().mg_xchg_caps(self._h, min_overlap, seed_k, _ptr(c)), "xchg_caps")
         return c
+
+    @staticmethod
+    def record_bytes(what: int) -> int:
+        """Bytes per exchange record of kind what (mg_record_bytes)."""
+        return int(lib().mg_record_bytes(what))
 
     def xchg_begin(self, min_overlap: int, seed_k: int = 0):
         self._check(lib().mg_xchg_begin(self._h, min_overlap, seed_k), "xchg_begin")

@@ -16,7 +16,14 @@ One step (``sharded_step``):
    containment probe of the received runs, all-reduce MAX of the per-read containment keys
    (``markContainedReads``, OverlapGraph.cpp:225-290);
 5. discovery probe + verify of the received runs (``insertAllEdgesOfRead``, OverlapGraph.cpp:529-565)
-   -> rows (+ twins, ``insertEdge`` :407-419) -> src owners.
+   -> rows (+ twins, ``insertEdge`` :407-419), held by the rank that verified them (the union over
+   ranks is the reference multiset); with ``route_rows`` they then go to their src owners, so each
+   rank ends with graph[u] of its own source reads.
+
+Record sizes on the wire (``engine.record_bytes``, mg_record_bytes): a key is its 8-B index entry
+and a run its 8-B meta (read slot, minimizer position, window range); the receiver re-hashes the
+minimizer m-mer from its own copy of the read (every rank holds all reads), so bucket and
+fingerprint never travel.  Rows are 12-B mg_edge records.
 
 Records travel in the library's SLOT LAYOUT (include/mg_overlap.h "exchange mode"): per peer a
 fixed-capacity stream of ``rounds * slot`` records, round t of all peers contiguous, so every round
@@ -41,7 +48,7 @@ from dataclasses import dataclass, field
 
 import numpy as np
 
-from .overlap import EDGE_DTYPE, MG_KEYS, MG_ROWS, MG_RUNS, RECORD_BYTES
+from .overlap import EDGE_DTYPE, MG_KEYS, MG_ROWS, MG_RUNS
 
 SLOT_ALIGN = 64  # slots are whole multiples of this many records (the probe tiles a slot by its divisors)
 BIG_SLOT_ALIGN = 1024
@@ -73,8 +80,8 @@ class XchgPlan:
     caps: dict = field(default_factory=dict)
     reruns: int = 0
 
-    def geometry(self, kind: int, world: int, chunk_bytes: int):
-        return slot_geometry(self.caps[kind], world, RECORD_BYTES[kind], chunk_bytes)
+    def geometry(self, kind: int, world: int, chunk_bytes: int, rec_bytes: int):
+        return slot_geometry(self.caps[kind], world, rec_bytes, chunk_bytes)
 
     def grow(self, used: dict) -> bool:
         """Fit the capacities to the counts seen (MAX over ranks and peers, identical on every
@@ -265,7 +272,7 @@ class LocalExchange(Exchange):
 
 @dataclass
 class ShardResult:
-    rows: list            # per local rank: (uint8 slot buffer, counts tensor, slot, rounds): rows it owns by src
+    rows: list            # route_rows: per local rank (uint8 slot buffer, counts tensor, slot, rounds): rows it owns by src
     ms: dict = field(default_factory=dict)
     contained: bool = False
     super_read_id: np.ndarray | None = None  # superReadID per ID (index 0 unused), if requested
@@ -280,6 +287,8 @@ class ShardResult:
     # one rank: nothing is routed, the rows stay in the engine (mg_xchg_pack at P = 1)
     engine_rows: list | None = None
     mode: str = "exchange"
+    rows_routed: bool = False  # rows moved to their src owners (route_rows) or held where verified
+    rec_bytes: dict = field(default_factory=dict)  # kind -> bytes per record on the wire
 
     @property
     def rows_in_slots(self) -> bool:
@@ -299,7 +308,7 @@ class ShardResult:
                         moved += slot * rounds
                         sent += int(v[p])
             out[{MG_KEYS: "keys", MG_RUNS: "runs", MG_ROWS: "rows"}[kind]] = {
-                "moved_records": moved, "sent_records": sent,
+                "moved_records": moved, "sent_records": sent, "record_bytes": self.rec_bytes.get(kind),
                 "padding_frac": (1.0 - sent / moved) if moved else 0.0}
         return out
 
@@ -333,18 +342,29 @@ def initial_plan(engine, world: int, min_overlap: int, seed_k: int) -> XchgPlan:
     return XchgPlan(caps={MG_KEYS: int(caps[0]), MG_RUNS: int(caps[1]), MG_ROWS: int(caps[2])})
 
 
+def route_rows_default() -> bool:
+    """MG_XCHG_ROUTE_ROWS=1: route the rows to their src owners (default: held where verified)."""
+    return os.environ.get("MG_XCHG_ROUTE_ROWS", "0") == "1"
+
+
 def sharded_step(engines: list, xchg: Exchange, min_overlap: int, seed_k: int = 0,
-                 want_super: bool = False, plan: XchgPlan | None = None) -> ShardResult:
+                 want_super: bool = False, plan: XchgPlan | None = None,
+                 route_rows: bool | None = None) -> ShardResult:
     """One exchange-mode step over the local ranks' engines (set up with
     ``set_shard(rank, world)`` and the full read set uploaded).  ``plan`` carries the
-    stream capacities from step to step (grown in place after an overflow)."""
+    stream capacities from step to step (grown in place after an overflow).
+    ``route_rows``: every row goes to the owner of its src (graph[u] by source range,
+    one more all-to-all); else (default) each rank keeps the rows it verified, and the
+    union over the ranks is the reference multiset all the same."""
+    if route_rows is None:
+        route_rows = route_rows_default()
     if any(e.max_len > EXCHANGE_MAX_BP for e in engines):
         return _replicated_step(engines, xchg, min_overlap, seed_k, want_super)
     if plan is None:
         plan = initial_plan(engines[0], xchg.world, min_overlap, seed_k)
     reruns = 0
     while True:
-        res, used = _step(engines, xchg, min_overlap, seed_k, want_super, plan)
+        res, used = _step(engines, xchg, min_overlap, seed_k, want_super, plan, route_rows)
         if not plan.grow(used):
             res.reruns = reruns
             res.plan = plan
@@ -403,8 +423,13 @@ def _replicated_step(engines, xchg, min_overlap, seed_k, want_super):
                        n_rows=n_rows, host_rows=host_rows, mode="replicated")
 
 
-def _step(engines, xchg, min_overlap, seed_k, want_super, plan):
+def _step(engines, xchg, min_overlap, seed_k, want_super, plan, route_rows):
     P = xchg.world
+    route_rows = route_rows and P > 1
+    kinds = KINDS if route_rows else (MG_KEYS, MG_RUNS)
+    for e in engines:  # the discovery probe counts rows per src owner only when they will move
+        e.set_option("xchg_route_rows", int(route_rows))
+    rec_bytes = {k: int(engines[0].record_bytes(k)) for k in KINDS}
     # cross-rank prefix marks (mg_xchg_prefix_marks): off by default -- at C5,
     # P = 8 the containment probe gained 0.14 ms per rank and the marks cost 0.21 ms plus a
     # 50 MB all-reduce; MG_XCHG_MARKS=1 turns them on
@@ -430,8 +455,8 @@ def _step(engines, xchg, min_overlap, seed_k, want_super, plan):
             sent[kind] = cnts
             geo[kind] = (0, 0)
             return [(None, c) for c in cnts], 0, 0
-        slot, rounds = plan.geometry(kind, P, ch)
-        rb = RECORD_BYTES[kind]
+        rb = rec_bytes[kind]
+        slot, rounds = plan.geometry(kind, P, ch, rb)
         sends, recvs, cnts = [], [], []
         for e in engines:
             recv = xchg.empty(rounds * P * slot * rb)
@@ -499,16 +524,18 @@ def _step(engines, xchg, min_overlap, seed_k, want_super, plan):
         for e, (buf, c) in zip(engines, runs):
             e.xchg_probe(False, buf.data_ptr() if buf is not None else 0, rs, rr, c.data_ptr())
             done()
-        rows, ws, wr = route(MG_ROWS)
+        if route_rows:
+            rows, ws, wr = route(MG_ROWS)
         # the step's one host read: MAX over ranks of every per-peer send count
-        mx = xchg.max_counts([[sent[k][i] for k in KINDS] for i in range(len(engines))])
-        n_rows = [e.num_rows() for e in engines] if P == 1 else [int(c.sum().item()) for _, c in rows]
+        mx = xchg.max_counts([[sent[k][i] for k in kinds] for i in range(len(engines))])
+        n_rows = [int(c.sum().item()) for _, c in rows] if route_rows else [e.num_rows() for e in engines]
         # (the key and run buffers stay referenced until here: with LocalExchange the
         # engines' streams may still read them when a del would let torch reuse the memory)
         del keys, runs
     ms["overlap"] = (time.perf_counter() - t2) * 1e3
-    used = {k: int(v) for k, v in zip(KINDS, mx)}
-    res = ShardResult(rows=[(b, c, ws, wr) for b, c in rows], ms=ms, contained=contained, super_read_id=sup,
-                      n_rows=n_rows, streams={k: geo[k] + (sent[k],) for k in KINDS},
-                      engine_rows=list(engines) if P == 1 else None)
+    used = {k: int(v) for k, v in zip(kinds, mx)}
+    res = ShardResult(rows=[(b, c, ws, wr) for b, c in rows] if route_rows else [], ms=ms, contained=contained,
+                      super_read_id=sup, n_rows=n_rows, streams={k: geo[k] + (sent[k],) for k in kinds},
+                      engine_rows=None if route_rows else list(engines), rows_routed=route_rows,
+                      rec_bytes=rec_bytes)
     return res, used

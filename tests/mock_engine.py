@@ -74,7 +74,7 @@ class MockEngine:
     def __init__(self, rank: int, world: int, rows: np.ndarray, n_reads: int, lengths_differ: bool = True,
                  caps=(64, 64, 64)):
         self.rank, self.world = rank, world
-        self.rows = rows  # the full directed multiset (EDGE_DTYPE)
+        self.all_rows = rows  # the full directed multiset (EDGE_DTYPE)
         self.n_reads = n_reads
         self.lengths_differ = lengths_differ
         self.max_len = 150  # (reads <= 1024 bp: the exchange path, not the long-read fallback)
@@ -86,6 +86,20 @@ class MockEngine:
         self.begins = 0
         self.marks_ptr = 0
         self.marks_seen = False
+
+    @staticmethod
+    def record_bytes(what):
+        return REC_DTYPE.itemsize if what in (MG_KEYS, MG_RUNS) else EDGE_DTYPE.itemsize
+
+    def set_option(self, name, value):
+        self.options = getattr(self, "options", {})
+        self.options[name] = value
+
+    def num_rows(self):
+        return 0 if self.out_rows is None else len(self.out_rows)
+
+    def rows(self, n=None):
+        return self.out_rows[: (len(self.out_rows) if n is None else n)].copy()
 
     def xchg_caps(self, min_overlap, seed_k=0):
         return np.array(self.caps, dtype=np.uint64)
@@ -152,8 +166,8 @@ class MockEngine:
             ctypes.memmove(self.sk_ptr, sk.tobytes(), sk.nbytes)
             return
         # every row is "discovered" by the rank that probed min(src, dst)'s run
-        mine = np.isin(np.minimum(self.rows["src"], self.rows["dst"]).astype(np.int64) - 1, a)
-        self.out_rows = self.rows[mine]
+        mine = np.isin(np.minimum(self.all_rows["src"], self.all_rows["dst"]).astype(np.int64) - 1, a)
+        self.out_rows = self.all_rows[mine]
 
     def finalize_contained(self, copy=False):
         if self.sk_ptr:

@@ -312,7 +312,7 @@ def test_repeatable(engine):
 
 # ---- exchange mode: P simulated ranks in this process, buffers
 # moved by LocalExchange on the device; the same sharded_step drives RCCL ranks
-def exchange_rows(ds, l, world, k=0, want_super=True, opts=None):
+def exchange_rows(ds, l, world, k=0, want_super=True, opts=None, route_rows=False):
     import torch
 
     from metagenomics_amd.sharded import LocalExchange, sharded_step, source_range
@@ -325,25 +325,32 @@ def exchange_rows(ds, l, world, k=0, want_super=True, opts=None):
         e.set_shard(r, world, 0, 0)
         e.upload(ds)
         engines.append(e)
-    res = sharded_step(engines, LocalExchange(world, torch.device("cuda:0")), l, k, want_super=want_super)
+    res = sharded_step(engines, LocalExchange(world, torch.device("cuda:0")), l, k, want_super=want_super,
+                       route_rows=route_rows)
     exchange_rows.counters = [e.counters() for e in engines]
     parts = []
     for r in range(world):
         rows = res.rows_numpy(r)
-        lo, hi = source_range(ds.num_unique, r, world)
-        assert np.all((rows["src"] >= lo + 1) & (rows["src"] <= hi)), "row at a rank that does not own its src"
+        if route_rows:
+            lo, hi = source_range(ds.num_unique, r, world)
+            assert np.all((rows["src"] >= lo + 1) & (rows["src"] <= hi)), "row at a rank that does not own its src"
         parts.append(rows)
     for e in engines:
         e.close()
     return np.concatenate(parts), res.super_read_id
 
 
-@pytest.mark.parametrize("name,world", [("small", 2), ("mixed", 3), ("tandem", 4), ("dirty", 3), ("tworead", 2),
-                                        ("wrapped", 5), ("mixed", 1), ("highdup", 1)])
-def test_exchange_mode_matches_reference(name, world):
+@pytest.mark.parametrize("name,world,route", [("small", 2, 0), ("mixed", 3, 0), ("tandem", 4, 0), ("dirty", 3, 0),
+                                              ("tworead", 2, 0), ("wrapped", 5, 0), ("mixed", 1, 0),
+                                              ("highdup", 1, 0), ("small", 2, 1), ("mixed", 3, 1), ("tandem", 4, 1),
+                                              ("highdup", 3, 1)])
+def test_exchange_mode_matches_reference(name, world, route):
+    """Keys and runs travel as 8-B records (the receiver re-hashes the minimizer
+    from its copy of the read); route = 1: the rows then go to their src owners
+    (each rank ends with graph[u] of its sources), else each keeps what it verified."""
     meta = load_meta(name)
     ds = Dataset.from_files([fixture_input(name)], meta["l"])
-    rows, sup = exchange_rows(ds, meta["l"], world)
+    rows, sup = exchange_rows(ds, meta["l"], world, route_rows=bool(route))
     assert np.array_equal(rows_to_tuples(rows), golden_rows(name))
     assert {str(i): int(s) for i, s in enumerate(sup) if s} == meta["super"]
 
@@ -458,7 +465,7 @@ def test_exchange_mode_cut_streams_rerun():
     xchg = LocalExchange(3, torch.device("cuda:0"), chunk_bytes=3 * 16 * 128)
     plan = XchgPlan(caps={MG_KEYS: 64, MG_RUNS: 64, MG_ROWS: 64})
     for attempt in range(2):
-        res = sharded_step(engines, xchg, meta["l"], 0, want_super=True, plan=plan)
+        res = sharded_step(engines, xchg, meta["l"], 0, want_super=True, plan=plan, route_rows=True)
         assert (res.reruns >= 1) if attempt == 0 else (res.reruns == 0)
         rows = np.concatenate([res.rows_numpy(r) for r in range(3)])
         assert np.array_equal(rows_to_tuples(rows), golden_rows("mixed"))
@@ -944,3 +951,32 @@ def test_explore_through_per_read_methods(tmp_path, name):
         assert [x for x in lines[1:] if x] == [x for x in f.read().split("\n") if x]
     with gzip.open(os.path.join(GOLDEN, meta["unitig"]["file"]), "rt") as f:
         assert open(prefix + ".unitig").read() == f.read()
+
+
+@pytest.mark.parametrize("name,cap", [("small", 1 << 16), ("mixed", 1 << 20)])
+def test_allocation_failure_names_its_cause(name, cap):
+    """A failed device allocation surfaces with the buffer's name, the bytes asked
+    for and the HIP error (option alloc_cap forces one), not as a generic
+    "launch failed"; the context then works again once the cap is lifted."""
+    from metagenomics_amd.overlap import MgError
+
+    meta = load_meta(name)
+    ds = Dataset.from_files([fixture_input(name)], meta["l"])
+    e = OverlapEngine(0)
+    try:
+        e.upload(ds)
+        e.set_option("alloc_cap", cap)
+        with pytest.raises(MgError) as exc:
+            e.build_index(meta["l"])
+            e.mark_contained()
+            e.find_overlaps()
+        msg = str(exc.value)
+        assert "device allocation of " in msg and " B) failed: " in msg and "alloc_cap" in msg, msg
+        assert "memory" in msg.lower(), msg
+        e.set_option("alloc_cap", 0)
+        e.build_index(meta["l"])
+        e.mark_contained()
+        t = rows_to_tuples(e.rows(e.find_overlaps()))
+        assert np.array_equal(t, golden_rows(name))
+    finally:
+        e.close()

@@ -177,8 +177,8 @@ def combine(ds):
 
 @pytest.mark.gpu
 @pytest.mark.timeout(900)
-@pytest.mark.parametrize("name,world", [("c3", 8), ("c5s", 8), ("c5", 8)])
-def test_exchange_scale_digest(name, world):
+@pytest.mark.parametrize("name,world,route", [("c3", 8, False), ("c5s", 8, True), ("c5", 8, False)])
+def test_exchange_scale_digest(name, world, route):
     """The multi-GPU exchange mode (bucket-range index shards,
     key / run / row all-to-alls, MAX all-reduce of the containment keys) with
     `world` simulated ranks on this GPU (LocalExchange moves the slot buffers):
@@ -186,7 +186,9 @@ def test_exchange_scale_digest(name, world):
     C5-shaped set, and BASELINE configs[4] itself (50M mixed reads, 8 ranks:
     the 8 contexts share the one 288 GB device, so each frees its layout's
     double buffers); the union of the ranks' rows has the reference's digest
-    (c5: the pinned oracle's, tests/golden/c5s_oracle_check.json)."""
+    (c5: the pinned oracle's, tests/golden/c5s_oracle_check.json).  route: the
+    rows also move to their src owners (c5s); else each rank keeps the rows it
+    verified (the default)."""
     import torch
 
     from metagenomics_amd.overlap import OverlapEngine
@@ -204,12 +206,17 @@ def test_exchange_scale_digest(name, world):
             e.upload(ds)
             engines.append(e)
         del ds  # (the host Dataset: 50M reads at c5)
-        res = sharded_step(engines, LocalExchange(world, torch.device("cuda:0")), m["workload"]["min_overlap"], 31)
-        rd = combine([e.slots_digest(b.data_ptr(), slot, rounds, c.data_ptr())
-                      for e, (b, c, slot, rounds) in zip(engines, res.rows)])
+        res = sharded_step(engines, LocalExchange(world, torch.device("cuda:0")), m["workload"]["min_overlap"], 31,
+                           route_rows=route)
+        assert res.rows_routed == route
+        if route:
+            rd = combine([e.slots_digest(b.data_ptr(), slot, rounds, c.data_ptr())
+                          for e, (b, c, slot, rounds) in zip(engines, res.rows)])
+        else:
+            rd = combine([e.rows_digest() for e in engines])
         assert rd == m["rows"]
         assert engines[0].super_digest() == m["super"]
-        # each rank holds the rows of the sources it owns (by reference ID)
+        # each rank holds rows (with route: those of the sources it owns, by reference ID)
         for r in range(world):
             assert res.n_rows[r] > 0
             lo, hi = source_range(m["n_unique"], r, world)

@@ -28,7 +28,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, name, outdir, chunk):
+def _worker(rank, world, port, name, outdir, chunk, route):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
     if chunk:
         os.environ["MG_A2A_CHUNK_BYTES"] = str(chunk)  # force the multi-round exchange
@@ -48,11 +48,13 @@ def _worker(rank, world, port, name, outdir, chunk):
     rows["src"], rows["dst"], rows["orient"], rows["offset"] = g[:, 0], g[:, 1], g[:, 2], g[:, 3]
     n = lm(name)["n_unique"]
     eng = MockEngine(rank, world, rows, n)
-    res = sharded_step([eng], TorchExchange(), lm(name)["l"], 0)
+    res = sharded_step([eng], TorchExchange(), lm(name)["l"], 0, route_rows=route)
     mine = res.rows_numpy(0)
     assert res.n_rows == [len(mine)]
+    assert res.rows_routed == route
     pad = res.padding(world, [rank])  # bench.py's exchange_padding
-    assert set(pad) == {"keys", "runs", "rows"}
+    assert set(pad) == ({"keys", "runs", "rows"} if route else {"keys", "runs"})
+    assert eng.options["xchg_route_rows"] == int(route)
     for v in pad.values():
         assert 0 <= v["sent_records"] <= v["moved_records"] and 0.0 <= v["padding_frac"] <= 1.0
     np.save(os.path.join(outdir, f"reruns{rank}.npy"), np.array([res.reruns, eng.begins]))
@@ -64,18 +66,23 @@ def _worker(rank, world, port, name, outdir, chunk):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("name,world,chunk", [("small", 2, 0), ("tandem", 3, 0), ("mixed", 2, 0),
-                                              ("small", 2, 4096), ("tandem", 3, 8192)])
-def test_exchange_routes_every_record(tmp_path, name, world, chunk):
+@pytest.mark.parametrize("name,world,chunk,route", [("small", 2, 0, True), ("tandem", 3, 0, True),
+                                                    ("mixed", 2, 0, True), ("small", 2, 4096, True),
+                                                    ("tandem", 3, 8192, True), ("small", 2, 0, False),
+                                                    ("mixed", 3, 4096, False)])
+def test_exchange_routes_every_record(tmp_path, name, world, chunk, route):
+    """route: rows to their src owners (MG_XCHG_ROUTE_ROWS=1); else each rank keeps the
+    rows it verified and only keys and runs travel (the default)."""
     from mock_engine import expected_super_keys, src_owner
 
-    mp.spawn(_worker, args=(world, _free_port(), name, str(tmp_path), chunk), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), name, str(tmp_path), chunk, route), nprocs=world, join=True)
     meta = load_meta(name)
     n = meta["n_unique"]
     parts, keys = [], 0
     for r in range(world):
         rows = np.load(tmp_path / f"rows{r}.npy")
-        assert np.all(src_owner(rows["src"], n, world) == r), "row at a rank that does not own its src"
+        if route:
+            assert np.all(src_owner(rows["src"], n, world) == r), "row at a rank that does not own its src"
         parts.append(rows)
         keys += np.load(tmp_path / f"keys{r}.npy").shape[0]
         assert np.array_equal(np.load(tmp_path / f"sk{r}.npy"), expected_super_keys(n))

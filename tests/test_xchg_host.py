@@ -152,3 +152,19 @@ def test_xchg_host_prefix_marks(name, world):
     g = golden_rows(name)
     assert r["rows"] == digest.rows_digest(g[:, 0], g[:, 1], g[:, 2], g[:, 3])
     assert r["super"] == golden_super_digest(meta)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,world", [("mixed", 3), ("highdup", 4), ("tandem", 2)])
+def test_xchg_host_route_rows(name, world):
+    """MG_XCHG_ROUTE_ROWS=1: after the discovery probe the rows travel to the
+    owners of their src IDs (mg_xchg_pack(MG_ROWS) + the slot all-to-all), so
+    each rank holds graph[u] of its own source reads; same union as the default
+    (rows held where they were verified)."""
+    meta = load_meta(name)
+    r = run_cli(fixture_input(name), meta["l"], world, env={"MG_XCHG_ROUTE_ROWS": "1"})
+    g = golden_rows(name)
+    assert r["rows_routed"] is True
+    assert r["rows"] == digest.rows_digest(g[:, 0], g[:, 1], g[:, 2], g[:, 3])
+    assert r["super"] == golden_super_digest(meta)
+    assert sum(r["rows_held"]) == g.shape[0]

@@ -8,7 +8,13 @@ per launch: FETCH_SIZE and WRITE_SIZE are in KiB (rocprofv3 derived metrics);
 on gfx950 FETCH_SIZE counts 64 B per TCC_EA0_RDREQ, which reads exactly half the
 bytes of 128-B streaming requests (MI355X_MICROARCH.md §HBM), so both the raw
 and the x2-corrected read figures are recorded.
+
+Provenance: the summary records the sha256 (first 16 hex digits) of the native
+library the counters were captured with (MG_LIB, else the in-tree
+metagenomics_amd/lib/libmgovl.so, which is what the profiled bench loaded), so
+bench.py can refuse to quote traffic measured on another build.
 """
+import hashlib
 import csv
 import glob
 import json
@@ -20,6 +26,17 @@ from collections import defaultdict
 def short(name):
     n = name.replace("void ", "").replace("(anonymous namespace)::", "")
     return n.split("(")[0].strip()
+
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def library_provenance():
+    path = os.environ.get("MG_LIB") or os.path.join(ROOT, "metagenomics_amd", "lib", "libmgovl.so")
+    if not os.path.exists(path):
+        return None
+    with open(path, "rb") as f:
+        return {"path": os.path.relpath(path, ROOT), "sha256_16": hashlib.sha256(f.read()).hexdigest()[:16]}
 
 
 def main():
@@ -44,7 +61,7 @@ def main():
                 per[disp] += v  # sum over dimensions (XCD/SE instances) per dispatch
             res[k][c] = sum(per.values()) / max(1, len(per))
             disp_n[k] = max(disp_n.get(k, 0), len(per))
-    summary = {"kernels": res}
+    summary = {"kernels": res, "library": library_provenance()}
     per_kernel = {}
     for k, cs in res.items():
         fetch, write = cs.get("FETCH_SIZE"), cs.get("WRITE_SIZE")
