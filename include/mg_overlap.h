@@ -219,6 +219,13 @@ int mg_xchg_caps(mg_ctx* ctx, uint32_t min_overlap, uint32_t seed_k, uint64_t* c
  * containment probe reads it) and the windows' minimizer runs
  * (OverlapGraph.cpp:534-537), in the scan's order. */
 int mg_xchg_begin(mg_ctx* ctx, uint32_t min_overlap, uint32_t seed_k);
+/* 1 when the current exchange build is KEYS FIRST (option xchg_keys_first,
+ * default: several ranks and reads of one length): mg_xchg_begin then made the
+ * key records only, and the window scan runs inside mg_xchg_insert_keys, which
+ * CAS-inserts the received key records as it goes (k_scan<RECV>: no sort, no
+ * separate cell build); MG_RUNS can be packed only after mg_xchg_insert_keys.
+ * 0: one scan in mg_xchg_begin made keys and runs (MG_RUNS packable at once). */
+int mg_xchg_keys_first(const mg_ctx* ctx);
 /* Route what = MG_KEYS / MG_RUNS (after mg_xchg_begin) or MG_ROWS (after
  * mg_xchg_probe(0)) into dst in the slot layout; counts = P device uint64.
  * With one rank (P = 1) every stream is the rank's own: nothing is copied and
@@ -245,6 +252,15 @@ int mg_xchg_insert_keys(mg_ctx* ctx, const void* recv, uint64_t slot, uint32_t r
  * the library's scratch until the step ends.  (Option xchg_sort_runs = 1: the
  * first call orders them by bucket into the context's own array instead.) */
 int mg_xchg_probe(mg_ctx* ctx, int contain, const void* recv, uint64_t slot, uint32_t rounds, const uint64_t* counts);
+/* Optional, after mg_finalize_contained and before mg_xchg_probe(0): the
+ * discovery probe of this rank's OWN run stream, which mg_xchg_pack(MG_RUNS)
+ * wrote straight into recv (send_counts = that pack's counts; only this
+ * rank's entry is read), so it runs while the peers' streams are still on the
+ * links; mg_xchg_probe(0) then probes the peers' streams and appends its rows.
+ * Same rows as one mg_xchg_probe(0).  A no-op (everything is left to
+ * mg_xchg_probe(0)) with one rank, mixed lengths (the containment probe needs
+ * every stream first) or option xchg_sort_runs. */
+int mg_xchg_probe_own(mg_ctx* ctx, const void* recv, uint64_t slot, uint32_t rounds, const uint64_t* send_counts);
 /* Containment: *needed = 1 when read lengths differ (OverlapGraph.cpp:228-233).
  * superkey = caller-owned device array of n_reads u64 (NULL: context-owned),
  * cleared here; the contain probe atomicMax-es (len << 32 | ~index) into it,
@@ -308,6 +324,15 @@ int mg_get_counters(const mg_ctx* ctx, mg_counters* c);
  *                   of a mixed-length set holds the o = 0 / 2 keys only;
  *  "xchg_sort_runs" exchange mode: order the received runs by bucket before
  *                   the probes (default 0: probed in place, arrival order);
+ *  "xchg_keys_first" exchange mode, one read length, P > 1: key records first,
+ *                   filed by CAS inside the receiver's window scan (default 1;
+ *                   0: one scan makes keys and runs, the receiver sorts the keys);
+ *  "xchg_scan_lds"  exchange mode, one read length: k_scan's LDS sliding minimum
+ *                   (default 1) instead of the register scan;
+ *  "xchg_split_max" mg_xchg_probe_own splits the discovery probe up to this many
+ *                   ranks (default 4);
+ *  "xchg_region"    records per probe region of the received runs (power of two,
+ *                   default 512);
  *  "xchg_route_rows" exchange mode: the discovery probe counts its rows per src
  *                   owner for mg_xchg_pack(MG_ROWS) (default 1); 0 when the
  *                   host keeps the rows where they were verified;

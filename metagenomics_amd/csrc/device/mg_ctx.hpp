@@ -176,7 +176,9 @@ struct mg_ctx {
   bool xchg_route_rows = true;
   // option "xchg_scan_lds": the exchange scan of equal lengths takes k_scan<KEYREC>
   // (LDS sliding minimum, all four keys in one pass) instead of k_scan_reg + k_rc_keys
-  bool xchg_scan_lds = false;
+  bool xchg_scan_lds = true;
+  uint32_t xchg_region = 512;  // option "xchg_region": records per probe region of the received runs (0: 1,024)
+  uint32_t xchg_split_max = 4;  // option "xchg_split_max": mg_xchg_probe_own splits the probe at up to this many ranks
   int packable = 0;                      // 1 << MG_KEYS | 1 << MG_RUNS | 1 << MG_ROWS
   unsigned long long* d_flat_cnt = nullptr;  // per-region counts of the received runs (probe input)
   size_t flat_cnt_cap = 0;
@@ -216,6 +218,19 @@ struct mg_ctx {
   size_t xsort_tmp_cap = 0;
   int xv_sel = 0;
   uint64_t xruns_n = 0;
+  bool own_probed = false;
+  // exchange mode, keys first (option xchg_keys_first, equal lengths, P > 1):
+  // mg_xchg_begin computes the key records only (k_xchg_keys); the window scan
+  // runs in mg_xchg_insert_keys and CAS-inserts the received key records
+  // (rk_*: slot layout) as it goes (k_scan<RECV>, rk_on during that launch)
+  bool xchg_keys_first = true;
+  bool keys_first = false;  // the current exchange build is a keys-first one
+  bool rk_on = false;
+  const uint64_t* rk_keys = nullptr;
+  const unsigned long long* rk_cnt = nullptr;
+  uint64_t rk_slot = 0, rk_total = 0;
+  int xruns_part = 0;       // the probe regions prepared: 0 all, 1 own stream, 2 the peers' (split probe)
+  uint64_t xruns_K = 0;     // probe regions per peer slot and round  // mg_xchg_probe_own probed this rank's own stream; mg_xchg_probe(0) appends the peers
   // the received runs expanded to 16-B probe records (k_xruns_expand), slot layout
   ulonglong2* d_xexp = nullptr;
   size_t xexp_cap = 0;

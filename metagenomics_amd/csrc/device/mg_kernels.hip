@@ -527,72 +527,90 @@ __device__ __forceinline__ uint64_t entry_hash(const uint64_t* __restrict__ word
   return mix64(o < 2 ? x >> (64 - 2 * m) : rc_word(x) & mmask);
 }
 
-// the received key records (8-B entries in the slot layout) -> dense (local
-// home cell, entry) pairs for the sort, the home cell recomputed from the read
+// The received records in the slot layout are walked one peer slot of one
+// round at a time: blockIdx.y = t P + s (round t, sender s), blockIdx.x tiles
+// the slot, so a record's stream index j = t slot + x needs no division (the
+// 64-bit divides of a flat index cost more than the records' own work).
+
+// the received key records (8-B entries) -> dense (local home cell, entry)
+// pairs for the sort, the home cell recomputed from the read: sender s's
+// records go to [sum over s' < s of its received count, ...) in stream order
 template <int MAXW>
 __global__ __launch_bounds__(kBlock) void k_xkeys_dense(const uint64_t* __restrict__ recv, uint64_t slot,
-                                                       uint32_t nranks, uint64_t total,
+                                                       uint32_t nranks, uint64_t lim,
                                                        const unsigned long long* __restrict__ counts,
                                                        const uint64_t* __restrict__ words,
                                                        const uint16_t* __restrict__ len, int h, int m, int w,
-                                                       uint32_t nb_log2, uint64_t cell_lo, uint32_t* __restrict__ key,
-                                                       uint64_t* __restrict__ ent) {
-  const uint64_t blk = (uint64_t)nranks * slot, lim = total / nranks;  // records per peer stream
+                                                       uint32_t nb_log2, uint64_t cell_lo, uint32_t cls, uint32_t fs,
+                                                       uint32_t* __restrict__ key, uint64_t* __restrict__ ent) {
+  const uint32_t ts = blockIdx.y, t = ts / nranks, sp = ts - t * nranks;
+  const uint64_t cnt = counts[sp] < lim ? counts[sp] : lim;  // (a cut stream: what arrived)
+  uint64_t base = 0;
+  for (uint32_t q = 0; q < sp; ++q) base += counts[q] < lim ? counts[q] : lim;
   const uint64_t nbmask = (1ULL << nb_log2) - 1;
-  for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < total; i += (uint64_t)gridDim.x * kBlock) {
-    const uint64_t t = i / blk, rem = i - t * blk, sp = rem / slot, j = t * slot + (rem - sp * slot);
-    if (j >= counts[sp]) continue;
-    uint64_t at = j;
-    for (uint64_t q = 0; q < sp; ++q) at += counts[q] < lim ? counts[q] : lim;
-    const uint64_t e = recv[i];
-    key[at] = (uint32_t)((entry_hash<MAXW>(words, len, e, h, m, w) & nbmask) - cell_lo);
-    ent[at] = e;
+  const uint64_t* src = recv + (uint64_t)ts * slot;
+  for (uint64_t x = (uint64_t)blockIdx.x * kBlock + threadIdx.x; x < slot; x += (uint64_t)gridDim.x * kBlock) {
+    const uint64_t j = (uint64_t)t * slot + x;
+    if (j >= cnt) break;
+    const uint64_t e = src[x];
+    const uint32_t cell = (uint32_t)((entry_hash<MAXW>(words, len, e, h, m, w) & nbmask) - cell_lo);
+    // the sort key of k_key_class, formed here: ((cell << cls | (o == 3)) << fs) | low fingerprint bits
+    const uint32_t c3 = (cls && ((uint32_t)(e >> 32) & 3u) == 3u) ? 1u : 0u;
+    key[base + j] = (((cell << cls) | c3) << fs) | (entry_fp(e) & ((1u << fs) - 1u));
+    ent[base + j] = e;
   }
 }
 
-// the received runs (8-B metas in the slot layout) -> 16-B probe records at
-// the same positions: x = mix64 of the minimizer m-mer at p of the run's read
-// (bucket | fingerprint, what the sender's scan hashed), y = the meta
+// the received runs (8-B metas) -> 16-B probe records at the same positions:
+// x = mix64 of the minimizer m-mer at p of the run's read (bucket |
+// fingerprint, what the sender's scan hashed), y = the meta
 template <int MAXW>
 __global__ __launch_bounds__(kBlock) void k_xruns_expand(const uint64_t* __restrict__ recv, uint64_t slot,
-                                                        uint32_t nranks, uint64_t total,
-                                                        const unsigned long long* __restrict__ counts,
+                                                        uint32_t nranks, const unsigned long long* __restrict__ counts,
                                                         const uint64_t* __restrict__ words, int m,
-                                                        ulonglong2* __restrict__ out) {
-  const uint64_t blk = (uint64_t)nranks * slot;
+                                                        ulonglong2* __restrict__ out, int part, uint32_t me) {
+  const uint32_t ts = blockIdx.y, t = ts / nranks, sp = ts - t * nranks;
+  if (part && (part == 1) != (sp == me)) return;  // (a split probe expands the own stream, then the peers')
+  const uint64_t cnt = counts[sp];
   const int msh = 64 - 2 * m;
-  for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < total; i += (uint64_t)gridDim.x * kBlock) {
-    const uint64_t t = i / blk, rem = i - t * blk, sp = rem / slot, j = t * slot + (rem - sp * slot);
-    if (j >= counts[sp]) continue;  // (the probe's regions stop at the counts)
-    const uint64_t meta = recv[i];
-    uint64_t x = 0;
+  const uint64_t* src = recv + (uint64_t)ts * slot;
+  ulonglong2* dst = out + (uint64_t)ts * slot;
+  for (uint64_t x = (uint64_t)blockIdx.x * kBlock + threadIdx.x; x < slot; x += (uint64_t)gridDim.x * kBlock) {
+    if ((uint64_t)t * slot + x >= cnt) break;  // (the probe's regions stop at the counts)
+    const uint64_t meta = src[x];
+    uint64_t v = 0;
     if (meta != kFlatHole) {
       const uint64_t* g = words + (meta & 0xFFFFFFFFull) * slot_words(MAXW);
-      x = mix64(ext_slot<MAXW>(g, (int)((meta >> 32) & 1023u)) >> msh);
+      v = mix64(ext_slot<MAXW>(g, (int)((meta >> 32) & 1023u)) >> msh);
     }
-    out[i] = make_ulonglong2(x, meta);
+    dst[x] = make_ulonglong2(v, meta);
   }
+}
+
+// grid of the slot-walking kernels: (tiles of a slot, rounds * P slots)
+inline dim3 slot_grid(uint64_t slot, uint32_t rounds, uint32_t nranks) {
+  // one record per thread: the kernels are a chain of dependent loads per record
+  const uint64_t tiles = std::max<uint64_t>(1, (slot + kBlock - 1) / kBlock);
+  return dim3((uint32_t)tiles, rounds * nranks);
 }
 
 template <int W>
 struct LaunchXkeysDense {
-  static int run(mg_ctx* ctx, const uint64_t* recv, uint64_t slot, uint64_t total, const unsigned long long* counts,
+  static int run(mg_ctx* ctx, const uint64_t* recv, uint64_t slot, uint32_t rounds, const unsigned long long* counts,
                  uint32_t* key, uint64_t* ent) {
-    const uint32_t grid = (uint32_t)std::min<uint64_t>((total + kBlock - 1) / kBlock, 65536);
-    hipLaunchKernelGGL(k_xkeys_dense<W>, dim3(grid), dim3(kBlock), 0, ctx->stream, recv, slot, ctx->nranks, total, counts,
-                       ctx->d_words, ctx->d_len, (int)ctx->h, (int)ctx->m, (int)ctx->w, ctx->nb_log2, ctx->cell_lo, key,
-                       ent);
+    hipLaunchKernelGGL(k_xkeys_dense<W>, slot_grid(slot, rounds, ctx->nranks), dim3(kBlock), 0, ctx->stream, recv, slot,
+                       ctx->nranks, (uint64_t)rounds * slot, counts, ctx->d_words, ctx->d_len, (int)ctx->h,
+                       (int)ctx->m, (int)ctx->w, ctx->nb_log2, ctx->cell_lo, ctx->xkey_cls, ctx->xkey_fs, key, ent);
     return hipGetLastError() == hipSuccess ? 0 : -1;
   }
 };
 
 template <int W>
 struct LaunchXrunsExpand {
-  static int run(mg_ctx* ctx, const uint64_t* recv, uint64_t slot, uint64_t total, const unsigned long long* counts,
-                 ulonglong2* out) {
-    const uint32_t grid = (uint32_t)std::min<uint64_t>((total + kBlock - 1) / kBlock, 65536);
-    hipLaunchKernelGGL(k_xruns_expand<W>, dim3(grid), dim3(kBlock), 0, ctx->stream, recv, slot, ctx->nranks, total,
-                       counts, ctx->d_words, (int)ctx->m, out);
+  static int run(mg_ctx* ctx, const uint64_t* recv, uint64_t slot, uint32_t rounds, const unsigned long long* counts,
+                 ulonglong2* out, int part) {
+    hipLaunchKernelGGL(k_xruns_expand<W>, slot_grid(slot, rounds, ctx->nranks), dim3(kBlock), 0, ctx->stream, recv,
+                       slot, ctx->nranks, counts, ctx->d_words, (int)ctx->m, out, part, ctx->rank);
     return hipGetLastError() == hipSuccess ? 0 : -1;
   }
 };
@@ -862,6 +880,14 @@ struct ScanParams {
   // dst_ranks + d] (nullptr: not counted; k_part's count pass does it)
   unsigned long long* dst_cnt;
   uint32_t dst_ranks;
+  // k_scan<RECV> (exchange mode, keys first): the key records this rank
+  // received (8-B entries in the slot layout: recv_P peers x recv_slot per
+  // round, recv_total positions, recv_cnt = the per-peer counts), CAS-inserted
+  // into the rank's cells (local cell = bucket - cell_lo) during the scan
+  const uint64_t* recv_keys;
+  const unsigned long long* recv_cnt;
+  uint64_t recv_slot, recv_total, cell_lo;
+  uint32_t recv_P;
 };
 
 // Exchange-mode key records are o-major in the order o = 0, 2, 3, 1: when the
@@ -929,7 +955,7 @@ __device__ __forceinline__ uint64_t ext_reg(const uint64_t* rw, int pos) {
 #ifndef MG_SCAN_WAVES_G
 #define MG_SCAN_WAVES_G 6  // waves/SIMD of the length-ranked (G > 1) scan (A/B builds override)
 #endif
-template <int MAXW, bool INDEX, bool KEYREC = false, int G = 1>
+template <int MAXW, bool INDEX, bool KEYREC = false, int G = 1, bool RECV = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(G > 1 ? MG_SCAN_WAVES_G : 6))) void k_scan(ScanParams p) {
   extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -970,6 +996,30 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(G > 1 ? 
     nbuf += (uint32_t)__popcll(bal);
   };
   const uint64_t nwin = (ngroups + G - 1) / G;
+  // RECV: this wavefront's share of the received key records (slot-layout
+  // positions [r_at, r_end), chunks of 64 -- slots are multiples of 64), a few
+  // chunks of CAS inserts after each window, so their latency hides behind the
+  // other wavefronts' scan as the fused path's own inserts do
+  uint64_t r_at = 0, r_end = 0, r_per = 0;
+  if constexpr (RECV) {
+    const uint64_t nch = (p.recv_total + 63) / 64;
+    const uint64_t ch0 = nch * gw / nw, ch1 = nch * (gw + 1) / nw;
+    r_at = ch0 * 64;
+    r_end = min(ch1 * 64, p.recv_total);
+    const uint64_t wins = gw < nwin ? (nwin - gw + nw - 1) / nw : 0;
+    r_per = wins ? ((ch1 - ch0) + wins - 1) / wins : 0;
+  }
+  auto recv_insert = [&](uint64_t nchunks) {
+    for (uint64_t c = 0; c < nchunks && r_at < r_end; ++c, r_at += 64) {
+      const uint64_t ts = r_at / p.recv_slot, x = r_at - ts * p.recv_slot + (uint64_t)lane;  // (one divide per chunk)
+      const uint64_t t = ts / p.recv_P, sp = ts - t * p.recv_P;
+      if (r_at + (uint64_t)lane < r_end && t * p.recv_slot + x < p.recv_cnt[sp]) {
+        const uint64_t e = p.recv_keys[r_at + lane];
+        const uint64_t v = entry_hash<MAXW>(p.words, p.len, e, h, m, w);
+        cell_insert(p.cells, (v & nbmask) - p.cell_lo, p.cell_n, e);
+      }
+    }
+  };
   for (uint64_t win = gw; win < nwin; win += nw) {
    const uint64_t A0 = p.a_lo + win * (G * kWave);  // the window's first slot
    // (length, slot) of the window's reads, ascending: pass q takes ranks
@@ -1130,7 +1180,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(G > 1 ? 
         if (flag && at < p.run_cap) region[grp * p.run_cap + at] = make_ulonglong2(v, meta);
 #endif
       }
-      if constexpr (KEYREC) {
+      if constexpr (KEYREC || RECV) {
         if (p.dst_cnt) {
           const bool st = flag && at_rec < p.run_cap;  // (k_part routes the stored records of a region)
           const uint32_t d = st ? (uint32_t)(((v & nbmask) * p.dst_ranks) >> p.nb_log2) : 0u;
@@ -1326,12 +1376,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(G > 1 ? 
       }
     }
    }
+   if constexpr (RECV) recv_insert(r_per);  // this window's share of the received keys
   }
+  if constexpr (RECV) recv_insert(~0ull);  // (what is left: a wavefront with fewer windows)
   uint64_t c = cur[0];
 #pragma unroll
   for (int j = 1; j < G; ++j) c = lane == j ? cur[j] : c;
   if (lane < G) p.run_cnt[gw * G + lane] = c;
-  if constexpr (KEYREC) {
+  if constexpr (KEYREC || RECV) {
     if (p.dst_cnt && (uint32_t)lane < (uint32_t)G * p.dst_ranks)  // region gw G + j, rank d at [(gw G + j) P + d]
       p.dst_cnt[(gw * G + lane / p.dst_ranks) * p.dst_ranks + lane % p.dst_ranks] = dcnt;
   }
@@ -1670,6 +1722,13 @@ struct ProbeParams {
   int contain_skip;               // CONTAIN: skip runs of sources already contained (their superkey != 0)
   int compact;                    // park the live items of sparse run batches (filled batches only)
   int share;                      // a block's wavefronts share its regions batch by batch (probe_share)
+  int append;                     // rows go after the ones a previous launch left in each region (reg_cnt)
+  // a split exchange probe walks one part of the slot-layout regions (K per
+  // peer slot and round): part 1 = peer rm_me's, part 2 = every other peer's;
+  // logical region L of the part -> physical region (run_cnt / runs index)
+  int rm_part;
+  uint32_t rm_P, rm_me;
+  uint64_t rm_K;
   const uint32_t* id;             // slot -> reference ID - 1 (nullptr: ID order); rows and superkeys carry IDs
   // DCNT (exchange-mode discovery): rows stored per destination rank (the
   // source ID's owner, k_part's OWN_SRC rule) into dst_cnt[gw * dst_ranks + d]
@@ -1737,7 +1796,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MG_PROBE
   extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
   __shared__ unsigned int s_dc[DCNT ? kWavesPerBlock * kWave : 1];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  if constexpr (DCNT) s_dc[wv * kWave + lane] = 0u;
+  if constexpr (DCNT) s_dc[wv * kWave + lane] = p.append && (uint32_t)lane < p.dst_ranks ?
+                                                   (unsigned)p.dst_cnt[(blockIdx.x * kWavesPerBlock + wv) * p.dst_ranks + lane]
+                                                   : 0u;
   unsigned char* base = reinterpret_cast<unsigned char*>(smem) + (size_t)wv * PL::bytes;
   uint64_t* s_a = reinterpret_cast<uint64_t*>(base + PL::o_a);
   uint64_t* s_pk = reinterpret_cast<uint64_t*>(base + PL::o_pk);
@@ -1751,7 +1812,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MG_PROBE
   const uint64_t nwp = (uint64_t)gridDim.x * kWavesPerBlock;
   const uint32_t seg = (uint32_t)(gw & (kSegs - 1));
   uint32_t* const region = p.rows + gw * p.reg_cap * 3;
-  uint64_t cursor = 0;
+  uint64_t cursor = (!CONTAIN && p.append) ? p.reg_cnt[gw] : 0;  // (the second part of a split probe)
   uint32_t ncand = 0, npend = 0;
   // diagnostics (p.stats): wavefront sum of a per-lane count into counter i
   // (runs probed, entries scanned, partners fetched, rows); call converged.
@@ -1909,7 +1970,17 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MG_PROBE
                  : gw + (uint64_t)r * nwp;
   };
   auto open_region = [&](uint32_t r) {
-    const uint64_t reg = reg_of(r);
+    uint64_t reg = reg_of(r);
+    if (p.rm_part) {  // (wavefront-uniform; once per region)
+      const uint64_t blk = reg / p.rm_K, k = reg - blk * p.rm_K;
+      uint64_t t = blk, sp = p.rm_me;
+      if (p.rm_part == 2) {
+        t = blk / (p.rm_P - 1);
+        sp = blk - t * (p.rm_P - 1);
+        sp += sp >= p.rm_me ? 1 : 0;
+      }
+      reg = (t * p.rm_P + sp) * p.rm_K + k;
+    }
     rbase = p.runs + reg * p.run_cap;
     const uint64_t c = p.run_cnt[reg];
     rcnt = c < p.run_cap ? c : p.run_cap;
@@ -2255,28 +2326,42 @@ __global__ __launch_bounds__(kBlock) void k_part(PartParams p) {
   for (uint64_t r = blockIdx.x; r < p.nreg; r += gridDim.x) {
     uint64_t c = p.cnt ? p.cnt[r] : (p.flat_n > r * p.cap ? p.flat_n - r * p.cap : 0);
     c = c < p.cap ? c : p.cap;
-    for (uint64_t i0 = 0; i0 < c; i0 += kBlock) {
+    // one record per thread and step, the next step's record loaded before
+    // this one is placed (the steps are otherwise one dependent round trip each)
+    struct Rec {
+      bool valid;
+      uint32_t d;
+      ulonglong2 x16;
+      uint3 x12;
+    };
+    auto fetch = [&](uint64_t i0) {
+      Rec q{false, 0u, make_ulonglong2(0, 0), make_uint3(0, 0, 0)};
       const uint64_t i = i0 + threadIdx.x;
-      bool valid = i < c;
-      uint32_t d = 0;
-      ulonglong2 x16 = make_ulonglong2(0, 0);
-      uint3 x12 = make_uint3(0, 0, 0);
-      if (valid) {
+      q.valid = i < c;
+      if (q.valid) {
         if (KIND == OWN_KEY) {
           const uint64_t at = r * p.cap + i;  // (the rank's records are contiguous, key_seg order)
           const uint64_t e = p.key_ent[at];
           const uint32_t b = p.key_bk[at];
-          valid = e != kEmpty;  // a read without keys (never after setup_index's length check)
-          x16 = make_ulonglong2(b, e);
-          d = (uint32_t)(((uint64_t)b * p.nranks) >> p.nb_log2);
+          q.valid = e != kEmpty;  // a read without keys (never after setup_index's length check)
+          q.x16 = make_ulonglong2(b, e);
+          q.d = (uint32_t)(((uint64_t)b * p.nranks) >> p.nb_log2);
         } else if (KIND == OWN_BUCKET) {
-          x16 = reinterpret_cast<const ulonglong2*>(p.base)[r * p.cap + i];
-          d = (uint32_t)(((x16.x & ((1ULL << p.nb_log2) - 1)) * p.nranks) >> p.nb_log2);
+          q.x16 = reinterpret_cast<const ulonglong2*>(p.base)[r * p.cap + i];
+          q.d = (uint32_t)(((q.x16.x & ((1ULL << p.nb_log2) - 1)) * p.nranks) >> p.nb_log2);
         } else {
-          x12 = reinterpret_cast<const uint3*>(p.base)[r * p.cap + i];
-          d = (uint32_t)(((uint64_t)x12.x * p.nranks - 1) / p.n_reads);  // src is the 1-based ID
+          q.x12 = reinterpret_cast<const uint3*>(p.base)[r * p.cap + i];
+          q.d = (uint32_t)(((uint64_t)q.x12.x * p.nranks - 1) / p.n_reads);  // src is the 1-based ID
         }
       }
+      return q;
+    };
+    Rec nxt = fetch(0);
+    for (uint64_t i0 = 0; i0 < c; i0 += kBlock) {
+      const Rec cur = nxt;
+      if (i0 + kBlock < c) nxt = fetch(i0 + kBlock);
+      const bool valid = cur.valid;
+      const uint32_t d = cur.d;
       // wavefront multi-split: one ballot per destination; lane dd then holds
       // destination dd's count and takes its LDS cursor step, all
       // destinations in one LDS atomic (no loop serialised per destination)
@@ -2294,10 +2379,15 @@ __global__ __launch_bounds__(kBlock) void k_part(PartParams p) {
         const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(at >> 32), (int)d);
         const uint64_t k = (((uint64_t)hi << 32) | lo) + lane_prefix(mine);
         if (valid && k < lim) {  // a stream cut at its capacity keeps its full count
-          const uint64_t q = k / p.slot, o = ((q * p.nranks) + d) * p.slot + (k - q * p.slot);
+          uint64_t q = 0, kk = k;  // (round, position in it): k < rounds * slot, rounds small: no 64-bit divide
+          while (kk >= p.slot) {
+            kk -= p.slot;
+            ++q;
+          }
+          const uint64_t o = ((q * p.nranks) + d) * p.slot + kk;
           void* dst = (p.self_out && d == p.self_rank) ? p.self_out : p.out;
-          if (KIND != OWN_SRC) reinterpret_cast<uint64_t*>(dst)[o] = x16.y;  // entry / run meta (8 B)
-          else reinterpret_cast<uint3*>(dst)[o] = x12;
+          if (KIND != OWN_SRC) reinterpret_cast<uint64_t*>(dst)[o] = cur.x16.y;  // entry / run meta (8 B)
+          else reinterpret_cast<uint3*>(dst)[o] = cur.x12;
         }
       }
     }
@@ -2342,15 +2432,18 @@ __global__ __launch_bounds__(1024) void k_part_scan(unsigned long long* blk, uin
 
 // Per-region counts of a slot-layout buffer cut into regions of `reg` records
 // (reg divides slot; region q covers records [q reg, q reg + reg)).
+// part (exchange mode's split discovery probe): 1 = only the regions of peer
+// `me` (this rank's own stream), 2 = every other peer's, 0 = all
 __global__ __launch_bounds__(kBlock) void k_slot_regions(unsigned long long* __restrict__ out,
                                                          const unsigned long long* __restrict__ counts,
                                                          uint64_t slot, uint64_t reg, uint64_t nreg,
-                                                         uint32_t nranks) {
+                                                         uint32_t nranks, int part, uint32_t me) {
   const uint64_t q = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
   if (q >= nreg) return;
   const uint64_t K = slot / reg, blk = q / K, k = q - blk * K, t = blk / nranks, s = blk - t * nranks;
   const uint64_t start = t * slot + k * reg, c = counts[s];
-  out[q] = c > start ? (c - start < reg ? c - start : reg) : 0;
+  const bool in = part == 0 || ((part == 1) == (s == me));
+  out[q] = (in && c > start) ? (c - start < reg ? c - start : reg) : 0;
 }
 
 // Exchange mode: the received runs (slot layout, one stream per peer) ->
@@ -2815,20 +2908,28 @@ __global__ __launch_bounds__(kBlock) void k_layout_keys(const uint64_t* __restri
   const int m = L < kM ? L : kM;
   const mer_t mmask = 2 * m == 8 * (int)sizeof(mer_t) ? ~(mer_t)0 : (((mer_t)1 << (2 * m)) - 1);
   const uint64_t* g = words + i * slot_words(MAXW);
+  // the read's words in flight together, then 32 bases per word with a
+  // compile-time shift (a load per 32 bases inside the loop made every word a
+  // dependent round trip: 0.75 ms at C3)
+  uint64_t rw[MAXW];
+#pragma unroll
+  for (int k = 0; k < MAXW; ++k) rw[k] = g[k];
   mer_t fw = 0, rc = 0;
   uint32_t best = 0xFFFFFFFFu, bpos = 0;
-  uint64_t cw = 0;
-  for (int t = 0; t < L; ++t) {
-    if ((t & 31) == 0) cw = g[t >> 5];
-    const uint32_t b = (uint32_t)(cw >> (62 - 2 * (t & 31))) & 3u;
-    fw = ((fw << 2) | b) & mmask;
-    rc = (rc >> 2) | ((mer_t)(3u - b) << (2 * m - 2));
-    if (t >= m - 1) {
+#pragma unroll
+  for (int k = 0; k < MAXW; ++k) {
+    if (32 * k >= L) break;
+    const uint64_t cw = rw[k];
+#pragma unroll 8
+    for (int u = 0; u < 32; ++u) {
+      const int t = 32 * k + u;
+      const uint32_t b = (uint32_t)(cw >> (62 - 2 * u)) & 3u;
+      fw = ((fw << 2) | b) & mmask;
+      rc = (rc >> 2) | ((mer_t)(3u - b) << (2 * m - 2));
       const uint32_t hv = fmix32(fw < rc ? fw : rc);
-      if (hv < best) {  // the hash, leftmost on ties
-        best = hv;
-        bpos = (uint32_t)(t - m + 1);
-      }
+      const bool take = t >= m - 1 && t < L && hv < best;  // the hash, leftmost on ties
+      best = take ? hv : best;
+      bpos = take ? (uint32_t)(t - m + 1) : bpos;
     }
   }
   const uint32_t pmax = (1u << pb) - 1u;
@@ -3020,6 +3121,59 @@ __global__ __launch_bounds__(kBlock) void k_index_keys(IndexParams p) {
   }
 }
 
+// Exchange mode, keys first (option xchg_keys_first, equal lengths): the
+// index key records of this rank's source reads [a_lo, a_hi) alone, before
+// any window is scanned, so they travel to their bucket owners while nothing
+// waits on them and the owners file them with CAS inserts inside their own
+// window scan (k_scan<RECV>), where the fused path's inserts hide too.  Same
+// keys (hashRead, HashTable.cpp:88-104) and rule as k_index_keys, written as
+// the KEYREC scan writes them: key o of source a at key_seg(o) * key_n + a - a_lo
+// (bucket, entry); o = 1 a hole when skip_o1.
+template <int MAXW>
+__global__ __launch_bounds__(kBlock) void k_xchg_keys(IndexParams p, uint64_t a_lo, uint64_t a_hi,
+                                                     uint32_t* __restrict__ key_bk, uint64_t* __restrict__ key_ent) {
+  const int h = p.h, m = p.m, w = p.w;
+  const int msh = 64 - 2 * m;
+  const uint64_t mmask = (m == 32) ? ~0ULL : ((1ULL << (2 * m)) - 1);
+  const uint64_t nbm = (1ULL << p.nb_log2) - 1, key_n = a_hi - a_lo;
+  for (uint64_t a = a_lo + (uint64_t)blockIdx.x * kBlock + threadIdx.x; a < a_hi; a += (uint64_t)gridDim.x * kBlock) {
+    uint64_t rw[MAXW + 1];
+    load_slot<MAXW>(p.words, (uint32_t)a, rw);
+    const int n = p.len[a];
+    uint32_t kf[2], kr[2];  // per pass: best forward (o = 0 / 1) and reverse (o = 3 / 2) key
+#pragma unroll
+    for (int pass = 0; pass < 2; ++pass) {
+      const int s0 = pass ? n - h : 0;
+      uint64_t f = ext_reg<MAXW>(rw, s0) >> msh;
+      uint64_t r = rc_word(f << msh) & mmask;
+      const uint64_t nx = ext_reg<MAXW>(rw, s0 + m);
+      uint32_t bf = order_key(f), br = order_key(r) | (uint32_t)(w - 1);
+      for (int t = 1; t < w; ++t) {
+        const uint64_t b = w <= 32 ? (nx >> (62 - 2 * (t - 1))) & 3u : (ext_reg<MAXW>(rw, s0 + m - 1 + t) >> 62) & 3u;
+        f = ((f << 2) | b) & mmask;
+        r = (r >> 2) | ((uint64_t)(3u - b) << (2 * m - 2));
+        bf = min(bf, order_key(f) | (uint32_t)t);
+        br = min(br, order_key(r) | (uint32_t)(w - 1 - t));
+      }
+      kf[pass] = bf;
+      kr[pass] = br;
+    }
+    const uint32_t kb[4] = {kf[0], kf[1], kr[1], kr[0]};
+    const int i0 = (int)(kb[0] & 1023u), i1 = (int)(kb[1] & 1023u), i2 = (int)(kb[2] & 1023u),
+              i3 = (int)(kb[3] & 1023u);
+    const uint64_t mb[4] = {ext_reg<MAXW>(rw, i0) >> msh, ext_reg<MAXW>(rw, n - h + i1) >> msh,
+                            rc_word(ext_reg<MAXW>(rw, n - m - i2)) & mmask,
+                            rc_word(ext_reg<MAXW>(rw, w - 1 - i3)) & mmask};
+#pragma unroll
+    for (int o = 0; o < 4; ++o) {
+      const uint64_t v = mix64(mb[o]);
+      const uint64_t at = key_seg(o) * key_n + a - a_lo;
+      key_bk[at] = (uint32_t)(v & nbm);
+      key_ent[at] = (o == 1 && p.skip_o1) ? kEmpty : make_entry(v, p.nb_log2, (int)(kb[o] & 1023u), o, (uint32_t)a, n);
+    }
+  }
+}
+
 template <int W>
 struct LaunchIndex {
   static int run(mg_ctx* ctx, uint64_t* cells = nullptr, bool all_keys = false) {
@@ -3076,6 +3230,7 @@ inline uint32_t scan_wpb(uint32_t w) {
 // windows too (option xchg_windows): one read per lane idles the lanes of
 // shorter reads, and longest first scans containers before their contents.
 inline bool scan_is_reg(const mg_ctx* ctx, bool index) {
+  if (ctx->rk_on) return false;  // (the received keys' CAS inserts ride on k_scan<RECV>)
   return ctx->w <= (uint32_t)kRegW &&
          (!index || (ctx->xchg && !ctx->xchg_scan_lds && !(ctx->xchg_windows && ctx->minlen != ctx->maxlen)));
 }
@@ -3101,6 +3256,7 @@ uint32_t scan_resident(mg_ctx* ctx, bool index, uint64_t want) {
   if (index && ctx->xchg)
     return scan_windows(ctx, index) > 1 ? resident_blocks(ctx, k_scan<W, true, true, kWinGroups>, lds, want, block)
                                         : resident_blocks(ctx, k_scan<W, true, true>, lds, want, block);
+  if (ctx->rk_on) return resident_blocks(ctx, k_scan<W, false, false, 1, true>, lds, want, block);
   return index ? (scan_windows(ctx, index) > 1 ? resident_blocks(ctx, k_scan<W, true, false, kWinGroups>, lds, want, block)
                                                 : resident_blocks(ctx, k_scan<W, true>, lds, want, block))
                : resident_blocks(ctx, k_scan<W, false>, lds, want, block);
@@ -3206,10 +3362,11 @@ struct LaunchScan {
     sp.skip_o1 = (index && !ctx->index_o1) ? 1 : 0;
     sp.skip_o3 = (index && !ctx->index_o3 && !ctx->xchg) ? 1 : 0;
     sp.no_insert = (index && ctx->phase_limit == 1) ? 1 : 0;
-    if (index && ctx->xchg) ctx->runs_counted = false;
+    const bool recv = ctx->rk_on;
+    if ((index || recv) && ctx->xchg) ctx->runs_counted = false;
     // the exchange scan counts its runs per destination rank as it stores them
     // (the register scan per region, k_scan<KEYREC> per region and group: G P <= 64)
-    if (index && ctx->xchg && ctx->nranks > 1 && G * ctx->nranks <= (uint64_t)kWave) {
+    if ((index || recv) && ctx->xchg && ctx->nranks > 1 && G * ctx->nranks <= (uint64_t)kWave) {
       MG_ENSURE(d_rcnt, rcnt_cap, nreg * ctx->nranks);
       sp.dst_cnt = ctx->d_rcnt;
       sp.dst_ranks = ctx->nranks;
@@ -3239,6 +3396,15 @@ struct LaunchScan {
     } else if (index && ctx->xchg) {
       allow_lds(k_scan<W, true, true>, lds);
       hipLaunchKernelGGL((k_scan<W, true, true>), dim3(sgrid), dim3(wpb * kWave), lds, stream, sp);
+    } else if (recv) {  // exchange mode, keys first: the runs + the received keys' CAS inserts
+      sp.recv_keys = ctx->rk_keys;
+      sp.recv_cnt = ctx->rk_cnt;
+      sp.recv_slot = ctx->rk_slot;
+      sp.recv_total = ctx->rk_total;
+      sp.recv_P = ctx->nranks;
+      sp.cell_lo = ctx->cell_lo;
+      allow_lds(k_scan<W, false, false, 1, true>, lds);
+      hipLaunchKernelGGL((k_scan<W, false, false, 1, true>), dim3(sgrid), dim3(wpb * kWave), lds, stream, sp);
     } else if (index && G > 1) {
       allow_lds(k_scan<W, true, false, kWinGroups>, lds);
       hipLaunchKernelGGL((k_scan<W, true, false, kWinGroups>), dim3(sgrid), dim3(wpb * kWave), lds, stream, sp);
@@ -3264,7 +3430,7 @@ template <int W>
 struct LaunchProbe {
   static int run(mg_ctx* ctx, bool contain, const ulonglong2* runs, const unsigned long long* run_cnt,
                  uint64_t run_cap, uint64_t run_regions, uint32_t grid, const uint32_t* src_super = nullptr,
-                 uint64_t src_lo = 0, uint64_t src_hi = 0) {
+                 uint64_t src_lo = 0, uint64_t src_hi = 0, bool append = false) {
     // discovery reads the o = 3 keys: a full table built without them (index_o3
     // = false) is only exact behind the live index that has them
     if (!contain && !ctx->index_o3 && !ctx->live_ready)
@@ -3323,6 +3489,13 @@ struct LaunchProbe {
     // containment probe (C5 35.0 vs 29.6 ms: contain_skip finds fewer containers marked in time)
     pp.share = (!contain && ctx->probe_share) ? 1 : 0;
     pp.id = ctx->d_id;
+    pp.append = append ? 1 : 0;
+    if (runs == ctx->xruns_base && ctx->xruns_part && ctx->nranks > 1) {  // (a split exchange probe)
+      pp.rm_part = ctx->xruns_part;
+      pp.rm_P = ctx->nranks;
+      pp.rm_me = ctx->rank;
+      pp.rm_K = ctx->xruns_K;
+    }
     const size_t lds = (size_t)kWavesPerBlock * ProbeLds<W>::bytes;
     const bool dcnt = !contain && ctx->xchg && ctx->xchg_route_rows && ctx->nranks > 1 &&
                       ctx->nranks <= (uint32_t)kWave && ctx->n;
@@ -3823,6 +3996,19 @@ int mg_set_option(mg_ctx* ctx, const char* name, int64_t value) {
     ctx->max_blocks = value > 0 ? (uint32_t)value : 8192u;
     return 0;
   }
+  if (!strcmp(name, "xchg_keys_first")) {  // exchange mode, equal lengths: key records first (default 1)
+    ctx->xchg_keys_first = value != 0;
+    return 0;
+  }
+  if (!strcmp(name, "xchg_split_max")) {  // exchange mode: mg_xchg_probe_own splits the probe up to this many ranks
+    ctx->xchg_split_max = (uint32_t)std::max<int64_t>(0, value);
+    return 0;
+  }
+  if (!strcmp(name, "xchg_region")) {  // exchange mode: records per probe region of the received runs (power of 2)
+    if (value < 0 || value > 65536 || (value & (value - 1))) return set_err(ctx, "xchg_region: a power of two <= 65536");
+    ctx->xchg_region = (uint32_t)value;
+    return 0;
+  }
   if (!strcmp(name, "alloc_cap")) {  // tests: device allocations above this many bytes fail (0 = no cap)
     ctx->alloc_cap = (uint64_t)std::max<int64_t>(0, value);
     return 0;
@@ -3911,6 +4097,8 @@ int setup_index(mg_ctx* ctx, uint32_t min_overlap, uint32_t seed_k, bool cells =
   ctx->key0_ready = false;  // set by the fused build when it writes the o = 0 keys
   ctx->xchg = false;        // mg_xchg_begin sets it after this
   ctx->xchg_fused = false;  // (a plain build after a one-rank exchange step takes no exchange shortcut)
+  ctx->xruns_part = 0;
+  ctx->own_probed = false;
   ctx->xmarks_done = false;
   ctx->xmarks = nullptr;
   ctx->packable = 0;
@@ -3962,12 +4150,12 @@ int route_slots(mg_ctx* ctx, PartParams pp, void* out, void* self_out, uint64_t 
   return 0;
 }
 
-constexpr uint64_t kFlatRegion = 4096;  // records per routing region of a flat array
+constexpr uint64_t kFlatRegion = 1024;  // records per routing region of a flat array (more blocks in flight)
 constexpr uint64_t kXRegion = 1024;     // records per probe region of the ordered received runs
 
 // region counts of a slot-layout buffer into *buf (grown as needed)
 int slot_regions(mg_ctx* ctx, unsigned long long** buf, size_t* cap, const unsigned long long* counts,
-                 uint64_t slot, uint64_t reg, uint64_t nreg) {
+                 uint64_t slot, uint64_t reg, uint64_t nreg, int part = 0) {
   if (*cap < nreg) {
     if (*buf) (void)hipFree(*buf);
     *buf = nullptr;
@@ -3977,7 +4165,7 @@ int slot_regions(mg_ctx* ctx, unsigned long long** buf, size_t* cap, const unsig
   }
   if (nreg)
     hipLaunchKernelGGL(k_slot_regions, dim3((uint32_t)((nreg + kBlock - 1) / kBlock)), dim3(kBlock), 0, ctx->stream,
-                       *buf, counts, slot, reg, nreg, ctx->nranks);
+                       *buf, counts, slot, reg, nreg, ctx->nranks, part, ctx->rank);
   MG_TRY(hipGetLastError());
   return 0;
 }
@@ -3993,15 +4181,40 @@ struct LaunchScanXchg {
   }
 };
 
+// exchange mode, keys first: the key records of this rank's sources alone
+template <int W>
+struct LaunchXchgKeys {
+  static int run(mg_ctx* ctx, uint64_t lo, uint64_t hi) {
+    IndexParams p = index_params(ctx);
+    p.skip_o1 = ctx->index_o1 ? 0 : 1;
+    const uint32_t grid = (uint32_t)std::max<uint64_t>(
+        1, std::min<uint64_t>((hi - lo + kBlock - 1) / kBlock, (uint64_t)ctx->n_cu * 16));
+    hipLaunchKernelGGL((k_xchg_keys<W>), dim3(grid), dim3(kBlock), 0, ctx->stream, p, lo, hi, ctx->d_kb, ctx->d_ke);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+  }
+};
+
+// ... and its window scan, which CAS-inserts the received key records (ctx->rk_on)
+template <int W>
+struct LaunchScanRecv {
+  static int run(mg_ctx* ctx, uint64_t lo, uint64_t hi) {
+    const uint32_t wpb = scan_block_waves(ctx, false);
+    const uint64_t groups = (hi - lo + kWave - 1) / kWave;
+    const uint32_t sgrid = scan_resident<W>(ctx, false, (groups + wpb - 1) / wpb);
+    return LaunchScan<W>::run(ctx, false, lo, hi, sgrid, false, ctx->stream, true, false);
+  }
+};
+
 // exchange-mode probe over received runs in the slot layout (regions of `reg`
 // records, counts in ctx->d_flat_cnt)
 template <int W>
 struct LaunchProbeSlots {
-  static int run(mg_ctx* ctx, bool contain, const ulonglong2* runs, uint64_t reg, uint64_t nregions) {
+  static int run(mg_ctx* ctx, bool contain, const ulonglong2* runs, uint64_t reg, uint64_t nregions,
+                 bool append = false) {
     const DiscGeom g = disc_geom<W>(ctx, contain, std::max<uint64_t>(1, ctx->n / ctx->nranks));
     const uint32_t* sup =
         (!contain && ctx->contained_done && ctx->super_any && !ctx->runs_live) ? ctx->d_super : nullptr;
-    return LaunchProbe<W>::run(ctx, contain, runs, ctx->xruns_cnt, reg, nregions, g.grid, sup);
+    return LaunchProbe<W>::run(ctx, contain, runs, ctx->xruns_cnt, reg, nregions, g.grid, sup, 0, 0, append);
   }
 };
 
@@ -4494,8 +4707,12 @@ static int sort_xruns(mg_ctx* ctx, const ulonglong2* recv, uint64_t slot, uint32
 // share cells and partners as in the fused path; ordering them by bucket
 // (option xchg_sort_runs) measured slower: C3 simulated P = 8 step 20.5 vs
 // 18.4 ms, C5 133.8 vs 123.0 ms (profiles/r04e_ab_xchg_sort_runs.txt).
+// part (the split discovery probe, mg_xchg_probe_own): 1 = this rank's own
+// stream only (in recv since mg_xchg_pack; counts = the send counts, of which
+// only this rank's entry is read), 2 = the peers' streams (after the
+// all-to-all), 0 = everything
 static int prepare_xruns(mg_ctx* ctx, const void* recv8, uint64_t slot, uint32_t rounds,
-                         const unsigned long long* counts) {
+                         const unsigned long long* counts, int part = 0) {
   if (ctx->nranks == 1) {  // one rank: the scan's own run regions, as the fused path probes them
     ctx->xruns_base = ctx->d_runs;
     ctx->xruns_cnt = ctx->d_run_cnt;
@@ -4509,11 +4726,11 @@ static int prepare_xruns(mg_ctx* ctx, const void* recv8, uint64_t slot, uint32_t
   // buffer, same slot positions, so the slot regions below apply unchanged
   const uint64_t total = (uint64_t)rounds * ctx->nranks * slot;
   MG_ENSURE(d_xexp, xexp_cap, std::max<uint64_t>(total, 1));
-  if (total && dispatch_w<LaunchXrunsExpand>(ctx->maxw, ctx, reinterpret_cast<const uint64_t*>(recv8), slot, total,
-                                             counts, ctx->d_xexp))
+  if (total && dispatch_w<LaunchXrunsExpand>(ctx->maxw, ctx, reinterpret_cast<const uint64_t*>(recv8), slot, rounds,
+                                             counts, ctx->d_xexp, part))
     return launch_fail(ctx, "run records launch failed");
   const void* recv = ctx->d_xexp;
-  if (ctx->xchg_sort_runs) {
+  if (ctx->xchg_sort_runs) {  // (never split: mg_xchg_probe_own leaves the step whole then)
     if (sort_xruns(ctx, reinterpret_cast<const ulonglong2*>(recv), slot, rounds, counts)) return -1;
     ctx->xruns_cnt = ctx->d_flat_cnt;  // (after sort_xruns: it may have grown the counts)
     ctx->xruns_base = ctx->d_xv[ctx->xv_sel];
@@ -4521,15 +4738,23 @@ static int prepare_xruns(mg_ctx* ctx, const void* recv8, uint64_t slot, uint32_t
     ctx->xruns_nreg = (ctx->xruns_n + kXRegion - 1) / kXRegion;
     return 0;
   }
-  uint64_t reg = kXRegion;
+  // regions of xchg_region records (default 512): at P = 8 a C3 rank receives
+  // 12.7 M runs; regions of 1,024 left the persistent probe grid (4,096
+  // wavefronts, a block's 4 sharing each quadruple) a fourth round of 22 blocks
+  uint64_t reg = ctx->xchg_region ? ctx->xchg_region : kXRegion;
   while (reg > 1 && slot % reg) reg >>= 1;
-  const uint64_t nreg = slot ? (uint64_t)rounds * ctx->nranks * (slot / reg) : 0;
-  if (slot_regions(ctx, &ctx->d_flat_cnt, &ctx->flat_cnt_cap, counts, slot, reg, nreg)) return -1;
+  const uint64_t K = slot ? slot / reg : 0;
+  const uint64_t nreg = (uint64_t)rounds * ctx->nranks * K;
+  // (part 1 reads only this rank's entry of the send counts; part 2 the received counts)
+  if (slot_regions(ctx, &ctx->d_flat_cnt, &ctx->flat_cnt_cap, counts, slot, reg, nreg, part)) return -1;
   ctx->xruns_cnt = ctx->d_flat_cnt;
   ctx->xruns_base = reinterpret_cast<ulonglong2*>(const_cast<void*>(recv));
   ctx->xruns_reg = reg;
-  ctx->xruns_nreg = nreg;
-  ctx->xruns_ready = true;
+  // a split probe walks only its part's regions (LaunchProbe maps them, ProbeParams::rm_*)
+  ctx->xruns_part = part;
+  ctx->xruns_K = K;
+  ctx->xruns_nreg = part == 0 ? nreg : (uint64_t)rounds * K * (part == 1 ? 1 : ctx->nranks - 1);
+  ctx->xruns_ready = part != 1;  // (after the own part, mg_xchg_probe prepares the peers')
   return 0;
 }
 
@@ -4848,6 +5073,8 @@ int mg_xchg_begin(mg_ctx* ctx, uint32_t min_overlap, uint32_t seed_k) {
   MG_ENSURE(d_cells, cells_cap, ctx->cell_n * kCell);
   ctx->xchg = true;
   ctx->xruns_ready = false;
+  ctx->own_probed = false;
+  ctx->xruns_part = 0;
   ctx->xchg_prefix = ctx->minlen != ctx->maxlen && ctx->prefix_contain;
   ctx->index_o1 = ctx->minlen != ctx->maxlen && !ctx->xchg_prefix;  // (key records of o = 1: holes otherwise)
   // the full table leaves out o = 3 as the fused path does (containment drops
@@ -4862,6 +5089,17 @@ int mg_xchg_begin(mg_ctx* ctx, uint32_t min_overlap, uint32_t seed_k) {
   ctx->scan_state = 0;
   ctx->shared_scan_ms = 0.f;
   ctx->t = mg_timings{};
+  // keys first (equal lengths, several ranks): only the key records now; the
+  // window scan runs in mg_xchg_insert_keys, with the received keys' CAS
+  // inserts riding on it (mixed lengths keep the one scan: their containment
+  // and live index read the received key records sorted)
+  ctx->keys_first = ctx->xchg_keys_first && ctx->nranks > 1 && ctx->minlen == ctx->maxlen;
+  if (ctx->keys_first) {
+    ctx->nrun_reg = 0;
+    if (hi > lo && dispatch_w<LaunchXchgKeys>(ctx->maxw, ctx, lo, hi)) return launch_fail(ctx, "key records launch failed");
+    ctx->packable = 1 << MG_KEYS;
+    return 0;
+  }
   if (hi > lo) {
     // one scan: the four keys of every source read (o-major records) + its
     // runs in per-wavefront regions, as the fused path writes them
@@ -4939,6 +5177,55 @@ int mg_xchg_insert_keys(mg_ctx* ctx, const void* recv, uint64_t slot, uint32_t r
   if (!ctx->xchg && !ctx->xchg_fused) return set_err(ctx, "mg_xchg_begin must run first");
   if (ctx->xchg_fused) return 0;  // one rank: the fused build filed the keys already
   const uint32_t P = ctx->nranks;
+  if (ctx->keys_first) {
+    // the cells cleared, then the window scan of this rank's sources, which
+    // CAS-inserts every received key record as it goes (k_scan<RECV>); a rerun
+    // after a run-region overflow inserts nothing again
+    const uint64_t total = (uint64_t)rounds * P * slot;
+    if (total && (!recv || !counts)) return set_err(ctx, "mg_xchg_insert_keys: null buffer");
+    if (setup_cells(ctx)) return -1;
+    ctx->rk_keys = reinterpret_cast<const uint64_t*>(recv);
+    ctx->rk_cnt = reinterpret_cast<const unsigned long long*>(counts);
+    ctx->rk_slot = slot;
+    ctx->rk_total = total;
+    const uint64_t lo = ctx->xchg_lo, hi = ctx->xchg_hi;
+    int rc = 0;
+    if (hi > lo) {
+      for (int attempt = 0;; ++attempt) {
+        if (attempt == 3) {
+          rc = set_err(ctx, "run buffers overflow after resize");
+          break;
+        }
+        ctx->rk_on = true;
+        rc = dispatch_w<LaunchScanRecv>(ctx->maxw, ctx, lo, hi);
+        ctx->rk_on = false;
+        if (rc) {
+          rc = launch_fail(ctx, "scan launch failed");
+          break;
+        }
+        bool again = false;
+        if ((rc = settle_runs(ctx, &again))) break;
+        if (!again) break;
+        ctx->rk_total = 0;  // (the keys are in)
+      }
+      if (!rc) ctx->shared_scan_ms = elapsed(ctx->ev[6], ctx->ev[7]);
+    } else if (total) {  // no sources of its own: the received keys still go in
+      ctx->rk_on = true;
+      rc = dispatch_w<LaunchScanRecv>(ctx->maxw, ctx, (uint64_t)0, (uint64_t)0);
+      ctx->rk_on = false;
+      if (rc) rc = launch_fail(ctx, "scan launch failed");
+      ctx->nrun_reg = 0;
+    }
+    ctx->rk_on = false;
+    ctx->rk_keys = nullptr;
+    ctx->rk_cnt = nullptr;
+    if (rc) return -1;
+    ctx->xkeys_n = 0;
+    ctx->packable = (1 << MG_KEYS) | (1 << MG_RUNS);
+    MG_TRY(hipEventRecord(ctx->ev[1], ctx->stream));
+    ctx->index_ready = true;
+    return 0;
+  }
   uint64_t n = 0;
   uint32_t* k0 = nullptr;
   uint64_t* e0 = nullptr;
@@ -4965,9 +5252,6 @@ int mg_xchg_insert_keys(mg_ctx* ctx, const void* recv, uint64_t slot, uint32_t r
     }
     k0 = ctx->d_xkk[0];
     e0 = ctx->d_xke[0];
-    if (n && dispatch_w<LaunchXkeysDense>(ctx->maxw, ctx, reinterpret_cast<const uint64_t*>(recv), slot, total,
-                                          reinterpret_cast<const unsigned long long*>(counts), k0, e0))
-      return launch_fail(ctx, "key records launch failed");
   }
   if (n > 0x7FFFFFFFull) return set_err(ctx, "exchange: more than 2^31 key records on one rank");
   ctx->xkey_k = k0;
@@ -4990,7 +5274,11 @@ int mg_xchg_insert_keys(mg_ctx* ctx, const void* recv, uint64_t slot, uint32_t r
   // different fingerprints interleave, and one walk per group is faster (one
   // RCCL rank, index 4.50 vs 4.68-4.75 ms, profiles/r04x2_ab_chain_par_xchg1.txt)
   ctx->xkey_par = ctx->chain_par && (fs >= 3 || ctx->xchg_fs >= 0);
-  if ((ctx->xkey_cls || fs) && n) {
+  if (P > 1 && n) {  // the received records made dense, their sort keys formed on the way
+    if (dispatch_w<LaunchXkeysDense>(ctx->maxw, ctx, reinterpret_cast<const uint64_t*>(recv), slot, rounds,
+                                     reinterpret_cast<const unsigned long long*>(counts), k0, e0))
+      return launch_fail(ctx, "key records launch failed");
+  } else if ((ctx->xkey_cls || fs) && n) {
     hipLaunchKernelGGL(k_key_class, dim3((uint32_t)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, ctx->stream, k0, e0,
                        n, ctx->xkey_cls, fs);
     MG_TRY(hipGetLastError());
@@ -5062,11 +5350,15 @@ int mg_xchg_probe(mg_ctx* ctx, int contain, const void* recv, uint64_t slot, uin
   if (!contain && !ctx->contained_done) return set_err(ctx, "containment must be settled first (mg_finalize_contained)");
   if (ctx->xchg_fused) return xchg_fused_probe(ctx, contain != 0);
   if (ctx->nranks > 1 && (uint64_t)rounds * slot && (!recv || !counts)) return set_err(ctx, "mg_xchg_probe: null buffer");
-  // the first probe of the step sets up the received runs (both probes read them)
-  if (!ctx->xruns_ready && prepare_xruns(ctx, recv, slot, rounds, reinterpret_cast<const unsigned long long*>(counts)))
+  // the first probe of the step sets up the received runs (both probes read
+  // them); after mg_xchg_probe_own, the peers' streams only
+  const bool split = !contain && ctx->own_probed;
+  ctx->own_probed = false;
+  if (!ctx->xruns_ready && prepare_xruns(ctx, recv, slot, rounds, reinterpret_cast<const unsigned long long*>(counts),
+                                         split ? 2 : 0))
     return -1;
   const uint64_t reg = ctx->xruns_reg;
-  const uint64_t nregions = ctx->xruns_nreg;
+  uint64_t nregions = ctx->xruns_nreg;
   ulonglong2* runs = ctx->xruns_base;
   ctx->nreg = 0;
   ctx->n_rows = 0;
@@ -5094,7 +5386,14 @@ int mg_xchg_probe(mg_ctx* ctx, int contain, const void* recv, uint64_t slot, uin
   if (ensure_rows(ctx, std::max<uint64_t>(1, ctx->n / ctx->nranks))) return -1;
   for (int attempt = 0;; ++attempt) {
     if (attempt == 3) return set_err(ctx, "row buffers overflow after resize");
-    MG_TRY(hipEventRecord(ctx->ev[4], ctx->stream));
+    if (split && attempt == 1) {  // a rerun probes every stream in one launch
+      ctx->xruns_part = 0;
+      nregions = (uint64_t)rounds * ctx->nranks * ctx->xruns_K;
+      if (slot_regions(ctx, &ctx->d_flat_cnt, &ctx->flat_cnt_cap, reinterpret_cast<const unsigned long long*>(counts),
+                       slot, reg, nregions, 0))
+        return -1;
+    }
+    if (!(split && attempt == 0)) MG_TRY(hipEventRecord(ctx->ev[4], ctx->stream));  // (split: at the own part)
     bool side = false;
     if (attempt == 0 && nregions && ctx->contained_done && ctx->super_any) {
       // runs of contained sources contribute nothing (:548): drop them from the
@@ -5106,7 +5405,7 @@ int mg_xchg_probe(mg_ctx* ctx, int contain, const void* recv, uint64_t slot, uin
     if (attempt == 0 && ctx->contained_done && (ctx->super_any || !ctx->index_o3) && build_live_index_xchg(ctx))
       return -1;
     if (live_runs_join(ctx, side)) return -1;
-    if (nregions && dispatch_w<LaunchProbeSlots>(ctx->maxw, ctx, false, runs, reg, nregions))
+    if (nregions && dispatch_w<LaunchProbeSlots>(ctx->maxw, ctx, false, runs, reg, nregions, split && attempt == 0))
       return launch_fail(ctx, "probe launch failed");
     MG_TRY(hipEventRecord(ctx->ev[5], ctx->stream));
     if (!nregions) break;
@@ -5127,6 +5426,36 @@ int mg_xchg_probe(mg_ctx* ctx, int contain, const void* recv, uint64_t slot, uin
   ctx->t.total_ms = elapsed(ctx->ev[0], ctx->ev[5]);
   read_stats(ctx, ctx->xchg_hi - ctx->xchg_lo);
   ctx->packable |= 1 << MG_ROWS;
+  return 0;
+}
+
+int mg_xchg_keys_first(const mg_ctx* ctx) { return ctx && ctx->xchg && ctx->keys_first ? 1 : 0; }
+
+int mg_xchg_probe_own(mg_ctx* ctx, const void* recv, uint64_t slot, uint32_t rounds, const uint64_t* send_counts) {
+  if (!ctx) return -1;
+  ctx->err.clear();  // (a message left by an earlier failed call is not this call's cause)
+  MG_TRY(hipSetDevice(ctx->device));
+  ctx->own_probed = false;
+  if ((!ctx->xchg && !ctx->xchg_fused) || !ctx->index_ready) return set_err(ctx, "mg_xchg_insert_keys must run first");
+  if (!ctx->contained_done) return set_err(ctx, "containment must be settled first (mg_finalize_contained)");
+  // the split pays where nothing else needs every stream first: equal lengths
+  // (no containment pass), several ranks, the runs probed in place
+  // and few ranks: the own stream is 1/P of the runs, and a launch over it
+  // costs more than it hides once the peers' transfers are short (C3 at P = 8:
+  // 0.09 ms for 1.6 M runs, the second part 0.53 vs one probe of 0.55 ms)
+  if (ctx->xchg_fused || ctx->nranks == 1 || ctx->nranks > ctx->xchg_split_max || ctx->super_any ||
+      ctx->minlen != ctx->maxlen || ctx->xchg_sort_runs || !((uint64_t)rounds * slot))
+    return 0;
+  if (!recv || !send_counts) return set_err(ctx, "mg_xchg_probe_own: null buffer");
+  if (ensure_rows(ctx, std::max<uint64_t>(1, ctx->n / ctx->nranks))) return -1;
+  ctx->nreg = 0;
+  ctx->n_rows = 0;
+  MG_TRY(hipEventRecord(ctx->ev[4], ctx->stream));
+  if (prepare_xruns(ctx, recv, slot, rounds, reinterpret_cast<const unsigned long long*>(send_counts), 1)) return -1;
+  if (ctx->xruns_nreg &&
+      dispatch_w<LaunchProbeSlots>(ctx->maxw, ctx, false, ctx->xruns_base, ctx->xruns_reg, ctx->xruns_nreg, false))
+    return launch_fail(ctx, "probe launch failed");
+  ctx->own_probed = true;
   return 0;
 }
 

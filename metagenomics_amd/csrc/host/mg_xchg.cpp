@@ -2,7 +2,7 @@
 // _step over the C-ABI of include/mg_overlap.h:
 //   mg_xchg_begin                          one window scan of this rank's sources
 //   mg_xchg_pack(KEYS) -> RCCL -> mg_xchg_insert_keys     HashTable::insertDataset
-//   mg_xchg_pack(RUNS) -> RCCL
+//   mg_xchg_pack(RUNS) -> RCCL (second stream)     [mg_xchg_probe_own meanwhile]
 //   mg_begin_contained; [mg_xchg_prefix_marks; ncclAllReduce MAX (u8);
 //                        mg_xchg_probe(1); ncclAllReduce MAX]; mg_finalize_contained
 //                                                          markContainedReads
@@ -340,13 +340,26 @@ int XchgStep::run() {
     // 2. keys -> bucket owners; 3. runs -> bucket owners (both probes read
     // them) on the second stream, in flight while 4. the received keys are
     // sorted and filed into the local cells (HashTable::insertDataset)
+    // (keys first, mg_xchg_keys_first: the runs come out of the window scan
+    // inside mg_xchg_insert_keys, so they are packed after it)
     route(MG_KEYS, s_);
-    route(MG_RUNS, P > 1 ? s2_ : s_);
-    if (P > 1) hip_check(hipEventRecord(ev_runs_, s2_), "hipEventRecord");
+    const bool keys_first = mg_xchg_keys_first(ctx_) == 1;
+    if (!keys_first) {
+      route(MG_RUNS, P > 1 ? s2_ : s_);
+      if (P > 1) hip_check(hipEventRecord(ev_runs_, s2_), "hipEventRecord");
+    }
     const Stream& ks = st_[MG_KEYS];
     check(mg_xchg_insert_keys(ctx_, ks.recv, ks.slot, ks.rounds, ks.rcounts), "mg_xchg_insert_keys");
-    if (P > 1) hip_check(hipStreamWaitEvent(s_, ev_runs_, 0), "hipStreamWaitEvent");
+    if (keys_first) {
+      route(MG_RUNS, P > 1 ? s2_ : s_);
+      if (P > 1) hip_check(hipEventRecord(ev_runs_, s2_), "hipEventRecord");
+    }
     const Stream& rs = st_[MG_RUNS];
+    bool runs_in = P == 1;  // the peers' run streams have arrived (s_ waited for ev_runs_)
+    auto wait_runs = [&]() {
+      if (!runs_in) hip_check(hipStreamWaitEvent(s_, ev_runs_, 0), "hipStreamWaitEvent");
+      runs_in = true;
+    };
     // 4. markContainedReads (lengths differ, OverlapGraph.cpp:228-233): MAX of the keys over ranks
     const uint64_t n = mg_num_reads(ctx_);
     if (n > superkey_n_) {
@@ -357,6 +370,7 @@ int XchgStep::run() {
     int needed = 0;
     check(mg_begin_contained(ctx_, superkey_, &needed), "mg_begin_contained");
     contained_ = needed != 0;
+    if (needed) wait_runs();  // (the containment probe reads every stream)
     if (needed && P > 1 && use_marks_) {
       // every rank's offset-0 containments first, their marks MAX-reduced: the
       // probe then skips the sources any rank found contained (contain_skip)
@@ -373,7 +387,12 @@ int XchgStep::run() {
       x_.allreduce_max_u64(reinterpret_cast<uint64_t*>(superkey_), n, s_);
     }
     check(mg_finalize_contained(ctx_, nullptr), "mg_finalize_contained");
-    // 5. insertAllEdgesOfRead: probe -> rows [-> src owners]
+    // 5. insertAllEdgesOfRead: probe -> rows [-> src owners].  Equal lengths:
+    // this rank's own stream (in rs.recv since the pack) first, while the
+    // peers' streams are still on the links (a no-op otherwise)
+    if (!runs_in)
+      check(mg_xchg_probe_own(ctx_, rs.recv, rs.slot, rs.rounds, rs.counts), "mg_xchg_probe_own");
+    wait_runs();
     check(mg_xchg_probe(ctx_, 0, rs.recv, rs.slot, rs.rounds, rs.rcounts), "mg_xchg_probe");
     const int nk = route_rows_ ? 3 : 2;  // the stream kinds that moved
     if (route_rows_) route(MG_ROWS, s_);

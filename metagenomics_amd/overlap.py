@@ -94,6 +94,8 @@ def lib() -> C.CDLL:
         "mg_xchg_pack": (i32, [vp, i32, vp, u64, u32, vp, vp]),
         "mg_xchg_insert_keys": (i32, [vp, vp, u64, u32, vp]),
         "mg_xchg_probe": (i32, [vp, i32, vp, u64, u32, vp]),
+        "mg_xchg_probe_own": (i32, [vp, vp, u64, u32, vp]),
+        "mg_xchg_keys_first": (i32, [vp]),
         "mg_slots_digest": (i32, [vp, vp, u64, u32, vp, vp]),
         "mg_begin_contained": (i32, [vp, vp, P(i32)]),
         "mg_xchg_prefix_marks": (i32, [vp, vp]),
@@ -450,6 +452,13 @@ class OverlapEngine:
     def xchg_probe(self, contain: bool, dptr: int, slot: int, rounds: int, counts_dptr: int):
         self._check(lib().mg_xchg_probe(self._h, int(contain), C.c_void_p(dptr), slot, rounds,
                                         C.c_void_p(counts_dptr)), "xchg_probe")
+
+    def xchg_probe_own(self, dptr: int, slot: int, rounds: int, send_counts_dptr: int):
+        """mg_xchg_probe_own: the discovery probe of this rank's own run stream (already in the
+        receive buffer after xchg_pack) while the peers' streams travel; xchg_probe(False) then
+        probes theirs and appends.  A no-op where the step cannot split (one rank, mixed lengths)."""
+        self._check(lib().mg_xchg_probe_own(self._h, C.c_void_p(dptr), slot, rounds, C.c_void_p(send_counts_dptr)),
+                    "xchg_probe_own")
 
     def xchg_prefix_marks(self, marks_dptr: int | None):
         """mg_xchg_prefix_marks: this rank's offset-0 containments now, their marks

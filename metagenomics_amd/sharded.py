@@ -122,6 +122,13 @@ class Exchange:
         slot and returns [(recv_buffer, recv_counts)] per local rank."""
         raise NotImplementedError
 
+    def all_to_all_slots_async(self, sends: list, recvs: list, counts: list, slot: int, rounds: int,
+                               rec_bytes: int):
+        """all_to_all_slots started now; returns finish() -> its result, after which the
+        engines' work may read the received slots.  The base class moves them at once."""
+        out = self.all_to_all_slots(sends, recvs, counts, slot, rounds, rec_bytes)
+        return lambda: out
+
     def allreduce_max(self, bufs: list) -> None:
         raise NotImplementedError
 
@@ -195,6 +202,29 @@ class TorchExchange(Exchange):
             dev_recv.copy_(recv)
             return [(dev_recv, rc.to(self.device))]
         return [(recv, rc)]
+
+    def all_to_all_slots_async(self, sends, recvs, counts, slot, rounds, rec_bytes):
+        """The transfers go out on a side stream that waits only for the packs so far, so
+        the engine stream's next work (the own-stream probe) runs while they are on the
+        links; finish() makes the engine stream wait for them."""
+        if self.staged or self.world == 1 or self.device.type != "cuda":
+            return super().all_to_all_slots_async(sends, recvs, counts, slot, rounds, rec_bytes)
+        torch = self.torch
+        main = torch.cuda.current_stream(self.device)
+        if getattr(self, "_side", None) is None:
+            self._side = torch.cuda.Stream(self.device)
+        packed = torch.cuda.Event()
+        packed.record(main)
+        with torch.cuda.stream(self._side):
+            self._side.wait_event(packed)
+            out = self.all_to_all_slots(sends, recvs, counts, slot, rounds, rec_bytes)
+            arrived = torch.cuda.Event()
+            arrived.record(self._side)
+
+        def finish():
+            main.wait_event(arrived)
+            return out
+        return finish
 
     def allreduce_max(self, bufs):
         (b,) = bufs
@@ -444,7 +474,9 @@ def _step(engines, xchg, min_overlap, seed_k, want_super, plan, route_rows):
     sent = {}
     geo = {}
 
-    def route(kind):
+    def route(kind, move=True):
+        """pack `kind` on every engine; move=False leaves the all-to-all to the caller
+        (returns the pack's buffers: (sends, recvs, counts), slot, rounds)"""
         if P == 1:  # one rank: every stream is its own, nothing is packed (counts = 0)
             cnts = []
             for e in engines:
@@ -470,6 +502,8 @@ def _step(engines, xchg, min_overlap, seed_k, want_super, plan, route_rows):
             cnts.append(c)
         sent[kind] = cnts
         geo[kind] = (slot, rounds)
+        if not move:
+            return (sends, recvs, cnts), slot, rounds
         return xchg.all_to_all_slots(sends, recvs, cnts, slot, rounds, rb), slot, rounds
 
     t0 = time.perf_counter()
@@ -483,14 +517,21 @@ def _step(engines, xchg, min_overlap, seed_k, want_super, plan, route_rows):
         for e, (buf, c) in zip(engines, keys):
             e.xchg_insert_keys(buf.data_ptr() if buf is not None else 0, ks, kr, c.data_ptr())
             done()
-        # 3. runs -> bucket owners (both probes read them)
-        runs, rs, rr = route(MG_RUNS)
+        # 3. runs -> bucket owners (both probes read them).  Equal lengths (no containment
+        # pass) split the discovery probe: each rank's own stream (written straight into its
+        # receive buffer by the pack) is probed while the peers' streams are on the links
+        contained = bool(engines[0].lengths_differ)
+        split = P > 1 and not contained
+        if split:
+            (rsend, rrecv, rcnt), rs, rr = route(MG_RUNS, move=False)
+            runs_in = xchg.all_to_all_slots_async(rsend, rrecv, rcnt, rs, rr, rec_bytes[MG_RUNS])
+        else:
+            runs, rs, rr = route(MG_RUNS)
         t1 = time.perf_counter()
         ms["index"] = (t1 - t0) * 1e3
 
         # 4. markContainedReads (only when lengths differ, OverlapGraph.cpp:228-233)
         # keys (len << 32 | ~index) < 2^48: int64 MAX is the library's unsigned atomicMax
-        contained = bool(engines[0].lengths_differ)
         skeys = [xchg.torch.empty(max(1, engines[0].n_reads), dtype=xchg.torch.int64, device=xchg.device)
                  if contained else None for _ in engines]
         for e, sk in zip(engines, skeys):
@@ -520,7 +561,12 @@ def _step(engines, xchg, min_overlap, seed_k, want_super, plan, route_rows):
         t2 = time.perf_counter()
         ms["contained"] = (t2 - t1) * 1e3
 
-        # 5. insertAllEdgesOfRead: probe the received runs -> rows -> src owners
+        # 5. insertAllEdgesOfRead: probe the received runs -> rows [-> src owners]
+        if split:
+            for e, buf, c in zip(engines, rrecv, rcnt):  # the own stream, while the peers' travel
+                e.xchg_probe_own(buf.data_ptr(), rs, rr, c.data_ptr())
+                done()
+            runs = runs_in()
         for e, (buf, c) in zip(engines, runs):
             e.xchg_probe(False, buf.data_ptr() if buf is not None else 0, rs, rr, c.data_ptr())
             done()

@@ -169,6 +169,19 @@ class MockEngine:
         mine = np.isin(np.minimum(self.all_rows["src"], self.all_rows["dst"]).astype(np.int64) - 1, a)
         self.out_rows = self.all_rows[mine]
 
+    def xchg_probe_own(self, ptr, slot, rounds, counts_ptr):
+        """the split discovery probe's first part: this rank's own stream is already in its
+        receive buffer (the pack wrote it there); the mock checks that and probes nothing yet"""
+        cnt = np.frombuffer(ctypes.string_at(counts_ptr, 8 * self.world), dtype=np.int64)
+        own = self.runs[bucket_owner(self.runs["x"], self.world) == self.rank]
+        assert int(cnt[self.rank]) == len(own)
+        rb = REC_DTYPE.itemsize
+        got = b"".join(ctypes.string_at(ptr + (t * self.world + self.rank) * slot * rb,
+                                        min(slot, max(0, len(own) - t * slot)) * rb) for t in range(rounds))
+        # (a stream longer than rounds * slot is cut: the step reruns with grown capacities)
+        assert got == own[: rounds * slot].tobytes(), "own run stream not in the receive buffer before the exchange"
+        self.own_probes = getattr(self, "own_probes", 0) + 1
+
     def finalize_contained(self, copy=False):
         if self.sk_ptr:
             self.super_keys = np.frombuffer(ctypes.string_at(self.sk_ptr, self.n_reads * 8), dtype=np.int64).copy()

@@ -47,7 +47,7 @@ def _worker(rank, world, port, name, outdir, chunk, route):
     rows = np.zeros(g.shape[0], dtype=EDGE_DTYPE)
     rows["src"], rows["dst"], rows["orient"], rows["offset"] = g[:, 0], g[:, 1], g[:, 2], g[:, 3]
     n = lm(name)["n_unique"]
-    eng = MockEngine(rank, world, rows, n)
+    eng = MockEngine(rank, world, rows, n, lengths_differ=(name != "small"))
     res = sharded_step([eng], TorchExchange(), lm(name)["l"], 0, route_rows=route)
     mine = res.rows_numpy(0)
     assert res.n_rows == [len(mine)]
@@ -62,6 +62,7 @@ def _worker(rank, world, port, name, outdir, chunk, route):
     np.save(os.path.join(outdir, f"keys{rank}.npy"), eng.received_keys)
     np.save(os.path.join(outdir, f"sk{rank}.npy"), eng.super_keys)
     np.save(os.path.join(outdir, f"marks{rank}.npy"), np.array([eng.marks_seen, eng.lengths_differ]))
+    np.save(os.path.join(outdir, f"own{rank}.npy"), np.array([getattr(eng, "own_probes", 0)]))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -85,8 +86,11 @@ def test_exchange_routes_every_record(tmp_path, name, world, chunk, route):
             assert np.all(src_owner(rows["src"], n, world) == r), "row at a rank that does not own its src"
         parts.append(rows)
         keys += np.load(tmp_path / f"keys{r}.npy").shape[0]
-        assert np.array_equal(np.load(tmp_path / f"sk{r}.npy"), expected_super_keys(n))
         seen, differ = np.load(tmp_path / f"marks{r}.npy")
+        if differ:
+            assert np.array_equal(np.load(tmp_path / f"sk{r}.npy"), expected_super_keys(n))
+        # equal lengths ("small"): the split discovery probe, own stream first
+        assert np.load(tmp_path / f"own{r}.npy")[0] == (0 if differ else np.load(tmp_path / f"reruns{r}.npy")[1])
         assert seen == differ  # the cross-rank prefix marks: made, all-reduced, seen by the containment probe
     assert keys == 4 * n
     rr = [np.load(tmp_path / f"reruns{r}.npy") for r in range(world)]

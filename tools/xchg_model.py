@@ -1,26 +1,32 @@
-"""Per-phase model of the multi-GPU step wall at P = 2 / 4 / 8 (VERDICT r4 item 2,
-DESIGN.md §6c), from measurements on ONE MI355X:
+"""Per-phase model of the multi-GPU step wall at P = 2 / 4 / 8, from
+measurements on ONE MI355X:
 
-* compute per rank: the simulated ranks' kernel tables (tools/rank_table.py
-  output of `tools/gpu_run.sh profsimP`: every simulated rank's kernels timed
-  alone, MG_SIM_SERIAL=1), "step compute kernels" = the step's kernels without
-  the simulated exchange's device copies;
-* bytes per rank: the exchange's own slot-layout counts (bench.py
-  `exchange_padding`: records moved between ranks, summed over the ranks), plus
-  the MAX all-reduce of the n x 8 B containment keys when lengths differ;
+* compute per rank: the simulated ranks' kernel tables (tools/rank_table.py output of
+  `tools/gpu_run.sh profsimP`: every simulated rank's kernels timed alone,
+  MG_SIM_SERIAL=1), "step compute kernels" = the step's kernels without the simulated
+  exchange's device copies;
+* bytes per rank: the exchange's own slot-layout counts (bench.py `exchange_padding`:
+  records moved between ranks, summed over the ranks, and the bytes per record on the
+  wire -- round 6: keys and runs 8 B, rows 12 B and only when routed), plus the MAX
+  all-reduce of the n x 8 B containment keys when lengths differ;
 * replicated mode: the slowest simulated rank of
   `bench.py --multi replicated --sim-world P` (no data-path collective).
 
-xGMI (MI355X, one node): every GPU has 7 point-to-point links to its 7 peers.
-An all-to-all moves each peer's share over that peer's own link, all links at
-once, so its time is the largest per-peer share / the per-direction link rate;
-a ring all-reduce of S bytes moves 2 (P-1)/P S per rank, spread here over the
-P - 1 links (the ideal; RCCL's channels approach it).  Link rates modelled:
-64 GB/s (MI300X-class, conservative), 76.5 GB/s (153 GB/s per link counted in
-both directions), 153 GB/s per direction (optimistic).  Each collective round
-adds a fixed latency alpha (30 us).  Two bounds: "serial" = compute + every
-transfer after it; "overlap" = the run exchange hidden behind the key build and
-the rows' behind nothing (what the C++ host's side stream can reach).
+xGMI (MI355X, one node): every GPU has 7 point-to-point links to its 7 peers.  An
+all-to-all moves each peer's share over that peer's own link, all links at once, so its
+time is the per-peer share / the per-direction link rate; a ring all-reduce of S bytes
+moves 2 (P-1)/P S per rank, spread over the P - 1 links.  Link rates modelled: 64 GB/s
+(MI300X-class, conservative), 76.5 GB/s (153 GB/s per link counted in both directions),
+153 GB/s per direction (optimistic).  Each collective round adds a fixed latency alpha
+(30 us).
+
+Two bounds: "serial" = compute + every transfer after it; "overlap" = what the hosts
+(sharded.py, csrc/host/mg_xchg.cpp) schedule: the run streams travel on a second stream
+while the received keys are sorted and filed, and -- equal lengths, no containment pass --
+while each rank probes its own run stream (mg_xchg_probe_own, ~1/P of the probe); with
+containment the runs must all be in before the containment probe, so only the key build
+hides them.  "+rows" lines add the rows' all-to-all (12-B mg_edge records to their src
+owners, bench.py --route-rows), estimated from the measured row count, after the probe.
 
 usage: xchg_model.py OUT.md FUSED_BENCH.json CONFIG DIR
   DIR holds profsim{P}_{CONFIG}_ranks.md, profsim{P}_{CONFIG}_bench.json and
@@ -32,7 +38,9 @@ import sys
 
 LINKS = (64.0, 76.5, 153.0)    # GB/s per direction per link
 ALPHA_MS = 0.030               # per collective round
-REC_BYTES = {"keys": 16, "runs": 16, "rows": 12}
+OLD_REC_BYTES = {"keys": 16, "runs": 16, "rows": 12}  # (bench lines before round 6 carry no record_bytes)
+KEY_BUILD = ("k_xkeys_dense", "k_key_class", "k_cells_", "k_over_heads",
+             "rocprim::trampoline_kernel<rocprim::wrapped_radix_sort", "rocprim::trampoline_kernel<rocprim::wrapped_scan")
 
 
 def step_compute_ms(md_path):
@@ -59,7 +67,7 @@ def main():
     mixed = fused["config"]["read_len"][0] != fused["config"]["read_len"][1]
     lines = [f"### {cfg}: modelled multi-GPU step wall (tools/xchg_model.py)\n",
              f"1 GPU (fused path): {t1:.3f} ms/step, {edges / t1 * 1e3:.3e} edges/s.\n",
-             "| mode | P | compute / rank (ms) | xGMI bytes / rank (MB) | link GB/s | transfer (ms) | "
+             "| mode | P | compute / rank (ms) | xGMI MB / rank (keys + runs [+ rows]) | link GB/s | transfer (ms) | "
              "wall serial (ms) | wall overlap (ms) | speedup vs 1 GPU (serial / overlap) |",
              "|---|---:|---:|---:|---:|---:|---:|---:|---|"]
     res = {"config": cfg, "fused_ms": t1, "rows": []}
@@ -68,25 +76,36 @@ def main():
         bj = os.path.join(d, f"profsim{P}_{cfg}_bench.json")
         if os.path.exists(md) and os.path.exists(bj):
             comp = step_compute_ms(md)
-            keybuild = sum(kernel_ms(md, k) for k in ("k_xkeys_dense", "k_key_class", "k_cells_", "k_over_heads",
-                                                     "rocprim::trampoline_kernel<rocprim::wrapped_radix_sort"))
+            keybuild = sum(kernel_ms(md, k) for k in KEY_BUILD)
+            probe = kernel_ms(md, "k_probe")
+            own_probe = 0.0 if mixed else probe / P  # mg_xchg_probe_own: the rank's own stream
             pad = json.load(open(bj))["exchange_padding"]
-            per_kind = {k: pad[k]["moved_records"] * REC_BYTES[k] / P for k in REC_BYTES}  # bytes per rank
+            per_kind = {k: v["moved_records"] * (v.get("record_bytes") or OLD_REC_BYTES[k]) / P
+                        for k, v in pad.items()}  # bytes per rank
+            # rows to their src owners (--route-rows): each rank's rows/P, (P-1)/P of them leave
+            rows_routed = 2 * edges / P * (P - 1) / P * 12
             ar = (2.0 * (P - 1) / P * n_reads * 8) if mixed else 0.0  # containment keys, ring all-reduce
-            tot_b = sum(per_kind.values()) + ar
-            for B in LINKS:
-                bw = B * 1e9
-                a2a = {k: v / (P - 1) / bw * 1e3 for k, v in per_kind.items()}
-                ar_ms = ar / (P - 1) / bw * 1e3
-                xfer = sum(a2a.values()) + ar_ms + ALPHA_MS * (3 + (2 if mixed else 0))
-                serial = comp + xfer
-                overlap = comp + xfer - min(a2a["runs"], keybuild)
-                lines.append(f"| exchange | {P} | {comp:.3f} | {tot_b / 1e6:.0f} | {B:.1f} | {xfer:.3f} | "
-                             f"{serial:.3f} | {overlap:.3f} | {t1 / serial:.2f}x / {t1 / overlap:.2f}x |")
-                res["rows"].append({"mode": "exchange", "P": P, "compute_ms": comp, "bytes_per_rank": tot_b,
-                                    "bytes_by_kind": per_kind, "allreduce_bytes": ar, "link_gbs": B,
-                                    "transfer_ms": xfer, "wall_serial_ms": serial, "wall_overlap_ms": overlap,
-                                    "key_build_ms": keybuild})
+            for variant in ("exchange", "exchange +rows"):
+                kinds = dict(per_kind)
+                if variant.endswith("rows") and "rows" not in kinds:
+                    kinds["rows"] = rows_routed
+                tot_b = sum(kinds.values()) + ar
+                for B in LINKS:
+                    bw = B * 1e9
+                    a2a = {k: v / (P - 1) / bw * 1e3 for k, v in kinds.items()}
+                    ar_ms = ar / (P - 1) / bw * 1e3
+                    rounds = len(kinds) + (2 if mixed else 0)
+                    xfer = sum(a2a.values()) + ar_ms + ALPHA_MS * rounds
+                    serial = comp + xfer
+                    overlap = serial - min(a2a.get("runs", 0.0), keybuild + own_probe)
+                    mb = " + ".join(f"{kinds[k] / 1e6:.0f}" for k in ("keys", "runs", "rows") if k in kinds)
+                    lines.append(f"| {variant} | {P} | {comp:.3f} | {tot_b / 1e6:.0f} ({mb}) | {B:.1f} | {xfer:.3f} | "
+                                 f"{serial:.3f} | {overlap:.3f} | {t1 / serial:.2f}x / {t1 / overlap:.2f}x |")
+                    res["rows"].append({"mode": variant, "P": P, "compute_ms": comp, "bytes_per_rank": tot_b,
+                                        "bytes_by_kind": kinds, "allreduce_bytes": ar, "link_gbs": B,
+                                        "transfer_ms": xfer, "wall_serial_ms": serial, "wall_overlap_ms": overlap,
+                                        "key_build_ms": keybuild, "own_probe_ms": own_probe,
+                                        "speedup_overlap": t1 / overlap})
         rj = os.path.join(d, f"bench_simrep{P}_{cfg}.json")
         if not os.path.exists(rj) and cfg == "c3":
             rj = os.path.join(d, f"bench_simrep{P}.json")
@@ -96,12 +115,14 @@ def main():
             lines.append(f"| replicated | {P} | {w:.3f} | 0 | — | 0 | {w:.3f} | {w:.3f} | "
                          f"{t1 / w:.2f}x / {t1 / w:.2f}x |")
             res["rows"].append({"mode": "replicated", "P": P, "compute_ms": w, "bytes_per_rank": 0,
-                                "wall_serial_ms": w, "wall_overlap_ms": w, "digest_ok": r["parity"].get("digest_ok")})
+                                "wall_serial_ms": w, "wall_overlap_ms": w, "speedup_overlap": t1 / w,
+                                "digest_ok": r["parity"].get("digest_ok")})
     lines.append("")
-    lines.append(f"Link model: all-to-all = largest per-peer share / link rate (P - 1 links at once); ring all-reduce "
+    lines.append(f"Link model: all-to-all = per-peer share / link rate (P - 1 links at once); ring all-reduce "
                  f"of the containment keys over P - 1 links; {ALPHA_MS * 1e3:.0f} us per collective round.  Compute = "
                  "simulated ranks' kernels, each rank timed alone on one MI355X; on N GPUs each rank has a whole "
-                 "GPU, so per-rank compute is what it is here.")
+                 "GPU, so per-rank compute is what it is here.  '+rows' adds the rows' transfer only (its routing "
+                 "kernel is not in the compute column).")
     open(out, "w").write("\n".join(lines) + "\n")
     json.dump(res, open(os.path.splitext(out)[0] + ".json", "w"), indent=1)
     print("\n".join(lines))
