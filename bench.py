@@ -10,22 +10,26 @@ Default workload = BASELINE.json configs[2] (C3): 10M x 150 bp synthetic
 reads, 20x coverage of a 75 Mb random genome, 50 % reverse-complemented,
 l = 50, seed k = 31.  Multi-GPU (torchrun, one process per GPU): the same 10M
 reads on N GPUs (strong scaling), DESIGN.md §6:
-  --multi auto (default): replicated when every read has one length (no
-    containment pass), exchange when lengths differ (DESIGN.md §6c);
-  --multi replicated: every rank builds the whole index and discovers from
-    its source-read range; no data-path collective (the process group carries
-    only the barrier and the step clock).  At C3 its modelled wall beats the
-    exchange mode's at P = 2, 4 and 8 on xGMI's per-link rate
-    (profiles/r05k_xchg_model_c3.md); its containment pass does not divide, so
-    mixed lengths take the exchange mode;
+  --multi auto (the default): bucket for one read length on <= 4 ranks, else
+    exchange -- the choice DESIGN.md §6c's per-rank tables and xGMI model make
+    (profiles/r06_xchg_model_c3.md);
   --multi exchange (north_star's bucket-range design, BASELINE configs[3]):
-    each rank owns a bucket range of the index and a source-read range; key
-    records, window runs and rows move between ranks with equal-split RCCL
-    all-to-alls over xGMI (torch.distributed "nccl"), ordered on the engine's
-    HIP stream.
+    each rank owns a bucket range of the index and a source-read range; 8-B
+    key records and 8-B window runs move to their bucket owners with
+    equal-split RCCL all-to-alls over xGMI (torch.distributed "nccl"), ordered
+    on the engine's HIP stream; every rank keeps the rows it verifies
+    (--route-rows: they move on to their src owners);
+  --multi bucket: each rank owns a bucket range of the index and scans EVERY
+    read, filing and keeping only its buckets' keys and runs, then probes
+    them; no data-path collective (SURVEY §8(e) alternative (i)): the scan
+    does not divide by P, but nothing crosses a link;
+  --multi replicated: every rank builds the whole index and discovers from
+    its source-read range; no data-path collective; SURVEY §8(e) alternative
+    (ii), kept as the comparison point (its index build and containment pass
+    do not divide by P).
 --sim-world P runs all P ranks of the chosen mode inside one process on one
-GPU (replicated: each rank timed alone, step = slowest rank; exchange:
-buffers exchanged on the device).
+GPU (replicated / bucket: each rank timed alone, step = slowest rank;
+exchange: buffers exchanged on the device).
 
 Prints ONE JSON line (rank 0).  See DESIGN.md §5 for the roofline numbers.
 """
@@ -369,12 +373,13 @@ def main():
                     help="run all SIM-WORLD ranks of the exchange mode in this process on one GPU")
     ap.add_argument("--exchange", action="store_true",
                     help="use the RCCL exchange mode even with one rank (checks the torch.distributed plumbing)")
-    ap.add_argument("--multi", choices=["auto", "replicated", "exchange"], default="auto",
-                    help="N > 1 (and --sim-world): auto (default) = replicated for one read length, exchange for "
-                         "mixed lengths; replicated = every rank builds the whole index and "
-                         "probes its source-read range, no data-path collective (SURVEY 8(e)(ii)); exchange "
-                         "(north_star, BASELINE configs[3]) = bucket-range index shards + RCCL all-to-all of keys, "
-                         "runs and rows (SURVEY 8(e) main design).  DESIGN.md 6c: per-rank tables + xGMI model")
+    ap.add_argument("--multi", choices=["auto", "replicated", "exchange", "bucket"], default="auto",
+                    help="N > 1 (and --sim-world): exchange (north_star, BASELINE configs[3]) = "
+                         "bucket-range index shards + RCCL all-to-all of 8-B key and run records; bucket = "
+                         "bucket-range index shards, every rank scans every read and keeps its buckets' runs, no "
+                         "data-path collective (SURVEY 8(e)(i)); replicated = every rank builds the whole index "
+                         "and probes its source-read range (SURVEY 8(e)(ii)); auto (default) = bucket for one read length "
+                         "on <= 4 ranks, else exchange.  DESIGN.md 6c")
     ap.add_argument("--route-rows", action="store_true",
                     help="exchange mode: route every row to the owner of its src after discovery (graph[u] by "
                          "source range; one more all-to-all); default: each rank keeps the rows it verified")
@@ -406,8 +411,13 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     cfg = CONFIGS[args.config]
     n, lo, hi, G, l, k, seed, desc = cfg
-    if args.multi == "auto":  # the replicated mode's containment pass does not divide by P
-        args.multi = "replicated" if lo == hi else "exchange"
+    if args.multi == "auto":
+        # DESIGN.md §6c (simulated per-rank tables + the xGMI model): one read length, up to 4
+        # ranks: the bucket mode (no data-path collective; the exchange's run streams cost
+        # more link time than the scan they save); more ranks or mixed lengths (containment
+        # needs every bucket): the exchange mode
+        Pm = world if world > 1 else max(1, args.sim_world)
+        args.multi = "bucket" if lo == hi and Pm <= 4 else "exchange"
     nthreads = max(2, 16 // max(1, world))
     ds, codes, lens, host_ingest_s = make_dataset(cfg, nthreads, args.config)
     N = ds.num_unique
@@ -439,8 +449,8 @@ def main():
         if args.multi == "exchange" or args.exchange:
             xchg = TorchExchange(torch.device("cuda", local))
             mode = "exchange"
-        else:
-            mode = "replicated"  # the process group only times the step (barrier, MAX of the clocks)
+        else:  # the process group only times the step (barrier, MAX of the clocks)
+            mode = args.multi
     elif args.sim_world > 1:
         if args.multi == "exchange":
             from metagenomics_amd.sharded import LocalExchange
@@ -448,17 +458,17 @@ def main():
             xchg = LocalExchange(args.sim_world, torch.device("cuda", local))
             mode = "exchange-sim"
         else:
-            mode = "replicated-sim"
+            mode = args.multi + "-sim"
     else:
         mode = "fused"
-    P = world if mode in ("exchange", "replicated") else max(1, args.sim_world)
+    P = world if mode in ("exchange", "replicated", "bucket") else max(1, args.sim_world)
 
     from metagenomics_amd.sharded import sharded_step, source_range
 
     engines = []
     layout_ms = 0.0
     t0 = time.time()
-    for r in ([rank] if mode in ("exchange", "replicated") else range(P)):
+    for r in ([rank] if mode in ("exchange", "replicated", "bucket") else range(P)):
         e = OverlapEngine(local)
         e.set_option("nb_log2", args.nb_log2)
         for kv in args.opt:
@@ -479,13 +489,13 @@ def main():
         engines.append(e)
     log(f"[bench] rank {rank}: upload {time.time() - t0:.2f}s ({mode}, P={P})")
 
-    rank_ms = [0.0] * len(engines)  # replicated-sim: per simulated rank, summed over the timed steps
+    rank_ms = [0.0] * len(engines)  # replicated-sim / bucket-sim: per simulated rank, summed over the timed steps
 
     def step():
         """one pass of the hot path; returns directed rows held by this process"""
-        if mode in ("fused", "replicated"):
+        if mode in ("fused", "replicated", "bucket"):
             return fused_step(engines[0]) if engines else 0
-        if mode == "replicated-sim":
+        if mode in ("replicated-sim", "bucket-sim"):
             tot = 0
             for i, e in enumerate(engines):  # the ranks one after the other, each timed alone
                 torch.cuda.synchronize(local)
@@ -552,7 +562,7 @@ def main():
     ms_step = (t1 - t0) * 1000.0 / args.steps
     dev_ms = {kk: v / args.steps for kk, v in dev_ms.items()}
     sim_rank_ms = None
-    if mode == "replicated-sim":
+    if mode in ("replicated-sim", "bucket-sim"):
         # P ranks with no data-path collective: the job's step is its slowest rank
         sim_rank_ms = [v / args.steps for v in rank_ms]
         ms_step = max(sim_rank_ms)
@@ -606,6 +616,8 @@ def main():
                 "frac": achieved / HBM_PEAK_GBS, "traffic": None,
                 "kernel": ("rank 0 step kernels (whole index build, scan + probe of its source range)"
                            if mode.startswith("replicated") else
+                           "rank 0 step kernels (scan of every read filing and keeping its buckets' keys and runs, "
+                           "probe of those runs)" if mode.startswith("bucket") else
                            "rank 0 step device wall (scan + run sort + key exchange + insert, "
                            "containment + discovery probes; ev0 -> discovery end on the engine's stream)"),
                 "alg_bytes_per_step": alg / P, "kernel_ms_per_step": kern_ms}
@@ -614,7 +626,11 @@ def main():
            "replicated-sim": f"{P} simulated ranks on 1 GPU (whole index each, source-read shards; step = slowest rank)",
            "exchange": f"{P} ranks: bucket-range index + source-range shards, RCCL all-to-all of 8-B key and "
                        f"run records" + (" and of the rows" if args.route_rows else ""),
-           "exchange-sim": f"{P} simulated ranks on 1 GPU (device-local exchange)"}[mode]
+           "exchange-sim": f"{P} simulated ranks on 1 GPU (device-local exchange)",
+           "bucket": f"{P} ranks: bucket-range index shards, every rank scans every read and keeps its buckets' "
+                     "runs, no data-path collective",
+           "bucket-sim": f"{P} simulated ranks on 1 GPU (bucket-range shards, every read scanned by each; "
+                         "step = slowest rank)"}[mode]
     res = {
         "metric": "overlap edges/sec",
         "value": edges / (ms_step / 1000.0),

@@ -39,6 +39,7 @@ struct mg_ctx {
   // slots [read_lo, read_hi) (clustered among themselves), so a shard's slot
   // range holds exactly its reference IDs.
   bool layout = true;
+  int layout_hash = 0;  // option "layout_hash": the layout's 16-mer hash (0 fmix32, 1 24-bit multiply-adds)
   uint32_t* d_id = nullptr;    // one of id_store[], or nullptr
   uint32_t* d_phys = nullptr;  // one of phys_store[], or nullptr
   uint32_t* id_store[2] = {nullptr, nullptr};  // a re-layout builds the maps in the unused pair
@@ -160,6 +161,11 @@ struct mg_ctx {
   // skips k_part's count pass (runs_counted: valid for the last scan)
   unsigned long long* d_rcnt = nullptr;
   size_t rcnt_cap = 0;
+  // k_xchg_keys' per-(flat region, rank) counts of the key records (keys first):
+  // mg_xchg_pack(MG_KEYS) skips k_part's count pass while keys_counted
+  unsigned long long* d_kblk = nullptr;
+  size_t kblk_cap = 0;
+  bool keys_counted = false;
   bool runs_counted = false;
   // mg_build_index leaves its timings (index_ms, shared_scan_ms) to be read once
   // its events have completed (settle_index_times): no host round trip between

@@ -1139,13 +1139,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(G > 1 ? 
         }
         if (flag) {
           v = mix64(funnel(w0, w1, (pos & 31) << 1) >> msh);
-          if (!INDEX) flag = owned(v & nbmask, p.nb_log2, p.rank, p.nranks);  // (index scans: all buckets)
+          // (an index scan keeps every bucket's runs unless it builds a bucket-range shard)
+          if (!INDEX || p.nranks > 1) flag = owned(v & nbmask, p.nb_log2, p.rank, p.nranks);
         }
       } else if (flag) {
         const uint64_t* g2 = p.words + (meta & 0xFFFFFFFFull) * slot_words(MAXW);
         const int pos = (int)((meta >> 32) & 1023u);
         v = mix64(funnel(g2[pos >> 5], g2[(pos >> 5) + 1], (pos & 31) << 1) >> msh);
-        if (!INDEX) flag = owned(v & nbmask, p.nb_log2, p.rank, p.nranks);
+        if (!INDEX || p.nranks > 1) flag = owned(v & nbmask, p.nb_log2, p.rank, p.nranks);
       }
       uint64_t at_rec = 0;  // the record's index in its region
       uint32_t grp_rec = 0;
@@ -1360,8 +1361,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(G > 1 ? 
       // measured slower: scan 3.06-3.13 vs 2.92-2.94 ms at C3, profiles/r03y_ab_scan.txt)
       if constexpr (!KEYREC) {
 #pragma unroll
-        for (int o = 0; o < 4; ++o)
-          if ((o != 1 || !p.skip_o1) && (o != 3 || !p.skip_o3) && !p.no_insert) cell_insert(p.cells, cb[o], p.cell_n, ce[o]);
+        for (int o = 0; o < 4; ++o)  // (a bucket-range shard files its own buckets' keys: local cell = bucket - cell_lo)
+          if ((o != 1 || !p.skip_o1) && (o != 3 || !p.skip_o3) && !p.no_insert && owned(cb[o], p.nb_log2, p.rank, p.nranks))
+            cell_insert(p.cells, cb[o] - p.cell_lo, p.cell_n, ce[o]);
       }
     } else if (INDEX && a < p.a_hi) {  // no keys (n <= l cannot pass setup_index): holes
       if (p.key0) p.key0[a] = kEmpty;
@@ -2403,31 +2405,51 @@ __global__ __launch_bounds__(kBlock) void k_part(PartParams p) {
 // caller's device counts).  One block per destination.
 __global__ __launch_bounds__(1024) void k_part_scan(unsigned long long* blk, uint32_t nblk, uint32_t nranks,
                                                     unsigned long long* totals) {
+  // thread t owns the contiguous blocks [t per, (t + 1) per): their sum, one
+  // block-wide scan of the 1,024 sums, then its blocks' offsets -- one
+  // synchronised scan per destination instead of one per 1,024 blocks
   __shared__ unsigned long long s_part[1024];
-  __shared__ unsigned long long s_base;
-  {
-    const uint32_t d = blockIdx.x;
-    if (threadIdx.x == 0) s_base = 0;
+  const uint32_t d = blockIdx.x, t = threadIdx.x;
+  const uint32_t per = (nblk + 1023) / 1024;
+  const uint32_t b0 = t * per, b1 = min(b0 + per, nblk);
+  // up to 8 blocks per thread (nblk <= 8,192): the counts stay in registers and
+  // their loads are all in flight at once (one round trip, not one per block)
+  constexpr uint32_t kRegs = 8;
+  unsigned long long v8[kRegs];
+  unsigned long long sum = 0;
+  if (per <= kRegs) {
+#pragma unroll
+    for (uint32_t i = 0; i < kRegs; ++i) v8[i] = b0 + i < b1 ? blk[(uint64_t)(b0 + i) * nranks + d] : 0ull;
+#pragma unroll
+    for (uint32_t i = 0; i < kRegs; ++i) sum += v8[i];
+  } else {
+    for (uint32_t b = b0; b < b1; ++b) sum += blk[(uint64_t)b * nranks + d];
+  }
+  s_part[t] = sum;
+  __syncthreads();
+  for (uint32_t o = 1; o < 1024; o <<= 1) {  // inclusive Hillis-Steele scan of the sums
+    const unsigned long long v = t >= o ? s_part[t - o] : 0;
     __syncthreads();
-    for (uint32_t b0 = 0; b0 < nblk; b0 += 1024) {
-      const uint32_t b = b0 + threadIdx.x;
-      const unsigned long long v = b < nblk ? blk[(uint64_t)b * nranks + d] : 0;
-      s_part[threadIdx.x] = v;
-      __syncthreads();
-      for (uint32_t o = 1; o < 1024; o <<= 1) {  // inclusive Hillis-Steele scan
-        const unsigned long long t = threadIdx.x >= o ? s_part[threadIdx.x - o] : 0;
-        __syncthreads();
-        s_part[threadIdx.x] += t;
-        __syncthreads();
-      }
-      if (b < nblk) blk[(uint64_t)b * nranks + d] = s_base + s_part[threadIdx.x] - v;
-      __syncthreads();
-      if (threadIdx.x == 1023) s_base += s_part[1023];
-      __syncthreads();
-    }
-    if (threadIdx.x == 0) totals[d] = s_base;
+    s_part[t] += v;
     __syncthreads();
   }
+  unsigned long long run = s_part[t] - sum;  // exclusive: the blocks before b0
+  if (per <= kRegs) {
+#pragma unroll
+    for (uint32_t i = 0; i < kRegs; ++i)
+      if (b0 + i < b1) {
+        blk[(uint64_t)(b0 + i) * nranks + d] = run;
+        run += v8[i];
+      }
+    if (t == 1023) totals[d] = s_part[1023];
+    return;
+  }
+  for (uint32_t b = b0; b < b1; ++b) {
+    const unsigned long long v = blk[(uint64_t)b * nranks + d];
+    blk[(uint64_t)b * nranks + d] = run;
+    run += v;
+  }
+  if (t == 1023) totals[d] = s_part[1023];
 }
 
 // Per-region counts of a slot-layout buffer cut into regions of `reg` records
@@ -2885,6 +2907,16 @@ namespace {
 // below / inside / above the range [lo, hi), so the range's reads take exactly
 // the slots [lo, hi).  One thread per slot (old_id: the slot's reference
 // ID - 1, nullptr = ID order).
+// a 32-bit hash from full-rate 24-bit multiply-adds (order_key's rounds,
+// keeping all 32 bits)
+__device__ __forceinline__ uint32_t lhash24(uint32_t x) {
+  uint32_t h = __umul24(x, 0x9E3779u) + (x >> 8);
+  h ^= h >> 15;
+  h = __umul24(h, 0xEBCA77u) + (h >> 8);
+  h ^= h >> 13;
+  h = __umul24(h, 0x85EBCAu) + (h >> 16);
+  return h;
+}
 __device__ __forceinline__ uint32_t fmix32(uint32_t x) {  // murmur3 finaliser (bijective)
   x ^= x >> 16;
   x *= 0x85ebca6bu;
@@ -2898,7 +2930,7 @@ template <int MAXW>
 __global__ __launch_bounds__(kBlock) void k_layout_keys(const uint64_t* __restrict__ words,
                                                        const uint16_t* __restrict__ len, uint64_t n,
                                                        const uint32_t* __restrict__ old_id, uint64_t lo, uint64_t hi,
-                                                       int grouped, int pb, uint64_t* __restrict__ key,
+                                                       int grouped, int pb, int hash24, uint64_t* __restrict__ key,
                                                        uint32_t* __restrict__ val) {
   const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
   if (i >= n) return;
@@ -2908,28 +2940,23 @@ __global__ __launch_bounds__(kBlock) void k_layout_keys(const uint64_t* __restri
   const int m = L < kM ? L : kM;
   const mer_t mmask = 2 * m == 8 * (int)sizeof(mer_t) ? ~(mer_t)0 : (((mer_t)1 << (2 * m)) - 1);
   const uint64_t* g = words + i * slot_words(MAXW);
-  // the read's words in flight together, then 32 bases per word with a
-  // compile-time shift (a load per 32 bases inside the loop made every word a
-  // dependent round trip: 0.75 ms at C3)
-  uint64_t rw[MAXW];
-#pragma unroll
-  for (int k = 0; k < MAXW; ++k) rw[k] = g[k];
   mer_t fw = 0, rc = 0;
   uint32_t best = 0xFFFFFFFFu, bpos = 0;
-#pragma unroll
-  for (int k = 0; k < MAXW; ++k) {
-    if (32 * k >= L) break;
-    const uint64_t cw = rw[k];
-#pragma unroll 8
-    for (int u = 0; u < 32; ++u) {
-      const int t = 32 * k + u;
-      const uint32_t b = (uint32_t)(cw >> (62 - 2 * u)) & 3u;
-      fw = ((fw << 2) | b) & mmask;
-      rc = (rc >> 2) | ((mer_t)(3u - b) << (2 * m - 2));
-      const uint32_t hv = fmix32(fw < rc ? fw : rc);
-      const bool take = t >= m - 1 && t < L && hv < best;  // the hash, leftmost on ties
-      best = take ? hv : best;
-      bpos = take ? (uint32_t)(t - m + 1) : bpos;
+  uint64_t cw = 0;
+  for (int t = 0; t < L; ++t) {
+    if ((t & 31) == 0) cw = g[t >> 5];
+    const uint32_t b = (uint32_t)(cw >> (62 - 2 * (t & 31))) & 3u;
+    fw = ((fw << 2) | b) & mmask;
+    rc = (rc >> 2) | ((mer_t)(3u - b) << (2 * m - 2));
+    if (t >= m - 1) {
+      const mer_t c = fw < rc ? fw : rc;
+      // fmix32 (two 32-bit multiplies, quarter rate) or, option layout_hash = 1,
+      // two full-rate 24-bit multiply-adds (ALU: the kernel is issue-bound)
+      const uint32_t hv = hash24 ? lhash24(c) : fmix32(c);
+      if (hv < best) {  // the hash, leftmost on ties
+        best = hv;
+        bpos = (uint32_t)(t - m + 1);
+      }
     }
   }
   const uint32_t pmax = (1u << pb) - 1u;
@@ -2988,7 +3015,7 @@ struct LaunchLayout {
   static int run(mg_ctx* ctx, uint64_t lo, uint64_t hi, int grouped, int pb, uint64_t* key, uint32_t* val) {
     const uint64_t n = ctx->n;
     hipLaunchKernelGGL((k_layout_keys<W>), dim3((uint32_t)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, ctx->stream,
-                       ctx->d_words, ctx->d_len, n, ctx->d_id, lo, hi, grouped, pb, key, val);
+                       ctx->d_words, ctx->d_len, n, ctx->d_id, lo, hi, grouped, pb, ctx->layout_hash, key, val);
     return hipGetLastError() == hipSuccess ? 0 : -1;
   }
 };
@@ -3129,14 +3156,29 @@ __global__ __launch_bounds__(kBlock) void k_index_keys(IndexParams p) {
 // keys (hashRead, HashTable.cpp:88-104) and rule as k_index_keys, written as
 // the KEYREC scan writes them: key o of source a at key_seg(o) * key_n + a - a_lo
 // (bucket, entry); o = 1 a hole when skip_o1.
+//   kblk (non-null): the routing pass's per-(region, destination) counts, region
+// = kFlatRegion records of the flat key array, so mg_xchg_pack runs no count
+// pass: a block's 256 sources put each key segment's records in at most two
+// regions, counted in LDS and added to kblk (cleared by the caller) with one
+// global atomic per (segment, region, destination)
 template <int MAXW>
 __global__ __launch_bounds__(kBlock) void k_xchg_keys(IndexParams p, uint64_t a_lo, uint64_t a_hi,
-                                                     uint32_t* __restrict__ key_bk, uint64_t* __restrict__ key_ent) {
+                                                     uint32_t* __restrict__ key_bk, uint64_t* __restrict__ key_ent,
+                                                     unsigned long long* __restrict__ kblk, uint32_t nranks) {
+  constexpr uint64_t kReg = 1024;  // (= kFlatRegion)
+  __shared__ unsigned int s_kc[4 * 2 * kMaxRanks];
   const int h = p.h, m = p.m, w = p.w;
   const int msh = 64 - 2 * m;
   const uint64_t mmask = (m == 32) ? ~0ULL : ((1ULL << (2 * m)) - 1);
   const uint64_t nbm = (1ULL << p.nb_log2) - 1, key_n = a_hi - a_lo;
-  for (uint64_t a = a_lo + (uint64_t)blockIdx.x * kBlock + threadIdx.x; a < a_hi; a += (uint64_t)gridDim.x * kBlock) {
+  const uint32_t ncnt = 4 * 2 * nranks;
+  for (uint64_t a0 = a_lo + (uint64_t)blockIdx.x * kBlock; a0 < a_hi; a0 += (uint64_t)gridDim.x * kBlock) {
+   if (kblk) {  // (block-uniform)
+     for (uint32_t i = threadIdx.x; i < ncnt; i += kBlock) s_kc[i] = 0;
+     __syncthreads();
+   }
+   const uint64_t a = a0 + threadIdx.x;
+   if (a < a_hi) {
     uint64_t rw[MAXW + 1];
     load_slot<MAXW>(p.words, (uint32_t)a, rw);
     const int n = p.len[a];
@@ -3169,8 +3211,27 @@ __global__ __launch_bounds__(kBlock) void k_xchg_keys(IndexParams p, uint64_t a_
       const uint64_t v = mix64(mb[o]);
       const uint64_t at = key_seg(o) * key_n + a - a_lo;
       key_bk[at] = (uint32_t)(v & nbm);
-      key_ent[at] = (o == 1 && p.skip_o1) ? kEmpty : make_entry(v, p.nb_log2, (int)(kb[o] & 1023u), o, (uint32_t)a, n);
+      const bool hole = o == 1 && p.skip_o1;
+      key_ent[at] = hole ? kEmpty : make_entry(v, p.nb_log2, (int)(kb[o] & 1023u), o, (uint32_t)a, n);
+      if (kblk && !hole) {  // k_part's OWN_KEY rule: owner = bucket range
+        const uint32_t d = (uint32_t)(((v & nbm) * nranks) >> p.nb_log2);
+        const uint32_t half = (uint32_t)(at / kReg - (key_seg(o) * key_n + a0 - a_lo) / kReg);
+        atomicAdd(&s_kc[((uint32_t)key_seg(o) * 2 + half) * nranks + d], 1u);
+      }
     }
+   }
+   if (kblk) {
+     __syncthreads();
+     for (uint32_t i = threadIdx.x; i < ncnt; i += kBlock) {
+       const uint32_t c = s_kc[i];
+       if (c) {
+         const uint32_t seg = i / (2 * nranks), half = (i / nranks) & 1u, d = i % nranks;
+         const uint64_t r = (seg * key_n + a0 - a_lo) / kReg + half;
+         atomicAdd(&kblk[r * nranks + d], (unsigned long long)c);
+       }
+     }
+     __syncthreads();  // (the next sources' counters are cleared after every lane read these)
+   }
   }
 }
 
@@ -3353,6 +3414,7 @@ struct LaunchScan {
     const size_t lds = scan_lds(ctx, index);
     sp.cells = ctx->d_cells;
     sp.cell_n = ctx->cell_n;
+    sp.cell_lo = ctx->cell_lo;  // (0 unless the cells are a bucket-range shard)
     if (index && ctx->key0_ready) {  // mg_build_index allocated it (mixed lengths)
       if (ctx->prefix_probe)
         sp.p0runs = ctx->d_p0runs;
@@ -3799,7 +3861,8 @@ void mg_destroy(mg_ctx* ctx) {
                   ctx->d_digest, ctx->id_store[0], ctx->id_store[1], ctx->phys_store[0], ctx->phys_store[1],
                   ctx->d_tmp32, ctx->d_lay_k[0], ctx->d_lay_k[1], ctx->d_lay_v[0], ctx->d_lay_v[1], ctx->d_lay_tmp,
                   ctx->d_words_alt, ctx->d_len_alt, ctx->d_cbits, ctx->d_ccnt, ctx->d_lcells, ctx->d_lkcells,
-                  ctx->d_rhead, ctx->d_rstart, ctx->d_rcnt, ctx->d_dcnt, ctx->d_p0runs, ctx->d_p0cnt, ctx->d_xexp};
+                  ctx->d_rhead, ctx->d_rstart, ctx->d_rcnt, ctx->d_dcnt, ctx->d_p0runs, ctx->d_p0cnt, ctx->d_xexp,
+                  ctx->d_kblk};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   for (auto& e : ctx->ev)
@@ -3996,6 +4059,10 @@ int mg_set_option(mg_ctx* ctx, const char* name, int64_t value) {
     ctx->max_blocks = value > 0 ? (uint32_t)value : 8192u;
     return 0;
   }
+  if (!strcmp(name, "layout_hash")) {  // slot layout's minimizer hash: 0 fmix32 (default), 1 24-bit multiplies
+    ctx->layout_hash = value ? 1 : 0;
+    return 0;
+  }
   if (!strcmp(name, "xchg_keys_first")) {  // exchange mode, equal lengths: key records first (default 1)
     ctx->xchg_keys_first = value != 0;
     return 0;
@@ -4189,8 +4256,21 @@ struct LaunchXchgKeys {
     p.skip_o1 = ctx->index_o1 ? 0 : 1;
     const uint32_t grid = (uint32_t)std::max<uint64_t>(
         1, std::min<uint64_t>((hi - lo + kBlock - 1) / kBlock, (uint64_t)ctx->n_cu * 16));
-    hipLaunchKernelGGL((k_xchg_keys<W>), dim3(grid), dim3(kBlock), 0, ctx->stream, p, lo, hi, ctx->d_kb, ctx->d_ke);
-    return hipGetLastError() == hipSuccess ? 0 : -1;
+    // the routing pass's counts per (flat region, destination): mg_xchg_pack's
+    // k_part then runs one block per region with no count pass
+    const uint64_t nreg = ((ctx->index_o1 ? 4 : 3) * (hi - lo) + kFlatRegion - 1) / kFlatRegion;
+    ctx->keys_counted = false;
+    unsigned long long* kblk = nullptr;
+    if (ctx->nranks > 1 && nreg && ctx->nranks <= kMaxRanks) {
+      MG_ENSURE(d_kblk, kblk_cap, nreg * ctx->nranks);
+      MG_TRY(hipMemsetAsync(ctx->d_kblk, 0, nreg * ctx->nranks * sizeof(unsigned long long), ctx->stream));
+      kblk = ctx->d_kblk;
+    }
+    hipLaunchKernelGGL((k_xchg_keys<W>), dim3(grid), dim3(kBlock), 0, ctx->stream, p, lo, hi, ctx->d_kb, ctx->d_ke,
+                       kblk, ctx->nranks);
+    if (hipGetLastError() != hipSuccess) return -1;
+    ctx->keys_counted = kblk != nullptr;
+    return 0;
   }
 };
 
@@ -4298,7 +4378,8 @@ struct LaunchScanAll {
     const uint32_t wpb = scan_block_waves(ctx, true);
     const uint64_t groups = (ctx->n + kWave - 1) / kWave;
     const uint32_t sgrid = scan_resident<W>(ctx, true, (groups + wpb - 1) / wpb);
-    return LaunchScan<W>::run(ctx, true, 0, ctx->n, sgrid, false, st, true, true);
+    // (a bucket-range shard of every source: its buckets' keys and runs only)
+    return LaunchScan<W>::run(ctx, true, 0, ctx->n, sgrid, ctx->nranks > 1, st, true, true);
   }
 };
 
@@ -4310,13 +4391,18 @@ struct LaunchScanRuns {
     const uint32_t wpb = scan_block_waves(ctx, false);
     const uint64_t groups = (ctx->n + kWave - 1) / kWave;
     const uint32_t sgrid = scan_resident<W>(ctx, false, (groups + wpb - 1) / wpb);
-    return LaunchScan<W>::run(ctx, true, 0, ctx->n, sgrid, false, ctx->stream, true, false);
+    return LaunchScan<W>::run(ctx, true, 0, ctx->n, sgrid, ctx->nranks > 1, ctx->stream, true, false);
   }
 };
 
 // one shared scan per build: an unsharded context over all its sources (a
 // source-read range takes the separate index build + a scan of its slots)
-bool shared_scan(const mg_ctx* ctx) { return ctx->nranks == 1 && ctx->read_lo == 0 && ctx->read_hi == 0; }
+// A bucket-range shard over every source (mg_set_shard(ctx, r, P, 0, 0), no
+// exchange: every rank scans every read) takes the same one pass, filing and
+// keeping only its own buckets' keys and runs (SURVEY §8(e) alternative (i)).
+bool shared_scan(const mg_ctx* ctx) {
+  return ctx->read_lo == 0 && ctx->read_hi == 0 && (ctx->nranks == 1 || ctx->minlen == ctx->maxlen);
+}
 
 // mg_build_index's timings from its events (before a rescan records ev[6] / ev[7] again)
 int settle_index_times(mg_ctx* ctx) {
@@ -5094,6 +5180,7 @@ int mg_xchg_begin(mg_ctx* ctx, uint32_t min_overlap, uint32_t seed_k) {
   // inserts riding on it (mixed lengths keep the one scan: their containment
   // and live index read the received key records sorted)
   ctx->keys_first = ctx->xchg_keys_first && ctx->nranks > 1 && ctx->minlen == ctx->maxlen;
+  ctx->keys_counted = false;  // (set by k_xchg_keys' launch: the scan's key records take k_part's count pass)
   if (ctx->keys_first) {
     ctx->nrun_reg = 0;
     if (hi > lo && dispatch_w<LaunchXchgKeys>(ctx->maxw, ctx, lo, hi)) return launch_fail(ctx, "key records launch failed");
@@ -5148,6 +5235,8 @@ int mg_xchg_pack(mg_ctx* ctx, int what, void* dst, uint64_t slot, uint32_t round
     pp.key_n = nsrc;  // (key o of source a - xchg_lo at o * nsrc + a - xchg_lo)
     pp.a_lo = 0;
     pp.nsrc = nsrc;
+    if (ctx->keys_counted && pp.nreg)  // k_xchg_keys counted them per (region, rank): no count pass
+      return route_slots<OWN_KEY>(ctx, pp, dst, self_dst, slot, rounds, cnt, ctx->d_kblk);
     return route_slots<OWN_KEY>(ctx, pp, dst, self_dst, slot, rounds, cnt);
   }
   if (what == MG_RUNS) {  // the scan's run regions, each run to its bucket's owner

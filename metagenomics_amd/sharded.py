@@ -477,13 +477,9 @@ def _step(engines, xchg, min_overlap, seed_k, want_super, plan, route_rows):
     def route(kind, move=True):
         """pack `kind` on every engine; move=False leaves the all-to-all to the caller
         (returns the pack's buffers: (sends, recvs, counts), slot, rounds)"""
-        if P == 1:  # one rank: every stream is its own, nothing is packed (counts = 0)
-            cnts = []
-            for e in engines:
-                c = xchg.counts()
-                e.xchg_pack(kind, 0, 1, 1, c.data_ptr(), 0)
-                done()
-                cnts.append(c)
+        if P == 1:  # one rank: every stream is its own, nothing is packed or sent (the
+            # consumers read the context's own key records and run regions; counts = 0)
+            cnts = [zero] * len(engines)
             sent[kind] = cnts
             geo[kind] = (0, 0)
             return [(None, c) for c in cnts], 0, 0
@@ -506,6 +502,7 @@ def _step(engines, xchg, min_overlap, seed_k, want_super, plan, route_rows):
             return (sends, recvs, cnts), slot, rounds
         return xchg.all_to_all_slots(sends, recvs, cnts, slot, rounds, rb), slot, rounds
 
+    zero = xchg.counts().zero_() if P == 1 else None
     t0 = time.perf_counter()
     with xchg.streams(engines):
         # 1. one scan of the rank's sources: index keys + sorted runs
@@ -573,7 +570,9 @@ def _step(engines, xchg, min_overlap, seed_k, want_super, plan, route_rows):
         if route_rows:
             rows, ws, wr = route(MG_ROWS)
         # the step's one host read: MAX over ranks of every per-peer send count
-        mx = xchg.max_counts([[sent[k][i] for k in kinds] for i in range(len(engines))])
+        # (one rank: nothing was sent, so no collective and no host read of counts)
+        mx = (xchg.max_counts([[sent[k][i] for k in kinds] for i in range(len(engines))]) if P > 1
+              else np.zeros(len(kinds), dtype=np.int64))
         n_rows = [int(c.sum().item()) for _, c in rows] if route_rows else [e.num_rows() for e in engines]
         # (the key and run buffers stay referenced until here: with LocalExchange the
         # engines' streams may still read them when a del would let torch reuse the memory)

@@ -121,10 +121,12 @@ def test_ascii_upload_equals_packed(engine):
     assert np.array_equal(rows_to_tuples(rows), golden_rows("mixed"))
 
 
-@pytest.mark.parametrize("name,nranks", [("small", 2), ("highdup", 3), ("tworead", 2)])
+@pytest.mark.parametrize("name,nranks", [("small", 2), ("highdup", 3), ("tworead", 2), ("highdup", 5), ("small", 8)])
 def test_bucket_shards_union(engine, name, nranks):
     """Bucket-range sharding through the single-context entry
-    points: the union over ranks is the multiset.  Equal-length sets only: a
+    points (bench --multi bucket: every rank's one scan of every read files and
+    keeps only its buckets' keys and runs): the union over ranks is the
+    multiset.  Equal-length sets only: a
     bucket shard cannot settle containment alone (markContainedReads needs every
     bucket), which is what the exchange mode's MAX all-reduce does
     (test_exchange_mode_* cover the mixed-length fixtures)."""

@@ -228,6 +228,39 @@ def test_exchange_scale_digest(name, world, route):
 
 @pytest.mark.gpu
 @pytest.mark.timeout(900)
+@pytest.mark.parametrize("name,world", [("c3", 8), ("c2", 3)])
+def test_bucket_scale_digest(name, world):
+    """The bucket mode (bench --multi bucket, SURVEY §8(e) alternative (i)):
+    `world` bucket-range shards over every source, each context's one scan of
+    every read filing and keeping only its buckets' keys and runs, then its probe;
+    no data-path collective.  The union of the ranks' rows has the reference's
+    digest."""
+    from metagenomics_amd.overlap import OverlapEngine
+
+    if not os.path.exists(SCALE[name]):
+        pytest.skip(f"{name}.json not generated")
+    m, ds = scale_dataset(name)
+    engines = []
+    try:
+        digests = []
+        for r in range(world):
+            e = OverlapEngine(0)
+            e.set_option("layout_scratch", 0)
+            e.set_shard(r, world, 0, 0)
+            e.upload(ds)
+            engines.append(e)
+            e.build_index(m["workload"]["min_overlap"], 31)
+            e.mark_contained(copy=False)
+            assert e.find_overlaps() > 0
+            digests.append(e.rows_digest())
+        assert combine(digests) == m["rows"]
+    finally:
+        for e in engines:
+            e.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(900)
 @pytest.mark.parametrize("name,launcher", [("c3", "direct"), ("c5s", "torchrun")])
 def test_cli_exchange_over_rccl(name, launcher, tmp_path):
     """The C++ host's exchange mode (mg_overlap -xchg, metagenomics_amd/csrc/host/
@@ -288,13 +321,14 @@ def test_exchange_two_processes(name):
 
 @pytest.mark.gpu
 @pytest.mark.timeout(900)
-@pytest.mark.parametrize("name,mode", [("c2", "whole index on every rank"), ("c5s", "bucket-range index")])
+@pytest.mark.parametrize("name,mode", [("c2", "bucket-range index"), ("c5s", "bucket-range index")])
 def test_two_processes_default_mode(name, mode):
-    """bench.py --gpus N with no --multi (auto: the replicated mode for one read
-    length, the exchange mode for mixed lengths) as the driver's
-    N-GPU runs launch it: two torchrun processes, each rank's own context; gloo
-    for the barrier and the clocks (two ranks share this one GPU).  The rows and
-    superReadIDs over both ranks have the reference's digests."""
+    """bench.py --gpus N with no --multi (auto, DESIGN.md §6c: the bucket mode for
+    one read length on 2 ranks (c2), the exchange mode for mixed lengths (c5s);
+    both bucket-range index shards) as the driver's N-GPU runs launch it: two
+    torchrun processes, each rank's own context; gloo stages the all-to-alls
+    (two ranks share this one GPU).  The rows and superReadIDs over both ranks
+    have the reference's digests."""
     import subprocess
     import sys
 
@@ -308,4 +342,30 @@ def test_two_processes_default_mode(name, mode):
     assert out.returncode == 0, out.stderr[-3000:]
     r = json.loads([x for x in out.stdout.splitlines() if x.startswith("{")][-1])
     assert r["n_gpus"] == 2 and mode in r["config"]["parallelism"]
+    assert r["parity"]["golden"] and r["parity"]["digest_ok"] is True, r["parity"]
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("mode,desc", [("replicated", "whole index on every rank"),
+                                       ("bucket", "every rank scans every read")])
+def test_two_processes_no_collective_modes(mode, desc):
+    """bench.py --gpus 2 --multi replicated / bucket (SURVEY §8(e) alternatives
+    (ii) / (i)): the whole index on every rank with
+    source-read shards, or bucket-range shards scanning every read; no data-path
+    collective; the union has the reference's C2 digest."""
+    import subprocess
+    import sys
+
+    if not os.path.exists(SCALE["c2"]):
+        pytest.skip("c2.json not generated")
+    env = dict(os.environ, MG_BENCH_PG_BACKEND="gloo")
+    args = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+            "--master-addr", "127.0.0.1", "--master-port", "29737", os.path.join(ROOT, "bench.py"),
+            "--gpus", "2", "--config", "c2", "--multi", mode, "--steps", "1", "--warmup", "1",
+            "--no-cpu-baseline", "--no-ingest"]
+    out = subprocess.run(args, capture_output=True, text=True, timeout=800, env=env)
+    assert out.returncode == 0, out.stderr[-3000:]
+    r = json.loads([x for x in out.stdout.splitlines() if x.startswith("{")][-1])
+    assert r["n_gpus"] == 2 and desc in r["config"]["parallelism"]
     assert r["parity"]["golden"] and r["parity"]["digest_ok"] is True, r["parity"]

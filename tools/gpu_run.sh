@@ -31,6 +31,11 @@ for s in $STEPS; do
       timeout -k 10 600 python -u bench.py --config ${SIMREP_CONFIG:-c3} --sim-world $P --multi replicated --steps 3 --no-cpu-baseline --no-ingest $SIMOPTS > $OUT/bench_simrep${P}_${SIMREP_CONFIG:-c3}.json 2> $OUT/bench_simrep$P.err
       rc=$?; echo "bench sim replicated $P rc=$rc"; python3 -c "import json;d=json.load(open('$OUT/bench_simrep${P}_${SIMREP_CONFIG:-c3}.json'));print(round(d['ms_per_step'],3), d['value'], d['undirected_edges'], d['parity'].get('digest_ok'), [round(x,3) for x in d.get('sim_rank_ms')], {k:round(v,3) for k,v in d['device_ms'].items()})"; [ $rc -ne 0 ] && break
     done ;;
+  simbkt)
+    for P in ${SIMP:-2 4 8}; do
+      timeout -k 10 600 python -u bench.py --config ${SIMREP_CONFIG:-c3} --sim-world $P --multi bucket --steps 3 --no-cpu-baseline --no-ingest $SIMOPTS > $OUT/bench_simbkt${P}_${SIMREP_CONFIG:-c3}.json 2> $OUT/bench_simbkt$P.err
+      rc=$?; echo "bench sim bucket $P rc=$rc"; python3 -c "import json;d=json.load(open('$OUT/bench_simbkt${P}_${SIMREP_CONFIG:-c3}.json'));print(round(d['ms_per_step'],3), d['value'], d['undirected_edges'], d['parity'].get('digest_ok'), [round(x,3) for x in d.get('sim_rank_ms')], {k:round(v,3) for k,v in d['device_ms'].items()})"; [ $rc -ne 0 ] && break
+    done ;;
   xchg1)
     timeout -k 10 300 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29511 bench.py --exchange --steps 5 --no-cpu-baseline --no-ingest > $OUT/bench_xchg1.json 2> $OUT/bench_xchg1.err
     rc=$?; echo "bench exchange(RCCL, 1 rank) rc=$rc"; python3 -c "import json;d=json.load(open('$OUT/bench_xchg1.json'));print('ms/step',round(d['ms_per_step'],3),'edges',d['undirected_edges'],'digest_ok',d['parity'].get('digest_ok'),'reruns',d.get('exchange_reruns'),{k:round(v,3) for k,v in d['device_ms'].items()},d.get('phase_wall_ms'))" ;;
@@ -39,7 +44,7 @@ for s in $STEPS; do
     timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/profxchg1 -o kt -- python3 bench.py --exchange --steps 5 --no-cpu-baseline --no-ingest > $OUT/profxchg1_bench.json 2> $OUT/profxchg1_bench.err
     rc=$?; unset MASTER_ADDR MASTER_PORT RANK WORLD_SIZE LOCAL_RANK; echo "profxchg1 rc=$rc"; cat $OUT/profxchg1_bench.json; head -24 $OUT/profxchg1/kt_kernel_stats.csv | cut -c1-160 ;;
   newtests)
-    timeout -k 10 900 python -u -m pytest tests/test_gpu_parity.py tests/test_long_reads.py -x -v -m gpu -k "exchange or live_index or falls_back" --timeout 300 --timeout-method thread > $OUT/new_tests.log 2>&1
+    timeout -k 10 900 python -u -m pytest tests/test_gpu_parity.py tests/test_long_reads.py -x -v -m gpu -k "${KT:-exchange or live_index or falls_back}" --timeout 300 --timeout-method thread > $OUT/new_tests.log 2>&1
     rc=$?; echo "new tests rc=$rc"; grep -E "PASS|FAIL|Error" $OUT/new_tests.log | tail -40 ;;
   xdigest)
     timeout -k 10 1100 python -u -m pytest tests/test_scale_digest.py -x -v -m gpu -k "exchange_scale" --timeout 1000 --timeout-method thread > $OUT/xdigest_tests.log 2>&1
@@ -148,6 +153,18 @@ for s in $STEPS; do
   profsim)
     timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/profsim -o kt -- python3 bench.py --sim-world 4 --multi exchange --steps 2 --no-cpu-baseline > $OUT/profsim_bench.json 2> $OUT/profsim_bench.err
     rc=$?; echo "profsim rc=$rc"; cat $OUT/profsim_bench.json; cat $OUT/profsim/kt_kernel_stats.csv ;;
+  pmclist)
+    timeout -k 10 120 rocprofv3 -L > $OUT/counters_all.txt 2>&1
+    rc=$?; echo "pmclist rc=$rc"; grep -oE '\b(TA|TD|TCP|TCC)_[A-Z0-9_]+' $OUT/counters_all.txt | sort -u > $OUT/counters_mem.txt; wc -l $OUT/counters_mem.txt ;;
+  pmcset)
+    # one pass per $PMCSETS entry (';'-separated counter sets) over a 1-step C3 bench
+    i=0; IFS=';' read -ra SETS <<< "$PMCSETS"
+    for set in "${SETS[@]}"; do
+      i=$((i+1))
+      timeout -s KILL 120 rocprofv3 --pmc $set --kernel-trace --output-format csv -d $OUT/pmcset_$i -o p -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-ingest --no-one-shot > $OUT/pmcset_$i.log 2>&1
+      rc=$?; echo "pmcset $i rc=$rc"; [ $rc -ne 0 ] && break
+    done
+    [ $rc -eq 0 ] && python3 tools/pmc_summary.py $OUT/pmcset_summary.json $OUT/pmcset_* > /dev/null ;;
   pmcsq)
     i=0
     for set in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY SQ_INSTS_VALU SQ_INSTS_VMEM_RD" \

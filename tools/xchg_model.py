@@ -9,8 +9,9 @@ measurements on ONE MI355X:
   records moved between ranks, summed over the ranks, and the bytes per record on the
   wire -- round 6: keys and runs 8 B, rows 12 B and only when routed), plus the MAX
   all-reduce of the n x 8 B containment keys when lengths differ;
-* replicated mode: the slowest simulated rank of
-  `bench.py --multi replicated --sim-world P` (no data-path collective).
+* replicated mode and bucket mode (every rank scans every read, keeps its
+  buckets' keys and runs): the slowest simulated rank of `bench.py --multi replicated|bucket
+  --sim-world P` (no data-path collective).
 
 xGMI (MI355X, one node): every GPU has 7 point-to-point links to its 7 peers.  An
 all-to-all moves each peer's share over that peer's own link, all links at once, so its
@@ -25,12 +26,15 @@ Two bounds: "serial" = compute + every transfer after it; "overlap" = what the h
 while the received keys are sorted and filed, and -- equal lengths, no containment pass --
 while each rank probes its own run stream (mg_xchg_probe_own, ~1/P of the probe); with
 containment the runs must all be in before the containment probe, so only the key build
-hides them.  "+rows" lines add the rows' all-to-all (12-B mg_edge records to their src
+hides them.  Keys first (the default since round 6: keys inserted inside the receiver's
+scan) leaves no key build to hide the runs behind, so only the own-stream probe does,
+and only up to P = 4 (xchg_split_max).  "+rows" lines add the rows' all-to-all (12-B mg_edge records to their src
 owners, bench.py --route-rows), estimated from the measured row count, after the probe.
 
 usage: xchg_model.py OUT.md FUSED_BENCH.json CONFIG DIR
   DIR holds profsim{P}_{CONFIG}_ranks.md, profsim{P}_{CONFIG}_bench.json and
-  bench_simrep{P}_{CONFIG}.json (replicated; bench_simrep{P}.json for c3) for P in 2 4 8."""
+  bench_simrep{P}_{CONFIG}.json / bench_simbkt{P}_{CONFIG}.json (replicated / bucket; without
+  the _{CONFIG} suffix for c3) for P in 2 4 8."""
 import json
 import os
 import re
@@ -39,6 +43,7 @@ import sys
 LINKS = (64.0, 76.5, 153.0)    # GB/s per direction per link
 ALPHA_MS = 0.030               # per collective round
 OLD_REC_BYTES = {"keys": 16, "runs": 16, "rows": 12}  # (bench lines before round 6 carry no record_bytes)
+SPLIT_MAX = 4                  # mg_ctx xchg_split_max: the discovery probe is split up to P = 4
 KEY_BUILD = ("k_xkeys_dense", "k_key_class", "k_cells_", "k_over_heads",
              "rocprim::trampoline_kernel<rocprim::wrapped_radix_sort", "rocprim::trampoline_kernel<rocprim::wrapped_scan")
 
@@ -76,9 +81,12 @@ def main():
         bj = os.path.join(d, f"profsim{P}_{cfg}_bench.json")
         if os.path.exists(md) and os.path.exists(bj):
             comp = step_compute_ms(md)
-            keybuild = sum(kernel_ms(md, k) for k in KEY_BUILD)
+            # the sorted key build (k_xkeys_dense + sort + cell fill) runs while the runs travel;
+            # keys first (round 6 default) inserts the keys inside the scan, before the runs exist
+            keybuild = sum(kernel_ms(md, k) for k in KEY_BUILD) if kernel_ms(md, "k_xkeys_dense") else 0.0
             probe = kernel_ms(md, "k_probe")
-            own_probe = 0.0 if mixed else probe / P  # mg_xchg_probe_own: the rank's own stream
+            # mg_xchg_probe_own: the rank's own stream, ~1/P of the probe (equal lengths, P <= 4)
+            own_probe = 0.0 if mixed or P > SPLIT_MAX else probe / P
             pad = json.load(open(bj))["exchange_padding"]
             per_kind = {k: v["moved_records"] * (v.get("record_bytes") or OLD_REC_BYTES[k]) / P
                         for k, v in pad.items()}  # bytes per rank
@@ -106,17 +114,18 @@ def main():
                                         "transfer_ms": xfer, "wall_serial_ms": serial, "wall_overlap_ms": overlap,
                                         "key_build_ms": keybuild, "own_probe_ms": own_probe,
                                         "speedup_overlap": t1 / overlap})
-        rj = os.path.join(d, f"bench_simrep{P}_{cfg}.json")
-        if not os.path.exists(rj) and cfg == "c3":
-            rj = os.path.join(d, f"bench_simrep{P}.json")
-        if os.path.exists(rj):
-            r = json.load(open(rj))
-            w = max(r["sim_rank_ms"])
-            lines.append(f"| replicated | {P} | {w:.3f} | 0 | — | 0 | {w:.3f} | {w:.3f} | "
-                         f"{t1 / w:.2f}x / {t1 / w:.2f}x |")
-            res["rows"].append({"mode": "replicated", "P": P, "compute_ms": w, "bytes_per_rank": 0,
-                                "wall_serial_ms": w, "wall_overlap_ms": w, "speedup_overlap": t1 / w,
-                                "digest_ok": r["parity"].get("digest_ok")})
+        for mode, stem in (("replicated", "simrep"), ("bucket", "simbkt")):
+            rj = os.path.join(d, f"bench_{stem}{P}_{cfg}.json")
+            if not os.path.exists(rj) and cfg == "c3":
+                rj = os.path.join(d, f"bench_{stem}{P}.json")
+            if os.path.exists(rj):
+                r = json.load(open(rj))
+                w = max(r["sim_rank_ms"])
+                lines.append(f"| {mode} | {P} | {w:.3f} | 0 | — | 0 | {w:.3f} | {w:.3f} | "
+                             f"{t1 / w:.2f}x / {t1 / w:.2f}x |")
+                res["rows"].append({"mode": mode, "P": P, "compute_ms": w, "bytes_per_rank": 0,
+                                    "wall_serial_ms": w, "wall_overlap_ms": w, "speedup_overlap": t1 / w,
+                                    "digest_ok": r["parity"].get("digest_ok")})
     lines.append("")
     lines.append(f"Link model: all-to-all = per-peer share / link rate (P - 1 links at once); ring all-reduce "
                  f"of the containment keys over P - 1 links; {ALPHA_MS * 1e3:.0f} us per collective round.  Compute = "
