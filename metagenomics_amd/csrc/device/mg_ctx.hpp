@@ -163,6 +163,11 @@ struct mg_ctx {
   size_t rcnt_cap = 0;
   // k_xchg_keys' per-(flat region, rank) counts of the key records (keys first):
   // mg_xchg_pack(MG_KEYS) skips k_part's count pass while keys_counted
+  // the keys-first receiver scan's run regions hold 8-B metas, d_rdst their owner ranks
+  uint8_t* d_rdst = nullptr;
+  size_t rdst_cap = 0;
+  bool runs_meta8 = false;
+  uint64_t super_zero_n = 0;  // leading d_super entries known to be 0 (skips the equal-length clear)
   unsigned long long* d_kblk = nullptr;
   size_t kblk_cap = 0;
   bool keys_counted = false;

@@ -888,6 +888,10 @@ struct ScanParams {
   const unsigned long long* recv_cnt;
   uint64_t recv_slot, recv_total, cell_lo;
   uint32_t recv_P;
+  // k_scan<RECV>: what leaves the rank is the run's 8-B meta, so the regions
+  // hold 8-B metas (runs viewed as uint64_t, same region positions) and
+  // run_dst the owner rank of each (k_part<OWN_META> routes them)
+  uint8_t* run_dst;
 };
 
 // Exchange-mode key records are o-major in the order o = 0, 2, 3, 1: when the
@@ -1154,11 +1158,18 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(G > 1 ? 
         const uint64_t bal = __ballot(flag);
         const uint64_t at = cur[0] + lane_prefix(bal);
         at_rec = at;
+        if constexpr (RECV) {  // the meta and its owner rank (the hash stays here: the owner re-hashes)
+          if (flag && at < p.run_cap) {
+            reinterpret_cast<uint64_t*>(p.runs)[gw * p.run_cap + at] = meta;
+            p.run_dst[gw * p.run_cap + at] = (uint8_t)(((v & nbmask) * p.dst_ranks) >> p.nb_log2);
+          }
+        } else {
 #if defined(MG_DIAG_STORE_NEVER)
         if (flag && at < p.run_cap && v == 0x0123456789ABCDEFull) region[at] = make_ulonglong2(v, meta);
 #elif !defined(MG_DIAG_NO_RUNSTORE)
         if (flag && at < p.run_cap) region[at] = make_ulonglong2(v, meta);
 #endif
+        }
         cur[0] += (uint64_t)__popcll(bal);
       } else {
 #ifdef MG_DIAG_ONE_REGION  // (diagnostics build: every run of a window into its first region)
@@ -2297,7 +2308,9 @@ __global__ __launch_bounds__(kBlock) void k_compact_rows(const uint32_t* __restr
 //            travels is the 8-B meta alone (read slot | p | jlo | jhi): the owner
 //            re-hashes the minimizer m-mer at p of its copy of the read
 //            (k_xruns_expand), so a run costs 8 B on xGMI instead of 16.
-enum OwnerKind { OWN_KEY = 0, OWN_SRC = 1, OWN_BUCKET = 2 };
+//   OWN_META: the keys-first receiver scan's regions (k_scan<RECV>): 8-B metas
+//            with their owner rank beside them in dst8 (one byte per record).
+enum OwnerKind { OWN_KEY = 0, OWN_SRC = 1, OWN_BUCKET = 2, OWN_META = 3 };
 constexpr int kMaxRanks = 64;
 
 struct PartParams {
@@ -2315,6 +2328,7 @@ struct PartParams {
   const uint32_t* key_bk;           // OWN_KEY: sources [a_lo, a_lo + nsrc), key o of read a at o * key_n + a
   const uint64_t* key_ent;
   uint64_t key_n, a_lo, nsrc;
+  const uint8_t* dst8;              // OWN_META: each record's owner rank
 };
 
 template <int KIND, int PASS>
@@ -2351,6 +2365,9 @@ __global__ __launch_bounds__(kBlock) void k_part(PartParams p) {
         } else if (KIND == OWN_BUCKET) {
           q.x16 = reinterpret_cast<const ulonglong2*>(p.base)[r * p.cap + i];
           q.d = (uint32_t)(((q.x16.x & ((1ULL << p.nb_log2) - 1)) * p.nranks) >> p.nb_log2);
+        } else if (KIND == OWN_META) {
+          q.x16.y = reinterpret_cast<const uint64_t*>(p.base)[r * p.cap + i];
+          q.d = p.dst8[r * p.cap + i];
         } else {
           q.x12 = reinterpret_cast<const uint3*>(p.base)[r * p.cap + i];
           q.d = (uint32_t)(((uint64_t)q.x12.x * p.nranks - 1) / p.n_reads);  // src is the 1-based ID
@@ -2408,7 +2425,7 @@ __global__ __launch_bounds__(1024) void k_part_scan(unsigned long long* blk, uin
   // thread t owns the contiguous blocks [t per, (t + 1) per): their sum, one
   // block-wide scan of the 1,024 sums, then its blocks' offsets -- one
   // synchronised scan per destination instead of one per 1,024 blocks
-  __shared__ unsigned long long s_part[1024];
+  __shared__ unsigned long long s_part[16];
   const uint32_t d = blockIdx.x, t = threadIdx.x;
   const uint32_t per = (nblk + 1023) / 1024;
   const uint32_t b0 = t * per, b1 = min(b0 + per, nblk);
@@ -2425,15 +2442,24 @@ __global__ __launch_bounds__(1024) void k_part_scan(unsigned long long* blk, uin
   } else {
     for (uint32_t b = b0; b < b1; ++b) sum += blk[(uint64_t)b * nranks + d];
   }
-  s_part[t] = sum;
-  __syncthreads();
-  for (uint32_t o = 1; o < 1024; o <<= 1) {  // inclusive Hillis-Steele scan of the sums
-    const unsigned long long v = t >= o ? s_part[t - o] : 0;
-    __syncthreads();
-    s_part[t] += v;
-    __syncthreads();
+  // inclusive scan of the 1,024 sums: within each wavefront by shuffles, then
+  // the 16 wavefront totals through LDS (two barriers, not twenty)
+  const int lane = (int)(t & 63u), wv = (int)(t >> 6);
+  unsigned long long inc = sum;
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1) {
+    const unsigned long long v = (unsigned long long)__shfl_up((long long)inc, o);
+    if (lane >= o) inc += v;
   }
-  unsigned long long run = s_part[t] - sum;  // exclusive: the blocks before b0
+  if (lane == kWave - 1) s_part[wv] = inc;
+  __syncthreads();
+  unsigned long long before = 0, total = 0;
+  for (int w2 = 0; w2 < 16; ++w2) {
+    const unsigned long long x = s_part[w2];
+    before += w2 < wv ? x : 0ull;
+    total += x;
+  }
+  unsigned long long run = before + inc - sum;  // exclusive: the blocks before b0
   if (per <= kRegs) {
 #pragma unroll
     for (uint32_t i = 0; i < kRegs; ++i)
@@ -2441,7 +2467,7 @@ __global__ __launch_bounds__(1024) void k_part_scan(unsigned long long* blk, uin
         blk[(uint64_t)(b0 + i) * nranks + d] = run;
         run += v8[i];
       }
-    if (t == 1023) totals[d] = s_part[1023];
+    if (t == 1023) totals[d] = total;
     return;
   }
   for (uint32_t b = b0; b < b1; ++b) {
@@ -2449,7 +2475,7 @@ __global__ __launch_bounds__(1024) void k_part_scan(unsigned long long* blk, uin
     blk[(uint64_t)b * nranks + d] = run;
     run += v;
   }
-  if (t == 1023) totals[d] = s_part[1023];
+  if (t == 1023) totals[d] = total;
 }
 
 // Per-region counts of a slot-layout buffer cut into regions of `reg` records
@@ -3425,6 +3451,7 @@ struct LaunchScan {
     sp.skip_o3 = (index && !ctx->index_o3 && !ctx->xchg) ? 1 : 0;
     sp.no_insert = (index && ctx->phase_limit == 1) ? 1 : 0;
     const bool recv = ctx->rk_on;
+    ctx->runs_meta8 = false;  // (set below by the keys-first receiver scan)
     if ((index || recv) && ctx->xchg) ctx->runs_counted = false;
     // the exchange scan counts its runs per destination rank as it stores them
     // (the register scan per region, k_scan<KEYREC> per region and group: G P <= 64)
@@ -3459,6 +3486,9 @@ struct LaunchScan {
       allow_lds(k_scan<W, true, true>, lds);
       hipLaunchKernelGGL((k_scan<W, true, true>), dim3(sgrid), dim3(wpb * kWave), lds, stream, sp);
     } else if (recv) {  // exchange mode, keys first: the runs + the received keys' CAS inserts
+      MG_ENSURE(d_rdst, rdst_cap, run_cap * nreg);
+      sp.run_dst = ctx->d_rdst;
+      ctx->runs_meta8 = true;
       sp.recv_keys = ctx->rk_keys;
       sp.recv_cnt = ctx->rk_cnt;
       sp.recv_slot = ctx->rk_slot;
@@ -3862,7 +3892,7 @@ void mg_destroy(mg_ctx* ctx) {
                   ctx->d_tmp32, ctx->d_lay_k[0], ctx->d_lay_k[1], ctx->d_lay_v[0], ctx->d_lay_v[1], ctx->d_lay_tmp,
                   ctx->d_words_alt, ctx->d_len_alt, ctx->d_cbits, ctx->d_ccnt, ctx->d_lcells, ctx->d_lkcells,
                   ctx->d_rhead, ctx->d_rstart, ctx->d_rcnt, ctx->d_dcnt, ctx->d_p0runs, ctx->d_p0cnt, ctx->d_xexp,
-                  ctx->d_kblk};
+                  ctx->d_kblk, ctx->d_rdst};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   for (auto& e : ctx->ev)
@@ -5003,7 +5033,9 @@ int mg_mark_contained(mg_ctx* ctx, uint32_t* super_out) {
   ctx->err.clear();  // (a message left by an earlier failed call is not this call's cause)
   MG_TRY(hipSetDevice(ctx->device));
   if (!ctx->index_ready) return set_err(ctx, "mg_build_index must run first");
+  const uint32_t* super_was = ctx->d_super;
   MG_ENSURE(d_super, super_cap, ctx->n + 1);
+  if (ctx->d_super != super_was) ctx->super_zero_n = 0;  // (a new buffer: nothing known about it)
   MG_ENSURE(d_cbits, cbits_cap, (ctx->n + 63) / 64 * 2);
   if (!ctx->d_any) MG_TRY(hipMalloc(&ctx->d_any, sizeof(unsigned int)));
   ctx->t.contained_ms = 0.f;
@@ -5033,6 +5065,7 @@ int mg_mark_contained(mg_ctx* ctx, uint32_t* super_out) {
     if (ctx->n)
       hipLaunchKernelGGL(k_super_finalize, dim3(super_grid(ctx)), dim3(kBlock), 0,
                          ctx->stream, ctx->d_superkey, ctx->n, ctx->d_super, ctx->d_any, ctx->d_cbits, ctx->d_ccnt);
+    ctx->super_zero_n = 0;
     MG_TRY(hipGetLastError());
     MG_TRY(hipEventRecord(ctx->ev[3], ctx->stream));
     unsigned int any = 0;
@@ -5057,7 +5090,12 @@ int mg_mark_contained(mg_ctx* ctx, uint32_t* super_out) {
       ctx->counters.c_contained = acc[3];
     }
   } else {
-    MG_TRY(hipMemsetAsync(ctx->d_super, 0, (ctx->n + 1) * sizeof(uint32_t), ctx->stream));
+    // every superReadID 0 (one read length: nothing is contained); the memset
+    // only when a finalize or a new buffer left other values
+    if (ctx->super_zero_n < ctx->n + 1) {
+      MG_TRY(hipMemsetAsync(ctx->d_super, 0, (ctx->n + 1) * sizeof(uint32_t), ctx->stream));
+      ctx->super_zero_n = ctx->n + 1;
+    }
     ctx->super_any = false;
   }
   ctx->contained_done = true;
@@ -5245,6 +5283,12 @@ int mg_xchg_pack(mg_ctx* ctx, int what, void* dst, uint64_t slot, uint32_t round
     pp.cap = ctx->run_cap;
     pp.cnt = ctx->d_run_cnt;
     pp.nreg = ctx->nrun_reg;
+    if (ctx->runs_meta8) {  // (the keys-first receiver scan: 8-B metas + owner bytes, counted per rank)
+      pp.dst8 = ctx->d_rdst;
+      if (ctx->runs_counted && pp.nreg)
+        return route_slots<OWN_META>(ctx, pp, dst, self_dst, slot, rounds, cnt, ctx->d_rcnt);
+      return route_slots<OWN_META>(ctx, pp, dst, self_dst, slot, rounds, cnt);
+    }
     if (ctx->runs_counted && pp.nreg)  // the scan counted them per rank: one block per region, no count pass
       return route_slots<OWN_BUCKET>(ctx, pp, dst, self_dst, slot, rounds, cnt, ctx->d_rcnt);
     return route_slots<OWN_BUCKET>(ctx, pp, dst, self_dst, slot, rounds, cnt);
@@ -5596,7 +5640,9 @@ int mg_finalize_contained(mg_ctx* ctx, uint32_t* super_out) {
   if (!ctx) return -1;
   ctx->err.clear();  // (a message left by an earlier failed call is not this call's cause)
   MG_TRY(hipSetDevice(ctx->device));
+  const uint32_t* super_was = ctx->d_super;
   MG_ENSURE(d_super, super_cap, ctx->n + 1);
+  if (ctx->d_super != super_was) ctx->super_zero_n = 0;  // (a new buffer: nothing known about it)
   MG_ENSURE(d_cbits, cbits_cap, (ctx->n + 63) / 64 * 2);
   if (!ctx->d_any) MG_TRY(hipMalloc(&ctx->d_any, sizeof(unsigned int)));
   ctx->super_any = false;
@@ -5607,6 +5653,7 @@ int mg_finalize_contained(mg_ctx* ctx, uint32_t* super_out) {
     if (ctx->n)
       hipLaunchKernelGGL(k_super_finalize, dim3(super_grid(ctx)), dim3(kBlock), 0,
                          ctx->stream, ctx->superkey, ctx->n, ctx->d_super, ctx->d_any, ctx->d_cbits, ctx->d_ccnt);
+    ctx->super_zero_n = 0;
     MG_TRY(hipGetLastError());
     unsigned int any = 0;
     unsigned int ccnt[64 * 16];
@@ -5617,7 +5664,12 @@ int mg_finalize_contained(mg_ctx* ctx, uint32_t* super_out) {
     ctx->n_contained = 0;
     for (int c = 0; c < 64; ++c) ctx->n_contained += ccnt[c * 16];
   } else {
-    MG_TRY(hipMemsetAsync(ctx->d_super, 0, (ctx->n + 1) * sizeof(uint32_t), ctx->stream));
+    // every superReadID 0 (one read length: nothing is contained); the memset
+    // only when a finalize or a new buffer left other values
+    if (ctx->super_zero_n < ctx->n + 1) {
+      MG_TRY(hipMemsetAsync(ctx->d_super, 0, (ctx->n + 1) * sizeof(uint32_t), ctx->stream));
+      ctx->super_zero_n = ctx->n + 1;
+    }
   }
   ctx->contained_done = true;
   ctx->superkey = nullptr;  // a caller-owned key array is not referenced past this call

@@ -420,7 +420,7 @@ int XchgStep::run() {
     bool over = false;
     for (int kind = 0; kind < nk; ++kind) {
       if (mx[kind] > caps_[kind]) over = true;
-      caps_[kind] = mx[kind] + mx[kind] * 15 / 100 + 64;
+      caps_[kind] = mx[kind] + mx[kind] * 6 / 100 + 64;  // (sharded.py XchgPlan.grow's margin)
     }
     rows_held_ = 0;
     for (int p = 0; p < P; ++p) rows_held_ += rc[p];

@@ -86,11 +86,13 @@ class XchgPlan:
     def grow(self, used: dict) -> bool:
         """Fit the capacities to the counts seen (MAX over ranks and peers, identical on every
         rank): streams that overflowed grow (True: rerun the step), the others shrink, so from
-        the second step on the slot layout moves ~15 % more than the largest stream instead of
-        the first guess (rows: 32 per source read, ~10x C5's)."""
+        the second step on the slot layout moves ~6 % more than the largest stream instead of
+        the first guess (rows: 32 per source read, ~10x C5's).  (15 % until round 6: the
+        per-peer counts of a step over the same reads repeat exactly; a batch of other reads
+        whose stream outgrows the margin costs one rerun of that step.)"""
         over = False
         for k, c in used.items():
-            want = int(c * 1.15) + SLOT_ALIGN
+            want = int(c * 1.06) + SLOT_ALIGN
             if c > self.caps[k]:
                 over = True
             self.caps[k] = want
