@@ -166,7 +166,10 @@ uint64_t mg_num_rows(const mg_ctx* ctx);
  * (insertAllEdgesOfRead of its sources, OverlapGraph.cpp:529-565).  The union
  * over ranks is the whole multiset.  With the clustered slot layout the
  * range's reads are re-clustered into slots [read_lo, read_hi) at the next
- * mg_build_index. */
+ * mg_build_index.  A bucket range over every source (rank, nranks, 0, 0) with
+ * one read length is the bucket mode (bench --multi bucket): mg_build_index's
+ * one window scan reads every read, files the keys and keeps the runs of the
+ * rank's buckets only, and mg_find_overlaps finds all of their discoveries. */
 int mg_set_shard(mg_ctx* ctx, uint32_t rank, uint32_t nranks, uint64_t read_lo, uint64_t read_hi);
 
 /* --- exchange mode: one process per GPU, SURVEY §8(e) ------------------------
@@ -194,9 +197,12 @@ int mg_set_shard(mg_ctx* ctx, uint32_t rank, uint32_t nranks, uint64_t read_lo, 
  * One step (HashTable::insertDataset + OverlapGraph markContainedReads +
  * insertAllEdgesOfRead, distributed):
  *   mg_xchg_begin                 one window scan of this rank's sources: their
- *                                 index keys + minimizer runs (in scan order)
- *   mg_xchg_pack(MG_KEYS) -> a2a -> mg_xchg_insert_keys        (insertDataset)
- *   mg_xchg_pack(MG_RUNS) -> a2a   (the received runs serve both probes)
+ *                                 index keys + minimizer runs (in scan order);
+ *                                 keys first (mg_xchg_keys_first): the keys only
+ *   mg_xchg_pack(MG_KEYS) -> a2a -> mg_xchg_insert_keys        (insertDataset;
+ *                                 keys first: the window scan runs here)
+ *   mg_xchg_pack(MG_RUNS) -> a2a   (the received runs serve both probes;
+ *                                 one length: mg_xchg_probe_own meanwhile)
  *   mg_begin_contained(superkey)
  *   [lengths differ: (mg_xchg_prefix_marks -> all-reduce MAX of the marks)
  *                    mg_xchg_probe(1) -> all-reduce MAX of superkey]
@@ -241,7 +247,10 @@ int mg_xchg_pack(mg_ctx* ctx, int what, void* dst, uint64_t slot, uint32_t round
 /* File the received key records into the local cells (insertIntoTable,
  * HashTable.cpp:163-195); recv / counts as the all-to-all delivered them.  The
  * records are sorted by home cell and stored without atomics (a cell's 9th+
- * entries chain on); one host read of the counts. */
+ * entries chain on); one host read of the counts.  Keys first
+ * (mg_xchg_keys_first): the rank's window scan runs here instead and
+ * CAS-inserts the received records between its windows, leaving the runs
+ * (OverlapGraph.cpp:534-537) for mg_xchg_pack(MG_RUNS). */
 int mg_xchg_insert_keys(mg_ctx* ctx, const void* recv, uint64_t slot, uint32_t rounds, const uint64_t* counts);
 /* Probe the received runs against the local cells: contain = 1 atomicMax-es
  * containment keys into the buffer of mg_begin_contained; contain = 0 verifies
@@ -253,7 +262,8 @@ int mg_xchg_insert_keys(mg_ctx* ctx, const void* recv, uint64_t slot, uint32_t r
  * first call orders them by bucket into the context's own array instead.) */
 int mg_xchg_probe(mg_ctx* ctx, int contain, const void* recv, uint64_t slot, uint32_t rounds, const uint64_t* counts);
 /* Optional, after mg_finalize_contained and before mg_xchg_probe(0): the
- * discovery probe of this rank's OWN run stream, which mg_xchg_pack(MG_RUNS)
+ * discovery probe (insertAllEdgesOfRead's window loop + checkOverlap,
+ * OverlapGraph.cpp:529-565, 354-383) of this rank's OWN run stream, which mg_xchg_pack(MG_RUNS)
  * wrote straight into recv (send_counts = that pack's counts; only this
  * rank's entry is read), so it runs while the peers' streams are still on the
  * links; mg_xchg_probe(0) then probes the peers' streams and appends its rows.

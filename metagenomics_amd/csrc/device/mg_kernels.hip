@@ -1803,8 +1803,13 @@ __device__ __forceinline__ uint32_t id_owner(uint32_t x1, uint32_t P, uint64_t n
 // DCNT (exchange mode, P > 1): the rows each wavefront stores are also counted
 // per destination rank, so their routing needs no count pass (a separate
 // instantiation: the fused path's probe keeps its registers)
-template <int MAXW, bool CONTAIN, bool DCNT = false>
+// XCHG: the exchange mode's split discovery probe (region remap rm_*, rows
+// appended after an earlier launch's); DCNT (exchange only) includes it.  A
+// separate instantiation: the remap's divides cost the fused probes registers
+// (C5 containment 126 -> 130 VGPRs, one wave per SIMD less, when it was shared)
+template <int MAXW, bool CONTAIN, bool DCNT = false, bool XCHG = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MG_PROBE_WAVES))) void k_probe(ProbeParams p) {
+  constexpr bool kXchg = DCNT || XCHG;
   using PL = ProbeLds<MAXW>;
   extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
   __shared__ unsigned int s_dc[DCNT ? kWavesPerBlock * kWave : 1];
@@ -1825,7 +1830,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MG_PROBE
   const uint64_t nwp = (uint64_t)gridDim.x * kWavesPerBlock;
   const uint32_t seg = (uint32_t)(gw & (kSegs - 1));
   uint32_t* const region = p.rows + gw * p.reg_cap * 3;
-  uint64_t cursor = (!CONTAIN && p.append) ? p.reg_cnt[gw] : 0;  // (the second part of a split probe)
+  uint64_t cursor = (kXchg && !CONTAIN && p.append) ? p.reg_cnt[gw] : 0;  // (the second part of a split probe)
   uint32_t ncand = 0, npend = 0;
   // diagnostics (p.stats): wavefront sum of a per-lane count into counter i
   // (runs probed, entries scanned, partners fetched, rows); call converged.
@@ -1984,7 +1989,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MG_PROBE
   };
   auto open_region = [&](uint32_t r) {
     uint64_t reg = reg_of(r);
-    if (p.rm_part) {  // (wavefront-uniform; once per region)
+    if (kXchg && p.rm_part) {  // (wavefront-uniform; once per region)
       const uint64_t blk = reg / p.rm_K, k = reg - blk * p.rm_K;
       uint64_t t = blk, sp = p.rm_me;
       if (p.rm_part == 2) {
@@ -3398,9 +3403,15 @@ struct LaunchScan {
     const uint64_t G = scan_is_reg(ctx, index) ? 1 : (uint64_t)scan_windows(ctx, index);
     const uint64_t nreg = nw * G;
     ctx->nrun_reg = nreg;
-    // expected runs per read ~ 2 J / (w + 1) + 1 (minimizer density)
-    const uint64_t J = ctx->maxlen > ctx->h + 1 ? ctx->maxlen - ctx->h - 1 : 1;
-    const uint64_t per_read = std::min<uint64_t>(J, 3 * (2 * J / (ctx->w + 1) + 2));
+    // expected runs per read ~ 2 J / (w + 1) + 1 (minimizer density), priced at
+    // the middle length with 2x headroom (measured: C3 10.9, C5 13.4 per read);
+    // a region that overflows is resized and rescanned (settle_runs).  Priced at
+    // the longest read with 3x until round 6, C5's first allocation was 53 GB
+    // per context: what failed for 8 replicated C5 contexts on one device
+    const uint64_t Jmax = ctx->maxlen > ctx->h + 1 ? ctx->maxlen - ctx->h - 1 : 1;
+    const uint64_t mid = ((uint64_t)ctx->minlen + ctx->maxlen) / 2;
+    const uint64_t J = mid > ctx->h + 1 ? mid - ctx->h - 1 : 1;
+    const uint64_t per_read = std::min<uint64_t>(Jmax, 2 * (2 * J / (ctx->w + 1) + 2));
     const uint64_t groups_per_region = ((ngroups + G - 1) / G + nw - 1) / nw;  // windows per wave
     uint64_t run_cap = std::max<uint64_t>(
         ctx->run_cap_need, ctx->run_cap_opt ? ctx->run_cap_opt : groups_per_region * kWave * per_read);
@@ -3602,7 +3613,11 @@ struct LaunchProbe {
       allow_lds(k_probe<W, false, true>, lds);
       hipLaunchKernelGGL((k_probe<W, false, true>), dim3(grid), dim3(kBlock), lds, ctx->stream, pp);
     } else if (contain) {
+      if (pp.rm_part || pp.append) return set_err(ctx, "containment probe: no split / append form");
       hipLaunchKernelGGL((k_probe<W, true>), dim3(grid), dim3(kBlock), lds, ctx->stream, pp);
+    } else if (pp.rm_part || pp.append) {  // a split exchange probe
+      allow_lds(k_probe<W, false, false, true>, lds);
+      hipLaunchKernelGGL((k_probe<W, false, false, true>), dim3(grid), dim3(kBlock), lds, ctx->stream, pp);
     } else {
       hipLaunchKernelGGL((k_probe<W, false>), dim3(grid), dim3(kBlock), lds, ctx->stream, pp);
     }
