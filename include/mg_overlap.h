@@ -350,6 +350,11 @@ int mg_get_counters(const mg_ctx* ctx, mg_counters* c);
  *                   windows of 256 reads (default 1);
  *  "layout_scratch" 0 = free the layout's double buffers after each layout
  *                   (many contexts on one device); default 1 keeps them;
+ *  "cells_double"   1 = two cell tables: each build takes the one the previous
+ *                   build cleared on the side stream and clears the table it
+ *                   retires there (2x the cells' memory; measured slower: the
+ *                   clear beside the scan slows the scan); 0 (default) = one
+ *                   table, cleared at the start of each build;
  *  "chain_par"      sorted cell builds (exchange mode): records past their home
  *                   cell placed in parallel by their index in their fingerprint's
  *                   run (default 1); 0 = one thread walks each overflowing cell;

@@ -66,6 +66,14 @@ struct mg_ctx {
   bool index_ready = false;
   uint64_t* d_cells = nullptr;  // cells of kCell entries (this rank's bucket range)
   size_t cells_cap = 0;
+  // option "cells_double" (default off): a second table, cleared on the side
+  // stream for the next build (cells_alt_clean entries, done at ev[13]).
+  // Measured: the clear beside the scan slowed the scan more than the clear
+  // costs (C3 scan 2.22 -> 2.72 ms, step 6.91 -> 7.26; profiles/r06s_ab_cells_double.txt)
+  uint64_t* d_cells_alt = nullptr;
+  size_t cells_alt_cap = 0;
+  size_t cells_alt_clean = 0;
+  bool cells_double = false;
   // the index holds the o = 1 keys (suffix keys of the forward strand) only
   // when a probe reads them: discovery never does (an o = 1 hit is the twin of
   // the partner's o = 0 hit) and containment only without the

@@ -3907,7 +3907,7 @@ void mg_destroy(mg_ctx* ctx) {
                   ctx->d_tmp32, ctx->d_lay_k[0], ctx->d_lay_k[1], ctx->d_lay_v[0], ctx->d_lay_v[1], ctx->d_lay_tmp,
                   ctx->d_words_alt, ctx->d_len_alt, ctx->d_cbits, ctx->d_ccnt, ctx->d_lcells, ctx->d_lkcells,
                   ctx->d_rhead, ctx->d_rstart, ctx->d_rcnt, ctx->d_dcnt, ctx->d_p0runs, ctx->d_p0cnt, ctx->d_xexp,
-                  ctx->d_kblk, ctx->d_rdst};
+                  ctx->d_kblk, ctx->d_rdst, ctx->d_cells_alt};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   for (auto& e : ctx->ev)
@@ -4132,7 +4132,7 @@ int mg_set_option(mg_ctx* ctx, const char* name, int64_t value) {
   }
   if (flag("stats", &ctx->stats) || flag("halving", &ctx->halving_low) || flag("layout", &ctx->layout) ||
       flag("contain_jcut", &ctx->contain_jcut) || flag("contain_skip", &ctx->contain_skip) ||
-      flag("contain_prune", &ctx->contain_prune) || flag("probe_share", &ctx->probe_share) ||
+      flag("contain_prune", &ctx->contain_prune) || flag("cells_double", &ctx->cells_double) || flag("probe_share", &ctx->probe_share) ||
       flag("probe_compact", &ctx->probe_compact) || flag("live_index", &ctx->live_index) ||
       flag("xchg_sort_runs", &ctx->xchg_sort_runs) || flag("layout_scratch", &ctx->layout_scratch) ||
       flag("xchg_windows", &ctx->xchg_windows) || flag("chain_par", &ctx->chain_par) ||
@@ -4219,8 +4219,32 @@ int setup_index(mg_ctx* ctx, uint32_t min_overlap, uint32_t seed_k, bool cells =
 
 // the (cleared) cell table of this rank's bucket range
 int setup_cells(mg_ctx* ctx) {
-  MG_ENSURE(d_cells, cells_cap, ctx->cell_n * kCell);
-  MG_TRY(hipMemsetAsync(ctx->d_cells, 0xFF, ctx->cell_n * kCell * sizeof(uint64_t), ctx->stream));  // kEmpty
+  const size_t need = ctx->cell_n * kCell;
+  if (!ctx->cells_double) {
+    MG_ENSURE(d_cells, cells_cap, need);
+    MG_TRY(hipMemsetAsync(ctx->d_cells, 0xFF, need * sizeof(uint64_t), ctx->stream));  // kEmpty
+    return 0;
+  }
+  // two tables (option cells_double): this build takes the one the previous
+  // build cleared on the side stream (its clear ran beside that step's
+  // kernels; the stream waits for it), and the table it retires -- the last
+  // index, which nothing reads once a new build starts -- is cleared there for
+  // the next build.  The first build after a resize clears its own table.
+  if (ctx->d_cells_alt && ctx->cells_alt_clean >= need) {
+    std::swap(ctx->d_cells, ctx->d_cells_alt);
+    std::swap(ctx->cells_cap, ctx->cells_alt_cap);
+    MG_TRY(hipStreamWaitEvent(ctx->stream, ctx->ev[13], 0));
+  } else {
+    MG_ENSURE(d_cells, cells_cap, need);
+    MG_TRY(hipMemsetAsync(ctx->d_cells, 0xFF, need * sizeof(uint64_t), ctx->stream));  // kEmpty
+  }
+  ctx->cells_alt_clean = 0;
+  MG_ENSURE(d_cells_alt, cells_alt_cap, need);
+  MG_TRY(hipEventRecord(ctx->ev[12], ctx->stream));  // (every reader of the retired table is before this point)
+  MG_TRY(hipStreamWaitEvent(ctx->side, ctx->ev[12], 0));
+  MG_TRY(hipMemsetAsync(ctx->d_cells_alt, 0xFF, need * sizeof(uint64_t), ctx->side));
+  MG_TRY(hipEventRecord(ctx->ev[13], ctx->side));
+  ctx->cells_alt_clean = need;
   return 0;
 }
 
