@@ -432,6 +432,7 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     cfg = CONFIGS[args.config]
     n, lo, hi, G, l, k, seed, desc = cfg
+    multi_auto = args.multi == "auto"
     if args.multi == "auto":
         # DESIGN.md §6c (simulated per-rank tables + the xGMI model): one read length, up to 4
         # ranks: the bucket mode (no data-path collective; the exchange's run streams cost
@@ -678,6 +679,13 @@ def main():
         "layout_ms": layout_ms,
         "layout_first_upload_ms": layout_ms,
         "phase_wall_ms": {kk: v / args.steps for kk, v in phase_ms.items()} or None,
+        # which multi-GPU mode ran and why (N > 1 / --sim-world): --multi auto's choice rests on
+        # simulated per-rank tables and the xGMI model, not on an 8-GPU run
+        "multi_mode": None if mode == "fused" else {
+            "mode": mode, "requested": "--exchange" if args.exchange else ("auto" if multi_auto else args.multi),
+            "rule": ("auto: bucket for one read length on <= 4 ranks, else exchange; chosen from simulated "
+                     "per-rank kernel tables + the xGMI link model (DESIGN.md §6c, profiles/r06_xchg_model_c3.md), "
+                     "not yet confirmed on a multi-GPU node") if multi_auto and not args.exchange else "explicit"},
         "exchange_reruns": reruns[0] if mode.startswith("exchange") else None,
         "exchange_rows": (("routed to their src owners" if args.route_rows and P > 1 else
                            "held by the rank that verified them (union = the multiset)")
