@@ -43,6 +43,13 @@
 #include "mg_ctx.hpp"
 #include "mg_overlap.h"
 
+// two window steps per loop trip in the scan (A/B builds: -DMG_SCAN_UNROLL=2).
+// Measured: C3 scan level (2.19-2.21 vs 2.21-2.23 ms), C5 -0.14 ms of 15.8
+// (profiles/r06v_ab_scan_unroll2.txt): the step is not bound by its loop control
+#ifndef MG_SCAN_UNROLL
+#define MG_SCAN_UNROLL 1
+#endif
+
 namespace {
 
 constexpr int kWave = 64;
@@ -1296,10 +1303,19 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(G > 1 ? 
         for (int t = t0, sh = 62 - 2 * ((t0 + m) & 31); t <= tf; ++t, sh -= 2) step_first(t, rw[k], sh);
         int t = max(t0, w + 1), sh = 62 - 2 * ((t + m) & 31);
         if (t <= t1) {
+#if MG_SCAN_UNROLL == 2
+          // two steps per trip: half the loop's scalar counting and branching
+          for (; t + 1 <= t1; t += 2, sh -= 4) {
+            step(t, rw[k], sh);
+            step(t + 1, rw[k], sh - 2);
+          }
+          if (t <= t1) step(t, rw[k], sh);
+#else
           do {  // (bottom-tested: one compare and branch per step)
             step(t, rw[k], sh);
             sh -= 2;
           } while (++t <= t1);
+#endif
         }
       }
     } else {
