@@ -683,6 +683,7 @@ def main():
         # simulated per-rank tables and the xGMI model, not on an 8-GPU run
         "multi_mode": None if mode == "fused" else {
             "mode": mode, "requested": "--exchange" if args.exchange else ("auto" if multi_auto else args.multi),
+            "process_group": dist.get_backend() if dist is not None else None,
             "rule": ("auto: bucket for one read length on <= 4 ranks, else exchange; chosen from simulated "
                      "per-rank kernel tables + the xGMI link model (DESIGN.md §6c, profiles/r06_xchg_model_c3.md), "
                      "not yet confirmed on a multi-GPU node") if multi_auto and not args.exchange else "explicit"},
