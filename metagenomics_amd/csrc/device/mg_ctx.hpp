@@ -298,6 +298,7 @@ struct mg_ctx {
   bool prefix_contain = true;  // option "prefix_contain"
   bool contain_jcut = true;    // option "contain_jcut": containment probe drops runs with jlo > n1 - minlen (C5: 60 -> 47 ms)
   bool contain_skip = true;    // option "contain_skip": skip runs of sources already known contained (C5: 42.8 -> 29.7 ms)
+  uint32_t probe_split_max = 8;  // option "probe_split_max": virtual run regions per region for the probe's balance (1 = off)
   bool contain_prune = true;   // option "contain_prune": skip candidates that cannot raise the superkey (C5: 388M -> 110M compares)
   float shared_scan_ms = 0.f;  // k_scan<INDEX> kernel time of the last mg_build_index
   mg_timings t{};

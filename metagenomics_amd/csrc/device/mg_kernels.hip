@@ -1731,6 +1731,11 @@ struct ProbeParams {
   const unsigned long long* run_cnt;
   uint64_t run_cap;
   uint64_t run_regions;           // probe wavefront r consumes run regions r, r + nw, r + 2 nw, ... < run_regions
+  // vsplit > 1 (not in the exchange split probe): every run region is walked as
+  // vsplit VIRTUAL regions (consecutive parts of its records, whole batch
+  // strides each), so the probe's waves get an equal count of them when the
+  // scan's region count is not a multiple of the probe's waves
+  uint32_t vsplit;
   const uint32_t* src_super;      // runs of sources with superReadID != 0 are dropped (:548; nullptr: none)
   uint64_t src_lo, src_hi;        // only runs of sources in [src_lo, src_hi) (src_hi = 0: all)
   uint32_t* rows;                 // 3 dwords per row (mg_edge); one region per wavefront
@@ -1991,7 +1996,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MG_PROBE
   uint32_t rg = 0;
   uint64_t rpos = 0, rcnt = 0;
   const ulonglong2* rbase = p.runs;
-  const uint64_t rlimit = p.run_regions;
+  const uint32_t vsplit = kXchg ? 1u : p.vsplit;
+  const uint64_t rlimit = p.run_regions * vsplit;
   // share (option probe_share): the block's 4 wavefronts walk the SAME regions
   // (4 b .. 4 b + 3, then + nwp, ...) and take every 4th batch of each, so a
   // block probes one scan group of 64 neighbouring reads at a time and their
@@ -2005,6 +2011,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MG_PROBE
   };
   auto open_region = [&](uint32_t r) {
     uint64_t reg = reg_of(r);
+    uint32_t part = 0;
+    if (!kXchg && vsplit > 1) {  // virtual region: part `part` of run region reg / vsplit (wavefront-uniform)
+      const uint32_t v = (uint32_t)reg;
+      reg = v / vsplit;
+      part = v - (uint32_t)reg * vsplit;
+    }
     if (kXchg && p.rm_part) {  // (wavefront-uniform; once per region)
       const uint64_t blk = reg / p.rm_K, k = reg - blk * p.rm_K;
       uint64_t t = blk, sp = p.rm_me;
@@ -2018,7 +2030,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MG_PROBE
     rbase = p.runs + reg * p.run_cap;
     const uint64_t c = p.run_cnt[reg];
     rcnt = c < p.run_cap ? c : p.run_cap;
-    rpos = share ? (uint64_t)wv * kWave : 0;
+    uint64_t lo = 0;
+    if (!kXchg && vsplit > 1) {  // records [lo, hi) of the region, lo a whole number of batch strides
+      const uint32_t c32 = (uint32_t)rcnt, st = (uint32_t)rstep;
+      const uint32_t per = ((c32 + vsplit - 1) / vsplit + st - 1) / st * st;
+      lo = min((uint64_t)part * per, rcnt);
+      rcnt = min(lo + per, rcnt);
+    }
+    rpos = lo + (share ? (uint64_t)wv * kWave : 0);
   };
   // skip to the next non-empty batch position; false once the regions are exhausted
   auto hbm_settle = [&]() -> bool {
@@ -3615,6 +3634,24 @@ struct LaunchProbe {
       pp.rm_me = ctx->rank;
       pp.rm_K = ctx->xruns_K;
     }
+    // virtual regions: the split (1..probe_split_max) that gives every probe
+    // wavefront (or block, with share) the same number of regions -- the fused
+    // scan writes one region per scan wavefront, and the scan keeps more
+    // wavefronts resident than the probe (C3: 6,144 regions for 4,096 probe
+    // wavefronts, so half of them probed two regions and half one)
+    pp.vsplit = 1;
+    if (!pp.rm_part && !pp.append && run_regions) {
+      const uint64_t nwp = (uint64_t)grid * kWavesPerBlock;
+      double best = 1e300;
+      for (uint32_t k = 1; k <= ctx->probe_split_max; ++k) {
+        const double V = (double)(run_regions * k), rounds = (double)((run_regions * k + nwp - 1) / nwp);
+        const double ratio = rounds * (double)nwp / V;  // slowest wavefront's share / the mean, >= 1
+        if (ratio < best - 1e-9) {
+          best = ratio;
+          pp.vsplit = k;
+        }
+      }
+    }
     const size_t lds = (size_t)kWavesPerBlock * ProbeLds<W>::bytes;
     const bool dcnt = !contain && ctx->xchg && ctx->xchg_route_rows && ctx->nranks > 1 &&
                       ctx->nranks <= (uint32_t)kWave && ctx->n;
@@ -4118,6 +4155,11 @@ int mg_set_option(mg_ctx* ctx, const char* name, int64_t value) {
   }
   if (!strcmp(name, "max_blocks")) {  // diagnostics: cap the persistent probe grid
     ctx->max_blocks = value > 0 ? (uint32_t)value : 8192u;
+    return 0;
+  }
+  if (!strcmp(name, "probe_split_max")) {  // largest virtual split of a run region (1 = off)
+    if (value < 1 || value > 64) return set_err(ctx, "probe_split_max out of range [1,64]");
+    ctx->probe_split_max = (uint32_t)value;
     return 0;
   }
   if (!strcmp(name, "layout_hash")) {  // slot layout's minimizer hash: 0 fmix32 (default), 1 24-bit multiplies
