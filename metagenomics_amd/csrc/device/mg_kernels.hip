@@ -3639,11 +3639,17 @@ struct LaunchProbe {
     // scan writes one region per scan wavefront, and the scan keeps more
     // wavefronts resident than the probe (C3: 6,144 regions for 4,096 probe
     // wavefronts, so half of them probed two regions and half one)
+    // Only regions of many batches are split (a part of a few batches costs its
+    // wavefront a region switch per batch: the exchange mode's 1,024-record
+    // slot regions probed 2x slower split 8 ways), and only while the regions
+    // are too few to even out by themselves (< 4 per probe wavefront)
     pp.vsplit = 1;
-    if (!pp.rm_part && !pp.append && run_regions) {
-      const uint64_t nwp = (uint64_t)grid * kWavesPerBlock;
+    const uint64_t nwp_all = (uint64_t)grid * kWavesPerBlock;
+    const uint32_t kmax = (uint32_t)std::min<uint64_t>(ctx->probe_split_max, std::max<uint64_t>(1, run_cap / 4096));
+    if (!pp.rm_part && !pp.append && run_regions && run_regions < 4 * nwp_all) {
+      const uint64_t nwp = nwp_all;
       double best = 1e300;
-      for (uint32_t k = 1; k <= ctx->probe_split_max; ++k) {
+      for (uint32_t k = 1; k <= kmax; ++k) {
         const double V = (double)(run_regions * k), rounds = (double)((run_regions * k + nwp - 1) / nwp);
         const double ratio = rounds * (double)nwp / V;  // slowest wavefront's share / the mean, >= 1
         if (ratio < best - 1e-9) {
