@@ -3658,6 +3658,9 @@ struct LaunchProbe {
         }
       }
     }
+#ifdef MG_PROBE_SPLIT_FORCE  // (A/B builds: a fixed split wherever one is allowed)
+    if (pp.vsplit > 1) pp.vsplit = MG_PROBE_SPLIT_FORCE;
+#endif
     const size_t lds = (size_t)kWavesPerBlock * ProbeLds<W>::bytes;
     const bool dcnt = !contain && ctx->xchg && ctx->xchg_route_rows && ctx->nranks > 1 &&
                       ctx->nranks <= (uint32_t)kWave && ctx->n;
